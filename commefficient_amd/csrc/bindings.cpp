@@ -1,0 +1,501 @@
+// torch.ops.commeff.* registrations: one schema per op, a CPU kernel (native
+// C++, cpu_ops.cpp) and a CUDA-dispatch-key kernel (HIP launchers for gfx950).
+// On ROCm builds of PyTorch HIP tensors dispatch under the CUDA key.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <torch/library.h>
+
+#include <cstring>
+
+#include "cpu_ops.h"
+#include "kernels.h"
+
+namespace commeff {
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+float* fptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+
+struct HashCtx {
+  RowHashes rows;
+  SketchGeom geom;
+  const int32_t* blk_off = nullptr;
+  const float* blk_sign = nullptr;
+};
+
+HashCtx make_ctx(const at::Tensor& hashes, const at::Tensor& blk_off, const at::Tensor& blk_sign,
+                 int64_t num_blocks, int64_t d, int64_t c, bool on_device) {
+  TORCH_CHECK(hashes.device().is_cpu() && hashes.scalar_type() == at::kLong &&
+                  hashes.dim() == 2 && hashes.size(1) == kHashParams,
+              "hashes must be a CPU int64 tensor [r, 6]");
+  const int64_t r = hashes.size(0);
+  TORCH_CHECK(r >= 1 && r <= kMaxRows, "num_rows must be in [1, 16]");
+  TORCH_CHECK(d >= 0 && d < (1ll << 31), "sketched vector length must be < 2^31");
+  TORCH_CHECK(c >= 1 && r * c < (1ll << 32), "r*c must be < 2^32");
+  HashCtx ctx;
+  auto hc = hashes.contiguous();
+  const int64_t* hp = hc.data_ptr<int64_t>();
+  for (int64_t j = 0; j < r; ++j) {
+    RowHash& rh = ctx.rows.row[j];
+    rh.a = static_cast<uint32_t>(hp[j * 6 + 0]);
+    rh.b = static_cast<uint32_t>(hp[j * 6 + 1]);
+    rh.c0 = static_cast<uint32_t>(hp[j * 6 + 2]);
+    rh.c1 = static_cast<uint32_t>(hp[j * 6 + 3]);
+    rh.c2 = static_cast<uint32_t>(hp[j * 6 + 4]);
+    rh.c3 = static_cast<uint32_t>(hp[j * 6 + 5]);
+  }
+  ctx.geom = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
+                       static_cast<uint32_t>(c), static_cast<uint32_t>(num_blocks));
+  if (ctx.geom.num_blocks > 1) {
+    TORCH_CHECK(blk_off.numel() == r * ctx.geom.num_blocks && blk_sign.numel() == r * ctx.geom.num_blocks,
+                "blk_off/blk_sign must be [r, num_blocks]");
+    TORCH_CHECK(blk_off.scalar_type() == at::kInt && blk_sign.scalar_type() == at::kFloat,
+                "blk_off int32, blk_sign float32");
+    TORCH_CHECK(blk_off.is_cuda() == on_device && blk_sign.is_cuda() == on_device,
+                "blk_off/blk_sign must live on the op's device");
+    ctx.blk_off = blk_off.data_ptr<int32_t>();
+    ctx.blk_sign = blk_sign.data_ptr<float>();
+  }
+  return ctx;
+}
+
+// ============================================================ CPU kernels
+
+void cs_encode_cpu(at::Tensor table, const at::Tensor& vec, const at::Tensor& hashes,
+                   const at::Tensor& blk_off, const at::Tensor& blk_sign, int64_t num_blocks,
+                   double scale, const c10::optional<at::Tensor>& wvec, double wscale,
+                   const c10::optional<at::Tensor>& scratch) {
+  check_f32(table, "table");
+  check_f32(vec, "vec");
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, vec.numel(), table.size(-1), false);
+  TORCH_CHECK(table.numel() == static_cast<int64_t>(ctx.geom.r) * ctx.geom.c, "table shape");
+  cpu::cs_encode(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
+                 static_cast<float>(scale), static_cast<float>(wscale), ctx.rows, ctx.geom,
+                 ctx.blk_off, ctx.blk_sign);
+}
+
+at::Tensor cs_query_cpu(const at::Tensor& table, const at::Tensor& hashes,
+                        const at::Tensor& blk_off, const at::Tensor& blk_sign,
+                        int64_t num_blocks, int64_t d) {
+  check_f32(table, "table");
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, table.size(-1), false);
+  auto est = at::empty({d}, table.options());
+  cpu::cs_query(table.data_ptr<float>(), est.data_ptr<float>(), ctx.rows, ctx.geom, ctx.blk_off,
+                ctx.blk_sign);
+  return est;
+}
+
+void cs_zero_buckets_cpu(at::Tensor t1, const c10::optional<at::Tensor>& t2,
+                         const at::Tensor& idx, const c10::optional<at::Tensor>& vals,
+                         const at::Tensor& hashes, const at::Tensor& blk_off,
+                         const at::Tensor& blk_sign, int64_t num_blocks, int64_t d) {
+  check_f32(t1, "t1");
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, t1.size(-1), false);
+  cpu::cs_zero_buckets(t1.data_ptr<float>(), fptr(t2), idx.data_ptr<int64_t>(), fptr(vals),
+                       idx.numel(), ctx.rows, ctx.geom, ctx.blk_off, ctx.blk_sign);
+}
+
+at::Tensor cs_l2estimate_cpu(const at::Tensor& table) {
+  check_f32(table, "table");
+  auto out = at::empty({}, table.options());
+  out.fill_(cpu::cs_l2estimate(table.data_ptr<float>(), static_cast<int>(table.size(0)),
+                               table.size(1)));
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> topk_abs_cpu(const at::Tensor& x, int64_t k) {
+  check_f32(x, "x");
+  const int64_t n = x.numel();
+  const int64_t kk = std::max<int64_t>(0, std::min(k, n));
+  auto idx = at::empty({kk}, x.options().dtype(at::kLong));
+  auto vals = at::empty({kk}, x.options());
+  cpu::topk_abs(x.data_ptr<float>(), n, kk, idx.data_ptr<int64_t>(), vals.data_ptr<float>());
+  return {idx, vals};
+}
+
+void momentum_ef_cpu(at::Tensor V, const c10::optional<at::Tensor>& E, const at::Tensor& G,
+                     double rho, double gscale, int64_t mode) {
+  check_f32(V, "V");
+  check_f32(G, "G");
+  TORCH_CHECK(mode == 0 || (E.has_value() && E->numel() == V.numel()), "E required for mode>0");
+  cpu::momentum_ef(V.data_ptr<float>(), fptr(E), G.data_ptr<float>(), V.numel(),
+                   static_cast<float>(rho), static_cast<float>(gscale), static_cast<int>(mode));
+}
+
+void sparse_apply_cpu(at::Tensor w, const at::Tensor& idx, const at::Tensor& vals, double lr,
+                      const c10::optional<at::Tensor>& lr_vec,
+                      const c10::optional<at::Tensor>& last_mod, int64_t round) {
+  check_f32(w, "w");
+  int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
+  cpu::sparse_apply(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                    idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
+                    static_cast<int32_t>(round));
+}
+
+void dense_apply_cpu(at::Tensor w, const at::Tensor& delta, double lr,
+                     const c10::optional<at::Tensor>& lr_vec,
+                     const c10::optional<at::Tensor>& last_mod, int64_t round) {
+  check_f32(w, "w");
+  check_f32(delta, "delta");
+  int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
+  cpu::dense_apply(w.data_ptr<float>(), delta.data_ptr<float>(), w.numel(),
+                   static_cast<float>(lr), fptr(lr_vec), lm, static_cast<int32_t>(round));
+}
+
+at::Tensor count_ge_cpu(const at::Tensor& last_mod, const at::Tensor& thr) {
+  auto thr_c = thr.to(at::kInt).contiguous();
+  const int T = static_cast<int>(thr_c.numel());
+  auto out = at::zeros({T}, last_mod.options().dtype(at::kLong));
+  if (T > 0)
+    cpu::count_ge(last_mod.data_ptr<int32_t>(), last_mod.numel(), thr_c.data_ptr<int32_t>(), T,
+                  out.data_ptr<int64_t>());
+  return out;
+}
+
+void axpby_cpu(at::Tensor out, const at::Tensor& a, double alpha,
+               const c10::optional<at::Tensor>& b, double beta) {
+  check_f32(out, "out");
+  check_f32(a, "a");
+  cpu::axpby(out.data_ptr<float>(), a.data_ptr<float>(), static_cast<float>(alpha), fptr(b),
+             static_cast<float>(beta), out.numel());
+}
+
+at::Tensor l2norm_cpu(const at::Tensor& x) {
+  check_f32(x, "x");
+  auto out = at::empty({}, x.options());
+  out.fill_(cpu::l2norm(x.data_ptr<float>(), x.numel()));
+  return out;
+}
+
+void clip_noise_cpu(at::Tensor x, const c10::optional<at::Tensor>& norm, double clip,
+                    double noise_std, int64_t seed, int64_t offset) {
+  check_f32(x, "x");
+  cpu::clip_noise(x.data_ptr<float>(), x.numel(), fptr(norm), static_cast<float>(clip),
+                  static_cast<float>(noise_std), static_cast<uint64_t>(seed),
+                  static_cast<uint64_t>(offset));
+}
+
+void client_state_cpu(const at::Tensor& g, const c10::optional<at::Tensor>& u,
+                      const c10::optional<at::Tensor>& e, double rho) {
+  check_f32(g, "g");
+  cpu::client_state(g.data_ptr<float>(), fptr(u), fptr(e), g.numel(), static_cast<float>(rho));
+}
+
+void zero_at_cpu(const c10::optional<at::Tensor>& a, const c10::optional<at::Tensor>& b,
+                 const c10::optional<at::Tensor>& c, const at::Tensor& idx) {
+  const int64_t* ip = idx.data_ptr<int64_t>();
+  for (float* p : {fptr(a), fptr(b), fptr(c)})
+    if (p)
+      for (int64_t q = 0; q < idx.numel(); ++q) p[ip[q]] = 0.f;
+}
+
+at::Tensor scatter_dense_cpu(const at::Tensor& idx, const at::Tensor& vals, int64_t n) {
+  auto out = at::zeros({n}, vals.options());
+  float* o = out.data_ptr<float>();
+  const int64_t* ip = idx.data_ptr<int64_t>();
+  const float* vp = vals.data_ptr<float>();
+  for (int64_t q = 0; q < idx.numel(); ++q) o[ip[q]] = vp[q];
+  return out;
+}
+
+at::Tensor augment_cpu(const at::Tensor& data, const at::Tensor& idx, int64_t pad, bool flip,
+                       const at::Tensor& mean, const at::Tensor& inv_std, int64_t seed,
+                       bool out_bf16) {
+  TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.is_contiguous(),
+              "data must be uint8 [N,H,W,C] contiguous");
+  const int64_t B = idx.numel(), H = data.size(1), W = data.size(2), C = data.size(3);
+  auto out = at::empty({B, H, W, C}, data.options().dtype(at::kFloat));
+  auto mc = mean.to(at::kFloat).contiguous(), sc = inv_std.to(at::kFloat).contiguous();
+  cpu::augment_u8_nhwc(data.data_ptr<uint8_t>(), idx.contiguous().data_ptr<int64_t>(), B,
+                       static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                       static_cast<int>(pad), flip ? 1 : 0, mc.data_ptr<float>(),
+                       sc.data_ptr<float>(), static_cast<uint64_t>(seed),
+                       out.data_ptr<float>());
+  auto o = out.permute({0, 3, 1, 2});  // logical NCHW, physical NHWC
+  return out_bf16 ? o.to(at::kBFloat16) : o;
+}
+
+// ============================================================ HIP kernels
+
+void cs_encode_hip(at::Tensor table, const at::Tensor& vec, const at::Tensor& hashes,
+                   const at::Tensor& blk_off, const at::Tensor& blk_sign, int64_t num_blocks,
+                   double scale, const c10::optional<at::Tensor>& wvec, double wscale,
+                   const c10::optional<at::Tensor>& scratch) {
+  check_f32(table, "table");
+  check_f32(vec, "vec");
+  c10::hip::HIPGuard guard(table.device());
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, vec.numel(), table.size(-1), true);
+  TORCH_CHECK(table.numel() == static_cast<int64_t>(ctx.geom.r) * ctx.geom.c, "table shape");
+  if (wvec.has_value() && wvec->defined()) check_f32(*wvec, "wvec");
+  if (scratch.has_value() && scratch->defined()) {
+    BinPlan plan = plan_cs_encode_binned(ctx.geom);
+    TORCH_CHECK(plan.num_tiles <= 2048, "binned encode supports r*c <= 2048*8192");
+    TORCH_CHECK(scratch->nbytes() >= static_cast<size_t>(cs_encode_binned_scratch_bytes(plan)),
+                "scratch too small for binned encode");
+    launch_cs_encode_binned(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
+                            static_cast<float>(scale), static_cast<float>(wscale), ctx.rows,
+                            ctx.geom, ctx.blk_off, ctx.blk_sign, plan, scratch->data_ptr(),
+                            cur_stream());
+  } else {
+    launch_cs_encode(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
+                     static_cast<float>(scale), static_cast<float>(wscale), ctx.rows, ctx.geom,
+                     ctx.blk_off, ctx.blk_sign, cur_stream());
+  }
+}
+
+at::Tensor cs_query_hip(const at::Tensor& table, const at::Tensor& hashes,
+                        const at::Tensor& blk_off, const at::Tensor& blk_sign,
+                        int64_t num_blocks, int64_t d) {
+  check_f32(table, "table");
+  c10::hip::HIPGuard guard(table.device());
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, table.size(-1), true);
+  auto est = at::empty({d}, table.options());
+  launch_cs_query(table.data_ptr<float>(), est.data_ptr<float>(), ctx.rows, ctx.geom, ctx.blk_off,
+                  ctx.blk_sign, cur_stream());
+  return est;
+}
+
+void cs_zero_buckets_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2,
+                         const at::Tensor& idx, const c10::optional<at::Tensor>& vals,
+                         const at::Tensor& hashes, const at::Tensor& blk_off,
+                         const at::Tensor& blk_sign, int64_t num_blocks, int64_t d) {
+  check_f32(t1, "t1");
+  c10::hip::HIPGuard guard(t1.device());
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, t1.size(-1), true);
+  launch_cs_zero_buckets(t1.data_ptr<float>(), fptr(t2), idx.data_ptr<int64_t>(), fptr(vals),
+                         idx.numel(), ctx.rows, ctx.geom, ctx.blk_off, ctx.blk_sign,
+                         cur_stream());
+}
+
+at::Tensor cs_l2estimate_hip(const at::Tensor& table) {
+  check_f32(table, "table");
+  c10::hip::HIPGuard guard(table.device());
+  const int r = static_cast<int>(table.size(0));
+  TORCH_CHECK(r <= kMaxRows, "rows");
+  auto partial = at::empty({r * 256}, table.options());
+  auto out = at::empty({}, table.options());
+  launch_cs_l2estimate(table.data_ptr<float>(), r, table.size(1), partial.data_ptr<float>(),
+                       out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> topk_abs_hip(const at::Tensor& x, int64_t k) {
+  check_f32(x, "x");
+  c10::hip::HIPGuard guard(x.device());
+  const int64_t n = x.numel();
+  const int64_t kk = std::max<int64_t>(0, std::min(k, n));
+  auto idx = at::empty({kk}, x.options().dtype(at::kLong));
+  auto vals = at::empty({kk}, x.options());
+  if (kk == 0) return {idx, vals};
+  if (kk == n) {  // everything selected, in index order
+    idx.copy_(at::arange(n, idx.options()));
+    vals.copy_(x.reshape({-1}));
+    return {idx, vals};
+  }
+  auto ws = at::empty({topk_workspace_bytes(n)}, x.options().dtype(at::kByte));
+  launch_topk_abs(x.data_ptr<float>(), n, kk, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                  ws.data_ptr(), cur_stream());
+  return {idx, vals};
+}
+
+void momentum_ef_hip(at::Tensor V, const c10::optional<at::Tensor>& E, const at::Tensor& G,
+                     double rho, double gscale, int64_t mode) {
+  check_f32(V, "V");
+  check_f32(G, "G");
+  TORCH_CHECK(mode == 0 || (E.has_value() && E->numel() == V.numel()), "E required for mode>0");
+  c10::hip::HIPGuard guard(V.device());
+  launch_momentum_ef(V.data_ptr<float>(), fptr(E), G.data_ptr<float>(), V.numel(),
+                     static_cast<float>(rho), static_cast<float>(gscale), static_cast<int>(mode),
+                     cur_stream());
+}
+
+void sparse_apply_hip(at::Tensor w, const at::Tensor& idx, const at::Tensor& vals, double lr,
+                      const c10::optional<at::Tensor>& lr_vec,
+                      const c10::optional<at::Tensor>& last_mod, int64_t round) {
+  check_f32(w, "w");
+  c10::hip::HIPGuard guard(w.device());
+  int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
+  launch_sparse_apply(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                      idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
+                      static_cast<int32_t>(round), cur_stream());
+}
+
+void dense_apply_hip(at::Tensor w, const at::Tensor& delta, double lr,
+                     const c10::optional<at::Tensor>& lr_vec,
+                     const c10::optional<at::Tensor>& last_mod, int64_t round) {
+  check_f32(w, "w");
+  check_f32(delta, "delta");
+  c10::hip::HIPGuard guard(w.device());
+  int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
+  launch_dense_apply(w.data_ptr<float>(), delta.data_ptr<float>(), w.numel(),
+                     static_cast<float>(lr), fptr(lr_vec), lm, static_cast<int32_t>(round),
+                     cur_stream());
+}
+
+at::Tensor count_ge_hip(const at::Tensor& last_mod, const at::Tensor& thr) {
+  c10::hip::HIPGuard guard(last_mod.device());
+  auto thr_c = thr.to(last_mod.device(), at::kInt).contiguous();
+  const int T = static_cast<int>(thr_c.numel());
+  TORCH_CHECK(T <= 1024, "count_ge supports at most 1024 thresholds per call");
+  auto buf = at::zeros({2 * (T + 1)}, last_mod.options().dtype(at::kLong));
+  if (T > 0)
+    launch_count_ge(last_mod.data_ptr<int32_t>(), last_mod.numel(), thr_c.data_ptr<int32_t>(), T,
+                    buf.data_ptr<int64_t>(), cur_stream());
+  return buf.narrow(0, T + 1, T);
+}
+
+void axpby_hip(at::Tensor out, const at::Tensor& a, double alpha,
+               const c10::optional<at::Tensor>& b, double beta) {
+  check_f32(out, "out");
+  check_f32(a, "a");
+  c10::hip::HIPGuard guard(out.device());
+  launch_axpby(out.data_ptr<float>(), a.data_ptr<float>(), static_cast<float>(alpha), fptr(b),
+               static_cast<float>(beta), out.numel(), cur_stream());
+}
+
+at::Tensor l2norm_hip(const at::Tensor& x) {
+  check_f32(x, "x");
+  c10::hip::HIPGuard guard(x.device());
+  auto partial = at::empty({1024}, x.options());
+  auto out = at::empty({}, x.options());
+  launch_l2norm(x.data_ptr<float>(), x.numel(), partial.data_ptr<float>(), out.data_ptr<float>(),
+                cur_stream());
+  return out;
+}
+
+void clip_noise_hip(at::Tensor x, const c10::optional<at::Tensor>& norm, double clip,
+                    double noise_std, int64_t seed, int64_t offset) {
+  check_f32(x, "x");
+  c10::hip::HIPGuard guard(x.device());
+  launch_clip_noise(x.data_ptr<float>(), x.numel(), fptr(norm), static_cast<float>(clip),
+                    static_cast<float>(noise_std), static_cast<uint64_t>(seed),
+                    static_cast<uint64_t>(offset), cur_stream());
+}
+
+void client_state_hip(const at::Tensor& g, const c10::optional<at::Tensor>& u,
+                      const c10::optional<at::Tensor>& e, double rho) {
+  check_f32(g, "g");
+  c10::hip::HIPGuard guard(g.device());
+  launch_client_state(g.data_ptr<float>(), fptr(u), fptr(e), g.numel(), static_cast<float>(rho),
+                      cur_stream());
+}
+
+void zero_at_hip(const c10::optional<at::Tensor>& a, const c10::optional<at::Tensor>& b,
+                 const c10::optional<at::Tensor>& c, const at::Tensor& idx) {
+  c10::hip::HIPGuard guard(idx.device());
+  launch_zero_at(fptr(a), fptr(b), fptr(c), idx.data_ptr<int64_t>(), idx.numel(), cur_stream());
+}
+
+at::Tensor scatter_dense_hip(const at::Tensor& idx, const at::Tensor& vals, int64_t n) {
+  c10::hip::HIPGuard guard(vals.device());
+  auto out = at::empty({n}, vals.options());
+  launch_scatter_dense(out.data_ptr<float>(), n, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                       idx.numel(), cur_stream());
+  return out;
+}
+
+at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pad, bool flip,
+                       const at::Tensor& mean, const at::Tensor& inv_std, int64_t seed,
+                       bool out_bf16) {
+  TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.is_contiguous(),
+              "data must be uint8 [N,H,W,C] contiguous");
+  TORCH_CHECK(data.size(3) <= 4, "at most 4 channels");
+  c10::hip::HIPGuard guard(data.device());
+  const int64_t B = idx.numel(), H = data.size(1), W = data.size(2), C = data.size(3);
+  auto out = at::empty({B, H, W, C}, data.options().dtype(at::kBFloat16));
+  auto mc = mean.to(data.device(), at::kFloat).contiguous();
+  auto sc = inv_std.to(data.device(), at::kFloat).contiguous();
+  auto ic = idx.contiguous();
+  launch_augment_u8_nhwc(data.data_ptr<uint8_t>(), ic.data_ptr<int64_t>(), B,
+                         static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                         static_cast<int>(pad), flip ? 1 : 0, mc.data_ptr<float>(),
+                         sc.data_ptr<float>(), static_cast<uint64_t>(seed),
+                         reinterpret_cast<uint16_t*>(out.data_ptr()), cur_stream());
+  auto o = out.permute({0, 3, 1, 2});
+  return out_bf16 ? o : o.to(at::kFloat);
+}
+
+int64_t binned_scratch_bytes(int64_t d, int64_t r, int64_t c, int64_t num_blocks) {
+  SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
+                           static_cast<uint32_t>(c), static_cast<uint32_t>(num_blocks));
+  return cs_encode_binned_scratch_bytes(plan_cs_encode_binned(g));
+}
+
+}  // namespace
+}  // namespace commeff
+
+TORCH_LIBRARY(commeff, m) {
+  m.def("cs_encode(Tensor(a!) table, Tensor vec, Tensor hashes, Tensor blk_off, Tensor blk_sign, "
+        "int num_blocks, float scale, Tensor? wvec, float wscale, Tensor? scratch) -> ()");
+  m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
+        "int d) -> Tensor");
+  m.def("cs_zero_buckets(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, Tensor hashes, "
+        "Tensor blk_off, Tensor blk_sign, int num_blocks, int d) -> ()");
+  m.def("cs_l2estimate(Tensor table) -> Tensor");
+  m.def("topk_abs(Tensor x, int k) -> (Tensor, Tensor)");
+  m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
+  m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "
+        "Tensor(b!)? last_mod, int round) -> ()");
+  m.def("dense_apply(Tensor(a!) w, Tensor delta, float lr, Tensor? lr_vec, Tensor(b!)? last_mod, "
+        "int round) -> ()");
+  m.def("count_ge(Tensor last_mod, Tensor thr) -> Tensor");
+  m.def("axpby(Tensor(a!) out, Tensor a, float alpha, Tensor? b, float beta) -> ()");
+  m.def("l2norm(Tensor x) -> Tensor");
+  m.def("clip_noise(Tensor(a!) x, Tensor? norm, float clip, float noise_std, int seed, int offset) -> ()");
+  m.def("client_state(Tensor g, Tensor(a!)? u, Tensor(b!)? e, float rho) -> ()");
+  m.def("zero_at(Tensor(a!)? a, Tensor(b!)? b, Tensor(c!)? c, Tensor idx) -> ()");
+  m.def("scatter_dense(Tensor idx, Tensor vals, int n) -> Tensor");
+  m.def("augment_u8_nhwc(Tensor data, Tensor idx, int pad, bool flip, Tensor mean, Tensor inv_std, "
+        "int seed, bool out_bf16) -> Tensor");
+  m.def("binned_scratch_bytes(int d, int r, int c, int num_blocks) -> int",
+        &commeff::binned_scratch_bytes);
+}
+
+TORCH_LIBRARY_IMPL(commeff, CPU, m) {
+  using namespace commeff;
+  m.impl("cs_encode", &cs_encode_cpu);
+  m.impl("cs_query", &cs_query_cpu);
+  m.impl("cs_zero_buckets", &cs_zero_buckets_cpu);
+  m.impl("cs_l2estimate", &cs_l2estimate_cpu);
+  m.impl("topk_abs", &topk_abs_cpu);
+  m.impl("momentum_ef", &momentum_ef_cpu);
+  m.impl("sparse_apply", &sparse_apply_cpu);
+  m.impl("dense_apply", &dense_apply_cpu);
+  m.impl("count_ge", &count_ge_cpu);
+  m.impl("axpby", &axpby_cpu);
+  m.impl("l2norm", &l2norm_cpu);
+  m.impl("clip_noise", &clip_noise_cpu);
+  m.impl("client_state", &client_state_cpu);
+  m.impl("zero_at", &zero_at_cpu);
+  m.impl("scatter_dense", &scatter_dense_cpu);
+  m.impl("augment_u8_nhwc", &augment_cpu);
+}
+
+TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
+  using namespace commeff;
+  m.impl("cs_encode", &cs_encode_hip);
+  m.impl("cs_query", &cs_query_hip);
+  m.impl("cs_zero_buckets", &cs_zero_buckets_hip);
+  m.impl("cs_l2estimate", &cs_l2estimate_hip);
+  m.impl("topk_abs", &topk_abs_hip);
+  m.impl("momentum_ef", &momentum_ef_hip);
+  m.impl("sparse_apply", &sparse_apply_hip);
+  m.impl("dense_apply", &dense_apply_hip);
+  m.impl("count_ge", &count_ge_hip);
+  m.impl("axpby", &axpby_hip);
+  m.impl("l2norm", &l2norm_hip);
+  m.impl("clip_noise", &clip_noise_hip);
+  m.impl("client_state", &client_state_hip);
+  m.impl("zero_at", &zero_at_hip);
+  m.impl("scatter_dense", &scatter_dense_hip);
+  m.impl("augment_u8_nhwc", &augment_hip);
+}

@@ -1,0 +1,335 @@
+// Fused streaming kernels of the federated round (gfx950).
+//
+//  momentum_ef   server V/E update           fed_aggregator.py:489-503,517-521,578-582 (K6)
+//  sparse_apply  w[idx] -= lr*delta + track  fed_aggregator.py:455,613 (K12, K13)
+//  dense_apply   w -= lr*delta + track       fed_aggregator.py:455,509,566 (K12, K13)
+//  count_ge      download accounting         fed_aggregator.py:239-289 (K13)
+//  l2norm        deterministic L2 norm       utils.py:305-313 (K14/K15)
+//  clip_noise    DP clip + Gaussian noise    fed_worker.py:304-309 (K14)
+//  client_state  local momentum / error      fed_worker.py:193-202 (K9)
+//  zero_at       error/momentum masking      fed_worker.py:209-216, fed_aggregator.py:531-540 (K9, K11)
+//  axpby         FedAvg local step / deltas  fed_worker.py:98-108 (K17)
+//
+// All streaming kernels use 16-byte vector accesses on aligned, length%4==0
+// inputs (the flat parameter/gradient buffers always are) and a scalar tail.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+
+namespace commeff {
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t n, int max_blocks = 4096) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  return static_cast<int>(b < max_blocks ? b : max_blocks);
+}
+
+inline bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// ----------------------------------------------------------- momentum / EF
+__global__ void __launch_bounds__(kBlock)
+momentum_ef_kernel(float4* __restrict__ V, float4* __restrict__ E, const float4* __restrict__ G,
+                   int64_t n4, float rho, float gscale, int mode) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n4; i += stride) {
+    float4 v = V[i], g = G[i];
+    v.x = rho * v.x + gscale * g.x;
+    v.y = rho * v.y + gscale * g.y;
+    v.z = rho * v.z + gscale * g.z;
+    v.w = rho * v.w + gscale * g.w;
+    V[i] = v;
+    if (mode == 1) {
+      float4 e = E[i];
+      e.x += v.x; e.y += v.y; e.z += v.z; e.w += v.w;
+      E[i] = e;
+    } else if (mode == 2) {
+      E[i] = v;
+    }
+  }
+}
+
+__global__ void momentum_ef_tail(float* V, float* E, const float* G, int64_t start, int64_t n,
+                                 float rho, float gscale, int mode) {
+  int64_t i = start + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i >= n) return;
+  float v = rho * V[i] + gscale * G[i];
+  V[i] = v;
+  if (mode == 1) E[i] += v;
+  else if (mode == 2) E[i] = v;
+}
+
+// ----------------------------------------------------------------- apply
+__global__ void __launch_bounds__(kBlock)
+sparse_apply_kernel(float* __restrict__ w, const int64_t* __restrict__ idx,
+                    const float* __restrict__ vals, int64_t k, float lr,
+                    const float* __restrict__ lr_vec, int32_t* __restrict__ last_mod,
+                    int32_t round) {
+  int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (q >= k) return;
+  int64_t i = idx[q];
+  float l = lr_vec != nullptr ? lr_vec[i] : lr;
+  float old = w[i];
+  float nw = old - l * vals[q];
+  w[i] = nw;
+  if (last_mod != nullptr && nw != old) last_mod[i] = round;
+}
+
+__global__ void __launch_bounds__(kBlock)
+dense_apply_kernel(float* __restrict__ w, const float* __restrict__ delta, int64_t n, float lr,
+                   const float* __restrict__ lr_vec, int32_t* __restrict__ last_mod,
+                   int32_t round) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    float l = lr_vec != nullptr ? lr_vec[i] : lr;
+    float old = w[i];
+    float nw = old - l * delta[i];
+    w[i] = nw;
+    if (last_mod != nullptr && nw != old) last_mod[i] = round;
+  }
+}
+
+// -------------------------------------------------------------- count_ge
+__global__ void __launch_bounds__(kBlock)
+count_ge_kernel(const int32_t* __restrict__ last_mod, int64_t n, const int32_t* __restrict__ thr,
+                int T, unsigned long long* __restrict__ counts) {
+  // counts[t] = #{i : last_mod[i] >= thr[t]}, thr ascending.  Histogram each
+  // element into the number of thresholds it passes (upper-bound search), then
+  // suffix-sum at the end (host side of the binding).
+  __shared__ unsigned int h[1025];
+  __shared__ int th[1024];
+  for (int t = threadIdx.x; t <= T; t += blockDim.x) h[t] = 0;
+  for (int t = threadIdx.x; t < T; t += blockDim.x) th[t] = thr[t];
+  __syncthreads();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    int v = last_mod[i];
+    // number of thresholds <= v
+    int lo = 0, hi = T;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (th[mid] <= v) lo = mid + 1; else hi = mid;
+    }
+    if (lo > 0) atomicAdd(h + lo, 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x + 1; t <= T; t += blockDim.x)
+    if (h[t]) atomicAdd(counts + t, static_cast<unsigned long long>(h[t]));
+}
+
+__global__ void count_ge_finish(unsigned long long* counts, int T, int64_t* out) {
+  // element histogrammed into bin b passes thresholds 0..b-1 ->
+  // out[t] = sum_{b > t} counts[b]
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    unsigned long long run = 0;
+    for (int b = T; b >= 1; --b) {
+      run += counts[b];
+      out[b - 1] = static_cast<int64_t>(run);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- axpby
+__global__ void __launch_bounds__(kBlock)
+axpby_kernel(float* __restrict__ out, const float* __restrict__ a, float alpha,
+             const float* __restrict__ b, float beta, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    float v = alpha * a[i];
+    if (b != nullptr) v += beta * b[i];
+    out[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------- l2norm
+__global__ void __launch_bounds__(kBlock)
+sqsum_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ partial) {
+  float acc = 0.f;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    float v = x[i];
+    acc += v * v;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o);
+  __shared__ float ws[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < kBlock / 64; ++w) s += ws[w];
+    partial[blockIdx.x] = s;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+sqrt_sum_kernel(const float* __restrict__ partial, int nb, float* __restrict__ out) {
+  __shared__ float s[1024];
+  s[threadIdx.x] = threadIdx.x < nb ? partial[threadIdx.x] : 0.f;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sqrtf(s[0]);
+}
+
+// ------------------------------------------------------ Philox + clip_noise
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox(uint64_t seed, uint64_t ctr) {
+  uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  U4 c{static_cast<uint32_t>(ctr), static_cast<uint32_t>(ctr >> 32), 0u, 0u};
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) {
+  return (static_cast<float>(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+__global__ void __launch_bounds__(kBlock)
+clip_noise_kernel(float* __restrict__ x, int64_t n, const float* __restrict__ norm, float clip,
+                  float noise_std, uint64_t seed, uint64_t offset) {
+  float scale = 1.f;
+  if (clip > 0.f && norm != nullptr) {
+    float nr = norm[0];
+    if (nr > clip) scale = clip / nr;  // utils.py:clip_grad: record / (norm/clip)
+  }
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    float v = x[i] * scale;
+    if (noise_std != 0.f) {
+      U4 r = philox(seed, offset + static_cast<uint64_t>(i));
+      float u1 = u01(r.x), u2 = u01(r.y);
+      float z = sqrtf(-2.f * __logf(u1)) * __cosf(6.28318530718f * u2);
+      v += noise_std * z;
+    }
+    x[i] = v;
+  }
+}
+
+// ---------------------------------------------------------- client state
+__global__ void __launch_bounds__(kBlock)
+client_state_kernel(const float* __restrict__ g, float* __restrict__ u, float* __restrict__ e,
+                    int64_t n, float rho) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
+    float t = g[i];
+    if (u != nullptr) {
+      t = rho * u[i] + t;
+      u[i] = t;
+    }
+    if (e != nullptr) e[i] += t;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+zero_at_kernel(float* a, float* b, float* c, const int64_t* __restrict__ idx, int64_t k) {
+  int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (q >= k) return;
+  int64_t i = idx[q];
+  if (a) a[i] = 0.f;
+  if (b) b[i] = 0.f;
+  if (c) c[i] = 0.f;
+}
+
+__global__ void __launch_bounds__(kBlock)
+scatter_kernel(float* __restrict__ out, const int64_t* __restrict__ idx,
+               const float* __restrict__ vals, int64_t k) {
+  int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (q < k) out[idx[q]] = vals[q];
+}
+
+}  // namespace
+
+void launch_momentum_ef(float* V, float* E, const float* G, int64_t n, float rho, float gscale,
+                        int mode, hipStream_t stream) {
+  if (n <= 0) return;
+  int64_t n4 = (aligned16(V) && aligned16(E) && aligned16(G)) ? n / 4 : 0;
+  if (n4 > 0)
+    hipLaunchKernelGGL(momentum_ef_kernel, dim3(grid_for(n4)), dim3(kBlock), 0, stream,
+                       reinterpret_cast<float4*>(V), reinterpret_cast<float4*>(E),
+                       reinterpret_cast<const float4*>(G), n4, rho, gscale, mode);
+  int64_t start = n4 * 4;
+  if (start < n)
+    hipLaunchKernelGGL(momentum_ef_tail, dim3((n - start + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       stream, V, E, G, start, n, rho, gscale, mode);
+}
+
+void launch_sparse_apply(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
+                         const float* lr_vec, int32_t* last_mod, int32_t round, hipStream_t stream) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(sparse_apply_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
+                     w, idx, vals, k, lr, lr_vec, last_mod, round);
+}
+
+void launch_dense_apply(float* w, const float* delta, int64_t n, float lr, const float* lr_vec,
+                        int32_t* last_mod, int32_t round, hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(dense_apply_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, w, delta, n,
+                     lr, lr_vec, last_mod, round);
+}
+
+void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr, int T, int64_t* counts,
+                     hipStream_t stream) {
+  // counts must hold 2*(T+1) int64: [0, T+1) scratch bins, [T+1, 2T+1) output
+  if (T <= 0) return;
+  unsigned long long* bins = reinterpret_cast<unsigned long long*>(counts);
+  (void)hipMemsetAsync(bins, 0, (T + 1) * sizeof(unsigned long long), stream);
+  hipLaunchKernelGGL(count_ge_kernel, dim3(grid_for(n, 1024)), dim3(kBlock), 0, stream, last_mod,
+                     n, thr, T, bins);
+  hipLaunchKernelGGL(count_ge_finish, dim3(1), dim3(64), 0, stream, bins, T, counts + T + 1);
+}
+
+void launch_axpby(float* out, const float* a, float alpha, const float* b, float beta, int64_t n,
+                  hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, out, a, alpha, b,
+                     beta, n);
+}
+
+void launch_l2norm(const float* x, int64_t n, float* partial, float* out, hipStream_t stream) {
+  int nb = grid_for(n, 1024);
+  hipLaunchKernelGGL(sqsum_kernel, dim3(nb), dim3(kBlock), 0, stream, x, n, partial);
+  hipLaunchKernelGGL(sqrt_sum_kernel, dim3(1), dim3(1024), 0, stream, partial, nb, out);
+}
+
+void launch_clip_noise(float* x, int64_t n, const float* norm, float clip, float noise_std,
+                       uint64_t seed, uint64_t offset, hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(clip_noise_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, x, n, norm,
+                     clip, noise_std, seed, offset);
+}
+
+void launch_client_state(const float* g, float* u, float* e, int64_t n, float rho,
+                         hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(client_state_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, u, e, n,
+                     rho);
+}
+
+void launch_zero_at(float* a, float* b, float* c, const int64_t* idx, int64_t k,
+                    hipStream_t stream) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(zero_at_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, a,
+                     b, c, idx, k);
+}
+
+void launch_scatter_dense(float* out, int64_t n, const int64_t* idx, const float* vals, int64_t k,
+                          hipStream_t stream) {
+  (void)hipMemsetAsync(out, 0, n * sizeof(float), stream);
+  if (k <= 0) return;
+  hipLaunchKernelGGL(scatter_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out,
+                     idx, vals, k);
+}
+
+}  // namespace commeff

@@ -1,0 +1,105 @@
+// Launcher declarations for the gfx950 HIP kernels of the codec engine.
+// The kernels (*.hip) are compiled by hipcc without any torch headers; the
+// torch-op bindings (bindings.cpp) call these launchers with raw device
+// pointers and the current HIP stream.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+#include "sketch_hash.h"
+
+namespace commeff {
+
+// ---------------------------------------------------------------- sketch --
+// table[j, b_j(i)] += s_j(i) * (scale*vec[i] + wscale*wvec[i])   (wvec optional)
+void launch_cs_encode(float* table, const float* vec, const float* wvec,
+                      float scale, float wscale, const RowHashes& h,
+                      const SketchGeom& g, const int32_t* blk_off,
+                      const float* blk_sign, hipStream_t stream);
+// Binned (LDS-privatised) encode for dense vectors: two passes through a
+// scratch buffer; see sketch.hip for the layout.  Returns false if the
+// geometry is unsupported (then call launch_cs_encode).
+struct BinPlan {
+  int64_t tile;        // buckets per LDS tile (flat over rows)
+  int64_t num_tiles;
+  int64_t chunk;       // coordinates per pass-1 block
+  int64_t num_chunks;
+  int64_t cap;         // entries reserved per (chunk, tile) segment
+};
+BinPlan plan_cs_encode_binned(const SketchGeom& g);
+int64_t cs_encode_binned_scratch_bytes(const BinPlan& p);
+void launch_cs_encode_binned(float* table, const float* vec, const float* wvec,
+                             float scale, float wscale, const RowHashes& h,
+                             const SketchGeom& g, const int32_t* blk_off,
+                             const float* blk_sign, const BinPlan& plan,
+                             void* scratch, hipStream_t stream);
+// est[i] = lower-median_j( s_j(i) * table[j, b_j(i)] )
+void launch_cs_query(const float* table, float* est, const RowHashes& h,
+                     const SketchGeom& g, const int32_t* blk_off,
+                     const float* blk_sign, hipStream_t stream);
+// For every selected coordinate idx[t] with vals[t] != 0 zero the r cells
+// (j, b_j(idx[t])) of t1 and (optionally) t2.
+void launch_cs_zero_buckets(float* t1, float* t2, const int64_t* idx,
+                            const float* vals, int64_t k, const RowHashes& h,
+                            const SketchGeom& g, const int32_t* blk_off,
+                            const float* blk_sign, hipStream_t stream);
+// out[0] = sqrt(lower-median_j sum_c table[j,c]^2); partial: >= r*256 floats
+void launch_cs_l2estimate(const float* table, int r, int64_t c, float* partial,
+                          float* out, hipStream_t stream);
+
+// ------------------------------------------------------------------ topk --
+struct TopkWorkspace {
+  // all device pointers; sizes given by topk_workspace_bytes
+  void* base;
+};
+int64_t topk_workspace_bytes(int64_t n);
+// Deterministic magnitude top-k: selects the k largest |x| (ties -> lower
+// index), writes idx (ascending) and vals = x[idx].  No host sync.
+void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx,
+                     float* vals, void* workspace, hipStream_t stream);
+
+// ----------------------------------------------------------- elementwise --
+// V = rho*V + gscale*G ; mode 1: E += V ; mode 2: E = V
+void launch_momentum_ef(float* V, float* E, const float* G, int64_t n,
+                        float rho, float gscale, int mode, hipStream_t stream);
+// w[idx] -= lr(idx) * vals ; last_mod[idx] = round where w changed
+void launch_sparse_apply(float* w, const int64_t* idx, const float* vals,
+                         int64_t k, float lr, const float* lr_vec,
+                         int32_t* last_mod, int32_t round, hipStream_t stream);
+// w -= lr(i) * delta ; last_mod[i] = round where w changed
+void launch_dense_apply(float* w, const float* delta, int64_t n, float lr,
+                        const float* lr_vec, int32_t* last_mod, int32_t round,
+                        hipStream_t stream);
+// counts[t] = #{i : last_mod[i] >= thr[t]}  (thr sorted ascending, T <= 1024)
+void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr,
+                     int T, int64_t* counts, hipStream_t stream);
+// out = alpha*a + beta*b   (b optional -> out = alpha*a)
+void launch_axpby(float* out, const float* a, float alpha, const float* b,
+                  float beta, int64_t n, hipStream_t stream);
+// partial sums of squares -> out[0] = sqrt(sum) ; partial >= 1024 floats
+void launch_l2norm(const float* x, int64_t n, float* partial, float* out,
+                   hipStream_t stream);
+// x = x * min(1, clip/norm[0]) (clip <= 0: no clipping) + std * N(0,1)
+// (Philox-4x32-10 keyed by seed, counter = offset + i)
+void launch_clip_noise(float* x, int64_t n, const float* norm, float clip,
+                       float noise_std, uint64_t seed, uint64_t offset,
+                       hipStream_t stream);
+// u = rho*u + g (if u) ; e += (u ? u : g) (if e)
+void launch_client_state(const float* g, float* u, float* e, int64_t n,
+                         float rho, hipStream_t stream);
+// x[idx[t]] = 0 for t < k  (up to 3 arrays)
+void launch_zero_at(float* a, float* b, float* c, const int64_t* idx,
+                    int64_t k, hipStream_t stream);
+// out[:] = 0 ; out[idx] = vals
+void launch_scatter_dense(float* out, int64_t n, const int64_t* idx,
+                          const float* vals, int64_t k, hipStream_t stream);
+
+// -------------------------------------------------------------- augment --
+// CIFAR-style augmentation of uint8 NHWC images into a bf16 NHWC
+// (channels_last) batch: reflect-pad `pad`, random crop, random h-flip,
+// normalise.  Randomness: counter hash of (seed, example slot).
+void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx,
+                            int64_t B, int H, int W, int C, int pad,
+                            int flip, const float* mean, const float* inv_std,
+                            uint64_t seed, uint16_t* out_bf16, hipStream_t stream);
+
+}  // namespace commeff

@@ -1,0 +1,405 @@
+// Count-Sketch kernels for gfx950 (MI355X).
+//
+// Reference semantics: CSVec.accumulateVec / unSketch / zero / l2estimate as
+// used at /root/reference/CommEfficient/fed_worker.py:313-320 and
+// fed_aggregator.py:584-611.
+//
+// Design (MI355X-first, not a translation of CSVec's torch code):
+//  * hashes are recomputed in registers from 6 u32 coefficients per row that
+//    travel in the kernel arguments (SGPRs) -- no r x d index tables;
+//  * encode has two forms:
+//      - direct: one fp32 global atomic per (coord,row).  Only used for
+//        sparse inputs: random per-lane atomics run at ~1/17 of the
+//        contiguous atomic rate on CDNA4 (MI355X_MICROARCH.md "Global float
+//        atomics"), so a dense 6.5M-coordinate encode would cost ~1.6 ms;
+//      - binned: pass 1 hashes a chunk of coordinates per workgroup,
+//        counting-sorts its (value, bucket) entries by 8192-bucket table tile
+//        in LDS and streams them out as contiguous per-tile segments;
+//        pass 2 gives each tile to one workgroup that accumulates all of
+//        the tile's entries with LDS float atomics (ds_add_f32) and writes
+//        the tile back with coalesced read-modify-write stores.  Every
+//        global access is then a coalesced stream.
+//  * query gathers r signed cells per coordinate and takes the lower median
+//    (torch.median convention, which CSVec relies on) in registers.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+
+namespace commeff {
+namespace {
+
+struct HashArgs {
+  RowHash row[kMaxRows];
+};
+
+constexpr int kTileShift = 13;                 // 8192 buckets per tile
+constexpr uint32_t kTile = 1u << kTileShift;   // 32 KiB of LDS in pass 2
+constexpr int kStageEntries = 8960;            // pass-1 LDS staging (70 KiB)
+
+struct Entry {
+  float v;
+  uint32_t gb;  // flat bucket index j*c + bucket
+};
+
+__device__ __forceinline__ float load_v(const float* vec, const float* wvec,
+                                        float scale, float wscale, uint32_t i) {
+  float v = scale * vec[i];
+  if (wvec != nullptr) v += wscale * wvec[i];
+  return v;
+}
+
+// ------------------------------------------------------------ direct encode
+__global__ void __launch_bounds__(256)
+cs_encode_direct_kernel(float* __restrict__ table, const float* __restrict__ vec,
+                        const float* __restrict__ wvec, float scale, float wscale,
+                        HashArgs h, SketchGeom g, const int32_t* __restrict__ blk_off,
+                        const float* __restrict__ blk_sign) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < g.d; i += stride) {
+    float v = load_v(vec, wvec, scale, wscale, i);
+    if (v == 0.f) continue;  // sparse inputs: nothing to add
+    for (uint32_t j = 0; j < g.r; ++j) {
+      uint32_t bk;
+      float s;
+      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
+                 blk_sign + j * g.num_blocks, &bk, &s);
+      atomicAdd(table + static_cast<size_t>(j) * g.c + bk, s * v);
+    }
+  }
+}
+
+// ------------------------------------------------------- binned encode, p1
+// scratch layout: [fill: num_tiles u32, padded to 256 B][entries: num_tiles * cap]
+__global__ void __launch_bounds__(256)
+cs_bin_kernel(float* __restrict__ table, const float* __restrict__ vec,
+              const float* __restrict__ wvec, float scale, float wscale,
+              HashArgs h, SketchGeom g, const int32_t* __restrict__ blk_off,
+              const float* __restrict__ blk_sign, uint32_t* __restrict__ fill,
+              Entry* __restrict__ entries, uint32_t num_tiles, uint32_t cap,
+              uint32_t chunk) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // carve: staging[kStageEntries] | tsum[256] | cnt | off | gbase  (num_tiles each)
+  Entry* stage = reinterpret_cast<Entry*>(smem);
+  uint32_t* tsum = reinterpret_cast<uint32_t*>(stage + kStageEntries);
+  uint32_t* cnt = tsum + 256;
+  uint32_t* off = cnt + num_tiles;
+  uint32_t* gbase = off + num_tiles;
+
+  const uint32_t i0 = blockIdx.x * chunk;
+  const uint32_t i1 = min(g.d, i0 + chunk);
+  for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) cnt[t] = 0;
+  __syncthreads();
+
+  // phase A: count entries per tile
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    float v = load_v(vec, wvec, scale, wscale, i);
+    if (v == 0.f) continue;
+    for (uint32_t j = 0; j < g.r; ++j) {
+      uint32_t bk;
+      float s;
+      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
+                 blk_sign + j * g.num_blocks, &bk, &s);
+      uint32_t gb = j * g.c + bk;
+      atomicAdd(cnt + (gb >> kTileShift), 1u);
+    }
+  }
+  __syncthreads();
+
+  // exclusive scan of cnt -> off (serial per thread over a contiguous run of
+  // tiles, then a scan over the 256 thread totals in LDS)
+  const uint32_t per = (num_tiles + blockDim.x - 1) / blockDim.x;
+  const uint32_t t0 = threadIdx.x * per;
+  const uint32_t t1 = min(num_tiles, t0 + per);
+  uint32_t acc = 0;
+  for (uint32_t t = t0; t < t1; ++t) acc += cnt[t];
+  tsum[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < blockDim.x; ++k) {
+      uint32_t x = tsum[k];
+      tsum[k] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  acc = tsum[threadIdx.x];
+  for (uint32_t t = t0; t < t1; ++t) {
+    off[t] = acc;
+    uint32_t c = cnt[t];
+    acc += c;
+    // reserve this block's contiguous run inside the tile's segment
+    gbase[t] = c ? atomicAdd(fill + t, c) : 0u;
+    cnt[t] = off[t];  // reuse as insertion cursor
+  }
+  __syncthreads();
+
+  // phase B: counting-sort the entries into LDS staging
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    float v = load_v(vec, wvec, scale, wscale, i);
+    if (v == 0.f) continue;
+    for (uint32_t j = 0; j < g.r; ++j) {
+      uint32_t bk;
+      float s;
+      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
+                 blk_sign + j * g.num_blocks, &bk, &s);
+      uint32_t gb = j * g.c + bk;
+      uint32_t pos = atomicAdd(cnt + (gb >> kTileShift), 1u);
+      stage[pos] = Entry{s * v, gb};
+    }
+  }
+  __syncthreads();
+
+  // phase C: stream the sorted entries out (consecutive threads write
+  // consecutive slots of one tile segment).  After phase B the cursor of the
+  // last tile equals the block's total entry count.
+  const uint32_t total = cnt[num_tiles - 1];
+  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
+    Entry en = stage[e];
+    uint32_t t = en.gb >> kTileShift;
+    uint32_t slot = gbase[t] + (e - off[t]);
+    if (slot < cap) {
+      entries[static_cast<size_t>(t) * cap + slot] = en;
+    } else {
+      // segment overflow (never expected: cap has >20% headroom): add directly
+      atomicAdd(table + en.gb, en.v);
+    }
+  }
+}
+
+// ------------------------------------------------------- binned encode, p2
+__global__ void __launch_bounds__(512)
+cs_accum_kernel(float* __restrict__ table, uint32_t* __restrict__ fill,
+                const Entry* __restrict__ entries, uint32_t cap, uint32_t total_buckets) {
+  __shared__ float tile[kTile];
+  __shared__ uint32_t n_sh;
+  const uint32_t t = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < kTile; b += blockDim.x) tile[b] = 0.f;
+  if (threadIdx.x == 0) n_sh = min(fill[t], cap);
+  __syncthreads();
+  const uint32_t n = n_sh;
+  const Entry* seg = entries + static_cast<size_t>(t) * cap;
+  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+    Entry en = seg[e];
+    atomicAdd(tile + (en.gb & (kTile - 1)), en.v);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) fill[t] = 0;  // re-arm for the next encode
+  const uint32_t base = t << kTileShift;
+  for (uint32_t b = threadIdx.x; b < kTile; b += blockDim.x) {
+    uint32_t gb = base + b;
+    float v = tile[b];
+    if (gb < total_buckets && v != 0.f) table[gb] += v;
+  }
+}
+
+// -------------------------------------------------------------------- query
+// Lower median (torch.median convention, which CSVec relies on) of the first
+// r values.  Branch-free odd-even transposition network over a statically
+// indexed register array: unused slots are +inf so they sort to the end.
+// R > 0 fixes r at compile time (R = 5 -> 10 compare-exchanges).
+template <int R>
+__device__ __forceinline__ float lower_median(float (&v)[kMaxRows], int r) {
+  constexpr int N = R > 0 ? R : kMaxRows;
+  if (R == 0) {
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+      if (q >= r) v[q] = __builtin_huge_valf();
+  }
+#pragma unroll
+  for (int pass = 0; pass < N; ++pass) {
+#pragma unroll
+    for (int q = pass & 1; q + 1 < N; q += 2) {
+      float a = v[q], b = v[q + 1];
+      v[q] = fminf(a, b);
+      v[q + 1] = fmaxf(a, b);
+    }
+  }
+  if (R > 0) return v[(N - 1) / 2];
+  const int m = (r - 1) / 2;
+  float res = v[0];
+#pragma unroll
+  for (int q = 0; q < N; ++q)
+    if (q == m) res = v[q];
+  return res;
+}
+
+template <int R>
+__global__ void __launch_bounds__(256)
+cs_query_kernel(const float* __restrict__ table, float* __restrict__ est, HashArgs h,
+                SketchGeom g, const int32_t* __restrict__ blk_off,
+                const float* __restrict__ blk_sign) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < g.d; i += stride) {
+    float v[kMaxRows];
+    const int r = R > 0 ? R : static_cast<int>(g.r);
+#pragma unroll
+    for (int j = 0; j < (R > 0 ? R : kMaxRows); ++j) {
+      v[j] = 0.f;
+      if (j >= r) continue;
+      uint32_t bk;
+      float s;
+      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
+                 blk_sign + j * g.num_blocks, &bk, &s);
+      v[j] = s * table[static_cast<size_t>(j) * g.c + bk];
+    }
+    est[i] = lower_median<R>(v, r);
+  }
+}
+
+// ------------------------------------------------------------- zero buckets
+__global__ void __launch_bounds__(256)
+cs_zero_kernel(float* __restrict__ t1, float* __restrict__ t2,
+               const int64_t* __restrict__ idx, const float* __restrict__ vals,
+               int64_t k, HashArgs h, SketchGeom g, const int32_t* __restrict__ blk_off,
+               const float* __restrict__ blk_sign) {
+  int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (q >= k) return;
+  if (vals != nullptr && vals[q] == 0.f) return;  // S(delta) has no mass here
+  uint32_t i = static_cast<uint32_t>(idx[q]);
+  for (uint32_t j = 0; j < g.r; ++j) {
+    uint32_t bk;
+    float s;
+    hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
+               blk_sign + j * g.num_blocks, &bk, &s);
+    size_t cell = static_cast<size_t>(j) * g.c + bk;
+    t1[cell] = 0.f;
+    if (t2 != nullptr) t2[cell] = 0.f;
+  }
+}
+
+// -------------------------------------------------------------- l2estimate
+__global__ void __launch_bounds__(256)
+row_sqsum_kernel(const float* __restrict__ table, int64_t c, float* __restrict__ partial) {
+  // grid (nb, r): partial[row * nb + blk]
+  const int row = blockIdx.y;
+  const float* t = table + row * c;
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < c;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float x = t[i];
+    acc += x * x;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o);
+  __shared__ float ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[row * gridDim.x + blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void l2est_final_kernel(const float* __restrict__ partial, int r, int nb,
+                                   float* __restrict__ out) {
+  // tiny: one thread per row, then thread 0 takes the lower median
+  __shared__ float rows[kMaxRows];
+  if (threadIdx.x < r) {
+    float acc = 0.f;
+    for (int b = 0; b < nb; ++b) acc += partial[threadIdx.x * nb + b];
+    rows[threadIdx.x] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v[kMaxRows];
+#pragma unroll
+    for (int j = 0; j < kMaxRows; ++j) v[j] = j < r ? rows[j] : 0.f;
+    out[0] = sqrtf(lower_median<0>(v, r));
+  }
+}
+
+HashArgs to_args(const RowHashes& h, const SketchGeom& g) {
+  HashArgs a;
+  for (uint32_t j = 0; j < g.r && j < static_cast<uint32_t>(kMaxRows); ++j) a.row[j] = h.row[j];
+  return a;
+}
+
+int grid_for(int64_t n, int block, int max_blocks) {
+  int64_t b = (n + block - 1) / block;
+  if (b < 1) b = 1;
+  return static_cast<int>(b < max_blocks ? b : max_blocks);
+}
+
+}  // namespace
+
+void launch_cs_encode(float* table, const float* vec, const float* wvec, float scale,
+                      float wscale, const RowHashes& h, const SketchGeom& g,
+                      const int32_t* blk_off, const float* blk_sign, hipStream_t stream) {
+  if (g.d == 0) return;
+  hipLaunchKernelGGL(cs_encode_direct_kernel, dim3(grid_for(g.d, 256, 8192)), dim3(256), 0,
+                     stream, table, vec, wvec, scale, wscale, to_args(h, g), g, blk_off,
+                     blk_sign);
+}
+
+BinPlan plan_cs_encode_binned(const SketchGeom& g) {
+  BinPlan p;
+  p.tile = kTile;
+  int64_t total = static_cast<int64_t>(g.r) * g.c;
+  p.num_tiles = (total + kTile - 1) / kTile;
+  int64_t chunk = (kStageEntries / static_cast<int64_t>(g.r)) / 64 * 64;
+  if (chunk < 64) chunk = 64;
+  p.chunk = chunk;
+  p.num_chunks = (static_cast<int64_t>(g.d) + chunk - 1) / chunk;
+  // expected entries per tile = d * r / num_tiles; 25% + 4096 headroom
+  double expect = static_cast<double>(g.d) * g.r / static_cast<double>(p.num_tiles);
+  p.cap = static_cast<int64_t>(expect * 1.25) + 4096;
+  return p;
+}
+
+int64_t cs_encode_binned_scratch_bytes(const BinPlan& p) {
+  int64_t fill_bytes = ((p.num_tiles * 4 + 255) / 256) * 256;
+  return fill_bytes + p.num_tiles * p.cap * static_cast<int64_t>(sizeof(Entry));
+}
+
+void launch_cs_encode_binned(float* table, const float* vec, const float* wvec, float scale,
+                             float wscale, const RowHashes& h, const SketchGeom& g,
+                             const int32_t* blk_off, const float* blk_sign, const BinPlan& p,
+                             void* scratch, hipStream_t stream) {
+  if (g.d == 0) return;
+  uint32_t* fill = reinterpret_cast<uint32_t*>(scratch);
+  int64_t fill_bytes = ((p.num_tiles * 4 + 255) / 256) * 256;
+  Entry* entries = reinterpret_cast<Entry*>(reinterpret_cast<char*>(scratch) + fill_bytes);
+  size_t lds = kStageEntries * sizeof(Entry) + (256 + 3 * p.num_tiles) * sizeof(uint32_t);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(cs_bin_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  HashArgs a = to_args(h, g);
+  hipLaunchKernelGGL(cs_bin_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256), lds,
+                     stream, table, vec, wvec, scale, wscale, a, g, blk_off, blk_sign, fill,
+                     entries, static_cast<uint32_t>(p.num_tiles), static_cast<uint32_t>(p.cap),
+                     static_cast<uint32_t>(p.chunk));
+  hipLaunchKernelGGL(cs_accum_kernel, dim3(static_cast<uint32_t>(p.num_tiles)), dim3(512), 0,
+                     stream, table, fill, entries, static_cast<uint32_t>(p.cap),
+                     static_cast<uint32_t>(static_cast<int64_t>(g.r) * g.c));
+}
+
+void launch_cs_query(const float* table, float* est, const RowHashes& h, const SketchGeom& g,
+                     const int32_t* blk_off, const float* blk_sign, hipStream_t stream) {
+  if (g.d == 0) return;
+  dim3 grid(grid_for(g.d, 256, 16384));
+  HashArgs a = to_args(h, g);
+  switch (g.r) {
+    case 1: hipLaunchKernelGGL(cs_query_kernel<1>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    case 3: hipLaunchKernelGGL(cs_query_kernel<3>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    case 5: hipLaunchKernelGGL(cs_query_kernel<5>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    case 7: hipLaunchKernelGGL(cs_query_kernel<7>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    default: hipLaunchKernelGGL(cs_query_kernel<0>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+  }
+}
+
+void launch_cs_zero_buckets(float* t1, float* t2, const int64_t* idx, const float* vals,
+                            int64_t k, const RowHashes& h, const SketchGeom& g,
+                            const int32_t* blk_off, const float* blk_sign, hipStream_t stream) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(cs_zero_kernel, dim3((k + 255) / 256), dim3(256), 0, stream, t1, t2, idx,
+                     vals, k, to_args(h, g), g, blk_off, blk_sign);
+}
+
+void launch_cs_l2estimate(const float* table, int r, int64_t c, float* partial, float* out,
+                          hipStream_t stream) {
+  const int nb = 256;
+  hipLaunchKernelGGL(row_sqsum_kernel, dim3(nb, r), dim3(256), 0, stream, table, c, partial);
+  hipLaunchKernelGGL(l2est_final_kernel, dim3(1), dim3(64), 0, stream, partial, r, nb, out);
+}
+
+}  // namespace commeff

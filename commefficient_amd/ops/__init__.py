@@ -1,0 +1,77 @@
+"""Native codec ops (HIP gfx950 + C++ CPU): Count Sketch, deterministic top-k,
+fused server/client state updates, DP clip+noise, download accounting and
+on-device augmentation.  See ``csrc/`` for the kernels."""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .._ext import ops as _ops
+from .sketch import CSVec, make_hashes
+
+__all__ = ["CSVec", "make_hashes", "topk_abs", "topk_dense", "momentum_ef", "sparse_apply",
+           "dense_apply", "count_ge", "axpby", "l2norm", "clip_noise", "client_state",
+           "zero_at", "scatter_dense", "augment_u8_nhwc"]
+
+ERROR_MODE = {"none": 0, "virtual": 1, "local": 2}
+
+
+def topk_abs(x: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Deterministic magnitude top-k: (idx ascending int64, vals=x[idx]); ties -> lower index."""
+    return _ops().topk_abs(x.reshape(-1).contiguous(), int(k))
+
+
+def topk_dense(x: torch.Tensor, k: int) -> torch.Tensor:
+    """Dense result of the reference ``_topk`` (utils.py:232-252): zeros except the top-k."""
+    if x.dim() == 2:
+        return torch.stack([topk_dense(row, k) for row in x])
+    idx, vals = topk_abs(x, k)
+    return _ops().scatter_dense(idx, vals, x.numel()).view_as(x)
+
+
+def momentum_ef(V: torch.Tensor, E: Optional[torch.Tensor], G: torch.Tensor, rho: float,
+                gscale: float = 1.0, error_type: str = "none") -> None:
+    """V = rho*V + gscale*G ; virtual: E += V ; local: E = V."""
+    _ops().momentum_ef(V, E, G, float(rho), float(gscale), ERROR_MODE[error_type])
+
+
+def sparse_apply(w, idx, vals, lr, lr_vec=None, last_mod=None, round_idx: int = 0):
+    _ops().sparse_apply(w, idx, vals, float(lr), lr_vec, last_mod, int(round_idx))
+
+
+def dense_apply(w, delta, lr, lr_vec=None, last_mod=None, round_idx: int = 0):
+    _ops().dense_apply(w, delta, float(lr), lr_vec, last_mod, int(round_idx))
+
+
+def count_ge(last_mod: torch.Tensor, thr: torch.Tensor) -> torch.Tensor:
+    return _ops().count_ge(last_mod, thr)
+
+
+def axpby(out, a, alpha, b=None, beta=0.0):
+    _ops().axpby(out, a, float(alpha), b, float(beta))
+
+
+def l2norm(x: torch.Tensor) -> torch.Tensor:
+    return _ops().l2norm(x.reshape(-1).contiguous())
+
+
+def clip_noise(x, norm=None, clip=0.0, noise_std=0.0, seed=0, offset=0):
+    _ops().clip_noise(x, norm, float(clip), float(noise_std), int(seed), int(offset))
+
+
+def client_state(g, u=None, e=None, rho=0.0):
+    _ops().client_state(g, u, e, float(rho))
+
+
+def zero_at(idx, a=None, b=None, c=None):
+    _ops().zero_at(a, b, c, idx)
+
+
+def scatter_dense(idx, vals, n):
+    return _ops().scatter_dense(idx, vals, int(n))
+
+
+def augment_u8_nhwc(data, idx, pad, flip, mean, inv_std, seed, out_bf16=True):
+    return _ops().augment_u8_nhwc(data, idx, int(pad), bool(flip), mean, inv_std, int(seed),
+                                  bool(out_bf16))

@@ -1,0 +1,135 @@
+"""Count Sketch backed by the native ``commeff`` ops.
+
+API-compatible with the ``csvec.CSVec`` object the reference uses
+(SURVEY.md §2.4 X1): ``CSVec(d, c, r, device, numBlocks)``, ``accumulateVec``,
+``accumulateTable``, ``unSketch(k)``, ``zero()``, ``l2estimate()``, ``.table``
+and ``/``.  Call sites in the reference:
+/root/reference/CommEfficient/fed_worker.py:313-320,
+/root/reference/CommEfficient/fed_aggregator.py:464-467,584-595,
+/root/reference/CommEfficient/utils.py:305-313.
+
+Differences by design (MI355X-first):
+* hashes are recomputed inside the kernels from 6 coefficients per row
+  (``hashes`` is a tiny CPU int64 tensor), so no r x d index tables exist;
+* ``unSketch`` returns the dense vector like CSVec, while ``unsketch_sparse``
+  returns the ``(idx, vals)`` pair straight from the deterministic radix
+  select, which is what the server step uses;
+* ``zero_heavy_hitters`` zeroes the r cells of each recovered coordinate
+  directly instead of re-sketching the update and taking ``nonzero()``
+  (identical except when two heavy hitters cancel exactly in a bucket).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from .._ext import ops
+
+MERSENNE_P = (1 << 31) - 1
+
+
+def make_hashes(r: int, c: int, num_blocks: int = 1, seed: int = 42):
+    """Deterministic hash coefficients (identical on every rank for one seed).
+
+    Returns ``(hashes[r,6] int64 cpu, blk_off[r,nb] int32 cpu, blk_sign[r,nb] f32 cpu)``.
+    """
+    rng = np.random.RandomState(seed)
+    a = rng.randint(1, MERSENNE_P, size=(r, 1), dtype=np.int64)
+    rest = rng.randint(0, MERSENNE_P, size=(r, 5), dtype=np.int64)
+    hashes = torch.from_numpy(np.concatenate([a, rest], axis=1))
+    nb = max(1, int(num_blocks))
+    blk_off = torch.from_numpy(rng.randint(0, c, size=(r, nb)).astype(np.int32))
+    blk_sign = torch.from_numpy(
+        (rng.randint(0, 2, size=(r, nb)) * 2 - 1).astype(np.float32))
+    return hashes, blk_off, blk_sign
+
+
+class CSVec:
+    """Count Sketch of a d-dimensional vector into an r x c fp32 table."""
+
+    def __init__(self, d: int, c: int, r: int, device="cpu", numBlocks: int = 1,
+                 seed: int = 42, table: Optional[torch.Tensor] = None,
+                 _hashes=None):
+        self.d = int(d)
+        self.c = int(c)
+        self.r = int(r)
+        self.device = torch.device(device)
+        self.numBlocks = max(1, int(numBlocks))
+        self.seed = seed
+        if _hashes is None:
+            h, bo, bs = make_hashes(self.r, self.c, self.numBlocks, seed)
+            bo = bo.to(self.device)
+            bs = bs.to(self.device)
+            _hashes = (h, bo, bs)
+        self.hashes, self.blk_off, self.blk_sign = _hashes
+        if table is None:
+            table = torch.zeros(self.r, self.c, device=self.device, dtype=torch.float32)
+        self.table = table
+        self._scratch = None
+
+    # -- construction helpers -------------------------------------------------
+    def like(self, table: Optional[torch.Tensor] = None) -> "CSVec":
+        """A sketch with the same hashes (cheap: shares the coefficient tensors)."""
+        return CSVec(self.d, self.c, self.r, self.device, self.numBlocks, self.seed,
+                     table=table, _hashes=(self.hashes, self.blk_off, self.blk_sign))
+
+    def _binned_scratch(self) -> Optional[torch.Tensor]:
+        if self.device.type != "cuda":
+            return None
+        if self._scratch is None:
+            nbytes = ops().binned_scratch_bytes(self.d, self.r, self.c, self.numBlocks)
+            self._scratch = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        return self._scratch
+
+    # -- CSVec API --------------------------------------------------------------
+    def zero(self):
+        self.table.zero_()
+
+    def accumulateVec(self, vec: torch.Tensor, scale: float = 1.0,
+                      wvec: Optional[torch.Tensor] = None, wscale: float = 0.0,
+                      dense: bool = True):
+        """table += S(scale*vec + wscale*wvec).  ``dense=False`` uses the
+        direct-atomic kernel (best for sparse vectors)."""
+        assert vec.numel() == self.d, (vec.numel(), self.d)
+        scratch = self._binned_scratch() if dense else None
+        ops().cs_encode(self.table, vec.reshape(-1), self.hashes, self.blk_off, self.blk_sign,
+                        self.numBlocks, float(scale), wvec, float(wscale), scratch)
+
+    def accumulateTable(self, table: torch.Tensor):
+        self.table.add_(table.view(self.r, self.c))
+
+    def query(self) -> torch.Tensor:
+        """Median-of-rows estimate of every coordinate (dense, length d)."""
+        return ops().cs_query(self.table, self.hashes, self.blk_off, self.blk_sign,
+                              self.numBlocks, self.d)
+
+    def unsketch_sparse(self, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        est = self.query()
+        return ops().topk_abs(est, int(k))
+
+    def unSketch(self, k: int) -> torch.Tensor:
+        idx, vals = self.unsketch_sparse(k)
+        return ops().scatter_dense(idx, vals, self.d)
+
+    def zero_heavy_hitters(self, idx: torch.Tensor, vals: Optional[torch.Tensor],
+                           other: Optional[torch.Tensor] = None):
+        """Zero cells (j, h_j(i)) of this table (and ``other``) for recovered
+        coordinates i with nonzero value -- the reference's
+        ``nz = S(delta).nonzero(); table[nz] = 0``."""
+        ops().cs_zero_buckets(self.table, other, idx, vals, self.hashes, self.blk_off,
+                              self.blk_sign, self.numBlocks, self.d)
+
+    def l2estimate(self) -> torch.Tensor:
+        return ops().cs_l2estimate(self.table)
+
+    def __truediv__(self, other):
+        return self.like(self.table / float(other))
+
+    def __iadd__(self, other):
+        if isinstance(other, CSVec):
+            self.table += other.table
+        else:
+            self.table += other
+        return self

@@ -1,0 +1,243 @@
+"""Numerics of the native codec ops (CPU C++ backend and HIP gfx950 backend)
+against the pure-torch oracles in tests/oracle.py."""
+import pytest
+import torch
+
+from commefficient_amd import ops
+from commefficient_amd.ops import CSVec, make_hashes
+from oracle import OracleSketch, topk_oracle
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _sketch_pair(d, c, r, nb, device, seed=42):
+    sk = CSVec(d, c, r, device=device, numBlocks=nb, seed=seed)
+    h, bo, bs = make_hashes(r, c, nb, seed)
+    orc = OracleSketch(h, bo, bs, d, c, r, nb)
+    return sk, orc
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("d,c,r,nb", [(1000, 37, 5, 1), (5000, 101, 3, 4), (777, 50, 1, 1),
+                                      (20000, 900, 5, 20), (3000, 64, 4, 1)])
+def test_encode_matches_oracle(device, d, c, r, nb):
+    torch.manual_seed(0)
+    sk, orc = _sketch_pair(d, c, r, nb, device)
+    v = torch.randn(d)
+    sk.accumulateVec(v.to(device))
+    orc.accumulate_vec(v)
+    torch.testing.assert_close(sk.table.cpu().double(), orc.table, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_encode_direct_and_scaled_weight_term(device):
+    torch.manual_seed(1)
+    d, c, r = 4000, 211, 5
+    sk, orc = _sketch_pair(d, c, r, 1, device)
+    g, w = torch.randn(d), torch.randn(d)
+    sk.accumulateVec(g.to(device), scale=3.0, wvec=w.to(device), wscale=0.25, dense=False)
+    orc.accumulate_vec(3.0 * g + 0.25 * w)
+    torch.testing.assert_close(sk.table.cpu().double(), orc.table, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_sketch_linearity(device):
+    torch.manual_seed(2)
+    d, c, r = 3000, 97, 5
+    a, b = torch.randn(d), torch.randn(d)
+    s1 = CSVec(d, c, r, device=device)
+    s2 = s1.like()
+    s3 = s1.like()
+    s1.accumulateVec(a.to(device))
+    s2.accumulateVec(b.to(device))
+    s3.accumulateVec((a + b).to(device))
+    torch.testing.assert_close(s1.table + s2.table, s3.table, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("r,nb", [(5, 1), (3, 7), (4, 1), (1, 1), (16, 2)])
+def test_query_matches_oracle(device, r, nb):
+    torch.manual_seed(3)
+    d, c = 5000, 257
+    sk, orc = _sketch_pair(d, c, r, nb, device)
+    v = torch.randn(d)
+    sk.accumulateVec(v.to(device))
+    orc.accumulate_vec(v)
+    est = sk.query().cpu().double()
+    torch.testing.assert_close(est, orc.query(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_heavy_hitter_recovery(device):
+    torch.manual_seed(4)
+    d, c, r, k = 50000, 2000, 5, 20
+    v = torch.randn(d) * 0.01
+    hh = torch.randperm(d)[:k]
+    v[hh] = torch.randn(k).sign() * (10 + torch.rand(k))
+    sk = CSVec(d, c, r, device=device, numBlocks=4)
+    sk.accumulateVec(v.to(device))
+    idx, vals = sk.unsketch_sparse(k)
+    assert set(idx.cpu().tolist()) == set(hh.tolist())
+    torch.testing.assert_close(vals.cpu(), v[idx.cpu()], rtol=0, atol=0.2)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_l2estimate(device):
+    torch.manual_seed(5)
+    d, c, r = 5000, 300, 5
+    sk, orc = _sketch_pair(d, c, r, 1, device)
+    v = torch.randn(d)
+    sk.accumulateVec(v.to(device))
+    orc.accumulate_vec(v)
+    torch.testing.assert_close(sk.l2estimate().cpu().double(), orc.l2estimate(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_zero_heavy_hitters_matches_nonzero_mask(device):
+    """zero_heavy_hitters == reference `nz = S(delta).nonzero(); T[nz] = 0`."""
+    torch.manual_seed(6)
+    d, c, r, k = 4000, 150, 5, 30
+    sk = CSVec(d, c, r, device=device)
+    sk.accumulateVec(torch.randn(d).to(device))
+    other = torch.randn(r, c).to(device)
+    idx, vals = sk.unsketch_sparse(k)
+    # reference semantics via re-sketching the sparse update
+    delta = torch.zeros(d)
+    delta[idx.cpu()] = vals.cpu()
+    resk = sk.like()
+    resk.accumulateVec(delta.to(device), dense=False)
+    mask = resk.table.cpu() != 0
+    exp_t = sk.table.cpu().clone()
+    exp_t[mask] = 0
+    exp_o = other.cpu().clone()
+    exp_o[mask] = 0
+    sk.zero_heavy_hitters(idx, vals, other)
+    torch.testing.assert_close(sk.table.cpu(), exp_t)
+    torch.testing.assert_close(other.cpu(), exp_o)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("n,k", [(1000, 10), (100000, 5000), (12345, 1), (4096, 4095),
+                                 (50, 50), (300000, 50000)])
+def test_topk_matches_oracle(device, n, k):
+    torch.manual_seed(7)
+    x = torch.randn(n)
+    idx, vals = ops.topk_abs(x.to(device), k)
+    if n <= 20000:
+        ei, ev = topk_oracle(x, k)
+        assert torch.equal(idx.cpu(), ei)
+        assert torch.equal(vals.cpu(), ev)
+    else:
+        thr = x.abs().sort(descending=True).values[k - 1]
+        assert idx.numel() == k
+        assert torch.all(idx.cpu()[1:] > idx.cpu()[:-1])
+        assert torch.all(x[idx.cpu()].abs() >= thr)
+        assert torch.equal(vals.cpu(), x[idx.cpu()])
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_topk_ties_lower_index_wins(device):
+    x = torch.tensor([1.0, -3.0, 3.0, 2.0, -3.0, 0.5, 3.0, 1.0])
+    idx, vals = ops.topk_abs(x.to(device), 2)
+    assert idx.cpu().tolist() == [1, 2]
+    idx, vals = ops.topk_abs(x.to(device), 4)
+    assert idx.cpu().tolist() == [1, 2, 4, 6]
+    # many identical values (sparse vectors are mostly zeros)
+    z = torch.zeros(10000)
+    z[[5, 500, 9000]] = torch.tensor([1.0, -2.0, 3.0])
+    idx, vals = ops.topk_abs(z.to(device), 10)
+    assert idx.cpu().tolist() == [0, 1, 2, 3, 4, 5, 6, 7, 500, 9000]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_topk_dense_matches_reference_topk(device):
+    torch.manual_seed(8)
+    x = torch.randn(5000)
+    out = ops.topk_dense(x.to(device), 100).cpu()
+    ref = torch.zeros_like(x)
+    ti = torch.topk(x ** 2, 100, sorted=False).indices
+    ref[ti] = x[ti]
+    torch.testing.assert_close(out, ref)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("mode", ["none", "virtual", "local"])
+def test_momentum_ef(device, mode):
+    torch.manual_seed(9)
+    n = 10003
+    V, E, G = torch.randn(n), torch.randn(n), torch.randn(n)
+    Vd, Ed, Gd = V.clone().to(device), E.clone().to(device), G.clone().to(device)
+    ops.momentum_ef(Vd, Ed, Gd, 0.9, 0.5, mode)
+    V2 = 0.9 * V + 0.5 * G
+    E2 = E + V2 if mode == "virtual" else (V2 if mode == "local" else E)
+    torch.testing.assert_close(Vd.cpu(), V2)
+    torch.testing.assert_close(Ed.cpu(), E2)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_apply_and_count(device):
+    torch.manual_seed(10)
+    n = 5000
+    w = torch.randn(n)
+    wd = w.clone().to(device)
+    lm = torch.full((n,), -1, dtype=torch.int32, device=device)
+    idx = torch.tensor([3, 10, 4000], dtype=torch.int64)
+    vals = torch.tensor([1.0, 0.0, -2.0])
+    ops.sparse_apply(wd, idx.to(device), vals.to(device), 0.1, None, lm, 0)
+    exp = w.clone()
+    exp[idx] -= 0.1 * vals
+    torch.testing.assert_close(wd.cpu(), exp)
+    assert (lm.cpu() == 0).sum().item() == 2  # the 0-valued update changed nothing
+    delta = torch.zeros(n)
+    delta[:100] = 1.0
+    lrv = torch.full((n,), 0.5)
+    ops.dense_apply(wd, delta.to(device), 0.0, lrv.to(device), lm, 1)
+    exp -= 0.5 * delta
+    torch.testing.assert_close(wd.cpu(), exp)
+    cnt = ops.count_ge(lm, torch.tensor([-1, 0, 1, 2], dtype=torch.int32))
+    # last_mod: 100 coords == 1 (incl. idx 3), idx 4000 == 0, rest -1
+    assert cnt.cpu().tolist() == [n, 101, 100, 0]
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_l2norm_clip_noise(device):
+    torch.manual_seed(11)
+    x = torch.randn(20000)
+    xd = x.clone().to(device)
+    nrm = ops.l2norm(xd)
+    torch.testing.assert_close(nrm.cpu(), x.norm(), rtol=1e-5, atol=1e-5)
+    ops.clip_noise(xd, nrm, clip=1.0, noise_std=0.0)
+    torch.testing.assert_close(xd.cpu(), x / x.norm(), rtol=1e-5, atol=1e-6)
+    z = torch.zeros(200000, device=device)
+    ops.clip_noise(z, None, 0.0, 2.0, seed=123, offset=0)
+    assert abs(z.mean().item()) < 0.05 and abs(z.std().item() - 2.0) < 0.05
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_client_state(device):
+    torch.manual_seed(12)
+    n = 3001
+    g, u, e = torch.randn(n), torch.randn(n), torch.randn(n)
+    gd, ud, ed = g.clone().to(device), u.clone().to(device), e.clone().to(device)
+    ops.client_state(gd, ud, ed, 0.9)
+    u2 = 0.9 * u + g
+    torch.testing.assert_close(ud.cpu(), u2)
+    torch.testing.assert_close(ed.cpu(), e + u2)
+    ops.zero_at(torch.tensor([0, 5]).to(device), ud, ed)
+    assert ud.cpu()[0] == 0 and ed.cpu()[5] == 0
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_augment_shapes_and_identity(device):
+    torch.manual_seed(13)
+    data = torch.randint(0, 256, (10, 8, 8, 3), dtype=torch.uint8)
+    idx = torch.tensor([3, 7, 0])
+    mean = torch.tensor([0.1, 0.2, 0.3])
+    inv = torch.tensor([2.0, 3.0, 4.0])
+    out = ops.augment_u8_nhwc(data.to(device), idx.to(device), 0, False, mean, inv, 0,
+                              out_bf16=False).cpu()
+    assert out.shape == (3, 3, 8, 8)
+    ref = (data[idx].permute(0, 3, 1, 2).float() / 255 - mean.view(1, 3, 1, 1)) * inv.view(1, 3, 1, 1)
+    torch.testing.assert_close(out, ref, rtol=1e-2, atol=2e-2)
+    out2 = ops.augment_u8_nhwc(data.to(device), idx.to(device), 4, True, mean, inv, 99).float().cpu()
+    assert out2.shape == (3, 3, 8, 8) and torch.isfinite(out2).all()
