@@ -1,0 +1,150 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json): images/s + bytes/step of ResNet-9 on
+CIFAR-10-shaped data with FetchSGD (Count Sketch, k=50,000, 5 x 500,000,
+virtual momentum 0.9, virtual error, no local momentum) on 1/2/4/8 MI355X.
+
+One "step" = one federated round: on-device batch assembly + augmentation,
+forward/backward of this rank's clients (bf16), Count-Sketch encode, ONE RCCL
+all-reduce of the 10 MB table (+ metrics), and the replicated server update
+(momentum/error, median unsketch, top-k, heavy-hitter zeroing, weight apply,
+download accounting).  Nothing is skipped in the timed region.
+
+Weak scaling: every GPU runs --clients-per-gpu clients of --client-size
+images per round (default 100 x 5 = 500 images/GPU/round; 10,000 non-iid
+clients of 5 images each as in the FetchSGD CIFAR-10 setup).  Synthetic data
+of CIFAR shape, random-init weights.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+METRIC = "images/sec + bytes/step, ResNet-9 CIFAR-10 FetchSGD at 1/2/4/8 MI355X"
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--clients-per-gpu", type=int, default=100)
+    p.add_argument("--client-size", type=int, default=5)
+    p.add_argument("--num-clients", type=int, default=10000)
+    p.add_argument("--encode", default="binned", choices=["binned", "direct"])
+    p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
+    b = p.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != b.gpus:
+        if b.gpus > 1 and world == 1:
+            sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.utils.args import parse_args
+    ctx = dist.init("cuda")
+    N = ctx.world_size
+    W = b.clients_per_gpu * N
+    n_train = b.num_clients * b.client_size
+    argv = ["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", str(n_train),
+            "--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
+            "--virtual_momentum", "0.9", "--k", "50000", "--num_rows", "5", "--num_cols", "500000",
+            "--num_blocks", "20", "--num_clients", str(b.num_clients), "--num_workers", str(W),
+            "--local_batch_size", "-1", "--weight_decay", "5e-4", "--dtype", "bf16",
+            "--device", "cuda", "--encode", b.encode, "--seed", "21"]
+    if b.profile:
+        argv += ["--profile_dir", "gpurun_out/bench_profile"]
+    args = parse_args(argv=argv, probe_port=False)
+
+    from commefficient_amd import models
+    from commefficient_amd.data import make_synthetic
+    from commefficient_amd.data.device_loader import DeviceFedLoader
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd.train.losses import cv_loss
+
+    torch.manual_seed(args.seed)
+    np.random.seed(args.seed)
+    ds = make_synthetic("CIFAR10", train=True, num_clients=b.num_clients, size=n_train,
+                        seed=args.seed)
+    loader = DeviceFedLoader(ds, W, -1, ctx.device, seed=args.seed, augment=True, out_bf16=True)
+    model = models.build_model(args, 10)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    fed = FedModel(model, cv_loss, args, num_clients=b.num_clients)
+    fopt = FedOptimizer(opt, args, fed)
+
+    # pre-draw the rounds' client/row index arrays (host sampler), full rounds only
+    rounds = []
+    need = b.warmup + b.steps
+    while len(rounds) < need:
+        for r in loader.sampler:
+            cids = ds.client_of(r)
+            if len(np.unique(cids)) < W:
+                continue
+            rounds.append((cids, ds.data_index(r)))
+            if len(rounds) >= need:
+                break
+
+    def step(i):
+        cids, rows = rounds[i]
+        out = fed(loader.make_batch(cids, rows))
+        fopt.step()
+        return out
+
+    for i in range(b.warmup):
+        out = step(i)
+    torch.cuda.synchronize()
+    first_loss = float(out[0].mean().item())
+    dist.barrier()
+    torch.cuda.synchronize()
+    dl_before = float(fed.accountant.client_download.sum().item())
+    if fed.timer.enabled:
+        fed.timer.summary()
+        fed.timer.totals.clear()
+        fed.timer.counts.clear()
+    t0 = time.perf_counter()
+    for i in range(b.warmup, b.warmup + b.steps):
+        out = step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    elapsed = dist.max_over_ranks(t1 - t0)
+    last_loss = float(out[0].mean().item())
+    dl = (float(fed.accountant.client_download.sum().item()) - dl_before) / b.steps
+    imgs_per_step = W * b.client_size
+    ms = elapsed / b.steps * 1000.0
+    value = imgs_per_step * b.steps / elapsed
+    up_ref = fed.accountant.upload_per_client * W
+    payload = fed.last_round.get("payload_bytes", 0)
+    wire = fed.accountant.wire_bytes_per_rank(payload // 4)
+    phases = fed.timer.summary() if fed.timer.enabled else {}
+    if ctx.is_main:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
+            "steps": b.steps, "warmup": b.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (CIFAR-10 shape, random-init ResNet-9)",
+            "config": {"model": "ResNet9", "global_batch": imgs_per_step, "seq_len": None,
+                       "image_hw": 32, "parallelism": f"dp{N}", "mode": "sketch",
+                       "k": 50000, "num_rows": 5, "num_cols": 500000, "num_blocks": 20,
+                       "clients_per_round": W, "client_size": b.client_size,
+                       "num_clients": b.num_clients, "encode": b.encode},
+            "bytes_per_step": {"upload_ref_accounting": up_ref,
+                               "download_ref_accounting": dl,
+                               "allreduce_payload_per_rank": payload,
+                               "wire_per_rank_ring": wire},
+            "loss_first": round(first_loss, 4), "loss_last": round(last_loss, 4),
+            "phase_ms": {k: round(v, 3) for k, v in phases.items()},
+        }), flush=True)
+    dist.barrier()
+    dist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

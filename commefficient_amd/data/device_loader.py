@@ -1,0 +1,105 @@
+"""Device-resident federated data loading.
+
+The reference builds every batch on the host (PIL decode + torchvision
+transforms per item in a DataLoader) and pickles it to the workers through
+queues (/root/reference/CommEfficient/cv_train.py:254-287,
+fed_aggregator.py:303-307).  On MI355X the whole uint8 image set sits in HBM
+(CIFAR-10: 150 MB of 288 GB) and a round is materialised by ONE kernel that
+gathers the round's rows and applies crop/flip/normalise, writing bf16 NHWC
+(``ops.augment_u8_nhwc``).  Only the rows of the clients assigned to this
+rank are materialised.  The sampler (``FedSampler`` semantics, seeded
+identically on every rank) runs on the host and costs microseconds.
+"""
+from __future__ import annotations
+
+from typing import Iterator, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..parallel.fed_model import RoundBatch
+from .fed_dataset import FedSampler
+
+
+class DeviceImageSource:
+    def __init__(self, dataset, device, augment: bool, pad: int = 4, flip: bool = True,
+                 out_bf16: bool = True):
+        images, targets = dataset.arrays()
+        self.device = torch.device(device)
+        self.data = torch.from_numpy(np.ascontiguousarray(images)).to(self.device)
+        self.targets = torch.from_numpy(np.asarray(targets, dtype=np.int64)).to(self.device)
+        mean = torch.tensor(dataset.mean, dtype=torch.float32)
+        std = torch.tensor(dataset.std, dtype=torch.float32)
+        self.mean = mean.to(self.device)
+        self.inv_std = (1.0 / std).to(self.device)
+        self.augment = augment
+        self.pad = pad if augment else 0
+        self.flip = flip if augment else False
+        self.out_bf16 = out_bf16 and self.device.type == "cuda"
+
+    def gather(self, rows: np.ndarray, seed: int):
+        idx = torch.from_numpy(np.asarray(rows, dtype=np.int64))
+        if self.device.type == "cuda":
+            idx = idx.pin_memory().to(self.device, non_blocking=True)
+        x = ops.augment_u8_nhwc(self.data, idx, self.pad, self.flip, self.mean, self.inv_std,
+                                seed, self.out_bf16)
+        y = self.targets[idx]
+        return x, y
+
+
+class DeviceFedLoader:
+    """Iterates federated training rounds as ``RoundBatch``es."""
+
+    def __init__(self, dataset, num_workers: int, local_batch_size: int, device, seed: int,
+                 augment: bool = True, out_bf16: bool = True, pad: int = 4, flip: bool = True):
+        self.dataset = dataset
+        self.sampler = FedSampler(dataset, num_workers, local_batch_size, seed=seed)
+        self.source = DeviceImageSource(dataset, device, augment, pad=pad, flip=flip,
+                                        out_bf16=out_bf16)
+        self.seed = seed
+        self._round = 0
+
+    def __len__(self):
+        return len(self.dataset)
+
+    def __iter__(self) -> Iterator[RoundBatch]:
+        for r in self.sampler:
+            cids = self.dataset.client_of(r)
+            rows = self.dataset.data_index(r)
+            yield self.make_batch(cids, rows)
+
+    def make_batch(self, cids, rows) -> RoundBatch:
+        rnd_seed = (self.seed * 1000003 + self._round) & 0x7FFFFFFFFFFF
+        self._round += 1
+        src = self.source
+
+        def take(pos, rows=rows, seed=rnd_seed):
+            # seed by round; the kernel further mixes in the batch slot
+            return src.gather(rows[pos], seed * 7 + int(pos[0]) if len(pos) else seed)
+
+        return RoundBatch(cids, take, n_inputs=1)
+
+
+class DeviceValLoader:
+    """Sequential validation batches of ``batch_size`` (client id -1)."""
+
+    def __init__(self, dataset, batch_size: int, device, out_bf16: bool = True):
+        self.dataset = dataset
+        self.batch_size = batch_size
+        self.source = DeviceImageSource(dataset, device, augment=False, out_bf16=out_bf16)
+
+    def __len__(self):
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = len(self.dataset)
+        for s in range(0, n, self.batch_size):
+            rows = np.arange(s, min(n, s + self.batch_size))
+            cids = np.full(len(rows), -1, dtype=np.int64)
+            src = self.source
+
+            def take(pos, rows=rows):
+                return src.gather(rows[pos], 0)
+
+            yield RoundBatch(cids, take, n_inputs=1)

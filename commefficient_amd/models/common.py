@@ -1,0 +1,109 @@
+"""Shared building blocks for the model zoo."""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Mul(nn.Module):
+    """Constant scale (ResNet-9 classifier ×0.125)."""
+
+    def __init__(self, weight: float):
+        super().__init__()
+        self.weight = weight
+
+    def forward(self, x):
+        return x * self.weight
+
+
+class ScalarScale(nn.Module):
+    """Learnable scalar multiplier (Fixup ``scale``)."""
+
+    def __init__(self):
+        super().__init__()
+        self.scale = nn.Parameter(torch.ones(1))
+
+    def forward(self, x):
+        return x * self.scale
+
+
+class ScalarBias(nn.Module):
+    """Learnable scalar bias (Fixup ``bias``)."""
+
+    def __init__(self):
+        super().__init__()
+        self.bias = nn.Parameter(torch.zeros(1))
+
+    def forward(self, x):
+        return x + self.bias
+
+
+class GhostBatchNorm2d(nn.BatchNorm2d):
+    """BatchNorm2d that can normalise G equal-size groups of the batch with
+    their own statistics.
+
+    The engine merges the clients of a round into one forward/backward when
+    that is exact (parallel/fed_model.py).  With BatchNorm, "exact" means each
+    client's examples are normalised with that client's batch statistics, as
+    in the reference where every client runs its own forward
+    (/root/reference/CommEfficient/fed_worker.py:162-176).  ``ghost_groups``
+    is set by the engine for the duration of a merged forward.
+    Running statistics are updated once with the group-averaged moments.
+    """
+
+    ghost_groups: int = 1
+
+    def forward(self, x):
+        G = self.ghost_groups
+        if not self.training or G <= 1:
+            return super().forward(x)
+        N, C = x.shape[0], x.shape[1]
+        assert N % G == 0, "ghost batch norm needs equal client batch sizes"
+        xf = x.float().reshape(G, N // G, C, -1)
+        mean = xf.mean(dim=(1, 3), keepdim=True)
+        var = xf.var(dim=(1, 3), keepdim=True, unbiased=False)
+        y = (xf - mean) * torch.rsqrt(var + self.eps)
+        if self.affine:
+            y = y * self.weight.view(1, 1, C, 1) + self.bias.view(1, 1, C, 1)
+        if self.track_running_stats and self.running_mean is not None:
+            with torch.no_grad():
+                n = xf.shape[1] * xf.shape[3]
+                m = self.momentum if self.momentum is not None else 0.1
+                self.running_mean.mul_(1 - m).add_(m * mean.mean(dim=0).view(C))
+                unb = var.mean(dim=0).view(C) * (n / max(1, n - 1))
+                self.running_var.mul_(1 - m).add_(m * unb)
+                self.num_batches_tracked += 1
+        return y.reshape(x.shape).to(x.dtype).contiguous(memory_format=_fmt(x))
+
+
+def _fmt(x):
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        return torch.channels_last
+    return torch.contiguous_format
+
+
+@contextlib.contextmanager
+def ghost_batchnorm(model: nn.Module, groups: int):
+    mods = [m for m in model.modules() if isinstance(m, GhostBatchNorm2d)]
+    for m in mods:
+        m.ghost_groups = groups
+    try:
+        yield
+    finally:
+        for m in mods:
+            m.ghost_groups = 1
+
+
+def has_batchnorm(model: nn.Module) -> bool:
+    return any(isinstance(m, nn.modules.batchnorm._BatchNorm) for m in model.modules())
+
+
+def conv3x3(c_in, c_out, stride=1):
+    return nn.Conv2d(c_in, c_out, kernel_size=3, stride=stride, padding=1, bias=False)
+
+
+def conv1x1(c_in, c_out, stride=1):
+    return nn.Conv2d(c_in, c_out, kernel_size=1, stride=stride, bias=False)

@@ -1,0 +1,295 @@
+"""Fixup-initialised residual networks, implemented natively (the reference
+imports them from the external, unvendored ``fixup`` package:
+/root/reference/CommEfficient/models/fixup_resnet9.py:6,
+fixup_resnet.py:4).
+
+* ``FixupResNet9``  -- ResNet-9 topology with Fixup scalar biases/scales
+  (reference fixup_resnet9.py:33-91).  Unlike the reference its constructor
+  accepts cv_train's model_config kwargs (Appendix C #12) and ``num_classes``.
+* ``FixupResNet18`` / ``ResNet18`` -- the reference's CIFAR variants with a
+  256-channel last stage and avg||max pooling into Linear(512)
+  (fixup_resnet18.py:24-216).
+* ``FixupResNet50`` -- ImageNet Fixup bottleneck ResNet-50 (fixup_resnet.py:8-10).
+
+Fixup init (Zhang et al. 2019): the first conv of each residual branch is He
+init scaled by L^(-1/(2m-2)) (m = convs per branch), the last conv and the
+classifier are zero-initialised.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .common import GhostBatchNorm2d, ScalarBias, ScalarScale, conv1x1, conv3x3
+
+__all__ = ["FixupResNet9", "FixupResNet18", "ResNet18", "FixupResNet50"]
+
+
+def _he_std(conv: nn.Conv2d) -> float:
+    return float(np.sqrt(2.0 / (conv.weight.shape[0] * np.prod(conv.weight.shape[2:]))))
+
+
+class FixupBasicBlock(nn.Module):
+    """x -> +b1a -> conv -> +b1b -> relu -> +b2a -> conv -> *s -> +b2b -> (+x) -> relu."""
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.bias1a = nn.Parameter(torch.zeros(1))
+        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.bias1b = nn.Parameter(torch.zeros(1))
+        self.bias2a = nn.Parameter(torch.zeros(1))
+        self.conv2 = conv3x3(planes, planes)
+        self.scale = nn.Parameter(torch.ones(1))
+        self.bias2b = nn.Parameter(torch.zeros(1))
+        self.downsample = downsample
+
+    def forward(self, x):
+        xa = x + self.bias1a
+        out = F.relu(self.conv1(xa) + self.bias1b)
+        out = self.conv2(out + self.bias2a) * self.scale + self.bias2b
+        idt = self.downsample(xa) if self.downsample is not None else x
+        return F.relu(out + idt)
+
+
+class FixupLayer(nn.Module):
+    """conv, bias, relu, pool, then num_blocks FixupBasicBlocks."""
+
+    def __init__(self, c_in, c_out, num_blocks, pool):
+        super().__init__()
+        self.conv = conv3x3(c_in, c_out)
+        self.bias1a = nn.Parameter(torch.zeros(1))
+        self.bias1b = nn.Parameter(torch.zeros(1))
+        self.scale = nn.Parameter(torch.ones(1))
+        self.pool = pool
+        self.blocks = nn.Sequential(*[FixupBasicBlock(c_out, c_out) for _ in range(num_blocks)])
+
+    def forward(self, x):
+        out = F.relu(self.conv(x + self.bias1a) * self.scale + self.bias1b)
+        if self.pool is not None:
+            out = self.pool(out)
+        return self.blocks(out)
+
+
+class FixupResNet9(nn.Module):
+    def __init__(self, channels=None, pool=None, num_classes=10, initial_channels=3, **kw):
+        super().__init__()
+        self.num_layers = 2
+        ch = channels or {"prep": 64, "layer1": 128, "layer2": 256, "layer3": 512}
+        self.channels = ch
+        pool = pool if pool is not None else nn.MaxPool2d(2)
+        self.conv1 = conv3x3(initial_channels, ch["prep"])
+        self.bias1a = nn.Parameter(torch.zeros(1))
+        self.bias1b = nn.Parameter(torch.zeros(1))
+        self.scale = nn.Parameter(torch.ones(1))
+        self.layer1 = FixupLayer(ch["prep"], ch["layer1"], 1, pool)
+        self.layer2 = FixupLayer(ch["layer1"], ch["layer2"], 0, pool)
+        self.layer3 = FixupLayer(ch["layer2"], ch["layer3"], 1, pool)
+        self.pool = nn.MaxPool2d(4)
+        self.bias2 = nn.Parameter(torch.zeros(1))
+        self.linear = nn.Linear(ch["layer3"], num_classes)
+        nn.init.normal_(self.conv1.weight, 0, _he_std(self.conv1))
+        for m in self.modules():
+            if isinstance(m, FixupBasicBlock):
+                nn.init.normal_(m.conv1.weight, 0, _he_std(m.conv1) * self.num_layers ** (-0.5))
+                nn.init.constant_(m.conv2.weight, 0)
+            elif isinstance(m, FixupLayer):
+                nn.init.normal_(m.conv.weight, 0, _he_std(m.conv))
+            elif isinstance(m, nn.Linear):
+                nn.init.constant_(m.weight, 0)
+                nn.init.constant_(m.bias, 0)
+
+    def forward(self, x):
+        out = F.relu(self.conv1(x + self.bias1a) * self.scale + self.bias1b)
+        out = self.layer3(self.layer2(self.layer1(out)))
+        out = self.pool(out).flatten(1)
+        return self.linear(out + self.bias2)
+
+
+# ---------------------------------------------------------------- ResNet-18s
+class _Mul(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.scale = nn.Parameter(torch.ones(1))
+
+    def forward(self, x):
+        return x * self.scale
+
+
+class _Add(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.bias = nn.Parameter(torch.zeros(1))
+
+    def forward(self, x):
+        return x + self.bias
+
+
+class FixupBlock18(nn.Module):
+    """Reference fixup_resnet18.py:24-63 (module names add1a/conv1/add1b/add2a/conv2/mul/add2b)."""
+
+    def __init__(self, in_channels, out_channels, stride=1):
+        super().__init__()
+        self.add1a = _Add()
+        self.conv1 = conv3x3(in_channels, out_channels, stride)
+        self.add1b = _Add()
+        self.add2a = _Add()
+        self.conv2 = conv3x3(out_channels, out_channels)
+        self.mul = _Mul()
+        self.add2b = _Add()
+        if stride != 1 or in_channels != out_channels:
+            self.shortcut = conv1x1(in_channels, out_channels, stride)
+
+    def forward(self, x):
+        sc = self.shortcut(x) if hasattr(self, "shortcut") else x
+        out = F.relu(self.add1b(self.conv1(self.add1a(x))))
+        out = self.add2b(self.mul(self.conv2(self.add2a(out))))
+        return F.relu(out + sc)
+
+
+class PreActBlock(nn.Module):
+    """Reference fixup_resnet18.py:138-165 (conv-bn-relu x2 + shortcut)."""
+
+    def __init__(self, in_channels, out_channels, stride=1):
+        super().__init__()
+        self.bn1 = GhostBatchNorm2d(out_channels)
+        self.conv1 = conv3x3(in_channels, out_channels, stride)
+        self.bn2 = GhostBatchNorm2d(out_channels)
+        self.conv2 = conv3x3(out_channels, out_channels)
+        if stride != 1 or in_channels != out_channels:
+            self.shortcut = nn.Sequential(conv1x1(in_channels, out_channels, stride))
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        sc = self.shortcut(x) if hasattr(self, "shortcut") else x
+        return out + sc
+
+
+def _avg_max_head(x):
+    return torch.cat([F.adaptive_avg_pool2d(x, 1).flatten(1), F.adaptive_max_pool2d(x, 1).flatten(1)], -1)
+
+
+class _ResNet18Base(nn.Module):
+    widths = (64, 128, 256, 256)
+
+    def _make(self, block, num_blocks):
+        layers, c_in = [], 64
+        for i, (w, n) in enumerate(zip(self.widths, num_blocks)):
+            stride = 1 if i == 0 else 2
+            blocks = []
+            for s in [stride] + [1] * (n - 1):
+                blocks.append(block(c_in, w, s))
+                c_in = w
+            layers.append(nn.Sequential(*blocks))
+        return nn.Sequential(*layers)
+
+
+class FixupResNet18(_ResNet18Base):
+    def __init__(self, num_blocks=(2, 2, 2, 2), num_classes=10, initial_channels=3, **kw):
+        super().__init__()
+        self.num_layers = sum(num_blocks)
+        self.prep = conv3x3(initial_channels, 64)
+        self.layers = self._make(FixupBlock18, num_blocks)
+        self.classifier = nn.Linear(512, num_classes)
+        for m in self.modules():
+            if isinstance(m, FixupBlock18):
+                nn.init.normal_(m.conv1.weight, 0, _he_std(m.conv1) * self.num_layers ** (-0.5))
+                nn.init.constant_(m.conv2.weight, 0)
+                if hasattr(m, "shortcut"):
+                    nn.init.normal_(m.shortcut.weight, 0, _he_std(m.shortcut))
+            elif isinstance(m, nn.Linear):
+                nn.init.constant_(m.weight, 0)
+                nn.init.constant_(m.bias, 0)
+        nn.init.normal_(self.prep.weight, 0, _he_std(self.prep))
+
+    def forward(self, x):
+        x = self.layers(F.relu(self.prep(x)))
+        return self.classifier(_avg_max_head(x))
+
+
+class ResNet18(_ResNet18Base):
+    def __init__(self, num_blocks=(2, 2, 2, 2), num_classes=10, initial_channels=3, **kw):
+        super().__init__()
+        self.prep = nn.Sequential(conv3x3(initial_channels, 64), nn.ReLU())
+        self.layers = self._make(PreActBlock, num_blocks)
+        self.classifier = nn.Linear(512, num_classes)
+
+    def forward(self, x):
+        return self.classifier(_avg_max_head(self.layers(self.prep(x))))
+
+
+# ---------------------------------------------------------------- ResNet-50
+class FixupBottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.bias1a = nn.Parameter(torch.zeros(1))
+        self.conv1 = conv1x1(inplanes, planes)
+        self.bias1b = nn.Parameter(torch.zeros(1))
+        self.bias2a = nn.Parameter(torch.zeros(1))
+        self.conv2 = conv3x3(planes, planes, stride)
+        self.bias2b = nn.Parameter(torch.zeros(1))
+        self.bias3a = nn.Parameter(torch.zeros(1))
+        self.conv3 = conv1x1(planes, planes * self.expansion)
+        self.scale = nn.Parameter(torch.ones(1))
+        self.bias3b = nn.Parameter(torch.zeros(1))
+        self.downsample = downsample
+
+    def forward(self, x):
+        xa = x + self.bias1a
+        out = F.relu(self.conv1(xa) + self.bias1b)
+        out = F.relu(self.conv2(out + self.bias2a) + self.bias2b)
+        out = self.conv3(out + self.bias3a) * self.scale + self.bias3b
+        idt = self.downsample(xa) if self.downsample is not None else x
+        return F.relu(out + idt)
+
+
+class FixupResNet(nn.Module):
+    def __init__(self, block, layers, num_classes=1000, initial_channels=3, **kw):
+        super().__init__()
+        self.num_layers = sum(layers)
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(initial_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bias1 = nn.Parameter(torch.zeros(1))
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.bias2 = nn.Parameter(torch.zeros(1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, FixupBottleneck):
+                f = self.num_layers ** (-0.25)
+                nn.init.normal_(m.conv1.weight, 0, _he_std(m.conv1) * f)
+                nn.init.normal_(m.conv2.weight, 0, _he_std(m.conv2) * f)
+                nn.init.constant_(m.conv3.weight, 0)
+                if m.downsample is not None:
+                    nn.init.normal_(m.downsample.weight, 0, _he_std(m.downsample))
+            elif isinstance(m, nn.Linear):
+                nn.init.constant_(m.weight, 0)
+                nn.init.constant_(m.bias, 0)
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = conv1x1(self.inplanes, planes * block.expansion, stride)
+        layers = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * block.expansion
+        layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(F.relu(self.conv1(x) + self.bias1))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(self.avgpool(x).flatten(1) + self.bias2)
+
+
+class FixupResNet50(FixupResNet):
+    def __init__(self, num_classes=1000, initial_channels=3, **kw):
+        super().__init__(FixupBottleneck, [3, 4, 6, 3], num_classes=num_classes,
+                         initial_channels=initial_channels)

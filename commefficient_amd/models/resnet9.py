@@ -1,0 +1,119 @@
+"""ResNet-9 (the cifar10-fast "Page" net) -- the flagship FetchSGD model.
+
+Architecture and parameter names follow /root/reference/CommEfficient/models/
+resnet9.py:32-148 so ``state_dict`` keys (``n.prep.conv.weight`` ...) and the
+flat parameter order match the reference checkpoint format:
+prep(c_in->64) -> layer1(64->128, pool) + res1 -> layer2(128->256, pool) ->
+layer3(256->512, pool) + res3 -> maxpool 4 -> linear(512->classes, no bias) -> ×0.125.
+BatchNorm is off unless ``do_batchnorm`` (cv_train.py:357).  6,568,640 params
+for 10 classes.
+
+MI355X notes: the convs run on MIOpen in bf16 channels_last under autocast;
+the ReLU+maxpool pairs are left to the framework's fusion.  Fixes reference
+quirk Appendix C #12: ``finetune_parameters`` no longer touches an undefined
+``self.iid``.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .common import GhostBatchNorm2d, Mul
+
+__all__ = ["ResNet9"]
+
+DEFAULT_CHANNELS = {"prep": 64, "layer1": 128, "layer2": 256, "layer3": 512}
+
+
+def _bn(c, bn_bias_init=None, bn_bias_freeze=False, bn_weight_init=None, bn_weight_freeze=False):
+    m = GhostBatchNorm2d(c)
+    if bn_bias_init is not None:
+        nn.init.constant_(m.bias, bn_bias_init)
+    if bn_weight_init is not None:
+        nn.init.constant_(m.weight, bn_weight_init)
+    m.bias.requires_grad = not bn_bias_freeze
+    m.weight.requires_grad = not bn_weight_freeze
+    return m
+
+
+class ConvBN(nn.Module):
+    def __init__(self, do_batchnorm, c_in, c_out, bn_weight_init=1.0, pool=None, **kw):
+        super().__init__()
+        self.pool = pool
+        self.conv = nn.Conv2d(c_in, c_out, kernel_size=3, padding=1, bias=False)
+        self.do_batchnorm = do_batchnorm
+        if do_batchnorm:
+            self.bn = _bn(c_out, bn_weight_init=bn_weight_init, **kw)
+
+    def forward(self, x):
+        x = self.conv(x)
+        if self.do_batchnorm:
+            x = self.bn(x)
+        x = F.relu(x, inplace=True)
+        return self.pool(x) if self.pool is not None else x
+
+
+class Residual(nn.Module):
+    def __init__(self, do_batchnorm, c, **kw):
+        super().__init__()
+        self.res1 = ConvBN(do_batchnorm, c, c, **kw)
+        self.res2 = ConvBN(do_batchnorm, c, c, **kw)
+
+    def forward(self, x):
+        return x + F.relu(self.res2(self.res1(x)))
+
+
+class BasicNet(nn.Module):
+    def __init__(self, do_batchnorm, channels, weight, pool, num_classes, initial_channels=3,
+                 new_num_classes=None, **kw):
+        super().__init__()
+        self.new_num_classes = new_num_classes
+        self.prep = ConvBN(do_batchnorm, initial_channels, channels["prep"], **kw)
+        self.layer1 = ConvBN(do_batchnorm, channels["prep"], channels["layer1"], pool=pool, **kw)
+        self.res1 = Residual(do_batchnorm, channels["layer1"], **kw)
+        self.layer2 = ConvBN(do_batchnorm, channels["layer1"], channels["layer2"], pool=pool, **kw)
+        self.layer3 = ConvBN(do_batchnorm, channels["layer2"], channels["layer3"], pool=pool, **kw)
+        self.res3 = Residual(do_batchnorm, channels["layer3"], **kw)
+        self.pool = nn.MaxPool2d(4)
+        self.linear = nn.Linear(channels["layer3"], num_classes, bias=False)
+        self.classifier = Mul(weight)
+
+    def forward(self, x):
+        x = self.prep(x)
+        x = self.res1(self.layer1(x))
+        x = self.layer2(x)
+        x = self.res3(self.layer3(x))
+        x = self.pool(x).flatten(1)
+        return self.classifier(self.linear(x))
+
+
+class ResNet9(nn.Module):
+    def __init__(self, do_batchnorm=False, channels=None, weight=0.125, pool=None,
+                 num_classes=10, new_num_classes=None, initial_channels=3,
+                 bn_bias_freeze=False, bn_weight_freeze=False, **kw):
+        super().__init__()
+        self.channels = dict(channels or DEFAULT_CHANNELS)
+        self.weight = weight
+        pool = pool if pool is not None else nn.MaxPool2d(2)
+        bn_kw = {}
+        if do_batchnorm:
+            bn_kw = dict(bn_bias_freeze=bn_bias_freeze, bn_weight_freeze=bn_weight_freeze)
+        self.n = BasicNet(do_batchnorm, self.channels, weight, pool, num_classes,
+                          initial_channels=initial_channels, new_num_classes=new_num_classes,
+                          **bn_kw)
+
+    def forward(self, x):
+        return self.n(x)
+
+    def finetune_parameters(self):
+        """Replace the head for ``new_num_classes`` and return its params
+        (reference resnet9.py:105-113)."""
+        n_new = self.n.new_num_classes or self.n.linear.out_features
+        self.n.linear = nn.Linear(self.channels["layer3"], n_new, bias=False).to(
+            self.n.linear.weight.device)
+        self.n.classifier = Mul(self.weight)
+        for p in self.n.linear.parameters():
+            p.requires_grad = True
+        return itertools.chain(self.n.linear.parameters())

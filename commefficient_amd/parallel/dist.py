@@ -1,0 +1,134 @@
+"""SPMD process-group plumbing: one process per GPU, RCCL over xGMI.
+
+Replaces the reference's parameter-server topology (PS on the last GPU,
+``torch.distributed.reduce`` to rank 0, weights shipped back through host
+shared memory -- /root/reference/CommEfficient/fed_aggregator.py:131-164,455,
+fed_worker.py:18-25,41,136-138).  Every rank holds the
+replicated weights and server state, executes its slice of the round's
+virtual clients, joins ONE all-reduce of the compressed payload, and applies
+the identical deterministic server update.
+
+Backend: ``nccl`` (= RCCL on ROCm) for GPU runs, ``gloo`` for CPU runs.
+Rendezvous: ``env://`` (torchrun, or our own spawner) on 127.0.0.1.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistCtx:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_CTX = DistCtx()
+
+
+def ctx() -> DistCtx:
+    return _CTX
+
+
+def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> DistCtx:
+    """Initialise from the environment (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    global _CTX
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device_type == "cuda":
+        n = torch.cuda.device_count()
+        if n == 0:
+            raise RuntimeError("--device cuda requested but no HIP device is visible")
+        torch.cuda.set_device(local % n)
+        device = torch.device("cuda", local % n)
+        backend = "nccl"
+    else:
+        device = torch.device("cpu")
+        backend = "gloo"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if port is not None:
+            os.environ.setdefault("MASTER_PORT", str(port))
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _CTX = DistCtx(rank, world, local, device, backend if world > 1 else "none")
+    return _CTX
+
+
+def all_reduce_(t: torch.Tensor) -> torch.Tensor:
+    if _CTX.distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if _CTX.distributed:
+        dist.broadcast(t, src=src)
+    return t
+
+
+def all_gather_object(obj):
+    if not _CTX.distributed:
+        return [obj]
+    out = [None] * _CTX.world_size
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def barrier():
+    if _CTX.distributed:
+        if _CTX.backend == "nccl":
+            dist.barrier(device_ids=[_CTX.device.index])
+        else:
+            dist.barrier()
+
+
+def max_over_ranks(x: float) -> float:
+    if not _CTX.distributed:
+        return x
+    t = torch.tensor([x], dtype=torch.float64,
+                     device=_CTX.device if _CTX.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown():
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def spawn(fn, nprocs: int, args=(), port: int = 29500):
+    """Launch ``fn(rank, *args)`` on ``nprocs`` fresh processes with env://
+    rendezvous on 127.0.0.1 (used when not started by torchrun).  The parent
+    must not have touched the GPU (the children are fresh interpreters)."""
+    import torch.multiprocessing as mp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["WORLD_SIZE"] = str(nprocs)
+    mp.spawn(_spawn_entry, args=(fn, nprocs, args), nprocs=nprocs, join=True)
+
+
+def _spawn_entry(rank, fn, nprocs, args):
+    os.environ["RANK"] = str(rank)
+    os.environ["LOCAL_RANK"] = str(rank)
+    os.environ["WORLD_SIZE"] = str(nprocs)
+    fn(rank, *args)

@@ -1,0 +1,104 @@
+"""Flat parameter / gradient buffers.
+
+The reference flattens every round: ``get_grad_vec`` is a ``torch.cat`` of all
+``p.grad`` and ``set_param_vec`` a per-parameter ``zero_()`` + ``add_()``
+(/root/reference/CommEfficient/utils.py:254-297).
+Here trainable parameters and their gradients are *views* into two
+contiguous fp32 buffers, so "flatten" and "load weights" are free and every
+codec kernel streams one aligned vector.  The flat order is
+``model.parameters()`` order restricted to ``requires_grad`` params, exactly
+the reference's grad-vector order.
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import torch
+import torch.nn as nn
+
+
+def trainable_params(model: nn.Module) -> List[nn.Parameter]:
+    return [p for p in model.parameters() if p.requires_grad]
+
+
+def grad_size(model: nn.Module) -> int:
+    return sum(p.numel() for p in trainable_params(model))
+
+
+class FlatParams:
+    """Re-homes a model's trainable params (and grads) into flat buffers."""
+
+    def __init__(self, model: nn.Module, device):
+        self.model = model
+        self.params = trainable_params(model)
+        self.shapes = [p.shape for p in self.params]
+        self.numels = [p.numel() for p in self.params]
+        # the codec kernels stream the whole (16-byte aligned) flat buffer,
+        # so per-parameter alignment inside it does not matter
+        self.offsets: List[int] = []
+        off = 0
+        for n in self.numels:
+            self.offsets.append(off)
+            off += n
+        self.d = off
+        self.device = torch.device(device)
+        self.w = torch.empty(self.d, dtype=torch.float32, device=self.device)
+        self.g = torch.zeros(self.d, dtype=torch.float32, device=self.device)
+        with torch.no_grad():
+            for p, o, n in zip(self.params, self.offsets, self.numels):
+                self.w[o:o + n].copy_(p.detach().reshape(-1).to(self.device, torch.float32))
+        self.bind(self.w)
+        self._bind_grads()
+        # non-trainable tensors (BN buffers, frozen params) follow the device
+        for m in model.modules():
+            for name, b in list(m.named_buffers(recurse=False)):
+                if b is not None:
+                    setattr(m, name, b.to(self.device))
+            for name, p in list(m.named_parameters(recurse=False)):
+                if not p.requires_grad:
+                    p.data = p.data.to(self.device)
+
+    def bind(self, buf: torch.Tensor) -> None:
+        """Make the model's params views of ``buf`` (a [d] fp32 tensor)."""
+        assert buf.numel() == self.d and buf.dtype == torch.float32
+        self.bound = buf
+        for p, o, n, s in zip(self.params, self.offsets, self.numels, self.shapes):
+            p.data = buf[o:o + n].view(s)
+
+    def _bind_grads(self):
+        for p, o, n, s in zip(self.params, self.offsets, self.numels, self.shapes):
+            p.grad = self.g[o:o + n].view(s)
+
+    def zero_grad(self):
+        self.g.zero_()
+        # autograd may have replaced .grad (e.g. set_to_none elsewhere)
+        for p, o, n in zip(self.params, self.offsets, self.numels):
+            if p.grad is None or p.grad.data_ptr() != self.g[o:o + n].data_ptr():
+                p.grad = self.g[o:o + n].view(p.shape)
+
+    def ranges_of(self, params) -> List[Tuple[int, int]]:
+        """Flat [start, end) ranges of the given parameters."""
+        pos = {id(p): (o, o + n) for p, o, n in zip(self.params, self.offsets, self.numels)}
+        return [pos[id(p)] for p in params if id(p) in pos]
+
+
+# reference-compatible helpers (utils.py:254-297) for tools and tests
+def get_param_vec(model: nn.Module) -> torch.Tensor:
+    return torch.cat([p.data.reshape(-1).float() for p in trainable_params(model)])
+
+
+def set_param_vec(model: nn.Module, vec: torch.Tensor) -> None:
+    start = 0
+    with torch.no_grad():
+        for p in trainable_params(model):
+            n = p.numel()
+            p.data.copy_(vec[start:start + n].view_as(p))
+            start += n
+
+
+def get_grad_vec(model: nn.Module) -> torch.Tensor:
+    out = []
+    for p in trainable_params(model):
+        out.append(torch.zeros(p.numel(), device=p.device) if p.grad is None
+                   else p.grad.reshape(-1).float())
+    return torch.cat(out)

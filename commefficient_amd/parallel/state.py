@@ -1,0 +1,165 @@
+"""Per-client state (local momentum, local error, stale downlink weights) and
+upload/download byte accounting.
+
+Reference: client state lives in host shared memory as ``[C, d]`` arrays
+(/root/reference/CommEfficient/fed_aggregator.py:105-129) and, on GPU runs,
+worker updates are made on ``.to(device)`` *copies* and lost
+(fed_worker.py:169-174).  Here rows are written
+back, live in HBM when they fit (288 GB per MI355X) and are allocated lazily
+on first participation, each row owned by rank ``client % world_size`` (the
+engine assigns a client's work to its owner whenever client state exists).
+
+Byte accounting reproduces fed_aggregator.py:170-299 exactly in both of the
+reference's regimes with one mechanism: a per-coordinate ``last_mod`` round
+index (written by the apply kernels) and a per-client ``last_seen`` round;
+a participating client downloads ``4 * #{i : last_mod[i] >= last_seen[c]}``
+bytes, computed by the ``count_ge`` kernel in one pass over ``last_mod``
+(no host history deque; the reference's 10/participation truncation
+disappears).  Upload is ``4 * {d | k | r*c}`` per participating client
+(fed_aggregator.py:291-298).  The true on-wire RCCL volume is reported too.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+
+
+class ClientStateStore:
+    KINDS = ("velocity", "error", "weights")
+
+    def __init__(self, args, d: int, num_clients: int, device, rank: int, world: int,
+                 init_weights: Optional[torch.Tensor] = None):
+        self.args = args
+        self.d = d
+        self.num_clients = num_clients
+        self.rank, self.world = rank, world
+        self.kinds = []
+        if args.local_momentum > 0 and args.mode != "sketch":
+            self.kinds.append("velocity")
+        if args.error_type == "local":
+            self.kinds.append("error")
+        if args.do_topk_down:
+            self.kinds.append("weights")
+        want = getattr(args, "client_state_device", "auto")
+        per_rank_bytes = len(self.kinds) * d * 4 * (num_clients // max(1, world) + 1)
+        if want == "auto":
+            want = "gpu"
+            if torch.device(device).type == "cuda":
+                free, _ = torch.cuda.mem_get_info(torch.device(device))
+                if per_rank_bytes > 0.6 * free:
+                    want = "cpu"
+        self.store_device = torch.device(device) if want == "gpu" else torch.device("cpu")
+        self.compute_device = torch.device(device)
+        self.rows: Dict[str, Dict[int, torch.Tensor]] = {k: {} for k in self.kinds}
+        self.init_weights = init_weights.detach().clone().to(self.store_device) \
+            if (init_weights is not None and "weights" in self.kinds) else None
+
+    @property
+    def active(self) -> bool:
+        return bool(self.kinds)
+
+    def owner(self, client: int) -> int:
+        return int(client) % self.world
+
+    def get(self, kind: str, client: int) -> Optional[torch.Tensor]:
+        """Device tensor for the row (created on first use).  For CPU-resident
+        storage the returned tensor is a device copy; call ``put`` after
+        mutating it."""
+        if kind not in self.kinds:
+            return None
+        rows = self.rows[kind]
+        c = int(client)
+        if c not in rows:
+            if kind == "weights":
+                rows[c] = self.init_weights.clone()
+            else:
+                rows[c] = torch.zeros(self.d, device=self.store_device,
+                                      pin_memory=self.store_device.type == "cpu" and
+                                      self.compute_device.type == "cuda")
+        t = rows[c]
+        if t.device != self.compute_device:
+            return t.to(self.compute_device, non_blocking=True)
+        return t
+
+    def put(self, kind: str, client: int, value: torch.Tensor):
+        if kind not in self.kinds:
+            return
+        row = self.rows[kind][int(client)]
+        if row.data_ptr() != value.data_ptr():
+            row.copy_(value, non_blocking=True)
+
+    def zero_velocity_at(self, clients: Iterable[int], idx: torch.Tensor):
+        """true_topk momentum masking of the participating clients' local
+        velocities (fed_aggregator.py:528-533)."""
+        if "velocity" not in self.kinds:
+            return
+        for c in clients:
+            c = int(c)
+            if self.owner(c) != self.rank or c not in self.rows["velocity"]:
+                continue
+            row = self.rows["velocity"][c]
+            if row.device == idx.device:
+                ops.zero_at(idx, row)
+            else:
+                row[idx.to(row.device)] = 0
+
+    def state_dict(self):
+        return {k: {c: t.cpu() for c, t in v.items()} for k, v in self.rows.items()}
+
+    def load_state_dict(self, sd):
+        for k, v in sd.items():
+            if k in self.rows:
+                self.rows[k] = {int(c): t.to(self.store_device) for c, t in v.items()}
+
+
+class ByteAccountant:
+    def __init__(self, args, d: int, num_clients: int, device, world: int, payload_numel: int):
+        self.args = args
+        self.d = d
+        self.num_clients = num_clients
+        self.device = device
+        self.world = world
+        self.last_mod = torch.full((d,), -1, dtype=torch.int32, device=device)
+        self.last_seen = np.zeros(num_clients, dtype=np.int64)
+        mode = args.mode
+        self.upload_per_client = 4 * {"uncompressed": d, "true_topk": d, "local_topk": args.k,
+                                      "sketch": args.num_rows * args.num_cols, "fedavg": d}[mode]
+        self.payload_numel = payload_numel
+        # on-device running totals (no host sync per round)
+        self.client_download = torch.zeros(num_clients, dtype=torch.float64, device=device)
+        self.client_upload = torch.zeros(num_clients, dtype=torch.float64, device=device)
+
+    def wire_bytes_per_rank(self, payload_numel: int) -> float:
+        """Bytes each rank sends in a ring all-reduce of the payload."""
+        n = self.world
+        return 0.0 if n == 1 else 2.0 * (n - 1) / n * payload_numel * 4
+
+    def round(self, clients: np.ndarray, round_idx: int):
+        """Account one round for the participating ``clients`` (unique, sorted).
+        Must be called before the round's server update (clients download the
+        pre-update weights).  Returns (download bytes [W] device f64,
+        upload bytes float)."""
+        seen = self.last_seen[clients].astype(np.int32)
+        thr, inv = np.unique(seen, return_inverse=True)
+        dl = torch.empty(len(clients), dtype=torch.float64, device=self.device)
+        counts_all = []
+        for s in range(0, len(thr), 1024):
+            counts_all.append(ops.count_ge(self.last_mod, torch.from_numpy(thr[s:s + 1024])))
+        counts = torch.cat(counts_all).to(torch.float64) * 4.0
+        dl.copy_(counts[torch.from_numpy(inv).to(self.device)])
+        cl = torch.from_numpy(clients.astype(np.int64)).to(self.device)
+        self.client_download.index_add_(0, cl, dl)
+        self.client_upload.index_add_(0, cl, torch.full_like(dl, float(self.upload_per_client)))
+        self.last_seen[clients] = round_idx
+        return dl, float(self.upload_per_client) * len(clients)
+
+    def state_dict(self):
+        return {"last_mod": self.last_mod.cpu(), "last_seen": torch.from_numpy(self.last_seen)}
+
+    def load_state_dict(self, sd):
+        self.last_mod.copy_(sd["last_mod"])
+        self.last_seen = sd["last_seen"].numpy().astype(np.int64)

@@ -1,0 +1,58 @@
+"""Loss functions in the engine's per-example form.
+
+``loss_fn(model, inputs: tuple, targets, args) -> (per_example_loss[n], [metric[n], ...])``
+
+The engine sums per-example losses for merged clients and averages them per
+client otherwise, so one definition serves both paths.  CV: cross-entropy +
+top-1 correctness (reference cv_train.py:31-84 ``compute_loss_ce`` /
+``Correct``).  GPT-2: see models/gpt2.py.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def cv_loss(model, inputs, targets, args):
+    logits = model(*inputs)
+    per_ex = F.cross_entropy(logits.float(), targets, reduction="none")
+    correct = (logits.argmax(dim=1) == targets).float()
+    return per_ex, [correct]
+
+
+def gpt2_loss_train(model, inputs, targets, args):
+    """inputs = (input_ids[B,C,L], mc_token_ids[B,C], lm_labels[B,C,L], token_type_ids[B,C,L]),
+    targets = mc_labels[B].  Per-example lm_coef*lm + mc_coef*mc
+    (gpt2_train.py:88-99; lm loss averaged over each example's labelled tokens)."""
+    input_ids, mc_token_ids, lm_labels, token_type_ids = inputs
+    m = model.model if hasattr(model, "model") and not hasattr(model, "transformer") else model
+    out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids)
+    lm_logits, mc_logits = out.logits, out.mc_logits
+    B = input_ids.shape[0]
+    shift_logits = lm_logits[..., :-1, :].float()
+    shift_labels = lm_labels[..., 1:]
+    tok = F.cross_entropy(shift_logits.reshape(-1, shift_logits.size(-1)), shift_labels.reshape(-1),
+                          ignore_index=-100, reduction="none").view(B, -1)
+    mask = (shift_labels.reshape(B, -1) != -100).float()
+    lm = (tok * mask).sum(1) / mask.sum(1).clamp_min(1.0)
+    mc = F.cross_entropy(mc_logits.float(), targets, reduction="none")
+    acc = (mc_logits.argmax(-1) == targets).float()
+    return args.lm_coef * lm + args.mc_coef * mc, [acc]
+
+
+def gpt2_loss_val(model, inputs, targets, args):
+    """Validation: (nll of the LM on the gold reply, mc accuracy) (gpt2_train.py:55-87)."""
+    input_ids, mc_token_ids, lm_labels, token_type_ids = inputs
+    m = model.model if hasattr(model, "model") and not hasattr(model, "transformer") else model
+    out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids)
+    lm_logits, mc_logits = out.logits, out.mc_logits
+    B = input_ids.shape[0]
+    # the gold candidate is the last one (PERSONA collate order)
+    lg = lm_logits[:, -1, :-1, :].float()
+    lb = lm_labels[:, -1, 1:]
+    tok = F.cross_entropy(lg.reshape(-1, lg.size(-1)), lb.reshape(-1), ignore_index=-100,
+                          reduction="none").view(B, -1)
+    mask = (lb != -100).float()
+    nll = (tok * mask).sum(1) / mask.sum(1).clamp_min(1.0)
+    acc = (mc_logits.argmax(-1) == targets).float()
+    return nll, [acc]

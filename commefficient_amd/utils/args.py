@@ -1,0 +1,206 @@
+"""Command-line flags: every flag of the reference (same names, dests and
+defaults; /root/reference/CommEfficient/utils.py:102-230)
+plus MI355X-build extensions (marked NEW below).
+
+The returned ``argparse.Namespace`` is the single config object passed through
+the framework, like the reference's.  Validity checks mirror the reference's
+asserts (utils.py:225-228, fed_worker.py:221-228, fed_aggregator.py:484-486,
+512,545,573-576) but raise ``ValueError`` with a readable message up-front
+instead of asserting deep inside a worker process.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import socket
+from typing import Optional, Sequence
+
+import numpy as np
+
+FED_DATASETS = {"CIFAR10": 10, "CIFAR100": 100, "EMNIST": 62, "ImageNet": 1000, "PERSONA": -1}
+MODES = ["sketch", "true_topk", "local_topk", "fedavg", "uncompressed"]
+ERROR_TYPES = ["none", "local", "virtual"]
+
+
+def num_classes_of_dataset(name: str) -> int:
+    return FED_DATASETS[name]
+
+
+def is_port_in_use(port: int) -> bool:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        return s.connect_ex(("127.0.0.1", port)) == 0
+
+
+def _model_names():
+    from .. import models
+    return models.model_names()
+
+
+def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="commefficient_amd federated / DP training")
+
+    # meta-args
+    p.add_argument("--test", action="store_true", dest="do_test")
+    p.add_argument("--mode", choices=MODES, default="sketch")
+    p.add_argument("--tensorboard", dest="use_tensorboard", action="store_true")
+    p.add_argument("--seed", type=int, default=21)
+
+    # data/model args
+    p.add_argument("--model", default="ResNet9", help="Name of the model.", choices=_model_names())
+    p.add_argument("--finetune", action="store_true", dest="do_finetune")
+    p.add_argument("--checkpoint", action="store_true", dest="do_checkpoint")
+    p.add_argument("--checkpoint_path", type=str, default="./checkpoint",
+                   help="Path or url to cache the model")
+    p.add_argument("--finetune_path", type=str, default="./finetune",
+                   help="Path or url of the model cache")
+    p.add_argument("--finetuned_from", type=str, choices=list(FED_DATASETS.keys()),
+                   help="Name of the dataset you pretrained on.")
+    p.add_argument("--num_results_train", type=int, default=2)
+    p.add_argument("--num_results_val", type=int, default=2)
+    p.add_argument("--dataset_name", type=str, default="", choices=list(FED_DATASETS.keys()),
+                   help="Name of the dataset.")
+    p.add_argument("--dataset_dir", type=str, default="./dataset",
+                   help="Path or url of the dataset cache")
+    p.add_argument("--batchnorm", action="store_true", dest="do_batchnorm")
+    p.add_argument("--nan_threshold", type=float, default=999)
+
+    # compression args
+    p.add_argument("--k", type=int, default=50000)
+    p.add_argument("--num_cols", type=int, default=500000)
+    p.add_argument("--num_rows", type=int, default=5)
+    p.add_argument("--num_blocks", type=int, default=20)
+    p.add_argument("--topk_down", action="store_true", dest="do_topk_down")
+
+    # optimization args
+    p.add_argument("--local_momentum", type=float, default=0.9)
+    p.add_argument("--virtual_momentum", type=float, default=0)
+    p.add_argument("--weight_decay", type=float, default=5e-4)
+    p.add_argument("--num_epochs", type=float, default=24, help="Number of training epochs")
+    p.add_argument("--num_fedavg_epochs", type=int, default=1)
+    p.add_argument("--fedavg_batch_size", type=int, default=-1)
+    p.add_argument("--fedavg_lr_decay", type=float, default=1)
+    p.add_argument("--error_type", choices=ERROR_TYPES, default="none")
+    p.add_argument("--lr_scale", type=float, default=default_lr)
+    p.add_argument("--pivot_epoch", type=float, default=5)
+
+    # parallelization args
+    p.add_argument("--port", type=int, default=5315)
+    p.add_argument("--num_clients", type=int)
+    p.add_argument("--num_workers", type=int, default=1)
+    p.add_argument("--device", type=str, choices=["cpu", "cuda"], default=None,
+                   help="Device (cuda or cpu)")
+    p.add_argument("--num_devices", type=int, default=1, help="Number of gpus")
+    p.add_argument("--share_ps_gpu", action="store_true")
+    p.add_argument("--iid", action="store_true", dest="do_iid")
+    p.add_argument("--train_dataloader_workers", type=int, default=0)
+    p.add_argument("--val_dataloader_workers", type=int, default=0)
+
+    # GPT2 args
+    p.add_argument("--model_checkpoint", type=str, default="gpt2",
+                   help="Path, url or short name of the model")
+    p.add_argument("--num_candidates", type=int, default=2, help="Number of candidates for training")
+    p.add_argument("--max_history", type=int, default=2,
+                   help="Number of previous exchanges to keep in history")
+    p.add_argument("--local_batch_size", type=int, default=8,
+                   help="Batch size for training (-1 uses all data the client has)")
+    p.add_argument("--valid_batch_size", type=int, default=8, help="Batch size for validation")
+    p.add_argument("--microbatch_size", type=int, default=-1,
+                   help="Size of each batch shard to be processed to save memory (-1 uses all data)")
+    p.add_argument("--lm_coef", type=float, default=1.0, help="LM loss coefficient")
+    p.add_argument("--mc_coef", type=float, default=1.0, help="Multiple-choice loss coefficient")
+    p.add_argument("--max_grad_norm", type=float, help="Clipping gradient norm, is per-worker")
+    p.add_argument("--personality_permutations", type=int, default=1,
+                   help="Number of permutations of personality sentences")
+    p.add_argument("--eval_before_start", action="store_true",
+                   help="If true start with a first evaluation before training")
+
+    # Differential Privacy args
+    p.add_argument("--dp", action="store_true", dest="do_dp",
+                   help="Whether to do differentially private training)")
+    p.add_argument("--dp_mode", choices=["worker", "server"], default="worker")
+    p.add_argument("--l2_norm_clip", type=float, default=1.0, help="What value to clip the l2 norm to")
+    p.add_argument("--noise_multiplier", type=float, default=0.0,
+                   help="Sigma, i.e. standard dev of noise")
+
+    # ---------------------------------------------------------------- NEW
+    g = p.add_argument_group("commefficient_amd (MI355X) extensions")
+    g.add_argument("--synthetic", action="store_true",
+                   help="use synthetic data shaped like --dataset_name (no files needed)")
+    g.add_argument("--synthetic_size", type=int, default=None,
+                   help="number of synthetic training examples (default: real dataset size)")
+    g.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                   help="compute dtype of forward/backward (master weights stay fp32)")
+    g.add_argument("--merge_clients", choices=["auto", "on", "off"], default="auto",
+                   help="merge the clients of a rank into one forward/backward when the "
+                        "mode is linear per client (exact; see parallel/fed_model.py)")
+    g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
+    g.add_argument("--encode", choices=["binned", "direct"], default="binned",
+                   help="client-side Count-Sketch encode kernel")
+    g.add_argument("--client_state_device", choices=["auto", "gpu", "cpu"], default="auto",
+                   help="where per-client momentum/error/weights live")
+    g.add_argument("--resume", type=str, default=None,
+                   help="resume from a *.fedstate.pt sidecar written with --checkpoint")
+    g.add_argument("--log_every", type=int, default=0,
+                   help="print a progress line every N rounds (0: per epoch only)")
+    g.add_argument("--max_rounds", type=int, default=0,
+                   help="stop after this many training rounds (0: no limit)")
+    g.add_argument("--profile_dir", type=str, default=None,
+                   help="write per-phase HIP-event timings + torch.profiler traces here")
+    g.add_argument("--channels_last", type=int, default=1, help="NHWC activations for convs")
+    return p
+
+
+def validate_args(args) -> None:
+    """Mode-validity constraints (reference asserts)."""
+    def bad(msg):
+        raise ValueError(msg)
+
+    if args.mode == "fedavg":
+        if args.local_batch_size != -1:
+            bad("--mode fedavg requires --local_batch_size -1 (utils.py:225-228)")
+        if args.local_momentum != 0:
+            bad("--mode fedavg requires --local_momentum 0")
+        if args.error_type != "none":
+            bad("--mode fedavg requires --error_type none")
+    if args.mode == "sketch":
+        if args.local_momentum != 0:
+            bad("--mode sketch requires --local_momentum 0: momentum lives in sketch space "
+                "on the server (fed_worker.py:227-228); use --virtual_momentum")
+        if args.error_type == "local":
+            bad("--mode sketch requires --error_type none or virtual (fed_worker.py:221-222)")
+    if args.mode == "true_topk" and args.error_type != "virtual":
+        bad("--mode true_topk requires --error_type virtual (fed_aggregator.py:512)")
+    if args.mode == "local_topk" and args.error_type not in ("local", "none"):
+        bad("--mode local_topk requires --error_type local or none (fed_aggregator.py:545)")
+    if args.mode == "uncompressed" and args.error_type == "local":
+        bad("--mode uncompressed does not support --error_type local (fed_worker.py:221-222)")
+    if args.error_type == "local" and args.virtual_momentum != 0 and args.mode == "sketch":
+        bad("local error requires virtual_momentum 0")
+    if args.num_rows > 16:
+        bad("--num_rows must be <= 16")
+
+
+def parse_args(default_lr: Optional[float] = None, argv: Optional[Sequence[str]] = None,
+               probe_port: bool = True):
+    parser = build_parser(default_lr)
+    args = parser.parse_args(argv)
+    finalize_args(args, probe_port=probe_port)
+    return args
+
+
+def finalize_args(args, probe_port: bool = True):
+    if args.device is None:
+        import torch
+        # device_count() does not initialise the HIP runtime (is_available()
+        # may), so a parent that later spawns ranks stays GPU-clean
+        args.device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
+    # torchrun-provided rendezvous wins; otherwise probe for a free port like
+    # the reference (utils.py:216-223)
+    if "MASTER_PORT" in os.environ:
+        args.port = int(os.environ["MASTER_PORT"])
+    elif probe_port:
+        rng = np.random.RandomState()
+        while is_port_in_use(args.port):
+            args.port += int(rng.randint(1, 1000))
+    validate_args(args)
+    return args
