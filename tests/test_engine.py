@@ -1,0 +1,185 @@
+"""End-to-end engine semantics on CPU against the numpy oracle of all five
+modes (tests/engine_oracle.py), merged-vs-per-client exactness, byte
+accounting and checkpoint round trips."""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from commefficient_amd.parallel import dist
+from commefficient_amd.parallel.fed_model import FedModel
+from commefficient_amd.parallel.server import FedOptimizer
+from commefficient_amd.utils.args import parse_args
+from engine_oracle import LinearFedOracle
+
+
+def lin_loss(model, inputs, targets, args):
+    pred = model(*inputs).squeeze(-1)
+    return (pred - targets) ** 2, [torch.zeros_like(targets)]
+
+
+def make_engine(d, argv, num_clients, lr):
+    dist.init("cpu")
+    args = parse_args(argv=argv + ["--device", "cpu", "--num_clients", str(num_clients),
+                                   "--dtype", "fp32"], probe_port=False)
+    model = nn.Linear(d, 1, bias=False)
+    nn.init.zeros_(model.weight)
+    fed = FedModel(model, lin_loss, args, num_clients=num_clients)
+    opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=lr), args, fed)
+    return fed, opt, args
+
+
+def data(N, d):
+    X = torch.arange(N * d, dtype=torch.float32).view(N, d) / (N * d)
+    y = torch.arange(N, dtype=torch.float32) / N
+    return X, y
+
+
+def split(N, W):
+    cids = torch.zeros(N, dtype=torch.int64)
+    for i in range(W):
+        cids[i * N // W:(i + 1) * N // W] = i
+    return cids
+
+
+CASES = [
+    # mode, extra argv, oracle kwargs
+    ("uncompressed", ["--virtual_momentum", "0.9", "--local_momentum", "0"],
+     dict(rho=0.9)),
+    ("uncompressed", ["--virtual_momentum", "0", "--local_momentum", "0.5"],
+     dict(rho_l=0.5)),
+    ("true_topk", ["--error_type", "virtual", "--virtual_momentum", "0.9", "--local_momentum", "0",
+                   "--k", "2"], dict(rho=0.9, k=2, error_type="virtual")),
+    ("true_topk", ["--error_type", "virtual", "--virtual_momentum", "0", "--local_momentum", "0.9",
+                   "--k", "1"], dict(rho_l=0.9, k=1, error_type="virtual")),
+    ("local_topk", ["--error_type", "local", "--virtual_momentum", "0.5", "--local_momentum", "0.9",
+                    "--k", "2"], dict(rho=0.5, rho_l=0.9, k=2, error_type="local")),
+    ("local_topk", ["--error_type", "none", "--virtual_momentum", "0", "--local_momentum", "0",
+                    "--k", "1"], dict(k=1)),
+    ("fedavg", ["--virtual_momentum", "0.9", "--local_momentum", "0", "--local_batch_size", "-1",
+                "--fedavg_batch_size", "2", "--num_fedavg_epochs", "2"],
+     dict(rho=0.9, fedavg_epochs=2, fedavg_bs=2)),
+    ("sketch", ["--error_type", "virtual", "--virtual_momentum", "0.9", "--local_momentum", "0",
+                "--k", "2", "--num_rows", "1", "--num_cols", "100003", "--num_blocks", "1"],
+     dict(rho=0.9, k=2, error_type="virtual")),
+]
+
+
+@pytest.mark.parametrize("W", [1, 2])
+@pytest.mark.parametrize("wd", [0.0, 5e-3])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_modes_match_numpy_oracle(case, W, wd):
+    mode, extra, okw = CASES[case]
+    N, d, lr = 8, 4, 0.3
+    argv = ["--mode", mode, "--num_workers", str(W), "--weight_decay", str(wd)] + extra
+    if mode != "fedavg":
+        argv += ["--local_batch_size", str(N // W)]
+    fed, opt, args = make_engine(d, argv, W, lr)
+    omode = "sketch_exact" if mode == "sketch" else mode
+    orc = LinearFedOracle(d, omode, wd=wd, num_workers=W, **okw)
+    X, y = data(N, d)
+    cids = split(N, W)
+    clients = [(i, X[cids == i].double().numpy(), y[cids == i].double().numpy()) for i in range(W)]
+    for rnd in range(4):
+        fed((cids, X, y))
+        opt.param_groups[0]["lr"] = lr
+        opt.step()
+        w_exp = orc.round(clients, lr)
+        np.testing.assert_allclose(fed.w.double().numpy(), w_exp, rtol=2e-4, atol=2e-6,
+                                   err_msg=f"round {rnd}")
+
+
+def test_reference_linear_scenario_first_steps():
+    """The unit_test.py:185 scenario (N=4, d=1, one worker, lr 0.005,
+    X=arange, y=arange, squared error) re-derived for mean-gradient
+    semantics: w1 = 0.005*7 = 0.035, w2 = w1 + 0.005*(2*(14 - 14*w1))/4."""
+    fed, opt, _ = make_engine(1, ["--mode", "uncompressed", "--local_momentum", "0",
+                                  "--virtual_momentum", "0", "--weight_decay", "0",
+                                  "--num_workers", "1", "--local_batch_size", "4"], 1, 0.005)
+    X = torch.arange(4, dtype=torch.float32).view(4, 1)
+    y = torch.arange(4, dtype=torch.float32)
+    cids = torch.zeros(4, dtype=torch.int64)
+    fed((cids, X, y))
+    opt.step()
+    assert abs(fed.w.item() - 0.035) < 1e-7
+    fed((cids, X, y))
+    opt.step()
+    w1 = 0.035
+    assert abs(fed.w.item() - (w1 + 0.005 * 2 * (14 - 14 * w1) / 4)) < 1e-6
+
+
+@pytest.mark.parametrize("mode", ["uncompressed", "true_topk", "sketch"])
+def test_merged_equals_per_client(mode):
+    """Merging a rank's clients into one forward/backward is exact."""
+    from commefficient_amd import models
+    from commefficient_amd.train.losses import cv_loss
+    dist.init("cpu")
+    outs = []
+    for merge in ("on", "off"):
+        torch.manual_seed(0)
+        argv = ["--mode", mode, "--local_momentum", "0", "--virtual_momentum", "0.9",
+                "--error_type", "virtual" if mode != "uncompressed" else "none", "--k", "500",
+                "--num_rows", "3", "--num_cols", "4000", "--num_workers", "4",
+                "--local_batch_size", "3", "--device", "cpu", "--dtype", "fp32",
+                "--num_clients", "4", "--merge_clients", merge, "--weight_decay", "5e-4"]
+        args = parse_args(argv=argv, probe_port=False)
+        model = models.ResNet9(channels={"prep": 4, "layer1": 8, "layer2": 8, "layer3": 16})
+        fed = FedModel(model, cv_loss, args, num_clients=4)
+        opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), args, fed)
+        g = torch.Generator().manual_seed(1)
+        X = torch.randn(12, 3, 32, 32, generator=g)
+        y = torch.randint(0, 10, (12,), generator=g)
+        cids = torch.tensor([0, 0, 0, 1, 1, 1, 2, 2, 2, 3, 3, 3])
+        res = fed((cids, X, y))
+        opt.step()
+        outs.append((fed.w.clone(), res[0].clone()))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-6)
+
+
+def test_byte_accounting_matches_reference_formulas():
+    fed, opt, args = make_engine(4, ["--mode", "true_topk", "--error_type", "virtual",
+                                     "--local_momentum", "0", "--k", "1", "--num_workers", "2",
+                                     "--local_batch_size", "2"], 4, 0.3)
+    X, y = data(8, 4)
+    # round 0: clients 0,1 (never seen anything changed) -> 0 download
+    cids = torch.tensor([0, 0, 1, 1, 0, 0, 1, 1])
+    _, _, dl, ul = fed((cids, X, y))
+    opt.step()
+    assert dl.tolist() == [0.0, 0.0]
+    assert ul == 2 * 4 * 4  # 4 bytes * d per client in true_topk
+    # round 1: clients 1,2. client 1 saw round 0's weights: 1 coord changed since;
+    # client 2 starts from the initial weights: same 1 coord
+    cids = torch.tensor([1, 1, 2, 2, 1, 1, 2, 2])
+    _, _, dl, _ = fed((cids, X, y))
+    opt.step()
+    assert dl.tolist() == [4.0, 4.0]
+    # round 2: client 0 last saw round 0 -> changes of rounds 0 and 1 (1 or 2 coords)
+    cids = torch.tensor([0, 0, 3, 3, 0, 0, 3, 3])
+    _, _, dl, _ = fed((cids, X, y))
+    changed = int((fed.w != 0).sum())
+    assert dl.tolist() == [4.0 * changed, 4.0 * changed]
+
+
+def test_checkpoint_state_dict_format(tmp_path):
+    from commefficient_amd import models
+    m = models.ResNet9()
+    keys = list(m.state_dict().keys())
+    assert keys[0] == "n.prep.conv.weight" and keys[-1] == "n.linear.weight"
+    fed, opt, args = make_engine(3, ["--mode", "uncompressed", "--local_momentum", "0",
+                                     "--num_workers", "1", "--local_batch_size", "2"], 1, 0.1)
+    X, y = data(2, 3)
+    fed((torch.zeros(2, dtype=torch.int64), X, y))
+    opt.step()
+    p = tmp_path / "ckpt.pt"
+    torch.save(fed.state_dict(), p)
+    sd = torch.load(p, weights_only=True)
+    torch.testing.assert_close(sd["weight"].view(-1), fed.w)
+    fs = fed.fed_state_dict()
+    torch.save(fs, tmp_path / "f.pt")
+    fs2 = torch.load(tmp_path / "f.pt", weights_only=True)
+    fed2, _, _ = make_engine(3, ["--mode", "uncompressed", "--local_momentum", "0",
+                                 "--num_workers", "1", "--local_batch_size", "2"], 1, 0.1)
+    fed2.load_fed_state_dict(fs2)
+    torch.testing.assert_close(fed2.w, fed.w)
+    assert fed2.round_idx == 1
