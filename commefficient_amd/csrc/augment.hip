@@ -7,8 +7,9 @@
 // (CIFAR-10 is 150 MB of 288 GB) and one kernel gathers the batch by index,
 // applies reflect-pad random crop + horizontal flip + normalisation, and
 // writes bf16 channels_last (NHWC) -- the layout the convolutions consume.
-// Randomness is a counter hash of (seed, batch slot): reproducible and
-// identical on every rank for the same seed.
+// Randomness is a counter hash of (seed, per-example key) -- the key is the
+// example's position in the round, so the result does not depend on how the
+// round's clients are split over ranks.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <cstdint>
@@ -41,7 +42,8 @@ __device__ __forceinline__ uint16_t to_bf16(float f) {
 __global__ void __launch_bounds__(256)
 augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx, int64_t B,
                int H, int W, int C, int pad, int flip, const float* __restrict__ mean,
-               const float* __restrict__ inv_std, uint64_t seed, uint16_t* __restrict__ out) {
+               const float* __restrict__ inv_std, uint64_t seed, const int64_t* __restrict__ keys,
+               uint16_t* __restrict__ out) {
   const int64_t npix = B * H * W;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   float m[4], s[4];
@@ -53,7 +55,8 @@ augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx
     const int64_t b = p / (H * W);
     const int rem = static_cast<int>(p - b * H * W);
     const int y = rem / W, x = rem - (rem / W) * W;
-    uint32_t rnd = mix32(seed * 0x9E3779B97F4A7C15ull + static_cast<uint64_t>(b));
+    const uint64_t key = keys != nullptr ? static_cast<uint64_t>(keys[b]) : static_cast<uint64_t>(b);
+    uint32_t rnd = mix32(seed * 0x9E3779B97F4A7C15ull + key);
     int dy = 0, dx = 0;
     bool fl = false;
     if (pad > 0) {
@@ -77,13 +80,14 @@ augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx
 
 void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx, int64_t B, int H, int W,
                             int C, int pad, int flip, const float* mean, const float* inv_std,
-                            uint64_t seed, uint16_t* out_bf16, hipStream_t stream) {
+                            uint64_t seed, const int64_t* keys, uint16_t* out_bf16,
+                            hipStream_t stream) {
   if (B <= 0) return;
   int64_t npix = B * H * W;
   int64_t blocks = (npix + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(augment_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
-                     data, idx, B, H, W, C, pad, flip, mean, inv_std, seed, out_bf16);
+                     data, idx, B, H, W, C, pad, flip, mean, inv_std, seed, keys, out_bf16);
 }
 
 }  // namespace commeff

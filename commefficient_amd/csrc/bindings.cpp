@@ -21,6 +21,13 @@ void check_f32(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+const int64_t* key_ptr(const c10::optional<at::Tensor>& k, int64_t n) {
+  if (!k.has_value() || !k->defined()) return nullptr;
+  TORCH_CHECK(k->scalar_type() == at::kLong && k->is_contiguous() && k->numel() == n,
+              "keys must be contiguous int64 [B]");
+  return k->data_ptr<int64_t>();
+}
+
 float* fptr(const c10::optional<at::Tensor>& t) {
   return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
 }
@@ -209,7 +216,7 @@ at::Tensor scatter_dense_cpu(const at::Tensor& idx, const at::Tensor& vals, int6
 
 at::Tensor augment_cpu(const at::Tensor& data, const at::Tensor& idx, int64_t pad, bool flip,
                        const at::Tensor& mean, const at::Tensor& inv_std, int64_t seed,
-                       bool out_bf16) {
+                       bool out_bf16, const c10::optional<at::Tensor>& keys) {
   TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.is_contiguous(),
               "data must be uint8 [N,H,W,C] contiguous");
   const int64_t B = idx.numel(), H = data.size(1), W = data.size(2), C = data.size(3);
@@ -218,7 +225,7 @@ at::Tensor augment_cpu(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   cpu::augment_u8_nhwc(data.data_ptr<uint8_t>(), idx.contiguous().data_ptr<int64_t>(), B,
                        static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                        static_cast<int>(pad), flip ? 1 : 0, mc.data_ptr<float>(),
-                       sc.data_ptr<float>(), static_cast<uint64_t>(seed),
+                       sc.data_ptr<float>(), static_cast<uint64_t>(seed), key_ptr(keys, B),
                        out.data_ptr<float>());
   auto o = out.permute({0, 3, 1, 2});  // logical NCHW, physical NHWC
   return out_bf16 ? o.to(at::kBFloat16) : o;
@@ -405,7 +412,7 @@ at::Tensor scatter_dense_hip(const at::Tensor& idx, const at::Tensor& vals, int6
 
 at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pad, bool flip,
                        const at::Tensor& mean, const at::Tensor& inv_std, int64_t seed,
-                       bool out_bf16) {
+                       bool out_bf16, const c10::optional<at::Tensor>& keys) {
   TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.is_contiguous(),
               "data must be uint8 [N,H,W,C] contiguous");
   TORCH_CHECK(data.size(3) <= 4, "at most 4 channels");
@@ -418,7 +425,7 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   launch_augment_u8_nhwc(data.data_ptr<uint8_t>(), ic.data_ptr<int64_t>(), B,
                          static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                          static_cast<int>(pad), flip ? 1 : 0, mc.data_ptr<float>(),
-                         sc.data_ptr<float>(), static_cast<uint64_t>(seed),
+                         sc.data_ptr<float>(), static_cast<uint64_t>(seed), key_ptr(keys, B),
                          reinterpret_cast<uint16_t*>(out.data_ptr()), cur_stream());
   auto o = out.permute({0, 3, 1, 2});
   return out_bf16 ? o : o.to(at::kFloat);
@@ -455,7 +462,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("zero_at(Tensor(a!)? a, Tensor(b!)? b, Tensor(c!)? c, Tensor idx) -> ()");
   m.def("scatter_dense(Tensor idx, Tensor vals, int n) -> Tensor");
   m.def("augment_u8_nhwc(Tensor data, Tensor idx, int pad, bool flip, Tensor mean, Tensor inv_std, "
-        "int seed, bool out_bf16) -> Tensor");
+        "int seed, bool out_bf16, Tensor? keys=None) -> Tensor");
   m.def("binned_scratch_bytes(int d, int r, int c, int num_blocks) -> int",
         &commeff::binned_scratch_bytes);
 }

@@ -222,7 +222,7 @@ void client_state(const float* g, float* u, float* e, int64_t n, float rho) {
 
 void augment_u8_nhwc(const uint8_t* data, const int64_t* idx, int64_t B, int H, int W, int C,
                      int pad, int flip, const float* mean, const float* inv_std, uint64_t seed,
-                     float* out) {
+                     const int64_t* keys, float* out) {
   // same random stream as the GPU kernel (splitmix-style finaliser of
   // seed*golden + slot)
   auto mix32 = [](uint64_t x) {
@@ -240,7 +240,8 @@ void augment_u8_nhwc(const uint8_t* data, const int64_t* idx, int64_t B, int H, 
   };
   at::parallel_for(0, B, 1, [&](int64_t b0, int64_t b1) {
     for (int64_t b = b0; b < b1; ++b) {
-      uint32_t rnd = mix32(seed * 0x9E3779B97F4A7C15ull + static_cast<uint64_t>(b));
+      const uint64_t key = keys ? static_cast<uint64_t>(keys[b]) : static_cast<uint64_t>(b);
+      uint32_t rnd = mix32(seed * 0x9E3779B97F4A7C15ull + key);
       int dy = 0, dx = 0;
       if (pad > 0) {
         dy = static_cast<int>(rnd % (2 * pad + 1));

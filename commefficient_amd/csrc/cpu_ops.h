@@ -29,6 +29,6 @@ void clip_noise(float* x, int64_t n, const float* norm, float clip, float noise_
 void client_state(const float* g, float* u, float* e, int64_t n, float rho);
 void augment_u8_nhwc(const uint8_t* data, const int64_t* idx, int64_t B, int H, int W, int C,
                      int pad, int flip, const float* mean, const float* inv_std, uint64_t seed,
-                     float* out);
+                     const int64_t* keys, float* out);
 }  // namespace cpu
 }  // namespace commeff

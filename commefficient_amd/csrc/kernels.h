@@ -96,10 +96,11 @@ void launch_scatter_dense(float* out, int64_t n, const int64_t* idx,
 // -------------------------------------------------------------- augment --
 // CIFAR-style augmentation of uint8 NHWC images into a bf16 NHWC
 // (channels_last) batch: reflect-pad `pad`, random crop, random h-flip,
-// normalise.  Randomness: counter hash of (seed, example slot).
+// normalise.  Randomness: counter hash of (seed, keys[b] or b).
 void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx,
                             int64_t B, int H, int W, int C, int pad,
                             int flip, const float* mean, const float* inv_std,
-                            uint64_t seed, uint16_t* out_bf16, hipStream_t stream);
+                            uint64_t seed, const int64_t* keys, uint16_t* out_bf16,
+                            hipStream_t stream);
 
 }  // namespace commeff

@@ -38,12 +38,19 @@ class DeviceImageSource:
         self.flip = flip if augment else False
         self.out_bf16 = out_bf16 and self.device.type == "cuda"
 
-    def gather(self, rows: np.ndarray, seed: int):
-        idx = torch.from_numpy(np.asarray(rows, dtype=np.int64))
+    def gather(self, rows: np.ndarray, seed: int, keys: Optional[np.ndarray] = None):
+        """Batch of ``rows``; ``keys`` (default: slot index) key the per-example
+        random crop/flip, so an example's augmentation does not depend on
+        which rank materialises it."""
+        host = np.asarray(rows, dtype=np.int64)
+        if keys is not None:
+            host = np.stack([host, np.asarray(keys, dtype=np.int64)])
+        t = torch.from_numpy(host)
         if self.device.type == "cuda":
-            idx = idx.pin_memory().to(self.device, non_blocking=True)
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        idx, kt = (t[0], t[1]) if keys is not None else (t, None)
         x = ops.augment_u8_nhwc(self.data, idx, self.pad, self.flip, self.mean, self.inv_std,
-                                seed, self.out_bf16)
+                                seed, self.out_bf16, kt)
         y = self.targets[idx]
         return x, y
 
@@ -75,8 +82,8 @@ class DeviceFedLoader:
         src = self.source
 
         def take(pos, rows=rows, seed=rnd_seed):
-            # seed by round; the kernel further mixes in the batch slot
-            return src.gather(rows[pos], seed * 7 + int(pos[0]) if len(pos) else seed)
+            # seed by round, key by the example's position in the round
+            return src.gather(rows[pos], seed, keys=pos)
 
         return RoundBatch(cids, take, n_inputs=1)
 

@@ -72,6 +72,6 @@ def scatter_dense(idx, vals, n):
     return _ops().scatter_dense(idx, vals, int(n))
 
 
-def augment_u8_nhwc(data, idx, pad, flip, mean, inv_std, seed, out_bf16=True):
+def augment_u8_nhwc(data, idx, pad, flip, mean, inv_std, seed, out_bf16=True, keys=None):
     return _ops().augment_u8_nhwc(data, idx, int(pad), bool(flip), mean, inv_std, int(seed),
-                                  bool(out_bf16))
+                                  bool(out_bf16), keys)

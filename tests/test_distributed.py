@@ -1,0 +1,75 @@
+"""Multi-process SPMD on CPU/gloo (world_size 2): the BASELINE.json "plumbing"
+configuration.  Two ranks must end with bit-identical replicated weights that
+equal a single-process run of the same rounds."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(rank, world, port, mode, out_dir, rounds):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(2)
+    from commefficient_amd import models
+    from commefficient_amd.data import make_synthetic
+    from commefficient_amd.data.device_loader import DeviceFedLoader
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd.train.losses import cv_loss
+    from commefficient_amd.utils.args import parse_args
+    dist.init("cpu")
+    extra = {"uncompressed": ["--local_momentum", "0", "--virtual_momentum", "0.9"],
+             "sketch": ["--error_type", "virtual", "--local_momentum", "0", "--virtual_momentum",
+                        "0.9", "--k", "300", "--num_rows", "3", "--num_cols", "2000"],
+             "local_topk": ["--error_type", "local", "--local_momentum", "0.9", "--k", "300"],
+             "fedavg": ["--local_momentum", "0", "--virtual_momentum", "0.5",
+                        "--fedavg_batch_size", "2"]}[mode]
+    lbs = "-1"
+    args = parse_args(argv=["--mode", mode, "--device", "cpu", "--dtype", "fp32",
+                            "--num_clients", "40", "--num_workers", "6", "--local_batch_size", lbs,
+                            "--dataset_name", "CIFAR10", "--synthetic"] + extra, probe_port=False)
+    torch.manual_seed(0)
+    model = models.ResNet9(channels={"prep": 4, "layer1": 8, "layer2": 8, "layer3": 16})
+    ds = make_synthetic("CIFAR10", train=True, num_clients=40, size=160, seed=3)
+    loader = DeviceFedLoader(ds, 6, -1, "cpu", seed=5, augment=True)
+    fed = FedModel(model, cv_loss, args, num_clients=40)
+    opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05), args, fed)
+    it = iter(loader)
+    losses = []
+    for _ in range(rounds):
+        loss, acc, dl, ul = fed(next(it))
+        opt.step()
+        losses.append(loss.clone())
+    torch.save({"w": fed.w.clone(), "loss": torch.stack(losses),
+                "dl": fed.accountant.client_download.clone()},
+               os.path.join(out_dir, f"r{rank}_w{world}.pt"))
+    dist.shutdown()
+
+
+@pytest.mark.parametrize("mode", ["uncompressed", "sketch", "local_topk", "fedavg"])
+def test_gloo_two_ranks_match_single_process(mode):
+    rounds = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_run, args=(2, _free_port(), mode, d, rounds), nprocs=2,
+                           start_method="spawn", join=True)
+        mp.start_processes(_run, args=(1, _free_port(), mode, d, rounds), nprocs=1,
+                           start_method="spawn", join=True)
+        r0 = torch.load(os.path.join(d, "r0_w2.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "r1_w2.pt"), weights_only=True)
+        s = torch.load(os.path.join(d, "r0_w1.pt"), weights_only=True)
+    assert torch.equal(r0["w"], r1["w"]), "replicas diverged"
+    torch.testing.assert_close(r0["w"], s["w"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(r0["loss"], s["loss"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(r0["dl"], s["dl"])
