@@ -1,0 +1,66 @@
+"""Round loaders for the PersonaChat datasets: the host builds token records
+only for the rows this rank computes, pads them to the selection's max length
+and ships one pinned H2D copy (non_blocking) per tensor."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..parallel.fed_model import RoundBatch
+from .fed_dataset import FedSampler
+from .fed_persona import collate
+
+
+def _to_dev(ts, device):
+    out = []
+    for t in ts:
+        if torch.device(device).type == "cuda":
+            t = t.pin_memory().to(device, non_blocking=True)
+        out.append(t)
+    return out
+
+
+class PersonaFedLoader:
+    def __init__(self, dataset, num_workers, local_batch_size, device, seed):
+        self.dataset = dataset
+        self.sampler = FedSampler(dataset, num_workers, local_batch_size, seed=seed)
+        self.device = device
+
+    def __len__(self):
+        return len(self.dataset)
+
+    def __iter__(self):
+        for r in self.sampler:
+            yield self.make_batch(r)
+
+    def make_batch(self, r):
+        ds, dev = self.dataset, self.device
+        cids = ds.client_of(r)
+
+        def take(pos, r=r):
+            recs = [ds[int(i)][1] for i in r[pos]]
+            ids, mc, lab, mcl, tt = _to_dev(collate(recs), dev)
+            return ids, mc, lab, tt, mcl
+
+        return RoundBatch(cids, take, n_inputs=4)
+
+
+class PersonaValLoader:
+    def __init__(self, dataset, batch_size, device):
+        self.dataset, self.batch_size, self.device = dataset, batch_size, device
+
+    def __len__(self):
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = len(self.dataset)
+        for s in range(0, n, self.batch_size):
+            rows = np.arange(s, min(n, s + self.batch_size))
+            ds, dev = self.dataset, self.device
+
+            def take(pos, rows=rows):
+                recs = [ds[int(i)][1] for i in rows[pos]]
+                ids, mc, lab, mcl, tt = _to_dev(collate(recs), dev)
+                return ids, mc, lab, tt, mcl
+
+            yield RoundBatch(np.full(len(rows), -1, dtype=np.int64), take, n_inputs=4)

@@ -1,0 +1,152 @@
+"""GPT-2 federated training driver (the reference's gpt2_train.py:115-365).
+
+Double-heads GPT-2 (LM + multiple choice) on PersonaChat, one client per
+personality, linear LR decay from ``lr_scale`` (default 4e-2) to 0, per-round
+logging, HF ``save_pretrained`` of the server weights after each epoch,
+validation reporting nll / acc / ppl = exp(mean nll) (gpt2_train.py:149-253).
+``--finetune`` only evaluates a saved model (gpt2_train.py:308-309).
+With ``--synthetic`` PersonaChat-shaped token data is generated (no tokenizer
+or downloads needed); otherwise the reference on-disk layout is read with a
+local HF tokenizer directory given by ``--model_checkpoint``.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..data.fed_persona import SPECIAL_TOKENS, FedPERSONA, SyntheticPersona
+from ..data.persona_loader import PersonaFedLoader, PersonaValLoader
+from ..models.gpt2 import ATTR_TO_SPECIAL_TOKEN, GPT2DoubleHeads
+from ..parallel import dist
+from ..parallel.fed_model import FedModel
+from ..parallel.server import FedOptimizer
+from ..utils import (ScalarWriter, TableLogger, Timer, linear_decay_lambda, make_logdir,
+                     steps_per_epoch)
+from .losses import gpt2_loss_train, gpt2_loss_val
+
+
+def get_data_loaders(args, device, tokenizer=None):
+    if args.synthetic:
+        n_pers = args.num_clients or 1000
+        tr = SyntheticPersona(num_personalities=n_pers, num_candidates=args.num_candidates,
+                              max_history=args.max_history, train=True, do_iid=args.do_iid,
+                              num_clients=args.num_clients, seed=args.seed)
+        te = SyntheticPersona(num_personalities=n_pers, num_candidates=args.num_candidates,
+                              max_history=args.max_history, train=False, seed=args.seed,
+                              n_val=max(args.valid_batch_size * args.num_workers, 200))
+    else:
+        tr = FedPERSONA(tokenizer, args.num_candidates, args.max_history,
+                        args.personality_permutations, args.dataset_dir, "PERSONA", None,
+                        args.do_iid, args.num_clients, train=True, download=True, seed=args.seed)
+        te = FedPERSONA(tokenizer, -1, args.max_history, 1, args.dataset_dir, "PERSONA",
+                        None, train=False)
+    train = PersonaFedLoader(tr, args.num_workers, args.local_batch_size, device, args.seed)
+    test = PersonaValLoader(te, args.valid_batch_size * args.num_workers, device)
+    return train, test
+
+
+def run_batches(model, opt, sched, loader, training, args, writer=None, log_step0=0):
+    model.train(training)
+    losses, accs = [], []
+    ctx = dist.ctx()
+    if training:
+        spe = steps_per_epoch(args.local_batch_size, loader.dataset, args.num_workers)
+        t0 = time.time()
+        for i, batch in enumerate(loader):
+            if i >= spe or (args.max_rounds and model.round_idx >= args.max_rounds):
+                break
+            sched.step()
+            if args.local_batch_size == -1:
+                if len(np.unique(batch.client_ids)) < args.num_workers:
+                    continue
+            elif len(batch) < args.num_workers * args.local_batch_size:
+                continue
+            loss, acc, dl, ul = model(batch)
+            opt.step()
+            losses.append(loss)
+            accs.append(acc)
+            if writer is not None and ctx.is_main:
+                writer.add_scalar("training/loss", loss.mean().item(), log_step0 + i)
+            if args.log_every and (i + 1) % args.log_every == 0 and ctx.is_main:
+                print("round {} loss {:.4f} ({:.2f} s/round)".format(
+                    model.round_idx, loss.mean().item(), (time.time() - t0) / (i + 1)))
+            if args.do_test and i >= 2:
+                break
+    else:
+        for i, batch in enumerate(loader):
+            nll, acc = model(batch)[:2]
+            losses.append(nll)
+            accs.append(acc)
+            if args.do_test and i >= 2:
+                break
+    if not losses:
+        return float("nan"), float("nan")
+    return torch.cat(losses).mean().item(), torch.cat(accs).mean().item()
+
+
+def main(args):
+    ctx = dist.init(args.device, port=args.port)
+    timer = Timer()
+    torch.manual_seed(args.seed)
+    np.random.seed(args.seed)
+    if args.lr_scale is None:
+        args.lr_scale = 4e-2
+    args.dataset_name = "PERSONA"
+    tokenizer = None
+    if not args.synthetic:
+        from transformers import AutoTokenizer
+        tokenizer = AutoTokenizer.from_pretrained(args.model_checkpoint)
+        tokenizer.add_special_tokens(ATTR_TO_SPECIAL_TOKEN)
+    tiny = args.do_test or args.gpt2_size == "tiny"
+    model = GPT2DoubleHeads(args.model_checkpoint if not args.do_test else "gpt2",
+                            **({"n_layer": 2, "n_embd": 64, "n_head": 2} if tiny else {}))
+    if tokenizer is not None:
+        model.model.resize_token_embeddings(len(tokenizer))
+    args.len_tokenizer = model.model.config.vocab_size
+    train_loader, test_loader = get_data_loaders(args, ctx.device, tokenizer)
+    if args.num_clients is None:
+        args.num_clients = train_loader.dataset.num_clients
+    opt = torch.optim.SGD(model.parameters(), lr=1)
+    fed = FedModel(model, gpt2_loss_train, args, gpt2_loss_val, num_clients=args.num_clients)
+    fopt = FedOptimizer(opt, args, fed)
+    spe = steps_per_epoch(args.local_batch_size, train_loader.dataset, args.num_workers)
+    sched = torch.optim.lr_scheduler.LambdaLR(fopt, lr_lambda=linear_decay_lambda(args, spe))
+    log_dir = make_logdir(args)
+    writer = ScalarWriter(log_dir) if ctx.is_main else None
+    if ctx.is_main:
+        print("Finished initializing in {:.2f} seconds".format(timer()))
+    logger = TableLogger()
+    if args.do_finetune:
+        nll, acc = run_batches(fed, None, None, test_loader, False, args)
+        if ctx.is_main:
+            print({"nll": nll, "acc": acc, "ppl": math.exp(nll)})
+        return fed
+    for epoch in range(math.ceil(args.num_epochs)):
+        d0 = fed.accountant.client_download.sum().item()
+        u0 = fed.accountant.client_upload.sum().item()
+        tl, ta = run_batches(fed, fopt, sched, train_loader, True, args, writer, epoch * int(spe))
+        ttime = timer()
+        down = (fed.accountant.client_download.sum().item() - d0) / 2 ** 20
+        up = (fed.accountant.client_upload.sum().item() - u0) / 2 ** 20
+        if ctx.is_main:
+            fed.save_pretrained(log_dir)
+        nll, acc = run_batches(fed, None, None, test_loader, False, args)
+        if ctx.is_main:
+            logger.append({"epoch": epoch + 1, "train_time": ttime, "train_loss": tl,
+                           "val_nll": nll, "val_acc": acc, "val_ppl": math.exp(min(nll, 50)),
+                           "down (MiB)": round(down), "up (MiB)": round(up),
+                           "total_time": timer.total_time})
+            if writer is not None:
+                writer.add_scalar("validation/nll", nll, epoch)
+                writer.add_scalar("validation/acc", acc, epoch)
+                writer.add_scalar("validation/ppl", math.exp(min(nll, 50)), epoch)
+        if args.max_rounds and fed.round_idx >= args.max_rounds:
+            break
+    fed.finalize()
+    if writer is not None:
+        writer.close()
+    return fed
