@@ -23,7 +23,10 @@ def topk_mask(v, k):
 
 class LinearFedOracle:
     def __init__(self, d, mode, k=1, rho=0.0, rho_l=0.0, error_type="none", wd=0.0,
-                 num_workers=1, fedavg_lr=0.0, fedavg_epochs=1, fedavg_bs=-1):
+                 num_workers=1, fedavg_lr=0.0, fedavg_epochs=1, fedavg_bs=-1, topk_down=False,
+                 max_grad_norm=None, dp_clip=None):
+        self.topk_down, self.max_grad_norm, self.dp_clip = topk_down, max_grad_norm, dp_clip
+        self.wc = {}
         self.d, self.mode, self.k = d, mode, k
         self.rho, self.rho_l, self.et, self.wd, self.W = rho, rho_l, error_type, wd, num_workers
         self.w = np.zeros(d)
@@ -35,7 +38,17 @@ class LinearFedOracle:
 
     def mean_grad(self, w, X, y):
         r = X @ w - y
-        return (2 * X * r[:, None]).mean(0) + self.wd / self.W * w
+        g = (2 * X * r[:, None]).mean(0)
+        if self.max_grad_norm is not None and self.mode != "sketch_exact":
+            nrm = np.linalg.norm(g)
+            if nrm > self.max_grad_norm:
+                g = g * (self.max_grad_norm / nrm)
+        g = g + self.wd / self.W * w
+        if self.dp_clip is not None:  # utils.clip_grad, noise_multiplier 0
+            nrm = np.linalg.norm(g)
+            if nrm > self.dp_clip:
+                g = g * (self.dp_clip / nrm)
+        return g
 
     def round(self, clients, lr):
         """clients: list of (client_id, X[n,d], y[n])"""
@@ -54,7 +67,13 @@ class LinearFedOracle:
                         step += 1
                 tot += (self.w - wl) * n
                 continue
-            g = self.mean_grad(self.w, X, y) * n
+            wloc = self.w
+            if self.topk_down:  # fed_worker.py:232-247, state written back
+                wc = self.wc.setdefault(c, np.zeros(self.d))
+                diff = self.w - wc
+                wc[:] = wc + np.where(topk_mask(diff, self.k), diff, 0.0)
+                wloc = wc.copy()
+            g = self.mean_grad(wloc, X, y) * n
             t = g
             if self.rho_l > 0:
                 u = self.u.setdefault(c, np.zeros(self.d))

@@ -89,6 +89,40 @@ def test_modes_match_numpy_oracle(case, W, wd):
                                    err_msg=f"round {rnd}")
 
 
+EXTRA_CASES = [
+    ("uncompressed", ["--topk_down", "--k", "2", "--local_momentum", "0",
+                      "--virtual_momentum", "0.5"], dict(topk_down=True, k=2, rho=0.5)),
+    ("local_topk", ["--topk_down", "--k", "2", "--error_type", "local", "--local_momentum", "0"],
+     dict(topk_down=True, k=2, error_type="local")),
+    ("uncompressed", ["--max_grad_norm", "0.05", "--local_momentum", "0"],
+     dict(max_grad_norm=0.05)),
+    ("true_topk", ["--dp", "--l2_norm_clip", "0.02", "--noise_multiplier", "0",
+                   "--error_type", "virtual", "--local_momentum", "0", "--k", "2"],
+     dict(dp_clip=0.02, k=2, error_type="virtual")),
+    ("uncompressed", ["--microbatch_size", "1", "--local_momentum", "0"], dict()),
+]
+
+
+@pytest.mark.parametrize("W", [1, 2])
+@pytest.mark.parametrize("case", range(len(EXTRA_CASES)))
+def test_client_side_options_match_oracle(case, W):
+    mode, extra, okw = EXTRA_CASES[case]
+    N, d, lr, wd = 8, 4, 0.3, 5e-3
+    argv = ["--mode", mode, "--num_workers", str(W), "--weight_decay", str(wd),
+            "--local_batch_size", str(N // W)] + extra
+    fed, opt, args = make_engine(d, argv, W, lr)
+    orc = LinearFedOracle(d, mode, wd=wd, num_workers=W, **okw)
+    X, y = data(N, d)
+    cids = split(N, W)
+    clients = [(i, X[cids == i].double().numpy(), y[cids == i].double().numpy()) for i in range(W)]
+    for rnd in range(4):
+        fed((cids, X, y))
+        opt.step()
+        w_exp = orc.round(clients, lr)
+        np.testing.assert_allclose(fed.w.double().numpy(), w_exp, rtol=2e-4, atol=2e-6,
+                                   err_msg=f"round {rnd}")
+
+
 def test_reference_linear_scenario_first_steps():
     """The unit_test.py:185 scenario (N=4, d=1, one worker, lr 0.005,
     X=arange, y=arange, squared error) re-derived for mean-gradient
