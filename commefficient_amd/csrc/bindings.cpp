@@ -1,9 +1,11 @@
 // torch.ops.commeff.* registrations: one schema per op, a CPU kernel (native
 // C++, cpu_ops.cpp) and a CUDA-dispatch-key kernel (HIP launchers for gfx950).
-// On ROCm builds of PyTorch HIP tensors dispatch under the CUDA key.
+// On ROCm builds of PyTorch HIP tensors dispatch under the CUDA key and report
+// DeviceType::CUDA, so the device guard / current stream come from the
+// "MasqueradingAsCUDA" HIP classes.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
 #include <cstring>
@@ -14,7 +16,7 @@
 namespace commeff {
 namespace {
 
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 void check_f32(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
@@ -239,7 +241,7 @@ void cs_encode_hip(at::Tensor table, const at::Tensor& vec, const at::Tensor& ha
                    const c10::optional<at::Tensor>& scratch) {
   check_f32(table, "table");
   check_f32(vec, "vec");
-  c10::hip::HIPGuard guard(table.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, vec.numel(), table.size(-1), true);
   TORCH_CHECK(table.numel() == static_cast<int64_t>(ctx.geom.r) * ctx.geom.c, "table shape");
   if (wvec.has_value() && wvec->defined()) check_f32(*wvec, "wvec");
@@ -263,7 +265,7 @@ at::Tensor cs_query_hip(const at::Tensor& table, const at::Tensor& hashes,
                         const at::Tensor& blk_off, const at::Tensor& blk_sign,
                         int64_t num_blocks, int64_t d) {
   check_f32(table, "table");
-  c10::hip::HIPGuard guard(table.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, table.size(-1), true);
   auto est = at::empty({d}, table.options());
   launch_cs_query(table.data_ptr<float>(), est.data_ptr<float>(), ctx.rows, ctx.geom, ctx.blk_off,
@@ -276,7 +278,7 @@ void cs_zero_buckets_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2,
                          const at::Tensor& hashes, const at::Tensor& blk_off,
                          const at::Tensor& blk_sign, int64_t num_blocks, int64_t d) {
   check_f32(t1, "t1");
-  c10::hip::HIPGuard guard(t1.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(t1.device());
   auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, t1.size(-1), true);
   launch_cs_zero_buckets(t1.data_ptr<float>(), fptr(t2), idx.data_ptr<int64_t>(), fptr(vals),
                          idx.numel(), ctx.rows, ctx.geom, ctx.blk_off, ctx.blk_sign,
@@ -285,7 +287,7 @@ void cs_zero_buckets_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2,
 
 at::Tensor cs_l2estimate_hip(const at::Tensor& table) {
   check_f32(table, "table");
-  c10::hip::HIPGuard guard(table.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   const int r = static_cast<int>(table.size(0));
   TORCH_CHECK(r <= kMaxRows, "rows");
   auto partial = at::empty({r * 256}, table.options());
@@ -297,7 +299,7 @@ at::Tensor cs_l2estimate_hip(const at::Tensor& table) {
 
 std::tuple<at::Tensor, at::Tensor> topk_abs_hip(const at::Tensor& x, int64_t k) {
   check_f32(x, "x");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t n = x.numel();
   const int64_t kk = std::max<int64_t>(0, std::min(k, n));
   auto idx = at::empty({kk}, x.options().dtype(at::kLong));
@@ -319,7 +321,7 @@ void momentum_ef_hip(at::Tensor V, const c10::optional<at::Tensor>& E, const at:
   check_f32(V, "V");
   check_f32(G, "G");
   TORCH_CHECK(mode == 0 || (E.has_value() && E->numel() == V.numel()), "E required for mode>0");
-  c10::hip::HIPGuard guard(V.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(V.device());
   launch_momentum_ef(V.data_ptr<float>(), fptr(E), G.data_ptr<float>(), V.numel(),
                      static_cast<float>(rho), static_cast<float>(gscale), static_cast<int>(mode),
                      cur_stream());
@@ -329,7 +331,7 @@ void sparse_apply_hip(at::Tensor w, const at::Tensor& idx, const at::Tensor& val
                       const c10::optional<at::Tensor>& lr_vec,
                       const c10::optional<at::Tensor>& last_mod, int64_t round) {
   check_f32(w, "w");
-  c10::hip::HIPGuard guard(w.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   launch_sparse_apply(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                       idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
@@ -341,7 +343,7 @@ void dense_apply_hip(at::Tensor w, const at::Tensor& delta, double lr,
                      const c10::optional<at::Tensor>& last_mod, int64_t round) {
   check_f32(w, "w");
   check_f32(delta, "delta");
-  c10::hip::HIPGuard guard(w.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   launch_dense_apply(w.data_ptr<float>(), delta.data_ptr<float>(), w.numel(),
                      static_cast<float>(lr), fptr(lr_vec), lm, static_cast<int32_t>(round),
@@ -349,7 +351,7 @@ void dense_apply_hip(at::Tensor w, const at::Tensor& delta, double lr,
 }
 
 at::Tensor count_ge_hip(const at::Tensor& last_mod, const at::Tensor& thr) {
-  c10::hip::HIPGuard guard(last_mod.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(last_mod.device());
   auto thr_c = thr.to(last_mod.device(), at::kInt).contiguous();
   const int T = static_cast<int>(thr_c.numel());
   TORCH_CHECK(T <= 1024, "count_ge supports at most 1024 thresholds per call");
@@ -364,14 +366,14 @@ void axpby_hip(at::Tensor out, const at::Tensor& a, double alpha,
                const c10::optional<at::Tensor>& b, double beta) {
   check_f32(out, "out");
   check_f32(a, "a");
-  c10::hip::HIPGuard guard(out.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
   launch_axpby(out.data_ptr<float>(), a.data_ptr<float>(), static_cast<float>(alpha), fptr(b),
                static_cast<float>(beta), out.numel(), cur_stream());
 }
 
 at::Tensor l2norm_hip(const at::Tensor& x) {
   check_f32(x, "x");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto partial = at::empty({1024}, x.options());
   auto out = at::empty({}, x.options());
   launch_l2norm(x.data_ptr<float>(), x.numel(), partial.data_ptr<float>(), out.data_ptr<float>(),
@@ -382,7 +384,7 @@ at::Tensor l2norm_hip(const at::Tensor& x) {
 void clip_noise_hip(at::Tensor x, const c10::optional<at::Tensor>& norm, double clip,
                     double noise_std, int64_t seed, int64_t offset) {
   check_f32(x, "x");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   launch_clip_noise(x.data_ptr<float>(), x.numel(), fptr(norm), static_cast<float>(clip),
                     static_cast<float>(noise_std), static_cast<uint64_t>(seed),
                     static_cast<uint64_t>(offset), cur_stream());
@@ -391,19 +393,19 @@ void clip_noise_hip(at::Tensor x, const c10::optional<at::Tensor>& norm, double 
 void client_state_hip(const at::Tensor& g, const c10::optional<at::Tensor>& u,
                       const c10::optional<at::Tensor>& e, double rho) {
   check_f32(g, "g");
-  c10::hip::HIPGuard guard(g.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
   launch_client_state(g.data_ptr<float>(), fptr(u), fptr(e), g.numel(), static_cast<float>(rho),
                       cur_stream());
 }
 
 void zero_at_hip(const c10::optional<at::Tensor>& a, const c10::optional<at::Tensor>& b,
                  const c10::optional<at::Tensor>& c, const at::Tensor& idx) {
-  c10::hip::HIPGuard guard(idx.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(idx.device());
   launch_zero_at(fptr(a), fptr(b), fptr(c), idx.data_ptr<int64_t>(), idx.numel(), cur_stream());
 }
 
 at::Tensor scatter_dense_hip(const at::Tensor& idx, const at::Tensor& vals, int64_t n) {
-  c10::hip::HIPGuard guard(vals.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(vals.device());
   auto out = at::empty({n}, vals.options());
   launch_scatter_dense(out.data_ptr<float>(), n, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                        idx.numel(), cur_stream());
@@ -416,7 +418,7 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.is_contiguous(),
               "data must be uint8 [N,H,W,C] contiguous");
   TORCH_CHECK(data.size(3) <= 4, "at most 4 channels");
-  c10::hip::HIPGuard guard(data.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(data.device());
   const int64_t B = idx.numel(), H = data.size(1), W = data.size(2), C = data.size(3);
   auto out = at::empty({B, H, W, C}, data.options().dtype(at::kBFloat16));
   auto mc = mean.to(data.device(), at::kFloat).contiguous();

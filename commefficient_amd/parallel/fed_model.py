@@ -180,7 +180,11 @@ class FedModel:
         a = self.args
         if a.merge_clients == "off" or a.do_test:
             return False
-        if a.mode not in ("sketch", "uncompressed", "true_topk"):
+        if a.mode == "fedavg":
+            # one full-batch local step: delta_i = lr * n_i * g_i(w) -- linear
+            if not (a.num_fedavg_epochs == 1 and a.fedavg_batch_size == -1):
+                return False
+        elif a.mode not in ("sketch", "uncompressed", "true_topk"):
             return False
         if self.client_state.active:
             return False
@@ -337,7 +341,9 @@ class FedModel:
                 sk.accumulateVec(self.flat.g, 1.0, self.w if wscale != 0 else None, wscale,
                                  dense=a.encode == "binned")
             else:
-                ops.axpby(out, self.flat.g, 1.0, self.w if wscale != 0 else None, wscale)
+                # fedavg (single local step): sum_i (w - (w - lr g_i)) n_i = lr * transmit
+                s = self.fedavg_lr if a.mode == "fedavg" else 1.0
+                ops.axpby(out, self.flat.g, s, self.w if wscale != 0 else None, s * wscale)
         return out, msum
 
     def _client_grad(self, inputs, targets, n: int, work: torch.Tensor):

@@ -1,0 +1,123 @@
+#!/usr/bin/env python
+"""Throughput of the secondary BASELINE.json configurations (synthetic data,
+random init, 1..N GPUs via torch.distributed.run):
+
+  imagenet_local_topk  ResNet-101 ImageNet-shaped (3x224x224, 1000 classes),
+                       local top-k + local error feedback
+  gpt2_sketch          GPT-2-small double heads on PersonaChat-shaped tokens,
+                       FetchSGD (k=50k, 5 x 500k)
+  cifar100_fedavg      ResNet-18 CIFAR-100, 10,000 non-iid clients, 100/round
+                       per GPU, FedAvg (1 local epoch)
+
+Prints one JSON line per config (rank 0) with examples/s and ms/round.
+Usage: python scripts/bench_configs.py --config NAME [--steps K --warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def cfg_args(name, N, b):
+    if name == "imagenet_local_topk":
+        W = b.clients or 8 * N
+        return W, ["--dataset_name", "ImageNet", "--synthetic", "--synthetic_size", str(W * 32 * 2),
+                   "--model", "ResNet101", "--mode", "local_topk", "--error_type", "local",
+                   "--local_momentum", "0.9", "--virtual_momentum", "0", "--k", "500000",
+                   "--num_clients", str(W * 2), "--num_workers", str(W), "--local_batch_size", "32",
+                   "--do_batchnorm" if False else "--batchnorm"]
+    if name == "gpt2_sketch":
+        W = b.clients or 4 * N
+        return W, ["--dataset_name", "PERSONA", "--synthetic", "--model", "GPT2DoubleHeads",
+                    "--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
+                    "--virtual_momentum", "0.9", "--k", "50000", "--num_rows", "5",
+                    "--num_cols", "500000", "--num_clients", "17568", "--num_workers", str(W),
+                    "--local_batch_size", "8", "--num_candidates", "2", "--max_history", "2"]
+    if name == "cifar100_fedavg":
+        W = b.clients or 100 * N
+        return W, ["--dataset_name", "CIFAR100", "--synthetic", "--model", "ResNet18",
+                   "--mode", "fedavg", "--error_type", "none", "--local_momentum", "0",
+                   "--virtual_momentum", "0.9", "--num_clients", "10000", "--num_workers", str(W),
+                   "--local_batch_size", "-1", "--fedavg_batch_size", "-1",
+                   "--num_fedavg_epochs", "1", "--batchnorm"]
+    raise ValueError(name)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--config", required=True,
+                   choices=["imagenet_local_topk", "gpt2_sketch", "cifar100_fedavg"])
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--clients", type=int, default=0, help="clients per round (total)")
+    b = p.parse_args()
+    from commefficient_amd import models
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd.utils.args import parse_args
+    ctx = dist.init("cuda")
+    N = ctx.world_size
+    W, argv = cfg_args(b.config, N, b)
+    args = parse_args(argv=argv + ["--device", "cuda", "--seed", "21"], probe_port=False)
+    torch.manual_seed(0)
+    if b.config == "gpt2_sketch":
+        from commefficient_amd.train import gpt2 as drv
+        from commefficient_amd.models.gpt2 import GPT2DoubleHeads
+        from commefficient_amd.train.losses import gpt2_loss_train, gpt2_loss_val
+        model = GPT2DoubleHeads("gpt2")
+        loader, _ = drv.get_data_loaders(args, ctx.device)
+        loss, vloss = gpt2_loss_train, gpt2_loss_val
+        unit = "utterances/s"
+    else:
+        from commefficient_amd.train import cv as drv
+        from commefficient_amd.train.losses import cv_loss
+        loader, _ = drv.get_data_loaders(args, ctx.device)
+        ncls = {"ImageNet": 1000, "CIFAR100": 100}[args.dataset_name]
+        model = models.build_model(args, ncls)
+        loss = vloss = cv_loss
+        unit = "images/s"
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    fed = FedModel(model, loss, args, vloss, num_clients=args.num_clients)
+    fopt = FedOptimizer(opt, args, fed)
+    batches = []
+    it = iter(loader)
+    while len(batches) < b.warmup + b.steps:
+        try:
+            rb = next(it)
+        except StopIteration:
+            it = iter(loader)
+            continue
+        if len(np.unique(rb.client_ids)) == W:
+            batches.append(rb)
+    n_ex = [len(x) for x in batches]
+    for i in range(b.warmup):
+        fed(batches[i])
+        fopt.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(b.warmup, b.warmup + b.steps):
+        out = fed(batches[i])
+        fopt.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = dist.max_over_ranks(time.perf_counter() - t0)
+    ex = sum(n_ex[b.warmup:])
+    if ctx.is_main:
+        print(json.dumps({"config": b.config, "n_gpus": N, "value": round(ex / el, 1),
+                          "unit": unit, "ms_per_round": round(el / b.steps * 1e3, 2),
+                          "clients_per_round": W, "examples_per_round": ex / b.steps,
+                          "grad_size": fed.d, "loss_last": float(out[0].mean().item()),
+                          "dtype": args.dtype, "data": "synthetic"}), flush=True)
+    dist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -59,6 +59,9 @@ CASES = [
     ("fedavg", ["--virtual_momentum", "0.9", "--local_momentum", "0", "--local_batch_size", "-1",
                 "--fedavg_batch_size", "2", "--num_fedavg_epochs", "2"],
      dict(rho=0.9, fedavg_epochs=2, fedavg_bs=2)),
+    # one full-batch local step: takes the merged (linear) path
+    ("fedavg", ["--virtual_momentum", "0.5", "--local_momentum", "0", "--local_batch_size", "-1"],
+     dict(rho=0.5)),
     ("sketch", ["--error_type", "virtual", "--virtual_momentum", "0.9", "--local_momentum", "0",
                 "--k", "2", "--num_rows", "1", "--num_cols", "100003", "--num_blocks", "1"],
      dict(rho=0.9, k=2, error_type="virtual")),
