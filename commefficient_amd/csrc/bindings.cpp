@@ -45,7 +45,7 @@ HashCtx make_ctx(const at::Tensor& hashes, const at::Tensor& blk_off, const at::
                  int64_t num_blocks, int64_t d, int64_t c, bool on_device) {
   TORCH_CHECK(hashes.device().is_cpu() && hashes.scalar_type() == at::kLong &&
                   hashes.dim() == 2 && hashes.size(1) == kHashParams,
-              "hashes must be a CPU int64 tensor [r, 6]");
+              "hashes must be a CPU int64 tensor [r, 4]");
   const int64_t r = hashes.size(0);
   TORCH_CHECK(r >= 1 && r <= kMaxRows, "num_rows must be in [1, 16]");
   TORCH_CHECK(d >= 0 && d < (1ll << 31), "sketched vector length must be < 2^31");
@@ -55,12 +55,10 @@ HashCtx make_ctx(const at::Tensor& hashes, const at::Tensor& blk_off, const at::
   const int64_t* hp = hc.data_ptr<int64_t>();
   for (int64_t j = 0; j < r; ++j) {
     RowHash& rh = ctx.rows.row[j];
-    rh.a = static_cast<uint32_t>(hp[j * 6 + 0]);
-    rh.b = static_cast<uint32_t>(hp[j * 6 + 1]);
-    rh.c0 = static_cast<uint32_t>(hp[j * 6 + 2]);
-    rh.c1 = static_cast<uint32_t>(hp[j * 6 + 3]);
-    rh.c2 = static_cast<uint32_t>(hp[j * 6 + 4]);
-    rh.c3 = static_cast<uint32_t>(hp[j * 6 + 5]);
+    rh.a = static_cast<uint64_t>(hp[j * kHashParams + 0]) | 1ull;
+    rh.b = static_cast<uint64_t>(hp[j * kHashParams + 1]);
+    rh.a2 = static_cast<uint64_t>(hp[j * kHashParams + 2]) | 1ull;
+    rh.b2 = static_cast<uint64_t>(hp[j * kHashParams + 3]);
   }
   ctx.geom = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
                        static_cast<uint32_t>(c), static_cast<uint32_t>(num_blocks));

@@ -105,25 +105,25 @@ cs_bin_kernel(float* __restrict__ table, const float* __restrict__ vec,
   }
   __syncthreads();
 
-  // exclusive scan of cnt -> off (serial per thread over a contiguous run of
-  // tiles, then a scan over the 256 thread totals in LDS)
+  // exclusive scan of cnt -> off: serial over each thread's contiguous run of
+  // tiles, then a wave-shuffle scan of the 256 thread totals (4 waves)
   const uint32_t per = (num_tiles + blockDim.x - 1) / blockDim.x;
   const uint32_t t0 = threadIdx.x * per;
   const uint32_t t1 = min(num_tiles, t0 + per);
   uint32_t acc = 0;
   for (uint32_t t = t0; t < t1; ++t) acc += cnt[t];
-  tsum[threadIdx.x] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (uint32_t k = 0; k < blockDim.x; ++k) {
-      uint32_t x = tsum[k];
-      tsum[k] = run;
-      run += x;
-    }
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = acc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(incl, o);
+    if (lane >= static_cast<uint32_t>(o)) incl += y;
   }
+  if (lane == 63) tsum[wave] = incl;
   __syncthreads();
-  acc = tsum[threadIdx.x];
+  uint32_t wbase = 0;
+  for (uint32_t w = 0; w < wave; ++w) wbase += tsum[w];
+  acc = wbase + incl - acc;  // exclusive prefix of this thread's run
   for (uint32_t t = t0; t < t1; ++t) {
     off[t] = acc;
     uint32_t c = cnt[t];
@@ -168,28 +168,58 @@ cs_bin_kernel(float* __restrict__ table, const float* __restrict__ vec,
 }
 
 // ------------------------------------------------------- binned encode, p2
-__global__ void __launch_bounds__(512)
-cs_accum_kernel(float* __restrict__ table, uint32_t* __restrict__ fill,
-                const Entry* __restrict__ entries, uint32_t cap, uint32_t total_buckets) {
+// grid = num_tiles * splits.  Block (t, s) accumulates its 1/splits share of
+// tile t's entries in LDS (ds_add_f32), then folds the partial tile into the
+// table: plain read-modify-write when it owns the tile, else contiguous
+// global atomics (256 B per wave-instruction: the full-rate atomic shape).
+// Entries are read as 16-byte pairs with 4 pairs in flight per thread.
+__global__ void __launch_bounds__(1024)
+cs_accum_kernel(float* __restrict__ table, const uint32_t* __restrict__ fill,
+                const Entry* __restrict__ entries, uint32_t cap, uint32_t total_buckets,
+                uint32_t splits) {
   __shared__ float tile[kTile];
-  __shared__ uint32_t n_sh;
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = blockIdx.x / splits;
+  const uint32_t s = blockIdx.x - t * splits;
   for (uint32_t b = threadIdx.x; b < kTile; b += blockDim.x) tile[b] = 0.f;
-  if (threadIdx.x == 0) n_sh = min(fill[t], cap);
+  const uint32_t n = min(fill[t], cap);
+  // even split boundaries so every range is a whole number of 16-B pairs
+  const uint32_t e0 = ((static_cast<uint64_t>(n) * s / splits) & ~1u);
+  const uint32_t e1 = s + 1 == splits ? n : ((static_cast<uint64_t>(n) * (s + 1) / splits) & ~1u);
   __syncthreads();
-  const uint32_t n = n_sh;
   const Entry* seg = entries + static_cast<size_t>(t) * cap;
-  for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
-    Entry en = seg[e];
-    atomicAdd(tile + (en.gb & (kTile - 1)), en.v);
+  const uint4* pairs = reinterpret_cast<const uint4*>(seg + e0);
+  const uint32_t np = (e1 - e0) / 2;
+  uint32_t p = threadIdx.x;
+  for (; p + 3 * blockDim.x < np; p += 4 * blockDim.x) {
+    uint4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q[u] = pairs[p + u * blockDim.x];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      atomicAdd(tile + (q[u].y & (kTile - 1)), __uint_as_float(q[u].x));
+      atomicAdd(tile + (q[u].w & (kTile - 1)), __uint_as_float(q[u].z));
+    }
+  }
+  for (; p < np; p += blockDim.x) {
+    uint4 q = pairs[p];
+    atomicAdd(tile + (q.y & (kTile - 1)), __uint_as_float(q.x));
+    atomicAdd(tile + (q.w & (kTile - 1)), __uint_as_float(q.z));
+  }
+  if ((e1 - e0) & 1u) {  // odd tail (last split only)
+    if (threadIdx.x == 0) {
+      Entry en = seg[e1 - 1];
+      atomicAdd(tile + (en.gb & (kTile - 1)), en.v);
+    }
   }
   __syncthreads();
-  if (threadIdx.x == 0) fill[t] = 0;  // re-arm for the next encode
   const uint32_t base = t << kTileShift;
   for (uint32_t b = threadIdx.x; b < kTile; b += blockDim.x) {
     uint32_t gb = base + b;
     float v = tile[b];
-    if (gb < total_buckets && v != 0.f) table[gb] += v;
+    if (gb < total_buckets && v != 0.f) {
+      if (splits == 1) table[gb] += v;
+      else atomicAdd(table + gb, v);
+    }
   }
 }
 
@@ -339,7 +369,7 @@ BinPlan plan_cs_encode_binned(const SketchGeom& g) {
   p.num_chunks = (static_cast<int64_t>(g.d) + chunk - 1) / chunk;
   // expected entries per tile = d * r / num_tiles; 25% + 4096 headroom
   double expect = static_cast<double>(g.d) * g.r / static_cast<double>(p.num_tiles);
-  p.cap = static_cast<int64_t>(expect * 1.25) + 4096;
+  p.cap = ((static_cast<int64_t>(expect * 1.25) + 4096) + 3) & ~int64_t(3);  // 16-B aligned segments
   return p;
 }
 
@@ -356,6 +386,8 @@ void launch_cs_encode_binned(float* table, const float* vec, const float* wvec, 
   uint32_t* fill = reinterpret_cast<uint32_t*>(scratch);
   int64_t fill_bytes = ((p.num_tiles * 4 + 255) / 256) * 256;
   Entry* entries = reinterpret_cast<Entry*>(reinterpret_cast<char*>(scratch) + fill_bytes);
+  // per-tile fill counters start at zero for every encode (a memset node)
+  (void)hipMemsetAsync(fill, 0, fill_bytes, stream);
   size_t lds = kStageEntries * sizeof(Entry) + (256 + 3 * p.num_tiles) * sizeof(uint32_t);
   static bool attr_set = false;
   if (!attr_set) {
@@ -368,9 +400,13 @@ void launch_cs_encode_binned(float* table, const float* vec, const float* wvec, 
                      stream, table, vec, wvec, scale, wscale, a, g, blk_off, blk_sign, fill,
                      entries, static_cast<uint32_t>(p.num_tiles), static_cast<uint32_t>(p.cap),
                      static_cast<uint32_t>(p.chunk));
-  hipLaunchKernelGGL(cs_accum_kernel, dim3(static_cast<uint32_t>(p.num_tiles)), dim3(512), 0,
-                     stream, table, fill, entries, static_cast<uint32_t>(p.cap),
-                     static_cast<uint32_t>(static_cast<int64_t>(g.r) * g.c));
+  // enough blocks to cover the 256 CUs ~2x
+  uint32_t splits = static_cast<uint32_t>((512 + p.num_tiles - 1) / p.num_tiles);
+  if (splits < 1) splits = 1;
+  if (splits > 8) splits = 8;
+  hipLaunchKernelGGL(cs_accum_kernel, dim3(static_cast<uint32_t>(p.num_tiles) * splits),
+                     dim3(1024), 0, stream, table, fill, entries, static_cast<uint32_t>(p.cap),
+                     static_cast<uint32_t>(static_cast<int64_t>(g.r) * g.c), splits);
 }
 
 void launch_cs_query(const float* table, float* est, const RowHashes& h, const SketchGeom& g,

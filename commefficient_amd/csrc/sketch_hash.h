@@ -4,18 +4,21 @@
 //
 // Semantics follow the CSVec used by the reference (SURVEY.md §2.4 X1;
 // call sites /root/reference/CommEfficient/fed_worker.py:313-320 and
-// fed_aggregator.py:464-467,584-595):
-//   * bucket hash: 2-wise independent  ((a*t + b) mod P) mod c
-//   * sign hash:   4-wise independent  ((c3 t^3 + c2 t^2 + c1 t + c0) mod P) & 1
-//   * P = 2^31 - 1 (Mersenne), so every product of two residues fits a u64.
-//   * numBlocks > 1: coordinate i = blk * blockSize + t reuses the hashes of t
-//     with a per-(row, block) bucket offset and sign flip.
-// Unlike CSVec nothing is materialised: hashes are recomputed on the fly, so
-// a GPT-2 sized vector (124M coords) needs no r x d index tables.
+// fed_aggregator.py:464-467,584-595): each row j has a bucket hash
+// h_j: [d] -> [c] and a sign hash s_j: [d] -> {-1,+1}; with numBlocks > 1
+// coordinate i = blk * blockSize + t reuses the hashes of t with a per-(row,
+// block) bucket offset and sign flip.
 //
-// Integer division/modulo by the runtime constants c and blockSize uses
-// Lemire's 64-bit multiply-high reciprocal (no hardware integer divide on
-// CDNA: a u32 `%` is ~40 VALU ops, this is ~6).
+// Family (MI355X-first choice): Dietzfelbinger multiply-add-shift on 64-bit
+// words -- strongly 2-universal for the top 32 bits of (a*t + b) mod 2^64 --
+// mapped to [0, c) with a multiply-high ("fastrange"), and the sign is the top
+// bit of an independent (a', b') pair.  Pairwise independence of buckets and
+// signs is what the Count Sketch unbiasedness/variance bounds use.  Cost: ~10
+// VALU ops per (coordinate, row) instead of ~100 for polynomials mod a
+// Mersenne prime (the first version of this file; measured 3x slower encode
+// and query on MI355X, profiles/r1_v1_bench_kernel_stats.txt).  Nothing is
+// materialised: no r x d index tables, so a 124M-coordinate GPT-2 gradient
+// needs no extra memory.
 #pragma once
 #include <cstdint>
 
@@ -27,9 +30,9 @@
 
 namespace commeff {
 
-constexpr uint64_t kMersenneP = (1ull << 31) - 1;
 // per-row parameter layout in the int64 `hashes` tensor [r, kHashParams]
-constexpr int kHashParams = 6;  // a, b, c0, c1, c2, c3
+// (bit patterns of u64): bucket (a, b), sign (a2, b2); a and a2 are odd.
+constexpr int kHashParams = 4;
 
 CE_HD uint64_t mul64hi(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -39,7 +42,8 @@ CE_HD uint64_t mul64hi(uint64_t a, uint64_t b) {
 #endif
 }
 
-// Reciprocal for x / d and x % d with x, d < 2^32, d >= 1.
+// Reciprocal for x / d with x, d < 2^32, d >= 1 (Lemire): no hardware integer
+// divide on CDNA, a u32 `/` is ~40 VALU ops, this is ~4.
 struct FastDivU32 {
   uint64_t M;
   uint32_t d;
@@ -53,19 +57,9 @@ inline FastDivU32 make_fastdiv(uint32_t d) {
 CE_HD uint32_t fdiv(uint32_t x, const FastDivU32& f) {
   return f.d <= 1 ? x : static_cast<uint32_t>(mul64hi(f.M, x));
 }
-CE_HD uint32_t fmod(uint32_t x, const FastDivU32& f) {
-  return f.d <= 1 ? 0u : static_cast<uint32_t>(mul64hi(f.M * x, f.d));
-}
-
-CE_HD uint64_t mod_p(uint64_t x) {
-  // x < 2^62  ->  result in [0, P)
-  x = (x & kMersenneP) + (x >> 31);
-  x = (x & kMersenneP) + (x >> 31);
-  return x >= kMersenneP ? x - kMersenneP : x;
-}
 
 struct RowHash {
-  uint32_t a, b, c0, c1, c2, c3;
+  uint64_t a, b, a2, b2;
 };
 
 constexpr int kMaxRows = 16;
@@ -80,7 +74,6 @@ struct SketchGeom {
   uint32_t r;          // rows
   uint32_t c;          // columns (buckets per row)
   uint32_t num_blocks; // CSVec numBlocks
-  FastDivU32 div_c;
   FastDivU32 div_bs;   // block size = ceil(d / num_blocks)
 };
 
@@ -92,29 +85,29 @@ inline SketchGeom make_geom(uint32_t d, uint32_t r, uint32_t c, uint32_t nb) {
   g.num_blocks = nb < 1 ? 1 : nb;
   uint32_t bs = (d + g.num_blocks - 1) / g.num_blocks;
   if (bs == 0) bs = 1;
-  g.div_c = make_fastdiv(c);
   g.div_bs = make_fastdiv(bs);
   return g;
 }
 
-// Full hash of coordinate i for one row.
-//   blk_off / blk_sign: per-row arrays of length num_blocks (unused if 1 block)
-CE_HD void hash_coord(const RowHash& h, uint32_t i, const SketchGeom& g,
-                      const int32_t* blk_off, const float* blk_sign,
-                      uint32_t* bucket, float* sign) {
-  uint32_t blk = 0, t = i;
+// block index / in-block coordinate (shared by all rows of one coordinate)
+CE_HD void split_block(uint32_t i, const SketchGeom& g, uint32_t* blk, uint32_t* t) {
   if (g.num_blocks > 1) {
-    blk = fdiv(i, g.div_bs);
-    t = i - blk * g.div_bs.d;
+    *blk = fdiv(i, g.div_bs);
+    *t = i - *blk * g.div_bs.d;
+  } else {
+    *blk = 0;
+    *t = i;
   }
-  // bucket: ((a t + b) mod P) mod c
-  uint32_t x = static_cast<uint32_t>(mod_p(static_cast<uint64_t>(h.a) * t + h.b));
-  uint32_t bk = fmod(x, g.div_c);
-  // sign: Horner over the cubic, mod P
-  uint64_t s = mod_p(static_cast<uint64_t>(h.c3) * t + h.c2);
-  s = mod_p(s * t + h.c1);
-  s = mod_p(s * t + h.c0);
-  float sg = (s & 1u) ? -1.f : 1.f;
+}
+
+// hash of the in-block coordinate t for one row (+ block offset / sign)
+CE_HD void hash_t(const RowHash& h, uint32_t t, uint32_t blk, const SketchGeom& g,
+                  const int32_t* blk_off, const float* blk_sign, uint32_t* bucket,
+                  float* sign) {
+  const uint64_t x = h.a * t + h.b;  // mod 2^64
+  uint32_t bk = static_cast<uint32_t>(((x >> 32) * static_cast<uint64_t>(g.c)) >> 32);
+  const uint64_t y = h.a2 * t + h.b2;
+  float sg = (y >> 63) ? -1.f : 1.f;
   if (g.num_blocks > 1) {
     bk += static_cast<uint32_t>(blk_off[blk]);  // blk_off in [0, c)
     if (bk >= g.c) bk -= g.c;
@@ -122,6 +115,15 @@ CE_HD void hash_coord(const RowHash& h, uint32_t i, const SketchGeom& g,
   }
   *bucket = bk;
   *sign = sg;
+}
+
+// Full hash of coordinate i for one row.
+CE_HD void hash_coord(const RowHash& h, uint32_t i, const SketchGeom& g,
+                      const int32_t* blk_off, const float* blk_sign, uint32_t* bucket,
+                      float* sign) {
+  uint32_t blk, t;
+  split_block(i, g, &blk, &t);
+  hash_t(h, t, blk, g, blk_off, blk_sign, bucket, sign);
 }
 
 }  // namespace commeff

@@ -27,18 +27,20 @@ import torch
 
 from .._ext import ops
 
-MERSENNE_P = (1 << 31) - 1
-
-
 def make_hashes(r: int, c: int, num_blocks: int = 1, seed: int = 42):
     """Deterministic hash coefficients (identical on every rank for one seed).
 
-    Returns ``(hashes[r,6] int64 cpu, blk_off[r,nb] int32 cpu, blk_sign[r,nb] f32 cpu)``.
+    Per row: multiply-add-shift parameters (a, b) for the bucket and (a2, b2)
+    for the sign, as u64 bit patterns in an int64 tensor (a, a2 odd); see
+    csrc/sketch_hash.h.  Returns ``(hashes[r,4] int64 cpu, blk_off[r,nb] int32
+    cpu, blk_sign[r,nb] f32 cpu)``.
     """
     rng = np.random.RandomState(seed)
-    a = rng.randint(1, MERSENNE_P, size=(r, 1), dtype=np.int64)
-    rest = rng.randint(0, MERSENNE_P, size=(r, 5), dtype=np.int64)
-    hashes = torch.from_numpy(np.concatenate([a, rest], axis=1))
+    u = rng.randint(0, 2 ** 32, size=(r, 4, 2), dtype=np.uint64)
+    words = (u[..., 0] << np.uint64(32)) | u[..., 1]
+    words[:, 0] |= np.uint64(1)
+    words[:, 2] |= np.uint64(1)
+    hashes = torch.from_numpy(words.view(np.int64).copy())
     nb = max(1, int(num_blocks))
     blk_off = torch.from_numpy(rng.randint(0, c, size=(r, nb)).astype(np.int32))
     blk_sign = torch.from_numpy(
@@ -51,7 +53,7 @@ class CSVec:
 
     def __init__(self, d: int, c: int, r: int, device="cpu", numBlocks: int = 1,
                  seed: int = 42, table: Optional[torch.Tensor] = None,
-                 _hashes=None):
+                 _hashes=None, _scratch=None):
         self.d = int(d)
         self.c = int(c)
         self.r = int(r)
@@ -67,21 +69,25 @@ class CSVec:
         if table is None:
             table = torch.zeros(self.r, self.c, device=self.device, dtype=torch.float32)
         self.table = table
-        self._scratch = None
+        # binned-encode scratch, shared by every sketch derived with like();
+        # the kernels leave it re-armed (fill counters zero) after each encode
+        self._scratch = _scratch if _scratch is not None else [None]
 
     # -- construction helpers -------------------------------------------------
     def like(self, table: Optional[torch.Tensor] = None) -> "CSVec":
-        """A sketch with the same hashes (cheap: shares the coefficient tensors)."""
+        """A sketch with the same hashes (cheap: shares the coefficient tensors
+        and the encode scratch)."""
         return CSVec(self.d, self.c, self.r, self.device, self.numBlocks, self.seed,
-                     table=table, _hashes=(self.hashes, self.blk_off, self.blk_sign))
+                     table=table, _hashes=(self.hashes, self.blk_off, self.blk_sign),
+                     _scratch=self._scratch)
 
     def _binned_scratch(self) -> Optional[torch.Tensor]:
         if self.device.type != "cuda":
             return None
-        if self._scratch is None:
+        if self._scratch[0] is None:
             nbytes = ops().binned_scratch_bytes(self.d, self.r, self.c, self.numBlocks)
-            self._scratch = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
-        return self._scratch
+            self._scratch[0] = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        return self._scratch[0]
 
     # -- CSVec API --------------------------------------------------------------
     def zero(self):

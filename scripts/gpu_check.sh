@@ -29,6 +29,9 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps ${BENCH_STEPS:-30} --warmup 5 ;;
     benchprof) run bench_prof 600 python bench.py --steps 20 --warmup 5 --profile ;;
+    codec) run codec 600 python scripts/bench_codec.py ;;
+    configs) for c in ${CONFIGS:-cifar100_fedavg imagenet_local_topk gpt2_sketch}; do
+               run cfg_$c 900 python scripts/bench_configs.py --config $c; done ;;
     rocprof) run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o bench \
                --output-format csv -- python3 bench.py --steps 10 --warmup 3 ;;
     *) echo "unknown step $s" ;;

@@ -13,30 +13,35 @@ P = (1 << 31) - 1
 
 
 def hash_coords(hashes, blk_off, blk_sign, d, c, num_blocks):
-    """buckets[r,d] int64, signs[r,d] f32 for every coordinate (int64 math)."""
+    """buckets[r,d] int64, signs[r,d] f32 for every coordinate (numpy u64 math,
+    the multiply-add-shift family of csrc/sketch_hash.h)."""
+    import numpy as np
     r = hashes.shape[0]
-    i = torch.arange(d, dtype=torch.int64)
+    i = np.arange(d, dtype=np.uint64)
     nb = max(1, num_blocks)
     if nb > 1:
-        bs = (d + nb - 1) // nb
-        blk = i // bs
-        t = i - blk * bs
+        bs = np.uint64((d + nb - 1) // nb)
+        blk = (i // bs).astype(np.int64)
+        t = i - blk.astype(np.uint64) * bs
     else:
+        blk = np.zeros(d, np.int64)
         t = i
+    H = hashes.numpy().view(np.uint64)
     buckets = torch.empty(r, d, dtype=torch.int64)
     signs = torch.empty(r, d, dtype=torch.float32)
-    for j in range(r):
-        a, b, c0, c1, c2, c3 = [int(v) for v in hashes[j]]
-        x = ((a * t + b) % P) % c
-        s = (c3 * t + c2) % P
-        s = (s * t + c1) % P
-        s = (s * t + c0) % P
-        sg = 1.0 - 2.0 * (s & 1).to(torch.float32)
-        if nb > 1:
-            x = (x + blk_off[j].to(torch.int64)[blk]) % c
-            sg = sg * blk_sign[j].to(torch.float32)[blk]
-        buckets[j] = x
-        signs[j] = sg
+    with np.errstate(over="ignore"):
+        for j in range(r):
+            a, b, a2, b2 = H[j, 0] | np.uint64(1), H[j, 1], H[j, 2] | np.uint64(1), H[j, 3]
+            x = a * t + b
+            bk = ((x >> np.uint64(32)) * np.uint64(c)) >> np.uint64(32)
+            y = a2 * t + b2
+            sg = np.where((y >> np.uint64(63)) == 1, -1.0, 1.0).astype(np.float32)
+            bk = bk.astype(np.int64)
+            if nb > 1:
+                bk = (bk + blk_off[j].numpy().astype(np.int64)[blk]) % c
+                sg = sg * blk_sign[j].numpy()[blk]
+            buckets[j] = torch.from_numpy(bk)
+            signs[j] = torch.from_numpy(sg)
     return buckets, signs
 
 
