@@ -80,7 +80,8 @@ HashCtx make_ctx(const at::Tensor& hashes, const at::Tensor& blk_off, const at::
 void cs_encode_cpu(at::Tensor table, const at::Tensor& vec, const at::Tensor& hashes,
                    const at::Tensor& blk_off, const at::Tensor& blk_sign, int64_t num_blocks,
                    double scale, const c10::optional<at::Tensor>& wvec, double wscale,
-                   const c10::optional<at::Tensor>& scratch) {
+                   at::TensorList layout) {
+  (void)layout;  // the CPU encode is row-parallel and needs no binning
   check_f32(table, "table");
   check_f32(vec, "vec");
   auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, vec.numel(), table.size(-1), false);
@@ -236,22 +237,30 @@ at::Tensor augment_cpu(const at::Tensor& data, const at::Tensor& idx, int64_t pa
 void cs_encode_hip(at::Tensor table, const at::Tensor& vec, const at::Tensor& hashes,
                    const at::Tensor& blk_off, const at::Tensor& blk_sign, int64_t num_blocks,
                    double scale, const c10::optional<at::Tensor>& wvec, double wscale,
-                   const c10::optional<at::Tensor>& scratch) {
+                   at::TensorList layout) {
   check_f32(table, "table");
   check_f32(vec, "vec");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, vec.numel(), table.size(-1), true);
   TORCH_CHECK(table.numel() == static_cast<int64_t>(ctx.geom.r) * ctx.geom.c, "table shape");
   if (wvec.has_value() && wvec->defined()) check_f32(*wvec, "wvec");
-  if (scratch.has_value() && scratch->defined()) {
+  if (!layout.empty()) {
+    // layout = [counts, base, seg, entries] from cs_layout for this geometry
+    TORCH_CHECK(layout.size() == 4, "layout must be [counts, base, seg, entries]");
     BinPlan plan = plan_cs_encode_binned(ctx.geom);
-    TORCH_CHECK(plan.num_tiles <= 2048, "binned encode supports r*c <= 2048*8192");
-    TORCH_CHECK(scratch->nbytes() >= static_cast<size_t>(cs_encode_binned_scratch_bytes(plan)),
-                "scratch too small for binned encode");
+    TORCH_CHECK(layout[0].numel() == plan.num_chunks * plan.num_tiles &&
+                    layout[1].numel() == plan.num_chunks * plan.num_tiles &&
+                    layout[2].numel() == plan.num_tiles + 1,
+                "layout does not match this sketch geometry");
+    TORCH_CHECK(layout[3].nbytes() >= static_cast<size_t>(cs_encode_binned_scratch_bytes(plan)),
+                "entry buffer too small for binned encode");
     launch_cs_encode_binned(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
                             static_cast<float>(scale), static_cast<float>(wscale), ctx.rows,
-                            ctx.geom, ctx.blk_off, ctx.blk_sign, plan, scratch->data_ptr(),
-                            cur_stream());
+                            ctx.geom, ctx.blk_off, ctx.blk_sign, plan,
+                            reinterpret_cast<const uint32_t*>(layout[0].data_ptr<int32_t>()),
+                            reinterpret_cast<const uint32_t*>(layout[1].data_ptr<int32_t>()),
+                            reinterpret_cast<const uint32_t*>(layout[2].data_ptr<int32_t>()),
+                            layout[3].data_ptr(), cur_stream());
   } else {
     launch_cs_encode(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
                      static_cast<float>(scale), static_cast<float>(wscale), ctx.rows, ctx.geom,
@@ -431,6 +440,28 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   return out_bf16 ? o : o.to(at::kFloat);
 }
 
+// One-time layout of the binned encode for a sketch geometry (hashes are
+// data-independent): counts[chunk, tile], base[chunk, tile] (global entry
+// index of the chunk's run in the tile's segment), seg[tile] (segment starts,
+// num_tiles + 1).  All int32 on the device of `like`.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cs_layout_hip(
+    const at::Tensor& hashes, const at::Tensor& blk_off, const at::Tensor& blk_sign,
+    int64_t num_blocks, int64_t d, int64_t c, const at::Tensor& like) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(like.device());
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, c, true);
+  BinPlan plan = plan_cs_encode_binned(ctx.geom);
+  TORCH_CHECK(cs_binned_supported(plan), "sketch geometry too large for the binned encode");
+  auto opt = like.options().dtype(at::kInt);
+  auto counts = at::empty({plan.num_chunks, plan.num_tiles}, opt);
+  launch_cs_layout(ctx.rows, ctx.geom, ctx.blk_off, ctx.blk_sign, plan,
+                   reinterpret_cast<uint32_t*>(counts.data_ptr<int32_t>()), cur_stream());
+  auto c64 = counts.to(at::kLong);
+  auto tile_tot = c64.sum(0);
+  auto seg = at::cat({at::zeros({1}, tile_tot.options()), at::cumsum(tile_tot, 0)});
+  auto base = at::cumsum(c64, 0) - c64 + seg.narrow(0, 0, plan.num_tiles).unsqueeze(0);
+  return {counts, base.to(at::kInt).contiguous(), seg.to(at::kInt).contiguous()};
+}
+
 int64_t binned_scratch_bytes(int64_t d, int64_t r, int64_t c, int64_t num_blocks) {
   SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
                            static_cast<uint32_t>(c), static_cast<uint32_t>(num_blocks));
@@ -442,7 +473,9 @@ int64_t binned_scratch_bytes(int64_t d, int64_t r, int64_t c, int64_t num_blocks
 
 TORCH_LIBRARY(commeff, m) {
   m.def("cs_encode(Tensor(a!) table, Tensor vec, Tensor hashes, Tensor blk_off, Tensor blk_sign, "
-        "int num_blocks, float scale, Tensor? wvec, float wscale, Tensor? scratch) -> ()");
+        "int num_blocks, float scale, Tensor? wvec, float wscale, Tensor[] layout) -> ()");
+  m.def("cs_layout(Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, int d, int c, "
+        "Tensor like) -> (Tensor, Tensor, Tensor)");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
         "int d) -> Tensor");
   m.def("cs_zero_buckets(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, Tensor hashes, "
@@ -491,6 +524,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   using namespace commeff;
   m.impl("cs_encode", &cs_encode_hip);
   m.impl("cs_query", &cs_query_hip);
+  m.impl("cs_layout", &cs_layout_hip);
   m.impl("cs_zero_buckets", &cs_zero_buckets_hip);
   m.impl("cs_l2estimate", &cs_l2estimate_hip);
   m.impl("topk_abs", &topk_abs_hip);

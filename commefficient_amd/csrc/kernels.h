@@ -15,23 +15,29 @@ void launch_cs_encode(float* table, const float* vec, const float* wvec,
                       float scale, float wscale, const RowHashes& h,
                       const SketchGeom& g, const int32_t* blk_off,
                       const float* blk_sign, hipStream_t stream);
-// Binned (LDS-privatised) encode for dense vectors: two passes through a
-// scratch buffer; see sketch.hip for the layout.  Returns false if the
-// geometry is unsupported (then call launch_cs_encode).
+// Binned (LDS-privatised) encode for dense vectors, see sketch.hip.  The
+// per-(chunk, tile) layout depends only on the hashes: build it once with
+// launch_cs_layout (counts), then base = exclusive scan over chunks + segment
+// start, seg = tile segment starts [num_tiles + 1].
 struct BinPlan {
   int64_t tile;        // buckets per LDS tile (flat over rows)
   int64_t num_tiles;
   int64_t chunk;       // coordinates per pass-1 block
   int64_t num_chunks;
-  int64_t cap;         // entries reserved per (chunk, tile) segment
+  int64_t cap;         // total entries = d * r
 };
 BinPlan plan_cs_encode_binned(const SketchGeom& g);
 int64_t cs_encode_binned_scratch_bytes(const BinPlan& p);
+bool cs_binned_supported(const BinPlan& p);
+void launch_cs_layout(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
+                      const float* blk_sign, const BinPlan& p, uint32_t* counts,
+                      hipStream_t stream);
 void launch_cs_encode_binned(float* table, const float* vec, const float* wvec,
                              float scale, float wscale, const RowHashes& h,
                              const SketchGeom& g, const int32_t* blk_off,
                              const float* blk_sign, const BinPlan& plan,
-                             void* scratch, hipStream_t stream);
+                             const uint32_t* counts, const uint32_t* base,
+                             const uint32_t* seg, void* entries, hipStream_t stream);
 // est[i] = lower-median_j( s_j(i) * table[j, b_j(i)] )
 void launch_cs_query(const float* table, float* est, const RowHashes& h,
                      const SketchGeom& g, const int32_t* blk_off,

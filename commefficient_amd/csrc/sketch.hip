@@ -5,20 +5,24 @@
 // fed_aggregator.py:584-611.
 //
 // Design (MI355X-first, not a translation of CSVec's torch code):
-//  * hashes are recomputed in registers from 6 u32 coefficients per row that
+//  * hashes are recomputed in registers from 4 u64 coefficients per row that
 //    travel in the kernel arguments (SGPRs) -- no r x d index tables;
 //  * encode has two forms:
-//      - direct: one fp32 global atomic per (coord,row).  Only used for
-//        sparse inputs: random per-lane atomics run at ~1/17 of the
-//        contiguous atomic rate on CDNA4 (MI355X_MICROARCH.md "Global float
-//        atomics"), so a dense 6.5M-coordinate encode would cost ~1.6 ms;
-//      - binned: pass 1 hashes a chunk of coordinates per workgroup,
-//        counting-sorts its (value, bucket) entries by 8192-bucket table tile
-//        in LDS and streams them out as contiguous per-tile segments;
-//        pass 2 gives each tile to one workgroup that accumulates all of
-//        the tile's entries with LDS float atomics (ds_add_f32) and writes
-//        the tile back with coalesced read-modify-write stores.  Every
-//        global access is then a coalesced stream.
+//      - direct: one fp32 global atomic per (coord, row).  Only for sparse
+//        inputs: random per-lane atomics run at ~1/17 of the contiguous
+//        atomic rate on CDNA4 (MI355X_MICROARCH.md "Global float atomics");
+//        a dense 6.5M-coordinate encode measured 1.56 ms;
+//      - binned: the hashes are data-independent, so the mapping of every
+//        (coordinate, row) entry to its 8192-bucket table tile is fixed.  A
+//        one-time layout pass counts entries per (coordinate chunk, tile) and
+//        an exclusive scan gives every chunk a private, exactly sized run in
+//        every tile's segment of one entry buffer.  Per encode, pass 1 hashes
+//        a chunk per workgroup, counting-sorts its (value, bucket) entries by
+//        tile in LDS and streams each tile's run out contiguously (no global
+//        atomics); pass 2 gives each tile (split over 1-8 workgroups) to
+//        workgroups that accumulate its entries with LDS float atomics and
+//        fold the tile into the table with coalesced stores / contiguous
+//        atomics.  Every global access is a coalesced stream.
 //  * query gathers r signed cells per coordinate and takes the lower median
 //    (torch.median convention, which CSVec relies on) in registers.
 #include <hip/hip_runtime.h>
@@ -48,6 +52,23 @@ __device__ __forceinline__ float load_v(const float* vec, const float* wvec,
   return v;
 }
 
+// Exclusive prefix of `x` over the 256 threads of a block (4 waves), via
+// wave shuffles + one LDS exchange.  `lds4` holds >= 4 u32.
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* lds4) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(incl, o);
+    if (lane >= static_cast<uint32_t>(o)) incl += y;
+  }
+  if (lane == 63) lds4[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t w = 0; w < wave; ++w) base += lds4[w];
+  return base + incl - x;
+}
+
 // ------------------------------------------------------------ direct encode
 __global__ void __launch_bounds__(256)
 cs_encode_direct_kernel(float* __restrict__ table, const float* __restrict__ vec,
@@ -58,137 +79,140 @@ cs_encode_direct_kernel(float* __restrict__ table, const float* __restrict__ vec
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < g.d; i += stride) {
     float v = load_v(vec, wvec, scale, wscale, i);
     if (v == 0.f) continue;  // sparse inputs: nothing to add
+    uint32_t blk, t;
+    split_block(i, g, &blk, &t);
     for (uint32_t j = 0; j < g.r; ++j) {
       uint32_t bk;
       float s;
-      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
-                 blk_sign + j * g.num_blocks, &bk, &s);
+      hash_t(h.row[j], t, blk, g, blk_off + j * g.num_blocks, blk_sign + j * g.num_blocks,
+             &bk, &s);
       atomicAdd(table + static_cast<size_t>(j) * g.c + bk, s * v);
     }
   }
 }
 
-// ------------------------------------------------------- binned encode, p1
-// scratch layout: [fill: num_tiles u32, padded to 256 B][entries: num_tiles * cap]
+// --------------------------------------------------------- binned: layout
+// counts[chunk][tile] = #entries of the chunk's coordinates (all rows) in tile
 __global__ void __launch_bounds__(256)
-cs_bin_kernel(float* __restrict__ table, const float* __restrict__ vec,
-              const float* __restrict__ wvec, float scale, float wscale,
-              HashArgs h, SketchGeom g, const int32_t* __restrict__ blk_off,
-              const float* __restrict__ blk_sign, uint32_t* __restrict__ fill,
-              Entry* __restrict__ entries, uint32_t num_tiles, uint32_t cap,
-              uint32_t chunk) {
+cs_layout_kernel(HashArgs h, SketchGeom g, const int32_t* __restrict__ blk_off,
+                 const float* __restrict__ blk_sign, uint32_t* __restrict__ counts,
+                 uint32_t num_tiles, uint32_t chunk) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // carve: staging[kStageEntries] | tsum[256] | cnt | off | gbase  (num_tiles each)
-  Entry* stage = reinterpret_cast<Entry*>(smem);
-  uint32_t* tsum = reinterpret_cast<uint32_t*>(stage + kStageEntries);
-  uint32_t* cnt = tsum + 256;
-  uint32_t* off = cnt + num_tiles;
-  uint32_t* gbase = off + num_tiles;
-
-  const uint32_t i0 = blockIdx.x * chunk;
-  const uint32_t i1 = min(g.d, i0 + chunk);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
   for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) cnt[t] = 0;
   __syncthreads();
-
-  // phase A: count entries per tile
+  const uint32_t i0 = blockIdx.x * chunk;
+  const uint32_t i1 = min(g.d, i0 + chunk);
   for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    float v = load_v(vec, wvec, scale, wscale, i);
-    if (v == 0.f) continue;
+    uint32_t blk, t;
+    split_block(i, g, &blk, &t);
     for (uint32_t j = 0; j < g.r; ++j) {
       uint32_t bk;
       float s;
-      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
-                 blk_sign + j * g.num_blocks, &bk, &s);
-      uint32_t gb = j * g.c + bk;
-      atomicAdd(cnt + (gb >> kTileShift), 1u);
+      hash_t(h.row[j], t, blk, g, blk_off + j * g.num_blocks, blk_sign + j * g.num_blocks,
+             &bk, &s);
+      atomicAdd(cnt + ((j * g.c + bk) >> kTileShift), 1u);
     }
   }
   __syncthreads();
+  uint32_t* out = counts + static_cast<size_t>(blockIdx.x) * num_tiles;
+  for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) out[t] = cnt[t];
+}
 
-  // exclusive scan of cnt -> off: serial over each thread's contiguous run of
-  // tiles, then a wave-shuffle scan of the 256 thread totals (4 waves)
+// --------------------------------------------------------- binned: pass 1
+// base[chunk][tile] = global entry index where this chunk's run in the
+// tile's segment starts (exclusive scan over chunks + segment start).
+__global__ void __launch_bounds__(256)
+cs_bin_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, float scale,
+              float wscale, HashArgs h, SketchGeom g, const int32_t* __restrict__ blk_off,
+              const float* __restrict__ blk_sign, const uint32_t* __restrict__ counts,
+              const uint32_t* __restrict__ base, Entry* __restrict__ entries,
+              uint32_t num_tiles, uint32_t chunk) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // carve: staging[kStageEntries] | lds4[4] | off | cur | gbase (num_tiles each)
+  Entry* stage = reinterpret_cast<Entry*>(smem);
+  uint32_t* lds4 = reinterpret_cast<uint32_t*>(stage + kStageEntries);
+  uint32_t* off = lds4 + 4;
+  uint32_t* cur = off + num_tiles;
+  uint32_t* gbase = cur + num_tiles;
+
+  const size_t row0 = static_cast<size_t>(blockIdx.x) * num_tiles;
+  // local offsets: exclusive scan of this chunk's per-tile counts
   const uint32_t per = (num_tiles + blockDim.x - 1) / blockDim.x;
   const uint32_t t0 = threadIdx.x * per;
   const uint32_t t1 = min(num_tiles, t0 + per);
   uint32_t acc = 0;
-  for (uint32_t t = t0; t < t1; ++t) acc += cnt[t];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t incl = acc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(incl, o);
-    if (lane >= static_cast<uint32_t>(o)) incl += y;
-  }
-  if (lane == 63) tsum[wave] = incl;
-  __syncthreads();
-  uint32_t wbase = 0;
-  for (uint32_t w = 0; w < wave; ++w) wbase += tsum[w];
-  acc = wbase + incl - acc;  // exclusive prefix of this thread's run
+  for (uint32_t t = t0; t < t1; ++t) acc += counts[row0 + t];
+  acc = block_excl_scan256(acc, lds4);
   for (uint32_t t = t0; t < t1; ++t) {
     off[t] = acc;
-    uint32_t c = cnt[t];
-    acc += c;
-    // reserve this block's contiguous run inside the tile's segment
-    gbase[t] = c ? atomicAdd(fill + t, c) : 0u;
-    cnt[t] = off[t];  // reuse as insertion cursor
+    cur[t] = acc;
+    acc += counts[row0 + t];
+    gbase[t] = base[row0 + t];
   }
   __syncthreads();
 
-  // phase B: counting-sort the entries into LDS staging
+  // counting-sort the chunk's entries into LDS staging
+  const uint32_t i0 = blockIdx.x * chunk;
+  const uint32_t i1 = min(g.d, i0 + chunk);
   for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    float v = load_v(vec, wvec, scale, wscale, i);
-    if (v == 0.f) continue;
+    const float v = load_v(vec, wvec, scale, wscale, i);
+    uint32_t blk, t;
+    split_block(i, g, &blk, &t);
     for (uint32_t j = 0; j < g.r; ++j) {
       uint32_t bk;
       float s;
-      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
-                 blk_sign + j * g.num_blocks, &bk, &s);
-      uint32_t gb = j * g.c + bk;
-      uint32_t pos = atomicAdd(cnt + (gb >> kTileShift), 1u);
+      hash_t(h.row[j], t, blk, g, blk_off + j * g.num_blocks, blk_sign + j * g.num_blocks,
+             &bk, &s);
+      const uint32_t gb = j * g.c + bk;
+      const uint32_t pos = atomicAdd(cur + (gb >> kTileShift), 1u);
       stage[pos] = Entry{s * v, gb};
     }
   }
   __syncthreads();
 
-  // phase C: stream the sorted entries out (consecutive threads write
-  // consecutive slots of one tile segment).  After phase B the cursor of the
-  // last tile equals the block's total entry count.
-  const uint32_t total = cnt[num_tiles - 1];
+  // stream out: consecutive threads write consecutive slots of one tile run
+  const uint32_t total = (i1 > i0 ? (i1 - i0) : 0u) * g.r;
   for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
-    Entry en = stage[e];
-    uint32_t t = en.gb >> kTileShift;
-    uint32_t slot = gbase[t] + (e - off[t]);
-    if (slot < cap) {
-      entries[static_cast<size_t>(t) * cap + slot] = en;
-    } else {
-      // segment overflow (never expected: cap has >20% headroom): add directly
-      atomicAdd(table + en.gb, en.v);
-    }
+    const Entry en = stage[e];
+    const uint32_t t = en.gb >> kTileShift;
+    entries[static_cast<size_t>(gbase[t]) + (e - off[t])] = en;
   }
 }
 
-// ------------------------------------------------------- binned encode, p2
+// --------------------------------------------------------- binned: pass 2
 // grid = num_tiles * splits.  Block (t, s) accumulates its 1/splits share of
-// tile t's entries in LDS (ds_add_f32), then folds the partial tile into the
-// table: plain read-modify-write when it owns the tile, else contiguous
-// global atomics (256 B per wave-instruction: the full-rate atomic shape).
-// Entries are read as 16-byte pairs with 4 pairs in flight per thread.
+// tile t's segment [seg[t], seg[t+1]) in LDS (ds_add_f32), then folds the
+// partial tile into the table: plain read-modify-write when it owns the tile,
+// else contiguous global atomics (256 B per wave-instruction: the full-rate
+// atomic shape).  Entries are read as 16-byte pairs, 4 pairs in flight per
+// thread.
 __global__ void __launch_bounds__(1024)
-cs_accum_kernel(float* __restrict__ table, const uint32_t* __restrict__ fill,
-                const Entry* __restrict__ entries, uint32_t cap, uint32_t total_buckets,
-                uint32_t splits) {
+cs_accum_kernel(float* __restrict__ table, const uint32_t* __restrict__ seg,
+                const Entry* __restrict__ entries, uint32_t total_buckets, uint32_t splits) {
   __shared__ float tile[kTile];
   const uint32_t t = blockIdx.x / splits;
   const uint32_t s = blockIdx.x - t * splits;
   for (uint32_t b = threadIdx.x; b < kTile; b += blockDim.x) tile[b] = 0.f;
-  const uint32_t n = min(fill[t], cap);
-  // even split boundaries so every range is a whole number of 16-B pairs
-  const uint32_t e0 = ((static_cast<uint64_t>(n) * s / splits) & ~1u);
-  const uint32_t e1 = s + 1 == splits ? n : ((static_cast<uint64_t>(n) * (s + 1) / splits) & ~1u);
+  const uint32_t lo = seg[t], hi = seg[t + 1];
+  const uint32_t n = hi - lo;
+  // split boundaries on even global indices so every range starts 16-B aligned
+  uint32_t e0 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * s / splits);
+  uint32_t e1 = s + 1 == splits ? hi : lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * (s + 1) / splits);
+  e0 = (s == 0) ? lo : (e0 & ~1u);
+  if (s + 1 != splits) e1 &= ~1u;
   __syncthreads();
-  const Entry* seg = entries + static_cast<size_t>(t) * cap;
-  const uint4* pairs = reinterpret_cast<const uint4*>(seg + e0);
-  const uint32_t np = (e1 - e0) / 2;
+  // scalar head so the pair loop starts 16-B aligned
+  uint32_t a0 = e0;
+  if ((a0 & 1u) && a0 < e1) {
+    if (threadIdx.x == 0) {
+      Entry en = entries[a0];
+      atomicAdd(tile + (en.gb & (kTile - 1)), en.v);
+    }
+    ++a0;
+  }
+  const uint32_t np = (e1 - a0) / 2;
+  const uint4* pairs = reinterpret_cast<const uint4*>(entries + a0);
   uint32_t p = threadIdx.x;
   for (; p + 3 * blockDim.x < np; p += 4 * blockDim.x) {
     uint4 q[4];
@@ -205,16 +229,14 @@ cs_accum_kernel(float* __restrict__ table, const uint32_t* __restrict__ fill,
     atomicAdd(tile + (q.y & (kTile - 1)), __uint_as_float(q.x));
     atomicAdd(tile + (q.w & (kTile - 1)), __uint_as_float(q.z));
   }
-  if ((e1 - e0) & 1u) {  // odd tail (last split only)
-    if (threadIdx.x == 0) {
-      Entry en = seg[e1 - 1];
-      atomicAdd(tile + (en.gb & (kTile - 1)), en.v);
-    }
+  if (((e1 - a0) & 1u) && threadIdx.x == 0) {  // scalar tail
+    Entry en = entries[e1 - 1];
+    atomicAdd(tile + (en.gb & (kTile - 1)), en.v);
   }
   __syncthreads();
-  const uint32_t base = t << kTileShift;
+  const uint32_t tb = t << kTileShift;
   for (uint32_t b = threadIdx.x; b < kTile; b += blockDim.x) {
-    uint32_t gb = base + b;
+    uint32_t gb = tb + b;
     float v = tile[b];
     if (gb < total_buckets && v != 0.f) {
       if (splits == 1) table[gb] += v;
@@ -263,14 +285,16 @@ cs_query_kernel(const float* __restrict__ table, float* __restrict__ est, HashAr
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < g.d; i += stride) {
     float v[kMaxRows];
     const int r = R > 0 ? R : static_cast<int>(g.r);
+    uint32_t blk, t;
+    split_block(i, g, &blk, &t);
 #pragma unroll
     for (int j = 0; j < (R > 0 ? R : kMaxRows); ++j) {
       v[j] = 0.f;
       if (j >= r) continue;
       uint32_t bk;
       float s;
-      hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
-                 blk_sign + j * g.num_blocks, &bk, &s);
+      hash_t(h.row[j], t, blk, g, blk_off + j * g.num_blocks, blk_sign + j * g.num_blocks,
+             &bk, &s);
       v[j] = s * table[static_cast<size_t>(j) * g.c + bk];
     }
     est[i] = lower_median<R>(v, r);
@@ -286,12 +310,13 @@ cs_zero_kernel(float* __restrict__ t1, float* __restrict__ t2,
   int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   if (q >= k) return;
   if (vals != nullptr && vals[q] == 0.f) return;  // S(delta) has no mass here
-  uint32_t i = static_cast<uint32_t>(idx[q]);
+  uint32_t blk, t;
+  split_block(static_cast<uint32_t>(idx[q]), g, &blk, &t);
   for (uint32_t j = 0; j < g.r; ++j) {
     uint32_t bk;
     float s;
-    hash_coord(h.row[j], i, g, blk_off + j * g.num_blocks,
-               blk_sign + j * g.num_blocks, &bk, &s);
+    hash_t(h.row[j], t, blk, g, blk_off + j * g.num_blocks, blk_sign + j * g.num_blocks, &bk,
+           &s);
     size_t cell = static_cast<size_t>(j) * g.c + bk;
     t1[cell] = 0.f;
     if (t2 != nullptr) t2[cell] = 0.f;
@@ -347,6 +372,10 @@ int grid_for(int64_t n, int block, int max_blocks) {
   return static_cast<int>(b < max_blocks ? b : max_blocks);
 }
 
+size_t bin_lds_bytes(const BinPlan& p) {
+  return kStageEntries * sizeof(Entry) + (4 + 3 * p.num_tiles) * sizeof(uint32_t);
+}
+
 }  // namespace
 
 void launch_cs_encode(float* table, const float* vec, const float* wvec, float scale,
@@ -367,45 +396,51 @@ BinPlan plan_cs_encode_binned(const SketchGeom& g) {
   if (chunk < 64) chunk = 64;
   p.chunk = chunk;
   p.num_chunks = (static_cast<int64_t>(g.d) + chunk - 1) / chunk;
-  // expected entries per tile = d * r / num_tiles; 25% + 4096 headroom
-  double expect = static_cast<double>(g.d) * g.r / static_cast<double>(p.num_tiles);
-  p.cap = ((static_cast<int64_t>(expect * 1.25) + 4096) + 3) & ~int64_t(3);  // 16-B aligned segments
+  p.cap = static_cast<int64_t>(g.d) * g.r;  // entries (exact)
   return p;
 }
 
 int64_t cs_encode_binned_scratch_bytes(const BinPlan& p) {
-  int64_t fill_bytes = ((p.num_tiles * 4 + 255) / 256) * 256;
-  return fill_bytes + p.num_tiles * p.cap * static_cast<int64_t>(sizeof(Entry));
+  return p.cap * static_cast<int64_t>(sizeof(Entry));
+}
+
+bool cs_binned_supported(const BinPlan& p) {
+  return p.num_tiles <= 2048 && bin_lds_bytes(p) <= 160 * 1024 && p.cap < (1ll << 32);
+}
+
+void launch_cs_layout(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
+                      const float* blk_sign, const BinPlan& p, uint32_t* counts,
+                      hipStream_t stream) {
+  if (g.d == 0) return;
+  size_t lds = p.num_tiles * sizeof(uint32_t);
+  hipLaunchKernelGGL(cs_layout_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256), lds,
+                     stream, to_args(h, g), g, blk_off, blk_sign, counts,
+                     static_cast<uint32_t>(p.num_tiles), static_cast<uint32_t>(p.chunk));
 }
 
 void launch_cs_encode_binned(float* table, const float* vec, const float* wvec, float scale,
                              float wscale, const RowHashes& h, const SketchGeom& g,
                              const int32_t* blk_off, const float* blk_sign, const BinPlan& p,
-                             void* scratch, hipStream_t stream) {
+                             const uint32_t* counts, const uint32_t* base, const uint32_t* seg,
+                             void* entries_buf, hipStream_t stream) {
   if (g.d == 0) return;
-  uint32_t* fill = reinterpret_cast<uint32_t*>(scratch);
-  int64_t fill_bytes = ((p.num_tiles * 4 + 255) / 256) * 256;
-  Entry* entries = reinterpret_cast<Entry*>(reinterpret_cast<char*>(scratch) + fill_bytes);
-  // per-tile fill counters start at zero for every encode (a memset node)
-  (void)hipMemsetAsync(fill, 0, fill_bytes, stream);
-  size_t lds = kStageEntries * sizeof(Entry) + (256 + 3 * p.num_tiles) * sizeof(uint32_t);
+  Entry* entries = reinterpret_cast<Entry*>(entries_buf);
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(cs_bin_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  HashArgs a = to_args(h, g);
-  hipLaunchKernelGGL(cs_bin_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256), lds,
-                     stream, table, vec, wvec, scale, wscale, a, g, blk_off, blk_sign, fill,
-                     entries, static_cast<uint32_t>(p.num_tiles), static_cast<uint32_t>(p.cap),
-                     static_cast<uint32_t>(p.chunk));
-  // enough blocks to cover the 256 CUs ~2x
+  hipLaunchKernelGGL(cs_bin_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256),
+                     bin_lds_bytes(p), stream, vec, wvec, scale, wscale, to_args(h, g), g,
+                     blk_off, blk_sign, counts, base, entries,
+                     static_cast<uint32_t>(p.num_tiles), static_cast<uint32_t>(p.chunk));
+  // enough workgroups to cover the 256 CUs ~2x
   uint32_t splits = static_cast<uint32_t>((512 + p.num_tiles - 1) / p.num_tiles);
   if (splits < 1) splits = 1;
   if (splits > 8) splits = 8;
   hipLaunchKernelGGL(cs_accum_kernel, dim3(static_cast<uint32_t>(p.num_tiles) * splits),
-                     dim3(1024), 0, stream, table, fill, entries, static_cast<uint32_t>(p.cap),
+                     dim3(1024), 0, stream, table, seg, entries,
                      static_cast<uint32_t>(static_cast<int64_t>(g.r) * g.c), splits);
 }
 

@@ -89,15 +89,30 @@ inline SketchGeom make_geom(uint32_t d, uint32_t r, uint32_t c, uint32_t nb) {
   return g;
 }
 
-// block index / in-block coordinate (shared by all rows of one coordinate)
+// Bijective 32-bit mixer (murmur3 finaliser: xor-shifts and odd multiplies
+// are invertible).  Applied to the in-block coordinate before the universal
+// hash: injectivity keeps the family pairwise independent, and it breaks the
+// arithmetic progression that multiply-shift maps consecutive keys onto --
+// consecutive lanes then hit pseudo-random table cells (no HBM-channel or LDS
+// bank camping).  Computed once per coordinate, shared by all rows.
+CE_HD uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x85ebca6bu;
+  x ^= x >> 13;
+  x *= 0xc2b2ae35u;
+  x ^= x >> 16;
+  return x;
+}
+
+// block index / mixed in-block key (shared by all rows of one coordinate)
 CE_HD void split_block(uint32_t i, const SketchGeom& g, uint32_t* blk, uint32_t* t) {
+  uint32_t tt = i;
+  *blk = 0;
   if (g.num_blocks > 1) {
     *blk = fdiv(i, g.div_bs);
-    *t = i - *blk * g.div_bs.d;
-  } else {
-    *blk = 0;
-    *t = i;
+    tt = i - *blk * g.div_bs.d;
   }
+  *t = mix32(tt);
 }
 
 // hash of the in-block coordinate t for one row (+ block offset / sign)

@@ -81,12 +81,18 @@ class CSVec:
                      table=table, _hashes=(self.hashes, self.blk_off, self.blk_sign),
                      _scratch=self._scratch)
 
-    def _binned_scratch(self) -> Optional[torch.Tensor]:
+    def _binned_layout(self):
+        """[counts, base, seg, entries] for the binned GPU encode, built once
+        per geometry (the hash -> tile mapping is data-independent) and shared
+        by every sketch derived with like()."""
         if self.device.type != "cuda":
-            return None
+            return []
         if self._scratch[0] is None:
+            counts, base, seg = ops().cs_layout(self.hashes, self.blk_off, self.blk_sign,
+                                                self.numBlocks, self.d, self.c, self.blk_off)
             nbytes = ops().binned_scratch_bytes(self.d, self.r, self.c, self.numBlocks)
-            self._scratch[0] = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+            entries = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._scratch[0] = [counts, base, seg, entries]
         return self._scratch[0]
 
     # -- CSVec API --------------------------------------------------------------
@@ -99,9 +105,9 @@ class CSVec:
         """table += S(scale*vec + wscale*wvec).  ``dense=False`` uses the
         direct-atomic kernel (best for sparse vectors)."""
         assert vec.numel() == self.d, (vec.numel(), self.d)
-        scratch = self._binned_scratch() if dense else None
+        layout = self._binned_layout() if dense else []
         ops().cs_encode(self.table, vec.reshape(-1), self.hashes, self.blk_off, self.blk_sign,
-                        self.numBlocks, float(scale), wvec, float(wscale), scratch)
+                        self.numBlocks, float(scale), wvec, float(wscale), layout)
 
     def accumulateTable(self, table: torch.Tensor):
         self.table.add_(table.view(self.r, self.c))

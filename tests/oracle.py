@@ -26,6 +26,15 @@ def hash_coords(hashes, blk_off, blk_sign, d, c, num_blocks):
     else:
         blk = np.zeros(d, np.int64)
         t = i
+    # murmur3 finaliser on u32 (sketch_hash.h mix32)
+    x = t.astype(np.uint32)
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x85ebca6b)
+        x ^= x >> np.uint32(13)
+        x *= np.uint32(0xc2b2ae35)
+        x ^= x >> np.uint32(16)
+    t = x.astype(np.uint64)
     H = hashes.numpy().view(np.uint64)
     buckets = torch.empty(r, d, dtype=torch.int64)
     signs = torch.empty(r, d, dtype=torch.float32)
