@@ -39,7 +39,10 @@ def main():
     p.add_argument("--num-clients", type=int, default=10000)
     p.add_argument("--encode", default="binned", choices=["binned", "direct"])
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
+    p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "0")),
+                   help="torch.backends.cudnn.benchmark (MIOpen exhaustive find during warmup)")
     b = p.parse_args()
+    torch.backends.cudnn.benchmark = bool(b.miopen_find)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != b.gpus:

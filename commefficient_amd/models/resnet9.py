@@ -62,7 +62,10 @@ class Residual(nn.Module):
         self.res2 = ConvBN(do_batchnorm, c, c, **kw)
 
     def forward(self, x):
-        return x + F.relu(self.res2(self.res1(x)))
+        # reference: x + relu(res2(res1(x))); res2 already ends in a ReLU, so
+        # the outer one is the identity and is dropped (saves a fwd+bwd pass
+        # over the activation)
+        return x + self.res2(self.res1(x))
 
 
 class BasicNet(nn.Module):
