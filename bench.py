@@ -39,10 +39,9 @@ def main():
     p.add_argument("--num-clients", type=int, default=10000)
     p.add_argument("--encode", default="binned", choices=["binned", "direct"])
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
-    p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "0")),
+    p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "1")),
                    help="torch.backends.cudnn.benchmark (MIOpen exhaustive find during warmup)")
     b = p.parse_args()
-    torch.backends.cudnn.benchmark = bool(b.miopen_find)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != b.gpus:
@@ -59,7 +58,8 @@ def main():
             "--virtual_momentum", "0.9", "--k", "50000", "--num_rows", "5", "--num_cols", "500000",
             "--num_blocks", "20", "--num_clients", str(b.num_clients), "--num_workers", str(W),
             "--local_batch_size", "-1", "--weight_decay", "5e-4", "--dtype", "bf16",
-            "--device", "cuda", "--encode", b.encode, "--seed", "21"]
+            "--device", "cuda", "--encode", b.encode, "--seed", "21",
+            "--miopen_find", str(b.miopen_find)]
     if b.profile:
         argv += ["--profile_dir", "gpurun_out/bench_profile"]
     args = parse_args(argv=argv, probe_port=False)

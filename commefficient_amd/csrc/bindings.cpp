@@ -440,6 +440,39 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   return out_bf16 ? o : o.to(at::kFloat);
 }
 
+std::tuple<at::Tensor, at::Tensor> relu_maxpool_hip(const at::Tensor& x, int64_t k) {
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "relu_maxpool: x must be bf16 NCHW with channels_last memory");
+  TORCH_CHECK(k == 2 || k == 4, "k must be 2 or 4");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && H % k == 0 && W % k == 0, "relu_maxpool: C%8, H%k, W%k");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, C, H / k, W / k}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({N, C, H / k, W / k},
+                       x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  launch_relu_maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                          reinterpret_cast<uint16_t*>(y.data_ptr()), idx.data_ptr<uint8_t>(),
+                          static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
+                          static_cast<int>(C), static_cast<int>(k), cur_stream());
+  return {y, idx};
+}
+
+at::Tensor relu_maxpool_backward_hip(const at::Tensor& gy, const at::Tensor& idx, int64_t k) {
+  TORCH_CHECK(gy.scalar_type() == at::kBFloat16 && idx.scalar_type() == at::kByte, "dtypes");
+  auto g = gy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(idx.is_contiguous(at::MemoryFormat::ChannelsLast), "idx layout");
+  const int64_t N = g.size(0), C = g.size(1), OH = g.size(2), OW = g.size(3);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gy.device());
+  auto gx = at::empty({N, C, OH * k, OW * k},
+                      gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_relu_maxpool_bwd(reinterpret_cast<const uint16_t*>(g.data_ptr()), idx.data_ptr<uint8_t>(),
+                          reinterpret_cast<uint16_t*>(gx.data_ptr()), static_cast<int>(N),
+                          static_cast<int>(OH * k), static_cast<int>(OW * k),
+                          static_cast<int>(C), static_cast<int>(k), cur_stream());
+  return gx;
+}
+
 // One-time layout of the binned encode for a sketch geometry (hashes are
 // data-independent): counts[chunk, tile], base[chunk, tile] (global entry
 // index of the chunk's run in the tile's segment), seg[tile] (segment starts,
@@ -476,6 +509,8 @@ TORCH_LIBRARY(commeff, m) {
         "int num_blocks, float scale, Tensor? wvec, float wscale, Tensor[] layout) -> ()");
   m.def("cs_layout(Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, int d, int c, "
         "Tensor like) -> (Tensor, Tensor, Tensor)");
+  m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
+  m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
         "int d) -> Tensor");
   m.def("cs_zero_buckets(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, Tensor hashes, "
@@ -525,6 +560,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("cs_encode", &cs_encode_hip);
   m.impl("cs_query", &cs_query_hip);
   m.impl("cs_layout", &cs_layout_hip);
+  m.impl("relu_maxpool", &relu_maxpool_hip);
+  m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("cs_zero_buckets", &cs_zero_buckets_hip);
   m.impl("cs_l2estimate", &cs_l2estimate_hip);
   m.impl("topk_abs", &topk_abs_hip);

@@ -99,6 +99,14 @@ void launch_zero_at(float* a, float* b, float* c, const int64_t* idx,
 void launch_scatter_dense(float* out, int64_t n, const int64_t* idx,
                           const float* vals, int64_t k, hipStream_t stream);
 
+// ----------------------------------------------------------------- pool --
+// y = maxpool_k(relu(x)) on NHWC bf16 (C % 8 == 0, H, W % k == 0), k in {2, 4};
+// idx = window position of the max (255: max <= 0, gradient 0)
+void launch_relu_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N, int H,
+                             int W, int C, int k, hipStream_t stream);
+void launch_relu_maxpool_bwd(const uint16_t* gy, const uint8_t* idx, uint16_t* gx, int N,
+                             int H, int W, int C, int k, hipStream_t stream);
+
 // -------------------------------------------------------------- augment --
 // CIFAR-style augmentation of uint8 NHWC images into a bf16 NHWC
 // (channels_last) batch: reflect-pad `pad`, random crop, random h-flip,

@@ -20,9 +20,22 @@ import itertools
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.nn import relu_maxpool
 from .common import GhostBatchNorm2d, Mul
 
 __all__ = ["ResNet9"]
+
+
+def _k(pool: nn.MaxPool2d) -> int:
+    k = pool.kernel_size
+    return k if isinstance(k, int) else k[0]
+
+
+def _square_pool(pool: nn.MaxPool2d) -> bool:
+    k, s = pool.kernel_size, pool.stride
+    k = k if isinstance(k, int) else (k[0] if k[0] == k[1] else -1)
+    s = s if isinstance(s, int) else (s[0] if s[0] == s[1] else -2)
+    return k == s and pool.padding in (0, (0, 0)) and pool.dilation in (1, (1, 1))
 
 DEFAULT_CHANNELS = {"prep": 64, "layer1": 128, "layer2": 256, "layer3": 512}
 
@@ -51,6 +64,9 @@ class ConvBN(nn.Module):
         x = self.conv(x)
         if self.do_batchnorm:
             x = self.bn(x)
+        if isinstance(self.pool, nn.MaxPool2d) and _square_pool(self.pool):
+            # fused relu + maxpool (native NHWC bf16 kernels on GPU)
+            return relu_maxpool(x, _k(self.pool))
         x = F.relu(x, inplace=True)
         return self.pool(x) if self.pool is not None else x
 
@@ -88,7 +104,9 @@ class BasicNet(nn.Module):
         x = self.res1(self.layer1(x))
         x = self.layer2(x)
         x = self.res3(self.layer3(x))
-        x = self.pool(x).flatten(1)
+        # res3's output is >= 0 (relu'd input + relu'd branch), so relu is the
+        # identity and the fused kernel computes exactly max_pool2d(x, 4)
+        x = relu_maxpool(x, 4).flatten(1)
         return self.classifier(self.linear(x))
 
 

@@ -105,6 +105,8 @@ class FedModel:
         args.num_clients = self.num_clients
 
         self.model.to(self.device)
+        if self.device.type == "cuda":
+            torch.backends.cudnn.benchmark = bool(getattr(args, "miopen_find", 1))
         self.flat = FlatParams(self.model, self.device)
         self.d = self.flat.d
         args.grad_size = self.d

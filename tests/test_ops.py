@@ -264,3 +264,20 @@ def test_large_sketch_gpu_matches_cpu_backend(d, c, r, nb):
     ic, vc = ops.topk_abs(est_c, 50000)
     ig, vg = ops.topk_abs(est_g, 50000)
     assert torch.equal(ig.cpu(), ic) and torch.equal(vg.cpu(), vc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,k", [((6, 16, 8, 8), 2), ((3, 64, 32, 32), 2), ((5, 32, 4, 4), 4)])
+def test_relu_maxpool_fused_matches_torch(shape, k):
+    from commefficient_amd.ops.nn import relu_maxpool
+    torch.manual_seed(0)
+    x = torch.randn(shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    y = relu_maxpool(x, k)
+    y2 = torch.nn.functional.max_pool2d(torch.relu(x2.float()), k)
+    torch.testing.assert_close(y.float(), y2, rtol=0, atol=0)
+    g = torch.randn_like(y2)
+    y.backward(g.to(torch.bfloat16))
+    y2.backward(g)
+    torch.testing.assert_close(x.grad.float(), x2.grad.float(), rtol=1e-2, atol=1e-2)
