@@ -440,6 +440,82 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   return out_bf16 ? o : o.to(at::kFloat);
 }
 
+// ------------------------------------------------------- planned sketch ops
+at::Tensor cs_hash_all_hip(const at::Tensor& hashes, const at::Tensor& blk_off,
+                           const at::Tensor& blk_sign, int64_t num_blocks, int64_t d, int64_t c,
+                           const at::Tensor& like) {
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(like.device());
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, c, true);
+  auto out = at::empty({d, static_cast<int64_t>(ctx.geom.r)}, like.options().dtype(at::kInt));
+  launch_cs_hash_all(ctx.rows, ctx.geom, ctx.blk_off, ctx.blk_sign, out.data_ptr<int32_t>(),
+                     cur_stream());
+  return out;
+}
+
+PlannedArgs planned_args(at::TensorList plan, const BinPlan& p, int64_t d, int64_t r) {
+  // plan = [src_info i16, ent_info i16, perm i32, csr i32, base i32, off i32, seg i32, vals f32]
+  TORCH_CHECK(plan.size() == 8, "plan must have 8 tensors");
+  const int64_t n = d * r;
+  // LDS: 8960 staged floats + 2 run tables of num_tiles words within 160 KB
+  TORCH_CHECK(p.num_tiles <= kPlannedMaxTiles && n < (int64_t{1} << 31) && r <= kMaxRows,
+              "planned sketch: geometry too large (r*c <= ", kPlannedMaxTiles * 8192,
+              ", d*r < 2^31, r <= ", kMaxRows, ")");
+  TORCH_CHECK(plan[0].numel() == n && plan[1].numel() == n && plan[2].numel() == n &&
+                  plan[3].numel() == p.num_tiles * 8192 + 1 &&
+                  plan[4].numel() == p.num_chunks * p.num_tiles &&
+                  plan[5].numel() == p.num_chunks * p.num_tiles &&
+                  plan[6].numel() == p.num_tiles + 1 && plan[7].numel() >= n,
+              "sketch plan does not match the geometry");
+  TORCH_CHECK(plan[0].scalar_type() == at::kShort && plan[1].scalar_type() == at::kShort &&
+                  plan[7].scalar_type() == at::kFloat,
+              "sketch plan dtypes");
+  PlannedArgs a;
+  a.src_info = reinterpret_cast<const uint16_t*>(plan[0].data_ptr<int16_t>());
+  a.ent_info = reinterpret_cast<const uint16_t*>(plan[1].data_ptr<int16_t>());
+  a.perm = plan[2].data_ptr<int32_t>();
+  a.csr = plan[3].data_ptr<int32_t>();
+  a.base = plan[4].data_ptr<int32_t>();
+  a.off = plan[5].data_ptr<int32_t>();
+  a.seg = plan[6].data_ptr<int32_t>();
+  a.vals = plan[7].data_ptr<float>();
+  return a;
+}
+
+void cs_encode_planned_hip(at::Tensor table, const at::Tensor& vec, double scale,
+                           const c10::optional<at::Tensor>& wvec, double wscale, int64_t c,
+                           at::TensorList plan) {
+  check_f32(table, "table");
+  check_f32(vec, "vec");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  const int64_t d = vec.numel(), r = table.numel() / c;
+  SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
+                           static_cast<uint32_t>(c), 1);
+  BinPlan p = plan_cs_encode_binned(g);
+  launch_cs_encode_planned(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
+                           static_cast<float>(scale), static_cast<float>(wscale), g, p,
+                           planned_args(plan, p, d, r), cur_stream());
+}
+
+at::Tensor cs_query_planned_hip(const at::Tensor& table, int64_t d, at::TensorList plan) {
+  check_f32(table, "table");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  const int64_t c = table.size(-1), r = table.numel() / c;
+  SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
+                           static_cast<uint32_t>(c), 1);
+  BinPlan p = plan_cs_encode_binned(g);
+  auto est = at::empty({d}, table.options());
+  launch_cs_query_planned(table.data_ptr<float>(), est.data_ptr<float>(), g, p,
+                          planned_args(plan, p, d, r), cur_stream());
+  return est;
+}
+
+std::vector<int64_t> binned_plan(int64_t d, int64_t r, int64_t c) {
+  SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
+                           static_cast<uint32_t>(c), 1);
+  BinPlan p = plan_cs_encode_binned(g);
+  return {p.tile, p.num_tiles, p.chunk, p.num_chunks};
+}
+
 std::tuple<at::Tensor, at::Tensor> relu_maxpool_hip(const at::Tensor& x, int64_t k) {
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -509,6 +585,12 @@ TORCH_LIBRARY(commeff, m) {
         "int num_blocks, float scale, Tensor? wvec, float wscale, Tensor[] layout) -> ()");
   m.def("cs_layout(Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, int d, int c, "
         "Tensor like) -> (Tensor, Tensor, Tensor)");
+  m.def("cs_hash_all(Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, int d, int c, "
+        "Tensor like) -> Tensor");
+  m.def("cs_encode_planned(Tensor(a!) table, Tensor vec, float scale, Tensor? wvec, float wscale, "
+        "int c, Tensor[] plan) -> ()");
+  m.def("cs_query_planned(Tensor table, int d, Tensor[] plan) -> Tensor");
+  m.def("binned_plan(int d, int r, int c) -> int[]", &commeff::binned_plan);
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
@@ -560,6 +642,9 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("cs_encode", &cs_encode_hip);
   m.impl("cs_query", &cs_query_hip);
   m.impl("cs_layout", &cs_layout_hip);
+  m.impl("cs_hash_all", &cs_hash_all_hip);
+  m.impl("cs_encode_planned", &cs_encode_planned_hip);
+  m.impl("cs_query_planned", &cs_query_planned_hip);
   m.impl("relu_maxpool", &relu_maxpool_hip);
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("cs_zero_buckets", &cs_zero_buckets_hip);

@@ -38,6 +38,25 @@ void launch_cs_encode_binned(float* table, const float* vec, const float* wvec,
                              const float* blk_sign, const BinPlan& plan,
                              const uint32_t* counts, const uint32_t* base,
                              const uint32_t* seg, void* entries, hipStream_t stream);
+// Planned (precomputed-permutation) encode / query, see sketch_planned.hip.
+constexpr int64_t kPlannedMaxTiles = 15000;
+struct PlannedArgs {
+  const uint16_t* src_info;  // [d*r]  in-chunk staging slot | sign << 15
+  const uint16_t* ent_info;  // [d*r]  in-tile bucket | sign << 15 (entry order)
+  const int32_t* perm;       // [d*r]  entry indices sorted by (tile, bucket)
+  const int32_t* csr;        // [num_tiles*8192 + 1]
+  const int32_t* base;       // [num_chunks, num_tiles]
+  const int32_t* off;        // [num_chunks, num_tiles]
+  const int32_t* seg;        // [num_tiles + 1]
+  float* vals;               // [d*r] scratch
+};
+void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
+                        const float* blk_sign, int32_t* out, hipStream_t stream);
+void launch_cs_encode_planned(float* table, const float* vec, const float* wvec, float scale,
+                              float wscale, const SketchGeom& g, const BinPlan& p,
+                              const PlannedArgs& a, hipStream_t stream);
+void launch_cs_query_planned(const float* table, float* est, const SketchGeom& g,
+                             const BinPlan& p, const PlannedArgs& a, hipStream_t stream);
 // est[i] = lower-median_j( s_j(i) * table[j, b_j(i)] )
 void launch_cs_query(const float* table, float* est, const RowHashes& h,
                      const SketchGeom& g, const int32_t* blk_off,

@@ -9,8 +9,11 @@ and ``/``.  Call sites in the reference:
 /root/reference/CommEfficient/utils.py:305-313.
 
 Differences by design (MI355X-first):
-* hashes are recomputed inside the kernels from 6 coefficients per row
-  (``hashes`` is a tiny CPU int64 tensor), so no r x d index tables exist;
+* hashes are recomputed inside the kernels from 4 coefficients per row
+  (``hashes`` is a tiny CPU int64 tensor), so no r x d index tables exist --
+  except for the default GPU "planned" kernels, which trade a one-time
+  permutation plan (ops/sketch_plan.py, ~0.4 GB at ResNet-9 size) for
+  atomic-free, bitwise-deterministic encode and query;
 * ``unSketch`` returns the dense vector like CSVec, while ``unsketch_sparse``
   returns the ``(idx, vals)`` pair straight from the deterministic radix
   select, which is what the server step uses;
@@ -53,13 +56,17 @@ class CSVec:
 
     def __init__(self, d: int, c: int, r: int, device="cpu", numBlocks: int = 1,
                  seed: int = 42, table: Optional[torch.Tensor] = None,
-                 _hashes=None, _scratch=None):
+                 _hashes=None, _scratch=None, kernel: str = "planned"):
         self.d = int(d)
         self.c = int(c)
         self.r = int(r)
         self.device = torch.device(device)
         self.numBlocks = max(1, int(numBlocks))
         self.seed = seed
+        # GPU encode/query kernels: "planned" (precomputed permutation, atomic
+        # free, deterministic), "binned" (LDS atomics) or "direct" (global
+        # atomics / random gathers)
+        self.kernel = kernel
         if _hashes is None:
             h, bo, bs = make_hashes(self.r, self.c, self.numBlocks, seed)
             bo = bo.to(self.device)
@@ -69,31 +76,43 @@ class CSVec:
         if table is None:
             table = torch.zeros(self.r, self.c, device=self.device, dtype=torch.float32)
         self.table = table
-        # binned-encode scratch, shared by every sketch derived with like();
-        # the kernels leave it re-armed (fill counters zero) after each encode
-        self._scratch = _scratch if _scratch is not None else [None]
+        # GPU encode/query plans, built once per geometry (the hash -> tile
+        # mapping is data-independent) and shared by every sketch derived
+        # with like()
+        self._scratch = _scratch if _scratch is not None else {}
 
     # -- construction helpers -------------------------------------------------
     def like(self, table: Optional[torch.Tensor] = None) -> "CSVec":
         """A sketch with the same hashes (cheap: shares the coefficient tensors
-        and the encode scratch)."""
+        and the kernel plans)."""
         return CSVec(self.d, self.c, self.r, self.device, self.numBlocks, self.seed,
                      table=table, _hashes=(self.hashes, self.blk_off, self.blk_sign),
-                     _scratch=self._scratch)
+                     _scratch=self._scratch, kernel=self.kernel)
 
     def _binned_layout(self):
-        """[counts, base, seg, entries] for the binned GPU encode, built once
-        per geometry (the hash -> tile mapping is data-independent) and shared
-        by every sketch derived with like()."""
-        if self.device.type != "cuda":
-            return []
-        if self._scratch[0] is None:
+        """[counts, base, seg, entries] for the binned GPU encode."""
+        if self.device.type != "cuda" or self.r * self.c > 2048 * 8192:
+            return []  # direct encode (binned run tables must fit in LDS)
+        if "binned" not in self._scratch:
             counts, base, seg = ops().cs_layout(self.hashes, self.blk_off, self.blk_sign,
                                                 self.numBlocks, self.d, self.c, self.blk_off)
             nbytes = ops().binned_scratch_bytes(self.d, self.r, self.c, self.numBlocks)
             entries = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-            self._scratch[0] = [counts, base, seg, entries]
-        return self._scratch[0]
+            self._scratch["binned"] = [counts, base, seg, entries]
+        return self._scratch["binned"]
+
+    def _plan(self):
+        if "planned" not in self._scratch:
+            from .sketch_plan import build_plan
+            self._scratch["planned"] = build_plan(self.hashes, self.blk_off, self.blk_sign,
+                                                  self.numBlocks, self.d, self.r, self.c,
+                                                  self.device)
+        return self._scratch["planned"]
+
+    def _use_plan(self) -> bool:
+        # limits of csrc/sketch_planned.hip (LDS run tables, int32 entry ids)
+        return (self.device.type == "cuda" and self.kernel == "planned"
+                and self.r * self.c <= 15000 * 8192 and self.d * self.r < 2 ** 31)
 
     # -- CSVec API --------------------------------------------------------------
     def zero(self):
@@ -105,7 +124,11 @@ class CSVec:
         """table += S(scale*vec + wscale*wvec).  ``dense=False`` uses the
         direct-atomic kernel (best for sparse vectors)."""
         assert vec.numel() == self.d, (vec.numel(), self.d)
-        layout = self._binned_layout() if dense else []
+        if dense and self._use_plan():
+            ops().cs_encode_planned(self.table, vec.reshape(-1), float(scale), wvec,
+                                    float(wscale), self.c, self._plan())
+            return
+        layout = self._binned_layout() if (dense and self.kernel != "direct") else []
         ops().cs_encode(self.table, vec.reshape(-1), self.hashes, self.blk_off, self.blk_sign,
                         self.numBlocks, float(scale), wvec, float(wscale), layout)
 
@@ -114,6 +137,8 @@ class CSVec:
 
     def query(self) -> torch.Tensor:
         """Median-of-rows estimate of every coordinate (dense, length d)."""
+        if self._use_plan():
+            return ops().cs_query_planned(self.table, self.d, self._plan())
         return ops().cs_query(self.table, self.hashes, self.blk_off, self.blk_sign,
                               self.numBlocks, self.d)
 

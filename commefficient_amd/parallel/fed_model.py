@@ -117,7 +117,8 @@ class FedModel:
         self.sketch = None
         if args.mode == "sketch":
             self.sketch = CSVec(self.d, args.num_cols, args.num_rows, device=self.device,
-                                numBlocks=args.num_blocks, seed=args.sketch_seed)
+                                numBlocks=args.num_blocks, seed=args.sketch_seed,
+                                kernel=args.encode)
         self.server = ServerState(args, self.d, self.device, self.sketch)
         self.client_state = ClientStateStore(args, self.d, self.num_clients, self.device,
                                              self.ctx.rank, self.ctx.world_size,
@@ -341,7 +342,7 @@ class FedModel:
                 out.zero_()
                 sk = self.sketch.like(out.view(a.num_rows, a.num_cols))
                 sk.accumulateVec(self.flat.g, 1.0, self.w if wscale != 0 else None, wscale,
-                                 dense=a.encode == "binned")
+                                 dense=a.encode != "direct")
             else:
                 # fedavg (single local step): sum_i (w - (w - lr g_i)) n_i = lr * transmit
                 s = self.fedavg_lr if a.mode == "fedavg" else 1.0
@@ -442,7 +443,7 @@ class FedModel:
         g = self.flat.g
         if a.mode == "sketch":
             sk = self.sketch.like(torch.zeros(a.num_rows, a.num_cols, device=self.device))
-            sk.accumulateVec(g, float(n), dense=a.encode == "binned")
+            sk.accumulateVec(g, float(n), dense=a.encode != "direct")
             if a.max_grad_norm is not None:
                 est = sk.l2estimate()
                 ops.clip_noise(sk.table.view(-1), est, a.max_grad_norm * n, 0.0)

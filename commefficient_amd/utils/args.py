@@ -134,8 +134,10 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="merge the clients of a rank into one forward/backward when the "
                         "mode is linear per client (exact; see parallel/fed_model.py)")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
-    g.add_argument("--encode", choices=["binned", "direct"], default="binned",
-                   help="client-side Count-Sketch encode kernel")
+    g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
+                   help="GPU Count-Sketch encode/query kernels: planned (precomputed "
+                        "permutation, atomic free), binned (LDS atomics) or direct "
+                        "(global atomics)")
     g.add_argument("--client_state_device", choices=["auto", "gpu", "cpu"], default="auto",
                    help="where per-client momentum/error/weights live")
     g.add_argument("--resume", type=str, default=None,

@@ -36,11 +36,24 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(0)
         v = torch.randn(d, device="cuda", generator=g)
         w = torch.randn(d, device="cuda", generator=g)
-        sk = CSVec(d, c, r, device="cuda", numBlocks=20)
         res = {"size": name, "d": d}
-        res["encode_binned_us"] = timeit(lambda: sk.accumulateVec(v, 1.0, w, 1e-3))
+        skb = CSVec(d, c, r, device="cuda", numBlocks=20, kernel="binned")
+        res["encode_binned_us"] = timeit(lambda: skb.accumulateVec(v, 1.0, w, 1e-3))
+        res["query_hash_us"] = timeit(lambda: skb.query())
         if d < 2e7:
-            res["encode_direct_us"] = timeit(lambda: sk.accumulateVec(v, 1.0, w, 1e-3, dense=False), 5)
+            res["encode_direct_us"] = timeit(lambda: skb.accumulateVec(v, 1.0, w, 1e-3, dense=False), 5)
+        del skb
+        torch.cuda.synchronize()
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        sk = CSVec(d, c, r, device="cuda", numBlocks=20, kernel="planned")
+        t0.record()
+        sk._plan()
+        t1.record()
+        t1.synchronize()
+        res["plan_build_ms"] = t0.elapsed_time(t1)
+        res["plan_mb"] = sum(t.numel() * t.element_size() for t in sk._plan()) / 2 ** 20
+        res["encode_planned_us"] = timeit(lambda: sk.accumulateVec(v, 1.0, w, 1e-3))
         res["query_us"] = timeit(lambda: sk.query())
         est = sk.query()
         res["topk_us"] = timeit(lambda: ops.topk_abs(est, k))

@@ -245,22 +245,29 @@ def test_augment_shapes_and_identity(device):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("d,c,r,nb", [(6568640, 500000, 5, 20), (1234567, 100003, 3, 1)])
-def test_large_sketch_gpu_matches_cpu_backend(d, c, r, nb):
-    """Full-size (ResNet-9 d) binned encode + query + top-k on the GPU vs the
+@pytest.mark.parametrize("kernel", ["planned", "binned"])
+def test_large_sketch_gpu_matches_cpu_backend(d, c, r, nb, kernel):
+    """Full-size (ResNet-9 d) encode + query + top-k on the GPU vs the
     native CPU backend (deterministic row-parallel encode)."""
     g = torch.Generator().manual_seed(0)
     v = torch.randn(d, generator=g) * torch.rand(d, generator=g) ** 4
     w = torch.randn(d, generator=g)
     cpu = CSVec(d, c, r, device="cpu", numBlocks=nb)
-    gpu = CSVec(d, c, r, device="cuda", numBlocks=nb)
+    gpu = CSVec(d, c, r, device="cuda", numBlocks=nb, kernel=kernel)
     cpu.accumulateVec(v, 2.0, w, 1e-3)
     gpu.accumulateVec(v.cuda(), 2.0, w.cuda(), 1e-3)
     torch.testing.assert_close(gpu.table.cpu(), cpu.table, rtol=1e-4, atol=1e-4)
     gpu.accumulateVec(v.cuda(), 2.0, w.cuda(), 1e-3)  # scratch re-armed: second encode adds
     torch.testing.assert_close(gpu.table.cpu(), 2 * cpu.table, rtol=1e-4, atol=2e-4)
     est_c = cpu.query()
-    est_g = CSVec(d, c, r, device="cuda", numBlocks=nb, table=cpu.table.cuda()).query()
+    est_g = gpu.like(cpu.table.cuda()).query()
     torch.testing.assert_close(est_g.cpu(), est_c)
+    if kernel == "planned":  # atomic-free: bitwise reproducible
+        t1 = gpu.like()
+        t1.accumulateVec(v.cuda(), 1.0)
+        t2 = gpu.like()
+        t2.accumulateVec(v.cuda(), 1.0)
+        assert torch.equal(t1.table, t2.table)
     ic, vc = ops.topk_abs(est_c, 50000)
     ig, vg = ops.topk_abs(est_g, 50000)
     assert torch.equal(ig.cpu(), ic) and torch.equal(vg.cpu(), vc)
