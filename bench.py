@@ -38,6 +38,8 @@ def main():
     p.add_argument("--client-size", type=int, default=5)
     p.add_argument("--num-clients", type=int, default=10000)
     p.add_argument("--encode", default="binned", choices=["planned", "binned", "direct"])
+    p.add_argument("--conv", default="native", choices=["native", "miopen"],
+                   help="3x3 conv units on the native MFMA kernels or on MIOpen")
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
     p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "1")),
                    help="torch.backends.cudnn.benchmark (MIOpen exhaustive find during warmup)")
@@ -59,7 +61,7 @@ def main():
             "--num_blocks", "20", "--num_clients", str(b.num_clients), "--num_workers", str(W),
             "--local_batch_size", "-1", "--weight_decay", "5e-4", "--dtype", "bf16",
             "--device", "cuda", "--encode", b.encode, "--seed", "21",
-            "--miopen_find", str(b.miopen_find)]
+            "--miopen_find", str(b.miopen_find), "--conv", b.conv]
     if b.profile:
         argv += ["--profile_dir", "gpurun_out/bench_profile"]
     args = parse_args(argv=argv, probe_port=False)

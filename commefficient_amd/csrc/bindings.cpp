@@ -549,6 +549,108 @@ at::Tensor relu_maxpool_backward_hip(const at::Tensor& gy, const at::Tensor& idx
   return gx;
 }
 
+// --------------------------------------------------------------- conv3x3
+const uint16_t* bf16_ptr(const at::Tensor& t) {
+  return reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+
+void check_nhwc_bf16(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 &&
+                  t.is_contiguous(at::MemoryFormat::ChannelsLast),
+              name, " must be a bf16 NCHW tensor with channels_last memory");
+}
+
+const uint16_t* opt_like(const c10::optional<at::Tensor>& t, const at::Tensor& y, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_nhwc_bf16(*t, name);
+  TORCH_CHECK(t->sizes() == y.sizes(), name, " must have the output's shape");
+  return bf16_ptr(*t);
+}
+
+// y = act(conv3x3(x, w)) ; w bf16 [K][3][3][C] contiguous
+at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
+                           const c10::optional<at::Tensor>& mask,
+                           const c10::optional<at::Tensor>& addend) {
+  check_nhwc_bf16(x, "conv3x3: x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 &&
+                  w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C,
+              "conv3x3: w must be contiguous bf16 [K, 3, 3, C]");
+  const int64_t K = w.size(0);
+  TORCH_CHECK(conv3x3_supported(static_cast<int>(C), static_cast<int>(K)),
+              "conv3x3: C and K must be multiples of 64");
+  TORCH_CHECK(N * H * W < (1ll << 31) && N * H * W * std::max(C, K) < (1ll << 40), "conv3x3: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, K, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  ConvFwdArgs a;
+  a.x = bf16_ptr(x);
+  a.w = bf16_ptr(w);
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.mask = opt_like(mask, y, "conv3x3: mask");
+  a.addend = opt_like(addend, y, "conv3x3: addend");
+  a.P = static_cast<int>(N * H * W);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.relu = relu ? 1 : 0;
+  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  return y;
+}
+
+// dw [K][C][3][3] fp32 = sum_p dy[p, k] x[p + (r-1, s-1), c]
+at::Tensor conv3x3_wgrad_hip(const at::Tensor& dy, const at::Tensor& x, int64_t splits) {
+  check_nhwc_bf16(dy, "conv3x3_wgrad: dy");
+  check_nhwc_bf16(x, "conv3x3_wgrad: x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "conv3x3_wgrad: shapes");
+  TORCH_CHECK(conv3x3_supported(static_cast<int>(C), static_cast<int>(K)) && K % 128 == 0,
+              "conv3x3_wgrad: C % 64 and K % 128 must be 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int P = static_cast<int>(N * H * W);
+  if (splits <= 0) splits = conv3x3_wgrad_splits(P, static_cast<int>(K), static_cast<int>(C));
+  auto dw = at::empty({K, C, 3, 3}, x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
+  auto slab = at::empty({splits * K * 9 * C}, dw.options());
+  ConvWgradArgs a;
+  a.dy = bf16_ptr(dy);
+  a.x = bf16_ptr(x);
+  a.slab = slab.data_ptr<float>();
+  a.P = P;
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.splits = static_cast<int>(splits);
+  launch_conv3x3_wgrad(a, dw.data_ptr<float>(), 0.f, cur_stream());
+  return dw;
+}
+
+// w fp32 [K][C][3][3] -> (wf bf16 [K][3][3][C], wt bf16 [C][3][3][K] flipped)
+std::tuple<at::Tensor, at::Tensor> conv_weight_prep_hip(const at::Tensor& w) {
+  check_f32(w, "conv_weight_prep: w");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "conv_weight_prep: [K, C, 3, 3]");
+  const int64_t K = w.size(0), C = w.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  auto wf = at::empty({K, 3, 3, C}, w.options().dtype(at::kBFloat16));
+  auto wt = at::empty({C, 3, 3, K}, w.options().dtype(at::kBFloat16));
+  launch_conv_weight_prep(w.data_ptr<float>(), reinterpret_cast<uint16_t*>(wf.data_ptr()),
+                          reinterpret_cast<uint16_t*>(wt.data_ptr()), static_cast<int>(K),
+                          static_cast<int>(C), cur_stream());
+  return {wf, wt};
+}
+
+at::Tensor relu_mask_hip(const at::Tensor& gy, const at::Tensor& y) {
+  check_nhwc_bf16(y, "relu_mask: y");
+  auto g = gy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(g, "relu_mask: gy");
+  TORCH_CHECK(g.sizes() == y.sizes() && y.numel() % 8 == 0, "relu_mask: shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  auto out = at::empty_like(g, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_relu_mask(bf16_ptr(g), bf16_ptr(y), reinterpret_cast<uint16_t*>(out.data_ptr()), y.numel(),
+                   cur_stream());
+  return out;
+}
+
 // One-time layout of the binned encode for a sketch geometry (hashes are
 // data-independent): counts[chunk, tile], base[chunk, tile] (global entry
 // index of the chunk's run in the tile's segment), seg[tile] (segment starts,
@@ -593,6 +695,10 @@ TORCH_LIBRARY(commeff, m) {
   m.def("binned_plan(int d, int r, int c) -> int[]", &commeff::binned_plan);
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
+  m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
+  m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
+  m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
+  m.def("relu_mask(Tensor gy, Tensor y) -> Tensor");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
         "int d) -> Tensor");
   m.def("cs_zero_buckets(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, Tensor hashes, "
@@ -647,6 +753,10 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("cs_query_planned", &cs_query_planned_hip);
   m.impl("relu_maxpool", &relu_maxpool_hip);
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
+  m.impl("conv3x3_fwd", &conv3x3_fwd_hip);
+  m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
+  m.impl("conv_weight_prep", &conv_weight_prep_hip);
+  m.impl("relu_mask", &relu_mask_hip);
   m.impl("cs_zero_buckets", &cs_zero_buckets_hip);
   m.impl("cs_l2estimate", &cs_l2estimate_hip);
   m.impl("topk_abs", &topk_abs_hip);

@@ -118,6 +118,39 @@ void launch_zero_at(float* a, float* b, float* c, const int64_t* idx,
 void launch_scatter_dense(float* out, int64_t n, const int64_t* idx,
                           const float* vals, int64_t k, hipStream_t stream);
 
+// ----------------------------------------------------------------- conv --
+// 3x3 / stride 1 / pad 1 NHWC bf16 convolution on MFMA (conv.hip).
+struct ConvFwdArgs {
+  const uint16_t* x;       // [P, C]  (P = N*H*W pixels, NHWC)
+  const uint16_t* w;       // [K, 3, 3, C]
+  uint16_t* y;             // [P, K]
+  const uint16_t* mask;    // optional [P, K]: y = 0 where mask <= 0
+  const uint16_t* addend;  // optional [P, K]: y += addend (after relu / mask)
+  int P, H, W, C, K;
+  int relu;
+};
+struct ConvWgradArgs {
+  const uint16_t* dy;  // [P, K]
+  const uint16_t* x;   // [P, C]
+  float* slab;         // [splits, K, 9, C] scratch
+  int P, H, W, C, K;
+  int splits;
+  int steps_per_split;  // set by the launcher
+  FastDivU32 div_w, div_h;
+};
+bool conv3x3_supported(int C, int K);
+void launch_conv3x3_fwd(const ConvFwdArgs& a, hipStream_t stream);
+int conv3x3_wgrad_splits(int P, int K, int C);
+// dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
+void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
+// w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 (either output optional) and
+// wt [C][3][3][K] bf16 spatially flipped (the dgrad weight)
+void launch_conv_weight_prep(const float* w, uint16_t* wf, uint16_t* wt, int K, int C,
+                             hipStream_t stream);
+// g = gy where y > 0 else 0 (bf16, n % 8 == 0)
+void launch_relu_mask(const uint16_t* gy, const uint16_t* y, uint16_t* g, int64_t n,
+                      hipStream_t stream);
+
 // ----------------------------------------------------------------- pool --
 // y = maxpool_k(relu(x)) on NHWC bf16 (C % 8 == 0, H, W % k == 0), k in {2, 4};
 // idx = window position of the max (255: max <= 0, gradient 0)

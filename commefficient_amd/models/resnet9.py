@@ -8,8 +8,9 @@ layer3(256->512, pool) + res3 -> maxpool 4 -> linear(512->classes, no bias) -> Ã
 BatchNorm is off unless ``do_batchnorm`` (cv_train.py:357).  6,568,640 params
 for 10 classes.
 
-MI355X notes: the convs run on MIOpen in bf16 channels_last under autocast;
-the ReLU+maxpool pairs are left to the framework's fusion.  Fixes reference
+MI355X notes: conv+ReLU(+maxpool) units run on the native MFMA implicit-GEMM
+kernels of csrc/conv.hip (bf16 channels_last, fused epilogues); the 3-channel
+prep conv and BatchNorm variants use MIOpen.  Fixes reference
 quirk Appendix C #12: ``finetune_parameters`` no longer touches an undefined
 ``self.iid``.
 """
@@ -20,7 +21,7 @@ import itertools
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import relu_maxpool
+from ..ops.nn import conv3x3_relu_pool, relu_maxpool
 from .common import GhostBatchNorm2d, Mul
 
 __all__ = ["ResNet9"]
@@ -61,6 +62,12 @@ class ConvBN(nn.Module):
             self.bn = _bn(c_out, bn_weight_init=bn_weight_init, **kw)
 
     def forward(self, x):
+        if not self.do_batchnorm and (self.pool is None or (
+                isinstance(self.pool, nn.MaxPool2d) and _square_pool(self.pool))):
+            # conv + relu (+ pool) as one unit: native MFMA conv kernels with
+            # fused epilogues when the shapes fit (csrc/conv.hip), else MIOpen
+            return conv3x3_relu_pool(x, self.conv.weight,
+                                     _k(self.pool) if self.pool is not None else 0)
         x = self.conv(x)
         if self.do_batchnorm:
             x = self.bn(x)

@@ -75,3 +75,26 @@ def scatter_dense(idx, vals, n):
 def augment_u8_nhwc(data, idx, pad, flip, mean, inv_std, seed, out_bf16=True, keys=None):
     return _ops().augment_u8_nhwc(data, idx, int(pad), bool(flip), mean, inv_std, int(seed),
                                   bool(out_bf16), keys)
+
+
+# ------------------------------------------------------------ conv3x3 (MFMA)
+def conv_weight_prep(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 [K, C, 3, 3] -> (bf16 [K, 3, 3, C], bf16 [C, 3, 3, K] spatially flipped)."""
+    return _ops().conv_weight_prep(w)
+
+
+def conv3x3_fwd(x, wf, relu: bool = False, mask=None, addend=None) -> torch.Tensor:
+    """act(conv3x3(x, wf)) on NHWC bf16; epilogue: relu, y=0 where mask<=0, y+=addend."""
+    return _ops().conv3x3_fwd(x, wf, bool(relu), mask, addend)
+
+
+def conv3x3_wgrad(dy, x, splits: int = 0) -> torch.Tensor:
+    """fp32 [K, C, 3, 3] weight gradient (deterministic split-K)."""
+    return _ops().conv3x3_wgrad(dy, x, int(splits))
+
+
+def relu_mask(gy, y) -> torch.Tensor:
+    return _ops().relu_mask(gy, y)
+
+
+__all__ += ["conv_weight_prep", "conv3x3_fwd", "conv3x3_wgrad", "relu_mask"]

@@ -38,3 +38,75 @@ def relu_maxpool(x: torch.Tensor, k: int) -> torch.Tensor:
     if fused_ok(x, k):
         return _ReluMaxPool.apply(x, k)
     return F.max_pool2d(F.relu(x), k)
+
+
+# ---------------------------------------------------------------- conv3x3
+# Backend switch for 3x3 convolutions that fit the native MFMA kernels
+# (csrc/conv.hip): "native" (default) or "miopen" (torch.nn.functional.conv2d).
+_CONV_BACKEND = ["native"]
+
+
+def set_conv_backend(name: str) -> None:
+    if name not in ("native", "miopen"):
+        raise ValueError(f"unknown conv backend {name!r}")
+    _CONV_BACKEND[0] = name
+
+
+def conv_backend() -> str:
+    return _CONV_BACKEND[0]
+
+
+class _Conv3x3Act(torch.autograd.Function):
+    """relu(conv3x3(x, w)) or maxpool_k(relu(conv3x3(x, w))), no bias.
+
+    Forward: the MFMA implicit-GEMM kernel with a fused ReLU epilogue (or the
+    fused relu+maxpool kernel on the conv output).  Backward: relu mask /
+    pool scatter, dgrad = the same forward kernel on the flipped, transposed
+    weight, wgrad = the transposed-LDS-read MFMA kernel with a deterministic
+    split-K reduction straight into the fp32 [K, C, 3, 3] gradient.
+    """
+
+    @staticmethod
+    def forward(ctx, x, weight, pool_k):
+        wf, wt = _ops().conv_weight_prep(weight.detach().contiguous())
+        if pool_k:
+            y = _ops().conv3x3_fwd(x, wf, False)
+            out, idx = _ops().relu_maxpool(y, pool_k)
+            del y
+            ctx.save_for_backward(x, wt, idx)
+        else:
+            out = _ops().conv3x3_fwd(x, wf, True)
+            ctx.save_for_backward(x, wt, out)
+        ctx.pool_k = pool_k
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, wt, aux = ctx.saved_tensors
+        gout = gout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if ctx.pool_k:
+            g = _ops().relu_maxpool_backward(gout, aux, ctx.pool_k)
+        else:
+            g = _ops().relu_mask(gout, aux)
+        gx = _ops().conv3x3_fwd(g, wt, False) if ctx.needs_input_grad[0] else None
+        gw = _ops().conv3x3_wgrad(g, x) if ctx.needs_input_grad[1] else None
+        return gx, gw, None
+
+
+def conv3x3_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    return (_CONV_BACKEND[0] == "native" and x.is_cuda and x.dtype == torch.bfloat16
+            and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and weight.dtype == torch.float32 and weight.dim() == 4
+            and tuple(weight.shape[2:]) == (3, 3) and weight.shape[1] == x.shape[1]
+            and x.shape[1] % 64 == 0 and weight.shape[0] % 128 == 0)
+
+
+def conv3x3_relu_pool(x: torch.Tensor, weight: torch.Tensor, pool_k: int = 0) -> torch.Tensor:
+    """``max_pool2d(relu(conv2d(x, weight, padding=1)), pool_k)`` (no pool when
+    ``pool_k == 0``).  Native MFMA kernels when :func:`conv3x3_native_ok`,
+    else the PyTorch (MIOpen) composition."""
+    if conv3x3_native_ok(x, weight) and (
+            pool_k == 0 or (x.shape[2] % pool_k == 0 and x.shape[3] % pool_k == 0)):
+        return _Conv3x3Act.apply(x, weight, int(pool_k))
+    y = F.conv2d(x, weight, padding=1)
+    return relu_maxpool(y, pool_k) if pool_k else F.relu(y)

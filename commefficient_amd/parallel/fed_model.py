@@ -107,6 +107,8 @@ class FedModel:
         self.model.to(self.device)
         if self.device.type == "cuda":
             torch.backends.cudnn.benchmark = bool(getattr(args, "miopen_find", 1))
+        from ..ops.nn import set_conv_backend
+        set_conv_backend(getattr(args, "conv", "native"))
         self.flat = FlatParams(self.model, self.device)
         self.d = self.flat.d
         args.grad_size = self.d

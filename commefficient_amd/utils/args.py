@@ -152,6 +152,9 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--miopen_find", type=int, default=1,
                    help="MIOpen exhaustive kernel search for each conv shape (cudnn.benchmark); "
                         "+14%% ResNet-9 throughput on MI355X")
+    g.add_argument("--conv", choices=["native", "miopen"], default="native",
+                   help="3x3 conv(+relu+pool) units: native MFMA kernels (csrc/conv.hip) "
+                        "where shapes fit, or MIOpen everywhere")
     g.add_argument("--gpt2_size", choices=["small", "tiny"], default="small",
                    help="GPT-2 architecture: 'small' = 124M GPT-2 (reference), 'tiny' for tests")
     return p

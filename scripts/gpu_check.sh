@@ -30,6 +30,8 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py --steps ${BENCH_STEPS:-30} --warmup 5 ;;
     benchprof) run bench_prof 600 python bench.py --steps 20 --warmup 5 --profile ;;
     codec) run codec 600 python scripts/bench_codec.py ;;
+    conv) run conv 600 python scripts/bench_conv.py ;;
+    convtest) run pytest_conv 600 python -m pytest tests/test_conv.py -x -q -m gpu ;;
     configs) for c in ${CONFIGS:-cifar100_fedavg imagenet_local_topk gpt2_sketch}; do
                run cfg_$c 900 python scripts/bench_configs.py --config $c; done ;;
     rocprof) run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o bench \

@@ -1,0 +1,149 @@
+"""Native MFMA conv3x3 kernels (csrc/conv.hip) vs fp32 PyTorch references of
+the same op (bf16 operands upcast, fp32 math)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from commefficient_amd import ops
+from commefficient_amd.ops import nn as cnn
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # N, C, H, W, K   (ResNet-9 layers at small batch + odd tiles)
+    (2, 64, 32, 32, 128),
+    (3, 128, 16, 16, 128),
+    (2, 128, 16, 16, 256),
+    (2, 256, 8, 8, 512),
+    (5, 512, 4, 4, 512),
+    (3, 64, 5, 7, 128),   # pixels not a multiple of the 128-pixel tile
+    (2, 128, 8, 8, 64),   # 64-wide output tile (dgrad of a 64-channel input)
+]
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _inputs(N, C, H, W, K, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = _nhwc(torch.randn(N, C, H, W, device="cuda", generator=g).to(torch.bfloat16))
+    w = torch.randn(K, C, 3, 3, device="cuda", generator=g) * (2.0 / (9 * C)) ** 0.5
+    return x, w
+
+
+def _close(a, b, rel=2e-2):
+    a, b = a.float(), b.float()
+    scale = b.abs().max().clamp_min(1e-6)
+    err = (a - b).abs().max() / scale
+    assert err < rel, f"max rel err {err.item():.3e}"
+
+
+@pytest.mark.parametrize("N,C,H,W,K", SHAPES)
+@pytest.mark.parametrize("relu", [False, True])
+def test_fwd_matches_fp32(N, C, H, W, K, relu):
+    x, w = _inputs(N, C, H, W, K)
+    wf, wt = ops.conv_weight_prep(w)
+    assert torch.equal(wf, w.permute(0, 2, 3, 1).to(torch.bfloat16))
+    assert torch.equal(wt, w.flip(2, 3).permute(1, 2, 3, 0).to(torch.bfloat16))
+    y = ops.conv3x3_fwd(x, wf, relu)
+    ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
+    if relu:
+        ref = ref.relu()
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == ref.shape
+    _close(y, ref)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", SHAPES[:3])
+def test_fwd_mask_and_addend_epilogue(N, C, H, W, K):
+    x, w = _inputs(N, C, H, W, K)
+    wf, _ = ops.conv_weight_prep(w)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    mask = _nhwc(torch.randn(N, K, H, W, device="cuda", generator=g).to(torch.bfloat16))
+    add = _nhwc(torch.randn(N, K, H, W, device="cuda", generator=g).to(torch.bfloat16))
+    y = ops.conv3x3_fwd(x, wf, False, mask, add)
+    ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
+    ref = torch.where(mask.float() > 0, ref, torch.zeros_like(ref)) + add.float()
+    _close(y, ref)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", SHAPES)
+def test_dgrad_matches_fp32(N, C, H, W, K):
+    # dx = conv(dy, wt): the forward kernel with C <-> K swapped
+    x, w = _inputs(N, C, H, W, K)
+    _, wt = ops.conv_weight_prep(w)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    dy = _nhwc(torch.randn(N, K, H, W, device="cuda", generator=g).to(torch.bfloat16))
+    if K % 64:
+        pytest.skip("dgrad input channels must be a multiple of 64")
+    dx = ops.conv3x3_fwd(dy, wt, False)
+    ref = torch.nn.grad.conv2d_input(x.shape, w.to(torch.bfloat16).float(), dy.float(), padding=1)
+    _close(dx, ref)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", [s for s in SHAPES if s[4] % 128 == 0])
+@pytest.mark.parametrize("splits", [0, 1, 3])
+def test_wgrad_matches_fp32(N, C, H, W, K, splits):
+    x, _ = _inputs(N, C, H, W, K)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    dy = _nhwc(torch.randn(N, K, H, W, device="cuda", generator=g).to(torch.bfloat16))
+    dw = ops.conv3x3_wgrad(dy, x, splits)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, 3, 3), dy.float(), padding=1)
+    assert dw.dtype == torch.float32 and dw.shape == ref.shape and dw.is_contiguous()
+    _close(dw, ref, rel=1e-3)
+    # deterministic: split-K slabs are reduced in a fixed order
+    assert torch.equal(dw, ops.conv3x3_wgrad(dy, x, splits))
+
+
+def test_relu_mask():
+    g = torch.Generator(device="cuda").manual_seed(4)
+    gy = _nhwc(torch.randn(2, 64, 8, 8, device="cuda", generator=g).to(torch.bfloat16))
+    y = _nhwc(torch.randn(2, 64, 8, 8, device="cuda", generator=g).to(torch.bfloat16).relu())
+    out = ops.relu_mask(gy, y)
+    assert torch.equal(out, torch.where(y > 0, gy, torch.zeros_like(gy)))
+
+
+@pytest.mark.parametrize("pool_k", [0, 2])
+@pytest.mark.parametrize("N,C,H,W,K", [(4, 64, 16, 16, 128), (3, 256, 8, 8, 512)])
+def test_conv_unit_autograd_matches_fp32(N, C, H, W, K, pool_k):
+    x, w = _inputs(N, C, H, W, K)
+    x = x.detach().requires_grad_(True)
+    w = w.detach().requires_grad_(True)
+    cnn.set_conv_backend("native")
+    assert cnn.conv3x3_native_ok(x, w)
+    y = cnn.conv3x3_relu_pool(x, w, pool_k)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    gy = torch.randn(y.shape, device="cuda", generator=g)
+    (y.float() * gy).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, padding=1).relu()
+    if pool_k:
+        yr = F.max_pool2d(yr, pool_k)
+    (yr * gy).sum().backward()
+    _close(y, yr)
+    # bf16 rounding of the forward output can flip a few relu/argmax decisions;
+    # compare gradients in a norm sense
+    for a, b in ((x.grad, xr.grad), (w.grad, wr.grad)):
+        rel = (a.float() - b).norm() / b.norm()
+        assert rel < 2e-2, rel.item()
+
+
+def test_resnet9_native_matches_miopen():
+    from commefficient_amd.models import ResNet9
+    torch.manual_seed(0)
+    m = ResNet9().cuda()
+    x = _nhwc(torch.randn(16, 3, 32, 32, device="cuda"))
+    out = {}
+    for backend in ("miopen", "native"):
+        cnn.set_conv_backend(backend)
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x.to(torch.bfloat16))
+        y.float().square().sum().backward()
+        out[backend] = (y.float().detach(), [p.grad.detach().clone() for p in m.parameters()])
+    cnn.set_conv_backend("native")
+    (ya, ga), (yb, gb) = out["miopen"], out["native"]
+    _close(yb, ya, rel=3e-2)
+    for a, b in zip(ga, gb):
+        rel = (a - b).norm() / a.norm().clamp_min(1e-12)
+        assert rel < 5e-2, rel.item()
