@@ -232,6 +232,180 @@ __global__ void __launch_bounds__(256, 2) conv_fwd_kernel(ConvFwdArgs a) {
   }
 }
 
+// --------------------------------------------- fwd / dgrad, LDS-DMA pipeline
+// 16 zero bytes: the source of every padding / tail row of the im2col operand,
+// so each LDS-DMA lane always loads (an exec-masked lane would leave stale LDS)
+__device__ __attribute__((aligned(16))) uint32_t g_conv_zero[4] = {0u, 0u, 0u, 0u};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Tile TBM (pixels) x BN (out channels) x 64, (TBM/64) x 2 waves of 64 x BN/2.
+// Operands go global -> LDS with global_load_lds_dwordx4 (no register staging)
+// through a 3-stage ring: the loads of step t+2 are in flight while step t
+// computes; one raw s_barrier per step (a __syncthreads would drain the
+// in-flight DMA with vmcnt(0)).  The LDS image is lane-linear per wave, the
+// XOR swizzle of off128 is applied on the SOURCE side (which 16-byte chunk a
+// lane fetches).
+template <int TBM, int BN>
+__global__ void __launch_bounds__(TBM * 2) conv_fwd_glds_kernel(ConvFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NT = TBM * 2;
+  constexpr int A_BYTES = TBM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int NSTAGE = 3;
+  constexpr int ALD = TBM * 8 / NT;  // 16-byte A chunks per thread per step (4)
+  constexpr int BLD = BN * 8 / NT;   // B chunks per thread per step
+  constexpr int NLD = ALD + BLD;
+  constexpr int NI = BN / 64;
+  static_assert(BLD >= 1, "B tile too small for the block");
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntn = a.K / BN;
+  const int tn = bid % ntn, tm = bid / ntn;
+  const int m0 = tm * TBM, n0 = tn * BN;
+  const int C = a.C, H = a.H, W = a.W;
+  const int CB = C >> 6;
+  const int KT = 9 * CB;
+
+  int a_pix[ALD], a_h[ALD], a_w[ALD], a_col[ALD];
+#pragma unroll
+  for (int i = 0; i < ALD; ++i) {
+    const int s = i * NT + tid;
+    const int row = s >> 3, lc = (s & 7) ^ ((row >> 1) & 7);
+    const int p = m0 + row;
+    a_pix[i] = p < a.P ? p : -1;
+    const int q = p / W;
+    a_w[i] = p - q * W;
+    a_h[i] = q % H;
+    a_col[i] = lc * 8;
+  }
+  const uint16_t* b_src[BLD];
+#pragma unroll
+  for (int j = 0; j < BLD; ++j) {
+    const int s = j * NT + tid;
+    const int row = s >> 3, lc = (s & 7) ^ ((row >> 1) & 7);
+    b_src[j] = a.w + static_cast<size_t>(n0 + row) * 9 * C + lc * 8;
+  }
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_conv_zero);
+  typedef __attribute__((address_space(3))) void lds_void_t;
+
+  int kr = 0, ks = 0, cb = 0;  // (r, s, channel block) of the next step to issue
+  auto issue = [&](int stage) __attribute__((always_inline)) {
+    unsigned char* base = smem + stage * STAGE + wid * 64 * 16;
+    const int dr = kr - 1, ds = ks - 1;
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+      const int hh = a_h[i] + dr, ww = a_w[i] + ds;
+      const bool ok = a_pix[i] >= 0 && static_cast<unsigned>(hh) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(ww) < static_cast<unsigned>(W);
+      const uint16_t* src =
+          ok ? a.x + static_cast<size_t>(a_pix[i] + dr * W + ds) * C + cb * 64 + a_col[i] : zero;
+      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(base + i * NT * 16), 16, 0, 0);
+    }
+    const int koff = (kr * 3 + ks) * C + cb * 64;
+#pragma unroll
+    for (int j = 0; j < BLD; ++j)
+      __builtin_amdgcn_global_load_lds(b_src[j] + koff,
+                                       (lds_void_t*)(base + A_BYTES + j * NT * 16),
+                                       16, 0, 0);
+    if (++cb == CB) {
+      cb = 0;
+      if (++ks == 3) { ks = 0; ++kr; }
+    }
+  };
+
+  f32x16_t acc[2][NI];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
+
+  issue(0);
+  if (KT > 1) issue(1);
+  const int hi = lane >> 5, lr = lane & 31;
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + 1 < KT) wait_vmcnt<NLD>(); else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < KT) issue((kt + 2) % NSTAGE);
+    const unsigned char* sA = smem + (kt % NSTAGE) * STAGE;
+    const unsigned char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int chk = 2 * kk + hi;
+      bf16x8_t af[2], bfr[NI];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+        af[mi] = *reinterpret_cast<const bf16x8_t*>(sA + off128(wr * 64 + mi * 32 + lr, chk));
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        bfr[ni] = *reinterpret_cast<const bf16x8_t*>(sB + off128(wc * (BN / 2) + ni * 32 + lr, chk));
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // ---- epilogue (as conv_fwd_kernel)
+  constexpr int LD = BN + 4;
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        const int col = wc * (BN / 2) + ni * 32 + lr;
+        ct[row * LD + col] = acc[mi][ni][e];
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+#pragma unroll 2
+  for (int e = tid; e < TBM * CPR; e += NT) {
+    const int row = e / CPR, cc = e - row * CPR;
+    const int p = m0 + row;
+    if (p >= a.P) continue;
+    const float4 lo = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8);
+    const float4 hi4 = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8 + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi4.x, hi4.y, hi4.z, hi4.w};
+    const size_t o = static_cast<size_t>(p) * a.K + n0 + cc * 8;
+    if (a.relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    if (a.mask != nullptr) {
+      const v4u m = *reinterpret_cast<const v4u*>(a.mask + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t hb = (m[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+        if ((hb & 0x8000u) || hb == 0u) v[j] = 0.f;
+      }
+    }
+    if (a.addend != nullptr) {
+      const v4u m = *reinterpret_cast<const v4u*>(a.addend + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += bf2f((m[j >> 1] >> (16 * (j & 1))) & 0xffffu);
+    }
+    v4u out;
+    out[0] = f2bf(v[0]) | (f2bf(v[1]) << 16);
+    out[1] = f2bf(v[2]) | (f2bf(v[3]) << 16);
+    out[2] = f2bf(v[4]) | (f2bf(v[5]) << 16);
+    out[3] = f2bf(v[6]) | (f2bf(v[7]) << 16);
+    *reinterpret_cast<v4u*>(a.y + o) = out;
+  }
+}
+
 // ------------------------------------------------------------------ wgrad
 // 256-byte rows (128 bf16), chunk 0..15; swizzle of cdna_hip_programming.md
 // T10 (b): conflict-free for the 32x32x16 transposed operand reads
@@ -452,7 +626,35 @@ void set_lds(F fn, int bytes) {
 
 bool conv3x3_supported(int C, int K) { return C % 64 == 0 && K % 64 == 0 && C >= 64 && K >= 64; }
 
+template <int TBM, int BN>
+void launch_fwd_glds(const ConvFwdArgs& a, hipStream_t stream) {
+  constexpr int lds_pipe = 3 * (TBM * 128 + BN * 128);
+  constexpr int lds_epi = TBM * (BN + 4) * 4;
+  constexpr int lds = lds_pipe > lds_epi ? lds_pipe : lds_epi;
+  static bool init = false;
+  if (!init) { set_lds(conv_fwd_glds_kernel<TBM, BN>, lds); init = true; }
+  const int mt = (a.P + TBM - 1) / TBM;
+  hipLaunchKernelGGL((conv_fwd_glds_kernel<TBM, BN>), dim3(mt * (a.K / BN)), dim3(TBM * 2), lds,
+                     stream, a);
+}
+
 void launch_conv3x3_fwd(const ConvFwdArgs& a, hipStream_t stream) {
+  static const int variant = [] {
+    const char* e = getenv("COMMEFF_CONV_FWD");
+    return e != nullptr && e[0] == 'r' ? 1 : 0;  // "regs": register-staged kernel
+  }();
+  if (variant == 0) {
+    const bool wide = a.K % 128 == 0;
+    const int bn = wide ? 128 : 64;
+    // 256-pixel tiles when they still give >= 2 blocks per CU, else 128
+    const bool big = static_cast<int64_t>((a.P + 255) / 256) * (a.K / bn) >= 512;
+    if (big) {
+      if (wide) launch_fwd_glds<256, 128>(a, stream); else launch_fwd_glds<256, 64>(a, stream);
+    } else {
+      if (wide) launch_fwd_glds<128, 128>(a, stream); else launch_fwd_glds<128, 64>(a, stream);
+    }
+    return;
+  }
   const int mt = (a.P + BM - 1) / BM;
   if (a.K % 128 == 0) {
     constexpr int BN = 128;
