@@ -237,6 +237,12 @@ __global__ void __launch_bounds__(256, 2) conv_fwd_kernel(ConvFwdArgs a) {
 // so each LDS-DMA lane always loads (an exec-masked lane would leave stale LDS)
 __device__ __attribute__((aligned(16))) uint32_t g_conv_zero[4] = {0u, 0u, 0u, 0u};
 
+// (a plain device function: referenced from a kernel template, the target
+// builtin would make the host-side instantiation fail)
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt");
@@ -292,8 +298,6 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_glds_kernel(ConvFwdArgs a) {
     b_src[j] = a.w + static_cast<size_t>(n0 + row) * 9 * C + lc * 8;
   }
   const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_conv_zero);
-  typedef __attribute__((address_space(3))) void lds_void_t;
-
   int kr = 0, ks = 0, cb = 0;  // (r, s, channel block) of the next step to issue
   auto issue = [&](int stage) __attribute__((always_inline)) {
     unsigned char* base = smem + stage * STAGE + wid * 64 * 16;
@@ -305,14 +309,12 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_glds_kernel(ConvFwdArgs a) {
                       static_cast<unsigned>(ww) < static_cast<unsigned>(W);
       const uint16_t* src =
           ok ? a.x + static_cast<size_t>(a_pix[i] + dr * W + ds) * C + cb * 64 + a_col[i] : zero;
-      __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(base + i * NT * 16), 16, 0, 0);
+      glds16(src, base + i * NT * 16);
     }
     const int koff = (kr * 3 + ks) * C + cb * 64;
 #pragma unroll
     for (int j = 0; j < BLD; ++j)
-      __builtin_amdgcn_global_load_lds(b_src[j] + koff,
-                                       (lds_void_t*)(base + A_BYTES + j * NT * 16),
-                                       16, 0, 0);
+      glds16(b_src[j] + koff, base + A_BYTES + j * NT * 16);
     if (++cb == CB) {
       cb = 0;
       if (++ks == 3) { ks = 0; ++kr; }
