@@ -128,6 +128,7 @@ struct ConvFwdArgs {
   const uint16_t* addend;  // optional [P, K]: y += addend (after relu / mask)
   int P, H, W, C, K;
   int relu;
+  FastDivU32 div_w, div_h;  // set by the launcher
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]
@@ -139,7 +140,7 @@ struct ConvWgradArgs {
   FastDivU32 div_w, div_h;
 };
 bool conv3x3_supported(int C, int K);
-void launch_conv3x3_fwd(const ConvFwdArgs& a, hipStream_t stream);
+void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
