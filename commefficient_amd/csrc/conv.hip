@@ -174,6 +174,22 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
   issue(0);
   if (NSTAGE == 3 && KT > 1) issue(1);
   const int hi = lane >> 5, lr = lane & 31;
+  // byte offsets (inside a stage's A / B image) of this lane's fragments
+  int offA[4][2], offB[4][NI];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int chk = 2 * kk + hi;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int row = wr * 64 + mi * 32 + lr;
+      offA[kk][mi] = row * 128 + ((chk ^ sw_rd128(row)) << 4);
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int row = wc * (BN / 2) + ni * 32 + lr;
+      offB[kk][ni] = row * 128 + ((chk ^ sw_rd128(row)) << 4);
+    }
+  }
   int rd = 0, wrs = NSTAGE - 1;  // stage read this step / stage written next
   for (int kt = 0; kt < KT; ++kt) {
     if constexpr (NSTAGE == 3) {
@@ -186,25 +202,28 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
     if (kt + NSTAGE - 1 < KT) issue(wrs);
     const unsigned char* sA = smem + rd * STAGE;
     const unsigned char* sB = sA + A_BYTES;
+    // fragments of sub-step kk+1 are read while the MFMAs of kk run
+    bf16x8_t af[2][2], bfr[2][NI];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) af[0][mi] = *reinterpret_cast<const bf16x8_t*>(sA + offA[0][mi]);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) bfr[0][ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[0][ni]);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      const int chk = 2 * kk + hi;
-      bf16x8_t af[2], bfr[NI];
+      const int cur = kk & 1, nxt = cur ^ 1;
+      if (kk + 1 < 4) {
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        const int row = wr * 64 + mi * 32 + lr;
-        af[mi] = *reinterpret_cast<const bf16x8_t*>(sA + row * 128 + ((chk ^ sw_rd128(row)) << 4));
-      }
+        for (int mi = 0; mi < 2; ++mi)
+          af[nxt][mi] = *reinterpret_cast<const bf16x8_t*>(sA + offA[kk + 1][mi]);
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        const int row = wc * (BN / 2) + ni * 32 + lr;
-        bfr[ni] = *reinterpret_cast<const bf16x8_t*>(sB + row * 128 + ((chk ^ sw_rd128(row)) << 4));
+        for (int ni = 0; ni < NI; ++ni)
+          bfr[nxt][ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[kk + 1][ni]);
       }
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
     }
     rd = rd + 1 == NSTAGE ? 0 : rd + 1;
     wrs = wrs + 1 == NSTAGE ? 0 : wrs + 1;
@@ -266,18 +285,23 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
 
 // ------------------------------------------------------------------ wgrad
 // one 32(col) x 16(k) MFMA operand from an image [k rows][cols]: lane holds
-// col = cb + (lane & 31), k = kbase + 8 * (lane >> 5) + j   (T10 recipe)
+// col = cb + (lane & 31), k = 8 * (lane >> 5) + j (T10 recipe: lane 4q+p of a
+// 16-lane group addresses row q, columns 4p..4p+3 of its 4 x 16 block).
+// Sub-step kk reads rows +16 kk: with either swizzle the XOR term is the same.
 template <int ROWB>
-__device__ __forceinline__ bf16x8_t tr_operand(const unsigned char* img, int kbase, int cb, int lane) {
+__device__ __forceinline__ void tr_offsets(int cb, int lane, int (&off)[2]) {
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int col = cb + 16 * (g & 1) + 4 * p;
-  const int row = kbase + 8 * (g >> 1) + q;
+  const int row = 8 * (g >> 1) + q;
   const int chk = col >> 3, inb = (p & 1) * 8;
+  off[0] = tr_off<ROWB>(row, chk) + inb;
+  off[1] = tr_off<ROWB>(row + 4, chk) + inb;
+}
+
+__device__ __forceinline__ bf16x8_t tr_read(const unsigned char* a0, const unsigned char* a1) {
   typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
-  lds_s16x4_t* p0 = (lds_s16x4_t*)(img + tr_off<ROWB>(row, chk) + inb);
-  lds_s16x4_t* p1 = (lds_s16x4_t*)(img + tr_off<ROWB>(row + 4, chk) + inb);
-  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(p0);
-  const s16x4_t up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(p1);
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)a0);
+  const s16x4_t up = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)a1);
   const s16x8_t r = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
   return __builtin_bit_cast(bf16x8_t, r);
 }
@@ -377,6 +401,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
 
   if (nsteps > 0) issue(0);
   if (NSTAGE == 3 && nsteps > 1) issue(1);
+  // this lane's transposed-read offsets at sub-step 0 (the swizzles do not
+  // depend on the sub-step: sub-step kk adds kk * 16 rows)
+  int toA[2][2], toB[NI][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) tr_offsets<256>(wr * 64 + mi * 32, lane, toA[mi]);
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) tr_offsets<BN * 2>(wc * (BN / 2) + ni * 32, lane, toB[ni]);
   int rd = 0, wrs = NSTAGE - 1;
   for (int st = 0; st < nsteps; ++st) {
     if constexpr (NSTAGE == 3) {
@@ -389,19 +420,28 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     if (st + NSTAGE - 1 < nsteps) issue(wrs);
     const unsigned char* sA = smem + rd * STAGE;
     const unsigned char* sB = sA + A_BYTES;
+    bf16x8_t af[2][2], bfr[2][NI];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) af[0][mi] = tr_read(sA + toA[mi][0], sA + toA[mi][1]);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) bfr[0][ni] = tr_read(sB + toB[ni][0], sB + toB[ni][1]);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      bf16x8_t af[2], bfr[NI];
+      const int cur = kk & 1, nxt = cur ^ 1;
+      if (kk + 1 < 4) {
+        const int da = (kk + 1) * 16 * 256, db = (kk + 1) * 16 * BN * 2;
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) af[mi] = tr_operand<256>(sA, kk * 16, wr * 64 + mi * 32, lane);
+        for (int mi = 0; mi < 2; ++mi)
+          af[nxt][mi] = tr_read(sA + toA[mi][0] + da, sA + toA[mi][1] + da);
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-        bfr[ni] = tr_operand<BN * 2>(sB, kk * 16, wc * (BN / 2) + ni * 32, lane);
+        for (int ni = 0; ni < NI; ++ni)
+          bfr[nxt][ni] = tr_read(sB + toB[ni][0] + db, sB + toB[ni][1] + db);
+      }
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
     }
     rd = rd + 1 == NSTAGE ? 0 : rd + 1;
     wrs = wrs + 1 == NSTAGE ? 0 : wrs + 1;
@@ -432,6 +472,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __r
   for (size_t i4 = blockIdx.x * 256ull + threadIdx.x; i4 < n4; i4 += static_cast<size_t>(gridDim.x) * 256) {
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     const float4* src = reinterpret_cast<const float4*>(slab) + i4;
+#pragma unroll 8
     for (int t = 0; t < splits; ++t) {
       const float4 v = src[t * n4];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
