@@ -17,6 +17,7 @@ import datetime
 import os
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -72,6 +73,20 @@ def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> 
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _CTX = DistCtx(rank, world, local, device, backend if world > 1 else "none")
     return _CTX
+
+
+def h2d(x, device, dtype=None) -> torch.Tensor:
+    """Host array / CPU tensor -> ``device`` without a stream sync: a pageable
+    ``.to(device)`` waits for every kernel queued before it (the GPU then
+    idles while the host enqueues the rest of the round), so stage through
+    pinned memory and copy asynchronously on the current stream."""
+    t = x if torch.is_tensor(x) else torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    device = torch.device(device)
+    if device.type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
 
 
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:

@@ -329,8 +329,8 @@ class FedModel:
         mets = [torch.cat([m[i] for m in metrics_all]) for i in range(len(metrics_all[0]))] \
             if metrics_all else []
         # per-client mean metrics into their global slots
-        slots_t = torch.from_numpy(slot_per_ex).to(self.device)
-        n_t = torch.from_numpy(counts.astype(np.float32)).to(self.device)
+        slots_t = dist.h2d(slot_per_ex, self.device)
+        n_t = dist.h2d(counts.astype(np.float32), self.device)
         rows = [per_ex] + mets
         msum = torch.zeros(len(rows), W, device=self.device)
         for i, r in enumerate(rows):

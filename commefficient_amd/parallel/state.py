@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from .dist import h2d
 
 
 class ClientStateStore:
@@ -148,10 +149,10 @@ class ByteAccountant:
         dl = torch.empty(len(clients), dtype=torch.float64, device=self.device)
         counts_all = []
         for s in range(0, len(thr), 1024):
-            counts_all.append(ops.count_ge(self.last_mod, torch.from_numpy(thr[s:s + 1024])))
+            counts_all.append(ops.count_ge(self.last_mod, h2d(thr[s:s + 1024], self.device)))
         counts = torch.cat(counts_all).to(torch.float64) * 4.0
-        dl.copy_(counts[torch.from_numpy(inv).to(self.device)])
-        cl = torch.from_numpy(clients.astype(np.int64)).to(self.device)
+        dl.copy_(counts[h2d(inv.astype(np.int64), self.device)])
+        cl = h2d(clients.astype(np.int64), self.device)
         self.client_download.index_add_(0, cl, dl)
         self.client_upload.index_add_(0, cl, torch.full_like(dl, float(self.upload_per_client)))
         self.last_seen[clients] = round_idx
