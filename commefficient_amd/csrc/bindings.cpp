@@ -4,6 +4,7 @@
 // DeviceType::CUDA, so the device guard / current stream come from the
 // "MasqueradingAsCUDA" HIP classes.
 #include <ATen/ATen.h>
+#include <ATen/Parallel.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
@@ -452,27 +453,60 @@ at::Tensor cs_hash_all_hip(const at::Tensor& hashes, const at::Tensor& blk_off,
   return out;
 }
 
-PlannedArgs planned_args(at::TensorList plan, const BinPlan& p, int64_t d, int64_t r) {
-  // plan = [src_info i16, ent_info i16, perm i32, csr i32, base i32, off i32, seg i32, vals f32]
+// CPU twin of cs_hash_all (same host/device hash code): lets the plan
+// builder and its invariants be tested without a GPU
+at::Tensor cs_hash_all_cpu(const at::Tensor& hashes, const at::Tensor& blk_off,
+                           const at::Tensor& blk_sign, int64_t num_blocks, int64_t d, int64_t c,
+                           const at::Tensor& like) {
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, c, false);
+  const int64_t r = ctx.geom.r;
+  const int64_t nb = ctx.geom.num_blocks;
+  auto out = at::empty({d, r}, like.options().dtype(at::kInt));
+  int32_t* o = out.data_ptr<int32_t>();
+  at::parallel_for(0, d, 1 << 14, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) {
+      uint32_t blk, t;
+      split_block(static_cast<uint32_t>(i), ctx.geom, &blk, &t);
+      for (int64_t j = 0; j < r; ++j) {
+        uint32_t bk;
+        float s;
+        hash_t(ctx.rows.row[j], t, blk, ctx.geom, ctx.blk_off + j * nb, ctx.blk_sign + j * nb, &bk,
+               &s);
+        o[i * r + j] = static_cast<int32_t>(bk | (s < 0.f ? 0x80000000u : 0u));
+      }
+    }
+  });
+  return out;
+}
+
+PlanGeom plan_geom_or_throw(int64_t d, int64_t r, int64_t c) {
+  PlanGeom p;
+  TORCH_CHECK(planned_geometry(d, r, c, &p), "planned sketch: unsupported geometry d=", d,
+              " r=", r, " c=", c);
+  return p;
+}
+
+PlannedArgs planned_args(at::TensorList plan, const PlanGeom& p, int64_t d, int64_t r) {
+  // plan = [src_info i16, ent_info i16, perm i16, csr i32, base i32, off i32, seg i32, vals f32]
   TORCH_CHECK(plan.size() == 8, "plan must have 8 tensors");
   const int64_t n = d * r;
-  // LDS: 8960 staged floats + 2 run tables of num_tiles words within 160 KB
-  TORCH_CHECK(p.num_tiles <= kPlannedMaxTiles && n < (int64_t{1} << 31) && r <= kMaxRows,
-              "planned sketch: geometry too large (r*c <= ", kPlannedMaxTiles * 8192,
-              ", d*r < 2^31, r <= ", kMaxRows, ")");
   TORCH_CHECK(plan[0].numel() == n && plan[1].numel() == n && plan[2].numel() == n &&
-                  plan[3].numel() == p.num_tiles * 8192 + 1 &&
+                  plan[3].numel() == p.num_tiles * p.tile + 1 &&
                   plan[4].numel() == p.num_chunks * p.num_tiles &&
-                  plan[5].numel() == p.num_chunks * p.num_tiles &&
+                  plan[5].numel() == p.num_chunks * (p.num_tiles + 1) &&
                   plan[6].numel() == p.num_tiles + 1 && plan[7].numel() >= n,
               "sketch plan does not match the geometry");
-  TORCH_CHECK(plan[0].scalar_type() == at::kShort && plan[1].scalar_type() == at::kShort &&
-                  plan[7].scalar_type() == at::kFloat,
-              "sketch plan dtypes");
+  for (int i = 0; i < 3; ++i)
+    TORCH_CHECK(plan[i].scalar_type() == at::kShort && plan[i].is_contiguous(), "plan[", i,
+                "] must be contiguous int16");
+  for (int i = 3; i < 7; ++i)
+    TORCH_CHECK(plan[i].scalar_type() == at::kInt && plan[i].is_contiguous(), "plan[", i,
+                "] must be contiguous int32");
+  TORCH_CHECK(plan[7].scalar_type() == at::kFloat, "plan[7] must be float32");
   PlannedArgs a;
   a.src_info = reinterpret_cast<const uint16_t*>(plan[0].data_ptr<int16_t>());
   a.ent_info = reinterpret_cast<const uint16_t*>(plan[1].data_ptr<int16_t>());
-  a.perm = plan[2].data_ptr<int32_t>();
+  a.perm = reinterpret_cast<const uint16_t*>(plan[2].data_ptr<int16_t>());
   a.csr = plan[3].data_ptr<int32_t>();
   a.base = plan[4].data_ptr<int32_t>();
   a.off = plan[5].data_ptr<int32_t>();
@@ -486,33 +520,33 @@ void cs_encode_planned_hip(at::Tensor table, const at::Tensor& vec, double scale
                            at::TensorList plan) {
   check_f32(table, "table");
   check_f32(vec, "vec");
+  if (wvec.has_value() && wvec->defined()) {
+    check_f32(*wvec, "wvec");
+    TORCH_CHECK(wvec->numel() == vec.numel(), "wvec must match vec");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   const int64_t d = vec.numel(), r = table.numel() / c;
-  SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
-                           static_cast<uint32_t>(c), 1);
-  BinPlan p = plan_cs_encode_binned(g);
+  const PlanGeom p = plan_geom_or_throw(d, r, c);
   launch_cs_encode_planned(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
-                           static_cast<float>(scale), static_cast<float>(wscale), g, p,
-                           planned_args(plan, p, d, r), cur_stream());
+                           static_cast<float>(scale), static_cast<float>(wscale), d,
+                           static_cast<int>(r), c, p, planned_args(plan, p, d, r), cur_stream());
 }
 
 at::Tensor cs_query_planned_hip(const at::Tensor& table, int64_t d, at::TensorList plan) {
   check_f32(table, "table");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   const int64_t c = table.size(-1), r = table.numel() / c;
-  SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
-                           static_cast<uint32_t>(c), 1);
-  BinPlan p = plan_cs_encode_binned(g);
+  const PlanGeom p = plan_geom_or_throw(d, r, c);
   auto est = at::empty({d}, table.options());
-  launch_cs_query_planned(table.data_ptr<float>(), est.data_ptr<float>(), g, p,
-                          planned_args(plan, p, d, r), cur_stream());
+  launch_cs_query_planned(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(r),
+                          c, p, planned_args(plan, p, d, r), cur_stream());
   return est;
 }
 
-std::vector<int64_t> binned_plan(int64_t d, int64_t r, int64_t c) {
-  SketchGeom g = make_geom(static_cast<uint32_t>(d), static_cast<uint32_t>(r),
-                           static_cast<uint32_t>(c), 1);
-  BinPlan p = plan_cs_encode_binned(g);
+// [tile, num_tiles, chunk, num_chunks] of the planned sketch, [] if unsupported
+std::vector<int64_t> plan_geometry(int64_t d, int64_t r, int64_t c) {
+  PlanGeom p;
+  if (!planned_geometry(d, r, c, &p)) return {};
   return {p.tile, p.num_tiles, p.chunk, p.num_chunks};
 }
 
@@ -692,7 +726,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("cs_encode_planned(Tensor(a!) table, Tensor vec, float scale, Tensor? wvec, float wscale, "
         "int c, Tensor[] plan) -> ()");
   m.def("cs_query_planned(Tensor table, int d, Tensor[] plan) -> Tensor");
-  m.def("binned_plan(int d, int r, int c) -> int[]", &commeff::binned_plan);
+  m.def("plan_geometry(int d, int r, int c) -> int[]", &commeff::plan_geometry);
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
@@ -741,6 +775,7 @@ TORCH_LIBRARY_IMPL(commeff, CPU, m) {
   m.impl("zero_at", &zero_at_cpu);
   m.impl("scatter_dense", &scatter_dense_cpu);
   m.impl("augment_u8_nhwc", &augment_cpu);
+  m.impl("cs_hash_all", &cs_hash_all_cpu);
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {

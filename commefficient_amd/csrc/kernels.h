@@ -38,25 +38,35 @@ void launch_cs_encode_binned(float* table, const float* vec, const float* wvec,
                              const float* blk_sign, const BinPlan& plan,
                              const uint32_t* counts, const uint32_t* base,
                              const uint32_t* seg, void* entries, hipStream_t stream);
-// Planned (precomputed-permutation) encode / query, see sketch_planned.hip.
-constexpr int64_t kPlannedMaxTiles = 15000;
+// Planned (precomputed-permutation, atomic-free) encode / query, see
+// sketch_planned.hip and ops/sketch_plan.py.
+constexpr int64_t kPlanSegCap = 32767;    // max entries of one tile segment (LDS, 15-bit ids)
+constexpr int64_t kPlanStageCap = 65535;  // max entries of one coordinate chunk (16-bit slots)
+struct PlanGeom {
+  int64_t tile;        // buckets per tile (power of 2, 512..4096)
+  int64_t num_tiles;   // ceil(r*c / tile)
+  int64_t chunk;       // coordinates per chunk
+  int64_t num_chunks;
+};
+// false when the geometry does not fit (too many entries per bucket)
+bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out);
 struct PlannedArgs {
-  const uint16_t* src_info;  // [d*r]  in-chunk staging slot | sign << 15
-  const uint16_t* ent_info;  // [d*r]  in-tile bucket | sign << 15 (entry order)
-  const int32_t* perm;       // [d*r]  entry indices sorted by (tile, bucket)
-  const int32_t* csr;        // [num_tiles*8192 + 1]
-  const int32_t* base;       // [num_chunks, num_tiles]
-  const int32_t* off;        // [num_chunks, num_tiles]
-  const int32_t* seg;        // [num_tiles + 1]
+  const uint16_t* src_info;  // [d*r]  slot of (i,j) in its chunk's stage
+  const uint16_t* ent_info;  // [d*r]  entry order: in-tile bucket | sign << 15
+  const uint16_t* perm;      // [d*r]  bucket order: segment-local entry | sign << 15
+  const int32_t* csr;        // [num_tiles*tile + 1] bucket starts in perm
+  const int32_t* base;       // [num_chunks, num_tiles] global run starts
+  const int32_t* off;        // [num_chunks, num_tiles + 1] in-chunk run starts
+  const int32_t* seg;        // [num_tiles + 1] tile segment starts
   float* vals;               // [d*r] scratch
 };
 void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
                         const float* blk_sign, int32_t* out, hipStream_t stream);
 void launch_cs_encode_planned(float* table, const float* vec, const float* wvec, float scale,
-                              float wscale, const SketchGeom& g, const BinPlan& p,
+                              float wscale, int64_t d, int r, int64_t c, const PlanGeom& p,
                               const PlannedArgs& a, hipStream_t stream);
-void launch_cs_query_planned(const float* table, float* est, const SketchGeom& g,
-                             const BinPlan& p, const PlannedArgs& a, hipStream_t stream);
+void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,
+                             const PlanGeom& p, const PlannedArgs& a, hipStream_t stream);
 // est[i] = lower-median_j( s_j(i) * table[j, b_j(i)] )
 void launch_cs_query(const float* table, float* est, const RowHashes& h,
                      const SketchGeom& g, const int32_t* blk_off,

@@ -1,25 +1,33 @@
-// "Planned" Count-Sketch encode and query for gfx950: atomic-free and
-// bitwise deterministic.
+// "Planned" Count-Sketch encode and query for gfx950: no atomics anywhere,
+// bitwise deterministic, every global access a coalesced stream or a short
+// contiguous run.
 //
-// Every hash is data-independent, so the scatter  table[j, h_j(i)] +=
-// s_j(i) v_i  (and its transpose, the query gather) is a FIXED sparse
-// pattern.  A one-time plan (ops/sketch_plan.py, built with torch sorts on
-// the device) lays the r*d entries (i, j) out tile-major -- 8192-bucket table
-// tiles, then coordinate chunks, then (i, j) order -- and records:
-//   src_info[i*r+j] : u16  LDS staging slot of (i,j) inside its chunk | sign<<15
-//   ent_info[e]     : u16  local bucket of entry e inside its tile   | sign<<15
-//   perm[x], csr    : entry indices of each tile sorted by local bucket (CSR)
-//   base/off [chunk][tile], seg[tile] : run starts (global / in-chunk), tile segments
-// Encode  P1 (per chunk):  stage[slot] = +-v_i  (LDS, no atomics), stream the
-//                          chunk's per-tile runs out contiguously -> vals[e]
-//         P2 (per bucket): table[b] += sum vals[perm[csr[b]..csr[b+1])]
-//                          (gathers stay inside one tile's L2-resident segment)
-// Query   Q1 (per tile):   vals[e] = +-table[tile, lb(e)]  (tile staged in LDS)
-//         Q2 (per chunk):  gather the chunk's runs into LDS, each thread takes
-//                          its coordinate's r values from LDS, lower median.
-// Replaces LDS/global atomics (measured ~220 us per pass at ResNet-9 size,
-// profiles/r1_v2_bench_kernel_stats.txt) and the 33M random table gathers of
-// the direct query with coalesced streams.
+// The hashes are data-independent, so the scatter table[j, h_j(i)] +=
+// s_j(i) v_i (and its transpose, the query gather) is a FIXED sparse pattern.
+// A one-time plan (ops/sketch_plan.py, built with device sorts) lays the r*d
+// entries (i, j) out tile-major -- T-bucket table tiles (T = 512..4096), then
+// coordinate chunks, then (i, j) order -- so that
+//   * a coordinate chunk's entries for one tile are a contiguous RUN of the
+//     tile's segment (runs of ~30 entries), and
+//   * a tile's whole segment (<= 32767 entries) fits in LDS.
+// Plan arrays:
+//   src_info[i*r+j] u16  slot of entry (i,j) in its chunk's LDS stage
+//   ent_info[e]     u16  in-tile bucket of entry e | sign << 15 (entry order)
+//   perm[x]         u16  segment-local entry index | sign << 15, bucket order
+//   csr[gb]         i32  bucket start in perm (global bucket gb = j*c + h)
+//   base/off        i32  run starts per (chunk, tile): global / in-chunk
+//   seg[t]          i32  tile segment starts
+//   vals            f32  d*r scratch shared by encode and query
+// Encode  P1 (block per chunk): stage[slot] = v_i (LDS, no atomics), then
+//            copy the chunk's runs out: vals[run] = stage[run']
+//         P2 (block per tile):  the segment -> LDS; thread per bucket sums
+//            +-S[perm[x]] over its csr range; table tile += sums
+// Query   Q1 (block per tile):  tile -> LDS; vals[e] = +-tile[lb(e)]
+//         Q2 (block per chunk): runs -> LDS stage; per coordinate the
+//            lower median of its r staged values
+// Measured predecessor (global-gather P2): 603 us at ResNet-9 size vs 229+215
+// for the LDS-atomic binned encode (profiles/, PMC: LDS float atomics retire
+// ~0.4 lanes/clk/CU, gathers from a 430 KB segment miss L2 every time).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "kernels.h"
@@ -27,106 +35,96 @@
 namespace commeff {
 namespace {
 
-constexpr int kTileShift = 13;
-constexpr uint32_t kTile = 1u << kTileShift;
-constexpr int kStageEntries = 8960;
+constexpr int kLdsBytes = 160 * 1024;
 
-__device__ __forceinline__ float signed_v(float v, uint16_t info) {
+__device__ __forceinline__ float signed_v(float v, uint32_t info) {
   return (info & 0x8000u) ? -v : v;
 }
 
-// index of the run (tile) containing in-chunk slot e: largest t with off[t] <= e
-__device__ __forceinline__ uint32_t run_of(const uint32_t* off, uint32_t num_tiles, uint32_t e) {
-  uint32_t lo = 0, hi = num_tiles;  // invariant: off[lo] <= e
-  while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
-    if (off[mid] <= e) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
 // ------------------------------------------------------------- encode P1
-__global__ void __launch_bounds__(256)
+template <int R>
+__global__ void __launch_bounds__(512)
 enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, float scale,
-              float wscale, uint32_t d, uint32_t r, uint32_t chunk, uint32_t num_tiles,
+              float wscale, uint32_t d, uint32_t r_rt, uint32_t chunk, uint32_t num_tiles,
               const uint16_t* __restrict__ src_info, const int32_t* __restrict__ base,
               const int32_t* __restrict__ off, float* __restrict__ vals) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* stage = reinterpret_cast<float*>(smem);
-  uint32_t* soff = reinterpret_cast<uint32_t*>(stage + kStageEntries);
-  uint32_t* sbase = soff + num_tiles;
-  const size_t row = static_cast<size_t>(blockIdx.x) * num_tiles;
-  for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) {
-    soff[t] = static_cast<uint32_t>(off[row + t]);
-    sbase[t] = static_cast<uint32_t>(base[row + t]);
-  }
+  const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
   const uint32_t i0 = blockIdx.x * chunk;
   const uint32_t i1 = min(d, i0 + chunk);
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+  const uint32_t total = (i1 - i0) * r;
+  float* stage = reinterpret_cast<float*>(smem);
+  uint32_t* soff = reinterpret_cast<uint32_t*>(stage + chunk * r);
+  uint32_t* sbase = soff + num_tiles + 1;
+  const size_t orow = static_cast<size_t>(blockIdx.x) * (num_tiles + 1);
+  const size_t brow = static_cast<size_t>(blockIdx.x) * num_tiles;
+  for (uint32_t t = threadIdx.x; t <= num_tiles; t += blockDim.x) soff[t] = off[orow + t];
+  for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
+  // entries in (i, j) order: coalesced src_info stream; v_i re-read from L1
+  const uint16_t* si = src_info + static_cast<size_t>(i0) * r;
+  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
+    const uint32_t i = i0 + e / r;
     float v = scale * vec[i];
     if (wvec != nullptr) v += wscale * wvec[i];
-    const uint16_t* si = src_info + static_cast<size_t>(i) * r;
-    for (uint32_t j = 0; j < r; ++j) {
-      const uint16_t info = si[j];
-      stage[info & 0x3fffu] = signed_v(v, info);
-    }
+    stage[si[e]] = v;
   }
   __syncthreads();
-  const uint32_t total = (i1 - i0) * r;
-  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
-    const uint32_t t = run_of(soff, num_tiles, e);
-    vals[static_cast<size_t>(sbase[t]) + (e - soff[t])] = stage[e];
+  // runs: one half-wave per (chunk, tile) run
+  const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
+  for (uint32_t t = hw; t < num_tiles; t += nhw) {
+    const uint32_t o = soff[t], len = soff[t + 1] - o;
+    float* dst = vals + sbase[t];
+    for (uint32_t k = l32; k < len; k += 32) dst[k] = stage[o + k];
   }
 }
 
 // ------------------------------------------------------------- encode P2
-// grid = num_tiles * splits, block 256; each thread owns whole buckets.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(512)
 enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
-              const int32_t* __restrict__ perm, const int32_t* __restrict__ csr,
-              uint32_t total_buckets, uint32_t splits) {
-  const uint32_t t = blockIdx.x / splits;
-  const uint32_t s = blockIdx.x - t * splits;
-  const uint32_t per = kTile / splits;
-  for (uint32_t lb = s * per + threadIdx.x; lb < (s + 1) * per; lb += blockDim.x) {
-    const uint32_t gb = (t << kTileShift) + lb;
+              const uint16_t* __restrict__ perm, const int32_t* __restrict__ csr,
+              const int32_t* __restrict__ seg, uint32_t tile, uint32_t total_buckets) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* S = reinterpret_cast<float*>(smem);
+  const uint32_t t = blockIdx.x;
+  const uint32_t lo = static_cast<uint32_t>(seg[t]), n = static_cast<uint32_t>(seg[t + 1]) - lo;
+  for (uint32_t x = threadIdx.x; x < n; x += blockDim.x) S[x] = vals[lo + x];
+  __syncthreads();
+  const uint32_t gb0 = t * tile;
+  for (uint32_t b = threadIdx.x; b < tile; b += blockDim.x) {
+    const uint32_t gb = gb0 + b;
     if (gb >= total_buckets) break;
-    const int32_t a = csr[gb], b = csr[gb + 1];
+    const int32_t x0 = csr[gb], x1 = csr[gb + 1];
     float acc = 0.f;
-    int32_t x = a;
-    for (; x + 3 < b; x += 4) {  // 4 independent gathers in flight
-      const float v0 = vals[perm[x]], v1 = vals[perm[x + 1]];
-      const float v2 = vals[perm[x + 2]], v3 = vals[perm[x + 3]];
-      acc += (v0 + v1) + (v2 + v3);
+    for (int32_t x = x0; x < x1; ++x) {
+      const uint32_t pl = perm[x];
+      acc += signed_v(S[pl & 0x7fffu], pl);
     }
-    for (; x < b; ++x) acc += vals[perm[x]];
-    if (b > a) table[gb] += acc;
+    if (x1 > x0) table[gb] += acc;
   }
 }
 
 // -------------------------------------------------------------- query Q1
-// grid = num_tiles * splits; the tile is staged in LDS, each block converts
-// its share of the tile's entries into signed cell values (entry order).
 __global__ void __launch_bounds__(256)
 qry_q1_kernel(const float* __restrict__ table, const uint16_t* __restrict__ ent_info,
-              const int32_t* __restrict__ seg, float* __restrict__ vals,
+              const int32_t* __restrict__ seg, float* __restrict__ vals, uint32_t tile,
               uint32_t total_buckets, uint32_t splits) {
-  __shared__ float tile[kTile];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* T = reinterpret_cast<float*>(smem);
   const uint32_t t = blockIdx.x / splits;
   const uint32_t s = blockIdx.x - t * splits;
-  const uint32_t tb = t << kTileShift;
-  for (uint32_t b = threadIdx.x; b < kTile; b += blockDim.x) {
+  const uint32_t tb = t * tile;
+  for (uint32_t b = threadIdx.x; b < tile; b += blockDim.x) {
     const uint32_t gb = tb + b;
-    tile[b] = gb < total_buckets ? table[gb] : 0.f;
+    T[b] = gb < total_buckets ? table[gb] : 0.f;
   }
   __syncthreads();
-  const uint32_t lo = static_cast<uint32_t>(seg[t]), hi = static_cast<uint32_t>(seg[t + 1]);
-  const uint32_t n = hi - lo;
+  const uint32_t lo = static_cast<uint32_t>(seg[t]), n = static_cast<uint32_t>(seg[t + 1]) - lo;
   const uint32_t e0 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * s / splits);
   const uint32_t e1 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * (s + 1) / splits);
+  const uint32_t mask = tile - 1;
   for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    const uint16_t info = ent_info[e];
-    vals[e] = signed_v(tile[info & 0x1fffu], info);
+    const uint32_t info = ent_info[e];
+    vals[e] = signed_v(T[info & mask], info);
   }
 }
 
@@ -143,7 +141,7 @@ __device__ __forceinline__ float lower_median_r(float (&v)[kMaxRows], int r) {
   for (int pass = 0; pass < N; ++pass) {
 #pragma unroll
     for (int q = pass & 1; q + 1 < N; q += 2) {
-      float a = v[q], b = v[q + 1];
+      const float a = v[q], b = v[q + 1];
       v[q] = fminf(a, b);
       v[q + 1] = fmaxf(a, b);
     }
@@ -158,37 +156,38 @@ __device__ __forceinline__ float lower_median_r(float (&v)[kMaxRows], int r) {
 }
 
 template <int R>
-__global__ void __launch_bounds__(256)
-qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r, uint32_t chunk,
+__global__ void __launch_bounds__(512)
+qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_t chunk,
               uint32_t num_tiles, const uint16_t* __restrict__ src_info,
               const int32_t* __restrict__ base, const int32_t* __restrict__ off,
               float* __restrict__ est) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* stage = reinterpret_cast<float*>(smem);
-  uint32_t* soff = reinterpret_cast<uint32_t*>(stage + kStageEntries);
-  uint32_t* sbase = soff + num_tiles;
-  const size_t row = static_cast<size_t>(blockIdx.x) * num_tiles;
-  for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) {
-    soff[t] = static_cast<uint32_t>(off[row + t]);
-    sbase[t] = static_cast<uint32_t>(base[row + t]);
-  }
-  __syncthreads();
+  const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
   const uint32_t i0 = blockIdx.x * chunk;
   const uint32_t i1 = min(d, i0 + chunk);
-  const uint32_t total = (i1 - i0) * r;
-  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
-    const uint32_t t = run_of(soff, num_tiles, e);
-    stage[e] = vals[static_cast<size_t>(sbase[t]) + (e - soff[t])];
+  float* stage = reinterpret_cast<float*>(smem);
+  uint32_t* soff = reinterpret_cast<uint32_t*>(stage + chunk * r);
+  uint32_t* sbase = soff + num_tiles + 1;
+  const size_t orow = static_cast<size_t>(blockIdx.x) * (num_tiles + 1);
+  const size_t brow = static_cast<size_t>(blockIdx.x) * num_tiles;
+  for (uint32_t t = threadIdx.x; t <= num_tiles; t += blockDim.x) soff[t] = off[orow + t];
+  for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
+  __syncthreads();
+  const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
+  for (uint32_t t = hw; t < num_tiles; t += nhw) {
+    const uint32_t o = soff[t], len = soff[t + 1] - o;
+    const float* src = vals + sbase[t];
+    for (uint32_t k = l32; k < len; k += 32) stage[o + k] = src[k];
   }
   __syncthreads();
   for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     float v[kMaxRows];
     const uint16_t* si = src_info + static_cast<size_t>(i) * r;
-    const int rr = R > 0 ? R : static_cast<int>(r);
+    const int rr = static_cast<int>(r);
 #pragma unroll
     for (int j = 0; j < (R > 0 ? R : kMaxRows); ++j) {
       v[j] = 0.f;
-      if (j < rr) v[j] = stage[si[j] & 0x3fffu];
+      if (j < rr) v[j] = stage[si[j]];
     }
     est[i] = lower_median_r<R>(v, rr);
   }
@@ -214,15 +213,38 @@ hash_all_kernel(RowHashes h, SketchGeom g, const int32_t* __restrict__ blk_off,
   }
 }
 
-size_t stage_lds(uint32_t num_tiles) {
-  return kStageEntries * sizeof(float) + 2 * num_tiles * sizeof(uint32_t);
+size_t stage_lds(const PlanGeom& p, int r) {
+  return static_cast<size_t>(p.chunk) * r * 4 + (2 * p.num_tiles + 1) * 4;
 }
 
 void set_lds_attr(const void* fn) {
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
 }
 
 }  // namespace
+
+bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
+  if (d <= 0 || r < 1 || r > kMaxRows || c < 1 || d * r >= (int64_t{1} << 31)) return false;
+  for (int64_t tile = 4096; tile >= 512; tile >>= 1) {
+    PlanGeom p;
+    p.tile = tile;
+    p.num_tiles = (r * c + tile - 1) / tile;
+    // expected segment d*r/(r*c) entries per bucket, 12 % headroom
+    const double seg = static_cast<double>(d) / static_cast<double>(c) * static_cast<double>(tile);
+    if (seg * 1.12 + 256 > kPlanSegCap) continue;
+    const int64_t tables = (2 * p.num_tiles + 1) * 4;
+    const int64_t stage_bytes = kLdsBytes - 1024 - tables;
+    if (stage_bytes < 64 * r * 4 * 16) continue;
+    int64_t chunk = (stage_bytes / 4 / r) / 64 * 64;
+    if (chunk > kPlanStageCap / r / 64 * 64) chunk = kPlanStageCap / r / 64 * 64;
+    if (chunk < 64) continue;
+    p.chunk = chunk;
+    p.num_chunks = (d + chunk - 1) / chunk;
+    *out = p;
+    return true;
+  }
+  return false;
+}
 
 void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
                         const float* blk_sign, int32_t* out, hipStream_t stream) {
@@ -234,36 +256,37 @@ void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* 
 }
 
 void launch_cs_encode_planned(float* table, const float* vec, const float* wvec, float scale,
-                              float wscale, const SketchGeom& g, const BinPlan& p,
+                              float wscale, int64_t d, int r, int64_t c, const PlanGeom& p,
                               const PlannedArgs& a, hipStream_t stream) {
-  if (g.d == 0) return;
+  if (d == 0) return;
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(reinterpret_cast<const void*>(enc_p1_kernel));
+    set_lds_attr(reinterpret_cast<const void*>(enc_p1_kernel<5>));
+    set_lds_attr(reinterpret_cast<const void*>(enc_p1_kernel<3>));
+    set_lds_attr(reinterpret_cast<const void*>(enc_p1_kernel<1>));
+    set_lds_attr(reinterpret_cast<const void*>(enc_p1_kernel<0>));
+    set_lds_attr(reinterpret_cast<const void*>(enc_p2_kernel));
     attr = true;
   }
-  const uint32_t nt = static_cast<uint32_t>(p.num_tiles);
-  hipLaunchKernelGGL(enc_p1_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256),
-                     stage_lds(nt), stream, vec, wvec, scale, wscale, g.d, g.r,
-                     static_cast<uint32_t>(p.chunk), nt, a.src_info, a.base, a.off, a.vals);
-  const uint32_t splits = 8;  // 1024 buckets per block, 4 per thread
-  hipLaunchKernelGGL(enc_p2_kernel, dim3(nt * splits), dim3(256), 0, stream, table, a.vals,
-                     a.perm, a.csr, static_cast<uint32_t>(static_cast<int64_t>(g.r) * g.c),
-                     splits);
+  const uint32_t nt = static_cast<uint32_t>(p.num_tiles), ch = static_cast<uint32_t>(p.chunk);
+  const dim3 g1(static_cast<uint32_t>(p.num_chunks));
+  const size_t l1 = stage_lds(p, r);
+  const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
+  switch (r) {
+    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
+    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
+    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
+    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
+  }
+  const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4;
+  hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(512), l2, stream, table, a.vals, a.perm, a.csr,
+                     a.seg, static_cast<uint32_t>(p.tile), static_cast<uint32_t>(r * c));
 }
 
-void launch_cs_query_planned(const float* table, float* est, const SketchGeom& g,
-                             const BinPlan& p, const PlannedArgs& a, hipStream_t stream) {
-  if (g.d == 0) return;
+void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,
+                             const PlanGeom& p, const PlannedArgs& a, hipStream_t stream) {
+  if (d == 0) return;
   static bool attr = false;
-  const uint32_t nt = static_cast<uint32_t>(p.num_tiles);
-  const uint32_t splits = 4;
-  hipLaunchKernelGGL(qry_q1_kernel, dim3(nt * splits), dim3(256), 0, stream, table, a.ent_info,
-                     a.seg, a.vals, static_cast<uint32_t>(static_cast<int64_t>(g.r) * g.c),
-                     splits);
-  const dim3 grid(static_cast<uint32_t>(p.num_chunks));
-  const size_t lds = stage_lds(nt);
-  const uint32_t ch = static_cast<uint32_t>(p.chunk);
   if (!attr) {
     set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<5>));
     set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<3>));
@@ -271,11 +294,19 @@ void launch_cs_query_planned(const float* table, float* est, const SketchGeom& g
     set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<0>));
     attr = true;
   }
-  switch (g.r) {
-    case 5: hipLaunchKernelGGL(qry_q2_kernel<5>, grid, dim3(256), lds, stream, a.vals, g.d, g.r, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 3: hipLaunchKernelGGL(qry_q2_kernel<3>, grid, dim3(256), lds, stream, a.vals, g.d, g.r, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 1: hipLaunchKernelGGL(qry_q2_kernel<1>, grid, dim3(256), lds, stream, a.vals, g.d, g.r, ch, nt, a.src_info, a.base, a.off, est); break;
-    default: hipLaunchKernelGGL(qry_q2_kernel<0>, grid, dim3(256), lds, stream, a.vals, g.d, g.r, ch, nt, a.src_info, a.base, a.off, est); break;
+  const uint32_t nt = static_cast<uint32_t>(p.num_tiles), ch = static_cast<uint32_t>(p.chunk);
+  const uint32_t splits = 4;
+  hipLaunchKernelGGL(qry_q1_kernel, dim3(nt * splits), dim3(256), p.tile * 4, stream, table,
+                     a.ent_info, a.seg, a.vals, static_cast<uint32_t>(p.tile),
+                     static_cast<uint32_t>(r * c), splits);
+  const dim3 g2(static_cast<uint32_t>(p.num_chunks));
+  const size_t l2 = stage_lds(p, r);
+  const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
+  switch (r) {
+    case 5: hipLaunchKernelGGL(qry_q2_kernel<5>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 3: hipLaunchKernelGGL(qry_q2_kernel<3>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 1: hipLaunchKernelGGL(qry_q2_kernel<1>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    default: hipLaunchKernelGGL(qry_q2_kernel<0>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
   }
 }
 

@@ -110,9 +110,9 @@ class CSVec:
         return self._scratch["planned"]
 
     def _use_plan(self) -> bool:
-        # limits of csrc/sketch_planned.hip (LDS run tables, int32 entry ids)
-        return (self.device.type == "cuda" and self.kernel == "planned"
-                and self.r * self.c <= 15000 * 8192 and self.d * self.r < 2 ** 31)
+        # the plan is None when the geometry does not fit the planned kernels
+        # (csrc/sketch_planned.hip); the binned kernels are used then
+        return self.device.type == "cuda" and self.kernel == "planned" and self._plan() is not None
 
     # -- CSVec API --------------------------------------------------------------
     def zero(self):

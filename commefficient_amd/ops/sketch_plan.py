@@ -1,27 +1,33 @@
-"""One-time plan of the atomic-free ("planned") Count-Sketch encode / query.
+"""One-time plan of the atomic-free ("planned") Count-Sketch encode / query
+(kernels: csrc/sketch_planned.hip).
 
-The hashes are data-independent, so the r*d (coordinate, row) entries can be
-laid out once, tile-major (8192-bucket table tile, then coordinate chunk, then
-(i, j) order), with everything the kernels of csrc/sketch_planned.hip need:
+The hashes are data-independent, so the r*d (coordinate, row) entries are laid
+out once, tile-major: T-bucket table tiles (T = 512..4096, chosen so that a
+tile's whole segment of entries fits in LDS), then coordinate chunks, then
+(i, j) order.  Returned tensors (all on ``device``):
 
-  src_info[i*r+j]  int16  in-chunk LDS staging slot | sign << 15
-  ent_info[e]      int16  bucket inside the tile    | sign << 15  (entry order)
-  perm[x]          int32  entry indices sorted by (tile, bucket)
-  csr              int32  [num_tiles*8192 + 1] bucket boundaries into perm
-  base, off        int32  [num_chunks, num_tiles] run starts (global / in-chunk)
+  src_info[i*r+j]  int16  slot of entry (i, j) in its chunk's LDS stage
+  ent_info[e]      int16  in-tile bucket | sign << 15, entry (segment) order
+  perm[x]          int16  segment-local entry index | sign << 15, bucket order
+  csr              int32  [num_tiles*T + 1] bucket starts in perm
+  base             int32  [num_chunks, num_tiles] global start of each run
+  off              int32  [num_chunks, num_tiles + 1] in-chunk run starts
   seg              int32  [num_tiles + 1] tile segment starts
   vals             f32    [d*r] scratch shared by encode and query
 
-Built with two stable device sorts (torch), so it costs one-time O(rd log rd)
-work; ~0.4 GB of plan for ResNet-9, ~7 GB for GPT-2 (288 GB HBM per MI355X).
+Built with device sorts (one-time O(rd log rd)): ~0.35 GB for ResNet-9.
+``build_plan`` returns None when the geometry does not fit (e.g. GPT-2's
+249 entries per bucket); callers then use the binned kernels.
 """
 from __future__ import annotations
 
-from typing import List
+from typing import List, Optional
 
 import torch
 
 from .._ext import ops
+
+SEG_CAP = 32767
 
 
 def _to_i16(x: torch.Tensor) -> torch.Tensor:
@@ -30,53 +36,61 @@ def _to_i16(x: torch.Tensor) -> torch.Tensor:
     return torch.where(x >= 32768, x - 65536, x).to(torch.int16)
 
 
+def _excl_cumsum(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
+    return torch.cumsum(x, dim) - x
+
+
 @torch.no_grad()
 def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: int,
-               device) -> List[torch.Tensor]:
-    tile, num_tiles, chunk, num_chunks = [int(v) for v in ops().binned_plan(d, r, c)]
+               device) -> Optional[List[torch.Tensor]]:
+    geo = [int(v) for v in ops().plan_geometry(d, r, c)]
+    if not geo:
+        return None
+    tile, num_tiles, chunk, num_chunks = geo
     n = d * r
-    if n >= 2 ** 31:
-        raise ValueError("planned sketch supports d*r < 2^31 entries")
+    i64 = torch.int64
     hs = ops().cs_hash_all(hashes, blk_off, blk_sign, num_blocks, d, c, blk_off)  # [d, r]
     neg = (hs < 0).view(-1)
-    bucket = (hs & 0x7FFFFFFF).to(torch.int64)
+    gb = ((hs & 0x7FFFFFFF).to(i64) + torch.arange(r, device=device, dtype=i64).view(1, r) * c)
+    gb = gb.view(-1)
     del hs
-    gb = bucket + torch.arange(r, device=device, dtype=torch.int64).view(1, r) * c
-    del bucket
-    tile_id = (gb >> 13).view(-1)
-    lb = (gb & (tile - 1)).view(-1)
-    del gb
-    chunk_id = (torch.arange(d, device=device, dtype=torch.int64) // chunk).repeat_interleave(r)
+    tile_id = gb // tile
+    chunk_id = (torch.arange(d, device=device, dtype=i64) // chunk).repeat_interleave(r)
     key = tile_id * num_chunks + chunk_id
-    # entries sorted by (tile, chunk), stable in (i, j) order
+    # global (segment) order: by (tile, chunk), stable in (i, j) order
     sorted_key, order = torch.sort(key, stable=True)
     global_pos = torch.empty_like(order)
     global_pos[order] = torch.arange(n, device=device, dtype=order.dtype)
-    counts_flat = torch.bincount(key, minlength=num_tiles * num_chunks)  # [tile, chunk] flat
+    counts_tc = torch.bincount(key, minlength=num_tiles * num_chunks).view(num_tiles, num_chunks)
     del key
-    base_flat = torch.cumsum(counts_flat, 0) - counts_flat
-    counts_ct = counts_flat.view(num_tiles, num_chunks).t().contiguous()      # [chunk, tile]
-    base = base_flat.view(num_tiles, num_chunks).t().contiguous()             # [chunk, tile]
-    off = torch.cumsum(counts_ct, 1) - counts_ct                              # in-chunk
+    seg_len = counts_tc.sum(1)
+    if int(seg_len.max()) > SEG_CAP:
+        return None
+    base_tc = _excl_cumsum(counts_tc.reshape(-1)).view(num_tiles, num_chunks)
+    base = base_tc.t().contiguous()                                  # [chunk, tile]
+    counts_ct = counts_tc.t().contiguous()
+    off = torch.zeros(num_chunks, num_tiles + 1, dtype=i64, device=device)
+    off[:, 1:] = torch.cumsum(counts_ct, 1)                          # in-chunk run starts
     local = off[chunk_id, tile_id] + (global_pos - base[chunk_id, tile_id])
     del chunk_id
-    sign_bit = neg.to(torch.int64) << 15
-    src_info = _to_i16(local | sign_bit)
+    src_info = _to_i16(local)
     del local
+    seg = torch.zeros(num_tiles + 1, dtype=i64, device=device)
+    seg[1:] = torch.cumsum(seg_len, 0)
+    sign_bit = neg.to(i64) << 15
+    lb = gb & (tile - 1)
     ent_info = torch.empty(n, dtype=torch.int16, device=device)
     ent_info[global_pos] = _to_i16(lb | sign_bit)
-    del global_pos, sign_bit
-    ent_tile = sorted_key // num_chunks
-    ent_lb = lb[order]
-    del sorted_key, order, lb, tile_id
-    key2 = ent_tile * tile + ent_lb
-    del ent_tile, ent_lb
-    _, perm = torch.sort(key2, stable=True)
-    csr = torch.cat([torch.zeros(1, dtype=torch.int64, device=device),
-                     torch.cumsum(torch.bincount(key2, minlength=num_tiles * tile), 0)])
-    del key2
-    seg = torch.cat([torch.zeros(1, dtype=torch.int64, device=device),
-                     torch.cumsum(counts_flat.view(num_tiles, num_chunks).sum(1), 0)])
+    del lb, tile_id, global_pos
+    # bucket order: entries (in segment order) stably sorted by global bucket
+    gb_pos = gb[order]
+    _, perm_pos = torch.sort(gb_pos, stable=True)
+    tile_of_pos = sorted_key // num_chunks
+    seg_local = perm_pos - seg[tile_of_pos[perm_pos]]
+    perm = _to_i16(seg_local | (neg[order][perm_pos].to(i64) << 15))
+    del gb_pos, tile_of_pos, seg_local, sorted_key, order, perm_pos, sign_bit
+    csr = torch.zeros(num_tiles * tile + 1, dtype=i64, device=device)
+    csr[1:] = torch.cumsum(torch.bincount(gb, minlength=num_tiles * tile), 0)
     vals = torch.empty(n, dtype=torch.float32, device=device)
-    return [src_info.contiguous(), ent_info, perm.to(torch.int32), csr.to(torch.int32),
-            base.to(torch.int32), off.to(torch.int32).contiguous(), seg.to(torch.int32), vals]
+    i32 = torch.int32
+    return [src_info, ent_info, perm, csr.to(i32), base.to(i32), off.to(i32), seg.to(i32), vals]

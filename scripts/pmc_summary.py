@@ -17,7 +17,7 @@ for part in ("sq", "tcc"):
         n = r["Kernel_Name"]
         if filt not in n:
             continue
-        n = n.split("(")[0].replace("void ", "").replace("commeff::(anonymous namespace)::", "")[:48]
+        n = n.replace("void ", "").replace("commeff::(anonymous namespace)::", "").split("(")[0][:48]
         agg.setdefault((n, r["Grid_Size"]), collections.defaultdict(list))[r["Counter_Name"]].append(
             float(r["Counter_Value"]))
 for (n, grid), d in agg.items():

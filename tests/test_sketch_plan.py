@@ -1,0 +1,116 @@
+"""The planned (atomic-free) Count-Sketch: plan invariants and a pure-torch
+simulation of the four kernels of csrc/sketch_planned.hip (P1/P2 encode,
+Q1/Q2 query) driven by the plan, checked against the native CPU encode /
+query.  Runs on CPU (the plan builder's hash op has a CPU twin); the GPU
+kernels themselves are checked in test_ops.py."""
+import pytest
+import torch
+
+from commefficient_amd._ext import ops as _ops
+from commefficient_amd.ops import CSVec
+from commefficient_amd.ops.sketch_plan import build_plan
+
+
+def _u16(t):
+    return t.to(torch.int64) & 0xFFFF
+
+
+def _plan(d, c, r, nb, seed=3):
+    sk = CSVec(d, c, r, device="cpu", numBlocks=nb, seed=seed)
+    geo = [int(v) for v in _ops().plan_geometry(d, r, c)]
+    plan = build_plan(sk.hashes, sk.blk_off, sk.blk_sign, sk.numBlocks, d, r, c, "cpu")
+    return sk, geo, plan
+
+
+def _gpos_of_slots(geo, plan, d, r):
+    """global (segment-order) position of every entry (i, j), via the runs"""
+    tile, nt, chunk, nch = geo
+    src_info, _, _, _, base, off, _, _ = plan
+    gpos = torch.empty(d * r, dtype=torch.int64)
+    for ch in range(nch):
+        i0, i1 = ch * chunk, min(d, (ch + 1) * chunk)
+        s = _u16(src_info[i0 * r:i1 * r])
+        o = off[ch].to(torch.int64)
+        t = torch.searchsorted(o[1:], s, right=True)
+        gpos[i0 * r:i1 * r] = base[ch].to(torch.int64)[t] + s - o[t]
+    return gpos
+
+
+def _simulate_encode(geo, plan, vec, r, c):
+    tile, nt, chunk, nch = geo
+    _, _, perm, csr, _, _, seg, _ = plan
+    d = vec.numel()
+    vals = torch.empty(d * r, dtype=torch.float64)
+    vals[_gpos_of_slots(geo, plan, d, r)] = vec.double().repeat_interleave(r)     # P1
+    csr = csr.to(torch.int64)
+    gb_of_x = torch.repeat_interleave(torch.arange(r * c), csr[1:r * c + 1] - csr[:r * c])
+    pl = _u16(perm)
+    idx = seg.to(torch.int64)[gb_of_x // tile] + (pl & 0x7FFF)
+    contrib = torch.where((pl & 0x8000) != 0, -vals[idx], vals[idx])               # P2
+    table = torch.zeros(r * c, dtype=torch.float64)
+    table.index_add_(0, gb_of_x, contrib)
+    return table.view(r, c)
+
+
+def _simulate_query(geo, plan, table, d, r):
+    tile, nt, chunk, nch = geo
+    _, ent_info, _, _, _, _, seg, _ = plan
+    n = d * r
+    seg = seg.to(torch.int64)
+    tile_of_e = torch.searchsorted(seg[1:], torch.arange(n), right=True)
+    info = _u16(ent_info)
+    flat = table.reshape(-1)
+    v = flat[tile_of_e * tile + (info & (tile - 1))]
+    vals = torch.where((info & 0x8000) != 0, -v, v)                                # Q1
+    per = vals[_gpos_of_slots(geo, plan, d, r)].view(d, r)                          # Q2
+    return per.sort(dim=1).values[:, (r - 1) // 2]
+
+
+@pytest.mark.parametrize("d,c,r,nb", [(20000, 900, 5, 1), (30011, 2003, 3, 4), (9000, 700, 1, 1),
+                                      (50000, 4000, 5, 20)])
+def test_plan_invariants_and_simulated_kernels(d, c, r, nb):
+    sk, geo, plan = _plan(d, c, r, nb)
+    assert geo and plan is not None
+    tile, nt, chunk, nch = geo
+    src_info, ent_info, perm, csr, base, off, seg, vals = plan
+    n = d * r
+    assert nt * tile >= r * c and nch * chunk >= d
+    assert int(seg[-1]) == n and int(csr[-1]) == n
+    assert int((seg[1:] - seg[:-1]).max()) <= 32767
+    # every chunk's stage slots are a permutation of 0..len-1
+    for ch in range(nch):
+        i0, i1 = ch * chunk, min(d, (ch + 1) * chunk)
+        s = _u16(src_info[i0 * r:i1 * r])
+        assert torch.equal(s.sort().values, torch.arange((i1 - i0) * r))
+    # global positions are a permutation of 0..n-1
+    assert torch.equal(_gpos_of_slots(geo, plan, d, r).sort().values, torch.arange(n))
+    g = torch.Generator().manual_seed(0)
+    vec = torch.randn(d, generator=g)
+    ref = sk.like()
+    ref.accumulateVec(vec)
+    sim = _simulate_encode(geo, plan, vec, r, c)
+    torch.testing.assert_close(sim.float(), ref.table, rtol=1e-5, atol=1e-5)
+    est = _simulate_query(geo, plan, ref.table, d, r)
+    assert torch.equal(est, sk.like(ref.table).query())
+
+
+def test_plan_unsupported_geometry_returns_none():
+    # ~250 entries per bucket (GPT-2 scale ratio): segments cannot fit in LDS
+    assert list(_ops().plan_geometry(2_000_000, 5, 8000)) == []
+    sk = CSVec(2_000_000, 8000, 5, device="cpu")
+    assert build_plan(sk.hashes, sk.blk_off, sk.blk_sign, 1, 2_000_000, 5, 8000, "cpu") is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,c,r,nb", [(20000, 900, 5, 1), (30011, 2003, 3, 4), (9000, 700, 1, 1),
+                                      (50000, 4000, 5, 20), (123457, 10007, 4, 2)])
+def test_planned_gpu_kernels_match_cpu(d, c, r, nb):
+    cpu = CSVec(d, c, r, device="cpu", numBlocks=nb, seed=5)
+    gpu = CSVec(d, c, r, device="cuda", numBlocks=nb, seed=5, kernel="planned")
+    assert gpu._use_plan()
+    g = torch.Generator().manual_seed(1)
+    v, w = torch.randn(d, generator=g), torch.randn(d, generator=g)
+    cpu.accumulateVec(v, 0.5, w, 1e-2)
+    gpu.accumulateVec(v.cuda(), 0.5, w.cuda(), 1e-2)
+    torch.testing.assert_close(gpu.table.cpu(), cpu.table, rtol=1e-5, atol=1e-5)
+    assert torch.equal(gpu.like(cpu.table.cuda()).query().cpu(), cpu.query())
