@@ -60,21 +60,37 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
   const size_t brow = static_cast<size_t>(blockIdx.x) * num_tiles;
   for (uint32_t t = threadIdx.x; t <= num_tiles; t += blockDim.x) soff[t] = off[orow + t];
   for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
-  // entries in (i, j) order: coalesced src_info stream; v_i re-read from L1
+  // entries in (i, j) order: coalesced src_info stream, v_i re-read from L1;
+  // batches of kB entries per thread keep kB loads of each kind in flight
+  constexpr uint32_t kB = 8;
   const uint16_t* si = src_info + static_cast<size_t>(i0) * r;
-  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
-    const uint32_t i = i0 + e / r;
-    float v = scale * vec[i];
-    if (wvec != nullptr) v += wscale * wvec[i];
-    stage[si[e]] = v;
+  const uint32_t nt = blockDim.x;
+  for (uint32_t e0 = 0; e0 < total; e0 += kB * nt) {
+    uint32_t slot[kB];
+    float v[kB];
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t e = e0 + q * nt + threadIdx.x;
+      slot[q] = 0xffffffffu;
+      v[q] = 0.f;
+      if (e < total) {
+        const uint32_t i = i0 + e / r;
+        slot[q] = si[e];
+        v[q] = scale * vec[i];
+        if (wvec != nullptr) v[q] += wscale * wvec[i];
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q)
+      if (slot[q] != 0xffffffffu) stage[slot[q]] = v[q];
   }
   __syncthreads();
-  // runs: one half-wave per (chunk, tile) run
-  const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
-  for (uint32_t t = hw; t < num_tiles; t += nhw) {
+  // runs: one wave per (chunk, tile) run (runs average ~30 entries)
+  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (uint32_t t = w; t < num_tiles; t += nw) {
     const uint32_t o = soff[t], len = soff[t + 1] - o;
     float* dst = vals + sbase[t];
-    for (uint32_t k = l32; k < len; k += 32) dst[k] = stage[o + k];
+    for (uint32_t k = l64; k < len; k += 64) dst[k] = stage[o + k];
   }
 }
 
@@ -87,15 +103,36 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
   float* S = reinterpret_cast<float*>(smem);
   const uint32_t t = blockIdx.x;
   const uint32_t lo = static_cast<uint32_t>(seg[t]), n = static_cast<uint32_t>(seg[t + 1]) - lo;
-  for (uint32_t x = threadIdx.x; x < n; x += blockDim.x) S[x] = vals[lo + x];
+  constexpr uint32_t kB = 8;
+  const uint32_t nt = blockDim.x;
+  for (uint32_t x0 = 0; x0 < n; x0 += kB * nt) {
+    float v[kB];
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t x = x0 + q * nt + threadIdx.x;
+      v[q] = x < n ? vals[lo + x] : 0.f;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t x = x0 + q * nt + threadIdx.x;
+      if (x < n) S[x] = v[q];
+    }
+  }
   __syncthreads();
+  // thread per bucket; its csr range of perm is read 4 entries at a time
   const uint32_t gb0 = t * tile;
-  for (uint32_t b = threadIdx.x; b < tile; b += blockDim.x) {
+  for (uint32_t b = threadIdx.x; b < tile; b += nt) {
     const uint32_t gb = gb0 + b;
     if (gb >= total_buckets) break;
     const int32_t x0 = csr[gb], x1 = csr[gb + 1];
     float acc = 0.f;
-    for (int32_t x = x0; x < x1; ++x) {
+    int32_t x = x0;
+    for (; x + 3 < x1; x += 4) {
+      const uint32_t p0 = perm[x], p1 = perm[x + 1], p2 = perm[x + 2], p3 = perm[x + 3];
+      acc += (signed_v(S[p0 & 0x7fffu], p0) + signed_v(S[p1 & 0x7fffu], p1)) +
+             (signed_v(S[p2 & 0x7fffu], p2) + signed_v(S[p3 & 0x7fffu], p3));
+    }
+    for (; x < x1; ++x) {
       const uint32_t pl = perm[x];
       acc += signed_v(S[pl & 0x7fffu], pl);
     }
@@ -122,9 +159,20 @@ qry_q1_kernel(const float* __restrict__ table, const uint16_t* __restrict__ ent_
   const uint32_t e0 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * s / splits);
   const uint32_t e1 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * (s + 1) / splits);
   const uint32_t mask = tile - 1;
-  for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
-    const uint32_t info = ent_info[e];
-    vals[e] = signed_v(T[info & mask], info);
+  constexpr uint32_t kB = 8;
+  const uint32_t nt = blockDim.x;
+  for (uint32_t eb = e0; eb < e1; eb += kB * nt) {
+    uint32_t info[kB];
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t e = eb + q * nt + threadIdx.x;
+      info[q] = e < e1 ? ent_info[e] : 0u;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t e = eb + q * nt + threadIdx.x;
+      if (e < e1) vals[e] = signed_v(T[info[q] & mask], info[q]);
+    }
   }
 }
 
@@ -173,22 +221,37 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
   for (uint32_t t = threadIdx.x; t <= num_tiles; t += blockDim.x) soff[t] = off[orow + t];
   for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
   __syncthreads();
-  const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
-  for (uint32_t t = hw; t < num_tiles; t += nhw) {
-    const uint32_t o = soff[t], len = soff[t + 1] - o;
-    const float* src = vals + sbase[t];
-    for (uint32_t k = l32; k < len; k += 32) stage[o + k] = src[k];
+  // runs -> stage: a wave per run, kB runs per wave in flight at once
+  constexpr uint32_t kB = 8;
+  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (uint32_t t0 = w * kB; t0 < num_tiles; t0 += nw * kB) {
+    float v[kB];
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t t = t0 + q;
+      v[q] = 0.f;
+      if (t < num_tiles && l64 < soff[t + 1] - soff[t]) v[q] = vals[sbase[t] + l64];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t t = t0 + q;
+      if (t < num_tiles) {
+        const uint32_t o = soff[t], len = soff[t + 1] - o;
+        if (l64 < len) stage[o + l64] = v[q];
+        for (uint32_t k = l64 + 64; k < len; k += 64) stage[o + k] = vals[sbase[t] + k];
+      }
+    }
   }
   __syncthreads();
+  const int rr = static_cast<int>(r);
   for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     float v[kMaxRows];
+    uint32_t sl[kMaxRows];
     const uint16_t* si = src_info + static_cast<size_t>(i) * r;
-    const int rr = static_cast<int>(r);
 #pragma unroll
-    for (int j = 0; j < (R > 0 ? R : kMaxRows); ++j) {
-      v[j] = 0.f;
-      if (j < rr) v[j] = stage[si[j]];
-    }
+    for (int j = 0; j < (R > 0 ? R : kMaxRows); ++j) sl[j] = j < rr ? si[j] : 0u;
+#pragma unroll
+    for (int j = 0; j < (R > 0 ? R : kMaxRows); ++j) v[j] = j < rr ? stage[sl[j]] : 0.f;
     est[i] = lower_median_r<R>(v, rr);
   }
 }
