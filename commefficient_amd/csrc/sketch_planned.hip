@@ -45,21 +45,14 @@ __device__ __forceinline__ float signed_v(float v, uint32_t info) {
 template <int R>
 __global__ void __launch_bounds__(512)
 enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, float scale,
-              float wscale, uint32_t d, uint32_t r_rt, uint32_t chunk, uint32_t num_tiles,
-              const uint16_t* __restrict__ src_info, const int32_t* __restrict__ base,
-              const int32_t* __restrict__ off, float* __restrict__ vals) {
+              float wscale, uint32_t d, uint32_t r_rt, uint32_t chunk,
+              const uint16_t* __restrict__ src_info, float* __restrict__ vals) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
   const uint32_t i0 = blockIdx.x * chunk;
   const uint32_t i1 = min(d, i0 + chunk);
   const uint32_t total = (i1 - i0) * r;
   float* stage = reinterpret_cast<float*>(smem);
-  uint32_t* soff = reinterpret_cast<uint32_t*>(stage + chunk * r);
-  uint32_t* sbase = soff + num_tiles + 1;
-  const size_t orow = static_cast<size_t>(blockIdx.x) * (num_tiles + 1);
-  const size_t brow = static_cast<size_t>(blockIdx.x) * num_tiles;
-  for (uint32_t t = threadIdx.x; t <= num_tiles; t += blockDim.x) soff[t] = off[orow + t];
-  for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
   // entries in (i, j) order: coalesced src_info stream, v_i re-read from L1;
   // batches of kB entries per thread keep kB loads of each kind in flight
   constexpr uint32_t kB = 8;
@@ -85,37 +78,54 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
       if (slot[q] != 0xffffffffu) stage[slot[q]] = v[q];
   }
   __syncthreads();
-  // runs: one wave per (chunk, tile) run (runs average ~30 entries)
-  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (uint32_t t = w; t < num_tiles; t += nw) {
-    const uint32_t o = soff[t], len = soff[t + 1] - o;
-    float* dst = vals + sbase[t];
-    for (uint32_t k = l64; k < len; k += 64) dst[k] = stage[o + k];
-  }
+  // the stage (already tile-ordered inside the chunk) goes out contiguously,
+  // chunk-major: full-line 16-byte stores; P2 gathers the runs (partial-line
+  // READS are cheap, partial-line writes are not)
+  float4* dst = reinterpret_cast<float4*>(vals + static_cast<size_t>(i0) * r);
+  const float4* src = reinterpret_cast<const float4*>(stage);
+  const uint32_t n4 = total / 4;
+  for (uint32_t k = threadIdx.x; k < n4; k += nt) dst[k] = src[k];
+  for (uint32_t k = n4 * 4 + threadIdx.x; k < total; k += nt)
+    vals[static_cast<size_t>(i0) * r + k] = stage[k];
 }
 
 // ------------------------------------------------------------- encode P2
 __global__ void __launch_bounds__(512)
 enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
               const uint16_t* __restrict__ perm, const int32_t* __restrict__ csr,
-              const int32_t* __restrict__ seg, uint32_t tile, uint32_t total_buckets) {
+              const int32_t* __restrict__ seg, const int32_t* __restrict__ base,
+              const int32_t* __restrict__ off, uint32_t tile, uint32_t total_buckets,
+              uint32_t num_tiles, uint32_t num_chunks, uint32_t chunk_entries) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* S = reinterpret_cast<float*>(smem);
   const uint32_t t = blockIdx.x;
-  const uint32_t lo = static_cast<uint32_t>(seg[t]), n = static_cast<uint32_t>(seg[t + 1]) - lo;
-  constexpr uint32_t kB = 8;
+  const uint32_t lo = static_cast<uint32_t>(seg[t]);
   const uint32_t nt = blockDim.x;
-  for (uint32_t x0 = 0; x0 < n; x0 += kB * nt) {
+  // the tile's segment = its run in every chunk (chunk-major vals from P1);
+  // a wave per run, kB runs per wave in flight
+  constexpr uint32_t kB = 16;
+  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = nt >> 6;
+  for (uint32_t c0 = w * kB; c0 < num_chunks; c0 += nw * kB) {
     float v[kB];
+    uint32_t dpos[kB], len[kB], src[kB];
 #pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
-      const uint32_t x = x0 + q * nt + threadIdx.x;
-      v[q] = x < n ? vals[lo + x] : 0.f;
+      const uint32_t ch = c0 + q;
+      len[q] = 0;
+      if (ch < num_chunks) {
+        const size_t orow = static_cast<size_t>(ch) * (num_tiles + 1);
+        const uint32_t o = static_cast<uint32_t>(off[orow + t]);
+        len[q] = static_cast<uint32_t>(off[orow + t + 1]) - o;
+        dpos[q] = static_cast<uint32_t>(base[static_cast<size_t>(ch) * num_tiles + t]) - lo;
+        src[q] = ch * chunk_entries + o;
+      }
     }
 #pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) v[q] = l64 < len[q] ? vals[src[q] + l64] : 0.f;
+#pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
-      const uint32_t x = x0 + q * nt + threadIdx.x;
-      if (x < n) S[x] = v[q];
+      if (l64 < len[q]) S[dpos[q] + l64] = v[q];
+      for (uint32_t k = l64 + 64; k < len[q]; k += 64) S[dpos[q] + k] = vals[src[q] + k];
     }
   }
   __syncthreads();
@@ -222,7 +232,7 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
   for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
   __syncthreads();
   // runs -> stage: a wave per run, kB runs per wave in flight at once
-  constexpr uint32_t kB = 8;
+  constexpr uint32_t kB = 16;
   const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = blockDim.x >> 6;
   for (uint32_t t0 = w * kB; t0 < num_tiles; t0 += nw * kB) {
     float v[kB];
@@ -333,17 +343,19 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
   }
   const uint32_t nt = static_cast<uint32_t>(p.num_tiles), ch = static_cast<uint32_t>(p.chunk);
   const dim3 g1(static_cast<uint32_t>(p.num_chunks));
-  const size_t l1 = stage_lds(p, r);
+  const size_t l1 = static_cast<size_t>(p.chunk) * r * 4;
   const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
   switch (r) {
-    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
-    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
-    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
-    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, nt, a.src_info, a.base, a.off, a.vals); break;
+    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
   }
   const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4;
   hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(512), l2, stream, table, a.vals, a.perm, a.csr,
-                     a.seg, static_cast<uint32_t>(p.tile), static_cast<uint32_t>(r * c));
+                     a.seg, a.base, a.off, static_cast<uint32_t>(p.tile),
+                     static_cast<uint32_t>(r * c), nt, static_cast<uint32_t>(p.num_chunks),
+                     static_cast<uint32_t>(p.chunk * r));
 }
 
 void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,
