@@ -487,19 +487,22 @@ PlanGeom plan_geom_or_throw(int64_t d, int64_t r, int64_t c) {
 }
 
 PlannedArgs planned_args(at::TensorList plan, const PlanGeom& p, int64_t d, int64_t r) {
-  // plan = [src_info i16, ent_info i16, perm i16, csr i32, base i32, off i32, seg i32, vals f32]
-  TORCH_CHECK(plan.size() == 8, "plan must have 8 tensors");
+  // plan = [src_info i16, ent_info i16, perm i16, csr i32, base i32, off i32, seg i32,
+  //         vals f32, p2_src i32, p2_pos i32]
+  TORCH_CHECK(plan.size() == 10, "plan must have 10 tensors");
   const int64_t n = d * r;
   TORCH_CHECK(plan[0].numel() == n && plan[1].numel() == n && plan[2].numel() == n &&
                   plan[3].numel() == p.num_tiles * p.tile + 1 &&
                   plan[4].numel() == p.num_chunks * p.num_tiles &&
                   plan[5].numel() == p.num_chunks * (p.num_tiles + 1) &&
-                  plan[6].numel() == p.num_tiles + 1 && plan[7].numel() >= n,
+                  plan[6].numel() == p.num_tiles + 1 && plan[7].numel() >= n &&
+                  plan[8].numel() == p.num_tiles * p.num_chunks &&
+                  plan[9].numel() == p.num_tiles * (p.num_chunks + 1),
               "sketch plan does not match the geometry");
   for (int i = 0; i < 3; ++i)
     TORCH_CHECK(plan[i].scalar_type() == at::kShort && plan[i].is_contiguous(), "plan[", i,
                 "] must be contiguous int16");
-  for (int i = 3; i < 7; ++i)
+  for (int i : {3, 4, 5, 6, 8, 9})
     TORCH_CHECK(plan[i].scalar_type() == at::kInt && plan[i].is_contiguous(), "plan[", i,
                 "] must be contiguous int32");
   TORCH_CHECK(plan[7].scalar_type() == at::kFloat, "plan[7] must be float32");
@@ -512,6 +515,8 @@ PlannedArgs planned_args(at::TensorList plan, const PlanGeom& p, int64_t d, int6
   a.off = plan[5].data_ptr<int32_t>();
   a.seg = plan[6].data_ptr<int32_t>();
   a.vals = plan[7].data_ptr<float>();
+  a.p2_src = plan[8].data_ptr<int32_t>();
+  a.p2_pos = plan[9].data_ptr<int32_t>();
   return a;
 }
 

@@ -59,6 +59,8 @@ struct PlannedArgs {
   const int32_t* off;        // [num_chunks, num_tiles + 1] in-chunk run starts
   const int32_t* seg;        // [num_tiles + 1] tile segment starts
   float* vals;               // [d*r] scratch
+  const int32_t* p2_src;     // [num_tiles, num_chunks] run start in chunk-major vals
+  const int32_t* p2_pos;     // [num_tiles, num_chunks + 1] run start in the segment
 };
 void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
                         const float* blk_sign, int32_t* out, hipStream_t stream);

@@ -53,29 +53,34 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
   const uint32_t i1 = min(d, i0 + chunk);
   const uint32_t total = (i1 - i0) * r;
   float* stage = reinterpret_cast<float*>(smem);
-  // entries in (i, j) order: coalesced src_info stream, v_i re-read from L1;
-  // batches of kB entries per thread keep kB loads of each kind in flight
-  constexpr uint32_t kB = 8;
-  const uint16_t* si = src_info + static_cast<size_t>(i0) * r;
+  // thread per coordinate, kB coordinates per thread in flight: v_i loaded
+  // once, its r slots read from the (i, j)-ordered src_info stream
+  constexpr uint32_t kB = 4;
+  constexpr uint32_t RR = R > 0 ? static_cast<uint32_t>(R) : kMaxRows;
   const uint32_t nt = blockDim.x;
-  for (uint32_t e0 = 0; e0 < total; e0 += kB * nt) {
-    uint32_t slot[kB];
+  for (uint32_t ib = i0 + threadIdx.x; ib < i1; ib += kB * nt) {
     float v[kB];
+    uint32_t sl[kB][RR];
 #pragma unroll
-    for (uint32_t q = 0; q < kB; ++q) {
-      const uint32_t e = e0 + q * nt + threadIdx.x;
-      slot[q] = 0xffffffffu;
-      v[q] = 0.f;
-      if (e < total) {
-        const uint32_t i = i0 + e / r;
-        slot[q] = si[e];
-        v[q] = scale * vec[i];
-        if (wvec != nullptr) v[q] += wscale * wvec[i];
+    for (uint32_t u = 0; u < kB; ++u) {
+      const uint32_t i = ib + u * nt;
+      v[u] = 0.f;
+      if (i < i1) {
+        v[u] = scale * vec[i];
+        if (wvec != nullptr) v[u] += wscale * wvec[i];
+        const uint16_t* s = src_info + static_cast<size_t>(i) * r;
+#pragma unroll
+        for (uint32_t j = 0; j < RR; ++j) sl[u][j] = j < r ? s[j] : 0u;
       }
     }
 #pragma unroll
-    for (uint32_t q = 0; q < kB; ++q)
-      if (slot[q] != 0xffffffffu) stage[slot[q]] = v[q];
+    for (uint32_t u = 0; u < kB; ++u) {
+      if (ib + u * nt < i1) {
+#pragma unroll
+        for (uint32_t j = 0; j < RR; ++j)
+          if (j < r) stage[sl[u][j]] = v[u];
+      }
+    }
   }
   __syncthreads();
   // the stage (already tile-ordered inside the chunk) goes out contiguously,
@@ -93,17 +98,18 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
 __global__ void __launch_bounds__(512)
 enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
               const uint16_t* __restrict__ perm, const int32_t* __restrict__ csr,
-              const int32_t* __restrict__ seg, const int32_t* __restrict__ base,
-              const int32_t* __restrict__ off, uint32_t tile, uint32_t total_buckets,
-              uint32_t num_tiles, uint32_t num_chunks, uint32_t chunk_entries) {
+              const int32_t* __restrict__ p2_src, const int32_t* __restrict__ p2_pos,
+              uint32_t tile, uint32_t total_buckets, uint32_t num_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* S = reinterpret_cast<float*>(smem);
   const uint32_t t = blockIdx.x;
-  const uint32_t lo = static_cast<uint32_t>(seg[t]);
   const uint32_t nt = blockDim.x;
   // the tile's segment = its run in every chunk (chunk-major vals from P1);
-  // a wave per run, kB runs per wave in flight
+  // run metadata is tile-major (one contiguous row per tile); a wave per
+  // run, kB runs per wave in flight
   constexpr uint32_t kB = 16;
+  const int32_t* psrc = p2_src + static_cast<size_t>(t) * num_chunks;
+  const int32_t* ppos = p2_pos + static_cast<size_t>(t) * (num_chunks + 1);
   const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = nt >> 6;
   for (uint32_t c0 = w * kB; c0 < num_chunks; c0 += nw * kB) {
     float v[kB];
@@ -113,11 +119,9 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
       const uint32_t ch = c0 + q;
       len[q] = 0;
       if (ch < num_chunks) {
-        const size_t orow = static_cast<size_t>(ch) * (num_tiles + 1);
-        const uint32_t o = static_cast<uint32_t>(off[orow + t]);
-        len[q] = static_cast<uint32_t>(off[orow + t + 1]) - o;
-        dpos[q] = static_cast<uint32_t>(base[static_cast<size_t>(ch) * num_tiles + t]) - lo;
-        src[q] = ch * chunk_entries + o;
+        dpos[q] = static_cast<uint32_t>(ppos[ch]);
+        len[q] = static_cast<uint32_t>(ppos[ch + 1]) - dpos[q];
+        src[q] = static_cast<uint32_t>(psrc[ch]);
       }
     }
 #pragma unroll
@@ -353,9 +357,8 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
   }
   const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4;
   hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(512), l2, stream, table, a.vals, a.perm, a.csr,
-                     a.seg, a.base, a.off, static_cast<uint32_t>(p.tile),
-                     static_cast<uint32_t>(r * c), nt, static_cast<uint32_t>(p.num_chunks),
-                     static_cast<uint32_t>(p.chunk * r));
+                     a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
+                     static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks));
 }
 
 void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,

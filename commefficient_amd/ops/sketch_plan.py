@@ -92,5 +92,13 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     csr = torch.zeros(num_tiles * tile + 1, dtype=i64, device=device)
     csr[1:] = torch.cumsum(torch.bincount(gb, minlength=num_tiles * tile), 0)
     vals = torch.empty(n, dtype=torch.float32, device=device)
+    # encode P2 gathers tile t's run of every chunk from the chunk-major P1
+    # output: tile-major run metadata (start in chunk-major vals, start in
+    # the segment)
+    p2_src = (torch.arange(num_chunks, device=device, dtype=i64).view(1, -1) * (chunk * r)
+              + off[:, :num_tiles].t())
+    p2_pos = torch.zeros(num_tiles, num_chunks + 1, dtype=i64, device=device)
+    p2_pos[:, 1:] = torch.cumsum(counts_tc, 1)
     i32 = torch.int32
-    return [src_info, ent_info, perm, csr.to(i32), base.to(i32), off.to(i32), seg.to(i32), vals]
+    return [src_info, ent_info, perm, csr.to(i32), base.to(i32), off.to(i32), seg.to(i32), vals,
+            p2_src.to(i32).contiguous(), p2_pos.to(i32)]

@@ -25,7 +25,7 @@ def _plan(d, c, r, nb, seed=3):
 def _gpos_of_slots(geo, plan, d, r):
     """global (segment-order) position of every entry (i, j), via the runs"""
     tile, nt, chunk, nch = geo
-    src_info, _, _, _, base, off, _, _ = plan
+    src_info, _, _, _, base, off, _, _ = plan[:8]
     gpos = torch.empty(d * r, dtype=torch.int64)
     for ch in range(nch):
         i0, i1 = ch * chunk, min(d, (ch + 1) * chunk)
@@ -38,7 +38,7 @@ def _gpos_of_slots(geo, plan, d, r):
 
 def _simulate_encode(geo, plan, vec, r, c):
     tile, nt, chunk, nch = geo
-    _, _, perm, csr, _, _, seg, _ = plan
+    _, _, perm, csr, _, _, seg, _ = plan[:8]
     d = vec.numel()
     vals = torch.empty(d * r, dtype=torch.float64)
     vals[_gpos_of_slots(geo, plan, d, r)] = vec.double().repeat_interleave(r)     # P1
@@ -54,7 +54,7 @@ def _simulate_encode(geo, plan, vec, r, c):
 
 def _simulate_query(geo, plan, table, d, r):
     tile, nt, chunk, nch = geo
-    _, ent_info, _, _, _, _, seg, _ = plan
+    _, ent_info, _, _, _, _, seg, _ = plan[:8]
     n = d * r
     seg = seg.to(torch.int64)
     tile_of_e = torch.searchsorted(seg[1:], torch.arange(n), right=True)
@@ -72,7 +72,7 @@ def test_plan_invariants_and_simulated_kernels(d, c, r, nb):
     sk, geo, plan = _plan(d, c, r, nb)
     assert geo and plan is not None
     tile, nt, chunk, nch = geo
-    src_info, ent_info, perm, csr, base, off, seg, vals = plan
+    src_info, ent_info, perm, csr, base, off, seg, vals = plan[:8]
     n = d * r
     assert nt * tile >= r * c and nch * chunk >= d
     assert int(seg[-1]) == n and int(csr[-1]) == n
@@ -84,6 +84,12 @@ def test_plan_invariants_and_simulated_kernels(d, c, r, nb):
         assert torch.equal(s.sort().values, torch.arange((i1 - i0) * r))
     # global positions are a permutation of 0..n-1
     assert torch.equal(_gpos_of_slots(geo, plan, d, r).sort().values, torch.arange(n))
+    # P2's tile-major run metadata agrees with the chunk-major one
+    p2_src, p2_pos = plan[8].long(), plan[9].long()
+    offl = off.long()
+    assert torch.equal(p2_pos[:, 1:] - p2_pos[:, :-1], (offl[:, 1:] - offl[:, :-1]).t())
+    assert torch.equal(p2_src, torch.arange(nch).view(1, -1) * chunk * r + offl[:, :nt].t())
+    assert torch.equal(p2_pos[:, -1], seg[1:].long() - seg[:-1].long())
     g = torch.Generator().manual_seed(0)
     vec = torch.randn(d, generator=g)
     ref = sk.like()
