@@ -36,6 +36,7 @@ namespace commeff {
 namespace {
 
 constexpr int kLdsBytes = 160 * 1024;
+constexpr int32_t kP2Win = 1280;  // encode P2: perm window entries per wave
 
 __device__ __forceinline__ float signed_v(float v, uint32_t info) {
   return (info & 0x8000u) ? -v : v;
@@ -101,56 +102,88 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
               const int32_t* __restrict__ p2_src, const int32_t* __restrict__ p2_pos,
               uint32_t tile, uint32_t total_buckets, uint32_t num_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // LDS: segment S [kPlanSegCap] | run metadata [2 * num_chunks + 1] |
+  //      per-wave perm window [8][kP2Win] u16
   float* S = reinterpret_cast<float*>(smem);
+  int32_t* msrc = reinterpret_cast<int32_t*>(S + kPlanSegCap);
+  int32_t* mpos = msrc + num_chunks;
+  uint16_t* win = reinterpret_cast<uint16_t*>(mpos + num_chunks + 1);
   const uint32_t t = blockIdx.x;
   const uint32_t nt = blockDim.x;
-  // the tile's segment = its run in every chunk (chunk-major vals from P1);
-  // run metadata is tile-major (one contiguous row per tile); a wave per
-  // run, kB runs per wave in flight
-  constexpr uint32_t kB = 16;
   const int32_t* psrc = p2_src + static_cast<size_t>(t) * num_chunks;
   const int32_t* ppos = p2_pos + static_cast<size_t>(t) * (num_chunks + 1);
-  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = nt >> 6;
-  for (uint32_t c0 = w * kB; c0 < num_chunks; c0 += nw * kB) {
-    float v[kB];
-    uint32_t dpos[kB], len[kB], src[kB];
+  for (uint32_t k = threadIdx.x; k < num_chunks; k += nt) msrc[k] = psrc[k];
+  for (uint32_t k = threadIdx.x; k <= num_chunks; k += nt) mpos[k] = ppos[k];
+  __syncthreads();
+  // the tile's segment = its run in every chunk (chunk-major vals from P1);
+  // a half-wave per run (runs average ~30), kB runs per half-wave in flight
+  {
+    constexpr uint32_t kB = 16;
+    const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = nt >> 5;
+    for (uint32_t c0 = hw * kB; c0 < num_chunks; c0 += nhw * kB) {
+      float v[kB];
 #pragma unroll
-    for (uint32_t q = 0; q < kB; ++q) {
-      const uint32_t ch = c0 + q;
-      len[q] = 0;
-      if (ch < num_chunks) {
-        dpos[q] = static_cast<uint32_t>(ppos[ch]);
-        len[q] = static_cast<uint32_t>(ppos[ch + 1]) - dpos[q];
-        src[q] = static_cast<uint32_t>(psrc[ch]);
+      for (uint32_t q = 0; q < kB; ++q) {
+        const uint32_t ch = c0 + q;
+        v[q] = 0.f;
+        if (ch < num_chunks && l32 < static_cast<uint32_t>(mpos[ch + 1] - mpos[ch]))
+          v[q] = vals[msrc[ch] + l32];
       }
-    }
 #pragma unroll
-    for (uint32_t q = 0; q < kB; ++q) v[q] = l64 < len[q] ? vals[src[q] + l64] : 0.f;
-#pragma unroll
-    for (uint32_t q = 0; q < kB; ++q) {
-      if (l64 < len[q]) S[dpos[q] + l64] = v[q];
-      for (uint32_t k = l64 + 64; k < len[q]; k += 64) S[dpos[q] + k] = vals[src[q] + k];
+      for (uint32_t q = 0; q < kB; ++q) {
+        const uint32_t ch = c0 + q;
+        if (ch < num_chunks) {
+          const uint32_t dp = mpos[ch], len = mpos[ch + 1] - mpos[ch];
+          if (l32 < len) S[dp + l32] = v[q];
+          for (uint32_t k = l32 + 32; k < len; k += 32) S[dp + k] = vals[msrc[ch] + k];
+        }
+      }
     }
   }
   __syncthreads();
-  // thread per bucket; its csr range of perm is read 4 entries at a time
+  // bucket sums: a wave takes 64 consecutive buckets, stages their (contiguous)
+  // perm window in LDS with coalesced loads, then each lane sums its bucket
+  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = nt >> 6;
+  uint16_t* mywin = win + w * kP2Win;
   const uint32_t gb0 = t * tile;
-  for (uint32_t b = threadIdx.x; b < tile; b += nt) {
-    const uint32_t gb = gb0 + b;
-    if (gb >= total_buckets) break;
-    const int32_t x0 = csr[gb], x1 = csr[gb + 1];
+  for (uint32_t b0 = w * 64; b0 < tile; b0 += nw * 64) {
+    const uint32_t gb = gb0 + b0 + l64;
+    const bool mine = b0 + l64 < tile && gb < total_buckets;
+    const int32_t x0 = mine ? csr[gb] : 0, x1 = mine ? csr[gb + 1] : 0;
+    const uint32_t glo = gb0 + b0;
+    const uint32_t ghi = min(min(gb0 + b0 + 64, gb0 + tile), total_buckets);
+    if (glo >= ghi) break;
+    const int32_t wlo = csr[glo], whi = csr[ghi];
+    const int32_t wn = whi - wlo;
     float acc = 0.f;
-    int32_t x = x0;
-    for (; x + 3 < x1; x += 4) {
-      const uint32_t p0 = perm[x], p1 = perm[x + 1], p2 = perm[x + 2], p3 = perm[x + 3];
-      acc += (signed_v(S[p0 & 0x7fffu], p0) + signed_v(S[p1 & 0x7fffu], p1)) +
-             (signed_v(S[p2 & 0x7fffu], p2) + signed_v(S[p3 & 0x7fffu], p3));
+    if (wn <= kP2Win) {
+      for (int32_t k0 = 0; k0 < wn; k0 += 64 * 8) {
+        uint32_t pv[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int32_t k = k0 + q * 64 + static_cast<int32_t>(l64);
+          pv[q] = k < wn ? perm[wlo + k] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int32_t k = k0 + q * 64 + static_cast<int32_t>(l64);
+          if (k < wn) mywin[k] = static_cast<uint16_t>(pv[q]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      for (int32_t x = x0; x < x1; ++x) {
+        const uint32_t pl = mywin[x - wlo];
+        acc += signed_v(S[pl & 0x7fffu], pl);
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      for (int32_t x = x0; x < x1; ++x) {
+        const uint32_t pl = perm[x];
+        acc += signed_v(S[pl & 0x7fffu], pl);
+      }
     }
-    for (; x < x1; ++x) {
-      const uint32_t pl = perm[x];
-      acc += signed_v(S[pl & 0x7fffu], pl);
-    }
-    if (x1 > x0) table[gb] += acc;
+    if (mine && x1 > x0) table[gb] += acc;
   }
 }
 
@@ -235,24 +268,25 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
   for (uint32_t t = threadIdx.x; t <= num_tiles; t += blockDim.x) soff[t] = off[orow + t];
   for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
   __syncthreads();
-  // runs -> stage: a wave per run, kB runs per wave in flight at once
+  // runs -> stage: a half-wave per run (runs average ~30), kB runs per
+  // half-wave in flight at once
   constexpr uint32_t kB = 16;
-  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (uint32_t t0 = w * kB; t0 < num_tiles; t0 += nw * kB) {
+  const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
+  for (uint32_t t0 = hw * kB; t0 < num_tiles; t0 += nhw * kB) {
     float v[kB];
 #pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
       const uint32_t t = t0 + q;
       v[q] = 0.f;
-      if (t < num_tiles && l64 < soff[t + 1] - soff[t]) v[q] = vals[sbase[t] + l64];
+      if (t < num_tiles && l32 < soff[t + 1] - soff[t]) v[q] = vals[sbase[t] + l32];
     }
 #pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
       const uint32_t t = t0 + q;
       if (t < num_tiles) {
         const uint32_t o = soff[t], len = soff[t + 1] - o;
-        if (l64 < len) stage[o + l64] = v[q];
-        for (uint32_t k = l64 + 64; k < len; k += 64) stage[o + k] = vals[sbase[t] + k];
+        if (l32 < len) stage[o + l32] = v[q];
+        for (uint32_t k = l32 + 32; k < len; k += 32) stage[o + k] = vals[sbase[t] + k];
       }
     }
   }
@@ -317,6 +351,9 @@ bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
     if (chunk < 64) continue;
     p.chunk = chunk;
     p.num_chunks = (d + chunk - 1) / chunk;
+    // encode P2 keeps a tile's run metadata (2 words per chunk) beside the
+    // segment and 8 perm windows in LDS
+    if (kPlanSegCap * 4 + (2 * p.num_chunks + 1) * 4 + 8 * kP2Win * 2 > kLdsBytes) continue;
     *out = p;
     return true;
   }
@@ -355,7 +392,8 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
     case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
     default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
   }
-  const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4;
+  const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4 + (2 * p.num_chunks + 1) * 4 +
+                    8 * kP2Win * 2;
   hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(512), l2, stream, table, a.vals, a.perm, a.csr,
                      a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
                      static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks));
