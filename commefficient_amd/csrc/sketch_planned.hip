@@ -17,17 +17,22 @@
 //   csr[gb]         i32  bucket start in perm (global bucket gb = j*c + h)
 //   base/off        i32  run starts per (chunk, tile): global / in-chunk
 //   seg[t]          i32  tile segment starts
+//   p2_src/p2_pos   i32  the same runs, tile-major (for encode P2)
 //   vals            f32  d*r scratch shared by encode and query
-// Encode  P1 (block per chunk): stage[slot] = v_i (LDS, no atomics), then
-//            copy the chunk's runs out: vals[run] = stage[run']
-//         P2 (block per tile):  the segment -> LDS; thread per bucket sums
-//            +-S[perm[x]] over its csr range; table tile += sums
+// Encode  P1 (block per chunk): stage[slot] = v_i (LDS, no atomics); the
+//            stage (tile-ordered inside the chunk) is written out chunk-major
+//            with full-line stores
+//         P2 (block per tile):  gather the tile's run of every chunk into an
+//            LDS segment; a wave per 64 buckets stages their perm window in
+//            LDS; lane per bucket sums +-S[perm[x]]; table tile += sums
 // Query   Q1 (block per tile):  tile -> LDS; vals[e] = +-tile[lb(e)]
 //         Q2 (block per chunk): runs -> LDS stage; per coordinate the
 //            lower median of its r staged values
-// Measured predecessor (global-gather P2): 603 us at ResNet-9 size vs 229+215
-// for the LDS-atomic binned encode (profiles/, PMC: LDS float atomics retire
-// ~0.4 lanes/clk/CU, gathers from a 430 KB segment miss L2 every time).
+// Every run-structured access is a READ (partial-line writes would be
+// read-modify-written); loads are batched 8-16 deep per thread because one
+// 150 KB block per CU leaves little occupancy to hide HBM latency.
+// History (ResNet-9 size, profiles/): a global-gather P2 took 603 us; LDS
+// float atomics (binned encode, 229+215 us) retire ~0.4 lanes/clk/CU.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "kernels.h"

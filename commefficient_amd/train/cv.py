@@ -29,6 +29,7 @@ from ..parallel.fed_model import FedModel
 from ..parallel.server import FedOptimizer
 from ..utils import (ScalarWriter, TableLogger, Timer, make_logdir, num_classes_of_dataset,
                      steps_per_epoch, triangular_lambda, union)
+from ..utils.trace import RoundProfiler
 from .losses import cv_loss
 
 DATASETS = {"CIFAR10": FedCIFAR10, "CIFAR100": FedCIFAR100, "EMNIST": FedEMNIST,
@@ -114,7 +115,8 @@ class _Done:
         pass
 
 
-def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args, nan_check=None):
+def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args, nan_check=None,
+                profiler=None):
     if not training and epoch_fraction != 1:
         raise ValueError("Must do full epochs for val")
     model.train(training)
@@ -147,6 +149,8 @@ def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args
                 print("LOSS IS NAN, TERMINATING TRAINING")
                 return float("nan"), float("nan")
             opt.step()
+            if profiler is not None:
+                profiler.step()
             losses.append(loss)
             accs.append(acc)
             rounds += 1
@@ -176,6 +180,8 @@ def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, log
     timer = timer or Timer()
     ctx = dist.ctx()
     nan_check = LagNaNCheck(model.device)
+    profiler = RoundProfiler(getattr(args, "profile_dir", None), ctx.rank,
+                             getattr(args, "profile_rounds", 5))
     total_down = total_up = 0.0
     acct = model.accountant
     summary = {}
@@ -189,7 +195,7 @@ def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, log
         d0 = acct.client_download.sum().item()
         u0 = acct.client_upload.sum().item()
         train_loss, train_acc = run_batches(model, opt, lr_scheduler, train_loader, True, frac,
-                                            args, nan_check)
+                                            args, nan_check, profiler)
         if math.isnan(train_loss):
             print("TERMINATING TRAINING DUE TO NAN LOSS")
             return summary
@@ -216,6 +222,7 @@ def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, log
                     writer.add_scalar(tag, v, epoch)
         if args.max_rounds and model.round_idx >= args.max_rounds:
             break
+    profiler.close(model.timer)
     if ctx.is_main:
         nc = train_loader.dataset.num_clients
         print("Total Download (MiB): {:0.2f}".format(total_down))

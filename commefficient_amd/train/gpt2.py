@@ -26,6 +26,7 @@ from ..parallel.fed_model import FedModel
 from ..parallel.server import FedOptimizer
 from ..utils import (ScalarWriter, TableLogger, Timer, linear_decay_lambda, make_logdir,
                      steps_per_epoch)
+from ..utils.trace import RoundProfiler
 from .losses import gpt2_loss_train, gpt2_loss_val
 
 
@@ -49,7 +50,8 @@ def get_data_loaders(args, device, tokenizer=None):
     return train, test
 
 
-def run_batches(model, opt, sched, loader, training, args, writer=None, log_step0=0):
+def run_batches(model, opt, sched, loader, training, args, writer=None, log_step0=0,
+                profiler=None):
     model.train(training)
     losses, accs = [], []
     ctx = dist.ctx()
@@ -67,6 +69,8 @@ def run_batches(model, opt, sched, loader, training, args, writer=None, log_step
                 continue
             loss, acc, dl, ul = model(batch)
             opt.step()
+            if profiler is not None:
+                profiler.step()
             losses.append(loss)
             accs.append(acc)
             if writer is not None and ctx.is_main:
@@ -120,6 +124,8 @@ def main(args):
     if ctx.is_main:
         print("Finished initializing in {:.2f} seconds".format(timer()))
     logger = TableLogger()
+    profiler = RoundProfiler(getattr(args, "profile_dir", None), ctx.rank,
+                             getattr(args, "profile_rounds", 5))
     if args.do_finetune:
         nll, acc = run_batches(fed, None, None, test_loader, False, args)
         if ctx.is_main:
@@ -128,7 +134,8 @@ def main(args):
     for epoch in range(math.ceil(args.num_epochs)):
         d0 = fed.accountant.client_download.sum().item()
         u0 = fed.accountant.client_upload.sum().item()
-        tl, ta = run_batches(fed, fopt, sched, train_loader, True, args, writer, epoch * int(spe))
+        tl, ta = run_batches(fed, fopt, sched, train_loader, True, args, writer, epoch * int(spe),
+                             profiler)
         ttime = timer()
         down = (fed.accountant.client_download.sum().item() - d0) / 2 ** 20
         up = (fed.accountant.client_upload.sum().item() - u0) / 2 ** 20
@@ -146,6 +153,7 @@ def main(args):
                 writer.add_scalar("validation/ppl", math.exp(min(nll, 50)), epoch)
         if args.max_rounds and fed.round_idx >= args.max_rounds:
             break
+    profiler.close(fed.timer)
     fed.finalize()
     if writer is not None:
         writer.close()

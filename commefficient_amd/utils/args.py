@@ -148,6 +148,8 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="stop after this many training rounds (0: no limit)")
     g.add_argument("--profile_dir", type=str, default=None,
                    help="write per-phase HIP-event timings + torch.profiler traces here")
+    g.add_argument("--profile_rounds", type=int, default=5,
+                   help="rounds captured by torch.profiler (after 1 wait + 1 warmup round)")
     g.add_argument("--channels_last", type=int, default=1, help="NHWC activations for convs")
     g.add_argument("--miopen_find", type=int, default=1,
                    help="MIOpen exhaustive kernel search for each conv shape (cudnn.benchmark); "

@@ -1,0 +1,76 @@
+"""End-to-end driver runs on CPU (synthetic data): the reference's ``--test``
+smoke mode (utils.py:106, cv_train.py:329-336) for every
+federated mode, checkpoint + resume, torch.profiler tracing, and the GPT-2
+driver on the tiny architecture."""
+import json
+import os
+
+import pytest
+import torch
+
+import fed_train
+
+BASE = ["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", "600",
+        "--num_clients", "30", "--num_workers", "5", "--local_batch_size", "-1",
+        "--device", "cpu", "--dtype", "fp32", "--num_epochs", "1", "--valid_batch_size", "16",
+        "--port", "29611"]
+
+MODES = {
+    "sketch": ["--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
+               "--virtual_momentum", "0.9", "--num_rows", "3", "--num_cols", "500", "--k", "50",
+               "--num_blocks", "2"],
+    "true_topk": ["--mode", "true_topk", "--error_type", "virtual", "--local_momentum", "0",
+                  "--virtual_momentum", "0.9", "--k", "100"],
+    "local_topk": ["--mode", "local_topk", "--error_type", "local", "--local_momentum", "0.9",
+                   "--k", "100"],
+    "fedavg": ["--mode", "fedavg", "--error_type", "none", "--local_momentum", "0",
+               "--num_fedavg_epochs", "2", "--fedavg_batch_size", "10"],
+    "uncompressed": ["--mode", "uncompressed", "--error_type", "none", "--local_momentum", "0.9"],
+}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_cv_driver_test_mode(mode, tmp_path, monkeypatch, capsys):
+    monkeypatch.chdir(tmp_path)
+    fed = fed_train.main(BASE + MODES[mode] + ["--test", "--max_rounds", "2"])
+    assert fed.round_idx >= 1
+    out = capsys.readouterr().out
+    assert "Total Upload (MiB)" in out
+    assert torch.isfinite(fed.w).all()
+
+
+def test_cv_driver_checkpoint_resume_and_profile(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    ck = str(tmp_path / "ck") + os.sep
+    base = [a if a != "1" or i == 0 or BASE[i - 1] != "--num_epochs" else "4"
+            for i, a in enumerate(BASE)]  # --test runs one round per epoch
+    args = base + MODES["sketch"] + ["--test", "--model", "ResNet9", "--max_rounds", "3",
+                                     "--checkpoint", "--checkpoint_path", ck,
+                                     "--profile_dir", str(tmp_path / "prof"),
+                                     "--profile_rounds", "1"]
+    fed = fed_train.main(args)
+    sd = torch.load(ck + "ResNet9.pt", map_location="cpu", weights_only=True)
+    assert "n.prep.conv.weight" in sd
+    side = ck + "ResNet9.fedstate.pt"
+    assert os.path.exists(side)
+    assert os.path.exists(tmp_path / "prof" / "rank0" / "kernels.txt")
+    traces = [f for f in os.listdir(tmp_path / "prof" / "rank0") if f.endswith(".json")]
+    assert traces
+    # resume continues the round counter and the server state
+    fed2 = fed_train.main(base + MODES["sketch"] + ["--test", "--max_rounds", "5",
+                                                    "--resume", side])
+    assert fed2.round_idx > fed.round_idx
+
+
+def test_gpt2_driver_tiny_synthetic(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    argv = ["--dataset_name", "PERSONA", "--model", "GPT2DoubleHeads", "--synthetic",
+            "--synthetic_size", "64", "--num_clients", "16", "--num_workers", "4",
+            "--local_batch_size", "2", "--valid_batch_size", "2", "--device", "cpu",
+            "--dtype", "fp32", "--gpt2_size", "tiny", "--mode", "sketch",
+            "--error_type", "virtual", "--local_momentum", "0", "--virtual_momentum", "0.9",
+            "--num_rows", "3", "--num_cols", "2000", "--k", "200", "--num_epochs", "1",
+            "--max_rounds", "2", "--num_results_train", "1", "--port", "29612"]
+    fed = fed_train.main(argv)
+    assert fed.round_idx == 2
+    assert torch.isfinite(fed.w).all()
