@@ -13,7 +13,8 @@
 // Plan arrays:
 //   src_info[i*r+j] u16  slot of entry (i,j) in its chunk's LDS stage
 //   ent_info[e]     u16  in-tile bucket of entry e | sign << 15 (entry order)
-//   perm[x]         u16  segment-local entry index | sign << 15, bucket order
+//   perm[cm]        u16  at an entry's chunk-major position (P1's output):
+//                        its segment-local bucket-order index | sign << 15
 //   csr[gb]         i32  bucket start in perm (global bucket gb = j*c + h)
 //   base/off        i32  run starts per (chunk, tile): global / in-chunk
 //   seg[t]          i32  tile segment starts
@@ -22,9 +23,9 @@
 // Encode  P1 (block per chunk): stage[slot] = v_i (LDS, no atomics); the
 //            stage (tile-ordered inside the chunk) is written out chunk-major
 //            with full-line stores
-//         P2 (block per tile):  gather the tile's run of every chunk into an
-//            LDS segment; a wave per 64 buckets stages their perm window in
-//            LDS; lane per bucket sums +-S[perm[x]]; table tile += sums
+//         P2 (block per tile):  gather the tile's run of every chunk and
+//            scatter each value (signed) to its bucket-order LDS slot;
+//            lane per bucket sums its contiguous range; table tile += sums
 // Query   Q1 (block per tile):  tile -> LDS; vals[e] = +-tile[lb(e)]
 //         Q2 (block per chunk): runs -> LDS stage; per coordinate the
 //            lower median of its r staged values
@@ -41,7 +42,6 @@ namespace commeff {
 namespace {
 
 constexpr int kLdsBytes = 160 * 1024;
-constexpr int32_t kP2Win = 1280;  // encode P2: perm window entries per wave
 
 __device__ __forceinline__ float signed_v(float v, uint32_t info) {
   return (info & 0x8000u) ? -v : v;
@@ -49,7 +49,7 @@ __device__ __forceinline__ float signed_v(float v, uint32_t info) {
 
 // ------------------------------------------------------------- encode P1
 template <int R>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(1024)
 enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, float scale,
               float wscale, uint32_t d, uint32_t r_rt, uint32_t chunk,
               const uint16_t* __restrict__ src_info, float* __restrict__ vals) {
@@ -101,18 +101,17 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
 }
 
 // ------------------------------------------------------------- encode P2
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(1024)
 enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
               const uint16_t* __restrict__ perm, const int32_t* __restrict__ csr,
-              const int32_t* __restrict__ p2_src, const int32_t* __restrict__ p2_pos,
-              uint32_t tile, uint32_t total_buckets, uint32_t num_chunks) {
+              const int32_t* __restrict__ seg, const int32_t* __restrict__ p2_src,
+              const int32_t* __restrict__ p2_pos, uint32_t tile, uint32_t total_buckets,
+              uint32_t num_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // LDS: segment S [kPlanSegCap] | run metadata [2 * num_chunks + 1] |
-  //      per-wave perm window [8][kP2Win] u16
+  // LDS: bucket-ordered segment S [kPlanSegCap] | run metadata [2*num_chunks+1]
   float* S = reinterpret_cast<float*>(smem);
   int32_t* msrc = reinterpret_cast<int32_t*>(S + kPlanSegCap);
   int32_t* mpos = msrc + num_chunks;
-  uint16_t* win = reinterpret_cast<uint16_t*>(mpos + num_chunks + 1);
   const uint32_t t = blockIdx.x;
   const uint32_t nt = blockDim.x;
   const int32_t* psrc = p2_src + static_cast<size_t>(t) * num_chunks;
@@ -120,75 +119,50 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
   for (uint32_t k = threadIdx.x; k < num_chunks; k += nt) msrc[k] = psrc[k];
   for (uint32_t k = threadIdx.x; k <= num_chunks; k += nt) mpos[k] = ppos[k];
   __syncthreads();
-  // the tile's segment = its run in every chunk (chunk-major vals from P1);
-  // a half-wave per run (runs average ~30), kB runs per half-wave in flight
+  // the tile's run in every chunk (chunk-major vals from P1) is read together
+  // with perm at the same positions and scattered (signed) straight into its
+  // bucket-order slot; a half-wave per run, kB runs per half-wave in flight
   {
     constexpr uint32_t kB = 16;
     const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = nt >> 5;
     for (uint32_t c0 = hw * kB; c0 < num_chunks; c0 += nhw * kB) {
       float v[kB];
+      uint32_t pl[kB];
 #pragma unroll
       for (uint32_t q = 0; q < kB; ++q) {
         const uint32_t ch = c0 + q;
         v[q] = 0.f;
-        if (ch < num_chunks && l32 < static_cast<uint32_t>(mpos[ch + 1] - mpos[ch]))
+        pl[q] = 0xffffffffu;
+        if (ch < num_chunks && l32 < static_cast<uint32_t>(mpos[ch + 1] - mpos[ch])) {
           v[q] = vals[msrc[ch] + l32];
+          pl[q] = perm[msrc[ch] + l32];
+        }
       }
 #pragma unroll
       for (uint32_t q = 0; q < kB; ++q) {
+        if (pl[q] != 0xffffffffu) S[pl[q] & 0x7fffu] = signed_v(v[q], pl[q]);
         const uint32_t ch = c0 + q;
         if (ch < num_chunks) {
-          const uint32_t dp = mpos[ch], len = mpos[ch + 1] - mpos[ch];
-          if (l32 < len) S[dp + l32] = v[q];
-          for (uint32_t k = l32 + 32; k < len; k += 32) S[dp + k] = vals[msrc[ch] + k];
+          const uint32_t len = mpos[ch + 1] - mpos[ch];
+          for (uint32_t k = l32 + 32; k < len; k += 32) {
+            const uint32_t x = msrc[ch] + k, p = perm[x];
+            S[p & 0x7fffu] = signed_v(vals[x], p);
+          }
         }
       }
     }
   }
   __syncthreads();
-  // bucket sums: a wave takes 64 consecutive buckets, stages their (contiguous)
-  // perm window in LDS with coalesced loads, then each lane sums its bucket
-  const uint32_t w = threadIdx.x >> 6, l64 = threadIdx.x & 63, nw = nt >> 6;
-  uint16_t* mywin = win + w * kP2Win;
+  // bucket sums: contiguous LDS ranges
+  const uint32_t lo = static_cast<uint32_t>(seg[t]);
   const uint32_t gb0 = t * tile;
-  for (uint32_t b0 = w * 64; b0 < tile; b0 += nw * 64) {
-    const uint32_t gb = gb0 + b0 + l64;
-    const bool mine = b0 + l64 < tile && gb < total_buckets;
-    const int32_t x0 = mine ? csr[gb] : 0, x1 = mine ? csr[gb + 1] : 0;
-    const uint32_t glo = gb0 + b0;
-    const uint32_t ghi = min(min(gb0 + b0 + 64, gb0 + tile), total_buckets);
-    if (glo >= ghi) break;
-    const int32_t wlo = csr[glo], whi = csr[ghi];
-    const int32_t wn = whi - wlo;
+  for (uint32_t b = threadIdx.x; b < tile; b += nt) {
+    const uint32_t gb = gb0 + b;
+    if (gb >= total_buckets) break;
+    const uint32_t x0 = static_cast<uint32_t>(csr[gb]) - lo, x1 = static_cast<uint32_t>(csr[gb + 1]) - lo;
     float acc = 0.f;
-    if (wn <= kP2Win) {
-      for (int32_t k0 = 0; k0 < wn; k0 += 64 * 8) {
-        uint32_t pv[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int32_t k = k0 + q * 64 + static_cast<int32_t>(l64);
-          pv[q] = k < wn ? perm[wlo + k] : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int32_t k = k0 + q * 64 + static_cast<int32_t>(l64);
-          if (k < wn) mywin[k] = static_cast<uint16_t>(pv[q]);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      for (int32_t x = x0; x < x1; ++x) {
-        const uint32_t pl = mywin[x - wlo];
-        acc += signed_v(S[pl & 0x7fffu], pl);
-      }
-      __builtin_amdgcn_wave_barrier();
-    } else {
-      for (int32_t x = x0; x < x1; ++x) {
-        const uint32_t pl = perm[x];
-        acc += signed_v(S[pl & 0x7fffu], pl);
-      }
-    }
-    if (mine && x1 > x0) table[gb] += acc;
+    for (uint32_t x = x0; x < x1; ++x) acc += S[x];
+    if (x1 > x0) table[gb] += acc;
   }
 }
 
@@ -256,7 +230,7 @@ __device__ __forceinline__ float lower_median_r(float (&v)[kMaxRows], int r) {
 }
 
 template <int R>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(1024)
 qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_t chunk,
               uint32_t num_tiles, const uint16_t* __restrict__ src_info,
               const int32_t* __restrict__ base, const int32_t* __restrict__ off,
@@ -357,8 +331,8 @@ bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
     p.chunk = chunk;
     p.num_chunks = (d + chunk - 1) / chunk;
     // encode P2 keeps a tile's run metadata (2 words per chunk) beside the
-    // segment and 8 perm windows in LDS
-    if (kPlanSegCap * 4 + (2 * p.num_chunks + 1) * 4 + 8 * kP2Win * 2 > kLdsBytes) continue;
+    // segment in LDS
+    if (kPlanSegCap * 4 + (2 * p.num_chunks + 1) * 4 > kLdsBytes) continue;
     *out = p;
     return true;
   }
@@ -392,15 +366,14 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
   const size_t l1 = static_cast<size_t>(p.chunk) * r * 4;
   const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
   switch (r) {
-    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
-    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
-    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
-    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(512), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
   }
-  const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4 + (2 * p.num_chunks + 1) * 4 +
-                    8 * kP2Win * 2;
-  hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(512), l2, stream, table, a.vals, a.perm, a.csr,
-                     a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
+  const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4 + (2 * p.num_chunks + 1) * 4;
+  hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(1024), l2, stream, table, a.vals, a.perm,
+                     a.csr, a.seg, a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
                      static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks));
 }
 
@@ -424,10 +397,10 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
   const size_t l2 = stage_lds(p, r);
   const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
   switch (r) {
-    case 5: hipLaunchKernelGGL(qry_q2_kernel<5>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 3: hipLaunchKernelGGL(qry_q2_kernel<3>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 1: hipLaunchKernelGGL(qry_q2_kernel<1>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    default: hipLaunchKernelGGL(qry_q2_kernel<0>, g2, dim3(512), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 5: hipLaunchKernelGGL(qry_q2_kernel<5>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 3: hipLaunchKernelGGL(qry_q2_kernel<3>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 1: hipLaunchKernelGGL(qry_q2_kernel<1>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    default: hipLaunchKernelGGL(qry_q2_kernel<0>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
   }
 }
 

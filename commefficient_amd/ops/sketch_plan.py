@@ -8,7 +8,8 @@ tile's whole segment of entries fits in LDS), then coordinate chunks, then
 
   src_info[i*r+j]  int16  slot of entry (i, j) in its chunk's LDS stage
   ent_info[e]      int16  in-tile bucket | sign << 15, entry (segment) order
-  perm[x]          int16  segment-local entry index | sign << 15, bucket order
+  perm[cm]         int16  at an entry's chunk-major position (encode P1's output
+                          layout): its segment-local bucket-order index | sign << 15
   csr              int32  [num_tiles*T + 1] bucket starts in perm
   base             int32  [num_chunks, num_tiles] global start of each run
   off              int32  [num_chunks, num_tiles + 1] in-chunk run starts
@@ -82,13 +83,26 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     ent_info = torch.empty(n, dtype=torch.int16, device=device)
     ent_info[global_pos] = _to_i16(lb | sign_bit)
     del lb, tile_id, global_pos
-    # bucket order: entries (in segment order) stably sorted by global bucket
+    # bucket order: entries (in segment order) stably sorted by global bucket;
+    # encode P2 scatters each entry straight to its bucket-order slot, so the
+    # plan stores, at the entry's CHUNK-MAJOR position (P1's output layout),
+    # its segment-local bucket-order index | sign << 15
     gb_pos = gb[order]
-    _, perm_pos = torch.sort(gb_pos, stable=True)
+    _, perm_pos = torch.sort(gb_pos, stable=True)           # bucket order -> segment pos
+    bo_of_pos = torch.empty_like(perm_pos)
+    bo_of_pos[perm_pos] = torch.arange(n, device=device, dtype=perm_pos.dtype)
     tile_of_pos = sorted_key // num_chunks
-    seg_local = perm_pos - seg[tile_of_pos[perm_pos]]
-    perm = _to_i16(seg_local | (neg[order][perm_pos].to(i64) << 15))
-    del gb_pos, tile_of_pos, seg_local, sorted_key, order, perm_pos, sign_bit
+    bo_local = bo_of_pos - seg[tile_of_pos]                 # per segment position
+    del gb_pos, perm_pos, bo_of_pos, tile_of_pos, sorted_key
+    # entry e = i*r+j: segment position global_pos_e, chunk-major position
+    # chunk(i)*chunk*r + slot_e
+    cm = (torch.arange(d, device=device, dtype=i64) // chunk).repeat_interleave(r) * (chunk * r) \
+        + src_info.to(i64).bitwise_and(0xFFFF)
+    gpos_e = torch.empty_like(order)
+    gpos_e[order] = torch.arange(n, device=device, dtype=order.dtype)
+    perm = torch.empty(n, dtype=torch.int16, device=device)
+    perm[cm] = _to_i16(bo_local[gpos_e] | sign_bit)
+    del cm, gpos_e, bo_local, order, sign_bit
     csr = torch.zeros(num_tiles * tile + 1, dtype=i64, device=device)
     csr[1:] = torch.cumsum(torch.bincount(gb, minlength=num_tiles * tile), 0)
     vals = torch.empty(n, dtype=torch.float32, device=device)

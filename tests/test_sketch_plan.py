@@ -38,17 +38,27 @@ def _gpos_of_slots(geo, plan, d, r):
 
 def _simulate_encode(geo, plan, vec, r, c):
     tile, nt, chunk, nch = geo
-    _, _, perm, csr, _, _, seg, _ = plan[:8]
+    src_info, _, perm, csr, _, _, seg, _ = plan[:8]
+    p2_src, p2_pos = plan[8].long(), plan[9].long()
     d = vec.numel()
-    vals = torch.empty(d * r, dtype=torch.float64)
-    vals[_gpos_of_slots(geo, plan, d, r)] = vec.double().repeat_interleave(r)     # P1
-    csr = csr.to(torch.int64)
-    gb_of_x = torch.repeat_interleave(torch.arange(r * c), csr[1:r * c + 1] - csr[:r * c])
+    # P1: chunk-major stage images
+    cm = (torch.arange(d) // chunk).repeat_interleave(r) * (chunk * r) + _u16(src_info)
+    vals = torch.zeros(nch * chunk * r, dtype=torch.float64)
+    vals[cm] = vec.double().repeat_interleave(r)
+    # P2: per tile, every chunk's run scattered to its bucket-order slot
     pl = _u16(perm)
-    idx = seg.to(torch.int64)[gb_of_x // tile] + (pl & 0x7FFF)
-    contrib = torch.where((pl & 0x8000) != 0, -vals[idx], vals[idx])               # P2
+    csr = csr.to(torch.int64)
+    seg = seg.to(torch.int64)
     table = torch.zeros(r * c, dtype=torch.float64)
-    table.index_add_(0, gb_of_x, contrib)
+    for t in range(nt):
+        S = torch.zeros(int(seg[t + 1] - seg[t]), dtype=torch.float64)
+        for ch in range(nch):
+            a, ln = int(p2_src[t, ch]), int(p2_pos[t, ch + 1] - p2_pos[t, ch])
+            x = torch.arange(a, a + ln)
+            S[pl[x] & 0x7FFF] = torch.where((pl[x] & 0x8000) != 0, -vals[x], vals[x])
+        g1 = min((t + 1) * tile, r * c)
+        for gb in range(t * tile, g1):
+            table[gb] = S[csr[gb] - seg[t]:csr[gb + 1] - seg[t]].sum()
     return table.view(r, c)
 
 
