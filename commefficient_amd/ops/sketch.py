@@ -11,7 +11,7 @@ and ``/``.  Call sites in the reference:
 Differences by design (MI355X-first):
 * hashes are recomputed inside the kernels from 4 coefficients per row
   (``hashes`` is a tiny CPU int64 tensor), so no r x d index tables exist --
-  except for the optional GPU "planned" kernels, which trade a one-time
+  except for the default GPU "planned" kernels, which trade a one-time
   permutation plan (ops/sketch_plan.py, ~0.4 GB at ResNet-9 size) for
   atomic-free, bitwise-deterministic encode and query;
 * ``unSketch`` returns the dense vector like CSVec, while ``unsketch_sparse``
@@ -56,7 +56,7 @@ class CSVec:
 
     def __init__(self, d: int, c: int, r: int, device="cpu", numBlocks: int = 1,
                  seed: int = 42, table: Optional[torch.Tensor] = None,
-                 _hashes=None, _scratch=None, kernel: str = "binned"):
+                 _hashes=None, _scratch=None, kernel: str = "planned"):
         self.d = int(d)
         self.c = int(c)
         self.r = int(r)

@@ -134,7 +134,7 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="merge the clients of a rank into one forward/backward when the "
                         "mode is linear per client (exact; see parallel/fed_model.py)")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
-    g.add_argument("--encode", choices=["planned", "binned", "direct"], default="binned",
+    g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
                    help="GPU Count-Sketch encode/query kernels: planned (precomputed "
                         "permutation, atomic free), binned (LDS atomics) or direct "
                         "(global atomics)")
