@@ -572,10 +572,24 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   const bool wide = a.K % 128 == 0;
   const int bn = wide ? 128 : 64;
+  // tile override for tuning experiments: COMMEFF_CONV_CFG = 256_3 | 256_2 | 128_3 | 128_2
+  static const int cfg = [] {
+    const char* e = getenv("COMMEFF_CONV_CFG");
+    if (e == nullptr) return 0;
+    return atoi(e) * 10 + (e[3] == '_' ? atoi(e + 4) : 0);
+  }();
+  if (cfg != 0) {
+    switch (cfg) {
+      case 2563: if (wide) launch_fwd<256, 128, 3>(a, stream); else launch_fwd<256, 64, 3>(a, stream); return;
+      case 2562: if (wide) launch_fwd<256, 128, 2>(a, stream); else launch_fwd<256, 64, 2>(a, stream); return;
+      case 1283: if (wide) launch_fwd<128, 128, 3>(a, stream); else launch_fwd<128, 64, 3>(a, stream); return;
+      default: break;
+    }
+  }
   // 256-pixel tiles (8 waves, 3-stage ring, 1 block/CU) while they still give
   // >= 2 waves of blocks; else 128-pixel tiles (4 waves, 2 stages, 2 blocks/CU)
   const bool big = static_cast<int64_t>((a.P + 255) / 256) * (a.K / bn) >= 512;
-  if (big) {
+  if (big && cfg != 1282) {
     if (wide) launch_fwd<256, 128, 3>(a, stream); else launch_fwd<256, 64, 3>(a, stream);
   } else {
     if (wide) launch_fwd<128, 128, 2>(a, stream); else launch_fwd<128, 64, 2>(a, stream);
@@ -597,7 +611,15 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
   a.steps_per_split = (steps + a.splits - 1) / a.splits;
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
-  if (a.C % 128 == 0) launch_wgrad<128, 2>(a, stream); else launch_wgrad<64, 2>(a, stream);
+  static const bool three = [] {  // tuning experiment: COMMEFF_WGRAD_STAGES=3
+    const char* e = getenv("COMMEFF_WGRAD_STAGES");
+    return e != nullptr && e[0] == '3';
+  }();
+  if (three) {
+    if (a.C % 128 == 0) launch_wgrad<128, 3>(a, stream); else launch_wgrad<64, 3>(a, stream);
+  } else {
+    if (a.C % 128 == 0) launch_wgrad<128, 2>(a, stream); else launch_wgrad<64, 2>(a, stream);
+  }
   const int64_t n4 = static_cast<int64_t>(a.K) * 9 * a.C / 4;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, stream,
                      a.slab, dw, a.K, a.C, a.splits, beta);
