@@ -586,11 +586,13 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
       default: break;
     }
   }
-  // 256-pixel tiles (8 waves, 3-stage ring, 1 block/CU) while they still give
-  // >= 2 waves of blocks; else 128-pixel tiles (4 waves, 2 stages, 2 blocks/CU)
+  // measured (scripts/bench_conv.py sweep, profiles/r1_conv_tile_sweep.txt):
+  // occupancy beats ring depth -- 128-pixel tiles with a 2-stage ring (2
+  // blocks/CU) everywhere, except 64-wide outputs of big layers, where 256
+  // pixels x 64 (8 waves, 2 stages) amortises the A operand better
   const bool big = static_cast<int64_t>((a.P + 255) / 256) * (a.K / bn) >= 512;
-  if (big && cfg != 1282) {
-    if (wide) launch_fwd<256, 128, 3>(a, stream); else launch_fwd<256, 64, 3>(a, stream);
+  if (!wide && big && cfg != 1282) {
+    launch_fwd<256, 64, 2>(a, stream);
   } else {
     if (wide) launch_fwd<128, 128, 2>(a, stream); else launch_fwd<128, 64, 2>(a, stream);
   }
