@@ -306,7 +306,7 @@ __device__ __forceinline__ bf16x8_t tr_read(const unsigned char* a0, const unsig
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
-template <int BN, int NSTAGE>
+template <int BN, int NSTAGE, bool ROWSTEP>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int A_BYTES = BK * WBM * 2;  // [64 px][128 k], 256-byte rows
@@ -357,36 +357,41 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     b_row[j] = p;
     const uint32_t q = fdiv(static_cast<uint32_t>(p), a.div_w);
     b_w[j] = p - static_cast<int>(q) * W;
-    b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H);
+    b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H) + dr;  // tap row of the source
     b_ptr[j] = a.x + static_cast<int64_t>(p + dr * W + ds) * C + c0 + lc * 8;
   }
-  // pixel advance per step = BK; when W | BK that is BK/W whole image rows
-  const bool rows_step = (BK % W) == 0;
-  const int dh = rows_step ? (BK / W) % H : 0;
+  // when W | BK a step advances every row by BK/W whole image rows: w is
+  // fixed per chunk and h advances incrementally (ROWSTEP); else recompute
+  bool b_wok[BLD];
+#pragma unroll
+  for (int j = 0; j < BLD; ++j)
+    b_wok[j] = static_cast<unsigned>(b_w[j] + ds) < static_cast<unsigned>(W);
+  const int dh = ROWSTEP ? (BK / W) % H : 0;
 
-  auto issue = [&](int stage) __attribute__((always_inline)) {
+  auto issue = [&](int stage, bool full) __attribute__((always_inline)) {
     unsigned char* base = smem + stage * STAGE + wid * 1024;
 #pragma unroll
     for (int i = 0; i < ALD; ++i) {
-      glds16(a_row[i] < pend ? a_ptr[i] : zero, base + i * 4096);
+      glds16(full || a_row[i] < pend ? a_ptr[i] : zero, base + i * 4096);
       a_row[i] += BK;
       a_ptr[i] += static_cast<size_t>(BK) * K;
     }
 #pragma unroll
     for (int j = 0; j < BLD; ++j) {
-      const int hh = b_h[j] + dr, ww = b_w[j] + ds;
-      const bool ok = b_row[j] < pend && static_cast<unsigned>(hh) < static_cast<unsigned>(H) &&
-                      static_cast<unsigned>(ww) < static_cast<unsigned>(W);
+      bool ok = static_cast<unsigned>(b_h[j]) < static_cast<unsigned>(H);
+      if constexpr (ROWSTEP) ok = ok && b_wok[j];
+      else ok = ok && static_cast<unsigned>(b_w[j] + ds) < static_cast<unsigned>(W);
+      if (!full) ok = ok && b_row[j] < pend;
       glds16(ok ? b_ptr[j] : zero, base + A_BYTES + j * 4096);
       b_row[j] += BK;
       b_ptr[j] += static_cast<size_t>(BK) * C;
-      if (rows_step) {
-        b_h[j] += dh;
-        if (b_h[j] >= H) b_h[j] -= H;
+      if constexpr (ROWSTEP) {
+        const int nh = b_h[j] + dh;
+        b_h[j] = nh - dr >= H ? nh - H : nh;
       } else {
         const uint32_t q = fdiv(static_cast<uint32_t>(b_row[j]), a.div_w);
         b_w[j] = b_row[j] - static_cast<int>(q) * W;
-        b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H);
+        b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H) + dr;
       }
     }
   };
@@ -399,8 +404,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
 
-  if (nsteps > 0) issue(0);
-  if (NSTAGE == 3 && nsteps > 1) issue(1);
+  if (nsteps > 0) issue(0, pbeg + BK <= pend);
+  if (NSTAGE == 3 && nsteps > 1) issue(1, pbeg + 2 * BK <= pend);
   // this lane's transposed-read offsets at sub-step 0 (the swizzles do not
   // depend on the sub-step: sub-step kk adds kk * 16 rows)
   int toA[2][2], toB[NI][2];
@@ -417,7 +422,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (st + NSTAGE - 1 < nsteps) issue(wrs);
+    if (st + NSTAGE - 1 < nsteps) issue(wrs, pbeg + (st + NSTAGE) * BK <= pend);
     const unsigned char* sA = smem + rd * STAGE;
     const unsigned char* sB = sA + A_BYTES;
     bf16x8_t af[2][2], bfr[2][NI];
@@ -550,16 +555,16 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t stream) {
                      stream, a);
 }
 
-template <int BN, int NSTAGE>
+template <int BN, int NSTAGE, bool ROWSTEP>
 void launch_wgrad(const ConvWgradArgs& a, hipStream_t stream) {
   constexpr int lds = NSTAGE * (BK * WBM * 2 + BK * BN * 2);
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_wgrad_kernel<BN, NSTAGE>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_wgrad_kernel<BN, NSTAGE, ROWSTEP>), lds);
     init = true;
   }
   const int tiles = (a.K / WBM) * 9 * (a.C / BN);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BN, NSTAGE>), dim3(tiles * a.splits), dim3(256), lds,
+  hipLaunchKernelGGL((conv_wgrad_kernel<BN, NSTAGE, ROWSTEP>), dim3(tiles * a.splits), dim3(256), lds,
                      stream, a);
 }
 
@@ -617,10 +622,14 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
     const char* e = getenv("COMMEFF_WGRAD_STAGES");
     return e != nullptr && e[0] == '3';
   }();
-  if (three) {
-    if (a.C % 128 == 0) launch_wgrad<128, 3>(a, stream); else launch_wgrad<64, 3>(a, stream);
+  const bool rowstep = BK % a.W == 0;
+  const bool wide = a.C % 128 == 0;
+  if (three && rowstep) {
+    if (wide) launch_wgrad<128, 3, true>(a, stream); else launch_wgrad<64, 3, true>(a, stream);
+  } else if (rowstep) {
+    if (wide) launch_wgrad<128, 2, true>(a, stream); else launch_wgrad<64, 2, true>(a, stream);
   } else {
-    if (a.C % 128 == 0) launch_wgrad<128, 2>(a, stream); else launch_wgrad<64, 2>(a, stream);
+    if (wide) launch_wgrad<128, 2, false>(a, stream); else launch_wgrad<64, 2, false>(a, stream);
   }
   const int64_t n4 = static_cast<int64_t>(a.K) * 9 * a.C / 4;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, stream,
