@@ -332,20 +332,22 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   const int pbeg = split * a.steps_per_split * BK;
   const int pend = min(a.P, pbeg + a.steps_per_split * BK);
   const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_conv_zero);
+  // DMA source addresses as integers (pointer arrays + selects made hipcc
+  // spill the array to scratch and index it dynamically)
+  const uint64_t zero = reinterpret_cast<uint64_t>(g_conv_zero);
 
   // A chunks: rows of dy
-  const uint16_t* a_ptr[ALD];
+  uint64_t a_ptr[ALD];
   int a_row[ALD];
 #pragma unroll
   for (int i = 0; i < ALD; ++i) {
     const int s = i * 256 + tid;
     const int row = s >> 4, lc = (s & 15) ^ sw_tr256(row);
     a_row[i] = pbeg + row;
-    a_ptr[i] = a.dy + static_cast<size_t>(pbeg + row) * K + k0 + lc * 8;
+    a_ptr[i] = reinterpret_cast<uint64_t>(a.dy + static_cast<size_t>(pbeg + row) * K + k0 + lc * 8);
   }
   // B chunks: rows of x at the tap offset; (h, w) of the row tracked per step
-  const uint16_t* b_ptr[BLD];
+  uint64_t b_ptr[BLD];
   int b_row[BLD], b_h[BLD], b_w[BLD];
 #pragma unroll
   for (int j = 0; j < BLD; ++j) {
@@ -358,33 +360,35 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     const uint32_t q = fdiv(static_cast<uint32_t>(p), a.div_w);
     b_w[j] = p - static_cast<int>(q) * W;
     b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H) + dr;  // tap row of the source
-    b_ptr[j] = a.x + static_cast<int64_t>(p + dr * W + ds) * C + c0 + lc * 8;
+    b_ptr[j] = reinterpret_cast<uint64_t>(a.x + static_cast<int64_t>(p + dr * W + ds) * C + c0 +
+                                          lc * 8);
   }
   // when W | BK a step advances every row by BK/W whole image rows: w is
   // fixed per chunk and h advances incrementally (ROWSTEP); else recompute
-  bool b_wok[BLD];
+  uint32_t b_wok = 0;  // bit j: column of chunk j stays inside the image at this tap
 #pragma unroll
   for (int j = 0; j < BLD; ++j)
-    b_wok[j] = static_cast<unsigned>(b_w[j] + ds) < static_cast<unsigned>(W);
+    b_wok |= (static_cast<unsigned>(b_w[j] + ds) < static_cast<unsigned>(W) ? 1u : 0u) << j;
   const int dh = ROWSTEP ? (BK / W) % H : 0;
 
   auto issue = [&](int stage, bool full) __attribute__((always_inline)) {
     unsigned char* base = smem + stage * STAGE + wid * 1024;
 #pragma unroll
     for (int i = 0; i < ALD; ++i) {
-      glds16(full || a_row[i] < pend ? a_ptr[i] : zero, base + i * 4096);
+      glds16(reinterpret_cast<const void*>(full || a_row[i] < pend ? a_ptr[i] : zero),
+             base + i * 4096);
       a_row[i] += BK;
-      a_ptr[i] += static_cast<size_t>(BK) * K;
+      a_ptr[i] += static_cast<uint64_t>(BK) * K * 2;
     }
 #pragma unroll
     for (int j = 0; j < BLD; ++j) {
       bool ok = static_cast<unsigned>(b_h[j]) < static_cast<unsigned>(H);
-      if constexpr (ROWSTEP) ok = ok && b_wok[j];
+      if constexpr (ROWSTEP) ok = ok && ((b_wok >> j) & 1u);
       else ok = ok && static_cast<unsigned>(b_w[j] + ds) < static_cast<unsigned>(W);
       if (!full) ok = ok && b_row[j] < pend;
-      glds16(ok ? b_ptr[j] : zero, base + A_BYTES + j * 4096);
+      glds16(reinterpret_cast<const void*>(ok ? b_ptr[j] : zero), base + A_BYTES + j * 4096);
       b_row[j] += BK;
-      b_ptr[j] += static_cast<size_t>(BK) * C;
+      b_ptr[j] += static_cast<uint64_t>(BK) * C * 2;
       if constexpr (ROWSTEP) {
         const int nh = b_h[j] + dh;
         b_h[j] = nh - dr >= H ? nh - H : nh;
