@@ -607,9 +607,9 @@ const uint16_t* opt_like(const c10::optional<at::Tensor>& t, const at::Tensor& y
 }
 
 // y = act(conv3x3(x, w)) ; w bf16 [K][3][3][C] contiguous
-at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
-                           const c10::optional<at::Tensor>& mask,
-                           const c10::optional<at::Tensor>& addend) {
+at::Tensor conv3x3_fwd_impl(const at::Tensor& x, const at::Tensor& w, bool relu,
+                            const c10::optional<at::Tensor>& mask,
+                            const c10::optional<at::Tensor>& addend, at::Tensor* pre) {
   check_nhwc_bf16(x, "conv3x3: x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 &&
@@ -633,8 +633,28 @@ at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
   a.C = static_cast<int>(C);
   a.K = static_cast<int>(K);
   a.relu = relu ? 1 : 0;
+  a.y_pre = nullptr;
+  if (pre != nullptr) {
+    TORCH_CHECK(a.addend != nullptr, "conv3x3: the pre-add output needs an addend");
+    *pre = at::empty_like(y, y.options().memory_format(at::MemoryFormat::ChannelsLast));
+    a.y_pre = reinterpret_cast<uint16_t*>(pre->data_ptr());
+  }
   if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
   return y;
+}
+
+at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
+                           const c10::optional<at::Tensor>& mask,
+                           const c10::optional<at::Tensor>& addend) {
+  return conv3x3_fwd_impl(x, w, relu, mask, addend, nullptr);
+}
+
+// residual unit tail: out = relu(conv3x3(x, w)) + addend, and pre = relu(conv3x3(x, w))
+std::tuple<at::Tensor, at::Tensor> conv3x3_relu_add_hip(const at::Tensor& x, const at::Tensor& w,
+                                                        const at::Tensor& addend) {
+  at::Tensor pre;
+  auto out = conv3x3_fwd_impl(x, w, true, c10::nullopt, addend, &pre);
+  return {out, pre};
 }
 
 // dw [K][C][3][3] fp32 = sum_p dy[p, k] x[p + (r-1, s-1), c]
@@ -735,6 +755,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
+  m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("relu_mask(Tensor gy, Tensor y) -> Tensor");
@@ -794,6 +815,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("relu_maxpool", &relu_maxpool_hip);
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("conv3x3_fwd", &conv3x3_fwd_hip);
+  m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);
   m.impl("relu_mask", &relu_mask_hip);

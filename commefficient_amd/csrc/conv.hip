@@ -270,6 +270,14 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
     if (a.addend != nullptr) {
+      if (a.y_pre != nullptr) {  // the activation before the residual add
+        v4u pre;
+        pre[0] = pack_bf16(v[0], v[1]);
+        pre[1] = pack_bf16(v[2], v[3]);
+        pre[2] = pack_bf16(v[4], v[5]);
+        pre[3] = pack_bf16(v[6], v[7]);
+        *reinterpret_cast<v4u*>(a.y_pre + o) = pre;
+      }
       const v4u m = *reinterpret_cast<const v4u*>(a.addend + o);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += bf2f((m[j >> 1] >> (16 * (j & 1))) & 0xffffu);
@@ -502,14 +510,22 @@ __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __r
 __global__ void __launch_bounds__(256) conv_weight_prep_kernel(const float* __restrict__ w,
                                                                __bf16* __restrict__ wf,
                                                                __bf16* __restrict__ wt, int K, int C) {
+  // thread per OUTPUT element (coalesced 2-byte stores; the strided 4-byte
+  // reads of the small fp32 weight hit L2): [0, n) -> wf, [n, 2n) -> wt
   const int n = K * C * 9;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const int rs = i % 9;
-    const int c = (i / 9) % C;
-    const int k = i / (9 * C);
-    const __bf16 b = static_cast<__bf16>(w[i]);
-    if (wf != nullptr) wf[(k * 9 + rs) * C + c] = b;
-    if (wt != nullptr) wt[(c * 9 + (8 - rs)) * K + k] = b;
+  for (int o = blockIdx.x * 256 + threadIdx.x; o < 2 * n; o += gridDim.x * 256) {
+    if (o < n) {
+      if (wf == nullptr) continue;
+      const int c = o % C, krs = o / C;           // wf[k][rs][c]
+      const int rs = krs % 9, k = krs / 9;
+      wf[o] = static_cast<__bf16>(w[(k * C + c) * 9 + rs]);
+    } else {
+      if (wt == nullptr) continue;
+      const int q = o - n;
+      const int k = q % K, crs = q / K;           // wt[c][rs'][k] = w[k][c][8 - rs']
+      const int rs = crs % 9, c = crs / 9;
+      wt[q] = static_cast<__bf16>(w[(k * C + c) * 9 + (8 - rs)]);
+    }
   }
 }
 
@@ -612,7 +628,7 @@ int conv3x3_wgrad_splits(int P, int K, int C) {
   const int tiles = (K / WBM) * 9 * (C / bn);
   const int steps = (P + BK - 1) / BK;
   // ~3 blocks per CU (2 resident) with >= 32 K-steps each
-  int s = (768 + tiles - 1) / tiles;
+  int s = (512 + tiles - 1) / tiles;
   if (s > steps / 32) s = steps / 32;
   return s < 1 ? 1 : s;
 }
@@ -642,7 +658,7 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 
 void launch_conv_weight_prep(const float* w, uint16_t* wf, uint16_t* wt, int K, int C,
                              hipStream_t stream) {
-  hipLaunchKernelGGL(conv_weight_prep_kernel, dim3(grid_for(static_cast<int64_t>(K) * C * 9, 256)),
+  hipLaunchKernelGGL(conv_weight_prep_kernel, dim3(grid_for(static_cast<int64_t>(K) * C * 18, 256)),
                      dim3(256), 0, stream, w, reinterpret_cast<__bf16*>(wf),
                      reinterpret_cast<__bf16*>(wt), K, C);
 }

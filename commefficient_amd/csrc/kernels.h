@@ -138,6 +138,7 @@ struct ConvFwdArgs {
   uint16_t* y;             // [P, K]
   const uint16_t* mask;    // optional [P, K]: y = 0 where mask <= 0
   const uint16_t* addend;  // optional [P, K]: y += addend (after relu / mask)
+  uint16_t* y_pre;         // optional [P, K]: the value before the addend (with addend only)
   int P, H, W, C, K;
   int relu;
   FastDivU32 div_w, div_h;  // set by the launcher

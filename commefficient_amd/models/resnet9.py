@@ -21,7 +21,7 @@ import itertools
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import conv3x3_relu_pool, relu_maxpool
+from ..ops.nn import conv3x3_relu_pool, relu_maxpool, residual_unit
 from .common import GhostBatchNorm2d, Mul
 
 __all__ = ["ResNet9"]
@@ -88,6 +88,9 @@ class Residual(nn.Module):
         # reference: x + relu(res2(res1(x))); res2 already ends in a ReLU, so
         # the outer one is the identity and is dropped (saves a fwd+bwd pass
         # over the activation)
+        if not self.res1.do_batchnorm:
+            # one native unit: skip-add and relu masks fused into conv epilogues
+            return residual_unit(x, self.res1.conv.weight, self.res2.conv.weight)
         return x + self.res2(self.res1(x))
 
 

@@ -93,6 +93,47 @@ class _Conv3x3Act(torch.autograd.Function):
         return gx, gw, None
 
 
+class _ResidualUnit(torch.autograd.Function):
+    """``x + relu(conv3x3(relu(conv3x3(x, w1)), w2))`` -- ResNet-9's Residual
+    (reference models/resnet9.py:61-72) as one native unit.
+
+    Forward: the second conv's epilogue applies the ReLU, adds the skip input
+    and also emits the pre-add activation (its ReLU mask is needed backward).
+    Backward: one relu-mask kernel; dgrad of conv2 masks by relu(conv1)'s
+    output in its epilogue (= conv1's ReLU backward); dgrad of conv1 adds the
+    skip gradient in its epilogue.  Two elementwise passes fewer each way
+    than the per-op composition.
+    """
+
+    @staticmethod
+    def forward(ctx, x, w1, w2):
+        w1f, w1t = _ops().conv_weight_prep(w1.detach().contiguous())
+        w2f, w2t = _ops().conv_weight_prep(w2.detach().contiguous())
+        y1 = _ops().conv3x3_fwd(x, w1f, True)
+        out, y2 = _ops().conv3x3_relu_add(y1, w2f, x)
+        ctx.save_for_backward(x, y1, y2, w1t, w2t)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y1, y2, w1t, w2t = ctx.saved_tensors
+        g = g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        g2 = _ops().relu_mask(g, y2)
+        g1 = _ops().conv3x3_fwd(g2, w2t, False, y1)  # masked by relu(conv1) > 0
+        dw2 = _ops().conv3x3_wgrad(g2, y1) if ctx.needs_input_grad[2] else None
+        gx = _ops().conv3x3_fwd(g1, w1t, False, None, g) if ctx.needs_input_grad[0] else None
+        dw1 = _ops().conv3x3_wgrad(g1, x) if ctx.needs_input_grad[1] else None
+        return gx, dw1, dw2
+
+
+def residual_unit(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    """``x + relu(conv2(relu(conv1(x))))`` (3x3, pad 1, no bias)."""
+    if conv3x3_native_ok(x, w1) and conv3x3_native_ok(x, w2) and w1.shape[0] == x.shape[1]:
+        return _ResidualUnit.apply(x, w1, w2)
+    y = F.relu(F.conv2d(x, w1, padding=1))
+    return x + F.relu(F.conv2d(y, w2, padding=1))
+
+
 def conv3x3_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return (_CONV_BACKEND[0] == "native" and x.is_cuda and x.dtype == torch.bfloat16
             and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)

@@ -131,6 +131,34 @@ def test_conv_unit_autograd_matches_fp32(N, C, H, W, K, pool_k):
         assert rel < 2e-2, rel.item()
 
 
+@pytest.mark.parametrize("N,C,H", [(4, 128, 16), (3, 512, 4)])
+def test_residual_unit_matches_fp32(N, C, H):
+    x, w1 = _inputs(N, C, H, H, C)
+    _, w2 = _inputs(N, C, H, H, C, seed=7)
+    x = x.relu().detach().requires_grad_(True)  # block inputs are post-ReLU
+    w1 = w1.detach().requires_grad_(True)
+    w2 = w2.detach().requires_grad_(True)
+    cnn.set_conv_backend("native")
+    y = cnn.residual_unit(x, w1, w2)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    gy = torch.randn(y.shape, device="cuda", generator=g)
+    (y.float() * gy).sum().backward()
+
+    def st(t):  # straight-through bf16 rounding (the kernels round conv outputs)
+        return t + (t.to(torch.bfloat16).float() - t).detach()
+    xr = x.detach().float().requires_grad_(True)
+    w1r = w1.detach().to(torch.bfloat16).float().requires_grad_(True)
+    w2r = w2.detach().to(torch.bfloat16).float().requires_grad_(True)
+    y1 = st(F.conv2d(xr, w1r, padding=1)).relu()
+    y1 = st(y1)
+    yr = xr + st(F.conv2d(y1, w2r, padding=1)).relu()
+    (yr * gy).sum().backward()
+    _close(y, yr)
+    for a, b in ((x.grad, xr.grad), (w1.grad, w1r.grad), (w2.grad, w2r.grad)):
+        rel = (a.float() - b).norm() / b.norm()
+        assert rel < 2e-2, rel.item()
+
+
 def test_resnet9_native_matches_miopen():
     from commefficient_amd.models import ResNet9
     torch.manual_seed(0)
