@@ -159,22 +159,30 @@ def test_residual_unit_matches_fp32(N, C, H):
         assert rel < 2e-2, rel.item()
 
 
-def test_resnet9_native_matches_miopen():
+def test_resnet9_native_as_accurate_as_miopen():
+    """Whole ResNet-9 fwd+bwd: the native bf16 path must be as close to an
+    fp32 run as MIOpen's bf16 path is (bf16 noise grows towards the input
+    layers, ~15% on the prep conv for both; measured per-layer in
+    scripts/dev/cmp_resnet9_grads.py)."""
     from commefficient_amd.models import ResNet9
     torch.manual_seed(0)
     m = ResNet9().cuda()
     x = _nhwc(torch.randn(16, 3, 32, 32, device="cuda"))
     out = {}
-    for backend in ("miopen", "native"):
-        cnn.set_conv_backend(backend)
+    for backend in ("fp32", "miopen", "native"):
+        cnn.set_conv_backend("miopen" if backend == "fp32" else backend)
         m.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = m(x.to(torch.bfloat16))
+        if backend == "fp32":
+            y = m(x)
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = m(x.to(torch.bfloat16))
         y.float().square().sum().backward()
-        out[backend] = (y.float().detach(), [p.grad.detach().clone() for p in m.parameters()])
+        out[backend] = (y.float().detach(), [p.grad.detach().float().clone() for p in m.parameters()])
     cnn.set_conv_backend("native")
-    (ya, ga), (yb, gb) = out["miopen"], out["native"]
-    _close(yb, ya, rel=3e-2)
-    for a, b in zip(ga, gb):
-        rel = (a - b).norm() / a.norm().clamp_min(1e-12)
-        assert rel < 5e-2, rel.item()
+    (yr, gr), (ya, ga), (yb, gb) = out["fp32"], out["miopen"], out["native"]
+    _close(yb, yr, rel=3e-2)
+    for r, a, b in zip(gr, ga, gb):
+        ea = ((a - r).norm() / r.norm()).item()
+        eb = ((b - r).norm() / r.norm()).item()
+        assert eb < 1.25 * ea + 5e-3, (eb, ea)
