@@ -41,6 +41,8 @@ def main():
     p.add_argument("--conv", default="native", choices=["native", "miopen"],
                    help="3x3 conv units on the native MFMA kernels or on MIOpen")
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
+    p.add_argument("--torch-profile", default=None,
+                   help="after the timed steps, trace 5 more with torch.profiler into this dir")
     p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "1")),
                    help="torch.backends.cudnn.benchmark (MIOpen exhaustive find during warmup)")
     b = p.parse_args()
@@ -113,12 +115,28 @@ def main():
         fed.timer.totals.clear()
         fed.timer.counts.clear()
     t0 = time.perf_counter()
+    host_s = 0.0  # host time spent enqueueing (no syncs inside a round)
     for i in range(b.warmup, b.warmup + b.steps):
+        h0 = time.perf_counter()
         out = step(i)
+        host_s += time.perf_counter() - h0
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if b.torch_profile:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for i in range(b.warmup, b.warmup + min(b.steps, 5)):
+                step(i)
+            torch.cuda.synchronize()
+        if ctx.is_main:
+            os.makedirs(b.torch_profile, exist_ok=True)
+            prof.export_chrome_trace(os.path.join(b.torch_profile, "bench_trace.json"))
+            with open(os.path.join(b.torch_profile, "bench_ops.txt"), "w") as f:
+                f.write(prof.key_averages().table(sort_by="cpu_time_total", row_limit=60))
+                f.write("\n")
+                f.write(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=60))
     elapsed = dist.max_over_ranks(t1 - t0)
     last_loss = float(out[0].mean().item())
     dl = (float(fed.accountant.client_download.sum().item()) - dl_before) / b.steps
@@ -146,6 +164,7 @@ def main():
                                "wire_per_rank_ring": wire},
             "loss_first": round(first_loss, 4), "loss_last": round(last_loss, 4),
             "phase_ms": {k: round(v, 3) for k, v in phases.items()},
+            "host_enqueue_ms_per_step": round(host_s / b.steps * 1000.0, 3),
         }), flush=True)
     dist.barrier()
     dist.shutdown()
