@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..parallel.dist import h2d
 from ..parallel.fed_model import RoundBatch
 from .fed_dataset import FedSampler
 
@@ -47,7 +48,7 @@ class DeviceImageSource:
             host = np.stack([host, np.asarray(keys, dtype=np.int64)])
         t = torch.from_numpy(host)
         if self.device.type == "cuda":
-            t = t.pin_memory().to(self.device, non_blocking=True)
+            t = h2d(t, self.device)
         idx, kt = (t[0], t[1]) if keys is not None else (t, None)
         x = ops.augment_u8_nhwc(self.data, idx, self.pad, self.flip, self.mean, self.inv_std,
                                 seed, self.out_bf16, kt)

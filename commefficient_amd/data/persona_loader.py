@@ -12,12 +12,8 @@ from .fed_persona import collate
 
 
 def _to_dev(ts, device):
-    out = []
-    for t in ts:
-        if torch.device(device).type == "cuda":
-            t = t.pin_memory().to(device, non_blocking=True)
-        out.append(t)
-    return out
+    from ..parallel.dist import h2d
+    return [h2d(t, device) if torch.device(device).type == "cuda" else t for t in ts]
 
 
 class PersonaFedLoader:

@@ -75,18 +75,60 @@ def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> 
     return _CTX
 
 
+class _PinnedRing:
+    """Persistent pinned staging buffers for small per-round H2D copies.
+
+    ``tensor.pin_memory()`` per call goes through the caching host allocator,
+    which falls back to a fresh (device-synchronising) pinned allocation
+    whenever its cached blocks still have pending copies -- that kept the
+    host in lockstep with the GPU every round.  A ring of fixed slots, each
+    guarded by an event recorded after its copy, never allocates: by the time
+    a slot comes round again its copy has long completed."""
+
+    def __init__(self, slots: int = 32, slot_bytes: int = 1 << 20):
+        self.slots = slots
+        self.slot_bytes = slot_bytes
+        self.bufs = None
+        self.events = None
+        self.i = 0
+
+    def copy(self, t: torch.Tensor, device) -> torch.Tensor:
+        nbytes = t.numel() * t.element_size()
+        if nbytes > self.slot_bytes:
+            return t.pin_memory().to(device, non_blocking=True)
+        if self.bufs is None:
+            self.bufs = [torch.empty(self.slot_bytes, dtype=torch.uint8, pin_memory=True)
+                         for _ in range(self.slots)]
+            self.events = [None] * self.slots
+        k = self.i
+        self.i = (self.i + 1) % self.slots
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        stage = self.bufs[k][:nbytes].view(t.dtype).view(t.shape)
+        stage.copy_(t)
+        out = torch.empty(t.shape, dtype=t.dtype, device=device)
+        out.copy_(stage, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        return out
+
+
+_RING = _PinnedRing()
+
+
 def h2d(x, device, dtype=None) -> torch.Tensor:
     """Host array / CPU tensor -> ``device`` without a stream sync: a pageable
     ``.to(device)`` waits for every kernel queued before it (the GPU then
     idles while the host enqueues the rest of the round), so stage through
-    pinned memory and copy asynchronously on the current stream."""
+    a persistent pinned ring and copy asynchronously on the current stream."""
     t = x if torch.is_tensor(x) else torch.from_numpy(np.ascontiguousarray(x))
     if dtype is not None and t.dtype != dtype:
         t = t.to(dtype)
     device = torch.device(device)
     if device.type != "cuda":
         return t.to(device)
-    return t.pin_memory().to(device, non_blocking=True)
+    return _RING.copy(t.contiguous(), device)
 
 
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:
