@@ -649,6 +649,26 @@ at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
   return conv3x3_fwd_impl(x, w, relu, mask, addend, nullptr);
 }
 
+// fused per-example cross-entropy: (loss f32 [B], correct f32 [B], softmax - onehot [B, C])
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ce_fwd_hip(const at::Tensor& logits,
+                                                          const at::Tensor& targets) {
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous() &&
+                  (logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat),
+              "ce_fwd: logits must be contiguous bf16/f32 [B, C]");
+  TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous() &&
+                  targets.numel() == logits.size(0),
+              "ce_fwd: targets must be contiguous int64 [B]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  const int64_t B = logits.size(0);
+  auto loss = at::empty({B}, logits.options().dtype(at::kFloat));
+  auto correct = at::empty({B}, logits.options().dtype(at::kFloat));
+  auto grad = at::empty_like(logits);
+  launch_ce_fwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16,
+                targets.data_ptr<int64_t>(), B, static_cast<int>(logits.size(1)),
+                loss.data_ptr<float>(), correct.data_ptr<float>(), grad.data_ptr(), cur_stream());
+  return {loss, correct, grad};
+}
+
 // residual unit tail: out = relu(conv3x3(x, w)) + addend, and pre = relu(conv3x3(x, w))
 std::tuple<at::Tensor, at::Tensor> conv3x3_relu_add_hip(const at::Tensor& x, const at::Tensor& w,
                                                         const at::Tensor& addend) {
@@ -658,7 +678,29 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_relu_add_hip(const at::Tensor& x, con
 }
 
 // dw [K][C][3][3] fp32 = sum_p dy[p, k] x[p + (r-1, s-1), c]
+void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits, at::Tensor& dw,
+                       float beta);
+
 at::Tensor conv3x3_wgrad_hip(const at::Tensor& dy, const at::Tensor& x, int64_t splits) {
+  auto dw = at::empty({dy.size(1), x.size(1), 3, 3},
+                      x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
+  conv3x3_wgrad_run(dy, x, splits, dw, 0.f);
+  return dw;
+}
+
+// dw += wgrad (accumulate straight into an existing fp32 gradient, e.g. a
+// view of the flat gradient buffer: no separate AccumulateGrad pass)
+void conv3x3_wgrad_into_hip(const at::Tensor& dy, const at::Tensor& x, at::Tensor dw,
+                            int64_t splits) {
+  check_f32(dw, "conv3x3_wgrad_into: dw");
+  TORCH_CHECK(dw.dim() == 4 && dw.size(0) == dy.size(1) && dw.size(1) == x.size(1) &&
+                  dw.size(2) == 3 && dw.size(3) == 3,
+              "conv3x3_wgrad_into: dw must be [K, C, 3, 3]");
+  conv3x3_wgrad_run(dy, x, splits, dw, 1.f);
+}
+
+void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits, at::Tensor& dw,
+                       float beta) {
   check_nhwc_bf16(dy, "conv3x3_wgrad: dy");
   check_nhwc_bf16(x, "conv3x3_wgrad: x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
@@ -668,7 +710,6 @@ at::Tensor conv3x3_wgrad_hip(const at::Tensor& dy, const at::Tensor& x, int64_t 
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int P = static_cast<int>(N * H * W);
   if (splits <= 0) splits = conv3x3_wgrad_splits(P, static_cast<int>(K), static_cast<int>(C));
-  auto dw = at::empty({K, C, 3, 3}, x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
   auto slab = at::empty({splits * K * 9 * C}, dw.options());
   ConvWgradArgs a;
   a.dy = bf16_ptr(dy);
@@ -680,8 +721,7 @@ at::Tensor conv3x3_wgrad_hip(const at::Tensor& dy, const at::Tensor& x, int64_t 
   a.C = static_cast<int>(C);
   a.K = static_cast<int>(K);
   a.splits = static_cast<int>(splits);
-  launch_conv3x3_wgrad(a, dw.data_ptr<float>(), 0.f, cur_stream());
-  return dw;
+  launch_conv3x3_wgrad(a, dw.data_ptr<float>(), beta, cur_stream());
 }
 
 // w fp32 [K][C][3][3] -> (wf bf16 [K][3][3][C], wt bf16 [C][3][3][K] flipped)
@@ -756,7 +796,9 @@ TORCH_LIBRARY(commeff, m) {
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
   m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
+  m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
+  m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("relu_mask(Tensor gy, Tensor y) -> Tensor");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
@@ -816,7 +858,9 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("conv3x3_fwd", &conv3x3_fwd_hip);
   m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
+  m.impl("ce_fwd", &ce_fwd_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
+  m.impl("conv3x3_wgrad_into", &conv3x3_wgrad_into_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);
   m.impl("relu_mask", &relu_mask_hip);
   m.impl("cs_zero_buckets", &cs_zero_buckets_hip);

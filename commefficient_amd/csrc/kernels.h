@@ -165,6 +165,12 @@ void launch_conv_weight_prep(const float* w, uint16_t* wf, uint16_t* wt, int K, 
 void launch_relu_mask(const uint16_t* gy, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream);
 
+// ----------------------------------------------------------------- loss --
+// per-example cross-entropy of logits [B, C] (bf16 or f32): loss, top-1
+// correctness and the unit gradient softmax - onehot (logits dtype)
+void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
+                   float* correct, void* grad, hipStream_t stream);
+
 // ----------------------------------------------------------------- pool --
 // y = maxpool_k(relu(x)) on NHWC bf16 (C % 8 == 0, H, W % k == 0), k in {2, 4};
 // idx = window position of the max (255: max <= 0, gradient 0)

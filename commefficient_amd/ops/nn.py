@@ -56,6 +56,19 @@ def conv_backend() -> str:
     return _CONV_BACKEND[0]
 
 
+def _wgrad_to(g: torch.Tensor, x: torch.Tensor, weight: torch.Tensor):
+    """Weight gradient of a native conv.  When ``weight.grad`` already exists
+    (FedModel keeps every .grad as a view of its flat gradient buffer) the
+    split-K reduction accumulates straight into it and None is handed back to
+    autograd -- no separate dW tensor and no AccumulateGrad add pass."""
+    gr = weight.grad
+    if (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
+            and gr.device == g.device and tuple(gr.shape) == tuple(weight.shape)):
+        _ops().conv3x3_wgrad_into(g, x, gr)
+        return None
+    return _ops().conv3x3_wgrad(g, x)
+
+
 class _Conv3x3Act(torch.autograd.Function):
     """relu(conv3x3(x, w)) or maxpool_k(relu(conv3x3(x, w))), no bias.
 
@@ -78,6 +91,7 @@ class _Conv3x3Act(torch.autograd.Function):
             out = _ops().conv3x3_fwd(x, wf, True)
             ctx.save_for_backward(x, wt, out)
         ctx.pool_k = pool_k
+        ctx.weight = weight
         return out
 
     @staticmethod
@@ -89,7 +103,7 @@ class _Conv3x3Act(torch.autograd.Function):
         else:
             g = _ops().relu_mask(gout, aux)
         gx = _ops().conv3x3_fwd(g, wt, False) if ctx.needs_input_grad[0] else None
-        gw = _ops().conv3x3_wgrad(g, x) if ctx.needs_input_grad[1] else None
+        gw = _wgrad_to(g, x, ctx.weight) if ctx.needs_input_grad[1] else None
         return gx, gw, None
 
 
@@ -112,6 +126,7 @@ class _ResidualUnit(torch.autograd.Function):
         y1 = _ops().conv3x3_fwd(x, w1f, True)
         out, y2 = _ops().conv3x3_relu_add(y1, w2f, x)
         ctx.save_for_backward(x, y1, y2, w1t, w2t)
+        ctx.w1, ctx.w2 = w1, w2
         return out
 
     @staticmethod
@@ -120,9 +135,9 @@ class _ResidualUnit(torch.autograd.Function):
         g = g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         g2 = _ops().relu_mask(g, y2)
         g1 = _ops().conv3x3_fwd(g2, w2t, False, y1)  # masked by relu(conv1) > 0
-        dw2 = _ops().conv3x3_wgrad(g2, y1) if ctx.needs_input_grad[2] else None
+        dw2 = _wgrad_to(g2, y1, ctx.w2) if ctx.needs_input_grad[2] else None
         gx = _ops().conv3x3_fwd(g1, w1t, False, None, g) if ctx.needs_input_grad[0] else None
-        dw1 = _ops().conv3x3_wgrad(g1, x) if ctx.needs_input_grad[1] else None
+        dw1 = _wgrad_to(g1, x, ctx.w1) if ctx.needs_input_grad[1] else None
         return gx, dw1, dw2
 
 
@@ -151,3 +166,31 @@ def conv3x3_relu_pool(x: torch.Tensor, weight: torch.Tensor, pool_k: int = 0) ->
         return _Conv3x3Act.apply(x, weight, int(pool_k))
     y = F.conv2d(x, weight, padding=1)
     return relu_maxpool(y, pool_k) if pool_k else F.relu(y)
+
+
+# ------------------------------------------------------------ loss
+class _FusedCE(torch.autograd.Function):
+    """Per-example cross-entropy + top-1 correctness in one kernel
+    (csrc/loss.hip); the unit gradient softmax - onehot is produced in the
+    same pass and scaled by dL/dloss in backward."""
+
+    @staticmethod
+    def forward(ctx, logits, targets):
+        loss, correct, gunit = _ops().ce_fwd(logits.contiguous(), targets.contiguous())
+        ctx.save_for_backward(gunit)
+        ctx.mark_non_differentiable(correct)
+        return loss, correct
+
+    @staticmethod
+    def backward(ctx, gl, gc):
+        (gunit,) = ctx.saved_tensors
+        return gunit * gl.unsqueeze(1).to(gunit.dtype), None
+
+
+def cross_entropy_correct(logits: torch.Tensor, targets: torch.Tensor):
+    """(per-example CE loss f32, top-1 correct f32) of ``logits`` [B, C]."""
+    if (logits.is_cuda and logits.dim() == 2 and targets.dtype == torch.int64
+            and logits.dtype in (torch.bfloat16, torch.float32)):
+        return _FusedCE.apply(logits, targets)
+    per_ex = F.cross_entropy(logits.float(), targets, reduction="none")
+    return per_ex, (logits.argmax(dim=1) == targets).float()

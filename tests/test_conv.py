@@ -131,6 +131,22 @@ def test_conv_unit_autograd_matches_fp32(N, C, H, W, K, pool_k):
         assert rel < 2e-2, rel.item()
 
 
+def test_wgrad_accumulates_into_existing_grad():
+    """An existing .grad (FedModel's flat-buffer views) receives += dW in place."""
+    x, w = _inputs(2, 128, 8, 8, 128)
+    w = w.detach().requires_grad_(True)
+    w.grad = torch.full_like(w, 0.5)
+    keep = w.grad
+    cnn.set_conv_backend("native")
+    y = cnn.conv3x3_relu_pool(x, w, 0)
+    gy = torch.randn(y.shape, device="cuda")
+    (y.float() * gy).sum().backward()
+    w2 = w.detach().clone().requires_grad_(True)
+    (cnn.conv3x3_relu_pool(x, w2, 0).float() * gy).sum().backward()
+    assert w.grad is keep  # same storage, accumulated in place
+    torch.testing.assert_close(w.grad, 0.5 + w2.grad, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("N,C,H", [(4, 128, 16), (3, 512, 4)])
 def test_residual_unit_matches_fp32(N, C, H):
     x, w1 = _inputs(N, C, H, H, C)
@@ -186,3 +202,21 @@ def test_resnet9_native_as_accurate_as_miopen():
         ea = ((a - r).norm() / r.norm()).item()
         eb = ((b - r).norm() / r.norm()).item()
         assert eb < 1.25 * ea + 5e-3, (eb, ea)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,C", [(500, 10), (37, 100), (8, 1000)])
+def test_fused_cross_entropy_matches_torch(dtype, B, C):
+    g = torch.Generator(device="cuda").manual_seed(11)
+    logits = (torch.randn(B, C, device="cuda", generator=g) * 3).to(dtype).requires_grad_(True)
+    t = torch.randint(0, C, (B,), device="cuda", generator=g)
+    loss, correct = cnn.cross_entropy_correct(logits, t)
+    w = torch.rand(B, device="cuda", generator=g)
+    (loss * w).sum().backward()
+    l2 = logits.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(l2, t, reduction="none")
+    (ref * w).sum().backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+    assert torch.equal(correct, (logits.detach().argmax(1) == t).float())
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(logits.grad.float(), l2.grad, rtol=tol, atol=tol)
