@@ -562,6 +562,8 @@ std::tuple<at::Tensor, at::Tensor> relu_maxpool_hip(const at::Tensor& x, int64_t
   TORCH_CHECK(k == 2 || k == 4, "k must be 2 or 4");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   TORCH_CHECK(C % 8 == 0 && H % k == 0 && W % k == 0, "relu_maxpool: C%8, H%k, W%k");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 32) && x.size(0) * H * W < (int64_t(1) << 31),
+              "relu_maxpool: 32-bit index range");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty({N, C, H / k, W / k}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto idx = at::empty({N, C, H / k, W / k},
@@ -725,17 +727,37 @@ void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits
 }
 
 // w fp32 [K][C][3][3] -> (wf bf16 [K][3][3][C], wt bf16 [C][3][3][K] flipped)
+std::vector<at::Tensor> conv_weight_prep_multi_hip(at::TensorList ws) {
+  TORCH_CHECK(!ws.empty(), "conv_weight_prep: no weights");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(ws[0].device());
+  std::vector<at::Tensor> out;
+  ConvPrepBatch b{};
+  b.n = 0;
+  auto flush = [&]() {
+    if (b.n > 0) launch_conv_weight_prep(b, cur_stream());
+    b.n = 0;
+  };
+  for (const auto& w : ws) {
+    check_f32(w, "conv_weight_prep: w");
+    TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "conv_weight_prep: [K, C, 3, 3]");
+    TORCH_CHECK(w.device() == ws[0].device(), "conv_weight_prep: one device");
+    const int64_t K = w.size(0), C = w.size(1);
+    auto wf = at::empty({K, 3, 3, C}, w.options().dtype(at::kBFloat16));
+    auto wt = at::empty({C, 3, 3, K}, w.options().dtype(at::kBFloat16));
+    if (b.n == kPrepMax) flush();
+    b.t[b.n++] = ConvPrepItem{w.data_ptr<float>(), reinterpret_cast<uint16_t*>(wf.data_ptr()),
+                              reinterpret_cast<uint16_t*>(wt.data_ptr()), static_cast<int>(K),
+                              static_cast<int>(C), 0};
+    out.push_back(wf);
+    out.push_back(wt);
+  }
+  flush();
+  return out;
+}
+
 std::tuple<at::Tensor, at::Tensor> conv_weight_prep_hip(const at::Tensor& w) {
-  check_f32(w, "conv_weight_prep: w");
-  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "conv_weight_prep: [K, C, 3, 3]");
-  const int64_t K = w.size(0), C = w.size(1);
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
-  auto wf = at::empty({K, 3, 3, C}, w.options().dtype(at::kBFloat16));
-  auto wt = at::empty({C, 3, 3, K}, w.options().dtype(at::kBFloat16));
-  launch_conv_weight_prep(w.data_ptr<float>(), reinterpret_cast<uint16_t*>(wf.data_ptr()),
-                          reinterpret_cast<uint16_t*>(wt.data_ptr()), static_cast<int>(K),
-                          static_cast<int>(C), cur_stream());
-  return {wf, wt};
+  auto r = conv_weight_prep_multi_hip({w});
+  return {r[0], r[1]};
 }
 
 at::Tensor relu_mask_hip(const at::Tensor& gy, const at::Tensor& y) {
@@ -800,6 +822,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
+  m.def("conv_weight_prep_multi(Tensor[] ws) -> Tensor[]");
   m.def("relu_mask(Tensor gy, Tensor y) -> Tensor");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
         "int d) -> Tensor");
@@ -862,6 +885,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
   m.impl("conv3x3_wgrad_into", &conv3x3_wgrad_into_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);
+  m.impl("conv_weight_prep_multi", &conv_weight_prep_multi_hip);
   m.impl("relu_mask", &relu_mask_hip);
   m.impl("cs_zero_buckets", &cs_zero_buckets_hip);
   m.impl("cs_l2estimate", &cs_l2estimate_hip);

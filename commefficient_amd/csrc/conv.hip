@@ -480,51 +480,88 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 // dw[k][c][r][s] (fp32, PyTorch layout) = beta*dw + sum_split slab[split][k][rs][c]
-// (4 consecutive c per thread, fixed summation order)
+// One block per (k, 64 channels).  Thread (c, part) sums the 9 taps of its
+// channel over splits part, part+4, ... (9 independent loads per split, read
+// along c: coalesced); the 4 partial sums are combined in a fixed order
+// (deterministic) and transposed in LDS, so dw is written as one contiguous
+// run of 576 floats.
 __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __restrict__ slab,
                                                                  float* __restrict__ dw, int K, int C,
                                                                  int splits, float beta) {
-  const size_t n = static_cast<size_t>(K) * 9 * C;
-  const size_t n4 = n / 4;
-  for (size_t i4 = blockIdx.x * 256ull + threadIdx.x; i4 < n4; i4 += static_cast<size_t>(gridDim.x) * 256) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4* src = reinterpret_cast<const float4*>(slab) + i4;
-#pragma unroll 8
-    for (int t = 0; t < splits; ++t) {
-      const float4 v = src[t * n4];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    const size_t i = i4 * 4;
-    const int c = static_cast<int>(i % C);
-    const size_t kr = i / C;
-    const int rs = static_cast<int>(kr % 9);
-    const size_t k = kr / 9;
-    float* o = dw + (k * C + c) * 9 + rs;
-    const float sv[4] = {s.x, s.y, s.z, s.w};
+  __shared__ float t[4][64 * 9];
+  const int ncb = C >> 6;
+  const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
+  const int cc = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const size_t sstride = static_cast<size_t>(K) * 9 * C;
+  const float* src = slab + static_cast<size_t>(k) * 9 * C + c0 + cc;
+  float acc[9];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[9 * j] = beta != 0.f ? beta * o[9 * j] + sv[j] : sv[j];
+  for (int rs = 0; rs < 9; ++rs) acc[rs] = 0.f;
+#pragma unroll 2
+  for (int sp = part; sp < splits; sp += 4) {
+    const float* p = src + sp * sstride;
+#pragma unroll
+    for (int rs = 0; rs < 9; ++rs) acc[rs] += p[rs * C];
+  }
+#pragma unroll
+  for (int rs = 0; rs < 9; ++rs) t[part][cc * 9 + rs] = acc[rs];
+  __syncthreads();
+  float* o = dw + (static_cast<size_t>(k) * C + c0) * 9;
+  for (int e = threadIdx.x; e < 576; e += 256) {
+    const float v = ((t[0][e] + t[1][e]) + t[2][e]) + t[3][e];
+    o[e] = beta != 0.f ? beta * o[e] + v : v;
   }
 }
 
-// w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16 (flipped)
-__global__ void __launch_bounds__(256) conv_weight_prep_kernel(const float* __restrict__ w,
-                                                               __bf16* __restrict__ wf,
-                                                               __bf16* __restrict__ wt, int K, int C) {
-  // thread per OUTPUT element (coalesced 2-byte stores; the strided 4-byte
-  // reads of the small fp32 weight hit L2): [0, n) -> wf, [n, 2n) -> wt
-  const int n = K * C * 9;
-  for (int o = blockIdx.x * 256 + threadIdx.x; o < 2 * n; o += gridDim.x * 256) {
-    if (o < n) {
-      if (wf == nullptr) continue;
-      const int c = o % C, krs = o / C;           // wf[k][rs][c]
-      const int rs = krs % 9, k = krs / 9;
-      wf[o] = static_cast<__bf16>(w[(k * C + c) * 9 + rs]);
-    } else {
-      if (wt == nullptr) continue;
-      const int q = o - n;
-      const int k = q % K, crs = q / K;           // wt[c][rs'][k] = w[k][c][8 - rs']
-      const int rs = crs % 9, c = crs / 9;
-      wt[q] = static_cast<__bf16>(w[(k * C + c) * 9 + (8 - rs)]);
+// w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16
+// (flipped) for up to kPrepMax tensors in one launch.  A block transposes one
+// 32(k) x 32(c) x 9 tile through LDS: the fp32 rows w[k][c0:c0+32][:] are
+// 1152 contiguous bytes (coalesced reads), and both outputs are written as
+// runs of 32 bf16 (64 B) along their fastest axis.
+constexpr int kPT = 32;
+__global__ void __launch_bounds__(256) conv_weight_prep_kernel(ConvPrepBatch b) {
+  __shared__ float s[kPT][kPT * 9 + 1];  // [k][c*9 + rs], +1: odd row stride
+  // pick this block's tensor with compile-time indices only (a dynamically
+  // indexed by-value argument struct would be copied to scratch)
+  ConvPrepItem it = b.t[0];
+#pragma unroll
+  for (int i = 1; i < kPrepMax; ++i)
+    if (i < b.n && static_cast<int>(blockIdx.x) >= b.t[i].block0) it = b.t[i];
+  const int tile = blockIdx.x - it.block0;
+  const int ntc = (it.C + kPT - 1) / kPT;
+  const int k0 = (tile / ntc) * kPT, c0 = (tile % ntc) * kPT;
+  const int nk = min(kPT, it.K - k0), nc = min(kPT, it.C - c0);
+  const int row = nc * 9;
+  // all 36 loads of a thread in flight before the first LDS store
+  constexpr int PER = kPT * kPT * 9 / 256;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = i * 256 + threadIdx.x;
+    const int kk = e / (kPT * 9), j = e - kk * (kPT * 9);
+    v[i] = (kk < nk && j < row) ? it.w[(static_cast<size_t>(k0 + kk) * it.C + c0) * 9 + j] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = i * 256 + threadIdx.x;
+    const int kk = e / (kPT * 9), j = e - kk * (kPT * 9);
+    s[kk][j] = v[i];
+  }
+  __syncthreads();
+  if (it.wf != nullptr) {  // wf[k][rs][c]: lanes run along c
+    for (int e = threadIdx.x; e < kPT * 9 * kPT; e += 256) {
+      const int cc = e % kPT, krs = e / kPT, rs = krs % 9, kk = krs / 9;
+      if (kk < nk && cc < nc)
+        reinterpret_cast<__bf16*>(it.wf)[(static_cast<size_t>(k0 + kk) * 9 + rs) * it.C + c0 + cc] =
+            static_cast<__bf16>(s[kk][cc * 9 + rs]);
+    }
+  }
+  if (it.wt != nullptr) {  // wt[c][rs'][k] = w[k][c][8 - rs']: lanes run along k
+    for (int e = threadIdx.x; e < kPT * 9 * kPT; e += 256) {
+      const int kk = e % kPT, crs = e / kPT, rs = crs % 9, cc = crs / 9;
+      if (kk < nk && cc < nc)
+        reinterpret_cast<__bf16*>(it.wt)[(static_cast<size_t>(c0 + cc) * 9 + rs) * it.K + k0 + kk] =
+            static_cast<__bf16>(s[kk][cc * 9 + 8 - rs]);
     }
   }
 }
@@ -651,16 +688,18 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
   } else {
     if (wide) launch_wgrad<128, 2, false>(a, stream); else launch_wgrad<64, 2, false>(a, stream);
   }
-  const int64_t n4 = static_cast<int64_t>(a.K) * 9 * a.C / 4;
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, stream,
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(a.K * (a.C / 64)), dim3(256), 0, stream,
                      a.slab, dw, a.K, a.C, a.splits, beta);
 }
 
-void launch_conv_weight_prep(const float* w, uint16_t* wf, uint16_t* wt, int K, int C,
-                             hipStream_t stream) {
-  hipLaunchKernelGGL(conv_weight_prep_kernel, dim3(grid_for(static_cast<int64_t>(K) * C * 18, 256)),
-                     dim3(256), 0, stream, w, reinterpret_cast<__bf16*>(wf),
-                     reinterpret_cast<__bf16*>(wt), K, C);
+void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream) {
+  int blocks = 0;
+  for (int i = 0; i < b.n; ++i) {
+    b.t[i].block0 = blocks;
+    blocks += ((b.t[i].K + kPT - 1) / kPT) * ((b.t[i].C + kPT - 1) / kPT);
+  }
+  if (blocks == 0) return;
+  hipLaunchKernelGGL(conv_weight_prep_kernel, dim3(blocks), dim3(256), 0, stream, b);
 }
 
 void launch_relu_mask(const uint16_t* gy, const uint16_t* y, uint16_t* g, int64_t n,

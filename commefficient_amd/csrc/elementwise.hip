@@ -103,16 +103,32 @@ count_ge_kernel(const int32_t* __restrict__ last_mod, int64_t n, const int32_t* 
   for (int t = threadIdx.x; t <= T; t += blockDim.x) h[t] = 0;
   for (int t = threadIdx.x; t < T; t += blockDim.x) th[t] = thr[t];
   __syncthreads();
+  // wave-aggregated histogram: most elements of a wave land in a few hot
+  // bins, so one LDS atomic per distinct bin per wave (per-lane atomics on a
+  // hot bin serialise)
+  const int lane = threadIdx.x & 63;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
-    int v = last_mod[i];
-    // number of thresholds <= v
-    int lo = 0, hi = T;
-    while (lo < hi) {
-      int mid = (lo + hi) >> 1;
-      if (th[mid] <= v) lo = mid + 1; else hi = mid;
+  for (int64_t base = blockIdx.x * static_cast<int64_t>(blockDim.x); base < n; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    int bin = 0;
+    if (i < n) {
+      const int v = last_mod[i];
+      // number of thresholds <= v
+      int lo = 0, hi = T;
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (th[mid] <= v) lo = mid + 1; else hi = mid;
+      }
+      bin = lo;
     }
-    if (lo > 0) atomicAdd(h + lo, 1u);
+    unsigned long long pending = __ballot(bin > 0);
+    while (pending) {  // wave-uniform
+      const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+      const int b = __shfl(bin, leader);
+      const unsigned long long same = __ballot(bin == b) & pending;
+      if (lane == leader) atomicAdd(h + b, static_cast<unsigned>(__popcll(same)));
+      pending &= ~same;
+    }
   }
   __syncthreads();
   for (int t = threadIdx.x + 1; t <= T; t += blockDim.x)

@@ -158,9 +158,21 @@ int conv3x3_wgrad_splits(int P, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 (either output optional) and
-// wt [C][3][3][K] bf16 spatially flipped (the dgrad weight)
-void launch_conv_weight_prep(const float* w, uint16_t* wf, uint16_t* wt, int K, int C,
-                             hipStream_t stream);
+// wt [C][3][3][K] bf16 spatially flipped (the dgrad weight), for up to
+// kPrepMax weights in one launch
+constexpr int kPrepMax = 16;
+struct ConvPrepItem {
+  const float* w;
+  uint16_t* wf;  // bf16
+  uint16_t* wt;
+  int K, C;
+  int block0;  // set by the launcher
+};
+struct ConvPrepBatch {
+  ConvPrepItem t[kPrepMax];
+  int n;
+};
+void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream);
 // g = gy where y > 0 else 0 (bf16, n % 8 == 0)
 void launch_relu_mask(const uint16_t* gy, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream);

@@ -30,21 +30,33 @@ struct alignas(16) V8 {
   bf16raw h[8];
 };
 
+// index math: 32-bit with precomputed reciprocals (64-bit div/mod is a long
+// software sequence per thread and made these kernels VALU-bound)
+struct PoolGeom {
+  int H, W, C, OH, OW, C8;
+  uint32_t total;
+  FastDivU32 d_c8, d_ow, d_oh;
+};
+
+__device__ __forceinline__ void pool_coords(uint32_t g, const PoolGeom& q, uint32_t& c8, uint32_t& ow,
+                                            uint32_t& oh, uint32_t& n) {
+  uint32_t p = fdiv(g, q.d_c8);
+  c8 = g - p * q.C8;
+  uint32_t p2 = fdiv(p, q.d_ow);
+  ow = p - p2 * q.OW;
+  n = fdiv(p2, q.d_oh);
+  oh = p2 - n * q.OH;
+}
+
 template <int K>
 __global__ void __launch_bounds__(256)
 relu_maxpool_fwd_kernel(const bf16raw* __restrict__ x, bf16raw* __restrict__ y,
-                        uint8_t* __restrict__ idx, int N, int H, int W, int C) {
-  const int OH = H / K, OW = W / K, C8 = C / 8;
-  const int64_t total = static_cast<int64_t>(N) * OH * OW * C8;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t g = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; g < total;
-       g += stride) {
-    const int c8 = static_cast<int>(g % C8);
-    int64_t p = g / C8;  // output pixel
-    const int ow = static_cast<int>(p % OW);
-    p /= OW;
-    const int oh = static_cast<int>(p % OH);
-    const int64_t n = p / OH;
+                        uint8_t* __restrict__ idx, PoolGeom q) {
+  const int H = q.H, W = q.W, C = q.C;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += stride) {
+    uint32_t c8, ow, oh, n;
+    pool_coords(g, q, c8, ow, oh, n);
     float best[8];
     uint8_t arg[8];
 #pragma unroll
@@ -56,7 +68,7 @@ relu_maxpool_fwd_kernel(const bf16raw* __restrict__ x, bf16raw* __restrict__ y,
     for (int dy = 0; dy < K; ++dy) {
 #pragma unroll
       for (int dx = 0; dx < K; ++dx) {
-        const int64_t off = (((n * H + oh * K + dy) * W + ow * K + dx) * C) + c8 * 8;
+        const size_t off = static_cast<size_t>((n * H + oh * K + dy) * W + ow * K + dx) * C + c8 * 8;
         V8 v = *reinterpret_cast<const V8*>(x + off);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -77,7 +89,7 @@ relu_maxpool_fwd_kernel(const bf16raw* __restrict__ x, bf16raw* __restrict__ y,
       o.h[q] = pos ? static_cast<bf16raw>(__float_as_uint(best[q]) >> 16) : static_cast<bf16raw>(0);
       codes |= static_cast<uint64_t>(pos ? arg[q] : 255u) << (8 * q);
     }
-    const int64_t oo = g * 8;  // == ((n*OH+oh)*OW+ow)*C + c8*8
+    const size_t oo = static_cast<size_t>(g) * 8;  // == ((n*OH+oh)*OW+ow)*C + c8*8
     *reinterpret_cast<V8*>(y + oo) = o;
     *reinterpret_cast<uint64_t*>(idx + oo) = codes;
   }
@@ -86,20 +98,14 @@ relu_maxpool_fwd_kernel(const bf16raw* __restrict__ x, bf16raw* __restrict__ y,
 template <int K>
 __global__ void __launch_bounds__(256)
 relu_maxpool_bwd_kernel(const bf16raw* __restrict__ gy, const uint8_t* __restrict__ idx,
-                        bf16raw* __restrict__ gx, int N, int H, int W, int C) {
-  const int OH = H / K, OW = W / K, C8 = C / 8;
-  const int64_t total = static_cast<int64_t>(N) * OH * OW * C8;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t g = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; g < total;
-       g += stride) {
-    const int c8 = static_cast<int>(g % C8);
-    int64_t p = g / C8;
-    const int ow = static_cast<int>(p % OW);
-    p /= OW;
-    const int oh = static_cast<int>(p % OH);
-    const int64_t n = p / OH;
-    const V8 gv = *reinterpret_cast<const V8*>(gy + g * 8);
-    const uint64_t codes = *reinterpret_cast<const uint64_t*>(idx + g * 8);
+                        bf16raw* __restrict__ gx, PoolGeom q) {
+  const int H = q.H, W = q.W, C = q.C;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += stride) {
+    uint32_t c8, ow, oh, n;
+    pool_coords(g, q, c8, ow, oh, n);
+    const V8 gv = *reinterpret_cast<const V8*>(gy + static_cast<size_t>(g) * 8);
+    const uint64_t codes = *reinterpret_cast<const uint64_t*>(idx + static_cast<size_t>(g) * 8);
 #pragma unroll
     for (int dy = 0; dy < K; ++dy) {
 #pragma unroll
@@ -110,11 +116,22 @@ relu_maxpool_bwd_kernel(const bf16raw* __restrict__ gy, const uint8_t* __restric
           const uint32_t code = static_cast<uint32_t>(codes >> (8 * q)) & 0xffu;
           o.h[q] = code == static_cast<uint32_t>(dy * K + dx) ? gv.h[q] : static_cast<bf16raw>(0);
         }
-        const int64_t off = (((n * H + oh * K + dy) * W + ow * K + dx) * C) + c8 * 8;
+        const size_t off = static_cast<size_t>((n * H + oh * K + dy) * W + ow * K + dx) * C + c8 * 8;
         *reinterpret_cast<V8*>(gx + off) = o;
       }
     }
   }
+}
+
+PoolGeom make_pool_geom(int N, int H, int W, int C, int k) {
+  PoolGeom q;
+  q.H = H; q.W = W; q.C = C;
+  q.OH = H / k; q.OW = W / k; q.C8 = C / 8;
+  q.total = static_cast<uint32_t>(static_cast<int64_t>(N) * q.OH * q.OW * q.C8);
+  q.d_c8 = make_fastdiv(q.C8);
+  q.d_ow = make_fastdiv(q.OW);
+  q.d_oh = make_fastdiv(q.OH);
+  return q;
 }
 
 int grid_for(int64_t n) {
@@ -129,24 +146,26 @@ void launch_relu_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N
                              int C, int k, hipStream_t stream) {
   const int64_t total = static_cast<int64_t>(N) * (H / k) * (W / k) * (C / 8);
   if (total == 0) return;
+  const PoolGeom q = make_pool_geom(N, H, W, C, k);
   if (k == 2)
     hipLaunchKernelGGL(relu_maxpool_fwd_kernel<2>, dim3(grid_for(total)), dim3(256), 0, stream, x,
-                       y, idx, N, H, W, C);
+                       y, idx, q);
   else
     hipLaunchKernelGGL(relu_maxpool_fwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, stream, x,
-                       y, idx, N, H, W, C);
+                       y, idx, q);
 }
 
 void launch_relu_maxpool_bwd(const uint16_t* gy, const uint8_t* idx, uint16_t* gx, int N, int H,
                              int W, int C, int k, hipStream_t stream) {
   const int64_t total = static_cast<int64_t>(N) * (H / k) * (W / k) * (C / 8);
   if (total == 0) return;
+  const PoolGeom q = make_pool_geom(N, H, W, C, k);
   if (k == 2)
     hipLaunchKernelGGL(relu_maxpool_bwd_kernel<2>, dim3(grid_for(total)), dim3(256), 0, stream,
-                       gy, idx, gx, N, H, W, C);
+                       gy, idx, gx, q);
   else
     hipLaunchKernelGGL(relu_maxpool_bwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, stream,
-                       gy, idx, gx, N, H, W, C);
+                       gy, idx, gx, q);
 }
 
 }  // namespace commeff

@@ -21,7 +21,7 @@ import itertools
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import conv3x3_relu_pool, relu_maxpool, residual_unit
+from ..ops.nn import conv3x3_relu_pool, prepared_conv_weights, relu_maxpool, residual_unit
 from .common import GhostBatchNorm2d, Mul
 
 __all__ = ["ResNet9"]
@@ -109,11 +109,16 @@ class BasicNet(nn.Module):
         self.linear = nn.Linear(channels["layer3"], num_classes, bias=False)
         self.classifier = Mul(weight)
 
+    def conv_weights(self):
+        return [m.weight for m in self.modules() if isinstance(m, nn.Conv2d)]
+
     def forward(self, x):
-        x = self.prep(x)
-        x = self.res1(self.layer1(x))
-        x = self.layer2(x)
-        x = self.res3(self.layer3(x))
+        # every conv weight -> bf16 GEMM images in one launch (native path)
+        with prepared_conv_weights(self.conv_weights() if x.is_cuda else []):
+            x = self.prep(x)
+            x = self.res1(self.layer1(x))
+            x = self.layer2(x)
+            x = self.res3(self.layer3(x))
         # res3's output is >= 0 (relu'd input + relu'd branch), so relu is the
         # identity and the fused kernel computes exactly max_pool2d(x, 4)
         x = relu_maxpool(x, 4).flatten(1)

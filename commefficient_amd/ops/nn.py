@@ -56,6 +56,43 @@ def conv_backend() -> str:
     return _CONV_BACKEND[0]
 
 
+# bf16 GEMM images of conv weights prepared for the current forward pass
+# (one batched launch for the whole model, see prepared_conv_weights)
+_PREP: dict = {}
+
+
+class prepared_conv_weights:
+    """``with prepared_conv_weights(ws): model(x)`` -- converts every weight in
+    ``ws`` to its two bf16 GEMM images (forward [K,3,3,C] and flipped dgrad
+    [C,3,3,K]) in ONE kernel launch; the native conv units of this forward
+    pick them up instead of preparing their weight one by one."""
+
+    def __init__(self, weights):
+        self.weights = [w for w in weights if w.is_cuda and w.dtype == torch.float32
+                        and w.dim() == 4 and tuple(w.shape[2:]) == (3, 3)
+                        and w.shape[1] % 64 == 0]
+        self.keys = []
+
+    def __enter__(self):
+        if self.weights and _CONV_BACKEND[0] == "native":
+            out = _ops().conv_weight_prep_multi([w.detach() for w in self.weights])
+            for i, w in enumerate(self.weights):
+                key = (w.data_ptr(), w._version)
+                _PREP[key] = (out[2 * i], out[2 * i + 1])
+                self.keys.append(key)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.keys:
+            _PREP.pop(k, None)
+        return False
+
+
+def _prep(weight: torch.Tensor):
+    hit = _PREP.get((weight.data_ptr(), weight._version))
+    return hit if hit is not None else _ops().conv_weight_prep(weight.detach().contiguous())
+
+
 def _wgrad_to(g: torch.Tensor, x: torch.Tensor, weight: torch.Tensor):
     """Weight gradient of a native conv.  When ``weight.grad`` already exists
     (FedModel keeps every .grad as a view of its flat gradient buffer) the
@@ -81,7 +118,7 @@ class _Conv3x3Act(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, pool_k):
-        wf, wt = _ops().conv_weight_prep(weight.detach().contiguous())
+        wf, wt = _prep(weight)
         if pool_k:
             y = _ops().conv3x3_fwd(x, wf, False)
             out, idx = _ops().relu_maxpool(y, pool_k)
@@ -121,8 +158,8 @@ class _ResidualUnit(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, w2):
-        w1f, w1t = _ops().conv_weight_prep(w1.detach().contiguous())
-        w2f, w2t = _ops().conv_weight_prep(w2.detach().contiguous())
+        w1f, w1t = _prep(w1)
+        w2f, w2t = _prep(w2)
         y1 = _ops().conv3x3_fwd(x, w1f, True)
         out, y2 = _ops().conv3x3_relu_add(y1, w2f, x)
         ctx.save_for_backward(x, y1, y2, w1t, w2t)

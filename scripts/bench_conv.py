@@ -57,6 +57,15 @@ def main():
         r["wgrad_miopen_us"] = timeit(
             lambda: torch.ops.aten.convolution_backward(dy, x, wb, None, [1, 1], [1, 1], [1, 1],
                                                         False, [0, 0], 1, [False, True, False]))
+        # calibration: a plain hipBLASLt GEMM of the same M x N x K (no im2col)
+        ga = torch.randn(N * H * H, 9 * C, device="cuda").to(torch.bfloat16)
+        gb = torch.randn(9 * C, K, device="cuda").to(torch.bfloat16)
+        r["gemm_us"] = timeit(lambda: torch.mm(ga, gb))
+        r["gemm_tflops"] = round(flops / (r["gemm_us"] * 1e-6) / 1e12, 1)
+        gt = torch.randn(K, N * H * H, device="cuda").to(torch.bfloat16)
+        r["gemm_wgrad_us"] = timeit(lambda: torch.mm(gt, ga))
+        r["gemm_wgrad_tflops"] = round(flops / (r["gemm_wgrad_us"] * 1e-6) / 1e12, 1)
+        del ga, gb, gt
         for kind in ("fwd", "dgrad", "wgrad"):
             for be in ("native", "miopen"):
                 r[f"{kind}_{be}_tflops"] = round(flops / (r[f"{kind}_{be}_us"] * 1e-6) / 1e12, 1)

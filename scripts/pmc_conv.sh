@@ -10,4 +10,6 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT
   --output-format csv -d gpurun_out/pmc/$V.sq -o run -- python3 scripts/prof_conv.py "$@" > gpurun_out/pmc/$V.sq.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
   --output-format csv -d gpurun_out/pmc/$V.tcc -o run -- python3 scripts/prof_conv.py "$@" > gpurun_out/pmc/$V.tcc.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
+  --output-format csv -d gpurun_out/pmc/$V.mfma -o run -- python3 scripts/prof_conv.py "$@" > gpurun_out/pmc/$V.mfma.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/$V.kt -o run -- python3 scripts/prof_conv.py "$@" > gpurun_out/pmc/$V.kt.log 2>&1

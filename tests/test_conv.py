@@ -220,3 +220,20 @@ def test_fused_cross_entropy_matches_torch(dtype, B, C):
     assert torch.equal(correct, (logits.detach().argmax(1) == t).float())
     tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
     torch.testing.assert_close(logits.grad.float(), l2.grad, rtol=tol, atol=tol)
+
+
+def test_weight_prep_multi_matches_permutes():
+    g = torch.Generator(device="cuda").manual_seed(12)
+    shapes = [(128, 64), (40, 3), (512, 512), (64, 96), (33, 70)]
+    ws = [torch.randn(K, C, 3, 3, device="cuda", generator=g) for K, C in shapes]
+    from commefficient_amd._ext import ops as _ops
+    out = _ops().conv_weight_prep_multi(ws)
+    for i, w in enumerate(ws):
+        assert torch.equal(out[2 * i], w.permute(0, 2, 3, 1).to(torch.bfloat16))
+        assert torch.equal(out[2 * i + 1], w.flip(2, 3).permute(1, 2, 3, 0).to(torch.bfloat16))
+    # the model-level batched prep is what the native units use
+    w = ws[0].requires_grad_(True)
+    with cnn.prepared_conv_weights([w]):
+        wf, wt = cnn._prep(w)
+    assert torch.equal(wf, out[0]) and torch.equal(wt, out[1])
+    assert not cnn._PREP

@@ -288,3 +288,15 @@ def test_relu_maxpool_fused_matches_torch(shape, k):
     y.backward(g.to(torch.bfloat16))
     y2.backward(g)
     torch.testing.assert_close(x.grad.float(), x2.grad.float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_count_ge_random_matches_torch(device):
+    g = torch.Generator().manual_seed(5)
+    n = 300_001
+    lm = torch.randint(-1, 200, (n,), generator=g, dtype=torch.int32)
+    lm[: n // 2] = 7  # one hot bin (wave-aggregated path)
+    thr = torch.unique(torch.randint(-1, 210, (90,), generator=g, dtype=torch.int32))
+    cnt = ops.count_ge(lm.to(device), thr.to(device)).cpu()
+    exp = torch.stack([(lm >= t).sum() for t in thr])
+    assert cnt.tolist() == exp.tolist()
