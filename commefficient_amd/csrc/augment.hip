@@ -38,12 +38,14 @@ __device__ __forceinline__ uint16_t to_bf16(float f) {
   return *reinterpret_cast<uint16_t*>(&b);
 }
 
-// one thread per output pixel; C <= 4 channels
+// one thread per output pixel; C <= 4 channels, written with a pixel stride of
+// CS >= C channels (CS = 4 for 3-channel images: one 8-byte pixel, padding
+// channel = 0 -- the layout of the native input conv, conv_prep.hip)
 __global__ void __launch_bounds__(256)
 augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx, int64_t B,
                int H, int W, int C, int pad, int flip, const float* __restrict__ mean,
                const float* __restrict__ inv_std, uint64_t seed, const int64_t* __restrict__ keys,
-               uint16_t* __restrict__ out) {
+               uint16_t* __restrict__ out, int CS) {
   const int64_t npix = B * H * W;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   float m[4], s[4];
@@ -68,11 +70,12 @@ augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx
     int sy = reflect(y + dy - pad, H);
     int sx = reflect(xx + dx - pad, W);
     const uint8_t* src = data + ((idx[b] * H + sy) * W + sx) * C;
-    uint16_t* dst = out + p * C;
+    uint16_t* dst = out + p * CS;
     for (int ch = 0; ch < C; ++ch) {
       float v = static_cast<float>(src[ch]) * (1.f / 255.f);
       dst[ch] = to_bf16((v - m[ch]) * s[ch]);
     }
+    for (int ch = C; ch < CS; ++ch) dst[ch] = 0;
   }
 }
 
@@ -81,13 +84,14 @@ augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx
 void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx, int64_t B, int H, int W,
                             int C, int pad, int flip, const float* mean, const float* inv_std,
                             uint64_t seed, const int64_t* keys, uint16_t* out_bf16,
-                            hipStream_t stream) {
+                            int out_cstride, hipStream_t stream) {
   if (B <= 0) return;
   int64_t npix = B * H * W;
   int64_t blocks = (npix + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(augment_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
-                     data, idx, B, H, W, C, pad, flip, mean, inv_std, seed, keys, out_bf16);
+                     data, idx, B, H, W, C, pad, flip, mean, inv_std, seed, keys, out_bf16,
+                     out_cstride);
 }
 
 }  // namespace commeff

@@ -428,7 +428,10 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   TORCH_CHECK(data.size(3) <= 4, "at most 4 channels");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(data.device());
   const int64_t B = idx.numel(), H = data.size(1), W = data.size(2), C = data.size(3);
-  auto out = at::empty({B, H, W, C}, data.options().dtype(at::kBFloat16));
+  // 3-channel bf16 batches are stored with a 4-channel pixel stride (the native
+  // input conv reads one 8-byte load per tap); the result is a [B, C, H, W] view
+  const int64_t CS = (out_bf16 && C == 3) ? 4 : C;
+  auto out = at::empty({B, H, W, CS}, data.options().dtype(at::kBFloat16));
   auto mc = mean.to(data.device(), at::kFloat).contiguous();
   auto sc = inv_std.to(data.device(), at::kFloat).contiguous();
   auto ic = idx.contiguous();
@@ -436,8 +439,9 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
                          static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                          static_cast<int>(pad), flip ? 1 : 0, mc.data_ptr<float>(),
                          sc.data_ptr<float>(), static_cast<uint64_t>(seed), key_ptr(keys, B),
-                         reinterpret_cast<uint16_t*>(out.data_ptr()), cur_stream());
-  auto o = out.permute({0, 3, 1, 2});
+                         reinterpret_cast<uint16_t*>(out.data_ptr()), static_cast<int>(CS),
+                         cur_stream());
+  auto o = out.narrow(3, 0, C).permute({0, 3, 1, 2});
   return out_bf16 ? o : o.to(at::kFloat);
 }
 
@@ -760,6 +764,78 @@ std::tuple<at::Tensor, at::Tensor> conv_weight_prep_hip(const at::Tensor& w) {
   return {r[0], r[1]};
 }
 
+// ---- ResNet-9 input conv (conv_prep.hip)
+// x: [B, 3, H, W] bf16 view of a 4-channel-stride pixel buffer (the layout the
+// augmentation kernel writes)
+void check_prep_input(const at::Tensor& x) {
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3,
+              "conv_prep: x must be bf16 [B, 3, H, W]");
+  const int64_t H = x.size(2), W = x.size(3);
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(3) == 4 && x.stride(2) == 4 * W && x.stride(0) == 4 * H * W,
+              "conv_prep: x must have a 4-channel pixel stride (augment_u8_nhwc layout)");
+  TORCH_CHECK(x.storage_offset() + x.size(0) * H * W * 4 <= static_cast<int64_t>(x.storage().nbytes() / 2),
+              "conv_prep: x storage too small");
+  TORCH_CHECK(x.size(0) * H * W < (int64_t(1) << 31), "conv_prep: 32-bit pixel index");
+}
+
+ConvPrepArgs prep_args(const at::Tensor& x) {
+  ConvPrepArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.P = static_cast<int>(x.size(0) * x.size(2) * x.size(3));
+  a.H = static_cast<int>(x.size(2));
+  a.W = static_cast<int>(x.size(3));
+  a.Cin = static_cast<int>(x.size(1));
+  return a;
+}
+
+std::tuple<at::Tensor, at::Tensor> conv_prep_fwd_hip(const at::Tensor& x, const at::Tensor& w) {
+  check_prep_input(x);
+  check_f32(w, "conv_prep: w");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == x.size(1) && w.size(2) == 3 &&
+                  w.size(3) == 3, "conv_prep: w must be [64, 3, 3, 3]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
+  auto y = at::empty({B, 64, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto mask = at::empty({B * H * W, 2}, x.options().dtype(at::kInt));
+  ConvPrepArgs a = prep_args(x);
+  a.w = w.data_ptr<float>();
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.mask = reinterpret_cast<uint32_t*>(mask.data_ptr());
+  launch_conv_prep_fwd(a, cur_stream());
+  return {y, mask};
+}
+
+void conv_prep_wgrad_run(const at::Tensor& gy_in, const at::Tensor& mask, const at::Tensor& x,
+                         at::Tensor& dw, float beta) {
+  check_prep_input(x);
+  auto gy = gy_in.to(at::kBFloat16).contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(gy.dim() == 4 && gy.size(0) == B && gy.size(1) == 64 && gy.size(2) == H && gy.size(3) == W,
+              "conv_prep_wgrad: gy shape");
+  TORCH_CHECK(mask.scalar_type() == at::kInt && mask.is_contiguous() && mask.numel() == B * H * W * 2,
+              "conv_prep_wgrad: mask");
+  check_f32(dw, "conv_prep_wgrad: dw");
+  TORCH_CHECK(dw.numel() == 64 * x.size(1) * 9, "conv_prep_wgrad: dw shape");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  ConvPrepArgs a = prep_args(x);
+  auto partial = at::empty({conv_prep_wgrad_blocks(a.P), 64 * 64}, x.options().dtype(at::kFloat));
+  a.gy = reinterpret_cast<const uint16_t*>(gy.data_ptr());
+  a.mask_in = reinterpret_cast<const uint32_t*>(mask.data_ptr());
+  a.partial = partial.data_ptr<float>();
+  launch_conv_prep_wgrad(a, dw.data_ptr<float>(), beta, cur_stream());
+}
+
+at::Tensor conv_prep_wgrad_hip(const at::Tensor& gy, const at::Tensor& mask, const at::Tensor& x) {
+  auto dw = at::empty({64, x.size(1), 3, 3}, x.options().dtype(at::kFloat));
+  conv_prep_wgrad_run(gy, mask, x, dw, 0.f);
+  return dw;
+}
+
+void conv_prep_wgrad_into_hip(const at::Tensor& gy, const at::Tensor& mask, const at::Tensor& x,
+                              at::Tensor dw) {
+  conv_prep_wgrad_run(gy, mask, x, dw, 1.f);
+}
+
 at::Tensor relu_mask_hip(const at::Tensor& gy, const at::Tensor& y) {
   check_nhwc_bf16(y, "relu_mask: y");
   auto g = gy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -823,6 +899,9 @@ TORCH_LIBRARY(commeff, m) {
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("conv_weight_prep_multi(Tensor[] ws) -> Tensor[]");
+  m.def("conv_prep_fwd(Tensor x, Tensor w) -> (Tensor, Tensor)");
+  m.def("conv_prep_wgrad(Tensor gy, Tensor mask, Tensor x) -> Tensor");
+  m.def("conv_prep_wgrad_into(Tensor gy, Tensor mask, Tensor x, Tensor(a!) dw) -> ()");
   m.def("relu_mask(Tensor gy, Tensor y) -> Tensor");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
         "int d) -> Tensor");
@@ -886,6 +965,9 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("conv3x3_wgrad_into", &conv3x3_wgrad_into_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);
   m.impl("conv_weight_prep_multi", &conv_weight_prep_multi_hip);
+  m.impl("conv_prep_fwd", &conv_prep_fwd_hip);
+  m.impl("conv_prep_wgrad", &conv_prep_wgrad_hip);
+  m.impl("conv_prep_wgrad_into", &conv_prep_wgrad_into_hip);
   m.impl("relu_mask", &relu_mask_hip);
   m.impl("cs_zero_buckets", &cs_zero_buckets_hip);
   m.impl("cs_l2estimate", &cs_l2estimate_hip);

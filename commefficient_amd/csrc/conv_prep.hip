@@ -1,0 +1,276 @@
+// The ResNet-9 input ("prep") convolution: 3x3 / pad 1, Cin <= 4 -> K = 64,
+// fused ReLU, on gfx950 (reference ConvBN(c_in, 64),
+// /root/reference/CommEfficient/models/resnet9.py:32-59, 118).
+//
+// With 3 input channels the layer is pure bandwidth: 27 MACs per output.
+// The augmentation kernel stores the input batch with a 4-channel pixel
+// stride (8 bytes, channel 3 = 0), so one tap of one pixel is one 8-byte load.
+//
+// Forward: y^T = W x im2col^T on v_mfma_f32_32x32x16_bf16 with the GEMM K
+// index = 4*tap + c (36 used, padded to 48 = 3 K-steps).  The weight operand
+// lives in registers for the whole kernel; a lane's B fragment of one K-step
+// is two taps of one pixel (two 8-byte loads).  Epilogue: ReLU, 8-byte bf16
+// stores (a wave writes 32 whole 128-byte output rows), and a 64-bit ReLU
+// mask per pixel (two 32-bit words in accumulator order) for the backward.
+//
+// Weight gradient: dW[k][c][tap] = sum_p g[p][k] x[p + tap][c] with
+// g = gy * mask, as a GEMM over pixels on the same MFMA: per 64-pixel step a
+// block stages g [64 px][64 k] (masked while loading) and the im2col tile
+// [64 px][16 taps x 4 ch] in LDS, and the waves read both operands with the
+// transposing ds_read_b64_tr_b16 (pixels become the reduction index).  Global
+// loads of step s+1 are in flight during the MFMAs of step s.  Per-block
+// partial [64][64] tiles are summed by a second kernel in a fixed order
+// (deterministic).  Reads gy once (bf16) and the 8-byte-per-pixel mask
+// instead of the 64-channel activation.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+#include "conv_common.h"
+
+namespace commeff {
+namespace {
+
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+constexpr int kPrepK = 64;
+
+struct PrepPix {
+  int p, h, w;
+  bool valid;
+};
+
+__device__ __forceinline__ PrepPix prep_pix(const ConvPrepArgs& a, int p) {
+  PrepPix r;
+  r.valid = p < a.P;
+  r.p = r.valid ? p : 0;
+  const uint32_t q = fdiv(static_cast<uint32_t>(r.p), a.div_w);
+  r.w = r.p - static_cast<int>(q) * a.W;
+  r.h = static_cast<int>(q - fdiv(q, a.div_h) * a.H);
+  return r;
+}
+
+// the 4 channels of tap `tap` of pixel x (8 bytes; zero outside the image / for
+// taps >= 9; channel 3 forced to 0 when Cin == 3 so even a NaN there is inert)
+__device__ __forceinline__ v2u prep_tap(const ConvPrepArgs& a, const PrepPix& x, int tap) {
+  v2u t = {0u, 0u};
+  if (tap < 9) {
+    const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+    const bool ok = x.valid && static_cast<unsigned>(x.h + dr) < static_cast<unsigned>(a.H) &&
+                    static_cast<unsigned>(x.w + ds) < static_cast<unsigned>(a.W);
+    if (ok) {
+      t = *reinterpret_cast<const v2u*>(a.x + static_cast<size_t>(x.p + dr * a.W + ds) * 4);
+      if (a.Cin <= 3) t[1] &= 0xffffu;
+    }
+  }
+  return t;
+}
+
+// B fragments of one 32-pixel tile: K-step s, lane half hi -> taps 4s+2hi, 4s+2hi+1
+__device__ __forceinline__ void prep_load_b(const ConvPrepArgs& a, int tile, int lr, int hi,
+                                            bf16x8_t (&b)[3]) {
+  const PrepPix x = prep_pix(a, tile * 32 + lr);
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const v2u t0 = prep_tap(a, x, 4 * s + 2 * hi), t1 = prep_tap(a, x, 4 * s + 2 * hi + 1);
+    const v4u v = {t0[0], t0[1], t1[0], t1[1]};
+    b[s] = __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+__global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
+  // weight fragments (row m = 32 mt + lr, GEMM k = 16 s + 8 hi + j -> tap k/4,
+  // channel k%4), built once per block in LDS
+  __shared__ bf16x8_t wsm[2][3][64];
+  for (int e = threadIdx.x; e < 2 * 3 * 64 * 8; e += 256) {
+    const int j = e & 7, ln = (e >> 3) & 63, ms = e >> 9;  // ms = mt*3 + s
+    const int mt = ms / 3, s = ms - 3 * mt;
+    const int kk = 16 * s + 8 * (ln >> 5) + j, tap = kk >> 2, c = kk & 3;
+    const int m = 32 * mt + (ln & 31);
+    reinterpret_cast<__bf16*>(&wsm[0][0][0])[e] =
+        static_cast<__bf16>((tap < 9 && c < a.Cin) ? a.w[(m * a.Cin + c) * 9 + tap] : 0.f);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, lr = lane & 31, hi = lane >> 5;
+  bf16x8_t wa[2][3];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) wa[mt][s] = wsm[mt][s][lane];
+  const int ntiles = (a.P + 31) >> 5;
+  const int nwaves = (gridDim.x * 256) >> 6;
+  int tile = (blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (tile >= ntiles) return;
+  bf16x8_t b[3];
+  prep_load_b(a, tile, lr, hi, b);
+  while (true) {
+    const int next = tile + nwaves;
+    bf16x8_t bn[3];
+    if (next < ntiles) prep_load_b(a, next, lr, hi, bn);  // in flight during this tile's work
+    f32x16_t acc[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mt][e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[mt][s], b[s], acc[mt], 0, 0, 0);
+    }
+    const int p = tile * 32 + lr;
+    if (p < a.P) {
+      // lane (pixel p, hi) holds channels 32 mt + 8 g + 4 hi + (0..3) in acc[mt][4 g ..]
+      uint32_t mbits = 0;
+      uint16_t* yrow = a.y + static_cast<size_t>(p) * kPrepK;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = fmaxf(acc[mt][4 * g + j], 0.f);
+            mbits |= (v[j] > 0.f ? 1u : 0u) << (16 * mt + 4 * g + j);
+          }
+          const v2u o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+          *reinterpret_cast<v2u*>(yrow + 32 * mt + 8 * g + 4 * hi) = o;
+        }
+      a.mask[2 * p + hi] = mbits;
+    }
+    if (next >= ntiles) break;
+    tile = next;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) b[s] = bn[s];
+  }
+}
+
+// Weight gradient.  LDS images (64 rows of 128 B, sw_tr128 swizzle):
+// A = g[px][k] (masked gy), B = im2col[px][4 tap + c] (taps 9..15 zero).
+struct PrepWgStage {
+  v4u g[2];  // 16-byte chunks of g: rows (tid + 256 i) >> 3, chunk (tid + 256 i) & 7
+  v4u xb[2]; // 16-byte chunks of im2col: two taps each
+};
+
+__device__ __forceinline__ void prep_wg_load(const ConvPrepArgs& a, int step, int tid, PrepWgStage& st) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + 256 * i, row = id >> 3, cc = id & 7;
+    const PrepPix x = prep_pix(a, step * 64 + row);
+    v4u g = {0u, 0u, 0u, 0u};
+    if (x.valid) {
+      g = *reinterpret_cast<const v4u*>(a.gy + static_cast<size_t>(x.p) * kPrepK + 8 * cc);
+      const v2u mw = *reinterpret_cast<const v2u*>(a.mask_in + 2 * x.p);
+      // channels 8cc + j: word j >> 2, bit 16 (cc >> 2) + 4 (cc & 3) + (j & 3)
+      const int sh = 16 * (cc >> 2) + 4 * (cc & 3);
+      const uint32_t m0 = mw[0] >> sh, m1 = mw[1] >> sh;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t bits = q < 2 ? m0 : m1;  // element pair q covers channels 2q, 2q+1
+        const int j0 = (2 * q) & 3;
+        const uint32_t keep = (((bits >> j0) & 1u) ? 0x0000ffffu : 0u) |
+                              (((bits >> (j0 + 1)) & 1u) ? 0xffff0000u : 0u);
+        g[q] &= keep;
+      }
+    }
+    st.g[i] = g;
+    const v2u t0 = prep_tap(a, x, 2 * cc), t1 = prep_tap(a, x, 2 * cc + 1);
+    st.xb[i] = v4u{t0[0], t0[1], t1[0], t1[1]};
+  }
+}
+
+__global__ void __launch_bounds__(256) prep_wgrad_kernel(ConvPrepArgs a, int steps_per_block) {
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2 * 64 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mi = wid >> 1, ni = wid & 1;
+  const int nsteps = (a.P + 63) / 64;
+  const int s0 = blockIdx.x * steps_per_block, s1 = min(nsteps, s0 + steps_per_block);
+  int toA[2], toB[2];
+  tr_offsets<128>(mi * 32, lane, toA);
+  tr_offsets<128>(ni * 32, lane, toB);
+  f32x16_t acc;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  PrepWgStage st;
+  if (s0 < s1) prep_wg_load(a, s0, tid, st);
+  for (int step = s0; step < s1; ++step) {
+    __syncthreads();  // the previous step's operand reads are done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int id = tid + 256 * i, row = id >> 3, cc = id & 7;
+      const int off = row * 128 + ((cc ^ sw_tr128(row)) << 4);
+      *reinterpret_cast<v4u*>(sm + off) = st.g[i];
+      *reinterpret_cast<v4u*>(sm + 8192 + off) = st.xb[i];
+    }
+    __syncthreads();
+    if (step + 1 < s1) prep_wg_load(a, step + 1, tid, st);  // lands during the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int d = kk * 16 * 128;
+      const bf16x8_t af = tr_read(sm + toA[0] + d, sm + toA[1] + d);
+      const bf16x8_t bf = tr_read(sm + 8192 + toB[0] + d, sm + 8192 + toB[1] + d);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+    }
+  }
+  // partial[block][k][n], n = 4 tap + c
+  float* out = a.partial + static_cast<size_t>(blockIdx.x) * kPrepK * 64;
+  const int hi = lane >> 5, lr = lane & 31;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int m = mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+    out[m * 64 + ni * 32 + lr] = acc[e];
+  }
+}
+
+// dw[k][c][tap] (= beta * dw +) sum over blocks of partial[b][k][4 tap + c]:
+// 16 threads per output, fixed combination order
+__global__ void __launch_bounds__(256) prep_wgrad_reduce_kernel(const float* __restrict__ partial,
+                                                                int nblocks, int Cin, float* __restrict__ dw,
+                                                                float beta) {
+  __shared__ float red[16][17];
+  const int o = blockIdx.x * 16 + (threadIdx.x & 15), part = threadIdx.x >> 4;  // o = k*27 + c*9 + tap
+  const int k = o / 27, r = o - k * 27, c = r / 9, tap = r - 9 * c;
+  const bool live = o < kPrepK * 27 && c < Cin;
+  float s = 0.f;
+  if (live) {
+    const float* src = partial + k * 64 + 4 * tap + c;
+#pragma unroll 4
+    for (int b = part; b < nblocks; b += 16) s += src[static_cast<size_t>(b) * kPrepK * 64];
+  }
+  red[part][threadIdx.x & 15] = s;
+  __syncthreads();
+  if (threadIdx.x < 16 && live) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][threadIdx.x];
+    float* d = dw + (k * Cin + c) * 9 + tap;
+    *d = beta != 0.f ? beta * *d + t : t;
+  }
+}
+
+}  // namespace
+
+int conv_prep_wgrad_blocks(int P) {
+  const int steps = (P + 63) / 64;
+  int b = (steps + 7) / 8;  // >= 8 pixel steps per block
+  return b < 1024 ? (b < 1 ? 1 : b) : 1024;
+}
+
+void launch_conv_prep_fwd(ConvPrepArgs a, hipStream_t stream) {
+  a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
+  a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
+  const int ntiles = (a.P + 31) / 32;
+  int blocks = (ntiles + 15) / 16;  // ~4 tiles per wave (weights are set up once per block)
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(prep_fwd_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, stream, a);
+}
+
+void launch_conv_prep_wgrad(ConvPrepArgs a, float* dw, float beta, hipStream_t stream) {
+  a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
+  a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
+  const int nb = conv_prep_wgrad_blocks(a.P);
+  const int steps = (a.P + 63) / 64;
+  const int spb = (steps + nb - 1) / nb;
+  hipLaunchKernelGGL(prep_wgrad_kernel, dim3(nb), dim3(256), 0, stream, a, spb);
+  hipLaunchKernelGGL(prep_wgrad_reduce_kernel, dim3((kPrepK * 27 + 15) / 16), dim3(256), 0, stream,
+                     a.partial, nb, a.Cin, dw, beta);
+}
+
+}  // namespace commeff

@@ -177,6 +177,25 @@ void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream);
 void launch_relu_mask(const uint16_t* gy, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream);
 
+// ResNet-9 input conv (conv_prep.hip): 3x3 pad 1, Cin <= 4 -> 64 channels,
+// ReLU.  x: bf16 pixels with a 4-channel stride; y: [P, 64] bf16; mask: two
+// 32-bit ReLU-mask words per pixel.
+struct ConvPrepArgs {
+  const uint16_t* x;        // [P, 4]
+  const float* w;           // [64, Cin, 3, 3]
+  uint16_t* y;              // [P, 64]
+  uint32_t* mask;           // [P, 2] (forward output)
+  const uint16_t* gy;       // [P, 64] (backward)
+  const uint32_t* mask_in;  // [P, 2] (backward)
+  float* partial;           // [conv_prep_wgrad_blocks(P), 64, 64] scratch (backward)
+  int P, H, W, Cin;
+  FastDivU32 div_w, div_h;  // set by the launchers
+};
+int conv_prep_wgrad_blocks(int P);
+void launch_conv_prep_fwd(ConvPrepArgs a, hipStream_t stream);
+// dw [64][Cin][3][3] fp32 = beta * dw + sum_p (gy * mask) x
+void launch_conv_prep_wgrad(ConvPrepArgs a, float* dw, float beta, hipStream_t stream);
+
 // ----------------------------------------------------------------- loss --
 // per-example cross-entropy of logits [B, C] (bf16 or f32): loss, top-1
 // correctness and the unit gradient softmax - onehot (logits dtype)
@@ -194,11 +213,12 @@ void launch_relu_maxpool_bwd(const uint16_t* gy, const uint8_t* idx, uint16_t* g
 // -------------------------------------------------------------- augment --
 // CIFAR-style augmentation of uint8 NHWC images into a bf16 NHWC
 // (channels_last) batch: reflect-pad `pad`, random crop, random h-flip,
-// normalise.  Randomness: counter hash of (seed, keys[b] or b).
+// normalise.  Randomness: counter hash of (seed, keys[b] or b).  Pixels are
+// written out_cstride (>= C) channels apart, the extra channels zeroed.
 void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx,
                             int64_t B, int H, int W, int C, int pad,
                             int flip, const float* mean, const float* inv_std,
                             uint64_t seed, const int64_t* keys, uint16_t* out_bf16,
-                            hipStream_t stream);
+                            int out_cstride, hipStream_t stream);
 
 }  // namespace commeff

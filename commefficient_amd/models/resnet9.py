@@ -9,8 +9,8 @@ BatchNorm is off unless ``do_batchnorm`` (cv_train.py:357).  6,568,640 params
 for 10 classes.
 
 MI355X notes: conv+ReLU(+maxpool) units run on the native MFMA implicit-GEMM
-kernels of csrc/conv.hip (bf16 channels_last, fused epilogues); the 3-channel
-prep conv and BatchNorm variants use MIOpen.  Fixes reference
+kernels of csrc/conv.hip (bf16 channels_last, fused epilogues), the 3-channel
+prep conv on csrc/conv_prep.hip; BatchNorm variants use MIOpen.  Fixes reference
 quirk Appendix C #12: ``finetune_parameters`` no longer touches an undefined
 ``self.iid``.
 """
@@ -21,7 +21,8 @@ import itertools
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import conv3x3_relu_pool, prepared_conv_weights, relu_maxpool, residual_unit
+from ..ops.nn import (conv3x3_input_relu, conv3x3_relu_pool, input_conv_native_ok,
+                      prepared_conv_weights, relu_maxpool, residual_unit)
 from .common import GhostBatchNorm2d, Mul
 
 __all__ = ["ResNet9"]
@@ -62,6 +63,10 @@ class ConvBN(nn.Module):
             self.bn = _bn(c_out, bn_weight_init=bn_weight_init, **kw)
 
     def forward(self, x):
+        if not self.do_batchnorm and self.pool is None and input_conv_native_ok(x, self.conv.weight):
+            # the 3-channel input conv: native kernel reading the augmentation
+            # kernel's padded pixels (csrc/conv_prep.hip)
+            return conv3x3_input_relu(x, self.conv.weight)
         if not self.do_batchnorm and (self.pool is None or (
                 isinstance(self.pool, nn.MaxPool2d) and _square_pool(self.pool))):
             # conv + relu (+ pool) as one unit: native MFMA conv kernels with

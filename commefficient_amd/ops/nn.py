@@ -205,6 +205,50 @@ def conv3x3_relu_pool(x: torch.Tensor, weight: torch.Tensor, pool_k: int = 0) ->
     return relu_maxpool(y, pool_k) if pool_k else F.relu(y)
 
 
+class _InputConv(torch.autograd.Function):
+    """relu(conv3x3(x, w)) for the 3-channel network input (csrc/conv_prep.hip):
+    MFMA forward with a fused ReLU that also emits a 1-bit ReLU mask per
+    output; backward computes only dW (the input is data) from gy and the
+    mask, accumulating into an existing flat-buffer ``.grad``."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        y, mask = _ops().conv_prep_fwd(x, weight.detach().contiguous())
+        ctx.save_for_backward(x, mask)
+        ctx.weight = weight
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, mask = ctx.saved_tensors
+        if not ctx.needs_input_grad[1]:
+            return None, None
+        gr = ctx.weight.grad
+        if (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
+                and gr.device == gy.device and gr.shape == ctx.weight.shape):
+            _ops().conv_prep_wgrad_into(gy, mask, x, gr)
+            return None, None
+        return None, _ops().conv_prep_wgrad(gy, mask, x)
+
+
+def input_conv_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """The augmentation kernel's 3-channel bf16 batch (4-channel pixel stride)
+    into a [64, 3, 3, 3] conv."""
+    if not (_CONV_BACKEND[0] == "native" and x.is_cuda and x.dtype == torch.bfloat16
+            and x.dim() == 4 and x.shape[1] == 3 and not x.requires_grad
+            and weight.dtype == torch.float32 and tuple(weight.shape) == (64, 3, 3, 3)):
+        return False
+    H, W = x.shape[2], x.shape[3]
+    return x.stride() == (4 * H * W, 1, 4 * W, 4)
+
+
+def conv3x3_input_relu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """``relu(conv2d(x, weight, padding=1))`` for the network input."""
+    if input_conv_native_ok(x, weight):
+        return _InputConv.apply(x, weight)
+    return F.relu(F.conv2d(x, weight, padding=1))
+
+
 # ------------------------------------------------------------ loss
 class _FusedCE(torch.autograd.Function):
     """Per-example cross-entropy + top-1 correctness in one kernel

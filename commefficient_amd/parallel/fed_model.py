@@ -206,8 +206,11 @@ class FedModel:
 
     def _prep(self, xs):
         if self.channels_last:
+            # pixels already channel-innermost (incl. the augmentation kernel's
+            # 4-channel-stride layout that the native input conv reads) stay as is
             xs = tuple(x.contiguous(memory_format=torch.channels_last)
-                       if (x.dim() == 4 and x.is_floating_point()) else x for x in xs)
+                       if (x.dim() == 4 and x.is_floating_point() and x.stride(1) != 1) else x
+                       for x in xs)
         return xs
 
     def _payload_buf(self, n_metric_slots: int) -> torch.Tensor:

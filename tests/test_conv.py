@@ -183,13 +183,13 @@ def test_resnet9_native_as_accurate_as_miopen():
     from commefficient_amd.models import ResNet9
     torch.manual_seed(0)
     m = ResNet9().cuda()
-    x = _nhwc(torch.randn(16, 3, 32, 32, device="cuda"))
+    x = _padded_input(16, 32, 32)  # the loader's layout: native input conv too
     out = {}
     for backend in ("fp32", "miopen", "native"):
         cnn.set_conv_backend("miopen" if backend == "fp32" else backend)
         m.zero_grad(set_to_none=True)
         if backend == "fp32":
-            y = m(x)
+            y = m(x.float())
         else:
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 y = m(x.to(torch.bfloat16))
@@ -237,3 +237,51 @@ def test_weight_prep_multi_matches_permutes():
         wf, wt = cnn._prep(w)
     assert torch.equal(wf, out[0]) and torch.equal(wt, out[1])
     assert not cnn._PREP
+
+
+def _padded_input(N, H, W, seed=0):
+    """A [N, 3, H, W] bf16 view of a 4-channel-stride pixel buffer (the layout
+    augment_u8_nhwc writes), padding channel zero."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    buf = torch.zeros(N, H, W, 4, device="cuda", dtype=torch.bfloat16)
+    buf[..., :3] = torch.randn(N, H, W, 3, device="cuda", generator=g).to(torch.bfloat16)
+    return buf[..., :3].permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("N,H,W", [(4, 32, 32), (3, 7, 5), (1, 1, 1)])
+def test_input_conv_matches_fp32(N, H, W):
+    x = _padded_input(N, H, W)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    w = (torch.randn(64, 3, 3, 3, device="cuda", generator=g) * 0.3).requires_grad_(True)
+    cnn.set_conv_backend("native")
+    assert cnn.input_conv_native_ok(x, w)
+    y = cnn.conv3x3_input_relu(x, w)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    pre = F.conv2d(x.float(), wr, padding=1)
+    yr = (pre + (pre.to(torch.bfloat16).float() - pre).detach()).relu()
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, yr)
+    gy = torch.randn(y.shape, device="cuda", generator=g)
+    (y.float() * gy).sum().backward()
+    (yr * gy.to(torch.bfloat16).float()).sum().backward()
+    rel = (w.grad - wr.grad).norm() / wr.grad.norm()
+    assert rel < 1e-2, rel.item()
+    # accumulates into an existing .grad; deterministic
+    keep = w.grad.clone()
+    y = cnn.conv3x3_input_relu(x, w)
+    (y.float() * gy).sum().backward()
+    assert torch.equal(w.grad, 2 * keep)
+
+
+def test_augment_writes_padded_pixels():
+    from commefficient_amd import ops as cops
+    data = torch.randint(0, 256, (10, 8, 8, 3), dtype=torch.uint8, device="cuda")
+    idx = torch.tensor([3, 1, 7], device="cuda")
+    mean = torch.tensor([0.5, 0.4, 0.3], device="cuda")
+    inv = torch.tensor([2.0, 3.0, 4.0], device="cuda")
+    x = cops.augment_u8_nhwc(data, idx, 0, False, mean, inv, 0)
+    assert x.shape == (3, 3, 8, 8) and x.stride() == (256, 1, 32, 4)
+    ref = ((data[idx].float() / 255 - mean) * inv).permute(0, 3, 1, 2)
+    torch.testing.assert_close(x.float(), ref, rtol=1e-2, atol=1e-2)
+    pad = torch.as_strided(x, (3, 8, 8), (256, 32, 4), x.storage_offset() + 3)
+    assert torch.all(pad == 0)
