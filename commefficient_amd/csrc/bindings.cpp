@@ -370,6 +370,26 @@ at::Tensor count_ge_hip(const at::Tensor& last_mod, const at::Tensor& thr) {
   return buf.narrow(0, T + 1, T);
 }
 
+at::Tensor account_round_hip(const at::Tensor& last_mod, const at::Tensor& meta, int64_t T, int64_t W,
+                             at::Tensor client_dl, at::Tensor client_ul, double upc) {
+  TORCH_CHECK(last_mod.scalar_type() == at::kInt && last_mod.is_contiguous(), "account_round: last_mod");
+  TORCH_CHECK(meta.scalar_type() == at::kLong && meta.is_contiguous() && meta.numel() == T + 2 * W &&
+                  meta.device() == last_mod.device(), "account_round: meta = [thr | inv | clients]");
+  TORCH_CHECK(T >= 0 && T <= 1024 && W >= 0, "account_round: at most 1024 thresholds");
+  TORCH_CHECK(client_dl.scalar_type() == at::kDouble && client_ul.scalar_type() == at::kDouble &&
+                  client_dl.is_contiguous() && client_ul.is_contiguous(), "account_round: totals");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(last_mod.device());
+  auto dl = at::empty({W}, last_mod.options().dtype(at::kDouble));
+  if (W == 0) return dl;
+  auto partial = at::empty({account_round_blocks(last_mod.numel()) * (T + 1)},
+                           last_mod.options().dtype(at::kInt));
+  launch_account_round(last_mod.data_ptr<int32_t>(), last_mod.numel(), meta.data_ptr<int64_t>(),
+                       static_cast<int>(T), static_cast<int>(W),
+                       reinterpret_cast<uint32_t*>(partial.data_ptr()), client_dl.data_ptr<double>(),
+                       client_ul.data_ptr<double>(), upc, dl.data_ptr<double>(), cur_stream());
+  return dl;
+}
+
 void axpby_hip(at::Tensor out, const at::Tensor& a, double alpha,
                const c10::optional<at::Tensor>& b, double beta) {
   check_f32(out, "out");
@@ -899,6 +919,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("conv_weight_prep_multi(Tensor[] ws) -> Tensor[]");
+  m.def("account_round(Tensor last_mod, Tensor meta, int T, int W, Tensor(a!) client_dl, "
+        "Tensor(b!) client_ul, float upc) -> Tensor");
   m.def("conv_prep_fwd(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def("conv_prep_wgrad(Tensor gy, Tensor mask, Tensor x) -> Tensor");
   m.def("conv_prep_wgrad_into(Tensor gy, Tensor mask, Tensor x, Tensor(a!) dw) -> ()");
@@ -976,6 +998,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("sparse_apply", &sparse_apply_hip);
   m.impl("dense_apply", &dense_apply_hip);
   m.impl("count_ge", &count_ge_hip);
+  m.impl("account_round", &account_round_hip);
   m.impl("axpby", &axpby_hip);
   m.impl("l2norm", &l2norm_hip);
   m.impl("clip_noise", &clip_noise_hip);

@@ -147,6 +147,86 @@ __global__ void count_ge_finish(unsigned long long* counts, int T, int64_t* out)
   }
 }
 
+// ------------------------------------------------------ round accounting
+// Fused download/upload accounting of one round (ByteAccountant.round):
+// per-block threshold histograms of last_mod (no global atomics: every block
+// writes its whole histogram row), then one block sums the rows in a fixed
+// order, suffix-sums them into counts[t] = #{i : last_mod[i] >= thr[t]} and
+// charges each participating client.
+__global__ void __launch_bounds__(kBlock)
+count_partial_kernel(const int32_t* __restrict__ last_mod, int64_t n, const int64_t* __restrict__ thr,
+                     int T, uint32_t* __restrict__ partial) {
+  __shared__ unsigned int h[1025];
+  __shared__ int th[1024];
+  for (int t = threadIdx.x; t <= T; t += blockDim.x) h[t] = 0;
+  for (int t = threadIdx.x; t < T; t += blockDim.x) th[t] = static_cast<int>(thr[t]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t base = blockIdx.x * static_cast<int64_t>(blockDim.x); base < n; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    int bin = 0;
+    if (i < n) {
+      const int v = last_mod[i];
+      int lo = 0, hi = T;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (th[mid] <= v) lo = mid + 1; else hi = mid;
+      }
+      bin = lo;
+    }
+    unsigned long long pending = __ballot(bin > 0);
+    while (pending) {
+      const int leader = __ffsll(static_cast<long long>(pending)) - 1;
+      const int b = __shfl(bin, leader);
+      const unsigned long long same = __ballot(bin == b) & pending;
+      if (lane == leader) atomicAdd(h + b, static_cast<unsigned>(__popcll(same)));
+      pending &= ~same;
+    }
+  }
+  __syncthreads();
+  uint32_t* row = partial + static_cast<size_t>(blockIdx.x) * (T + 1);
+  for (int t = threadIdx.x; t <= T; t += blockDim.x) row[t] = h[t];
+}
+
+__global__ void __launch_bounds__(1024)
+account_finish_kernel(const uint32_t* __restrict__ partial, int nb, int T, const int64_t* __restrict__ meta,
+                      int W, double* __restrict__ client_dl, double* __restrict__ client_ul, double upc,
+                      double* __restrict__ dl) {
+  __shared__ uint32_t red[2048];
+  __shared__ uint32_t cnt[1025];
+  const int nbins = T + 1;
+  const int parts = nbins >= 1024 ? 1 : 1024 / nbins;
+  for (int e = threadIdx.x; e < parts * nbins; e += 1024) {
+    const int part = e / nbins, bin = e - part * nbins;
+    uint32_t s = 0;
+#pragma unroll 4
+    for (int b = part; b < nb; b += parts) s += partial[static_cast<size_t>(b) * nbins + bin];
+    red[e] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // bin b holds elements passing thresholds 0..b-1: cnt[t] = sum_{b > t} bins[b]
+    uint32_t run = 0;
+    for (int b = T; b >= 1; --b) {
+      uint32_t v = 0;
+      for (int q = 0; q < parts; ++q) v += red[q * nbins + b];
+      run += v;
+      cnt[b - 1] = run;
+    }
+  }
+  __syncthreads();
+  const int64_t* inv = meta + T;
+  const int64_t* clients = meta + T + W;
+  for (int j = threadIdx.x; j < W; j += 1024) {
+    const double v = 4.0 * static_cast<double>(cnt[inv[j]]);
+    const int64_t c = clients[j];
+    dl[j] = v;
+    client_dl[c] += v;  // clients are unique within a round
+    client_ul[c] += upc;
+  }
+}
+
 // ----------------------------------------------------------------- axpby
 __global__ void __launch_bounds__(kBlock)
 axpby_kernel(float* __restrict__ out, const float* __restrict__ a, float alpha,
@@ -304,6 +384,19 @@ void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr, int
   hipLaunchKernelGGL(count_ge_kernel, dim3(grid_for(n, 1024)), dim3(kBlock), 0, stream, last_mod,
                      n, thr, T, bins);
   hipLaunchKernelGGL(count_ge_finish, dim3(1), dim3(64), 0, stream, bins, T, counts + T + 1);
+}
+
+int account_round_blocks(int64_t n) { return grid_for(n, 256); }
+
+void launch_account_round(const int32_t* last_mod, int64_t n, const int64_t* meta, int T, int W,
+                          uint32_t* partial, double* client_dl, double* client_ul, double upc,
+                          double* dl, hipStream_t stream) {
+  const int nb = account_round_blocks(n);
+  if (T > 0)
+    hipLaunchKernelGGL(count_partial_kernel, dim3(nb), dim3(kBlock), 0, stream, last_mod, n, meta, T,
+                       partial);
+  hipLaunchKernelGGL(account_finish_kernel, dim3(1), dim3(1024), 0, stream, partial, T > 0 ? nb : 0, T,
+                     meta, W, client_dl, client_ul, upc, dl);
 }
 
 void launch_axpby(float* out, const float* a, float alpha, const float* b, float beta, int64_t n,

@@ -109,6 +109,13 @@ void launch_dense_apply(float* w, const float* delta, int64_t n, float lr,
 // counts[t] = #{i : last_mod[i] >= thr[t]}  (thr sorted ascending, T <= 1024)
 void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr,
                      int T, int64_t* counts, hipStream_t stream);
+// one round of byte accounting: meta = [thr (T, ascending) | inv (W) | clients (W)]
+// (int64); dl[j] = 4 * #{i : last_mod[i] >= thr[inv[j]]}; client_dl[clients[j]] +=
+// dl[j]; client_ul[clients[j]] += upc.  partial: account_round_blocks(n) * (T+1) u32.
+int account_round_blocks(int64_t n);
+void launch_account_round(const int32_t* last_mod, int64_t n, const int64_t* meta, int T, int W,
+                          uint32_t* partial, double* client_dl, double* client_ul, double upc,
+                          double* dl, hipStream_t stream);
 // out = alpha*a + beta*b   (b optional -> out = alpha*a)
 void launch_axpby(float* out, const float* a, float alpha, const float* b,
                   float beta, int64_t n, hipStream_t stream);

@@ -12,7 +12,7 @@ from .sketch import CSVec, make_hashes
 
 __all__ = ["CSVec", "make_hashes", "topk_abs", "topk_dense", "momentum_ef", "sparse_apply",
            "dense_apply", "count_ge", "axpby", "l2norm", "clip_noise", "client_state",
-           "zero_at", "scatter_dense", "augment_u8_nhwc"]
+           "zero_at", "scatter_dense", "augment_u8_nhwc", "account_round"]
 
 ERROR_MODE = {"none": 0, "virtual": 1, "local": 2}
 
@@ -46,6 +46,13 @@ def dense_apply(w, delta, lr, lr_vec=None, last_mod=None, round_idx: int = 0):
 
 def count_ge(last_mod: torch.Tensor, thr: torch.Tensor) -> torch.Tensor:
     return _ops().count_ge(last_mod, thr)
+
+
+def account_round(last_mod, meta, T: int, W: int, client_dl, client_ul, upload_per_client: float):
+    """Fused round accounting (HIP): meta = int64 [thr (T) | inv (W) | clients (W)];
+    returns per-client download bytes and adds them (and the upload) to the totals."""
+    return _ops().account_round(last_mod, meta, int(T), int(W), client_dl, client_ul,
+                                float(upload_per_client))
 
 
 def axpby(out, a, alpha, b=None, beta=0.0):

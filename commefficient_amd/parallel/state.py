@@ -146,6 +146,14 @@ class ByteAccountant:
         upload bytes float)."""
         seen = self.last_seen[clients].astype(np.int32)
         thr, inv = np.unique(seen, return_inverse=True)
+        if self.last_mod.is_cuda and len(thr) <= 1024:
+            # one fused native op: histogram, suffix counts and per-client totals
+            meta = h2d(np.concatenate([thr, inv, clients]).astype(np.int64), self.device)
+            dl = ops.account_round(self.last_mod, meta, len(thr), len(clients),
+                                   self.client_download, self.client_upload,
+                                   float(self.upload_per_client))
+            self.last_seen[clients] = round_idx
+            return dl, float(self.upload_per_client) * len(clients)
         dl = torch.empty(len(clients), dtype=torch.float64, device=self.device)
         counts_all = []
         for s in range(0, len(thr), 1024):

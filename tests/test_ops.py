@@ -300,3 +300,29 @@ def test_count_ge_random_matches_torch(device):
     cnt = ops.count_ge(lm.to(device), thr.to(device)).cpu()
     exp = torch.stack([(lm >= t).sum() for t in thr])
     assert cnt.tolist() == exp.tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 37, 1024])
+def test_account_round_matches_reference(T):
+    g = torch.Generator().manual_seed(T)
+    d, C = 1_000_003, 5000
+    lm = torch.randint(-1, 3000, (d,), generator=g, dtype=torch.int32)
+    lm[: d // 3] = 17
+    thr = torch.unique(torch.randint(-1, 3000, (4 * T,), generator=g, dtype=torch.int64))[:T]
+    T = thr.numel()
+    W = 3 * T
+    inv = torch.randint(0, T, (W,), generator=g)
+    inv[:T] = torch.arange(T)
+    clients = torch.randperm(C, generator=g)[:W]
+    cdl = torch.rand(C, generator=g, dtype=torch.float64)
+    cul = torch.rand(C, generator=g, dtype=torch.float64)
+    meta = torch.cat([thr, inv, clients]).cuda()
+    cdl_d, cul_d = cdl.cuda(), cul.cuda()
+    dl = ops.account_round(lm.cuda(), meta, T, W, cdl_d, cul_d, 123.0).cpu()
+    cnt = torch.stack([(lm >= t).sum() for t in thr]).to(torch.float64) * 4
+    exp = cnt[inv]
+    assert torch.equal(dl, exp)
+    cdl[clients] += exp
+    cul[clients] += 123.0
+    assert torch.equal(cdl_d.cpu(), cdl) and torch.equal(cul_d.cpu(), cul)
