@@ -140,9 +140,30 @@ void momentum_ef_cpu(at::Tensor V, const c10::optional<at::Tensor>& E, const at:
                    static_cast<float>(rho), static_cast<float>(gscale), static_cast<int>(mode));
 }
 
+// step: optional int32 [2] = (bits of lr, round) overriding lr / round
+static void read_step(const c10::optional<at::Tensor>& step, double& lr, int64_t& round) {
+  if (!step.has_value() || !step->defined()) return;
+  auto s = step->to(at::kCPU).contiguous();
+  TORCH_CHECK(s.scalar_type() == at::kInt && s.numel() == 2, "step must be int32 [2]");
+  const int32_t* p = s.data_ptr<int32_t>();
+  float f;
+  std::memcpy(&f, p, sizeof(float));
+  lr = f;
+  round = p[1];
+}
+
+static const int32_t* step_ptr(const c10::optional<at::Tensor>& step) {
+  if (!step.has_value() || !step->defined()) return nullptr;
+  TORCH_CHECK(step->scalar_type() == at::kInt && step->numel() == 2 && step->is_contiguous(),
+              "step must be a contiguous int32 [2]");
+  return step->data_ptr<int32_t>();
+}
+
 void sparse_apply_cpu(at::Tensor w, const at::Tensor& idx, const at::Tensor& vals, double lr,
                       const c10::optional<at::Tensor>& lr_vec,
-                      const c10::optional<at::Tensor>& last_mod, int64_t round) {
+                      const c10::optional<at::Tensor>& last_mod, int64_t round,
+                      const c10::optional<at::Tensor>& step) {
+  read_step(step, lr, round);
   check_f32(w, "w");
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   cpu::sparse_apply(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
@@ -152,7 +173,9 @@ void sparse_apply_cpu(at::Tensor w, const at::Tensor& idx, const at::Tensor& val
 
 void dense_apply_cpu(at::Tensor w, const at::Tensor& delta, double lr,
                      const c10::optional<at::Tensor>& lr_vec,
-                     const c10::optional<at::Tensor>& last_mod, int64_t round) {
+                     const c10::optional<at::Tensor>& last_mod, int64_t round,
+                     const c10::optional<at::Tensor>& step) {
+  read_step(step, lr, round);
   check_f32(w, "w");
   check_f32(delta, "delta");
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
@@ -337,25 +360,27 @@ void momentum_ef_hip(at::Tensor V, const c10::optional<at::Tensor>& E, const at:
 
 void sparse_apply_hip(at::Tensor w, const at::Tensor& idx, const at::Tensor& vals, double lr,
                       const c10::optional<at::Tensor>& lr_vec,
-                      const c10::optional<at::Tensor>& last_mod, int64_t round) {
+                      const c10::optional<at::Tensor>& last_mod, int64_t round,
+                      const c10::optional<at::Tensor>& step) {
   check_f32(w, "w");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   launch_sparse_apply(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                       idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
-                      static_cast<int32_t>(round), cur_stream());
+                      static_cast<int32_t>(round), step_ptr(step), cur_stream());
 }
 
 void dense_apply_hip(at::Tensor w, const at::Tensor& delta, double lr,
                      const c10::optional<at::Tensor>& lr_vec,
-                     const c10::optional<at::Tensor>& last_mod, int64_t round) {
+                     const c10::optional<at::Tensor>& last_mod, int64_t round,
+                     const c10::optional<at::Tensor>& step) {
   check_f32(w, "w");
   check_f32(delta, "delta");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   launch_dense_apply(w.data_ptr<float>(), delta.data_ptr<float>(), w.numel(),
                      static_cast<float>(lr), fptr(lr_vec), lm, static_cast<int32_t>(round),
-                     cur_stream());
+                     step_ptr(step), cur_stream());
 }
 
 at::Tensor count_ge_hip(const at::Tensor& last_mod, const at::Tensor& thr) {
@@ -933,9 +958,9 @@ TORCH_LIBRARY(commeff, m) {
   m.def("topk_abs(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
   m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "
-        "Tensor(b!)? last_mod, int round) -> ()");
+        "Tensor(b!)? last_mod, int round, Tensor? step=None) -> ()");
   m.def("dense_apply(Tensor(a!) w, Tensor delta, float lr, Tensor? lr_vec, Tensor(b!)? last_mod, "
-        "int round) -> ()");
+        "int round, Tensor? step=None) -> ()");
   m.def("count_ge(Tensor last_mod, Tensor thr) -> Tensor");
   m.def("axpby(Tensor(a!) out, Tensor a, float alpha, Tensor? b, float beta) -> ()");
   m.def("l2norm(Tensor x) -> Tensor");

@@ -66,9 +66,13 @@ __global__ void __launch_bounds__(kBlock)
 sparse_apply_kernel(float* __restrict__ w, const int64_t* __restrict__ idx,
                     const float* __restrict__ vals, int64_t k, float lr,
                     const float* __restrict__ lr_vec, int32_t* __restrict__ last_mod,
-                    int32_t round) {
+                    int32_t round, const int32_t* __restrict__ step) {
   int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   if (q >= k) return;
+  if (step != nullptr) {  // graph replay: [lr bits, round] from device memory
+    lr = __int_as_float(step[0]);
+    round = step[1];
+  }
   int64_t i = idx[q];
   float l = lr_vec != nullptr ? lr_vec[i] : lr;
   float old = w[i];
@@ -80,7 +84,11 @@ sparse_apply_kernel(float* __restrict__ w, const int64_t* __restrict__ idx,
 __global__ void __launch_bounds__(kBlock)
 dense_apply_kernel(float* __restrict__ w, const float* __restrict__ delta, int64_t n, float lr,
                    const float* __restrict__ lr_vec, int32_t* __restrict__ last_mod,
-                   int32_t round) {
+                   int32_t round, const int32_t* __restrict__ step) {
+  if (step != nullptr) {
+    lr = __int_as_float(step[0]);
+    round = step[1];
+  }
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
     float l = lr_vec != nullptr ? lr_vec[i] : lr;
@@ -362,17 +370,19 @@ void launch_momentum_ef(float* V, float* E, const float* G, int64_t n, float rho
 }
 
 void launch_sparse_apply(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
-                         const float* lr_vec, int32_t* last_mod, int32_t round, hipStream_t stream) {
+                         const float* lr_vec, int32_t* last_mod, int32_t round,
+                         const int32_t* step, hipStream_t stream) {
   if (k <= 0) return;
   hipLaunchKernelGGL(sparse_apply_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
-                     w, idx, vals, k, lr, lr_vec, last_mod, round);
+                     w, idx, vals, k, lr, lr_vec, last_mod, round, step);
 }
 
 void launch_dense_apply(float* w, const float* delta, int64_t n, float lr, const float* lr_vec,
-                        int32_t* last_mod, int32_t round, hipStream_t stream) {
+                        int32_t* last_mod, int32_t round, const int32_t* step,
+                        hipStream_t stream) {
   if (n <= 0) return;
   hipLaunchKernelGGL(dense_apply_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, w, delta, n,
-                     lr, lr_vec, last_mod, round);
+                     lr, lr_vec, last_mod, round, step);
 }
 
 void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr, int T, int64_t* counts,

@@ -101,11 +101,14 @@ void launch_momentum_ef(float* V, float* E, const float* G, int64_t n,
 // w[idx] -= lr(idx) * vals ; last_mod[idx] = round where w changed
 void launch_sparse_apply(float* w, const int64_t* idx, const float* vals,
                          int64_t k, float lr, const float* lr_vec,
-                         int32_t* last_mod, int32_t round, hipStream_t stream);
+                         int32_t* last_mod, int32_t round, const int32_t* step,
+                         hipStream_t stream);
 // w -= lr(i) * delta ; last_mod[i] = round where w changed
+// (step != nullptr: lr = bits of step[0], round = step[1], read on the device
+// so a captured HIP graph replays with the current round's values)
 void launch_dense_apply(float* w, const float* delta, int64_t n, float lr,
                         const float* lr_vec, int32_t* last_mod, int32_t round,
-                        hipStream_t stream);
+                        const int32_t* step, hipStream_t stream);
 // counts[t] = #{i : last_mod[i] >= thr[t]}  (thr sorted ascending, T <= 1024)
 void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr,
                      int T, int64_t* counts, hipStream_t stream);

@@ -23,6 +23,10 @@ from ..parallel.fed_model import RoundBatch
 from .fed_dataset import FedSampler
 
 
+_GOLDEN = 0x9E3779B97F4A7C15
+_MASK64 = (1 << 64) - 1
+
+
 class DeviceImageSource:
     def __init__(self, dataset, device, augment: bool, pad: int = 4, flip: bool = True,
                  out_bf16: bool = True):
@@ -55,6 +59,15 @@ class DeviceImageSource:
         y = self.targets[idx]
         return x, y
 
+    def gather_device(self, idx2: torch.Tensor):
+        """Batch from a device int64 [2, B] = (rows, pre-mixed keys) with seed
+        0 -- the same pixels as ``gather(rows, seed, keys)`` when
+        ``keys' = seed * 0x9E3779B97F4A7C15 + keys`` (mod 2^64), so a captured
+        HIP graph can replay it with new rows / seed from a static buffer."""
+        x = ops.augment_u8_nhwc(self.data, idx2[0], self.pad, self.flip, self.mean,
+                                self.inv_std, 0, self.out_bf16, idx2[1])
+        return x, self.targets[idx2[0]]
+
 
 class DeviceFedLoader:
     """Iterates federated training rounds as ``RoundBatch``es."""
@@ -86,7 +99,18 @@ class DeviceFedLoader:
             # seed by round, key by the example's position in the round
             return src.gather(rows[pos], seed, keys=pos)
 
-        return RoundBatch(cids, take, n_inputs=1)
+        rb = RoundBatch(cids, take, n_inputs=1)
+        if src.device.type == "cuda":
+            mix = np.array([(rnd_seed * _GOLDEN) & _MASK64], dtype=np.uint64)
+
+            def index(pos, rows=rows, mix=mix):
+                pos = np.asarray(pos, dtype=np.int64)
+                keys = (pos.astype(np.uint64) + mix).view(np.int64)  # wraps mod 2^64
+                return np.stack([np.asarray(rows, dtype=np.int64)[pos], keys])
+
+            rb.graph_index = index
+            rb.graph_gather = src.gather_device
+        return rb
 
 
 class DeviceValLoader:

@@ -36,12 +36,15 @@ def momentum_ef(V: torch.Tensor, E: Optional[torch.Tensor], G: torch.Tensor, rho
     _ops().momentum_ef(V, E, G, float(rho), float(gscale), ERROR_MODE[error_type])
 
 
-def sparse_apply(w, idx, vals, lr, lr_vec=None, last_mod=None, round_idx: int = 0):
-    _ops().sparse_apply(w, idx, vals, float(lr), lr_vec, last_mod, int(round_idx))
+def sparse_apply(w, idx, vals, lr, lr_vec=None, last_mod=None, round_idx: int = 0, step=None):
+    """w[idx] -= lr * vals; last_mod[idx] = round where w changed.  ``step``
+    (int32 [2] = lr bits, round) overrides lr/round from device memory (HIP
+    graph replay)."""
+    _ops().sparse_apply(w, idx, vals, float(lr), lr_vec, last_mod, int(round_idx), step)
 
 
-def dense_apply(w, delta, lr, lr_vec=None, last_mod=None, round_idx: int = 0):
-    _ops().dense_apply(w, delta, float(lr), lr_vec, last_mod, int(round_idx))
+def dense_apply(w, delta, lr, lr_vec=None, last_mod=None, round_idx: int = 0, step=None):
+    _ops().dense_apply(w, delta, float(lr), lr_vec, last_mod, int(round_idx), step)
 
 
 def count_ge(last_mod: torch.Tensor, thr: torch.Tensor) -> torch.Tensor:

@@ -93,9 +93,13 @@ class _PinnedRing:
         self.i = 0
 
     def copy(self, t: torch.Tensor, device) -> torch.Tensor:
+        return self.copy_into(t, torch.empty(t.shape, dtype=t.dtype, device=device))
+
+    def copy_into(self, t: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         nbytes = t.numel() * t.element_size()
         if nbytes > self.slot_bytes:
-            return t.pin_memory().to(device, non_blocking=True)
+            out.copy_(t.pin_memory(), non_blocking=True)
+            return out
         if self.bufs is None:
             self.bufs = [torch.empty(self.slot_bytes, dtype=torch.uint8, pin_memory=True)
                          for _ in range(self.slots)]
@@ -106,7 +110,6 @@ class _PinnedRing:
             self.events[k].synchronize()
         stage = self.bufs[k][:nbytes].view(t.dtype).view(t.shape)
         stage.copy_(t)
-        out = torch.empty(t.shape, dtype=t.dtype, device=device)
         out.copy_(stage, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -129,6 +132,17 @@ def h2d(x, device, dtype=None) -> torch.Tensor:
     if device.type != "cuda":
         return t.to(device)
     return _RING.copy(t.contiguous(), device)
+
+
+def h2d_into(out: torch.Tensor, x) -> torch.Tensor:
+    """Stream-ordered copy of a host array into an existing device tensor
+    (e.g. a captured HIP graph's static input) through the pinned ring."""
+    t = x if torch.is_tensor(x) else torch.from_numpy(np.ascontiguousarray(x))
+    t = t.to(out.dtype).reshape(out.shape).contiguous()
+    if out.device.type != "cuda":
+        out.copy_(t)
+        return out
+    return _RING.copy_into(t, out)
 
 
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:

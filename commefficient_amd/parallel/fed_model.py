@@ -41,6 +41,7 @@ from ..ops import CSVec
 from ..utils.logging import PhaseTimer
 from . import dist
 from .flat import FlatParams
+from .graph import RoundGraphs
 from .server import ServerState
 from .state import ByteAccountant, ClientStateStore
 
@@ -60,6 +61,11 @@ class RoundBatch:
         self.client_ids = np.asarray(client_ids, dtype=np.int64)
         self._take = take_fn
         self.n_inputs = n_inputs
+        # optional HIP-graph hooks (device loaders): graph_index(pos) -> host
+        # int64 [2, n] staged into a static buffer; graph_gather(idx2) -> the
+        # model inputs + targets computed from that buffer on the device
+        self.graph_index = None
+        self.graph_gather = None
 
     def __len__(self):
         return len(self.client_ids)
@@ -141,6 +147,7 @@ class FedModel:
         self._payload = None
         self._work = None  # separate work buffer for topk_down / fedavg
         self.last_round = {}
+        self.graphs = RoundGraphs(self) if self.device.type == "cuda" else None
 
     # ------------------------------------------------------------------ API
     def attach_optimizer(self, opt):
@@ -199,9 +206,11 @@ class FedModel:
             return False
         return True
 
-    def _autocast(self):
+    def _autocast(self, cache: bool = True):
         if self.use_bf16:
-            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+            # no cast cache while a HIP graph is captured (the cached casts
+            # would outlive the capture's memory pool)
+            return torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=cache)
         return nullcontext()
 
     def _prep(self, xs):
@@ -230,12 +239,12 @@ class FedModel:
         return clients[R * W // N:(R + 1) * W // N]
 
     def _fwd_bwd(self, inputs, targets, loss_weight: Optional[float], groups: int = 1,
-                 want_grad=True):
+                 want_grad=True, capture: bool = False):
         """Forward (+backward) of one (micro)batch.  ``loss_weight`` None ->
         backward of the SUM of per-example losses; else of
         ``loss_weight * sum`` (per-client mean normalisation).  Returns the
         per-example losses and metrics (detached)."""
-        with self._autocast():
+        with self._autocast(cache=not capture):
             with (ghost_batchnorm(self.model, groups) if (groups > 1 and self.has_bn)
                   else nullcontext()):
                 per_ex, metrics = self.compute_loss_train(self.model, self._prep(inputs), targets,
@@ -271,6 +280,13 @@ class FedModel:
         if merged and self.has_bn:
             sizes = counts[my_slots]
             merged = bool(np.all(sizes == sizes[0]))
+        if merged and self.graphs is not None:
+            n_local = int(counts[my_slots].sum())
+            if self.graphs.usable(rb, n_local):
+                gkey = self.graphs.key(rb, n_local, W, B)
+                if self.graphs.seen(gkey) and getattr(self, "_n_metrics", None) is not None:
+                    return self._train_graph(gkey, rb, order, starts, my_slots, counts, W, B,
+                                             clients)
         # metric slots: [n_metrics, W] appended to the payload; allocate after
         # we know n_metrics -> run compute first into a local list
         with self.timer.phase("compute"):
@@ -295,10 +311,68 @@ class FedModel:
         # clone: the payload buffer is reused by the next round
         metrics = payload[self.main_numel:].view(n_res, W).clone()
         dl, ul = self.accountant.round(clients, self.round_idx)
-        self._pending = (G, clients)
+        self._pending = (G, clients, False)
         self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
                            "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel())}
         return [metrics[i] for i in range(n_res)] + [dl, ul]
+
+    def _train_graph(self, gkey, rb, order, starts, my_slots, counts, W, B, clients):
+        """The merged round through the captured HIP graphs (parallel/graph.py)."""
+        pos, slot_per_ex = self._merged_positions(order, starts, my_slots, counts)
+        n_res = self._n_metrics
+        payload = self.graphs.compute(gkey, rb, pos, slot_per_ex, counts, W, B, n_res)
+        dist.all_reduce_(payload)
+        G = payload[:self.main_numel]  # scaled by 1/B inside the server graph
+        metrics = payload[self.main_numel:].view(n_res, W).clone()
+        dl, ul = self.accountant.round(clients, self.round_idx)
+        self._pending = (G, clients, True)
+        self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
+                           "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel()),
+                           "graph": True}
+        return [metrics[i] for i in range(n_res)] + [dl, ul]
+
+    @staticmethod
+    def _merged_positions(order, starts, my_slots, counts):
+        pos = np.concatenate([order[starts[s]:starts[s + 1]] for s in my_slots]) \
+            if len(my_slots) else np.zeros(0, dtype=np.int64)
+        slot_per_ex = np.concatenate([np.full(counts[s], s) for s in my_slots]) \
+            if len(my_slots) else np.zeros(0, dtype=np.int64)
+        return pos, slot_per_ex.astype(np.int64)
+
+    def _metric_sums(self, rows, slots_t, n_t, W):
+        """Per-client mean loss / metrics in their global client slots."""
+        msum = torch.zeros(len(rows), W, device=self.device)
+        for i, r in enumerate(rows):
+            msum[i].index_add_(0, slots_t, r)
+        msum /= n_t
+        return msum
+
+    def _encode_merged(self, out: torch.Tensor, n_local: int):
+        """transmit = grad(sum loss) + (wd/W) * n_local * w  (utils.py:257-258,
+        fed_worker.py:190), Count-Sketched or dense into ``out``."""
+        a = self.args
+        wscale = a.weight_decay / a.num_workers * n_local
+        if a.mode == "sketch":
+            out.zero_()
+            sk = self.sketch.like(out.view(a.num_rows, a.num_cols))
+            sk.accumulateVec(self.flat.g, 1.0, self.w if wscale != 0 else None, wscale,
+                             dense=a.encode != "direct")
+        else:
+            # fedavg (single local step): sum_i (w - (w - lr g_i)) n_i = lr * transmit
+            s = self.fedavg_lr if a.mode == "fedavg" else 1.0
+            ops.axpby(out, self.flat.g, s, self.w if wscale != 0 else None, s * wscale)
+
+    def _merged_body(self, get_data, slots_t, n_t, n_local: int, W: int, payload: torch.Tensor,
+                     capture: bool = False):
+        """Whole merged-client round up to the all-reduce, on device inputs only
+        (captured into a HIP graph by parallel/graph.py)."""
+        self.flat.zero_grad()
+        data = get_data()
+        inputs, targets = data[:-1], data[-1]
+        pe, ms = self._fwd_bwd(inputs, targets, None, groups=1, capture=capture)
+        msum = self._metric_sums([pe] + ms, slots_t, n_t, W)
+        self._encode_merged(payload[:self.main_numel], n_local)
+        payload[self.main_numel:].copy_(msum.reshape(-1))
 
     def _transmit_buffer(self) -> torch.Tensor:
         buf = self._payload_buf(0)[:self.main_numel]
@@ -308,10 +382,7 @@ class FedModel:
         """One forward/backward over all of this rank's clients (exact for the
         linear modes, see module docstring)."""
         a = self.args
-        pos = np.concatenate([order[starts[s]:starts[s + 1]] for s in my_slots]) \
-            if len(my_slots) else np.zeros(0, dtype=np.int64)
-        slot_per_ex = np.concatenate([np.full(counts[s], s) for s in my_slots]) \
-            if len(my_slots) else np.zeros(0, dtype=np.int64)
+        pos, slot_per_ex = self._merged_positions(order, starts, my_slots, counts)
         n_local = len(pos)
         self.flat.zero_grad()
         data = rb.take(pos)
@@ -334,24 +405,11 @@ class FedModel:
         # per-client mean metrics into their global slots
         slots_t = dist.h2d(slot_per_ex, self.device)
         n_t = dist.h2d(counts.astype(np.float32), self.device)
-        rows = [per_ex] + mets
-        msum = torch.zeros(len(rows), W, device=self.device)
-        for i, r in enumerate(rows):
-            msum[i].index_add_(0, slots_t, r)
-        msum /= n_t
-        # transmit = grad(sum loss) + (wd/W) * n_local * w   (utils.py:257-258, fed_worker.py:190)
-        wscale = a.weight_decay / a.num_workers * n_local
+        msum = self._metric_sums([per_ex] + mets, slots_t, n_t, W)
+        self._n_metrics = msum.shape[0]
         out = self._transmit_buffer()
         with self.timer.phase("encode"):
-            if a.mode == "sketch":
-                out.zero_()
-                sk = self.sketch.like(out.view(a.num_rows, a.num_cols))
-                sk.accumulateVec(self.flat.g, 1.0, self.w if wscale != 0 else None, wscale,
-                                 dense=a.encode != "direct")
-            else:
-                # fedavg (single local step): sum_i (w - (w - lr g_i)) n_i = lr * transmit
-                s = self.fedavg_lr if a.mode == "fedavg" else 1.0
-                ops.axpby(out, self.flat.g, s, self.w if wscale != 0 else None, s * wscale)
+            self._encode_merged(out, n_local)
         return out, msum
 
     def _client_grad(self, inputs, targets, n: int, work: torch.Tensor):
@@ -515,8 +573,12 @@ class FedModel:
     def server_step(self, lr):
         if self._pending is None:
             return  # e.g. the reference's "HACK STEP" before the first round
-        G, clients = self._pending
+        G, clients, via_graph = self._pending
         self._pending = None
+        if via_graph:
+            self.graphs.server(G, float(lr), self.round_idx)
+            self.round_idx += 1
+            return
         if self.args.mode == "fedavg":
             if torch.is_tensor(lr):
                 raise ValueError("fedavg supports a scalar LR only (fed_aggregator.py:441-444)")
