@@ -26,6 +26,8 @@ import time
 import numpy as np
 import torch
 
+import commefficient_amd  # noqa: F401  (sets HIP runtime env before the GPU initialises)
+
 METRIC = "images/sec + bytes/step, ResNet-9 CIFAR-10 FetchSGD at 1/2/4/8 MI355X"
 
 
@@ -41,7 +43,7 @@ def main():
     p.add_argument("--conv", default="native", choices=["native", "miopen"],
                    help="3x3 conv units on the native MFMA kernels or on MIOpen")
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
-    p.add_argument("--graph", default="off", choices=["on", "off"],
+    p.add_argument("--graph", default="off", choices=["auto", "on", "off"],
                    help="HIP-graph replay of the round (parallel/graph.py)")
     p.add_argument("--torch-profile", default=None,
                    help="after the timed steps, trace 5 more with torch.profiler into this dir")

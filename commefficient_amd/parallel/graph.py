@@ -22,13 +22,18 @@ round index) which the apply kernels read on the device.  The augmentation
 seed is folded into the keys (data/device_loader.py ``gather_device``), so
 replays are bit-identical to the eager path.
 
-STATUS (experimental, off by default): the first replay of both graphs is
-bitwise identical to the eager round at the ResNet-9 bench geometry
-(scripts/dev/graph_cmp.py), and small geometries replay correctly for many
-rounds (tests/test_graph.py), but at the bench geometry the SECOND replay of
-the compute graph raises a memory-access fault.  Ruled out so far: the
-empty_cache() of torch.cuda.graph (capture is done by hand, below), the
-80 KB-LDS conv tile, hipBLASLt (a BLAS-free head faults too).
+ROCm note: with ROCclr's graph packet capture (AQL packets pre-built at
+instantiation, the default in ROCm 7.2) the SECOND launch of the compute
+graph at the ResNet-9 bench geometry raises a memory-access fault, although
+the first launch is bitwise identical to the eager round
+(scripts/dev/graph_cmp.py); with DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 (set by
+``commefficient_amd/__init__.py`` before HIP initialises) every replay is
+correct.  Graphs are therefore only used when that variable is 0.
+
+Measured (1x MI355X, bench.py, 50 rounds): 176.9k img/s replayed vs 176.5k
+eager, host enqueue 2.44 vs 2.39 ms/round -- without packet capture the
+runtime dispatches each node much like an eager launch, and the GPU (not
+the host) bounds this round, so capture is off by default (``--graph on``).
 
 A geometry is first run eagerly (lazy initialisation: sketch plans, kernel
 attributes, library handles), captured the second time it is seen, and
@@ -38,6 +43,8 @@ groups, the phase timer).
 """
 from __future__ import annotations
 
+import os
+import warnings
 from typing import Dict, Optional, Tuple
 
 import numpy as np
@@ -98,8 +105,12 @@ class RoundGraphs:
     def __init__(self, fed_model):
         self.fm = fed_model
         a = fed_model.args
-        self.enabled = (fed_model.device.type == "cuda" and
-                        str(getattr(a, "graph", "off")).lower() in ("on", "auto", "1", "true"))
+        want = str(getattr(a, "graph", "auto")).lower()
+        safe = os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0"
+        if want == "on" and not safe:
+            warnings.warn("--graph on ignored: DEBUG_CLR_GRAPH_PACKET_CAPTURE must be 0 before "
+                          "HIP initialises (import commefficient_amd first)")
+        self.enabled = fed_model.device.type == "cuda" and want in ("on", "auto") and safe
         self.pool = None
         self.entries: Dict[Tuple, _Entry] = {}
         self.step = torch.zeros(2, dtype=torch.int32, device=fed_model.device) \

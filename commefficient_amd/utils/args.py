@@ -157,11 +157,10 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--conv", choices=["native", "miopen"], default="native",
                    help="3x3 conv(+relu+pool) units: native MFMA kernels (csrc/conv.hip) "
                         "where shapes fit, or MIOpen everywhere")
-    g.add_argument("--graph", choices=["on", "off"], default="off",
+    g.add_argument("--graph", choices=["auto", "on", "off"], default="off",
                    help="replay merged-client rounds from captured HIP graphs "
-                        "(parallel/graph.py) once a round geometry repeats (experimental: "
-                        "the second replay of the compute graph faults at the ResNet-9 bench "
-                        "geometry on ROCm 7.2, see the module docstring)")
+                        "(parallel/graph.py) once a round geometry repeats (auto/on: "
+                        "eligible configurations; measured throughput-neutral for ResNet-9)")
     g.add_argument("--gpt2_size", choices=["small", "tiny"], default="small",
                    help="GPT-2 architecture: 'small' = 124M GPT-2 (reference), 'tiny' for tests")
     return p

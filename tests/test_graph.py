@@ -1,18 +1,13 @@
 """HIP-graph replay of merged-client rounds (parallel/graph.py) must reproduce
 the eager round exactly: same weights, server state, metrics and download
 accounting after several rounds with a changing LR."""
-import os
-
 import pytest
 import torch
 
-# opt-in until the graph path is unconditionally safe (parallel/graph.py STATUS)
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("COMMEFF_TEST_GRAPH") != "1",
-                                 reason="experimental HIP-graph path; set COMMEFF_TEST_GRAPH=1")]
+pytestmark = pytest.mark.gpu
 
 
-def _run(graph: str, mode: str, rounds: int = 5):
+def _run(graph: str, mode: str, rounds: int = 6):
     from commefficient_amd import models
     from commefficient_amd.data import make_synthetic
     from commefficient_amd.data.device_loader import DeviceFedLoader
@@ -43,7 +38,12 @@ def _run(graph: str, mode: str, rounds: int = 5):
     losses = []
     for r in range(rounds):
         opt.param_groups[0]["lr"] = 0.1 / (1 + r)  # the LR reaches the graph via `step`
-        out = fed(next(it))
+        try:
+            rb = next(it)
+        except StopIteration:  # next epoch
+            it = iter(loader)
+            rb = next(it)
+        out = fed(rb)
         fopt.step()
         losses.append(out[0].clone())
     torch.cuda.synchronize()
