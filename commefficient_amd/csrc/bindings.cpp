@@ -159,28 +159,37 @@ static const int32_t* step_ptr(const c10::optional<at::Tensor>& step) {
   return step->data_ptr<int32_t>();
 }
 
+static int32_t* hist_ptr(const c10::optional<at::Tensor>& hist) {
+  if (!hist.has_value() || !hist->defined()) return nullptr;
+  TORCH_CHECK(hist->scalar_type() == at::kInt && hist->is_contiguous(), "hist must be contiguous int32");
+  return hist->data_ptr<int32_t>();
+}
+
 void sparse_apply_cpu(at::Tensor w, const at::Tensor& idx, const at::Tensor& vals, double lr,
                       const c10::optional<at::Tensor>& lr_vec,
                       const c10::optional<at::Tensor>& last_mod, int64_t round,
-                      const c10::optional<at::Tensor>& step) {
+                      const c10::optional<at::Tensor>& step,
+                      const c10::optional<at::Tensor>& hist) {
   read_step(step, lr, round);
   check_f32(w, "w");
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   cpu::sparse_apply(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                     idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
-                    static_cast<int32_t>(round));
+                    static_cast<int32_t>(round), hist_ptr(hist));
 }
 
 void dense_apply_cpu(at::Tensor w, const at::Tensor& delta, double lr,
                      const c10::optional<at::Tensor>& lr_vec,
                      const c10::optional<at::Tensor>& last_mod, int64_t round,
-                     const c10::optional<at::Tensor>& step) {
+                     const c10::optional<at::Tensor>& step,
+                     const c10::optional<at::Tensor>& hist) {
   read_step(step, lr, round);
   check_f32(w, "w");
   check_f32(delta, "delta");
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   cpu::dense_apply(w.data_ptr<float>(), delta.data_ptr<float>(), w.numel(),
-                   static_cast<float>(lr), fptr(lr_vec), lm, static_cast<int32_t>(round));
+                   static_cast<float>(lr), fptr(lr_vec), lm, static_cast<int32_t>(round),
+                   hist_ptr(hist));
 }
 
 at::Tensor count_ge_cpu(const at::Tensor& last_mod, const at::Tensor& thr) {
@@ -361,26 +370,28 @@ void momentum_ef_hip(at::Tensor V, const c10::optional<at::Tensor>& E, const at:
 void sparse_apply_hip(at::Tensor w, const at::Tensor& idx, const at::Tensor& vals, double lr,
                       const c10::optional<at::Tensor>& lr_vec,
                       const c10::optional<at::Tensor>& last_mod, int64_t round,
-                      const c10::optional<at::Tensor>& step) {
+                      const c10::optional<at::Tensor>& step,
+                      const c10::optional<at::Tensor>& hist) {
   check_f32(w, "w");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   launch_sparse_apply(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                       idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
-                      static_cast<int32_t>(round), step_ptr(step), cur_stream());
+                      static_cast<int32_t>(round), step_ptr(step), hist_ptr(hist), cur_stream());
 }
 
 void dense_apply_hip(at::Tensor w, const at::Tensor& delta, double lr,
                      const c10::optional<at::Tensor>& lr_vec,
                      const c10::optional<at::Tensor>& last_mod, int64_t round,
-                     const c10::optional<at::Tensor>& step) {
+                     const c10::optional<at::Tensor>& step,
+                     const c10::optional<at::Tensor>& hist) {
   check_f32(w, "w");
   check_f32(delta, "delta");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   launch_dense_apply(w.data_ptr<float>(), delta.data_ptr<float>(), w.numel(),
                      static_cast<float>(lr), fptr(lr_vec), lm, static_cast<int32_t>(round),
-                     step_ptr(step), cur_stream());
+                     step_ptr(step), hist_ptr(hist), cur_stream());
 }
 
 at::Tensor count_ge_hip(const at::Tensor& last_mod, const at::Tensor& thr) {
@@ -393,6 +404,37 @@ at::Tensor count_ge_hip(const at::Tensor& last_mod, const at::Tensor& thr) {
     launch_count_ge(last_mod.data_ptr<int32_t>(), last_mod.numel(), thr_c.data_ptr<int32_t>(), T,
                     buf.data_ptr<int64_t>(), cur_stream());
   return buf.narrow(0, T + 1, T);
+}
+
+static void check_account_hist(const at::Tensor& hist, const at::Tensor& meta, int64_t W,
+                               const at::Tensor& client_dl, const at::Tensor& client_ul) {
+  TORCH_CHECK(hist.scalar_type() == at::kInt && hist.is_contiguous() && hist.dim() == 1,
+              "account_hist: hist int32 [bins]");
+  TORCH_CHECK(meta.scalar_type() == at::kLong && meta.is_contiguous() && meta.numel() == 2 * W &&
+                  meta.device() == hist.device(), "account_hist: meta = [last_seen | clients]");
+  TORCH_CHECK(client_dl.scalar_type() == at::kDouble && client_ul.scalar_type() == at::kDouble &&
+                  client_dl.is_contiguous() && client_ul.is_contiguous(), "account_hist: totals");
+}
+
+at::Tensor account_hist_cpu(const at::Tensor& hist, const at::Tensor& meta, int64_t W,
+                            at::Tensor client_dl, at::Tensor client_ul, double upc) {
+  check_account_hist(hist, meta, W, client_dl, client_ul);
+  auto dl = at::empty({W}, hist.options().dtype(at::kDouble));
+  cpu::account_hist(hist.data_ptr<int32_t>(), static_cast<int>(hist.numel()), meta.data_ptr<int64_t>(),
+                    static_cast<int>(W), client_dl.data_ptr<double>(), client_ul.data_ptr<double>(),
+                    upc, dl.data_ptr<double>());
+  return dl;
+}
+
+at::Tensor account_hist_hip(const at::Tensor& hist, const at::Tensor& meta, int64_t W,
+                            at::Tensor client_dl, at::Tensor client_ul, double upc) {
+  check_account_hist(hist, meta, W, client_dl, client_ul);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(hist.device());
+  auto dl = at::empty({W}, hist.options().dtype(at::kDouble));
+  launch_account_hist(hist.data_ptr<int32_t>(), static_cast<int>(hist.numel()), meta.data_ptr<int64_t>(),
+                      static_cast<int>(W), client_dl.data_ptr<double>(), client_ul.data_ptr<double>(),
+                      upc, dl.data_ptr<double>(), cur_stream());
+  return dl;
 }
 
 at::Tensor account_round_hip(const at::Tensor& last_mod, const at::Tensor& meta, int64_t T, int64_t W,
@@ -685,6 +727,8 @@ at::Tensor conv3x3_fwd_impl(const at::Tensor& x, const at::Tensor& w, bool relu,
   a.K = static_cast<int>(K);
   a.relu = relu ? 1 : 0;
   a.y_pre = nullptr;
+  a.pool_idx = nullptr;
+  a.pool = 0;
   if (pre != nullptr) {
     TORCH_CHECK(a.addend != nullptr, "conv3x3: the pre-add output needs an addend");
     *pre = at::empty_like(y, y.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -698,6 +742,42 @@ at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
                            const c10::optional<at::Tensor>& mask,
                            const c10::optional<at::Tensor>& addend) {
   return conv3x3_fwd_impl(x, w, relu, mask, addend, nullptr);
+}
+
+// y = maxpool2(relu(conv3x3(x, w))) [N, K, H/2, W/2] (channels_last) and the
+// 1-byte window codes of csrc/pool.hip (for relu_maxpool_backward)
+std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_pool2_hip(const at::Tensor& x, const at::Tensor& w) {
+  check_nhwc_bf16(x, "conv3x3_pool: x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 &&
+                  w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C,
+              "conv3x3_pool: w must be contiguous bf16 [K, 3, 3, C]");
+  const int64_t K = w.size(0);
+  TORCH_CHECK(conv3x3_supported(static_cast<int>(C), static_cast<int>(K)) &&
+                  conv3x3_pool_supported(static_cast<int>(H), static_cast<int>(W), static_cast<int>(K)),
+              "conv3x3_pool: unsupported shape");
+  TORCH_CHECK(N * H * W < (1ll << 31), "conv3x3_pool: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, K, H / 2, W / 2}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({N, K, H / 2, W / 2},
+                       x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  ConvFwdArgs a{};
+  a.x = bf16_ptr(x);
+  a.w = bf16_ptr(w);
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.mask = nullptr;
+  a.addend = nullptr;
+  a.y_pre = nullptr;
+  a.pool_idx = idx.data_ptr<uint8_t>();
+  a.P = static_cast<int>(N * H * W);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.relu = 1;
+  a.pool = 2;
+  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  return {y, idx};
 }
 
 // fused per-example cross-entropy: (loss f32 [B], correct f32 [B], softmax - onehot [B, C])
@@ -938,6 +1018,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
+  m.def("conv3x3_fwd_pool2(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
@@ -958,9 +1039,11 @@ TORCH_LIBRARY(commeff, m) {
   m.def("topk_abs(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
   m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "
-        "Tensor(b!)? last_mod, int round, Tensor? step=None) -> ()");
+        "Tensor(b!)? last_mod, int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");
   m.def("dense_apply(Tensor(a!) w, Tensor delta, float lr, Tensor? lr_vec, Tensor(b!)? last_mod, "
-        "int round, Tensor? step=None) -> ()");
+        "int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");
+  m.def("account_hist(Tensor hist, Tensor meta, int W, Tensor(a!) client_dl, Tensor(b!) client_ul, "
+        "float upc) -> Tensor");
   m.def("count_ge(Tensor last_mod, Tensor thr) -> Tensor");
   m.def("axpby(Tensor(a!) out, Tensor a, float alpha, Tensor? b, float beta) -> ()");
   m.def("l2norm(Tensor x) -> Tensor");
@@ -983,6 +1066,7 @@ TORCH_LIBRARY_IMPL(commeff, CPU, m) {
   m.impl("topk_abs", &topk_abs_cpu);
   m.impl("momentum_ef", &momentum_ef_cpu);
   m.impl("sparse_apply", &sparse_apply_cpu);
+  m.impl("account_hist", &account_hist_cpu);
   m.impl("dense_apply", &dense_apply_cpu);
   m.impl("count_ge", &count_ge_cpu);
   m.impl("axpby", &axpby_cpu);
@@ -1006,6 +1090,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("relu_maxpool", &relu_maxpool_hip);
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("conv3x3_fwd", &conv3x3_fwd_hip);
+  m.impl("conv3x3_fwd_pool2", &conv3x3_fwd_pool2_hip);
   m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
   m.impl("ce_fwd", &ce_fwd_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
@@ -1021,6 +1106,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("topk_abs", &topk_abs_hip);
   m.impl("momentum_ef", &momentum_ef_hip);
   m.impl("sparse_apply", &sparse_apply_hip);
+  m.impl("account_hist", &account_hist_hip);
   m.impl("dense_apply", &dense_apply_hip);
   m.impl("count_ge", &count_ge_hip);
   m.impl("account_round", &account_round_hip);

@@ -62,7 +62,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // ------------------------------------------------------------ fwd / dgrad
-template <int TBM, int BN, int NSTAGE>
+template <int TBM, int BN, int NSTAGE, bool POOL = false>
 __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NT = TBM * 2;                   // (TBM/64) x 2 waves
@@ -213,6 +213,61 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
       }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-byte output chunks per row
+  if constexpr (POOL) {
+    // fused ReLU + 2x2 max-pool (csrc/pool.hip semantics): the tile holds
+    // whole image-row pairs (TBM % 2W == 0, m0 % 2W == 0), so its pooled
+    // outputs are the contiguous pooled pixels [m0/4, (m0+TBM)/4).  Values are
+    // compared after bf16 rounding (as the unfused path pools the stored bf16
+    // conv output); code = window position of the max, 255 when max <= 0.
+    const int W = a.W, OWl = W >> 1;
+    const int q0 = m0 >> 2;
+#pragma unroll 1
+    for (int e = tid; e < (TBM / 4) * CPR; e += NT) {
+      const int pq = e / CPR, cc = e - pq * CPR;
+      const int r2 = pq / OWl, ow = pq - r2 * OWl;
+      const int row0 = 2 * r2 * W + 2 * ow;
+      if (m0 + row0 >= a.P) continue;
+      float best[8];
+      uint32_t arg[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        best[j] = -__builtin_huge_valf();
+        arg[j] = 0;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float* src = ct + (row0 + (t >> 1) * W + (t & 1)) * LD + cc * 8;
+        const float4 lo = *reinterpret_cast<const float4*>(src);
+        const float4 up = *reinterpret_cast<const float4*>(src + 4);
+        const uint32_t pk[4] = {pack_bf16(lo.x, lo.y), pack_bf16(lo.z, lo.w), pack_bf16(up.x, up.y),
+                                pack_bf16(up.z, up.w)};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f((pk[j >> 1] >> (16 * (j & 1))) & 0xffffu);
+          if (f > best[j]) {
+            best[j] = f;
+            arg[j] = static_cast<uint32_t>(t);
+          }
+        }
+      }
+      v4u out;
+      uint64_t codes = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const bool p0 = best[j] > 0.f, p1 = best[j + 1] > 0.f;
+        // the maxima are bf16 values: exact upper halves
+        const uint32_t h0 = p0 ? (__float_as_uint(best[j]) >> 16) : 0u;
+        const uint32_t h1 = p1 ? (__float_as_uint(best[j + 1]) >> 16) : 0u;
+        out[j >> 1] = h0 | (h1 << 16);
+        codes |= static_cast<uint64_t>(p0 ? arg[j] : 255u) << (8 * j);
+        codes |= static_cast<uint64_t>(p1 ? arg[j + 1] : 255u) << (8 * (j + 1));
+      }
+      const size_t o = static_cast<size_t>(q0 + pq) * a.K + n0 + cc * 8;
+      *reinterpret_cast<v4u*>(a.y + o) = out;
+      *reinterpret_cast<uint64_t*>(a.pool_idx + o) = codes;
+    }
+    return;
+  }
   const bool relu = a.relu != 0;
 #pragma unroll 2
   for (int e = tid; e < TBM * CPR; e += NT) {
@@ -542,19 +597,19 @@ void set_lds(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-template <int TBM, int BN, int NSTAGE>
+template <int TBM, int BN, int NSTAGE, bool POOL = false>
 void launch_fwd(const ConvFwdArgs& a, hipStream_t stream) {
   constexpr int lds_pipe = NSTAGE * (TBM * 128 + BN * 128);
   constexpr int lds_epi = TBM * (BN + 4) * 4;
   constexpr int lds = lds_pipe > lds_epi ? lds_pipe : lds_epi;
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_kernel<TBM, BN, NSTAGE>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_kernel<TBM, BN, NSTAGE, POOL>), lds);
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  hipLaunchKernelGGL((conv_fwd_kernel<TBM, BN, NSTAGE>), dim3(mt * (a.K / BN)), dim3(TBM * 2), lds,
-                     stream, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<TBM, BN, NSTAGE, POOL>), dim3(mt * (a.K / BN)), dim3(TBM * 2),
+                     lds, stream, a);
 }
 
 template <int BN, int NSTAGE, bool ROWSTEP>
@@ -574,9 +629,17 @@ void launch_wgrad(const ConvWgradArgs& a, hipStream_t stream) {
 
 bool conv3x3_supported(int C, int K) { return C % 64 == 0 && K % 64 == 0 && C >= 64 && K >= 64; }
 
+bool conv3x3_pool_supported(int H, int W, int K) {
+  return K % 128 == 0 && H % 2 == 0 && W % 2 == 0 && 128 % (2 * W) == 0;
+}
+
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
+  if (a.pool == 2) {  // caller checked conv3x3_pool_supported
+    launch_fwd<128, 128, 2, true>(a, stream);
+    return;
+  }
   const bool wide = a.K % 128 == 0;
   const int bn = wide ? 128 : 64;
   // tile override for tuning experiments: COMMEFF_CONV_CFG = 256_3 | 256_2 | 128_3 | 128_2

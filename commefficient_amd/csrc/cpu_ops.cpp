@@ -144,26 +144,57 @@ void momentum_ef(float* V, float* E, const float* G, int64_t n, float rho, float
 }
 
 void sparse_apply(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
-                  const float* lr_vec, int32_t* last_mod, int32_t round) {
+                  const float* lr_vec, int32_t* last_mod, int32_t round, int32_t* hist) {
   for (int64_t q = 0; q < k; ++q) {
     int64_t i = idx[q];
     float l = lr_vec ? lr_vec[i] : lr;
     float old = w[i], nw = old - l * vals[q];
     w[i] = nw;
-    if (last_mod && nw != old) last_mod[i] = round;
+    if (last_mod && nw != old) {
+      const int32_t from = last_mod[i];
+      last_mod[i] = round;
+      if (hist && from != round) {
+        --hist[from + 1];
+        ++hist[round + 1];
+      }
+    }
   }
 }
 
 void dense_apply(float* w, const float* delta, int64_t n, float lr, const float* lr_vec,
-                 int32_t* last_mod, int32_t round) {
-  at::parallel_for(0, n, 1 << 14, [&](int64_t a, int64_t b) {
+                 int32_t* last_mod, int32_t round, int32_t* hist) {
+  // serial when the change histogram is maintained (shared counters)
+  const int64_t grain = hist ? n + 1 : (1 << 14);
+  at::parallel_for(0, n, grain, [&](int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i) {
       float l = lr_vec ? lr_vec[i] : lr;
       float old = w[i], nw = old - l * delta[i];
       w[i] = nw;
-      if (last_mod && nw != old) last_mod[i] = round;
+      if (last_mod && nw != old) {
+        const int32_t from = last_mod[i];
+        last_mod[i] = round;
+        if (hist && from != round) {
+          --hist[from + 1];
+          ++hist[round + 1];
+        }
+      }
     }
   });
+}
+
+void account_hist(const int32_t* hist, int nbins, const int64_t* meta, int W, double* client_dl,
+                  double* client_ul, double upc, double* dl) {
+  std::vector<int64_t> suffix(nbins + 1, 0);
+  for (int b = nbins - 1; b >= 0; --b) suffix[b] = suffix[b + 1] + hist[b];
+  for (int j = 0; j < W; ++j) {
+    int64_t b0 = meta[j] + 1;
+    if (b0 < 0) b0 = 0;
+    const double v = 4.0 * static_cast<double>(b0 < nbins ? suffix[b0] : 0);
+    const int64_t c = meta[W + j];
+    dl[j] = v;
+    client_dl[c] += v;
+    client_ul[c] += upc;
+  }
 }
 
 void count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr, int T, int64_t* out) {

@@ -18,9 +18,11 @@ void topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals);
 void momentum_ef(float* V, float* E, const float* G, int64_t n, float rho, float gscale,
                  int mode);
 void sparse_apply(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
-                  const float* lr_vec, int32_t* last_mod, int32_t round);
+                  const float* lr_vec, int32_t* last_mod, int32_t round, int32_t* hist);
 void dense_apply(float* w, const float* delta, int64_t n, float lr, const float* lr_vec,
-                 int32_t* last_mod, int32_t round);
+                 int32_t* last_mod, int32_t round, int32_t* hist);
+void account_hist(const int32_t* hist, int nbins, const int64_t* meta, int W, double* client_dl,
+                  double* client_ul, double upc, double* dl);
 void count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr, int T, int64_t* out);
 void axpby(float* out, const float* a, float alpha, const float* b, float beta, int64_t n);
 float l2norm(const float* x, int64_t n);

@@ -62,40 +62,172 @@ __global__ void momentum_ef_tail(float* V, float* E, const float* G, int64_t sta
 }
 
 // ----------------------------------------------------------------- apply
-__global__ void __launch_bounds__(kBlock)
+// Change histogram for download accounting: hist[r + 1] = #{i : last_mod[i]
+// == r} (bin 0: never changed).  A coordinate whose stamp moves from `from`
+// to `round` leaves bin from+1 and enters bin round+1.  The moves of a block
+// are first counted in an LDS window -- bin 0 and the kHistWin most recent
+// rounds, where nearly all stamps live -- and flushed with one global atomic
+// per nonzero bin; only stamps older than the window go to global memory
+// directly.  A round's accounting is then a suffix sum over the bins
+// (account_hist) instead of a pass over d stamps.
+constexpr int kHistWin = 4095;  // LDS bins: [0] = never changed, [1..kHistWin] = recent rounds
+
+struct HistWin {
+  int32_t* lh;  // LDS, kHistWin + 1 bins
+  int32_t round;
+  // LDS slot of global bin b (b = from + 1), or -1 outside the window
+  __device__ __forceinline__ int slot(int32_t b) const {
+    if (b == 0) return 0;
+    const int32_t off = b - (round + 1 - (kHistWin - 1));  // recent bins [round+2-kHistWin, round+1]
+    return (off >= 0 && off < kHistWin) ? off + 1 : -1;
+  }
+  __device__ __forceinline__ int32_t bin(int s) const {
+    return s == 0 ? 0 : round + 1 - (kHistWin - 1) + (s - 1);
+  }
+};
+
+__device__ __forceinline__ void hist_init(int32_t* lh) {
+  for (int b = threadIdx.x; b <= kHistWin; b += blockDim.x) lh[b] = 0;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void hist_move(const HistWin& hw, int32_t* hist, bool moved, int32_t from) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t act = __ballot(moved);
+  if (act == 0) return;
+  const int leader = __ffsll(static_cast<long long>(act)) - 1;
+  // every mover enters bin round+1; the leader's source bin (usually the
+  // previous round) is aggregated over the wave, the rest one LDS atomic each
+  const int32_t b0 = __shfl(from, leader) + 1;
+  const uint64_t same = __ballot(moved && from + 1 == b0);
+  if (lane == leader) {
+    atomicAdd(hw.lh + hw.slot(hw.round + 1), static_cast<int32_t>(__popcll(act)));
+    const int s0 = hw.slot(b0);
+    if (s0 >= 0) atomicSub(hw.lh + s0, static_cast<int32_t>(__popcll(same)));
+    else atomicSub(hist + b0, static_cast<int32_t>(__popcll(same)));
+  }
+  if (moved && from + 1 != b0) {
+    const int s = hw.slot(from + 1);
+    if (s >= 0) atomicSub(hw.lh + s, 1);
+    else atomicSub(hist + from + 1, 1);
+  }
+}
+
+__device__ __forceinline__ void hist_flush(const HistWin& hw, int32_t* hist) {
+  __syncthreads();
+  for (int s = threadIdx.x; s <= kHistWin; s += blockDim.x) {
+    const int32_t v = hw.lh[s];
+    const int32_t b = hw.bin(s);
+    if (v != 0 && b >= 0) atomicAdd(hist + b, v);
+  }
+}
+
+constexpr int kApplyBlock = 1024;
+
+__global__ void __launch_bounds__(kApplyBlock)
 sparse_apply_kernel(float* __restrict__ w, const int64_t* __restrict__ idx,
                     const float* __restrict__ vals, int64_t k, float lr,
                     const float* __restrict__ lr_vec, int32_t* __restrict__ last_mod,
-                    int32_t round, const int32_t* __restrict__ step) {
-  int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
-  if (q >= k) return;
+                    int32_t round, const int32_t* __restrict__ step, int32_t* __restrict__ hist) {
+  __shared__ int32_t lh[kHistWin + 1];
+  const int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   if (step != nullptr) {  // graph replay: [lr bits, round] from device memory
     lr = __int_as_float(step[0]);
     round = step[1];
   }
-  int64_t i = idx[q];
-  float l = lr_vec != nullptr ? lr_vec[i] : lr;
-  float old = w[i];
-  float nw = old - l * vals[q];
-  w[i] = nw;
-  if (last_mod != nullptr && nw != old) last_mod[i] = round;
+  const HistWin hw{lh, round};
+  if (hist != nullptr) hist_init(lh);
+  bool moved = false;
+  int32_t from = 0;
+  if (q < k) {
+    const int64_t i = idx[q];
+    const float l = lr_vec != nullptr ? lr_vec[i] : lr;
+    const float old = w[i];
+    const float nw = old - l * vals[q];
+    w[i] = nw;
+    if (last_mod != nullptr && nw != old) {
+      from = last_mod[i];
+      last_mod[i] = round;
+      moved = from != round;
+    }
+  }
+  if (hist != nullptr) {
+    hist_move(hw, hist, moved, from);
+    hist_flush(hw, hist);
+  }
 }
 
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kApplyBlock)
 dense_apply_kernel(float* __restrict__ w, const float* __restrict__ delta, int64_t n, float lr,
                    const float* __restrict__ lr_vec, int32_t* __restrict__ last_mod,
-                   int32_t round, const int32_t* __restrict__ step) {
+                   int32_t round, const int32_t* __restrict__ step, int32_t* __restrict__ hist) {
+  __shared__ int32_t lh[kHistWin + 1];
   if (step != nullptr) {
     lr = __int_as_float(step[0]);
     round = step[1];
   }
+  const HistWin hw{lh, round};
+  if (hist != nullptr) hist_init(lh);
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
-    float l = lr_vec != nullptr ? lr_vec[i] : lr;
-    float old = w[i];
-    float nw = old - l * delta[i];
-    w[i] = nw;
-    if (last_mod != nullptr && nw != old) last_mod[i] = round;
+  // wave-uniform trip count (hist_move uses wave ballots)
+  for (int64_t base = blockIdx.x * static_cast<int64_t>(blockDim.x); base < n; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    bool moved = false;
+    int32_t from = 0;
+    if (i < n) {
+      const float l = lr_vec != nullptr ? lr_vec[i] : lr;
+      const float old = w[i];
+      const float nw = old - l * delta[i];
+      w[i] = nw;
+      if (last_mod != nullptr && nw != old) {
+        from = last_mod[i];
+        last_mod[i] = round;
+        moved = from != round;
+      }
+    }
+    if (hist != nullptr) hist_move(hw, hist, moved, from);
+  }
+  if (hist != nullptr) hist_flush(hw, hist);
+}
+
+// Round accounting from the change histogram (one block): per participating
+// client j, dl[j] = 4 * #{i : last_mod[i] >= last_seen_j} = 4 * sum of bins
+// >= last_seen_j + 1; running per-client totals updated.  meta = int64
+// [last_seen (W) | clients (W)].
+__global__ void __launch_bounds__(1024)
+account_hist_kernel(const int32_t* __restrict__ hist, int nbins, const int64_t* __restrict__ meta,
+                    int W, double* __restrict__ client_dl, double* __restrict__ client_ul,
+                    double upc, double* __restrict__ dl) {
+  __shared__ long long seg_suffix[1025];
+  const int seg = (nbins + 1023) / 1024;
+  const int t = threadIdx.x;
+  long long s = 0;
+  for (int b = t * seg; b < min(nbins, (t + 1) * seg); ++b) s += hist[b];
+  seg_suffix[t] = s;
+  if (t == 0) seg_suffix[1024] = 0;
+  __syncthreads();
+  // suffix scan over the 1024 segment sums (Hillis-Steele, in place)
+  for (int off = 1; off < 1024; off <<= 1) {
+    const long long v = t + off < 1024 ? seg_suffix[t + off] : 0;
+    __syncthreads();
+    seg_suffix[t] += v;
+    __syncthreads();
+  }
+  const int64_t* clients = meta + W;
+  for (int j = t; j < W; j += 1024) {
+    int64_t b0 = meta[j] + 1;  // first counted bin
+    if (b0 < 0) b0 = 0;
+    long long cnt = 0;
+    if (b0 < nbins) {
+      const int sg = static_cast<int>(b0 / seg);
+      cnt = seg_suffix[sg + 1];
+      for (int64_t b = b0; b < min<int64_t>(nbins, static_cast<int64_t>(sg + 1) * seg); ++b) cnt += hist[b];
+    }
+    const double v = 4.0 * static_cast<double>(cnt);
+    const int64_t c = clients[j];
+    dl[j] = v;
+    client_dl[c] += v;  // clients are unique within a round
+    client_ul[c] += upc;
   }
 }
 
@@ -371,18 +503,28 @@ void launch_momentum_ef(float* V, float* E, const float* G, int64_t n, float rho
 
 void launch_sparse_apply(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
                          const float* lr_vec, int32_t* last_mod, int32_t round,
-                         const int32_t* step, hipStream_t stream) {
+                         const int32_t* step, int32_t* hist, hipStream_t stream) {
   if (k <= 0) return;
-  hipLaunchKernelGGL(sparse_apply_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream,
-                     w, idx, vals, k, lr, lr_vec, last_mod, round, step);
+  hipLaunchKernelGGL(sparse_apply_kernel, dim3((k + kApplyBlock - 1) / kApplyBlock), dim3(kApplyBlock),
+                     0, stream, w, idx, vals, k, lr, lr_vec, last_mod, round, step, hist);
 }
 
 void launch_dense_apply(float* w, const float* delta, int64_t n, float lr, const float* lr_vec,
-                        int32_t* last_mod, int32_t round, const int32_t* step,
+                        int32_t* last_mod, int32_t round, const int32_t* step, int32_t* hist,
                         hipStream_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(dense_apply_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, w, delta, n,
-                     lr, lr_vec, last_mod, round, step);
+  int64_t nb = (n + kApplyBlock - 1) / kApplyBlock;
+  if (nb > 512) nb = 512;  // each block flushes its LDS histogram window once
+  hipLaunchKernelGGL(dense_apply_kernel, dim3(static_cast<int>(nb)), dim3(kApplyBlock), 0, stream, w,
+                     delta, n, lr, lr_vec, last_mod, round, step, hist);
+}
+
+void launch_account_hist(const int32_t* hist, int nbins, const int64_t* meta, int W,
+                         double* client_dl, double* client_ul, double upc, double* dl,
+                         hipStream_t stream) {
+  if (W <= 0) return;
+  hipLaunchKernelGGL(account_hist_kernel, dim3(1), dim3(1024), 0, stream, hist, nbins, meta, W,
+                     client_dl, client_ul, upc, dl);
 }
 
 void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr, int T, int64_t* counts,

@@ -102,13 +102,20 @@ void launch_momentum_ef(float* V, float* E, const float* G, int64_t n,
 void launch_sparse_apply(float* w, const int64_t* idx, const float* vals,
                          int64_t k, float lr, const float* lr_vec,
                          int32_t* last_mod, int32_t round, const int32_t* step,
-                         hipStream_t stream);
+                         int32_t* hist, hipStream_t stream);
 // w -= lr(i) * delta ; last_mod[i] = round where w changed
 // (step != nullptr: lr = bits of step[0], round = step[1], read on the device
 // so a captured HIP graph replays with the current round's values)
+// hist (optional): change histogram, hist[r+1] = #{i : last_mod[i] == r},
+// maintained incrementally as stamps move
 void launch_dense_apply(float* w, const float* delta, int64_t n, float lr,
                         const float* lr_vec, int32_t* last_mod, int32_t round,
-                        const int32_t* step, hipStream_t stream);
+                        const int32_t* step, int32_t* hist, hipStream_t stream);
+// per-client download bytes from the change histogram (meta = int64
+// [last_seen (W) | clients (W)])
+void launch_account_hist(const int32_t* hist, int nbins, const int64_t* meta, int W,
+                         double* client_dl, double* client_ul, double upc, double* dl,
+                         hipStream_t stream);
 // counts[t] = #{i : last_mod[i] >= thr[t]}  (thr sorted ascending, T <= 1024)
 void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr,
                      int T, int64_t* counts, hipStream_t stream);
@@ -149,8 +156,10 @@ struct ConvFwdArgs {
   const uint16_t* mask;    // optional [P, K]: y = 0 where mask <= 0
   const uint16_t* addend;  // optional [P, K]: y += addend (after relu / mask)
   uint16_t* y_pre;         // optional [P, K]: the value before the addend (with addend only)
+  uint8_t* pool_idx;       // pool == 2: y = maxpool2(relu(conv)) [P/4, K], codes [P/4, K]
   int P, H, W, C, K;
   int relu;
+  int pool;                // 0, or 2: fused relu + 2x2 max-pool epilogue (128 % (2W) == 0)
   FastDivU32 div_w, div_h;  // set by the launcher
 };
 struct ConvWgradArgs {
@@ -163,6 +172,7 @@ struct ConvWgradArgs {
   FastDivU32 div_w, div_h;
 };
 bool conv3x3_supported(int C, int K);
+bool conv3x3_pool_supported(int H, int W, int K);
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)

@@ -12,7 +12,7 @@ from .sketch import CSVec, make_hashes
 
 __all__ = ["CSVec", "make_hashes", "topk_abs", "topk_dense", "momentum_ef", "sparse_apply",
            "dense_apply", "count_ge", "axpby", "l2norm", "clip_noise", "client_state",
-           "zero_at", "scatter_dense", "augment_u8_nhwc", "account_round"]
+           "zero_at", "scatter_dense", "augment_u8_nhwc", "account_round", "account_hist"]
 
 ERROR_MODE = {"none": 0, "virtual": 1, "local": 2}
 
@@ -36,15 +36,25 @@ def momentum_ef(V: torch.Tensor, E: Optional[torch.Tensor], G: torch.Tensor, rho
     _ops().momentum_ef(V, E, G, float(rho), float(gscale), ERROR_MODE[error_type])
 
 
-def sparse_apply(w, idx, vals, lr, lr_vec=None, last_mod=None, round_idx: int = 0, step=None):
+def sparse_apply(w, idx, vals, lr, lr_vec=None, last_mod=None, round_idx: int = 0, step=None,
+                 hist=None):
     """w[idx] -= lr * vals; last_mod[idx] = round where w changed.  ``step``
     (int32 [2] = lr bits, round) overrides lr/round from device memory (HIP
-    graph replay)."""
-    _ops().sparse_apply(w, idx, vals, float(lr), lr_vec, last_mod, int(round_idx), step)
+    graph replay); ``hist`` (int32, hist[r+1] = #{i: last_mod[i] == r}) is
+    kept in step with the stamps."""
+    _ops().sparse_apply(w, idx, vals, float(lr), lr_vec, last_mod, int(round_idx), step, hist)
 
 
-def dense_apply(w, delta, lr, lr_vec=None, last_mod=None, round_idx: int = 0, step=None):
-    _ops().dense_apply(w, delta, float(lr), lr_vec, last_mod, int(round_idx), step)
+def dense_apply(w, delta, lr, lr_vec=None, last_mod=None, round_idx: int = 0, step=None,
+                hist=None):
+    _ops().dense_apply(w, delta, float(lr), lr_vec, last_mod, int(round_idx), step, hist)
+
+
+def account_hist(hist, meta, W: int, client_dl, client_ul, upload_per_client: float):
+    """Round accounting from the change histogram: meta = int64 [last_seen (W) |
+    clients (W)]; returns per-client download bytes 4 * #{i : last_mod[i] >=
+    last_seen} and adds them (and the upload) to the running totals."""
+    return _ops().account_hist(hist, meta, int(W), client_dl, client_ul, float(upload_per_client))
 
 
 def count_ge(last_mod: torch.Tensor, thr: torch.Tensor) -> torch.Tensor:

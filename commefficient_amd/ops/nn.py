@@ -106,6 +106,13 @@ def _wgrad_to(g: torch.Tensor, x: torch.Tensor, weight: torch.Tensor):
     return _ops().conv3x3_wgrad(g, x)
 
 
+def _pool_fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """The fused conv + relu + maxpool2 epilogue needs whole image-row pairs
+    per 128-pixel tile (csrc/conv.hip ``conv3x3_pool_supported``)."""
+    H, W = x.shape[2], x.shape[3]
+    return weight.shape[0] % 128 == 0 and H % 2 == 0 and W % 2 == 0 and 128 % (2 * W) == 0
+
+
 class _Conv3x3Act(torch.autograd.Function):
     """relu(conv3x3(x, w)) or maxpool_k(relu(conv3x3(x, w))), no bias.
 
@@ -119,7 +126,12 @@ class _Conv3x3Act(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, pool_k):
         wf, wt = _prep(weight)
-        if pool_k:
+        if pool_k == 2 and _pool_fusable(x, weight):
+            # relu + 2x2 max-pool in the conv epilogue: the full-resolution
+            # activation is never written
+            out, idx = _ops().conv3x3_fwd_pool2(x, wf)
+            ctx.save_for_backward(x, wt, idx)
+        elif pool_k:
             y = _ops().conv3x3_fwd(x, wf, False)
             out, idx = _ops().relu_maxpool(y, pool_k)
             del y

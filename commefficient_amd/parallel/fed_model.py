@@ -148,6 +148,7 @@ class FedModel:
         self._work = None  # separate work buffer for topk_down / fedavg
         self.last_round = {}
         self.graphs = RoundGraphs(self) if self.device.type == "cuda" else None
+        self._acct_meta = None  # accounting meta staged with the round's inputs
 
     # ------------------------------------------------------------------ API
     def attach_optimizer(self, opt):
@@ -266,13 +267,12 @@ class FedModel:
         W = len(clients)
         B = len(cids)
         mine = self._assign(clients)
-        slot_of = {int(c): i for i, c in enumerate(clients)}
         n_res = None
 
         # positions of this rank's examples, grouped client by client
         order = np.argsort(inverse, kind="stable")
         starts = np.concatenate([[0], np.cumsum(counts)])
-        my_slots = np.array([slot_of[int(c)] for c in mine], dtype=np.int64)
+        my_slots = np.searchsorted(clients, mine).astype(np.int64)  # clients sorted unique
 
         # ---- per-client metrics / transmit payload
         self.model.train()
@@ -291,7 +291,7 @@ class FedModel:
         # we know n_metrics -> run compute first into a local list
         with self.timer.phase("compute"):
             if merged:
-                res = self._compute_merged(rb, order, starts, my_slots, counts, W)
+                res = self._compute_merged(rb, order, starts, my_slots, counts, W, clients)
             else:
                 res = self._compute_per_client(rb, order, starts, my_slots, mine, counts, W)
         main, metric_sums = res  # main: transmit (device, main_numel); metric_sums [m, W]
@@ -310,7 +310,8 @@ class FedModel:
         G.mul_(1.0 / B)
         # clone: the payload buffer is reused by the next round
         metrics = payload[self.main_numel:].view(n_res, W).clone()
-        dl, ul = self.accountant.round(clients, self.round_idx)
+        dl, ul = self.accountant.round(clients, self.round_idx, meta=self._acct_meta)
+        self._acct_meta = None
         self._pending = (G, clients, False)
         self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
                            "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel())}
@@ -378,14 +379,31 @@ class FedModel:
         buf = self._payload_buf(0)[:self.main_numel]
         return buf
 
-    def _compute_merged(self, rb, order, starts, my_slots, counts, W):
+    def _compute_merged(self, rb, order, starts, my_slots, counts, W, clients):
         """One forward/backward over all of this rank's clients (exact for the
         linear modes, see module docstring)."""
         a = self.args
         pos, slot_per_ex = self._merged_positions(order, starts, my_slots, counts)
         n_local = len(pos)
         self.flat.zero_grad()
-        data = rb.take(pos)
+        packed = None
+        if rb.graph_index is not None and self.device.type == "cuda":
+            # every per-round host array in ONE pinned H2D copy: (rows, keys),
+            # client slots, client sizes, accounting meta
+            idx2 = rb.graph_index(pos)
+            meta = self.accountant.round_meta(clients)
+            host = np.concatenate([idx2.reshape(-1), slot_per_ex, counts.astype(np.int64), meta])
+            dev = dist.h2d(host, self.device)
+            o = 0
+            parts = []
+            for n in (2 * n_local, n_local, W, len(meta)):
+                parts.append(dev[o:o + n])
+                o += n
+            packed = parts
+            data = rb.graph_gather(parts[0].view(2, n_local))
+            self._acct_meta = parts[3]
+        else:
+            data = rb.take(pos)
         inputs, targets = data[:-1], data[-1]
         mb = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else n_local
         groups_total = len(my_slots)
@@ -403,8 +421,11 @@ class FedModel:
         mets = [torch.cat([m[i] for m in metrics_all]) for i in range(len(metrics_all[0]))] \
             if metrics_all else []
         # per-client mean metrics into their global slots
-        slots_t = dist.h2d(slot_per_ex, self.device)
-        n_t = dist.h2d(counts.astype(np.float32), self.device)
+        if packed is not None:
+            slots_t, n_t = packed[1], packed[2]
+        else:
+            slots_t = dist.h2d(slot_per_ex, self.device)
+            n_t = dist.h2d(counts.astype(np.float32), self.device)
         msum = self._metric_sums([per_ex] + mets, slots_t, n_t, W)
         self._n_metrics = msum.shape[0]
         out = self._transmit_buffer()
@@ -576,6 +597,8 @@ class FedModel:
         G, clients, via_graph = self._pending
         self._pending = None
         if via_graph:
+            if self.accountant.hist_for(self.round_idx).data_ptr() != self.graphs.hist_ptr:
+                self.graphs.invalidate_server()  # histogram grew: recapture
             self.graphs.server(G, float(lr), self.round_idx)
             self.round_idx += 1
             return
@@ -585,7 +608,8 @@ class FedModel:
             self.fedavg_lr = float(lr)
         with self.timer.phase("server"):
             self.server.update(G, lr, self.w, self.accountant.last_mod, self.round_idx,
-                               self.client_state, clients)
+                               self.client_state, clients,
+                               hist=self.accountant.hist_for(self.round_idx))
         self.round_idx += 1
 
     # ------------------------------------------------------------------ val

@@ -118,6 +118,7 @@ class RoundGraphs:
         self.pending: Optional[_Entry] = None
         self.replays = 0
         self.stream = torch.cuda.Stream(fed_model.device) if self.enabled else None
+        self._hist_ptr = None
 
     # ---------------------------------------------------------------- policy
     def usable(self, rb, n_local: int) -> bool:
@@ -145,6 +146,14 @@ class RoundGraphs:
     def invalidate(self):
         self.entries.clear()
         self.pending = None
+
+    def invalidate_server(self):
+        for e in self.entries.values():
+            e.g_server = None
+
+    @property
+    def hist_ptr(self):
+        return self._hist_ptr
 
     # ------------------------------------------------------------ execution
     def compute(self, key, rb, pos: np.ndarray, slot_per_ex: np.ndarray, counts: np.ndarray,
@@ -194,7 +203,8 @@ class RoundGraphs:
             with _capture(g, self.pool, self.stream):
                 G.mul_(inv_b)
                 fm.server.update(G, 0.0, fm.w, fm.accountant.last_mod, 0, None, None,
-                                 step=self.step)
+                                 step=self.step, hist=fm.accountant.hist)
+            self._hist_ptr = fm.accountant.hist.data_ptr()
             self.pool = g.pool()
             e.g_server = g
         e.g_server.replay()

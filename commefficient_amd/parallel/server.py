@@ -95,11 +95,13 @@ class ServerState:
         self.noise_round = 0
 
     def update(self, G: torch.Tensor, lr, w: torch.Tensor, last_mod: torch.Tensor, round_idx: int,
-               client_state=None, participating=None, step: Optional[torch.Tensor] = None):
+               client_state=None, participating=None, step: Optional[torch.Tensor] = None,
+               hist: Optional[torch.Tensor] = None):
         """Apply one server step.  ``G`` is the summed transmit already scaled
         by 1/B.  ``step`` (device int32 [2] = lr bits, round) replaces the
         scalar lr / round_idx when the update runs inside a captured HIP
-        graph (parallel/graph.py).  Returns (idx, vals) for sparse modes (the
+        graph (parallel/graph.py); ``hist`` is the accountant's change histogram,
+        updated with the stamps.  Returns (idx, vals) for sparse modes (the
         un-scaled update), else None."""
         a = self.args
         rho = float(a.virtual_momentum)
@@ -117,7 +119,7 @@ class ServerState:
             idx, vals = sk.unsketch_sparse(a.k)
             # error feedback (virtual) + momentum-factor masking in sketch space
             sk.zero_heavy_hitters(idx, vals, self.V if et == "virtual" else None)
-            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step)
+            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
             return idx, vals
         if mode == "true_topk":
             ops.momentum_ef(self.V, self.E, G, rho, 1.0, "virtual")
@@ -125,7 +127,7 @@ class ServerState:
             if client_state is not None and participating is not None:
                 client_state.zero_velocity_at(participating, idx)
             ops.zero_at(idx, self.E, self.V)
-            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step)
+            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
             return idx, vals
         if mode in ("local_topk", "uncompressed"):
             ops.momentum_ef(self.V, None, G, rho, 1.0, "none")
@@ -136,11 +138,11 @@ class ServerState:
                 ops.clip_noise(self.V, None, 0.0, a.noise_multiplier, seed=a.seed * 7919 + 17,
                                offset=self.noise_round * self.d)
                 self.noise_round += 1
-            ops.dense_apply(w, self.V, lr_s, lr_v, last_mod, round_idx, step)
+            ops.dense_apply(w, self.V, lr_s, lr_v, last_mod, round_idx, step, hist)
             return None
         if mode == "fedavg":
             ops.momentum_ef(self.V, None, G, rho, 1.0, "none")
-            ops.dense_apply(w, self.V, 1.0, None, last_mod, round_idx)
+            ops.dense_apply(w, self.V, 1.0, None, last_mod, round_idx, step, hist)
             return None
         raise ValueError(mode)
 

@@ -13,9 +13,8 @@ Byte accounting reproduces fed_aggregator.py:170-299 exactly in both of the
 reference's regimes with one mechanism: a per-coordinate ``last_mod`` round
 index (written by the apply kernels) and a per-client ``last_seen`` round;
 a participating client downloads ``4 * #{i : last_mod[i] >= last_seen[c]}``
-bytes, computed by the ``count_ge`` kernel in one pass over ``last_mod``
-(no host history deque; the reference's 10/participation truncation
-disappears).  Upload is ``4 * {d | k | r*c}`` per participating client
+bytes, read off a change histogram the apply kernels maintain (no host
+history deque; the reference's 10/participation truncation disappears).  Upload is ``4 * {d | k | r*c}`` per participating client
 (fed_aggregator.py:291-298).  The true on-wire RCCL volume is reported too.
 """
 from __future__ import annotations
@@ -118,6 +117,18 @@ class ClientStateStore:
 
 
 class ByteAccountant:
+    """Upload / download byte accounting (fed_aggregator.py:170-299).
+
+    Download: every apply kernel stamps ``last_mod[i] = round`` where a weight
+    changes and moves the coordinate between the bins of a change histogram
+    ``hist[r + 1] = #{i : last_mod[i] == r}`` (bin 0: never changed).  A
+    client that last synchronised at round s downloads
+    ``4 * #{i : last_mod[i] >= s}`` = 4 * (sum of bins >= s + 1), so a round's
+    accounting is one tiny kernel over the bins (``account_hist``) instead of
+    a pass over all d stamps."""
+
+    HIST_CAP = 1 << 16  # rounds before the histogram grows
+
     def __init__(self, args, d: int, num_clients: int, device, world: int, payload_numel: int):
         self.args = args
         self.d = d
@@ -125,6 +136,8 @@ class ByteAccountant:
         self.device = device
         self.world = world
         self.last_mod = torch.full((d,), -1, dtype=torch.int32, device=device)
+        self.hist = torch.zeros(self.HIST_CAP, dtype=torch.int32, device=device)
+        self.hist[0] = d
         self.last_seen = np.zeros(num_clients, dtype=np.int64)
         mode = args.mode
         self.upload_per_client = 4 * {"uncompressed": d, "true_topk": d, "local_topk": args.k,
@@ -134,37 +147,41 @@ class ByteAccountant:
         self.client_download = torch.zeros(num_clients, dtype=torch.float64, device=device)
         self.client_upload = torch.zeros(num_clients, dtype=torch.float64, device=device)
 
+    def hist_for(self, round_idx: int) -> torch.Tensor:
+        """The change histogram, grown (doubling) so that round ``round_idx``
+        has a bin."""
+        if round_idx + 2 > self.hist.numel():
+            cap = self.hist.numel()
+            while round_idx + 2 > cap:
+                cap *= 2
+            h = torch.zeros(cap, dtype=torch.int32, device=self.device)
+            h[:self.hist.numel()].copy_(self.hist)
+            self.hist = h
+        return self.hist
+
     def wire_bytes_per_rank(self, payload_numel: int) -> float:
         """Bytes each rank sends in a ring all-reduce of the payload."""
         n = self.world
         return 0.0 if n == 1 else 2.0 * (n - 1) / n * payload_numel * 4
 
-    def round(self, clients: np.ndarray, round_idx: int):
+    def round_meta(self, clients: np.ndarray) -> np.ndarray:
+        """Host int64 [last_seen (W) | clients (W)] for ``round``."""
+        return np.concatenate([self.last_seen[clients], clients]).astype(np.int64)
+
+    def round(self, clients: np.ndarray, round_idx: int, meta: Optional[torch.Tensor] = None):
         """Account one round for the participating ``clients`` (unique, sorted).
         Must be called before the round's server update (clients download the
-        pre-update weights).  Returns (download bytes [W] device f64,
-        upload bytes float)."""
-        seen = self.last_seen[clients].astype(np.int32)
-        thr, inv = np.unique(seen, return_inverse=True)
-        if self.last_mod.is_cuda and len(thr) <= 1024:
-            # one fused native op: histogram, suffix counts and per-client totals
-            meta = h2d(np.concatenate([thr, inv, clients]).astype(np.int64), self.device)
-            dl = ops.account_round(self.last_mod, meta, len(thr), len(clients),
-                                   self.client_download, self.client_upload,
-                                   float(self.upload_per_client))
-            self.last_seen[clients] = round_idx
-            return dl, float(self.upload_per_client) * len(clients)
-        dl = torch.empty(len(clients), dtype=torch.float64, device=self.device)
-        counts_all = []
-        for s in range(0, len(thr), 1024):
-            counts_all.append(ops.count_ge(self.last_mod, h2d(thr[s:s + 1024], self.device)))
-        counts = torch.cat(counts_all).to(torch.float64) * 4.0
-        dl.copy_(counts[h2d(inv.astype(np.int64), self.device)])
-        cl = h2d(clients.astype(np.int64), self.device)
-        self.client_download.index_add_(0, cl, dl)
-        self.client_upload.index_add_(0, cl, torch.full_like(dl, float(self.upload_per_client)))
+        pre-update weights).  ``meta``: ``round_meta(clients)`` already on the
+        device.  Returns (download bytes [W] device f64, upload bytes float)."""
+        W = len(clients)
+        if meta is None:
+            meta = h2d(self.round_meta(clients), self.device)
+        # bins above the current round are empty: scan only [0, round + 1]
+        nb = min(self.hist.numel(), round_idx + 2)
+        dl = ops.account_hist(self.hist[:nb], meta, W, self.client_download, self.client_upload,
+                              float(self.upload_per_client))
         self.last_seen[clients] = round_idx
-        return dl, float(self.upload_per_client) * len(clients)
+        return dl, float(self.upload_per_client) * W
 
     def state_dict(self):
         return {"last_mod": self.last_mod.cpu(), "last_seen": torch.from_numpy(self.last_seen)}
@@ -172,3 +189,9 @@ class ByteAccountant:
     def load_state_dict(self, sd):
         self.last_mod.copy_(sd["last_mod"])
         self.last_seen = sd["last_seen"].numpy().astype(np.int64)
+        top = int(self.last_mod.max().item()) if self.d else -1
+        cap = self.HIST_CAP
+        while top + 2 > cap:
+            cap *= 2
+        counts = torch.bincount((self.last_mod.long() + 1), minlength=cap)
+        self.hist = counts.to(torch.int32).to(self.device)

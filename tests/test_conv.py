@@ -285,3 +285,18 @@ def test_augment_writes_padded_pixels():
     torch.testing.assert_close(x.float(), ref, rtol=1e-2, atol=1e-2)
     pad = torch.as_strided(x, (3, 8, 8), (256, 32, 4), x.storage_offset() + 3)
     assert torch.all(pad == 0)
+
+
+@pytest.mark.parametrize("N, C, H, K", [(3, 64, 32, 128), (5, 128, 16, 256), (7, 256, 8, 512),
+                                        (2, 64, 4, 128)])
+def test_fused_pool_epilogue_matches_unfused(N, C, H, K):
+    """conv3x3_fwd_pool2 == relu_maxpool(conv3x3_fwd(x), 2) bit for bit
+    (values and window codes)."""
+    x, w = _inputs(N, C, H, H, K, seed=N)
+    wf, _ = ops.conv_weight_prep(w)
+    y_ref = ops.conv3x3_fwd(x, wf, False)
+    p_ref, i_ref = torch.ops.commeff.relu_maxpool(y_ref, 2)
+    p, i = torch.ops.commeff.conv3x3_fwd_pool2(x, wf)
+    assert p.shape == p_ref.shape and i.shape == i_ref.shape
+    assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
+    assert torch.equal(i, i_ref)

@@ -326,3 +326,47 @@ def test_account_round_matches_reference(T):
     cdl[clients] += exp
     cul[clients] += 123.0
     assert torch.equal(cdl_d.cpu(), cdl) and torch.equal(cul_d.cpu(), cul)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_apply_maintains_change_histogram(device):
+    """sparse/dense apply keep hist[r+1] == #{i : last_mod[i] == r} exactly."""
+    g = torch.Generator().manual_seed(11)
+    d, cap = 200_003, 64
+    w = torch.randn(d, generator=g).to(device)
+    lm = torch.full((d,), -1, dtype=torch.int32, device=device)
+    hist = torch.zeros(cap, dtype=torch.int32, device=device)
+    hist[0] = d
+    for r in range(6):
+        if r % 3 == 2:
+            delta = torch.randn(d, generator=g)
+            delta[torch.rand(d, generator=g) < 0.3] = 0  # unchanged coordinates keep their stamp
+            ops.dense_apply(w, delta.to(device), 0.1, None, lm, r, None, hist)
+        else:
+            idx = torch.randperm(d, generator=g)[:5000].sort().values
+            vals = torch.randn(5000, generator=g)
+            vals[:100] = 0
+            ops.sparse_apply(w, idx.to(device), vals.to(device), 0.1, None, lm, r, None, hist)
+        exp = torch.bincount(lm.cpu().long() + 1, minlength=cap).to(torch.int32)
+        assert torch.equal(hist.cpu(), exp), r
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_account_hist_matches_count(device):
+    g = torch.Generator().manual_seed(3)
+    d, C, W, cap = 500_001, 3000, 700, 4096
+    lm = torch.randint(-1, 2500, (d,), generator=g, dtype=torch.int32)
+    lm[: d // 4] = 9
+    hist = torch.bincount(lm.long() + 1, minlength=cap).to(torch.int32)
+    seen = torch.randint(0, 2600, (W,), generator=g)
+    clients = torch.randperm(C, generator=g)[:W]
+    cdl = torch.rand(C, generator=g, dtype=torch.float64)
+    cul = torch.rand(C, generator=g, dtype=torch.float64)
+    cdl_d, cul_d = cdl.to(device), cul.to(device)
+    meta = torch.cat([seen, clients]).to(device)
+    dl = ops.account_hist(hist.to(device), meta, W, cdl_d, cul_d, 7.0).cpu()
+    exp = torch.stack([(lm >= s).sum() for s in seen]).to(torch.float64) * 4
+    assert torch.equal(dl, exp)
+    cdl[clients] += exp
+    cul[clients] += 7.0
+    assert torch.equal(cdl_d.cpu(), cdl) and torch.equal(cul_d.cpu(), cul)
