@@ -780,6 +780,52 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_pool2_hip(const at::Tensor& x, co
   return {y, idx};
 }
 
+// ---- ResNet-9 head (head.hip): x = res3 output [B, C, h, w] bf16 channels_last,
+// w = linear weight fp32 [classes, C]
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_fwd_hip(
+    const at::Tensor& x, const at::Tensor& w, const at::Tensor& targets, double scale) {
+  check_nhwc_bf16(x, "head: x");
+  check_f32(w, "head: w");
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == C && head_supported(static_cast<int>(C), static_cast<int>(K)),
+              "head: w must be [classes <= 128, C], C % 8 == 0");
+  TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous() && targets.numel() == B,
+              "head: targets int64 [B]");
+  TORCH_CHECK(H * W <= 255, "head: at most 255 pooled pixels");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto f = x.options().dtype(at::kFloat);
+  auto loss = at::empty({B}, f), correct = at::empty({B}, f), gunit = at::empty({B, K}, f);
+  auto pooled = at::empty({B, C}, x.options());
+  auto codes = at::empty({B, C}, x.options().dtype(at::kByte));
+  launch_head_fwd(bf16_ptr(x), w.data_ptr<float>(), targets.data_ptr<int64_t>(), static_cast<int>(B),
+                  static_cast<int>(C), static_cast<int>(H * W), static_cast<int>(K), static_cast<float>(scale),
+                  loss.data_ptr<float>(), correct.data_ptr<float>(), gunit.data_ptr<float>(),
+                  reinterpret_cast<uint16_t*>(pooled.data_ptr()), codes.data_ptr<uint8_t>(), cur_stream());
+  return {loss, correct, gunit, pooled, codes};
+}
+
+// returns dx [B, C, h, w] (channels_last bf16); dw = beta * dw + dW
+at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at::Tensor& w,
+                        const at::Tensor& pooled, const at::Tensor& codes, int64_t H, int64_t W,
+                        double scale, at::Tensor dw, double beta) {
+  check_f32(w, "head: w");
+  const int64_t B = pooled.size(0), C = pooled.size(1), K = w.size(0);
+  TORCH_CHECK(gunit.is_contiguous() && gunit.size(0) == B && gunit.size(1) == K && codes.is_contiguous() &&
+                  pooled.is_contiguous(), "head_bwd: saved tensors");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  auto g = gl.to(at::kFloat).contiguous();
+  TORCH_CHECK(g.numel() == B, "head_bwd: grad of loss [B]");
+  auto dx = at::empty({B, C, H, W}, pooled.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_f32(dw, "head_bwd: dw");
+  TORCH_CHECK(dw.sizes() == w.sizes(), "head_bwd: dw shape");
+  launch_head_bwd(g.data_ptr<float>(), gunit.data_ptr<float>(), w.data_ptr<float>(),
+                  reinterpret_cast<const uint16_t*>(pooled.data_ptr()), codes.data_ptr<uint8_t>(),
+                  static_cast<int>(B), static_cast<int>(C), static_cast<int>(H * W), static_cast<int>(K),
+                  static_cast<float>(scale), reinterpret_cast<uint16_t*>(dx.data_ptr()), dw.data_ptr<float>(),
+                  static_cast<float>(beta), cur_stream());
+  return dx;
+}
+
 // fused per-example cross-entropy: (loss f32 [B], correct f32 [B], softmax - onehot [B, C])
 std::tuple<at::Tensor, at::Tensor, at::Tensor> ce_fwd_hip(const at::Tensor& logits,
                                                           const at::Tensor& targets) {
@@ -1019,6 +1065,9 @@ TORCH_LIBRARY(commeff, m) {
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
   m.def("conv3x3_fwd_pool2(Tensor x, Tensor w) -> (Tensor, Tensor)");
+  m.def("head_fwd(Tensor x, Tensor w, Tensor targets, float scale) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("head_bwd(Tensor gl, Tensor gunit, Tensor w, Tensor pooled, Tensor codes, int H, int W, float scale, "
+        "Tensor(a!) dw, float beta) -> Tensor");
   m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
@@ -1091,6 +1140,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("conv3x3_fwd", &conv3x3_fwd_hip);
   m.impl("conv3x3_fwd_pool2", &conv3x3_fwd_pool2_hip);
+  m.impl("head_fwd", &head_fwd_hip);
+  m.impl("head_bwd", &head_bwd_hip);
   m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
   m.impl("ce_fwd", &ce_fwd_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);

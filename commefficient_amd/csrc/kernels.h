@@ -219,6 +219,14 @@ void launch_conv_prep_wgrad(ConvPrepArgs a, float* dw, float beta, hipStream_t s
 // ----------------------------------------------------------------- loss --
 // per-example cross-entropy of logits [B, C] (bf16 or f32): loss, top-1
 // correctness and the unit gradient softmax - onehot (logits dtype)
+// ResNet-9 head (head.hip): maxpool(HxW) -> scale * linear (no bias) -> CE
+bool head_supported(int C, int NCLS);
+void launch_head_fwd(const uint16_t* x, const float* w, const int64_t* tgt, int B, int C, int NPIX, int NCLS,
+                     float scale, float* loss, float* correct, float* gunit, uint16_t* pooled, uint8_t* codes,
+                     hipStream_t stream);
+void launch_head_bwd(const float* gl, const float* gunit, const float* w, const uint16_t* pooled,
+                     const uint8_t* codes, int B, int C, int NPIX, int NCLS, float scale, uint16_t* dx,
+                     float* dw, float beta, hipStream_t stream);
 void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
                    float* correct, void* grad, hipStream_t stream);
 

@@ -21,7 +21,8 @@ import itertools
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import (conv3x3_input_relu, conv3x3_relu_pool, input_conv_native_ok,
+from ..ops.nn import (conv3x3_input_relu, conv3x3_relu_pool, cross_entropy_correct,
+                      fused_head_loss, head_native_ok, input_conv_native_ok,
                       prepared_conv_weights, relu_maxpool, residual_unit)
 from .common import GhostBatchNorm2d, Mul
 
@@ -117,17 +118,32 @@ class BasicNet(nn.Module):
     def conv_weights(self):
         return [m.weight for m in self.modules() if isinstance(m, nn.Conv2d)]
 
-    def forward(self, x):
+    def features(self, x):
         # every conv weight -> bf16 GEMM images in one launch (native path)
         with prepared_conv_weights(self.conv_weights() if x.is_cuda else []):
             x = self.prep(x)
             x = self.res1(self.layer1(x))
             x = self.layer2(x)
-            x = self.res3(self.layer3(x))
+            return self.res3(self.layer3(x))
+
+    def head(self, x):
         # res3's output is >= 0 (relu'd input + relu'd branch), so relu is the
         # identity and the fused kernel computes exactly max_pool2d(x, 4)
         x = relu_maxpool(x, 4).flatten(1)
         return self.classifier(self.linear(x))
+
+    def forward(self, x):
+        return self.head(self.features(x))
+
+    def loss(self, x, targets):
+        """(per-example CE loss, top-1 correct): with the final pool covering
+        the whole 4x4 map, the head + loss run as one native kernel each way
+        (csrc/head.hip); otherwise the module head + fused CE."""
+        f = self.features(x)
+        if (f.shape[2] == 4 and f.shape[3] == 4 and head_native_ok(f, self.linear.weight)
+                and self.linear.bias is None and isinstance(self.classifier, Mul)):
+            return fused_head_loss(f, self.linear.weight, targets, self.classifier.weight)
+        return cross_entropy_correct(self.head(f), targets)
 
 
 class ResNet9(nn.Module):
@@ -147,6 +163,9 @@ class ResNet9(nn.Module):
 
     def forward(self, x):
         return self.n(x)
+
+    def loss(self, x, targets):
+        return self.n.loss(x, targets)
 
     def finetune_parameters(self):
         """Replace the head for ``new_num_classes`` and return its params

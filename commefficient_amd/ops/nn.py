@@ -261,6 +261,47 @@ def conv3x3_input_relu(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return F.relu(F.conv2d(x, weight, padding=1))
 
 
+# ------------------------------------------------------------ head
+class _FusedHead(torch.autograd.Function):
+    """``CE(scale * linear(maxpool_HxW(relu(x))), targets)`` per example, plus
+    top-1 correctness -- ResNet-9's pool/flatten/linear/Mul head and the CV
+    loss in one native kernel each way (csrc/head.hip).  The weight gradient
+    accumulates straight into an existing flat-buffer ``.grad``."""
+
+    @staticmethod
+    def forward(ctx, x, weight, targets, scale):
+        loss, correct, gunit, pooled, codes = _ops().head_fwd(x, weight.detach(), targets,
+                                                              float(scale))
+        ctx.save_for_backward(gunit, pooled, codes)
+        ctx.weight, ctx.scale, ctx.hw = weight, float(scale), (x.shape[2], x.shape[3])
+        ctx.mark_non_differentiable(correct)
+        return loss, correct
+
+    @staticmethod
+    def backward(ctx, gl, gc):
+        gunit, pooled, codes = ctx.saved_tensors
+        w = ctx.weight
+        gr = w.grad
+        into = (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
+                and gr.shape == w.shape and gr.device == w.device)
+        dw = gr if into else torch.empty_like(w, dtype=torch.float32)
+        dx = _ops().head_bwd(gl.contiguous(), gunit, w.detach(), pooled, codes, ctx.hw[0],
+                             ctx.hw[1], ctx.scale, dw, 1.0 if into else 0.0)
+        return dx, (None if into else dw), None, None
+
+
+def head_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 8 == 0
+            and x.shape[2] * x.shape[3] <= 255 and weight.dtype == torch.float32
+            and weight.dim() == 2 and weight.shape[1] == x.shape[1] and weight.shape[0] <= 128)
+
+
+def fused_head_loss(x, weight, targets, scale: float):
+    """(per-example CE loss, correct) of ``scale * maxpool_all(relu(x)) @ weight.T``."""
+    return _FusedHead.apply(x, weight, targets.contiguous(), float(scale))
+
+
 # ------------------------------------------------------------ loss
 class _FusedCE(torch.autograd.Function):
     """Per-example cross-entropy + top-1 correctness in one kernel

@@ -300,3 +300,37 @@ def test_fused_pool_epilogue_matches_unfused(N, C, H, K):
     assert p.shape == p_ref.shape and i.shape == i_ref.shape
     assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
     assert torch.equal(i, i_ref)
+
+
+@pytest.mark.parametrize("B, C, ncls", [(37, 512, 10), (8, 512, 100), (5, 64, 3)])
+def test_fused_head_matches_fp32(B, C, ncls):
+    """ResNet-9 head (maxpool 4x4 -> linear -> x0.125 -> CE) native fwd/bwd
+    against the fp32 PyTorch composition of the same op."""
+    g = torch.Generator(device="cuda").manual_seed(B)
+    # distinct values in every 4x4 window (no argmax ties: routing is
+    # unambiguous) and some all-negative windows (relu zeroes their gradient)
+    rank = torch.argsort(torch.rand(B, C, 16, device="cuda", generator=g), dim=-1).float()
+    scale_bc = torch.rand(B, C, 1, device="cuda", generator=g) + 0.5
+    sign = torch.where(torch.rand(B, C, 1, device="cuda", generator=g) < 0.1, -1.0, 1.0)
+    x = ((rank + 1) / 16 * scale_bc * sign).view(B, C, 4, 4).to(torch.bfloat16)
+    x = _nhwc(x).requires_grad_(True)
+    w = (torch.randn(ncls, C, device="cuda", generator=g) * 0.05).requires_grad_(True)
+    t = torch.randint(0, ncls, (B,), device="cuda", generator=g)
+    gl = torch.rand(B, device="cuda", generator=g)
+    loss, correct = cnn.fused_head_loss(x, w, t, 0.125)
+    (loss * gl).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    logits = 0.125 * torch.nn.functional.max_pool2d(torch.relu(xr), 4).flatten(1) @ wr.t()
+    lr = torch.nn.functional.cross_entropy(logits, t, reduction="none")
+    (lr * gl).sum().backward()
+    torch.testing.assert_close(loss, lr.detach(), rtol=1e-4, atol=1e-5)
+    assert torch.equal(correct, (logits.argmax(1) == t).float())
+    _close(x.grad, xr.grad, rel=1e-2)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=1e-4, atol=1e-6)
+    # accumulate-into-.grad path (the flat-buffer case)
+    w2 = w.detach().clone().requires_grad_(True)
+    w2.grad = torch.ones_like(w2)
+    loss2, _ = cnn.fused_head_loss(x.detach(), w2, t, 0.125)
+    (loss2 * gl).sum().backward()
+    torch.testing.assert_close(w2.grad, wr.grad + 1, rtol=1e-4, atol=1e-6)
