@@ -668,12 +668,27 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   }
 }
 
+// resident wgrad blocks per CU (64 KB LDS, 88 VGPRs: 2 blocks) x CUs
+static int wgrad_slots() {
+  static const int slots = [] {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    }
+    return 2 * cus;
+  }();
+  return slots;
+}
+
 int conv3x3_wgrad_splits(int P, int K, int C) {
   const int bn = C % 128 == 0 ? 128 : 64;
   const int tiles = (K / WBM) * 9 * (C / bn);
   const int steps = (P + BK - 1) / BK;
-  // ~3 blocks per CU (2 resident) with >= 32 K-steps each
-  int s = (512 + tiles - 1) / tiles;
+  // every block resident at once (equal-work blocks: one block past the
+  // resident slots costs a whole extra block time), >= 32 K-steps each
+  int s = wgrad_slots() / tiles;
   if (s > steps / 32) s = steps / 32;
   return s < 1 ? 1 : s;
 }

@@ -58,7 +58,9 @@ def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> 
             raise RuntimeError("--device cuda requested but no HIP device is visible")
         torch.cuda.set_device(local % n)
         device = torch.device("cuda", local % n)
-        backend = "nccl"
+        # COMMEFF_DIST_BACKEND=gloo: several ranks sharing one GPU (RCCL refuses
+        # duplicate devices) -- rehearses the multi-rank GPU path on a 1-GPU box
+        backend = os.environ.get("COMMEFF_DIST_BACKEND", "nccl")
     else:
         device = torch.device("cpu")
         backend = "gloo"
@@ -147,6 +149,9 @@ def h2d_into(out: torch.Tensor, x) -> torch.Tensor:
 
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:
     if _CTX.distributed:
+        if t.is_cuda and _CTX.backend == "gloo":
+            # gloo reads device memory without ordering against the stream
+            torch.cuda.current_stream().synchronize()
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
 
