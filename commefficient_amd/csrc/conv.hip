@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int BLD = BN * 8 / NT;              // B chunks per thread per step
   constexpr int NLD = ALD + BLD;
   constexpr int NI = BN / 64;                   // 32-wide MFMA tiles per wave along N
-  static_assert(BLD >= 1 && NSTAGE >= 2 && NSTAGE <= 3, "tile config");
+  static_assert(BLD >= 1 && NSTAGE >= 2 && NSTAGE <= 3 && TBM % 64 == 0, "tile config");
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;

@@ -311,6 +311,18 @@ void set_lds_attr(const void* fn) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
 }
 
+int64_t device_cus() {
+  static const int64_t cus = [] {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+        prop.multiProcessorCount > 0)
+      return static_cast<int64_t>(prop.multiProcessorCount);
+    return int64_t{256};  // MI355X (CPU-side plan checks)
+  }();
+  return cus;
+}
+
 }  // namespace
 
 bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
@@ -328,6 +340,15 @@ bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
     int64_t chunk = (stage_bytes / 4 / r) / 64 * 64;
     if (chunk > kPlanStageCap / r / 64 * 64) chunk = kPlanStageCap / r / 64 * 64;
     if (chunk < 64) continue;
+    // P1 / Q2 run one LDS-filling block per CU: shrink the chunk so the
+    // chunk count is just under a whole number of block rounds (863 chunks
+    // on 256 CUs would leave the 4th round 37 % busy; 1017 fills it)
+    {
+      const int64_t cus = device_cus();
+      const int64_t rounds = (d + cus * chunk - 1) / (cus * chunk);
+      const int64_t bal = ((d + cus * rounds - 1) / (cus * rounds) + 63) / 64 * 64;
+      if (bal >= 64 && bal < chunk) chunk = bal;
+    }
     p.chunk = chunk;
     p.num_chunks = (d + chunk - 1) / chunk;
     // encode P2 keeps a tile's run metadata (2 words per chunk) beside the
