@@ -314,7 +314,10 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
 }
 
 // ------------------------------------------------------------------ wgrad
-template <int BN, int NSTAGE, bool ROWSTEP>
+// PAIR (C == 64, BN == 128): a tile's 128 columns are TWO taps x 64 input
+// channels (taps 2q, 2q+1; the 10th tap of the last pair is a zero operand
+// that is never stored), so 64-channel layers run the 128-wide wave tiles
+template <int BN, int NSTAGE, bool ROWSTEP, bool PAIR = false>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int A_BYTES = BK * WBM * 2;  // [64 px][128 k], 256-byte rows
@@ -326,17 +329,18 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int NLD = ALD + BLD;
   constexpr int NI = BN / 64;
   static_assert(NSTAGE >= 2 && NSTAGE <= 3, "stages");
+  static_assert(!PAIR || BN == 128, "tap pairs fill a 128-wide tile");
+  constexpr int NTAPG = PAIR ? 5 : 9;     // tap groups per (k, c) tile
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int C = a.C, K = a.K, H = a.H, W = a.W;
-  const int ntc = C / BN, ntk = K / WBM;
-  const int ntiles = ntk * 9 * ntc;
+  const int ntc = PAIR ? 1 : C / BN, ntk = K / WBM;
+  const int ntiles = ntk * NTAPG * ntc;
   const int tile = bid % ntiles, split = bid / ntiles;
-  const int tc = tile % ntc, rs = (tile / ntc) % 9, tk = tile / (ntc * 9);
+  const int tc = tile % ntc, rs = (tile / ntc) % NTAPG, tk = tile / (ntc * NTAPG);
   const int k0 = tk * WBM, c0 = tc * BN;
-  const int dr = rs / 3 - 1, ds = rs % 3 - 1;
   const int pbeg = split * a.steps_per_split * BK;
   const int pend = min(a.P, pbeg + a.steps_per_split * BK);
   const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
@@ -356,27 +360,35 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   }
   // B chunks: rows of x at the tap offset; (h, w) of the row tracked per step
   uint64_t b_ptr[BLD];
-  int b_row[BLD], b_h[BLD], b_w[BLD];
+  int b_row[BLD], b_h[BLD], b_w[BLD], b_dr[BLD], b_ds[BLD];
+  uint32_t b_tok = 0;  // bit j: chunk j belongs to a real tap (PAIR: not the 10th)
 #pragma unroll
   for (int j = 0; j < BLD; ++j) {
     const int s = j * 256 + tid;
     int row, lc;
     if constexpr (BN == 128) { row = s >> 4; lc = (s & 15) ^ sw_tr256(row); }
     else { row = s >> 3; lc = (s & 7) ^ sw_tr128(row); }
+    int tap = rs, cc = lc;
+    if constexpr (PAIR) { tap = 2 * rs + (lc >> 3); cc = lc & 7; }
+    b_tok |= (tap < 9 ? 1u : 0u) << j;
+    if (tap > 8) tap = 8;
+    b_dr[j] = tap / 3 - 1;
+    b_ds[j] = tap % 3 - 1;
     const int p = pbeg + row;
     b_row[j] = p;
     const uint32_t q = fdiv(static_cast<uint32_t>(p), a.div_w);
     b_w[j] = p - static_cast<int>(q) * W;
-    b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H) + dr;  // tap row of the source
-    b_ptr[j] = reinterpret_cast<uint64_t>(a.x + static_cast<int64_t>(p + dr * W + ds) * C + c0 +
-                                          lc * 8);
+    b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H) + b_dr[j];  // tap row of the source
+    b_ptr[j] = reinterpret_cast<uint64_t>(a.x + static_cast<int64_t>(p + b_dr[j] * W + b_ds[j]) * C +
+                                          c0 + cc * 8);
   }
   // when W | BK a step advances every row by BK/W whole image rows: w is
   // fixed per chunk and h advances incrementally (ROWSTEP); else recompute
-  uint32_t b_wok = 0;  // bit j: column of chunk j stays inside the image at this tap
+  uint32_t b_wok = 0;  // bit j: column of chunk j stays inside the image at its tap
 #pragma unroll
   for (int j = 0; j < BLD; ++j)
-    b_wok |= (static_cast<unsigned>(b_w[j] + ds) < static_cast<unsigned>(W) ? 1u : 0u) << j;
+    b_wok |= (static_cast<unsigned>(b_w[j] + b_ds[j]) < static_cast<unsigned>(W) ? 1u : 0u) << j;
+  b_wok &= b_tok;
   const int dh = ROWSTEP ? (BK / W) % H : 0;
 
   auto issue = [&](int stage, bool full) __attribute__((always_inline)) {
@@ -392,18 +404,18 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
     for (int j = 0; j < BLD; ++j) {
       bool ok = static_cast<unsigned>(b_h[j]) < static_cast<unsigned>(H);
       if constexpr (ROWSTEP) ok = ok && ((b_wok >> j) & 1u);
-      else ok = ok && static_cast<unsigned>(b_w[j] + ds) < static_cast<unsigned>(W);
+      else ok = ok && ((b_tok >> j) & 1u) && static_cast<unsigned>(b_w[j] + b_ds[j]) < static_cast<unsigned>(W);
       if (!full) ok = ok && b_row[j] < pend;
       glds16(reinterpret_cast<const void*>(ok ? b_ptr[j] : zero), base + A_BYTES + j * 4096);
       b_row[j] += BK;
       b_ptr[j] += static_cast<uint64_t>(BK) * C * 2;
       if constexpr (ROWSTEP) {
         const int nh = b_h[j] + dh;
-        b_h[j] = nh - dr >= H ? nh - H : nh;
+        b_h[j] = nh - b_dr[j] >= H ? nh - H : nh;
       } else {
         const uint32_t q = fdiv(static_cast<uint32_t>(b_row[j]), a.div_w);
         b_w[j] = b_row[j] - static_cast<int>(q) * W;
-        b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H) + dr;
+        b_h[j] = static_cast<int>(q - fdiv(q, a.div_h) * H) + b_dr[j];
       }
     }
   };
@@ -474,8 +486,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int k = k0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-        const int c = c0 + wc * (BN / 2) + ni * 32 + lr;
-        slab[(static_cast<size_t>(k) * 9 + rs) * C + c] = acc[mi][ni][e];
+        const int n = wc * (BN / 2) + ni * 32 + lr;
+        if constexpr (PAIR) {  // column n = (tap 2 rs + n / 64, channel n % 64)
+          const int tap = 2 * rs + (n >> 6);
+          if (tap < 9) slab[(static_cast<size_t>(k) * 9 + tap) * C + (n & 63)] = acc[mi][ni][e];
+        } else {
+          slab[(static_cast<size_t>(k) * 9 + rs) * C + c0 + n] = acc[mi][ni][e];
+        }
       }
 }
 
@@ -593,6 +610,12 @@ int grid_for(int64_t n, int per_block) {
   return static_cast<int>(b < 1 ? 1 : b);
 }
 
+// (k, c) x tap-group tiles of one wgrad: 64-channel inputs pair taps (PAIR)
+int wgrad_tiles(int K, int C) {
+  if (C == 64) return (K / WBM) * 5;
+  return (K / WBM) * 9 * (C / (C % 128 == 0 ? 128 : 64));
+}
+
 void set_lds(const void* fn, int bytes) {
   (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
@@ -612,17 +635,17 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t stream) {
                      lds, stream, a);
 }
 
-template <int BN, int NSTAGE, bool ROWSTEP>
+template <int BN, int NSTAGE, bool ROWSTEP, bool PAIR = false>
 void launch_wgrad(const ConvWgradArgs& a, hipStream_t stream) {
   constexpr int lds = NSTAGE * (BK * WBM * 2 + BK * BN * 2);
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_wgrad_kernel<BN, NSTAGE, ROWSTEP>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_wgrad_kernel<BN, NSTAGE, ROWSTEP, PAIR>), lds);
     init = true;
   }
-  const int tiles = (a.K / WBM) * 9 * (a.C / BN);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BN, NSTAGE, ROWSTEP>), dim3(tiles * a.splits), dim3(256), lds,
-                     stream, a);
+  const int tiles = wgrad_tiles(a.K, a.C);
+  hipLaunchKernelGGL((conv_wgrad_kernel<BN, NSTAGE, ROWSTEP, PAIR>), dim3(tiles * a.splits), dim3(256),
+                     lds, stream, a);
 }
 
 }  // namespace
@@ -683,8 +706,7 @@ static int wgrad_slots() {
 }
 
 int conv3x3_wgrad_splits(int P, int K, int C) {
-  const int bn = C % 128 == 0 ? 128 : 64;
-  const int tiles = (K / WBM) * 9 * (C / bn);
+  const int tiles = wgrad_tiles(K, C);
   const int steps = (P + BK - 1) / BK;
   // every block resident at once (equal-work blocks: one block past the
   // resident slots costs a whole extra block time), >= 32 K-steps each
@@ -704,7 +726,9 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
   }();
   const bool rowstep = BK % a.W == 0;
   const bool wide = a.C % 128 == 0;
-  if (three && rowstep) {
+  if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)
+    if (rowstep) launch_wgrad<128, 2, true, true>(a, stream); else launch_wgrad<128, 2, false, true>(a, stream);
+  } else if (three && rowstep) {
     if (wide) launch_wgrad<128, 3, true>(a, stream); else launch_wgrad<64, 3, true>(a, stream);
   } else if (rowstep) {
     if (wide) launch_wgrad<128, 2, true>(a, stream); else launch_wgrad<64, 2, true>(a, stream);

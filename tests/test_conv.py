@@ -17,6 +17,7 @@ SHAPES = [  # N, C, H, W, K   (ResNet-9 layers at small batch + odd tiles)
     (5, 512, 4, 4, 512),
     (3, 64, 5, 7, 128),   # pixels not a multiple of the 128-pixel tile
     (2, 128, 8, 8, 64),   # 64-wide output tile (dgrad of a 64-channel input)
+    (2, 64, 8, 8, 256),   # tap-paired wgrad over two output-channel tiles
 ]
 
 
