@@ -826,6 +826,32 @@ at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at:
   return dx;
 }
 
+// per-client mean metrics into out [m, W] (f32, contiguous): see loss.hip
+void client_means_hip(at::Tensor out, at::TensorList rows, const at::Tensor& slot,
+                      const at::Tensor& counts) {
+  const int64_t m = static_cast<int64_t>(rows.size());
+  TORCH_CHECK(m >= 1 && m <= kClientMeanRows, "client_means: 1..4 metric rows");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 2 && out.size(0) == m,
+              "client_means: out f32 [m, W]");
+  const int64_t W = out.size(1), n = slot.numel();
+  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.is_contiguous(), "client_means: slot int64");
+  TORCH_CHECK(counts.numel() == W && counts.is_contiguous() &&
+                  (counts.scalar_type() == at::kLong || counts.scalar_type() == at::kFloat),
+              "client_means: counts int64/f32 [W]");
+  ClientMeanRows r{};
+  r.m = static_cast<int>(m);
+  for (int64_t i = 0; i < m; ++i) {
+    TORCH_CHECK(rows[i].scalar_type() == at::kFloat && rows[i].is_contiguous() && rows[i].numel() == n,
+                "client_means: rows f32 [n]");
+    r.p[i] = rows[i].data_ptr<float>();
+  }
+  for (int64_t i = m; i < kClientMeanRows; ++i) r.p[i] = r.p[0];
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
+  launch_client_means(r, slot.data_ptr<int64_t>(), static_cast<int>(n), counts.data_ptr(),
+                      counts.scalar_type() == at::kFloat, static_cast<int>(W), out.data_ptr<float>(),
+                      cur_stream());
+}
+
 // fused per-example cross-entropy: (loss f32 [B], correct f32 [B], softmax - onehot [B, C])
 std::tuple<at::Tensor, at::Tensor, at::Tensor> ce_fwd_hip(const at::Tensor& logits,
                                                           const at::Tensor& targets) {
@@ -1070,6 +1096,7 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor(a!) dw, float beta) -> Tensor");
   m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
+  m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
@@ -1144,6 +1171,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("head_bwd", &head_bwd_hip);
   m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
   m.impl("ce_fwd", &ce_fwd_hip);
+  m.impl("client_means", &client_means_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
   m.impl("conv3x3_wgrad_into", &conv3x3_wgrad_into_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);

@@ -227,6 +227,13 @@ void launch_head_fwd(const uint16_t* x, const float* w, const int64_t* tgt, int 
 void launch_head_bwd(const float* gl, const float* gunit, const float* w, const uint16_t* pooled,
                      const uint8_t* codes, int B, int C, int NPIX, int NCLS, float scale, uint16_t* dx,
                      float* dw, float beta, hipStream_t stream);
+constexpr int kClientMeanRows = 4;
+struct ClientMeanRows {
+  const float* p[kClientMeanRows];
+  int m;
+};
+void launch_client_means(const ClientMeanRows& rows, const int64_t* slot, int n, const void* counts,
+                         bool counts_f32, int W, float* out, hipStream_t stream);
 void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
                    float* correct, void* grad, hipStream_t stream);
 

@@ -95,4 +95,41 @@ void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int 
                        static_cast<float*>(grad));
 }
 
+// Per-client mean metrics (fed_model.py _metric_sums): out[i, w] = mean of
+// rows[i][e] over the examples e with slot[e] == w (slot sorted ascending:
+// each client's examples are contiguous), 0 for clients without examples on
+// this rank.  Thread per (metric, client), sequential sum in example order
+// (deterministic); replaces zeros + index_add per metric + divide + copy.
+namespace {
+__global__ void __launch_bounds__(256)
+client_means_kernel(ClientMeanRows rows, const int64_t* __restrict__ slot, int n,
+                    const void* __restrict__ counts, bool counts_f32, int W, float* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= rows.m * W) return;
+  const int i = t / W, w = t - i * W;
+  int lo = 0, hi = n;  // first e with slot[e] >= w
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (slot[mid] < w) lo = mid + 1; else hi = mid;
+  }
+  const float* r = rows.p[0];
+#pragma unroll
+  for (int q = 1; q < kClientMeanRows; ++q)
+    if (q == i) r = rows.p[q];
+  float s = 0.f;
+  for (int e = lo; e < n && slot[e] == w; ++e) s += r[e];
+  const float c = counts_f32 ? static_cast<const float*>(counts)[w]
+                             : static_cast<float>(static_cast<const int64_t*>(counts)[w]);
+  out[t] = s / c;
+}
+}  // namespace
+
+void launch_client_means(const ClientMeanRows& rows, const int64_t* slot, int n, const void* counts,
+                         bool counts_f32, int W, float* out, hipStream_t stream) {
+  const int total = rows.m * W;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(client_means_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, rows, slot,
+                     n, counts, counts_f32, W, out);
+}
+
 }  // namespace commeff

@@ -117,4 +117,10 @@ def relu_mask(gy, y) -> torch.Tensor:
     return _ops().relu_mask(gy, y)
 
 
-__all__ += ["conv_weight_prep", "conv3x3_fwd", "conv3x3_wgrad", "relu_mask"]
+def client_means(out, rows, slot, counts) -> None:
+    """out[i, w] = mean of rows[i][e] over examples e with slot[e] == w (slot
+    ascending), 0 where a client has no examples here; one native kernel."""
+    _ops().client_means(out, list(rows), slot, counts)
+
+
+__all__ += ["conv_weight_prep", "conv3x3_fwd", "conv3x3_wgrad", "relu_mask", "client_means"]

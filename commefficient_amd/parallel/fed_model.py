@@ -214,6 +214,13 @@ class FedModel:
             return torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=cache)
         return nullcontext()
 
+    def _ones(self, like: torch.Tensor) -> torch.Tensor:
+        o = getattr(self, "_ones_cache", None)
+        if o is None or o.numel() < like.numel() or o.device != like.device:
+            o = torch.ones(max(like.numel(), 1024), device=like.device)
+            self._ones_cache = o
+        return o[:like.numel()]
+
     def _prep(self, xs):
         if self.channels_last:
             # pixels already channel-innermost (incl. the augmentation kernel's
@@ -252,10 +259,15 @@ class FedModel:
                                                           self.args) if want_grad else \
                     self.compute_loss_val(self.model, self._prep(inputs), targets, self.args)
         if want_grad:
-            total = per_ex.float().sum()
-            if loss_weight is not None:
-                total = total * loss_weight
-            total.backward()
+            if (loss_weight is None and not capture and per_ex.dtype == torch.float32
+                    and per_ex.dim() == 1):
+                # d(sum)/d(per_ex) = 1: a cached ones vector (no sum / fill kernels)
+                torch.autograd.backward(per_ex, grad_tensors=self._ones(per_ex))
+            else:
+                total = per_ex.float().sum()
+                if loss_weight is not None:
+                    total = total * loss_weight
+                total.backward()
         return per_ex.detach().float(), [m.detach().float() for m in metrics]
 
     # --------------------------------------------------------------- train
@@ -301,18 +313,19 @@ class FedModel:
             payload[:self.main_numel].copy_(main)
         elif main is None:
             payload[:self.main_numel].zero_()
-        payload[self.main_numel:].copy_(metric_sums.reshape(-1))
+        tail = payload[self.main_numel:]
+        if metric_sums.data_ptr() != tail.data_ptr():
+            tail.copy_(metric_sums.reshape(-1))
         with self.timer.phase("allreduce"):
             dist.all_reduce_(payload)
         # G = summed transmit / B  (fed_aggregator.py:332); the division is
-        # folded into the server's momentum kernel via gscale -> keep a view
+        # folded into the server's momentum kernel (gscale) -> keep a view
         G = payload[:self.main_numel]
-        G.mul_(1.0 / B)
         # clone: the payload buffer is reused by the next round
         metrics = payload[self.main_numel:].view(n_res, W).clone()
         dl, ul = self.accountant.round(clients, self.round_idx, meta=self._acct_meta)
         self._acct_meta = None
-        self._pending = (G, clients, False)
+        self._pending = (G, clients, False, 1.0 / B)
         self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
                            "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel())}
         return [metrics[i] for i in range(n_res)] + [dl, ul]
@@ -326,7 +339,7 @@ class FedModel:
         G = payload[:self.main_numel]  # scaled by 1/B inside the server graph
         metrics = payload[self.main_numel:].view(n_res, W).clone()
         dl, ul = self.accountant.round(clients, self.round_idx)
-        self._pending = (G, clients, True)
+        self._pending = (G, clients, True, 1.0)
         self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
                            "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel()),
                            "graph": True}
@@ -340,8 +353,15 @@ class FedModel:
             if len(my_slots) else np.zeros(0, dtype=np.int64)
         return pos, slot_per_ex.astype(np.int64)
 
-    def _metric_sums(self, rows, slots_t, n_t, W):
-        """Per-client mean loss / metrics in their global client slots."""
+    def _metric_sums(self, rows, slots_t, n_t, W, out: Optional[torch.Tensor] = None):
+        """Per-client mean loss / metrics in their global client slots
+        (``slots_t`` ascending: a client's examples are contiguous).  On the GPU
+        one native kernel writes them straight into ``out`` (the payload tail)."""
+        if (self.device.type == "cuda" and 1 <= len(rows) <= 4
+                and all(r.dtype == torch.float32 for r in rows)):
+            msum = out if out is not None else torch.empty(len(rows), W, device=self.device)
+            ops.client_means(msum, [r.contiguous() for r in rows], slots_t, n_t)
+            return msum
         msum = torch.zeros(len(rows), W, device=self.device)
         for i, r in enumerate(rows):
             msum[i].index_add_(0, slots_t, r)
@@ -417,16 +437,21 @@ class FedModel:
             pe, ms = self._fwd_bwd(xi, targets[s:e], None, groups=g)
             per_ex_all.append(pe)
             metrics_all.append(ms)
-        per_ex = torch.cat(per_ex_all) if per_ex_all else torch.zeros(0, device=self.device)
-        mets = [torch.cat([m[i] for m in metrics_all]) for i in range(len(metrics_all[0]))] \
-            if metrics_all else []
+        if len(per_ex_all) == 1:  # one microbatch: no concatenation copies
+            per_ex, mets = per_ex_all[0], list(metrics_all[0])
+        else:
+            per_ex = torch.cat(per_ex_all) if per_ex_all else torch.zeros(0, device=self.device)
+            mets = [torch.cat([m[i] for m in metrics_all]) for i in range(len(metrics_all[0]))] \
+                if metrics_all else []
         # per-client mean metrics into their global slots
         if packed is not None:
             slots_t, n_t = packed[1], packed[2]
         else:
             slots_t = dist.h2d(slot_per_ex, self.device)
             n_t = dist.h2d(counts.astype(np.float32), self.device)
-        msum = self._metric_sums([per_ex] + mets, slots_t, n_t, W)
+        rows = [per_ex] + mets
+        tail = self._payload_buf(len(rows) * W)[self.main_numel:].view(len(rows), W)
+        msum = self._metric_sums(rows, slots_t, n_t, W, out=tail)
         self._n_metrics = msum.shape[0]
         out = self._transmit_buffer()
         with self.timer.phase("encode"):
@@ -594,7 +619,7 @@ class FedModel:
     def server_step(self, lr):
         if self._pending is None:
             return  # e.g. the reference's "HACK STEP" before the first round
-        G, clients, via_graph = self._pending
+        G, clients, via_graph, gscale = self._pending
         self._pending = None
         if via_graph:
             if self.accountant.hist_for(self.round_idx).data_ptr() != self.graphs.hist_ptr:
@@ -609,7 +634,7 @@ class FedModel:
         with self.timer.phase("server"):
             self.server.update(G, lr, self.w, self.accountant.last_mod, self.round_idx,
                                self.client_state, clients,
-                               hist=self.accountant.hist_for(self.round_idx))
+                               hist=self.accountant.hist_for(self.round_idx), gscale=gscale)
         self.round_idx += 1
 
     # ------------------------------------------------------------------ val

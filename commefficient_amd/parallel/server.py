@@ -96,9 +96,9 @@ class ServerState:
 
     def update(self, G: torch.Tensor, lr, w: torch.Tensor, last_mod: torch.Tensor, round_idx: int,
                client_state=None, participating=None, step: Optional[torch.Tensor] = None,
-               hist: Optional[torch.Tensor] = None):
-        """Apply one server step.  ``G`` is the summed transmit already scaled
-        by 1/B.  ``step`` (device int32 [2] = lr bits, round) replaces the
+               hist: Optional[torch.Tensor] = None, gscale: float = 1.0):
+        """Apply one server step.  ``gscale * G`` is the summed transmit / B
+        (the scale is folded into the momentum kernel).  ``step`` (device int32 [2] = lr bits, round) replaces the
         scalar lr / round_idx when the update runs inside a captured HIP
         graph (parallel/graph.py); ``hist`` is the accountant's change histogram,
         updated with the stamps.  Returns (idx, vals) for sparse modes (the
@@ -110,10 +110,10 @@ class ServerState:
         if mode == "sketch":
             et = a.error_type
             if et == "virtual":
-                ops.momentum_ef(self.V.view(-1), self.E.view(-1), G.view(-1), rho, 1.0, "virtual")
+                ops.momentum_ef(self.V.view(-1), self.E.view(-1), G.view(-1), rho, gscale, "virtual")
                 src = self.E
             else:  # local / none: un-sketch V itself (see module docstring)
-                ops.momentum_ef(self.V.view(-1), None, G.view(-1), rho, 1.0, "none")
+                ops.momentum_ef(self.V.view(-1), None, G.view(-1), rho, gscale, "none")
                 src = self.V
             sk = self.sketch.like(src)
             idx, vals = sk.unsketch_sparse(a.k)
@@ -122,7 +122,7 @@ class ServerState:
             ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
             return idx, vals
         if mode == "true_topk":
-            ops.momentum_ef(self.V, self.E, G, rho, 1.0, "virtual")
+            ops.momentum_ef(self.V, self.E, G, rho, gscale, "virtual")
             idx, vals = ops.topk_abs(self.E, a.k)
             if client_state is not None and participating is not None:
                 client_state.zero_velocity_at(participating, idx)
@@ -130,7 +130,7 @@ class ServerState:
             ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
             return idx, vals
         if mode in ("local_topk", "uncompressed"):
-            ops.momentum_ef(self.V, None, G, rho, 1.0, "none")
+            ops.momentum_ef(self.V, None, G, rho, gscale, "none")
             if mode == "uncompressed" and a.do_dp and a.dp_mode == "server":
                 # the reference adds the noise to Vvelocity itself (``grad`` aliases
                 # it, fed_aggregator.py:502-508), so it persists in the momentum;
@@ -141,7 +141,7 @@ class ServerState:
             ops.dense_apply(w, self.V, lr_s, lr_v, last_mod, round_idx, step, hist)
             return None
         if mode == "fedavg":
-            ops.momentum_ef(self.V, None, G, rho, 1.0, "none")
+            ops.momentum_ef(self.V, None, G, rho, gscale, "none")
             ops.dense_apply(w, self.V, 1.0, None, last_mod, round_idx, step, hist)
             return None
         raise ValueError(mode)

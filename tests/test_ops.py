@@ -370,3 +370,24 @@ def test_account_hist_matches_count(device):
     cdl[clients] += exp
     cul[clients] += 7.0
     assert torch.equal(cdl_d.cpu(), cdl) and torch.equal(cul_d.cpu(), cul)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("counts_dtype", [torch.int64, torch.float32])
+def test_client_means_matches_index_add(counts_dtype):
+    """Native per-client mean metrics vs the zeros + index_add + divide
+    composition it replaces (fed_model.py _metric_sums)."""
+    g = torch.Generator().manual_seed(0)
+    W = 37
+    counts = torch.randint(1, 9, (W,), generator=g)
+    local = torch.rand(W, generator=g) < 0.6          # clients computed on this rank
+    slot = torch.cat([torch.full((int(counts[w]),), w) for w in range(W) if local[w]])
+    n = slot.numel()
+    rows = [torch.randn(n, generator=g), (torch.rand(n, generator=g) < 0.5).float()]
+    ref = torch.zeros(2, W)
+    for i, r in enumerate(rows):
+        ref[i].index_add_(0, slot, r)
+    ref /= counts.float()
+    out = torch.full((2, W), float("nan"), device="cuda")
+    ops.client_means(out, [r.cuda() for r in rows], slot.cuda(), counts.to(counts_dtype).cuda())
+    torch.testing.assert_close(out.cpu(), ref, rtol=1e-6, atol=1e-6)
