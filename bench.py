@@ -130,7 +130,9 @@ def main():
     t1 = time.perf_counter()
     if b.torch_profile:
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        stack = bool(os.environ.get("COMMEFF_PROF_STACK"))
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA],
+                     with_stack=stack) as prof:
             for i in range(b.warmup, b.warmup + min(b.steps, 5)):
                 step(i)
             torch.cuda.synchronize()
@@ -141,6 +143,10 @@ def main():
                 f.write(prof.key_averages().table(sort_by="cpu_time_total", row_limit=60))
                 f.write("\n")
                 f.write(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=60))
+                if stack:
+                    f.write("\n")
+                    f.write(prof.key_averages(group_by_stack_n=8).table(
+                        sort_by="self_cuda_time_total", row_limit=80))
     elapsed = dist.max_over_ranks(t1 - t0)
     last_loss = float(out[0].mean().item())
     dl = (float(fed.accountant.client_download.sum().item()) - dl_before) / b.steps

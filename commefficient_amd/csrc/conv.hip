@@ -496,6 +496,172 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
       }
 }
 
+// Wide wgrad tile (K >= 256): 256 out channels x 256 columns per block, 8
+// waves as 4 (k) x 2 (columns), each wave 64 x 128 (2 x 4 MFMA tiles).  Per
+// 64-pixel K-step a wave issues the same 8 LDS-DMA pieces as the 128 x 128
+// kernel but runs twice the MFMAs (the DMA issue cost, ~60-180 cycles a
+// piece, is what bounds the 128 x 128 tile).  Columns are TPG taps x 256/TPG
+// input channels (TPG = 2 for 128-channel inputs: taps 2g, 2g+1; the 10th
+// tap of the last group is a zero operand that is never stored).  The
+// operand images are pairs of the 128-wide [64 px][128] images of the small
+// kernel (same swizzle and transposed reads), one block per CU (128 KB LDS);
+// split-K over pixels fills the chip, slabs as in conv_wgrad_kernel.
+template <bool ROWSTEP, int TPG>
+__global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int HALF = BK * 128 * 2;           // one [64 px][128] image, 16 KB
+  constexpr int A_BYTES = 2 * HALF, STAGE = 4 * HALF;
+  constexpr int NLD = 8;
+  constexpr int NTAPG = TPG == 2 ? 5 : 9;
+  constexpr int CPT = 256 / TPG;               // input channels per tap in a tile
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int C = a.C, K = a.K, H = a.H, W = a.W;
+  const int ntc = C / CPT, ntk = K / 256;
+  const int ntiles = ntk * NTAPG * ntc;
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int tc = tile % ntc, rs = (tile / ntc) % NTAPG, tk = tile / (ntc * NTAPG);
+  const int k0 = tk * 256, c0 = tc * CPT;
+  const int pbeg = split * a.steps_per_split * BK;
+  const int pend = min(a.P, pbeg + a.steps_per_split * BK);
+  const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
+  const uint64_t zero = reinterpret_cast<uint64_t>(g_conv_zero);
+
+  // piece i (0..3) of thread tid: image half h = i >> 1, chunk s' in the half
+  uint64_t a_ptr[4], b_ptr[4];
+  int a_row[4], b_row[4], b_h[4], b_w[4], b_dr[4], b_ds[4];
+  uint32_t b_ok = 0;  // bit i: piece i belongs to a real tap and its column stays inside the image
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = i >> 1, sp = (i & 1) * 512 + tid;
+    const int row = sp >> 4, lc = (sp & 15) ^ sw_tr256(row);
+    a_row[i] = pbeg + row;
+    a_ptr[i] = reinterpret_cast<uint64_t>(a.dy + static_cast<size_t>(pbeg + row) * K + k0 + h * 128 + lc * 8);
+    const int n = h * 128 + lc * 8;  // tile column of the piece
+    int tap = rs, cc = c0 + n;
+    if constexpr (TPG == 2) { tap = 2 * rs + h; cc = c0 + lc * 8; }
+    const bool real = tap < 9;
+    if (tap > 8) tap = 8;
+    b_dr[i] = tap / 3 - 1;
+    b_ds[i] = tap % 3 - 1;
+    const int p = pbeg + row;
+    b_row[i] = p;
+    const uint32_t q = fdiv(static_cast<uint32_t>(p), a.div_w);
+    b_w[i] = p - static_cast<int>(q) * W;
+    b_h[i] = static_cast<int>(q - fdiv(q, a.div_h) * H) + b_dr[i];
+    b_ptr[i] = reinterpret_cast<uint64_t>(a.x + static_cast<int64_t>(p + b_dr[i] * W + b_ds[i]) * C + cc);
+    if (real && static_cast<unsigned>(b_w[i] + b_ds[i]) < static_cast<unsigned>(W)) b_ok |= 1u << i;
+    if (!ROWSTEP && real) b_ok |= 16u << i;  // (recomputed per step below)
+  }
+  const int dh = ROWSTEP ? (BK / W) % H : 0;
+
+  auto issue = [&](int stage, bool full) __attribute__((always_inline)) {
+    unsigned char* base = smem + stage * STAGE + wid * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(reinterpret_cast<const void*>(full || a_row[i] < pend ? a_ptr[i] : zero),
+             base + (i >> 1) * HALF + (i & 1) * 8192);
+      a_row[i] += BK;
+      a_ptr[i] += static_cast<uint64_t>(BK) * K * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bool ok = static_cast<unsigned>(b_h[i]) < static_cast<unsigned>(H);
+      if constexpr (ROWSTEP) ok = ok && ((b_ok >> i) & 1u);
+      else ok = ok && ((b_ok >> (4 + i)) & 1u) && static_cast<unsigned>(b_w[i] + b_ds[i]) < static_cast<unsigned>(W);
+      if (!full) ok = ok && b_row[i] < pend;
+      glds16(reinterpret_cast<const void*>(ok ? b_ptr[i] : zero),
+             base + A_BYTES + (i >> 1) * HALF + (i & 1) * 8192);
+      b_row[i] += BK;
+      b_ptr[i] += static_cast<uint64_t>(BK) * C * 2;
+      if constexpr (ROWSTEP) {
+        const int nh = b_h[i] + dh;
+        b_h[i] = nh - b_dr[i] >= H ? nh - H : nh;
+      } else {
+        const uint32_t q = fdiv(static_cast<uint32_t>(b_row[i]), a.div_w);
+        b_w[i] = b_row[i] - static_cast<int>(q) * W;
+        b_h[i] = static_cast<int>(q - fdiv(q, a.div_h) * H) + b_dr[i];
+      }
+    }
+  };
+
+  f32x16_t acc[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
+
+  if (nsteps > 0) issue(0, pbeg + BK <= pend);
+  // transposed-read offsets: A rows k = wr*64 + mi*32 live in half wr >> 1;
+  // B columns wc*128 + ni*32 in half wc
+  int toA[2][2], toB[4][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    tr_offsets<256>((wr & 1) * 64 + mi * 32, lane, toA[mi]);
+    toA[mi][0] += (wr >> 1) * HALF;
+    toA[mi][1] += (wr >> 1) * HALF;
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    tr_offsets<256>(ni * 32, lane, toB[ni]);
+    toB[ni][0] += A_BYTES + wc * HALF;
+    toB[ni][1] += A_BYTES + wc * HALF;
+  }
+  int rd = 0;
+  for (int st = 0; st < nsteps; ++st) {
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + 1 < nsteps) issue(rd ^ 1, pbeg + (st + 2) * BK <= pend);
+    const unsigned char* sb = smem + rd * STAGE;
+    bf16x8_t af[2][2], bfr[2][4];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) af[0][mi] = tr_read(sb + toA[mi][0], sb + toA[mi][1]);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) bfr[0][ni] = tr_read(sb + toB[ni][0], sb + toB[ni][1]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int cur = kk & 1, nxt = cur ^ 1;
+      if (kk + 1 < 4) {
+        const int dd = (kk + 1) * 16 * 256;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+          af[nxt][mi] = tr_read(sb + toA[mi][0] + dd, sb + toA[mi][1] + dd);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          bfr[nxt][ni] = tr_read(sb + toB[ni][0] + dd, sb + toB[ni][1] + dd);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
+    }
+    rd ^= 1;
+  }
+
+  float* slab = a.slab + static_cast<size_t>(split) * K * 9 * C;
+  const int hi = lane >> 5, lr = lane & 31;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = wc * 128 + ni * 32 + lr;
+      int tap = rs, c = c0 + n;
+      if constexpr (TPG == 2) { tap = 2 * rs + (n >> 7); c = c0 + (n & 127); }
+      if (tap > 8) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int k = k0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        slab[(static_cast<size_t>(k) * 9 + tap) * C + c] = acc[mi][ni][e];
+      }
+    }
+}
+
 // dw[k][c][r][s] (fp32, PyTorch layout) = beta*dw + sum_split slab[split][k][rs][c]
 // One block per (k, 64 channels).  Thread (c, part) sums the 9 taps of its
 // channel over splits part, part+4, ... (9 independent loads per split, read
@@ -610,8 +776,19 @@ int grid_for(int64_t n, int per_block) {
   return static_cast<int>(b < 1 ? 1 : b);
 }
 
+// the wide (256 x 256) wgrad kernel: K a multiple of 256, C = 128 (tap pairs)
+// or a multiple of 256
+bool wgrad_wide(int K, int C) {
+  static const bool off = [] {
+    const char* e = getenv("COMMEFF_WGRAD_WIDE");
+    return e != nullptr && e[0] == '0';
+  }();
+  return !off && K % 256 == 0 && (C == 128 || C % 256 == 0);
+}
+
 // (k, c) x tap-group tiles of one wgrad: 64-channel inputs pair taps (PAIR)
 int wgrad_tiles(int K, int C) {
+  if (wgrad_wide(K, C)) return (K / 256) * (C == 128 ? 5 : 9 * (C / 256));
   if (C == 64) return (K / WBM) * 5;
   return (K / WBM) * 9 * (C / (C % 128 == 0 ? 128 : 64));
 }
@@ -705,9 +882,35 @@ static int wgrad_slots() {
   return slots;
 }
 
+template <bool ROWSTEP>
+void launch_wgrad_wide(const ConvWgradArgs& a, hipStream_t stream) {
+  constexpr int lds = 2 * 4 * BK * 128 * 2;
+  const int tiles = wgrad_tiles(a.K, a.C);
+  if (a.C == 128) {
+    static bool init = false;
+    if (!init) {
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 2>), lds);
+      init = true;
+    }
+    hipLaunchKernelGGL((conv_wgrad_wide_kernel<ROWSTEP, 2>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+  } else {
+    static bool init = false;
+    if (!init) {
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 1>), lds);
+      init = true;
+    }
+    hipLaunchKernelGGL((conv_wgrad_wide_kernel<ROWSTEP, 1>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+  }
+}
+
 int conv3x3_wgrad_splits(int P, int K, int C) {
   const int tiles = wgrad_tiles(K, C);
   const int steps = (P + BK - 1) / BK;
+  if (wgrad_wide(K, C)) {  // one 128 KB block per CU, >= 16 K-steps each
+    int s = wgrad_slots() / 2 / tiles;
+    if (s > steps / 16) s = steps / 16;
+    return s < 1 ? 1 : s;
+  }
   // every block resident at once (equal-work blocks: one block past the
   // resident slots costs a whole extra block time), >= 32 K-steps each
   int s = wgrad_slots() / tiles;
@@ -726,7 +929,9 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
   }();
   const bool rowstep = BK % a.W == 0;
   const bool wide = a.C % 128 == 0;
-  if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)
+  if (wgrad_wide(a.K, a.C)) {
+    if (rowstep) launch_wgrad_wide<true>(a, stream); else launch_wgrad_wide<false>(a, stream);
+  } else if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)
     if (rowstep) launch_wgrad<128, 2, true, true>(a, stream); else launch_wgrad<128, 2, false, true>(a, stream);
   } else if (three && rowstep) {
     if (wide) launch_wgrad<128, 3, true>(a, stream); else launch_wgrad<64, 3, true>(a, stream);

@@ -18,6 +18,8 @@ SHAPES = [  # N, C, H, W, K   (ResNet-9 layers at small batch + odd tiles)
     (3, 64, 5, 7, 128),   # pixels not a multiple of the 128-pixel tile
     (2, 128, 8, 8, 64),   # 64-wide output tile (dgrad of a 64-channel input)
     (2, 64, 8, 8, 256),   # tap-paired wgrad over two output-channel tiles
+    (3, 128, 5, 7, 256),  # wide wgrad, tap pairs, W not dividing the 64-pixel step
+    (2, 256, 6, 10, 256), # wide wgrad, one tap per tile, W not dividing the step
 ]
 
 
