@@ -199,20 +199,28 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
   __builtin_amdgcn_s_barrier();
 
   // ---- epilogue: fp32 tile in LDS -> fused ops -> 16-byte bf16 stores
+  // (tiles taller than 128 rows go through LDS in 128-row passes)
   constexpr int LD = BN + 4;
+  constexpr int EPR = TBM > 128 ? 128 : TBM;
   float* ct = reinterpret_cast<float*>(smem);
+  constexpr int CPR = BN / 8;  // 16-byte output chunks per row
+#pragma unroll 1
+  for (int ps = 0; ps < TBM / EPR; ++ps) {
+  if (ps > 0) __syncthreads();  // the previous pass has read ct
+  if ((wr * 64) / EPR == ps) {
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        const int row = wr * 64 - ps * EPR + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
         const int col = wc * (BN / 2) + ni * 32 + lr;
         ct[row * LD + col] = acc[mi][ni][e];
       }
+  }
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 16-byte output chunks per row
+  const int mp = m0 + ps * EPR;  // first pixel of this pass
   if constexpr (POOL) {
     // fused ReLU + 2x2 max-pool (csrc/pool.hip semantics): the tile holds
     // whole image-row pairs (TBM % 2W == 0, m0 % 2W == 0), so its pooled
@@ -220,13 +228,13 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
     // compared after bf16 rounding (as the unfused path pools the stored bf16
     // conv output); code = window position of the max, 255 when max <= 0.
     const int W = a.W, OWl = W >> 1;
-    const int q0 = m0 >> 2;
+    const int q0 = mp >> 2;
 #pragma unroll 1
-    for (int e = tid; e < (TBM / 4) * CPR; e += NT) {
+    for (int e = tid; e < (EPR / 4) * CPR; e += NT) {
       const int pq = e / CPR, cc = e - pq * CPR;
       const int r2 = pq / OWl, ow = pq - r2 * OWl;
       const int row0 = 2 * r2 * W + 2 * ow;
-      if (m0 + row0 >= a.P) continue;
+      if (mp + row0 >= a.P) continue;
       float best[8];
       uint32_t arg[8];
 #pragma unroll
@@ -266,13 +274,13 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
       *reinterpret_cast<v4u*>(a.y + o) = out;
       *reinterpret_cast<uint64_t*>(a.pool_idx + o) = codes;
     }
-    return;
+    continue;
   }
   const bool relu = a.relu != 0;
 #pragma unroll 2
-  for (int e = tid; e < TBM * CPR; e += NT) {
+  for (int e = tid; e < EPR * CPR; e += NT) {
     const int row = e / CPR, cc = e - row * CPR;
-    const int p = m0 + row;
+    const int p = mp + row;
     if (p >= a.P) continue;
     const float4 lo = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8);
     const float4 up = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8 + 4);
@@ -311,6 +319,7 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
     out[3] = pack_bf16(v[6], v[7]);
     *reinterpret_cast<v4u*>(a.y + o) = out;
   }
+  }  // pass
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -800,7 +809,7 @@ void set_lds(const void* fn, int bytes) {
 template <int TBM, int BN, int NSTAGE, bool POOL = false>
 void launch_fwd(const ConvFwdArgs& a, hipStream_t stream) {
   constexpr int lds_pipe = NSTAGE * (TBM * 128 + BN * 128);
-  constexpr int lds_epi = TBM * (BN + 4) * 4;
+  constexpr int lds_epi = (TBM > 128 ? 128 : TBM) * (BN + 4) * 4;
   constexpr int lds = lds_pipe > lds_epi ? lds_pipe : lds_epi;
   static bool init = false;
   if (!init) {
@@ -827,6 +836,8 @@ void launch_wgrad(const ConvWgradArgs& a, hipStream_t stream) {
 
 }  // namespace
 
+static int wgrad_slots();
+
 bool conv3x3_supported(int C, int K) { return C % 64 == 0 && K % 64 == 0 && C >= 64 && K >= 64; }
 
 bool conv3x3_pool_supported(int H, int W, int K) {
@@ -837,7 +848,19 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   if (a.pool == 2) {  // caller checked conv3x3_pool_supported
-    launch_fwd<128, 128, 2, true>(a, stream);
+    // opt-in (COMMEFF_CONV_WIDE=1): 256 x 256 tiles (8 waves of 64 x 128, half
+    // the LDS-DMA pieces per MFMA) when they still give every CU a block --
+    // measured throughput-neutral on ResNet-9 (profiles/r1_experiments.md),
+    // unlike the wide wgrad
+    static const bool wide_on = [] {
+      const char* e = getenv("COMMEFF_CONV_WIDE");
+      return e != nullptr && e[0] == '1';
+    }();
+    const int64_t wide_blocks = static_cast<int64_t>((a.P + 255) / 256) * (a.K / 256);
+    if (wide_on && a.K % 256 == 0 && wide_blocks * 10 >= static_cast<int64_t>(wgrad_slots()) / 2 * 9)
+      launch_fwd<256, 256, 2, true>(a, stream);
+    else
+      launch_fwd<128, 128, 2, true>(a, stream);
     return;
   }
   const bool wide = a.K % 128 == 0;

@@ -291,7 +291,9 @@ def test_augment_writes_padded_pixels():
 
 
 @pytest.mark.parametrize("N, C, H, K", [(3, 64, 32, 128), (5, 128, 16, 256), (7, 256, 8, 512),
-                                        (2, 64, 4, 128)])
+                                        (2, 64, 4, 128),
+                                        # batches big enough for the 256 x 256 tile
+                                        (467, 128, 16, 256), (481, 256, 8, 512)])
 def test_fused_pool_epilogue_matches_unfused(N, C, H, K):
     """conv3x3_fwd_pool2 == relu_maxpool(conv3x3_fwd(x), 2) bit for bit
     (values and window codes)."""
