@@ -70,28 +70,12 @@ hist_kernel(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ hist,
   for (int b = threadIdx.x; b < kBins; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const uint32_t prefix = PASS == 0 ? 0u : st->prefix;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x * 4;
-  // 16-byte loads where possible
-  const int64_t n4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 ? (n / 4) * 4 : 0;
-  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4; i < n4;
-       i += stride) {
-    float4 v = *reinterpret_cast<const float4*>(x + i);
-    float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t k = key_of(vv[q]);
-      if (PASS == 0) {
-        atomicAdd(h + (k >> 20), 1u);
-      } else if (PASS == 1) {
-        if ((k >> 20) == prefix) atomicAdd(h + ((k >> 9) & 0x7ff), 1u);
-      } else {
-        if ((k >> 9) == prefix) atomicAdd(h + (k & 0x1ff), 1u);
-      }
-    }
-  }
-  for (int64_t i = n4 + static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    uint32_t k = key_of(x[i]);
+  // (LDS atomics retire ~0.4 lanes/clk/CU and bound pass 0; per-wave
+  // sub-histograms measured no faster, wave-aggregated atomics 4x slower:
+  // normal-ish data spreads a wave over too many distinct bins)
+  auto add = [&](float v, bool in) __attribute__((always_inline)) {
+    if (!in) return;
+    const uint32_t k = key_of(v);
     if (PASS == 0) {
       atomicAdd(h + (k >> 20), 1u);
     } else if (PASS == 1) {
@@ -99,10 +83,37 @@ hist_kernel(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ hist,
     } else {
       if ((k >> 9) == prefix) atomicAdd(h + (k & 0x1ff), 1u);
     }
+  };
+  // 16-byte loads, kU of them in flight per thread before the LDS atomics
+  // (one load at a time left the pass latency-bound)
+  constexpr int kU = 4;
+  const int64_t n4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 ? n / 4 : 0;  // float4 count
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  const int64_t nt = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * blockDim.x; i0 < n4; i0 += kU * nt) {
+    const int64_t i = i0 + threadIdx.x;
+    float4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      v[u] = i + u * nt < n4 ? x4[i + u * nt] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const bool in = i + u * nt < n4;
+      add(v[u].x, in);
+      add(v[u].y, in);
+      add(v[u].z, in);
+      add(v[u].w, in);
+    }
+  }
+  // scalar tail
+  const int64_t t0 = n4 * 4 + static_cast<int64_t>(blockIdx.x) * blockDim.x;
+  for (int64_t i = t0; i < n; i += nt) {
+    const int64_t j = i + threadIdx.x;
+    add(j < n ? x[j] : 0.f, j < n);
   }
   __syncthreads();
   for (int b = threadIdx.x; b < kBins; b += blockDim.x) {
-    uint32_t c = h[b];
+    const uint32_t c = h[b];
     if (c) atomicAdd(hist + b, c);
   }
 }
@@ -179,10 +190,17 @@ count_kernel(const float* __restrict__ x, int64_t n, int64_t span,
   const int64_t i0 = blockIdx.x * span;
   const int64_t i1 = min(n, i0 + span);
   uint32_t gt = 0, eq = 0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    uint32_t k = key_of(x[i]);
-    gt += k > thr;
-    eq += k == thr;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += 4 * blockDim.x) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = i + u * blockDim.x < i1 ? x[i + u * blockDim.x] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t k = key_of(v[u]);
+      const bool in = i + u * blockDim.x < i1;
+      gt += in && k > thr;
+      eq += in && k == thr;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) {
     gt += __shfl_down(gt, o);
@@ -226,6 +244,28 @@ scan_kernel(int nb, const State* __restrict__ st, const uint32_t* __restrict__ c
   }
 }
 
+// exclusive prefix sum over a 256-thread block (4 waves); `wt` is a 4-entry
+// LDS array private to this call site; returns the block total in `total`
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wt, uint32_t& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wt[wave] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) before += w < wave ? wt[w] : 0u;
+  total = wt[0] + wt[1] + wt[2] + wt[3];
+  return before + inc - v;
+}
+
+// ordered compaction: a block owns [i0, i1); per iteration each thread takes
+// 4 consecutive elements (one 16-byte load), tie ranks and output slots come
+// from two block-wide exclusive scans (elements stay in ascending order)
 __global__ void __launch_bounds__(256)
 write_kernel(const float* __restrict__ x, int64_t n, int64_t span,
              const State* __restrict__ st, const uint32_t* __restrict__ off_sel,
@@ -237,46 +277,48 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span,
   const int64_t i1 = min(n, i0 + span);
   uint32_t sel_base = off_sel[blockIdx.x];
   uint32_t eq_base = off_eq[blockIdx.x];
-  __shared__ uint32_t wsel[4], weq[4];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int64_t base = i0; base < i1; base += blockDim.x) {
-    int64_t i = base + threadIdx.x;
-    float v = 0.f;
-    uint32_t k = 0;
-    bool in = i < i1;
-    if (in) {
-      v = x[i];
-      k = key_of(v);
+  __shared__ uint32_t wt_eq[4], wt_sel[4];
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  for (int64_t base = i0; base < i1; base += 1024) {
+    const int64_t i = base + 4 * threadIdx.x;
+    float v[4];
+    if (al && i + 3 < i1) {
+      const float4 q = *reinterpret_cast<const float4*>(x + i);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i + u < i1 ? x[i + u] : 0.f;
     }
-    bool gt = in && k > thr;
-    bool eq = in && k == thr;
-    uint64_t bal_eq = __ballot(eq);
-    // tie rank needs the eq-prefix first
-    uint32_t eq_lane = __popcll(bal_eq & lt_mask);
-    if (lane == 0) weq[wave] = __popcll(bal_eq);
-    __syncthreads();
-    uint32_t eq_wave = 0;
-    for (int w = 0; w < wave; ++w) eq_wave += weq[w];
-    uint32_t eq_tot = weq[0] + weq[1] + weq[2] + weq[3];
-    uint32_t tie_rank = eq_base + eq_wave + eq_lane;
-    bool sel = gt || (eq && tie_rank < ties);
-    uint64_t bal_sel = __ballot(sel);
-    uint32_t sel_lane = __popcll(bal_sel & lt_mask);
-    if (lane == 0) wsel[wave] = __popcll(bal_sel);
-    __syncthreads();
-    uint32_t sel_wave = 0;
-    for (int w = 0; w < wave; ++w) sel_wave += wsel[w];
-    uint32_t sel_tot = wsel[0] + wsel[1] + wsel[2] + wsel[3];
-    if (sel) {
-      uint32_t pos = sel_base + sel_wave + sel_lane;
-      idx[pos] = i;
-      vals[pos] = v;
+    uint32_t gtm = 0, eqm = 0;  // bit u: element i+u is > thr / == thr
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t k = key_of(v[u]);
+      const bool in = i + u < i1;
+      gtm |= (in && k > thr ? 1u : 0u) << u;
+      eqm |= (in && k == thr ? 1u : 0u) << u;
+    }
+    uint32_t eq_tot, sel_tot;
+    uint32_t er = eq_base + block_excl_scan(__popc(eqm), wt_eq, eq_tot);
+    uint32_t selm = gtm;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if ((eqm >> u) & 1u) {
+        if (er < ties) selm |= 1u << u;
+        ++er;
+      }
+    }
+    uint32_t pos = sel_base + block_excl_scan(__popc(selm), wt_sel, sel_tot);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if ((selm >> u) & 1u) {
+        idx[pos] = i + u;
+        vals[pos] = v[u];
+        ++pos;
+      }
     }
     sel_base += sel_tot;
     eq_base += eq_tot;
-    __syncthreads();  // wsel/weq reuse
+    __syncthreads();  // wt_eq / wt_sel reuse
   }
 }
 
@@ -304,7 +346,7 @@ void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* 
   int nb = static_cast<int>((n + 255) / 256);
   if (nb > kNB) nb = kNB;
   int64_t span = (n + nb - 1) / nb;
-  span = ((span + 255) / 256) * 256;
+  span = ((span + 1023) / 1024) * 1024;  // write_kernel: 1024 elements per block step
   nb = static_cast<int>((n + span - 1) / span);
   hipLaunchKernelGGL(count_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w.st, w.cnt_gt,
                      w.cnt_eq);
