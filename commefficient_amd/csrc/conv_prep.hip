@@ -81,6 +81,10 @@ __global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
   // weight fragments (row m = 32 mt + lr, GEMM k = 16 s + 8 hi + j -> tap k/4,
   // channel k%4), built once per block in LDS
   __shared__ bf16x8_t wsm[2][3][64];
+  // per-wave output staging: 32 pixel rows of 64 channels, 144-byte row pitch
+  // (16-byte aligned, 2-way bank aliasing for the 8-byte fragment writes)
+  constexpr int kPitch = 144;
+  __shared__ __attribute__((aligned(16))) unsigned char ysm[4][32 * kPitch];
   for (int e = threadIdx.x; e < 2 * 3 * 64 * 8; e += 256) {
     const int j = e & 7, ln = (e >> 3) & 63, ms = e >> 9;  // ms = mt*3 + s
     const int mt = ms / 3, s = ms - 3 * mt;
@@ -116,25 +120,35 @@ __global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
         acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[mt][s], b[s], acc[mt], 0, 0, 0);
     }
     const int p = tile * 32 + lr;
-    if (p < a.P) {
-      // lane (pixel p, hi) holds channels 32 mt + 8 g + 4 hi + (0..3) in acc[mt][4 g ..]
-      uint32_t mbits = 0;
-      uint16_t* yrow = a.y + static_cast<size_t>(p) * kPrepK;
+    // lane (pixel p, hi) holds channels 32 mt + 8 g + 4 hi + (0..3) in
+    // acc[mt][4 g ..]: ReLU + bf16 into the wave's LDS rows, then whole
+    // 128-byte output rows leave with 16-byte stores (8 rows per instruction)
+    unsigned char* ys = ysm[threadIdx.x >> 6];
+    uint32_t mbits = 0;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float v[4];
+      for (int g = 0; g < 4; ++g) {
+        float v[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[j] = fmaxf(acc[mt][4 * g + j], 0.f);
-            mbits |= (v[j] > 0.f ? 1u : 0u) << (16 * mt + 4 * g + j);
-          }
-          const v2u o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
-          *reinterpret_cast<v2u*>(yrow + 32 * mt + 8 * g + 4 * hi) = o;
+        for (int j = 0; j < 4; ++j) {
+          v[j] = fmaxf(acc[mt][4 * g + j], 0.f);
+          mbits |= (v[j] > 0.f ? 1u : 0u) << (16 * mt + 4 * g + j);
         }
-      a.mask[2 * p + hi] = mbits;
+        const v2u o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3])};
+        *reinterpret_cast<v2u*>(ys + lr * kPitch + (32 * mt + 8 * g + 4 * hi) * 2) = o;
+      }
+    if (p < a.P) a.mask[2 * p + hi] = mbits;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = q * 64 + lane, row = c >> 3, col = c & 7;
+      const v4u o = *reinterpret_cast<const v4u*>(ys + row * kPitch + col * 16);
+      if (tile * 32 + row < a.P)
+        *reinterpret_cast<v4u*>(a.y + static_cast<size_t>(tile * 32 + row) * kPrepK + col * 8) = o;
     }
+    __builtin_amdgcn_wave_barrier();  // rows read before the next tile overwrites them
     if (next >= ntiles) break;
     tile = next;
 #pragma unroll
