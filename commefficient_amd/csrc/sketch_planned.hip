@@ -126,25 +126,34 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
     constexpr uint32_t kB = 16;
     const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = nt >> 5;
     for (uint32_t c0 = hw * kB; c0 < num_chunks; c0 += nhw * kB) {
-      float v[kB];
-      uint32_t pl[kB];
+      // entries l32 and l32 + 32 of every run in flight at once (runs average
+      // ~26 entries; a serial second round trip for the ~10 % of runs longer
+      // than 32 used to stall the whole batch)
+      float v[kB], v2[kB];
+      uint32_t pl[kB], pl2[kB];
 #pragma unroll
       for (uint32_t q = 0; q < kB; ++q) {
         const uint32_t ch = c0 + q;
-        v[q] = 0.f;
-        pl[q] = 0xffffffffu;
-        if (ch < num_chunks && l32 < static_cast<uint32_t>(mpos[ch + 1] - mpos[ch])) {
+        v[q] = v2[q] = 0.f;
+        pl[q] = pl2[q] = 0xffffffffu;
+        const uint32_t len = ch < num_chunks ? static_cast<uint32_t>(mpos[ch + 1] - mpos[ch]) : 0u;
+        if (l32 < len) {
           v[q] = vals[msrc[ch] + l32];
           pl[q] = perm[msrc[ch] + l32];
+        }
+        if (l32 + 32 < len) {
+          v2[q] = vals[msrc[ch] + l32 + 32];
+          pl2[q] = perm[msrc[ch] + l32 + 32];
         }
       }
 #pragma unroll
       for (uint32_t q = 0; q < kB; ++q) {
         if (pl[q] != 0xffffffffu) S[pl[q] & 0x7fffu] = signed_v(v[q], pl[q]);
+        if (pl2[q] != 0xffffffffu) S[pl2[q] & 0x7fffu] = signed_v(v2[q], pl2[q]);
         const uint32_t ch = c0 + q;
         if (ch < num_chunks) {
           const uint32_t len = mpos[ch + 1] - mpos[ch];
-          for (uint32_t k = l32 + 32; k < len; k += 32) {
+          for (uint32_t k = l32 + 64; k < len; k += 32) {
             const uint32_t x = msrc[ch] + k, p = perm[x];
             S[p & 0x7fffu] = signed_v(vals[x], p);
           }
@@ -252,12 +261,14 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
   constexpr uint32_t kB = 16;
   const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
   for (uint32_t t0 = hw * kB; t0 < num_tiles; t0 += nhw * kB) {
-    float v[kB];
+    float v[kB], v2[kB];
 #pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
       const uint32_t t = t0 + q;
-      v[q] = 0.f;
-      if (t < num_tiles && l32 < soff[t + 1] - soff[t]) v[q] = vals[sbase[t] + l32];
+      v[q] = v2[q] = 0.f;
+      const uint32_t len = t < num_tiles ? soff[t + 1] - soff[t] : 0u;
+      if (l32 < len) v[q] = vals[sbase[t] + l32];
+      if (l32 + 32 < len) v2[q] = vals[sbase[t] + l32 + 32];
     }
 #pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
@@ -265,7 +276,8 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
       if (t < num_tiles) {
         const uint32_t o = soff[t], len = soff[t + 1] - o;
         if (l32 < len) stage[o + l32] = v[q];
-        for (uint32_t k = l32 + 32; k < len; k += 32) stage[o + k] = vals[sbase[t] + k];
+        if (l32 + 32 < len) stage[o + l32 + 32] = v2[q];
+        for (uint32_t k = l32 + 64; k < len; k += 32) stage[o + k] = vals[sbase[t] + k];
       }
     }
   }
