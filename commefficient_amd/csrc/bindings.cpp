@@ -826,6 +826,71 @@ at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at:
   return dx;
 }
 
+// ghost batch norm: x [N, C, H, W] bf16 channels_last, G | N groups.
+// returns (y, stat [G, 2, C] = mean, rstd); running stats updated in place
+std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c10::optional<at::Tensor>& w,
+                                                    const c10::optional<at::Tensor>& b, int64_t G, double eps,
+                                                    double momentum, const c10::optional<at::Tensor>& run_mean,
+                                                    const c10::optional<at::Tensor>& run_var) {
+  check_nhwc_bf16(x, "ghost_bn: x");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  TORCH_CHECK(G >= 1 && N % G == 0 && C % 8 == 0 && C <= 2048, "ghost_bn: G | N, C % 8 == 0, C <= 2048");
+  const int64_t M = N / G * HW;
+  TORCH_CHECK(G * M * C / 8 < (int64_t{1} << 31), "ghost_bn: tensor too large");
+  auto f32 = [&](const c10::optional<at::Tensor>& t, const char* n) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C, n);
+    return t->data_ptr<float>();
+  };
+  float* wp = f32(w, "ghost_bn: weight f32 [C]");
+  float* bp = f32(b, "ghost_bn: bias f32 [C]");
+  TORCH_CHECK((wp == nullptr) == (bp == nullptr), "ghost_bn: weight and bias together");
+  float* rm = f32(run_mean, "ghost_bn: running_mean f32 [C]");
+  float* rv = f32(run_var, "ghost_bn: running_var f32 [C]");
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "ghost_bn: running stats together");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
+  auto fo = x.options().dtype(at::kFloat);
+  auto part = at::empty({G * S * 2 * C}, fo);
+  auto stat = at::empty({G, 2, C}, fo);
+  auto y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_bn_fwd(bf16_ptr(x), wp, bp, static_cast<int>(G), static_cast<int>(M), static_cast<int>(C),
+                static_cast<float>(eps), static_cast<float>(momentum), rm, rv, part.data_ptr<float>(),
+                stat.data_ptr<float>(), reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
+  return {y, stat};
+}
+
+// returns (dx, dweight, dbias) (dweight / dbias undefined without affine)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor& dy, const at::Tensor& x,
+                                                                const at::Tensor& stat,
+                                                                const c10::optional<at::Tensor>& w, int64_t G) {
+  check_nhwc_bf16(x, "ghost_bn_bwd: x");
+  check_nhwc_bf16(dy, "ghost_bn_bwd: dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "ghost_bn_bwd: dy shape");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  const int64_t M = N / G * HW;
+  TORCH_CHECK(stat.scalar_type() == at::kFloat && stat.is_contiguous() && stat.numel() == G * 2 * C,
+              "ghost_bn_bwd: stat");
+  const bool affine = w.has_value() && w->defined();
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
+  auto fo = x.options().dtype(at::kFloat);
+  auto part = at::empty({G * S * 2 * C}, fo);
+  auto coef = at::empty({G * 3 * C}, fo);
+  at::Tensor dw, db;
+  if (affine) {
+    dw = at::empty({C}, fo);
+    db = at::empty({C}, fo);
+  }
+  auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_bn_bwd(bf16_ptr(x), bf16_ptr(dy), stat.data_ptr<float>(), affine ? w->data_ptr<float>() : nullptr,
+                static_cast<int>(G), static_cast<int>(M), static_cast<int>(C), part.data_ptr<float>(),
+                coef.data_ptr<float>(), affine ? dw.data_ptr<float>() : nullptr,
+                affine ? db.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                cur_stream());
+  return {dx, dw, db};
+}
+
 // per-client mean metrics into out [m, W] (f32, contiguous): see loss.hip
 void client_means_hip(at::Tensor out, at::TensorList rows, const at::Tensor& slot,
                       const at::Tensor& counts) {
@@ -1097,6 +1162,9 @@ TORCH_LIBRARY(commeff, m) {
   m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
+  m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
+        "Tensor(b!)? run_var) -> (Tensor, Tensor)");
+  m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
@@ -1172,6 +1240,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
   m.impl("ce_fwd", &ce_fwd_hip);
   m.impl("client_means", &client_means_hip);
+  m.impl("ghost_bn_fwd", &ghost_bn_fwd_hip);
+  m.impl("ghost_bn_bwd", &ghost_bn_bwd_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
   m.impl("conv3x3_wgrad_into", &conv3x3_wgrad_into_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);

@@ -1,0 +1,286 @@
+// Ghost batch norm (per-client batch statistics) for gfx950, NHWC bf16.
+//
+// The engine merges a round's clients into one forward/backward; with
+// BatchNorm each client's examples must still be normalised with that
+// client's own batch statistics, as in the reference where every client runs
+// its own forward (/root/reference/CommEfficient/fed_worker.py:162-176,
+// models/resnets.py BatchNorm2d).  The batch is G equal groups of
+// M = (N/G)*H*W pixels; statistics are per (group, channel).
+//
+// Forward  (3 launches): partial shifted sums per (group, pixel slab) ->
+//          per-(group, channel) mean / rstd (+ running-stat update with the
+//          group-averaged moments, one thread per channel, fixed order) ->
+//          y = (x - mean) * rstd * w + b, 16-byte loads/stores.
+// Backward (3 launches): partial sums of dy and dy*xhat per (group, slab) ->
+//          per-(group, channel) coefficients, dweight / dbias (fixed-order
+//          sums over groups: deterministic) -> dx = w rstd (dy - mean(dy) -
+//          xhat mean(dy xhat)).
+// Sums are shifted by the group's first pixel (E[(x-K)^2] - E[x-K]^2 keeps
+// fp32 accurate when |mean| >> std).  Replaces ~40 PyTorch kernels (reshape
+// copies, reductions, elementwise, autograd) per BN layer.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+
+namespace commeff {
+namespace {
+
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ void unpack8(const u4 v, float (&f)[8]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = lo_bf(v[q]);
+    f[2 * q + 1] = hi_bf(v[q]);
+  }
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const b2 t = {static_cast<__bf16>(a), static_cast<__bf16>(b)};
+  return __builtin_bit_cast(uint32_t, t);
+}
+
+// thread layout of the partial-sum kernels: CL = C/8 chunk lanes (16 bytes =
+// 8 channels each) x PL = 256/CL pixel lanes; a block covers pixel slab s of
+// group g, every channel.
+template <bool BWD>
+__global__ void __launch_bounds__(256)
+bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                  const float* __restrict__ stat, int C, int M, int S,
+                  float* __restrict__ part) {
+  // part[(g*S + s)*2*C + {0: sum, C: sum2}][c]
+  __shared__ float red[2][256][8];
+  const int g = blockIdx.x / S, s = blockIdx.x - g * S;
+  const int CL = C >> 3, PL = 256 / CL;
+  const int cl = threadIdx.x % CL, pl = threadIdx.x / CL;
+  const bool active = pl < PL;
+  const int per = (M + S - 1) / S;
+  const int p0 = s * per, p1 = min(M, p0 + per);
+  const size_t gbase = static_cast<size_t>(g) * M;
+  float a[8], b[8], k[8], r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = k[j] = r[j] = 0.f;
+  if (!BWD) {
+    // shift: the group's first pixel
+    const u4 kv = *reinterpret_cast<const u4*>(x + gbase * C + cl * 8);
+    unpack8(kv, k);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k[j] = stat[(static_cast<size_t>(g) * 2) * C + cl * 8 + j];      // mean
+      r[j] = stat[(static_cast<size_t>(g) * 2 + 1) * C + cl * 8 + j];  // rstd
+    }
+  }
+  if (active) {
+    for (int p = p0 + pl; p < p1; p += 2 * PL) {
+      const bool two = p + PL < p1;
+      const size_t o0 = (gbase + p) * C + cl * 8, o1 = (gbase + p + PL) * C + cl * 8;
+      const u4 x0 = *reinterpret_cast<const u4*>(x + o0);
+      const u4 x1 = two ? *reinterpret_cast<const u4*>(x + o1) : x0;
+      u4 d0 = {0u, 0u, 0u, 0u}, d1 = {0u, 0u, 0u, 0u};
+      if (BWD) {
+        d0 = *reinterpret_cast<const u4*>(dy + o0);
+        if (two) d1 = *reinterpret_cast<const u4*>(dy + o1);
+      }
+      float f0[8], f1[8];
+      unpack8(x0, f0);
+      unpack8(x1, f1);
+      if (!BWD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float u = f0[j] - k[j], v = two ? f1[j] - k[j] : 0.f;
+          a[j] += u + v;
+          b[j] += u * u + v * v;
+        }
+      } else {
+        float e0[8], e1[8];
+        unpack8(d0, e0);
+        unpack8(d1, e1);  // zero when !two
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[j] += e0[j] + e1[j];
+          b[j] += e0[j] * (f0[j] - k[j]) * r[j] + e1[j] * (f1[j] - k[j]) * r[j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x][j] = a[j];
+    red[1][threadIdx.x][j] = b[j];
+  }
+  __syncthreads();
+  // fixed-order combine over the pixel lanes: thread t < CL*8 owns (cl, j)
+  for (int t = threadIdx.x; t < CL * 8; t += 256) {
+    const int c8 = t >> 3, j = t & 7;
+    float sa = 0.f, sb = 0.f;
+    for (int q = 0; q < PL; ++q) {
+      sa += red[0][q * CL + c8][j];
+      sb += red[1][q * CL + c8][j];
+    }
+    float* o = part + static_cast<size_t>(blockIdx.x) * 2 * C;
+    o[c8 * 8 + j] = sa;
+    o[C + c8 * 8 + j] = sb;
+  }
+}
+
+// Finalize kernels: block per 64 channels, 4 group lanes (thread (c, gl)
+// takes groups gl, gl + 4, ...); the cross-group sums (running stats,
+// dweight / dbias) are combined over the 4 lanes in a fixed order.
+// forward: stat[g][0][c] = mean, stat[g][1][c] = rstd
+__global__ void __launch_bounds__(256)
+bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__ part, int C,
+                       int M, int S, int G, float eps, float momentum, float* __restrict__ stat,
+                       float* __restrict__ run_mean, float* __restrict__ run_var) {
+  __shared__ float red[2][4][64];
+  const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc;
+  float msum = 0.f, vsum = 0.f;
+  if (c < C) {
+    for (int g = gl; g < G; g += 4) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int s = 0; s < S; ++s) {
+        const float* p = part + (static_cast<size_t>(g) * S + s) * 2 * C;
+        s1 += p[c];
+        s2 += p[C + c];
+      }
+      const float kk = __uint_as_float(static_cast<uint32_t>(x[static_cast<size_t>(g) * M * C + c]) << 16);
+      const float d = s1 / M;
+      const float var = fmaxf(s2 / M - d * d, 0.f);
+      const float mean = kk + d;
+      stat[(static_cast<size_t>(g) * 2) * C + c] = mean;
+      stat[(static_cast<size_t>(g) * 2 + 1) * C + c] = rsqrtf(var + eps);
+      msum += mean;
+      vsum += var;
+    }
+  }
+  red[0][gl][cc] = msum;
+  red[1][gl][cc] = vsum;
+  __syncthreads();
+  if (gl == 0 && c < C && run_mean != nullptr) {
+    const float ms = ((red[0][0][cc] + red[0][1][cc]) + red[0][2][cc]) + red[0][3][cc];
+    const float vs = ((red[1][0][cc] + red[1][1][cc]) + red[1][2][cc]) + red[1][3][cc];
+    const float unb = M > 1 ? static_cast<float>(M) / static_cast<float>(M - 1) : 1.f;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (ms / G);
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (vs / G) * unb;
+  }
+}
+
+// backward: coef[g][0][c] = w rstd, [1] = mean(dy), [2] = mean(dy xhat);
+// dw[c] = sum_g sum(dy xhat), db[c] = sum_g sum(dy)
+__global__ void __launch_bounds__(256)
+bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__ stat,
+                       const float* __restrict__ w, int C, int M, int S, int G,
+                       float* __restrict__ coef, float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[2][4][64];
+  const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc;
+  float tw = 0.f, tb = 0.f;
+  if (c < C) {
+    const float wc = w != nullptr ? w[c] : 1.f;
+    for (int g = gl; g < G; g += 4) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int s = 0; s < S; ++s) {
+        const float* p = part + (static_cast<size_t>(g) * S + s) * 2 * C;
+        s1 += p[c];
+        s2 += p[C + c];
+      }
+      tb += s1;
+      tw += s2;
+      float* o = coef + static_cast<size_t>(g) * 3 * C;
+      o[c] = wc * stat[(static_cast<size_t>(g) * 2 + 1) * C + c];
+      o[C + c] = s1 / M;
+      o[2 * C + c] = s2 / M;
+    }
+  }
+  red[0][gl][cc] = tw;
+  red[1][gl][cc] = tb;
+  __syncthreads();
+  if (gl == 0 && c < C) {
+    if (dw != nullptr) dw[c] = ((red[0][0][cc] + red[0][1][cc]) + red[0][2][cc]) + red[0][3][cc];
+    if (db != nullptr) db[c] = ((red[1][0][cc] + red[1][1][cc]) + red[1][2][cc]) + red[1][3][cc];
+  }
+}
+
+// y = (x - mean) rstd w + b  (fwd)   or   dx = coef0 (dy - coef1 - xhat coef2)  (bwd)
+template <bool BWD>
+__global__ void __launch_bounds__(256)
+bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                const float* __restrict__ stat, const float* __restrict__ coef,
+                const float* __restrict__ w, const float* __restrict__ b, int C, int M,
+                uint32_t nchunks, uint16_t* __restrict__ out) {
+  const uint32_t CL = static_cast<uint32_t>(C) >> 3;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nchunks; i += gridDim.x * 256u) {
+    const uint32_t p = i / CL;
+    const int c0 = static_cast<int>(i - p * CL) * 8;
+    const int g = static_cast<int>(p / static_cast<uint32_t>(M));
+    const float* mean = stat + (static_cast<size_t>(g) * 2) * C + c0;
+    const float* rstd = mean + C;
+    float f[8], o[8];
+    unpack8(*reinterpret_cast<const u4*>(x + static_cast<size_t>(i) * 8), f);
+    if (!BWD) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (f[j] - mean[j]) * rstd[j];
+        o[j] = w != nullptr ? xh * w[c0 + j] + b[c0 + j] : xh;
+      }
+    } else {
+      float d[8];
+      unpack8(*reinterpret_cast<const u4*>(dy + static_cast<size_t>(i) * 8), d);
+      const float* k0 = coef + static_cast<size_t>(g) * 3 * C + c0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (f[j] - mean[j]) * rstd[j];
+        o[j] = k0[j] * (d[j] - k0[C + j] - xh * k0[2 * C + j]);
+      }
+    }
+    const u4 v = {pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
+    *reinterpret_cast<u4*>(out + static_cast<size_t>(i) * 8) = v;
+  }
+}
+
+int apply_grid(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return static_cast<int>(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+int bn_slabs(int G, int M) {
+  // >= ~512 partial blocks over the whole batch, >= 64 pixels each
+  int s = (512 + G - 1) / G;
+  const int cap = M / 64 > 1 ? M / 64 : 1;
+  if (s > cap) s = cap;
+  return s < 1 ? 1 : s;
+}
+
+void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C,
+                   float eps, float momentum, float* run_mean, float* run_var, float* part,
+                   float* stat, uint16_t* y, hipStream_t stream) {
+  const int S = bn_slabs(G, M);
+  hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
+                     C, M, S, part);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, x, part, C, M,
+                     S, G, eps, momentum, stat, run_mean, run_var);
+  const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
+  hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
+                     stat, nullptr, w, b, C, M, static_cast<uint32_t>(nchunks), y);
+}
+
+void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const float* stat, const float* w, int G,
+                   int M, int C, float* part, float* coef, float* dw, float* db, uint16_t* dx,
+                   hipStream_t stream) {
+  const int S = bn_slabs(G, M);
+  hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, stat, C, M, S,
+                     part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, part, stat, w,
+                     C, M, S, G, coef, dw, db);
+  const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
+  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, stat,
+                     coef, nullptr, nullptr, C, M, static_cast<uint32_t>(nchunks), dx);
+}
+
+}  // namespace commeff

@@ -7,6 +7,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.nn import ghost_batch_norm, ghost_bn_native_ok
+
 
 class Mul(nn.Module):
     """Constant scale (ResNet-9 classifier ×0.125)."""
@@ -62,6 +64,16 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
             return super().forward(x)
         N, C = x.shape[0], x.shape[1]
         assert N % G == 0, "ghost batch norm needs equal client batch sizes"
+        if self.momentum is not None and ghost_bn_native_ok(x, self.weight if self.affine else None):
+            # native per-group BN (csrc/bn.hip)
+            track = self.track_running_stats and self.running_mean is not None
+            y = ghost_batch_norm(x, self.weight if self.affine else None,
+                                 self.bias if self.affine else None, G, self.eps, self.momentum,
+                                 self.running_mean if track else None,
+                                 self.running_var if track else None)
+            if track:
+                self.num_batches_tracked += 1
+            return y
         xf = x.float().reshape(G, N // G, C, -1)
         mean = xf.mean(dim=(1, 3), keepdim=True)
         var = xf.var(dim=(1, 3), keepdim=True, unbiased=False)

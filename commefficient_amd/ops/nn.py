@@ -302,6 +302,42 @@ def fused_head_loss(x, weight, targets, scale: float):
     return _FusedHead.apply(x, weight, targets.contiguous(), float(scale))
 
 
+# ------------------------------------------------------------ ghost batch norm
+class _GhostBN(torch.autograd.Function):
+    """Per-group batch norm over NHWC bf16 (csrc/bn.hip): 3 kernels forward,
+    3 backward; running statistics updated in place with the group-averaged
+    moments (the torch path in models/common.py GhostBatchNorm2d)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var):
+        y, stat = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
+                                      running_mean, running_var)
+        ctx.save_for_backward(x, stat, weight)
+        ctx.groups = int(groups)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, stat, weight = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx, dw, db = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups)
+        if weight is None:
+            dw = db = None
+        return dx, dw, db, None, None, None, None, None
+
+
+def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
+            and (weight is None or weight.dtype == torch.float32))
+
+
+def ghost_batch_norm(x, weight, bias, groups: int, eps: float, momentum: float,
+                     running_mean=None, running_var=None):
+    return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var)
+
+
 # ------------------------------------------------------------ loss
 class _FusedCE(torch.autograd.Function):
     """Per-example cross-entropy + top-1 correctness in one kernel

@@ -339,3 +339,39 @@ def test_fused_head_matches_fp32(B, C, ncls):
     loss2, _ = cnn.fused_head_loss(x.detach(), w2, t, 0.125)
     (loss2 * gl).sum().backward()
     torch.testing.assert_close(w2.grad, wr.grad + 1, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("N, G, C, H", [(20, 4, 64, 8), (10, 10, 128, 4), (6, 3, 512, 2), (4, 1, 96, 5)])
+@pytest.mark.parametrize("affine", [True, False])
+def test_ghost_bn_matches_fp32(N, G, C, H, affine):
+    """Native per-group batch norm (csrc/bn.hip) fwd/bwd + running stats vs
+    the fp32 PyTorch composition (GhostBatchNorm2d's torch path)."""
+    from commefficient_amd.models.common import GhostBatchNorm2d
+    g = torch.Generator(device="cuda").manual_seed(N * C)
+    x = (torch.randn(N, C, H, H, device="cuda", generator=g) * 2 + 3).to(torch.bfloat16)
+    x = _nhwc(x).requires_grad_(True)
+    bn = GhostBatchNorm2d(C, affine=affine).cuda()
+    ref = GhostBatchNorm2d(C, affine=affine).cuda()
+    if affine:
+        with torch.no_grad():
+            bn.weight.copy_(torch.rand(C, device="cuda", generator=g) + 0.5)
+            bn.bias.copy_(torch.randn(C, device="cuda", generator=g))
+            ref.weight.copy_(bn.weight)
+            ref.bias.copy_(bn.bias)
+    bn.ghost_groups = ref.ghost_groups = G
+    gy = torch.randn(N, C, H, H, device="cuda", generator=g)
+    y = bn(x)
+    (y.float() * gy).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    # fp32 reference: the torch path of the same module on fp32 input
+    yr = ref(xr)
+    # the native backward sees dL/dy rounded to bf16 (y is bf16): same here
+    (yr * gy.to(torch.bfloat16).float()).sum().backward()
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, yr)
+    _close(x.grad, xr.grad, rel=3e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
+    if affine:
+        torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=2e-2, atol=2e-2)
+        torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=2e-2, atol=2e-2)
