@@ -831,7 +831,7 @@ at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at:
 std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c10::optional<at::Tensor>& w,
                                                     const c10::optional<at::Tensor>& b, int64_t G, double eps,
                                                     double momentum, const c10::optional<at::Tensor>& run_mean,
-                                                    const c10::optional<at::Tensor>& run_var) {
+                                                    const c10::optional<at::Tensor>& run_var, bool relu) {
   check_nhwc_bf16(x, "ghost_bn: x");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   TORCH_CHECK(G >= 1 && N % G == 0 && C % 8 == 0 && C <= 2048, "ghost_bn: G | N, C % 8 == 0, C <= 2048");
@@ -853,18 +853,26 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
   auto fo = x.options().dtype(at::kFloat);
   auto part = at::empty({G * S * 2 * C}, fo);
   auto stat = at::empty({G, 2, C}, fo);
+  auto ab = at::empty({G, 2, C}, fo);
   auto y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   launch_bn_fwd(bf16_ptr(x), wp, bp, static_cast<int>(G), static_cast<int>(M), static_cast<int>(C),
                 static_cast<float>(eps), static_cast<float>(momentum), rm, rv, part.data_ptr<float>(),
-                stat.data_ptr<float>(), reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
+                stat.data_ptr<float>(), ab.data_ptr<float>(), relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
+                cur_stream());
   return {y, stat};
 }
 
 // returns (dx, dweight, dbias) (dweight / dbias undefined without affine)
 std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor& dy, const at::Tensor& x,
                                                                 const at::Tensor& stat,
-                                                                const c10::optional<at::Tensor>& w, int64_t G) {
+                                                                const c10::optional<at::Tensor>& w, int64_t G,
+                                                                const c10::optional<at::Tensor>& y_relu) {
   check_nhwc_bf16(x, "ghost_bn_bwd: x");
+  const bool fused_relu = y_relu.has_value() && y_relu->defined();
+  if (fused_relu) {
+    check_nhwc_bf16(*y_relu, "ghost_bn_bwd: y");
+    TORCH_CHECK(y_relu->sizes() == x.sizes(), "ghost_bn_bwd: y shape");
+  }
   check_nhwc_bf16(dy, "ghost_bn_bwd: dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "ghost_bn_bwd: dy shape");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
@@ -883,7 +891,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
     db = at::empty({C}, fo);
   }
   auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  launch_bn_bwd(bf16_ptr(x), bf16_ptr(dy), stat.data_ptr<float>(), affine ? w->data_ptr<float>() : nullptr,
+  launch_bn_bwd(bf16_ptr(x), bf16_ptr(dy), fused_relu ? bf16_ptr(*y_relu) : nullptr, stat.data_ptr<float>(),
+                affine ? w->data_ptr<float>() : nullptr,
                 static_cast<int>(G), static_cast<int>(M), static_cast<int>(C), part.data_ptr<float>(),
                 coef.data_ptr<float>(), affine ? dw.data_ptr<float>() : nullptr,
                 affine ? db.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dx.data_ptr()),
@@ -1163,8 +1172,9 @@ TORCH_LIBRARY(commeff, m) {
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
-        "Tensor(b!)? run_var) -> (Tensor, Tensor)");
-  m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G) -> (Tensor, Tensor, Tensor)");
+        "Tensor(b!)? run_var, bool relu=False) -> (Tensor, Tensor)");
+  m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None) -> "
+        "(Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");

@@ -8,13 +8,13 @@
 // M = (N/G)*H*W pixels; statistics are per (group, channel).
 //
 // Forward  (3 launches): partial shifted sums per (group, pixel slab) ->
-//          per-(group, channel) mean / rstd (+ running-stat update with the
-//          group-averaged moments, one thread per channel, fixed order) ->
-//          y = (x - mean) * rstd * w + b, 16-byte loads/stores.
+//          per-(group, channel) mean / rstd and y = x A + B coefficients
+//          (+ running-stat update with the group-averaged moments, fixed
+//          order) -> y, 16-byte loads/stores.
 // Backward (3 launches): partial sums of dy and dy*xhat per (group, slab) ->
 //          per-(group, channel) coefficients, dweight / dbias (fixed-order
 //          sums over groups: deterministic) -> dx = w rstd (dy - mean(dy) -
-//          xhat mean(dy xhat)).
+//          xhat mean(dy xhat)) = P dy + Q x + R.
 // Sums are shifted by the group's first pixel (E[(x-K)^2] - E[x-K]^2 keeps
 // fp32 accurate when |mean| >> std).  Replaces ~40 PyTorch kernels (reshape
 // copies, reductions, elementwise, autograd) per BN layer.
@@ -42,14 +42,26 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, t);
 }
 
+// keep the bf16 lanes of d where the bf16 lanes of y are > 0
+__device__ __forceinline__ u4 relu_mask8(u4 d, const u4 y) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t lo = y[q] & 0xffffu, hi = y[q] >> 16;
+    const uint32_t keep = ((lo & 0x8000u) == 0u && lo != 0u ? 0x0000ffffu : 0u) |
+                          ((hi & 0x8000u) == 0u && hi != 0u ? 0xffff0000u : 0u);
+    d[q] &= keep;
+  }
+  return d;
+}
+
 // thread layout of the partial-sum kernels: CL = C/8 chunk lanes (16 bytes =
 // 8 channels each) x PL = 256/CL pixel lanes; a block covers pixel slab s of
 // group g, every channel.
 template <bool BWD>
 __global__ void __launch_bounds__(256)
 bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                  const float* __restrict__ stat, int C, int M, int S,
-                  float* __restrict__ part) {
+                  const uint16_t* __restrict__ ymask, const float* __restrict__ stat, int C, int M,
+                  int S, float* __restrict__ part) {
   // part[(g*S + s)*2*C + {0: sum, C: sum2}][c]
   __shared__ float red[2][256][8];
   const int g = blockIdx.x / S, s = blockIdx.x - g * S;
@@ -83,6 +95,10 @@ bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
       if (BWD) {
         d0 = *reinterpret_cast<const u4*>(dy + o0);
         if (two) d1 = *reinterpret_cast<const u4*>(dy + o1);
+        if (ymask != nullptr) {  // fused ReLU: dy where y > 0
+          d0 = relu_mask8(d0, *reinterpret_cast<const u4*>(ymask + o0));
+          if (two) d1 = relu_mask8(d1, *reinterpret_cast<const u4*>(ymask + o1));
+        }
       }
       float f0[8], f1[8];
       unpack8(x0, f0);
@@ -126,20 +142,26 @@ bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
   }
 }
 
-// Finalize kernels: block per 64 channels, 4 group lanes (thread (c, gl)
-// takes groups gl, gl + 4, ...); the cross-group sums (running stats,
-// dweight / dbias) are combined over the 4 lanes in a fixed order.
-// forward: stat[g][0][c] = mean, stat[g][1][c] = rstd
-__global__ void __launch_bounds__(256)
-bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__ part, int C,
-                       int M, int S, int G, float eps, float momentum, float* __restrict__ stat,
-                       float* __restrict__ run_mean, float* __restrict__ run_var) {
-  __shared__ float red[2][4][64];
+// Finalize kernels: block per 64 channels, 16 group lanes (thread (c, gl)
+// takes groups gl, gl + 16, ...); the cross-group sums (running stats,
+// dweight / dbias) are combined over the lanes in a fixed order.
+constexpr int kGL = 16;
+
+// forward: stat[g][0][c] = mean, stat[g][1][c] = rstd (kept for backward),
+// ab[g][0][c] = A = w rstd, ab[g][1][c] = B = b - mean A  (y = x A + B)
+__global__ void __launch_bounds__(1024)
+bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__ part,
+                       const float* __restrict__ w, const float* __restrict__ bias, int C, int M,
+                       int S, int G, float eps, float momentum, float* __restrict__ stat,
+                       float* __restrict__ ab, float* __restrict__ run_mean,
+                       float* __restrict__ run_var) {
+  __shared__ float red[2][kGL][64];
   const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cc;
   float msum = 0.f, vsum = 0.f;
   if (c < C) {
-    for (int g = gl; g < G; g += 4) {
+    const float wc = w != nullptr ? w[c] : 1.f, bc = w != nullptr ? bias[c] : 0.f;
+    for (int g = gl; g < G; g += kGL) {
       float s1 = 0.f, s2 = 0.f;
       for (int s = 0; s < S; ++s) {
         const float* p = part + (static_cast<size_t>(g) * S + s) * 2 * C;
@@ -149,9 +171,12 @@ bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__
       const float kk = __uint_as_float(static_cast<uint32_t>(x[static_cast<size_t>(g) * M * C + c]) << 16);
       const float d = s1 / M;
       const float var = fmaxf(s2 / M - d * d, 0.f);
-      const float mean = kk + d;
-      stat[(static_cast<size_t>(g) * 2) * C + c] = mean;
-      stat[(static_cast<size_t>(g) * 2 + 1) * C + c] = rsqrtf(var + eps);
+      const float mean = kk + d, rstd = rsqrtf(var + eps);
+      const size_t o = static_cast<size_t>(g) * 2 * C + c;
+      stat[o] = mean;
+      stat[o + C] = rstd;
+      ab[o] = wc * rstd;
+      ab[o + C] = bc - mean * wc * rstd;
       msum += mean;
       vsum += var;
     }
@@ -160,27 +185,31 @@ bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__
   red[1][gl][cc] = vsum;
   __syncthreads();
   if (gl == 0 && c < C && run_mean != nullptr) {
-    const float ms = ((red[0][0][cc] + red[0][1][cc]) + red[0][2][cc]) + red[0][3][cc];
-    const float vs = ((red[1][0][cc] + red[1][1][cc]) + red[1][2][cc]) + red[1][3][cc];
+    float ms = 0.f, vs = 0.f;
+    for (int q = 0; q < kGL; ++q) {
+      ms += red[0][q][cc];
+      vs += red[1][q][cc];
+    }
     const float unb = M > 1 ? static_cast<float>(M) / static_cast<float>(M - 1) : 1.f;
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (ms / G);
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * (vs / G) * unb;
   }
 }
 
-// backward: coef[g][0][c] = w rstd, [1] = mean(dy), [2] = mean(dy xhat);
-// dw[c] = sum_g sum(dy xhat), db[c] = sum_g sum(dy)
-__global__ void __launch_bounds__(256)
+// backward: with k0 = w rstd, k1 = mean(dy), k2 = mean(dy xhat) and
+// xhat = (x - mean) rstd, dx = k0 (dy - k1 - xhat k2) = P dy + Q x + R:
+// coef[g][0..2][c] = P, Q, R.  dw[c] = sum_g sum(dy xhat), db[c] = sum_g sum(dy)
+__global__ void __launch_bounds__(1024)
 bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__ stat,
                        const float* __restrict__ w, int C, int M, int S, int G,
                        float* __restrict__ coef, float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[2][4][64];
+  __shared__ float red[2][kGL][64];
   const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cc;
   float tw = 0.f, tb = 0.f;
   if (c < C) {
     const float wc = w != nullptr ? w[c] : 1.f;
-    for (int g = gl; g < G; g += 4) {
+    for (int g = gl; g < G; g += kGL) {
       float s1 = 0.f, s2 = 0.f;
       for (int s = 0; s < S; ++s) {
         const float* p = part + (static_cast<size_t>(g) * S + s) * 2 * C;
@@ -189,52 +218,65 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__
       }
       tb += s1;
       tw += s2;
+      const float mean = stat[static_cast<size_t>(g) * 2 * C + c];
+      const float rstd = stat[static_cast<size_t>(g) * 2 * C + C + c];
+      const float k0 = wc * rstd, k1 = s1 / M, k2 = s2 / M;
       float* o = coef + static_cast<size_t>(g) * 3 * C;
-      o[c] = wc * stat[(static_cast<size_t>(g) * 2 + 1) * C + c];
-      o[C + c] = s1 / M;
-      o[2 * C + c] = s2 / M;
+      o[c] = k0;
+      o[C + c] = -k0 * k2 * rstd;
+      o[2 * C + c] = -k0 * k1 + k0 * k2 * rstd * mean;
     }
   }
   red[0][gl][cc] = tw;
   red[1][gl][cc] = tb;
   __syncthreads();
   if (gl == 0 && c < C) {
-    if (dw != nullptr) dw[c] = ((red[0][0][cc] + red[0][1][cc]) + red[0][2][cc]) + red[0][3][cc];
-    if (db != nullptr) db[c] = ((red[1][0][cc] + red[1][1][cc]) + red[1][2][cc]) + red[1][3][cc];
+    float sw = 0.f, sb = 0.f;
+    for (int q = 0; q < kGL; ++q) {
+      sw += red[0][q][cc];
+      sb += red[1][q][cc];
+    }
+    if (dw != nullptr) dw[c] = sw;
+    if (db != nullptr) db[c] = sb;
   }
 }
 
-// y = (x - mean) rstd w + b  (fwd)   or   dx = coef0 (dy - coef1 - xhat coef2)  (bwd)
+__device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// fwd: y = x A + B ;  bwd: dx = P dy + Q x + R  (per-(group, channel) coefficients)
 template <bool BWD>
 __global__ void __launch_bounds__(256)
 bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                const float* __restrict__ stat, const float* __restrict__ coef,
-                const float* __restrict__ w, const float* __restrict__ b, int C, int M,
-                uint32_t nchunks, uint16_t* __restrict__ out) {
+                const uint16_t* __restrict__ ymask, const float* __restrict__ coef, int C, int M,
+                uint32_t nchunks, bool relu, uint16_t* __restrict__ out) {
   const uint32_t CL = static_cast<uint32_t>(C) >> 3;
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nchunks; i += gridDim.x * 256u) {
     const uint32_t p = i / CL;
     const int c0 = static_cast<int>(i - p * CL) * 8;
     const int g = static_cast<int>(p / static_cast<uint32_t>(M));
-    const float* mean = stat + (static_cast<size_t>(g) * 2) * C + c0;
-    const float* rstd = mean + C;
-    float f[8], o[8];
+    const float* k = coef + static_cast<size_t>(g) * (BWD ? 3 : 2) * C + c0;
+    float f[8], A[8], B[8], o[8];
     unpack8(*reinterpret_cast<const u4*>(x + static_cast<size_t>(i) * 8), f);
+    load8f(k, A);
+    load8f(k + C, B);
     if (!BWD) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (f[j] - mean[j]) * rstd[j];
-        o[j] = w != nullptr ? xh * w[c0 + j] + b[c0 + j] : xh;
+      for (int j = 0; j < 8; ++j) o[j] = f[j] * A[j] + B[j];
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
       }
     } else {
-      float d[8];
-      unpack8(*reinterpret_cast<const u4*>(dy + static_cast<size_t>(i) * 8), d);
-      const float* k0 = coef + static_cast<size_t>(g) * 3 * C + c0;
+      float d[8], R[8];
+      u4 dv = *reinterpret_cast<const u4*>(dy + static_cast<size_t>(i) * 8);
+      if (ymask != nullptr) dv = relu_mask8(dv, *reinterpret_cast<const u4*>(ymask + static_cast<size_t>(i) * 8));
+      unpack8(dv, d);
+      load8f(k + 2 * C, R);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float xh = (f[j] - mean[j]) * rstd[j];
-        o[j] = k0[j] * (d[j] - k0[C + j] - xh * k0[2 * C + j]);
-      }
+      for (int j = 0; j < 8; ++j) o[j] = d[j] * A[j] + f[j] * B[j] + R[j];
     }
     const u4 v = {pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
     *reinterpret_cast<u4*>(out + static_cast<size_t>(i) * 8) = v;
@@ -259,28 +301,28 @@ int bn_slabs(int G, int M) {
 
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C,
                    float eps, float momentum, float* run_mean, float* run_var, float* part,
-                   float* stat, uint16_t* y, hipStream_t stream) {
+                   float* stat, float* ab, bool relu, uint16_t* y, hipStream_t stream) {
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
-                     C, M, S, part);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, x, part, C, M,
-                     S, G, eps, momentum, stat, run_mean, run_var);
+                     nullptr, C, M, S, part);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part, w,
+                     b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var);
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
-                     stat, nullptr, w, b, C, M, static_cast<uint32_t>(nchunks), y);
+                     nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y);
 }
 
-void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const float* stat, const float* w, int G,
-                   int M, int C, float* part, float* coef, float* dw, float* db, uint16_t* dx,
-                   hipStream_t stream) {
+void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
+                   const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
+                   uint16_t* dx, hipStream_t stream) {
   const int S = bn_slabs(G, M);
-  hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, stat, C, M, S,
-                     part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, part, stat, w,
+  hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
+                     S, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat, w,
                      C, M, S, G, coef, dw, db);
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
-  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, stat,
-                     coef, nullptr, nullptr, C, M, static_cast<uint32_t>(nchunks), dx);
+  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
+                     coef, C, M, static_cast<uint32_t>(nchunks), false, dx);
 }
 
 }  // namespace commeff

@@ -58,10 +58,20 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
 
     ghost_groups: int = 1
 
+    def __init__(self, num_features, *args, fuse_relu: bool = False, **kw):
+        super().__init__(num_features, *args, **kw)
+        # relu(bn(x)) in one module (one native kernel each way when merged)
+        self.fuse_relu = fuse_relu
+
     def forward(self, x):
+        y, relu_done = self._bn(x)
+        return F.relu(y) if self.fuse_relu and not relu_done else y
+
+    def _bn(self, x):
+        """(normalised x, whether the fused ReLU was already applied)"""
         G = self.ghost_groups
         if not self.training or G <= 1:
-            return super().forward(x)
+            return super().forward(x), False
         N, C = x.shape[0], x.shape[1]
         assert N % G == 0, "ghost batch norm needs equal client batch sizes"
         if self.momentum is not None and ghost_bn_native_ok(x, self.weight if self.affine else None):
@@ -70,10 +80,10 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
             y = ghost_batch_norm(x, self.weight if self.affine else None,
                                  self.bias if self.affine else None, G, self.eps, self.momentum,
                                  self.running_mean if track else None,
-                                 self.running_var if track else None)
+                                 self.running_var if track else None, relu=self.fuse_relu)
             if track:
                 self.num_batches_tracked += 1
-            return y
+            return y, self.fuse_relu
         xf = x.float().reshape(G, N // G, C, -1)
         mean = xf.mean(dim=(1, 3), keepdim=True)
         var = xf.var(dim=(1, 3), keepdim=True, unbiased=False)
@@ -88,7 +98,7 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
                 unb = var.mean(dim=0).view(C) * (n / max(1, n - 1))
                 self.running_var.mul_(1 - m).add_(m * unb)
                 self.num_batches_tracked += 1
-        return y.reshape(x.shape).to(x.dtype).contiguous(memory_format=_fmt(x))
+        return y.reshape(x.shape).to(x.dtype).contiguous(memory_format=_fmt(x)), False
 
 
 def _fmt(x):

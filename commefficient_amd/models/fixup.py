@@ -153,16 +153,17 @@ class PreActBlock(nn.Module):
 
     def __init__(self, in_channels, out_channels, stride=1):
         super().__init__()
-        self.bn1 = GhostBatchNorm2d(out_channels)
+        # BN + ReLU fused (one native kernel each way in merged rounds)
+        self.bn1 = GhostBatchNorm2d(out_channels, fuse_relu=True)
         self.conv1 = conv3x3(in_channels, out_channels, stride)
-        self.bn2 = GhostBatchNorm2d(out_channels)
+        self.bn2 = GhostBatchNorm2d(out_channels, fuse_relu=True)
         self.conv2 = conv3x3(out_channels, out_channels)
         if stride != 1 or in_channels != out_channels:
             self.shortcut = nn.Sequential(conv1x1(in_channels, out_channels, stride))
 
     def forward(self, x):
-        out = F.relu(self.bn1(self.conv1(x)))
-        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn1(self.conv1(x))  # relu(bn(.))
+        out = self.bn2(self.conv2(out))
         sc = self.shortcut(x) if hasattr(self, "shortcut") else x
         return out + sc
 

@@ -309,21 +309,21 @@ class _GhostBN(torch.autograd.Function):
     moments (the torch path in models/common.py GhostBatchNorm2d)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var):
+    def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var, relu):
         y, stat = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
-                                      running_mean, running_var)
-        ctx.save_for_backward(x, stat, weight)
+                                      running_mean, running_var, bool(relu))
+        ctx.save_for_backward(x, stat, weight, y if relu else None)
         ctx.groups = int(groups)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, stat, weight = ctx.saved_tensors
+        x, stat, weight, y = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        dx, dw, db = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups)
+        dx, dw, db = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y)
         if weight is None:
             dw = db = None
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
@@ -334,8 +334,9 @@ def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
 
 
 def ghost_batch_norm(x, weight, bias, groups: int, eps: float, momentum: float,
-                     running_mean=None, running_var=None):
-    return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var)
+                     running_mean=None, running_var=None, relu: bool = False):
+    """Per-group batch norm (+ ReLU when ``relu``) on the native kernels."""
+    return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var, relu)
 
 
 # ------------------------------------------------------------ loss

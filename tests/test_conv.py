@@ -342,16 +342,16 @@ def test_fused_head_matches_fp32(B, C, ncls):
 
 
 @pytest.mark.parametrize("N, G, C, H", [(20, 4, 64, 8), (10, 10, 128, 4), (6, 3, 512, 2), (4, 1, 96, 5)])
-@pytest.mark.parametrize("affine", [True, False])
-def test_ghost_bn_matches_fp32(N, G, C, H, affine):
+@pytest.mark.parametrize("affine, relu", [(True, False), (False, False), (True, True)])
+def test_ghost_bn_matches_fp32(N, G, C, H, affine, relu):
     """Native per-group batch norm (csrc/bn.hip) fwd/bwd + running stats vs
     the fp32 PyTorch composition (GhostBatchNorm2d's torch path)."""
     from commefficient_amd.models.common import GhostBatchNorm2d
     g = torch.Generator(device="cuda").manual_seed(N * C)
     x = (torch.randn(N, C, H, H, device="cuda", generator=g) * 2 + 3).to(torch.bfloat16)
     x = _nhwc(x).requires_grad_(True)
-    bn = GhostBatchNorm2d(C, affine=affine).cuda()
-    ref = GhostBatchNorm2d(C, affine=affine).cuda()
+    bn = GhostBatchNorm2d(C, affine=affine, fuse_relu=relu).cuda()
+    ref = GhostBatchNorm2d(C, affine=affine, fuse_relu=relu).cuda()
     if affine:
         with torch.no_grad():
             bn.weight.copy_(torch.rand(C, device="cuda", generator=g) + 0.5)
