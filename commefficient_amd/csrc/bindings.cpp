@@ -831,7 +831,8 @@ at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at:
 std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c10::optional<at::Tensor>& w,
                                                     const c10::optional<at::Tensor>& b, int64_t G, double eps,
                                                     double momentum, const c10::optional<at::Tensor>& run_mean,
-                                                    const c10::optional<at::Tensor>& run_var, bool relu) {
+                                                    const c10::optional<at::Tensor>& run_var, bool relu,
+                                                    const c10::optional<at::Tensor>& nbt) {
   check_nhwc_bf16(x, "ghost_bn: x");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   TORCH_CHECK(G >= 1 && N % G == 0 && C % 8 == 0 && C <= 2048, "ghost_bn: G | N, C % 8 == 0, C <= 2048");
@@ -848,6 +849,11 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
   float* rm = f32(run_mean, "ghost_bn: running_mean f32 [C]");
   float* rv = f32(run_var, "ghost_bn: running_var f32 [C]");
   TORCH_CHECK((rm == nullptr) == (rv == nullptr), "ghost_bn: running stats together");
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->numel() == 1, "ghost_bn: num_batches_tracked int64 []");
+    nb = nbt->data_ptr<int64_t>();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
   auto fo = x.options().dtype(at::kFloat);
@@ -857,8 +863,8 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
   auto y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   launch_bn_fwd(bf16_ptr(x), wp, bp, static_cast<int>(G), static_cast<int>(M), static_cast<int>(C),
                 static_cast<float>(eps), static_cast<float>(momentum), rm, rv, part.data_ptr<float>(),
-                stat.data_ptr<float>(), ab.data_ptr<float>(), relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
-                cur_stream());
+                stat.data_ptr<float>(), ab.data_ptr<float>(), relu, nb,
+                reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
   return {y, stat};
 }
 
@@ -1172,7 +1178,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
-        "Tensor(b!)? run_var, bool relu=False) -> (Tensor, Tensor)");
+        "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None) -> (Tensor, Tensor)");
   m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None) -> "
         "(Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");

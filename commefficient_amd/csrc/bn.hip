@@ -142,9 +142,11 @@ bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
   }
 }
 
-// Finalize kernels: block per 64 channels, 16 group lanes (thread (c, gl)
-// takes groups gl, gl + 16, ...); the cross-group sums (running stats,
-// dweight / dbias) are combined over the lanes in a fixed order.
+// Finalize kernels: block per 64 channels x 16 lanes.  With >= 16 groups
+// thread (c, gl) takes groups gl, gl + 16, ...; with fewer (the per-client
+// path: one group) the lanes split each group's slabs instead.  Every
+// combine over lanes (per-group sums, running stats, dweight / dbias) runs
+// in a fixed order: deterministic.
 constexpr int kGL = 16;
 
 // forward: stat[g][0][c] = mean, stat[g][1][c] = rstd (kept for backward),
@@ -154,13 +156,53 @@ bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__
                        const float* __restrict__ w, const float* __restrict__ bias, int C, int M,
                        int S, int G, float eps, float momentum, float* __restrict__ stat,
                        float* __restrict__ ab, float* __restrict__ run_mean,
-                       float* __restrict__ run_var) {
+                       float* __restrict__ run_var, int64_t* __restrict__ nbt) {
+  if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked
   __shared__ float red[2][kGL][64];
   const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cc;
   float msum = 0.f, vsum = 0.f;
-  if (c < C) {
-    const float wc = w != nullptr ? w[c] : 1.f, bc = w != nullptr ? bias[c] : 0.f;
+  const float wc = c < C && w != nullptr ? w[c] : 1.f, bc = c < C && w != nullptr ? bias[c] : 0.f;
+  auto finish = [&](int g, float s1, float s2) __attribute__((always_inline)) {
+    const float kk = __uint_as_float(static_cast<uint32_t>(x[static_cast<size_t>(g) * M * C + c]) << 16);
+    const float d = s1 / M;
+    const float var = fmaxf(s2 / M - d * d, 0.f);
+    const float mean = kk + d, rstd = rsqrtf(var + eps);
+    const size_t o = static_cast<size_t>(g) * 2 * C + c;
+    stat[o] = mean;
+    stat[o + C] = rstd;
+    ab[o] = wc * rstd;
+    ab[o + C] = bc - mean * wc * rstd;
+    msum += mean;
+    vsum += var;
+  };
+  if (G < kGL) {
+    // few groups (one per client-step on the per-client path): the lanes
+    // split the slabs of each group instead, combined in a fixed order
+    for (int g = 0; g < G; ++g) {
+      float s1 = 0.f, s2 = 0.f;
+      if (c < C) {
+        for (int s = gl; s < S; s += kGL) {
+          const float* p = part + (static_cast<size_t>(g) * S + s) * 2 * C;
+          s1 += p[c];
+          s2 += p[C + c];
+        }
+      }
+      __syncthreads();  // red reuse
+      red[0][gl][cc] = s1;
+      red[1][gl][cc] = s2;
+      __syncthreads();
+      if (gl == 0 && c < C) {
+        float t1 = 0.f, t2 = 0.f;
+        for (int q = 0; q < kGL; ++q) {
+          t1 += red[0][q][cc];
+          t2 += red[1][q][cc];
+        }
+        finish(g, t1, t2);
+      }
+    }
+    __syncthreads();
+  } else if (c < C) {
     for (int g = gl; g < G; g += kGL) {
       float s1 = 0.f, s2 = 0.f;
       for (int s = 0; s < S; ++s) {
@@ -168,17 +210,7 @@ bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__
         s1 += p[c];
         s2 += p[C + c];
       }
-      const float kk = __uint_as_float(static_cast<uint32_t>(x[static_cast<size_t>(g) * M * C + c]) << 16);
-      const float d = s1 / M;
-      const float var = fmaxf(s2 / M - d * d, 0.f);
-      const float mean = kk + d, rstd = rsqrtf(var + eps);
-      const size_t o = static_cast<size_t>(g) * 2 * C + c;
-      stat[o] = mean;
-      stat[o + C] = rstd;
-      ab[o] = wc * rstd;
-      ab[o + C] = bc - mean * wc * rstd;
-      msum += mean;
-      vsum += var;
+      finish(g, s1, s2);
     }
   }
   red[0][gl][cc] = msum;
@@ -207,8 +239,43 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__
   const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cc;
   float tw = 0.f, tb = 0.f;
-  if (c < C) {
-    const float wc = w != nullptr ? w[c] : 1.f;
+  const float wc = c < C && w != nullptr ? w[c] : 1.f;
+  auto finish = [&](int g, float s1, float s2) __attribute__((always_inline)) {
+    tb += s1;
+    tw += s2;
+    const float mean = stat[static_cast<size_t>(g) * 2 * C + c];
+    const float rstd = stat[static_cast<size_t>(g) * 2 * C + C + c];
+    const float k0 = wc * rstd, k1 = s1 / M, k2 = s2 / M;
+    float* o = coef + static_cast<size_t>(g) * 3 * C;
+    o[c] = k0;
+    o[C + c] = -k0 * k2 * rstd;
+    o[2 * C + c] = -k0 * k1 + k0 * k2 * rstd * mean;
+  };
+  if (G < kGL) {  // lanes split the slabs (see the forward finalize)
+    for (int g = 0; g < G; ++g) {
+      float s1 = 0.f, s2 = 0.f;
+      if (c < C) {
+        for (int s = gl; s < S; s += kGL) {
+          const float* p = part + (static_cast<size_t>(g) * S + s) * 2 * C;
+          s1 += p[c];
+          s2 += p[C + c];
+        }
+      }
+      __syncthreads();
+      red[0][gl][cc] = s1;
+      red[1][gl][cc] = s2;
+      __syncthreads();
+      if (gl == 0 && c < C) {
+        float t1 = 0.f, t2 = 0.f;
+        for (int q = 0; q < kGL; ++q) {
+          t1 += red[0][q][cc];
+          t2 += red[1][q][cc];
+        }
+        finish(g, t1, t2);
+      }
+    }
+    __syncthreads();
+  } else if (c < C) {
     for (int g = gl; g < G; g += kGL) {
       float s1 = 0.f, s2 = 0.f;
       for (int s = 0; s < S; ++s) {
@@ -216,15 +283,7 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__
         s1 += p[c];
         s2 += p[C + c];
       }
-      tb += s1;
-      tw += s2;
-      const float mean = stat[static_cast<size_t>(g) * 2 * C + c];
-      const float rstd = stat[static_cast<size_t>(g) * 2 * C + C + c];
-      const float k0 = wc * rstd, k1 = s1 / M, k2 = s2 / M;
-      float* o = coef + static_cast<size_t>(g) * 3 * C;
-      o[c] = k0;
-      o[C + c] = -k0 * k2 * rstd;
-      o[2 * C + c] = -k0 * k1 + k0 * k2 * rstd * mean;
+      finish(g, s1, s2);
     }
   }
   red[0][gl][cc] = tw;
@@ -301,12 +360,12 @@ int bn_slabs(int G, int M) {
 
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C,
                    float eps, float momentum, float* run_mean, float* run_var, float* part,
-                   float* stat, float* ab, bool relu, uint16_t* y, hipStream_t stream) {
+                   float* stat, float* ab, bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream) {
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
                      nullptr, C, M, S, part);
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part, w,
-                     b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var);
+                     b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var, nbt);
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                      nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y);

@@ -69,21 +69,22 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
 
     def _bn(self, x):
         """(normalised x, whether the fused ReLU was already applied)"""
-        G = self.ghost_groups
-        if not self.training or G <= 1:
-            return super().forward(x), False
-        N, C = x.shape[0], x.shape[1]
-        assert N % G == 0, "ghost batch norm needs equal client batch sizes"
-        if self.momentum is not None and ghost_bn_native_ok(x, self.weight if self.affine else None):
-            # native per-group BN (csrc/bn.hip)
+        G = max(1, self.ghost_groups)
+        if (self.training and self.momentum is not None and x.shape[0] % G == 0
+                and ghost_bn_native_ok(x, self.weight if self.affine else None)):
+            # native per-group BN (csrc/bn.hip), also for one group (the
+            # per-client path): MIOpen's bf16 NHWC BN took 5 launches + casts
             track = self.track_running_stats and self.running_mean is not None
             y = ghost_batch_norm(x, self.weight if self.affine else None,
                                  self.bias if self.affine else None, G, self.eps, self.momentum,
                                  self.running_mean if track else None,
-                                 self.running_var if track else None, relu=self.fuse_relu)
-            if track:
-                self.num_batches_tracked += 1
+                                 self.running_var if track else None, relu=self.fuse_relu,
+                                 num_batches_tracked=self.num_batches_tracked if track else None)
             return y, self.fuse_relu
+        if not self.training or G <= 1:
+            return super().forward(x), False
+        N, C = x.shape[0], x.shape[1]
+        assert N % G == 0, "ghost batch norm needs equal client batch sizes"
         xf = x.float().reshape(G, N // G, C, -1)
         mean = xf.mean(dim=(1, 3), keepdim=True)
         var = xf.var(dim=(1, 3), keepdim=True, unbiased=False)

@@ -23,9 +23,11 @@ __all__ = ["ResNet", "ResNet101", "resnet18", "resnet34", "resnet50", "resnet101
            "resnext50_32x4d", "resnext101_32x8d", "wide_resnet50_2", "wide_resnet101_2"]
 
 
-def _norm(kind: str, c: int, hw: int):
+def _norm(kind: str, c: int, hw: int, relu: bool = False):
+    """Normalisation layer; ``relu`` marks a BN followed by ReLU (fused into
+    one native kernel each way; LayerNorm keeps the separate ReLU)."""
     if kind == "bn":
-        return GhostBatchNorm2d(c)
+        return GhostBatchNorm2d(c, fuse_relu=relu)
     if kind == "ln":
         return nn.LayerNorm((c, hw, hw))
     raise ValueError(kind)
@@ -41,7 +43,7 @@ class BasicBlock(nn.Module):
             raise ValueError("BasicBlock only supports groups=1 and base_width=64")
         out_hw = math.ceil(hw / stride)
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = _norm(norm, planes, out_hw)
+        self.bn1 = _norm(norm, planes, out_hw, relu=True)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
         self.bn2 = _norm(norm, planes, out_hw)
@@ -49,9 +51,15 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
+        out = _norm_relu(self.bn1, self.relu, self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.relu(out + idt)
+
+
+def _norm_relu(norm: nn.Module, relu: nn.Module, x):
+    """relu(norm(x)); a fused GhostBatchNorm2d already applied the ReLU."""
+    y = norm(x)
+    return y if getattr(norm, "fuse_relu", False) else relu(y)
 
 
 class Bottleneck(nn.Module):
@@ -63,10 +71,10 @@ class Bottleneck(nn.Module):
         width = int(planes * (base_width / 64.0)) * groups
         out_hw = math.ceil(hw / stride)
         self.conv1 = conv1x1(inplanes, width)
-        self.bn1 = _norm(norm, width, hw)
+        self.bn1 = _norm(norm, width, hw, relu=True)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=dilation, groups=groups,
                                bias=False, dilation=dilation)
-        self.bn2 = _norm(norm, width, out_hw)
+        self.bn2 = _norm(norm, width, out_hw, relu=True)
         self.conv3 = conv1x1(width, planes * self.expansion)
         self.bn3 = _norm(norm, planes * self.expansion, out_hw)
         self.relu = nn.ReLU(inplace=True)
@@ -74,8 +82,8 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
+        out = _norm_relu(self.bn1, self.relu, self.conv1(x))
+        out = _norm_relu(self.bn2, self.relu, self.conv2(out))
         out = self.bn3(self.conv3(out))
         return self.relu(out + idt)
 
@@ -93,7 +101,7 @@ class ResNet(nn.Module):
         self.base_width = width_per_group
         self.conv1 = nn.Conv2d(in_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
         hw = (input_hw + 2 * 3 - 7) // 2 + 1
-        self.bn1 = _norm(norm, 64, hw)
+        self.bn1 = _norm(norm, 64, hw, relu=True)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         hw = (hw + 2 - 3) // 2 + 1
@@ -131,7 +139,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers), out_hw
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_norm_relu(self.bn1, self.relu, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

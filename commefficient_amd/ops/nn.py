@@ -309,9 +309,9 @@ class _GhostBN(torch.autograd.Function):
     moments (the torch path in models/common.py GhostBatchNorm2d)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var, relu):
+    def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var, relu, nbt):
         y, stat = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
-                                      running_mean, running_var, bool(relu))
+                                      running_mean, running_var, bool(relu), nbt)
         ctx.save_for_backward(x, stat, weight, y if relu else None)
         ctx.groups = int(groups)
         return y
@@ -323,7 +323,7 @@ class _GhostBN(torch.autograd.Function):
         dx, dw, db = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y)
         if weight is None:
             dw = db = None
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
@@ -334,9 +334,12 @@ def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
 
 
 def ghost_batch_norm(x, weight, bias, groups: int, eps: float, momentum: float,
-                     running_mean=None, running_var=None, relu: bool = False):
-    """Per-group batch norm (+ ReLU when ``relu``) on the native kernels."""
-    return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var, relu)
+                     running_mean=None, running_var=None, relu: bool = False,
+                     num_batches_tracked=None):
+    """Per-group batch norm (+ ReLU when ``relu``) on the native kernels; the
+    running statistics and ``num_batches_tracked`` are updated on the device."""
+    return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var, relu,
+                          num_batches_tracked)
 
 
 # ------------------------------------------------------------ loss

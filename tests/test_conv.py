@@ -370,6 +370,7 @@ def test_ghost_bn_matches_fp32(N, G, C, H, affine, relu):
     assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
     _close(y, yr)
     _close(x.grad, xr.grad, rel=3e-2)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 1
     torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-3, atol=1e-4)
     if affine:
