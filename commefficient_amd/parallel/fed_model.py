@@ -28,6 +28,7 @@ one process per MI355X:
 from __future__ import annotations
 
 import math
+import os
 from contextlib import nullcontext
 from typing import List, Optional, Sequence
 
@@ -495,8 +496,22 @@ class FedModel:
         a = self.args
         out = self._transmit_buffer()
         out.zero_()
-        msum = None
         self._dp_ctr = getattr(self, "_dp_ctr", 0)
+        # every client computes at the same weights (except FedAvg's local
+        # steps and per-client top-k-down weights): one autocast context
+        # around the loop lets the clients share the bf16 weight casts
+        shared_w = (a.mode != "fedavg" and "weights" not in self.client_state.kinds
+                    and not a.do_test and os.environ.get("COMMEFF_SHARED_CASTS", "1") != "0")
+        with (self._autocast() if shared_w else nullcontext()):
+            msum = self._per_client_loop(rb, order, starts, my_slots, mine, counts, W, out)
+        if msum is None:  # no clients on this rank this round
+            msum = torch.zeros(self._n_metrics_guess(), W, device=self.device)
+        self._n_metrics = msum.shape[0]
+        return out, msum
+
+    def _per_client_loop(self, rb, order, starts, my_slots, mine, counts, W, out):
+        a = self.args
+        msum = None
         for slot, c in zip(my_slots, mine):
             c = int(c)
             n = int(counts[slot])
@@ -537,10 +552,7 @@ class FedModel:
                 out.index_add_(0, idx, vals)
             else:
                 out.add_(transmit.view(-1))
-        if msum is None:  # no clients on this rank this round
-            msum = torch.zeros(self._n_metrics_guess(), W, device=self.device)
-        self._n_metrics = msum.shape[0]
-        return out, msum
+        return msum
 
     def _n_metrics_guess(self):
         return getattr(self, "_n_metrics", 2)
