@@ -313,6 +313,20 @@ at::Tensor cs_query_hip(const at::Tensor& table, const at::Tensor& hashes,
   return est;
 }
 
+// two-pass row-wise query (large d without a plan): r x d fp32 scratch
+at::Tensor cs_query_rows_hip(const at::Tensor& table, const at::Tensor& hashes,
+                             const at::Tensor& blk_off, const at::Tensor& blk_sign,
+                             int64_t num_blocks, int64_t d) {
+  check_f32(table, "table");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  auto ctx = make_ctx(hashes, blk_off, blk_sign, num_blocks, d, table.size(-1), true);
+  auto est = at::empty({d}, table.options());
+  auto vals = at::empty({static_cast<int64_t>(ctx.geom.r) * d}, table.options());
+  launch_cs_query_rows(table.data_ptr<float>(), vals.data_ptr<float>(), est.data_ptr<float>(), ctx.rows,
+                       ctx.geom, ctx.blk_off, ctx.blk_sign, cur_stream());
+  return est;
+}
+
 void cs_zero_buckets_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2,
                          const at::Tensor& idx, const c10::optional<at::Tensor>& vals,
                          const at::Tensor& hashes, const at::Tensor& blk_off,
@@ -1191,6 +1205,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("conv_prep_wgrad(Tensor gy, Tensor mask, Tensor x) -> Tensor");
   m.def("conv_prep_wgrad_into(Tensor gy, Tensor mask, Tensor x, Tensor(a!) dw) -> ()");
   m.def("relu_mask(Tensor gy, Tensor y) -> Tensor");
+  m.def("cs_query_rows(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
+        "int d) -> Tensor");
   m.def("cs_query(Tensor table, Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, "
         "int d) -> Tensor");
   m.def("cs_zero_buckets(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, Tensor hashes, "
@@ -1243,6 +1259,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   using namespace commeff;
   m.impl("cs_encode", &cs_encode_hip);
   m.impl("cs_query", &cs_query_hip);
+  m.impl("cs_query_rows", &cs_query_rows_hip);
   m.impl("cs_layout", &cs_layout_hip);
   m.impl("cs_hash_all", &cs_hash_all_hip);
   m.impl("cs_encode_planned", &cs_encode_planned_hip);

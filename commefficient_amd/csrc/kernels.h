@@ -73,6 +73,11 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
 void launch_cs_query(const float* table, float* est, const RowHashes& h,
                      const SketchGeom& g, const int32_t* blk_off,
                      const float* blk_sign, hipStream_t stream);
+// the same estimate in r gather passes (one table row each, L2-resident) into
+// vals [r, d] and a median pass
+void launch_cs_query_rows(const float* table, float* vals, float* est, const RowHashes& h,
+                          const SketchGeom& g, const int32_t* blk_off, const float* blk_sign,
+                          hipStream_t stream);
 // For every selected coordinate idx[t] with vals[t] != 0 zero the r cells
 // (j, b_j(idx[t])) of t1 and (optionally) t2.
 void launch_cs_zero_buckets(float* t1, float* t2, const int64_t* idx,

@@ -301,6 +301,53 @@ cs_query_kernel(const float* __restrict__ table, float* __restrict__ est, HashAr
   }
 }
 
+// ------------------------------------------------------- row-wise query
+// Two-pass query for large d (no plan needed): pass j gathers row j only,
+// vals[j][i] = s_j(i) table[j][h_j(i)] -- one 2 MB table row is re-read by
+// every XCD from its own L2 instead of the whole r x c table from the MALL;
+// then a streaming pass takes the lower median of the r rows per coordinate.
+__global__ void __launch_bounds__(256)
+cs_query_row_kernel(const float* __restrict__ trow, float* __restrict__ vrow, HashArgs h,
+                    SketchGeom g, const int32_t* __restrict__ blk_off,
+                    const float* __restrict__ blk_sign, uint32_t j) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const RowHash hr = h.row[j];
+  for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < g.d; i0 += 4 * stride) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + u * stride;
+      v[u] = 0.f;
+      if (i < g.d) {
+        uint32_t blk, t, bk;
+        float sg;
+        split_block(i, g, &blk, &t);
+        hash_t(hr, t, blk, g, blk_off + j * g.num_blocks, blk_sign + j * g.num_blocks, &bk, &sg);
+        v[u] = sg * trow[bk];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + u * stride;
+      if (i < g.d) vrow[i] = v[u];
+    }
+  }
+}
+
+template <int R>
+__global__ void __launch_bounds__(256)
+cs_median_rows_kernel(const float* __restrict__ vals, float* __restrict__ est, uint32_t d,
+                      uint32_t r_rt) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const int r = R > 0 ? R : static_cast<int>(r_rt);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d; i += stride) {
+    float v[kMaxRows];
+#pragma unroll
+    for (int j = 0; j < (R > 0 ? R : kMaxRows); ++j) v[j] = j < r ? vals[static_cast<size_t>(j) * d + i] : 0.f;
+    est[i] = lower_median<R>(v, r);
+  }
+}
+
 // ------------------------------------------------------------- zero buckets
 __global__ void __launch_bounds__(256)
 cs_zero_kernel(float* __restrict__ t1, float* __restrict__ t2,
@@ -455,6 +502,24 @@ void launch_cs_query(const float* table, float* est, const RowHashes& h, const S
     case 5: hipLaunchKernelGGL(cs_query_kernel<5>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
     case 7: hipLaunchKernelGGL(cs_query_kernel<7>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
     default: hipLaunchKernelGGL(cs_query_kernel<0>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+  }
+}
+
+void launch_cs_query_rows(const float* table, float* vals, float* est, const RowHashes& h,
+                          const SketchGeom& g, const int32_t* blk_off, const float* blk_sign,
+                          hipStream_t stream) {
+  if (g.d == 0) return;
+  HashArgs a = to_args(h, g);
+  const dim3 grid(grid_for(g.d, 1024, 8192));
+  for (uint32_t j = 0; j < g.r; ++j)
+    hipLaunchKernelGGL(cs_query_row_kernel, grid, dim3(256), 0, stream, table + static_cast<size_t>(j) * g.c,
+                       vals + static_cast<size_t>(j) * g.d, a, g, blk_off, blk_sign, j);
+  const dim3 g2(grid_for(g.d, 256, 16384));
+  switch (g.r) {
+    case 5: hipLaunchKernelGGL(cs_median_rows_kernel<5>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
+    case 3: hipLaunchKernelGGL(cs_median_rows_kernel<3>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
+    case 1: hipLaunchKernelGGL(cs_median_rows_kernel<1>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
+    default: hipLaunchKernelGGL(cs_median_rows_kernel<0>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
   }
 }
 

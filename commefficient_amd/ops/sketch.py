@@ -139,6 +139,12 @@ class CSVec:
         """Median-of-rows estimate of every coordinate (dense, length d)."""
         if self._use_plan():
             return ops().cs_query_planned(self.table, self.d, self._plan())
+        if self.device.type == "cuda" and self.kernel != "direct":
+            # no plan (e.g. GPT-2's 249 entries per bucket): one gather pass per
+            # table row (an L2-resident 2 MB row) + a median pass; 2x the
+            # hash-on-the-fly query at GPT-2 size (scripts/bench_codec.py)
+            return ops().cs_query_rows(self.table, self.hashes, self.blk_off, self.blk_sign,
+                                       self.numBlocks, self.d)
         return ops().cs_query(self.table, self.hashes, self.blk_off, self.blk_sign,
                               self.numBlocks, self.d)
 

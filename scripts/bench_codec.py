@@ -40,6 +40,11 @@ def main():
         skb = CSVec(d, c, r, device="cuda", numBlocks=20, kernel="binned")
         res["encode_binned_us"] = timeit(lambda: skb.accumulateVec(v, 1.0, w, 1e-3))
         res["query_hash_us"] = timeit(lambda: skb.query())
+        from commefficient_amd._ext import ops as _o
+        res["query_rows_us"] = timeit(lambda: _o().cs_query_rows(
+            skb.table, skb.hashes, skb.blk_off, skb.blk_sign, skb.numBlocks, skb.d))
+        torch.testing.assert_close(_o().cs_query_rows(skb.table, skb.hashes, skb.blk_off, skb.blk_sign,
+                                                      skb.numBlocks, skb.d), skb.query())
         if d < 2e7:
             res["encode_direct_us"] = timeit(lambda: skb.accumulateVec(v, 1.0, w, 1e-3, dense=False), 5)
         del skb

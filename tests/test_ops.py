@@ -391,3 +391,19 @@ def test_client_means_matches_index_add(counts_dtype):
     out = torch.full((2, W), float("nan"), device="cuda")
     ops.client_means(out, [r.cuda() for r in rows], slot.cuda(), counts.to(counts_dtype).cuda())
     torch.testing.assert_close(out.cpu(), ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("r,nb", [(5, 1), (3, 7), (4, 1), (16, 2)])
+def test_query_rows_matches_oracle(r, nb):
+    """Row-wise two-pass query (the GPU path without a plan) vs the oracle."""
+    torch.manual_seed(5)
+    d, c = 30011, 997
+    sk = CSVec(d, c, r, device="cuda", numBlocks=nb, kernel="binned")
+    h, bo, bs = make_hashes(r, c, nb, 42)
+    orc = OracleSketch(h, bo, bs, d, c, r, nb)
+    v = torch.randn(d)
+    sk.accumulateVec(v.cuda())
+    orc.accumulate_vec(v)
+    est = sk.query().cpu().double()
+    torch.testing.assert_close(est, orc.query(), rtol=1e-5, atol=1e-4)
