@@ -1,3 +1,5 @@
+"""Debug helper: which state diverges between two identical GPU FetchSGD runs (used to
+find that only the binned, LDS-atomic sketch path is not bitwise reproducible)."""
 import sys, torch
 sys.path.insert(0, '.')
 from commefficient_amd import models
