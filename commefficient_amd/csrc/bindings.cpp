@@ -627,7 +627,7 @@ PlannedArgs planned_args(at::TensorList plan, const PlanGeom& p, int64_t d, int6
 
 void cs_encode_planned_hip(at::Tensor table, const at::Tensor& vec, double scale,
                            const c10::optional<at::Tensor>& wvec, double wscale, int64_t c,
-                           at::TensorList plan) {
+                           at::TensorList plan, bool overwrite) {
   check_f32(table, "table");
   check_f32(vec, "vec");
   if (wvec.has_value() && wvec->defined()) {
@@ -639,7 +639,7 @@ void cs_encode_planned_hip(at::Tensor table, const at::Tensor& vec, double scale
   const PlanGeom p = plan_geom_or_throw(d, r, c);
   launch_cs_encode_planned(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
                            static_cast<float>(scale), static_cast<float>(wscale), d,
-                           static_cast<int>(r), c, p, planned_args(plan, p, d, r), cur_stream());
+                           static_cast<int>(r), c, p, planned_args(plan, p, d, r), overwrite, cur_stream());
 }
 
 at::Tensor cs_query_planned_hip(const at::Tensor& table, int64_t d, at::TensorList plan) {
@@ -1178,7 +1178,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("cs_hash_all(Tensor hashes, Tensor blk_off, Tensor blk_sign, int num_blocks, int d, int c, "
         "Tensor like) -> Tensor");
   m.def("cs_encode_planned(Tensor(a!) table, Tensor vec, float scale, Tensor? wvec, float wscale, "
-        "int c, Tensor[] plan) -> ()");
+        "int c, Tensor[] plan, bool overwrite=False) -> ()");
   m.def("cs_query_planned(Tensor table, int d, Tensor[] plan) -> Tensor");
   m.def("plan_geometry(int d, int r, int c) -> int[]", &commeff::plan_geometry);
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");

@@ -64,9 +64,10 @@ struct PlannedArgs {
 };
 void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
                         const float* blk_sign, int32_t* out, hipStream_t stream);
+// overwrite: table = S(v) (every bucket written, no prior zeroing) instead of +=
 void launch_cs_encode_planned(float* table, const float* vec, const float* wvec, float scale,
                               float wscale, int64_t d, int r, int64_t c, const PlanGeom& p,
-                              const PlannedArgs& a, hipStream_t stream);
+                              const PlannedArgs& a, bool overwrite, hipStream_t stream);
 void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,
                              const PlanGeom& p, const PlannedArgs& a, hipStream_t stream);
 // est[i] = lower-median_j( s_j(i) * table[j, b_j(i)] )

@@ -106,7 +106,7 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
               const uint16_t* __restrict__ perm, const int32_t* __restrict__ csr,
               const int32_t* __restrict__ seg, const int32_t* __restrict__ p2_src,
               const int32_t* __restrict__ p2_pos, uint32_t tile, uint32_t total_buckets,
-              uint32_t num_chunks) {
+              uint32_t num_chunks, bool overwrite) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // LDS: bucket-ordered segment S [kPlanSegCap] | run metadata [2*num_chunks+1]
   float* S = reinterpret_cast<float*>(smem);
@@ -171,7 +171,8 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
     const uint32_t x0 = static_cast<uint32_t>(csr[gb]) - lo, x1 = static_cast<uint32_t>(csr[gb + 1]) - lo;
     float acc = 0.f;
     for (uint32_t x = x0; x < x1; ++x) acc += S[x];
-    if (x1 > x0) table[gb] += acc;
+    if (overwrite) table[gb] = acc;
+    else if (x1 > x0) table[gb] += acc;
   }
 }
 
@@ -383,7 +384,7 @@ void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* 
 
 void launch_cs_encode_planned(float* table, const float* vec, const float* wvec, float scale,
                               float wscale, int64_t d, int r, int64_t c, const PlanGeom& p,
-                              const PlannedArgs& a, hipStream_t stream) {
+                              const PlannedArgs& a, bool overwrite, hipStream_t stream) {
   if (d == 0) return;
   static bool attr = false;
   if (!attr) {
@@ -407,7 +408,7 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
   const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4 + (2 * p.num_chunks + 1) * 4;
   hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(1024), l2, stream, table, a.vals, a.perm,
                      a.csr, a.seg, a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
-                     static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks));
+                     static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks), overwrite);
 }
 
 void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,

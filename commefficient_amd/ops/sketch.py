@@ -120,14 +120,17 @@ class CSVec:
 
     def accumulateVec(self, vec: torch.Tensor, scale: float = 1.0,
                       wvec: Optional[torch.Tensor] = None, wscale: float = 0.0,
-                      dense: bool = True):
-        """table += S(scale*vec + wscale*wvec).  ``dense=False`` uses the
-        direct-atomic kernel (best for sparse vectors)."""
+                      dense: bool = True, overwrite: bool = False):
+        """table += S(scale*vec + wscale*wvec) (``overwrite``: table = S(...),
+        no separate zeroing pass on the planned path).  ``dense=False`` uses
+        the direct-atomic kernel (best for sparse vectors)."""
         assert vec.numel() == self.d, (vec.numel(), self.d)
         if dense and self._use_plan():
             ops().cs_encode_planned(self.table, vec.reshape(-1), float(scale), wvec,
-                                    float(wscale), self.c, self._plan())
+                                    float(wscale), self.c, self._plan(), bool(overwrite))
             return
+        if overwrite:
+            self.table.zero_()
         layout = self._binned_layout() if (dense and self.kernel != "direct") else []
         ops().cs_encode(self.table, vec.reshape(-1), self.hashes, self.blk_off, self.blk_sign,
                         self.numBlocks, float(scale), wvec, float(wscale), layout)

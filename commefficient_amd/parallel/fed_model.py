@@ -375,10 +375,9 @@ class FedModel:
         a = self.args
         wscale = a.weight_decay / a.num_workers * n_local
         if a.mode == "sketch":
-            out.zero_()
             sk = self.sketch.like(out.view(a.num_rows, a.num_cols))
             sk.accumulateVec(self.flat.g, 1.0, self.w if wscale != 0 else None, wscale,
-                             dense=a.encode != "direct")
+                             dense=a.encode != "direct", overwrite=True)
         else:
             # fedavg (single local step): sum_i (w - (w - lr g_i)) n_i = lr * transmit
             s = self.fedavg_lr if a.mode == "fedavg" else 1.0

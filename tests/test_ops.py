@@ -407,3 +407,20 @@ def test_query_rows_matches_oracle(r, nb):
     orc.accumulate_vec(v)
     est = sk.query().cpu().double()
     torch.testing.assert_close(est, orc.query(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_planned_encode_overwrite_equals_zero_then_add():
+    """overwrite=True writes every bucket (no separate zeroing pass) and equals
+    zero + accumulate bitwise."""
+    torch.manual_seed(9)
+    d, c, r = 200003, 50000, 5
+    sk = CSVec(d, c, r, device="cuda", numBlocks=3)
+    assert sk._use_plan()
+    v = torch.randn(d, device="cuda")
+    w = torch.randn(d, device="cuda")
+    sk.table.normal_()  # garbage that overwrite must not keep
+    sk.accumulateVec(v, 0.5, w, 0.1, overwrite=True)
+    ref = sk.like()
+    ref.accumulateVec(v, 0.5, w, 0.1)
+    assert torch.equal(sk.table, ref.table)
