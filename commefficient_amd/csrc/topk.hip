@@ -10,13 +10,15 @@
 //
 // Algorithm (no host sync, fixed launch sequence -> hipGraph capturable):
 //   key(i) = bits(x[i]) & 0x7fffffff        (monotone in |x| for finite x)
-//   three histogram passes over 11/11/9-bit digits of the key, each followed
-//   by a one-workgroup "select" kernel that walks the histogram from the top
-//   and fixes the next digit of the k-th largest key T (state in device
-//   memory);  then a count pass (per-block #>T, #==T), a one-workgroup scan,
-//   and an ordered compaction pass that uses wave ballots for intra-block
-//   prefix sums.  Histograms are privatised in LDS; only non-empty bins are
-//   flushed to global memory with atomics.
+//   three histogram passes over 11/11/9-bit digits of the key (one histogram
+//   buffer each), a count pass (per-block #>T, #==T) and an ordered
+//   compaction pass.  The digit selections (walk a histogram from the top to
+//   the bin holding the k-th largest key) and the scan of the per-block
+//   counts are not kernels of their own: every block of the following pass
+//   redoes them in its prologue from the (L2-resident) histograms / counts --
+//   identical integer work in every block, so the result stays deterministic
+//   -- which saves four one-workgroup launches per top-k.  Histograms are
+//   privatised in LDS; only non-empty bins are flushed with atomics.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "kernels.h"
@@ -27,31 +29,21 @@ namespace {
 constexpr int kBins = 2048;
 constexpr int kNB = 1024;  // blocks for count/write passes (upper bound)
 
-struct State {
-  uint32_t prefix;     // key bits fixed so far (right-aligned)
-  uint32_t remaining;  // how many still needed among keys matching prefix
-  uint32_t thr;        // final threshold key
-  uint32_t ties;       // number of keys == thr to take
-};
-
 struct WS {
-  uint32_t* hist;   // kBins
-  State* st;
-  uint32_t* cnt_gt; // kNB
-  uint32_t* cnt_eq; // kNB
-  uint32_t* off_sel;// kNB: selected before block
-  uint32_t* off_eq; // kNB: ties before block
+  uint32_t* hist[3];  // kBins each (pass 2 uses 512)
+  uint32_t* cnt_gt;   // kNB
+  uint32_t* cnt_eq;   // kNB
 };
 
 WS carve(void* base) {
   char* p = reinterpret_cast<char*>(base);
   WS w;
-  w.hist = reinterpret_cast<uint32_t*>(p); p += kBins * 4;
-  w.st = reinterpret_cast<State*>(p); p += 256;
+  for (int i = 0; i < 3; ++i) {
+    w.hist[i] = reinterpret_cast<uint32_t*>(p);
+    p += kBins * 4;
+  }
   w.cnt_gt = reinterpret_cast<uint32_t*>(p); p += kNB * 4;
   w.cnt_eq = reinterpret_cast<uint32_t*>(p); p += kNB * 4;
-  w.off_sel = reinterpret_cast<uint32_t*>(p); p += kNB * 4;
-  w.off_eq = reinterpret_cast<uint32_t*>(p); p += kNB * 4;
   return w;
 }
 
@@ -59,17 +51,96 @@ __device__ __forceinline__ uint32_t key_of(float x) {
   return __float_as_uint(x) & 0x7fffffffu;
 }
 
+// Block-wide (256 threads) digit selection: the bin of `hist` (nbins, walked
+// from the top) that holds the `remaining`-th largest key and the count of
+// keys in higher bins.  Every thread gets the result.
+struct Sel {
+  uint32_t bin, above;
+};
+template <int NBINS>
+__device__ Sel select_bin(const uint32_t* __restrict__ hist, uint32_t remaining, uint32_t* tot,
+                          uint32_t* res) {
+  constexpr int per = NBINS / 256;
+  uint32_t c[per];
+  uint32_t s = 0;
+#pragma unroll
+  for (int q = 0; q < per; ++q) {
+    c[q] = hist[NBINS - 1 - (threadIdx.x * per + q)];
+    s += c[q];
+  }
+  // inclusive scan over threads: wave scans + 4 wave totals
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) tot[wave] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) before += w < wave ? tot[w] : 0u;
+  const uint32_t above = before + inc - s;
+  if (threadIdx.x == 0) {
+    res[0] = 0;
+    res[1] = 0;
+  }
+  __syncthreads();
+  if (above < remaining && above + s >= remaining) {
+    uint32_t run = above;
+#pragma unroll
+    for (int q = 0; q < per; ++q) {
+      if (run + c[q] >= remaining) {
+        res[0] = NBINS - 1 - (threadIdx.x * per + q);
+        res[1] = run;
+        break;
+      }
+      run += c[q];
+    }
+  }
+  __syncthreads();
+  const Sel r = {res[0], res[1]};
+  __syncthreads();  // tot / res reusable
+  return r;
+}
+
+// the (prefix, remaining) after PASSES digit selections; thr/ties when 3
+struct Walk {
+  uint32_t prefix, remaining;
+};
+template <int PASSES>
+__device__ Walk walk(const WS& w, uint32_t k, uint32_t* tot, uint32_t* res) {
+  Walk s = {0u, k};
+  if (PASSES >= 1) {
+    const Sel a = select_bin<2048>(w.hist[0], s.remaining, tot, res);
+    s.prefix = a.bin;
+    s.remaining -= a.above;
+  }
+  if (PASSES >= 2) {
+    const Sel a = select_bin<2048>(w.hist[1], s.remaining, tot, res);
+    s.prefix = (s.prefix << 11) | a.bin;
+    s.remaining -= a.above;
+  }
+  if (PASSES >= 3) {
+    const Sel a = select_bin<512>(w.hist[2], s.remaining, tot, res);
+    s.prefix = (s.prefix << 9) | a.bin;  // = the k-th largest key
+    s.remaining -= a.above;              // = how many keys == thr to take
+  }
+  return s;
+}
+
 // PASS 0: digit = key >> 20 (11 bits)
 // PASS 1: digit = (key >> 9) & 0x7ff, needs (key >> 20) == prefix
 // PASS 2: digit = key & 0x1ff,         needs (key >> 9)  == prefix
 template <int PASS>
 __global__ void __launch_bounds__(256)
-hist_kernel(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ hist,
-            const State* __restrict__ st) {
+hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk) {
   __shared__ uint32_t h[kBins];
+  __shared__ uint32_t tot[4], res[2];
   for (int b = threadIdx.x; b < kBins; b += blockDim.x) h[b] = 0;
-  __syncthreads();
-  const uint32_t prefix = PASS == 0 ? 0u : st->prefix;
+  const uint32_t prefix = walk<PASS>(ws, kk, tot, res).prefix;
+  __syncthreads();  // h zeroed before any atomic
   // (LDS atomics retire ~0.4 lanes/clk/CU and bound pass 0; per-wave
   // sub-histograms measured no faster, wave-aggregated atomics 4x slower:
   // normal-ish data spreads a wave over too many distinct bins)
@@ -112,81 +183,17 @@ hist_kernel(const float* __restrict__ x, int64_t n, uint32_t* __restrict__ hist,
     add(j < n ? x[j] : 0.f, j < n);
   }
   __syncthreads();
+  uint32_t* hist = ws.hist[PASS];
   for (int b = threadIdx.x; b < kBins; b += blockDim.x) {
     const uint32_t c = h[b];
     if (c) atomicAdd(hist + b, c);
   }
 }
 
-// One workgroup of 256 threads.  Finds the bin holding the `remaining`-th
-// largest key among the histogrammed ones, updates prefix/remaining and
-// zeroes the histogram for the next pass.
-template <int PASS>
 __global__ void __launch_bounds__(256)
-select_kernel(uint32_t* __restrict__ hist, State* __restrict__ st, uint32_t k_init) {
-  constexpr int nbins = PASS == 2 ? 512 : 2048;
-  constexpr int per = nbins / 256;  // bins per thread (8 or 2)
-  __shared__ uint32_t tot[256];
-  __shared__ uint32_t found_bin, found_above;
-  const uint32_t remaining = PASS == 0 ? k_init : st->remaining;
-  // thread t owns bins [nbins-1 - t*per - (per-1), nbins-1 - t*per]: scanning
-  // from the top means thread 0 has the largest bins.
-  uint32_t c[per];
-  uint32_t s = 0;
-#pragma unroll
-  for (int q = 0; q < per; ++q) {
-    int b = nbins - 1 - (threadIdx.x * per + q);
-    c[q] = hist[b];
-    s += c[q];
-  }
-  tot[threadIdx.x] = s;
-  __syncthreads();
-  // exclusive prefix over threads (Hillis-Steele in LDS, 8 steps)
-  for (int o = 1; o < 256; o <<= 1) {
-    uint32_t v = threadIdx.x >= o ? tot[threadIdx.x - o] : 0u;
-    __syncthreads();
-    tot[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint32_t above = threadIdx.x ? tot[threadIdx.x - 1] : 0u;  // keys in higher bins
-  if (threadIdx.x == 0) {
-    found_bin = 0;
-    found_above = 0;
-  }
-  __syncthreads();
-  if (above < remaining && above + s >= remaining) {
-    uint32_t run = above;
-#pragma unroll
-    for (int q = 0; q < per; ++q) {
-      if (run + c[q] >= remaining) {
-        found_bin = nbins - 1 - (threadIdx.x * per + q);
-        found_above = run;
-        break;
-      }
-      run += c[q];
-    }
-  }
-  __syncthreads();
-  // zero the histogram for the next pass / next call
-  for (int b = threadIdx.x; b < kBins; b += 256) hist[b] = 0;
-  if (threadIdx.x == 0) {
-    uint32_t prefix = PASS == 0 ? 0u : st->prefix;
-    const int bits = PASS == 2 ? 9 : 11;
-    prefix = (prefix << bits) | found_bin;
-    st->prefix = prefix;
-    st->remaining = remaining - found_above;
-    if (PASS == 2) {
-      st->thr = prefix;
-      st->ties = remaining - found_above;
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256)
-count_kernel(const float* __restrict__ x, int64_t n, int64_t span,
-             const State* __restrict__ st, uint32_t* __restrict__ cnt_gt,
-             uint32_t* __restrict__ cnt_eq) {
-  const uint32_t thr = st->thr;
+count_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32_t kk) {
+  __shared__ uint32_t tot[4], res[2];
+  const uint32_t thr = walk<3>(ws, kk, tot, res).prefix;
   const int64_t i0 = blockIdx.x * span;
   const int64_t i1 = min(n, i0 + span);
   uint32_t gt = 0, eq = 0;
@@ -213,34 +220,8 @@ count_kernel(const float* __restrict__ x, int64_t n, int64_t span,
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    cnt_gt[blockIdx.x] = sg[0] + sg[1] + sg[2] + sg[3];
-    cnt_eq[blockIdx.x] = se[0] + se[1] + se[2] + se[3];
-  }
-}
-
-__global__ void __launch_bounds__(1024)
-scan_kernel(int nb, const State* __restrict__ st, const uint32_t* __restrict__ cnt_gt,
-            const uint32_t* __restrict__ cnt_eq, uint32_t* __restrict__ off_sel,
-            uint32_t* __restrict__ off_eq) {
-  __shared__ uint32_t a[kNB], b[kNB];
-  const int t = threadIdx.x;
-  a[t] = t < nb ? cnt_gt[t] : 0u;
-  b[t] = t < nb ? cnt_eq[t] : 0u;
-  __syncthreads();
-  for (int o = 1; o < kNB; o <<= 1) {
-    uint32_t va = t >= o ? a[t - o] : 0u;
-    uint32_t vb = t >= o ? b[t - o] : 0u;
-    __syncthreads();
-    a[t] += va;
-    b[t] += vb;
-    __syncthreads();
-  }
-  if (t < nb) {
-    uint32_t gt_before = t ? a[t - 1] : 0u;
-    uint32_t eq_before = t ? b[t - 1] : 0u;
-    uint32_t ties = st->ties;
-    off_sel[t] = gt_before + min(eq_before, ties);
-    off_eq[t] = eq_before;
+    ws.cnt_gt[blockIdx.x] = sg[0] + sg[1] + sg[2] + sg[3];
+    ws.cnt_eq[blockIdx.x] = se[0] + se[1] + se[2] + se[3];
   }
 }
 
@@ -263,21 +244,33 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wt, ui
   return before + inc - v;
 }
 
-// ordered compaction: a block owns [i0, i1); per iteration each thread takes
-// 4 consecutive elements (one 16-byte load), tie ranks and output slots come
-// from two block-wide exclusive scans (elements stay in ascending order)
+// ordered compaction: a block owns [i0, i1); its output offsets are the sums
+// of the counts of the blocks before it (computed here, in a fixed order);
+// per iteration each thread takes 4 consecutive elements (one 16-byte load),
+// tie ranks and output slots come from two block-wide exclusive scans
+// (elements stay in ascending order)
 __global__ void __launch_bounds__(256)
-write_kernel(const float* __restrict__ x, int64_t n, int64_t span,
-             const State* __restrict__ st, const uint32_t* __restrict__ off_sel,
-             const uint32_t* __restrict__ off_eq, int64_t* __restrict__ idx,
-             float* __restrict__ vals) {
-  const uint32_t thr = st->thr;
-  const uint32_t ties = st->ties;
+write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32_t kk,
+             int64_t* __restrict__ idx, float* __restrict__ vals) {
+  __shared__ uint32_t tot[4], res[2];
+  __shared__ uint32_t wt_eq[4], wt_sel[4];
+  const Walk wk = walk<3>(ws, kk, tot, res);
+  const uint32_t thr = wk.prefix, ties = wk.remaining;
+  // counts of the blocks before this one
+  uint32_t g = 0, e = 0;
+  for (int b = threadIdx.x; b < static_cast<int>(blockIdx.x); b += 256) {
+    g += ws.cnt_gt[b];
+    e += ws.cnt_eq[b];
+  }
+  uint32_t gt_before, eq_before;
+  (void)block_excl_scan(g, wt_sel, gt_before);
+  __syncthreads();
+  (void)block_excl_scan(e, wt_eq, eq_before);
+  __syncthreads();
+  uint32_t sel_base = gt_before + min(eq_before, ties);
+  uint32_t eq_base = eq_before;
   const int64_t i0 = blockIdx.x * span;
   const int64_t i1 = min(n, i0 + span);
-  uint32_t sel_base = off_sel[blockIdx.x];
-  uint32_t eq_base = off_eq[blockIdx.x];
-  __shared__ uint32_t wt_eq[4], wt_sel[4];
   const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   for (int64_t base = i0; base < i1; base += 1024) {
     const int64_t i = base + 4 * threadIdx.x;
@@ -325,35 +318,28 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span,
 }  // namespace
 
 int64_t topk_workspace_bytes(int64_t) {
-  return kBins * 4 + 256 + 4 * kNB * 4;
+  return 3 * kBins * 4 + 2 * kNB * 4;
 }
 
 void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,
                      void* workspace, hipStream_t stream) {
   if (k <= 0 || n <= 0) return;
   WS w = carve(workspace);
-  (void)hipMemsetAsync(w.hist, 0, kBins * 4, stream);
+  (void)hipMemsetAsync(w.hist[0], 0, 3 * kBins * 4, stream);
   int hb = static_cast<int>((n + 1023) / 1024);
   if (hb > 1024) hb = 1024;
   if (hb < 1) hb = 1;
-  uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
-  hipLaunchKernelGGL(hist_kernel<0>, dim3(hb), dim3(256), 0, stream, x, n, w.hist, w.st);
-  hipLaunchKernelGGL(select_kernel<0>, dim3(1), dim3(256), 0, stream, w.hist, w.st, kk);
-  hipLaunchKernelGGL(hist_kernel<1>, dim3(hb), dim3(256), 0, stream, x, n, w.hist, w.st);
-  hipLaunchKernelGGL(select_kernel<1>, dim3(1), dim3(256), 0, stream, w.hist, w.st, kk);
-  hipLaunchKernelGGL(hist_kernel<2>, dim3(hb), dim3(256), 0, stream, x, n, w.hist, w.st);
-  hipLaunchKernelGGL(select_kernel<2>, dim3(1), dim3(256), 0, stream, w.hist, w.st, kk);
+  const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
+  hipLaunchKernelGGL(hist_kernel<0>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
+  hipLaunchKernelGGL(hist_kernel<1>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
+  hipLaunchKernelGGL(hist_kernel<2>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
   int nb = static_cast<int>((n + 255) / 256);
   if (nb > kNB) nb = kNB;
   int64_t span = (n + nb - 1) / nb;
   span = ((span + 1023) / 1024) * 1024;  // write_kernel: 1024 elements per block step
   nb = static_cast<int>((n + span - 1) / span);
-  hipLaunchKernelGGL(count_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w.st, w.cnt_gt,
-                     w.cnt_eq);
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(kNB), 0, stream, nb, w.st, w.cnt_gt, w.cnt_eq,
-                     w.off_sel, w.off_eq);
-  hipLaunchKernelGGL(write_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w.st, w.off_sel,
-                     w.off_eq, idx, vals);
+  hipLaunchKernelGGL(count_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk);
+  hipLaunchKernelGGL(write_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, idx, vals);
 }
 
 }  // namespace commeff
