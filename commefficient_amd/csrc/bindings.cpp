@@ -882,41 +882,50 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
   return {y, stat};
 }
 
-// returns (dx, dweight, dbias) (dweight / dbias undefined without affine)
+// returns (dx, dweight, dbias) (dweight / dbias undefined without affine, or
+// when gw / gb -- existing fp32 .grad tensors -- receive them: += in place)
 std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor& dy, const at::Tensor& x,
                                                                 const at::Tensor& stat,
                                                                 const c10::optional<at::Tensor>& w, int64_t G,
-                                                                const c10::optional<at::Tensor>& y_relu) {
+                                                                const c10::optional<at::Tensor>& y_relu,
+                                                                const c10::optional<at::Tensor>& gw,
+                                                                const c10::optional<at::Tensor>& gb) {
   check_nhwc_bf16(x, "ghost_bn_bwd: x");
+  check_nhwc_bf16(dy, "ghost_bn_bwd: dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "ghost_bn_bwd: dy shape");
   const bool fused_relu = y_relu.has_value() && y_relu->defined();
   if (fused_relu) {
     check_nhwc_bf16(*y_relu, "ghost_bn_bwd: y");
     TORCH_CHECK(y_relu->sizes() == x.sizes(), "ghost_bn_bwd: y shape");
   }
-  check_nhwc_bf16(dy, "ghost_bn_bwd: dy");
-  TORCH_CHECK(dy.sizes() == x.sizes(), "ghost_bn_bwd: dy shape");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   const int64_t M = N / G * HW;
   TORCH_CHECK(stat.scalar_type() == at::kFloat && stat.is_contiguous() && stat.numel() == G * 2 * C,
               "ghost_bn_bwd: stat");
   const bool affine = w.has_value() && w->defined();
+  const bool into = affine && gw.has_value() && gw->defined() && gb.has_value() && gb->defined();
+  if (into) {
+    check_f32(*gw, "ghost_bn_bwd: weight grad");
+    check_f32(*gb, "ghost_bn_bwd: bias grad");
+    TORCH_CHECK(gw->numel() == C && gb->numel() == C, "ghost_bn_bwd: grad shapes");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
   auto fo = x.options().dtype(at::kFloat);
   auto part = at::empty({G * S * 2 * C}, fo);
   auto coef = at::empty({G * 3 * C}, fo);
   at::Tensor dw, db;
-  if (affine) {
+  if (affine && !into) {
     dw = at::empty({C}, fo);
     db = at::empty({C}, fo);
   }
+  float* dwp = into ? gw->data_ptr<float>() : (affine ? dw.data_ptr<float>() : nullptr);
+  float* dbp = into ? gb->data_ptr<float>() : (affine ? db.data_ptr<float>() : nullptr);
   auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   launch_bn_bwd(bf16_ptr(x), bf16_ptr(dy), fused_relu ? bf16_ptr(*y_relu) : nullptr, stat.data_ptr<float>(),
-                affine ? w->data_ptr<float>() : nullptr,
-                static_cast<int>(G), static_cast<int>(M), static_cast<int>(C), part.data_ptr<float>(),
-                coef.data_ptr<float>(), affine ? dw.data_ptr<float>() : nullptr,
-                affine ? db.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dx.data_ptr()),
-                cur_stream());
+                affine ? w->data_ptr<float>() : nullptr, static_cast<int>(G), static_cast<int>(M),
+                static_cast<int>(C), part.data_ptr<float>(), coef.data_ptr<float>(), dwp, dbp,
+                into ? 1.f : 0.f, reinterpret_cast<uint16_t*>(dx.data_ptr()), cur_stream());
   return {dx, dw, db};
 }
 
@@ -1193,8 +1202,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
         "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None) -> (Tensor, Tensor)");
-  m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None) -> "
-        "(Tensor, Tensor, Tensor)");
+  m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None, "
+        "Tensor(a!)? gw=None, Tensor(b!)? gb=None) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");

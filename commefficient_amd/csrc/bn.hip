@@ -234,7 +234,8 @@ bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__
 __global__ void __launch_bounds__(1024)
 bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__ stat,
                        const float* __restrict__ w, int C, int M, int S, int G,
-                       float* __restrict__ coef, float* __restrict__ dw, float* __restrict__ db) {
+                       float* __restrict__ coef, float* __restrict__ dw, float* __restrict__ db,
+                       float beta) {
   __shared__ float red[2][kGL][64];
   const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cc;
@@ -295,8 +296,9 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__
       sw += red[0][q][cc];
       sb += red[1][q][cc];
     }
-    if (dw != nullptr) dw[c] = sw;
-    if (db != nullptr) db[c] = sb;
+    // beta 1: accumulate into an existing .grad (flat-buffer views)
+    if (dw != nullptr) dw[c] = beta != 0.f ? dw[c] + sw : sw;
+    if (db != nullptr) db[c] = beta != 0.f ? db[c] + sb : sb;
   }
 }
 
@@ -373,12 +375,12 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
 
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
-                   uint16_t* dx, hipStream_t stream) {
+                   float beta, uint16_t* dx, hipStream_t stream) {
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
                      S, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat, w,
-                     C, M, S, G, coef, dw, db);
+                     C, M, S, G, coef, dw, db, beta);
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
                      coef, C, M, static_cast<uint32_t>(nchunks), false, dx);

@@ -314,14 +314,25 @@ class _GhostBN(torch.autograd.Function):
                                       running_mean, running_var, bool(relu), nbt)
         ctx.save_for_backward(x, stat, weight, y if relu else None)
         ctx.groups = int(groups)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, stat, weight, y = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        dx, dw, db = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y)
-        if weight is None:
+        # existing fp32 .grad tensors (FedModel's flat-buffer views) receive
+        # dweight / dbias in place: no AccumulateGrad launches
+        pw, pb = ctx.params
+        gw = pw.grad if pw is not None else None
+        gb = pb.grad if pb is not None else None
+        into = (gw is not None and gb is not None and gw.dtype == torch.float32
+                and gb.dtype == torch.float32 and gw.is_contiguous() and gb.is_contiguous()
+                and gw.device == x.device and gb.device == x.device
+                and ctx.needs_input_grad[1] and ctx.needs_input_grad[2])
+        dx, dw, db = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y,
+                                         gw if into else None, gb if into else None)
+        if weight is None or into:
             dw = db = None
         return dx, dw, db, None, None, None, None, None, None, None
 

@@ -376,3 +376,10 @@ def test_ghost_bn_matches_fp32(N, G, C, H, affine, relu):
     if affine:
         torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=2e-2, atol=2e-2)
         torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=2e-2, atol=2e-2)
+        # existing .grad tensors (FedModel's flat-buffer views) accumulate in place
+        gw0, gb0 = bn.weight.grad.clone(), bn.bias.grad.clone()
+        keep = bn.weight.grad
+        (bn(x.detach()).float() * gy).sum().backward()
+        assert bn.weight.grad is keep
+        torch.testing.assert_close(bn.weight.grad, 2 * gw0, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(bn.bias.grad, 2 * gb0, rtol=1e-5, atol=1e-5)
