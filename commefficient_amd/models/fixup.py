@@ -108,36 +108,18 @@ class FixupResNet9(nn.Module):
 
 
 # ---------------------------------------------------------------- ResNet-18s
-class _Mul(nn.Module):
-    def __init__(self):
-        super().__init__()
-        self.scale = nn.Parameter(torch.ones(1))
-
-    def forward(self, x):
-        return x * self.scale
-
-
-class _Add(nn.Module):
-    def __init__(self):
-        super().__init__()
-        self.bias = nn.Parameter(torch.zeros(1))
-
-    def forward(self, x):
-        return x + self.bias
-
-
 class FixupBlock18(nn.Module):
     """Reference fixup_resnet18.py:24-63 (module names add1a/conv1/add1b/add2a/conv2/mul/add2b)."""
 
     def __init__(self, in_channels, out_channels, stride=1):
         super().__init__()
-        self.add1a = _Add()
+        self.add1a = ScalarBias()
         self.conv1 = conv3x3(in_channels, out_channels, stride)
-        self.add1b = _Add()
-        self.add2a = _Add()
+        self.add1b = ScalarBias()
+        self.add2a = ScalarBias()
         self.conv2 = conv3x3(out_channels, out_channels)
-        self.mul = _Mul()
-        self.add2b = _Add()
+        self.mul = ScalarScale()
+        self.add2b = ScalarBias()
         if stride != 1 or in_channels != out_channels:
             self.shortcut = conv1x1(in_channels, out_channels, stride)
 
