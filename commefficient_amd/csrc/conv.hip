@@ -346,14 +346,22 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
 struct HaloGeom {
   int G, Rg, PW, PR, NPW;  // images / rows per image in a tile, padded width / rows, padded rows
 };
-constexpr int kHaloWinBytes = 288 * 128;
-constexpr int kHaloLds = kHaloWinBytes + 2 * 128 * 128;
-constexpr int kHaloWinLd = (288 * 8 + 255) / 256;  // window pieces per thread
+// TBM = 128 (4 waves, window <= 288 rows) or 256 (8 waves, <= 384 rows:
+// 48 KB + B ring 32 KB = 80 KB, still 2 blocks/CU; the B tile then feeds 256
+// pixels, halving its pieces per MFMA once more)
+template <int TBM>
+struct HaloCfg {
+  static constexpr int kMaxRows = TBM == 256 ? 384 : 288;
+  static constexpr int kWinBytes = kMaxRows * 128;
+  static constexpr int kLds = kWinBytes + 2 * 128 * 128;
+  static constexpr int kWinLd = (kMaxRows * 8 + TBM * 2 - 1) / (TBM * 2);  // window pieces per thread
+};
 
-template <bool POOL>
-__global__ void __launch_bounds__(256) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
+template <int TBM, bool POOL>
+__global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int TBM = 128, BN = 128, NI = 2, BLD = 4;
+  constexpr int BN = 128, NI = 2, NT = TBM * 2, BLD = BN * 8 / NT;
+  constexpr int kHaloWinBytes = HaloCfg<TBM>::kWinBytes, kHaloWinLd = HaloCfg<TBM>::kWinLd;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -370,7 +378,7 @@ __global__ void __launch_bounds__(256) conv_fwd_halo_kernel(ConvFwdArgs a, HaloG
   int win_off[kHaloWinLd];
 #pragma unroll
   for (int i = 0; i < kHaloWinLd; ++i) {
-    const int sl = i * 256 + tid;
+    const int sl = i * NT + tid;
     const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
     int off = -1;
     if (row < hg.NPW) {
@@ -384,16 +392,16 @@ __global__ void __launch_bounds__(256) conv_fwd_halo_kernel(ConvFwdArgs a, HaloG
   const uint16_t* b_ptr[BLD];
 #pragma unroll
   for (int j = 0; j < BLD; ++j) {
-    const int sl = j * 256 + tid;
+    const int sl = j * NT + tid;
     const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
     b_ptr[j] = a.w + static_cast<size_t>(n0 + row) * 9 * C + lc * 8;
   }
   auto issue_window = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < kHaloWinLd; ++i) {
-      if (i * 256 + (tid & ~63) < hg.NPW * 8) {  // wave-uniform: pieces past the window skipped
+      if (i * NT + (tid & ~63) < hg.NPW * 8) {  // wave-uniform: pieces past the window skipped
         const int off = win_off[i];
-        glds16(off >= 0 ? a.x + off + cb * 64 : zero, smem + i * 4096 + wid * 1024);
+        glds16(off >= 0 ? a.x + off + cb * 64 : zero, smem + i * NT * 16 + wid * 1024);
       }
     }
   };
@@ -402,7 +410,7 @@ __global__ void __launch_bounds__(256) conv_fwd_halo_kernel(ConvFwdArgs a, HaloG
     unsigned char* base = smem + kHaloWinBytes + (step & 1) * (BN * 128) + wid * 1024;
     const int boff = (step % 9) * C + (step / 9) * 64;
 #pragma unroll
-    for (int j = 0; j < BLD; ++j) glds16(b_ptr[j] + boff, base + j * 4096);
+    for (int j = 0; j < BLD; ++j) glds16(b_ptr[j] + boff, base + j * NT * 16);
   };
 
   // this lane's output pixels (rows of the A fragments) -> padded window rows
@@ -1013,9 +1021,11 @@ bool conv3x3_pool_supported(int H, int W, int K) {
 
 // halo-window geometry of a 128-pixel tile (false: not whole image rows, or
 // the padded window exceeds 288 rows)
-bool halo_geom(int H, int W, int K, HaloGeom* g) {
-  if (K % 128 != 0 || W <= 0 || 128 % W != 0) return false;
-  const int R = 128 / W;
+static int wgrad_slots();
+
+bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g) {
+  if (K % 128 != 0 || W <= 0 || TBM % W != 0) return false;
+  const int R = TBM / W;
   if (R <= H) {
     if (H % R != 0) return false;
     g->G = 1;
@@ -1036,19 +1046,20 @@ bool halo_geom(int H, int W, int K, HaloGeom* g) {
     const int v = e != nullptr ? atoi(e) : 288;
     return v > 288 ? 288 : v;
   }();
-  return g->NPW <= cap;
+  return g->NPW <= (TBM == 256 ? HaloCfg<256>::kMaxRows : cap);
 }
 
-template <bool POOL>
+template <int TBM, bool POOL>
 void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
+  constexpr int lds = HaloCfg<TBM>::kLds;
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<POOL>), kHaloLds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL>), lds);
     init = true;
   }
-  const int mt = (a.P + 127) / 128;
-  hipLaunchKernelGGL(conv_fwd_halo_kernel<POOL>, dim3(mt * (a.K / 128)), dim3(256), kHaloLds, stream, a,
-                     hg);
+  const int mt = (a.P + TBM - 1) / TBM;
+  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL>), dim3(mt * (a.K / 128)), dim3(TBM * 2), lds, stream,
+                     a, hg);
 }
 
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
@@ -1058,9 +1069,19 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
     const char* e = getenv("COMMEFF_CONV_HALO");
     return !(e != nullptr && e[0] == '0');
   }();
+  static const int halo_tbm = [] {  // COMMEFF_CONV_HALO_TBM=128: only the 4-wave tile
+    const char* e = getenv("COMMEFF_CONV_HALO_TBM");
+    return e != nullptr ? atoi(e) : 256;
+  }();
   HaloGeom hg;
-  if (halo_on && halo_geom(a.H, a.W, a.K, &hg)) {
-    if (a.pool == 2) launch_fwd_halo<true>(a, hg, stream); else launch_fwd_halo<false>(a, hg, stream);
+  // 256-pixel tiles when they still give every resident slot (2 per CU) a block
+  if (halo_on && halo_tbm == 256 && halo_geom(a.H, a.W, a.K, 256, &hg) &&
+      static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) >= wgrad_slots()) {
+    if (a.pool == 2) launch_fwd_halo<256, true>(a, hg, stream); else launch_fwd_halo<256, false>(a, hg, stream);
+    return;
+  }
+  if (halo_on && halo_geom(a.H, a.W, a.K, 128, &hg)) {
+    if (a.pool == 2) launch_fwd_halo<128, true>(a, hg, stream); else launch_fwd_halo<128, false>(a, hg, stream);
     return;
   }
   if (a.pool == 2) {  // caller checked conv3x3_pool_supported

@@ -383,3 +383,22 @@ def test_ghost_bn_matches_fp32(N, G, C, H, affine, relu):
         assert bn.weight.grad is keep
         torch.testing.assert_close(bn.weight.grad, 2 * gw0, rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(bn.bias.grad, 2 * gb0, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,C,H,K", [(600, 64, 32, 128), (520, 128, 16, 256)])
+def test_fwd_large_batch_matches_fp32(N, C, H, K):
+    """Batches big enough for the 256-pixel halo tile (8 waves) -- forward,
+    dgrad and the fused pool epilogue against fp32 references."""
+    x, w = _inputs(N, C, H, H, K)
+    wf, wt = ops.conv_weight_prep(w)
+    y = ops.conv3x3_fwd(x, wf, True)
+    ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1).relu()
+    _close(y, ref)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    dy = _nhwc(torch.randn(N, K, H, H, device="cuda", generator=g).to(torch.bfloat16))
+    dx = ops.conv3x3_fwd(dy, wt, False)
+    dref = torch.nn.grad.conv2d_input(x.shape, w.to(torch.bfloat16).float(), dy.float(), padding=1)
+    _close(dx, dref)
+    p, i = torch.ops.commeff.conv3x3_fwd_pool2(x, wf)
+    p_ref, _ = torch.ops.commeff.relu_maxpool(ops.conv3x3_fwd(x, wf, False), 2)
+    assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
