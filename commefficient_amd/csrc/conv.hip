@@ -344,7 +344,10 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_kernel(ConvFwdArgs a) {
 // ~5 per thread (the 128 x 128 loop is bound by per-CU load issue).
 // LDS: window (<= 288 padded rows, 36 KB) + B ring 2 x 16 KB: 68 KB, 2 blocks/CU.
 struct HaloGeom {
-  int G, Rg, PW, PR, NPW;  // images / rows per image in a tile, padded width / rows, padded rows
+  // images / rows per image in a tile, padded width, padded rows (images
+  // stacked with ONE shared zero row between them: G * (Rg + 1) + 1), window
+  // rows (padded rows x padded width)
+  int G, Rg, PW, PR, NPW;
 };
 // TBM = 128 (4 waves, window <= 288 rows) or 256 (8 waves, <= 384 rows:
 // 48 KB + B ring 32 KB = 80 KB, still 2 blocks/CU; the B tile then feeds 256
@@ -382,9 +385,15 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, H
     const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
     int off = -1;
     if (row < hg.NPW) {
-      const int g = row / (hg.PR * hg.PW), rem = row - g * hg.PR * hg.PW;
-      const int pr = rem / hg.PW, pc = rem - pr * hg.PW;
-      const int img = img0 + g, h = h0 + pr - 1, w = pc - 1;
+      const int pr = row / hg.PW, pc = row - pr * hg.PW, w = pc - 1;
+      // padded row pr: G == 1 -> image row h0 + pr - 1 (zero outside the
+      // image); else pr = g (Rg + 1) + 1 + h, separators (pr % (Rg+1) == 0) zero
+      int img = img0, h = h0 + pr - 1;
+      if (hg.G > 1) {
+        const int q = pr / (hg.Rg + 1), rr = pr - q * (hg.Rg + 1);
+        img = img0 + q;
+        h = rr - 1;  // -1 on a separator row
+      }
       if (img < nimg && h >= 0 && h < H && w >= 0 && w < W) off = ((img * H + h) * W + w) * C + lc * 8;
     }
     win_off[i] = off;
@@ -421,7 +430,7 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, H
     const int m = wr * 64 + mi * 32 + lr;
     const int g = m / (hg.Rg * W), rem = m - g * hg.Rg * W;
     const int r = rem / W, w = rem - r * W;
-    pb[mi] = g * hg.PR * hg.PW + (r + 1) * hg.PW + (w + 1);
+    pb[mi] = (g * (hg.Rg + 1) + r + 1) * hg.PW + (w + 1);
   }
   int offB[4][NI];
 #pragma unroll
@@ -1036,8 +1045,8 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g) {
     g->Rg = H;
   }
   g->PW = W + 2;
-  g->PR = g->Rg + 2;
-  g->NPW = g->G * g->PR * g->PW;
+  g->PR = g->G * (g->Rg + 1) + 1;
+  g->NPW = g->PR * g->PW;
   // (ResNet-9 res3, W = 4: 288 padded rows for 128 pixels -- slower alone in
   // scripts/bench_conv.py, but faster inside the round: bench 222-223k with a
   // 256-row cap vs 224-227k with 288, profiles/r1_experiments.md)
@@ -1074,9 +1083,9 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
     return e != nullptr ? atoi(e) : 256;
   }();
   HaloGeom hg;
-  // 256-pixel tiles when they still give every resident slot (2 per CU) a block
+  // 256-pixel tiles when they still give ~every resident slot (2 per CU) a block
   if (halo_on && halo_tbm == 256 && halo_geom(a.H, a.W, a.K, 256, &hg) &&
-      static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) >= wgrad_slots()) {
+      static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) * 10 >= wgrad_slots() * 9) {
     if (a.pool == 2) launch_fwd_halo<256, true>(a, hg, stream); else launch_fwd_halo<256, false>(a, hg, stream);
     return;
   }
