@@ -360,19 +360,28 @@ struct HaloCfg {
   static constexpr int kWinLd = (kMaxRows * 8 + TBM * 2 - 1) / (TBM * 2);  // window pieces per thread
 };
 
-template <int TBM, bool POOL>
-__global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
+// SPLIT: two blocks per output tile, each running half of the 64-channel
+// blocks and writing its fp32 partial tile to ws[tile][half] in fragment
+// order; conv_split_combine_kernel then adds the halves (fixed order) and
+// runs the shared epilogue.  For grids that would leave half the resident
+// slots empty (ResNet-9 res3: 252 tiles on 256 CUs).  (A last-arriver
+// combine inside this kernel needs device-scope release fences -- L2
+// writebacks across the 8 XCDs -- and measured 140 us vs 62 unsplit.)
+template <int TBM, bool POOL, bool SPLIT = false>
+__global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg, float* ws) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int BN = 128, NI = 2, NT = TBM * 2, BLD = BN * 8 / NT;
   constexpr int kHaloWinBytes = HaloCfg<TBM>::kWinBytes, kHaloWinLd = HaloCfg<TBM>::kWinLd;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = SPLIT ? rid >> 1 : rid, half = SPLIT ? rid & 1 : 0;
   const int ntn = a.K / BN;
   const int tn = bid % ntn, tm = bid / ntn;
   const int m0 = tm * TBM, n0 = tn * BN;
   const int C = a.C, H = a.H, W = a.W, HW = H * W;
   const int KT = 9 * (C >> 6);
+  const int s_beg = SPLIT ? half * (KT / 2) : 0, s_end = SPLIT ? s_beg + KT / 2 : KT;
   const int img0 = m0 / HW, h0 = (m0 - img0 * HW) / W;  // first image / row of the tile
   const int nimg = a.P / HW;
   const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_conv_zero);
@@ -451,11 +460,11 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, H
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
 
-  issue_window(0);
-  issue_b(0);
-  for (int s = 0; s < KT; ++s) {
+  issue_window(s_beg / 9);
+  issue_b(s_beg);
+  for (int s = s_beg; s < s_end; ++s) {
     const int tap = s % 9, cb = s / 9;
-    if (tap == 0 && s > 0) {  // every wave is past the old window's reads
+    if (tap == 0 && s > s_beg) {  // every wave is past the old window's reads
       // (staging the next window behind the last tap's MFMAs instead needs
       // all A fragments in registers: 220 VGPRs, measured 6 % slower)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -465,7 +474,7 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, H
     wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + 1 < KT) issue_b(s + 1);
+    if (s + 1 < s_end) issue_b(s + 1);
     const int dsh = (tap / 3 - 1) * hg.PW + (tap % 3 - 1);
     int offA[2];
     int swA[2];
@@ -501,9 +510,43 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, H
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
     }
   }
+  if constexpr (SPLIT) {  // publish the partial tile; conv_split_combine_kernel finishes it
+    float* mine = ws + (static_cast<size_t>(bid) * 2 + half) * (TBM * BN);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) mine[((mi * NI + ni) * 16 + e) * NT + tid] = acc[mi][ni][e];
+    return;
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, m0, n0, tid, wr, wc, hi, lr);
+}
+
+template <int TBM, bool POOL>
+__global__ void __launch_bounds__(TBM * 2) conv_split_combine_kernel(ConvFwdArgs a, const float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int BN = 128, NI = 2, NT = TBM * 2;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int bid = blockIdx.x;
+  const int ntn = a.K / BN;
+  const int tn = bid % ntn, tm = bid / ntn;
+  const float* p0 = ws + static_cast<size_t>(bid) * 2 * (TBM * BN);
+  const float* p1 = p0 + TBM * BN;
+  f32x16_t acc[2][NI];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int o = ((mi * NI + ni) * 16 + e) * NT + tid;
+        acc[mi][ni][e] = __builtin_nontemporal_load(p0 + o) + __builtin_nontemporal_load(p1 + o);
+      }
+  conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, tm * TBM, tn * BN, tid, wr, wc, lane >> 5, lane & 31);
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -1058,17 +1101,38 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g) {
   return g->NPW <= (TBM == 256 ? HaloCfg<256>::kMaxRows : cap);
 }
 
-template <int TBM, bool POOL>
-void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
+template <int TBM, bool POOL, bool SPLIT = false>
+void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream, float* ws = nullptr) {
   constexpr int lds = HaloCfg<TBM>::kLds;
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT>), lds);
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL>), dim3(mt * (a.K / 128)), dim3(TBM * 2), lds, stream,
-                     a, hg);
+  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL, SPLIT>), dim3(mt * (a.K / 128) * (SPLIT ? 2 : 1)),
+                     dim3(TBM * 2), lds, stream, a, hg, ws);
+  if constexpr (SPLIT) {
+    static bool cinit = false;
+    if (!cinit) {
+      set_lds(reinterpret_cast<const void*>(conv_split_combine_kernel<TBM, POOL>), lds);
+      cinit = true;
+    }
+    hipLaunchKernelGGL((conv_split_combine_kernel<TBM, POOL>), dim3(mt * (a.K / 128)), dim3(TBM * 2), lds,
+                       stream, a, static_cast<const float*>(ws));
+  }
+}
+
+// split-K halo workspace: fp32 partial tiles [tiles][2][128 x 128], allocated
+// on the first split launch (eager, before any graph capture).
+constexpr int kSplitMaxTiles = 512;
+static float* split_ws() {
+  static float* w = [] {
+    float* r = nullptr;
+    const size_t bytes = static_cast<size_t>(kSplitMaxTiles) * 2 * 128 * 128 * sizeof(float);
+    return hipMalloc(&r, bytes) == hipSuccess ? r : nullptr;
+  }();
+  return w;
 }
 
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
@@ -1090,6 +1154,19 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
     return;
   }
   if (halo_on && halo_geom(a.H, a.W, a.K, 128, &hg)) {
+    static const bool split_on = [] {  // COMMEFF_CONV_SPLIT=0: one block per tile always
+      const char* e = getenv("COMMEFF_CONV_SPLIT");
+      return !(e != nullptr && e[0] == '0');
+    }();
+    const int64_t tiles = static_cast<int64_t>((a.P + 127) / 128) * (a.K / 128);
+    if (split_on && (a.C / 64) % 2 == 0 && tiles <= kSplitMaxTiles && tiles * 2 <= wgrad_slots()) {
+      float* ws = split_ws();
+      if (ws != nullptr) {
+        if (a.pool == 2) launch_fwd_halo<128, true, true>(a, hg, stream, ws);
+        else launch_fwd_halo<128, false, true>(a, hg, stream, ws);
+        return;
+      }
+    }
     if (a.pool == 2) launch_fwd_halo<128, true>(a, hg, stream); else launch_fwd_halo<128, false>(a, hg, stream);
     return;
   }

@@ -56,6 +56,31 @@ def test_fwd_matches_fp32(N, C, H, W, K, relu):
     _close(y, ref)
 
 
+@pytest.mark.parametrize("N,C,H,W,K,pool", [(500, 512, 4, 4, 512, False),   # ResNet-9 res3
+                                             (64, 256, 8, 8, 128, True)])
+def test_fwd_split_k_halo(N, C, H, W, K, pool):
+    """Grids under half the resident slots run split-K (two blocks per tile,
+    conv.hip SPLIT): fp32-close and bitwise run-to-run deterministic; the
+    residual epilogue (mask + addend) still applies once."""
+    x, w = _inputs(N, C, H, W, K)
+    wf, _ = ops.conv_weight_prep(w)
+    ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
+    if pool:
+        y = cnn.conv3x3_relu_pool(x, w, 2)
+        _close(y, F.max_pool2d(ref.relu(), 2))
+        assert torch.equal(y, cnn.conv3x3_relu_pool(x, w, 2))
+        return
+    y1 = ops.conv3x3_fwd(x, wf, True)
+    y2 = ops.conv3x3_fwd(x, wf, True)
+    _close(y1, ref.relu())
+    assert torch.equal(y1, y2)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    mask = _nhwc(torch.randn(N, K, H, W, device="cuda", generator=g).to(torch.bfloat16))
+    add = _nhwc(torch.randn(N, K, H, W, device="cuda", generator=g).to(torch.bfloat16))
+    y = ops.conv3x3_fwd(x, wf, False, mask, add)
+    _close(y, torch.where(mask.float() > 0, ref, torch.zeros_like(ref)) + add.float())
+
+
 @pytest.mark.parametrize("N,C,H,W,K", SHAPES[:3])
 def test_fwd_mask_and_addend_epilogue(N, C, H, W, K):
     x, w = _inputs(N, C, H, W, K)
