@@ -64,11 +64,13 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Epilogue shared by the conv forward kernels: the fp32 accumulator tile
 // (wave (wr, wc) holds rows wr*64.., columns wc*BN/2..) through LDS, fused
 // ReLU / mask / residual add or ReLU + 2x2 max-pool, 16-byte bf16 stores.
-template <int TBM, int BN, bool POOL>
+// NTE threads take part (tid in [0, NTE)); only threads with own = true hold
+// accumulator fragments (the in-block split-K kernel's second half does not).
+template <int TBM, int BN, bool POOL, int NTE = TBM * 2>
 __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x16_t (&acc)[2][BN / 64],
                                                   unsigned char* smem, int m0, int n0, int tid,
-                                                  int wr, int wc, int hi, int lr) {
-  constexpr int NT = TBM * 2;
+                                                  int wr, int wc, int hi, int lr, bool own = true) {
+  constexpr int NT = NTE;
   constexpr int NI = BN / 64;
   // ---- epilogue: fp32 tile in LDS -> fused ops -> 16-byte bf16 stores
   // (tiles taller than 128 rows go through LDS in 128-row passes)
@@ -79,7 +81,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x16_t
 #pragma unroll 1
   for (int ps = 0; ps < TBM / EPR; ++ps) {
   if (ps > 0) __syncthreads();  // the previous pass has read ct
-  if ((wr * 64) / EPR == ps) {
+  if (own && (wr * 64) / EPR == ps) {
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -360,22 +362,26 @@ struct HaloCfg {
   static constexpr int kWinLd = (kMaxRows * 8 + TBM * 2 - 1) / (TBM * 2);  // window pieces per thread
 };
 
-// SPLIT: two blocks per output tile, each running half of the 64-channel
-// blocks and writing its fp32 partial tile to ws[tile][half] in fragment
-// order; conv_split_combine_kernel then adds the halves (fixed order) and
-// runs the shared epilogue.  For grids that would leave half the resident
-// slots empty (ResNet-9 res3: 252 tiles on 256 CUs).  (A last-arriver
-// combine inside this kernel needs device-scope release fences -- L2
-// writebacks across the 8 XCDs -- and measured 140 us vs 62 unsplit.)
+// SPLIT: one 8-wave block per output tile, two 4-wave groups each running
+// half of the 64-channel blocks in its own LDS window + B ring (2 x 68 KB, 1
+// block/CU).  The second group's partial tile is added to the first's through
+// LDS (fixed order: bitwise deterministic) and all 8 waves run the epilogue.
+// For grids that would leave half the resident slots empty (ResNet-9 res3:
+// 252 tiles on 256 CUs).  (Measured alternatives: two blocks per tile with a
+// last-arriver combine needs device-scope release fences -- L2 writebacks
+// across the 8 XCDs, 140 us vs 62 unsplit; partial tiles through an HBM
+// workspace + a combine kernel: 44 + 12 us.)
 template <int TBM, bool POOL, bool SPLIT = false>
-__global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg, float* ws) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
+  // group g (split-K half) of this block: its own window + B ring
+  const int half = SPLIT ? static_cast<int>(threadIdx.x) / (TBM * 2) : 0;
+  unsigned char* const smem = smem_base + half * HaloCfg<TBM>::kLds;
   constexpr int BN = 128, NI = 2, NT = TBM * 2, BLD = BN * 8 / NT;
   constexpr int kHaloWinBytes = HaloCfg<TBM>::kWinBytes, kHaloWinLd = HaloCfg<TBM>::kWinLd;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x & (NT - 1), lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int rid = xcd_remap(blockIdx.x, gridDim.x);
-  const int bid = SPLIT ? rid >> 1 : rid, half = SPLIT ? rid & 1 : 0;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int ntn = a.K / BN;
   const int tn = bid % ntn, tm = bid / ntn;
   const int m0 = tm * TBM, n0 = tn * BN;
@@ -510,43 +516,36 @@ __global__ void __launch_bounds__(TBM * 2) conv_fwd_halo_kernel(ConvFwdArgs a, H
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
     }
   }
-  if constexpr (SPLIT) {  // publish the partial tile; conv_split_combine_kernel finishes it
-    float* mine = ws + (static_cast<size_t>(bid) * 2 + half) * (TBM * BN);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if constexpr (SPLIT) {
+    // group 1 parks its fragments in group 0's region (read by nobody now);
+    // group 0 adds them lane for lane, then both groups run the epilogue
+    float* red = reinterpret_cast<float*>(smem_base);
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) mine[((mi * NI + ni) * 16 + e) * NT + tid] = acc[mi][ni][e];
-    return;
+        for (int e = 0; e < 16; ++e) {
+          const int o = ((mi * NI + ni) * 16 + e) * NT + tid;
+          if (half == 1) red[o] = acc[mi][ni][e];
+        }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[mi][ni][e] += red[((mi * NI + ni) * 16 + e) * NT + tid];
+    }
+    __syncthreads();  // red is read before the epilogue overwrites the region
+    conv_fwd_epilogue<TBM, BN, POOL, TBM * 4>(a, acc, smem_base, m0, n0, threadIdx.x, wr, wc, hi, lr,
+                                              half == 0);
+  } else {
+    conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, m0, n0, tid, wr, wc, hi, lr);
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, m0, n0, tid, wr, wc, hi, lr);
-}
-
-template <int TBM, bool POOL>
-__global__ void __launch_bounds__(TBM * 2) conv_split_combine_kernel(ConvFwdArgs a, const float* __restrict__ ws) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int BN = 128, NI = 2, NT = TBM * 2;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int bid = blockIdx.x;
-  const int ntn = a.K / BN;
-  const int tn = bid % ntn, tm = bid / ntn;
-  const float* p0 = ws + static_cast<size_t>(bid) * 2 * (TBM * BN);
-  const float* p1 = p0 + TBM * BN;
-  f32x16_t acc[2][NI];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int o = ((mi * NI + ni) * 16 + e) * NT + tid;
-        acc[mi][ni][e] = __builtin_nontemporal_load(p0 + o) + __builtin_nontemporal_load(p1 + o);
-      }
-  conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, tm * TBM, tn * BN, tid, wr, wc, lane >> 5, lane & 31);
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -1102,37 +1101,16 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g) {
 }
 
 template <int TBM, bool POOL, bool SPLIT = false>
-void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream, float* ws = nullptr) {
-  constexpr int lds = HaloCfg<TBM>::kLds;
+void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
+  constexpr int lds = HaloCfg<TBM>::kLds * (SPLIT ? 2 : 1);
   static bool init = false;
   if (!init) {
     set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT>), lds);
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL, SPLIT>), dim3(mt * (a.K / 128) * (SPLIT ? 2 : 1)),
-                     dim3(TBM * 2), lds, stream, a, hg, ws);
-  if constexpr (SPLIT) {
-    static bool cinit = false;
-    if (!cinit) {
-      set_lds(reinterpret_cast<const void*>(conv_split_combine_kernel<TBM, POOL>), lds);
-      cinit = true;
-    }
-    hipLaunchKernelGGL((conv_split_combine_kernel<TBM, POOL>), dim3(mt * (a.K / 128)), dim3(TBM * 2), lds,
-                       stream, a, static_cast<const float*>(ws));
-  }
-}
-
-// split-K halo workspace: fp32 partial tiles [tiles][2][128 x 128], allocated
-// on the first split launch (eager, before any graph capture).
-constexpr int kSplitMaxTiles = 512;
-static float* split_ws() {
-  static float* w = [] {
-    float* r = nullptr;
-    const size_t bytes = static_cast<size_t>(kSplitMaxTiles) * 2 * 128 * 128 * sizeof(float);
-    return hipMalloc(&r, bytes) == hipSuccess ? r : nullptr;
-  }();
-  return w;
+  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL, SPLIT>), dim3(mt * (a.K / 128)),
+                     dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
 }
 
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
@@ -1159,13 +1137,9 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
       return !(e != nullptr && e[0] == '0');
     }();
     const int64_t tiles = static_cast<int64_t>((a.P + 127) / 128) * (a.K / 128);
-    if (split_on && (a.C / 64) % 2 == 0 && tiles <= kSplitMaxTiles && tiles * 2 <= wgrad_slots()) {
-      float* ws = split_ws();
-      if (ws != nullptr) {
-        if (a.pool == 2) launch_fwd_halo<128, true, true>(a, hg, stream, ws);
-        else launch_fwd_halo<128, false, true>(a, hg, stream, ws);
-        return;
-      }
+    if (split_on && (a.C / 64) % 2 == 0 && tiles * 2 <= wgrad_slots()) {
+      if (a.pool == 2) launch_fwd_halo<128, true, true>(a, hg, stream); else launch_fwd_halo<128, false, true>(a, hg, stream);
+      return;
     }
     if (a.pool == 2) launch_fwd_halo<128, true>(a, hg, stream); else launch_fwd_halo<128, false>(a, hg, stream);
     return;
