@@ -26,7 +26,7 @@ import time
 import numpy as np
 import torch
 
-import commefficient_amd  # noqa: F401  (sets HIP runtime env before the GPU initialises)
+import commefficient_amd
 
 METRIC = "images/sec + bytes/step, ResNet-9 CIFAR-10 FetchSGD at 1/2/4/8 MI355X"
 
@@ -51,6 +51,8 @@ def main():
                    help="torch.backends.cudnn.benchmark (MIOpen exhaustive find during warmup)")
     b = p.parse_args()
 
+    if b.graph != "off":
+        commefficient_amd.request_graph_replay()  # must precede HIP initialisation
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != b.gpus:
         if b.gpus > 1 and world == 1:

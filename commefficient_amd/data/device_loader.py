@@ -80,19 +80,33 @@ class DeviceFedLoader:
                                         out_bf16=out_bf16)
         self.seed = seed
         self._round = 0
+        self.epoch = 0  # epochs started (the next __iter__ runs epoch ``self.epoch``)
 
     def __len__(self):
         return len(self.dataset)
 
     def __iter__(self) -> Iterator[RoundBatch]:
+        ep = self.epoch
+        self.epoch += 1
         for r in self.sampler:
             cids = self.dataset.client_of(r)
             rows = self.dataset.data_index(r)
-            yield self.make_batch(cids, rows)
+            # augmentation keyed by (epoch, round in epoch): a resumed run
+            # (FedSampler skip) reproduces the same pixels
+            yield self.make_batch(cids, rows, key=(ep << 24) + self.sampler.pos - 1)
 
-    def make_batch(self, cids, rows) -> RoundBatch:
-        rnd_seed = (self.seed * 1000003 + self._round) & 0x7FFFFFFFFFFF
-        self._round += 1
+    def state_dict(self, pos=None):
+        return {"sampler": self.sampler.state_dict(pos), "epoch": max(0, self.epoch - 1)}
+
+    def load_state_dict(self, sd):
+        self.sampler.load_state_dict(sd["sampler"])
+        self.epoch = int(sd["epoch"])
+
+    def make_batch(self, cids, rows, key=None) -> RoundBatch:
+        if key is None:
+            key = self._round
+            self._round += 1
+        rnd_seed = (self.seed * 1000003 + key) & 0x7FFFFFFFFFFF
         src = self.source
 
         def take(pos, rows=rows, seed=rnd_seed):

@@ -137,7 +137,14 @@ class FedDataset(torch.utils.data.Dataset):
 
 
 class FedSampler:
-    """batch_sampler yielding index arrays, one federated round per batch."""
+    """batch_sampler yielding index arrays, one federated round per batch
+    (/root/reference/CommEfficient/data_utils/fed_sampler.py:5-71).
+
+    Resumable: ``state_dict()`` holds the RNG state at the start of the
+    current epoch and ``pos`` (rounds drawn so far in it); after
+    ``load_state_dict`` the next epoch replays the same draws and skips the
+    first ``pos`` rounds, so a resumed run sees exactly the rounds it would
+    have seen."""
 
     def __init__(self, dataset: FedDataset, num_workers: int, local_batch_size: int,
                  shuffle_clients: bool = True, seed: Optional[int] = None):
@@ -147,9 +154,15 @@ class FedSampler:
         self.shuffle_clients = shuffle_clients
         # an explicit RandomState makes every rank draw the same client sets
         self.rng = np.random.RandomState(seed) if seed is not None else np.random
+        self.pos = 0  # rounds drawn in the current epoch
+        self._epoch_state = None
+        self._skip = 0
 
     def __iter__(self):
         rng = self.rng
+        self._epoch_state = rng.get_state()
+        self.pos = 0
+        skip, self._skip = self._skip, 0
         dpc = self.dataset.data_per_client
         cumsum = np.hstack([[0], np.cumsum(dpc)])
         permuted = np.hstack([s + rng.permutation(u) for s, u in zip(cumsum, dpc)]).astype(np.int64)
@@ -166,9 +179,28 @@ class FedSampler:
             else:
                 sizes = np.clip(remaining, 0, self.local_batch_size)
             starts = cumsum[workers] + cur[workers]
-            r = np.concatenate([permuted[s:s + n] for s, n in zip(starts, sizes)])
-            yield r
+            self.pos += 1
+            if self.pos > skip:
+                r = np.concatenate([permuted[s:s + n] for s, n in zip(starts, sizes)])
+                yield r
             cur[workers] += sizes
+
+    def state_dict(self, pos: Optional[int] = None):
+        """RNG state at the start of the current epoch + rounds consumed
+        (``pos``: override, e.g. the rounds the driver actually processed)."""
+        pos = self.pos if pos is None else pos
+        # pos 0 = between epochs: the next epoch starts from the current state
+        st = self._epoch_state if (pos > 0 and self._epoch_state is not None) \
+            else self.rng.get_state()
+        return {"keys": torch.from_numpy(np.asarray(st[1], dtype=np.int64)),
+                "rng_pos": int(st[2]), "has_gauss": int(st[3]), "gauss": float(st[4]),
+                "pos": int(pos)}
+
+    def load_state_dict(self, sd):
+        keys = sd["keys"].numpy().astype(np.uint32)
+        self.rng.set_state(("MT19937", keys, int(sd["rng_pos"]), int(sd["has_gauss"]),
+                            float(sd["gauss"])))
+        self._skip = int(sd["pos"])
 
     def __len__(self):
         return len(self.dataset)

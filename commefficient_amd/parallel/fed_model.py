@@ -27,6 +27,7 @@ one process per MI355X:
 """
 from __future__ import annotations
 
+import inspect
 import math
 import os
 from contextlib import nullcontext
@@ -92,6 +93,13 @@ def as_round_batch(batch, device) -> RoundBatch:
     return RoundBatch(cids, take, n_inputs=len(rest) - 1)
 
 
+def _accepts_groups(fn) -> bool:
+    try:
+        return "groups" in inspect.signature(fn).parameters
+    except (TypeError, ValueError):
+        return False
+
+
 class FedModel:
     def __init__(self, input_model: nn.Module, compute_loss, args, compute_loss_val=None,
                  num_clients: Optional[int] = None):
@@ -102,6 +110,10 @@ class FedModel:
         self.model = input_model
         self.compute_loss_train = compute_loss
         self.compute_loss_val = compute_loss_val or compute_loss
+        # losses that normalise over a client's whole batch (the GPT-2 LM term is
+        # a token-weighted mean, gpt2_train.py:88-99) take the per-example
+        # client slot of a merged batch as ``groups=``
+        self._loss_groups = _accepts_groups(compute_loss)
         if num_clients is None:
             num_clients = args.num_clients
         if num_clients is None:
@@ -248,17 +260,22 @@ class FedModel:
         return clients[R * W // N:(R + 1) * W // N]
 
     def _fwd_bwd(self, inputs, targets, loss_weight: Optional[float], groups: int = 1,
-                 want_grad=True, capture: bool = False):
+                 want_grad=True, capture: bool = False, ex_groups=None):
         """Forward (+backward) of one (micro)batch.  ``loss_weight`` None ->
         backward of the SUM of per-example losses; else of
-        ``loss_weight * sum`` (per-client mean normalisation).  Returns the
-        per-example losses and metrics (detached)."""
+        ``loss_weight * sum`` (per-client mean normalisation).  ``ex_groups``:
+        per-example client slot (merged batches) for losses that normalise per
+        client.  Returns the per-example losses and metrics (detached)."""
         with self._autocast(cache=not capture):
             with (ghost_batchnorm(self.model, groups) if (groups > 1 and self.has_bn)
                   else nullcontext()):
-                per_ex, metrics = self.compute_loss_train(self.model, self._prep(inputs), targets,
-                                                          self.args) if want_grad else \
-                    self.compute_loss_val(self.model, self._prep(inputs), targets, self.args)
+                if want_grad:
+                    kw = {"groups": ex_groups} if self._loss_groups else {}
+                    per_ex, metrics = self.compute_loss_train(
+                        self.model, self._prep(inputs), targets, self.args, **kw)
+                else:
+                    per_ex, metrics = self.compute_loss_val(self.model, self._prep(inputs),
+                                                            targets, self.args)
         if want_grad:
             if (loss_weight is None and not capture and per_ex.dtype == torch.float32
                     and per_ex.dim() == 1):
@@ -291,8 +308,14 @@ class FedModel:
         self.model.train()
         merged = self.mergeable and len(mine) > 0
         if merged and self.has_bn:
+            # ghost BN keeps per-client statistics only when every client has
+            # the same size and microbatches hold whole clients; otherwise the
+            # groups would straddle clients -> per-client path
             sizes = counts[my_slots]
             merged = bool(np.all(sizes == sizes[0]))
+            mbs = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else 0
+            if merged and 0 < mbs < int(sizes.sum()) and mbs % int(sizes[0]) != 0:
+                merged = False
         if merged and self.graphs is not None:
             n_local = int(counts[my_slots].sum())
             if self.graphs.usable(rb, n_local):
@@ -425,6 +448,11 @@ class FedModel:
         else:
             data = rb.take(pos)
         inputs, targets = data[:-1], data[-1]
+        if packed is not None:
+            slots_t, n_t = packed[1], packed[2]
+        else:
+            slots_t = dist.h2d(slot_per_ex, self.device)
+            n_t = dist.h2d(counts.astype(np.float32), self.device)
         mb = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else n_local
         groups_total = len(my_slots)
         per_ex_all, metrics_all = [], []
@@ -432,9 +460,11 @@ class FedModel:
             e = min(n_local, s + mb)
             xi = tuple(x[s:e] for x in inputs)
             # ghost-BN groups: client boundaries align with microbatches only
-            # when mb is a multiple of the (equal) client size
+            # when mb is a multiple of the (equal) client size (``mergeable``
+            # falls back to the per-client path otherwise)
             g = groups_total if mb >= n_local else max(1, (e - s) // max(1, counts[my_slots[0]]))
-            pe, ms = self._fwd_bwd(xi, targets[s:e], None, groups=g)
+            pe, ms = self._fwd_bwd(xi, targets[s:e], None, groups=g,
+                                   ex_groups=slots_t[s:e] if self._loss_groups else None)
             per_ex_all.append(pe)
             metrics_all.append(ms)
         if len(per_ex_all) == 1:  # one microbatch: no concatenation copies
@@ -444,11 +474,6 @@ class FedModel:
             mets = [torch.cat([m[i] for m in metrics_all]) for i in range(len(metrics_all[0]))] \
                 if metrics_all else []
         # per-client mean metrics into their global slots
-        if packed is not None:
-            slots_t, n_t = packed[1], packed[2]
-        else:
-            slots_t = dist.h2d(slot_per_ex, self.device)
-            n_t = dist.h2d(counts.astype(np.float32), self.device)
         rows = [per_ex] + mets
         tail = self._payload_buf(len(rows) * W)[self.main_numel:].view(len(rows), W)
         msum = self._metric_sums(rows, slots_t, n_t, W, out=tail)
@@ -628,6 +653,14 @@ class FedModel:
 
     # -------------------------------------------------------------- server
     def server_step(self, lr):
+        if self.args.mode == "fedavg":
+            # FedOptimizer.step writes g_lr before anything else
+            # (fed_aggregator.py:441-444), so the reference's "HACK STEP"
+            # (cv_train.py:198-203: lr == 0, no round pending) still sets the
+            # LR the next round's local SGD uses.
+            if torch.is_tensor(lr):
+                raise ValueError("fedavg supports a scalar LR only (fed_aggregator.py:441-444)")
+            self.fedavg_lr = float(lr)
         if self._pending is None:
             return  # e.g. the reference's "HACK STEP" before the first round
         G, clients, via_graph, gscale = self._pending
@@ -638,10 +671,6 @@ class FedModel:
             self.graphs.server(G, float(lr), self.round_idx)
             self.round_idx += 1
             return
-        if self.args.mode == "fedavg":
-            if torch.is_tensor(lr):
-                raise ValueError("fedavg supports a scalar LR only (fed_aggregator.py:441-444)")
-            self.fedavg_lr = float(lr)
         with self.timer.phase("server"):
             self.server.update(G, lr, self.w, self.accountant.last_mod, self.round_idx,
                                self.client_state, clients,
@@ -680,7 +709,9 @@ class FedModel:
     def fed_state_dict(self):
         return {"round_idx": self.round_idx, "fedavg_lr": self.fedavg_lr,
                 "server": self.server.state_dict(), "accountant": self.accountant.state_dict(),
-                "client_state": self.client_state.state_dict(), "w": self.w.cpu()}
+                "client_state": self.client_state.state_dict(), "w": self.w.cpu(),
+                # BatchNorm running statistics etc. (not part of the flat weights)
+                "buffers": {n: b.detach().cpu() for n, b in self.model.named_buffers()}}
 
     def load_fed_state_dict(self, sd):
         self.round_idx = int(sd["round_idx"])
@@ -689,3 +720,7 @@ class FedModel:
         self.accountant.load_state_dict(sd["accountant"])
         self.client_state.load_state_dict(sd["client_state"])
         self.w.copy_(sd["w"])
+        bufs = dict(self.model.named_buffers())
+        for n, b in sd.get("buffers", {}).items():
+            if n in bufs:
+                bufs[n].copy_(b)

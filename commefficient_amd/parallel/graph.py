@@ -27,8 +27,9 @@ instantiation, the default in ROCm 7.2) the SECOND launch of the compute
 graph at the ResNet-9 bench geometry raises a memory-access fault, although
 the first launch is bitwise identical to the eager round
 (scripts/dev/graph_cmp.py); with DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 (set by
-``commefficient_amd/__init__.py`` before HIP initialises) every replay is
-correct.  Graphs are therefore only used when that variable is 0.
+``commefficient_amd.request_graph_replay()`` when ``--graph`` is requested,
+before HIP initialises) every replay is correct.  Graphs are therefore only
+used when that variable is 0.
 
 Measured (1x MI355X, bench.py, 50 rounds): 176.9k img/s replayed vs 176.5k
 eager, host enqueue 2.44 vs 2.39 ms/round -- without packet capture the

@@ -184,11 +184,16 @@ class ByteAccountant:
         return dl, float(self.upload_per_client) * W
 
     def state_dict(self):
-        return {"last_mod": self.last_mod.cpu(), "last_seen": torch.from_numpy(self.last_seen)}
+        return {"last_mod": self.last_mod.cpu(), "last_seen": torch.from_numpy(self.last_seen),
+                "client_download": self.client_download.cpu(),
+                "client_upload": self.client_upload.cpu()}
 
     def load_state_dict(self, sd):
         self.last_mod.copy_(sd["last_mod"])
         self.last_seen = sd["last_seen"].numpy().astype(np.int64)
+        if "client_download" in sd:
+            self.client_download.copy_(sd["client_download"])
+            self.client_upload.copy_(sd["client_upload"])
         top = int(self.last_mod.max().item()) if self.d else -1
         cap = self.HIST_CAP
         while top + 2 > cap:

@@ -116,7 +116,7 @@ class _Done:
 
 
 def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args, nan_check=None,
-                profiler=None):
+                profiler=None, progress=None):
     if not training and epoch_fraction != 1:
         raise ValueError("Must do full epochs for val")
     model.train(training)
@@ -126,11 +126,19 @@ def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args
     if training:
         spe = steps_per_epoch(args.local_batch_size, ds, args.num_workers)
         t0 = time.time()
-        for i, batch in enumerate(loader):
+        # resumed mid-epoch: the sampler skips the rounds already processed
+        start = progress["iter"] if progress is not None else 0
+        if progress is not None:
+            progress["epoch_done"] = True
+        for i, batch in enumerate(loader, start=start):
             if i >= spe * epoch_fraction:
                 break
             if args.max_rounds and model.round_idx >= args.max_rounds:
+                if progress is not None:
+                    progress["epoch_done"] = False
                 break
+            if progress is not None:
+                progress["iter"] = i + 1  # loader rounds consumed in this epoch
             lr_scheduler.step()
             if lr_scheduler.get_last_lr()[0] == 0:
                 opt.step()  # reference "HACK STEP": no pending round -> only sets fedavg LR
@@ -147,6 +155,8 @@ def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args
             loss, acc, _dl, _ul = model(batch)
             if nan_check is not None and nan_check.push(loss):
                 print("LOSS IS NAN, TERMINATING TRAINING")
+                if progress is not None:
+                    progress["nan"] = True
                 return float("nan"), float("nan")
             opt.step()
             if profiler is not None:
@@ -154,12 +164,17 @@ def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args
             losses.append(loss)
             accs.append(acc)
             rounds += 1
+            if (args.checkpoint_every and progress is not None
+                    and model.round_idx % args.checkpoint_every == 0):
+                save_checkpoint(model, args, progress)
             if args.log_every and rounds % args.log_every == 0 and dist.ctx().is_main:
                 print("round {} lr {:.5f} loss {:.4f} acc {:.4f} ({:.1f} rounds/s)".format(
                     model.round_idx, lr_scheduler.get_last_lr()[0], loss.mean().item(),
                     acc.mean().item(), rounds / (time.time() - t0)))
             if args.do_test:
                 break
+        if progress is not None:
+            progress["rounds"] = rounds
     else:
         for batch in loader:
             if len(batch) < args.valid_batch_size:
@@ -176,8 +191,14 @@ def run_batches(model, opt, lr_scheduler, loader, training, epoch_fraction, args
 
 
 def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, loggers=(),
-          timer=None):
+          timer=None, progress=None):
+    """``progress``: {"epoch", "iter", "loader", "sched"} -- where training
+    stands (restored by --resume, saved in the .fedstate.pt sidecar)."""
     timer = timer or Timer()
+    if progress is None:
+        progress = {"epoch": 0, "iter": 0}
+    progress["loader"] = train_loader
+    progress["sched"] = lr_scheduler
     ctx = dist.ctx()
     nan_check = LagNaNCheck(model.device)
     profiler = RoundProfiler(getattr(args, "profile_dir", None), ctx.rank,
@@ -190,13 +211,15 @@ def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, log
         timer()
         if ctx.is_main:
             print("Test acc at epoch 0: {:0.4f}".format(test_acc))
-    for epoch in range(math.ceil(args.num_epochs)):
+    for epoch in range(progress["epoch"], math.ceil(args.num_epochs)):
+        if epoch != progress["epoch"]:
+            progress["epoch"], progress["iter"] = epoch, 0
         frac = args.num_epochs - epoch if epoch == math.ceil(args.num_epochs) - 1 else 1
         d0 = acct.client_download.sum().item()
         u0 = acct.client_upload.sum().item()
         train_loss, train_acc = run_batches(model, opt, lr_scheduler, train_loader, True, frac,
-                                            args, nan_check, profiler)
-        if math.isnan(train_loss):
+                                            args, nan_check, profiler, progress)
+        if progress.get("nan") or (math.isnan(train_loss) and progress.get("rounds", 0) > 0):
             print("TERMINATING TRAINING DUE TO NAN LOSS")
             return summary
         train_time = timer()
@@ -220,6 +243,8 @@ def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, log
                                ("Time/train", train_time), ("Time/test", test_time),
                                ("Time/total", timer.total_time), ("Lr", lr)):
                     writer.add_scalar(tag, v, epoch)
+        if progress.get("epoch_done", True):
+            progress["epoch"], progress["iter"] = epoch + 1, 0  # epoch complete
         if args.max_rounds and model.round_idx >= args.max_rounds:
             break
     profiler.close(model.timer)
@@ -232,7 +257,41 @@ def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, log
     return summary
 
 
-def save_checkpoint(model: FedModel, args):
+def driver_state(progress) -> dict:
+    """Epoch / in-epoch position, sampler RNG and LR-schedule step."""
+    if not progress:
+        return {}
+    out = {"epoch": int(progress["epoch"]), "iter": int(progress["iter"])}
+    ld = progress.get("loader")
+    if ld is not None and hasattr(ld, "state_dict"):
+        out["loader"] = ld.state_dict(pos=progress["iter"])
+        out["loader"]["epoch"] = int(progress["epoch"])
+    elif ld is not None and hasattr(getattr(ld, "batch_sampler", None), "state_dict"):
+        out["loader"] = {"sampler": ld.batch_sampler.state_dict(pos=progress["iter"]),
+                         "epoch": int(progress["epoch"])}
+    sch = progress.get("sched")
+    if sch is not None:
+        out["sched_steps"] = int(sch.last_epoch)
+    return out
+
+
+def restore_driver_state(sd: dict, loader, sched) -> dict:
+    """Inverse of ``driver_state``: position the sampler and the schedule."""
+    drv = sd.get("driver") or {}
+    progress = {"epoch": int(drv.get("epoch", 0)), "iter": int(drv.get("iter", 0))}
+    ls = drv.get("loader")
+    if ls is not None:
+        if hasattr(loader, "load_state_dict"):
+            loader.load_state_dict(ls)
+        elif hasattr(getattr(loader, "batch_sampler", None), "load_state_dict"):
+            loader.batch_sampler.load_state_dict(ls["sampler"])
+    if "sched_steps" in drv:
+        while sched.last_epoch < drv["sched_steps"]:
+            sched.step()
+    return progress
+
+
+def save_checkpoint(model: FedModel, args, progress=None):
     if not dist.ctx().is_main:
         return
     path = args.checkpoint_path + args.model + ".pt"
@@ -240,7 +299,9 @@ def save_checkpoint(model: FedModel, args):
     if d:
         os.makedirs(d, exist_ok=True)
     torch.save(model.state_dict(), path)
-    torch.save(model.fed_state_dict(), args.checkpoint_path + args.model + ".fedstate.pt")
+    fs = model.fed_state_dict()
+    fs["driver"] = driver_state(progress)
+    torch.save(fs, args.checkpoint_path + args.model + ".fedstate.pt")
     print("saved", path)
 
 
@@ -269,20 +330,21 @@ def main(args):
     if args.lr_scale is None:
         args.lr_scale = 0.4
     sched = torch.optim.lr_scheduler.LambdaLR(fopt, lr_lambda=triangular_lambda(args, spe))
+    progress = None
     if args.resume:
         sd = torch.load(args.resume, map_location="cpu", weights_only=True)
         fed.load_fed_state_dict(sd)
-        for _ in range(fed.round_idx):
-            sched.step()
+        progress = restore_driver_state(sd, train_loader, sched)
     log_dir = make_logdir(args)
     writer = ScalarWriter(log_dir) if (args.use_tensorboard and ctx.is_main) else None
     if ctx.is_main:
         print("Finished initializing in {:.2f} seconds".format(timer()))
+    progress = progress or {"epoch": 0, "iter": 0}
     train(fed, fopt, sched, train_loader, test_loader, args, writer, loggers=(TableLogger(),),
-          timer=timer)
+          timer=timer, progress=progress)
     fed.finalize()
     if args.do_checkpoint:
-        save_checkpoint(fed, args)
+        save_checkpoint(fed, args, progress)
     if writer is not None:
         writer.close()
     if fed.timer.enabled and ctx.is_main:

@@ -27,10 +27,16 @@ def cv_loss(model, inputs, targets, args):
     return per_ex, [correct]
 
 
-def gpt2_loss_train(model, inputs, targets, args):
+def gpt2_loss_train(model, inputs, targets, args, groups=None):
     """inputs = (input_ids[B,C,L], mc_token_ids[B,C], lm_labels[B,C,L], token_type_ids[B,C,L]),
-    targets = mc_labels[B].  Per-example lm_coef*lm + mc_coef*mc
-    (gpt2_train.py:88-99; lm loss averaged over each example's labelled tokens)."""
+    targets = mc_labels[B].  Per-example ``lm_coef*lm + mc_coef*mc`` whose mean
+    over a client's examples is the reference objective (gpt2_train.py:88-99):
+    HF's lm loss is ONE token-weighted mean over every labelled token of the
+    client's (micro)batch, so example e carries ``n_g * tokloss_e / ntok_g``
+    (n_g examples and ntok_g labelled tokens of its client g in this call).
+    ``groups``: per-example client slot of a merged multi-client batch (None:
+    one client).  With --microbatch_size the token mean is per microbatch, as
+    in the reference (fed_worker.py:266-287)."""
     input_ids, mc_token_ids, lm_labels, token_type_ids = inputs
     m = model.model if hasattr(model, "model") and not hasattr(model, "transformer") else model
     out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids)
@@ -41,10 +47,27 @@ def gpt2_loss_train(model, inputs, targets, args):
     tok = F.cross_entropy(shift_logits.reshape(-1, shift_logits.size(-1)), shift_labels.reshape(-1),
                           ignore_index=-100, reduction="none").view(B, -1)
     mask = (shift_labels.reshape(B, -1) != -100).float()
-    lm = (tok * mask).sum(1) / mask.sum(1).clamp_min(1.0)
+    tok_sum = (tok * mask).sum(1)
+    ntok = mask.sum(1)
+    lm = token_weighted(tok_sum, ntok, groups)
     mc = F.cross_entropy(mc_logits.float(), targets, reduction="none")
     acc = (mc_logits.argmax(-1) == targets).float()
     return args.lm_coef * lm + args.mc_coef * mc, [acc]
+
+
+def token_weighted(tok_sum: torch.Tensor, ntok: torch.Tensor, groups=None) -> torch.Tensor:
+    """Per-example terms whose per-group MEAN is sum(tok_sum)/sum(ntok) of the group."""
+    B = tok_sum.shape[0]
+    if groups is None:
+        return tok_sum * (B / ntok.sum().clamp_min(1.0))
+    # a client's examples are contiguous: local ids 0.. by run (no host sync)
+    g = groups.long()
+    g = torch.cat([g.new_zeros(1), (g[1:] != g[:-1]).long()]).cumsum(0) if B else g
+    ng = torch.zeros(max(B, 1), device=tok_sum.device)
+    tg = torch.zeros_like(ng)
+    ng.index_add_(0, g, torch.ones_like(ntok))
+    tg.index_add_(0, g, ntok.detach())
+    return tok_sum * (ng[g] / tg[g].clamp_min(1.0))
 
 
 def gpt2_loss_val(model, inputs, targets, args):

@@ -142,6 +142,8 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="where per-client momentum/error/weights live")
     g.add_argument("--resume", type=str, default=None,
                    help="resume from a *.fedstate.pt sidecar written with --checkpoint")
+    g.add_argument("--checkpoint_every", type=int, default=0,
+                   help="also write the checkpoint + resume sidecar every N rounds")
     g.add_argument("--log_every", type=int, default=0,
                    help="print a progress line every N rounds (0: per epoch only)")
     g.add_argument("--max_rounds", type=int, default=0,
@@ -219,4 +221,7 @@ def finalize_args(args, probe_port: bool = True):
         while is_port_in_use(args.port):
             args.port += int(rng.randint(1, 1000))
     validate_args(args)
+    if getattr(args, "graph", "off") != "off" and args.device != "cpu":
+        from .. import request_graph_replay
+        request_graph_replay()  # before the HIP runtime initialises
     return args

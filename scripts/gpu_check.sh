@@ -25,7 +25,7 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     build) run build 300 python -m commefficient_amd.build ;;
-    tests) run pytest_gpu 900 python -m pytest tests/ -x -q -m gpu ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests/ -x -v -m gpu --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps ${BENCH_STEPS:-30} --warmup 5 ;;
     benchprof) run bench_prof 600 python bench.py --steps 20 --warmup 5 --profile ;;

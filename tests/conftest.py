@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
-import commefficient_amd  # noqa: E402,F401  (HIP runtime env, before any GPU call)
+import commefficient_amd  # noqa: E402,F401
 
 
 def pytest_configure(config):

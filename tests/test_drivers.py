@@ -74,3 +74,26 @@ def test_gpt2_driver_tiny_synthetic(tmp_path, monkeypatch):
     fed = fed_train.main(argv)
     assert fed.round_idx == 2
     assert torch.isfinite(fed.w).all()
+
+
+@pytest.mark.parametrize("stop", [3, 5])
+def test_resume_reproduces_uninterrupted_run(stop, tmp_path, monkeypatch):
+    """Checkpoint after ``stop`` rounds (mid-epoch: 3; epoch boundary: 5 of
+    5 rounds/epoch), resume, finish: the weights, server state and byte totals
+    equal those of one uninterrupted run (sampler position, augmentation keys,
+    LR schedule and accounting all restored)."""
+    monkeypatch.chdir(tmp_path)
+    base = ["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", "40",
+            "--num_clients", "20", "--num_workers", "4", "--local_batch_size", "2",
+            "--device", "cpu", "--dtype", "fp32", "--num_epochs", "2", "--valid_batch_size", "16",
+            "--port", "29613", "--mode", "true_topk", "--error_type", "virtual",
+            "--local_momentum", "0", "--virtual_momentum", "0.9", "--k", "5000",
+            "--lr_scale", "0.1", "--pivot_epoch", "1"]
+    full = fed_train.main(base + ["--max_rounds", "8"])
+    ck = str(tmp_path / "ck") + os.sep
+    fed_train.main(base + ["--max_rounds", str(stop), "--checkpoint", "--checkpoint_path", ck])
+    res = fed_train.main(base + ["--max_rounds", "8", "--resume", ck + "ResNet9.fedstate.pt"])
+    assert res.round_idx == full.round_idx == 8
+    torch.testing.assert_close(res.w, full.w, rtol=0, atol=0)
+    torch.testing.assert_close(res.server.V, full.server.V, rtol=0, atol=0)
+    torch.testing.assert_close(res.accountant.client_download, full.accountant.client_download)

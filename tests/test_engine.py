@@ -220,3 +220,27 @@ def test_checkpoint_state_dict_format(tmp_path):
     fed2.load_fed_state_dict(fs2)
     torch.testing.assert_close(fed2.w, fed.w)
     assert fed2.round_idx == 1
+
+
+def test_fedavg_hack_step_sets_lr_without_pending_round():
+    """cv_train.py:198-203 'HACK STEP': with no round pending, FedOptimizer.step
+    still writes g_lr (fed_aggregator.py:441-444).  When the schedule reaches
+    lr=0, the next round's local SGD must run at lr 0 (no weight change apart
+    from the server momentum V)."""
+    fed, opt, args = make_engine(4, ["--mode", "fedavg", "--virtual_momentum", "0",
+                                     "--local_momentum", "0", "--local_batch_size", "-1",
+                                     "--num_workers", "2"], 2, 0.3)
+    X, y = data(8, 4)
+    cids = split(8, 2)
+    opt.step()  # hack step before the first round: sets the LR only
+    assert fed.fedavg_lr == pytest.approx(0.3)
+    fed((cids, X, y))
+    opt.step()
+    w1 = fed.w.clone()
+    assert (w1 != 0).any()
+    opt.param_groups[0]["lr"] = 0.0
+    opt.step()  # no round pending: hack step with lr 0
+    assert fed.fedavg_lr == 0.0
+    fed((cids, X, y))
+    opt.step()
+    torch.testing.assert_close(fed.w, w1)
