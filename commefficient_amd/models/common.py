@@ -7,7 +7,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import ghost_batch_norm, ghost_bn_native_ok
+from ..ops.nn import conv2d_native, conv2d_native_kind, ghost_batch_norm, ghost_bn_native_ok
 
 
 class Mul(nn.Module):
@@ -124,9 +124,24 @@ def has_batchnorm(model: nn.Module) -> bool:
     return any(isinstance(m, nn.modules.batchnorm._BatchNorm) for m in model.modules())
 
 
+class NativeConv2d(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters / state_dict keys) whose bias-free 1x1
+    and stride-1 3x3 convolutions of bf16 channels_last activations run on
+    hipBLASLt GEMMs / the native MFMA kernels (ops/nn.py ``conv2d_native``);
+    every other case is the stock (MIOpen) convolution."""
+
+    def forward(self, x):
+        if self.bias is None and self.padding_mode == "zeros":
+            kind = conv2d_native_kind(x, self.weight, self.stride, self.padding, self.dilation,
+                                      self.groups)
+            if kind:
+                return conv2d_native(x, self.weight, kind, self.stride[0])
+        return super().forward(x)
+
+
 def conv3x3(c_in, c_out, stride=1):
-    return nn.Conv2d(c_in, c_out, kernel_size=3, stride=stride, padding=1, bias=False)
+    return NativeConv2d(c_in, c_out, kernel_size=3, stride=stride, padding=1, bias=False)
 
 
 def conv1x1(c_in, c_out, stride=1):
-    return nn.Conv2d(c_in, c_out, kernel_size=1, stride=stride, bias=False)
+    return NativeConv2d(c_in, c_out, kernel_size=1, stride=stride, bias=False)

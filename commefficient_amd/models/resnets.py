@@ -17,7 +17,7 @@ import math
 import torch
 import torch.nn as nn
 
-from .common import GhostBatchNorm2d, conv1x1, conv3x3
+from .common import GhostBatchNorm2d, NativeConv2d, conv1x1, conv3x3
 
 __all__ = ["ResNet", "ResNet101", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152",
            "resnext50_32x4d", "resnext101_32x8d", "wide_resnet50_2", "wide_resnet101_2"]
@@ -72,8 +72,8 @@ class Bottleneck(nn.Module):
         out_hw = math.ceil(hw / stride)
         self.conv1 = conv1x1(inplanes, width)
         self.bn1 = _norm(norm, width, hw, relu=True)
-        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=dilation, groups=groups,
-                               bias=False, dilation=dilation)
+        self.conv2 = NativeConv2d(width, width, 3, stride=stride, padding=dilation,
+                                  groups=groups, bias=False, dilation=dilation)
         self.bn2 = _norm(norm, width, out_hw, relu=True)
         self.conv3 = conv1x1(width, planes * self.expansion)
         self.bn3 = _norm(norm, planes * self.expansion, out_hw)

@@ -379,3 +379,158 @@ def cross_entropy_correct(logits: torch.Tensor, targets: torch.Tensor):
         return _FusedCE.apply(logits, targets)
     per_ex = F.cross_entropy(logits.float(), targets, reduction="none")
     return per_ex, (logits.argmax(dim=1) == targets).float()
+
+
+# ------------------------------------------------------------ generic convs
+# ResNet-family convolutions (models/common.py NativeConv2d).  MIOpen's
+# per-call host cost (solver lookup, find-db, workspace) and its bf16-grad ->
+# fp32 cast + AccumulateGrad passes dominated the per-client ImageNet round
+# (profiles/r2_cfg_imagenet_round.txt: >50 % GPU idle at ~1,650 kernels per
+# client).  Here:
+#   * 1x1 convs are plain GEMMs on the NHWC activation ([P, C] x [C, K]) on
+#     hipBLASLt; the weight gradient is ONE bf16 x bf16 -> fp32 GEMM that
+#     accumulates (beta = 1) straight into the flat fp32 gradient view;
+#   * stride-1 3x3 convs with C % 64 == 0 and K % 64 == 0 run on the native
+#     MFMA kernels of csrc/conv.hip (forward, dgrad on the flipped weights,
+#     wgrad accumulating into the flat gradient when K % 128 == 0);
+#   * everything else (7x7 stems, strided 3x3) stays on MIOpen.
+def _grad_view(weight: torch.Tensor, shape):
+    """``weight.grad`` viewed as ``shape`` when it can receive an in-place fp32
+    accumulation (FedModel keeps every .grad as a flat-buffer view)."""
+    gr = weight.grad
+    if (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
+            and gr.device == weight.device and tuple(gr.shape) == tuple(weight.shape)):
+        return gr.view(shape)
+    return None
+
+
+def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> its [N*H*W, C] row-major image (a view)."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None) -> torch.Tensor:
+    """dW [K, C] fp32 (+)= g2d^T x2d, a reduction over the P = N*H*W rows.
+
+    P is 10^3-10^5 while K x C can be as small as 64 x 256, so one GEMM
+    launches only a handful of output tiles, each looping over all of P
+    (hipBLASLt picked 64x64 tiles without split-K: 12 TF/s, ~270 us per
+    ResNet-101 layer-4 weight gradient).  The rows are split into S chunks
+    so S x tiles fills the chip: one batched bf16 x bf16 -> fp32 GEMM writes
+    S partial products, one reduction adds them (into ``into`` when given).
+    Without a split the GEMM accumulates straight into ``into`` (beta = 1)."""
+    P, K = g2d.shape
+    C = x2d.shape[1]
+    tiles = max(1, (K // 128) * (C // 128))
+    S = 1
+    while S < 64 and P % (2 * S) == 0 and P // (2 * S) >= 256 and S * tiles < 1024:
+        S *= 2
+    if S == 1:
+        if into is not None:
+            return torch.addmm(into, g2d.t(), x2d, out_dtype=torch.float32, out=into)
+        return torch.mm(g2d.t(), x2d, out_dtype=torch.float32)
+    part = torch.bmm(g2d.view(S, P // S, K).transpose(1, 2), x2d.view(S, P // S, C),
+                     out_dtype=torch.float32)
+    if into is not None:
+        return into.add_(part.sum(0))
+    return part.sum(0)
+
+
+class _Conv1x1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride):
+        ctx.in_hw = (x.shape[2], x.shape[3])
+        if stride > 1:
+            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
+        n, c, h, w = x.shape
+        k = weight.shape[0]
+        wb = weight.detach().view(k, c).to(torch.bfloat16)
+        y2d = torch.mm(_nhwc2d(x), wb.t())
+        ctx.save_for_backward(x, wb)
+        ctx.weight, ctx.stride = weight, stride
+        return y2d.view(n, h, w, k).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wb = ctx.saved_tensors
+        n, c, h, w = x.shape
+        k = wb.shape[0]
+        g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gsub = torch.mm(g2d, wb).view(n, h, w, c).permute(0, 3, 1, 2)
+            s = ctx.stride
+            if s > 1:
+                H, W = ctx.in_hw
+                gx = torch.zeros(n, H, W, c, dtype=gsub.dtype, device=gsub.device).permute(0, 3, 1, 2)
+                gx[:, :, ::s, ::s] = gsub
+            else:
+                gx = gsub
+        gw = None
+        if ctx.needs_input_grad[1]:
+            into = _grad_view(ctx.weight, (k, c))
+            gw = _wgrad_gemm(g2d, _nhwc2d(x), into)
+            gw = None if into is not None else gw.view(k, c, 1, 1)
+        return gx, gw, None
+
+
+class _Conv3x3(torch.autograd.Function):
+    """conv3x3 (stride 1, pad 1, no bias) on the native MFMA kernels."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        wf, wt = _prep(weight)
+        ctx.save_for_backward(x, wt)
+        ctx.weight = weight
+        return _ops().conv3x3_fwd(x, wf, False)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wt = ctx.saved_tensors
+        g = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        gx = _ops().conv3x3_fwd(g, wt, False) if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            w = ctx.weight
+            if w.shape[0] % 128 == 0:
+                gw = _wgrad_to(g, x, w)
+            else:  # the native wgrad tiles need K % 128 == 0
+                gw = torch.ops.aten.convolution_backward(
+                    g, x, w.detach().to(torch.bfloat16), None, [1, 1], [1, 1], [1, 1], False,
+                    [0, 0], 1, [False, True, False])[1].float()
+        return gx, gw
+
+
+def _gpu_bf16_nhwc(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def conv2d_native_kind(x: torch.Tensor, weight: torch.Tensor, stride, padding, dilation,
+                       groups) -> str:
+    """Which native path serves this convolution: "1x1", "3x3" or "" (MIOpen)."""
+    if _CONV_BACKEND[0] != "native" or groups != 1 or not _gpu_bf16_nhwc(x):
+        return ""
+    if weight.dtype != torch.float32 or weight.dim() != 4 or weight.shape[1] != x.shape[1]:
+        return ""
+    kh, kw = weight.shape[2], weight.shape[3]
+    s = stride if isinstance(stride, int) else (stride[0] if stride[0] == stride[1] else -1)
+    p = padding if isinstance(padding, int) else (padding[0] if padding[0] == padding[1] else -1)
+    dl = dilation if isinstance(dilation, int) else (dilation[0] if dilation[0] == dilation[1]
+                                                     else -1)
+    if dl != 1:
+        return ""
+    if (kh, kw) == (1, 1) and p == 0 and s >= 1 and x.shape[1] % 8 == 0 \
+            and weight.shape[0] % 8 == 0:
+        return "1x1"
+    if ((kh, kw) == (3, 3) and s == 1 and p == 1 and x.shape[1] % 64 == 0
+            and weight.shape[0] % 64 == 0):
+        return "3x3"
+    return ""
+
+
+def conv2d_native(x: torch.Tensor, weight: torch.Tensor, kind: str, stride: int = 1):
+    if kind == "1x1":
+        return _Conv1x1.apply(x, weight, int(stride))
+    return _Conv3x3.apply(x, weight)

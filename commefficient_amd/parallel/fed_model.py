@@ -38,7 +38,8 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ..models.common import ghost_batchnorm, has_batchnorm
+from ..models.common import NativeConv2d, ghost_batchnorm, has_batchnorm
+from ..ops.nn import prepared_conv_weights
 from ..ops import CSVec
 from ..utils.logging import PhaseTimer
 from . import dist
@@ -526,12 +527,25 @@ class FedModel:
         # around the loop lets the clients share the bf16 weight casts
         shared_w = (a.mode != "fedavg" and "weights" not in self.client_state.kinds
                     and not a.do_test and os.environ.get("COMMEFF_SHARED_CASTS", "1") != "0")
-        with (self._autocast() if shared_w else nullcontext()):
+        # ... and the native 3x3 convs share one batched bf16 weight preparation
+        prep = (prepared_conv_weights(self._native_3x3_weights())
+                if shared_w and self.device.type == "cuda" else nullcontext())
+        with (self._autocast() if shared_w else nullcontext()), prep:
             msum = self._per_client_loop(rb, order, starts, my_slots, mine, counts, W, out)
         if msum is None:  # no clients on this rank this round
             msum = torch.zeros(self._n_metrics_guess(), W, device=self.device)
         self._n_metrics = msum.shape[0]
         return out, msum
+
+    def _native_3x3_weights(self):
+        ws = getattr(self, "_n3x3", None)
+        if ws is None:
+            ws = [m.weight for m in self.model.modules()
+                  if isinstance(m, NativeConv2d) and tuple(m.kernel_size) == (3, 3)
+                  and tuple(m.stride) == (1, 1) and m.groups == 1 and m.bias is None
+                  and m.weight.shape[0] % 64 == 0]
+            self._n3x3 = ws
+        return ws
 
     def _per_client_loop(self, rb, order, starts, my_slots, mine, counts, W, out):
         a = self.args

@@ -56,6 +56,8 @@ def main():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--clients", type=int, default=0, help="clients per round (total)")
+    p.add_argument("extra", nargs=argparse.REMAINDER,
+                   help="extra fed_train flags after '--' (e.g. -- --encode direct)")
     b = p.parse_args()
     from commefficient_amd import models
     from commefficient_amd.parallel import dist
@@ -65,7 +67,8 @@ def main():
     ctx = dist.init("cuda")
     N = ctx.world_size
     W, argv = cfg_args(b.config, N, b)
-    args = parse_args(argv=argv + ["--device", "cuda", "--seed", "21"], probe_port=False)
+    extra = [x for x in b.extra if x != "--"]
+    args = parse_args(argv=argv + ["--device", "cuda", "--seed", "21"] + extra, probe_port=False)
     torch.manual_seed(0)
     if b.config == "gpt2_sketch":
         from commefficient_amd.train import gpt2 as drv

@@ -28,17 +28,24 @@ def main():
     ap.add_argument("--marker", default="enc_p1_kernel")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--tail-ms", type=float, default=0.0,
+                    help="no marker: take the kernels of the trace's last TAIL_MS ms "
+                         "(e.g. rounds * ms_per_round of the timed steps)")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    starts = [i for i, r in enumerate(rows) if a.marker in r[2]]
-    if len(starts) < a.rounds + 1:
-        raise SystemExit(f"only {len(starts)} marker kernels")
-    lo, hi = starts[-a.rounds - 1], starts[-1]
-    sel = rows[lo:hi]
+    if a.tail_ms > 0:
+        t_end = max(r[1] for r in rows)
+        sel = [r for r in rows if r[0] >= t_end - a.tail_ms * 1e6]
+    else:
+        starts = [i for i, r in enumerate(rows) if a.marker in r[2]]
+        if len(starts) < a.rounds + 1:
+            raise SystemExit(f"only {len(starts)} marker kernels")
+        lo, hi = starts[-a.rounds - 1], starts[-1]
+        sel = rows[lo:hi]
     n = a.rounds
     wall = (sel[-1][1] - sel[0][0]) / n
     busy = collections.Counter()

@@ -427,3 +427,42 @@ def test_fwd_large_batch_matches_fp32(N, C, H, K):
     p, i = torch.ops.commeff.conv3x3_fwd_pool2(x, wf)
     p_ref, _ = torch.ops.commeff.relu_maxpool(ops.conv3x3_fwd(x, wf, False), 2)
     assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
+
+
+# ---------------------------------------------------------------- NativeConv2d
+# ResNet-family convs (models/common.py NativeConv2d): 1x1 on hipBLASLt GEMMs
+# (stride 1 and 2), stride-1 3x3 on the native kernels (K % 128 wgrad native,
+# K = 64 wgrad on MIOpen), vs an fp32 reference of the same op.
+NATIVE_CONV = [  # N, C, H, W, K, ksize, stride
+    (4, 64, 14, 14, 256, 1, 1),
+    (4, 256, 14, 14, 64, 1, 1),
+    (4, 256, 14, 14, 512, 1, 2),
+    (3, 512, 7, 7, 2048, 1, 1),
+    (4, 64, 14, 14, 64, 3, 1),     # ResNet-101 layer1 3x3 (wgrad K=64 -> MIOpen)
+    (4, 128, 28, 28, 128, 3, 1),
+    (2, 512, 7, 7, 512, 3, 1),
+]
+
+
+@pytest.mark.parametrize("N,C,H,W,K,ks,stride", NATIVE_CONV)
+def test_native_conv2d_fwd_bwd(N, C, H, W, K, ks, stride):
+    from commefficient_amd.models.common import NativeConv2d
+    torch.manual_seed(0)
+    conv = NativeConv2d(C, K, ks, stride=stride, padding=ks // 2, bias=False).cuda()
+    x = _nhwc(torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    kind = cnn.conv2d_native_kind(x, conv.weight, conv.stride, conv.padding, conv.dilation, 1)
+    assert kind == ("1x1" if ks == 1 else "3x3")
+    # the flat-buffer convention: an existing fp32 .grad receives the wgrad in place
+    prior = torch.randn_like(conv.weight) * 0.01
+    conv.weight.grad = prior.clone()
+    y = conv(x)
+    gy = _nhwc(torch.randn(y.shape, device="cuda").to(torch.bfloat16))
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=stride, padding=ks // 2)
+    yr.backward(gy.float())
+    assert y.shape == yr.shape and y.dtype == torch.bfloat16
+    _close(y, yr)
+    _close(x.grad, xr.grad)
+    _close(conv.weight.grad - prior, wr.grad)
