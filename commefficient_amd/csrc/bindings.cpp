@@ -889,7 +889,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
                                                                 const c10::optional<at::Tensor>& w, int64_t G,
                                                                 const c10::optional<at::Tensor>& y_relu,
                                                                 const c10::optional<at::Tensor>& gw,
-                                                                const c10::optional<at::Tensor>& gb) {
+                                                                const c10::optional<at::Tensor>& gb,
+                                                                const c10::optional<at::Tensor>& ggw,
+                                                                const c10::optional<at::Tensor>& ggb) {
   check_nhwc_bf16(x, "ghost_bn_bwd: x");
   check_nhwc_bf16(dy, "ghost_bn_bwd: dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "ghost_bn_bwd: dy shape");
@@ -909,23 +911,36 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
     check_f32(*gb, "ghost_bn_bwd: bias grad");
     TORCH_CHECK(gw->numel() == C && gb->numel() == C, "ghost_bn_bwd: grad shapes");
   }
+  // grouped (per-client) dweight / dbias: [G, C] fp32 rows of any row stride
+  // (views of the client-major grouped gradient buffer, parallel/grouped.py)
+  const bool grouped = affine && ggw.has_value() && ggw->defined() && ggb.has_value() && ggb->defined();
+  if (grouped) {
+    TORCH_CHECK(!into, "ghost_bn_bwd: flat and grouped gradients are exclusive");
+    for (const auto* t : {&*ggw, &*ggb}) {
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() == 2 && t->size(0) == G && t->size(1) == C &&
+                      t->stride(1) == 1 && t->stride(0) == ggw->stride(0) && t->device() == x.device(),
+                  "ghost_bn_bwd: grouped grads must be f32 [G, C] rows of one stride");
+    }
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
   auto fo = x.options().dtype(at::kFloat);
   auto part = at::empty({G * S * 2 * C}, fo);
   auto coef = at::empty({G * 3 * C}, fo);
   at::Tensor dw, db;
-  if (affine && !into) {
+  if (affine && !into && !grouped) {
     dw = at::empty({C}, fo);
     db = at::empty({C}, fo);
   }
-  float* dwp = into ? gw->data_ptr<float>() : (affine ? dw.data_ptr<float>() : nullptr);
-  float* dbp = into ? gb->data_ptr<float>() : (affine ? db.data_ptr<float>() : nullptr);
+  float* dwp = into ? gw->data_ptr<float>() : (affine && !grouped ? dw.data_ptr<float>() : nullptr);
+  float* dbp = into ? gb->data_ptr<float>() : (affine && !grouped ? db.data_ptr<float>() : nullptr);
   auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   launch_bn_bwd(bf16_ptr(x), bf16_ptr(dy), fused_relu ? bf16_ptr(*y_relu) : nullptr, stat.data_ptr<float>(),
                 affine ? w->data_ptr<float>() : nullptr, static_cast<int>(G), static_cast<int>(M),
                 static_cast<int>(C), part.data_ptr<float>(), coef.data_ptr<float>(), dwp, dbp,
-                into ? 1.f : 0.f, reinterpret_cast<uint16_t*>(dx.data_ptr()), cur_stream());
+                into ? 1.f : 0.f, reinterpret_cast<uint16_t*>(dx.data_ptr()), cur_stream(),
+                grouped ? ggw->data_ptr<float>() : nullptr, grouped ? ggb->data_ptr<float>() : nullptr,
+                grouped ? ggw->stride(0) : 0);
   return {dx, dw, db};
 }
 
@@ -1203,7 +1218,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
         "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None) -> (Tensor, Tensor)");
   m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None, "
-        "Tensor(a!)? gw=None, Tensor(b!)? gb=None) -> (Tensor, Tensor, Tensor)");
+        "Tensor(a!)? gw=None, Tensor(b!)? gb=None, Tensor(c!)? ggw=None, Tensor(d!)? ggb=None) "
+        "-> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");

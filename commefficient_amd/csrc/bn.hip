@@ -230,12 +230,15 @@ bn_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__
 
 // backward: with k0 = w rstd, k1 = mean(dy), k2 = mean(dy xhat) and
 // xhat = (x - mean) rstd, dx = k0 (dy - k1 - xhat k2) = P dy + Q x + R:
-// coef[g][0..2][c] = P, Q, R.  dw[c] = sum_g sum(dy xhat), db[c] = sum_g sum(dy)
+// coef[g][0..2][c] = P, Q, R.  dw[c] = sum_g sum(dy xhat), db[c] = sum_g sum(dy);
+// grouped weight gradients (parallel/grouped.py): gdw[g * gstride + c] +=
+// sum(dy xhat) and gdb[...] += sum(dy) of group g alone
 __global__ void __launch_bounds__(1024)
 bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__ stat,
                        const float* __restrict__ w, int C, int M, int S, int G,
                        float* __restrict__ coef, float* __restrict__ dw, float* __restrict__ db,
-                       float beta) {
+                       float beta, float* __restrict__ gdw, float* __restrict__ gdb,
+                       int64_t gstride) {
   __shared__ float red[2][kGL][64];
   const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cc;
@@ -244,6 +247,10 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__
   auto finish = [&](int g, float s1, float s2) __attribute__((always_inline)) {
     tb += s1;
     tw += s2;
+    if (gdw != nullptr) {  // per-group (per-client) dweight / dbias, accumulated
+      gdw[g * gstride + c] += s2;
+      gdb[g * gstride + c] += s1;
+    }
     const float mean = stat[static_cast<size_t>(g) * 2 * C + c];
     const float rstd = stat[static_cast<size_t>(g) * 2 * C + C + c];
     const float k0 = wc * rstd, k1 = s1 / M, k2 = s2 / M;
@@ -375,12 +382,13 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
 
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
-                   float beta, uint16_t* dx, hipStream_t stream) {
+                   float beta, uint16_t* dx, hipStream_t stream, float* gdw, float* gdb,
+                   int64_t gstride) {
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
                      S, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat, w,
-                     C, M, S, G, coef, dw, db, beta);
+                     C, M, S, G, coef, dw, db, beta, gdw, gdb, gstride);
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
                      coef, C, M, static_cast<uint32_t>(nchunks), false, dx);

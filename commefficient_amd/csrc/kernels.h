@@ -242,7 +242,8 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
                    bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
-                   float beta, uint16_t* dx, hipStream_t stream);
+                   float beta, uint16_t* dx, hipStream_t stream, float* gdw = nullptr,
+                   float* gdb = nullptr, int64_t gstride = 0);
 
 constexpr int kClientMeanRows = 4;
 struct ClientMeanRows {

@@ -7,7 +7,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import conv2d_native, conv2d_native_kind, ghost_batch_norm, ghost_bn_native_ok
+from ..ops import grouped as _grouped
+from ..ops.nn import (_AffineGrouped, conv2d_grouped, conv2d_native, conv2d_native_kind,
+                      ghost_batch_norm, ghost_bn_native_ok, linear_grouped)
 
 
 class Mul(nn.Module):
@@ -70,6 +72,9 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
     def _bn(self, x):
         """(normalised x, whether the fused ReLU was already applied)"""
         G = max(1, self.ghost_groups)
+        gg = _grouped.active() if (self.training and self.affine) else None
+        if gg is not None and gg.view(self.weight) is None:
+            gg = None
         if (self.training and self.momentum is not None and x.shape[0] % G == 0
                 and ghost_bn_native_ok(x, self.weight if self.affine else None)):
             # native per-group BN (csrc/bn.hip), also for one group (the
@@ -79,9 +84,10 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
                                  self.bias if self.affine else None, G, self.eps, self.momentum,
                                  self.running_mean if track else None,
                                  self.running_var if track else None, relu=self.fuse_relu,
-                                 num_batches_tracked=self.num_batches_tracked if track else None)
+                                 num_batches_tracked=self.num_batches_tracked if track else None,
+                                 gg=gg)
             return y, self.fuse_relu
-        if not self.training or G <= 1:
+        if gg is None and (not self.training or G <= 1):
             return super().forward(x), False
         N, C = x.shape[0], x.shape[1]
         assert N % G == 0, "ghost batch norm needs equal client batch sizes"
@@ -89,7 +95,9 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
         mean = xf.mean(dim=(1, 3), keepdim=True)
         var = xf.var(dim=(1, 3), keepdim=True, unbiased=False)
         y = (xf - mean) * torch.rsqrt(var + self.eps)
-        if self.affine:
+        if self.affine and gg is not None:  # per-group dweight / dbias
+            y = _AffineGrouped.apply(y.reshape(N, C, -1), self.weight, self.bias, gg)
+        elif self.affine:
             y = y * self.weight.view(1, 1, C, 1) + self.bias.view(1, 1, C, 1)
         if self.track_running_stats and self.running_mean is not None:
             with torch.no_grad():
@@ -131,12 +139,51 @@ class NativeConv2d(nn.Conv2d):
     every other case is the stock (MIOpen) convolution."""
 
     def forward(self, x):
+        gg = _grouped.active() if self.weight.requires_grad else None
+        if gg is not None and gg.view(self.weight) is None:
+            gg = None
         if self.bias is None and self.padding_mode == "zeros":
             kind = conv2d_native_kind(x, self.weight, self.stride, self.padding, self.dilation,
                                       self.groups)
             if kind:
-                return conv2d_native(x, self.weight, kind, self.stride[0])
+                return conv2d_native(x, self.weight, kind, self.stride[0], gg)
+            if gg is not None:
+                return conv2d_grouped(x, self.weight, self.stride, self.padding, self.dilation,
+                                      self.groups, gg)
         return super().forward(x)
+
+
+class NativeLinear(nn.Linear):
+    """``nn.Linear`` that writes per-group weight gradients under
+    ``ops.grouped.grouped_grads`` (one batched GEMM over the groups)."""
+
+    def forward(self, x):
+        gg = _grouped.active() if self.weight.requires_grad else None
+        if gg is not None and gg.view(self.weight) is not None and (
+                self.bias is None or gg.view(self.bias) is not None):
+            return linear_grouped(x, self.weight, self.bias, gg)
+        return super().forward(x)
+
+
+GROUPED_MODULES = (NativeConv2d, NativeLinear)
+
+
+def groupable(model: nn.Module) -> bool:
+    """Every trainable parameter belongs to a module that can write per-group
+    weight gradients (ops/grouped.py): NativeConv2d (no bias), NativeLinear,
+    affine GhostBatchNorm2d."""
+    for m in model.modules():
+        own = [p for p in m.parameters(recurse=False) if p.requires_grad]
+        if not own:
+            continue
+        if isinstance(m, NativeConv2d) and m.bias is None:
+            continue
+        if isinstance(m, NativeLinear):
+            continue
+        if isinstance(m, GhostBatchNorm2d) and m.affine:
+            continue
+        return False
+    return True
 
 
 def conv3x3(c_in, c_out, stride=1):

@@ -22,7 +22,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .common import GhostBatchNorm2d, ScalarBias, ScalarScale, conv1x1, conv3x3
+from .common import (GhostBatchNorm2d, NativeConv2d, NativeLinear, ScalarBias, ScalarScale, conv1x1,
+                     conv3x3)
 
 __all__ = ["FixupResNet9", "FixupResNet18", "ResNet18", "FixupResNet50"]
 
@@ -175,7 +176,7 @@ class FixupResNet18(_ResNet18Base):
         self.num_layers = sum(num_blocks)
         self.prep = conv3x3(initial_channels, 64)
         self.layers = self._make(FixupBlock18, num_blocks)
-        self.classifier = nn.Linear(512, num_classes)
+        self.classifier = NativeLinear(512, num_classes)
         for m in self.modules():
             if isinstance(m, FixupBlock18):
                 nn.init.normal_(m.conv1.weight, 0, _he_std(m.conv1) * self.num_layers ** (-0.5))
@@ -197,7 +198,7 @@ class ResNet18(_ResNet18Base):
         super().__init__()
         self.prep = nn.Sequential(conv3x3(initial_channels, 64), nn.ReLU())
         self.layers = self._make(PreActBlock, num_blocks)
-        self.classifier = nn.Linear(512, num_classes)
+        self.classifier = NativeLinear(512, num_classes)
 
     def forward(self, x):
         return self.classifier(_avg_max_head(self.layers(self.prep(x))))
@@ -235,7 +236,7 @@ class FixupResNet(nn.Module):
         super().__init__()
         self.num_layers = sum(layers)
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(initial_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = NativeConv2d(initial_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
         self.bias1 = nn.Parameter(torch.zeros(1))
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
@@ -244,7 +245,7 @@ class FixupResNet(nn.Module):
         self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
         self.bias2 = nn.Parameter(torch.zeros(1))
-        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        self.fc = NativeLinear(512 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, FixupBottleneck):
                 f = self.num_layers ** (-0.25)

@@ -17,7 +17,7 @@ import math
 import torch
 import torch.nn as nn
 
-from .common import GhostBatchNorm2d, NativeConv2d, conv1x1, conv3x3
+from .common import GhostBatchNorm2d, NativeConv2d, NativeLinear, conv1x1, conv3x3
 
 __all__ = ["ResNet", "ResNet101", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152",
            "resnext50_32x4d", "resnext101_32x8d", "wide_resnet50_2", "wide_resnet101_2"]
@@ -99,7 +99,7 @@ class ResNet(nn.Module):
         self.inplanes = 64
         self.groups = groups
         self.base_width = width_per_group
-        self.conv1 = nn.Conv2d(in_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = NativeConv2d(in_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
         hw = (input_hw + 2 * 3 - 7) // 2 + 1
         self.bn1 = _norm(norm, 64, hw, relu=True)
         self.relu = nn.ReLU(inplace=True)
@@ -110,7 +110,7 @@ class ResNet(nn.Module):
         self.layer3, hw = self._make_layer(block, 256, layers[2], hw, stride=2)
         self.layer4, hw = self._make_layer(block, 512, layers[3], hw, stride=2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
-        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        self.fc = NativeLinear(512 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")

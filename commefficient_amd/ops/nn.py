@@ -309,12 +309,14 @@ class _GhostBN(torch.autograd.Function):
     moments (the torch path in models/common.py GhostBatchNorm2d)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var, relu, nbt):
+    def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var, relu, nbt,
+                gg=None):
         y, stat = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
                                       running_mean, running_var, bool(relu), nbt)
         ctx.save_for_backward(x, stat, weight, y if relu else None)
         ctx.groups = int(groups)
         ctx.params = (weight, bias)
+        ctx.gg = gg
         return y
 
     @staticmethod
@@ -324,6 +326,13 @@ class _GhostBN(torch.autograd.Function):
         # existing fp32 .grad tensors (FedModel's flat-buffer views) receive
         # dweight / dbias in place: no AccumulateGrad launches
         pw, pb = ctx.params
+        if ctx.gg is not None and pw is not None:
+            # grouped (per-client) dweight / dbias rows, ops/grouped.py; the
+            # BN groups are the gradient groups
+            assert ctx.gg.G == ctx.groups, "grouped grads need ghost-BN groups == gradient groups"
+            dx, _, _ = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y, None, None,
+                                           ctx.gg.view(pw), ctx.gg.view(pb))
+            return dx, None, None, None, None, None, None, None, None, None, None
         gw = pw.grad if pw is not None else None
         gb = pb.grad if pb is not None else None
         into = (gw is not None and gb is not None and gw.dtype == torch.float32
@@ -334,7 +343,7 @@ class _GhostBN(torch.autograd.Function):
                                          gw if into else None, gb if into else None)
         if weight is None or into:
             dw = db = None
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
 def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
@@ -346,11 +355,12 @@ def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
 
 def ghost_batch_norm(x, weight, bias, groups: int, eps: float, momentum: float,
                      running_mean=None, running_var=None, relu: bool = False,
-                     num_batches_tracked=None):
+                     num_batches_tracked=None, gg=None):
     """Per-group batch norm (+ ReLU when ``relu``) on the native kernels; the
-    running statistics and ``num_batches_tracked`` are updated on the device."""
+    running statistics and ``num_batches_tracked`` are updated on the device.
+    ``gg``: per-group weight gradients (ops/grouped.py)."""
     return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var, relu,
-                          num_batches_tracked)
+                          num_batches_tracked, gg)
 
 
 # ------------------------------------------------------------ loss
@@ -385,15 +395,17 @@ def cross_entropy_correct(logits: torch.Tensor, targets: torch.Tensor):
 # ResNet-family convolutions (models/common.py NativeConv2d).  MIOpen's
 # per-call host cost (solver lookup, find-db, workspace) and its bf16-grad ->
 # fp32 cast + AccumulateGrad passes dominated the per-client ImageNet round
-# (profiles/r2_cfg_imagenet_round.txt: >50 % GPU idle at ~1,650 kernels per
-# client).  Here:
+# (profiles/r2_v1_imagenet_round_kernels.txt: >50 % GPU idle at ~1,650 kernels
+# per client).  Here:
 #   * 1x1 convs are plain GEMMs on the NHWC activation ([P, C] x [C, K]) on
-#     hipBLASLt; the weight gradient is ONE bf16 x bf16 -> fp32 GEMM that
-#     accumulates (beta = 1) straight into the flat fp32 gradient view;
+#     hipBLASLt; the weight gradient is a bf16 x bf16 -> fp32 GEMM that
+#     accumulates straight into the flat fp32 gradient view;
 #   * stride-1 3x3 convs with C % 64 == 0 and K % 64 == 0 run on the native
 #     MFMA kernels of csrc/conv.hip (forward, dgrad on the flipped weights,
 #     wgrad accumulating into the flat gradient when K % 128 == 0);
 #   * everything else (7x7 stems, strided 3x3) stays on MIOpen.
+# Under ``ops.grouped.grouped_grads`` every path writes per-group weight
+# gradients instead (see ops/grouped.py).
 def _grad_view(weight: torch.Tensor, shape):
     """``weight.grad`` viewed as ``shape`` when it can receive an in-place fp32
     accumulation (FedModel keeps every .grad as a flat-buffer view)."""
@@ -410,36 +422,41 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
 
 
-def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None) -> torch.Tensor:
-    """dW [K, C] fp32 (+)= g2d^T x2d, a reduction over the P = N*H*W rows.
+def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> torch.Tensor:
+    """dW (+)= g2d^T x2d, a reduction over the P rows, per group of P/G rows.
 
+    ``into``: [K, C] (G == 1) or [G, K, C] (rows may be strided) fp32.
     P is 10^3-10^5 while K x C can be as small as 64 x 256, so one GEMM
     launches only a handful of output tiles, each looping over all of P
     (hipBLASLt picked 64x64 tiles without split-K: 12 TF/s, ~270 us per
-    ResNet-101 layer-4 weight gradient).  The rows are split into S chunks
-    so S x tiles fills the chip: one batched bf16 x bf16 -> fp32 GEMM writes
-    S partial products, one reduction adds them (into ``into`` when given).
+    ResNet-101 layer-4 weight gradient).  Each group's rows are split into S
+    chunks so G x S x tiles fills the chip: one batched bf16 x bf16 -> fp32
+    GEMM writes the G x S partial products, one reduction adds them.
     Without a split the GEMM accumulates straight into ``into`` (beta = 1)."""
     P, K = g2d.shape
     C = x2d.shape[1]
+    Pg = P // G
     tiles = max(1, (K // 128) * (C // 128))
     S = 1
-    while S < 64 and P % (2 * S) == 0 and P // (2 * S) >= 256 and S * tiles < 1024:
+    while S < 64 and Pg % (2 * S) == 0 and Pg // (2 * S) >= 256 and G * S * tiles < 1024:
         S *= 2
-    if S == 1:
+    if G == 1 and S == 1:
         if into is not None:
             return torch.addmm(into, g2d.t(), x2d, out_dtype=torch.float32, out=into)
         return torch.mm(g2d.t(), x2d, out_dtype=torch.float32)
-    part = torch.bmm(g2d.view(S, P // S, K).transpose(1, 2), x2d.view(S, P // S, C),
+    part = torch.bmm(g2d.view(G * S, Pg // S, K).transpose(1, 2), x2d.view(G * S, Pg // S, C),
                      out_dtype=torch.float32)
+    if S > 1:
+        part = part.view(G, S, K, C).sum(1)
+    part = part.view(G, K, C) if G > 1 else part.view(K, C)
     if into is not None:
-        return into.add_(part.sum(0))
-    return part.sum(0)
+        return into.add_(part)
+    return part
 
 
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride):
+    def forward(ctx, x, weight, stride, gg):
         ctx.in_hw = (x.shape[2], x.shape[3])
         if stride > 1:
             x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
@@ -448,7 +465,7 @@ class _Conv1x1(torch.autograd.Function):
         wb = weight.detach().view(k, c).to(torch.bfloat16)
         y2d = torch.mm(_nhwc2d(x), wb.t())
         ctx.save_for_backward(x, wb)
-        ctx.weight, ctx.stride = weight, stride
+        ctx.weight, ctx.stride, ctx.gg = weight, stride, gg
         return y2d.view(n, h, w, k).permute(0, 3, 1, 2)
 
     @staticmethod
@@ -469,20 +486,39 @@ class _Conv1x1(torch.autograd.Function):
                 gx = gsub
         gw = None
         if ctx.needs_input_grad[1]:
-            into = _grad_view(ctx.weight, (k, c))
-            gw = _wgrad_gemm(g2d, _nhwc2d(x), into)
-            gw = None if into is not None else gw.view(k, c, 1, 1)
-        return gx, gw, None
+            if ctx.gg is not None:
+                G = ctx.gg.G
+                _wgrad_gemm(g2d, _nhwc2d(x), ctx.gg.view(ctx.weight).view(G, k, c), G)
+            else:
+                into = _grad_view(ctx.weight, (k, c))
+                gw = _wgrad_gemm(g2d, _nhwc2d(x), into)
+                gw = None if into is not None else gw.view(k, c, 1, 1)
+        return gx, gw, None, None
+
+
+def _wgrad_mopen(g, x, weight, stride, padding, dilation, groups):
+    """MIOpen weight gradient (fp32) of one conv."""
+    return torch.ops.aten.convolution_backward(
+        g, x, weight.detach().to(g.dtype), None, list(stride), list(padding), list(dilation), False,
+        [0, 0], groups, [False, True, False])[1].float()
+
+
+def _grouped_wgrad_slices(g, x, gview, fn):
+    """Per-group weight gradients from each group's slice of the batch."""
+    G = gview.shape[0]
+    ng = g.shape[0] // G
+    for j in range(G):
+        fn(g[j * ng:(j + 1) * ng], x[j * ng:(j + 1) * ng], gview[j])
 
 
 class _Conv3x3(torch.autograd.Function):
     """conv3x3 (stride 1, pad 1, no bias) on the native MFMA kernels."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, gg):
         wf, wt = _prep(weight)
         ctx.save_for_backward(x, wt)
-        ctx.weight = weight
+        ctx.weight, ctx.gg = weight, gg
         return _ops().conv3x3_fwd(x, wf, False)
 
     @staticmethod
@@ -493,13 +529,50 @@ class _Conv3x3(torch.autograd.Function):
         gw = None
         if ctx.needs_input_grad[1]:
             w = ctx.weight
-            if w.shape[0] % 128 == 0:
+            native = w.shape[0] % 128 == 0  # the native wgrad tiles need K % 128 == 0
+
+            def one(gs, xs, dst):
+                if native:
+                    _ops().conv3x3_wgrad_into(gs, xs, dst)
+                else:
+                    dst.add_(_wgrad_mopen(gs, xs, w, (1, 1), (1, 1), (1, 1), 1))
+
+            if ctx.gg is not None:
+                _grouped_wgrad_slices(g, x, ctx.gg.view(w), one)
+            elif native:
                 gw = _wgrad_to(g, x, w)
-            else:  # the native wgrad tiles need K % 128 == 0
-                gw = torch.ops.aten.convolution_backward(
-                    g, x, w.detach().to(torch.bfloat16), None, [1, 1], [1, 1], [1, 1], False,
-                    [0, 0], 1, [False, True, False])[1].float()
-        return gx, gw
+            else:
+                gw = _wgrad_mopen(g, x, w, (1, 1), (1, 1), (1, 1), 1)
+        return gx, gw, None
+
+
+class _ConvGrouped(torch.autograd.Function):
+    """Any convolution (MIOpen) with per-group weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, dilation, groups, gg):
+        wc = weight.detach().to(x.dtype)
+        ctx.save_for_backward(x, wc)
+        ctx.conf = (tuple(stride), tuple(padding), tuple(dilation), groups)
+        ctx.weight, ctx.gg = weight, gg
+        return F.conv2d(x, wc, None, stride, padding, dilation, groups)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wc = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.conf
+        g = gy.to(x.dtype)
+        if x.is_cuda and x.is_contiguous(memory_format=torch.channels_last):
+            g = g.contiguous(memory_format=torch.channels_last)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.ops.aten.convolution_backward(
+                g, x, wc, None, list(stride), list(padding), list(dilation), False, [0, 0], groups,
+                [True, False, False])[0]
+        _grouped_wgrad_slices(g, x, ctx.gg.view(ctx.weight),
+                              lambda gs, xs, dst: dst.add_(
+                                  _wgrad_mopen(gs, xs, wc, stride, padding, dilation, groups)))
+        return gx, None, None, None, None, None, None
 
 
 def _gpu_bf16_nhwc(x: torch.Tensor) -> bool:
@@ -530,7 +603,85 @@ def conv2d_native_kind(x: torch.Tensor, weight: torch.Tensor, stride, padding, d
     return ""
 
 
-def conv2d_native(x: torch.Tensor, weight: torch.Tensor, kind: str, stride: int = 1):
+def conv2d_native(x: torch.Tensor, weight: torch.Tensor, kind: str, stride: int = 1, gg=None):
     if kind == "1x1":
-        return _Conv1x1.apply(x, weight, int(stride))
-    return _Conv3x3.apply(x, weight)
+        return _Conv1x1.apply(x, weight, int(stride), gg)
+    return _Conv3x3.apply(x, weight, gg)
+
+
+def conv2d_grouped(x, weight, stride, padding, dilation, groups, gg):
+    """Convolution whose weight gradient goes to the per-group rows of ``gg``."""
+    if weight.dtype != x.dtype and not torch.is_autocast_enabled(x.device.type):
+        x = x.to(weight.dtype)
+    elif torch.is_autocast_enabled(x.device.type) and x.is_floating_point():
+        x = x.to(torch.get_autocast_dtype(x.device.type))
+    return _ConvGrouped.apply(x, weight, stride, padding, dilation, groups, gg)
+
+
+# ------------------------------------------------------------ grouped linear
+class _LinearGrouped(torch.autograd.Function):
+    """y = x W^T + b with per-group dW / db (batched GEMM over the groups)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gg):
+        wc = weight.detach().to(x.dtype)
+        ctx.save_for_backward(x, wc)
+        ctx.params, ctx.gg = (weight, bias), gg
+        y = F.linear(x, wc, None if bias is None else bias.detach().to(x.dtype))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wc = ctx.saved_tensors
+        weight, bias = ctx.params
+        gg = ctx.gg
+        G = gg.G
+        g = gy.to(x.dtype)
+        gx = g.matmul(wc) if ctx.needs_input_grad[0] else None
+        out_f, in_f = wc.shape
+        g2d, x2d = g.reshape(-1, out_f), x.reshape(-1, in_f)
+        gw = gg.view(weight)
+        if g2d.is_cuda and g2d.dtype == torch.bfloat16:
+            _wgrad_gemm(g2d, x2d, gw, G)
+        else:
+            gw.add_(torch.bmm(g2d.view(G, -1, out_f).transpose(1, 2).float(),
+                              x2d.view(G, -1, in_f).float()))
+        if bias is not None:
+            gw_b = gg.view(bias)
+            gw_b.add_(g2d.view(G, -1, out_f).float().sum(1))
+        return gx, None, None, None
+
+
+def linear_grouped(x, weight, bias, gg):
+    if torch.is_autocast_enabled(x.device.type) and x.is_floating_point():
+        x = x.to(torch.get_autocast_dtype(x.device.type))
+    elif x.dtype != weight.dtype:
+        x = x.to(weight.dtype)
+    return _LinearGrouped.apply(x, weight, bias, gg)
+
+
+# ------------------------------------------------------------ grouped affine
+class _AffineGrouped(torch.autograd.Function):
+    """y = xhat * w + b per channel (dim 1) of an [N, C, ...] tensor, with
+    per-group dw / db: the torch fallback of ghost BN under grouped grads."""
+
+    @staticmethod
+    def forward(ctx, xhat, weight, bias, gg):
+        shape = [1, -1] + [1] * (xhat.dim() - 2)
+        ctx.save_for_backward(xhat, weight)
+        ctx.params, ctx.gg = (weight, bias), gg
+        return xhat * weight.view(shape) + bias.view(shape)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xhat, weight = ctx.saved_tensors
+        w, b = ctx.params
+        G = ctx.gg.G
+        shape = [1, -1] + [1] * (xhat.dim() - 2)
+        red = [1] + list(range(3, xhat.dim() + 1))
+        gyf = gy.float()
+        gw = (gyf * xhat.float()).reshape(G, -1, *xhat.shape[1:]).sum(dim=red)
+        gb = gyf.reshape(G, -1, *xhat.shape[1:]).sum(dim=red)
+        ctx.gg.view(w).add_(gw)
+        ctx.gg.view(b).add_(gb)
+        return gy * weight.view(shape).to(gy.dtype), None, None, None

@@ -38,7 +38,8 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ..models.common import NativeConv2d, ghost_batchnorm, has_batchnorm
+from ..models.common import NativeConv2d, ghost_batchnorm, groupable, has_batchnorm
+from ..ops.grouped import GroupedGrads, grouped_grads
 from ..ops.nn import prepared_conv_weights
 from ..ops import CSVec
 from ..utils.logging import PhaseTimer
@@ -163,6 +164,9 @@ class FedModel:
         self.last_round = {}
         self.graphs = RoundGraphs(self) if self.device.type == "cuda" else None
         self._acct_meta = None  # accounting meta staged with the round's inputs
+        self._groupable = None  # grouped (per-client) weight gradients, ops/grouped.py
+        self._gindex = None
+        self._gbuf = None
 
     # ------------------------------------------------------------------ API
     def attach_optimizer(self, opt):
@@ -503,7 +507,14 @@ class FedModel:
             pm.append(ms)
         loss = torch.cat(pl).mean()
         mets = [torch.cat([m[i] for m in pm]).mean() for i in range(len(pm[0]))]
-        g = self.flat.g
+        self._client_tail(self.flat.g, work)
+        return loss, mets
+
+    def _client_tail(self, g: torch.Tensor, work: torch.Tensor):
+        """Client-side processing of one client's mean gradient ``g`` (in
+        place) before the transmit: clipping, weight decay at the client's
+        weights ``work``, worker-side DP (fed_worker.py:288-309, utils.py:257-258)."""
+        a = self.args
         if a.max_grad_norm is not None and a.mode != "sketch":
             nrm = ops.l2norm(g)
             ops.clip_noise(g, nrm, a.max_grad_norm, 0.0)
@@ -515,7 +526,6 @@ class FedModel:
             seed = (a.seed * 1000003 + self.round_idx * 8191 + self.ctx.rank) & 0x7FFFFFFF
             ops.clip_noise(g, nrm, a.l2_norm_clip, std, seed=seed, offset=self._dp_ctr)
             self._dp_ctr += self.d
-        return loss, mets
 
     def _compute_per_client(self, rb, order, starts, my_slots, mine, counts, W):
         a = self.args
@@ -531,7 +541,10 @@ class FedModel:
         prep = (prepared_conv_weights(self._native_3x3_weights())
                 if shared_w and self.device.type == "cuda" else nullcontext())
         with (self._autocast() if shared_w else nullcontext()), prep:
-            msum = self._per_client_loop(rb, order, starts, my_slots, mine, counts, W, out)
+            if shared_w and self._grouped_ok(counts[my_slots]):
+                msum = self._grouped_loop(rb, order, starts, my_slots, mine, counts, W, out)
+            else:
+                msum = self._per_client_loop(rb, order, starts, my_slots, mine, counts, W, out)
         if msum is None:  # no clients on this rank this round
             msum = torch.zeros(self._n_metrics_guess(), W, device=self.device)
         self._n_metrics = msum.shape[0]
@@ -546,6 +559,84 @@ class FedModel:
                   and m.weight.shape[0] % 64 == 0]
             self._n3x3 = ws
         return ws
+
+    # -------------------------------------------------------- grouped grads
+    def _grouped_ok(self, sizes: np.ndarray) -> bool:
+        """One merged forward/backward with per-client weight gradients
+        (ops/grouped.py) serves this round: every client computes at the
+        shared weights (checked by the caller), the model's layers can write
+        grouped gradients, and the clients have equal sizes (ghost BN groups
+        and batched wgrad GEMMs are equal-size groups)."""
+        a = self.args
+        if a.grouped_grads == "off" or a.do_test or len(sizes) < 2:
+            return False
+        if self._groupable is None:
+            self._groupable = groupable(self.model)
+        if not self._groupable:
+            if a.grouped_grads == "on":
+                raise ValueError("--grouped_grads on: the model has layers without grouped "
+                                 "weight gradients (models/common.py groupable)")
+            return False
+        return bool(np.all(sizes == sizes[0])) and int(sizes[0]) > 0
+
+    def _grouped_index(self):
+        if self._gindex is None:
+            f = self.flat
+            self._gindex = {id(p): (o, p.shape) for p, o in zip(f.params, f.offsets)}
+        return self._gindex
+
+    def _grouped_loop(self, rb, order, starts, my_slots, mine, counts, W, out):
+        """The clients of this rank in merged forward/backward passes that
+        write each client's mean gradient into its own row of a [G, d]
+        buffer, then the reference's per-client tail / transmit per row
+        (numerically the per-client path, one kernel chain per layer)."""
+        a = self.args
+        n = int(counts[my_slots[0]])
+        cap = max(1, int(a.grouped_gb * 2 ** 30) // (4 * self.d))
+        # microbatches hold whole clients (ghost-BN and gradient groups)
+        mb = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else 0
+        mbc = max(1, mb // n) if mb else len(mine)
+        per_pass = max(1, min(cap, len(mine)))
+        index = self._grouped_index()
+        rows_all, slots_all = [], []
+        for p0 in range(0, len(mine), per_pass):
+            slots = my_slots[p0:p0 + per_pass]
+            cl = mine[p0:p0 + per_pass]
+            Gp = len(slots)
+            buf = self._gbuf
+            if buf is None or buf.shape[0] < Gp:
+                buf = self._gbuf = torch.empty(Gp, self.d, device=self.device)
+            buf = buf[:Gp]
+            buf.zero_()
+            pos = np.concatenate([order[starts[s]:starts[s + 1]] for s in slots])
+            data = rb.take(pos)
+            inputs, targets = data[:-1], data[-1]
+            pe_l, ms_l = [], []
+            for c0 in range(0, Gp, mbc):
+                c1 = min(Gp, c0 + mbc)
+                e0, e1 = c0 * n, c1 * n
+                gg = GroupedGrads(c1 - c0, buf[c0:c1], index)
+                with grouped_grads(gg):
+                    pe, ms = self._fwd_bwd(tuple(x[e0:e1] for x in inputs), targets[e0:e1],
+                                           1.0 / n, groups=c1 - c0)
+                pe_l.append(pe)
+                ms_l.append(ms)
+            rows_all.append([torch.cat(pe_l)] + [torch.cat([m[i] for m in ms_l])
+                                                 for i in range(len(ms_l[0]))])
+            slots_all.append(np.repeat(slots, n))
+            for j, c in enumerate(cl):
+                g = buf[j]
+                self._client_tail(g, self.w)
+                transmit = self._finish_client(int(c), n, g)
+                if a.mode == "local_topk":
+                    idx, vals = transmit
+                    out.index_add_(0, idx, vals)
+                else:
+                    out.add_(transmit.view(-1))
+        rows = [torch.cat([r[i] for r in rows_all]) for i in range(len(rows_all[0]))]
+        slots_t = dist.h2d(np.concatenate(slots_all).astype(np.int64), self.device)
+        n_t = dist.h2d(counts.astype(np.float32), self.device)
+        return self._metric_sums(rows, slots_t, n_t, W)
 
     def _per_client_loop(self, rb, order, starts, my_slots, mine, counts, W, out):
         a = self.args
@@ -595,11 +686,12 @@ class FedModel:
     def _n_metrics_guess(self):
         return getattr(self, "_n_metrics", 2)
 
-    def _finish_client(self, c: int, n: int):
-        """fed_worker.py:184-230 local_step after the gradient: sketch/clip,
-        scale by n, local momentum / error, local top-k + masking."""
+    def _finish_client(self, c: int, n: int, g: Optional[torch.Tensor] = None):
+        """fed_worker.py:184-230 local_step after the gradient ``g`` (default:
+        the flat gradient): sketch/clip, scale by n, local momentum / error,
+        local top-k + masking."""
         a = self.args
-        g = self.flat.g
+        g = self.flat.g if g is None else g
         if a.mode == "sketch":
             sk = self.sketch.like(torch.zeros(a.num_rows, a.num_cols, device=self.device))
             sk.accumulateVec(g, float(n), dense=a.encode != "direct")

@@ -133,6 +133,13 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--merge_clients", choices=["auto", "on", "off"], default="auto",
                    help="merge the clients of a rank into one forward/backward when the "
                         "mode is linear per client (exact; see parallel/fed_model.py)")
+    g.add_argument("--grouped_grads", choices=["auto", "on", "off"], default="auto",
+                   help="for per-client (nonlinear) modes at shared weights: one merged "
+                        "forward/backward that writes every client's weight gradient "
+                        "separately (ops/grouped.py) instead of one pass per client")
+    g.add_argument("--grouped_gb", type=float, default=16.0,
+                   help="HBM budget (GB) of the [clients, d] grouped gradient buffer; more "
+                        "clients than fit run in several grouped passes")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
     g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
                    help="GPU Count-Sketch encode/query kernels: planned (precomputed "
