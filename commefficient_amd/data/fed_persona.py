@@ -94,6 +94,24 @@ def collate(records: List[dict], pad_id: int = 0):
     return ids, mc, lab, mcl, tt
 
 
+def label_positions(lab: torch.Tensor) -> torch.Tensor:
+    """[B, R] flat positions p = c*L + l of the tokens whose NEXT token is a
+    labelled LM target (lab[b, c, l+1] != -100), in order; -1 pads rows to the
+    batch's largest count R.  Lets the loss run the LM head on the R labelled
+    positions of an example instead of all C*L (the reference's HF model
+    computes logits for every position, gpt2_train.py:88-99; only the gold
+    reply is labelled, ~15 of ~260 positions per example)."""
+    B, C, L = lab.shape
+    nxt = torch.zeros(B, C, L, dtype=torch.bool)
+    nxt[:, :, :-1] = lab[:, :, 1:] != IGNORE
+    m = nxt.reshape(B, C * L)
+    cnt = m.sum(1)
+    R = max(1, int(cnt.max())) if B else 1
+    order = torch.argsort((~m).to(torch.int8), dim=1, stable=True)[:, :R]
+    keep = torch.arange(R).unsqueeze(0) < cnt.unsqueeze(1)
+    return torch.where(keep, order, torch.full_like(order, -1))
+
+
 def personachat_collate_fn(records):
     """DataLoader collate: records are (client_id, record-dict)."""
     cids = torch.tensor([r[0] for r in records], dtype=torch.long)

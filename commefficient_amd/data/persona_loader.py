@@ -8,7 +8,7 @@ import torch
 
 from ..parallel.fed_model import RoundBatch
 from .fed_dataset import FedSampler
-from .fed_persona import collate
+from .fed_persona import collate, label_positions
 
 
 def _to_dev(ts, device):
@@ -35,10 +35,11 @@ class PersonaFedLoader:
 
         def take(pos, r=r):
             recs = [ds[int(i)][1] for i in r[pos]]
-            ids, mc, lab, mcl, tt = _to_dev(collate(recs), dev)
-            return ids, mc, lab, tt, mcl
+            host = collate(recs)
+            ids, mc, lab, mcl, tt, lp = _to_dev(list(host) + [label_positions(host[2])], dev)
+            return ids, mc, lab, tt, lp, mcl
 
-        return RoundBatch(cids, take, n_inputs=4)
+        return RoundBatch(cids, take, n_inputs=5)
 
 
 class PersonaValLoader:

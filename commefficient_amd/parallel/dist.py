@@ -156,6 +156,22 @@ def all_reduce_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
+    """[rows, ...] on every rank -> [world * rows, ...] in rank order (one
+    RCCL all-gather; every rank passes the same shape)."""
+    if not _CTX.distributed:
+        return t
+    out = torch.empty((_CTX.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
+                      device=t.device)
+    if t.is_cuda and _CTX.backend == "gloo":
+        torch.cuda.current_stream().synchronize()
+        chunks = list(out.chunk(_CTX.world_size))
+        dist.all_gather(chunks, t.contiguous())
+        return out
+    dist.all_gather_into_tensor(out, t.contiguous())
+    return out
+
+
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if _CTX.distributed:
         dist.broadcast(t, src=src)

@@ -167,6 +167,7 @@ class FedModel:
         self._groupable = None  # grouped (per-client) weight gradients, ops/grouped.py
         self._gindex = None
         self._gbuf = None
+        self._sparse = None  # per-round local top-k list buffer (_sparse_plan)
 
     # ------------------------------------------------------------------ API
     def attach_optimizer(self, opt):
@@ -334,19 +335,27 @@ class FedModel:
             if merged:
                 res = self._compute_merged(rb, order, starts, my_slots, counts, W, clients)
             else:
-                res = self._compute_per_client(rb, order, starts, my_slots, mine, counts, W)
+                res = self._compute_per_client(rb, order, starts, my_slots, mine, counts, W,
+                                               clients)
         main, metric_sums = res  # main: transmit (device, main_numel); metric_sums [m, W]
         n_res = metric_sums.shape[0]
         payload = self._payload_buf(n_res * W)
-        if main is not None and main.data_ptr() != payload.data_ptr():
-            payload[:self.main_numel].copy_(main)
-        elif main is None:
-            payload[:self.main_numel].zero_()
         tail = payload[self.main_numel:]
         if metric_sums.data_ptr() != tail.data_ptr():
             tail.copy_(metric_sums.reshape(-1))
-        with self.timer.phase("allreduce"):
-            dist.all_reduce_(payload)
+        sparse_bytes = None
+        if self._sparse is not None:
+            # local top-k lists: all-gather them, all-reduce only the metrics
+            with self.timer.phase("allreduce"):
+                dist.all_reduce_(tail)
+                sparse_bytes = self._sparse_gather_into(payload[:self.main_numel])
+        else:
+            if main is not None and main.data_ptr() != payload.data_ptr():
+                payload[:self.main_numel].copy_(main)
+            elif main is None:
+                payload[:self.main_numel].zero_()
+            with self.timer.phase("allreduce"):
+                dist.all_reduce_(payload)
         # G = summed transmit / B  (fed_aggregator.py:332); the division is
         # folded into the server's momentum kernel (gscale) -> keep a view
         G = payload[:self.main_numel]
@@ -355,8 +364,15 @@ class FedModel:
         dl, ul = self.accountant.round(clients, self.round_idx, meta=self._acct_meta)
         self._acct_meta = None
         self._pending = (G, clients, False, 1.0 / B)
-        self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
-                           "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel())}
+        if sparse_bytes is not None:
+            Nw = self.ctx.world_size
+            self.last_round = {"clients": W, "examples": B, "payload_bytes": sparse_bytes,
+                               "wire_bytes": float((Nw - 1) * sparse_bytes)
+                               + self.accountant.wire_bytes_per_rank(tail.numel()),
+                               "sparse_allgather": True}
+        else:
+            self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
+                               "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel())}
         return [metrics[i] for i in range(n_res)] + [dl, ul]
 
     def _train_graph(self, gkey, rb, order, starts, my_slots, counts, W, B, clients):
@@ -527,10 +543,12 @@ class FedModel:
             ops.clip_noise(g, nrm, a.l2_norm_clip, std, seed=seed, offset=self._dp_ctr)
             self._dp_ctr += self.d
 
-    def _compute_per_client(self, rb, order, starts, my_slots, mine, counts, W):
+    def _compute_per_client(self, rb, order, starts, my_slots, mine, counts, W, clients=None):
         a = self.args
         out = self._transmit_buffer()
-        out.zero_()
+        self._sparse = self._sparse_plan(clients) if clients is not None else None
+        if self._sparse is None:
+            out.zero_()
         self._dp_ctr = getattr(self, "_dp_ctr", 0)
         # every client computes at the same weights (except FedAvg's local
         # steps and per-client top-k-down weights): one autocast context
@@ -627,12 +645,7 @@ class FedModel:
             for j, c in enumerate(cl):
                 g = buf[j]
                 self._client_tail(g, self.w)
-                transmit = self._finish_client(int(c), n, g)
-                if a.mode == "local_topk":
-                    idx, vals = transmit
-                    out.index_add_(0, idx, vals)
-                else:
-                    out.add_(transmit.view(-1))
+                self._emit(out, self._finish_client(int(c), n, g))
         rows = [torch.cat([r[i] for r in rows_all]) for i in range(len(rows_all[0]))]
         slots_t = dist.h2d(np.concatenate(slots_all).astype(np.int64), self.device)
         n_t = dist.h2d(counts.astype(np.float32), self.device)
@@ -676,12 +689,68 @@ class FedModel:
             msum[0, slot] = loss
             for i, m in enumerate(mets):
                 msum[1 + i, slot] = m
-            if a.mode == "local_topk":
-                idx, vals = transmit
-                out.index_add_(0, idx, vals)
-            else:
-                out.add_(transmit.view(-1))
+            self._emit(out, transmit)
         return msum
+
+    # ---------------------------------------------------- sparse transmit
+    def _emit(self, out: torch.Tensor, transmit):
+        """Add one client's transmit to the rank's upload: dense, or (local
+        top-k) its (index, value) pairs -- appended to the rank's list when the
+        round all-gathers sparse lists (``_sparse_plan``)."""
+        if isinstance(transmit, tuple):
+            idx, vals = transmit
+            sp = self._sparse
+            if sp is not None:
+                j = sp["n"]
+                sp["buf"][j, :sp["k"]].copy_(idx)
+                sp["buf"][j, sp["k"]:].copy_(vals.view(torch.int32))
+                sp["n"] = j + 1
+            else:
+                out.index_add_(0, idx, vals)
+        else:
+            out.add_(transmit.view(-1))
+
+    def _assign_counts(self, clients: np.ndarray):
+        N = self.ctx.world_size
+        if self.client_state.active:
+            return [int(np.sum(clients % N == r)) for r in range(N)]
+        W = len(clients)
+        return [(r + 1) * W // N - r * W // N for r in range(N)]
+
+    def _sparse_plan(self, clients: np.ndarray):
+        """local_topk upload as all-gathered (index, value) lists instead of a
+        dense d-vector all-reduce: a ring all-reduce moves
+        2(N-1)/N * 4d bytes per rank, the all-gather (N-1) * W_max * 8k; auto
+        picks the sparse lists when that is smaller (and the per-list
+        accumulation stays a few hundred launches)."""
+        a = self.args
+        if a.mode != "local_topk" or a.sparse_allgather == "off":
+            return None
+        N = self.ctx.world_size
+        counts = self._assign_counts(clients)
+        wmax = max(counts)
+        if a.sparse_allgather == "auto" and (N == 1 or wmax * N * a.k >= self.d
+                                              or wmax * N > 512):
+            return None
+        k = min(int(a.k), self.d)
+        buf = torch.zeros(wmax, 2 * k, dtype=torch.int32, device=self.device)
+        return {"buf": buf, "n": 0, "k": k, "counts": counts, "wmax": wmax}
+
+    def _sparse_gather_into(self, G: torch.Tensor) -> int:
+        """All-gather every rank's client lists and accumulate them into the
+        dense ``G`` in (rank, client) order -- each list has distinct indices,
+        so every index_add is collision-free and the sum is bitwise identical
+        on all ranks.  Returns the bytes each rank contributed."""
+        sp = self._sparse
+        self._sparse = None
+        k, wmax = sp["k"], sp["wmax"]
+        allb = dist.all_gather_rows(sp["buf"])
+        G.zero_()
+        for r, cnt in enumerate(sp["counts"]):
+            for j in range(cnt):
+                row = allb[r * wmax + j]
+                G.index_add_(0, row[:k].long(), row[k:].view(torch.float32))
+        return int(sp["buf"].numel() * 4)
 
     def _n_metrics_guess(self):
         return getattr(self, "_n_metrics", 2)

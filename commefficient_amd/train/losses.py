@@ -37,22 +37,49 @@ def gpt2_loss_train(model, inputs, targets, args, groups=None):
     ``groups``: per-example client slot of a merged multi-client batch (None:
     one client).  With --microbatch_size the token mean is per microbatch, as
     in the reference (fed_worker.py:266-287)."""
-    input_ids, mc_token_ids, lm_labels, token_type_ids = inputs
+    input_ids, mc_token_ids, lm_labels, token_type_ids = inputs[:4]
     m = model.model if hasattr(model, "model") and not hasattr(model, "transformer") else model
-    out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids)
-    lm_logits, mc_logits = out.logits, out.mc_logits
     B = input_ids.shape[0]
-    shift_logits = lm_logits[..., :-1, :].float()
-    shift_labels = lm_labels[..., 1:]
-    tok = F.cross_entropy(shift_logits.reshape(-1, shift_logits.size(-1)), shift_labels.reshape(-1),
-                          ignore_index=-100, reduction="none").view(B, -1)
-    mask = (shift_labels.reshape(B, -1) != -100).float()
-    tok_sum = (tok * mask).sum(1)
-    ntok = mask.sum(1)
+    if len(inputs) > 4 and hasattr(m, "transformer") and hasattr(m, "multiple_choice_head"):
+        # LM head only at the labelled positions (data/fed_persona.py
+        # label_positions): same loss, ~1/17 of the vocabulary GEMM + softmax
+        tok_sum, ntok, mc_logits = _lm_at_labels(m, input_ids, mc_token_ids, lm_labels,
+                                                  token_type_ids, inputs[4])
+    else:
+        out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids,
+                use_cache=False)
+        lm_logits, mc_logits = out.logits, out.mc_logits
+        shift_logits = lm_logits[..., :-1, :].float()
+        shift_labels = lm_labels[..., 1:]
+        tok = F.cross_entropy(shift_logits.reshape(-1, shift_logits.size(-1)),
+                              shift_labels.reshape(-1), ignore_index=-100,
+                              reduction="none").view(B, -1)
+        mask = (shift_labels.reshape(B, -1) != -100).float()
+        tok_sum = (tok * mask).sum(1)
+        ntok = mask.sum(1)
     lm = token_weighted(tok_sum, ntok, groups)
     mc = F.cross_entropy(mc_logits.float(), targets, reduction="none")
     acc = (mc_logits.argmax(-1) == targets).float()
     return args.lm_coef * lm + args.mc_coef * mc, [acc]
+
+
+def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos):
+    """(per-example sum of LM token losses, labelled-token count, mc logits)
+    with the LM head evaluated only at ``lm_pos`` [B, R] (-1 = pad)."""
+    hid = m.transformer(input_ids=input_ids, token_type_ids=token_type_ids,
+                        use_cache=False)[0]                           # [B, C, L, H]
+    B, C, L, H = hid.shape
+    mc_logits = m.multiple_choice_head(hid, mc_token_ids).squeeze(-1)
+    valid = lm_pos >= 0
+    p = lm_pos.clamp_min(0)
+    h = torch.gather(hid.reshape(B, C * L, H), 1, p.unsqueeze(-1).expand(-1, -1, H))
+    logits = m.lm_head(h)                                                # [B, R, V]
+    tgt = torch.gather(lm_labels.reshape(B, C * L), 1, (p + 1).clamp_max(C * L - 1))
+    tgt = torch.where(valid, tgt, torch.full_like(tgt, -100))
+    tok = F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), tgt.reshape(-1),
+                          ignore_index=-100, reduction="none").view(B, -1)
+    mask = (tgt != -100).float()
+    return (tok * mask).sum(1), mask.sum(1), mc_logits
 
 
 def token_weighted(tok_sum: torch.Tensor, ntok: torch.Tensor, groups=None) -> torch.Tensor:
@@ -72,9 +99,10 @@ def token_weighted(tok_sum: torch.Tensor, ntok: torch.Tensor, groups=None) -> to
 
 def gpt2_loss_val(model, inputs, targets, args):
     """Validation: (nll of the LM on the gold reply, mc accuracy) (gpt2_train.py:55-87)."""
-    input_ids, mc_token_ids, lm_labels, token_type_ids = inputs
+    input_ids, mc_token_ids, lm_labels, token_type_ids = inputs[:4]
     m = model.model if hasattr(model, "model") and not hasattr(model, "transformer") else model
-    out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids)
+    out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids,
+            use_cache=False)
     lm_logits, mc_logits = out.logits, out.mc_logits
     B = input_ids.shape[0]
     # the gold candidate is the last one (PERSONA collate order)

@@ -140,6 +140,10 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--grouped_gb", type=float, default=16.0,
                    help="HBM budget (GB) of the [clients, d] grouped gradient buffer; more "
                         "clients than fit run in several grouped passes")
+    g.add_argument("--sparse_allgather", choices=["auto", "on", "off"], default="auto",
+                   help="local_topk: all-gather every client's k (index, value) pairs "
+                        "instead of all-reducing the dense d-vector (auto: when that moves "
+                        "fewer bytes over xGMI)")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
     g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
                    help="GPU Count-Sketch encode/query kernels: planned (precomputed "

@@ -34,10 +34,13 @@ def _run(rank, world, port, mode, out_dir, rounds):
              "sketch": ["--error_type", "virtual", "--local_momentum", "0", "--virtual_momentum",
                         "0.9", "--k", "300", "--num_rows", "3", "--num_cols", "2000"],
              "local_topk": ["--error_type", "local", "--local_momentum", "0.9", "--k", "300"],
+             # (index, value) lists all-gathered instead of the dense all-reduce
+             "local_topk_sparse": ["--error_type", "local", "--local_momentum", "0.9", "--k",
+                                   "300", "--sparse_allgather", "on"],
              "fedavg": ["--local_momentum", "0", "--virtual_momentum", "0.5",
                         "--fedavg_batch_size", "2"]}[mode]
     lbs = "-1"
-    args = parse_args(argv=["--mode", mode, "--device", "cpu", "--dtype", "fp32",
+    args = parse_args(argv=["--mode", mode.replace("_sparse", ""), "--device", "cpu", "--dtype", "fp32",
                             "--num_clients", "40", "--num_workers", "6", "--local_batch_size", lbs,
                             "--dataset_name", "CIFAR10", "--synthetic"] + extra, probe_port=False)
     torch.manual_seed(0)
@@ -52,13 +55,16 @@ def _run(rank, world, port, mode, out_dir, rounds):
         loss, acc, dl, ul = fed(next(it))
         opt.step()
         losses.append(loss.clone())
+    if mode.endswith("_sparse"):
+        assert fed.last_round.get("sparse_allgather"), fed.last_round
     torch.save({"w": fed.w.clone(), "loss": torch.stack(losses),
                 "dl": fed.accountant.client_download.clone()},
                os.path.join(out_dir, f"r{rank}_w{world}.pt"))
     dist.shutdown()
 
 
-@pytest.mark.parametrize("mode", ["uncompressed", "sketch", "local_topk", "fedavg"])
+@pytest.mark.parametrize("mode", ["uncompressed", "sketch", "local_topk", "local_topk_sparse",
+                                  "fedavg"])
 def test_gloo_two_ranks_match_single_process(mode):
     rounds = 3
     with tempfile.TemporaryDirectory() as d:

@@ -78,3 +78,21 @@ def test_gpt2_merged_equals_per_client():
         opt.step()
         res.append(fed.w.clone())
     torch.testing.assert_close(res[0], res[1], rtol=1e-4, atol=1e-6)
+
+
+def test_gpt2_label_position_lm_head_matches_full_logits():
+    """LM head evaluated only at the labelled positions (data/fed_persona.py
+    label_positions) gives the full-logit loss and gradients."""
+    from commefficient_amd.data.fed_persona import label_positions
+    ids, mc_tok, labels, tt, mc = _batch()
+    labels[1, 0, 3:5] = ids[1, 0, 3:5]  # labels in a non-final candidate too
+    lp = label_positions(labels)
+    assert lp.shape[0] == 4 and (lp >= 0).sum() == (labels[..., 1:] != -100).sum()
+    grads = []
+    for inputs in ((ids, mc_tok, labels, tt), (ids, mc_tok, labels, tt, lp)):
+        model = _tiny().eval()
+        per_ex, _ = gpt2_loss_train(model, inputs, mc, _A())
+        per_ex.sum().backward()
+        grads.append((per_ex.detach(), torch.cat([p.grad.reshape(-1) for p in model.parameters()])))
+    torch.testing.assert_close(grads[0][0], grads[1][0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(grads[0][1], grads[1][1], rtol=1e-4, atol=1e-6)
