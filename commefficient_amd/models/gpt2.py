@@ -38,6 +38,10 @@ def build_double_heads(model_checkpoint: str = "gpt2", n_special: int = 5, n_lay
         cfg._attn_implementation = "sdpa"
     except Exception:
         pass
+    if is_gpt2 and cfg.activation_function == "gelu_new":
+        # the same tanh-approximation GELU as one fused kernel each way
+        # (torch's gelu(approximate="tanh")) instead of HF's ~8 elementwise ops
+        cfg.activation_function = "gelu_pytorch_tanh"
     model = (GPT2DoubleHeadsModel if is_gpt2 else OpenAIGPTDoubleHeadsModel)(cfg)
     if n_special:
         model.resize_token_embeddings(cfg.vocab_size + n_special, mean_resizing=False)

@@ -168,6 +168,16 @@ class FedModel:
         self._gindex = None
         self._gbuf = None
         self._sparse = None  # per-round local top-k list buffer (_sparse_plan)
+        # bf16 compute replica (parallel/flat.py make_bf16_shadow)
+        wc = getattr(args, "weight_cast", "auto")
+        if wc == "auto":
+            # HF transformer models (GPT-2): hundreds of per-weight casts per round
+            hf = any(hasattr(m, "config") and hasattr(m, "save_pretrained")
+                     for m in self.model.modules())
+            wc = "once" if (self.use_bf16 and hf and not self.has_bn) else "autocast"
+        if wc == "once" and not self.use_bf16:
+            wc = "autocast"
+        self._shadow = self.flat.make_bf16_shadow() if wc == "once" else None
 
     # ------------------------------------------------------------------ API
     def attach_optimizer(self, opt):
@@ -272,15 +282,21 @@ class FedModel:
         ``loss_weight * sum`` (per-client mean normalisation).  ``ex_groups``:
         per-example client slot (merged batches) for losses that normalise per
         client.  Returns the per-example losses and metrics (detached)."""
-        with self._autocast(cache=not capture):
-            with (ghost_batchnorm(self.model, groups) if (groups > 1 and self.has_bn)
+        model = self.model
+        shadow = self._shadow
+        if shadow is not None:
+            self.flat.refresh_shadow()  # one cast of the current (bound) weights
+            shadow.train(self.model.training)
+            model = shadow
+        with (self._autocast(cache=not capture) if shadow is None else nullcontext()):
+            with (ghost_batchnorm(model, groups) if (groups > 1 and self.has_bn)
                   else nullcontext()):
                 if want_grad:
                     kw = {"groups": ex_groups} if self._loss_groups else {}
                     per_ex, metrics = self.compute_loss_train(
-                        self.model, self._prep(inputs), targets, self.args, **kw)
+                        model, self._prep(inputs), targets, self.args, **kw)
                 else:
-                    per_ex, metrics = self.compute_loss_val(self.model, self._prep(inputs),
+                    per_ex, metrics = self.compute_loss_val(model, self._prep(inputs),
                                                             targets, self.args)
         if want_grad:
             if (loss_weight is None and not capture and per_ex.dtype == torch.float32
@@ -292,6 +308,8 @@ class FedModel:
                 if loss_weight is not None:
                     total = total * loss_weight
                 total.backward()
+            if shadow is not None:
+                self.flat.collect_shadow_grads()
         return per_ex.detach().float(), [m.detach().float() for m in metrics]
 
     # --------------------------------------------------------------- train

@@ -76,6 +76,41 @@ class FlatParams:
             if p.grad is None or p.grad.data_ptr() != self.g[o:o + n].data_ptr():
                 p.grad = self.g[o:o + n].view(p.shape)
 
+    # ----------------------------------------------------- bf16 compute copy
+    def make_bf16_shadow(self) -> nn.Module:
+        """A bf16 replica of the model for the forward/backward (``--weight_cast
+        once``): its trainable params are views of ONE flat bf16 buffer ``wb``,
+        refreshed from the fp32 master weights by a single cast kernel
+        (``refresh_shadow``), and its gradients are gathered into the fp32 flat
+        gradient by one concatenation + one add (``collect_shadow_grads``).
+        Autocast instead casts every weight tensor on each forward and every
+        weight gradient back to fp32 with its own cast + AccumulateGrad add
+        (~3 launches per parameter: ~450 for GPT-2)."""
+        import copy
+        shadow = copy.deepcopy(self.model).to(torch.bfloat16)
+        sp = trainable_params(shadow)
+        assert [p.shape for p in sp] == list(self.shapes)
+        self.wb = torch.empty(self.d, dtype=torch.bfloat16, device=self.device)
+        self.gb = torch.empty(self.d, dtype=torch.bfloat16, device=self.device)
+        for p, o, n, s in zip(sp, self.offsets, self.numels, self.shapes):
+            p.data = self.wb[o:o + n].view(s)
+            p.grad = None
+        self.shadow_params = sp
+        return shadow
+
+    def refresh_shadow(self) -> None:
+        self.wb.copy_(self.bound)
+
+    def collect_shadow_grads(self) -> None:
+        """g += the shadow's bf16 gradients (flat order); clears them."""
+        gs = []
+        for p, n in zip(self.shadow_params, self.numels):
+            gs.append(p.grad.reshape(-1) if p.grad is not None
+                      else torch.zeros(n, dtype=torch.bfloat16, device=self.device))
+            p.grad = None
+        torch.cat(gs, out=self.gb)
+        self.g.add_(self.gb)
+
     def ranges_of(self, params) -> List[Tuple[int, int]]:
         """Flat [start, end) ranges of the given parameters."""
         pos = {id(p): (o, o + n) for p, o, n in zip(self.params, self.offsets, self.numels)}

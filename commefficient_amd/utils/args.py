@@ -144,6 +144,11 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="local_topk: all-gather every client's k (index, value) pairs "
                         "instead of all-reducing the dense d-vector (auto: when that moves "
                         "fewer bytes over xGMI)")
+    g.add_argument("--weight_cast", choices=["auto", "once", "autocast"], default="auto",
+                   help="bf16 compute weights: 'once' = one cast of the flat fp32 master "
+                        "weights into a bf16 model replica per forward and one gradient "
+                        "gather back (parallel/flat.py); 'autocast' = torch.autocast per-op "
+                        "casts; auto = once for GPT-2 on a GPU, else autocast")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
     g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
                    help="GPU Count-Sketch encode/query kernels: planned (precomputed "

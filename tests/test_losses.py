@@ -1,6 +1,7 @@
 """Loss-function parity: the GPT-2 train loss reproduces the reference's HF
 lm_loss -- ONE token-weighted mean over all labelled tokens of a client's batch
 (gpt2_train.py:88-99) -- both per client and in a merged multi-client batch."""
+import pytest
 import torch
 import torch.nn.functional as F
 
@@ -96,3 +97,31 @@ def test_gpt2_label_position_lm_head_matches_full_logits():
         grads.append((per_ex.detach(), torch.cat([p.grad.reshape(-1) for p in model.parameters()])))
     torch.testing.assert_close(grads[0][0], grads[1][0], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(grads[0][1], grads[1][1], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpt2_weight_cast_once_matches_autocast_gpu():
+    """bf16 model replica refreshed by one cast per forward (--weight_cast
+    once, parallel/flat.py) vs per-op autocast: same update to bf16 accuracy,
+    and the flat fp32 gradient receives every parameter's gradient."""
+    dist.init("cuda")
+    ids, mc_tok, labels, tt, mc = (t.cuda() for t in _batch())
+    res = []
+    for wc in ("once", "autocast"):
+        model = _tiny()
+        args = parse_args(argv=["--mode", "uncompressed", "--local_momentum", "0",
+                                "--virtual_momentum", "0", "--num_workers", "2",
+                                "--local_batch_size", "2", "--device", "cuda", "--dtype", "bf16",
+                                "--num_clients", "2", "--weight_decay", "0",
+                                "--weight_cast", wc], probe_port=False)
+        fed = FedModel(model, gpt2_loss_train, args, num_clients=2)
+        assert (fed._shadow is not None) == (wc == "once")
+        opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), args, fed)
+        w0 = fed.w.clone()
+        loss = fed((torch.tensor([0, 0, 1, 1]), ids, mc_tok, labels, tt, mc))[0]
+        opt.step()
+        res.append((fed.w - w0, loss))
+    (d1, l1), (d2, l2) = res
+    torch.testing.assert_close(l1, l2, rtol=3e-2, atol=3e-2)
+    assert (d1 != 0).float().mean() > 0.9  # every parameter got its gradient
+    assert ((d1 - d2).norm() / d2.norm()) < 5e-2
