@@ -584,9 +584,14 @@ at::Tensor cs_hash_all_cpu(const at::Tensor& hashes, const at::Tensor& blk_off,
   return out;
 }
 
+// the exact (atomic-free) plan when its LDS segment fits, else the dense one
+bool any_plan_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* p) {
+  return planned_geometry(d, r, c, p) || planned_geometry_dense(d, r, c, p);
+}
+
 PlanGeom plan_geom_or_throw(int64_t d, int64_t r, int64_t c) {
   PlanGeom p;
-  TORCH_CHECK(planned_geometry(d, r, c, &p), "planned sketch: unsupported geometry d=", d,
+  TORCH_CHECK(any_plan_geometry(d, r, c, &p), "planned sketch: unsupported geometry d=", d,
               " r=", r, " c=", c);
   return p;
 }
@@ -653,11 +658,11 @@ at::Tensor cs_query_planned_hip(const at::Tensor& table, int64_t d, at::TensorLi
   return est;
 }
 
-// [tile, num_tiles, chunk, num_chunks] of the planned sketch, [] if unsupported
+// [tile, num_tiles, chunk, num_chunks, dense] of the planned sketch, [] if unsupported
 std::vector<int64_t> plan_geometry(int64_t d, int64_t r, int64_t c) {
   PlanGeom p;
-  if (!planned_geometry(d, r, c, &p)) return {};
-  return {p.tile, p.num_tiles, p.chunk, p.num_chunks};
+  if (!any_plan_geometry(d, r, c, &p)) return {};
+  return {p.tile, p.num_tiles, p.chunk, p.num_chunks, p.dense ? 1 : 0};
 }
 
 std::tuple<at::Tensor, at::Tensor> relu_maxpool_hip(const at::Tensor& x, int64_t k) {

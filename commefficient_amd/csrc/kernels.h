@@ -43,13 +43,18 @@ void launch_cs_encode_binned(float* table, const float* vec, const float* wvec,
 constexpr int64_t kPlanSegCap = 32767;    // max entries of one tile segment (LDS, 15-bit ids)
 constexpr int64_t kPlanStageCap = 65535;  // max entries of one coordinate chunk (16-bit slots)
 struct PlanGeom {
-  int64_t tile;        // buckets per tile (power of 2, 512..4096)
+  int64_t tile;        // buckets per tile (power of 2, 512..4096; 8192 when dense)
   int64_t num_tiles;   // ceil(r*c / tile)
   int64_t chunk;       // coordinates per chunk
   int64_t num_chunks;
+  bool dense = false;  // many entries per bucket (GPT-2): encode P2 accumulates
+                       // with LDS atomics, plan slot 2 holds chunk-major
+                       // in-tile bucket | sign instead of the bucket-order perm
 };
 // false when the geometry does not fit (too many entries per bucket)
 bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out);
+// the dense variant (any entries per bucket; false only for d*r >= 2^31)
+bool planned_geometry_dense(int64_t d, int64_t r, int64_t c, PlanGeom* out);
 struct PlannedArgs {
   const uint16_t* src_info;  // [d*r]  slot of (i,j) in its chunk's stage
   const uint16_t* ent_info;  // [d*r]  entry order: in-tile bucket | sign << 15

@@ -176,6 +176,87 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
   }
 }
 
+// ------------------------------------------------------ encode P2 (dense)
+// Many entries per bucket (GPT-2: ~249): a tile's segment (2M entries for
+// 8192 buckets) cannot sit in LDS in bucket order, so the tile accumulates
+// in LDS with float atomics instead.  grid = num_tiles x splits; block (t, s)
+// takes the runs of its 1/splits share of the chunks (read straight from the
+// tile's metadata rows in global memory), a half-wave per run with kB runs in
+// flight, and adds its partial tile to the table (plain stores when it owns
+// the tile, else contiguous 256-B-per-wave global atomics).  Not bitwise
+// deterministic (LDS atomic order) -- client-side encode only; every rank
+// still receives the identical all-reduced table.
+__global__ void __launch_bounds__(1024)
+enc_p2_dense_kernel(float* __restrict__ table, const float* __restrict__ vals,
+                    const uint16_t* __restrict__ cm_info, const int32_t* __restrict__ p2_src,
+                    const int32_t* __restrict__ p2_pos, uint32_t tile, uint32_t total_buckets,
+                    uint32_t num_chunks, uint32_t splits, bool overwrite) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* T = reinterpret_cast<float*>(smem);
+  const uint32_t t = blockIdx.x / splits, s = blockIdx.x - t * splits;
+  const uint32_t nt = blockDim.x;
+  for (uint32_t b = threadIdx.x; b < tile; b += nt) T[b] = 0.f;
+  __syncthreads();
+  const uint32_t c0 = static_cast<uint32_t>(static_cast<uint64_t>(num_chunks) * s / splits);
+  const uint32_t c1 = static_cast<uint32_t>(static_cast<uint64_t>(num_chunks) * (s + 1) / splits);
+  const int32_t* psrc = p2_src + static_cast<size_t>(t) * num_chunks;
+  const int32_t* ppos = p2_pos + static_cast<size_t>(t) * (num_chunks + 1);
+  const uint32_t mask = tile - 1;
+  constexpr uint32_t kB = 8;
+  const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = nt >> 5;
+  for (uint32_t cb = c0 + hw * kB; cb < c1; cb += nhw * kB) {
+    uint32_t src[kB], len[kB];
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t ch = cb + q;
+      src[q] = ch < c1 ? static_cast<uint32_t>(psrc[ch]) : 0u;
+      len[q] = ch < c1 ? static_cast<uint32_t>(ppos[ch + 1] - ppos[ch]) : 0u;
+    }
+    // runs average ~127 entries at GPT-2 size: 4 entries per lane in flight
+    for (uint32_t k0 = 0;; k0 += 128) {
+      float v[kB][4];
+      uint32_t info[kB][4];
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) {
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+          const uint32_t k = k0 + u * 32 + l32;
+          info[q][u] = 0xffffffffu;
+          v[q][u] = 0.f;
+          if (k < len[q]) {
+            v[q][u] = vals[src[q] + k];
+            info[q][u] = cm_info[src[q] + k];
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) {
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+          if (info[q][u] != 0xffffffffu)
+            atomicAdd(T + (info[q][u] & mask), signed_v(v[q][u], info[q][u]));
+      }
+      // half-wave-uniform exit: every lane of the half-wave sees the same len[]
+      bool more = false;
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) more |= k0 + 128 < len[q];
+      if (!more) break;
+    }
+  }
+  __syncthreads();
+  const uint32_t gb0 = t * tile;
+  for (uint32_t b = threadIdx.x; b < tile; b += nt) {
+    const uint32_t gb = gb0 + b;
+    if (gb >= total_buckets) break;
+    if (splits == 1) {
+      if (overwrite) table[gb] = T[b];
+      else table[gb] += T[b];
+    } else if (T[b] != 0.f) {
+      atomicAdd(table + gb, T[b]);
+    }
+  }
+}
+
 // -------------------------------------------------------------- query Q1
 __global__ void __launch_bounds__(256)
 qry_q1_kernel(const float* __restrict__ table, const uint16_t* __restrict__ ent_info,
@@ -259,26 +340,32 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
   __syncthreads();
   // runs -> stage: a half-wave per run (runs average ~30), kB runs per
   // half-wave in flight at once
+  // (dense plans: runs of ~127 entries -> up to DEEP x 32 entries per run in
+  // flight, the serial tail only beyond that)
   constexpr uint32_t kB = 16;
+  constexpr uint32_t DEEP = 4;
   const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
   for (uint32_t t0 = hw * kB; t0 < num_tiles; t0 += nhw * kB) {
-    float v[kB], v2[kB];
+    float v[kB][DEEP];
 #pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
       const uint32_t t = t0 + q;
-      v[q] = v2[q] = 0.f;
       const uint32_t len = t < num_tiles ? soff[t + 1] - soff[t] : 0u;
-      if (l32 < len) v[q] = vals[sbase[t] + l32];
-      if (l32 + 32 < len) v2[q] = vals[sbase[t] + l32 + 32];
+#pragma unroll
+      for (uint32_t u = 0; u < DEEP; ++u) {
+        v[q][u] = 0.f;
+        if (l32 + 32 * u < len) v[q][u] = vals[sbase[t] + l32 + 32 * u];
+      }
     }
 #pragma unroll
     for (uint32_t q = 0; q < kB; ++q) {
       const uint32_t t = t0 + q;
       if (t < num_tiles) {
         const uint32_t o = soff[t], len = soff[t + 1] - o;
-        if (l32 < len) stage[o + l32] = v[q];
-        if (l32 + 32 < len) stage[o + l32 + 32] = v2[q];
-        for (uint32_t k = l32 + 64; k < len; k += 32) stage[o + k] = vals[sbase[t] + k];
+#pragma unroll
+        for (uint32_t u = 0; u < DEEP; ++u)
+          if (l32 + 32 * u < len) stage[o + l32 + 32 * u] = v[q][u];
+        for (uint32_t k = l32 + 32 * DEEP; k < len; k += 32) stage[o + k] = vals[sbase[t] + k];
       }
     }
   }
@@ -373,6 +460,30 @@ bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
   return false;
 }
 
+bool planned_geometry_dense(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
+  if (d <= 0 || r < 1 || r > kMaxRows || c < 1 || d * r >= (int64_t{1} << 31)) return false;
+  PlanGeom p;
+  p.dense = true;
+  p.tile = 8192;  // in-tile bucket in 13 bits of the u16 entry info (sign: bit 15)
+  p.num_tiles = (r * c + p.tile - 1) / p.tile;
+  const int64_t tables = (2 * p.num_tiles + 1) * 4;
+  const int64_t stage_bytes = kLdsBytes - 1024 - tables;
+  if (stage_bytes < 64 * r * 4 * 16) return false;
+  int64_t chunk = (stage_bytes / 4 / r) / 64 * 64;
+  if (chunk > kPlanStageCap / r / 64 * 64) chunk = kPlanStageCap / r / 64 * 64;
+  if (chunk < 64) return false;
+  {
+    const int64_t cus = device_cus();
+    const int64_t rounds = (d + cus * chunk - 1) / (cus * chunk);
+    const int64_t bal = ((d + cus * rounds - 1) / (cus * rounds) + 63) / 64 * 64;
+    if (bal >= 64 && bal < chunk) chunk = bal;
+  }
+  p.chunk = chunk;
+  p.num_chunks = (d + chunk - 1) / chunk;
+  *out = p;
+  return true;
+}
+
 void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
                         const float* blk_sign, int32_t* out, hipStream_t stream) {
   if (g.d == 0) return;
@@ -405,6 +516,19 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
     case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
     default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
   }
+  if (p.dense) {
+    // enough blocks for every CU: split each tile's chunk range
+    uint32_t splits = 1;
+    while (nt * splits < 4 * static_cast<uint32_t>(device_cus()) && splits < 64) splits *= 2;
+    if (overwrite && splits > 1) {
+      (void)hipMemsetAsync(table, 0, static_cast<size_t>(r) * c * sizeof(float), stream);
+    }
+    hipLaunchKernelGGL(enc_p2_dense_kernel, dim3(nt * splits), dim3(1024), p.tile * 4, stream, table,
+                       a.vals, a.perm, a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
+                       static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks), splits,
+                       overwrite);
+    return;
+  }
   const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4 + (2 * p.num_chunks + 1) * 4;
   hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(1024), l2, stream, table, a.vals, a.perm,
                      a.csr, a.seg, a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
@@ -423,7 +547,9 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
     attr = true;
   }
   const uint32_t nt = static_cast<uint32_t>(p.num_tiles), ch = static_cast<uint32_t>(p.chunk);
-  const uint32_t splits = 4;
+  // >= 8 blocks per CU (dense plans have few, long tiles)
+  uint32_t splits = 4;
+  while (nt * splits < 8 * static_cast<uint32_t>(device_cus()) && splits < 64) splits *= 2;
   hipLaunchKernelGGL(qry_q1_kernel, dim3(nt * splits), dim3(256), p.tile * 4, stream, table,
                      a.ent_info, a.seg, a.vals, static_cast<uint32_t>(p.tile),
                      static_cast<uint32_t>(r * c), splits);

@@ -17,8 +17,11 @@ tile's whole segment of entries fits in LDS), then coordinate chunks, then
   vals             f32    [d*r] scratch shared by encode and query
 
 Built with device sorts (one-time O(rd log rd)): ~0.35 GB for ResNet-9.
-``build_plan`` returns None when the geometry does not fit (e.g. GPT-2's
-249 entries per bucket); callers then use the binned kernels.
+Dense geometries (GPT-2: ~249 entries per bucket, a tile's segment does not
+fit in LDS) get the dense plan: 8192-bucket tiles, encode P2 accumulating
+with LDS atomics, and slot 2 (``perm``) holding each entry's in-tile bucket |
+sign at its chunk-major position; the query kernels are the same.  ``build_plan``
+returns None only when d*r >= 2^31.
 """
 from __future__ import annotations
 
@@ -47,7 +50,7 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     geo = [int(v) for v in ops().plan_geometry(d, r, c)]
     if not geo:
         return None
-    tile, num_tiles, chunk, num_chunks = geo
+    tile, num_tiles, chunk, num_chunks, dense = geo
     n = d * r
     i64 = torch.int64
     hs = ops().cs_hash_all(hashes, blk_off, blk_sign, num_blocks, d, c, blk_off)  # [d, r]
@@ -65,7 +68,7 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     counts_tc = torch.bincount(key, minlength=num_tiles * num_chunks).view(num_tiles, num_chunks)
     del key
     seg_len = counts_tc.sum(1)
-    if int(seg_len.max()) > SEG_CAP:
+    if not dense and int(seg_len.max()) > SEG_CAP:
         return None
     base_tc = _excl_cumsum(counts_tc.reshape(-1)).view(num_tiles, num_chunks)
     base = base_tc.t().contiguous()                                  # [chunk, tile]
@@ -82,29 +85,23 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     lb = gb & (tile - 1)
     ent_info = torch.empty(n, dtype=torch.int16, device=device)
     ent_info[global_pos] = _to_i16(lb | sign_bit)
-    del lb, tile_id, global_pos
-    # bucket order: entries (in segment order) stably sorted by global bucket;
-    # encode P2 scatters each entry straight to its bucket-order slot, so the
-    # plan stores, at the entry's CHUNK-MAJOR position (P1's output layout),
-    # its segment-local bucket-order index | sign << 15
-    gb_pos = gb[order]
-    _, perm_pos = torch.sort(gb_pos, stable=True)           # bucket order -> segment pos
-    bo_of_pos = torch.empty_like(perm_pos)
-    bo_of_pos[perm_pos] = torch.arange(n, device=device, dtype=perm_pos.dtype)
-    tile_of_pos = sorted_key // num_chunks
-    bo_local = bo_of_pos - seg[tile_of_pos]                 # per segment position
-    del gb_pos, perm_pos, bo_of_pos, tile_of_pos, sorted_key
-    # entry e = i*r+j: segment position global_pos_e, chunk-major position
-    # chunk(i)*chunk*r + slot_e
-    cm = (torch.arange(d, device=device, dtype=i64) // chunk).repeat_interleave(r) * (chunk * r) \
-        + src_info.to(i64).bitwise_and(0xFFFF)
-    gpos_e = torch.empty_like(order)
-    gpos_e[order] = torch.arange(n, device=device, dtype=order.dtype)
-    perm = torch.empty(n, dtype=torch.int16, device=device)
-    perm[cm] = _to_i16(bo_local[gpos_e] | sign_bit)
-    del cm, gpos_e, bo_local, order, sign_bit
-    csr = torch.zeros(num_tiles * tile + 1, dtype=i64, device=device)
-    csr[1:] = torch.cumsum(torch.bincount(gb, minlength=num_tiles * tile), 0)
+    del tile_id, global_pos
+    if dense:
+        # encode P2 accumulates with LDS atomics: slot 2 holds each entry's
+        # in-tile bucket | sign at its CHUNK-MAJOR position (P1's output
+        # layout); no bucket-order permutation
+        cm = (torch.arange(d, device=device, dtype=i64) // chunk).repeat_interleave(r) \
+            * (chunk * r) + src_info.to(i64).bitwise_and(0xFFFF)
+        cm_info = torch.empty(n, dtype=torch.int16, device=device)
+        cm_info[cm] = _to_i16(lb | sign_bit)
+        del cm, lb, sign_bit, order, sorted_key
+        csr = torch.zeros(num_tiles * tile + 1, dtype=i64, device=device)
+        perm = cm_info
+    else:
+        del lb
+        perm, csr = _bucket_order(gb, order, sorted_key, num_chunks, seg, src_info, chunk, d, r,
+                                  n, sign_bit, tile, num_tiles, device)
+    del gb
     vals = torch.empty(n, dtype=torch.float32, device=device)
     # encode P2 gathers tile t's run of every chunk from the chunk-major P1
     # output: tile-major run metadata (start in chunk-major vals, start in
@@ -116,3 +113,33 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     i32 = torch.int32
     return [src_info, ent_info, perm, csr.to(i32), base.to(i32), off.to(i32), seg.to(i32), vals,
             p2_src.to(i32).contiguous(), p2_pos.to(i32)]
+
+
+def _bucket_order(gb, order, sorted_key, num_chunks, seg, src_info, chunk, d, r, n, sign_bit,
+                  tile, num_tiles, device):
+    """(perm, csr) of the exact plan: each entry's segment-local bucket-order
+    index | sign at its chunk-major position, and the bucket starts."""
+    i64 = torch.int64
+    # bucket order: entries (in segment order) stably sorted by global bucket;
+    # encode P2 scatters each entry straight to its bucket-order slot, so the
+    # plan stores, at the entry's CHUNK-MAJOR position (P1's output layout),
+    # its segment-local bucket-order index | sign << 15
+    gb_pos = gb[order]
+    _, perm_pos = torch.sort(gb_pos, stable=True)           # bucket order -> segment pos
+    bo_of_pos = torch.empty_like(perm_pos)
+    bo_of_pos[perm_pos] = torch.arange(n, device=device, dtype=perm_pos.dtype)
+    tile_of_pos = sorted_key // num_chunks
+    bo_local = bo_of_pos - seg[tile_of_pos]                 # per segment position
+    del gb_pos, perm_pos, bo_of_pos, tile_of_pos
+    # entry e = i*r+j: segment position global_pos_e, chunk-major position
+    # chunk(i)*chunk*r + slot_e
+    cm = (torch.arange(d, device=device, dtype=i64) // chunk).repeat_interleave(r) * (chunk * r) \
+        + src_info.to(i64).bitwise_and(0xFFFF)
+    gpos_e = torch.empty_like(order)
+    gpos_e[order] = torch.arange(n, device=device, dtype=order.dtype)
+    perm = torch.empty(n, dtype=torch.int16, device=device)
+    perm[cm] = _to_i16(bo_local[gpos_e] | sign_bit)
+    del cm, gpos_e, bo_local
+    csr = torch.zeros(num_tiles * tile + 1, dtype=i64, device=device)
+    csr[1:] = torch.cumsum(torch.bincount(gb, minlength=num_tiles * tile), 0)
+    return perm, csr

@@ -24,7 +24,7 @@ def _plan(d, c, r, nb, seed=3):
 
 def _gpos_of_slots(geo, plan, d, r):
     """global (segment-order) position of every entry (i, j), via the runs"""
-    tile, nt, chunk, nch = geo
+    tile, nt, chunk, nch = geo[:4]
     src_info, _, _, _, base, off, _, _ = plan[:8]
     gpos = torch.empty(d * r, dtype=torch.int64)
     for ch in range(nch):
@@ -37,7 +37,7 @@ def _gpos_of_slots(geo, plan, d, r):
 
 
 def _simulate_encode(geo, plan, vec, r, c):
-    tile, nt, chunk, nch = geo
+    tile, nt, chunk, nch = geo[:4]
     src_info, _, perm, csr, _, _, seg, _ = plan[:8]
     p2_src, p2_pos = plan[8].long(), plan[9].long()
     d = vec.numel()
@@ -63,7 +63,7 @@ def _simulate_encode(geo, plan, vec, r, c):
 
 
 def _simulate_query(geo, plan, table, d, r):
-    tile, nt, chunk, nch = geo
+    tile, nt, chunk, nch = geo[:4]
     _, ent_info, _, _, _, _, seg, _ = plan[:8]
     n = d * r
     seg = seg.to(torch.int64)
@@ -81,7 +81,7 @@ def _simulate_query(geo, plan, table, d, r):
 def test_plan_invariants_and_simulated_kernels(d, c, r, nb):
     sk, geo, plan = _plan(d, c, r, nb)
     assert geo and plan is not None
-    tile, nt, chunk, nch = geo
+    tile, nt, chunk, nch = geo[:4]
     src_info, ent_info, perm, csr, base, off, seg, vals = plan[:8]
     n = d * r
     assert nt * tile >= r * c and nch * chunk >= d
@@ -110,11 +110,58 @@ def test_plan_invariants_and_simulated_kernels(d, c, r, nb):
     assert torch.equal(est, sk.like(ref.table).query())
 
 
-def test_plan_unsupported_geometry_returns_none():
-    # ~250 entries per bucket (GPT-2 scale ratio): segments cannot fit in LDS
-    assert list(_ops().plan_geometry(2_000_000, 5, 8000)) == []
-    sk = CSVec(2_000_000, 8000, 5, device="cpu")
-    assert build_plan(sk.hashes, sk.blk_off, sk.blk_sign, 1, 2_000_000, 5, 8000, "cpu") is None
+def _simulate_encode_dense(geo, plan, vec, r, c):
+    """Dense plan: P1 as the exact plan, P2 adds each run entry (chunk-major
+    in-tile bucket | sign in plan slot 2) into its tile."""
+    tile, nt, chunk, nch = geo[:4]
+    src_info, _, cm_info = plan[:3]
+    p2_src, p2_pos = plan[8].long(), plan[9].long()
+    d = vec.numel()
+    cm = (torch.arange(d) // chunk).repeat_interleave(r) * (chunk * r) + _u16(src_info)
+    vals = torch.zeros(nch * chunk * r, dtype=torch.float64)
+    vals[cm] = vec.double().repeat_interleave(r)
+    info = _u16(cm_info)
+    table = torch.zeros(nt * tile, dtype=torch.float64)
+    for t in range(nt):
+        for ch in range(nch):
+            a, ln = int(p2_src[t, ch]), int(p2_pos[t, ch + 1] - p2_pos[t, ch])
+            x = torch.arange(a, a + ln)
+            sv = torch.where((info[x] & 0x8000) != 0, -vals[x], vals[x])
+            table.index_add_(0, t * tile + (info[x] & (tile - 1)), sv)
+    return table[:r * c].view(r, c)
+
+
+@pytest.mark.parametrize("d,c,r,nb", [(2_000_000, 8000, 5, 20), (300_000, 1000, 3, 1)])
+def test_dense_plan_for_many_entries_per_bucket(d, c, r, nb):
+    """~250 entries per bucket (GPT-2's ratio): the exact plan's segments do
+    not fit in LDS, the dense plan (LDS-atomic encode P2) takes over; the
+    query kernels (Q1/Q2) are the exact plan's."""
+    sk, geo, plan = _plan(d, c, r, nb)
+    assert geo and geo[4] == 1 and geo[0] == 8192 and plan is not None
+    g = torch.Generator().manual_seed(0)
+    vec = torch.randn(d, generator=g)
+    ref = sk.like()
+    ref.accumulateVec(vec)
+    sim = _simulate_encode_dense(geo, plan, vec, r, c)
+    torch.testing.assert_close(sim.float(), ref.table, rtol=1e-4, atol=1e-4)
+    est = _simulate_query(geo, plan, ref.table, d, r)
+    assert torch.equal(est, sk.like(ref.table).query())
+
+
+@pytest.mark.gpu
+def test_dense_planned_gpu_kernels_match_cpu():
+    d, c, r, nb = 3_000_001, 12007, 5, 20
+    cpu = CSVec(d, c, r, device="cpu", numBlocks=nb, seed=5)
+    gpu = CSVec(d, c, r, device="cuda", numBlocks=nb, seed=5, kernel="planned")
+    assert gpu._use_plan()
+    g = torch.Generator().manual_seed(1)
+    v, w = torch.randn(d, generator=g), torch.randn(d, generator=g)
+    cpu.accumulateVec(v, 0.5, w, 1e-2)
+    gpu.accumulateVec(v.cuda(), 0.5, w.cuda(), 1e-2, overwrite=True)
+    torch.testing.assert_close(gpu.table.cpu(), cpu.table, rtol=1e-4, atol=1e-4)
+    gpu.accumulateVec(v.cuda(), 0.5, w.cuda(), 1e-2)  # += path
+    torch.testing.assert_close(gpu.table.cpu(), 2 * cpu.table, rtol=1e-4, atol=1e-4)
+    assert torch.equal(gpu.like(cpu.table.cuda()).query().cpu(), cpu.query())
 
 
 @pytest.mark.gpu
