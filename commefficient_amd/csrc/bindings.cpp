@@ -851,8 +851,14 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
                                                     const c10::optional<at::Tensor>& b, int64_t G, double eps,
                                                     double momentum, const c10::optional<at::Tensor>& run_mean,
                                                     const c10::optional<at::Tensor>& run_var, bool relu,
-                                                    const c10::optional<at::Tensor>& nbt) {
+                                                    const c10::optional<at::Tensor>& nbt,
+                                                    const c10::optional<at::Tensor>& addend) {
   check_nhwc_bf16(x, "ghost_bn: x");
+  const bool has_add = addend.has_value() && addend->defined();
+  if (has_add) {
+    check_nhwc_bf16(*addend, "ghost_bn: addend");
+    TORCH_CHECK(addend->sizes() == x.sizes(), "ghost_bn: addend must have x's shape");
+  }
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   TORCH_CHECK(G >= 1 && N % G == 0 && C % 8 == 0 && C <= 2048, "ghost_bn: G | N, C % 8 == 0, C <= 2048");
   const int64_t M = N / G * HW;
@@ -883,7 +889,8 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
   launch_bn_fwd(bf16_ptr(x), wp, bp, static_cast<int>(G), static_cast<int>(M), static_cast<int>(C),
                 static_cast<float>(eps), static_cast<float>(momentum), rm, rv, part.data_ptr<float>(),
                 stat.data_ptr<float>(), ab.data_ptr<float>(), relu, nb,
-                reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream());
+                reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream(),
+                has_add ? bf16_ptr(*addend) : nullptr);
   return {y, stat};
 }
 
@@ -896,7 +903,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
                                                                 const c10::optional<at::Tensor>& gw,
                                                                 const c10::optional<at::Tensor>& gb,
                                                                 const c10::optional<at::Tensor>& ggw,
-                                                                const c10::optional<at::Tensor>& ggb) {
+                                                                const c10::optional<at::Tensor>& ggb,
+                                                                const c10::optional<at::Tensor>& dadd) {
   check_nhwc_bf16(x, "ghost_bn_bwd: x");
   check_nhwc_bf16(dy, "ghost_bn_bwd: dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "ghost_bn_bwd: dy shape");
@@ -904,6 +912,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
   if (fused_relu) {
     check_nhwc_bf16(*y_relu, "ghost_bn_bwd: y");
     TORCH_CHECK(y_relu->sizes() == x.sizes(), "ghost_bn_bwd: y shape");
+  }
+  if (dadd.has_value() && dadd->defined()) {  // receives the ReLU-masked dy
+    check_nhwc_bf16(*dadd, "ghost_bn_bwd: dadd");
+    TORCH_CHECK(dadd->sizes() == x.sizes() && fused_relu, "ghost_bn_bwd: dadd needs y and x's shape");
   }
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   const int64_t M = N / G * HW;
@@ -945,7 +957,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
                 static_cast<int>(C), part.data_ptr<float>(), coef.data_ptr<float>(), dwp, dbp,
                 into ? 1.f : 0.f, reinterpret_cast<uint16_t*>(dx.data_ptr()), cur_stream(),
                 grouped ? ggw->data_ptr<float>() : nullptr, grouped ? ggb->data_ptr<float>() : nullptr,
-                grouped ? ggw->stride(0) : 0);
+                grouped ? ggw->stride(0) : 0,
+                (dadd.has_value() && dadd->defined()) ? reinterpret_cast<uint16_t*>(dadd->data_ptr())
+                                                      : nullptr);
   return {dx, dw, db};
 }
 
@@ -1221,10 +1235,11 @@ TORCH_LIBRARY(commeff, m) {
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
-        "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None) -> (Tensor, Tensor)");
+        "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None, Tensor? addend=None) "
+        "-> (Tensor, Tensor)");
   m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None, "
-        "Tensor(a!)? gw=None, Tensor(b!)? gb=None, Tensor(c!)? ggw=None, Tensor(d!)? ggb=None) "
-        "-> (Tensor, Tensor, Tensor)");
+        "Tensor(a!)? gw=None, Tensor(b!)? gb=None, Tensor(c!)? ggw=None, Tensor(d!)? ggb=None, "
+        "Tensor(e!)? dadd=None) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");

@@ -9,6 +9,7 @@
 //
 // Forward  (3 launches): partial shifted sums per (group, pixel slab) ->
 //          per-(group, channel) mean / rstd and y = x A + B coefficients
+//          (optionally y = relu(x A + B + residual): a ResNet block's tail)
 //          (+ running-stat update with the group-averaged moments, fixed
 //          order) -> y, 16-byte loads/stores.
 // Backward (3 launches): partial sums of dy and dy*xhat per (group, slab) ->
@@ -315,11 +316,14 @@ __device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
 }
 
 // fwd: y = x A + B ;  bwd: dx = P dy + Q x + R  (per-(group, channel) coefficients)
+// ``aux``: forward -- a residual addend (y = act(x A + B + addend)); backward --
+// an output for the ReLU-masked dy (the addend's gradient)
 template <bool BWD>
 __global__ void __launch_bounds__(256)
 bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                 const uint16_t* __restrict__ ymask, const float* __restrict__ coef, int C, int M,
-                uint32_t nchunks, bool relu, uint16_t* __restrict__ out) {
+                uint32_t nchunks, bool relu, uint16_t* __restrict__ out,
+                uint16_t* __restrict__ aux) {
   const uint32_t CL = static_cast<uint32_t>(C) >> 3;
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nchunks; i += gridDim.x * 256u) {
     const uint32_t p = i / CL;
@@ -333,6 +337,12 @@ bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
     if (!BWD) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f[j] * A[j] + B[j];
+      if (aux != nullptr) {  // fused residual add (before the ReLU)
+        float r8[8];
+        unpack8(*reinterpret_cast<const u4*>(aux + static_cast<size_t>(i) * 8), r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += r8[j];
+      }
       if (relu) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
@@ -341,6 +351,7 @@ bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
       float d[8], R[8];
       u4 dv = *reinterpret_cast<const u4*>(dy + static_cast<size_t>(i) * 8);
       if (ymask != nullptr) dv = relu_mask8(dv, *reinterpret_cast<const u4*>(ymask + static_cast<size_t>(i) * 8));
+      if (aux != nullptr) *reinterpret_cast<u4*>(aux + static_cast<size_t>(i) * 8) = dv;
       unpack8(dv, d);
       load8f(k + 2 * C, R);
 #pragma unroll
@@ -369,7 +380,8 @@ int bn_slabs(int G, int M) {
 
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C,
                    float eps, float momentum, float* run_mean, float* run_var, float* part,
-                   float* stat, float* ab, bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream) {
+                   float* stat, float* ab, bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream,
+                   const uint16_t* addend) {
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
                      nullptr, C, M, S, part);
@@ -377,13 +389,14 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
                      b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var, nbt);
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
-                     nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y);
+                     nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
+                     const_cast<uint16_t*>(addend));
 }
 
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw, float* gdb,
-                   int64_t gstride) {
+                   int64_t gstride, uint16_t* dadd) {
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
                      S, part);
@@ -391,7 +404,7 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu
                      C, M, S, G, coef, dw, db, beta, gdw, gdb, gstride);
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
-                     coef, C, M, static_cast<uint32_t>(nchunks), false, dx);
+                     coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd);
 }
 
 }  // namespace commeff

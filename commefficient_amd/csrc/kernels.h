@@ -244,11 +244,12 @@ int bn_slabs(int G, int M);
 // relu: y = max(BN(x), 0); its backward passes y_relu (the saved output)
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C, float eps,
                    float momentum, float* run_mean, float* run_var, float* part, float* stat, float* ab,
-                   bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream);
+                   bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream,
+                   const uint16_t* addend = nullptr);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw = nullptr,
-                   float* gdb = nullptr, int64_t gstride = 0);
+                   float* gdb = nullptr, int64_t gstride = 0, uint16_t* dadd = nullptr);
 
 constexpr int kClientMeanRows = 4;
 struct ClientMeanRows {

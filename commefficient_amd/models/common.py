@@ -65,12 +65,17 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
         # relu(bn(x)) in one module (one native kernel each way when merged)
         self.fuse_relu = fuse_relu
 
-    def forward(self, x):
+    def forward(self, x, addend=None):
+        """``addend``: a residual block's tail ``relu(bn(x) + addend)`` (one
+        native pass each way; the module's own ``fuse_relu`` is ignored)."""
+        if addend is not None:
+            y, done = self._bn(x, addend)
+            return y if done else F.relu(y + addend)
         y, relu_done = self._bn(x)
         return F.relu(y) if self.fuse_relu and not relu_done else y
 
-    def _bn(self, x):
-        """(normalised x, whether the fused ReLU was already applied)"""
+    def _bn(self, x, addend=None):
+        """(normalised x, whether the fused ReLU (and the addend) was applied)"""
         G = max(1, self.ghost_groups)
         gg = _grouped.active() if (self.training and self.affine) else None
         if gg is not None and gg.view(self.weight) is None:
@@ -80,13 +85,15 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
             # native per-group BN (csrc/bn.hip), also for one group (the
             # per-client path): MIOpen's bf16 NHWC BN took 5 launches + casts
             track = self.track_running_stats and self.running_mean is not None
+            fused_add = addend is not None and addend.shape == x.shape and addend.is_cuda
             y = ghost_batch_norm(x, self.weight if self.affine else None,
                                  self.bias if self.affine else None, G, self.eps, self.momentum,
                                  self.running_mean if track else None,
-                                 self.running_var if track else None, relu=self.fuse_relu,
+                                 self.running_var if track else None,
+                                 relu=fused_add or (self.fuse_relu and addend is None),
                                  num_batches_tracked=self.num_batches_tracked if track else None,
-                                 gg=gg)
-            return y, self.fuse_relu
+                                 gg=gg, addend=addend if fused_add else None)
+            return y, (fused_add or self.fuse_relu) if addend is None or fused_add else False
         if gg is None and (not self.training or G <= 1):
             return super().forward(x), False
         N, C = x.shape[0], x.shape[1]

@@ -52,14 +52,21 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
         out = _norm_relu(self.bn1, self.relu, self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        return _norm_add_relu(self.bn2, self.relu, self.conv2(out), idt)
 
 
 def _norm_relu(norm: nn.Module, relu: nn.Module, x):
     """relu(norm(x)); a fused GhostBatchNorm2d already applied the ReLU."""
     y = norm(x)
     return y if getattr(norm, "fuse_relu", False) else relu(y)
+
+
+def _norm_add_relu(norm: nn.Module, relu: nn.Module, x, idt):
+    """relu(norm(x) + idt): one native pass each way with GhostBatchNorm2d
+    (the residual add and the ReLU in the BN apply kernels)."""
+    if isinstance(norm, GhostBatchNorm2d):
+        return norm(x, addend=idt)
+    return relu(norm(x) + idt)
 
 
 class Bottleneck(nn.Module):
@@ -84,8 +91,7 @@ class Bottleneck(nn.Module):
         idt = x if self.downsample is None else self.downsample(x)
         out = _norm_relu(self.bn1, self.relu, self.conv1(x))
         out = _norm_relu(self.bn2, self.relu, self.conv2(out))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        return _norm_add_relu(self.bn3, self.relu, self.conv3(out), idt)
 
 
 class ResNet(nn.Module):

@@ -310,13 +310,16 @@ class _GhostBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var, relu, nbt,
-                gg=None):
+                gg=None, addend=None):
+        if addend is not None:  # y = relu(bn(x) + addend): a residual block's tail
+            addend = addend.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         y, stat = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
-                                      running_mean, running_var, bool(relu), nbt)
+                                      running_mean, running_var, bool(relu), nbt, addend)
         ctx.save_for_backward(x, stat, weight, y if relu else None)
         ctx.groups = int(groups)
         ctx.params = (weight, bias)
         ctx.gg = gg
+        ctx.has_add = addend is not None
         return y
 
     @staticmethod
@@ -326,13 +329,16 @@ class _GhostBN(torch.autograd.Function):
         # existing fp32 .grad tensors (FedModel's flat-buffer views) receive
         # dweight / dbias in place: no AccumulateGrad launches
         pw, pb = ctx.params
+        # the residual addend's gradient: the ReLU-masked dy, written by the
+        # backward apply kernel
+        dadd = torch.empty_like(dy) if ctx.has_add else None
         if ctx.gg is not None and pw is not None:
             # grouped (per-client) dweight / dbias rows, ops/grouped.py; the
             # BN groups are the gradient groups
             assert ctx.gg.G == ctx.groups, "grouped grads need ghost-BN groups == gradient groups"
             dx, _, _ = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y, None, None,
-                                           ctx.gg.view(pw), ctx.gg.view(pb))
-            return dx, None, None, None, None, None, None, None, None, None, None
+                                           ctx.gg.view(pw), ctx.gg.view(pb), dadd)
+            return dx, None, None, None, None, None, None, None, None, None, None, dadd
         gw = pw.grad if pw is not None else None
         gb = pb.grad if pb is not None else None
         into = (gw is not None and gb is not None and gw.dtype == torch.float32
@@ -340,10 +346,11 @@ class _GhostBN(torch.autograd.Function):
                 and gw.device == x.device and gb.device == x.device
                 and ctx.needs_input_grad[1] and ctx.needs_input_grad[2])
         dx, dw, db = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y,
-                                         gw if into else None, gb if into else None)
+                                         gw if into else None, gb if into else None, None, None,
+                                         dadd)
         if weight is None or into:
             dw = db = None
-        return dx, dw, db, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, dadd
 
 
 def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
@@ -355,12 +362,14 @@ def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
 
 def ghost_batch_norm(x, weight, bias, groups: int, eps: float, momentum: float,
                      running_mean=None, running_var=None, relu: bool = False,
-                     num_batches_tracked=None, gg=None):
+                     num_batches_tracked=None, gg=None, addend=None):
     """Per-group batch norm (+ ReLU when ``relu``) on the native kernels; the
     running statistics and ``num_batches_tracked`` are updated on the device.
-    ``gg``: per-group weight gradients (ops/grouped.py)."""
+    ``gg``: per-group weight gradients (ops/grouped.py).  ``addend``: y =
+    relu(bn(x) + addend) in the same pass (needs ``relu``)."""
+    assert addend is None or relu, "the fused residual add is followed by the ReLU"
     return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var, relu,
-                          num_batches_tracked, gg)
+                          num_batches_tracked, gg, addend)
 
 
 # ------------------------------------------------------------ loss

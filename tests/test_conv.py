@@ -410,6 +410,39 @@ def test_ghost_bn_matches_fp32(N, G, C, H, affine, relu):
         torch.testing.assert_close(bn.bias.grad, 2 * gb0, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("N, G, C, H", [(8, 2, 64, 7), (12, 4, 256, 4)])
+def test_ghost_bn_residual_add_relu_matches_fp32(N, G, C, H):
+    """relu(bn(x) + addend) in the BN apply kernels (a ResNet block tail):
+    forward, dx, d(addend) and dweight / dbias vs the fp32 composition."""
+    from commefficient_amd.models.common import GhostBatchNorm2d
+    g = torch.Generator(device="cuda").manual_seed(C)
+    x = _nhwc((torch.randn(N, C, H, H, device="cuda", generator=g) + 1).to(torch.bfloat16))
+    a = _nhwc(torch.randn(N, C, H, H, device="cuda", generator=g).to(torch.bfloat16))
+    x.requires_grad_(True)
+    a.requires_grad_(True)
+    bn = GhostBatchNorm2d(C).cuda()
+    ref = GhostBatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, device="cuda", generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, device="cuda", generator=g))
+        ref.weight.copy_(bn.weight)
+        ref.bias.copy_(bn.bias)
+    bn.ghost_groups = ref.ghost_groups = G
+    gy = torch.randn(N, C, H, H, device="cuda", generator=g)
+    y = bn(x, addend=a)
+    (y.float() * gy).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    ar = a.detach().float().requires_grad_(True)
+    yr = torch.relu(ref(xr) + ar)
+    (yr * gy.to(torch.bfloat16).float()).sum().backward()
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, yr)
+    _close(x.grad, xr.grad, rel=3e-2)
+    _close(a.grad, ar.grad, rel=1e-2)
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("N,C,H,K", [(600, 64, 32, 128), (520, 128, 16, 256)])
 def test_fwd_large_batch_matches_fp32(N, C, H, K):
     """Batches big enough for the 256-pixel halo tile (8 waves) -- forward,
