@@ -1039,6 +1039,44 @@ void conv3x3_wgrad_into_hip(const at::Tensor& dy, const at::Tensor& x, at::Tenso
   conv3x3_wgrad_run(dy, x, splits, dw, 1.f);
 }
 
+// grouped (per-client) weight gradients: dw [G, K*C*9] fp32 rows (any row
+// stride) += the wgrad of each of G equal pixel groups -- one GEMM launch for
+// every group's split-K slabs and one per-group reduction (ops/grouped.py)
+void conv3x3_wgrad_grouped_hip(const at::Tensor& dy, const at::Tensor& x, int64_t G, at::Tensor dw) {
+  check_nhwc_bf16(dy, "conv3x3_wgrad_grouped: dy");
+  check_nhwc_bf16(x, "conv3x3_wgrad_grouped: x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "conv3x3_wgrad_grouped: shapes");
+  TORCH_CHECK(conv3x3_supported(static_cast<int>(C), static_cast<int>(K)) && K % 128 == 0,
+              "conv3x3_wgrad_grouped: C % 64 and K % 128 must be 0");
+  TORCH_CHECK(G >= 1 && N % G == 0, "conv3x3_wgrad_grouped: G must divide the batch");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.size(0) == G &&
+                  dw.size(1) == K * C * 9 && dw.stride(1) == 1 && dw.device() == x.device(),
+              "conv3x3_wgrad_grouped: dw must be f32 [G, K*C*9] rows");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int P = static_cast<int>(N * H * W);
+  const int Pg = P / static_cast<int>(G);
+  const int total = conv3x3_wgrad_splits(P, static_cast<int>(K), static_cast<int>(C));
+  int spg = static_cast<int>((total + G - 1) / G);
+  const int steps_g = (Pg + 63) / 64;
+  const int min_steps = 16;  // a split keeps >= 16 K-steps
+  if (spg > steps_g / min_steps) spg = steps_g / min_steps;
+  if (spg < 1) spg = 1;
+  auto slab = at::empty({G * spg * K * 9 * C}, dw.options());
+  ConvWgradArgs a;
+  a.dy = bf16_ptr(dy);
+  a.x = bf16_ptr(x);
+  a.slab = slab.data_ptr<float>();
+  a.P = P;
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.splits = static_cast<int>(G) * spg;
+  launch_conv3x3_wgrad_grouped(a, static_cast<int>(G), dw.data_ptr<float>(), dw.stride(0), 1.f,
+                               cur_stream());
+}
+
 void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits, at::Tensor& dw,
                        float beta) {
   check_nhwc_bf16(dy, "conv3x3_wgrad: dy");
@@ -1242,6 +1280,7 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor(e!)? dadd=None) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
+  m.def("conv3x3_wgrad_grouped(Tensor dy, Tensor x, int G, Tensor(a!) dw) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("conv_weight_prep_multi(Tensor[] ws) -> Tensor[]");
   m.def("account_round(Tensor last_mod, Tensor meta, int T, int W, Tensor(a!) client_dl, "
@@ -1322,6 +1361,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("ghost_bn_bwd", &ghost_bn_bwd_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
   m.impl("conv3x3_wgrad_into", &conv3x3_wgrad_into_hip);
+  m.impl("conv3x3_wgrad_grouped", &conv3x3_wgrad_grouped_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);
   m.impl("conv_weight_prep_multi", &conv_weight_prep_multi_hip);
   m.impl("conv_prep_fwd", &conv_prep_fwd_hip);

@@ -549,6 +549,22 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
 }
 
 // ------------------------------------------------------------------ wgrad
+// pixel range [pbeg, pend) of one split: consecutive steps_per_split * BK
+// pixels, or (grouped) the split's share of its group's pixels -- rows past
+// pend are masked, so a range need not start or end on a K-step
+__device__ __forceinline__ void wgrad_split_range(const ConvWgradArgs& a, int split, int* pbeg,
+                                                  int* pend) {
+  if (a.group_px > 0) {
+    const int g = split / a.splits_per_group, s = split - g * a.splits_per_group;
+    const int g0 = g * a.group_px;
+    *pbeg = g0 + s * a.steps_per_split * BK;
+    *pend = min(g0 + a.group_px, *pbeg + a.steps_per_split * BK);
+    return;
+  }
+  *pbeg = split * a.steps_per_split * BK;
+  *pend = min(a.P, *pbeg + a.steps_per_split * BK);
+}
+
 // PAIR (C == 64, BN == 128): a tile's 128 columns are TWO taps x 64 input
 // channels (taps 2q, 2q+1; the 10th tap of the last pair is a zero operand
 // that is never stored), so 64-channel layers run the 128-wide wave tiles
@@ -576,8 +592,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
   const int tile = bid % ntiles, split = bid / ntiles;
   const int tc = tile % ntc, rs = (tile / ntc) % NTAPG, tk = tile / (ntc * NTAPG);
   const int k0 = tk * WBM, c0 = tc * BN;
-  const int pbeg = split * a.steps_per_split * BK;
-  const int pend = min(a.P, pbeg + a.steps_per_split * BK);
+  int pbeg, pend;
+  wgrad_split_range(a, split, &pbeg, &pend);
   const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
   // DMA source addresses as integers (pointer arrays + selects made hipcc
   // spill the array to scratch and index it dynamically)
@@ -759,8 +775,8 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
   const int tile = bid % ntiles, split = bid / ntiles;
   const int tc = tile % ntc, rs = (tile / ntc) % NTAPG, tk = tile / (ntc * NTAPG);
   const int k0 = tk * 256, c0 = tc * CPT;
-  const int pbeg = split * a.steps_per_split * BK;
-  const int pend = min(a.P, pbeg + a.steps_per_split * BK);
+  int pbeg, pend;
+  wgrad_split_range(a, split, &pbeg, &pend);
   const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
   const uint64_t zero = reinterpret_cast<uint64_t>(g_conv_zero);
 
@@ -903,12 +919,17 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
 // along c: coalesced); the 4 partial sums are combined in a fixed order
 // (deterministic) and transposed in LDS, so dw is written as one contiguous
 // run of 576 floats.
+// Grouped (blockIdx.y = group g): sums the group's own splits [g*splits,
+// (g+1)*splits) into dw + g * gstride.
 __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __restrict__ slab,
                                                                  float* __restrict__ dw, int K, int C,
-                                                                 int splits, float beta) {
+                                                                 int splits, float beta,
+                                                                 int64_t gstride) {
   __shared__ float t[4][64 * 9];
   const int ncb = C >> 6;
   const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
+  slab += static_cast<size_t>(blockIdx.y) * splits * K * 9 * C;
+  dw += static_cast<size_t>(blockIdx.y) * gstride;
   const int cc = threadIdx.x & 63, part = threadIdx.x >> 6;
   const size_t sstride = static_cast<size_t>(K) * 9 * C;
   const float* src = slab + static_cast<size_t>(k) * 9 * C + c0 + cc;
@@ -1238,9 +1259,19 @@ int conv3x3_wgrad_splits(int P, int K, int C) {
   return s < 1 ? 1 : s;
 }
 
+void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_t stream);
+
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream) {
   const int steps = (a.P + BK - 1) / BK;
-  a.steps_per_split = (steps + a.splits - 1) / a.splits;
+  a.group_px = 0;
+  launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(a.K * (a.C / 64)), dim3(256), 0, stream,
+                     a.slab, dw, a.K, a.C, a.splits, beta, int64_t{0});
+}
+
+// the wgrad GEMM kernels (slabs only) with a given split length
+void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_t stream) {
+  a.steps_per_split = steps_per_split;
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   static const bool three = [] {  // tuning experiment: COMMEFF_WGRAD_STAGES=3
@@ -1260,8 +1291,18 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
   } else {
     if (wide) launch_wgrad<128, 2, false>(a, stream); else launch_wgrad<64, 2, false>(a, stream);
   }
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(a.K * (a.C / 64)), dim3(256), 0, stream,
-                     a.slab, dw, a.K, a.C, a.splits, beta);
+}
+
+void launch_conv3x3_wgrad_grouped(ConvWgradArgs a, int G, float* dw, int64_t gstride, float beta,
+                                  hipStream_t stream) {
+  // one launch for every group's splits (each split's pixel range inside its
+  // group), then one per-group reduction
+  a.group_px = a.P / G;
+  a.splits_per_group = a.splits / G;
+  const int steps = (a.group_px + BK - 1) / BK;
+  launch_conv3x3_wgrad_steps(a, (steps + a.splits_per_group - 1) / a.splits_per_group, stream);
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(a.K * (a.C / 64), G), dim3(256), 0, stream,
+                     a.slab, dw, a.K, a.C, a.splits_per_group, beta, gstride);
 }
 
 void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream) {

@@ -181,6 +181,11 @@ struct ConvWgradArgs {
   int splits;
   int steps_per_split;  // set by the launcher
   FastDivU32 div_w, div_h;
+  // grouped (per-client) weight gradients, ops/grouped.py: the P pixels are
+  // G groups of group_px; the splits are G x splits_per_group, each split
+  // inside one group (0: ungrouped)
+  int group_px = 0;
+  int splits_per_group = 0;
 };
 bool conv3x3_supported(int C, int K);
 bool conv3x3_pool_supported(int H, int W, int K);
@@ -188,6 +193,10 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
+// per-group dw_g [K][C][3][3] (+)= the wgrad of group g's pixels, dw_g at
+// dw + g * gstride floats (a.splits = G x splits_per_group, set by the caller)
+void launch_conv3x3_wgrad_grouped(ConvWgradArgs a, int G, float* dw, int64_t gstride, float beta,
+                                  hipStream_t stream);
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 (either output optional) and
 // wt [C][3][3][K] bf16 spatially flipped (the dgrad weight), for up to
 // kPrepMax weights in one launch

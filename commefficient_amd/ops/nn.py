@@ -546,7 +546,11 @@ class _Conv3x3(torch.autograd.Function):
                 else:
                     dst.add_(_wgrad_mopen(gs, xs, w, (1, 1), (1, 1), (1, 1), 1))
 
-            if ctx.gg is not None:
+            if ctx.gg is not None and native:
+                # every group's split-K slabs in one launch + a per-group reduction
+                gv = ctx.gg.view(w)
+                _ops().conv3x3_wgrad_grouped(g, x, gv.shape[0], gv.view(gv.shape[0], -1))
+            elif ctx.gg is not None:
                 _grouped_wgrad_slices(g, x, ctx.gg.view(w), one)
             elif native:
                 gw = _wgrad_to(g, x, w)

@@ -1,37 +1,8 @@
 """Federated training entry point (the name referenced by the reference's
-imagenet.sh:1 and BASELINE.json).  Same flags as the reference
-(commefficient_amd/utils/args.py); dispatches to the CV or GPT-2 driver.
-
-Multi-GPU: launch with torchrun (one process per GPU), e.g.
-  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 fed_train.py --dataset_name CIFAR10 ...
-or pass --num_devices N and the ranks are spawned here (127.0.0.1 rendezvous).
-"""
-import os
+imagenet.sh:1 and BASELINE.json); see commefficient_amd/cli.py."""
 import sys
 
-from commefficient_amd.utils.args import parse_args
-
-
-def _run(args):
-    if args.model == "GPT2DoubleHeads" or args.dataset_name == "PERSONA":
-        from commefficient_amd.train import gpt2
-        return gpt2.main(args)
-    from commefficient_amd.train import cv
-    return cv.main(args)
-
-
-def _spawned(rank, args):
-    _run(args)
-
-
-def main(argv=None, default_lr=None):
-    args = parse_args(default_lr=default_lr, argv=argv)
-    if args.num_devices > 1 and "WORLD_SIZE" not in os.environ:
-        from commefficient_amd.parallel import dist
-        dist.spawn(_spawned, args.num_devices, args=(args,), port=args.port)
-        return None
-    return _run(args)
-
+from commefficient_amd.cli import main
 
 if __name__ == "__main__":
     main(sys.argv[1:])

@@ -499,3 +499,25 @@ def test_native_conv2d_fwd_bwd(N, C, H, W, K, ks, stride):
     _close(y, yr)
     _close(x.grad, xr.grad)
     _close(conv.weight.grad - prior, wr.grad)
+
+
+@pytest.mark.parametrize("N,G,C,H,K", [(8, 4, 128, 14, 128), (16, 8, 256, 7, 256), (6, 3, 64, 9, 128),
+                                       (4, 2, 512, 7, 512)])
+def test_wgrad_grouped_matches_per_group(N, G, C, H, K):
+    """One launch for every group's split-K slabs + a per-group reduction
+    (grouped per-client gradients) vs the ungrouped kernel on each group's
+    slice; rows of a strided [G, d] buffer accumulate (+=)."""
+    x, _ = _inputs(N, C, H, H, K)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    dy = _nhwc(torch.randn(N, K, H, H, device="cuda", generator=g).to(torch.bfloat16))
+    n = K * C * 9
+    buf = torch.randn(G, n + 37, device="cuda", generator=g)  # row stride != n
+    before = buf.clone()
+    ops_ = torch.ops.commeff
+    ops_.conv3x3_wgrad_grouped(dy, x, G, buf[:, 5:5 + n])
+    ng = N // G
+    for j in range(G):
+        ref = ops_.conv3x3_wgrad(dy[j * ng:(j + 1) * ng], x[j * ng:(j + 1) * ng], 0).reshape(-1)
+        got = buf[j, 5:5 + n] - before[j, 5:5 + n]
+        torch.testing.assert_close(got, ref, rtol=1e-3, atol=1e-3)
+    assert torch.equal(buf[:, :5], before[:, :5]) and torch.equal(buf[:, 5 + n:], before[:, 5 + n:])
