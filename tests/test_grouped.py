@@ -128,7 +128,10 @@ def test_engine_grouped_matches_per_client_gpu():
     assert fa._gbuf is not None
     fb, ob = _engine("off", "cuda", "bf16")
     wb, lb = _rounds(fb, ob, "cuda")
-    torch.testing.assert_close(la, lb, rtol=2e-2, atol=2e-2)
+    # round 0 at identical weights: close; round 1 after one bf16 update (local
+    # top-k near-ties may select differently): loosely
+    torch.testing.assert_close(la[0], lb[0], rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(la[1], lb[1], rtol=0.1, atol=0.1)
     w0 = fa.w.new_zeros(fa.w.shape)
     # the two paths round differently (bf16 batch shapes): updates agree to
     # bf16 accuracy relative to their magnitude
