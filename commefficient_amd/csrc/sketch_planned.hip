@@ -320,7 +320,7 @@ __device__ __forceinline__ float lower_median_r(float (&v)[kMaxRows], int r) {
   return res;
 }
 
-template <int R>
+template <int R, int DEEP>
 __global__ void __launch_bounds__(1024)
 qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_t chunk,
               uint32_t num_tiles, const uint16_t* __restrict__ src_info,
@@ -340,10 +340,10 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
   __syncthreads();
   // runs -> stage: a half-wave per run (runs average ~30), kB runs per
   // half-wave in flight at once
-  // (dense plans: runs of ~127 entries -> up to DEEP x 32 entries per run in
-  // flight, the serial tail only beyond that)
+  // DEEP x 32 entries of every run in flight before the serial tail (exact
+  // plans: runs of ~30 -> 2; dense plans: runs of ~127 -> 4; 4 on the exact
+  // plan measured 97 -> 107 us at ResNet-9 size)
   constexpr uint32_t kB = 16;
-  constexpr uint32_t DEEP = 4;
   const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = blockDim.x >> 5;
   for (uint32_t t0 = hw * kB; t0 < num_tiles; t0 += nhw * kB) {
     float v[kB][DEEP];
@@ -540,10 +540,12 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
   if (d == 0) return;
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<5>));
-    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<3>));
-    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<1>));
-    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<0>));
+    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<5, 2>));
+    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<3, 2>));
+    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<1, 2>));
+    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<0, 2>));
+    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<5, 4>));
+    set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<0, 4>));
     attr = true;
   }
   const uint32_t nt = static_cast<uint32_t>(p.num_tiles), ch = static_cast<uint32_t>(p.chunk);
@@ -556,11 +558,16 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
   const dim3 g2(static_cast<uint32_t>(p.num_chunks));
   const size_t l2 = stage_lds(p, r);
   const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
+  if (p.dense) {
+    if (r == 5) hipLaunchKernelGGL((qry_q2_kernel<5, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est);
+    else hipLaunchKernelGGL((qry_q2_kernel<0, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est);
+    return;
+  }
   switch (r) {
-    case 5: hipLaunchKernelGGL(qry_q2_kernel<5>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 3: hipLaunchKernelGGL(qry_q2_kernel<3>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 1: hipLaunchKernelGGL(qry_q2_kernel<1>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    default: hipLaunchKernelGGL(qry_q2_kernel<0>, g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 5: hipLaunchKernelGGL((qry_q2_kernel<5, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 3: hipLaunchKernelGGL((qry_q2_kernel<3, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 1: hipLaunchKernelGGL((qry_q2_kernel<1, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    default: hipLaunchKernelGGL((qry_q2_kernel<0, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
   }
 }
 

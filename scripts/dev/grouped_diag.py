@@ -11,11 +11,14 @@ from commefficient_amd.parallel.flat import FlatParams
 from test_grouped import _per_group_reference
 
 G = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+HW = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 torch.manual_seed(0)
-model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=7, input_hw=32).cuda().to(memory_format=torch.channels_last)
-x = torch.randn(4 * G, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
+model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=7, input_hw=HW).cuda().to(memory_format=torch.channels_last)
+x = torch.randn(4 * G, 3, HW, HW, device="cuda").to(memory_format=torch.channels_last)
 y = torch.randint(0, 7, (4 * G,), device="cuda")
-ref_model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=7, input_hw=32).cuda().float()
+ref_model = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=7, input_hw=HW).cuda().float()
+with torch.no_grad():
+    model.fc.weight.mul_(float(os.environ.get("FC_SCALE", "1")))
 ref_model.load_state_dict(model.state_dict())
 with torch.no_grad():
     for p in ref_model.parameters():
