@@ -495,17 +495,11 @@ class FedModel:
         mb = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else n_local
         groups_total = len(my_slots)
         per_ex_all, metrics_all = [], []
-        for s in range(0, n_local, mb):
-            e = min(n_local, s + mb)
-            xi = tuple(x[s:e] for x in inputs)
-            # ghost-BN groups: client boundaries align with microbatches only
-            # when mb is a multiple of the (equal) client size (``mergeable``
-            # falls back to the per-client path otherwise)
-            g = groups_total if mb >= n_local else max(1, (e - s) // max(1, counts[my_slots[0]]))
-            pe, ms = self._fwd_bwd(xi, targets[s:e], None, groups=g,
-                                   ex_groups=slots_t[s:e] if self._loss_groups else None)
-            per_ex_all.append(pe)
-            metrics_all.append(ms)
+        # the native 3x3 convs' bf16 weight images in ONE launch for the pass
+        with (prepared_conv_weights(self._native_3x3_weights())
+              if self.device.type == "cuda" else nullcontext()):
+            self._merged_microbatches(inputs, targets, n_local, mb, groups_total, counts, my_slots,
+                                      slots_t, per_ex_all, metrics_all)
         if len(per_ex_all) == 1:  # one microbatch: no concatenation copies
             per_ex, mets = per_ex_all[0], list(metrics_all[0])
         else:
@@ -521,6 +515,20 @@ class FedModel:
         with self.timer.phase("encode"):
             self._encode_merged(out, n_local)
         return out, msum
+
+    def _merged_microbatches(self, inputs, targets, n_local, mb, groups_total, counts, my_slots,
+                             slots_t, per_ex_all, metrics_all):
+        for s in range(0, n_local, mb):
+            e = min(n_local, s + mb)
+            xi = tuple(x[s:e] for x in inputs)
+            # ghost-BN groups: client boundaries align with microbatches only
+            # when mb is a multiple of the (equal) client size (``mergeable``
+            # falls back to the per-client path otherwise)
+            g = groups_total if mb >= n_local else max(1, (e - s) // max(1, counts[my_slots[0]]))
+            pe, ms = self._fwd_bwd(xi, targets[s:e], None, groups=g,
+                                   ex_groups=slots_t[s:e] if self._loss_groups else None)
+            per_ex_all.append(pe)
+            metrics_all.append(ms)
 
     def _client_grad(self, inputs, targets, n: int, work: torch.Tensor):
         """Mean gradient of one client's batch + the reference's client-side
