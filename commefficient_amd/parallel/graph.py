@@ -31,6 +31,20 @@ the first launch is bitwise identical to the eager round
 before HIP initialises) every replay is correct.  Graphs are therefore only
 used when that variable is 0.
 
+Status of that fault (round 2): not reproduced on purpose -- a faulting
+kernel can reset every GPU of a shared host -- so its cause is open.  What is
+known: the first replay is bitwise identical to eager (so the captured
+arguments and buffers are right at capture time), every replay is correct
+with the capture off, and none of this package's kernels uses device-side
+assert / printf (no hostcall buffer).  The two packet-capture-specific
+candidates are (a) PyTorch kernels compiled with device asserts
+(``CUDA_KERNEL_ASSERT`` in its indexing kernels, which the round's gather /
+index ops launch) whose hidden hostcall argument is baked into the pre-built
+packet, and (b) the >256-byte by-value kernel arguments of the sketch and
+conv kernels (``RowHashes`` is 512 bytes) in the pre-built kernarg segment.
+Graph replay therefore stays opt-in (``--graph on``), and only then is
+DEBUG_CLR_GRAPH_PACKET_CAPTURE set (before HIP initialises).
+
 Measured (1x MI355X, bench.py, 50 rounds): 176.9k img/s replayed vs 176.5k
 eager, host enqueue 2.44 vs 2.39 ms/round -- without packet capture the
 runtime dispatches each node much like an eager launch, and the GPU (not
