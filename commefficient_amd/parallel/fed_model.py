@@ -178,6 +178,9 @@ class FedModel:
         if wc == "once" and not self.use_bf16:
             wc = "autocast"
         self._shadow = self.flat.make_bf16_shadow() if wc == "once" else None
+        self._overlap = None  # bucketed all-reduce overlapped with backward (overlap.py)
+        self._overlap_armed = False
+        self._overlap_round = False
 
     # ------------------------------------------------------------------ API
     def attach_optimizer(self, opt):
@@ -308,7 +311,7 @@ class FedModel:
                 if loss_weight is not None:
                     total = total * loss_weight
                 total.backward()
-            if shadow is not None:
+            if shadow is not None and not self._overlap_armed:
                 self.flat.collect_shadow_grads()
         return per_ex.detach().float(), [m.detach().float() for m in metrics]
 
@@ -362,7 +365,13 @@ class FedModel:
         if metric_sums.data_ptr() != tail.data_ptr():
             tail.copy_(metric_sums.reshape(-1))
         sparse_bytes = None
-        if self._sparse is not None:
+        if merged and self._overlap_round:
+            # the gradient buckets were all-reduced during the backward
+            with self.timer.phase("allreduce"):
+                if main is not None and main.data_ptr() != payload.data_ptr():
+                    payload[:self.main_numel].copy_(main)
+                dist.all_reduce_(tail)
+        elif self._sparse is not None:
             # local top-k lists: all-gather them, all-reduce only the metrics
             with self.timer.phase("allreduce"):
                 dist.all_reduce_(tail)
@@ -382,7 +391,14 @@ class FedModel:
         dl, ul = self.accountant.round(clients, self.round_idx, meta=self._acct_meta)
         self._acct_meta = None
         self._pending = (G, clients, False, 1.0 / B)
-        if sparse_bytes is not None:
+        overlapped = merged and self._overlap_round
+        self._overlap_round = False
+        if overlapped:
+            self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
+                               "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel()),
+                               "overlapped_buckets": len(self._overlap.buckets),
+                               "buckets_during_backward": getattr(self, "last_overlap_early", 0)}
+        elif sparse_bytes is not None:
             Nw = self.ctx.world_size
             self.last_round = {"clients": W, "examples": B, "payload_bytes": sparse_bytes,
                                "wire_bytes": float((Nw - 1) * sparse_bytes)
@@ -496,10 +512,16 @@ class FedModel:
         groups_total = len(my_slots)
         per_ex_all, metrics_all = [], []
         # the native 3x3 convs' bf16 weight images in ONE launch for the pass
+        ovl = self._overlap_reducer(W, counts)
         with (prepared_conv_weights(self._native_3x3_weights())
               if self.device.type == "cuda" else nullcontext()):
             self._merged_microbatches(inputs, targets, n_local, mb, groups_total, counts, my_slots,
-                                      slots_t, per_ex_all, metrics_all)
+                                      slots_t, per_ex_all, metrics_all, ovl)
+        self._overlap_round = ovl is not None
+        if ovl is not None:
+            with self.timer.phase("allreduce"):
+                self.last_overlap_early = ovl.finish()
+            self._overlap_armed = False
         if len(per_ex_all) == 1:  # one microbatch: no concatenation copies
             per_ex, mets = per_ex_all[0], list(metrics_all[0])
         else:
@@ -513,13 +535,39 @@ class FedModel:
         self._n_metrics = msum.shape[0]
         out = self._transmit_buffer()
         with self.timer.phase("encode"):
-            self._encode_merged(out, n_local)
+            # overlapped: flat.g already holds the sum over ranks; the weight
+            # decay term of the whole round (B examples) is added once
+            self._encode_merged(out, int(counts.sum()) if self._overlap_round else n_local)
         return out, msum
 
+    def _overlap_reducer(self, W: int, counts: np.ndarray):
+        """The bucketed overlapped all-reduce when it serves this round: a
+        dense merged mode on >1 rank where EVERY rank takes the merged path
+        (so every rank issues the same collectives: each has clients, and with
+        BatchNorm all clients have one size), RCCL (or gloo on CPU tensors)."""
+        a, ctx = self.args, self.ctx
+        if (a.overlap_allreduce == "off" or ctx.world_size < 2 or W < ctx.world_size
+                or a.mode not in ("uncompressed", "true_topk", "fedavg")):
+            return None
+        if self.has_bn and not bool(np.all(counts == counts[0])):
+            return None
+        if self.device.type == "cuda" and ctx.backend != "nccl":
+            return None  # gloo reads device memory unordered with the stream
+        if self._overlap is None:
+            from .overlap import OverlapReducer
+            shadow = self._shadow is not None
+            params = self.flat.shadow_params if shadow else self.flat.params
+            self._overlap = OverlapReducer(self.flat, params,
+                                           int(a.allreduce_bucket_mb * 2 ** 20), shadow=shadow)
+        return self._overlap
+
     def _merged_microbatches(self, inputs, targets, n_local, mb, groups_total, counts, my_slots,
-                             slots_t, per_ex_all, metrics_all):
+                             slots_t, per_ex_all, metrics_all, ovl=None):
         for s in range(0, n_local, mb):
             e = min(n_local, s + mb)
+            if ovl is not None and e == n_local:  # the backward that completes the grads
+                ovl.arm()
+                self._overlap_armed = True
             xi = tuple(x[s:e] for x in inputs)
             # ghost-BN groups: client boundaries align with microbatches only
             # when mb is a multiple of the (equal) client size (``mergeable``

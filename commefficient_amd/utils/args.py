@@ -149,6 +149,11 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                         "weights into a bf16 model replica per forward and one gradient "
                         "gather back (parallel/flat.py); 'autocast' = torch.autocast per-op "
                         "casts; auto = once for GPT-2 on a GPU, else autocast")
+    g.add_argument("--overlap_allreduce", choices=["auto", "on", "off"], default="auto",
+                   help="dense merged modes on >1 rank: all-reduce gradient buckets as the "
+                        "backward completes them (parallel/overlap.py)")
+    g.add_argument("--allreduce_bucket_mb", type=float, default=32.0,
+                   help="bucket size of the overlapped gradient all-reduce")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
     g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
                    help="GPU Count-Sketch encode/query kernels: planned (precomputed "

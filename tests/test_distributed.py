@@ -30,7 +30,8 @@ def _run(rank, world, port, mode, out_dir, rounds):
     from commefficient_amd.train.losses import cv_loss
     from commefficient_amd.utils.args import parse_args
     dist.init("cpu")
-    extra = {"uncompressed": ["--local_momentum", "0", "--virtual_momentum", "0.9"],
+    extra = {"uncompressed": ["--local_momentum", "0", "--virtual_momentum", "0.9",
+                              "--allreduce_bucket_mb", "0.01"],
              "sketch": ["--error_type", "virtual", "--local_momentum", "0", "--virtual_momentum",
                         "0.9", "--k", "300", "--num_rows", "3", "--num_cols", "2000"],
              "local_topk": ["--error_type", "local", "--local_momentum", "0.9", "--k", "300"],
@@ -57,6 +58,9 @@ def _run(rank, world, port, mode, out_dir, rounds):
         losses.append(loss.clone())
     if mode.endswith("_sparse"):
         assert fed.last_round.get("sparse_allgather"), fed.last_round
+    if mode == "uncompressed" and world > 1:  # gradient buckets reduced during the backward
+        assert fed.last_round.get("overlapped_buckets", 0) >= 2, fed.last_round
+        assert fed.last_round.get("buckets_during_backward", 0) >= 1, fed.last_round
     torch.save({"w": fed.w.clone(), "loss": torch.stack(losses),
                 "dl": fed.accountant.client_download.clone()},
                os.path.join(out_dir, f"r{rank}_w{world}.pt"))
@@ -106,3 +110,47 @@ def test_two_ranks_one_gpu(mode):
     # bf16 forward/backward over a different per-rank batch split: close, not equal
     torch.testing.assert_close(r0["loss"], s["loss"], rtol=2e-2, atol=2e-2)
     assert (r0["w"] - s["w"]).abs().max() < 0.05
+
+
+def _overlap_shadow_worker(rank, port, out_dir):
+    os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    import torch.distributed as tdist
+    import torch.nn as nn
+    from commefficient_amd.parallel.flat import FlatParams
+    from commefficient_amd.parallel.overlap import OverlapReducer
+    tdist.init_process_group("gloo", rank=0, world_size=1)
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(8, 16), nn.ReLU(), nn.Linear(16, 16), nn.ReLU(),
+                          nn.Linear(16, 3))
+    flat = FlatParams(model, "cpu")
+    shadow = flat.make_bf16_shadow()
+    x = torch.randn(5, 8)
+    res = []
+    for use_overlap in (False, True):
+        flat.zero_grad()
+        flat.refresh_shadow()
+        red = OverlapReducer(flat, flat.shadow_params, 200, shadow=True) if use_overlap else None
+        if red:
+            red.arm()
+        shadow(x.to(torch.bfloat16)).float().pow(2).sum().backward()
+        if red:
+            early = red.finish()
+            red.remove()
+            assert early >= 1 and len(red.buckets) >= 2
+        else:
+            flat.collect_shadow_grads()
+        res.append(flat.g.clone())
+    torch.save(res, os.path.join(out_dir, "ovl.pt"))
+    tdist.destroy_process_group()
+
+
+def test_overlap_reducer_moves_replica_grads():
+    """The overlapped reducer's hooks on the bf16 replica gather exactly what
+    collect_shadow_grads gathers (world 1: the all-reduce is the identity)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_overlap_shadow_worker, args=(_free_port(), d), nprocs=1,
+                           start_method="spawn", join=True)
+        a, b = torch.load(os.path.join(d, "ovl.pt"), weights_only=True)
+    assert a.abs().sum() > 0
+    torch.testing.assert_close(a, b)
