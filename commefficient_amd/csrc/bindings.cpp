@@ -882,7 +882,7 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
   auto fo = x.options().dtype(at::kFloat);
-  auto part = at::empty({G * S * 2 * C}, fo);
+  auto part = at::empty({bn_scratch_floats(static_cast<int>(G), static_cast<int>(M), static_cast<int>(C))}, fo);
   auto stat = at::empty({G, 2, C}, fo);
   auto ab = at::empty({G, 2, C}, fo);
   auto y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -942,7 +942,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
   auto fo = x.options().dtype(at::kFloat);
-  auto part = at::empty({G * S * 2 * C}, fo);
+  auto part = at::empty({bn_scratch_floats(static_cast<int>(G), static_cast<int>(M), static_cast<int>(C))}, fo);
   auto coef = at::empty({G * 3 * C}, fo);
   at::Tensor dw, db;
   if (affine && !into && !grouped) {

@@ -310,6 +310,124 @@ bn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__
   }
 }
 
+// ---- few groups (2 <= G < 16, e.g. 8 clients of a grouped round): the
+// finalize kernels above loop over the groups serially inside 1-32 blocks
+// (~17 us each at C <= 512, latency-bound).  Here one block per (64
+// channels, group): its 16 lanes split the group's slabs, one fixed-order LDS
+// combine.  Cross-group sums (running statistics; dweight / dbias when they
+// are not grouped) go to small per-group buffers summed in a fixed order by
+// one more tiny kernel.
+__device__ __forceinline__ void group_slab_sums(const float* __restrict__ part, int C, int S, int g,
+                                                int c, int cc, int gl, float (&red)[2][kGL][64],
+                                                float* t1, float* t2) {
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C) {
+    for (int s = gl; s < S; s += kGL) {
+      const float* p = part + (static_cast<size_t>(g) * S + s) * 2 * C;
+      s1 += p[c];
+      s2 += p[C + c];
+    }
+  }
+  red[0][gl][cc] = s1;
+  red[1][gl][cc] = s2;
+  __syncthreads();
+  float a = 0.f, b = 0.f;
+  for (int q = 0; q < kGL; ++q) {
+    a += red[0][q][cc];
+    b += red[1][q][cc];
+  }
+  *t1 = a;
+  *t2 = b;
+}
+
+// grid (C/64, G).  gmv[g][0][c] = mean, gmv[g][1][c] = var (running stats)
+__global__ void __launch_bounds__(1024)
+bn_fwd_finalize_group_kernel(const uint16_t* __restrict__ x, const float* __restrict__ part,
+                             const float* __restrict__ w, const float* __restrict__ bias, int C,
+                             int M, int S, float eps, float* __restrict__ stat,
+                             float* __restrict__ ab, float* __restrict__ gmv) {
+  __shared__ float red[2][kGL][64];
+  const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc, g = blockIdx.y;
+  float t1, t2;
+  group_slab_sums(part, C, S, g, c, cc, gl, red, &t1, &t2);
+  if (gl != 0 || c >= C) return;
+  const float wc = w != nullptr ? w[c] : 1.f, bc = w != nullptr ? bias[c] : 0.f;
+  const float kk = __uint_as_float(static_cast<uint32_t>(x[static_cast<size_t>(g) * M * C + c]) << 16);
+  const float dd = t1 / M;
+  const float var = fmaxf(t2 / M - dd * dd, 0.f);
+  const float mean = kk + dd, rstd = rsqrtf(var + eps);
+  const size_t o = static_cast<size_t>(g) * 2 * C + c;
+  stat[o] = mean;
+  stat[o + C] = rstd;
+  ab[o] = wc * rstd;
+  ab[o + C] = bc - mean * wc * rstd;
+  gmv[o] = mean;
+  gmv[o + C] = var;
+}
+
+// running statistics from the group-averaged moments (fixed group order)
+__global__ void __launch_bounds__(256)
+bn_running_kernel(const float* __restrict__ gmv, int C, int M, int G, float momentum,
+                  float* __restrict__ run_mean, float* __restrict__ run_var,
+                  int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (nbt != nullptr && c == 0) *nbt += 1;
+  if (c >= C || run_mean == nullptr) return;
+  float ms = 0.f, vs = 0.f;
+  for (int g = 0; g < G; ++g) {
+    ms += gmv[static_cast<size_t>(g) * 2 * C + c];
+    vs += gmv[static_cast<size_t>(g) * 2 * C + C + c];
+  }
+  const float unb = M > 1 ? static_cast<float>(M) / static_cast<float>(M - 1) : 1.f;
+  run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (ms / G);
+  run_var[c] = (1.f - momentum) * run_var[c] + momentum * (vs / G) * unb;
+}
+
+// grid (C/64, G).  Grouped: gdw / gdb rows += the group's sums; else the
+// per-group sums go to gsum[g][0..1][c] for bn_dwdb_kernel
+__global__ void __launch_bounds__(1024)
+bn_bwd_finalize_group_kernel(const float* __restrict__ part, const float* __restrict__ stat,
+                             const float* __restrict__ w, int C, int M, int S,
+                             float* __restrict__ coef, float* __restrict__ gdw,
+                             float* __restrict__ gdb, int64_t gstride, float* __restrict__ gsum) {
+  __shared__ float red[2][kGL][64];
+  const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc, g = blockIdx.y;
+  float s1, s2;
+  group_slab_sums(part, C, S, g, c, cc, gl, red, &s1, &s2);
+  if (gl != 0 || c >= C) return;
+  const float wc = w != nullptr ? w[c] : 1.f;
+  const float mean = stat[static_cast<size_t>(g) * 2 * C + c];
+  const float rstd = stat[static_cast<size_t>(g) * 2 * C + C + c];
+  const float k0 = wc * rstd, k1 = s1 / M, k2 = s2 / M;
+  float* o = coef + static_cast<size_t>(g) * 3 * C;
+  o[c] = k0;
+  o[C + c] = -k0 * k2 * rstd;
+  o[2 * C + c] = -k0 * k1 + k0 * k2 * rstd * mean;
+  if (gdw != nullptr) {
+    gdw[g * gstride + c] += s2;
+    gdb[g * gstride + c] += s1;
+  } else if (gsum != nullptr) {
+    gsum[static_cast<size_t>(g) * 2 * C + c] = s2;
+    gsum[static_cast<size_t>(g) * 2 * C + C + c] = s1;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_dwdb_kernel(const float* __restrict__ gsum, int C, int G, float* __restrict__ dw,
+               float* __restrict__ db, float beta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float sw = 0.f, sb = 0.f;
+  for (int g = 0; g < G; ++g) {
+    sw += gsum[static_cast<size_t>(g) * 2 * C + c];
+    sb += gsum[static_cast<size_t>(g) * 2 * C + C + c];
+  }
+  if (dw != nullptr) dw[c] = beta != 0.f ? dw[c] + sw : sw;
+  if (db != nullptr) db[c] = beta != 0.f ? db[c] + sb : sb;
+}
+
 __device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
@@ -370,6 +488,12 @@ int apply_grid(int64_t n) {
 
 }  // namespace
 
+// floats of the ``part`` scratch: the partial sums + (few groups) the
+// per-group moments / dweight-dbias sums behind them
+int64_t bn_scratch_floats(int G, int M, int C) {
+  return static_cast<int64_t>(G) * bn_slabs(G, M) * 2 * C + static_cast<int64_t>(G) * 2 * C;
+}
+
 int bn_slabs(int G, int M) {
   // >= ~512 partial blocks over the whole batch, >= 64 pixels each
   int s = (512 + G - 1) / G;
@@ -385,8 +509,17 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
                      nullptr, C, M, S, part);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part, w,
-                     b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var, nbt);
+  if (G >= 2 && G < kGL) {
+    // per-group mean / var behind the partial sums (bn_scratch_floats)
+    float* gmv = part + static_cast<size_t>(G) * S * 2 * C;
+    hipLaunchKernelGGL(bn_fwd_finalize_group_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
+                       x, part, w, b, C, M, S, eps, stat, ab, gmv);
+    hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gmv, C, M, G,
+                       momentum, run_mean, run_var, nbt);
+  } else {
+    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part,
+                       w, b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var, nbt);
+  }
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                      nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
@@ -400,8 +533,19 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
                      S, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat, w,
-                     C, M, S, G, coef, dw, db, beta, gdw, gdb, gstride);
+  if (G >= 2 && G < kGL) {
+    float* gsum = part + static_cast<size_t>(G) * S * 2 * C;  // see bn_scratch_floats
+    const bool grouped = gdw != nullptr;
+    hipLaunchKernelGGL(bn_bwd_finalize_group_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
+                       part, stat, w, C, M, S, coef, gdw, gdb, gstride,
+                       (!grouped && (dw != nullptr || db != nullptr)) ? gsum : nullptr);
+    if (!grouped && (dw != nullptr || db != nullptr))
+      hipLaunchKernelGGL(bn_dwdb_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gsum, C, G, dw, db,
+                         beta);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat,
+                       w, C, M, S, G, coef, dw, db, beta, gdw, gdb, gstride);
+  }
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
                      coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd);

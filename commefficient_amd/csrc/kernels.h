@@ -248,8 +248,9 @@ void launch_head_bwd(const float* gl, const float* gunit, const float* w, const 
                      const uint8_t* codes, int B, int C, int NPIX, int NCLS, float scale, uint16_t* dx,
                      float* dw, float beta, hipStream_t stream);
 // ghost batch norm (bn.hip): x NHWC bf16, G groups of M pixels, C % 8 == 0,
-// C <= 2048; part = bn_slabs(G, M) * G * 2C floats, stat = ab = 2GC, coef = 3GC
+// C <= 2048; part = bn_scratch_floats(G, M, C) floats, stat = ab = 2GC, coef = 3GC
 int bn_slabs(int G, int M);
+int64_t bn_scratch_floats(int G, int M, int C);
 // relu: y = max(BN(x), 0); its backward passes y_relu (the saved output)
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C, float eps,
                    float momentum, float* run_mean, float* run_var, float* part, float* stat, float* ab,
