@@ -8,8 +8,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import grouped as _grouped
-from ..ops.nn import (_AffineGrouped, conv2d_grouped, conv2d_native, conv2d_native_kind,
-                      ghost_batch_norm, ghost_bn_native_ok, linear_grouped)
+from ..ops.nn import (_AffineGrouped, conv1x1_passthrough, conv2d_grouped, conv2d_native,
+                      conv2d_native_kind, ghost_batch_norm, ghost_bn_native_ok, linear_grouped)
 
 
 class Mul(nn.Module):
@@ -158,6 +158,20 @@ class NativeConv2d(nn.Conv2d):
                 return conv2d_grouped(x, self.weight, self.stride, self.padding, self.dilation,
                                       self.groups, gg)
         return super().forward(x)
+
+
+    def forward_with_identity(self, x):
+        """(conv(x), x): a 1x1 stride-1 conv on the native path returns the
+        input through the same autograd node, so the residual block's two
+        input gradients are summed inside the dgrad GEMM."""
+        gg = _grouped.active() if self.weight.requires_grad else None
+        if gg is not None and gg.view(self.weight) is None:
+            gg = None
+        if (self.bias is None and conv2d_native_kind(x, self.weight, self.stride, self.padding,
+                                                     self.dilation, self.groups) == "1x1"
+                and tuple(self.stride) == (1, 1)):
+            return conv1x1_passthrough(x, self.weight, gg)
+        return self(x), x
 
 
 class NativeLinear(nn.Linear):

@@ -88,8 +88,13 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        out = _norm_relu(self.bn1, self.relu, self.conv1(x))
+        if self.downsample is None:
+            # conv1 hands x through to the identity branch: its dgrad GEMM
+            # adds the identity gradient (no separate accumulation pass)
+            h, idt = self.conv1.forward_with_identity(x)
+        else:
+            h, idt = self.conv1(x), self.downsample(x)
+        out = _norm_relu(self.bn1, self.relu, h)
         out = _norm_relu(self.bn2, self.relu, self.conv2(out))
         return _norm_add_relu(self.bn3, self.relu, self.conv3(out), idt)
 

@@ -505,6 +505,53 @@ class _Conv1x1(torch.autograd.Function):
         return gx, gw, None, None
 
 
+class _Conv1x1Pass(torch.autograd.Function):
+    """(conv1x1(x), x) for a residual block whose input also feeds the
+    identity branch: backward receives both gradients and sums them inside
+    the dgrad GEMM (D = dY W + dX_identity, beta = 1) instead of a separate
+    autograd accumulation pass over the block input."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gg):
+        n, c, h, w = x.shape
+        k = weight.shape[0]
+        wb = weight.detach().view(k, c).to(torch.bfloat16)
+        y2d = torch.mm(_nhwc2d(x), wb.t())
+        ctx.save_for_backward(x, wb)
+        ctx.weight, ctx.gg = weight, gg
+        return y2d.view(n, h, w, k).permute(0, 3, 1, 2), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, gy, gid):
+        x, wb = ctx.saved_tensors
+        n, c, h, w = x.shape
+        k = wb.shape[0]
+        g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        gx = None
+        if ctx.needs_input_grad[0]:
+            if gid is not None:
+                gi = _nhwc2d(gid.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+                gx2d = torch.addmm(gi, g2d, wb)
+            else:
+                gx2d = torch.mm(g2d, wb)
+            gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            if ctx.gg is not None:
+                G = ctx.gg.G
+                _wgrad_gemm(g2d, _nhwc2d(x), ctx.gg.view(ctx.weight).view(G, k, c), G)
+            else:
+                into = _grad_view(ctx.weight, (k, c))
+                gw = _wgrad_gemm(g2d, _nhwc2d(x), into)
+                gw = None if into is not None else gw.view(k, c, 1, 1)
+        return gx, gw, None
+
+
+def conv1x1_passthrough(x, weight, gg=None):
+    """(conv1x1(x, weight), x) with the two input gradients summed in one GEMM."""
+    return _Conv1x1Pass.apply(x, weight, gg)
+
+
 def _wgrad_mopen(g, x, weight, stride, padding, dilation, groups):
     """MIOpen weight gradient (fp32) of one conv."""
     return torch.ops.aten.convolution_backward(

@@ -521,3 +521,22 @@ def test_wgrad_grouped_matches_per_group(N, G, C, H, K):
         got = buf[j, 5:5 + n] - before[j, 5:5 + n]
         torch.testing.assert_close(got, ref, rtol=1e-3, atol=1e-3)
     assert torch.equal(buf[:, :5], before[:, :5]) and torch.equal(buf[:, 5 + n:], before[:, 5 + n:])
+
+
+def test_conv1x1_passthrough_sums_identity_grad():
+    """(conv1x1(x), x) from one node: dX = dY W + dX_identity in one GEMM."""
+    from commefficient_amd.models.common import NativeConv2d
+    torch.manual_seed(0)
+    conv = NativeConv2d(256, 64, 1, bias=False).cuda()
+    x = _nhwc(torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    y, idt = conv.forward_with_identity(x)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    gy = torch.randn(y.shape, device="cuda", generator=g)
+    gi = torch.randn(idt.shape, device="cuda", generator=g)
+    ((y.float() * gy).sum() + (idt.float() * gi).sum()).backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().to(torch.bfloat16).float()
+    yr = F.conv2d(xr, wr)
+    ((yr * gy.to(torch.bfloat16).float()).sum() + (xr * gi.to(torch.bfloat16).float()).sum()).backward()
+    _close(y, yr)
+    _close(x.grad, xr.grad)
