@@ -12,7 +12,7 @@ is captured ONCE into two HIP graphs and afterwards replayed:
                   metric sums -> Count-Sketch encode (or dense transmit)
                   -> payload (static buffer)
   [eager]         RCCL all-reduce of the payload; download accounting
-  server graph    G /= B -> momentum / error -> unsketch (query + top-k) ->
+  server graph    momentum / error (G / B folded in) -> unsketch (query + top-k) ->
                   heavy-hitter zeroing -> sparse apply + change stamps
 
 Per-round data reaches the graphs through static device buffers filled by
@@ -216,9 +216,11 @@ class RoundGraphs:
             inv_b = 1.0 / e.B
             g = torch.cuda.CUDAGraph()
             with _capture(g, self.pool, self.stream):
-                G.mul_(inv_b)
+                # 1/B folded into the momentum kernel exactly as in the eager
+                # step (a separate G *= 1/B rounds differently and can flip a
+                # top-k near-tie between the two paths)
                 fm.server.update(G, 0.0, fm.w, fm.accountant.last_mod, 0, None, None,
-                                 step=self.step, hist=fm.accountant.hist)
+                                 step=self.step, hist=fm.accountant.hist, gscale=inv_b)
             self._hist_ptr = fm.accountant.hist.data_ptr()
             self.pool = g.pool()
             e.g_server = g
