@@ -16,8 +16,10 @@ Formats (reference files):
 * ImageNet (fed_imagenet.py:21-64): class-per-client; ``stats.json`` with
   per-class counts; images read from ``train/<wnid>/*`` and ``val/<wnid>/*``.
 
-``prepare_datasets`` for the real datasets needs the raw downloads
-(torchvision is not available here); the synthetic datasets need nothing.
+``prepare_datasets`` converts the raw releases already on disk (no network,
+no torchvision here): the CIFAR binary release (``cifar-10-batches-bin`` /
+``cifar-100-binary``), LEAF FEMNIST JSON, the ImageNet folder layout; the
+synthetic datasets need nothing.
 """
 from __future__ import annotations
 
@@ -73,10 +75,26 @@ class FedCIFAR10(ArrayImageFedDataset):
                 self.test_images = np.ascontiguousarray(t["test_images"])
                 self.test_targets = np.asarray(t["test_targets"]).astype(np.int64)
 
+    # the CIFAR binary release (raw bytes: no pickles), cs.toronto.edu/~kriz
+    BIN_DIR, BIN_TRAIN, BIN_TEST, LABEL_BYTES, NUM_CLASSES = (
+        "cifar-10-batches-bin", [f"data_batch_{i}.bin" for i in range(1, 6)], ["test_batch.bin"],
+        1, 10)
+
     def prepare_datasets(self, download=False):
-        raise FileNotFoundError(
-            f"{self.stats_fn()} not found.  Prepare CIFAR in the reference layout "
-            "(client{i}.npy, test.npz, stats.json) or run with --synthetic.")
+        """Reference layout (fed_cifar.py:28-75: one natural client per class)
+        from the binary release unpacked under ``dataset_dir``; the reference
+        downloads through torchvision, which is not available here."""
+        src = os.path.join(self.dataset_dir, self.BIN_DIR)
+        if not os.path.isdir(src):
+            raise FileNotFoundError(
+                f"{self.stats_fn()} not found and no {src}: unpack the CIFAR binary release "
+                "there, provide the reference layout (client{i}.npy, test.npz, stats.json), "
+                "or run with --synthetic.")
+        tr_x, tr_y = read_cifar_bin([os.path.join(src, f) for f in self.BIN_TRAIN],
+                                    self.LABEL_BYTES)
+        te_x, te_y = read_cifar_bin([os.path.join(src, f) for f in self.BIN_TEST],
+                                    self.LABEL_BYTES)
+        self.write_split(self.dataset_dir, tr_x, tr_y, te_x, te_y, self.NUM_CLASSES)
 
     def client_fn(self, client_id):
         return os.path.join(self.dataset_dir, f"client{client_id}.npy")
@@ -100,9 +118,27 @@ class FedCIFAR10(ArrayImageFedDataset):
             json.dump({"images_per_client": ipc, "num_val_images": int(len(test_targets))}, f)
 
 
+def read_cifar_bin(files, label_bytes: int):
+    """(images uint8 [N,32,32,3], fine labels int64 [N]) of CIFAR binary files:
+    records of ``label_bytes`` label bytes (CIFAR-100: coarse, fine) and 3072
+    pixel bytes (R, G, B planes of 32x32)."""
+    xs, ys = [], []
+    rec = label_bytes + 3072
+    for fn in files:
+        raw = np.fromfile(fn, dtype=np.uint8)
+        if raw.size % rec:
+            raise ValueError(f"{fn}: size {raw.size} is not a multiple of {rec}-byte records")
+        raw = raw.reshape(-1, rec)
+        ys.append(raw[:, label_bytes - 1].astype(np.int64))
+        xs.append(raw[:, label_bytes:].reshape(-1, 3, 32, 32).transpose(0, 2, 3, 1))
+    return np.ascontiguousarray(np.concatenate(xs)), np.concatenate(ys)
+
+
 class FedCIFAR100(FedCIFAR10):
     mean = (0.5071, 0.4867, 0.4408)
     std = (0.2675, 0.2565, 0.2761)
+    BIN_DIR, BIN_TRAIN, BIN_TEST, LABEL_BYTES, NUM_CLASSES = (
+        "cifar-100-binary", ["train.bin"], ["test.bin"], 2, 100)
 
 
 # ----------------------------------------------------------------- FEMNIST
@@ -127,9 +163,41 @@ class FedEMNIST(ArrayImageFedDataset):
             self.test_targets = np.asarray(d["y"]).astype(np.int64)
 
     def prepare_datasets(self, download=False):
-        raise FileNotFoundError(
-            f"{self.stats_fn()} not found.  Convert LEAF FEMNIST to the reference layout "
-            "(train/client{i}.pt, test/test.pt, stats.json) or run with --synthetic.")
+        """LEAF FEMNIST JSON (``train/*.json``, ``test/*.json``: {"users",
+        "user_data": {user: {"x": [[784 floats]], "y": [...]}}}) -> one
+        ``train/client{i}.pt`` per writer, ``test/test.pt`` and ``stats.json``
+        (fed_emnist.py:82-138; torch files read ~25x faster than the JSON)."""
+        if os.path.exists(self.stats_fn()):
+            raise RuntimeError("won't overwrite existing stats file")
+        train = read_leaf_json(os.path.join(self.dataset_dir, "train"))
+        ipc = []
+        for cid, cdata in enumerate(train.values()):
+            x = torch.tensor(cdata["x"], dtype=torch.float32).view(-1, 28, 28)
+            y = torch.tensor(cdata["y"], dtype=torch.int64)
+            ipc.append(int(y.numel()))
+            fn = os.path.join(self.dataset_dir, "train", f"client{cid}.pt")
+            if not os.path.exists(fn):
+                torch.save({"x": x, "y": y}, fn)
+        test = read_leaf_json(os.path.join(self.dataset_dir, "test"))
+        xs = [torch.tensor(c["x"], dtype=torch.float32).view(-1, 28, 28) for c in test.values()]
+        ys = [torch.tensor(c["y"], dtype=torch.int64) for c in test.values()]
+        torch.save({"x": torch.cat(xs), "y": torch.cat(ys)},
+                   os.path.join(self.dataset_dir, "test", "test.pt"))
+        with open(self.stats_fn(), "w") as f:
+            json.dump({"images_per_client": ipc, "num_val_images": int(sum(len(y) for y in ys))},
+                      f)
+
+
+def read_leaf_json(data_dir):
+    """{user: {"x": [...], "y": [...]}} merged over the LEAF .json files of a
+    directory, in file then user order (fed_emnist.py:11-34)."""
+    if not os.path.isdir(data_dir):
+        raise FileNotFoundError(f"{data_dir}: LEAF FEMNIST json files expected (or use --synthetic)")
+    out = {}
+    for fn in sorted(f for f in os.listdir(data_dir) if f.endswith(".json")):
+        with open(os.path.join(data_dir, fn)) as f:
+            out.update(json.load(f)["user_data"])
+    return out
 
 
 def _to_u8(x):

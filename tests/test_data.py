@@ -152,3 +152,50 @@ def test_synthetic_persona_shapes():
     assert len(ds) == 60 and ds.num_clients == 10
     cid, rec = ds[7]
     assert cid == 1 and len(rec["input_ids"]) == 2
+
+
+def test_prepare_cifar_from_binary_release(tmp_path):
+    """CIFAR-10/100 binary records -> the reference layout (one client per
+    class) -> readable by FedCIFAR10/100."""
+    import json as _json
+    from commefficient_amd.data.image_datasets import FedCIFAR10, FedCIFAR100
+    rng = np.random.RandomState(0)
+    for cls, sub, files, lb, ncls in ((FedCIFAR10, "cifar-10-batches-bin",
+                                       [f"data_batch_{i}.bin" for i in range(1, 6)] + ["test_batch.bin"],
+                                       1, 10),
+                                      (FedCIFAR100, "cifar-100-binary", ["train.bin", "test.bin"],
+                                       2, 100)):
+        root = tmp_path / sub
+        root.mkdir(parents=True)
+        for fn in files:
+            n = 30
+            lab = rng.randint(0, ncls, size=(n, lb)).astype(np.uint8)
+            px = rng.randint(0, 256, size=(n, 3072)).astype(np.uint8)
+            np.concatenate([lab, px], 1).tofile(str(root / fn))
+        ds = cls(str(tmp_path), cls.__name__[3:], None, False, None, train=True, download=True)
+        x, y = ds.arrays()
+        assert x.shape[1:] == (32, 32, 3) and x.dtype == np.uint8
+        stats = _json.load(open(tmp_path / "stats.json"))
+        assert len(stats["images_per_client"]) == ncls and sum(stats["images_per_client"]) == len(y)
+        for p in tmp_path.iterdir():  # next dataset in a clean dir
+            if p.is_file():
+                p.unlink()
+
+
+def test_prepare_femnist_from_leaf_json(tmp_path):
+    import json as _json
+    from commefficient_amd.data.image_datasets import FedEMNIST
+    rng = np.random.RandomState(1)
+    for split, users in (("train", ["w0", "w1", "w2"]), ("test", ["w0", "w3"])):
+        (tmp_path / split).mkdir()
+        data = {"users": users, "num_samples": [], "user_data": {}}
+        for u in users:
+            n = rng.randint(2, 5)
+            data["user_data"][u] = {"x": rng.rand(n, 784).tolist(), "y": rng.randint(0, 62, n).tolist()}
+        (tmp_path / split / "all_data_0.json").write_text(_json.dumps(data))
+    ds = FedEMNIST(str(tmp_path), "EMNIST", None, False, None, train=True, download=True)
+    x, y = ds.arrays()
+    assert x.shape[1:] == (28, 28, 1) and x.dtype == np.uint8
+    assert len(ds.images_per_client) == 3 and int(np.sum(ds.images_per_client)) == len(y)
+    te = FedEMNIST(str(tmp_path), "EMNIST", None, False, None, train=False)
+    assert len(te.arrays()[1]) == ds.num_val_images
