@@ -276,19 +276,39 @@ qry_q1_kernel(const float* __restrict__ table, const uint16_t* __restrict__ ent_
   const uint32_t e0 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * s / splits);
   const uint32_t e1 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * (s + 1) / splits);
   const uint32_t mask = tile - 1;
-  constexpr uint32_t kB = 8;
   const uint32_t nt = blockDim.x;
-  for (uint32_t eb = e0; eb < e1; eb += kB * nt) {
-    uint32_t info[kB];
+  // 8 consecutive entries per lane: one 16-byte load of their u16 infos and
+  // two 16-byte stores of their values (2-byte loads / 4-byte stores per lane
+  // left this pass latency-bound at ~2.3 TB/s, profiles/r2_pmc_gpt2.txt);
+  // kU such units per lane in flight.  Unaligned head / tail: scalar.
+  const uint32_t ea = min(e1, (e0 + 7u) & ~7u), eb = max(ea, e1 & ~7u);
+  for (uint32_t e = e0 + threadIdx.x; e < ea; e += nt) vals[e] = signed_v(T[ent_info[e] & mask], ent_info[e]);
+  for (uint32_t e = eb + threadIdx.x; e < e1; e += nt) vals[e] = signed_v(T[ent_info[e] & mask], ent_info[e]);
+  constexpr uint32_t kU = 4;
+  const uint32_t u0 = ea >> 3, u1 = eb >> 3;
+  const uint4* info4 = reinterpret_cast<const uint4*>(ent_info);
+  float4* out4 = reinterpret_cast<float4*>(vals);
+  for (uint32_t ub = u0 + threadIdx.x; ub < u1; ub += kU * nt) {
+    uint4 w[kU];
 #pragma unroll
-    for (uint32_t q = 0; q < kB; ++q) {
-      const uint32_t e = eb + q * nt + threadIdx.x;
-      info[q] = e < e1 ? ent_info[e] : 0u;
+    for (uint32_t q = 0; q < kU; ++q) {
+      const uint32_t u = ub + q * nt;
+      if (u < u1) w[q] = info4[u];
     }
 #pragma unroll
-    for (uint32_t q = 0; q < kB; ++q) {
-      const uint32_t e = eb + q * nt + threadIdx.x;
-      if (e < e1) vals[e] = signed_v(T[info[q] & mask], info[q]);
+    for (uint32_t q = 0; q < kU; ++q) {
+      const uint32_t u = ub + q * nt;
+      if (u < u1) {
+        const uint32_t h[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t inf = (h[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+          o[k] = signed_v(T[inf & mask], inf);
+        }
+        out4[2 * u] = make_float4(o[0], o[1], o[2], o[3]);
+        out4[2 * u + 1] = make_float4(o[4], o[5], o[6], o[7]);
+      }
     }
   }
 }
