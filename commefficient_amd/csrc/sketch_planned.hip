@@ -52,19 +52,64 @@ template <int R>
 __global__ void __launch_bounds__(1024)
 enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, float scale,
               float wscale, uint32_t d, uint32_t r_rt, uint32_t chunk,
-              const uint16_t* __restrict__ src_info, float* __restrict__ vals) {
+              const uint16_t* __restrict__ src_info, float* __restrict__ vals, bool vec16) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
   const uint32_t i0 = blockIdx.x * chunk;
   const uint32_t i1 = min(d, i0 + chunk);
   const uint32_t total = (i1 - i0) * r;
   float* stage = reinterpret_cast<float*>(smem);
+  const uint32_t nt = blockDim.x;
+  uint32_t iscalar = i0;  // first coordinate left to the per-coordinate loop
+  if constexpr (R > 0) {
+    if (vec16) {
+      // 8 consecutive coordinates per lane: their values in two 16-byte loads
+      // (per operand), their 8R u16 slots in R 16-byte loads (chunk % 64 == 0:
+      // every unit is 16-byte aligned); kU units per lane in flight
+      constexpr uint32_t kU = 2;
+      const uint32_t ua = i0 >> 3, ue = ua + ((i1 - i0) >> 3);
+      const float4* v4 = reinterpret_cast<const float4*>(vec);
+      const float4* w4 = reinterpret_cast<const float4*>(wvec);
+      const uint4* s4 = reinterpret_cast<const uint4*>(src_info);
+      for (uint32_t ub = ua + threadIdx.x; ub < ue; ub += kU * nt) {
+        float v[kU][8];
+        uint4 sw[kU][R];
+#pragma unroll
+        for (uint32_t q = 0; q < kU; ++q) {
+          const uint32_t u = ub + q * nt;
+          if (u < ue) {
+            const float4 a = v4[2 * u], b = v4[2 * u + 1];
+            v[q][0] = scale * a.x; v[q][1] = scale * a.y; v[q][2] = scale * a.z; v[q][3] = scale * a.w;
+            v[q][4] = scale * b.x; v[q][5] = scale * b.y; v[q][6] = scale * b.z; v[q][7] = scale * b.w;
+            if (wvec != nullptr) {
+              const float4 c = w4[2 * u], e = w4[2 * u + 1];
+              v[q][0] += wscale * c.x; v[q][1] += wscale * c.y; v[q][2] += wscale * c.z; v[q][3] += wscale * c.w;
+              v[q][4] += wscale * e.x; v[q][5] += wscale * e.y; v[q][6] += wscale * e.z; v[q][7] += wscale * e.w;
+            }
+#pragma unroll
+            for (int k = 0; k < R; ++k) sw[q][k] = s4[static_cast<size_t>(u) * R + k];
+          }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kU; ++q) {
+          if (ub + q * nt < ue) {
+#pragma unroll
+            for (int x = 0; x < 8 * R; ++x) {  // entry (coordinate x / R, row x % R)
+              const uint4 wv = sw[q][x >> 3];
+              const uint32_t word = (x & 7) < 2 ? wv.x : (x & 7) < 4 ? wv.y : (x & 7) < 6 ? wv.z : wv.w;
+              stage[(word >> (16 * (x & 1))) & 0xffffu] = v[q][x / R];
+            }
+          }
+        }
+      }
+      iscalar = i0 + ((i1 - i0) & ~7u);
+    }
+  }
   // thread per coordinate, kB coordinates per thread in flight: v_i loaded
   // once, its r slots read from the (i, j)-ordered src_info stream
   constexpr uint32_t kB = 4;
   constexpr uint32_t RR = R > 0 ? static_cast<uint32_t>(R) : kMaxRows;
-  const uint32_t nt = blockDim.x;
-  for (uint32_t ib = i0 + threadIdx.x; ib < i1; ib += kB * nt) {
+  for (uint32_t ib = iscalar + threadIdx.x; ib < i1; ib += kB * nt) {
     float v[kB];
     uint32_t sl[kB][RR];
 #pragma unroll
@@ -345,7 +390,7 @@ __global__ void __launch_bounds__(1024)
 qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_t chunk,
               uint32_t num_tiles, const uint16_t* __restrict__ src_info,
               const int32_t* __restrict__ base, const int32_t* __restrict__ off,
-              float* __restrict__ est) {
+              float* __restrict__ est, bool vec16) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
   const uint32_t i0 = blockIdx.x * chunk;
@@ -391,7 +436,38 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
   }
   __syncthreads();
   const int rr = static_cast<int>(r);
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+  uint32_t iscalar = i0;
+  if constexpr (R > 0) {
+    if (vec16) {
+      // 8 consecutive coordinates per lane: R 16-byte loads of their slots,
+      // two 16-byte stores of their medians
+      const uint32_t ua = i0 >> 3, ue = ua + ((i1 - i0) >> 3);
+      const uint4* s4 = reinterpret_cast<const uint4*>(src_info);
+      float4* e4 = reinterpret_cast<float4*>(est);
+      for (uint32_t u = ua + threadIdx.x; u < ue; u += blockDim.x) {
+        uint4 sw[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) sw[k] = s4[static_cast<size_t>(u) * R + k];
+        float m[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float v[kMaxRows];
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            const int x = c * R + j;
+            const uint4 wv = sw[x >> 3];
+            const uint32_t word = (x & 7) < 2 ? wv.x : (x & 7) < 4 ? wv.y : (x & 7) < 6 ? wv.z : wv.w;
+            v[j] = stage[(word >> (16 * (x & 1))) & 0xffffu];
+          }
+          m[c] = lower_median_r<R>(v, rr);
+        }
+        e4[2 * u] = make_float4(m[0], m[1], m[2], m[3]);
+        e4[2 * u + 1] = make_float4(m[4], m[5], m[6], m[7]);
+      }
+      iscalar = i0 + ((i1 - i0) & ~7u);
+    }
+  }
+  for (uint32_t i = iscalar + threadIdx.x; i < i1; i += blockDim.x) {
     float v[kMaxRows];
     uint32_t sl[kMaxRows];
     const uint16_t* si = src_info + static_cast<size_t>(i) * r;
@@ -530,11 +606,14 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
   const dim3 g1(static_cast<uint32_t>(p.num_chunks));
   const size_t l1 = static_cast<size_t>(p.chunk) * r * 4;
   const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
+  const bool v16 = (reinterpret_cast<uintptr_t>(vec) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(wvec) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(a.src_info) % 16 == 0) && ch % 8 == 0;
   switch (r) {
-    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
-    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
-    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
-    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals); break;
+    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
+    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
+    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
+    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
   }
   if (p.dense) {
     // enough blocks for every CU: split each tile's chunk range
@@ -578,16 +657,18 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
   const dim3 g2(static_cast<uint32_t>(p.num_chunks));
   const size_t l2 = stage_lds(p, r);
   const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
+  const bool v16 = (reinterpret_cast<uintptr_t>(est) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(a.src_info) % 16 == 0) && ch % 8 == 0;
   if (p.dense) {
-    if (r == 5) hipLaunchKernelGGL((qry_q2_kernel<5, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est);
-    else hipLaunchKernelGGL((qry_q2_kernel<0, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est);
+    if (r == 5) hipLaunchKernelGGL((qry_q2_kernel<5, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16);
+    else hipLaunchKernelGGL((qry_q2_kernel<0, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16);
     return;
   }
   switch (r) {
-    case 5: hipLaunchKernelGGL((qry_q2_kernel<5, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 3: hipLaunchKernelGGL((qry_q2_kernel<3, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    case 1: hipLaunchKernelGGL((qry_q2_kernel<1, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
-    default: hipLaunchKernelGGL((qry_q2_kernel<0, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est); break;
+    case 5: hipLaunchKernelGGL((qry_q2_kernel<5, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
+    case 3: hipLaunchKernelGGL((qry_q2_kernel<3, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
+    case 1: hipLaunchKernelGGL((qry_q2_kernel<1, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
+    default: hipLaunchKernelGGL((qry_q2_kernel<0, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
   }
 }
 
