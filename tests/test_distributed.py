@@ -112,6 +112,31 @@ def test_two_ranks_one_gpu(mode):
     assert (r0["w"] - s["w"]).abs().max() < 0.05
 
 
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu():
+    """bench.py's multi-rank path (the driver's N>1 scaling run) end to end:
+    two ranks over gloo sharing cuda:0, one JSON line from rank 0 with the
+    whole-job throughput over both ranks' clients."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, COMMEFF_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+           "--clients-per-gpu", "20", "--num-clients", "2000"]
+    out = subprocess.run(cmd, env=env, check=True, timeout=300, capture_output=True, text=True,
+                         cwd=root).stdout
+    lines = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out
+    r = lines[0]
+    assert r["n_gpus"] == 2 and r["steps"] == 3 and r["warmup"] == 2
+    assert r["config"]["global_batch"] == 2 * 20 * 5 and r["config"]["parallelism"] == "dp2"
+    assert r["value"] > 0 and abs(r["value"] - 200 * 1000 / r["ms_per_step"]) < 0.01 * r["value"]
+    assert r["bytes_per_step"]["allreduce_payload_per_rank"] > 0
+
+
 def _overlap_shadow_worker(rank, port, out_dir):
     os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port)})

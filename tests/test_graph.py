@@ -27,7 +27,11 @@ def _run(graph: str, mode: str, rounds: int = 6):
     dist.init("cuda")
     extra = ["--error_type", "virtual", "--k", "3000"]
     if mode == "sketch":
-        extra += ["--num_rows", "5", "--num_cols", "40000"]
+        # d / c = 33 entries per bucket: the exact (atomic-free, bitwise
+        # deterministic) planned sketch.  (At 40,000 columns the dense plan's
+        # LDS-atomic encode sums in a timing-dependent order, so eager and
+        # replayed tables differ in the last bits and a top-k near-tie can flip.)
+        extra += ["--num_rows", "5", "--num_cols", "200000"]
     args = parse_args(argv=["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", "600",
                             "--mode", mode, "--local_momentum", "0", "--virtual_momentum", "0.9",
                             "--num_clients", "60", "--num_workers", "12",
