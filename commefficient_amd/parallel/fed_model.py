@@ -178,6 +178,7 @@ class FedModel:
         if wc == "once" and not self.use_bf16:
             wc = "autocast"
         self._shadow = self.flat.make_bf16_shadow() if wc == "once" else None
+        self.skipped_rounds = 0  # rounds dropped by --skip_nonfinite
         self._overlap = None  # bucketed all-reduce overlapped with backward (overlap.py)
         self._overlap_armed = False
         self._overlap_round = False
@@ -316,9 +317,30 @@ class FedModel:
         return per_ex.detach().float(), [m.detach().float() for m in metrics]
 
     # --------------------------------------------------------------- train
+    def _drop_clients(self, rb: RoundBatch):
+        """--client_dropout: remove the round's failed clients (one draw per
+        selected client from (seed, round), identical on every rank).  At least
+        one client survives.  Returns (RoundBatch of the survivors, #dropped)."""
+        p = float(self.args.client_dropout)
+        clients = np.unique(rb.client_ids)
+        rng = np.random.default_rng([int(self.args.seed), self.round_idx, 0x0D40])
+        u = rng.random(len(clients))
+        keep_c = clients[u >= p]
+        if len(keep_c) == 0:
+            keep_c = clients[np.argmax(u)[None]]
+        if len(keep_c) == len(clients):
+            return rb, 0
+        keep = np.flatnonzero(np.isin(rb.client_ids, keep_c))
+        out = RoundBatch(rb.client_ids[keep], lambda pos, rb=rb, keep=keep: rb.take(keep[pos]),
+                         n_inputs=rb.n_inputs)
+        return out, len(clients) - len(keep_c)
+
     def _call_train(self, batch):
         a = self.args
         rb = as_round_batch(batch, self.device)
+        dropped = 0
+        if getattr(a, "client_dropout", 0.0) > 0:
+            rb, dropped = self._drop_clients(rb)
         cids = rb.client_ids
         clients, inverse, counts = np.unique(cids, return_inverse=True, return_counts=True)
         W = len(clients)
@@ -343,7 +365,7 @@ class FedModel:
             mbs = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else 0
             if merged and 0 < mbs < int(sizes.sum()) and mbs % int(sizes[0]) != 0:
                 merged = False
-        if merged and self.graphs is not None:
+        if merged and self.graphs is not None and not self._fault_handling():
             n_local = int(counts[my_slots].sum())
             if self.graphs.usable(rb, n_local):
                 gkey = self.graphs.key(rb, n_local, W, B)
@@ -386,6 +408,8 @@ class FedModel:
         # G = summed transmit / B  (fed_aggregator.py:332); the division is
         # folded into the server's momentum kernel (gscale) -> keep a view
         G = payload[:self.main_numel]
+        if self.round_idx == getattr(a, "inject_nonfinite_round", -1):
+            G[:1].fill_(float("nan"))  # fault injection: a corrupted aggregate
         # clone: the payload buffer is reused by the next round
         metrics = payload[self.main_numel:].view(n_res, W).clone()
         dl, ul = self.accountant.round(clients, self.round_idx, meta=self._acct_meta)
@@ -407,7 +431,14 @@ class FedModel:
         else:
             self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
                                "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel())}
+        if dropped:
+            self.last_round["dropped_clients"] = dropped
         return [metrics[i] for i in range(n_res)] + [dl, ul]
+
+    def _fault_handling(self) -> bool:
+        a = self.args
+        return (getattr(a, "client_dropout", 0.0) > 0 or bool(getattr(a, "skip_nonfinite", 0))
+                or getattr(a, "inject_nonfinite_round", -1) >= 0)
 
     def _train_graph(self, gkey, rb, order, starts, my_slots, counts, W, B, clients):
         """The merged round through the captured HIP graphs (parallel/graph.py)."""
@@ -914,6 +945,13 @@ class FedModel:
             return  # e.g. the reference's "HACK STEP" before the first round
         G, clients, via_graph, gscale = self._pending
         self._pending = None
+        if getattr(self.args, "skip_nonfinite", 0) and not bool(torch.isfinite(G).all()):
+            # failure detection: a NaN/Inf in the aggregate (a diverged or faulty
+            # client) would poison V, E and the weights for good -> drop the round
+            self.skipped_rounds += 1
+            self.last_round["skipped_nonfinite"] = True
+            self.round_idx += 1
+            return
         if via_graph:
             if self.accountant.hist_for(self.round_idx).data_ptr() != self.graphs.hist_ptr:
                 self.graphs.invalidate_server()  # histogram grew: recapture

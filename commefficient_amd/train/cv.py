@@ -254,6 +254,8 @@ def train(model, opt, lr_scheduler, train_loader, test_loader, args, writer, log
         print("Total Upload (MiB): {:0.2f}".format(total_up))
         print("Avg Download Per Client: {:0.2f}".format(total_down / nc))
         print("Avg Upload Per Client: {:0.2f}".format(total_up / nc))
+        if getattr(model, "skipped_rounds", 0):
+            print("Rounds dropped by --skip_nonfinite: {}".format(model.skipped_rounds))
     return summary
 
 

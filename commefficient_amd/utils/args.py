@@ -154,6 +154,15 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                         "backward completes them (parallel/overlap.py)")
     g.add_argument("--allreduce_bucket_mb", type=float, default=32.0,
                    help="bucket size of the overlapped gradient all-reduce")
+    g.add_argument("--client_dropout", type=float, default=0.0,
+                   help="simulated client failures: each client selected for a round drops out "
+                        "with this probability (same draw on every rank) and neither downloads "
+                        "nor uploads; the round averages over the surviving examples")
+    g.add_argument("--skip_nonfinite", type=int, default=0,
+                   help="1: a round whose aggregated upload holds a NaN/Inf is dropped at the "
+                        "server (weights and server state untouched) instead of poisoning them")
+    g.add_argument("--inject_nonfinite_round", type=int, default=-1,
+                   help="fault injection: corrupt the aggregated upload of this round with a NaN")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
     g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
                    help="GPU Count-Sketch encode/query kernels: planned (precomputed "

@@ -39,9 +39,17 @@ def _run(rank, world, port, mode, out_dir, rounds):
              "local_topk_sparse": ["--error_type", "local", "--local_momentum", "0.9", "--k",
                                    "300", "--sparse_allgather", "on"],
              "fedavg": ["--local_momentum", "0", "--virtual_momentum", "0.5",
-                        "--fedavg_batch_size", "2"]}[mode]
+                        "--fedavg_batch_size", "2"],
+             # simulated client failures (same draw on every rank)
+             "sketch_dropout": ["--error_type", "virtual", "--local_momentum", "0",
+                                "--virtual_momentum", "0.9", "--k", "300", "--num_rows", "3",
+                                "--num_cols", "2000", "--client_dropout", "0.5"],
+             # one survivor: rank 1 computes nothing some rounds
+             "uncompressed_dropout": ["--local_momentum", "0", "--virtual_momentum", "0.9",
+                                      "--client_dropout", "0.95"]}[mode]
     lbs = "-1"
-    args = parse_args(argv=["--mode", mode.replace("_sparse", ""), "--device", "cpu", "--dtype", "fp32",
+    base = mode.replace("_sparse", "").replace("_dropout", "")
+    args = parse_args(argv=["--mode", base, "--device", "cpu", "--dtype", "fp32",
                             "--num_clients", "40", "--num_workers", "6", "--local_batch_size", lbs,
                             "--dataset_name", "CIFAR10", "--synthetic"] + extra, probe_port=False)
     torch.manual_seed(0)
@@ -61,14 +69,14 @@ def _run(rank, world, port, mode, out_dir, rounds):
     if mode == "uncompressed" and world > 1:  # gradient buckets reduced during the backward
         assert fed.last_round.get("overlapped_buckets", 0) >= 2, fed.last_round
         assert fed.last_round.get("buckets_during_backward", 0) >= 1, fed.last_round
-    torch.save({"w": fed.w.clone(), "loss": torch.stack(losses),
+    torch.save({"w": fed.w.clone(), "loss": torch.cat([l.reshape(-1) for l in losses]),
                 "dl": fed.accountant.client_download.clone()},
                os.path.join(out_dir, f"r{rank}_w{world}.pt"))
     dist.shutdown()
 
 
 @pytest.mark.parametrize("mode", ["uncompressed", "sketch", "local_topk", "local_topk_sparse",
-                                  "fedavg"])
+                                  "fedavg", "sketch_dropout", "uncompressed_dropout"])
 def test_gloo_two_ranks_match_single_process(mode):
     rounds = 3
     with tempfile.TemporaryDirectory() as d:

@@ -244,3 +244,54 @@ def test_fedavg_hack_step_sets_lr_without_pending_round():
     fed((cids, X, y))
     opt.step()
     torch.testing.assert_close(fed.w, w1)
+
+
+def test_client_dropout_equals_round_of_survivors():
+    """--client_dropout removes whole clients before the round: the update
+    equals a dropout-free round over the surviving clients' examples."""
+    N, d, W = 24, 6, 6
+    X, y = data(N, d)
+    cids = split(N, W)
+    argv = ["--mode", "uncompressed", "--virtual_momentum", "0.9", "--local_momentum", "0",
+            "--num_workers", str(W), "--local_batch_size", "-1", "--weight_decay", "0"]
+    fa, oa, _ = make_engine(d, argv + ["--client_dropout", "0.5"], W, 0.1)
+    out_a = fa((cids, X, y))
+    oa.step()
+    dropped = fa.last_round.get("dropped_clients", 0)
+    assert 0 < dropped < W
+    # the survivors of round 0, drawn as the engine does
+    rng = np.random.default_rng([int(fa.args.seed), 0, 0x0D40])
+    keep_c = np.arange(W)[rng.random(W) >= 0.5]
+    assert len(keep_c) == W - dropped
+    keep = np.isin(cids.numpy(), keep_c)
+    fb, ob, _ = make_engine(d, argv, W, 0.1)
+    out_b = fb((cids[keep], X[keep], y[keep]))
+    ob.step()
+    torch.testing.assert_close(fa.w, fb.w)
+    assert len(out_a[0]) == len(keep_c) == len(out_b[0])
+    # accounting: only the survivors downloaded / uploaded
+    assert (fa.accountant.client_upload > 0).sum().item() == len(keep_c)
+
+
+def test_nonfinite_round_skipped_and_injected():
+    """Fault injection corrupts round 1's aggregate; with --skip_nonfinite the
+    server drops that round (weights, V unchanged) and training goes on;
+    without it the NaN reaches the weights (the reference's behaviour: the
+    driver then stops on the NaN loss)."""
+    N, d, W = 12, 5, 3
+    X, y = data(N, d)
+    cids = split(N, W)
+    argv = ["--mode", "uncompressed", "--virtual_momentum", "0.9", "--local_momentum", "0",
+            "--num_workers", str(W), "--local_batch_size", "-1", "--inject_nonfinite_round", "1"]
+    fa, oa, _ = make_engine(d, argv + ["--skip_nonfinite", "1"], W, 0.1)
+    fa((cids, X, y)); oa.step()
+    w0, V0 = fa.w.clone(), fa.server.V.clone()
+    fa((cids, X, y)); oa.step()
+    assert fa.skipped_rounds == 1 and fa.last_round.get("skipped_nonfinite")
+    assert torch.equal(fa.w, w0) and torch.equal(fa.server.V, V0)
+    fa((cids, X, y)); oa.step()
+    assert torch.isfinite(fa.w).all() and not torch.equal(fa.w, w0)
+    fb, ob, _ = make_engine(d, argv, W, 0.1)
+    for _ in range(2):
+        fb((cids, X, y)); ob.step()
+    assert fb.skipped_rounds == 0 and not torch.isfinite(fb.w).all()
