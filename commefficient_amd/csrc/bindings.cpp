@@ -599,7 +599,7 @@ PlanGeom plan_geom_or_throw(int64_t d, int64_t r, int64_t c) {
 PlannedArgs planned_args(at::TensorList plan, const PlanGeom& p, int64_t d, int64_t r) {
   // plan = [src_info i16, ent_info i16, perm i16, csr i32, base i32, off i32, seg i32,
   //         vals f32, p2_src i32, p2_pos i32]
-  TORCH_CHECK(plan.size() == 10, "plan must have 10 tensors");
+  TORCH_CHECK(plan.size() == 10 || plan.size() == 11, "plan must have 10 or 11 tensors");
   const int64_t n = d * r;
   TORCH_CHECK(plan[0].numel() == n && plan[1].numel() == n && plan[2].numel() == n &&
                   plan[3].numel() == p.num_tiles * p.tile + 1 &&
@@ -627,6 +627,16 @@ PlannedArgs planned_args(at::TensorList plan, const PlanGeom& p, int64_t d, int6
   a.vals = plan[7].data_ptr<float>();
   a.p2_src = plan[8].data_ptr<int32_t>();
   a.p2_pos = plan[9].data_ptr<int32_t>();
+  if (plan.size() == 11 && p.dense) {
+    // int64 split partials, then max|v| per chunk and overall (as floats)
+    const int64_t nfx = p.p2_splits * p.num_tiles * p.tile;  // split stride num_tiles*tile
+    TORCH_CHECK(plan[10].scalar_type() == at::kLong && plan[10].is_contiguous() &&
+                    plan[10].numel() * 2 >= nfx * 2 + p.num_chunks + 1,
+                "plan[10] must be the dense plan's int64 scratch");
+    a.fx = plan[10].data_ptr<int64_t>();
+    a.bmax = reinterpret_cast<float*>(a.fx + nfx);
+    a.gmax = a.bmax + p.num_chunks;
+  }
   return a;
 }
 
@@ -658,11 +668,11 @@ at::Tensor cs_query_planned_hip(const at::Tensor& table, int64_t d, at::TensorLi
   return est;
 }
 
-// [tile, num_tiles, chunk, num_chunks, dense] of the planned sketch, [] if unsupported
+// [tile, num_tiles, chunk, num_chunks, dense, p2_splits] of the planned sketch, [] if unsupported
 std::vector<int64_t> plan_geometry(int64_t d, int64_t r, int64_t c) {
   PlanGeom p;
   if (!any_plan_geometry(d, r, c, &p)) return {};
-  return {p.tile, p.num_tiles, p.chunk, p.num_chunks, p.dense ? 1 : 0};
+  return {p.tile, p.num_tiles, p.chunk, p.num_chunks, p.dense ? 1 : 0, p.p2_splits};
 }
 
 std::tuple<at::Tensor, at::Tensor> relu_maxpool_hip(const at::Tensor& x, int64_t k) {

@@ -50,6 +50,7 @@ struct PlanGeom {
   bool dense = false;  // many entries per bucket (GPT-2): encode P2 accumulates
                        // with LDS atomics, plan slot 2 holds chunk-major
                        // in-tile bucket | sign instead of the bucket-order perm
+  int64_t p2_splits = 1;  // dense: blocks per tile of encode P2 (chunk-range shares)
 };
 // false when the geometry does not fit (too many entries per bucket)
 bool planned_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* out);
@@ -66,6 +67,10 @@ struct PlannedArgs {
   float* vals;               // [d*r] scratch
   const int32_t* p2_src;     // [num_tiles, num_chunks] run start in chunk-major vals
   const int32_t* p2_pos;     // [num_tiles, num_chunks + 1] run start in the segment
+  // dense plans, fixed-point encode P2 (plan slot 10; nullptr: fp32 LDS atomics)
+  int64_t* fx = nullptr;     // [p2_splits, num_tiles*tile] per-split tile partials (int64)
+  float* bmax = nullptr;     // [num_chunks] max |v| of each P1 chunk
+  float* gmax = nullptr;     // [1] max |v| of the vector
 };
 void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* blk_off,
                         const float* blk_sign, int32_t* out, hipStream_t stream);

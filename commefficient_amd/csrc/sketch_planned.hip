@@ -52,9 +52,11 @@ template <int R>
 __global__ void __launch_bounds__(1024)
 enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, float scale,
               float wscale, uint32_t d, uint32_t r_rt, uint32_t chunk,
-              const uint16_t* __restrict__ src_info, float* __restrict__ vals, bool vec16) {
+              const uint16_t* __restrict__ src_info, float* __restrict__ vals, bool vec16,
+              float* __restrict__ bmax) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
+  uint32_t amax = 0u;  // max |v| bits (as unsigned: NaN > Inf > finite)
   const uint32_t i0 = blockIdx.x * chunk;
   const uint32_t i1 = min(d, i0 + chunk);
   const uint32_t total = (i1 - i0) * r;
@@ -86,6 +88,8 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
               v[q][0] += wscale * c.x; v[q][1] += wscale * c.y; v[q][2] += wscale * c.z; v[q][3] += wscale * c.w;
               v[q][4] += wscale * e.x; v[q][5] += wscale * e.y; v[q][6] += wscale * e.z; v[q][7] += wscale * e.w;
             }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) amax = max(amax, __float_as_uint(v[q][k]) & 0x7fffffffu);
 #pragma unroll
             for (int k = 0; k < R; ++k) sw[q][k] = s4[static_cast<size_t>(u) * R + k];
           }
@@ -119,6 +123,7 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
       if (i < i1) {
         v[u] = scale * vec[i];
         if (wvec != nullptr) v[u] += wscale * wvec[i];
+        amax = max(amax, __float_as_uint(v[u]) & 0x7fffffffu);
         const uint16_t* s = src_info + static_cast<size_t>(i) * r;
 #pragma unroll
         for (uint32_t j = 0; j < RR; ++j) sl[u][j] = j < r ? s[j] : 0u;
@@ -143,6 +148,155 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
   for (uint32_t k = threadIdx.x; k < n4; k += nt) dst[k] = src[k];
   for (uint32_t k = n4 * 4 + threadIdx.x; k < total; k += nt)
     vals[static_cast<size_t>(i0) * r + k] = stage[k];
+  if (bmax != nullptr) {
+    // chunk max |v| for the fixed-point encode P2 (dense plans): wave max,
+    // then an LDS max over the waves (the stage is free again)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = max(amax, static_cast<uint32_t>(__shfl_xor(static_cast<int>(amax), o)));
+    __syncthreads();
+    uint32_t* red = reinterpret_cast<uint32_t*>(smem);
+    if (threadIdx.x == 0) red[0] = 0u;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicMax(red, amax);
+    __syncthreads();
+    if (threadIdx.x == 0) bmax[blockIdx.x] = __uint_as_float(red[0]);
+  }
+}
+
+// ----------------------------------------------- encode P2 (dense, fixed point)
+// gfx950 retires LDS float atomics at ~0.33 lanes/clk/CU but 64-bit integer
+// ones at ~5.9 (scripts/dev/lds_atomic_bench.hip, measured), so the dense P2
+// accumulates in 64-bit fixed point: every value is scaled by the same power
+// of two 2^shift with max|v| * 2^shift < 2^46 (18 bits of headroom: buckets of
+// up to 65536 entries, checked when the plan is built), rounded to an integer
+// and added with ds_add_u64.  Integer sums are order independent, so the
+// encode is bitwise deterministic; the quantum max|v| * 2^-46 lies far below
+// the fp32 resolution of every value within 2^22 of the maximum.  A NaN/Inf
+// anywhere in the vector makes the whole table NaN (detected downstream).
+constexpr int kFxBits = 46;
+constexpr double kFxMagic = 6755399441055744.0;  // 1.5 * 2^52
+
+__device__ __forceinline__ int fx_shift(float m) {
+  int ex = 0;
+  (void)frexpf(m, &ex);  // m = f * 2^ex, f in [0.5, 1); m == 0 -> ex = 0
+  return kFxBits - ex;
+}
+
+__device__ __forceinline__ bool fx_finite(float m) {
+  return (__float_as_uint(m) & 0x7fffffffu) < 0x7f800000u;
+}
+
+__global__ void __launch_bounds__(1024) fx_max_kernel(const float* __restrict__ bmax, uint32_t n,
+                                                      float* __restrict__ gmax) {
+  __shared__ uint32_t red;
+  if (threadIdx.x == 0) red = 0u;
+  __syncthreads();
+  uint32_t m = 0u;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) m = max(m, __float_as_uint(bmax[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), o)));
+  if ((threadIdx.x & 63) == 0) atomicMax(&red, m);
+  __syncthreads();
+  if (threadIdx.x == 0) gmax[0] = __uint_as_float(red);
+}
+
+__global__ void __launch_bounds__(1024)
+enc_p2_dense_fx_kernel(float* __restrict__ table, long long* __restrict__ slab,
+                       const float* __restrict__ gmax, const float* __restrict__ vals,
+                       const uint16_t* __restrict__ cm_info, const int32_t* __restrict__ p2_src,
+                       const int32_t* __restrict__ p2_pos, uint32_t tile, uint32_t total_buckets,
+                       uint32_t num_chunks, uint32_t splits, bool overwrite) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long* T = reinterpret_cast<unsigned long long*>(smem);
+  const uint32_t t = blockIdx.x / splits, s = blockIdx.x - t * splits;
+  const uint32_t nt = blockDim.x;
+  const float m = gmax[0];
+  const bool finite = fx_finite(m);
+  const int shift = fx_shift(m);
+  for (uint32_t b = threadIdx.x; b < tile; b += nt) T[b] = 0ull;
+  __syncthreads();
+  const uint32_t c0 = static_cast<uint32_t>(static_cast<uint64_t>(num_chunks) * s / splits);
+  const uint32_t c1 = static_cast<uint32_t>(static_cast<uint64_t>(num_chunks) * (s + 1) / splits);
+  const int32_t* psrc = p2_src + static_cast<size_t>(t) * num_chunks;
+  const int32_t* ppos = p2_pos + static_cast<size_t>(t) * (num_chunks + 1);
+  const uint32_t mask = tile - 1;
+  constexpr uint32_t kB = 8;
+  const uint32_t hw = threadIdx.x >> 5, l32 = threadIdx.x & 31, nhw = nt >> 5;
+  for (uint32_t cb = c0 + hw * kB; finite && cb < c1; cb += nhw * kB) {
+    uint32_t src[kB], len[kB];
+#pragma unroll
+    for (uint32_t q = 0; q < kB; ++q) {
+      const uint32_t ch = cb + q;
+      src[q] = ch < c1 ? static_cast<uint32_t>(psrc[ch]) : 0u;
+      len[q] = ch < c1 ? static_cast<uint32_t>(ppos[ch + 1] - ppos[ch]) : 0u;
+    }
+    for (uint32_t k0 = 0;; k0 += 128) {
+      float v[kB][4];
+      uint32_t info[kB][4];
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) {
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+          const uint32_t k = k0 + u * 32 + l32;
+          info[q][u] = 0xffffffffu;
+          v[q][u] = 0.f;
+          if (k < len[q]) {
+            v[q][u] = vals[src[q] + k];
+            info[q][u] = cm_info[src[q] + k];
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) {
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+          if (info[q][u] != 0xffffffffu) {
+            // round(v * 2^shift) to an integer through the double magic number
+            // 1.5 * 2^52 (|.| < 2^46): 4 VALU ops instead of the ~20 of a
+            // generic f32 -> i64 conversion
+            const double x = ldexp(static_cast<double>(signed_v(v[q][u], info[q][u])), shift) +
+                             kFxMagic;
+            const long long qi = __double_as_longlong(x) - __double_as_longlong(kFxMagic);
+            atomicAdd(T + (info[q][u] & mask), static_cast<unsigned long long>(qi));
+          }
+      }
+      bool more = false;
+#pragma unroll
+      for (uint32_t q = 0; q < kB; ++q) more |= k0 + 128 < len[q];
+      if (!more) break;
+    }
+  }
+  __syncthreads();
+  const uint32_t gb0 = t * tile;
+  for (uint32_t b = threadIdx.x; b < tile; b += nt) {
+    const uint32_t gb = gb0 + b;
+    if (gb >= total_buckets) break;
+    if (splits == 1) {
+      const float f = finite ? static_cast<float>(ldexp(static_cast<double>(static_cast<long long>(T[b])), -shift))
+                             : __builtin_nanf("");
+      table[gb] = overwrite ? f : table[gb] + f;
+    } else {
+      slab[static_cast<size_t>(s) * gridDim.x / splits * tile + gb] = static_cast<long long>(T[b]);
+    }
+  }
+}
+
+// the splits' partial tiles, summed in integers (order free) and scaled back
+__global__ void __launch_bounds__(256)
+enc_fx_reduce_kernel(float* __restrict__ table, const long long* __restrict__ slab,
+                     const float* __restrict__ gmax, uint32_t total_buckets, size_t stride,
+                     uint32_t splits, bool overwrite) {
+  const float m = gmax[0];
+  const bool finite = fx_finite(m);
+  const int shift = fx_shift(m);
+  for (uint32_t gb = blockIdx.x * blockDim.x + threadIdx.x; gb < total_buckets;
+       gb += gridDim.x * blockDim.x) {
+    long long acc = 0;
+    for (uint32_t s = 0; s < splits; ++s) acc += slab[s * stride + gb];
+    const float f = finite ? static_cast<float>(ldexp(static_cast<double>(acc), -shift))
+                           : __builtin_nanf("");
+    table[gb] = overwrite ? f : table[gb] + f;
+  }
 }
 
 // ------------------------------------------------------------- encode P2
@@ -576,6 +730,9 @@ bool planned_geometry_dense(int64_t d, int64_t r, int64_t c, PlanGeom* out) {
   }
   p.chunk = chunk;
   p.num_chunks = (d + chunk - 1) / chunk;
+  // encode P2: enough blocks for every CU -> split each tile's chunk range
+  p.p2_splits = 1;
+  while (p.num_tiles * p.p2_splits < 4 * device_cus() && p.p2_splits < 64) p.p2_splits *= 2;
   *out = p;
   return true;
 }
@@ -600,6 +757,7 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
     set_lds_attr(reinterpret_cast<const void*>(enc_p1_kernel<1>));
     set_lds_attr(reinterpret_cast<const void*>(enc_p1_kernel<0>));
     set_lds_attr(reinterpret_cast<const void*>(enc_p2_kernel));
+    set_lds_attr(reinterpret_cast<const void*>(enc_p2_dense_fx_kernel));
     attr = true;
   }
   const uint32_t nt = static_cast<uint32_t>(p.num_tiles), ch = static_cast<uint32_t>(p.chunk);
@@ -609,16 +767,33 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
   const bool v16 = (reinterpret_cast<uintptr_t>(vec) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(wvec) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(a.src_info) % 16 == 0) && ch % 8 == 0;
+  const bool fxp = p.dense && a.fx != nullptr;  // fixed-point dense P2
   switch (r) {
-    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
-    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
-    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
-    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16); break;
+    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+  }
+  if (fxp) {
+    const uint32_t splits = static_cast<uint32_t>(p.p2_splits);
+    const uint32_t total = static_cast<uint32_t>(r * c);
+    hipLaunchKernelGGL(fx_max_kernel, dim3(1), dim3(1024), 0, stream, a.bmax,
+                       static_cast<uint32_t>(p.num_chunks), a.gmax);
+    hipLaunchKernelGGL(enc_p2_dense_fx_kernel, dim3(nt * splits), dim3(1024), p.tile * 8, stream,
+                       table, reinterpret_cast<long long*>(a.fx), a.gmax, a.vals, a.perm, a.p2_src,
+                       a.p2_pos, static_cast<uint32_t>(p.tile), total,
+                       static_cast<uint32_t>(p.num_chunks), splits, overwrite);
+    if (splits > 1) {
+      const uint32_t blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+      hipLaunchKernelGGL(enc_fx_reduce_kernel, dim3(blocks), dim3(256), 0, stream, table,
+                         reinterpret_cast<const long long*>(a.fx), a.gmax, total,
+                         static_cast<size_t>(p.num_tiles) * p.tile, splits, overwrite);
+    }
+    return;
   }
   if (p.dense) {
     // enough blocks for every CU: split each tile's chunk range
-    uint32_t splits = 1;
-    while (nt * splits < 4 * static_cast<uint32_t>(device_cus()) && splits < 64) splits *= 2;
+    uint32_t splits = static_cast<uint32_t>(p.p2_splits);
     if (overwrite && splits > 1) {
       (void)hipMemsetAsync(table, 0, static_cast<size_t>(r) * c * sizeof(float), stream);
     }

@@ -19,8 +19,10 @@ tile's whole segment of entries fits in LDS), then coordinate chunks, then
 Built with device sorts (one-time O(rd log rd)): ~0.35 GB for ResNet-9.
 Dense geometries (GPT-2: ~249 entries per bucket, a tile's segment does not
 fit in LDS) get the dense plan: 8192-bucket tiles, encode P2 accumulating
-with LDS atomics, and slot 2 (``perm``) holding each entry's in-tile bucket |
-sign at its chunk-major position; the query kernels are the same.  ``build_plan``
+in LDS in 64-bit fixed point (integer atomics: fast and order independent),
+slot 2 (``perm``) holding each entry's in-tile bucket | sign at its
+chunk-major position, and slot 10 the fixed-point scratch; the query kernels
+are the same.  ``build_plan``
 returns None only when d*r >= 2^31.
 """
 from __future__ import annotations
@@ -32,6 +34,9 @@ import torch
 from .._ext import ops
 
 SEG_CAP = 32767
+# entries per bucket the dense plan's 64-bit fixed-point encode has headroom for
+# (2^(62 - 46), csrc/sketch_planned.hip kFxBits)
+FX_BUCKET_CAP = 1 << 16
 
 
 def _to_i16(x: torch.Tensor) -> torch.Tensor:
@@ -50,7 +55,7 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     geo = [int(v) for v in ops().plan_geometry(d, r, c)]
     if not geo:
         return None
-    tile, num_tiles, chunk, num_chunks, dense = geo
+    tile, num_tiles, chunk, num_chunks, dense, p2_splits = geo
     n = d * r
     i64 = torch.int64
     hs = ops().cs_hash_all(hashes, blk_off, blk_sign, num_blocks, d, c, blk_off)  # [d, r]
@@ -86,6 +91,8 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     ent_info = torch.empty(n, dtype=torch.int16, device=device)
     ent_info[global_pos] = _to_i16(lb | sign_bit)
     del tile_id, global_pos
+    if dense and int(torch.bincount(gb, minlength=r * c).max()) > FX_BUCKET_CAP:
+        return None  # the fixed-point encode's headroom (never at hashed loads)
     if dense:
         # encode P2 accumulates with LDS atomics: slot 2 holds each entry's
         # in-tile bucket | sign at its CHUNK-MAJOR position (P1's output
@@ -111,8 +118,14 @@ def build_plan(hashes, blk_off, blk_sign, num_blocks: int, d: int, r: int, c: in
     p2_pos = torch.zeros(num_tiles, num_chunks + 1, dtype=i64, device=device)
     p2_pos[:, 1:] = torch.cumsum(counts_tc, 1)
     i32 = torch.int32
-    return [src_info, ent_info, perm, csr.to(i32), base.to(i32), off.to(i32), seg.to(i32), vals,
+    plan = [src_info, ent_info, perm, csr.to(i32), base.to(i32), off.to(i32), seg.to(i32), vals,
             p2_src.to(i32).contiguous(), p2_pos.to(i32)]
+    if dense:
+        # fixed-point encode P2 scratch: int64 split partials [p2_splits,
+        # num_tiles*tile], then (as floats) max|v| per chunk and overall
+        plan.append(torch.empty(p2_splits * num_tiles * tile + (num_chunks + 2) // 2 + 1,
+                                dtype=torch.int64, device=device))
+    return plan
 
 
 def _bucket_order(gb, order, sorted_key, num_chunks, seg, src_info, chunk, d, r, n, sign_bit,

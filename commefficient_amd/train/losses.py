@@ -15,6 +15,33 @@ import torch.nn.functional as F
 from ..ops.nn import cross_entropy_correct
 
 
+class _unpacked_sequences:
+    """HF transformers (>= 4.5x) checks every causal-mask forward without an
+    attention mask for "packed" sequences (several sequences in one row, told
+    apart by position-id jumps) with ``(mask[:, -1] == 0).all()`` -- a
+    device->host sync in the middle of each forward, which stalls the host's
+    launch queue (GPT-2 PersonaChat round: ~5 ms of GPU idle per round).  Our
+    rows are single sequences (position ids 0..L-1), for which that check
+    returns None; this context skips it for the duration of our own forward."""
+
+    def __enter__(self):
+        try:
+            from transformers import masking_utils as mu
+        except ImportError:  # older transformers: no such check
+            self.mu = None
+            return self
+        self.mu = mu
+        self.orig = getattr(mu, "find_packed_sequence_indices", None)
+        if self.orig is not None:
+            mu.find_packed_sequence_indices = lambda position_ids: None
+        return self
+
+    def __exit__(self, *exc):
+        if self.mu is not None and self.orig is not None:
+            self.mu.find_packed_sequence_indices = self.orig
+        return False
+
+
 def cv_loss(model, inputs, targets, args):
     fused = getattr(model, "loss", None)
     if callable(fused) and len(inputs) == 1:
@@ -46,8 +73,9 @@ def gpt2_loss_train(model, inputs, targets, args, groups=None):
         tok_sum, ntok, mc_logits = _lm_at_labels(m, input_ids, mc_token_ids, lm_labels,
                                                   token_type_ids, inputs[4])
     else:
-        out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids,
-                use_cache=False)
+        with _unpacked_sequences():
+            out = m(input_ids=input_ids, token_type_ids=token_type_ids,
+                    mc_token_ids=mc_token_ids, use_cache=False)
         lm_logits, mc_logits = out.logits, out.mc_logits
         shift_logits = lm_logits[..., :-1, :].float()
         shift_labels = lm_labels[..., 1:]
@@ -66,8 +94,9 @@ def gpt2_loss_train(model, inputs, targets, args, groups=None):
 def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos):
     """(per-example sum of LM token losses, labelled-token count, mc logits)
     with the LM head evaluated only at ``lm_pos`` [B, R] (-1 = pad)."""
-    hid = m.transformer(input_ids=input_ids, token_type_ids=token_type_ids,
-                        use_cache=False)[0]                           # [B, C, L, H]
+    with _unpacked_sequences():
+        hid = m.transformer(input_ids=input_ids, token_type_ids=token_type_ids,
+                            use_cache=False)[0]                       # [B, C, L, H]
     B, C, L, H = hid.shape
     mc_logits = m.multiple_choice_head(hid, mc_token_ids).squeeze(-1)
     valid = lm_pos >= 0
@@ -101,8 +130,9 @@ def gpt2_loss_val(model, inputs, targets, args):
     """Validation: (nll of the LM on the gold reply, mc accuracy) (gpt2_train.py:55-87)."""
     input_ids, mc_token_ids, lm_labels, token_type_ids = inputs[:4]
     m = model.model if hasattr(model, "model") and not hasattr(model, "transformer") else model
-    out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids,
-            use_cache=False)
+    with _unpacked_sequences():
+        out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids,
+                use_cache=False)
     lm_logits, mc_logits = out.logits, out.mc_logits
     B = input_ids.shape[0]
     # the gold candidate is the last one (PERSONA collate order)

@@ -107,6 +107,20 @@ def main():
         fopt.step()
     torch.cuda.synchronize()
     dist.barrier()
+    if os.environ.get("COMMEFF_SYNC_DEBUG"):
+        # report every host<->device synchronisation of the timed rounds with
+        # the Python stack that caused it (they stall the host's enqueue-ahead)
+        import traceback
+        import warnings
+
+        def _show(msg, cat, fn, ln, file=None, line=None):
+            st = [f for f in traceback.extract_stack()[:-1] if "commefficient_amd" in f.filename
+                  or "bench_configs" in f.filename or "transformers" in f.filename]
+            print("SYNC:", str(msg)[:80], "|", " <- ".join(
+                f"{os.path.basename(f.filename)}:{f.lineno}" for f in reversed(st[-6:])), flush=True)
+        warnings.showwarning = _show
+        warnings.simplefilter("always")
+        torch.cuda.set_sync_debug_mode("warn")
     t0 = time.perf_counter()
     for i in range(b.warmup, b.warmup + b.steps):
         out = fed(batches[i])

@@ -177,3 +177,30 @@ def test_planned_gpu_kernels_match_cpu(d, c, r, nb):
     gpu.accumulateVec(v.cuda(), 0.5, w.cuda(), 1e-2)
     torch.testing.assert_close(gpu.table.cpu(), cpu.table, rtol=1e-5, atol=1e-5)
     assert torch.equal(gpu.like(cpu.table.cuda()).query().cpu(), cpu.query())
+
+
+@pytest.mark.gpu
+def test_dense_fixed_point_encode_deterministic_and_accurate():
+    """The dense plan's 64-bit fixed-point encode P2: bitwise identical on
+    repeats, at least as close to a float64 table as fp32 accumulation, and
+    NaN-poisoned by a NaN input."""
+    d, c, r, nb = 3_000_001, 12007, 5, 20
+    gpu = CSVec(d, c, r, device="cuda", numBlocks=nb, seed=5, kernel="planned")
+    assert gpu._use_plan() and len(gpu._plan()) == 11
+    g = torch.Generator().manual_seed(2)
+    # heavy-tailed values: a few large coordinates among many small ones
+    v = torch.randn(d, generator=g) * torch.exp(3 * torch.randn(d, generator=g))
+    vc = v.cuda()
+    gpu.accumulateVec(vc, 1.0, overwrite=True)
+    t1 = gpu.table.clone()
+    for _ in range(3):
+        gpu.accumulateVec(vc, 1.0, overwrite=True)
+        assert torch.equal(gpu.table, t1)
+    cpu = CSVec(d, c, r, device="cpu", numBlocks=nb, seed=5)
+    cpu.accumulateVec(v, 1.0)
+    err = (t1.cpu().double() - cpu.table.double()).abs().max().item()
+    assert err <= 1e-4 * cpu.table.abs().max().item()
+    bad = vc.clone()
+    bad[12345] = float("nan")
+    gpu.accumulateVec(bad, 1.0, overwrite=True)
+    assert torch.isnan(gpu.table).all()
