@@ -1258,6 +1258,121 @@ int64_t binned_scratch_bytes(int64_t d, int64_t r, int64_t c, int64_t num_blocks
   return cs_encode_binned_scratch_bytes(plan_cs_encode_binned(g));
 }
 
+// ------------------------------------------------- GPT-2 block junctions --
+void check_rows_bf16(const at::Tensor& t, int64_t M, int64_t H, const char* name) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.dim() == 2 &&
+                  t.size(0) == M && t.size(1) == H,
+              name, " must be contiguous bf16 [", M, ", ", H, "]");
+}
+
+void check_vec_bf16(const at::Tensor& t, int64_t H, const char* name) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() == H, name,
+              " must be contiguous bf16 [", H, "]");
+}
+
+const void* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr() : nullptr;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> resid_ln_fwd_hip(
+    const at::Tensor& x, const c10::optional<at::Tensor>& p, const c10::optional<at::Tensor>& bias,
+    const at::Tensor& gamma, const at::Tensor& beta, double p_drop, int64_t seed, double eps,
+    bool want_h) {
+  TORCH_CHECK(x.dim() == 2, "resid_ln_fwd: x must be [M, H]");
+  const int64_t M = x.size(0), H = x.size(1);
+  TORCH_CHECK(resid_ln_supported(H), "resid_ln_fwd: H must be 256*V, V in 1..6 (got ", H, ")");
+  check_rows_bf16(x, M, H, "resid_ln_fwd: x");
+  if (p.has_value() && p->defined()) check_rows_bf16(*p, M, H, "resid_ln_fwd: p");
+  if (bias.has_value() && bias->defined()) check_vec_bf16(*bias, H, "resid_ln_fwd: bias");
+  check_vec_bf16(gamma, H, "resid_ln_fwd: gamma");
+  check_vec_bf16(beta, H, "resid_ln_fwd: beta");
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "resid_ln_fwd: p_drop must be in [0, 1)");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto h = want_h ? at::empty_like(x) : at::empty({0}, x.options());
+  auto y = at::empty_like(x);
+  auto f = x.options().dtype(at::kFloat);
+  auto mean = at::empty({M}, f), rstd = at::empty({M}, f);
+  launch_resid_ln_fwd(x.data_ptr(), opt_ptr(p), opt_ptr(bias), gamma.data_ptr(), beta.data_ptr(),
+                      want_h ? h.data_ptr() : nullptr, y.data_ptr(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), M, H, static_cast<float>(p_drop),
+                      static_cast<uint32_t>(seed), static_cast<float>(eps), cur_stream());
+  return {h, y, mean, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> resid_ln_bwd_hip(
+    const at::Tensor& gy, const c10::optional<at::Tensor>& gh, const at::Tensor& h,
+    const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& gamma, double p_drop,
+    int64_t seed, bool want_dp, bool want_dbias) {
+  TORCH_CHECK(h.dim() == 2, "resid_ln_bwd: h must be [M, H]");
+  const int64_t M = h.size(0), H = h.size(1);
+  TORCH_CHECK(resid_ln_supported(H), "resid_ln_bwd: unsupported H ", H);
+  check_rows_bf16(h, M, H, "resid_ln_bwd: h");
+  check_rows_bf16(gy, M, H, "resid_ln_bwd: gy");
+  if (gh.has_value() && gh->defined()) check_rows_bf16(*gh, M, H, "resid_ln_bwd: gh");
+  check_vec_bf16(gamma, H, "resid_ln_bwd: gamma");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == M && rstd.numel() == M &&
+                  rstd.scalar_type() == at::kFloat,
+              "resid_ln_bwd: mean/rstd must be float32 [M]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(h.device());
+  auto dh = at::empty_like(h);
+  auto dp = want_dp ? at::empty_like(h) : at::empty({0}, h.options());
+  auto dgamma = at::empty({H}, gamma.options());
+  auto dbeta = at::empty({H}, gamma.options());
+  auto dbias = want_dbias ? at::empty({H}, gamma.options()) : at::empty({0}, gamma.options());
+  const int G = resid_ln_bwd_blocks(M);
+  auto part = at::empty({G, 3, H}, h.options().dtype(at::kFloat));
+  launch_resid_ln_bwd(gy.data_ptr(), opt_ptr(gh), h.data_ptr(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), gamma.data_ptr(), dh.data_ptr(),
+                      want_dp ? dp.data_ptr() : nullptr, part.data_ptr<float>(), M, H,
+                      static_cast<float>(p_drop), static_cast<uint32_t>(seed), cur_stream());
+  ColsumOut out{{dgamma.data_ptr(), dbeta.data_ptr(),
+                 (want_dp && want_dbias) ? dbias.data_ptr() : nullptr},
+                true};
+  launch_colsum_final(part.data_ptr<float>(), G, (want_dp && want_dbias) ? 3 : 2, H, 3 * H, out,
+                      cur_stream());
+  if (want_dbias && !want_dp) dbias.zero_();
+  return {dh, dp, dgamma, dbeta, dbias};
+}
+
+at::Tensor bias_gelu_fwd_hip(const at::Tensor& u, const at::Tensor& b) {
+  TORCH_CHECK(u.dim() == 2 && u.size(1) % 8 == 0, "bias_gelu_fwd: u must be [M, N], N % 8 == 0");
+  check_rows_bf16(u, u.size(0), u.size(1), "bias_gelu_fwd: u");
+  check_vec_bf16(b, u.size(1), "bias_gelu_fwd: b");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(u.device());
+  auto f = at::empty_like(u);
+  launch_bias_gelu_fwd(u.data_ptr(), b.data_ptr(), f.data_ptr(), u.size(0), u.size(1), cur_stream());
+  return f;
+}
+
+std::tuple<at::Tensor, at::Tensor> bias_act_bwd_hip(const at::Tensor& gf,
+                                                    const c10::optional<at::Tensor>& u,
+                                                    const at::Tensor& b, bool gelu) {
+  TORCH_CHECK(gf.dim() == 2 && gf.size(1) % 8 == 0 && gf.size(1) / 8 <= 1024,
+              "bias_act_bwd: gf must be [M, N], N % 8 == 0, N <= 8192");
+  const int64_t M = gf.size(0), N = gf.size(1);
+  check_rows_bf16(gf, M, N, "bias_act_bwd: gf");
+  check_vec_bf16(b, N, "bias_act_bwd: b");
+  if (gelu) {
+    TORCH_CHECK(u.has_value() && u->defined(), "bias_act_bwd: gelu needs u");
+    check_rows_bf16(*u, M, N, "bias_act_bwd: u");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gf.device());
+  auto du = gelu ? at::empty_like(gf) : at::empty({0}, gf.options());
+  auto db = at::empty({N}, b.options());
+  if (M == 0) {
+    db.zero_();
+    return {du, db};
+  }
+  const int G = bias_act_bwd_blocks(M);
+  auto part = at::empty({G, N}, gf.options().dtype(at::kFloat));
+  launch_bias_act_bwd(gf.data_ptr(), gelu ? u->data_ptr() : nullptr, b.data_ptr(),
+                      gelu ? du.data_ptr() : nullptr, part.data_ptr<float>(), M, N, gelu,
+                      cur_stream());
+  ColsumOut out{{db.data_ptr(), nullptr, nullptr}, true};
+  launch_colsum_final(part.data_ptr<float>(), G, 1, N, N, out, cur_stream());
+  return {du, db};
+}
+
 }  // namespace
 }  // namespace commeff
 
@@ -1325,6 +1440,13 @@ TORCH_LIBRARY(commeff, m) {
         "int seed, bool out_bf16, Tensor? keys=None) -> Tensor");
   m.def("binned_scratch_bytes(int d, int r, int c, int num_blocks) -> int",
         &commeff::binned_scratch_bytes);
+  m.def("resid_ln_fwd(Tensor x, Tensor? p, Tensor? bias, Tensor gamma, Tensor beta, float p_drop, "
+        "int seed, float eps, bool want_h) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("resid_ln_bwd(Tensor gy, Tensor? gh, Tensor h, Tensor mean, Tensor rstd, Tensor gamma, "
+        "float p_drop, int seed, bool want_dp, bool want_dbias) "
+        "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("bias_gelu_fwd(Tensor u, Tensor b) -> Tensor");
+  m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CPU, m) {
@@ -1394,4 +1516,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("zero_at", &zero_at_hip);
   m.impl("scatter_dense", &scatter_dense_hip);
   m.impl("augment_u8_nhwc", &augment_hip);
+  m.impl("resid_ln_fwd", &resid_ln_fwd_hip);
+  m.impl("resid_ln_bwd", &resid_ln_bwd_hip);
+  m.impl("bias_gelu_fwd", &bias_gelu_fwd_hip);
+  m.impl("bias_act_bwd", &bias_act_bwd_hip);
 }

@@ -295,4 +295,34 @@ void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx,
                             uint64_t seed, const int64_t* keys, uint16_t* out_bf16,
                             int out_cstride, hipStream_t stream);
 
+// ---------------------------------------------------------- transformer --
+// GPT-2 block junctions on bf16 [M, H] rows (transformer.hip, ops/transformer.py).
+// h = x + drop(p + bias) (p null: h = drop(x)); y = LN(h)*gamma + beta
+bool resid_ln_supported(int64_t H);  // H = 256*V, V in 1..6
+void launch_resid_ln_fwd(const void* x, const void* p, const void* bias, const void* gamma,
+                         const void* beta, void* h_out, void* y_out, float* mean, float* rstd,
+                         int64_t M, int64_t H, float p_drop, uint32_t seed, float eps,
+                         hipStream_t stream);
+// dh = LN'(gy) + gh; dp = drop'(dh); part [blocks][3][H] = column partials of
+// (gy*xhat, gy, dp)
+int resid_ln_bwd_blocks(int64_t M);
+void launch_resid_ln_bwd(const void* gy, const void* gh, const void* h, const float* mean,
+                         const float* rstd, const void* gamma, void* dh_out, void* dp_out,
+                         float* part, int64_t M, int64_t H, float p_drop, uint32_t seed,
+                         hipStream_t stream);
+// f = gelu_tanh(u + b), N % 8 == 0
+void launch_bias_gelu_fwd(const void* u, const void* b, void* f, int64_t M, int64_t N,
+                          hipStream_t stream);
+// du = gf * gelu_tanh'(u + b) (gelu) or gf; part [blocks][N] = column partials of du
+int bias_act_bwd_blocks(int64_t M);
+void launch_bias_act_bwd(const void* gf, const void* u, const void* b, void* du, float* part,
+                         int64_t M, int64_t N, bool gelu, hipStream_t stream);
+struct ColsumOut {
+  void* p[3];  // [N] outputs per partial quantity (nullptr: skip)
+  bool bf16;
+};
+// out_q[c] = sum over b < G of part[b*stride + q*N + c], q < Q (fixed order)
+void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,
+                         const ColsumOut& out, hipStream_t stream);
+
 }  // namespace commeff

@@ -1,0 +1,311 @@
+"""GPT-2 transformer forward/backward on the native block-junction kernels.
+
+The reference trains HF ``GPT2DoubleHeadsModel`` (/root/reference/CommEfficient/
+gpt2_train.py:4-6,262-273), whose pre-LN block runs, per sublayer, separate
+kernels for the residual add, dropout, LayerNorm (forward and three backward
+kernels), GELU and the bias-gradient reductions.  ``gpt2_hidden`` computes the
+same function over the same HF parameters with one native kernel per
+junction (csrc/transformer.hip):
+
+    y0 = LN1_0(drop(wte[ids] + wpe[pos] + wte[tt]))              _EmbedLN
+    per block:
+      qkv = y @ W_attn + b_attn                                     _Linear (bias grad native)
+      o   = SDPA(q, k, v, causal, attn dropout)                     fused attention kernels
+      h, y = h + drop(o @ W_proj + b_proj), LN2(h)                  _ResidLN
+      f   = gelu_tanh(y @ W_fc + b_fc)                              _FcGelu
+      h, y = h + drop(f @ W_mproj + b_mproj), LN1_next|LN_f(h)      _ResidLN
+
+GEMMs stay on hipBLASLt (``torch.mm``).  Backward of each junction is one
+kernel (LN backward + residual gradient + dropout backward + column partials
+of dgamma/dbeta/dbias) plus one fixed-order column reduction, so every
+gradient is deterministic for a given dropout seed.  Dropout masks are a
+32-bit counter hash of (seed, element) recomputed in backward (no mask
+tensors).  Seeds come from a host-side counter per model: no device syncs.
+
+On CPU the same Functions run on the PyTorch reference implementations below
+(``_ref_*``), which mirror the kernels' bf16 rounding points; they are the
+numerics oracle of tests/test_transformer.py.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .._ext import ops as _ops
+
+_M32 = 0xFFFFFFFF
+
+
+# ------------------------------------------------------------- references
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def drop_keep(numel: int, seed: int, p: float, device=None) -> torch.Tensor:
+    """The kernels' dropout keep-mask of ``numel`` consecutive elements."""
+    idx = torch.arange(numel, dtype=torch.int64, device=device)
+    hi = _mix32(((idx >> 32) + (seed & _M32)) & _M32)
+    h = _mix32((idx & _M32) ^ hi)
+    thresh = min(int(p * 4294967296.0), _M32) if p > 0 else 0
+    return h >= thresh
+
+
+def _bf(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.bfloat16).float()
+
+
+def _ref_resid_ln_fwd(x, p, bias, gamma, beta, p_drop, seed, eps, want_h):
+    M, H = x.shape
+    v = x.float()
+    scale = 1.0 / (1.0 - p_drop) if p_drop > 0 else 1.0
+    keep = drop_keep(M * H, seed, p_drop, x.device).view(M, H) if p_drop > 0 else None
+    if p is not None:
+        t = _bf(p.float() + (bias.float() if bias is not None else 0.0))
+        if keep is not None:
+            t = torch.where(keep, _bf(t * scale), torch.zeros_like(t))
+        v = _bf(v + t)
+    elif keep is not None:
+        v = torch.where(keep, _bf(v * scale), torch.zeros_like(v))
+    mean = v.mean(1)
+    rstd = torch.rsqrt(((v - mean[:, None]) ** 2).mean(1) + eps)
+    y = ((v - mean[:, None]) * rstd[:, None] * gamma.float() + beta.float()).to(torch.bfloat16)
+    h = v.to(torch.bfloat16) if want_h else x.new_empty(0)
+    return h, y, mean, rstd
+
+
+def _ref_resid_ln_bwd(gy, gh, h, mean, rstd, gamma, p_drop, seed, want_dp, want_dbias):
+    M, H = h.shape
+    xh = (h.float() - mean[:, None]) * rstd[:, None]
+    dy = gy.float()
+    dx = dy * gamma.float()
+    s1 = dx.mean(1, keepdim=True)
+    s2 = (dx * xh).mean(1, keepdim=True)
+    dh = rstd[:, None] * (dx - s1 - xh * s2)
+    if gh is not None:
+        dh = dh + gh.float()
+    dh = _bf(dh)
+    dgamma = (dy * xh).sum(0).to(gamma.dtype)
+    dbeta = dy.sum(0).to(gamma.dtype)
+    dp = h.new_empty(0)
+    dbias = gamma.new_empty(0) if not want_dbias else torch.zeros_like(gamma)
+    if want_dp:
+        dpf = dh
+        if p_drop > 0:
+            keep = drop_keep(M * H, seed, p_drop, h.device).view(M, H)
+            dpf = torch.where(keep, _bf(dh / (1.0 - p_drop)), torch.zeros_like(dh))
+        dp = dpf.to(torch.bfloat16)
+        if want_dbias:
+            dbias = dpf.sum(0).to(gamma.dtype)
+    return dh.to(torch.bfloat16), dp, dgamma, dbeta, dbias
+
+
+_GK = 0.7978845608028654
+_GC = 0.044715
+
+
+def _ref_bias_gelu_fwd(u, b):
+    x = _bf(u.float() + b.float())
+    return (0.5 * x * (1.0 + torch.tanh(_GK * (x + _GC * x ** 3)))).to(torch.bfloat16)
+
+
+def _ref_bias_act_bwd(gf, u, b, gelu):
+    g = gf.float()
+    if gelu:
+        x = _bf(u.float() + b.float())
+        t = torch.tanh(_GK * (x + _GC * x ** 3))
+        g = _bf(g * (0.5 * (1.0 + t) + 0.5 * x * (1.0 - t * t) * _GK * (1.0 + 3.0 * _GC * x * x)))
+        return g.to(torch.bfloat16), g.sum(0).to(b.dtype)
+    return gf.new_empty(0), g.sum(0).to(b.dtype)
+
+
+class _Impl:
+    """torch.ops.commeff on HIP tensors, the references on CPU."""
+
+    @staticmethod
+    def resid_ln_fwd(x, *a):
+        return (_ops().resid_ln_fwd if x.is_cuda else _ref_resid_ln_fwd)(x, *a)
+
+    @staticmethod
+    def resid_ln_bwd(gy, *a):
+        return (_ops().resid_ln_bwd if gy.is_cuda else _ref_resid_ln_bwd)(gy, *a)
+
+    @staticmethod
+    def bias_gelu_fwd(u, b):
+        return (_ops().bias_gelu_fwd if u.is_cuda else _ref_bias_gelu_fwd)(u, b)
+
+    @staticmethod
+    def bias_act_bwd(gf, u, b, gelu):
+        return (_ops().bias_act_bwd if gf.is_cuda else _ref_bias_act_bwd)(gf, u, b, gelu)
+
+
+def _c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    return None if t is None else t.contiguous()
+
+
+# ---------------------------------------------------------------- autograd
+class _EmbedLN(torch.autograd.Function):
+    """h = drop(x); y = LN(h)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, p_drop, seed, eps):
+        h, y, mean, rstd = _Impl.resid_ln_fwd(x, None, None, gamma, beta, p_drop, seed, eps, True)
+        ctx.save_for_backward(h, mean, rstd, gamma)
+        ctx.cfg = (p_drop, seed)
+        return h, y
+
+    @staticmethod
+    def backward(ctx, gh, gy):
+        h, mean, rstd, gamma = ctx.saved_tensors
+        p_drop, seed = ctx.cfg
+        gy = torch.zeros_like(h) if gy is None else gy.contiguous()
+        _, dx, dgamma, dbeta, _ = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma, p_drop,
+                                                     seed, True, False)
+        return dx, dgamma, dbeta, None, None, None
+
+
+class _ResidLN(torch.autograd.Function):
+    """p = o @ W; h = x + drop(p + b); y = LN(h)."""
+
+    @staticmethod
+    def forward(ctx, x, o, W, b, gamma, beta, p_drop, seed, eps):
+        p = torch.mm(o, W)
+        h, y, mean, rstd = _Impl.resid_ln_fwd(x, p, b, gamma, beta, p_drop, seed, eps, True)
+        ctx.save_for_backward(o, W, h, mean, rstd, gamma)
+        ctx.cfg = (p_drop, seed)
+        return h, y
+
+    @staticmethod
+    def backward(ctx, gh, gy):
+        o, W, h, mean, rstd, gamma = ctx.saved_tensors
+        p_drop, seed = ctx.cfg
+        gy = torch.zeros_like(h) if gy is None else gy.contiguous()
+        dh, dp, dgamma, dbeta, dbias = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma,
+                                                          p_drop, seed, True, True)
+        do = torch.mm(dp, W.t()) if ctx.needs_input_grad[1] else None
+        dW = torch.mm(o.t(), dp) if ctx.needs_input_grad[2] else None
+        return dh, do, dW, dbias, dgamma, dbeta, None, None, None
+
+
+class _FcGelu(torch.autograd.Function):
+    """f = gelu_tanh(a @ W + b)."""
+
+    @staticmethod
+    def forward(ctx, a, W, b):
+        u = torch.mm(a, W)
+        f = _Impl.bias_gelu_fwd(u, b)
+        ctx.save_for_backward(a, W, u, b)
+        return f
+
+    @staticmethod
+    def backward(ctx, gf):
+        a, W, u, b = ctx.saved_tensors
+        du, db = _Impl.bias_act_bwd(gf.contiguous(), u, b, True)
+        da = torch.mm(du, W.t()) if ctx.needs_input_grad[0] else None
+        dW = torch.mm(a.t(), du) if ctx.needs_input_grad[1] else None
+        return da, dW, db
+
+
+class _Linear(torch.autograd.Function):
+    """y = a @ W + b (bias in the GEMM epilogue forward, native column sum backward)."""
+
+    @staticmethod
+    def forward(ctx, a, W, b):
+        ctx.save_for_backward(a, W, b)
+        return torch.addmm(b, a, W)
+
+    @staticmethod
+    def backward(ctx, gy):
+        a, W, b = ctx.saved_tensors
+        gy = gy.contiguous()
+        _, db = _Impl.bias_act_bwd(gy, None, b, False)
+        da = torch.mm(gy, W.t()) if ctx.needs_input_grad[0] else None
+        dW = torch.mm(a.t(), gy) if ctx.needs_input_grad[1] else None
+        return da, dW, db
+
+
+# ------------------------------------------------------------------ model
+class _Seeds:
+    """Host-side dropout seed stream (64-bit LCG), one per model."""
+
+    def __init__(self, base: int):
+        self.s = (int(base) * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF
+
+    def next(self) -> int:
+        self.s = (self.s * 6364136223846793005 + 1442695040888963407) & 0xFFFFFFFFFFFFFFFF
+        return self.s >> 32
+
+
+def native_ok(tr, input_ids: torch.Tensor) -> bool:
+    """The native path covers HF GPT2Model blocks as configured for GPT-2
+    (pre-LN, tanh GELU, default attention scaling) with bf16 weights."""
+    cfg = getattr(tr, "config", None)
+    if cfg is None or getattr(cfg, "model_type", "") != "gpt2" or not hasattr(tr, "h"):
+        return False
+    H = cfg.n_embd
+    return (tr.wte.weight.dtype == torch.bfloat16
+            and (not input_ids.is_cuda or _native_hidden_size(H))
+            and cfg.activation_function in ("gelu_new", "gelu_pytorch_tanh")
+            and (cfg.n_inner is None or cfg.n_inner == 4 * H)
+            and cfg.scale_attn_weights and not cfg.scale_attn_by_inverse_layer_idx
+            and not cfg.reorder_and_upcast_attn and not cfg.add_cross_attention
+            and H % cfg.n_head == 0)
+
+
+def _native_hidden_size(H: int) -> bool:
+    return H % 256 == 0 and 1 <= H // 256 <= 6
+
+
+def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tensor] = None):
+    """``ln_f`` output of HF ``GPT2Model`` ``tr`` for ``input_ids`` [..., L]
+    (same as ``tr(input_ids, token_type_ids=...)[0]``) on the native junction
+    kernels.  Dropout follows ``tr.training`` like the HF modules."""
+    cfg = tr.config
+    shp = input_ids.shape
+    L = shp[-1]
+    H = cfg.n_embd
+    ids = input_ids.reshape(-1, L)
+    Nn = ids.shape[0]
+    M = Nn * L
+    nh = cfg.n_head
+    eps = float(cfg.layer_norm_epsilon)
+    train = tr.training
+
+    def _p(mod, default):  # the HF dropout module's rate (tests may zero it)
+        return float(getattr(mod, "p", default)) if train else 0.0
+
+    pe = _p(getattr(tr, "drop", None), cfg.embd_pdrop)
+    seeds = getattr(tr, "_commeff_seeds", None)
+    if seeds is None:
+        seeds = _Seeds(torch.initial_seed())
+        tr._commeff_seeds = seeds
+    pos = torch.arange(L, device=ids.device)
+    e = tr.wte(ids) + tr.wpe(pos)
+    if token_type_ids is not None:
+        e = e + tr.wte(token_type_ids.reshape(-1, L))
+    blocks = tr.h
+    ln = blocks[0].ln_1
+    h, y = _EmbedLN.apply(e.reshape(M, H), ln.weight, ln.bias, pe, seeds.next(), eps)
+    for i, blk in enumerate(blocks):
+        at = blk.attn
+        qkv = _Linear.apply(y, at.c_attn.weight, at.c_attn.bias)
+        # split (not a [3, ...] view + unbind): its backward is one contiguous cat
+        q, k, v = (t.view(Nn, L, nh, H // nh).transpose(1, 2) for t in qkv.split(H, dim=1))
+        o = F.scaled_dot_product_attention(
+            q, k, v, dropout_p=_p(getattr(at, "attn_dropout", None), cfg.attn_pdrop),
+            is_causal=True)
+        o = o.transpose(1, 2).reshape(M, H)
+        h, y = _ResidLN.apply(h, o, at.c_proj.weight, at.c_proj.bias, blk.ln_2.weight,
+                              blk.ln_2.bias, _p(getattr(at, "resid_dropout", None), cfg.resid_pdrop),
+                              seeds.next(), eps)
+        f = _FcGelu.apply(y, blk.mlp.c_fc.weight, blk.mlp.c_fc.bias)
+        nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else tr.ln_f
+        h, y = _ResidLN.apply(h, f, blk.mlp.c_proj.weight, blk.mlp.c_proj.bias, nxt.weight,
+                              nxt.bias, _p(getattr(blk.mlp, "dropout", None), cfg.resid_pdrop),
+                              seeds.next(), eps)
+    return y.view(*shp, H)

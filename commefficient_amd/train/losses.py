@@ -13,6 +13,7 @@ import torch
 import torch.nn.functional as F
 
 from ..ops.nn import cross_entropy_correct
+from ..ops import transformer as _tx
 
 
 class _unpacked_sequences:
@@ -40,6 +41,17 @@ class _unpacked_sequences:
         if self.mu is not None and self.orig is not None:
             self.mu.find_packed_sequence_indices = self.orig
         return False
+
+
+def gpt2_hidden_states(m, input_ids, token_type_ids, args=None):
+    """Final hidden states of the double-heads model's transformer: the native
+    junction kernels (ops/transformer.py) unless ``--transformer hf`` or the
+    config is outside what they cover (then the HF module forward)."""
+    tr = m.transformer
+    if getattr(args, "transformer", "native") == "native" and _tx.native_ok(tr, input_ids):
+        return _tx.gpt2_hidden(tr, input_ids, token_type_ids)
+    with _unpacked_sequences():
+        return tr(input_ids=input_ids, token_type_ids=token_type_ids, use_cache=False)[0]
 
 
 def cv_loss(model, inputs, targets, args):
@@ -71,12 +83,9 @@ def gpt2_loss_train(model, inputs, targets, args, groups=None):
         # LM head only at the labelled positions (data/fed_persona.py
         # label_positions): same loss, ~1/17 of the vocabulary GEMM + softmax
         tok_sum, ntok, mc_logits = _lm_at_labels(m, input_ids, mc_token_ids, lm_labels,
-                                                  token_type_ids, inputs[4])
+                                                  token_type_ids, inputs[4], args)
     else:
-        with _unpacked_sequences():
-            out = m(input_ids=input_ids, token_type_ids=token_type_ids,
-                    mc_token_ids=mc_token_ids, use_cache=False)
-        lm_logits, mc_logits = out.logits, out.mc_logits
+        lm_logits, mc_logits = _double_heads(m, input_ids, token_type_ids, mc_token_ids, args)
         shift_logits = lm_logits[..., :-1, :].float()
         shift_labels = lm_labels[..., 1:]
         tok = F.cross_entropy(shift_logits.reshape(-1, shift_logits.size(-1)),
@@ -91,12 +100,24 @@ def gpt2_loss_train(model, inputs, targets, args, groups=None):
     return args.lm_coef * lm + args.mc_coef * mc, [acc]
 
 
-def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos):
+def _double_heads(m, input_ids, token_type_ids, mc_token_ids, args, last_only=False):
+    """(lm_logits, mc_logits) of HF's double-heads forward (``last_only``: LM
+    logits of the last candidate only)."""
+    if hasattr(m, "transformer") and hasattr(m, "multiple_choice_head"):
+        hid = gpt2_hidden_states(m, input_ids, token_type_ids, args)
+        mc_logits = m.multiple_choice_head(hid, mc_token_ids).squeeze(-1)
+        lm_logits = m.lm_head(hid[:, -1] if last_only else hid)
+        return lm_logits, mc_logits
+    with _unpacked_sequences():
+        out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids,
+                use_cache=False)
+    return (out.logits[:, -1] if last_only else out.logits), out.mc_logits
+
+
+def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos, args=None):
     """(per-example sum of LM token losses, labelled-token count, mc logits)
     with the LM head evaluated only at ``lm_pos`` [B, R] (-1 = pad)."""
-    with _unpacked_sequences():
-        hid = m.transformer(input_ids=input_ids, token_type_ids=token_type_ids,
-                            use_cache=False)[0]                       # [B, C, L, H]
+    hid = gpt2_hidden_states(m, input_ids, token_type_ids, args)          # [B, C, L, H]
     B, C, L, H = hid.shape
     mc_logits = m.multiple_choice_head(hid, mc_token_ids).squeeze(-1)
     valid = lm_pos >= 0
@@ -130,13 +151,11 @@ def gpt2_loss_val(model, inputs, targets, args):
     """Validation: (nll of the LM on the gold reply, mc accuracy) (gpt2_train.py:55-87)."""
     input_ids, mc_token_ids, lm_labels, token_type_ids = inputs[:4]
     m = model.model if hasattr(model, "model") and not hasattr(model, "transformer") else model
-    with _unpacked_sequences():
-        out = m(input_ids=input_ids, token_type_ids=token_type_ids, mc_token_ids=mc_token_ids,
-                use_cache=False)
-    lm_logits, mc_logits = out.logits, out.mc_logits
-    B = input_ids.shape[0]
     # the gold candidate is the last one (PERSONA collate order)
-    lg = lm_logits[:, -1, :-1, :].float()
+    lm_last, mc_logits = _double_heads(m, input_ids, token_type_ids, mc_token_ids, args,
+                                       last_only=True)
+    B = input_ids.shape[0]
+    lg = lm_last[:, :-1, :].float()
     lb = lm_labels[:, -1, 1:]
     tok = F.cross_entropy(lg.reshape(-1, lg.size(-1)), lb.reshape(-1), ignore_index=-100,
                           reduction="none").view(B, -1)

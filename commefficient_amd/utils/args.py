@@ -189,6 +189,10 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--conv", choices=["native", "miopen"], default="native",
                    help="3x3 conv(+relu+pool) units: native MFMA kernels (csrc/conv.hip) "
                         "where shapes fit, or MIOpen everywhere")
+    g.add_argument("--transformer", choices=["native", "hf"], default="native",
+                   help="GPT-2 blocks: native junction kernels (csrc/transformer.hip: fused "
+                        "residual+dropout+LayerNorm, bias+GELU, bias gradients) around "
+                        "hipBLASLt GEMMs and SDPA, or the HF module forward")
     g.add_argument("--graph", choices=["auto", "on", "off"], default="off",
                    help="replay merged-client rounds from captured HIP graphs "
                         "(parallel/graph.py) once a round geometry repeats (auto/on: "

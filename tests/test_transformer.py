@@ -1,0 +1,180 @@
+"""GPT-2 block-junction kernels (csrc/transformer.hip, ops/transformer.py).
+
+CPU: the native-path forward/backward (on the PyTorch references of the
+kernels) equals HF's GPT2Model in fp32 to bf16 accuracy, dropout masks have
+the requested rate and the backward uses the forward's mask.
+GPU: every kernel against its fp32 PyTorch reference (same dropout hash), and
+the whole native GPT-2 hidden-state forward/backward against HF on the GPU.
+"""
+import pytest
+import torch
+
+from commefficient_amd.models.gpt2 import build_double_heads
+from commefficient_amd.ops import transformer as tx
+
+
+def _tiny_gpt2(n_embd=256, n_layer=2, n_head=4, seed=0):
+    torch.manual_seed(seed)
+    m = build_double_heads("gpt2", n_special=0, n_layer=n_layer, n_embd=n_embd, n_head=n_head,
+                           n_positions=64)
+    return m
+
+
+def _inputs(Nb=3, C=2, L=20, V=500, seed=1, device="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, V, (Nb, C, L), generator=g)
+    tt = torch.randint(0, V, (Nb, C, L), generator=g)
+    return ids.to(device), tt.to(device)
+
+
+def _grads(model):
+    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters()
+            if p.grad is not None}
+
+
+def _hf_vs_native(device):
+    import copy
+    ref = _tiny_gpt2().to(device).eval()
+    # bf16-representable weights so both sides start from identical parameters
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    nat = copy.deepcopy(ref).to(torch.bfloat16)
+    ids, tt = _inputs(device=device)
+    gw = torch.randn(*ids.shape, 256, generator=torch.Generator().manual_seed(3)).to(device)
+    h_ref = ref.transformer(input_ids=ids, token_type_ids=tt, use_cache=False)[0]
+    (h_ref * gw).sum().backward()
+    assert tx.native_ok(nat.transformer, ids)
+    h_nat = tx.gpt2_hidden(nat.transformer, ids, tt)
+    (h_nat.float() * gw).sum().backward()
+    torch.testing.assert_close(h_nat.float(), h_ref, rtol=3e-2, atol=6e-2)
+    gr, gn = _grads(ref), _grads(nat)
+    assert set(gr) == set(gn)
+    for n in gr:
+        if "multiple_choice" in n or "lm_head" in n:
+            continue
+        rel = (gn[n] - gr[n]).norm() / gr[n].norm().clamp_min(1e-6)
+        assert rel < 6e-2, (n, float(rel))
+
+
+def test_native_path_matches_hf_cpu():
+    _hf_vs_native("cpu")
+
+
+def test_dropout_mask_rate_and_determinism():
+    k = tx.drop_keep(1 << 16, seed=12345, p=0.1)
+    assert abs(1 - k.float().mean().item() - 0.1) < 0.01
+    assert torch.equal(k, tx.drop_keep(1 << 16, seed=12345, p=0.1))
+    assert not torch.equal(k, tx.drop_keep(1 << 16, seed=12346, p=0.1))
+
+
+def test_resid_ln_dropout_backward_uses_forward_mask():
+    """With dropout the junction's gradient equals autograd through an explicit
+    composition that uses the same keep mask."""
+    torch.manual_seed(0)
+    M, H, p = 16, 256, 0.25
+    x = torch.randn(M, H).to(torch.bfloat16).requires_grad_()
+    o = torch.randn(M, 64).to(torch.bfloat16).requires_grad_()
+    W = (torch.randn(64, H) * 0.1).to(torch.bfloat16).requires_grad_()
+    b = (torch.randn(H) * 0.1).to(torch.bfloat16).requires_grad_()
+    gam = (1 + 0.1 * torch.randn(H)).to(torch.bfloat16).requires_grad_()
+    bet = (0.1 * torch.randn(H)).to(torch.bfloat16).requires_grad_()
+    h, y = tx._ResidLN.apply(x, o, W, b, gam, bet, p, 777, 1e-5)
+    gy, gh = torch.randn(M, H), torch.randn(M, H)
+    (y.float() * gy).sum().add_((h.float() * gh).sum()).backward()
+    keep = tx.drop_keep(M * H, 777, p).view(M, H).float()
+    leaves = [t.detach().float().requires_grad_() for t in (x, o, W, b, gam, bet)]
+    xf, of, Wf, bf, gf, bef = leaves
+    hf = xf + keep * (of @ Wf + bf) / (1 - p)
+    yf = torch.nn.functional.layer_norm(hf, (H,), gf, bef, 1e-5)
+    (yf * gy).sum().add_((hf * gh).sum()).backward()
+    torch.testing.assert_close(h.float(), hf, rtol=2e-2, atol=5e-2)
+    for a, r in zip((x, o, W, b, gam, bet), leaves):
+        rel = (a.grad.float() - r.grad).norm() / r.grad.norm()
+        assert rel < 3e-2, float(rel)
+
+
+# ---------------------------------------------------------------- GPU
+def _rows(M, H, dev, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(M, H, generator=g) * scale).to(torch.bfloat16).to(dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H", [256, 768, 1024])
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+@pytest.mark.parametrize("branch", [True, False])
+def test_resid_ln_kernels_vs_reference_gpu(H, p_drop, branch):
+    from commefficient_amd._ext import ops
+    dev = "cuda"
+    M = 1000
+    x, p = _rows(M, H, dev, seed=1), _rows(M, H, dev, 0.5, seed=2)
+    bias = _rows(1, H, dev, 0.1, seed=3).view(H)
+    gam = (1 + _rows(1, H, dev, 0.1, seed=4).float()).to(torch.bfloat16).view(H)
+    bet = _rows(1, H, dev, 0.1, seed=5).view(H)
+    pb = p if branch else None
+    bb = bias if branch else None
+    out = ops().resid_ln_fwd(x, pb, bb, gam, bet, p_drop, 99, 1e-5, True)
+    ref = tx._ref_resid_ln_fwd(x, pb, bb, gam, bet, p_drop, 99, 1e-5, True)
+    torch.testing.assert_close(out[0].float(), ref[0].float(), rtol=1e-2, atol=1e-2)
+    assert torch.equal(out[0] == 0, ref[0] == 0)  # identical dropout masks
+    torch.testing.assert_close(out[1].float(), ref[1].float(), rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(out[2], ref[2], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(out[3], ref[3], rtol=1e-3, atol=1e-3)
+    gy, gh = _rows(M, H, dev, seed=6), _rows(M, H, dev, seed=7)
+    h = out[0]
+    bo = ops().resid_ln_bwd(gy, gh, h, out[2], out[3], gam, p_drop, 99, True, branch)
+    br = tx._ref_resid_ln_bwd(gy, gh, h, out[2], out[3], gam, p_drop, 99, True, branch)
+    for a, r in zip(bo, br):
+        if r.numel() == 0:
+            continue
+        rel = (a.float() - r.float()).norm() / r.float().norm().clamp_min(1e-6)
+        assert rel < 1e-2, float(rel)
+    assert torch.equal(bo[1] == 0, br[1] == 0) or p_drop == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [768, 2304, 3072])
+def test_bias_gelu_kernels_vs_reference_gpu(N):
+    from commefficient_amd._ext import ops
+    dev = "cuda"
+    M = 777
+    u = _rows(M, N, dev, 2.0, seed=1)
+    b = _rows(1, N, dev, 0.5, seed=2).view(N)
+    f = ops().bias_gelu_fwd(u, b)
+    torch.testing.assert_close(f.float(), tx._ref_bias_gelu_fwd(u, b).float(), rtol=1e-2,
+                               atol=1e-2)
+    gf = _rows(M, N, dev, seed=3)
+    for gelu in (True, False):
+        du, db = ops().bias_act_bwd(gf, u, b, gelu)
+        rdu, rdb = tx._ref_bias_act_bwd(gf, u, b, gelu)
+        if gelu:
+            torch.testing.assert_close(du.float(), rdu.float(), rtol=2e-2, atol=2e-2)
+        rel = (db.float() - rdb.float()).norm() / rdb.float().norm()
+        assert rel < 1e-2, float(rel)
+
+
+@pytest.mark.gpu
+def test_native_path_matches_hf_gpu():
+    _hf_vs_native("cuda")
+
+
+@pytest.mark.gpu
+def test_native_gpt2_loss_grad_deterministic_gpu():
+    """Same seeds -> bitwise identical gradients (fixed-order reductions) for
+    every parameter whose gradient does not pass through the attention
+    backward (the last block's MLP / ln_2 and ln_f)."""
+    import copy
+    base = _tiny_gpt2().cuda().to(torch.bfloat16).train()
+    ids, tt = _inputs(device="cuda")
+    out = []
+    for _ in range(2):
+        m = copy.deepcopy(base)
+        m.transformer._commeff_seeds = tx._Seeds(5)
+        torch.manual_seed(0)  # attention dropout
+        h = tx.gpt2_hidden(m.transformer, ids, tt)
+        h.float().square().mean().backward()
+        keep = ("h.1.mlp", "h.1.ln_2", "ln_f", "h.1.attn.c_proj")
+        out.append(torch.cat([p.grad.reshape(-1).float() for n, p in m.named_parameters()
+                              if p.grad is not None and any(k in n for k in keep)]))
+    assert torch.equal(out[0], out[1])
