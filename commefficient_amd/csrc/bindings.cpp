@@ -1299,10 +1299,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> resid_ln_fwd_hip(
   return {h, y, mean, rstd};
 }
 
+// an optional fp32 gradient sink: out += colsum (mode 2) instead of a new bf16 tensor
+void* sink_ptr(const c10::optional<at::Tensor>& sink, int64_t n, const char* name) {
+  if (!sink.has_value() || !sink->defined()) return nullptr;
+  TORCH_CHECK(sink->scalar_type() == at::kFloat && sink->is_contiguous() && sink->numel() == n,
+              name, " sink must be contiguous float32 [", n, "]");
+  return sink->data_ptr();
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> resid_ln_bwd_hip(
     const at::Tensor& gy, const c10::optional<at::Tensor>& gh, const at::Tensor& h,
     const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& gamma, double p_drop,
-    int64_t seed, bool want_dp, bool want_dbias) {
+    int64_t seed, bool want_dp, bool want_dbias, const c10::optional<at::Tensor>& sgamma,
+    const c10::optional<at::Tensor>& sbeta, const c10::optional<at::Tensor>& sbias) {
   TORCH_CHECK(h.dim() == 2, "resid_ln_bwd: h must be [M, H]");
   const int64_t M = h.size(0), H = h.size(1);
   TORCH_CHECK(resid_ln_supported(H), "resid_ln_bwd: unsupported H ", H);
@@ -1313,24 +1322,27 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> resid_ln_
   TORCH_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == M && rstd.numel() == M &&
                   rstd.scalar_type() == at::kFloat,
               "resid_ln_bwd: mean/rstd must be float32 [M]");
+  TORCH_CHECK(want_dp || !want_dbias, "resid_ln_bwd: dbias needs dp");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(h.device());
+  void* pg = sink_ptr(sgamma, H, "resid_ln_bwd: gamma");
+  void* pb = sink_ptr(sbeta, H, "resid_ln_bwd: beta");
+  void* pc = want_dbias ? sink_ptr(sbias, H, "resid_ln_bwd: bias") : nullptr;
+  auto empty = at::empty({0}, gamma.options());
   auto dh = at::empty_like(h);
   auto dp = want_dp ? at::empty_like(h) : at::empty({0}, h.options());
-  auto dgamma = at::empty({H}, gamma.options());
-  auto dbeta = at::empty({H}, gamma.options());
-  auto dbias = want_dbias ? at::empty({H}, gamma.options()) : at::empty({0}, gamma.options());
+  auto dgamma = pg ? empty : at::empty({H}, gamma.options());
+  auto dbeta = pb ? empty : at::empty({H}, gamma.options());
+  auto dbias = (want_dbias && !pc) ? at::empty({H}, gamma.options()) : empty;
   const int G = resid_ln_bwd_blocks(M);
   auto part = at::empty({G, 3, H}, h.options().dtype(at::kFloat));
   launch_resid_ln_bwd(gy.data_ptr(), opt_ptr(gh), h.data_ptr(), mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), gamma.data_ptr(), dh.data_ptr(),
                       want_dp ? dp.data_ptr() : nullptr, part.data_ptr<float>(), M, H,
                       static_cast<float>(p_drop), static_cast<uint32_t>(seed), cur_stream());
-  ColsumOut out{{dgamma.data_ptr(), dbeta.data_ptr(),
-                 (want_dp && want_dbias) ? dbias.data_ptr() : nullptr},
-                true};
-  launch_colsum_final(part.data_ptr<float>(), G, (want_dp && want_dbias) ? 3 : 2, H, 3 * H, out,
-                      cur_stream());
-  if (want_dbias && !want_dp) dbias.zero_();
+  ColsumOut out{{pg ? pg : dgamma.data_ptr(), pb ? pb : dbeta.data_ptr(),
+                 want_dbias ? (pc ? pc : dbias.data_ptr()) : nullptr},
+                {pg ? 2 : 0, pb ? 2 : 0, pc ? 2 : 0}};
+  launch_colsum_final(part.data_ptr<float>(), G, want_dbias ? 3 : 2, H, 3 * H, out, cur_stream());
   return {dh, dp, dgamma, dbeta, dbias};
 }
 
@@ -1346,7 +1358,8 @@ at::Tensor bias_gelu_fwd_hip(const at::Tensor& u, const at::Tensor& b) {
 
 std::tuple<at::Tensor, at::Tensor> bias_act_bwd_hip(const at::Tensor& gf,
                                                     const c10::optional<at::Tensor>& u,
-                                                    const at::Tensor& b, bool gelu) {
+                                                    const at::Tensor& b, bool gelu,
+                                                    const c10::optional<at::Tensor>& sbias) {
   TORCH_CHECK(gf.dim() == 2 && gf.size(1) % 8 == 0 && gf.size(1) / 8 <= 1024,
               "bias_act_bwd: gf must be [M, N], N % 8 == 0, N <= 8192");
   const int64_t M = gf.size(0), N = gf.size(1);
@@ -1357,10 +1370,11 @@ std::tuple<at::Tensor, at::Tensor> bias_act_bwd_hip(const at::Tensor& gf,
     check_rows_bf16(*u, M, N, "bias_act_bwd: u");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(gf.device());
+  void* ps = sink_ptr(sbias, N, "bias_act_bwd: bias");
   auto du = gelu ? at::empty_like(gf) : at::empty({0}, gf.options());
-  auto db = at::empty({N}, b.options());
+  auto db = ps ? at::empty({0}, b.options()) : at::empty({N}, b.options());
   if (M == 0) {
-    db.zero_();
+    if (!ps) db.zero_();
     return {du, db};
   }
   const int G = bias_act_bwd_blocks(M);
@@ -1368,7 +1382,7 @@ std::tuple<at::Tensor, at::Tensor> bias_act_bwd_hip(const at::Tensor& gf,
   launch_bias_act_bwd(gf.data_ptr(), gelu ? u->data_ptr() : nullptr, b.data_ptr(),
                       gelu ? du.data_ptr() : nullptr, part.data_ptr<float>(), M, N, gelu,
                       cur_stream());
-  ColsumOut out{{db.data_ptr(), nullptr, nullptr}, true};
+  ColsumOut out{{ps ? ps : db.data_ptr(), nullptr, nullptr}, {ps ? 2 : 0, 0, 0}};
   launch_colsum_final(part.data_ptr<float>(), G, 1, N, N, out, cur_stream());
   return {du, db};
 }
@@ -1443,10 +1457,12 @@ TORCH_LIBRARY(commeff, m) {
   m.def("resid_ln_fwd(Tensor x, Tensor? p, Tensor? bias, Tensor gamma, Tensor beta, float p_drop, "
         "int seed, float eps, bool want_h) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("resid_ln_bwd(Tensor gy, Tensor? gh, Tensor h, Tensor mean, Tensor rstd, Tensor gamma, "
-        "float p_drop, int seed, bool want_dp, bool want_dbias) "
+        "float p_drop, int seed, bool want_dp, bool want_dbias, Tensor(a!)? sgamma=None, "
+        "Tensor(b!)? sbeta=None, Tensor(c!)? sbias=None) "
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor u, Tensor b) -> Tensor");
-  m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu) -> (Tensor, Tensor)");
+  m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu, Tensor(a!)? sbias=None) "
+        "-> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CPU, m) {

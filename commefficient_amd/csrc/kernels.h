@@ -318,8 +318,8 @@ int bias_act_bwd_blocks(int64_t M);
 void launch_bias_act_bwd(const void* gf, const void* u, const void* b, void* du, float* part,
                          int64_t M, int64_t N, bool gelu, hipStream_t stream);
 struct ColsumOut {
-  void* p[3];  // [N] outputs per partial quantity (nullptr: skip)
-  bool bf16;
+  void* p[3];   // [N] outputs per partial quantity (nullptr: skip)
+  int mode[3];  // 0: store bf16, 1: store fp32, 2: fp32 += (a flat fp32 gradient view)
 };
 // out_q[c] = sum over b < G of part[b*stride + q*N + c], q < Q (fixed order)
 void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,

@@ -358,11 +358,14 @@ colsum_final_kernel(const float* __restrict__ part, int G, int Q, int64_t N, int
     const int q = static_cast<int>(col / N);
     const int64_t c = col - q * N;
     void* o = q == 0 ? out.p[0] : (q == 1 ? out.p[1] : out.p[2]);
+    const int mode = q == 0 ? out.mode[0] : (q == 1 ? out.mode[1] : out.mode[2]);
     if (o != nullptr) {
-      if (out.bf16)
+      if (mode == 0)
         static_cast<uint16_t*>(o)[c] = static_cast<uint16_t>(bf16_bits(t));
-      else
+      else if (mode == 1)
         static_cast<float*>(o)[c] = t;
+      else
+        static_cast<float*>(o)[c] += t;
     }
   }
 }

@@ -28,7 +28,8 @@ numerics oracle of tests/test_transformer.py.
 """
 from __future__ import annotations
 
-from typing import Optional
+from contextlib import contextmanager
+from typing import Dict, Optional
 
 import torch
 import torch.nn.functional as F
@@ -79,7 +80,8 @@ def _ref_resid_ln_fwd(x, p, bias, gamma, beta, p_drop, seed, eps, want_h):
     return h, y, mean, rstd
 
 
-def _ref_resid_ln_bwd(gy, gh, h, mean, rstd, gamma, p_drop, seed, want_dp, want_dbias):
+def _ref_resid_ln_bwd(gy, gh, h, mean, rstd, gamma, p_drop, seed, want_dp, want_dbias,
+                      sgamma=None, sbeta=None, sbias=None):
     M, H = h.shape
     xh = (h.float() - mean[:, None]) * rstd[:, None]
     dy = gy.float()
@@ -102,6 +104,15 @@ def _ref_resid_ln_bwd(gy, gh, h, mean, rstd, gamma, p_drop, seed, want_dp, want_
         dp = dpf.to(torch.bfloat16)
         if want_dbias:
             dbias = dpf.sum(0).to(gamma.dtype)
+            if sbias is not None:
+                sbias.add_(dpf.sum(0))
+                dbias = gamma.new_empty(0)
+    if sgamma is not None:
+        sgamma.add_((dy * xh).sum(0))
+        dgamma = gamma.new_empty(0)
+    if sbeta is not None:
+        sbeta.add_(dy.sum(0))
+        dbeta = gamma.new_empty(0)
     return dh.to(torch.bfloat16), dp, dgamma, dbeta, dbias
 
 
@@ -114,14 +125,18 @@ def _ref_bias_gelu_fwd(u, b):
     return (0.5 * x * (1.0 + torch.tanh(_GK * (x + _GC * x ** 3)))).to(torch.bfloat16)
 
 
-def _ref_bias_act_bwd(gf, u, b, gelu):
+def _ref_bias_act_bwd(gf, u, b, gelu, sbias=None):
     g = gf.float()
+    du = gf.new_empty(0)
     if gelu:
         x = _bf(u.float() + b.float())
         t = torch.tanh(_GK * (x + _GC * x ** 3))
         g = _bf(g * (0.5 * (1.0 + t) + 0.5 * x * (1.0 - t * t) * _GK * (1.0 + 3.0 * _GC * x * x)))
-        return g.to(torch.bfloat16), g.sum(0).to(b.dtype)
-    return gf.new_empty(0), g.sum(0).to(b.dtype)
+        du = g.to(torch.bfloat16)
+    if sbias is not None:
+        sbias.add_(g.sum(0))
+        return du, b.new_empty(0)
+    return du, g.sum(0).to(b.dtype)
 
 
 class _Impl:
@@ -140,12 +155,57 @@ class _Impl:
         return (_ops().bias_gelu_fwd if u.is_cuda else _ref_bias_gelu_fwd)(u, b)
 
     @staticmethod
-    def bias_act_bwd(gf, u, b, gelu):
-        return (_ops().bias_act_bwd if gf.is_cuda else _ref_bias_act_bwd)(gf, u, b, gelu)
+    def bias_act_bwd(gf, u, b, gelu, sbias=None):
+        return (_ops().bias_act_bwd if gf.is_cuda else _ref_bias_act_bwd)(gf, u, b, gelu, sbias)
 
 
 def _c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None else t.contiguous()
+
+
+# ------------------------------------------------------- gradient sinks
+# With the bf16 model replica (parallel/flat.py make_bf16_shadow) the weight
+# gradients would be produced in bf16, concatenated into one bf16 buffer and
+# added to the fp32 flat gradient (one 124M-element cat + one add per pass).
+# Inside ``grad_sinks({id(param): fp32 view of the flat gradient})`` the
+# junctions instead accumulate their weight / bias / LayerNorm gradients
+# straight into those fp32 views (GEMM with an fp32 C and beta = 1; the
+# column sums add in fp32) and return no gradient for them.
+_SINKS: list = [None]
+
+
+@contextmanager
+def grad_sinks(mapping: Optional[Dict[int, torch.Tensor]]):
+    prev = _SINKS[0]
+    _SINKS[0] = mapping
+    try:
+        yield
+    finally:
+        _SINKS[0] = prev
+
+
+def _sink(p: torch.Tensor) -> Optional[torch.Tensor]:
+    m = _SINKS[0]
+    return None if m is None else m.get(id(p))
+
+
+def _sinks(*params):
+    return tuple(_sink(p) for p in params)
+
+
+def _acc_mm(sink: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
+    """sink (fp32) += a @ b (bf16 operands, fp32 accumulation and output)."""
+    if sink.is_cuda:
+        torch.addmm(sink, a, b, out_dtype=torch.float32, out=sink)
+    else:
+        sink.add_(a.float() @ b.float())
+
+
+def _wgrad(sink, a, b):
+    if sink is None:
+        return torch.mm(a, b)
+    _acc_mm(sink, a, b)
+    return None
 
 
 # ---------------------------------------------------------------- autograd
@@ -157,16 +217,19 @@ class _EmbedLN(torch.autograd.Function):
         h, y, mean, rstd = _Impl.resid_ln_fwd(x, None, None, gamma, beta, p_drop, seed, eps, True)
         ctx.save_for_backward(h, mean, rstd, gamma)
         ctx.cfg = (p_drop, seed)
+        ctx.sinks = _sinks(gamma, beta)
         return h, y
 
     @staticmethod
     def backward(ctx, gh, gy):
         h, mean, rstd, gamma = ctx.saved_tensors
         p_drop, seed = ctx.cfg
+        sg, sb = ctx.sinks
         gy = torch.zeros_like(h) if gy is None else gy.contiguous()
         _, dx, dgamma, dbeta, _ = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma, p_drop,
-                                                     seed, True, False)
-        return dx, dgamma, dbeta, None, None, None
+                                                     seed, True, False, sg, sb, None)
+        return (dx, None if sg is not None else dgamma, None if sb is not None else dbeta,
+                None, None, None)
 
 
 class _ResidLN(torch.autograd.Function):
@@ -178,18 +241,22 @@ class _ResidLN(torch.autograd.Function):
         h, y, mean, rstd = _Impl.resid_ln_fwd(x, p, b, gamma, beta, p_drop, seed, eps, True)
         ctx.save_for_backward(o, W, h, mean, rstd, gamma)
         ctx.cfg = (p_drop, seed)
+        ctx.sinks = _sinks(W, b, gamma, beta)
         return h, y
 
     @staticmethod
     def backward(ctx, gh, gy):
         o, W, h, mean, rstd, gamma = ctx.saved_tensors
         p_drop, seed = ctx.cfg
+        sW, sb, sg, sbe = ctx.sinks
         gy = torch.zeros_like(h) if gy is None else gy.contiguous()
         dh, dp, dgamma, dbeta, dbias = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma,
-                                                          p_drop, seed, True, True)
+                                                          p_drop, seed, True, True, sg, sbe, sb)
         do = torch.mm(dp, W.t()) if ctx.needs_input_grad[1] else None
-        dW = torch.mm(o.t(), dp) if ctx.needs_input_grad[2] else None
-        return dh, do, dW, dbias, dgamma, dbeta, None, None, None
+        dW = _wgrad(sW, o.t(), dp) if ctx.needs_input_grad[2] else None
+        return (dh, do, dW, None if sb is not None else dbias,
+                None if sg is not None else dgamma, None if sbe is not None else dbeta,
+                None, None, None)
 
 
 class _FcGelu(torch.autograd.Function):
@@ -200,15 +267,17 @@ class _FcGelu(torch.autograd.Function):
         u = torch.mm(a, W)
         f = _Impl.bias_gelu_fwd(u, b)
         ctx.save_for_backward(a, W, u, b)
+        ctx.sinks = _sinks(W, b)
         return f
 
     @staticmethod
     def backward(ctx, gf):
         a, W, u, b = ctx.saved_tensors
-        du, db = _Impl.bias_act_bwd(gf.contiguous(), u, b, True)
+        sW, sb = ctx.sinks
+        du, db = _Impl.bias_act_bwd(gf.contiguous(), u, b, True, sb)
         da = torch.mm(du, W.t()) if ctx.needs_input_grad[0] else None
-        dW = torch.mm(a.t(), du) if ctx.needs_input_grad[1] else None
-        return da, dW, db
+        dW = _wgrad(sW, a.t(), du) if ctx.needs_input_grad[1] else None
+        return da, dW, None if sb is not None else db
 
 
 class _Linear(torch.autograd.Function):
@@ -217,16 +286,18 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, W, b):
         ctx.save_for_backward(a, W, b)
+        ctx.sinks = _sinks(W, b)
         return torch.addmm(b, a, W)
 
     @staticmethod
     def backward(ctx, gy):
         a, W, b = ctx.saved_tensors
+        sW, sb = ctx.sinks
         gy = gy.contiguous()
-        _, db = _Impl.bias_act_bwd(gy, None, b, False)
+        _, db = _Impl.bias_act_bwd(gy, None, b, False, sb)
         da = torch.mm(gy, W.t()) if ctx.needs_input_grad[0] else None
-        dW = torch.mm(a.t(), gy) if ctx.needs_input_grad[1] else None
-        return da, dW, db
+        dW = _wgrad(sW, a.t(), gy) if ctx.needs_input_grad[1] else None
+        return da, dW, None if sb is not None else db
 
 
 # ------------------------------------------------------------------ model

@@ -42,6 +42,7 @@ from ..models.common import NativeConv2d, ghost_batchnorm, groupable, has_batchn
 from ..ops.grouped import GroupedGrads, grouped_grads
 from ..ops.nn import prepared_conv_weights
 from ..ops import CSVec
+from ..ops import transformer as _tx
 from ..utils.logging import PhaseTimer
 from . import dist
 from .flat import FlatParams
@@ -292,7 +293,13 @@ class FedModel:
             self.flat.refresh_shadow()  # one cast of the current (bound) weights
             shadow.train(self.model.training)
             model = shadow
-        with (self._autocast(cache=not capture) if shadow is None else nullcontext()):
+        # bf16 replica: native GPT-2 junctions accumulate weight gradients
+        # straight into the fp32 flat gradient (not with the overlapped
+        # bucket hooks, which watch the replica's .grad)
+        sinks = (self.flat.grad_sink_map() if (shadow is not None and want_grad
+                                                and not self._overlap_armed) else None)
+        with (self._autocast(cache=not capture) if shadow is None else nullcontext()), \
+                _tx.grad_sinks(sinks):
             with (ghost_batchnorm(model, groups) if (groups > 1 and self.has_bn)
                   else nullcontext()):
                 if want_grad:

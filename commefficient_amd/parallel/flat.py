@@ -102,7 +102,21 @@ class FlatParams:
         self.wb.copy_(self.bound)
 
     def collect_shadow_grads(self) -> None:
-        """g += the shadow's bf16 gradients (flat order); clears them."""
+        """g += the shadow's bf16 gradients (flat order); clears them.  When
+        most parameters accumulated their gradient straight into ``g`` (no
+        ``.grad``: ops/transformer.py ``grad_sinks``) only the others are
+        added, one slice each."""
+        have = [p.grad is not None for p in self.shadow_params]
+        if sum(have) * 2 < len(have):
+            dst, src = [], []
+            for p, o, n in zip(self.shadow_params, self.offsets, self.numels):
+                if p.grad is not None:
+                    dst.append(self.g[o:o + n])
+                    src.append(p.grad.reshape(-1))
+                    p.grad = None
+            if dst:
+                torch._foreach_add_(dst, src)
+            return
         gs = []
         for p, n in zip(self.shadow_params, self.numels):
             gs.append(p.grad.reshape(-1) if p.grad is not None
@@ -110,6 +124,13 @@ class FlatParams:
             p.grad = None
         torch.cat(gs, out=self.gb)
         self.g.add_(self.gb)
+
+    def grad_sink_map(self):
+        """{id(shadow param): its fp32 view of g} for ops/transformer.py grad_sinks."""
+        if getattr(self, "_sink_map", None) is None:
+            self._sink_map = {id(p): self.g[o:o + n].view(s) for p, o, n, s in
+                              zip(self.shadow_params, self.offsets, self.numels, self.shapes)}
+        return self._sink_map
 
     def ranges_of(self, params) -> List[Tuple[int, int]]:
         """Flat [start, end) ranges of the given parameters."""
