@@ -1387,6 +1387,59 @@ std::tuple<at::Tensor, at::Tensor> bias_act_bwd_hip(const at::Tensor& gf,
   return {du, db};
 }
 
+at::Tensor pad_rows_hip(const at::Tensor& src, const c10::optional<at::Tensor>& inv, int64_t rows) {
+  TORCH_CHECK(src.scalar_type() == at::kBFloat16 && src.dim() == 2 && src.stride(1) == 1 &&
+                  src.size(1) % 8 == 0 && src.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0,
+              "pad_rows: src must be bf16 [Mr, K] rows, K % 8 == 0, 16-byte aligned");
+  const int32_t* ip = nullptr;
+  if (inv.has_value() && inv->defined()) {
+    TORCH_CHECK(inv->scalar_type() == at::kInt && inv->is_contiguous() && inv->numel() == rows,
+                "pad_rows: inv must be int32 [rows]");
+    ip = inv->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(src.size(0) == rows, "pad_rows: without inv src must have `rows` rows");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+  auto out = at::empty({rows, src.size(1)}, src.options());
+  launch_pad_rows(src.data_ptr(), src.stride(0), src.size(1), ip, rows, out.data_ptr(), cur_stream());
+  return out;
+}
+
+at::Tensor heads_to_rows_hip(at::TensorList srcs, const c10::optional<at::Tensor>& tok, int64_t Mr) {
+  const int64_t P = static_cast<int64_t>(srcs.size());
+  TORCH_CHECK(P >= 1 && P <= 3, "heads_to_rows: 1..3 sources");
+  const auto& s0 = srcs[0];
+  TORCH_CHECK(s0.dim() == 4, "heads_to_rows: sources must be [N, nh, L, hd]");
+  const int64_t N = s0.size(0), nh = s0.size(1), L = s0.size(2), hd = s0.size(3);
+  TORCH_CHECK(hd % 8 == 0, "heads_to_rows: head dim must be a multiple of 8");
+  HeadSrcs hs{};
+  for (int64_t p = 0; p < P; ++p) {
+    const auto& s = srcs[p];
+    TORCH_CHECK(s.scalar_type() == at::kBFloat16 && s.sizes() == s0.sizes() && s.stride(3) == 1 &&
+                    s.stride(0) % 8 == 0 && s.stride(1) % 8 == 0 && s.stride(2) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(s.data_ptr()) % 16 == 0,
+                "heads_to_rows: sources must be bf16 with 16-byte aligned head rows");
+    hs.p[p] = s.data_ptr();
+    hs.stride[p][0] = s.stride(0);
+    hs.stride[p][1] = s.stride(1);
+    hs.stride[p][2] = s.stride(2);
+  }
+  const int32_t* tp = nullptr;
+  if (tok.has_value() && tok->defined()) {
+    TORCH_CHECK(tok->scalar_type() == at::kInt && tok->is_contiguous() && tok->numel() == Mr,
+                "heads_to_rows: tok must be int32 [Mr]");
+    tp = tok->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(Mr == N * L, "heads_to_rows: without tok Mr must be N*L");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(s0.device());
+  auto out = at::empty({Mr, P * nh * hd}, s0.options());
+  launch_heads_to_rows(hs, static_cast<int>(P), nh * hd, hd, L, tp, Mr, out.data_ptr(),
+                       cur_stream());
+  return out;
+}
+
 }  // namespace
 }  // namespace commeff
 
@@ -1461,6 +1514,8 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor(b!)? sbeta=None, Tensor(c!)? sbias=None) "
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor u, Tensor b) -> Tensor");
+  m.def("pad_rows(Tensor src, Tensor? inv, int rows) -> Tensor");
+  m.def("heads_to_rows(Tensor[] srcs, Tensor? tok, int Mr) -> Tensor");
   m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu, Tensor(a!)? sbias=None) "
         "-> (Tensor, Tensor)");
 }
@@ -1536,4 +1591,6 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("resid_ln_bwd", &resid_ln_bwd_hip);
   m.impl("bias_gelu_fwd", &bias_gelu_fwd_hip);
   m.impl("bias_act_bwd", &bias_act_bwd_hip);
+  m.impl("pad_rows", &pad_rows_hip);
+  m.impl("heads_to_rows", &heads_to_rows_hip);
 }

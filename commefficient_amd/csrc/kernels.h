@@ -321,6 +321,16 @@ struct ColsumOut {
   void* p[3];   // [N] outputs per partial quantity (nullptr: skip)
   int mode[3];  // 0: store bf16, 1: store fp32, 2: fp32 += (a flat fp32 gradient view)
 };
+// token rows [Mr, P*H] <-> padded per-head tensors [N, nh, L, hd] (bf16, hd % 8 == 0)
+struct HeadSrcs {
+  const void* p[3];
+  int64_t stride[3][3];  // element strides of (n, h, t) per source, multiples of 8; d contiguous
+};
+// out[pos] = src[inv[pos]] (row of K bf16) or 0 where inv[pos] < 0 (inv null: identity)
+void launch_pad_rows(const void* src, int64_t src_ld, int64_t K, const int32_t* inv, int64_t rows,
+                     void* out, hipStream_t stream);
+void launch_heads_to_rows(const HeadSrcs& src, int P, int64_t H, int64_t hd, int64_t L,
+                          const int32_t* tok, int64_t Mr, void* out, hipStream_t stream);
 // out_q[c] = sum over b < G of part[b*stride + q*N + c], q < Q (fixed order)
 void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,
                          const ColsumOut& out, hipStream_t stream);

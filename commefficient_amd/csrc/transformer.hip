@@ -472,3 +472,68 @@ void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t str
 }
 
 }  // namespace commeff
+
+// ---------------------------------------------------- token rows <-> heads
+// GPT-2 attention layout changes with padding removal folded in.  Token rows
+// are the real (unpadded) tokens, [Mr, P*H]; the attention runs on padded
+// per-head tensors [N, nh, L, hd].  inv[n*L + t] = token row of position
+// (n, t) or -1 for a pad (nullptr: identity, no padding); tok[i] = n*L + t of
+// token row i (nullptr: identity).
+namespace commeff {
+namespace {
+
+// one block per padded position: out[pos, :] = src[inv[pos], :] or 0 at a pad
+// (the padded row layout [N, L, K] is the attention's [N, L, heads, hd]
+// memory layout: q/k/v/dO are its head views without another copy)
+__global__ void __launch_bounds__(256)
+pad_rows_kernel(const V8* __restrict__ src, int64_t src_ld8, int K8, const int32_t* __restrict__ inv,
+                V8* __restrict__ out) {
+  const int64_t pos = blockIdx.x;
+  const int64_t r = inv != nullptr ? inv[pos] : pos;
+  for (int v = threadIdx.x; v < K8; v += 256) {
+    V8 val;
+    if (r >= 0) {
+      val = src[r * src_ld8 + v];
+    } else {
+      val.w[0] = val.w[1] = val.w[2] = val.w[3] = 0u;
+    }
+    out[pos * K8 + v] = val;
+  }
+}
+
+// one block per token row i: out[i, p*H + h*hd + d] = src_p[n, h, t, d]
+__global__ void __launch_bounds__(256)
+heads_to_rows_kernel(HeadSrcs src, int P, int H8, int hd8, int64_t L,
+                     const int32_t* __restrict__ tok, V8* __restrict__ out) {
+  const int64_t i = blockIdx.x;
+  const int64_t pos = tok != nullptr ? tok[i] : i;
+  const int64_t n = pos / L, t = pos - n * L;
+  for (int v = threadIdx.x; v < P * H8; v += 256) {
+    const int p = v / H8;
+    const int c = v - p * H8;
+    const int h = c / hd8, d = c - h * hd8;
+    const int64_t* st = p == 0 ? src.stride[0] : (p == 1 ? src.stride[1] : src.stride[2]);
+    const V8* s = static_cast<const V8*>(p == 0 ? src.p[0] : (p == 1 ? src.p[1] : src.p[2]));
+    out[i * P * H8 + v] = s[(n * st[0] + h * st[1] + t * st[2]) / 8 + d];
+  }
+}
+
+}  // namespace
+
+void launch_pad_rows(const void* src, int64_t src_ld, int64_t K, const int32_t* inv, int64_t rows,
+                     void* out, hipStream_t stream) {
+  if (rows == 0) return;
+  hipLaunchKernelGGL(pad_rows_kernel, dim3(static_cast<uint32_t>(rows)), dim3(256), 0, stream,
+                     static_cast<const V8*>(src), src_ld / 8, static_cast<int>(K / 8), inv,
+                     static_cast<V8*>(out));
+}
+
+void launch_heads_to_rows(const HeadSrcs& src, int P, int64_t H, int64_t hd, int64_t L,
+                          const int32_t* tok, int64_t Mr, void* out, hipStream_t stream) {
+  if (Mr == 0) return;
+  hipLaunchKernelGGL(heads_to_rows_kernel, dim3(static_cast<uint32_t>(Mr)), dim3(256), 0, stream,
+                     src, P, static_cast<int>(H / 8), static_cast<int>(hd / 8), L, tok,
+                     static_cast<V8*>(out));
+}
+
+}  // namespace commeff

@@ -37,9 +37,12 @@ class PersonaFedLoader:
             recs = [ds[int(i)][1] for i in r[pos]]
             host = collate(recs)
             ids, mc, lab, mcl, tt, lp = _to_dev(list(host) + [label_positions(host[2])], dev)
-            return ids, mc, lab, tt, lp, mcl
+            # sequence lengths stay on the host (mc token = last real token):
+            # the transformer runs its token-wise ops on the real tokens only
+            lens = host[1] + 1
+            return ids, mc, lab, tt, lp, lens, mcl
 
-        return RoundBatch(cids, take, n_inputs=5)
+        return RoundBatch(cids, take, n_inputs=6)
 
 
 class PersonaValLoader:

@@ -332,10 +332,124 @@ def _native_hidden_size(H: int) -> bool:
     return H % 256 == 0 and 1 <= H // 256 <= 6
 
 
-def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tensor] = None):
+def _ref_pad_rows(src, inv, rows):
+    if inv is None:
+        return src.clone()
+    inv = inv.long()
+    out = src.new_zeros(rows, src.shape[1])
+    real = inv >= 0
+    out[real] = src[inv[real]]
+    return out
+
+
+def _ref_heads_to_rows(srcs, tok, Mr):
+    N, nh, L, hd = srcs[0].shape
+    rows = torch.cat([s.permute(0, 2, 1, 3).reshape(N * L, nh * hd) for s in srcs], dim=1)
+    return rows if tok is None else rows.index_select(0, tok.long())
+
+
+def _pad_rows(src, inv, rows):
+    return (_ops().pad_rows if src.is_cuda else _ref_pad_rows)(src, inv, rows)
+
+
+def _heads_to_rows(srcs, tok, Mr):
+    return (_ops().heads_to_rows if srcs[0].is_cuda else _ref_heads_to_rows)(srcs, tok, Mr)
+
+
+def _heads(rows: torch.Tensor, N: int, L: int, nh: int):
+    """[N*L, H] padded rows -> the [N, nh, L, hd] head view (HF's layout)."""
+    H = rows.shape[1]
+    return rows.view(N, L, nh, H // nh).transpose(1, 2)
+
+
+class _RowsToHeads(torch.autograd.Function):
+    """qkv token rows [Mr, 3H] -> q, k, v [N, nh, L, hd] views of ONE padded
+    [N*L, 3H] buffer (zero at pads); backward gathers dq, dk, dv straight
+    into the token rows of dqkv (no concatenation)."""
+
+    @staticmethod
+    def forward(ctx, qkv, tok, inv, N, L, nh):
+        ctx.save_for_backward(tok)
+        ctx.Mr = qkv.shape[0]
+        H = qkv.shape[1] // 3
+        pad = _pad_rows(qkv, inv, N * L)
+        return tuple(_heads(t, N, L, nh) for t in pad.split(H, dim=1))
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        (tok,) = ctx.saved_tensors
+        like = next(g for g in (dq, dk, dv) if g is not None)
+        gs = [g if g is not None else torch.zeros_like(like) for g in (dq, dk, dv)]
+        return _heads_to_rows(gs, tok, ctx.Mr), None, None, None, None, None
+
+
+class _HeadsToRows(torch.autograd.Function):
+    """attention output [N, nh, L, hd] (any strides) -> token rows [Mr, H]."""
+
+    @staticmethod
+    def forward(ctx, o, tok, inv, Mr):
+        ctx.save_for_backward(inv)
+        ctx.dims = (o.shape[0], o.shape[1], o.shape[2])
+        return _heads_to_rows([o], tok, Mr)
+
+    @staticmethod
+    def backward(ctx, g):
+        (inv,) = ctx.saved_tensors
+        N, nh, L = ctx.dims
+        return _heads(_pad_rows(g.contiguous(), inv, N * L), N, L, nh), None, None, None
+
+
+class _ToPadded(torch.autograd.Function):
+    """[Mr, K] token rows -> [rows, K] with the rows at ``tok`` (others 0)."""
+
+    @staticmethod
+    def forward(ctx, x, tok, rows):
+        ctx.save_for_backward(tok)
+        return x.new_zeros(rows, x.shape[1]).index_copy_(0, tok.long(), x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (tok,) = ctx.saved_tensors
+        return g.index_select(0, tok.long()), None, None
+
+
+def real_token_index(lengths: torch.Tensor, L: int, device):
+    """(tok, inv) for host-side sequence lengths: tok = flat positions n*L + t
+    (t < lengths[n]) of the real tokens, inv = token row of every padded
+    position or -1; built on the host (their sizes are known without a
+    sync), one int32 H2D copy."""
+    import numpy as np
+    ln = lengths.reshape(-1).numpy().astype(np.int64)
+    if ln.size == 0 or int(ln.min()) < 0 or int(ln.max()) > L:
+        return None
+    Mr = int(ln.sum())
+    starts = np.repeat(np.arange(ln.size, dtype=np.int64) * L - np.concatenate(
+        [[0], np.cumsum(ln)[:-1]]), ln)
+    tok = starts + np.arange(Mr, dtype=np.int64)
+    inv = np.full(ln.size * L, -1, dtype=np.int64)
+    inv[tok] = np.arange(Mr)
+    both = np.concatenate([tok, inv]).astype(np.int32)
+    if torch.device(device).type == "cuda":
+        from ..parallel.dist import h2d
+        both = h2d(both, device)
+    else:
+        both = torch.from_numpy(both)
+    return both[:Mr], both[Mr:]
+
+
+def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tensor] = None,
+                lengths: Optional[torch.Tensor] = None):
     """``ln_f`` output of HF ``GPT2Model`` ``tr`` for ``input_ids`` [..., L]
     (same as ``tr(input_ids, token_type_ids=...)[0]``) on the native junction
-    kernels.  Dropout follows ``tr.training`` like the HF modules."""
+    kernels.  Dropout follows ``tr.training`` like the HF modules.
+
+    ``lengths`` (host int64, one per sequence; PersonaChat: mc_token_ids + 1)
+    marks each row's real tokens, padding being at the end: every token-wise
+    op (embeddings, GEMMs, junctions) then runs on the real tokens only and
+    just the attention sees the padded [N, heads, L, d] layout.  With causal
+    attention right padding never reaches a real position, so the hidden
+    states at real positions -- everything the losses read -- are the padded
+    forward's; padded positions come back as 0."""
     cfg = tr.config
     shp = input_ids.shape
     L = shp[-1]
@@ -355,22 +469,36 @@ def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tens
     if seeds is None:
         seeds = _Seeds(torch.initial_seed())
         tr._commeff_seeds = seeds
-    pos = torch.arange(L, device=ids.device)
-    e = tr.wte(ids) + tr.wpe(pos)
-    if token_type_ids is not None:
-        e = e + tr.wte(token_type_ids.reshape(-1, L))
+    tok = inv = None
+    if lengths is not None and not lengths.is_cuda and int(lengths.sum()) < M:
+        ti = real_token_index(lengths, L, ids.device)
+        if ti is not None:
+            tok, inv = ti
+    Mr = M if tok is None else tok.shape[0]
+    if tok is None:
+        pos = torch.arange(L, device=ids.device)
+        e = (tr.wte(ids) + tr.wpe(pos)).reshape(M, H)
+        if token_type_ids is not None:
+            e = e + tr.wte(token_type_ids.reshape(M))
+    else:
+        tl = tok.long()
+        e = tr.wte(ids.reshape(M).index_select(0, tl)) + tr.wpe(tl % L)
+        if token_type_ids is not None:
+            e = e + tr.wte(token_type_ids.reshape(M).index_select(0, tl))
     blocks = tr.h
     ln = blocks[0].ln_1
-    h, y = _EmbedLN.apply(e.reshape(M, H), ln.weight, ln.bias, pe, seeds.next(), eps)
+    h, y = _EmbedLN.apply(e, ln.weight, ln.bias, pe, seeds.next(), eps)
     for i, blk in enumerate(blocks):
         at = blk.attn
         qkv = _Linear.apply(y, at.c_attn.weight, at.c_attn.bias)
-        # split (not a [3, ...] view + unbind): its backward is one contiguous cat
-        q, k, v = (t.view(Nn, L, nh, H // nh).transpose(1, 2) for t in qkv.split(H, dim=1))
+        # token rows -> padded per-head q, k, v and back in one kernel each
+        # (the layout change, the padding and, backward, the q/k/v gradient
+        # concatenation in the same pass)
+        q, k, v = _RowsToHeads.apply(qkv, tok, inv, Nn, L, nh)
         o = F.scaled_dot_product_attention(
             q, k, v, dropout_p=_p(getattr(at, "attn_dropout", None), cfg.attn_pdrop),
             is_causal=True)
-        o = o.transpose(1, 2).reshape(M, H)
+        o = _HeadsToRows.apply(o, tok, inv, Mr)
         h, y = _ResidLN.apply(h, o, at.c_proj.weight, at.c_proj.bias, blk.ln_2.weight,
                               blk.ln_2.bias, _p(getattr(at, "resid_dropout", None), cfg.resid_pdrop),
                               seeds.next(), eps)
@@ -379,4 +507,6 @@ def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tens
         h, y = _ResidLN.apply(h, f, blk.mlp.c_proj.weight, blk.mlp.c_proj.bias, nxt.weight,
                               nxt.bias, _p(getattr(blk.mlp, "dropout", None), cfg.resid_pdrop),
                               seeds.next(), eps)
+    if tok is not None:
+        y = _ToPadded.apply(y, tok, M)
     return y.view(*shp, H)

@@ -43,13 +43,15 @@ class _unpacked_sequences:
         return False
 
 
-def gpt2_hidden_states(m, input_ids, token_type_ids, args=None):
+def gpt2_hidden_states(m, input_ids, token_type_ids, args=None, lengths=None):
     """Final hidden states of the double-heads model's transformer: the native
-    junction kernels (ops/transformer.py) unless ``--transformer hf`` or the
+    junction kernels (ops/transformer.py; with host ``lengths`` only the real
+    tokens run through the token-wise ops) unless ``--transformer hf`` or the
     config is outside what they cover (then the HF module forward)."""
     tr = m.transformer
     if getattr(args, "transformer", "native") == "native" and _tx.native_ok(tr, input_ids):
-        return _tx.gpt2_hidden(tr, input_ids, token_type_ids)
+        return _tx.gpt2_hidden(tr, input_ids, token_type_ids,
+                               lengths if getattr(args, "unpad", "on") == "on" else None)
     with _unpacked_sequences():
         return tr(input_ids=input_ids, token_type_ids=token_type_ids, use_cache=False)[0]
 
@@ -83,7 +85,8 @@ def gpt2_loss_train(model, inputs, targets, args, groups=None):
         # LM head only at the labelled positions (data/fed_persona.py
         # label_positions): same loss, ~1/17 of the vocabulary GEMM + softmax
         tok_sum, ntok, mc_logits = _lm_at_labels(m, input_ids, mc_token_ids, lm_labels,
-                                                  token_type_ids, inputs[4], args)
+                                                  token_type_ids, inputs[4], args,
+                                                  inputs[5] if len(inputs) > 5 else None)
     else:
         lm_logits, mc_logits = _double_heads(m, input_ids, token_type_ids, mc_token_ids, args)
         shift_logits = lm_logits[..., :-1, :].float()
@@ -114,10 +117,11 @@ def _double_heads(m, input_ids, token_type_ids, mc_token_ids, args, last_only=Fa
     return (out.logits[:, -1] if last_only else out.logits), out.mc_logits
 
 
-def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos, args=None):
+def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos, args=None,
+                  lengths=None):
     """(per-example sum of LM token losses, labelled-token count, mc logits)
     with the LM head evaluated only at ``lm_pos`` [B, R] (-1 = pad)."""
-    hid = gpt2_hidden_states(m, input_ids, token_type_ids, args)          # [B, C, L, H]
+    hid = gpt2_hidden_states(m, input_ids, token_type_ids, args, lengths)  # [B, C, L, H]
     B, C, L, H = hid.shape
     mc_logits = m.multiple_choice_head(hid, mc_token_ids).squeeze(-1)
     valid = lm_pos >= 0

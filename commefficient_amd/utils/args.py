@@ -193,6 +193,10 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="GPT-2 blocks: native junction kernels (csrc/transformer.hip: fused "
                         "residual+dropout+LayerNorm, bias+GELU, bias gradients) around "
                         "hipBLASLt GEMMs and SDPA, or the HF module forward")
+    g.add_argument("--unpad", choices=["on", "off"], default="on",
+                   help="native GPT-2 path: token-wise ops (embeddings, GEMMs, LayerNorm/"
+                        "GELU junctions) on the real tokens only, attention on the padded "
+                        "layout (exact: right padding never reaches a real token)")
     g.add_argument("--graph", choices=["auto", "on", "off"], default="off",
                    help="replay merged-client rounds from captured HIP graphs "
                         "(parallel/graph.py) once a round geometry repeats (auto/on: "

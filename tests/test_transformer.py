@@ -252,3 +252,57 @@ def test_fedmodel_native_transformer_matches_hf_gpu():
     torch.testing.assert_close(l1, l2, rtol=2e-2, atol=2e-2)
     assert (d1 != 0).float().mean() > 0.9
     assert ((d1 - d2).norm() / d2.norm()) < 5e-2
+
+
+def _unpad_vs_padded(device):
+    """Token-wise ops on the real tokens only (host lengths) == the padded
+    forward at every real position, and the same parameter gradients."""
+    import copy
+    base = _tiny_gpt2().to(device).to(torch.bfloat16).eval()
+    ids, tt = _inputs(device=device)
+    lens = torch.tensor([[20, 13], [7, 16], [20, 1]])  # host lengths, right padding
+    mask = (torch.arange(20)[None, None, :] < lens[..., None]).to(device)
+    gw = torch.randn(*ids.shape, 256, generator=torch.Generator().manual_seed(3)).to(device)
+    gw = gw * mask[..., None]  # the losses read real positions only
+    outs = []
+    for use in (False, True):
+        m = copy.deepcopy(base)
+        h = tx.gpt2_hidden(m.transformer, ids, tt, lens if use else None)
+        (h.float() * gw).sum().backward()
+        outs.append((h.float() * mask[..., None], _grads(m)))
+    (h0, g0), (h1, g1) = outs
+    torch.testing.assert_close(h1, h0, rtol=2e-2, atol=3e-2)
+    for n in g0:
+        rel = (g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-6)
+        assert rel < 3e-2, (n, float(rel))
+
+
+def test_unpadded_tokens_match_padded_cpu():
+    _unpad_vs_padded("cpu")
+
+
+@pytest.mark.gpu
+def test_unpadded_tokens_match_padded_gpu():
+    _unpad_vs_padded("cuda")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("unpad", [False, True])
+def test_rows_heads_layout_kernels_gpu(unpad):
+    from commefficient_amd._ext import ops
+    N, L, nh, hd = 5, 24, 12, 64
+    H = nh * hd
+    lens = torch.tensor([24, 3, 17, 1, 10]) if unpad else torch.full((5,), 24)
+    tok, inv = tx.real_token_index(lens, L, "cpu")
+    Mr = tok.numel()
+    g = torch.Generator().manual_seed(0)
+    qkv = torch.randn(Mr, 3 * H, generator=g).to(torch.bfloat16)
+    ti, ii = (tok.cuda(), inv.cuda()) if unpad else (None, None)
+    out = ops().pad_rows(qkv.cuda(), ii, N * L)
+    assert torch.equal(out.cpu(), tx._ref_pad_rows(qkv, inv if unpad else None, N * L))
+    # strided sources (a transposed [N, L, nh, hd] tensor) back to rows
+    srcs = [torch.randn(N, L, nh, hd, generator=g).to(torch.bfloat16).transpose(1, 2)
+            for _ in range(3)]
+    got = ops().heads_to_rows([s.cuda() for s in srcs], ti, Mr)
+    exp = tx._ref_heads_to_rows(srcs, tok if unpad else None, Mr)
+    assert torch.equal(got.cpu(), exp)
