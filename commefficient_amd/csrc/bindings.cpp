@@ -657,14 +657,19 @@ void cs_encode_planned_hip(at::Tensor table, const at::Tensor& vec, double scale
                            static_cast<int>(r), c, p, planned_args(plan, p, d, r), overwrite, cur_stream());
 }
 
-at::Tensor cs_query_planned_hip(const at::Tensor& table, int64_t d, at::TensorList plan) {
+// est [d]; with 0 <= c0 < c1 only the coordinates of plan chunks [c0, c1) are
+// computed (a rank's shard of the unsketch; the rest of est is left unset)
+at::Tensor cs_query_planned_hip(const at::Tensor& table, int64_t d, at::TensorList plan, int64_t c0,
+                                int64_t c1) {
   check_f32(table, "table");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   const int64_t c = table.size(-1), r = table.numel() / c;
   const PlanGeom p = plan_geom_or_throw(d, r, c);
+  TORCH_CHECK(c0 >= 0 && (c1 < 0 || (c1 > c0 && c1 <= p.num_chunks)),
+              "cs_query_planned: chunk range out of bounds");
   auto est = at::empty({d}, table.options());
   launch_cs_query_planned(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(r),
-                          c, p, planned_args(plan, p, d, r), cur_stream());
+                          c, p, planned_args(plan, p, d, r), cur_stream(), c0, c1);
   return est;
 }
 
@@ -1452,7 +1457,7 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor like) -> Tensor");
   m.def("cs_encode_planned(Tensor(a!) table, Tensor vec, float scale, Tensor? wvec, float wscale, "
         "int c, Tensor[] plan, bool overwrite=False) -> ()");
-  m.def("cs_query_planned(Tensor table, int d, Tensor[] plan) -> Tensor");
+  m.def("cs_query_planned(Tensor table, int d, Tensor[] plan, int c0=0, int c1=-1) -> Tensor");
   m.def("plan_geometry(int d, int r, int c) -> int[]", &commeff::plan_geometry);
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");

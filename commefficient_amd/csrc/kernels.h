@@ -78,8 +78,10 @@ void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* 
 void launch_cs_encode_planned(float* table, const float* vec, const float* wvec, float scale,
                               float wscale, int64_t d, int r, int64_t c, const PlanGeom& p,
                               const PlannedArgs& a, bool overwrite, hipStream_t stream);
+// est[i] for the coordinates of plan chunks [c0, c1) only (c1 < 0: all)
 void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,
-                             const PlanGeom& p, const PlannedArgs& a, hipStream_t stream);
+                             const PlanGeom& p, const PlannedArgs& a, hipStream_t stream,
+                             int64_t c0 = 0, int64_t c1 = -1);
 // est[i] = lower-median_j( s_j(i) * table[j, b_j(i)] )
 void launch_cs_query(const float* table, float* est, const RowHashes& h,
                      const SketchGeom& g, const int32_t* blk_off,

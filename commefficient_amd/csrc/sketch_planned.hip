@@ -460,7 +460,8 @@ enc_p2_dense_kernel(float* __restrict__ table, const float* __restrict__ vals,
 __global__ void __launch_bounds__(256)
 qry_q1_kernel(const float* __restrict__ table, const uint16_t* __restrict__ ent_info,
               const int32_t* __restrict__ seg, float* __restrict__ vals, uint32_t tile,
-              uint32_t total_buckets, uint32_t splits) {
+              uint32_t total_buckets, uint32_t splits, const int32_t* __restrict__ base,
+              uint32_t num_tiles, uint32_t c0, uint32_t c1, uint32_t num_chunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* T = reinterpret_cast<float*>(smem);
   const uint32_t t = blockIdx.x / splits;
@@ -471,7 +472,12 @@ qry_q1_kernel(const float* __restrict__ table, const uint16_t* __restrict__ ent_
     T[b] = gb < total_buckets ? table[gb] : 0.f;
   }
   __syncthreads();
-  const uint32_t lo = static_cast<uint32_t>(seg[t]), n = static_cast<uint32_t>(seg[t + 1]) - lo;
+  // entries of coordinate chunks [c0, c1) only (a rank's shard of the query):
+  // a tile's segment is chunk-major, so they are one contiguous sub-range
+  const uint32_t lo = static_cast<uint32_t>(c0 == 0 ? seg[t] : base[static_cast<size_t>(c0) * num_tiles + t]);
+  const uint32_t hi = static_cast<uint32_t>(c1 >= num_chunks ? seg[t + 1]
+                                                             : base[static_cast<size_t>(c1) * num_tiles + t]);
+  const uint32_t n = hi - lo;
   const uint32_t e0 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * s / splits);
   const uint32_t e1 = lo + static_cast<uint32_t>(static_cast<uint64_t>(n) * (s + 1) / splits);
   const uint32_t mask = tile - 1;
@@ -544,16 +550,17 @@ __global__ void __launch_bounds__(1024)
 qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_t chunk,
               uint32_t num_tiles, const uint16_t* __restrict__ src_info,
               const int32_t* __restrict__ base, const int32_t* __restrict__ off,
-              float* __restrict__ est, bool vec16) {
+              float* __restrict__ est, bool vec16, uint32_t c0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
-  const uint32_t i0 = blockIdx.x * chunk;
+  const uint32_t cb = blockIdx.x + c0;  // coordinate chunk of this block
+  const uint32_t i0 = cb * chunk;
   const uint32_t i1 = min(d, i0 + chunk);
   float* stage = reinterpret_cast<float*>(smem);
   uint32_t* soff = reinterpret_cast<uint32_t*>(stage + chunk * r);
   uint32_t* sbase = soff + num_tiles + 1;
-  const size_t orow = static_cast<size_t>(blockIdx.x) * (num_tiles + 1);
-  const size_t brow = static_cast<size_t>(blockIdx.x) * num_tiles;
+  const size_t orow = static_cast<size_t>(cb) * (num_tiles + 1);
+  const size_t brow = static_cast<size_t>(cb) * num_tiles;
   for (uint32_t t = threadIdx.x; t <= num_tiles; t += blockDim.x) soff[t] = off[orow + t];
   for (uint32_t t = threadIdx.x; t < num_tiles; t += blockDim.x) sbase[t] = base[brow + t];
   __syncthreads();
@@ -810,8 +817,12 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
 }
 
 void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, int64_t c,
-                             const PlanGeom& p, const PlannedArgs& a, hipStream_t stream) {
+                             const PlanGeom& p, const PlannedArgs& a, hipStream_t stream,
+                             int64_t c0, int64_t c1) {
   if (d == 0) return;
+  if (c1 < 0 || c1 > p.num_chunks) c1 = p.num_chunks;
+  if (c0 < 0) c0 = 0;
+  if (c0 >= c1) return;
   static bool attr = false;
   if (!attr) {
     set_lds_attr(reinterpret_cast<const void*>(qry_q2_kernel<5, 2>));
@@ -828,22 +839,24 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
   while (nt * splits < 8 * static_cast<uint32_t>(device_cus()) && splits < 64) splits *= 2;
   hipLaunchKernelGGL(qry_q1_kernel, dim3(nt * splits), dim3(256), p.tile * 4, stream, table,
                      a.ent_info, a.seg, a.vals, static_cast<uint32_t>(p.tile),
-                     static_cast<uint32_t>(r * c), splits);
-  const dim3 g2(static_cast<uint32_t>(p.num_chunks));
+                     static_cast<uint32_t>(r * c), splits, a.base, nt, static_cast<uint32_t>(c0),
+                     static_cast<uint32_t>(c1), static_cast<uint32_t>(p.num_chunks));
+  const dim3 g2(static_cast<uint32_t>(c1 - c0));
+  const uint32_t cc0 = static_cast<uint32_t>(c0);
   const size_t l2 = stage_lds(p, r);
   const uint32_t dd = static_cast<uint32_t>(d), rr = static_cast<uint32_t>(r);
   const bool v16 = (reinterpret_cast<uintptr_t>(est) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(a.src_info) % 16 == 0) && ch % 8 == 0;
   if (p.dense) {
-    if (r == 5) hipLaunchKernelGGL((qry_q2_kernel<5, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16);
-    else hipLaunchKernelGGL((qry_q2_kernel<0, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16);
+    if (r == 5) hipLaunchKernelGGL((qry_q2_kernel<5, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0);
+    else hipLaunchKernelGGL((qry_q2_kernel<0, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0);
     return;
   }
   switch (r) {
-    case 5: hipLaunchKernelGGL((qry_q2_kernel<5, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
-    case 3: hipLaunchKernelGGL((qry_q2_kernel<3, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
-    case 1: hipLaunchKernelGGL((qry_q2_kernel<1, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
-    default: hipLaunchKernelGGL((qry_q2_kernel<0, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16); break;
+    case 5: hipLaunchKernelGGL((qry_q2_kernel<5, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
+    case 3: hipLaunchKernelGGL((qry_q2_kernel<3, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
+    case 1: hipLaunchKernelGGL((qry_q2_kernel<1, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
+    default: hipLaunchKernelGGL((qry_q2_kernel<0, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
   }
 }
 

@@ -155,6 +155,57 @@ class CSVec:
         est = self.query()
         return ops().topk_abs(est, int(k))
 
+    def shard_bounds(self, world: int) -> Optional[list]:
+        """Coordinate shard boundaries [b_0 = 0, ..., b_world = d] at plan-chunk
+        granularity (shard q = chunks [nch*q//world, nch*(q+1)//world)), or
+        None when the query is not planned (no chunk structure)."""
+        if not self._use_plan():
+            return None
+        geom = ops().plan_geometry(self.d, self.r, self.c)
+        chunk, nch = int(geom[2]), int(geom[3])
+        return [min(self.d, (nch * q // world) * chunk) for q in range(world + 1)]
+
+    def unsketch_sparse_sharded(self, k: int, rank: int, world: int, all_gather_rows):
+        """``unsketch_sparse`` with the median query and the top-k split over
+        ``world`` ranks: rank r estimates only its coordinate shard, selects
+        the shard's k largest |estimates| (ties -> lower index), the k-lists
+        are all-gathered (one collective of 2k int64 per rank) and every rank
+        selects the k best of the N*k candidates.  The candidates are in
+        ascending coordinate order (shards ascend with the rank, each list is
+        sorted), so "lower position" is "lower index" and the result is
+        bitwise the unsharded one: every member of the global top-k is in its
+        shard's top-k.  Falls back to the unsharded path when a shard holds
+        fewer than k coordinates or the query is not planned."""
+        k = int(k)
+        b = self.shard_bounds(world) if world > 1 else None
+        if b is None or min(b[q + 1] - b[q] for q in range(world)) < k:
+            return self.unsketch_sparse(k)
+        pack = self.unsketch_shard(k, rank, world, b)
+        return self.merge_shards(all_gather_rows(pack.view(1, 2 * k)), world, k)
+
+    def unsketch_shard(self, k: int, rank: int, world: int, bounds=None) -> torch.Tensor:
+        """This rank's candidates: [2, k] int64 = (global indices, fp32 bits of
+        the estimates) of its shard's top-k."""
+        b = bounds if bounds is not None else self.shard_bounds(world)
+        nch = int(ops().plan_geometry(self.d, self.r, self.c)[3])
+        lo, hi = b[rank], b[rank + 1]
+        est = ops().cs_query_planned(self.table, self.d, self._plan(), nch * rank // world,
+                                     nch * (rank + 1) // world)
+        li, lv = ops().topk_abs(est[lo:hi], k)
+        pack = torch.empty(2, k, dtype=torch.int64, device=self.device)
+        pack[0] = li + lo
+        pack[1] = lv.view(torch.int32)
+        return pack
+
+    @staticmethod
+    def merge_shards(allp: torch.Tensor, world: int, k: int):
+        """(idx, vals) of the k best of every rank's candidates (rank order)."""
+        allp = allp.view(world, 2, k)
+        idx_all = allp[:, 0].reshape(-1)
+        val_all = allp[:, 1].to(torch.int32).view(torch.float32).reshape(-1)
+        pos, vals = ops().topk_abs(val_all, k)
+        return idx_all.index_select(0, pos), vals
+
     def unSketch(self, k: int) -> torch.Tensor:
         idx, vals = self.unsketch_sparse(k)
         return ops().scatter_dense(idx, vals, self.d)

@@ -38,6 +38,7 @@ import torch
 
 from .. import ops
 from ..ops import CSVec
+from . import dist
 
 
 class FedOptimizer(torch.optim.Optimizer):
@@ -116,7 +117,15 @@ class ServerState:
                 ops.momentum_ef(self.V.view(-1), None, G.view(-1), rho, gscale, "none")
                 src = self.V
             sk = self.sketch.like(src)
-            idx, vals = sk.unsketch_sparse(a.k)
+            ctx = dist.ctx()
+            if (ctx.world_size > 1 and step is None
+                    and getattr(a, "shard_unsketch", "on") == "on"):
+                # every rank estimates 1/N of the coordinates and the k-lists
+                # are merged (bitwise the replicated result, ops/sketch.py)
+                idx, vals = sk.unsketch_sparse_sharded(a.k, ctx.rank, ctx.world_size,
+                                                       dist.all_gather_rows)
+            else:
+                idx, vals = sk.unsketch_sparse(a.k)
             # error feedback (virtual) + momentum-factor masking in sketch space
             sk.zero_heavy_hitters(idx, vals, self.V if et == "virtual" else None)
             ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)

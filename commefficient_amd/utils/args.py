@@ -193,6 +193,10 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="GPT-2 blocks: native junction kernels (csrc/transformer.hip: fused "
                         "residual+dropout+LayerNorm, bias+GELU, bias gradients) around "
                         "hipBLASLt GEMMs and SDPA, or the HF module forward")
+    g.add_argument("--shard_unsketch", choices=["on", "off"], default="on",
+                   help="sketch mode on >1 rank: each rank runs the median query + top-k on "
+                        "its 1/N of the coordinates, the k-lists are all-gathered and merged "
+                        "(bitwise the replicated result; one all-gather of 2k int64 per rank)")
     g.add_argument("--unpad", choices=["on", "off"], default="on",
                    help="native GPT-2 path: token-wise ops (embeddings, GEMMs, LayerNorm/"
                         "GELU junctions) on the real tokens only, attention on the padded "

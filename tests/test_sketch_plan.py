@@ -204,3 +204,26 @@ def test_dense_fixed_point_encode_deterministic_and_accurate():
     bad[12345] = float("nan")
     gpu.accumulateVec(bad, 1.0, overwrite=True)
     assert torch.isnan(gpu.table).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("shape", [(6568640, 5, 500000), (2_000_003, 5, 100_000)])
+def test_sharded_unsketch_equals_replicated_gpu(world, shape):
+    """Each rank's shard query + top-k, merged over the ranks' candidate lists,
+    is bitwise the replicated unsketch (same indices, same values)."""
+    import torch
+    from commefficient_amd.ops import CSVec
+    d, r, c = shape
+    k = 50000
+    torch.manual_seed(0)
+    sk = CSVec(d, c, r, device="cuda", numBlocks=20, kernel="planned")
+    v = torch.randn(d, device="cuda") * torch.rand(d, device="cuda").pow(8)
+    sk.accumulateVec(v)
+    ref_i, ref_v = sk.unsketch_sparse(k)
+    b = sk.shard_bounds(world)
+    assert b is not None and b[0] == 0 and b[-1] == d
+    packs = [sk.unsketch_shard(k, q, world, b) for q in range(world)]
+    idx, vals = CSVec.merge_shards(torch.cat([p.view(1, -1) for p in packs]), world, k)
+    assert torch.equal(idx, ref_i)
+    assert torch.equal(vals, ref_v)
