@@ -201,9 +201,42 @@ def _acc_mm(sink: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
         sink.add_(a.float() @ b.float())
 
 
+# Weight-gradient GEMMs into the sinks run on a side stream: they have few
+# output tiles (768 x 768 .. 768 x 3072 over K = tokens: 36-144 tiles of
+# 128 x 128 on 256 CUs) and nothing in the backward waits for them, so they
+# overlap the input-gradient GEMMs, attention backward and junction kernels
+# of the layers below.  ``join_wgrad_stream()`` orders the main stream after
+# them before the flat gradient is read.
+_SIDE: dict = {"enabled": True, "stream": None, "pending": False}
+
+
+def set_wgrad_stream(enabled: bool) -> None:
+    _SIDE["enabled"] = bool(enabled)
+
+
+def join_wgrad_stream() -> None:
+    if _SIDE["pending"]:
+        torch.cuda.current_stream().wait_stream(_SIDE["stream"])
+        _SIDE["pending"] = False
+
+
 def _wgrad(sink, a, b):
     if sink is None:
         return torch.mm(a, b)
+    if sink.is_cuda and _SIDE["enabled"]:
+        main = torch.cuda.current_stream()
+        if _SIDE["stream"] is None:
+            _SIDE["stream"] = torch.cuda.Stream(device=sink.device)
+        side = _SIDE["stream"]
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            _acc_mm(sink, a, b)
+        # the operands were allocated on the main stream: keep their memory
+        # until the side stream has consumed them
+        a.record_stream(side)
+        b.record_stream(side)
+        _SIDE["pending"] = True
+        return None
     _acc_mm(sink, a, b)
     return None
 

@@ -298,6 +298,7 @@ class FedModel:
         # bucket hooks, which watch the replica's .grad)
         sinks = (self.flat.grad_sink_map() if (shadow is not None and want_grad
                                                 and not self._overlap_armed) else None)
+        _tx.set_wgrad_stream(getattr(self.args, "wgrad_stream", "on") == "on")
         with (self._autocast(cache=not capture) if shadow is None else nullcontext()), \
                 _tx.grad_sinks(sinks):
             with (ghost_batchnorm(model, groups) if (groups > 1 and self.has_bn)
@@ -319,6 +320,8 @@ class FedModel:
                 if loss_weight is not None:
                     total = total * loss_weight
                 total.backward()
+            if sinks is not None:
+                _tx.join_wgrad_stream()  # side-stream weight gradients into flat.g
             if shadow is not None and not self._overlap_armed:
                 self.flat.collect_shadow_grads()
         return per_ex.detach().float(), [m.detach().float() for m in metrics]

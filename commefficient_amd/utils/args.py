@@ -197,6 +197,9 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="sketch mode on >1 rank: each rank runs the median query + top-k on "
                         "its 1/N of the coordinates, the k-lists are all-gathered and merged "
                         "(bitwise the replicated result; one all-gather of 2k int64 per rank)")
+    g.add_argument("--wgrad_stream", choices=["on", "off"], default="on",
+                   help="native GPT-2 path: weight-gradient GEMMs on a side HIP stream, "
+                        "overlapping the rest of the backward")
     g.add_argument("--unpad", choices=["on", "off"], default="on",
                    help="native GPT-2 path: token-wise ops (embeddings, GEMMs, LayerNorm/"
                         "GELU junctions) on the real tokens only, attention on the padded "

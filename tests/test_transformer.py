@@ -197,6 +197,7 @@ def _sink_vs_cat(device):
             with tx.grad_sinks(flat.grad_sink_map() if use_sinks else None):
                 h = tx.gpt2_hidden(sh.transformer, ids[:, :, rep:], tt[:, :, rep:])
             h.float().square().mean().backward()
+            tx.join_wgrad_stream()
             flat.collect_shadow_grads()
         res.append(flat.g.clone())
     a, b = res
