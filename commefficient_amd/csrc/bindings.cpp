@@ -1445,6 +1445,68 @@ at::Tensor heads_to_rows_hip(at::TensorList srcs, const c10::optional<at::Tensor
   return out;
 }
 
+void check_seqs(const at::Tensor& start, const at::Tensor& len) {
+  TORCH_CHECK(start.scalar_type() == at::kInt && len.scalar_type() == at::kInt &&
+                  start.is_contiguous() && len.is_contiguous() && start.numel() == len.numel(),
+              "attn: start / len must be contiguous int32 [N]");
+}
+
+std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& qkv, const at::Tensor& start,
+                                                const at::Tensor& len, int64_t nh, double p_drop,
+                                                int64_t seed) {
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 2 && qkv.is_contiguous() &&
+                  qkv.size(1) == 3 * nh * 64,
+              "attn_fwd: qkv must be contiguous bf16 [M, 3 * nh * 64]");
+  check_seqs(start, len);
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "attn_fwd: p_drop in [0, 1)");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  const int64_t M = qkv.size(0), N = start.numel(), H = nh * 64;
+  auto o = at::empty({M, H}, qkv.options());
+  auto lse = at::empty({N * nh * 128}, qkv.options().dtype(at::kFloat));
+  AttnArgs a{};
+  a.qkv = reinterpret_cast<const uint16_t*>(qkv.data_ptr());
+  a.o = reinterpret_cast<uint16_t*>(o.data_ptr());
+  a.lse = lse.data_ptr<float>();
+  a.start = start.data_ptr<int32_t>();
+  a.len = len.data_ptr<int32_t>();
+  a.nh = static_cast<int>(nh);
+  a.scale = 0.125f;  // 1 / sqrt(64)
+  a.seed = static_cast<uint32_t>(seed);
+  launch_attn_fwd(a, N, static_cast<float>(p_drop), cur_stream());
+  return {o, lse};
+}
+
+at::Tensor attn_bwd_hip(const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& dout,
+                        const at::Tensor& lse, const at::Tensor& start, const at::Tensor& len,
+                        int64_t nh, double p_drop, int64_t seed) {
+  const int64_t H = nh * 64;
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 2 && qkv.is_contiguous() &&
+                  qkv.size(1) == 3 * H,
+              "attn_bwd: qkv must be contiguous bf16 [M, 3H]");
+  const int64_t M = qkv.size(0), N = start.numel();
+  for (const at::Tensor* t : {&o, &dout})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2 &&
+                    t->size(0) == M && t->size(1) == H,
+                "attn_bwd: o / dout must be contiguous bf16 [M, H]");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == N * nh * 128, "attn_bwd: lse");
+  check_seqs(start, len);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  auto dqkv = at::empty_like(qkv);
+  AttnArgs a{};
+  a.qkv = reinterpret_cast<const uint16_t*>(qkv.data_ptr());
+  a.o = reinterpret_cast<uint16_t*>(o.data_ptr());
+  a.lse = lse.data_ptr<float>();
+  a.dout = reinterpret_cast<const uint16_t*>(dout.data_ptr());
+  a.dqkv = reinterpret_cast<uint16_t*>(dqkv.data_ptr());
+  a.start = start.data_ptr<int32_t>();
+  a.len = len.data_ptr<int32_t>();
+  a.nh = static_cast<int>(nh);
+  a.scale = 0.125f;
+  a.seed = static_cast<uint32_t>(seed);
+  launch_attn_bwd(a, N, static_cast<float>(p_drop), cur_stream());
+  return dqkv;
+}
+
 }  // namespace
 }  // namespace commeff
 
@@ -1520,6 +1582,9 @@ TORCH_LIBRARY(commeff, m) {
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor u, Tensor b) -> Tensor");
   m.def("pad_rows(Tensor src, Tensor? inv, int rows) -> Tensor");
+  m.def("attn_fwd(Tensor qkv, Tensor start, Tensor len, int nh, float p_drop, int seed) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, Tensor start, Tensor len, int nh, "
+        "float p_drop, int seed) -> Tensor");
   m.def("heads_to_rows(Tensor[] srcs, Tensor? tok, int Mr) -> Tensor");
   m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu, Tensor(a!)? sbias=None) "
         "-> (Tensor, Tensor)");
@@ -1597,5 +1662,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("bias_gelu_fwd", &bias_gelu_fwd_hip);
   m.impl("bias_act_bwd", &bias_act_bwd_hip);
   m.impl("pad_rows", &pad_rows_hip);
+  m.impl("attn_fwd", &attn_fwd_hip);
+  m.impl("attn_bwd", &attn_bwd_hip);
   m.impl("heads_to_rows", &heads_to_rows_hip);
 }

@@ -333,6 +333,24 @@ void launch_pad_rows(const void* src, int64_t src_ld, int64_t K, const int32_t* 
                      void* out, hipStream_t stream);
 void launch_heads_to_rows(const HeadSrcs& src, int P, int64_t H, int64_t hd, int64_t L,
                           const int32_t* tok, int64_t Mr, void* out, hipStream_t stream);
+// fused causal attention over unpadded token rows (attention.hip): sequence n
+// = rows [start[n], start[n] + len[n]), len <= 128, head dim 64
+struct AttnArgs {
+  const uint16_t* qkv;  // [M, 3H] bf16 (q | k | v)
+  uint16_t* o;          // [M, H] bf16 (forward output, backward input)
+  float* lse;           // [N * nh * 128] fp32
+  const uint16_t* dout; // [M, H] bf16 (backward)
+  uint16_t* dqkv;       // [M, 3H] bf16 (backward)
+  const int32_t* start;
+  const int32_t* len;
+  int nh;
+  float scale;
+  uint32_t thresh;  // set by the launchers from p_drop
+  float dscale;
+  uint32_t seed;
+};
+void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream);
+void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream);
 // out_q[c] = sum over b < G of part[b*stride + q*N + c], q < Q (fixed order)
 void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,
                          const ColsumOut& out, hipStream_t stream);

@@ -50,7 +50,11 @@ def _mix32(x: torch.Tensor) -> torch.Tensor:
 
 def drop_keep(numel: int, seed: int, p: float, device=None) -> torch.Tensor:
     """The kernels' dropout keep-mask of ``numel`` consecutive elements."""
-    idx = torch.arange(numel, dtype=torch.int64, device=device)
+    return keep_at(torch.arange(numel, dtype=torch.int64, device=device), seed, p)
+
+
+def keep_at(idx: torch.Tensor, seed: int, p: float) -> torch.Tensor:
+    """The kernels' dropout keep-mask at element indices ``idx`` (int64)."""
     hi = _mix32(((idx >> 32) + (seed & _M32)) & _M32)
     h = _mix32((idx & _M32) ^ hi)
     thresh = min(int(p * 4294967296.0), _M32) if p > 0 else 0
@@ -218,6 +222,13 @@ def join_wgrad_stream() -> None:
     if _SIDE["pending"]:
         torch.cuda.current_stream().wait_stream(_SIDE["stream"])
         _SIDE["pending"] = False
+
+
+_ATTN = {"enabled": True}
+
+
+def set_fused_attention(enabled: bool) -> None:
+    _ATTN["enabled"] = bool(enabled)
 
 
 def _wgrad(sink, a, b):
@@ -447,27 +458,97 @@ class _ToPadded(torch.autograd.Function):
 
 
 def real_token_index(lengths: torch.Tensor, L: int, device):
-    """(tok, inv) for host-side sequence lengths: tok = flat positions n*L + t
-    (t < lengths[n]) of the real tokens, inv = token row of every padded
-    position or -1; built on the host (their sizes are known without a
-    sync), one int32 H2D copy."""
+    """(tok, inv, start, len) for host-side sequence lengths: tok = flat
+    positions n*L + t (t < lengths[n]) of the real tokens, inv = token row of
+    every padded position or -1, start / len = each sequence's token rows;
+    built on the host (their sizes are known without a sync), one int32 H2D
+    copy."""
     import numpy as np
     ln = lengths.reshape(-1).numpy().astype(np.int64)
     if ln.size == 0 or int(ln.min()) < 0 or int(ln.max()) > L:
         return None
     Mr = int(ln.sum())
-    starts = np.repeat(np.arange(ln.size, dtype=np.int64) * L - np.concatenate(
-        [[0], np.cumsum(ln)[:-1]]), ln)
+    cs = np.concatenate([[0], np.cumsum(ln)[:-1]])
+    starts = np.repeat(np.arange(ln.size, dtype=np.int64) * L - cs, ln)
     tok = starts + np.arange(Mr, dtype=np.int64)
     inv = np.full(ln.size * L, -1, dtype=np.int64)
     inv[tok] = np.arange(Mr)
-    both = np.concatenate([tok, inv]).astype(np.int32)
+    both = np.concatenate([tok, inv, cs, ln]).astype(np.int32)
     if torch.device(device).type == "cuda":
         from ..parallel.dist import h2d
         both = h2d(both, device)
     else:
         both = torch.from_numpy(both)
-    return both[:Mr], both[Mr:]
+    n = ln.size
+    return both[:Mr], both[Mr:Mr + n * L], both[Mr + n * L:Mr + n * L + n], both[Mr + n * L + n:]
+
+
+# ------------------------------------------------------- fused attention
+ATTN_MAX_LEN = 128
+
+
+def _ref_attn(qkv, start, lens, nh, p, seed):
+    """fp32 reference of csrc/attention.hip over unpadded token rows (same
+    dropout hash; P_drop rounded to bf16 as the kernel feeds it to the MFMA)."""
+    M, H3 = qkv.shape
+    H = H3 // 3
+    hd = H // nh
+    o = qkv.new_zeros(M, H, dtype=torch.float32)
+    lse = torch.zeros(start.numel() * nh * ATTN_MAX_LEN, dtype=torch.float32, device=qkv.device)
+    for n in range(start.numel()):
+        s0, L = int(start[n]), int(lens[n])
+        if L == 0:
+            continue
+        x = qkv[s0:s0 + L].float().view(L, 3, nh, hd).permute(1, 2, 0, 3)  # [3, nh, L, hd]
+        q, k, v = x[0], x[1], x[2]
+        S = (q @ k.transpose(1, 2)) * (hd ** -0.5)
+        mask = torch.ones(L, L, dtype=torch.bool, device=qkv.device).tril()
+        S = S.masked_fill(~mask, float("-inf"))
+        m = S.amax(-1, keepdim=True)
+        e = torch.exp(S - m)
+        ssum = e.sum(-1, keepdim=True)
+        P = e / ssum
+        base = (n * nh + torch.arange(nh, device=qkv.device)) * ATTN_MAX_LEN
+        i = torch.arange(L, device=qkv.device)
+        idx = ((base[:, None, None] + i[None, :, None]) * ATTN_MAX_LEN + i[None, None, :])
+        if p > 0:
+            keep = keep_at(idx.long(), seed, p)
+            P = torch.where(keep, P / (1.0 - p), torch.zeros_like(P))
+        P = _bf(P)
+        o[s0:s0 + L] = (P @ v).transpose(0, 1).reshape(L, H)
+        lse.view(-1, ATTN_MAX_LEN)[n * nh:(n + 1) * nh, :L] = (m + torch.log(ssum)).squeeze(-1)
+    return o.to(qkv.dtype), lse
+
+
+class _Attention(torch.autograd.Function):
+    """o [M, H] = causal self-attention of every sequence's token rows of
+    qkv [M, 3H] (csrc/attention.hip on HIP tensors)."""
+
+    @staticmethod
+    def forward(ctx, qkv, start, lens, nh, p, seed):
+        if qkv.is_cuda:
+            o, lse = _ops().attn_fwd(qkv, start, lens, nh, p, seed)
+            ctx.save_for_backward(qkv, o, lse, start, lens)
+        else:
+            o, _ = _ref_attn(qkv, start, lens, nh, p, seed)
+            ctx.save_for_backward(qkv, start, lens)
+        ctx.cfg = (nh, p, seed)
+        return o
+
+    @staticmethod
+    def backward(ctx, g):
+        nh, p, seed = ctx.cfg
+        if g.is_cuda:
+            qkv, o, lse, start, lens = ctx.saved_tensors
+            dqkv = _ops().attn_bwd(qkv, o, g.contiguous(), lse, start, lens, nh, p, seed)
+        else:
+            qkv, start, lens = ctx.saved_tensors
+            with torch.enable_grad():
+                x = qkv.detach().float().requires_grad_()
+                o, _ = _ref_attn(x, start, lens, nh, p, seed)
+                o.float().backward(g.float())
+            dqkv = x.grad.to(qkv.dtype)
+        return dqkv, None, None, None, None, None
 
 
 def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tensor] = None,
@@ -502,12 +583,24 @@ def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tens
     if seeds is None:
         seeds = _Seeds(torch.initial_seed())
         tr._commeff_seeds = seeds
-    tok = inv = None
-    if lengths is not None and not lengths.is_cuda and int(lengths.sum()) < M:
-        ti = real_token_index(lengths, L, ids.device)
-        if ti is not None:
-            tok, inv = ti
+    tok = inv = sstart = slen = None
+    max_len = L
+    if lengths is not None and not lengths.is_cuda:
+        max_len = int(lengths.max()) if lengths.numel() else 0
+        if int(lengths.sum()) < M:
+            ti = real_token_index(lengths, L, ids.device)
+            if ti is not None:
+                tok, inv, sstart, slen = ti
     Mr = M if tok is None else tok.shape[0]
+    # fused short-sequence attention (csrc/attention.hip) straight on the
+    # token rows; the padded-layout SDPA path otherwise
+    fused_attn = (_ATTN["enabled"] and ids.is_cuda and H // nh == 64 and max_len <= ATTN_MAX_LEN)
+    if fused_attn and sstart is None:
+        import numpy as np
+        se = np.concatenate([np.arange(Nn) * L, np.full(Nn, L)]).astype(np.int32)
+        from ..parallel.dist import h2d
+        se = h2d(se, ids.device)
+        sstart, slen = se[:Nn], se[Nn:]
     if tok is None:
         pos = torch.arange(L, device=ids.device)
         e = (tr.wte(ids) + tr.wpe(pos)).reshape(M, H)
@@ -524,14 +617,16 @@ def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tens
     for i, blk in enumerate(blocks):
         at = blk.attn
         qkv = _Linear.apply(y, at.c_attn.weight, at.c_attn.bias)
-        # token rows -> padded per-head q, k, v and back in one kernel each
-        # (the layout change, the padding and, backward, the q/k/v gradient
-        # concatenation in the same pass)
-        q, k, v = _RowsToHeads.apply(qkv, tok, inv, Nn, L, nh)
-        o = F.scaled_dot_product_attention(
-            q, k, v, dropout_p=_p(getattr(at, "attn_dropout", None), cfg.attn_pdrop),
-            is_causal=True)
-        o = _HeadsToRows.apply(o, tok, inv, Mr)
+        pa = _p(getattr(at, "attn_dropout", None), cfg.attn_pdrop)
+        if fused_attn:
+            o = _Attention.apply(qkv, sstart, slen, nh, pa, seeds.next())
+        else:
+            # token rows -> padded per-head q, k, v and back in one kernel each
+            # (the layout change, the padding and, backward, the q/k/v
+            # gradient concatenation in the same pass)
+            q, k, v = _RowsToHeads.apply(qkv, tok, inv, Nn, L, nh)
+            o = F.scaled_dot_product_attention(q, k, v, dropout_p=pa, is_causal=True)
+            o = _HeadsToRows.apply(o, tok, inv, Mr)
         h, y = _ResidLN.apply(h, o, at.c_proj.weight, at.c_proj.bias, blk.ln_2.weight,
                               blk.ln_2.bias, _p(getattr(at, "resid_dropout", None), cfg.resid_pdrop),
                               seeds.next(), eps)

@@ -294,7 +294,7 @@ def test_rows_heads_layout_kernels_gpu(unpad):
     N, L, nh, hd = 5, 24, 12, 64
     H = nh * hd
     lens = torch.tensor([24, 3, 17, 1, 10]) if unpad else torch.full((5,), 24)
-    tok, inv = tx.real_token_index(lens, L, "cpu")
+    tok, inv, _, _ = tx.real_token_index(lens, L, "cpu")
     Mr = tok.numel()
     g = torch.Generator().manual_seed(0)
     qkv = torch.randn(Mr, 3 * H, generator=g).to(torch.bfloat16)
@@ -307,3 +307,76 @@ def test_rows_heads_layout_kernels_gpu(unpad):
     got = ops().heads_to_rows([s.cuda() for s in srcs], ti, Mr)
     exp = tx._ref_heads_to_rows(srcs, tok if unpad else None, Mr)
     assert torch.equal(got.cpu(), exp)
+
+
+def _attn_case(device, lens=(37, 128, 1, 90), nh=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    lens_t = torch.tensor(lens, dtype=torch.int32)
+    start = torch.cat([torch.zeros(1, dtype=torch.int32), lens_t.cumsum(0)[:-1].int()])
+    M = int(lens_t.sum())
+    qkv = (torch.randn(M, 3 * nh * 64, generator=g) * 0.5).to(torch.bfloat16).to(device)
+    return qkv, start.to(device), lens_t.to(device), nh
+
+
+def test_fused_attention_reference_matches_sdpa_cpu():
+    """The kernel's fp32 reference (no dropout) == per-sequence causal SDPA."""
+    import torch.nn.functional as F
+    qkv, start, lens, nh = _attn_case("cpu")
+    o, _ = tx._ref_attn(qkv, start, lens, nh, 0.0, 0)
+    for n in range(start.numel()):
+        s0, L = int(start[n]), int(lens[n])
+        x = qkv[s0:s0 + L].float().view(L, 3, nh, 64).permute(1, 2, 0, 3)
+        ref = F.scaled_dot_product_attention(x[0], x[1], x[2], is_causal=True)
+        torch.testing.assert_close(o[s0:s0 + L].float(), ref.transpose(0, 1).reshape(L, -1),
+                                   rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_fused_attention_kernels_vs_reference_gpu(p):
+    from commefficient_amd._ext import ops
+    qkv, start, lens, nh = _attn_case("cuda")
+    o, lse = ops().attn_fwd(qkv, start, lens, nh, p, 1234)
+    ro, rlse = tx._ref_attn(qkv.cpu(), start.cpu(), lens.cpu(), nh, p, 1234)
+    torch.testing.assert_close(o.float().cpu(), ro.float(), rtol=2e-2, atol=2e-2)
+    valid = torch.zeros(start.numel() * nh, 128, dtype=torch.bool)
+    for n, L in enumerate(lens.tolist()):
+        valid[n * nh:(n + 1) * nh, :L] = True
+    torch.testing.assert_close(lse.cpu().view(-1, 128)[valid], rlse.view(-1, 128)[valid],
+                               rtol=1e-3, atol=1e-3)
+    gout = (torch.randn(o.shape, generator=torch.Generator().manual_seed(5)) * 0.5).to(
+        torch.bfloat16)
+    dq = ops().attn_bwd(qkv, o, gout.cuda(), lse, start, lens, nh, p, 1234)
+    x = qkv.cpu().float().requires_grad_()
+    rref, _ = tx._ref_attn(x, start.cpu(), lens.cpu(), nh, p, 1234)
+    rref.float().backward(gout.float())
+    for part in range(3):
+        a = dq.float().cpu()[:, part * nh * 64:(part + 1) * nh * 64]
+        r = x.grad[:, part * nh * 64:(part + 1) * nh * 64]
+        rel = (a - r).norm() / r.norm()
+        assert rel < 3e-2, (part, float(rel))
+
+
+@pytest.mark.gpu
+def test_native_path_fused_attention_matches_sdpa_path_gpu():
+    """gpt2_hidden with the fused attention == with the SDPA path (no dropout)."""
+    import copy
+    base = _tiny_gpt2().cuda().to(torch.bfloat16).eval()
+    ids, tt = _inputs(device="cuda")
+    lens = torch.tensor([[20, 13], [7, 16], [20, 1]])
+    mask = (torch.arange(20)[None, None, :] < lens[..., None]).cuda()
+    gw = torch.randn(*ids.shape, 256, generator=torch.Generator().manual_seed(3)).cuda()
+    gw = gw * mask[..., None]
+    outs = []
+    for fused in (True, False):
+        tx.set_fused_attention(fused)
+        m = copy.deepcopy(base)
+        h = tx.gpt2_hidden(m.transformer, ids, tt, lens)
+        (h.float() * gw).sum().backward()
+        outs.append((h.float() * mask[..., None], _grads(m)))
+    tx.set_fused_attention(True)
+    (h0, g0), (h1, g1) = outs
+    torch.testing.assert_close(h0, h1, rtol=2e-2, atol=3e-2)
+    for n in g0:
+        rel = (g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-6)
+        assert rel < 3e-2, (n, float(rel))
