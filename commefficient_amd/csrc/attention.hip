@@ -39,7 +39,6 @@ constexpr int HD = 64;       // head dim
 constexpr int LM = 128;      // max sequence length
 constexpr int RS = HD + 8;   // row stride (elements) of [LM][HD] bf16 tiles
 constexpr int TS = LM + 8;   // row stride of [HD][LM] and [LM][LM] bf16 tiles
-constexpr int SS = LM + 4;   // row stride of the fp32 score tile
 constexpr int OS = HD + 4;   // row stride of the fp32 output staging tile
 
 __device__ __forceinline__ uint16_t bfbits(float f) {
@@ -71,14 +70,16 @@ __device__ __forceinline__ f32x16_t zero16() {
 }
 
 // ------------------------------------------------------------------ forward
+// LDS: Q, K [LM][RS] and V^T [HD][TS] (54 KB: 2 workgroups per CU); the
+// score strip and its softmax stay in registers (row max / sum over the 32
+// lanes that hold a row: 5 xor-shuffles), P_drop goes to LDS over Q / K.
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);          // [LM][RS]
   uint16_t* sK = sQ + LM * RS;                                 // [LM][RS]
   uint16_t* sVt = sK + LM * RS;                                // [HD][TS]
-  float* sS = reinterpret_cast<float*>(sVt + HD * TS);         // [LM][SS]
   uint16_t* sP = sQ;                                           // [LM][TS] over Q, K
-  float* sO = sS;                                              // [LM][OS] over S
+  float* sO = reinterpret_cast<float*>(smem);                  // [LM][OS] over Q, K
   const int bh = blockIdx.x;
   const int n = bh / a.nh, h = bh - n * a.nh;
   const int L = a.len[n];
@@ -87,82 +88,95 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
   const int H = a.nh * HD;
 
-  for (int c = tid; c < LM * 8; c += 256) {
-    const int i = c >> 3, ch = c & 7;
-    v4u q = {0u, 0u, 0u, 0u}, k = q, v = q;
-    if (i < L) {
-      const uint16_t* row = a.qkv + (r0 + i) * (3 * H) + h * HD + ch * 8;
-      q = *reinterpret_cast<const v4u*>(row);
-      k = *reinterpret_cast<const v4u*>(row + H);
-      v = *reinterpret_cast<const v4u*>(row + 2 * H);
-    }
-    *reinterpret_cast<v4u*>(sQ + i * RS + ch * 8) = q;
-    *reinterpret_cast<v4u*>(sK + i * RS + ch * 8) = k;
+  {  // all of this thread's 16-byte pieces in flight before any LDS store
+    v4u q[4], k[4], v[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      sVt[(ch * 8 + e) * TS + i] = static_cast<uint16_t>((v[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + 256 * u, i = c >> 3, ch = c & 7;
+      q[u] = k[u] = v[u] = v4u{0u, 0u, 0u, 0u};
+      if (i < L) {
+        const uint16_t* row = a.qkv + (r0 + i) * (3 * H) + h * HD + ch * 8;
+        q[u] = *reinterpret_cast<const v4u*>(row);
+        k[u] = *reinterpret_cast<const v4u*>(row + H);
+        v[u] = *reinterpret_cast<const v4u*>(row + 2 * H);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + 256 * u, i = c >> 3, ch = c & 7;
+      *reinterpret_cast<v4u*>(sQ + i * RS + ch * 8) = q[u];
+      *reinterpret_cast<v4u*>(sK + i * RS + ch * 8) = k[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        sVt[(ch * 8 + e) * TS + i] = static_cast<uint16_t>((v[u][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+    }
   }
   __syncthreads();
 
-  if (32 * w < L) {
+  const bool active = 32 * w < L;
+  f32x16_t sc[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) sc[ct] = zero16();
+  if (active) {
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       if (ct > w) break;  // causal: these key tiles are all masked for this strip
-      f32x16_t acc = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sQ + (32 * w + lr) * RS + 16 * ks + 8 * hi);
         const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sK + (32 * ct + lr) * RS + 16 * ks + 8 * hi);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+        sc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, sc[ct], 0, 0, 0);
+      }
+    }
+    // softmax of the strip's 16 rows per lane (row = 32 w + crow(e, hi), the
+    // 32 lanes of this half-wave hold its 32-column slices of every tile)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = 32 * w + crow(e, hi);
+      float m = -__builtin_huge_valf();
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int col = 32 * ct + lr;
+        const bool ok = ct <= w && col <= row && col < L;
+        sc[ct][e] = ok ? sc[ct][e] * a.scale : -__builtin_huge_valf();
+        m = fmaxf(m, sc[ct][e]);
       }
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = 32 * w + crow(e, hi), col = 32 * ct + lr;
-        sS[row * SS + col] = (col <= row && col < L) ? acc[e] * a.scale : -__builtin_huge_valf();
+      for (int o = 16; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const float pv = ct <= w ? __expf(sc[ct][e] - m) : 0.f;  // exp(-inf) = 0 past the diagonal
+        sc[ct][e] = pv;
+        sum += pv;
       }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      if (lr == 0 && row < L) a.lse[static_cast<int64_t>(bh) * LM + row] = m + __logf(sum);
+      const float inv = 1.f / sum;
+      const uint64_t ib = (static_cast<uint64_t>(bh) * LM + row) * LM;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        float pv = sc[ct][e] * inv;
+        if (a.thresh != 0u && pv != 0.f)
+          pv = akeep(ib + 32 * ct + lr, a.seed, a.thresh) ? pv * a.dscale : 0.f;
+        sc[ct][e] = pv;
+      }
+    }
+  }
+  __syncthreads();  // every wave is done reading Q / K: P goes over them
+  if (active) {
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      if (ct > w) break;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sP[(32 * w + crow(e, hi)) * TS + 32 * ct + lr] = bfbits(sc[ct][e]);
     }
   }
   __syncthreads();
 
-  // row softmax, 2 threads per row; P_drop -> sP (bf16, zeros past the diagonal)
-  {
-    const int i = tid >> 1, half = tid & 1;
-    const int jmax = i + 1 < L ? i + 1 : L;  // valid keys [0, jmax)
-    float p[64];
-    float m = -__builtin_huge_valf();
-#pragma unroll
-    for (int t = 0; t < 64; ++t) {
-      const int j = half * 64 + t;
-      p[t] = j < jmax ? sS[i * SS + j] : -__builtin_huge_valf();
-      m = fmaxf(m, p[t]);
-    }
-    m = fmaxf(m, __shfl_xor(m, 1, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < 64; ++t) {
-      const int j = half * 64 + t;
-      p[t] = j < jmax ? __expf(p[t] - m) : 0.f;
-      sum += p[t];
-    }
-    sum += __shfl_xor(sum, 1, 64);
-    if (i < L && half == 0) a.lse[static_cast<int64_t>(bh) * LM + i] = m + __logf(sum);
-    const float inv = 1.f / sum;
-    const uint64_t ib = (static_cast<uint64_t>(bh) * LM + i) * LM + half * 64;
-#pragma unroll
-    for (int t = 0; t < 64; t += 2) {
-      float v0 = p[t] * inv, v1 = p[t + 1] * inv;
-      if (a.thresh != 0u) {
-        v0 = akeep(ib + t, a.seed, a.thresh) ? v0 * a.dscale : 0.f;
-        v1 = akeep(ib + t + 1, a.seed, a.thresh) ? v1 * a.dscale : 0.f;
-      }
-      *reinterpret_cast<uint32_t*>(sP + i * TS + half * 64 + t) =
-          static_cast<uint32_t>(bfbits(v0)) | (static_cast<uint32_t>(bfbits(v1)) << 16);
-    }
-  }
-  __syncthreads();
-
-  if (32 * w < L) {
-    f32x16_t acc[2] = {zero16(), zero16()};
+  f32x16_t acc[2] = {zero16(), zero16()};
+  if (active) {
     for (int ks = 0; ks < 2 * w + 2; ++ks) {
       const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sP + (32 * w + lr) * TS + 16 * ks + 8 * hi);
 #pragma unroll
@@ -171,7 +185,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
         acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[ct], 0, 0, 0);
       }
     }
-    // sO aliases sS: every wave's softmax reads finished at the barrier above
+  }
+  __syncthreads();  // P reads done: stage O over it
+  if (active) {
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -218,27 +234,36 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
   const int H = a.nh * HD;
 
-  // ---- phase 1: loads (rows past L are zero)
-  for (int c = tid; c < LM * 8; c += 256) {
-    const int i = c >> 3, ch = c & 7;
-    v4u q = {0u, 0u, 0u, 0u}, k = q, v = q, g = q;
-    if (i < L) {
-      const uint16_t* row = a.qkv + (r0 + i) * (3 * H) + h * HD + ch * 8;
-      q = *reinterpret_cast<const v4u*>(row);
-      k = *reinterpret_cast<const v4u*>(row + H);
-      v = *reinterpret_cast<const v4u*>(row + 2 * H);
-      g = *reinterpret_cast<const v4u*>(a.dout + (r0 + i) * H + h * HD + ch * 8);
-    }
-    *reinterpret_cast<v4u*>(sQ + i * RS + ch * 8) = q;
-    *reinterpret_cast<v4u*>(sK + i * RS + ch * 8) = k;
-    *reinterpret_cast<v4u*>(sV + i * RS + ch * 8) = v;
-    *reinterpret_cast<v4u*>(sdO + i * RS + ch * 8) = g;
+  // ---- phase 1: loads (rows past L are zero), all pieces in flight first
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int d = ch * 8 + e, sh = 16 * (e & 1);
-      sQt[d * TS + i] = static_cast<uint16_t>((q[e >> 1] >> sh) & 0xffffu);
-      sKt[d * TS + i] = static_cast<uint16_t>((k[e >> 1] >> sh) & 0xffffu);
-      sdOt[d * TS + i] = static_cast<uint16_t>((g[e >> 1] >> sh) & 0xffffu);
+  for (int half = 0; half < 2; ++half) {
+    v4u q[2], k[2], v[2], g[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * (2 * half + u), i = c >> 3, ch = c & 7;
+      q[u] = k[u] = v[u] = g[u] = v4u{0u, 0u, 0u, 0u};
+      if (i < L) {
+        const uint16_t* row = a.qkv + (r0 + i) * (3 * H) + h * HD + ch * 8;
+        q[u] = *reinterpret_cast<const v4u*>(row);
+        k[u] = *reinterpret_cast<const v4u*>(row + H);
+        v[u] = *reinterpret_cast<const v4u*>(row + 2 * H);
+        g[u] = *reinterpret_cast<const v4u*>(a.dout + (r0 + i) * H + h * HD + ch * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = tid + 256 * (2 * half + u), i = c >> 3, ch = c & 7;
+      *reinterpret_cast<v4u*>(sQ + i * RS + ch * 8) = q[u];
+      *reinterpret_cast<v4u*>(sK + i * RS + ch * 8) = k[u];
+      *reinterpret_cast<v4u*>(sV + i * RS + ch * 8) = v[u];
+      *reinterpret_cast<v4u*>(sdO + i * RS + ch * 8) = g[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = ch * 8 + e, sh = 16 * (e & 1);
+        sQt[d * TS + i] = static_cast<uint16_t>((q[u][e >> 1] >> sh) & 0xffffu);
+        sKt[d * TS + i] = static_cast<uint16_t>((k[u][e >> 1] >> sh) & 0xffffu);
+        sdOt[d * TS + i] = static_cast<uint16_t>((g[u][e >> 1] >> sh) & 0xffffu);
+      }
     }
   }
   {  // D_i = dO_i . O_i (2 threads per row), LSE_i
@@ -377,10 +402,10 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
   }
 }
 
-constexpr size_t kFwdLds = (2 * LM * RS + HD * TS) * 2 + LM * SS * 4;
+constexpr size_t kFwdLds = (2 * LM * RS + HD * TS) * 2;
 constexpr size_t kBwdLds = 3 * HD * TS * 2 + 2 * LM * 4 + 3 * LM * TS * 2;
 static_assert(2 * LM * RS >= LM * TS, "P must fit over Q and K");
-static_assert(LM * SS >= LM * OS, "O staging must fit over S");
+static_assert(2 * LM * RS * 2 >= LM * OS * 4, "O staging must fit over Q and K");
 static_assert(3 * LM * TS >= 4 * LM * RS, "row tiles must fit in R2");
 static_assert(kBwdLds <= 160 * 1024, "backward LDS");
 
