@@ -39,6 +39,7 @@ constexpr int HD = 64;       // head dim
 constexpr int LM = 128;      // max sequence length
 constexpr int RS = HD + 8;   // row stride (elements) of [LM][HD] bf16 tiles
 constexpr int TS = LM + 8;   // row stride of [HD][LM] and [LM][LM] bf16 tiles
+constexpr int SS = LM + 4;   // row stride of the fp32 score tile
 constexpr int OS = HD + 4;   // row stride of the fp32 output staging tile
 
 __device__ __forceinline__ uint16_t bfbits(float f) {
@@ -70,16 +71,17 @@ __device__ __forceinline__ f32x16_t zero16() {
 }
 
 // ------------------------------------------------------------------ forward
-// LDS: Q, K [LM][RS] and V^T [HD][TS] (54 KB: 2 workgroups per CU); the
-// score strip and its softmax stay in registers (row max / sum over the 32
-// lanes that hold a row: 5 xor-shuffles), P_drop goes to LDS over Q / K.
+// LDS: Q, K [LM][RS], V^T [HD][TS] and the fp32 score tile (122 KB).  (A
+// variant with the softmax in registers -- 54 KB, 2 workgroups per CU, row
+// reductions by 10 xor-shuffles per row -- measured 460 vs 366 us/round.)
 __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);          // [LM][RS]
   uint16_t* sK = sQ + LM * RS;                                 // [LM][RS]
   uint16_t* sVt = sK + LM * RS;                                // [HD][TS]
+  float* sS = reinterpret_cast<float*>(sVt + HD * TS);         // [LM][SS]
   uint16_t* sP = sQ;                                           // [LM][TS] over Q, K
-  float* sO = reinterpret_cast<float*>(smem);                  // [LM][OS] over Q, K
+  float* sO = sS;                                              // [LM][OS] over S
   const int bh = blockIdx.x;
   const int n = bh / a.nh, h = bh - n * a.nh;
   const int L = a.len[n];
@@ -113,70 +115,65 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   }
   __syncthreads();
 
-  const bool active = 32 * w < L;
-  f32x16_t sc[4];
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) sc[ct] = zero16();
-  if (active) {
+  if (32 * w < L) {
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) {
       if (ct > w) break;  // causal: these key tiles are all masked for this strip
+      f32x16_t acc = zero16();
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sQ + (32 * w + lr) * RS + 16 * ks + 8 * hi);
         const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sK + (32 * ct + lr) * RS + 16 * ks + 8 * hi);
-        sc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, sc[ct], 0, 0, 0);
-      }
-    }
-    // softmax of the strip's 16 rows per lane (row = 32 w + crow(e, hi), the
-    // 32 lanes of this half-wave hold its 32-column slices of every tile)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int row = 32 * w + crow(e, hi);
-      float m = -__builtin_huge_valf();
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const int col = 32 * ct + lr;
-        const bool ok = ct <= w && col <= row && col < L;
-        sc[ct][e] = ok ? sc[ct][e] * a.scale : -__builtin_huge_valf();
-        m = fmaxf(m, sc[ct][e]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-      float sum = 0.f;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const float pv = ct <= w ? __expf(sc[ct][e] - m) : 0.f;  // exp(-inf) = 0 past the diagonal
-        sc[ct][e] = pv;
-        sum += pv;
+      for (int e = 0; e < 16; ++e) {
+        const int row = 32 * w + crow(e, hi), col = 32 * ct + lr;
+        sS[row * SS + col] = (col <= row && col < L) ? acc[e] * a.scale : -__builtin_huge_valf();
       }
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-      if (lr == 0 && row < L) a.lse[static_cast<int64_t>(bh) * LM + row] = m + __logf(sum);
-      const float inv = 1.f / sum;
-      const uint64_t ib = (static_cast<uint64_t>(bh) * LM + row) * LM;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        float pv = sc[ct][e] * inv;
-        if (a.thresh != 0u && pv != 0.f)
-          pv = akeep(ib + 32 * ct + lr, a.seed, a.thresh) ? pv * a.dscale : 0.f;
-        sc[ct][e] = pv;
-      }
-    }
-  }
-  __syncthreads();  // every wave is done reading Q / K: P goes over them
-  if (active) {
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      if (ct > w) break;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) sP[(32 * w + crow(e, hi)) * TS + 32 * ct + lr] = bfbits(sc[ct][e]);
     }
   }
   __syncthreads();
 
-  f32x16_t acc[2] = {zero16(), zero16()};
-  if (active) {
+  // row softmax, 2 threads per row; P_drop -> sP (bf16, zeros past the diagonal)
+  {
+    const int i = tid >> 1, half = tid & 1;
+    const int jmax = i + 1 < L ? i + 1 : L;  // valid keys [0, jmax)
+    float p[64];
+    float m = -__builtin_huge_valf();
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      const int j = half * 64 + t;
+      p[t] = j < jmax ? sS[i * SS + j] : -__builtin_huge_valf();
+      m = fmaxf(m, p[t]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      const int j = half * 64 + t;
+      p[t] = j < jmax ? __expf(p[t] - m) : 0.f;
+      sum += p[t];
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    if (i < L && half == 0) a.lse[static_cast<int64_t>(bh) * LM + i] = m + __logf(sum);
+    const float inv = 1.f / sum;
+    const uint64_t ib = (static_cast<uint64_t>(bh) * LM + i) * LM + half * 64;
+#pragma unroll
+    for (int t = 0; t < 64; t += 2) {
+      float v0 = p[t] * inv, v1 = p[t + 1] * inv;
+      if (a.thresh != 0u) {
+        v0 = akeep(ib + t, a.seed, a.thresh) ? v0 * a.dscale : 0.f;
+        v1 = akeep(ib + t + 1, a.seed, a.thresh) ? v1 * a.dscale : 0.f;
+      }
+      *reinterpret_cast<uint32_t*>(sP + i * TS + half * 64 + t) =
+          static_cast<uint32_t>(bfbits(v0)) | (static_cast<uint32_t>(bfbits(v1)) << 16);
+    }
+  }
+  __syncthreads();
+
+  if (32 * w < L) {
+    f32x16_t acc[2] = {zero16(), zero16()};
     for (int ks = 0; ks < 2 * w + 2; ++ks) {
       const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sP + (32 * w + lr) * TS + 16 * ks + 8 * hi);
 #pragma unroll
@@ -185,9 +182,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
         acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[ct], 0, 0, 0);
       }
     }
-  }
-  __syncthreads();  // P reads done: stage O over it
-  if (active) {
+    // sO aliases sS: every wave's softmax reads finished at the barrier above
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
@@ -402,10 +397,10 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
   }
 }
 
-constexpr size_t kFwdLds = (2 * LM * RS + HD * TS) * 2;
+constexpr size_t kFwdLds = (2 * LM * RS + HD * TS) * 2 + LM * SS * 4;
 constexpr size_t kBwdLds = 3 * HD * TS * 2 + 2 * LM * 4 + 3 * LM * TS * 2;
 static_assert(2 * LM * RS >= LM * TS, "P must fit over Q and K");
-static_assert(2 * LM * RS * 2 >= LM * OS * 4, "O staging must fit over Q and K");
+static_assert(LM * SS >= LM * OS, "O staging must fit over S");
 static_assert(3 * LM * TS >= 4 * LM * RS, "row tiles must fit in R2");
 static_assert(kBwdLds <= 160 * 1024, "backward LDS");
 
