@@ -20,6 +20,7 @@
 //   -- which saves four one-workgroup launches per top-k.  Histograms are
 //   privatised in LDS; only non-empty bins are flushed with atomics.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include "kernels.h"
 
@@ -27,7 +28,7 @@ namespace commeff {
 namespace {
 
 constexpr int kBins = 2048;
-constexpr int kNB = 1024;  // blocks for count/write passes (upper bound)
+constexpr int kNB = 4096;  // blocks for count/write passes (upper bound)
 
 struct WS {
   uint32_t* hist[3];  // kBins each (pass 2 uses 512)
@@ -197,16 +198,37 @@ count_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
   const int64_t i0 = blockIdx.x * span;
   const int64_t i1 = min(n, i0 + span);
   uint32_t gt = 0, eq = 0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += 4 * blockDim.x) {
-    float v[4];
+  auto add = [&](float v, bool in) __attribute__((always_inline)) {
+    const uint32_t k = key_of(v);
+    gt += in && k > thr;
+    eq += in && k == thr;
+  };
+  // 16-byte loads, 4 per thread in flight (4-byte loads left this pass
+  // latency-bound at ~2 TB/s on GPT-2-size vectors); span is a multiple of
+  // 1024, so every block's range starts 16-byte aligned
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  constexpr int kU = 4;
+  for (int64_t base = i0 + 4 * threadIdx.x; base < i1; base += 1024 * kU) {
+    float4 q[kU];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = i + u * blockDim.x < i1 ? x[i + u * blockDim.x] : 0.f;
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = base + 1024 * u;
+      if (al && i + 3 < i1) {
+        q[u] = *reinterpret_cast<const float4*>(x + i);
+      } else {
+        q[u].x = i < i1 ? x[i] : 0.f;
+        q[u].y = i + 1 < i1 ? x[i + 1] : 0.f;
+        q[u].z = i + 2 < i1 ? x[i + 2] : 0.f;
+        q[u].w = i + 3 < i1 ? x[i + 3] : 0.f;
+      }
+    }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t k = key_of(v[u]);
-      const bool in = i + u * blockDim.x < i1;
-      gt += in && k > thr;
-      eq += in && k == thr;
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = base + 1024 * u;
+      add(q[u].x, i < i1);
+      add(q[u].y, i + 1 < i1);
+      add(q[u].z, i + 2 < i1);
+      add(q[u].w, i + 3 < i1);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -272,46 +294,60 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
   const int64_t i0 = blockIdx.x * span;
   const int64_t i1 = min(n, i0 + span);
   const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  for (int64_t base = i0; base < i1; base += 1024) {
-    const int64_t i = base + 4 * threadIdx.x;
-    float v[4];
-    if (al && i + 3 < i1) {
-      const float4 q = *reinterpret_cast<const float4*>(x + i);
-      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-    } else {
+  // 4 steps of 1024 elements loaded at once (the steps are processed in
+  // order); a step without any element >= thr -- almost all of them for a
+  // k << n selection -- costs one block-wide OR instead of two scans
+  constexpr int kU = 4;
+  for (int64_t outer = i0; outer < i1; outer += 1024 * kU) {
+    float vv[kU][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = i + u < i1 ? x[i + u] : 0.f;
-    }
-    uint32_t gtm = 0, eqm = 0;  // bit u: element i+u is > thr / == thr
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = outer + 1024 * u + 4 * threadIdx.x;
+      if (al && i + 3 < i1) {
+        const float4 q = *reinterpret_cast<const float4*>(x + i);
+        vv[u][0] = q.x; vv[u][1] = q.y; vv[u][2] = q.z; vv[u][3] = q.w;
+      } else {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t k = key_of(v[u]);
-      const bool in = i + u < i1;
-      gtm |= (in && k > thr ? 1u : 0u) << u;
-      eqm |= (in && k == thr ? 1u : 0u) << u;
-    }
-    uint32_t eq_tot, sel_tot;
-    uint32_t er = eq_base + block_excl_scan(__popc(eqm), wt_eq, eq_tot);
-    uint32_t selm = gtm;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if ((eqm >> u) & 1u) {
-        if (er < ties) selm |= 1u << u;
-        ++er;
+        for (int t = 0; t < 4; ++t) vv[u][t] = i + t < i1 ? x[i + t] : 0.f;
       }
     }
-    uint32_t pos = sel_base + block_excl_scan(__popc(selm), wt_sel, sel_tot);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if ((selm >> u) & 1u) {
-        idx[pos] = i + u;
-        vals[pos] = v[u];
-        ++pos;
+    for (int u = 0; u < kU; ++u) {
+      const int64_t base = outer + 1024 * u;
+      if (base >= i1) break;  // block-uniform
+      const int64_t i = base + 4 * threadIdx.x;
+      uint32_t gtm = 0, eqm = 0;  // bit t: element i+t is > thr / == thr
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t k = key_of(vv[u][t]);
+        const bool in = i + t < i1;
+        gtm |= (in && k > thr ? 1u : 0u) << t;
+        eqm |= (in && k == thr ? 1u : 0u) << t;
       }
+      if (!__syncthreads_or(static_cast<int>(gtm | eqm))) continue;
+      uint32_t eq_tot, sel_tot;
+      uint32_t er = eq_base + block_excl_scan(__popc(eqm), wt_eq, eq_tot);
+      uint32_t selm = gtm;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if ((eqm >> t) & 1u) {
+          if (er < ties) selm |= 1u << t;
+          ++er;
+        }
+      }
+      uint32_t pos = sel_base + block_excl_scan(__popc(selm), wt_sel, sel_tot);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if ((selm >> t) & 1u) {
+          idx[pos] = i + t;
+          vals[pos] = vv[u][t];
+          ++pos;
+        }
+      }
+      sel_base += sel_tot;
+      eq_base += eq_tot;
+      __syncthreads();  // wt_eq / wt_sel reuse
     }
-    sel_base += sel_tot;
-    eq_base += eq_tot;
-    __syncthreads();  // wt_eq / wt_sel reuse
   }
 }
 
@@ -333,8 +369,12 @@ void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* 
   hipLaunchKernelGGL(hist_kernel<0>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
   hipLaunchKernelGGL(hist_kernel<1>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
   hipLaunchKernelGGL(hist_kernel<2>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
+  // compaction blocks: 1,024 (every block's prologue sums the counts of the
+  // blocks before it), up to kNB for very long vectors (>= 32 K elements a
+  // block: GPT-2 size 151 -> 128 us for the ordered write pass)
   int nb = static_cast<int>((n + 255) / 256);
-  if (nb > kNB) nb = kNB;
+  const int cap = static_cast<int>(std::min<int64_t>(kNB, std::max<int64_t>(1024, n / 32768)));
+  if (nb > cap) nb = cap;
   int64_t span = (n + nb - 1) / nb;
   span = ((span + 1023) / 1024) * 1024;  // write_kernel: 1024 elements per block step
   nb = static_cast<int>((n + span - 1) / span);
