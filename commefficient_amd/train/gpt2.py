@@ -105,9 +105,11 @@ def main(args):
         from transformers import AutoTokenizer
         tokenizer = AutoTokenizer.from_pretrained(args.model_checkpoint)
         tokenizer.add_special_tokens(ATTR_TO_SPECIAL_TOKEN)
-    tiny = args.do_test or args.gpt2_size == "tiny"
-    model = GPT2DoubleHeads(args.model_checkpoint if not args.do_test else "gpt2",
-                            **({"n_layer": 2, "n_embd": 64, "n_head": 2} if tiny else {}))
+    size = "tiny" if args.do_test else args.gpt2_size
+    dims = {"tiny": {"n_layer": 2, "n_embd": 64, "n_head": 2},
+            # smallest shape on the native junction + attention kernels
+            "mini": {"n_layer": 2, "n_embd": 256, "n_head": 4}}.get(size, {})
+    model = GPT2DoubleHeads(args.model_checkpoint if not args.do_test else "gpt2", **dims)
     if tokenizer is not None:
         model.model.resize_token_embeddings(len(tokenizer))
     args.len_tokenizer = model.model.config.vocab_size

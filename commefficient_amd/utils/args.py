@@ -208,8 +208,9 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="replay merged-client rounds from captured HIP graphs "
                         "(parallel/graph.py) once a round geometry repeats (auto/on: "
                         "eligible configurations; measured throughput-neutral for ResNet-9)")
-    g.add_argument("--gpt2_size", choices=["small", "tiny"], default="small",
-                   help="GPT-2 architecture: 'small' = 124M GPT-2 (reference), 'tiny' for tests")
+    g.add_argument("--gpt2_size", choices=["small", "mini", "tiny"], default="small",
+                   help="GPT-2 architecture: 'small' = 124M GPT-2 (reference); 'mini' (2 x 256, "
+                        "4 heads: native kernels) and 'tiny' (2 x 64) for tests")
     return p
 
 

@@ -97,3 +97,28 @@ def test_resume_reproduces_uninterrupted_run(stop, tmp_path, monkeypatch):
     torch.testing.assert_close(res.w, full.w, rtol=0, atol=0)
     torch.testing.assert_close(res.server.V, full.server.V, rtol=0, atol=0)
     torch.testing.assert_close(res.accountant.client_download, full.accountant.client_download)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [
+    ["--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
+     "--virtual_momentum", "0.9", "--num_rows", "5", "--num_cols", "20000", "--k", "2000"],
+    ["--mode", "local_topk", "--error_type", "local", "--local_momentum", "0.9",
+     "--virtual_momentum", "0", "--k", "2000"],
+    ["--mode", "uncompressed", "--error_type", "none", "--local_momentum", "0",
+     "--virtual_momentum", "0.9", "--microbatch_size", "2"],
+])
+def test_gpt2_driver_native_kernels_gpu(mode, tmp_path, monkeypatch):
+    """GPT-2 driver rounds on the GPU with the native transformer path
+    (junction kernels, fused attention, unpadded tokens, gradient sinks,
+    side-stream weight gradients) in a linear (merged) and two per-client
+    modes: finite weights that moved, finite losses."""
+    monkeypatch.chdir(tmp_path)
+    argv = ["--dataset_name", "PERSONA", "--model", "GPT2DoubleHeads", "--synthetic",
+            "--synthetic_size", "64", "--num_clients", "16", "--num_workers", "4",
+            "--local_batch_size", "2", "--valid_batch_size", "2", "--device", "cuda",
+            "--dtype", "bf16", "--gpt2_size", "mini", "--num_epochs", "1",
+            "--max_rounds", "3", "--num_results_train", "1", "--port", "29614"] + mode
+    fed = fed_train.main(argv)
+    assert fed.round_idx == 3
+    assert torch.isfinite(fed.w).all()
