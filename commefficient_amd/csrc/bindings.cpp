@@ -9,7 +9,9 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "cpu_ops.h"
 #include "kernels.h"
@@ -586,6 +588,9 @@ at::Tensor cs_hash_all_cpu(const at::Tensor& hashes, const at::Tensor& blk_off,
 
 // the exact (atomic-free) plan when its LDS segment fits, else the dense one
 bool any_plan_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* p) {
+  // COMMEFF_SKETCH_PLAN=dense forces the fixed-point dense plan (measurement)
+  const char* force = std::getenv("COMMEFF_SKETCH_PLAN");
+  if (force != nullptr && std::string(force) == "dense") return planned_geometry_dense(d, r, c, p);
   return planned_geometry(d, r, c, p) || planned_geometry_dense(d, r, c, p);
 }
 
@@ -1071,7 +1076,7 @@ void conv3x3_wgrad_grouped_hip(const at::Tensor& dy, const at::Tensor& x, int64_
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int P = static_cast<int>(N * H * W);
   const int Pg = P / static_cast<int>(G);
-  const int total = conv3x3_wgrad_splits(P, static_cast<int>(K), static_cast<int>(C));
+  const int total = conv3x3_wgrad_splits(P, static_cast<int>(H), static_cast<int>(W), static_cast<int>(K), static_cast<int>(C));
   int spg = static_cast<int>((total + G - 1) / G);
   const int steps_g = (Pg + 63) / 64;
   const int min_steps = 16;  // a split keeps >= 16 K-steps
@@ -1102,7 +1107,7 @@ void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits
               "conv3x3_wgrad: C % 64 and K % 128 must be 0");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int P = static_cast<int>(N * H * W);
-  if (splits <= 0) splits = conv3x3_wgrad_splits(P, static_cast<int>(K), static_cast<int>(C));
+  if (splits <= 0) splits = conv3x3_wgrad_splits(P, static_cast<int>(H), static_cast<int>(W), static_cast<int>(K), static_cast<int>(C));
   auto slab = at::empty({splits * K * 9 * C}, dw.options());
   ConvWgradArgs a;
   a.dy = bf16_ptr(dy);

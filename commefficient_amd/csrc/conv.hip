@@ -371,13 +371,19 @@ struct HaloCfg {
 // last-arriver combine needs device-scope release fences -- L2 writebacks
 // across the 8 XCDs, 140 us vs 62 unsplit; partial tiles through an HBM
 // workspace + a combine kernel: 44 + 12 us.)
-template <int TBM, bool POOL, bool SPLIT = false>
+// BN = 64: 64-wide outputs (ResNet-9 layer-1 dgrad, 128 -> 64 channels), wave
+// tiles of 64 x 32 (one MFMA column), B ring 2 x 8 KB.
+template <int TBM, int BN>
+constexpr int halo_lds() { return HaloCfg<TBM>::kWinBytes + 2 * BN * 128; }
+
+template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
 __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
+  static_assert(BN == 128 || (BN == 64 && !SPLIT && !POOL), "halo tile width");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
   // group g (split-K half) of this block: its own window + B ring
   const int half = SPLIT ? static_cast<int>(threadIdx.x) / (TBM * 2) : 0;
-  unsigned char* const smem = smem_base + half * HaloCfg<TBM>::kLds;
-  constexpr int BN = 128, NI = 2, NT = TBM * 2, BLD = BN * 8 / NT;
+  unsigned char* const smem = smem_base + half * halo_lds<TBM, BN>();
+  constexpr int NI = BN / 64, NT = TBM * 2, BLD = BN * 8 / NT;
   constexpr int kHaloWinBytes = HaloCfg<TBM>::kWinBytes, kHaloWinLd = HaloCfg<TBM>::kWinLd;
   const int tid = threadIdx.x & (NT - 1), lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
@@ -913,6 +919,176 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
     }
 }
 
+// Halo wgrad (16 | W, 64 % W == 0, H*W % 64 == 0: ResNet-9 layer 1 / res1 /
+// layer 2): one block per (128 out channels, kernel row r, 64 in channels)
+// computes the three taps (r, 0..2) at once -- a 128 x 192 tile, 4 waves of
+// 64 x 96.  The three taps of one kernel row read the same input rows shifted
+// by one column, so the B operand of a 64-pixel K-step is ONE padded window
+// (the step's R = 64 / W image rows at row offset r - 1, each with a zero
+// column either side: R * (W + 2) rows of 64 channels), and tap s reads it
+// shifted by s rows (16 | W: a 16-pixel MFMA sub-step never leaves an image
+// row, so its window rows are consecutive).  Per K-step the block stages
+// 16 KB of dy + <= 9.2 KB of window for 24 MFMAs per wave, where the
+// per-tap kernel stages 32 KB for 16 (the LDS-DMA issue count bounds those
+// loops).  Same transposed reads, swizzles and slab layout as
+// conv_wgrad_kernel; K-steps never straddle an image (H*W % 64 == 0).
+// Window pieces: rounds 0 and 1 (512 pieces, 64 rows) always, round 2 only
+// for waves whose pieces start inside the window (wave-uniform), so a stage
+// holds 72 window rows and every wave has >= ALD + 2 DMA loads per stage.
+constexpr int kHaloWRows = 72;  // window rows staged per K-step (>= R * (W + 2) > 64)
+template <int NSTAGE>
+__global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int A_BYTES = BK * WBM * 2;         // [64 px][128 k], 256-byte rows
+  constexpr int B_BYTES = kHaloWRows * 128;     // window [rows][64 c], 128-byte rows
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int ALD = 4, BLD = 3, NLD_MIN = ALD + 2;
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "stages");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int C = a.C, K = a.K, H = a.H, W = a.W, HW = H * W;
+  const int ntc = C >> 6;
+  const int ntiles = (K / WBM) * 3 * ntc;
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int tc = tile % ntc, r = (tile / ntc) % 3, tk = tile / (3 * ntc);
+  const int k0 = tk * WBM, c0 = tc * 64, dr = r - 1;
+  const int R = BK / W, PW = W + 2, NROW = R * PW;
+  int pbeg, pend;
+  wgrad_split_range(a, split, &pbeg, &pend);
+  const int nsteps = pend > pbeg ? (pend - pbeg) / BK : 0;  // whole K-steps (host-checked)
+  const uint64_t zero = reinterpret_cast<uint64_t>(g_conv_zero);
+
+  // A pieces: rows of dy (every K-step is full)
+  uint64_t a_ptr[ALD];
+#pragma unroll
+  for (int i = 0; i < ALD; ++i) {
+    const int sl = i * 256 + tid;
+    const int row = sl >> 4, lc = (sl & 15) ^ sw_tr256(row);
+    a_ptr[i] = reinterpret_cast<uint64_t>(a.dy + static_cast<size_t>(pbeg + row) * K + k0 + lc * 8);
+  }
+  // window pieces: window row -> (image row j of the step, column w); the
+  // source pixel is p0 + (j + dr) * W + w when 0 <= h0 + j + dr < H, 0 <= w < W
+  int b_rel[BLD], b_jj[BLD];
+  uint32_t b_ok = 0;
+#pragma unroll
+  for (int i = 0; i < BLD; ++i) {
+    const int sl = i * 256 + tid;
+    const int row = sl >> 3, lc = (sl & 7) ^ sw_tr128(row);
+    const int j = row / PW, w = row - j * PW - 1;
+    b_jj[i] = j + dr;
+    b_rel[i] = (j + dr) * W + w;
+    if (row < NROW && w >= 0 && w < W) b_ok |= 1u << i;
+    b_rel[i] = b_rel[i] * C + c0 + lc * 8;  // element offset from pixel p0's row start
+  }
+
+  auto issue = [&](int stage, int p0) __attribute__((always_inline)) {
+    unsigned char* base = smem + stage * STAGE + wid * 1024;
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) {
+      glds16(reinterpret_cast<const void*>(a_ptr[i]), base + i * 4096);
+      a_ptr[i] += static_cast<uint64_t>(BK) * K * 2;
+    }
+    const int h0 = (p0 % HW) / W;  // first image row of the step (uniform)
+    const uint16_t* xs = a.x + static_cast<size_t>(p0) * C;
+#pragma unroll
+    for (int i = 0; i < BLD; ++i) {
+      if (i < 2 || i * 256 + wid * 64 < NROW * 8) {
+        const bool ok = ((b_ok >> i) & 1u) && static_cast<unsigned>(h0 + b_jj[i]) < static_cast<unsigned>(H);
+        glds16(ok ? reinterpret_cast<const void*>(xs + b_rel[i]) : reinterpret_cast<const void*>(zero),
+               base + A_BYTES + i * 4096);
+      }
+    }
+  };
+
+  f32x16_t acc[2][3];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 3; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
+
+  if (nsteps > 0) issue(0, pbeg);
+  if (NSTAGE == 3 && nsteps > 1) issue(1, pbeg + BK);
+  int toA[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) tr_offsets<256>(wr * 64 + mi * 32, lane, toA[mi]);
+  // B: column n = wc*96 + ni*32 is tap s = n / 64, channels (n % 64)..+31;
+  // sub-step kk's pixels 16kk.. sit in image row j = 16kk / W from column
+  // w0 = 16kk % W, so tap s reads window rows j*PW + w0 + s + 0..15
+  int offB[4][3][2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int rowr = 8 * (g >> 1) + q, inb = (pp & 1) * 8;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int l0 = 16 * kk, j = l0 / W, w0 = l0 - j * W;
+#pragma unroll
+      for (int ni = 0; ni < 3; ++ni) {
+        const int n = wc * 96 + ni * 32, sft = n >> 6, cb = n & 63;
+        const int chk = (cb + 16 * (g & 1) + 4 * pp) >> 3;
+        const int base = j * PW + w0 + sft;
+        offB[kk][ni][0] = A_BYTES + tr_off<128>(base + rowr, chk) + inb;
+        offB[kk][ni][1] = A_BYTES + tr_off<128>(base + rowr + 4, chk) + inb;
+      }
+    }
+  }
+  int rd = 0, wrs = NSTAGE - 1;
+  for (int st = 0; st < nsteps; ++st) {
+    if constexpr (NSTAGE == 3) {
+      // the newest stage's loads may stay in flight (every wave has >= NLD_MIN)
+      if (st + 1 < nsteps) wait_vmcnt<NLD_MIN>(); else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + NSTAGE - 1 < nsteps) issue(wrs, pbeg + (st + NSTAGE - 1) * BK);
+    const unsigned char* sb = smem + rd * STAGE;
+    bf16x8_t af[2][2], bfr[2][3];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) af[0][mi] = tr_read(sb + toA[mi][0], sb + toA[mi][1]);
+#pragma unroll
+    for (int ni = 0; ni < 3; ++ni) bfr[0][ni] = tr_read(sb + offB[0][ni][0], sb + offB[0][ni][1]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int cur = kk & 1, nxt = cur ^ 1;
+      if (kk + 1 < 4) {
+        const int da = (kk + 1) * 16 * 256;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+          af[nxt][mi] = tr_read(sb + toA[mi][0] + da, sb + toA[mi][1] + da);
+#pragma unroll
+        for (int ni = 0; ni < 3; ++ni)
+          bfr[nxt][ni] = tr_read(sb + offB[kk + 1][ni][0], sb + offB[kk + 1][ni][1]);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 3; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
+    }
+    rd = rd + 1 == NSTAGE ? 0 : rd + 1;
+    wrs = wrs + 1 == NSTAGE ? 0 : wrs + 1;
+  }
+
+  float* slab = a.slab + static_cast<size_t>(split) * K * 9 * C;
+  const int hi = lane >> 5, lr = lane & 31;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 3; ++ni) {
+      const int n = wc * 96 + ni * 32 + lr;
+      const int tap = 3 * r + (n >> 6), c = c0 + (n & 63);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int k = k0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        slab[(static_cast<size_t>(k) * 9 + tap) * C + c] = acc[mi][ni][e];
+      }
+    }
+}
+
 // dw[k][c][r][s] (fp32, PyTorch layout) = beta*dw + sum_split slab[split][k][rs][c]
 // One block per (k, 64 channels).  Thread (c, part) sums the 9 taps of its
 // channel over splits part, part+4, ... (9 independent loads per split, read
@@ -1042,6 +1218,17 @@ bool wgrad_wide(int K, int C) {
   return !off && K % 256 == 0 && (C == 128 || C % 256 == 0);
 }
 
+// the halo wgrad kernel (three taps of a kernel row per block): 16 | W,
+// 64 % W == 0 and whole K-steps per image (COMMEFF_WGRAD_HALO=0: off)
+bool wgrad_halo(int H, int W, int K, int C) {
+  static const bool off = [] {
+    const char* e = getenv("COMMEFF_WGRAD_HALO");
+    return e != nullptr && e[0] == '0';
+  }();
+  return !off && W % 16 == 0 && BK % W == 0 && (H * W) % BK == 0 && K % WBM == 0 && C % 64 == 0 &&
+         (BK / W) * (W + 2) <= kHaloWRows;
+}
+
 // (k, c) x tap-group tiles of one wgrad: 64-channel inputs pair taps (PAIR)
 int wgrad_tiles(int K, int C) {
   if (wgrad_wide(K, C)) return (K / 256) * (C == 128 ? 5 : 9 * (C / 256));
@@ -1095,8 +1282,8 @@ bool conv3x3_pool_supported(int H, int W, int K) {
 // the padded window exceeds 288 rows)
 static int wgrad_slots();
 
-bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g) {
-  if (K % 128 != 0 || W <= 0 || TBM % W != 0) return false;
+bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g, int BN = 128) {
+  if (K % BN != 0 || W <= 0 || TBM % W != 0) return false;
   const int R = TBM / W;
   if (R <= H) {
     if (H % R != 0) return false;
@@ -1121,16 +1308,16 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g) {
   return g->NPW <= (TBM == 256 ? HaloCfg<256>::kMaxRows : cap);
 }
 
-template <int TBM, bool POOL, bool SPLIT = false>
+template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
 void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
-  constexpr int lds = HaloCfg<TBM>::kLds * (SPLIT ? 2 : 1);
+  constexpr int lds = halo_lds<TBM, BN>() * (SPLIT ? 2 : 1);
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), lds);
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL, SPLIT>), dim3(mt * (a.K / 128)),
+  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), dim3(mt * (a.K / BN)),
                      dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
 }
 
@@ -1163,6 +1350,19 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
       return;
     }
     if (a.pool == 2) launch_fwd_halo<128, true>(a, hg, stream); else launch_fwd_halo<128, false>(a, hg, stream);
+    return;
+  }
+  // 64-wide outputs of big layers (ResNet-9 layer-1 dgrad): the halo window
+  // replaces 9 staged 256 x 64 A tiles per channel block (the per-tap kernel
+  // streams ~3x the L2 bytes per MFMA)
+  static const bool halo64_on = [] {  // COMMEFF_CONV_HALO64=0: per-tap kernel
+    const char* e = getenv("COMMEFF_CONV_HALO64");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  if (halo_on && halo64_on && a.pool == 0 && a.K % 128 != 0 &&
+      halo_geom(a.H, a.W, a.K, 256, &hg, 64) &&
+      static_cast<int64_t>((a.P + 255) / 256) * (a.K / 64) >= 512) {
+    launch_fwd_halo<256, false, false, 64>(a, hg, stream);
     return;
   }
   if (a.pool == 2) {  // caller checked conv3x3_pool_supported
@@ -1244,9 +1444,15 @@ void launch_wgrad_wide(const ConvWgradArgs& a, hipStream_t stream) {
   }
 }
 
-int conv3x3_wgrad_splits(int P, int K, int C) {
-  const int tiles = wgrad_tiles(K, C);
+int conv3x3_wgrad_splits(int P, int H, int W, int K, int C) {
   const int steps = (P + BK - 1) / BK;
+  if (wgrad_halo(H, W, K, C)) {  // 2 blocks per CU (56 KB LDS), >= 16 K-steps each
+    const int tiles = (K / WBM) * 3 * (C / 64);
+    int s = wgrad_slots() / tiles;
+    if (s > steps / 16) s = steps / 16;
+    return s < 1 ? 1 : s;
+  }
+  const int tiles = wgrad_tiles(K, C);
   if (wgrad_wide(K, C)) {  // one 128 KB block per CU, >= 16 K-steps each
     int s = wgrad_slots() / 2 / tiles;
     if (s > steps / 16) s = steps / 16;
@@ -1280,7 +1486,26 @@ void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_
   }();
   const bool rowstep = BK % a.W == 0;
   const bool wide = a.C % 128 == 0;
-  if (wgrad_wide(a.K, a.C)) {
+  if (wgrad_halo(a.H, a.W, a.K, a.C) && (a.group_px == 0 || a.group_px % BK == 0)) {
+    // ring depth (COMMEFF_WGRAD_HALO_STAGES = 2 | 3; 3 x 25 KB still fits 2 blocks/CU,
+    // measured equal to 2 in the ResNet-9 round)
+    static const int stages = [] {
+      const char* e = getenv("COMMEFF_WGRAD_HALO_STAGES");
+      return e != nullptr && e[0] == '3' ? 3 : 2;
+    }();
+    const int tiles = (a.K / WBM) * 3 * (a.C / 64);
+    constexpr int stage_bytes = BK * WBM * 2 + kHaloWRows * 128;
+    static bool init = false;
+    if (!init) {
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2>), 2 * stage_bytes);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<3>), 3 * stage_bytes);
+      init = true;
+    }
+    if (stages == 3)
+      hipLaunchKernelGGL(conv_wgrad_halo_kernel<3>, dim3(tiles * a.splits), dim3(256), 3 * stage_bytes, stream, a);
+    else
+      hipLaunchKernelGGL(conv_wgrad_halo_kernel<2>, dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
+  } else if (wgrad_wide(a.K, a.C)) {
     if (rowstep) launch_wgrad_wide<true>(a, stream); else launch_wgrad_wide<false>(a, stream);
   } else if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)
     if (rowstep) launch_wgrad<128, 2, true, true>(a, stream); else launch_wgrad<128, 2, false, true>(a, stream);

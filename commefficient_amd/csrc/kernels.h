@@ -197,7 +197,7 @@ struct ConvWgradArgs {
 bool conv3x3_supported(int C, int K);
 bool conv3x3_pool_supported(int H, int W, int K);
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
-int conv3x3_wgrad_splits(int P, int K, int C);
+int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
 // per-group dw_g [K][C][3][3] (+)= the wgrad of group g's pixels, dw_g at

@@ -81,6 +81,25 @@ def test_fwd_split_k_halo(N, C, H, W, K, pool):
     _close(y, torch.where(mask.float() > 0, ref, torch.zeros_like(ref)) + add.float())
 
 
+@pytest.mark.parametrize("N,C,H,K", [(132, 128, 32, 64), (520, 256, 16, 64)])
+def test_fwd_halo_64_wide_matches_fp32(N, C, H, K):
+    """64-wide outputs of big layers (ResNet-9 layer-1 dgrad: 128 -> 64
+    channels at 32x32) run the halo-window kernel with 64 x 32 wave tiles
+    (conv.hip BN = 64): plain, ReLU and mask + addend epilogues."""
+    x, w = _inputs(N, C, H, H, K)
+    wf, _ = ops.conv_weight_prep(w)
+    ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
+    _close(ops.conv3x3_fwd(x, wf, False), ref)
+    y = ops.conv3x3_fwd(x, wf, True)
+    _close(y, ref.relu())
+    assert torch.equal(y, ops.conv3x3_fwd(x, wf, True))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    mask = _nhwc(torch.randn(N, K, H, H, device="cuda", generator=g).to(torch.bfloat16))
+    add = _nhwc(torch.randn(N, K, H, H, device="cuda", generator=g).to(torch.bfloat16))
+    y = ops.conv3x3_fwd(x, wf, False, mask, add)
+    _close(y, torch.where(mask.float() > 0, ref, torch.zeros_like(ref)) + add.float())
+
+
 @pytest.mark.parametrize("N,C,H,W,K", SHAPES[:3])
 def test_fwd_mask_and_addend_epilogue(N, C, H, W, K):
     x, w = _inputs(N, C, H, W, K)
