@@ -1097,11 +1097,14 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
 // run of 576 floats.
 // Grouped (blockIdx.y = group g): sums the group's own splits [g*splits,
 // (g+1)*splits) into dw + g * gstride.
-__global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                                 float* __restrict__ dw, int K, int C,
-                                                                 int splits, float beta,
-                                                                 int64_t gstride) {
-  __shared__ float t[4][64 * 9];
+// PARTS = 4 (256 threads) or 16 (1024 threads, many splits: the grid has only
+// K * C / 64 blocks -- 128 for ResNet-9 layer 1 -- so more loads in flight per block)
+template <int PARTS>
+__global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                                       float* __restrict__ dw, int K, int C,
+                                                                       int splits, float beta,
+                                                                       int64_t gstride) {
+  __shared__ float t[PARTS][64 * 9];
   const int ncb = C >> 6;
   const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
   slab += static_cast<size_t>(blockIdx.y) * splits * K * 9 * C;
@@ -1113,7 +1116,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __r
 #pragma unroll
   for (int rs = 0; rs < 9; ++rs) acc[rs] = 0.f;
 #pragma unroll 2
-  for (int sp = part; sp < splits; sp += 4) {
+  for (int sp = part; sp < splits; sp += PARTS) {
     const float* p = src + sp * sstride;
 #pragma unroll
     for (int rs = 0; rs < 9; ++rs) acc[rs] += p[rs * C];
@@ -1122,10 +1125,23 @@ __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __r
   for (int rs = 0; rs < 9; ++rs) t[part][cc * 9 + rs] = acc[rs];
   __syncthreads();
   float* o = dw + (static_cast<size_t>(k) * C + c0) * 9;
-  for (int e = threadIdx.x; e < 576; e += 256) {
-    const float v = ((t[0][e] + t[1][e]) + t[2][e]) + t[3][e];
+  for (int e = threadIdx.x; e < 576; e += 64 * PARTS) {
+    float v = t[0][e];
+#pragma unroll
+    for (int q = 1; q < PARTS; ++q) v += t[q][e];  // fixed order: deterministic
     o[e] = beta != 0.f ? beta * o[e] + v : v;
   }
+}
+
+void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
+                         int64_t gstride, int groups, hipStream_t stream) {
+  const dim3 grid(K * (C / 64), groups);
+  if (splits >= 32)
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
+                       beta, gstride);
+  else
+    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
+                       beta, gstride);
 }
 
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16
@@ -1471,8 +1487,7 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
   const int steps = (a.P + BK - 1) / BK;
   a.group_px = 0;
   launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(a.K * (a.C / 64)), dim3(256), 0, stream,
-                     a.slab, dw, a.K, a.C, a.splits, beta, int64_t{0});
+  launch_wgrad_reduce(a.slab, dw, a.K, a.C, a.splits, beta, int64_t{0}, 1, stream);
 }
 
 // the wgrad GEMM kernels (slabs only) with a given split length
@@ -1526,8 +1541,7 @@ void launch_conv3x3_wgrad_grouped(ConvWgradArgs a, int G, float* dw, int64_t gst
   a.splits_per_group = a.splits / G;
   const int steps = (a.group_px + BK - 1) / BK;
   launch_conv3x3_wgrad_steps(a, (steps + a.splits_per_group - 1) / a.splits_per_group, stream);
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(a.K * (a.C / 64), G), dim3(256), 0, stream,
-                     a.slab, dw, a.K, a.C, a.splits_per_group, beta, gstride);
+  launch_wgrad_reduce(a.slab, dw, a.K, a.C, a.splits_per_group, beta, gstride, G, stream);
 }
 
 void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream) {

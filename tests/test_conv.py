@@ -128,7 +128,7 @@ def test_dgrad_matches_fp32(N, C, H, W, K):
 
 
 @pytest.mark.parametrize("N,C,H,W,K", [s for s in SHAPES if s[4] % 128 == 0])
-@pytest.mark.parametrize("splits", [0, 1, 3])
+@pytest.mark.parametrize("splits", [0, 1, 3, 40])
 def test_wgrad_matches_fp32(N, C, H, W, K, splits):
     x, _ = _inputs(N, C, H, W, K)
     g = torch.Generator(device="cuda").manual_seed(3)
