@@ -783,6 +783,47 @@ at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
   return conv3x3_fwd_impl(x, w, relu, mask, addend, nullptr);
 }
 
+// dgrad with the relu + 2x2 max-pool backward of the layer below fused into
+// the epilogue: y [N, K, 2H, 2W] (channels_last) = unpool(conv3x3(x, w) +
+// addend) with idx [N, K, H, W] the pool's window codes (conv3x3_fwd_pool2)
+at::Tensor conv3x3_fwd_unpool_hip(const at::Tensor& x, const at::Tensor& w,
+                                  const c10::optional<at::Tensor>& addend, const at::Tensor& idx) {
+  check_nhwc_bf16(x, "conv3x3_unpool: x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 &&
+                  w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C,
+              "conv3x3_unpool: w must be contiguous bf16 [K, 3, 3, C]");
+  const int64_t K = w.size(0);
+  TORCH_CHECK(conv3x3_supported(static_cast<int>(C), static_cast<int>(K)),
+              "conv3x3_unpool: C and K must be multiples of 64");
+  TORCH_CHECK(N * 4 * H * W < (1ll << 31), "conv3x3_unpool: size");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.dim() == 4 && idx.size(0) == N &&
+                  idx.size(1) == K && idx.size(2) == H && idx.size(3) == W && idx.device() == x.device() &&
+                  idx.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_unpool: idx must be uint8 channels_last [N, K, H, W]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, K, 2 * H, 2 * W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto pooled = at::empty({N, K, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  ConvFwdArgs a{};
+  a.x = bf16_ptr(x);
+  a.w = bf16_ptr(w);
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.mask = nullptr;
+  a.addend = opt_like(addend, pooled, "conv3x3_unpool: addend");
+  a.y_pre = nullptr;
+  a.pool_idx = nullptr;
+  a.unpool_idx = idx.data_ptr<uint8_t>();
+  a.P = static_cast<int>(N * H * W);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.relu = 0;
+  a.pool = 0;
+  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  return y;
+}
+
 // y = maxpool2(relu(conv3x3(x, w))) [N, K, H/2, W/2] (channels_last) and the
 // 1-byte window codes of csrc/pool.hip (for relu_maxpool_backward)
 std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_pool2_hip(const at::Tensor& x, const at::Tensor& w) {
@@ -1529,6 +1570,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("relu_maxpool(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
+  m.def("conv3x3_fwd_unpool(Tensor x, Tensor w, Tensor? addend, Tensor idx) -> Tensor");
   m.def("conv3x3_fwd_pool2(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def("head_fwd(Tensor x, Tensor w, Tensor targets, float scale) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("head_bwd(Tensor gl, Tensor gunit, Tensor w, Tensor pooled, Tensor codes, int H, int W, float scale, "
@@ -1629,6 +1671,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("relu_maxpool", &relu_maxpool_hip);
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("conv3x3_fwd", &conv3x3_fwd_hip);
+  m.impl("conv3x3_fwd_unpool", &conv3x3_fwd_unpool_hip);
   m.impl("conv3x3_fwd_pool2", &conv3x3_fwd_pool2_hip);
   m.impl("head_fwd", &head_fwd_hip);
   m.impl("head_bwd", &head_bwd_hip);

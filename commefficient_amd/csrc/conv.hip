@@ -174,7 +174,7 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x16_t
       }
     }
     if (a.addend != nullptr) {
-      if (a.y_pre != nullptr) {  // the activation before the residual add
+      if (a.y_pre != nullptr && a.unpool_idx == nullptr) {  // the activation before the residual add
         v4u pre;
         pre[0] = pack_bf16(v[0], v[1]);
         pre[1] = pack_bf16(v[2], v[3]);
@@ -191,6 +191,30 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x16_t
     out[1] = pack_bf16(v[2], v[3]);
     out[2] = pack_bf16(v[4], v[5]);
     out[3] = pack_bf16(v[6], v[7]);
+    if (a.unpool_idx != nullptr) {
+      // relu + max-pool backward: the value goes to its window position t
+      // (code byte per channel, 255 = relu-dead), zeros to the other three
+      const uint64_t codes = *reinterpret_cast<const uint64_t*>(a.unpool_idx + o);
+      const uint32_t q = fdiv(static_cast<uint32_t>(p), a.div_w);
+      const int ow = p - static_cast<int>(q) * a.W;
+      const uint32_t n = fdiv(q, a.div_h);
+      const int oh = static_cast<int>(q - n * static_cast<uint32_t>(a.H));
+      const int FW = 2 * a.W;
+      const size_t f0 = (static_cast<size_t>(n * 2 * a.H + 2 * oh) * FW + 2 * ow) * a.K + n0 + cc * 8;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v4u ot;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t c0 = static_cast<uint32_t>(codes >> (16 * h)) & 0xffu;
+          const uint32_t c1 = static_cast<uint32_t>(codes >> (16 * h + 8)) & 0xffu;
+          ot[h] = (c0 == static_cast<uint32_t>(t) ? (out[h] & 0xffffu) : 0u) |
+                  (c1 == static_cast<uint32_t>(t) ? (out[h] & 0xffff0000u) : 0u);
+        }
+        *reinterpret_cast<v4u*>(a.y + f0 + static_cast<size_t>((t >> 1) * FW + (t & 1)) * a.K) = ot;
+      }
+      continue;
+    }
     *reinterpret_cast<v4u*>(a.y + o) = out;
   }
   }  // pass

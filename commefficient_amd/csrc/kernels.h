@@ -179,6 +179,11 @@ struct ConvFwdArgs {
   int relu;
   int pool;                // 0, or 2: fused relu + 2x2 max-pool epilogue (128 % (2W) == 0)
   FastDivU32 div_w, div_h;  // set by the launcher
+  // optional [P, K] 2x2 max-pool window codes (csrc/pool.hip) of the layer whose
+  // pooled output is this conv's OUTPUT grid: y is then the [N, 2H, 2W, K]
+  // un-pooled tensor, each value routed to its code's window position (zeros
+  // elsewhere) -- the relu + max-pool backward fused into the dgrad epilogue
+  const uint8_t* unpool_idx = nullptr;
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]

@@ -113,6 +113,62 @@ def _pool_fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return weight.shape[0] % 128 == 0 and H % 2 == 0 and W % 2 == 0 and 128 % (2 * W) == 0
 
 
+class _UnpoolLink:
+    """Hand-off between a fused conv + relu + 2x2 max-pool unit and the native
+    unit that consumes its pooled output (ResNet-9: layer1 -> res1, layer2 ->
+    layer3, layer3 -> res3).  The consumer's backward computes its input
+    gradient with the pool backward fused into the dgrad epilogue
+    (``conv3x3_fwd_unpool``: the full-resolution gradient, each value at its
+    window's argmax) and parks it here; autograd gets a zero-stride zero
+    tensor of the pooled shape instead, and the producer's backward takes the
+    parked gradient (adding the unfused expansion of anything else autograd
+    accumulated into its output gradient) -- one kernel and one pooled-size
+    round trip fewer per pooled layer."""
+
+    __slots__ = ("idx", "grad", "dummy", "claimed")
+
+    def __init__(self, idx):
+        self.idx = idx
+        self.grad = None
+        self.dummy = None
+        self.claimed = False  # one consumer only (a second one uses the unfused path)
+
+    def park(self, full, like):
+        self.grad = full
+        self.dummy = torch.zeros((1, 1, 1, 1), dtype=like.dtype, device=like.device).expand(like.shape)
+        return self.dummy
+
+    def take(self, gout):
+        """The producer's full-resolution gradient (None: nothing parked)."""
+        full, dummy = self.grad, self.dummy
+        self.grad = self.dummy = None
+        if full is None:
+            return None
+        if gout is dummy or (gout.data_ptr() == dummy.data_ptr() and gout.stride() == dummy.stride()):
+            return full
+        # autograd added other consumers' gradients to the dummy's zeros
+        g = gout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        return full + _ops().relu_maxpool_backward(g, self.idx, 2)
+
+
+_UNPOOL_ON = [True]
+
+
+def set_fused_unpool(on: bool) -> None:
+    """Fuse the relu + max-pool backward into the consumer's dgrad epilogue
+    (default on; off = the separate csrc/pool.hip backward kernel)."""
+    _UNPOOL_ON[0] = bool(on)
+
+
+def _link_of(x: torch.Tensor):
+    link = getattr(x, "_commeff_unpool", None)
+    if not (_UNPOOL_ON[0] and link is not None and not link.claimed and link.idx.shape == x.shape
+            and torch.is_grad_enabled() and x.requires_grad):
+        return None
+    link.claimed = True
+    return link
+
+
 class _Conv3x3Act(torch.autograd.Function):
     """relu(conv3x3(x, w)) or maxpool_k(relu(conv3x3(x, w))), no bias.
 
@@ -123,14 +179,19 @@ class _Conv3x3Act(torch.autograd.Function):
     split-K reduction straight into the fp32 [K, C, 3, 3] gradient.
     """
 
+    last_out_link = None  # forward -> conv3x3_relu_pool side channel (no autograd state)
+
     @staticmethod
-    def forward(ctx, x, weight, pool_k):
+    def forward(ctx, x, weight, pool_k, in_link=None):
         wf, wt = _prep(weight)
+        ctx.in_link = in_link
+        ctx.out_link = None
         if pool_k == 2 and _pool_fusable(x, weight):
             # relu + 2x2 max-pool in the conv epilogue: the full-resolution
             # activation is never written
             out, idx = _ops().conv3x3_fwd_pool2(x, wf)
             ctx.save_for_backward(x, wt, idx)
+            ctx.out_link = _UnpoolLink(idx)
         elif pool_k:
             y = _ops().conv3x3_fwd(x, wf, False)
             out, idx = _ops().relu_maxpool(y, pool_k)
@@ -141,19 +202,28 @@ class _Conv3x3Act(torch.autograd.Function):
             ctx.save_for_backward(x, wt, out)
         ctx.pool_k = pool_k
         ctx.weight = weight
+        _Conv3x3Act.last_out_link = ctx.out_link
         return out
 
     @staticmethod
     def backward(ctx, gout):
         x, wt, aux = ctx.saved_tensors
-        gout = gout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        if ctx.pool_k:
-            g = _ops().relu_maxpool_backward(gout, aux, ctx.pool_k)
-        else:
-            g = _ops().relu_mask(gout, aux)
-        gx = _ops().conv3x3_fwd(g, wt, False) if ctx.needs_input_grad[0] else None
+        g = ctx.out_link.take(gout) if ctx.out_link is not None else None
+        if g is None:
+            gout = gout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            if ctx.pool_k:
+                g = _ops().relu_maxpool_backward(gout, aux, ctx.pool_k)
+            else:
+                g = _ops().relu_mask(gout, aux)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            link = ctx.in_link
+            if link is not None:  # the input's relu + max-pool backward in the epilogue
+                gx = link.park(_ops().conv3x3_fwd_unpool(g, wt, None, link.idx), x)
+            else:
+                gx = _ops().conv3x3_fwd(g, wt, False)
         gw = _wgrad_to(g, x, ctx.weight) if ctx.needs_input_grad[1] else None
-        return gx, gw, None
+        return gx, gw, None, None
 
 
 class _ResidualUnit(torch.autograd.Function):
@@ -169,13 +239,14 @@ class _ResidualUnit(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, w1, w2):
+    def forward(ctx, x, w1, w2, in_link=None):
         w1f, w1t = _prep(w1)
         w2f, w2t = _prep(w2)
         y1 = _ops().conv3x3_fwd(x, w1f, True)
         out, y2 = _ops().conv3x3_relu_add(y1, w2f, x)
         ctx.save_for_backward(x, y1, y2, w1t, w2t)
         ctx.w1, ctx.w2 = w1, w2
+        ctx.in_link = in_link
         return out
 
     @staticmethod
@@ -185,15 +256,21 @@ class _ResidualUnit(torch.autograd.Function):
         g2 = _ops().relu_mask(g, y2)
         g1 = _ops().conv3x3_fwd(g2, w2t, False, y1)  # masked by relu(conv1) > 0
         dw2 = _wgrad_to(g2, y1, ctx.w2) if ctx.needs_input_grad[2] else None
-        gx = _ops().conv3x3_fwd(g1, w1t, False, None, g) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            link = ctx.in_link
+            if link is not None:  # + the input's relu + max-pool backward in the epilogue
+                gx = link.park(_ops().conv3x3_fwd_unpool(g1, w1t, g, link.idx), x)
+            else:
+                gx = _ops().conv3x3_fwd(g1, w1t, False, None, g)
         dw1 = _wgrad_to(g1, x, ctx.w1) if ctx.needs_input_grad[1] else None
-        return gx, dw1, dw2
+        return gx, dw1, dw2, None
 
 
 def residual_unit(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
     """``x + relu(conv2(relu(conv1(x))))`` (3x3, pad 1, no bias)."""
     if conv3x3_native_ok(x, w1) and conv3x3_native_ok(x, w2) and w1.shape[0] == x.shape[1]:
-        return _ResidualUnit.apply(x, w1, w2)
+        return _ResidualUnit.apply(x, w1, w2, _link_of(x))
     y = F.relu(F.conv2d(x, w1, padding=1))
     return x + F.relu(F.conv2d(y, w2, padding=1))
 
@@ -212,7 +289,11 @@ def conv3x3_relu_pool(x: torch.Tensor, weight: torch.Tensor, pool_k: int = 0) ->
     else the PyTorch (MIOpen) composition."""
     if conv3x3_native_ok(x, weight) and (
             pool_k == 0 or (x.shape[2] % pool_k == 0 and x.shape[3] % pool_k == 0)):
-        return _Conv3x3Act.apply(x, weight, int(pool_k))
+        out = _Conv3x3Act.apply(x, weight, int(pool_k), _link_of(x))
+        link = _Conv3x3Act.last_out_link
+        if link is not None:
+            out._commeff_unpool = link
+        return out
     y = F.conv2d(x, weight, padding=1)
     return relu_maxpool(y, pool_k) if pool_k else F.relu(y)
 

@@ -559,3 +559,39 @@ def test_conv1x1_passthrough_sums_identity_grad():
     ((yr * gy.to(torch.bfloat16).float()).sum() + (xr * gi.to(torch.bfloat16).float()).sum()).backward()
     _close(y, yr)
     _close(x.grad, xr.grad)
+
+
+@pytest.mark.parametrize("chain", ["pool_res", "pool_pool", "two_consumers"])
+def test_fused_unpool_backward_bitwise(chain):
+    """The relu + 2x2 max-pool backward fused into the consumer's dgrad
+    epilogue (ops/nn.py _UnpoolLink, conv3x3_fwd_unpool) gives bitwise the
+    gradients of the separate pool-backward kernel (same bf16 values routed
+    to the same window positions), also when the pooled output has two
+    consumers (the second one takes the unfused path)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x0 = _nhwc(torch.randn(6, 64, 16, 16, device="cuda", generator=g).to(torch.bfloat16))
+    w1 = torch.randn(128, 64, 3, 3, device="cuda", generator=g) * 0.06
+    w2 = torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.04
+    w3 = torch.randn(128, 128, 3, 3, device="cuda", generator=g) * 0.04
+
+    def run(fused):
+        cnn.set_fused_unpool(fused)
+        try:
+            x = x0.clone().requires_grad_(True)
+            ws = [w.clone().requires_grad_(True) for w in (w1, w2, w3)]
+            y = cnn.conv3x3_relu_pool(x, ws[0], 2)
+            if chain == "pool_res":
+                out = cnn.residual_unit(y, ws[1], ws[2])
+            elif chain == "pool_pool":
+                out = cnn.conv3x3_relu_pool(y, ws[1], 2) * 1.0 + ws[2].sum() * 0
+            else:
+                out = cnn.residual_unit(y, ws[1], ws[2]) + cnn.conv3x3_relu_pool(y, ws[1], 0)
+            gy = torch.randn(out.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(6))
+            out.float().backward(gy.to(out.dtype).float())
+            return [x.grad] + [w.grad for w in ws]
+        finally:
+            cnn.set_fused_unpool(True)
+
+    a, b = run(True), run(False)
+    for ga, gb in zip(a, b):
+        assert torch.equal(ga, gb)
