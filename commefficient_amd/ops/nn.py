@@ -135,7 +135,11 @@ class _UnpoolLink:
 
     def park(self, full, like):
         self.grad = full
-        self.dummy = torch.zeros((1, 1, 1, 1), dtype=like.dtype, device=like.device).expand(like.shape)
+        key = (like.dtype, like.device)
+        z = _ZERO.get(key)
+        if z is None:  # one cached zero per dtype/device: no fill kernel per backward
+            z = _ZERO[key] = torch.zeros((1, 1, 1, 1), dtype=like.dtype, device=like.device)
+        self.dummy = z.expand(like.shape)
         return self.dummy
 
     def take(self, gout):
@@ -152,6 +156,7 @@ class _UnpoolLink:
 
 
 _UNPOOL_ON = [True]
+_ZERO: dict = {}
 
 
 def set_fused_unpool(on: bool) -> None:
