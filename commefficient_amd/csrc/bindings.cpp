@@ -1192,6 +1192,43 @@ std::vector<at::Tensor> conv_weight_prep_multi_hip(at::TensorList ws) {
   return out;
 }
 
+// images = [wf0, wt0, wf1, wt1, ...] of ``weights`` (views into w_flat)
+void conv_images_patch_hip(const at::Tensor& w_flat, const at::Tensor& idx, at::TensorList weights,
+                           at::TensorList images) {
+  check_f32(w_flat, "conv_images_patch: w_flat");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous() &&
+                  idx.device() == w_flat.device(), "conv_images_patch: idx must be int64 [k]");
+  TORCH_CHECK(images.size() == 2 * weights.size() && weights.size() <= static_cast<size_t>(kPrepMax),
+              "conv_images_patch: 2 images per weight, <= ", kPrepMax, " weights");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w_flat.device());
+  ConvPatchBatch b{};
+  b.w_flat = w_flat.data_ptr<float>();
+  b.n = 0;
+  const int64_t d = w_flat.numel();
+  for (size_t j = 0; j < weights.size(); ++j) {
+    const auto& w = weights[j];
+    TORCH_CHECK(w.scalar_type() == at::kFloat && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
+                    w.is_contiguous(), "conv_images_patch: weights must be contiguous f32 [K, C, 3, 3]");
+    const int64_t off = (reinterpret_cast<const char*>(w.data_ptr()) -
+                         reinterpret_cast<const char*>(w_flat.data_ptr())) / 4;
+    TORCH_CHECK(off >= 0 && off + w.numel() <= d, "conv_images_patch: weight is not a view of w_flat");
+    const int64_t K = w.size(0), C = w.size(1);
+    const auto& wf = images[2 * j];
+    const auto& wt = images[2 * j + 1];
+    TORCH_CHECK(wf.scalar_type() == at::kBFloat16 && wt.scalar_type() == at::kBFloat16 &&
+                    wf.is_contiguous() && wt.is_contiguous() && wf.numel() == w.numel() &&
+                    wt.numel() == w.numel(), "conv_images_patch: images must be contiguous bf16");
+    b.off[b.n] = off;
+    b.numel[b.n] = w.numel();
+    b.wf[b.n] = reinterpret_cast<uint16_t*>(wf.data_ptr());
+    b.wt[b.n] = reinterpret_cast<uint16_t*>(wt.data_ptr());
+    b.K[b.n] = static_cast<int>(K);
+    b.C[b.n] = static_cast<int>(C);
+    ++b.n;
+  }
+  launch_conv_images_patch(b, idx.data_ptr<int64_t>(), idx.numel(), cur_stream());
+}
+
 std::tuple<at::Tensor, at::Tensor> conv_weight_prep_hip(const at::Tensor& w) {
   auto r = conv_weight_prep_multi_hip({w});
   return {r[0], r[1]};
@@ -1589,6 +1626,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("conv3x3_wgrad_grouped(Tensor dy, Tensor x, int G, Tensor(a!) dw) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("conv_weight_prep_multi(Tensor[] ws) -> Tensor[]");
+  m.def("conv_images_patch(Tensor w_flat, Tensor idx, Tensor[] weights, Tensor[] images) -> ()");
   m.def("account_round(Tensor last_mod, Tensor meta, int T, int W, Tensor(a!) client_dl, "
         "Tensor(b!) client_ul, float upc) -> Tensor");
   m.def("conv_prep_fwd(Tensor x, Tensor w) -> (Tensor, Tensor)");
@@ -1685,6 +1723,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("conv3x3_wgrad_grouped", &conv3x3_wgrad_grouped_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);
   m.impl("conv_weight_prep_multi", &conv_weight_prep_multi_hip);
+  m.impl("conv_images_patch", &conv_images_patch_hip);
   m.impl("conv_prep_fwd", &conv_prep_fwd_hip);
   m.impl("conv_prep_wgrad", &conv_prep_wgrad_hip);
   m.impl("conv_prep_wgrad_into", &conv_prep_wgrad_into_hip);

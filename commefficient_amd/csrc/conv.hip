@@ -1568,6 +1568,44 @@ void launch_conv3x3_wgrad_grouped(ConvWgradArgs a, int G, float* dw, int64_t gst
   launch_wgrad_reduce(a.slab, dw, a.K, a.C, a.splits_per_group, beta, gstride, G, stream);
 }
 
+namespace {
+__global__ void __launch_bounds__(256) conv_images_patch_kernel(ConvPatchBatch b, const int64_t* __restrict__ idx,
+                                                                int64_t k) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= k) return;
+  const int64_t i = idx[e];
+  // the weight holding coordinate i (compile-time indices only: a dynamically
+  // indexed by-value argument array would be copied to scratch)
+  int64_t local = -1;
+  uint16_t *wf = nullptr, *wt = nullptr;
+  int K = 0, C = 0;
+#pragma unroll
+  for (int j = 0; j < kPrepMax; ++j) {
+    if (j < b.n && i >= b.off[j] && i < b.off[j] + b.numel[j]) {
+      local = i - b.off[j];
+      wf = b.wf[j];
+      wt = b.wt[j];
+      K = b.K[j];
+      C = b.C[j];
+    }
+  }
+  if (local < 0) return;  // not a conv weight with images
+  const int rs = static_cast<int>(local % 9);
+  const int64_t kc = local / 9;
+  const int c = static_cast<int>(kc % C), kk = static_cast<int>(kc / C);
+  const __bf16 v = static_cast<__bf16>(b.w_flat[i]);
+  reinterpret_cast<__bf16*>(wf)[(static_cast<size_t>(kk) * 9 + rs) * C + c] = v;
+  reinterpret_cast<__bf16*>(wt)[(static_cast<size_t>(c) * 9 + 8 - rs) * K + kk] = v;
+}
+}  // namespace
+
+void launch_conv_images_patch(const ConvPatchBatch& b, const int64_t* idx, int64_t k,
+                              hipStream_t stream) {
+  if (k <= 0 || b.n <= 0) return;
+  hipLaunchKernelGGL(conv_images_patch_kernel, dim3(static_cast<uint32_t>((k + 255) / 256)), dim3(256), 0,
+                     stream, b, idx, k);
+}
+
 void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream) {
   int blocks = 0;
   for (int i = 0; i < b.n; ++i) {

@@ -225,6 +225,20 @@ struct ConvPrepBatch {
   int n;
 };
 void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream);
+// re-convert the coordinates idx of the flat fp32 weight vector w_flat into
+// the bf16 GEMM images of the conv weights laid out at off[j] (the images of
+// conv_weight_prep): a sparse server update touches only these
+struct ConvPatchBatch {
+  const float* w_flat;
+  int64_t off[kPrepMax];
+  int64_t numel[kPrepMax];
+  uint16_t* wf[kPrepMax];
+  uint16_t* wt[kPrepMax];
+  int K[kPrepMax], C[kPrepMax];
+  int n;
+};
+void launch_conv_images_patch(const ConvPatchBatch& b, const int64_t* idx, int64_t k,
+                              hipStream_t stream);
 // g = gy where y > 0 else 0 (bf16, n % 8 == 0)
 void launch_relu_mask(const uint16_t* gy, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream);

@@ -61,11 +61,82 @@ def conv_backend() -> str:
 _PREP: dict = {}
 
 
+class _ImageCache:
+    """The bf16 GEMM images of one set of conv weights, kept across forward
+    passes.  They are reused only after a sparse server step (FetchSGD /
+    true top-k: k of d coordinates change) has patched the changed
+    coordinates in place (``weights_begin_update`` / ``weights_end_update``);
+    any other change of the weights -- a dense server step, local SGD steps
+    on a work buffer, a resume -- leaves them stale, so a freshly converted
+    set is never reused as is."""
+
+    __slots__ = ("weights", "images", "versions", "valid", "synced")
+
+    def __init__(self, weights, images):
+        self.weights = weights
+        self.images = images
+        self.versions = [w._version for w in weights]
+        self.valid = False   # reusable by the next pass (set by a patch)
+        self.synced = True   # converted from the weights as they are now
+
+    def _unchanged(self) -> bool:
+        return all(w._version == v for w, v in zip(self.weights, self.versions))
+
+    def fresh(self) -> bool:
+        return self.valid and self._unchanged()
+
+    # weight-mirror protocol (weights_begin_update / weights_end_update)
+    def begin(self, w_flat: torch.Tensor) -> bool:
+        lo, hi = w_flat.data_ptr(), w_flat.data_ptr() + 4 * w_flat.numel()
+        ok = ((self.valid or self.synced) and self._unchanged() and len(self.weights) <= 16
+              and all(lo <= w.data_ptr() < hi for w in self.weights))
+        self.valid = self.synced = False
+        return ok
+
+    def patch(self, w_flat: torch.Tensor, idx: torch.Tensor) -> None:
+        _ops().conv_images_patch(w_flat, idx, self.weights, self.images)
+        self.versions = [w._version for w in self.weights]
+        self.valid = True
+
+
+_IMAGES: dict = {}  # key: weight data pointers -> _ImageCache (one model at a time)
+_MIRRORS: list = []  # other derived copies of the flat weights (parallel/flat.py bf16 replica)
+_IMAGE_CACHE_ON = [True]
+
+
+def set_conv_image_cache(on: bool) -> None:
+    """Keep derived weight copies (conv images, the bf16 replica) across
+    passes; FedModel turns this off when HIP-graph replay may change the
+    weights without Python seeing it."""
+    _IMAGE_CACHE_ON[0] = bool(on)
+    _IMAGES.clear()
+
+
+def register_weight_mirror(m) -> None:
+    """``m`` (begin(w_flat) -> bool, patch(w_flat, idx)) follows sparse
+    server steps like the conv images (weakly held by identity)."""
+    if all(x is not m for x in _MIRRORS):
+        _MIRRORS.append(m)
+
+
+def mirrors_enabled() -> bool:
+    return _IMAGE_CACHE_ON[0]
+
+
+def invalidate_conv_images() -> None:
+    """The flat weights were rewritten outside a server step (e.g. a resume):
+    kept derived copies must be rebuilt."""
+    for c in list(_IMAGES.values()) + _MIRRORS:
+        c.begin(torch.empty(0))
+
+
 class prepared_conv_weights:
     """``with prepared_conv_weights(ws): model(x)`` -- converts every weight in
     ``ws`` to its two bf16 GEMM images (forward [K,3,3,C] and flipped dgrad
-    [C,3,3,K]) in ONE kernel launch; the native conv units of this forward
-    pick them up instead of preparing their weight one by one."""
+    [C,3,3,K]) in ONE kernel launch, or reuses the images kept from the last
+    pass when the weights have not changed since (or were patched by a sparse
+    server update); the native conv units of this forward pick them up
+    instead of preparing their weight one by one."""
 
     def __init__(self, weights):
         self.weights = [w for w in weights if w.is_cuda and w.dtype == torch.float32
@@ -75,7 +146,17 @@ class prepared_conv_weights:
 
     def __enter__(self):
         if self.weights and _CONV_BACKEND[0] == "native":
-            out = _ops().conv_weight_prep_multi([w.detach() for w in self.weights])
+            ws = [w.detach() for w in self.weights]
+            capturing = torch.cuda.is_current_stream_capturing() or not _IMAGE_CACHE_ON[0]
+            ck = tuple(w.data_ptr() for w in ws)
+            cache = None if capturing else _IMAGES.get(ck)
+            if cache is not None and cache.fresh():
+                out = cache.images
+            else:
+                out = _ops().conv_weight_prep_multi(ws)
+                if not capturing:
+                    _IMAGES.clear()
+                    _IMAGES[ck] = _ImageCache(ws, out)
             for i, w in enumerate(self.weights):
                 key = (w.data_ptr(), w._version)
                 _PREP[key] = (out[2 * i], out[2 * i + 1])
@@ -86,6 +167,24 @@ class prepared_conv_weights:
         for k in self.keys:
             _PREP.pop(k, None)
         return False
+
+
+def weights_begin_update(w_flat: torch.Tensor):
+    """Call before a server step modifies the flat weights ``w_flat``: every
+    kept derived copy becomes stale; returns the ones that were in sync with
+    ``w_flat`` for ``weights_end_update``."""
+    if not w_flat.is_cuda:
+        return []
+    return [m for m in list(_IMAGES.values()) + _MIRRORS if m.begin(w_flat)]
+
+
+def weights_end_update(sync, w_flat: torch.Tensor, idx: torch.Tensor) -> None:
+    """The server step changed exactly the coordinates ``idx`` of ``w_flat``:
+    patch those into the copies that were in sync (one small kernel each)."""
+    if sync:
+        idx = idx.contiguous()
+        for m in sync:
+            m.patch(w_flat, idx)
 
 
 def _prep(weight: torch.Tensor):

@@ -40,7 +40,7 @@ import torch.nn as nn
 from .. import ops
 from ..models.common import NativeConv2d, ghost_batchnorm, groupable, has_batchnorm
 from ..ops.grouped import GroupedGrads, grouped_grads
-from ..ops.nn import prepared_conv_weights
+from ..ops.nn import invalidate_conv_images, prepared_conv_weights, set_conv_image_cache
 from ..ops import CSVec
 from ..ops import transformer as _tx
 from ..utils.logging import PhaseTimer
@@ -164,6 +164,12 @@ class FedModel:
         self._work = None  # separate work buffer for topk_down / fedavg
         self.last_round = {}
         self.graphs = RoundGraphs(self) if self.device.type == "cuda" else None
+        # bf16 conv-weight images kept across rounds and patched by sparse server
+        # steps (ops/nn.py) -- not with graph replay (the replayed server step
+        # changes the weights without Python seeing it)
+        # (COMMEFF_WEIGHT_MIRRORS=0: re-derive them every pass)
+        set_conv_image_cache((self.graphs is None or not self.graphs.enabled)
+                             and os.environ.get("COMMEFF_WEIGHT_MIRRORS", "1") != "0")
         self._acct_meta = None  # accounting meta staged with the round's inputs
         self._groupable = None  # grouped (per-client) weight gradients, ops/grouped.py
         self._gindex = None
@@ -1017,6 +1023,7 @@ class FedModel:
         self.accountant.load_state_dict(sd["accountant"])
         self.client_state.load_state_dict(sd["client_state"])
         self.w.copy_(sd["w"])
+        invalidate_conv_images()
         bufs = dict(self.model.named_buffers())
         for n, b in sd.get("buffers", {}).items():
             if n in bufs:

@@ -96,10 +96,34 @@ class FlatParams:
             p.data = self.wb[o:o + n].view(s)
             p.grad = None
         self.shadow_params = sp
+        # the replica follows sparse server steps by a k-element patch instead
+        # of a full cast (ops/nn.py weight-mirror protocol)
+        self._wb_valid = None   # fp32 buffer the replica mirrors AFTER a patch (reusable)
+        self._wb_synced = None  # fp32 buffer of the last full cast
+        if self.device.type == "cuda":
+            from ..ops.nn import register_weight_mirror
+            register_weight_mirror(self)
         return shadow
 
     def refresh_shadow(self) -> None:
+        from ..ops.nn import mirrors_enabled
+        ptr = self.bound.data_ptr()
+        if self._wb_valid == ptr and mirrors_enabled():
+            return  # patched by the last (sparse) server step: already current
         self.wb.copy_(self.bound)
+        self._wb_valid = None
+        self._wb_synced = ptr
+
+    # weight-mirror protocol (ops/nn.py weights_begin_update / weights_end_update)
+    def begin(self, w_flat: torch.Tensor) -> bool:
+        ptr = w_flat.data_ptr() if w_flat.numel() == self.d else None
+        ok = ptr is not None and ptr in (self._wb_valid, self._wb_synced)
+        self._wb_valid = self._wb_synced = None
+        return ok
+
+    def patch(self, w_flat: torch.Tensor, idx: torch.Tensor) -> None:
+        self.wb.index_copy_(0, idx, w_flat.index_select(0, idx).to(torch.bfloat16))
+        self._wb_valid = w_flat.data_ptr()
 
     def collect_shadow_grads(self) -> None:
         """g += the shadow's bf16 gradients (flat order); clears them.  When

@@ -36,6 +36,7 @@ from typing import Optional
 
 import torch
 
+from ..ops.nn import weights_begin_update, weights_end_update
 from .. import ops
 from ..ops import CSVec
 from . import dist
@@ -108,6 +109,12 @@ class ServerState:
         rho = float(a.virtual_momentum)
         lr_s, lr_v = (lr, None) if not torch.is_tensor(lr) else (0.0, lr)
         mode = a.mode
+        # kept derived weight copies (bf16 conv images, bf16 replica): stale from
+        # here on, unless the step is sparse (then the k changed coordinates
+        # are patched into them)
+        img_sync = weights_begin_update(w)
+        if step is not None:  # captured graph step: no Python bookkeeping at replay
+            img_sync = []
         if mode == "sketch":
             et = a.error_type
             if et == "virtual":
@@ -129,6 +136,7 @@ class ServerState:
             # error feedback (virtual) + momentum-factor masking in sketch space
             sk.zero_heavy_hitters(idx, vals, self.V if et == "virtual" else None)
             ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
+            weights_end_update(img_sync, w, idx)
             return idx, vals
         if mode == "true_topk":
             ops.momentum_ef(self.V, self.E, G, rho, gscale, "virtual")
@@ -137,6 +145,7 @@ class ServerState:
                 client_state.zero_velocity_at(participating, idx)
             ops.zero_at(idx, self.E, self.V)
             ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
+            weights_end_update(img_sync, w, idx)
             return idx, vals
         if mode in ("local_topk", "uncompressed"):
             ops.momentum_ef(self.V, None, G, rho, gscale, "none")

@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_conv.py -x -q -k unpool --timeout 120 --timeout-method thread > gpurun_out/unpool_test.log 2>&1 && \
+timeout -k 10 300 python -u -m pytest tests/test_conv.py -x -q -k "unpool or kept_conv" --timeout 120 --timeout-method thread > gpurun_out/unpool_test.log 2>&1 && \
 timeout -k 10 900 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps 40 --warmup 5 > gpurun_out/bench_a.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps 40 --warmup 5 > gpurun_out/bench_b.log 2>&1 && \

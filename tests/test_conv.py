@@ -595,3 +595,45 @@ def test_fused_unpool_backward_bitwise(chain):
     a, b = run(True), run(False)
     for ga, gb in zip(a, b):
         assert torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("mode", ["sketch", "true_topk", "uncompressed"])
+def test_kept_conv_images_match_fresh_prep(mode):
+    """ResNet-9 rounds through FedModel: the bf16 conv-weight images kept
+    across rounds and patched at the k coordinates a sparse server step
+    changed (ops/nn.py _ImageCache, csrc conv_images_patch) equal a fresh
+    conversion of the current weights after every round."""
+    from commefficient_amd import models
+    from commefficient_amd.data import make_synthetic
+    from commefficient_amd.data.device_loader import DeviceFedLoader
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd._ext import ops as _xops
+    from commefficient_amd.train.losses import cv_loss
+    from commefficient_amd.utils.args import parse_args
+
+    dist.init("cuda")
+    extra = ["--error_type", "virtual"] if mode != "uncompressed" else ["--error_type", "none"]
+    args = parse_args(argv=["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", "400",
+                            "--mode", mode, "--local_momentum", "0", "--virtual_momentum", "0.9",
+                            "--k", "3000", "--num_rows", "5", "--num_cols", "50000",
+                            "--num_clients", "40", "--num_workers", "8", "--local_batch_size", "-1",
+                            "--device", "cuda", "--graph", "off"] + extra, probe_port=False)
+    ds = make_synthetic("CIFAR10", train=True, num_clients=40, size=400, seed=0)
+    loader = DeviceFedLoader(ds, 8, -1, "cuda", seed=0)
+    model = models.build_model(args, 10)
+    fed = FedModel(model, cv_loss, args, num_clients=40)
+    opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), args, fed)
+    it = iter(loader)
+    for _ in range(3):
+        fed(next(it))
+        opt.step()
+        for c in cnn._IMAGES.values():
+            if not c.fresh():
+                continue  # (dense modes: rebuilt at the next pass)
+            fresh = _xops().conv_weight_prep_multi([w for w in c.weights])
+            for a, b in zip(c.images, fresh):
+                assert torch.equal(a, b)
+    if mode != "uncompressed":
+        assert any(c.fresh() for c in cnn._IMAGES.values())

@@ -380,3 +380,46 @@ def test_native_path_fused_attention_matches_sdpa_path_gpu():
     for n in g0:
         rel = (g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-6)
         assert rel < 3e-2, (n, float(rel))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sketch", "uncompressed"])
+def test_bf16_replica_follows_sparse_server_steps_gpu(mode):
+    """--weight_cast once: after a sparse (FetchSGD) server step the bf16
+    replica is patched at the k changed coordinates instead of re-cast
+    (parallel/flat.py weight mirror); it must equal bf16(w) bitwise before
+    every forward, in sparse and dense modes alike."""
+    from commefficient_amd.models.gpt2 import GPT2DoubleHeads
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd.train.losses import gpt2_loss_train
+    from commefficient_amd.utils.args import parse_args
+    dist.init("cuda")
+    ids, tt = _inputs(Nb=4, device="cuda")
+    mc_tok = torch.full((4, 2), 19, device="cuda")
+    labels = torch.full((4, 2, 20), -100, device="cuda")
+    labels[:, -1, 12:] = ids[:, -1, 12:]
+    mc = torch.ones(4, dtype=torch.long, device="cuda")
+    torch.manual_seed(0)
+    model = GPT2DoubleHeads("gpt2", n_layer=2, n_embd=256, n_head=4, n_positions=64)
+    extra = (["--error_type", "virtual", "--k", "5000", "--num_rows", "5", "--num_cols", "20000"]
+             if mode == "sketch" else [])
+    args = parse_args(argv=["--mode", mode, "--local_momentum", "0", "--virtual_momentum", "0.9",
+                            "--num_workers", "2", "--local_batch_size", "2", "--device", "cuda",
+                            "--dtype", "bf16", "--num_clients", "2", "--weight_cast", "once",
+                            "--graph", "off"] + extra, probe_port=False)
+    fed = FedModel(model, gpt2_loss_train, args, num_clients=2)
+    opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), args, fed)
+    flat = fed.flat
+    for r in range(3):
+        w0 = fed.w.clone()
+        fed((torch.tensor([0, 0, 1, 1]), ids, mc_tok, labels, tt, mc))
+        assert torch.equal(flat.wb, fed.w.to(torch.bfloat16))  # what this round's forward used
+        opt.step()
+        assert not torch.equal(fed.w, w0)
+        if mode == "sketch":
+            assert flat._wb_valid == fed.w.data_ptr()  # patched, not re-cast next round
+            assert torch.equal(flat.wb, fed.w.to(torch.bfloat16))
+        else:
+            assert flat._wb_valid is None
