@@ -45,7 +45,7 @@ head_fwd_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w, con
                 uint8_t* __restrict__ codes) {
   __shared__ float logit_s[4][kMaxCls];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b = blockIdx.x * 4 + wv;
+  const int b = blockIdx.x * (blockDim.x >> 6) + wv;
   if (b >= B) return;
   const uint16_t* xb = x + static_cast<size_t>(b) * NPIX * C;
   // each lane owns 8 consecutive channels per 512-channel chunk
@@ -61,14 +61,23 @@ head_fwd_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w, con
       best[j] = -__builtin_huge_valf();
       arg[j] = 0;
     }
-    for (int p = 0; p < NPIX; ++p) {
-      const H8 v = *reinterpret_cast<const H8*>(xb + static_cast<size_t>(p) * C + ch);
+    // 8 pixels' loads in flight at a time (a load-compare chain per pixel
+    // left the kernel latency-bound)
+    for (int p0 = 0; p0 < NPIX; p0 += 8) {
+      H8 v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = bfv(v.h[j]);
-        if (f > best[j]) {
-          best[j] = f;
-          arg[j] = static_cast<uint32_t>(p);
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < NPIX) v[u] = *reinterpret_cast<const H8*>(xb + static_cast<size_t>(p0 + u) * C + ch);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (p0 + u >= NPIX) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bfv(v[u].h[j]);
+          if (f > best[j]) {
+            best[j] = f;
+            arg[j] = static_cast<uint32_t>(p0 + u);
+          }
         }
       }
     }
@@ -83,14 +92,28 @@ head_fwd_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w, con
     }
     *reinterpret_cast<H8*>(pooled + static_cast<size_t>(b) * C + ch) = pv;
     *reinterpret_cast<uint64_t*>(codes + static_cast<size_t>(b) * C + ch) = cd;
-    // partial logits of this lane's 8 channels
-    for (int k = 0; k < NCLS; ++k) {
-      const float4 w0 = *reinterpret_cast<const float4*>(w + static_cast<size_t>(k) * C + ch);
-      const float4 w1 = *reinterpret_cast<const float4*>(w + static_cast<size_t>(k) * C + ch + 4);
-      float s = best[0] * w0.x + best[1] * w0.y + best[2] * w0.z + best[3] * w0.w + best[4] * w1.x +
-                best[5] * w1.y + best[6] * w1.z + best[7] * w1.w;
-      s = wsum(s);
-      if (lane == 0) logit_s[wv][k] += s;
+    // partial logits of this lane's 8 channels, 4 classes at a time (loads
+    // first, then 4 independent wave sums)
+    for (int k0 = 0; k0 < NCLS; k0 += 4) {
+      float4 w0[4], w1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u < NCLS ? k0 + u : NCLS - 1;
+        w0[u] = *reinterpret_cast<const float4*>(w + static_cast<size_t>(k) * C + ch);
+        w1[u] = *reinterpret_cast<const float4*>(w + static_cast<size_t>(k) * C + ch + 4);
+      }
+      float sv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        sv[u] = best[0] * w0[u].x + best[1] * w0[u].y + best[2] * w0[u].z + best[3] * w0[u].w +
+                best[4] * w1[u].x + best[5] * w1[u].y + best[6] * w1[u].z + best[7] * w1[u].w;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sv[u] += __shfl_xor(sv[u], o, 64);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (lane == 0 && k0 + u < NCLS) logit_s[wv][k0 + u] += sv[u];
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -211,7 +234,8 @@ void launch_head_fwd(const uint16_t* x, const float* w, const int64_t* tgt, int 
                      float scale, float* loss, float* correct, float* gunit, uint16_t* pooled, uint8_t* codes,
                      hipStream_t stream) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, x, w, tgt, B, C, NPIX, NCLS,
+  // two waves (examples) per block: 250 blocks for B = 500 fill the 256 CUs
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 1) / 2), dim3(128), 0, stream, x, w, tgt, B, C, NPIX, NCLS,
                      scale, loss, correct, gunit, pooled, codes);
 }
 
