@@ -24,6 +24,7 @@
 // instead of the 64-channel activation.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "kernels.h"
 #include "conv_common.h"
 
@@ -271,7 +272,12 @@ void launch_conv_prep_fwd(ConvPrepArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   const int ntiles = (a.P + 31) / 32;
-  int blocks = (ntiles + 15) / 16;  // ~4 tiles per wave (weights are set up once per block)
+  static const int tpw = [] {  // tiles per wave (weights are set up once per block); tuning knob
+    const char* e = std::getenv("COMMEFF_PREP_TPW");
+    const int v = e != nullptr ? std::atoi(e) : 8;
+    return v < 1 ? 1 : v;
+  }();
+  int blocks = (ntiles + 4 * tpw - 1) / (4 * tpw);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(prep_fwd_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, stream, a);
 }
