@@ -123,7 +123,8 @@ at::Tensor cs_l2estimate_cpu(const at::Tensor& table) {
   return out;
 }
 
-std::tuple<at::Tensor, at::Tensor> topk_abs_cpu(const at::Tensor& x, int64_t k) {
+std::tuple<at::Tensor, at::Tensor> topk_abs_cpu(const at::Tensor& x, int64_t k,
+                                                const c10::optional<at::Tensor>& /*hint: GPU only*/) {
   check_f32(x, "x");
   const int64_t n = x.numel();
   const int64_t kk = std::max<int64_t>(0, std::min(k, n));
@@ -353,7 +354,10 @@ at::Tensor cs_l2estimate_hip(const at::Tensor& table) {
   return out;
 }
 
-std::tuple<at::Tensor, at::Tensor> topk_abs_hip(const at::Tensor& x, int64_t k) {
+// hint: optional int32 [1] device tensor carried between calls of one
+// selection site (previous threshold / 2; 0 = no bound) -- see topk.hip
+std::tuple<at::Tensor, at::Tensor> topk_abs_hip(const at::Tensor& x, int64_t k,
+                                                const c10::optional<at::Tensor>& hint) {
   check_f32(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t n = x.numel();
@@ -367,8 +371,14 @@ std::tuple<at::Tensor, at::Tensor> topk_abs_hip(const at::Tensor& x, int64_t k) 
     return {idx, vals};
   }
   auto ws = at::empty({topk_workspace_bytes(n)}, x.options().dtype(at::kByte));
+  uint32_t* hp = nullptr;
+  if (hint.has_value() && hint->defined()) {
+    TORCH_CHECK(hint->scalar_type() == at::kInt && hint->numel() >= 1 && hint->device() == x.device(),
+                "topk_abs: hint must be an int32 device tensor");
+    hp = reinterpret_cast<uint32_t*>(hint->data_ptr<int32_t>());
+  }
   launch_topk_abs(x.data_ptr<float>(), n, kk, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
-                  ws.data_ptr(), cur_stream());
+                  ws.data_ptr(), cur_stream(), hp);
   return {idx, vals};
 }
 
@@ -1640,7 +1650,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("cs_zero_buckets(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, Tensor hashes, "
         "Tensor blk_off, Tensor blk_sign, int num_blocks, int d) -> ()");
   m.def("cs_l2estimate(Tensor table) -> Tensor");
-  m.def("topk_abs(Tensor x, int k) -> (Tensor, Tensor)");
+  m.def("topk_abs(Tensor x, int k, Tensor? hint=None) -> (Tensor, Tensor)");
   m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
   m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "
         "Tensor(b!)? last_mod, int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");

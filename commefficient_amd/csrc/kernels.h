@@ -110,7 +110,8 @@ int64_t topk_workspace_bytes(int64_t n);
 // Deterministic magnitude top-k: selects the k largest |x| (ties -> lower
 // index), writes idx (ascending) and vals = x[idx].  No host sync.
 void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx,
-                     float* vals, void* workspace, hipStream_t stream);
+                     float* vals, void* workspace, hipStream_t stream,
+                     uint32_t* hint = nullptr);
 
 // ----------------------------------------------------------- elementwise --
 // V = rho*V + gscale*G ; mode 1: E += V ; mode 2: E = V

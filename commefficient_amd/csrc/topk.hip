@@ -11,7 +11,7 @@
 // Algorithm (no host sync, fixed launch sequence -> hipGraph capturable):
 //   key(i) = bits(x[i]) & 0x7fffffff        (monotone in |x| for finite x)
 //   three histogram passes over 11/11/9-bit digits of the key (one histogram
-//   buffer each), a count pass (per-block #>T, #==T) and an ordered
+//   buffer each; pass 0 optionally bounded below by a hint, see hist_kernel), a count pass (per-block #>T, #==T) and an ordered
 //   compaction pass.  The digit selections (walk a histogram from the top to
 //   the bin holding the k-th largest key) and the scan of the per-block
 //   counts are not kernels of their own: every block of the following pass
@@ -31,7 +31,7 @@ constexpr int kBins = 2048;
 constexpr int kNB = 4096;  // blocks for count/write passes (upper bound)
 
 struct WS {
-  uint32_t* hist[3];  // kBins each (pass 2 uses 512)
+  uint32_t* hist[4];  // kBins each (pass 2 uses 512; [3]: pass-0 fill-in below the hint)
   uint32_t* cnt_gt;   // kNB
   uint32_t* cnt_eq;   // kNB
 };
@@ -39,7 +39,7 @@ struct WS {
 WS carve(void* base) {
   char* p = reinterpret_cast<char*>(base);
   WS w;
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 4; ++i) {
     w.hist[i] = reinterpret_cast<uint32_t*>(p);
     p += kBins * 4;
   }
@@ -60,13 +60,14 @@ struct Sel {
 };
 template <int NBINS>
 __device__ Sel select_bin(const uint32_t* __restrict__ hist, uint32_t remaining, uint32_t* tot,
-                          uint32_t* res) {
+                          uint32_t* res, const uint32_t* __restrict__ hist2 = nullptr) {
   constexpr int per = NBINS / 256;
   uint32_t c[per];
   uint32_t s = 0;
 #pragma unroll
   for (int q = 0; q < per; ++q) {
-    c[q] = hist[NBINS - 1 - (threadIdx.x * per + q)];
+    const int b = NBINS - 1 - (threadIdx.x * per + q);
+    c[q] = hist[b] + (hist2 != nullptr ? hist2[b] : 0u);
     s += c[q];
   }
   // inclusive scan over threads: wave scans + 4 wave totals
@@ -114,7 +115,7 @@ template <int PASSES>
 __device__ Walk walk(const WS& w, uint32_t k, uint32_t* tot, uint32_t* res) {
   Walk s = {0u, k};
   if (PASSES >= 1) {
-    const Sel a = select_bin<2048>(w.hist[0], s.remaining, tot, res);
+    const Sel a = select_bin<2048>(w.hist[0], s.remaining, tot, res, w.hist[3]);
     s.prefix = a.bin;
     s.remaining -= a.above;
   }
@@ -134,13 +135,32 @@ __device__ Walk walk(const WS& w, uint32_t k, uint32_t* tot, uint32_t* res) {
 // PASS 0: digit = key >> 20 (11 bits)
 // PASS 1: digit = (key >> 9) & 0x7ff, needs (key >> 20) == prefix
 // PASS 2: digit = key & 0x1ff,         needs (key >> 9)  == prefix
+// With a lower-bound hint L (the previous call's threshold / 2, ``hint``):
+// PASS 0 histograms only keys >= L -- for a tail selection almost every
+// element is below L, so the pass streams instead of queueing on
+// same-bin LDS atomics -- and PASS 3 (the fill-in) adds the keys < L only if
+// fewer than k keys were >= L (the bound was too high).  Bins at and above
+// L's bin then hold exact counts of every key >= L, which is all the top-down
+// walk reads whenever >= k keys are >= L; otherwise the fill-in makes the
+// histogram exact.  Deterministic either way (integer counts).
 template <int PASS>
 __global__ void __launch_bounds__(256)
-hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk) {
+hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk, const uint32_t* __restrict__ hint) {
   __shared__ uint32_t h[kBins];
   __shared__ uint32_t tot[4], res[2];
   for (int b = threadIdx.x; b < kBins; b += blockDim.x) h[b] = 0;
-  const uint32_t prefix = walk<PASS>(ws, kk, tot, res).prefix;
+  const uint32_t lb = hint != nullptr ? hint[0] : 0u;
+  if constexpr (PASS == 3) {
+    // skip the fill-in when >= k keys were >= L (every block agrees)
+    uint32_t c = 0;
+    for (int b = threadIdx.x; b < kBins; b += blockDim.x) c += ws.hist[0][b];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+    if ((threadIdx.x & 63) == 0) tot[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (tot[0] + tot[1] + tot[2] + tot[3] >= kk) return;
+    __syncthreads();
+  }
+  const uint32_t prefix = PASS == 3 ? 0u : walk<PASS>(ws, kk, tot, res).prefix;
   __syncthreads();  // h zeroed before any atomic
   // (LDS atomics retire ~0.4 lanes/clk/CU and bound pass 0; per-wave
   // sub-histograms measured no faster, wave-aggregated atomics 4x slower:
@@ -149,7 +169,9 @@ hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk) {
     if (!in) return;
     const uint32_t k = key_of(v);
     if (PASS == 0) {
-      atomicAdd(h + (k >> 20), 1u);
+      if (k >= lb) atomicAdd(h + (k >> 20), 1u);
+    } else if (PASS == 3) {
+      if (k < lb) atomicAdd(h + (k >> 20), 1u);
     } else if (PASS == 1) {
       if ((k >> 20) == prefix) atomicAdd(h + ((k >> 9) & 0x7ff), 1u);
     } else {
@@ -273,11 +295,14 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wt, ui
 // (elements stay in ascending order)
 __global__ void __launch_bounds__(256)
 write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32_t kk,
-             int64_t* __restrict__ idx, float* __restrict__ vals) {
+             int64_t* __restrict__ idx, float* __restrict__ vals, uint32_t* __restrict__ hint) {
   __shared__ uint32_t tot[4], res[2];
   __shared__ uint32_t wt_eq[4], wt_sel[4];
   const Walk wk = walk<3>(ws, kk, tot, res);
   const uint32_t thr = wk.prefix, ties = wk.remaining;
+  // next call's lower bound: half this threshold (finite thresholds only)
+  if (hint != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    hint[0] = thr < 0x7f800000u ? __float_as_uint(__uint_as_float(thr) * 0.5f) : 0u;
   // counts of the blocks before this one
   uint32_t g = 0, e = 0;
   for (int b = threadIdx.x; b < static_cast<int>(blockIdx.x); b += 256) {
@@ -354,21 +379,23 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
 }  // namespace
 
 int64_t topk_workspace_bytes(int64_t) {
-  return 3 * kBins * 4 + 2 * kNB * 4;
+  return 4 * kBins * 4 + 2 * kNB * 4;
 }
 
 void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,
-                     void* workspace, hipStream_t stream) {
+                     void* workspace, hipStream_t stream, uint32_t* hint) {
   if (k <= 0 || n <= 0) return;
   WS w = carve(workspace);
-  (void)hipMemsetAsync(w.hist[0], 0, 3 * kBins * 4, stream);
+  (void)hipMemsetAsync(w.hist[0], 0, 4 * kBins * 4, stream);
   int hb = static_cast<int>((n + 1023) / 1024);
   if (hb > 1024) hb = 1024;
   if (hb < 1) hb = 1;
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
-  hipLaunchKernelGGL(hist_kernel<0>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
-  hipLaunchKernelGGL(hist_kernel<1>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
-  hipLaunchKernelGGL(hist_kernel<2>, dim3(hb), dim3(256), 0, stream, x, n, w, kk);
+  hipLaunchKernelGGL(hist_kernel<0>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
+  if (hint != nullptr)
+    hipLaunchKernelGGL(hist_kernel<3>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
+  hipLaunchKernelGGL(hist_kernel<1>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
+  hipLaunchKernelGGL(hist_kernel<2>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
   // compaction blocks: 1,024 (every block's prologue sums the counts of the
   // blocks before it), up to kNB for very long vectors (>= 32 K elements a
   // block: GPT-2 size 151 -> 128 us for the ordered write pass)
@@ -379,7 +406,7 @@ void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* 
   span = ((span + 1023) / 1024) * 1024;  // write_kernel: 1024 elements per block step
   nb = static_cast<int>((n + span - 1) / span);
   hipLaunchKernelGGL(count_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk);
-  hipLaunchKernelGGL(write_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, idx, vals);
+  hipLaunchKernelGGL(write_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, idx, vals, hint);
 }
 
 }  // namespace commeff

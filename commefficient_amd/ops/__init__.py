@@ -17,9 +17,28 @@ __all__ = ["CSVec", "make_hashes", "topk_abs", "topk_dense", "momentum_ef", "spa
 ERROR_MODE = {"none": 0, "virtual": 1, "local": 2}
 
 
-def topk_abs(x: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Deterministic magnitude top-k: (idx ascending int64, vals=x[idx]); ties -> lower index."""
-    return _ops().topk_abs(x.reshape(-1).contiguous(), int(k))
+_TOPK_HINTS: dict = {}
+
+
+def topk_hint(tag, device) -> Optional[torch.Tensor]:
+    """Persistent per-site lower-bound hint for ``topk_abs`` (csrc/topk.hip:
+    the previous call's threshold / 2 bounds the first histogram pass; the
+    result never depends on it).  One per selection site (``tag``)."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return None
+    key = (tag, str(device))
+    h = _TOPK_HINTS.get(key)
+    if h is None:
+        h = _TOPK_HINTS[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return h
+
+
+def topk_abs(x: torch.Tensor, k: int, hint: Optional[torch.Tensor] = None
+             ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Deterministic magnitude top-k: (idx ascending int64, vals=x[idx]); ties -> lower index.
+    ``hint``: a ``topk_hint`` tensor of the call site (speed only)."""
+    return _ops().topk_abs(x.reshape(-1).contiguous(), int(k), hint)
 
 
 def topk_dense(x: torch.Tensor, k: int) -> torch.Tensor:

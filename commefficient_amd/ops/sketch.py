@@ -51,6 +51,11 @@ def make_hashes(r: int, c: int, num_blocks: int = 1, seed: int = 42):
     return hashes, blk_off, blk_sign
 
 
+
+def _topk_hint(tag, device):
+    from . import topk_hint
+    return topk_hint(tag, device)
+
 class CSVec:
     """Count Sketch of a d-dimensional vector into an r x c fp32 table."""
 
@@ -153,7 +158,7 @@ class CSVec:
 
     def unsketch_sparse(self, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         est = self.query()
-        return ops().topk_abs(est, int(k))
+        return ops().topk_abs(est, int(k), _topk_hint(("unsketch", self.d, int(k)), est.device))
 
     def shard_bounds(self, world: int) -> Optional[list]:
         """Coordinate shard boundaries [b_0 = 0, ..., b_world = d] at plan-chunk
@@ -191,7 +196,8 @@ class CSVec:
         lo, hi = b[rank], b[rank + 1]
         est = ops().cs_query_planned(self.table, self.d, self._plan(), nch * rank // world,
                                      nch * (rank + 1) // world)
-        li, lv = ops().topk_abs(est[lo:hi], k)
+        li, lv = ops().topk_abs(est[lo:hi], k, _topk_hint(("unsketch_shard", self.d, k, rank, world),
+                                                         est.device))
         pack = torch.empty(2, k, dtype=torch.int64, device=self.device)
         pack[0] = li + lo
         pack[1] = lv.view(torch.int32)

@@ -140,7 +140,7 @@ class ServerState:
             return idx, vals
         if mode == "true_topk":
             ops.momentum_ef(self.V, self.E, G, rho, gscale, "virtual")
-            idx, vals = ops.topk_abs(self.E, a.k)
+            idx, vals = ops.topk_abs(self.E, a.k, ops.topk_hint(("true_topk", self.d, a.k), self.E.device))
             if client_state is not None and participating is not None:
                 client_state.zero_velocity_at(participating, idx)
             ops.zero_at(idx, self.E, self.V)

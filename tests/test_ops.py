@@ -424,3 +424,28 @@ def test_planned_encode_overwrite_equals_zero_then_add():
     ref = sk.like()
     ref.accumulateVec(v, 0.5, w, 0.1)
     assert torch.equal(sk.table, ref.table)
+
+
+@pytest.mark.gpu
+def test_topk_hint_never_changes_the_result():
+    """topk_abs with a per-site lower-bound hint (csrc/topk.hip: pass 0 counts
+    only keys >= the previous threshold / 2, a fill-in pass adds the rest when
+    that was too few) returns bitwise the unhinted result over a sequence of
+    vectors whose scale jumps up and down (stale-bound fallback), with ties,
+    zeros, NaN-free sparse vectors and k close to n."""
+    if not torch.cuda.is_available():
+        pytest.skip("GPU only")
+    g = torch.Generator().manual_seed(11)
+    hint = ops.topk_hint(("test_hint", 0), "cuda")
+    hint.zero_()
+    seq = []
+    for scale in (1.0, 1.3, 0.01, 100.0, 100.0, 0.5):
+        seq.append((torch.randn(300000, generator=g) * scale, 5000))
+    z = torch.zeros(300000)
+    z[::97] = torch.randn(z[::97].numel(), generator=g)
+    seq += [(z, 5000), (z, 3000), (torch.ones(300000), 7), (torch.randn(4096, generator=g), 4000)]
+    for x, k in seq:
+        a = ops.topk_abs(x.cuda(), k)
+        b = ops.topk_abs(x.cuda(), k, hint)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert int(hint.item()) != 0
