@@ -47,20 +47,29 @@ def main():
                    help="HIP-graph replay of the round (parallel/graph.py)")
     p.add_argument("--torch-profile", default=None,
                    help="after the timed steps, trace 5 more with torch.profiler into this dir")
-    p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "1")),
-                   help="torch.backends.cudnn.benchmark (MIOpen exhaustive find during warmup)")
+    p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "0")),
+                   help="torch.backends.cudnn.benchmark (ResNet-9 runs no MIOpen conv)")
+    p.add_argument("--check-every", type=int, default=50,
+                   help="cross-rank bitwise weight check every N rounds outside the timed "
+                        "region (and once after it); exits non-zero on drift")
     b = p.parse_args()
 
     if b.graph != "off":
         commefficient_amd.request_graph_replay()  # must precede HIP initialisation
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != b.gpus:
-        if b.gpus > 1 and world == 1:
-            sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+        sys.exit(f"--gpus {b.gpus} but WORLD_SIZE={world}: for --gpus > 1 launch with "
+                 "torch.distributed.run --nproc-per-node N")
     from commefficient_amd.parallel import dist
     from commefficient_amd.utils.args import parse_args
     ctx = dist.init("cuda")
     N = ctx.world_size
+    assert N == b.gpus, (N, b.gpus)
+    if N > 1:
+        # one rank per GPU over RCCL (gloo rehearsals are not benchmarks)
+        assert ctx.backend == "nccl", f"backend {ctx.backend!r}: the bench runs on RCCL"
+        assert torch.cuda.device_count() >= N or os.environ.get("LOCAL_WORLD_SIZE") != str(N), \
+            "fewer visible GPUs than ranks"
     W = b.clients_per_gpu * N
     n_train = b.num_clients * b.client_size
     argv = ["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", str(n_train),
@@ -90,6 +99,9 @@ def main():
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
     fed = FedModel(model, cv_loss, args, num_clients=b.num_clients)
     fopt = FedOptimizer(opt, args, fed)
+    if not b.profile:
+        # per-round all-reduce time from HIP events (no syncs in the round)
+        fed.timer.enable_only({"allreduce"})
 
     # pre-draw the rounds' client/row index arrays (host sampler), full rounds only
     rounds = []
@@ -111,6 +123,8 @@ def main():
 
     for i in range(b.warmup):
         out = step(i)
+        if b.check_every and N > 1 and (i + 1) % b.check_every == 0:
+            dist.check_replicas(fed.w)
     torch.cuda.synchronize()
     first_loss = float(out[0].mean().item())
     dist.barrier()
@@ -130,6 +144,14 @@ def main():
     dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    elapsed = dist.max_over_ranks(t1 - t0)
+    phases = fed.timer.summary() if fed.timer.enabled else {}
+    checksum = None
+    if b.check_every:
+        # the replicated weights must be bitwise identical on every rank
+        checksum = dist.check_replicas(fed.w)
+    last_loss = float(out[0].mean().item())
+    dl = (float(fed.accountant.client_download.sum().item()) - dl_before) / b.steps
     if b.torch_profile:
         from torch.profiler import ProfilerActivity, profile
         stack = bool(os.environ.get("COMMEFF_PROF_STACK"))
@@ -149,16 +171,12 @@ def main():
                     f.write("\n")
                     f.write(prof.key_averages(group_by_stack_n=8).table(
                         sort_by="self_cuda_time_total", row_limit=80))
-    elapsed = dist.max_over_ranks(t1 - t0)
-    last_loss = float(out[0].mean().item())
-    dl = (float(fed.accountant.client_download.sum().item()) - dl_before) / b.steps
     imgs_per_step = W * b.client_size
     ms = elapsed / b.steps * 1000.0
     value = imgs_per_step * b.steps / elapsed
     up_ref = fed.accountant.upload_per_client * W
     payload = fed.last_round.get("payload_bytes", 0)
     wire = fed.accountant.wire_bytes_per_rank(payload // 4)
-    phases = fed.timer.summary() if fed.timer.enabled else {}
     if ctx.is_main:
         print(json.dumps({
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
@@ -176,6 +194,7 @@ def main():
                                "wire_per_rank_ring": wire},
             "loss_first": round(first_loss, 4), "loss_last": round(last_loss, 4),
             "phase_ms": {k: round(v, 3) for k, v in phases.items()},
+            "backend": ctx.backend, "weights_checksum": checksum,
             "host_enqueue_ms_per_step": round(host_s / b.steps * 1000.0, 3),
             "graph_replays": fed.graphs.replays if fed.graphs is not None else 0,
         }), flush=True)

@@ -8,6 +8,8 @@ composition (CPU runs, fp32 runs, odd shapes).
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn.functional as F
 
@@ -100,7 +102,9 @@ class _ImageCache:
 
 
 _IMAGES: dict = {}  # key: weight data pointers -> _ImageCache (one model at a time)
-_MIRRORS: list = []  # other derived copies of the flat weights (parallel/flat.py bf16 replica)
+# other derived copies of the flat weights (parallel/flat.py bf16 replica),
+# weakly held: a torn-down FedModel's replica is not kept alive or updated
+_MIRRORS = weakref.WeakSet()
 _IMAGE_CACHE_ON = [True]
 
 
@@ -115,8 +119,7 @@ def set_conv_image_cache(on: bool) -> None:
 def register_weight_mirror(m) -> None:
     """``m`` (begin(w_flat) -> bool, patch(w_flat, idx)) follows sparse
     server steps like the conv images (weakly held by identity)."""
-    if all(x is not m for x in _MIRRORS):
-        _MIRRORS.append(m)
+    _MIRRORS.add(m)
 
 
 def mirrors_enabled() -> bool:
@@ -126,7 +129,7 @@ def mirrors_enabled() -> bool:
 def invalidate_conv_images() -> None:
     """The flat weights were rewritten outside a server step (e.g. a resume):
     kept derived copies must be rebuilt."""
-    for c in list(_IMAGES.values()) + _MIRRORS:
+    for c in list(_IMAGES.values()) + list(_MIRRORS):
         c.begin(torch.empty(0))
 
 
@@ -175,7 +178,7 @@ def weights_begin_update(w_flat: torch.Tensor):
     ``w_flat`` for ``weights_end_update``."""
     if not w_flat.is_cuda:
         return []
-    return [m for m in list(_IMAGES.values()) + _MIRRORS if m.begin(w_flat)]
+    return [m for m in list(_IMAGES.values()) + list(_MIRRORS) if m.begin(w_flat)]
 
 
 def weights_end_update(sync, w_flat: torch.Tensor, idx: torch.Tensor) -> None:

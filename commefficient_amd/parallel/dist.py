@@ -46,6 +46,42 @@ def ctx() -> DistCtx:
     return _CTX
 
 
+# RCCL defaults for one MI355X node (8 GPUs, each with 7 point-to-point xGMI
+# links to the others).  Set only when the user has not set them:
+# * TORCH_NCCL_HIGH_PRIORITY=1 -- RCCL kernels on a high-priority HIP stream, so
+#   the bucketed gradient all-reduces issued during the backward
+#   (parallel/overlap.py) are not queued behind the compute kernels;
+# * TORCH_NCCL_AVOID_RECORD_STREAMS=1 -- no record_stream on the payload, whose
+#   buffer is reused round after round (no allocator retention);
+# * NCCL_MIN_NCHANNELS=16 -- at least 16 channels (rings) for the 10 MB sketch
+#   all-reduce, so every one of the 7 links carries traffic (the default channel
+#   search can settle on fewer for medium messages; a ring is link-bound on xGMI);
+# * RCCL_MSCCL_ENABLE=1 -- RCCL's MSCCL single-node all-reduce schedules for the
+#   fully connected xGMI mesh (used where RCCL finds them faster than rings).
+# Override any of them from the environment; COMMEFF_RCCL_DEFAULTS=0 sets none.
+RCCL_DEFAULTS = {
+    "TORCH_NCCL_HIGH_PRIORITY": "1",
+    "TORCH_NCCL_AVOID_RECORD_STREAMS": "1",
+    "NCCL_MIN_NCHANNELS": "16",
+    "RCCL_MSCCL_ENABLE": "1",
+}
+
+
+def apply_rccl_defaults(env=None) -> dict:
+    """Fill in ``RCCL_DEFAULTS`` (before ``init_process_group``); returns the
+    values that were set."""
+    env = os.environ if env is None else env
+    if env.get("COMMEFF_RCCL_DEFAULTS", "1") == "0":
+        return {}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
+    out = {}
+    for k, v in RCCL_DEFAULTS.items():
+        if k not in env:
+            env[k] = v
+            out[k] = v
+    return out
+
+
 def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> DistCtx:
     """Initialise from the environment (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
     global _CTX
@@ -70,6 +106,7 @@ def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> 
             os.environ.setdefault("MASTER_PORT", str(port))
         kw = {}
         if backend == "nccl":
+            apply_rccl_defaults()
             kw["device_id"] = device
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
@@ -201,6 +238,32 @@ def max_over_ranks(x: float) -> float:
                      device=_CTX.device if _CTX.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def replica_checksum(w: torch.Tensor) -> int:
+    """Order-sensitive 64-bit checksum of the BIT pattern of a float tensor
+    (one device reduction, one host sync)."""
+    x = w.detach().reshape(-1)
+    if x.dtype != torch.int32:
+        x = x.contiguous().view(torch.int32)
+    n = x.numel()
+    # position weights keep swapped values from cancelling
+    pos = torch.arange(n, device=x.device, dtype=torch.int64).mul_(2654435761).remainder_(
+        1 << 31).add_(1)
+    return int((x.to(torch.int64) * pos).sum().item())
+
+
+def check_replicas(w: torch.Tensor, what: str = "weights") -> int:
+    """Every rank applies the same deterministic update, so the replicated
+    weights must be bitwise identical; a drifted rank (a nondeterministic
+    kernel, a missed collective) raises here.  Returns the checksum."""
+    c = replica_checksum(w)
+    if not _CTX.distributed:
+        return c
+    allc = all_gather_object(c)
+    if len(set(allc)) != 1:
+        raise RuntimeError(f"replicated {what} drifted across ranks: checksums {allc}")
+    return c
 
 
 def shutdown():

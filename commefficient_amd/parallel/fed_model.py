@@ -128,7 +128,11 @@ class FedModel:
 
         self.model.to(self.device)
         if self.device.type == "cuda":
-            torch.backends.cudnn.benchmark = bool(getattr(args, "miopen_find", 1))
+            find = bool(getattr(args, "miopen_find", 0))
+            # the reference: cudnn.deterministic = True, benchmark = False
+            # (cv_train.py:323-326, gpt2_train.py:361-364)
+            torch.backends.cudnn.benchmark = find
+            torch.backends.cudnn.deterministic = not find
         from ..ops.nn import set_conv_backend
         set_conv_backend(getattr(args, "conv", "native"))
         self.flat = FlatParams(self.model, self.device)
@@ -216,6 +220,7 @@ class FedModel:
     def load_state_dict(self, sd, strict=True):
         r = self.model.load_state_dict(sd, strict=strict)
         self.flat.bind(self.w)  # load_state_dict copies into the views
+        invalidate_conv_images()  # kept bf16 conv images / replica are stale
         return r
 
     def save_pretrained(self, log_dir):
@@ -1009,12 +1014,28 @@ class FedModel:
         return [res[i] for i in range(res.shape[0])]
 
     # ---------------------------------------------------------- checkpoint
+    def _seed_streams(self):
+        """Host-side dropout seed streams of the native GPT-2 path
+        (ops/transformer.py _Seeds), keyed by model and module name."""
+        out = {}
+        for tag, m in (("model", self.model), ("shadow", self._shadow)):
+            if m is None:
+                continue
+            for name, mod in m.named_modules():
+                s = getattr(mod, "_commeff_seeds", None)
+                if s is not None:
+                    out[f"{tag}:{name}"] = (mod, s)
+        return out
+
     def fed_state_dict(self):
         return {"round_idx": self.round_idx, "fedavg_lr": self.fedavg_lr,
                 "server": self.server.state_dict(), "accountant": self.accountant.state_dict(),
                 "client_state": self.client_state.state_dict(), "w": self.w.cpu(),
                 # BatchNorm running statistics etc. (not part of the flat weights)
-                "buffers": {n: b.detach().cpu() for n, b in self.model.named_buffers()}}
+                "buffers": {n: b.detach().cpu() for n, b in self.model.named_buffers()},
+                # native dropout masks continue where they stopped
+                "dropout_seeds": {k: int(s.s) for k, (_, s) in self._seed_streams().items()},
+                "dp_ctr": int(getattr(self, "_dp_ctr", 0))}
 
     def load_fed_state_dict(self, sd):
         self.round_idx = int(sd["round_idx"])
@@ -1028,3 +1049,17 @@ class FedModel:
         for n, b in sd.get("buffers", {}).items():
             if n in bufs:
                 bufs[n].copy_(b)
+        if "dp_ctr" in sd:
+            self._dp_ctr = int(sd["dp_ctr"])
+        seeds = sd.get("dropout_seeds", {})
+        if seeds:
+            from ..ops.transformer import _Seeds
+            for tag, m in (("model", self.model), ("shadow", self._shadow)):
+                if m is None:
+                    continue
+                for name, mod in m.named_modules():
+                    v = seeds.get(f"{tag}:{name}")
+                    if v is not None:
+                        st = getattr(mod, "_commeff_seeds", None) or _Seeds(0)
+                        st.s = int(v)
+                        mod._commeff_seeds = st

@@ -100,30 +100,42 @@ class FlatParams:
         # of a full cast (ops/nn.py weight-mirror protocol)
         self._wb_valid = None   # fp32 buffer the replica mirrors AFTER a patch (reusable)
         self._wb_synced = None  # fp32 buffer of the last full cast
+        self._wb_sig = None     # write signature of the weights the replica matches
         if self.device.type == "cuda":
             from ..ops.nn import register_weight_mirror
             register_weight_mirror(self)
         return shadow
 
+    def _write_sig(self) -> int:
+        """Monotone signature of writes to the bound fp32 weights: in-place
+        writes to the flat buffer bump its version counter, writes through the
+        parameter views (``load_state_dict``, ``set_param_vec``) bump the
+        parameters' own counters (views made by ``.data =`` do not share it)."""
+        return self.bound._version + sum(p._version for p in self.params)
+
     def refresh_shadow(self) -> None:
         from ..ops.nn import mirrors_enabled
         ptr = self.bound.data_ptr()
-        if self._wb_valid == ptr and mirrors_enabled():
+        sig = self._write_sig()
+        if self._wb_valid == ptr and self._wb_sig == sig and mirrors_enabled():
             return  # patched by the last (sparse) server step: already current
         self.wb.copy_(self.bound)
         self._wb_valid = None
         self._wb_synced = ptr
+        self._wb_sig = sig
 
     # weight-mirror protocol (ops/nn.py weights_begin_update / weights_end_update)
     def begin(self, w_flat: torch.Tensor) -> bool:
         ptr = w_flat.data_ptr() if w_flat.numel() == self.d else None
-        ok = ptr is not None and ptr in (self._wb_valid, self._wb_synced)
+        ok = (ptr is not None and ptr in (self._wb_valid, self._wb_synced)
+              and ptr == self.bound.data_ptr() and self._wb_sig == self._write_sig())
         self._wb_valid = self._wb_synced = None
         return ok
 
     def patch(self, w_flat: torch.Tensor, idx: torch.Tensor) -> None:
         self.wb.index_copy_(0, idx, w_flat.index_select(0, idx).to(torch.bfloat16))
         self._wb_valid = w_flat.data_ptr()
+        self._wb_sig = self._write_sig()
 
     def collect_shadow_grads(self) -> None:
         """g += the shadow's bf16 gradients (flat order); clears them.  When
@@ -172,7 +184,9 @@ def set_param_vec(model: nn.Module, vec: torch.Tensor) -> None:
     with torch.no_grad():
         for p in trainable_params(model):
             n = p.numel()
-            p.data.copy_(vec[start:start + n].view_as(p))
+            # through the parameter (not ``p.data``): bumps its version counter,
+            # which the derived weight copies (conv images, bf16 replica) watch
+            p.copy_(vec[start:start + n].view_as(p))
             start += n
 
 

@@ -307,7 +307,9 @@ def save_checkpoint(model: FedModel, args, progress=None):
     print("saved", path)
 
 
-def main(args):
+def main(args, loggers=()):
+    """``loggers``: extra per-epoch row sinks (``.append(dict)``), e.g. the
+    convergence script's JSONL curve, next to the TableLogger."""
     ctx = dist.init(args.device, port=args.port)
     timer = Timer()
     np.random.seed(args.seed)
@@ -342,8 +344,8 @@ def main(args):
     if ctx.is_main:
         print("Finished initializing in {:.2f} seconds".format(timer()))
     progress = progress or {"epoch": 0, "iter": 0}
-    train(fed, fopt, sched, train_loader, test_loader, args, writer, loggers=(TableLogger(),),
-          timer=timer, progress=progress)
+    train(fed, fopt, sched, train_loader, test_loader, args, writer,
+          loggers=(TableLogger(),) + tuple(loggers), timer=timer, progress=progress)
     fed.finalize()
     if args.do_checkpoint:
         save_checkpoint(fed, args, progress)

@@ -183,9 +183,11 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--profile_rounds", type=int, default=5,
                    help="rounds captured by torch.profiler (after 1 wait + 1 warmup round)")
     g.add_argument("--channels_last", type=int, default=1, help="NHWC activations for convs")
-    g.add_argument("--miopen_find", type=int, default=1,
-                   help="MIOpen exhaustive kernel search for each conv shape (cudnn.benchmark); "
-                        "+14%% ResNet-9 throughput on MI355X")
+    g.add_argument("--miopen_find", type=int, default=0,
+                   help="1: MIOpen exhaustive kernel search per conv shape (cudnn.benchmark; "
+                        "algorithm choice may differ run to run).  Default 0 = the reference's "
+                        "cudnn.deterministic=True, benchmark=False (cv_train.py:325-326); "
+                        "only convs outside the native kernels reach MIOpen")
     g.add_argument("--conv", choices=["native", "miopen"], default="native",
                    help="3x3 conv(+relu+pool) units: native MFMA kernels (csrc/conv.hip) "
                         "where shapes fit, or MIOpen everywhere")

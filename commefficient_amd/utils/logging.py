@@ -113,12 +113,21 @@ class PhaseTimer:
     def __init__(self, enabled: bool, device):
         import torch
         self.enabled = enabled and torch.device(device).type == "cuda"
+        self.only = None  # optional set of phase names to time (others are free)
         self._pending = []
         self.totals: Dict[str, float] = {}
         self.counts: Dict[str, int] = {}
 
     def phase(self, name: str):
         return _Phase(self, name)
+
+    def enable_only(self, names) -> None:
+        """Time just these phases (e.g. the bench's all-reduce): two event
+        records per phase and round, no syncs."""
+        import torch
+        if torch.cuda.is_available():
+            self.enabled = True
+            self.only = set(names)
 
     def summary(self) -> Dict[str, float]:
         import torch
@@ -137,7 +146,8 @@ class _Phase:
         self.t, self.name = timer, name
 
     def __enter__(self):
-        if self.t.enabled:
+        self.on = self.t.enabled and (self.t.only is None or self.name in self.t.only)
+        if self.on:
             import torch
             self.a = torch.cuda.Event(enable_timing=True)
             self.b = torch.cuda.Event(enable_timing=True)
@@ -145,7 +155,7 @@ class _Phase:
         return self
 
     def __exit__(self, *exc):
-        if self.t.enabled:
+        if self.on:
             self.b.record()
             self.t._pending.append((self.name, self.a, self.b))
         return False

@@ -295,3 +295,95 @@ def test_nonfinite_round_skipped_and_injected():
     for _ in range(2):
         fb((cids, X, y)); ob.step()
     assert fb.skipped_rounds == 0 and not torch.isfinite(fb.w).all()
+
+
+def _ref_scenario(d, W, k, r, c, lr=0.005):
+    """Two FetchSGD rounds of the unit_test.py:23-26 linear problem (X =
+    arange(4d).view(4, d), y = arange(4), squared error, w0 = 0, momentum 0,
+    virtual error) on ``W`` clients with an r x c sketch."""
+    argv = ["--mode", "sketch", "--error_type", "virtual", "--virtual_momentum", "0",
+            "--local_momentum", "0", "--weight_decay", "0", "--k", str(k), "--num_rows", str(r),
+            "--num_cols", str(c), "--num_blocks", "1", "--num_workers", str(W),
+            "--local_batch_size", str(4 // W)]
+    fed, opt, _ = make_engine(d, argv, W, lr)
+    X = torch.arange(4 * d, dtype=torch.float32).view(4, d)
+    y = torch.arange(4, dtype=torch.float32)
+    cids = split(4, W)
+    ws = []
+    for _ in range(2):
+        fed((cids, X, y))
+        opt.param_groups[0]["lr"] = lr
+        opt.step()
+        ws.append(fed.w.double().numpy().copy())
+    return ws, X.double().numpy(), y.double().numpy()
+
+
+def _G(w, X, y):
+    """Round gradient = mean over the round's examples of d/dw (x.w - y)^2
+    (each client's mean gradient weighted n_i / B)."""
+    return 2.0 * X.T @ (X @ w - y) / len(y)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_reference_oracle_one_weight_tiny_sketch(W):
+    """unit_test.py:185-186 (d=1, k=1, 1x1 sketch, 1 or 2 workers): one
+    coordinate, so the sketch estimate s*s*g is exact and every round is a
+    plain gradient step.  Re-derived: G(0) = -7 -> w1 = 0.035;
+    G(w1) = 7 w1 - 7 -> w2 = w1 + 0.005 (7 - 7 w1) = 0.068775."""
+    (w1, w2), X, y = _ref_scenario(1, W, 1, 1, 1)
+    np.testing.assert_allclose(w1, [0.035], rtol=1e-6)
+    np.testing.assert_allclose(w2, [0.068775], rtol=1e-6)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_reference_oracle_two_weights_large_sketch(W):
+    """unit_test.py:187,191 (d=2, k=2, 9x1000 sketch, 1 or 2 workers): the
+    median of 9 rows recovers both coordinates exactly and k = d, so two
+    plain gradient steps: G(0) = (-14, -17) -> w1 = (0.07, 0.085)."""
+    (w1, w2), X, y = _ref_scenario(2, W, 2, 9, 1000)
+    e1 = -0.005 * _G(np.zeros(2), X, y)
+    np.testing.assert_allclose(e1, [0.07, 0.085], rtol=1e-12)
+    e2 = e1 - 0.005 * _G(e1, X, y)
+    np.testing.assert_allclose(w1, e1, rtol=1e-6)
+    np.testing.assert_allclose(w2, e2, rtol=1e-6)
+
+
+def test_reference_oracle_two_weights_one_bucket():
+    """unit_test.py:188-190 (d=2, k=2, 1x1 sketch): both coordinates share
+    the single bucket, table = s0 g0 + s1 g1 and est_i = s_i * table, so the
+    update is (g0+g1, g0+g1) when the signs agree and (g0-g1, g1-g0) when
+    they differ (the reference's three admissible w1).  Both are selected
+    (k = d) and heavy-hitter zeroing clears the bucket, so round 2 repeats
+    the construction at w1 with the same signs."""
+    (w1, w2), X, y = _ref_scenario(2, 1, 2, 1, 1)
+    lr = 0.005
+
+    def step(w, same):
+        g = _G(w, X, y)
+        t = g[0] + g[1] if same else g[0] - g[1]
+        return w - lr * (np.array([t, t]) if same else np.array([t, -t]))
+
+    opts = {same: step(np.zeros(2), same) for same in (True, False)}
+    same = [s for s, e in opts.items() if np.allclose(w1, e, rtol=1e-6)]
+    assert same, (w1, opts)
+    np.testing.assert_allclose(w2, step(opts[same[0]], same[0]), rtol=1e-6)
+
+
+def test_reference_oracle_two_workers_top1():
+    """unit_test.py:192 (d=2, W=2, k=1, 9x1000 sketch): exact estimates but
+    only the largest coordinate moves; the other stays in the virtual error
+    and is added to the next round's gradient before the next top-1."""
+    (w1, w2), X, y = _ref_scenario(2, 2, 1, 9, 1000)
+    lr = 0.005
+    g0 = _G(np.zeros(2), X, y)            # (-14, -17): coordinate 1 wins
+    i = int(np.argmax(np.abs(g0)))
+    e1 = np.zeros(2)
+    e1[i] = -lr * g0[i]
+    err = g0.copy()
+    err[i] = 0.0                          # E[nz] = 0
+    est = err + _G(e1, X, y)              # E += V (momentum 0: V = S)
+    j = int(np.argmax(np.abs(est)))
+    e2 = e1.copy()
+    e2[j] -= lr * est[j]
+    np.testing.assert_allclose(w1, e1, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(w2, e2, rtol=1e-6, atol=1e-9)
