@@ -16,7 +16,7 @@
 //
 // Forward:  S = Q K^T * scale (causal tiles only), row softmax (2 threads per
 //           row, LSE saved), P_drop = dropout(P) (32-bit counter hash of
-//           (seed, (seq*heads + h)*128*128 + i*128 + j), the backward
+//           (seed, ((seq*heads + h)*1024 + i)*1024 + j), the backward
 //           regenerates it), O = P_drop V.
 // Backward: D_i = dO_i . O_i; S, dP_drop = dO V^T recomputed in registers;
 //           P = exp(S - LSE), dS = P (dP - D) * scale (dP = dropout'(dP_drop));
@@ -36,7 +36,8 @@ namespace commeff {
 namespace {
 
 constexpr int HD = 64;       // head dim
-constexpr int LM = 128;      // max sequence length
+constexpr int LM = 128;      // max sequence length of the short (all-in-LDS) kernels
+constexpr int DS = 1024;     // dropout index stride: idx = ((seq*heads + h)*DS + i)*DS + j
 constexpr int RS = HD + 8;   // row stride (elements) of [LM][HD] bf16 tiles
 constexpr int TS = LM + 8;   // row stride of [HD][LM] and [LM][LM] bf16 tiles
 constexpr int SS = LM + 4;   // row stride of the fp32 score tile
@@ -84,7 +85,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   float* sO = sS;                                              // [LM][OS] over S
   const int bh = blockIdx.x;
   const int n = bh / a.nh, h = bh - n * a.nh;
-  const int L = a.len[n];
+  const int L = min(a.len[n], LM);
   if (L <= 0) return;
   const int64_t r0 = a.start[n];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
@@ -158,7 +159,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     sum += __shfl_xor(sum, 1, 64);
     if (i < L && half == 0) a.lse[static_cast<int64_t>(bh) * LM + i] = m + __logf(sum);
     const float inv = 1.f / sum;
-    const uint64_t ib = (static_cast<uint64_t>(bh) * LM + i) * LM + half * 64;
+    const uint64_t ib = (static_cast<uint64_t>(bh) * DS + i) * DS + half * 64;
 #pragma unroll
     for (int t = 0; t < 64; t += 2) {
       float v0 = p[t] * inv, v1 = p[t + 1] * inv;
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
 
   const int bh = blockIdx.x;
   const int n = bh / a.nh, h = bh - n * a.nh;
-  const int L = a.len[n];
+  const int L = min(a.len[n], LM);
   if (L <= 0) return;
   const int64_t r0 = a.start[n];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
@@ -317,7 +318,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
         const float P = valid ? __expf(s[e] * a.scale - sL[row]) : 0.f;
         bool keep = true;
         if (a.thresh != 0u)
-          keep = akeep((static_cast<uint64_t>(bh) * LM + row) * LM + col, a.seed, a.thresh);
+          keep = akeep((static_cast<uint64_t>(bh) * DS + row) * DS + col, a.seed, a.thresh);
         const float dP = keep ? dp[e] * a.dscale : 0.f;
         pd[ct][e] = keep ? P * a.dscale : 0.f;
         ds[ct][e] = P * (dP - sD[row]) * a.scale;
@@ -397,6 +398,408 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
   }
 }
 
+
+// ============================================================ long sequences
+// Flash-style kernels for sequences longer than LM (up to DS = 1024 tokens,
+// GPT-2's n_positions): a workgroup owns 128 rows of one (sequence, head) --
+// 32 per wave -- and streams the other operand through LDS in 64-row tiles
+// with an online softmax, so LDS no longer bounds the length.
+//   forward   (query rows):  S = Q K^T per 64-key tile into a per-wave fp32
+//             tile, row max / rescale / exp / dropout by 2 threads per row,
+//             O = alpha O + P_drop V on the MFMA; O / l and LSE at the end;
+//   backward  dQ kernel (query rows): S, dP = dO V^T per 64-key tile, dS in
+//             registers -> per-wave LDS, dQ += dS K;  it also writes
+//             D_i = dO_i . O_i for the second kernel;
+//             dK/dV kernel (key rows): S^T = K Q^T, dP^T = V dO^T per 64-query
+//             tile, dV += P_drop^T dO, dK += dS^T Q.
+// Every output element is written once by one workgroup: deterministic, no
+// atomics.  Dropout masks use the same (seq, head, i, j) hash as the short
+// kernels, so the two families are interchangeable.
+constexpr int QB = 128;  // rows per workgroup
+constexpr int TT = 64;   // streamed tile rows
+constexpr int T2 = 72;   // bf16 row stride of [64][64] tiles (and per-wave [32][64])
+constexpr int F2 = 68;   // fp32 row stride of per-wave [32][64] tiles
+
+// 64 rows x 64 columns (bf16) of a row block starting at token row r0 + t0
+// (column offset col) into LDS row-major [64][T2] and/or transposed [64][T2];
+// rows >= L are zero.  256 threads, two 16-byte pieces each.
+__device__ __forceinline__ void tile_load(uint16_t* dst, uint16_t* dstT, const uint16_t* base,
+                                          int64_t ld, int64_t r0, int t0, int L, int tid) {
+  v4u v[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = tid + 256 * u, i = c >> 3, ch = c & 7;
+    v[u] = v4u{0u, 0u, 0u, 0u};
+    if (t0 + i < L) v[u] = *reinterpret_cast<const v4u*>(base + (r0 + t0 + i) * ld + ch * 8);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = tid + 256 * u, i = c >> 3, ch = c & 7;
+    if (dst) *reinterpret_cast<v4u*>(dst + i * T2 + ch * 8) = v[u];
+    if (dstT) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        dstT[(ch * 8 + e) * T2 + i] = static_cast<uint16_t>((v[u][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+    }
+  }
+}
+
+// A-operand fragments of 32 rows x 64 columns straight from global memory
+// (lane: row lr, k = 16 ks + 8 hi); rows >= L are zero
+__device__ __forceinline__ void frag_load(bf16x8_t f[4], const uint16_t* base, int64_t ld, int64_t row,
+                                          bool valid, int hi) {
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    v4u v = v4u{0u, 0u, 0u, 0u};
+    if (valid) v = *reinterpret_cast<const v4u*>(base + row * ld + 16 * ks + 8 * hi);
+    f[ks] = __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+// 32 rows x 64 columns staged bf16 in a per-wave [32][T2] tile -> token rows
+// r0 + g0 + row (< L) of a [M, ld] bf16 matrix at column offset col
+__device__ __forceinline__ void rows_store(uint16_t* out, int64_t ld, int64_t r0, int g0, int L,
+                                           const uint16_t* stage, int lane) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = lane + 64 * u, row = c >> 3, ch = c & 7;
+    if (g0 + row < L)
+      *reinterpret_cast<v4u*>(out + (r0 + g0 + row) * ld + ch * 8) =
+          *reinterpret_cast<const v4u*>(stage + row * T2 + ch * 8);
+  }
+}
+
+__device__ __forceinline__ void stage_acc(uint16_t* stage, const f32x16_t acc[2], int hi, int lr,
+                                          const float* rowscale) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = crow(e, hi);
+      const float v = rowscale ? acc[ct][e] * rowscale[row] : acc[ct][e];
+      stage[row * T2 + 32 * ct + lr] = bfbits(v);
+    }
+}
+
+// LDS: K [64][T2], V^T [64][T2], per wave: S fp32 [32][F2], P bf16 [32][T2],
+// alpha [32]  (~72 KB: 2 workgroups per CU)
+__global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sVt = sK + TT * T2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
+  float* sS = reinterpret_cast<float*>(sVt + TT * T2) + w * 32 * F2;
+  uint16_t* sP = reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(sVt + TT * T2) + 4 * 32 * F2) +
+                 w * 32 * T2;
+  float* sA = reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(
+                  reinterpret_cast<float*>(sVt + TT * T2) + 4 * 32 * F2) + 4 * 32 * T2) + w * 32;
+  const int tiles = a.lse_ld / QB;
+  const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
+  const int n = bh / a.nh, h = bh - n * a.nh;
+  const int L = min(a.len[n], a.lse_ld);
+  if (q0 >= L) return;
+  const int64_t r0 = a.start[n];
+  const int H = a.nh * HD;
+  const int64_t ld3 = 3 * static_cast<int64_t>(H);
+  const int wq0 = q0 + 32 * w;
+  const bool wvalid = wq0 < L;
+  bf16x8_t qf[4];
+  frag_load(qf, a.qkv + h * HD, ld3, r0 + wq0 + lr, wq0 + lr < L, hi);
+  f32x16_t o[2] = {zero16(), zero16()};
+  // softmax state of row (lane >> 1) of this wave, columns half*32 ..
+  const int srow = lane >> 1, half = lane & 1, gi = wq0 + srow;
+  float m_run = -__builtin_huge_valf(), l_run = 0.f;
+  const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();  // every wave is done with the previous K / V tile
+    tile_load(sK, nullptr, a.qkv + H + h * HD, ld3, r0, kt * TT, L, tid);
+    tile_load(nullptr, sVt, a.qkv + 2 * H + h * HD, ld3, r0, kt * TT, L, tid);
+    __syncthreads();
+    const bool act = wvalid && kt * TT <= wq0 + 31;
+    if (act) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x16_t acc = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sK + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[ks], bf, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = crow(e, hi), col = 32 * ct + lr;
+          const int i = wq0 + row, j = kt * TT + col;
+          sS[row * F2 + col] = (j <= i && i < L) ? acc[e] * a.scale : -__builtin_huge_valf();
+        }
+      }
+    }
+    __syncthreads();
+    if (act) {
+      float p[32];
+      float mt = -__builtin_huge_valf();
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        p[t] = sS[srow * F2 + half * 32 + t];
+        mt = fmaxf(mt, p[t]);
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 1, 64));
+      const float m_new = fmaxf(m_run, mt);
+      const bool live = gi < L && m_new > -__builtin_huge_valf();
+      const float alpha = live ? __expf(m_run - m_new) : 1.f;
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 32; ++t) {
+        p[t] = live ? __expf(p[t] - m_new) : 0.f;
+        sum += p[t];
+      }
+      l_run = l_run * alpha + sum;
+      m_run = live ? m_new : m_run;
+      const uint64_t ib = (static_cast<uint64_t>(bh) * DS + gi) * DS + kt * TT + half * 32;
+#pragma unroll
+      for (int t = 0; t < 32; t += 2) {
+        float v0 = p[t], v1 = p[t + 1];
+        if (a.thresh != 0u) {
+          v0 = akeep(ib + t, a.seed, a.thresh) ? v0 * a.dscale : 0.f;
+          v1 = akeep(ib + t + 1, a.seed, a.thresh) ? v1 * a.dscale : 0.f;
+        }
+        *reinterpret_cast<uint32_t*>(sP + srow * T2 + half * 32 + t) =
+            static_cast<uint32_t>(bfbits(v0)) | (static_cast<uint32_t>(bfbits(v1)) << 16);
+      }
+      if (half == 0) sA[srow] = alpha;
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[ct][e] *= sA[crow(e, hi)];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sP + lr * T2 + 16 * ks + 8 * hi);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sVt + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
+          o[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, o[ct], 0, 0, 0);
+        }
+      }
+    }
+  }
+  const float l = l_run + __shfl_xor(l_run, 1, 64);
+  __syncthreads();
+  if (wvalid) {
+    if (half == 0) {
+      sA[srow] = gi < L ? 1.f / l : 0.f;
+      if (gi < L) a.lse[static_cast<int64_t>(bh) * a.lse_ld + gi] = m_run + __logf(l);
+    }
+  }
+  __syncthreads();
+  if (wvalid) {
+    stage_acc(sP, o, hi, lr, sA);
+    __syncthreads();
+    rows_store(a.o + h * HD, H, r0, wq0, L, sP, lane);
+  } else {
+    __syncthreads();
+  }
+}
+
+// dQ (+ D): LDS K, V [64][T2], K^T [64][T2], per wave dS bf16 [32][T2],
+// D / LSE [32]  (~46 KB)
+__global__ void __launch_bounds__(256) attn_long_dq_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sV = sK + TT * T2;
+  uint16_t* sKt = sV + TT * T2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
+  uint16_t* sdS = sKt + TT * T2 + w * 32 * T2;
+  float* sDr = reinterpret_cast<float*>(sKt + TT * T2 + 4 * 32 * T2) + w * 64;
+  float* sLr = sDr + 32;
+  const int tiles = a.lse_ld / QB;
+  const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
+  const int n = bh / a.nh, h = bh - n * a.nh;
+  const int L = min(a.len[n], a.lse_ld);
+  if (q0 >= L) return;
+  const int64_t r0 = a.start[n];
+  const int H = a.nh * HD;
+  const int64_t ld3 = 3 * static_cast<int64_t>(H);
+  const int wq0 = q0 + 32 * w;
+  const bool wvalid = wq0 < L;
+  bf16x8_t qf[4], gf[4];
+  frag_load(qf, a.qkv + h * HD, ld3, r0 + wq0 + lr, wq0 + lr < L, hi);
+  frag_load(gf, a.dout + h * HD, H, r0 + wq0 + lr, wq0 + lr < L, hi);
+  {  // D_i = dO_i . O_i and LSE_i of this wave's rows (2 threads per row)
+    const int srow = lane >> 1, half = lane & 1, i = wq0 + srow;
+    float s = 0.f;
+    if (i < L) {
+      const uint16_t* orow = a.o + (r0 + i) * H + h * HD + half * 32;
+      const uint16_t* grow = a.dout + (r0 + i) * H + h * HD + half * 32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const v4u ov = *reinterpret_cast<const v4u*>(orow + 8 * q);
+        const v4u gv = *reinterpret_cast<const v4u*>(grow + 8 * q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int sh = 16 * (e & 1);
+          s += bfval(static_cast<uint16_t>((ov[e >> 1] >> sh) & 0xffffu)) *
+               bfval(static_cast<uint16_t>((gv[e >> 1] >> sh) & 0xffffu));
+        }
+      }
+    }
+    s += __shfl_xor(s, 1, 64);
+    if (half == 0) {
+      sDr[srow] = s;
+      sLr[srow] = i < L ? a.lse[static_cast<int64_t>(bh) * a.lse_ld + i] : 0.f;
+      if (i < L) a.dbuf[static_cast<int64_t>(bh) * a.lse_ld + i] = s;
+    }
+  }
+  f32x16_t gq[2] = {zero16(), zero16()};
+  const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    tile_load(sK, sKt, a.qkv + H + h * HD, ld3, r0, kt * TT, L, tid);
+    tile_load(sV, nullptr, a.qkv + 2 * H + h * HD, ld3, r0, kt * TT, L, tid);
+    __syncthreads();
+    const bool act = wvalid && kt * TT <= wq0 + 31;
+    if (act) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x16_t s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int ko = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[ks], *reinterpret_cast<const bf16x8_t*>(sK + ko), s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[ks], *reinterpret_cast<const bf16x8_t*>(sV + ko), dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = crow(e, hi), col = 32 * ct + lr;
+          const int i = wq0 + row, j = kt * TT + col;
+          const bool valid = j <= i && i < L;
+          const float P = valid ? __expf(s[e] * a.scale - sLr[row]) : 0.f;
+          bool keep = true;
+          if (a.thresh != 0u) keep = akeep((static_cast<uint64_t>(bh) * DS + i) * DS + j, a.seed, a.thresh);
+          const float dP = keep ? dp[e] * a.dscale : 0.f;
+          sdS[row * T2 + col] = bfbits(P * (dP - sDr[row]) * a.scale);
+        }
+      }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sdS + lr * T2 + 16 * ks + 8 * hi);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sKt + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
+          gq[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, gq[ct], 0, 0, 0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (wvalid) {
+    stage_acc(sdS, gq, hi, lr, nullptr);
+    __syncthreads();
+    rows_store(a.dqkv + h * HD, ld3, r0, wq0, L, sdS, lane);
+  } else {
+    __syncthreads();
+  }
+}
+
+// dK, dV: LDS Q, dO [64][T2], Q^T, dO^T [64][T2], LSE / D [64], per wave
+// P_drop^T, dS^T bf16 [32][T2] (~74 KB)
+__global__ void __launch_bounds__(256) attn_long_dkdv_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sG = sQ + TT * T2;
+  uint16_t* sQt = sG + TT * T2;
+  uint16_t* sGt = sQt + TT * T2;
+  float* sL = reinterpret_cast<float*>(sGt + TT * T2);
+  float* sD = sL + TT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
+  uint16_t* sPt = reinterpret_cast<uint16_t*>(sD + TT) + w * 2 * 32 * T2;
+  uint16_t* sSt = sPt + 32 * T2;
+  const int tiles = a.lse_ld / QB;
+  const int bh = blockIdx.x / tiles, k0 = (blockIdx.x - bh * tiles) * QB;
+  const int n = bh / a.nh, h = bh - n * a.nh;
+  const int L = min(a.len[n], a.lse_ld);
+  if (k0 >= L) return;
+  const int64_t r0 = a.start[n];
+  const int H = a.nh * HD;
+  const int64_t ld3 = 3 * static_cast<int64_t>(H);
+  const int wk0 = k0 + 32 * w;
+  const bool wvalid = wk0 < L;
+  bf16x8_t kf[4], vf[4];
+  frag_load(kf, a.qkv + H + h * HD, ld3, r0 + wk0 + lr, wk0 + lr < L, hi);
+  frag_load(vf, a.qkv + 2 * H + h * HD, ld3, r0 + wk0 + lr, wk0 + lr < L, hi);
+  f32x16_t gk[2] = {zero16(), zero16()}, gv[2] = {zero16(), zero16()};
+  for (int qs = k0; qs < L; qs += TT) {
+    __syncthreads();
+    tile_load(sQ, sQt, a.qkv + h * HD, ld3, r0, qs, L, tid);
+    tile_load(sG, sGt, a.dout + h * HD, H, r0, qs, L, tid);
+    if (tid < TT) {
+      const int i = qs + tid;
+      sL[tid] = i < L ? a.lse[static_cast<int64_t>(bh) * a.lse_ld + i] : 0.f;
+      sD[tid] = i < L ? a.dbuf[static_cast<int64_t>(bh) * a.lse_ld + i] : 0.f;
+    }
+    __syncthreads();
+    const bool act = wvalid && qs + TT - 1 >= wk0;
+    if (act) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x16_t s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int ko = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], *reinterpret_cast<const bf16x8_t*>(sQ + ko), s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks], *reinterpret_cast<const bf16x8_t*>(sG + ko), dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = crow(e, hi), col = 32 * ct + lr;  // row: key, col: query
+          const int j = wk0 + row, i = qs + col;
+          const bool valid = j <= i && i < L;
+          const float P = valid ? __expf(s[e] * a.scale - sL[col]) : 0.f;
+          bool keep = true;
+          if (a.thresh != 0u) keep = akeep((static_cast<uint64_t>(bh) * DS + i) * DS + j, a.seed, a.thresh);
+          const float dP = keep ? dp[e] * a.dscale : 0.f;
+          sPt[row * T2 + col] = bfbits(keep ? P * a.dscale : 0.f);
+          sSt[row * T2 + col] = bfbits(P * (dP - sD[col]) * a.scale);
+        }
+      }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int ao = lr * T2 + 16 * ks + 8 * hi;
+        const bf16x8_t pa = *reinterpret_cast<const bf16x8_t*>(sPt + ao);
+        const bf16x8_t sa = *reinterpret_cast<const bf16x8_t*>(sSt + ao);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const int bo = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
+          gv[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, *reinterpret_cast<const bf16x8_t*>(sGt + bo), gv[ct], 0, 0, 0);
+          gk[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, *reinterpret_cast<const bf16x8_t*>(sQt + bo), gk[ct], 0, 0, 0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (wvalid) {
+    stage_acc(sPt, gk, hi, lr, nullptr);
+    stage_acc(sSt, gv, hi, lr, nullptr);
+    __syncthreads();
+    rows_store(a.dqkv + H + h * HD, ld3, r0, wk0, L, sPt, lane);
+    rows_store(a.dqkv + 2 * H + h * HD, ld3, r0, wk0, L, sSt, lane);
+  } else {
+    __syncthreads();
+  }
+}
+
+constexpr size_t kLongFwdLds = 2 * TT * T2 * 2 + 4 * 32 * F2 * 4 + 4 * 32 * T2 * 2 + 4 * 32 * 4;
+constexpr size_t kLongDqLds = 3 * TT * T2 * 2 + 4 * 32 * T2 * 2 + 4 * 64 * 4;
+constexpr size_t kLongDkdvLds = 4 * TT * T2 * 2 + 2 * TT * 4 + 4 * 2 * 32 * T2 * 2;
+static_assert(kLongDkdvLds <= 80 * 1024 && kLongFwdLds <= 80 * 1024, "2 workgroups per CU");
+
 constexpr size_t kFwdLds = (2 * LM * RS + HD * TS) * 2 + LM * SS * 4;
 constexpr size_t kBwdLds = 3 * HD * TS * 2 + 2 * LM * 4 + 3 * LM * TS * 2;
 static_assert(2 * LM * RS >= LM * TS, "P must fit over Q and K");
@@ -414,6 +817,19 @@ uint32_t attn_thresh(float p) {
 
 void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream) {
   if (nseq == 0) return;
+  if (a.lse_ld > LM) {  // long sequences: flash-style kernel
+    static bool lattr = false;
+    if (!lattr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_fwd_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongFwdLds));
+      lattr = true;
+    }
+    a.thresh = attn_thresh(p_drop);
+    a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    hipLaunchKernelGGL(attn_long_fwd_kernel, dim3(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB))),
+                       dim3(256), kLongFwdLds, stream, a);
+    return;
+  }
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_fwd_kernel),
@@ -428,6 +844,22 @@ void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
 
 void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream) {
   if (nseq == 0) return;
+  if (a.lse_ld > LM) {  // long sequences: dQ (+ D) kernel, then dK / dV kernel
+    static bool lattr = false;
+    if (!lattr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dq_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongDqLds));
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dkdv_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongDkdvLds));
+      lattr = true;
+    }
+    a.thresh = attn_thresh(p_drop);
+    a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    const dim3 grid(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB)));
+    hipLaunchKernelGGL(attn_long_dq_kernel, grid, dim3(256), kLongDqLds, stream, a);
+    hipLaunchKernelGGL(attn_long_dkdv_kernel, grid, dim3(256), kLongDkdvLds, stream, a);
+    return;
+  }
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_bwd_kernel),

@@ -1544,9 +1544,16 @@ void check_seqs(const at::Tensor& start, const at::Tensor& len) {
               "attn: start / len must be contiguous int32 [N]");
 }
 
+// LSE row stride for sequences of up to max_len tokens: 128 selects the
+// all-in-LDS short kernels, longer sequences the flash-style kernels
+int64_t attn_lse_ld(int64_t max_len) {
+  TORCH_CHECK(max_len >= 0 && max_len <= 1024, "attn: sequences of up to 1024 tokens, got ", max_len);
+  return max_len <= 128 ? 128 : (max_len + 127) / 128 * 128;
+}
+
 std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& qkv, const at::Tensor& start,
                                                 const at::Tensor& len, int64_t nh, double p_drop,
-                                                int64_t seed) {
+                                                int64_t seed, int64_t max_len) {
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 2 && qkv.is_contiguous() &&
                   qkv.size(1) == 3 * nh * 64,
               "attn_fwd: qkv must be contiguous bf16 [M, 3 * nh * 64]");
@@ -1555,8 +1562,10 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& qkv, const at:
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   const int64_t M = qkv.size(0), N = start.numel(), H = nh * 64;
   auto o = at::empty({M, H}, qkv.options());
-  auto lse = at::empty({N * nh * 128}, qkv.options().dtype(at::kFloat));
+  const int64_t ld = attn_lse_ld(max_len);
+  auto lse = at::empty({N * nh * ld}, qkv.options().dtype(at::kFloat));
   AttnArgs a{};
+  a.lse_ld = static_cast<int>(ld);
   a.qkv = reinterpret_cast<const uint16_t*>(qkv.data_ptr());
   a.o = reinterpret_cast<uint16_t*>(o.data_ptr());
   a.lse = lse.data_ptr<float>();
@@ -1571,7 +1580,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd_hip(const at::Tensor& qkv, const at:
 
 at::Tensor attn_bwd_hip(const at::Tensor& qkv, const at::Tensor& o, const at::Tensor& dout,
                         const at::Tensor& lse, const at::Tensor& start, const at::Tensor& len,
-                        int64_t nh, double p_drop, int64_t seed) {
+                        int64_t nh, double p_drop, int64_t seed, int64_t max_len) {
   const int64_t H = nh * 64;
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 2 && qkv.is_contiguous() &&
                   qkv.size(1) == 3 * H,
@@ -1581,11 +1590,18 @@ at::Tensor attn_bwd_hip(const at::Tensor& qkv, const at::Tensor& o, const at::Te
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2 &&
                     t->size(0) == M && t->size(1) == H,
                 "attn_bwd: o / dout must be contiguous bf16 [M, H]");
-  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == N * nh * 128, "attn_bwd: lse");
+  const int64_t ld = attn_lse_ld(max_len);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == N * nh * ld, "attn_bwd: lse");
   check_seqs(start, len);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   auto dqkv = at::empty_like(qkv);
+  at::Tensor dbuf;
   AttnArgs a{};
+  a.lse_ld = static_cast<int>(ld);
+  if (ld > 128) {
+    dbuf = at::empty({N * nh * ld}, lse.options());
+    a.dbuf = dbuf.data_ptr<float>();
+  }
   a.qkv = reinterpret_cast<const uint16_t*>(qkv.data_ptr());
   a.o = reinterpret_cast<uint16_t*>(o.data_ptr());
   a.lse = lse.data_ptr<float>();
@@ -1677,9 +1693,9 @@ TORCH_LIBRARY(commeff, m) {
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("bias_gelu_fwd(Tensor u, Tensor b) -> Tensor");
   m.def("pad_rows(Tensor src, Tensor? inv, int rows) -> Tensor");
-  m.def("attn_fwd(Tensor qkv, Tensor start, Tensor len, int nh, float p_drop, int seed) -> (Tensor, Tensor)");
+  m.def("attn_fwd(Tensor qkv, Tensor start, Tensor len, int nh, float p_drop, int seed, int max_len) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, Tensor start, Tensor len, int nh, "
-        "float p_drop, int seed) -> Tensor");
+        "float p_drop, int seed, int max_len) -> Tensor");
   m.def("heads_to_rows(Tensor[] srcs, Tensor? tok, int Mr) -> Tensor");
   m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu, Tensor(a!)? sbias=None) "
         "-> (Tensor, Tensor)");

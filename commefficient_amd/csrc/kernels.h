@@ -354,11 +354,15 @@ void launch_pad_rows(const void* src, int64_t src_ld, int64_t K, const int32_t* 
 void launch_heads_to_rows(const HeadSrcs& src, int P, int64_t H, int64_t hd, int64_t L,
                           const int32_t* tok, int64_t Mr, void* out, hipStream_t stream);
 // fused causal attention over unpadded token rows (attention.hip): sequence n
-// = rows [start[n], start[n] + len[n]), len <= 128, head dim 64
+// = rows [start[n], start[n] + len[n]), len <= lse_ld <= 1024, head dim 64;
+// lse_ld == 128: the all-in-LDS short kernels, else (a multiple of 128) the
+// flash-style long kernels
 struct AttnArgs {
   const uint16_t* qkv;  // [M, 3H] bf16 (q | k | v)
   uint16_t* o;          // [M, H] bf16 (forward output, backward input)
-  float* lse;           // [N * nh * 128] fp32
+  float* lse;           // [N * nh * lse_ld] fp32
+  float* dbuf;          // [N * nh * lse_ld] fp32 (long backward: dO . O per row)
+  int lse_ld;
   const uint16_t* dout; // [M, H] bf16 (backward)
   uint16_t* dqkv;       // [M, 3H] bf16 (backward)
   const int32_t* start;

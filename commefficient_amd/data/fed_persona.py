@@ -219,14 +219,24 @@ def _hash64(key, ctr):
 
 
 class SyntheticPersona(FedDataset):
-    """PersonaChat-shaped token data: clients = personalities with a few
-    dialogs each; personas of 4 sentences, utterances of random length,
-    ``num_candidates`` candidates (gold last).  Token ids < ``vocab`` and the 5
-    special tokens are ``vocab .. vocab+4`` (as after ``add_special_tokens_``)."""
+    """PersonaChat-shaped token data built like the reference's records
+    (/root/reference/CommEfficient/data_utils/fed_persona.py:245-258,330-358):
+    clients = personalities with a few dialogs each; a persona of
+    ``persona_sents`` (5) sentences; utterance u of a dialog sees the u-th
+    history of that dialog -- the 2u+1 previous turns, truncated to the last
+    ``2 * max_history + 1`` -- and ``num_candidates`` candidate replies (gold
+    last).  Token ids < ``vocab`` and the 5 special tokens are
+    ``vocab .. vocab+4`` (as after ``add_special_tokens_``).
+
+    Length assumption (no PersonaChat copy is available here, so parity of
+    the length distribution is unpinned): every sentence is 8..19 GPT-2 BPE
+    tokens, uniform (mean 13.5, the typical length of a PersonaChat turn), so
+    with max_history 2 the model input is ~70..240 tokens -- past the
+    128-token short attention kernels, as real PersonaChat inputs are."""
 
     def __init__(self, num_personalities=1000, dialogs_per_client=2, utterances_per_dialog=7,
                  num_candidates=2, max_history=2, vocab=50257, train=True, do_iid=False,
-                 num_clients=None, seed=0, sent_len=(6, 14), n_val=500):
+                 num_clients=None, seed=0, sent_len=(8, 20), n_val=500, persona_sents=5):
         self.num_candidates, self.max_history, self.vocab = num_candidates, max_history, vocab
         self._np, self._dpc, self._upd = num_personalities, dialogs_per_client, utterances_per_dialog
         self._n_val = n_val
@@ -234,7 +244,7 @@ class SyntheticPersona(FedDataset):
         self._sent_len = sent_len
         super().__init__("", "PERSONA", None, do_iid, num_clients, train=train, seed=seed)
         self.special_ids = [vocab + i for i in range(5)]
-        self._personas = [self._sents(4) for _ in range(num_personalities)]
+        self._personas = [self._sents(persona_sents) for _ in range(num_personalities)]
 
     def _meta_ready(self):
         return True
@@ -248,12 +258,13 @@ class SyntheticPersona(FedDataset):
         return [self._rng.randint(0, self.vocab, size=self._rng.randint(lo, hi)).tolist()
                 for _ in range(n)]
 
-    def _rec(self, key, persona, train):
-        """Deterministic record of item ``key``: every random number comes
-        from one vectorised counter hash (a per-item RandomState took ~40 us
-        to construct, the round's batch assembly ~15 ms at 32 items)."""
+    def _rec(self, key, persona, train, u):
+        """Deterministic record of item ``key``, utterance ``u`` of its dialog:
+        every random number comes from one vectorised counter hash (a per-item
+        RandomState took ~40 us to construct, the round's batch assembly ~15 ms
+        at 32 items)."""
         lo, hi = self._sent_len
-        n_hist = 1 + int(_hash64(key, 0) % np.uint64(2 * self.max_history + 1))
+        n_hist = min(2 * int(u) + 1, 2 * self.max_history + 1)
         n_sent = n_hist + max(2, self.num_candidates)
         lens = lo + (_hash64(key, np.arange(1, n_sent + 1)) % np.uint64(hi - lo)).astype(np.int64)
         toks = (_hash64(key, np.arange(1000, 1000 + int(lens.sum()))) % np.uint64(self.vocab))
@@ -266,10 +277,11 @@ class SyntheticPersona(FedDataset):
                                    self.num_candidates, self.max_history, train)
 
     def _get_train_item(self, nat, idx_within_client):
-        return self._rec(nat * 100003 + idx_within_client, self._personas[nat], True)
+        return self._rec(nat * 100003 + idx_within_client, self._personas[nat], True,
+                         idx_within_client % self._upd)
 
     def _get_val_item(self, idx):
-        return self._rec(10 ** 9 + idx, self._personas[idx % self._np], False)
+        return self._rec(10 ** 9 + idx, self._personas[idx % self._np], False, idx % self._upd)
 
     def __getitem__(self, idx):
         out = super().__getitem__(idx)

@@ -26,8 +26,18 @@ class PersonaFedLoader:
         return len(self.dataset)
 
     def __iter__(self):
+        self.epoch = getattr(self, "epoch", 0) + 1
         for r in self.sampler:
             yield self.make_batch(r)
+
+    def state_dict(self, pos=None):
+        """Sampler position (resume mid-epoch) -- the records themselves are a
+        pure function of the item index."""
+        return {"sampler": self.sampler.state_dict(pos), "epoch": max(0, getattr(self, "epoch", 0) - 1)}
+
+    def load_state_dict(self, sd):
+        self.sampler.load_state_dict(sd["sampler"])
+        self.epoch = int(sd.get("epoch", 0))
 
     def make_batch(self, r):
         ds, dev = self.dataset, self.device

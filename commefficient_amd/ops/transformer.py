@@ -484,17 +484,28 @@ def real_token_index(lengths: torch.Tensor, L: int, device):
 
 
 # ------------------------------------------------------- fused attention
-ATTN_MAX_LEN = 128
+# csrc/attention.hip: sequences of <= 128 tokens run the all-in-LDS kernels,
+# longer ones (up to GPT-2's 1024 positions) the flash-style kernels; both
+# draw dropout from the same (sequence, head, i, j) hash
+ATTN_MAX_LEN = 1024
+ATTN_SHORT_LEN = 128
+_DS = 1024  # dropout index stride (csrc/attention.hip DS)
 
 
-def _ref_attn(qkv, start, lens, nh, p, seed):
+def attn_lse_ld(max_len: int) -> int:
+    """LSE row stride (and kernel family) for sequences of <= max_len tokens."""
+    return 128 if max_len <= ATTN_SHORT_LEN else (max_len + 127) // 128 * 128
+
+
+def _ref_attn(qkv, start, lens, nh, p, seed, max_len=ATTN_SHORT_LEN):
     """fp32 reference of csrc/attention.hip over unpadded token rows (same
     dropout hash; P_drop rounded to bf16 as the kernel feeds it to the MFMA)."""
     M, H3 = qkv.shape
     H = H3 // 3
     hd = H // nh
+    ld = attn_lse_ld(max_len)
     o = qkv.new_zeros(M, H, dtype=torch.float32)
-    lse = torch.zeros(start.numel() * nh * ATTN_MAX_LEN, dtype=torch.float32, device=qkv.device)
+    lse = torch.zeros(start.numel() * nh * ld, dtype=torch.float32, device=qkv.device)
     for n in range(start.numel()):
         s0, L = int(start[n]), int(lens[n])
         if L == 0:
@@ -508,47 +519,48 @@ def _ref_attn(qkv, start, lens, nh, p, seed):
         e = torch.exp(S - m)
         ssum = e.sum(-1, keepdim=True)
         P = e / ssum
-        base = (n * nh + torch.arange(nh, device=qkv.device)) * ATTN_MAX_LEN
+        base = (n * nh + torch.arange(nh, device=qkv.device)) * _DS
         i = torch.arange(L, device=qkv.device)
-        idx = ((base[:, None, None] + i[None, :, None]) * ATTN_MAX_LEN + i[None, None, :])
+        idx = ((base[:, None, None] + i[None, :, None]) * _DS + i[None, None, :])
         if p > 0:
             keep = keep_at(idx.long(), seed, p)
             P = torch.where(keep, P / (1.0 - p), torch.zeros_like(P))
         P = _bf(P)
         o[s0:s0 + L] = (P @ v).transpose(0, 1).reshape(L, H)
-        lse.view(-1, ATTN_MAX_LEN)[n * nh:(n + 1) * nh, :L] = (m + torch.log(ssum)).squeeze(-1)
+        lse.view(-1, ld)[n * nh:(n + 1) * nh, :L] = (m + torch.log(ssum)).squeeze(-1)
     return o.to(qkv.dtype), lse
 
 
 class _Attention(torch.autograd.Function):
     """o [M, H] = causal self-attention of every sequence's token rows of
-    qkv [M, 3H] (csrc/attention.hip on HIP tensors)."""
+    qkv [M, 3H] (csrc/attention.hip on HIP tensors); ``max_len`` (host int)
+    bounds every sequence's length and selects the kernel family."""
 
     @staticmethod
-    def forward(ctx, qkv, start, lens, nh, p, seed):
+    def forward(ctx, qkv, start, lens, nh, p, seed, max_len=ATTN_SHORT_LEN):
         if qkv.is_cuda:
-            o, lse = _ops().attn_fwd(qkv, start, lens, nh, p, seed)
+            o, lse = _ops().attn_fwd(qkv, start, lens, nh, p, seed, max_len)
             ctx.save_for_backward(qkv, o, lse, start, lens)
         else:
-            o, _ = _ref_attn(qkv, start, lens, nh, p, seed)
+            o, _ = _ref_attn(qkv, start, lens, nh, p, seed, max_len)
             ctx.save_for_backward(qkv, start, lens)
-        ctx.cfg = (nh, p, seed)
+        ctx.cfg = (nh, p, seed, max_len)
         return o
 
     @staticmethod
     def backward(ctx, g):
-        nh, p, seed = ctx.cfg
+        nh, p, seed, max_len = ctx.cfg
         if g.is_cuda:
             qkv, o, lse, start, lens = ctx.saved_tensors
-            dqkv = _ops().attn_bwd(qkv, o, g.contiguous(), lse, start, lens, nh, p, seed)
+            dqkv = _ops().attn_bwd(qkv, o, g.contiguous(), lse, start, lens, nh, p, seed, max_len)
         else:
             qkv, start, lens = ctx.saved_tensors
             with torch.enable_grad():
                 x = qkv.detach().float().requires_grad_()
-                o, _ = _ref_attn(x, start, lens, nh, p, seed)
+                o, _ = _ref_attn(x, start, lens, nh, p, seed, max_len)
                 o.float().backward(g.float())
             dqkv = x.grad.to(qkv.dtype)
-        return dqkv, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None
 
 
 def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tensor] = None,
@@ -619,7 +631,7 @@ def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tens
         qkv = _Linear.apply(y, at.c_attn.weight, at.c_attn.bias)
         pa = _p(getattr(at, "attn_dropout", None), cfg.attn_pdrop)
         if fused_attn:
-            o = _Attention.apply(qkv, sstart, slen, nh, pa, seeds.next())
+            o = _Attention.apply(qkv, sstart, slen, nh, pa, seeds.next(), max_len)
         else:
             # token rows -> padded per-head q, k, v and back in one kernel each
             # (the layout change, the padding and, backward, the q/k/v

@@ -1035,7 +1035,11 @@ class FedModel:
                 "buffers": {n: b.detach().cpu() for n, b in self.model.named_buffers()},
                 # native dropout masks continue where they stopped
                 "dropout_seeds": {k: int(s.s) for k, (_, s) in self._seed_streams().items()},
-                "dp_ctr": int(getattr(self, "_dp_ctr", 0))}
+                "dp_ctr": int(getattr(self, "_dp_ctr", 0)),
+                # torch's generators (HF-module dropout, anything drawn from them)
+                "torch_rng": torch.get_rng_state(),
+                **({"cuda_rng": torch.cuda.get_rng_state(self.device)}
+                   if self.device.type == "cuda" else {})}
 
     def load_fed_state_dict(self, sd):
         self.round_idx = int(sd["round_idx"])
@@ -1051,6 +1055,10 @@ class FedModel:
                 bufs[n].copy_(b)
         if "dp_ctr" in sd:
             self._dp_ctr = int(sd["dp_ctr"])
+        if "torch_rng" in sd:
+            torch.set_rng_state(sd["torch_rng"])
+        if "cuda_rng" in sd and self.device.type == "cuda":
+            torch.cuda.set_rng_state(sd["cuda_rng"], self.device)
         seeds = sd.get("dropout_seeds", {})
         if seeds:
             from ..ops.transformer import _Seeds

@@ -28,6 +28,7 @@ from ..utils import (ScalarWriter, TableLogger, Timer, linear_decay_lambda, make
                      steps_per_epoch)
 from ..utils.trace import RoundProfiler
 from .losses import gpt2_loss_train, gpt2_loss_val
+from .cv import restore_driver_state, save_checkpoint
 
 
 def get_data_loaders(args, device, tokenizer=None):
@@ -51,16 +52,26 @@ def get_data_loaders(args, device, tokenizer=None):
 
 
 def run_batches(model, opt, sched, loader, training, args, writer=None, log_step0=0,
-                profiler=None):
+                profiler=None, progress=None):
     model.train(training)
     losses, accs = [], []
     ctx = dist.ctx()
     if training:
         spe = steps_per_epoch(args.local_batch_size, loader.dataset, args.num_workers)
         t0 = time.time()
-        for i, batch in enumerate(loader):
-            if i >= spe or (args.max_rounds and model.round_idx >= args.max_rounds):
+        # resumed mid-epoch: the sampler skips the rounds already processed
+        start = progress["iter"] if progress is not None else 0
+        if progress is not None:
+            progress["epoch_done"] = True
+        for i, batch in enumerate(loader, start=start):
+            if i >= spe:
                 break
+            if args.max_rounds and model.round_idx >= args.max_rounds:
+                if progress is not None:
+                    progress["epoch_done"] = False
+                break
+            if progress is not None:
+                progress["iter"] = i + 1
             sched.step()
             if args.local_batch_size == -1:
                 if len(np.unique(batch.client_ids)) < args.num_workers:
@@ -71,6 +82,9 @@ def run_batches(model, opt, sched, loader, training, args, writer=None, log_step
             opt.step()
             if profiler is not None:
                 profiler.step()
+            if (args.checkpoint_every and progress is not None
+                    and model.round_idx % args.checkpoint_every == 0):
+                save_checkpoint(model, args, progress)
             losses.append(loss)
             accs.append(acc)
             if writer is not None and ctx.is_main:
@@ -121,6 +135,15 @@ def main(args):
     fopt = FedOptimizer(opt, args, fed)
     spe = steps_per_epoch(args.local_batch_size, train_loader.dataset, args.num_workers)
     sched = torch.optim.lr_scheduler.LambdaLR(fopt, lr_lambda=linear_decay_lambda(args, spe))
+    progress = {"epoch": 0, "iter": 0}
+    if args.resume:
+        # weights, server / client state, accounting, dropout seed streams,
+        # sampler position and LR-schedule step (the cv driver's sidecar format)
+        sd = torch.load(args.resume, map_location="cpu", weights_only=True)
+        fed.load_fed_state_dict(sd)
+        progress = restore_driver_state(sd, train_loader, sched)
+    progress["loader"] = train_loader
+    progress["sched"] = sched
     log_dir = make_logdir(args)
     writer = ScalarWriter(log_dir) if ctx.is_main else None
     if ctx.is_main:
@@ -133,11 +156,13 @@ def main(args):
         if ctx.is_main:
             print({"nll": nll, "acc": acc, "ppl": math.exp(nll)})
         return fed
-    for epoch in range(math.ceil(args.num_epochs)):
+    for epoch in range(progress["epoch"], math.ceil(args.num_epochs)):
+        if epoch != progress["epoch"]:
+            progress["epoch"], progress["iter"] = epoch, 0
         d0 = fed.accountant.client_download.sum().item()
         u0 = fed.accountant.client_upload.sum().item()
         tl, ta = run_batches(fed, fopt, sched, train_loader, True, args, writer, epoch * int(spe),
-                             profiler)
+                             profiler, progress)
         ttime = timer()
         down = (fed.accountant.client_download.sum().item() - d0) / 2 ** 20
         up = (fed.accountant.client_upload.sum().item() - u0) / 2 ** 20
@@ -153,10 +178,14 @@ def main(args):
                 writer.add_scalar("validation/nll", nll, epoch)
                 writer.add_scalar("validation/acc", acc, epoch)
                 writer.add_scalar("validation/ppl", math.exp(min(nll, 50)), epoch)
+        if progress.get("epoch_done", True):
+            progress["epoch"], progress["iter"] = epoch + 1, 0
         if args.max_rounds and fed.round_idx >= args.max_rounds:
             break
     profiler.close(fed.timer)
     fed.finalize()
+    if args.do_checkpoint:
+        save_checkpoint(fed, args, progress)
     if writer is not None:
         writer.close()
     return fed

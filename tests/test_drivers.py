@@ -122,3 +122,24 @@ def test_gpt2_driver_native_kernels_gpu(mode, tmp_path, monkeypatch):
     fed = fed_train.main(argv)
     assert fed.round_idx == 3
     assert torch.isfinite(fed.w).all()
+
+
+def test_gpt2_resume_reproduces_uninterrupted_run(tmp_path, monkeypatch):
+    """GPT-2 driver (tiny, dropout on): checkpoint mid-epoch, resume, finish ==
+    one uninterrupted run, bitwise (sampler position, LR step, server state,
+    dropout generators all restored)."""
+    monkeypatch.chdir(tmp_path)
+    base = ["--dataset_name", "PERSONA", "--model", "GPT2DoubleHeads", "--synthetic",
+            "--num_clients", "16", "--num_workers", "4", "--local_batch_size", "2",
+            "--valid_batch_size", "2", "--device", "cpu", "--dtype", "fp32", "--gpt2_size", "tiny",
+            "--mode", "true_topk", "--error_type", "virtual", "--local_momentum", "0",
+            "--virtual_momentum", "0.9", "--k", "500", "--num_epochs", "1",
+            "--num_results_train", "1", "--port", "29615"]
+    full = fed_train.main(base + ["--max_rounds", "4"])
+    ck = str(tmp_path / "ck") + os.sep
+    fed_train.main(base + ["--max_rounds", "2", "--checkpoint", "--checkpoint_path", ck])
+    res = fed_train.main(base + ["--max_rounds", "4", "--resume",
+                                 ck + "GPT2DoubleHeads.fedstate.pt"])
+    assert res.round_idx == full.round_idx == 4
+    torch.testing.assert_close(res.w, full.w, rtol=0, atol=0)
+    torch.testing.assert_close(res.server.V, full.server.V, rtol=0, atol=0)

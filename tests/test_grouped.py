@@ -119,24 +119,47 @@ def test_engine_grouped_matches_per_client():
     torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-5)
 
 
+def _round0_rows(grouped: str, device: str, dtype: str):
+    """Each client's mean gradient of round 0 (identical weights on both
+    paths) as the engine hands it to the client tail -- before clipping,
+    weight decay, local momentum / error and top-k."""
+    rows = []
+    orig = FedModel._client_tail
+
+    def rec(self, g, work):
+        rows.append(g.detach().clone())
+        return orig(self, g, work)
+
+    FedModel._client_tail = rec
+    try:
+        fed, opt = _engine(grouped, device, dtype)
+        _rounds(fed, opt, device, R=1)
+    finally:
+        FedModel._client_tail = orig
+    return fed, torch.stack(rows)
+
+
 @pytest.mark.gpu
 def test_engine_grouped_matches_per_client_gpu():
-    """bf16 on the native kernels (GEMM 1x1, native 3x3, ghost BN, MIOpen
-    stem): grouped vs one client at a time."""
-    fa, oa = _engine("on", "cuda", "bf16")
-    wa, la = _rounds(fa, oa, "cuda")
-    assert fa._gbuf is not None
-    fb, ob = _engine("off", "cuda", "bf16")
-    wb, lb = _rounds(fb, ob, "cuda")
-    # round 0 at identical weights: close; round 1 after one bf16 update (local
-    # top-k near-ties may select differently): loosely
-    torch.testing.assert_close(la[0], lb[0], rtol=2e-2, atol=2e-2)
-    torch.testing.assert_close(la[1], lb[1], rtol=0.1, atol=0.1)
-    w0 = fa.w.new_zeros(fa.w.shape)
-    # the two paths round differently (bf16 batch shapes): updates agree to
-    # bf16 accuracy relative to their magnitude
-    dw = (wa - wb).abs().max() / (wb - w0).abs().max()
-    assert dw < 5e-2, dw
+    """bf16 on the native kernels (GEMM 1x1, native 3x3, ghost BN, MIOpen stem
+    with deterministic algorithms): the grouped path's per-client gradient
+    rows vs one client at a time, at the same weights (round 0).  Measured on
+    MI355X: relative errors 7e-6 .. 7e-5 (bf16 batch-shape rounding), and
+    the local top-k of every row picks the same coordinates.  (Later rounds
+    are NOT compared: one bf16 update later a top-k near-tie may resolve
+    differently and the trajectories legitimately separate.)"""
+    fa, ra = _round0_rows("on", "cuda", "bf16")
+    assert fa._gbuf is not None  # the grouped path ran
+    fb, rb = _round0_rows("off", "cuda", "bf16")
+    assert fb._gbuf is None
+    assert ra.shape == rb.shape == (4, fa.d)
+    for c in range(4):
+        err = ((ra[c] - rb[c]).norm() / rb[c].norm()).item()
+        assert err < 1e-3, (c, err)
+        # the transmit: the same k = 300 coordinates (local top-k of the row)
+        ia = set(ra[c].abs().topk(300).indices.tolist())
+        ib = set(rb[c].abs().topk(300).indices.tolist())
+        assert len(ia & ib) >= 297, (c, len(ia & ib))
 
 
 @pytest.mark.gpu

@@ -332,29 +332,51 @@ def test_fused_attention_reference_matches_sdpa_cpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("lens", [(37, 128, 1, 90),             # all-in-LDS kernels
+                                  (200, 64, 1, 129),            # flash kernels, ld 256
+                                  (512, 300, 17),               # ld 512
+                                  (1024, 5)])                   # GPT-2's n_positions
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_fused_attention_kernels_vs_reference_gpu(p):
+def test_fused_attention_kernels_vs_reference_gpu(p, lens):
+    """csrc/attention.hip forward (O, LSE) and backward (dQ, dK, dV) vs the
+    fp32 PyTorch reference of the same math and dropout hash, for the short
+    (<= 128 tokens) and the long (flash-style, up to 1024) kernel families."""
     from commefficient_amd._ext import ops
-    qkv, start, lens, nh = _attn_case("cuda")
-    o, lse = ops().attn_fwd(qkv, start, lens, nh, p, 1234)
-    ro, rlse = tx._ref_attn(qkv.cpu(), start.cpu(), lens.cpu(), nh, p, 1234)
+    qkv, start, lens_t, nh = _attn_case("cuda", lens=lens)
+    L = max(lens)
+    ld = tx.attn_lse_ld(L)
+    o, lse = ops().attn_fwd(qkv, start, lens_t, nh, p, 1234, L)
+    assert lse.numel() == len(lens) * nh * ld
+    ro, rlse = tx._ref_attn(qkv.cpu(), start.cpu(), lens_t.cpu(), nh, p, 1234, L)
     torch.testing.assert_close(o.float().cpu(), ro.float(), rtol=2e-2, atol=2e-2)
-    valid = torch.zeros(start.numel() * nh, 128, dtype=torch.bool)
-    for n, L in enumerate(lens.tolist()):
-        valid[n * nh:(n + 1) * nh, :L] = True
-    torch.testing.assert_close(lse.cpu().view(-1, 128)[valid], rlse.view(-1, 128)[valid],
+    valid = torch.zeros(len(lens) * nh, ld, dtype=torch.bool)
+    for n, Ln in enumerate(lens):
+        valid[n * nh:(n + 1) * nh, :Ln] = True
+    torch.testing.assert_close(lse.cpu().view(-1, ld)[valid], rlse.view(-1, ld)[valid],
                                rtol=1e-3, atol=1e-3)
     gout = (torch.randn(o.shape, generator=torch.Generator().manual_seed(5)) * 0.5).to(
         torch.bfloat16)
-    dq = ops().attn_bwd(qkv, o, gout.cuda(), lse, start, lens, nh, p, 1234)
+    dq = ops().attn_bwd(qkv, o, gout.cuda(), lse, start, lens_t, nh, p, 1234, L)
     x = qkv.cpu().float().requires_grad_()
-    rref, _ = tx._ref_attn(x, start.cpu(), lens.cpu(), nh, p, 1234)
+    rref, _ = tx._ref_attn(x, start.cpu(), lens_t.cpu(), nh, p, 1234, L)
     rref.float().backward(gout.float())
     for part in range(3):
         a = dq.float().cpu()[:, part * nh * 64:(part + 1) * nh * 64]
         r = x.grad[:, part * nh * 64:(part + 1) * nh * 64]
         rel = (a - r).norm() / r.norm()
         assert rel < 3e-2, (part, float(rel))
+
+
+def test_attention_reference_long_matches_sdpa_cpu():
+    """The reference at a flash-kernel length (LSE stride 256) == causal SDPA."""
+    import torch.nn.functional as F
+    qkv, start, lens, nh = _attn_case("cpu", lens=(200, 3), nh=2)
+    o, lse = tx._ref_attn(qkv, start, lens, nh, 0.0, 0, 200)
+    assert lse.numel() == 2 * 2 * 256
+    x = qkv[:200].float().view(200, 3, nh, 64).permute(1, 2, 0, 3)
+    ref = F.scaled_dot_product_attention(x[0], x[1], x[2], is_causal=True)
+    torch.testing.assert_close(o[:200].float(), ref.transpose(0, 1).reshape(200, -1),
+                               rtol=2e-2, atol=2e-2)
 
 
 @pytest.mark.gpu
