@@ -43,8 +43,6 @@ def main():
     p.add_argument("--conv", default="native", choices=["native", "miopen"],
                    help="3x3 conv units on the native MFMA kernels or on MIOpen")
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
-    p.add_argument("--graph", default="off", choices=["auto", "on", "off"],
-                   help="HIP-graph replay of the round (parallel/graph.py)")
     p.add_argument("--torch-profile", default=None,
                    help="after the timed steps, trace 5 more with torch.profiler into this dir")
     p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "0")),
@@ -54,8 +52,6 @@ def main():
                         "region (and once after it); exits non-zero on drift")
     b = p.parse_args()
 
-    if b.graph != "off":
-        commefficient_amd.request_graph_replay()  # must precede HIP initialisation
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != b.gpus:
         sys.exit(f"--gpus {b.gpus} but WORLD_SIZE={world}: for --gpus > 1 launch with "
@@ -80,7 +76,7 @@ def main():
             "--num_blocks", "20", "--num_clients", str(b.num_clients), "--num_workers", str(W),
             "--local_batch_size", "-1", "--weight_decay", "5e-4", "--dtype", "bf16",
             "--device", "cuda", "--encode", b.encode, "--seed", "21",
-            "--miopen_find", str(b.miopen_find), "--conv", b.conv, "--graph", b.graph]
+            "--miopen_find", str(b.miopen_find), "--conv", b.conv]
     if b.profile:
         argv += ["--profile_dir", "gpurun_out/bench_profile"]
     args = parse_args(argv=argv, probe_port=False)
@@ -199,7 +195,6 @@ def main():
             "backend": ctx.backend, "weights_checksum": checksum,
             **({"rehearsal": "gloo, ranks sharing one GPU"} if rehearsal and N > 1 else {}),
             "host_enqueue_ms_per_step": round(host_s / b.steps * 1000.0, 3),
-            "graph_replays": fed.graphs.replays if fed.graphs is not None else 0,
         }), flush=True)
     dist.barrier()
     dist.shutdown()

@@ -62,8 +62,8 @@ class DeviceImageSource:
     def gather_device(self, idx2: torch.Tensor):
         """Batch from a device int64 [2, B] = (rows, pre-mixed keys) with seed
         0 -- the same pixels as ``gather(rows, seed, keys)`` when
-        ``keys' = seed * 0x9E3779B97F4A7C15 + keys`` (mod 2^64), so a captured
-        HIP graph can replay it with new rows / seed from a static buffer."""
+        ``keys' = seed * 0x9E3779B97F4A7C15 + keys`` (mod 2^64), so the rows and
+        keys ride in the round's one packed H2D copy."""
         x = ops.augment_u8_nhwc(self.data, idx2[0], self.pad, self.flip, self.mean,
                                 self.inv_std, 0, self.out_bf16, idx2[1])
         return x, self.targets[idx2[0]]
@@ -122,8 +122,8 @@ class DeviceFedLoader:
                 keys = (pos.astype(np.uint64) + mix).view(np.int64)  # wraps mod 2^64
                 return np.stack([np.asarray(rows, dtype=np.int64)[pos], keys])
 
-            rb.graph_index = index
-            rb.graph_gather = src.gather_device
+            rb.device_index = index
+            rb.device_gather = src.gather_device
         return rb
 
 

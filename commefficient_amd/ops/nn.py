@@ -110,8 +110,7 @@ _IMAGE_CACHE_ON = [True]
 
 def set_conv_image_cache(on: bool) -> None:
     """Keep derived weight copies (conv images, the bf16 replica) across
-    passes; FedModel turns this off when HIP-graph replay may change the
-    weights without Python seeing it."""
+    passes; COMMEFF_WEIGHT_MIRRORS=0 turns this off (re-derive every pass)."""
     _IMAGE_CACHE_ON[0] = bool(on)
     _IMAGES.clear()
 

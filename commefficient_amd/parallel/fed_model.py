@@ -46,7 +46,6 @@ from ..ops import transformer as _tx
 from ..utils.logging import PhaseTimer
 from . import dist
 from .flat import FlatParams
-from .graph import RoundGraphs
 from .server import ServerState
 from .state import ByteAccountant, ClientStateStore
 
@@ -66,11 +65,11 @@ class RoundBatch:
         self.client_ids = np.asarray(client_ids, dtype=np.int64)
         self._take = take_fn
         self.n_inputs = n_inputs
-        # optional HIP-graph hooks (device loaders): graph_index(pos) -> host
-        # int64 [2, n] staged into a static buffer; graph_gather(idx2) -> the
-        # model inputs + targets computed from that buffer on the device
-        self.graph_index = None
-        self.graph_gather = None
+        # optional device-loader hooks: device_index(pos) -> host int64 [2, n]
+        # (rows, keys) shipped in the round's one packed H2D copy;
+        # device_gather(idx2) -> the model inputs + targets computed on the device
+        self.device_index = None
+        self.device_gather = None
 
     def __len__(self):
         return len(self.client_ids)
@@ -167,13 +166,9 @@ class FedModel:
         self._payload = None
         self._work = None  # separate work buffer for topk_down / fedavg
         self.last_round = {}
-        self.graphs = RoundGraphs(self) if self.device.type == "cuda" else None
         # bf16 conv-weight images kept across rounds and patched by sparse server
-        # steps (ops/nn.py) -- not with graph replay (the replayed server step
-        # changes the weights without Python seeing it)
-        # (COMMEFF_WEIGHT_MIRRORS=0: re-derive them every pass)
-        set_conv_image_cache((self.graphs is None or not self.graphs.enabled)
-                             and os.environ.get("COMMEFF_WEIGHT_MIRRORS", "1") != "0")
+        # steps (ops/nn.py); COMMEFF_WEIGHT_MIRRORS=0: re-derive them every pass
+        set_conv_image_cache(os.environ.get("COMMEFF_WEIGHT_MIRRORS", "1") != "0")
         self._acct_meta = None  # accounting meta staged with the round's inputs
         self._groupable = None  # grouped (per-client) weight gradients, ops/grouped.py
         self._gindex = None
@@ -386,13 +381,6 @@ class FedModel:
             mbs = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else 0
             if merged and 0 < mbs < int(sizes.sum()) and mbs % int(sizes[0]) != 0:
                 merged = False
-        if merged and self.graphs is not None and not self._fault_handling():
-            n_local = int(counts[my_slots].sum())
-            if self.graphs.usable(rb, n_local):
-                gkey = self.graphs.key(rb, n_local, W, B)
-                if self.graphs.seen(gkey) and getattr(self, "_n_metrics", None) is not None:
-                    return self._train_graph(gkey, rb, order, starts, my_slots, counts, W, B,
-                                             clients)
         # metric slots: [n_metrics, W] appended to the payload; allocate after
         # we know n_metrics -> run compute first into a local list
         with self.timer.phase("compute"):
@@ -435,7 +423,7 @@ class FedModel:
         metrics = payload[self.main_numel:].view(n_res, W).clone()
         dl, ul = self.accountant.round(clients, self.round_idx, meta=self._acct_meta)
         self._acct_meta = None
-        self._pending = (G, clients, False, 1.0 / B)
+        self._pending = (G, clients, 1.0 / B)
         overlapped = merged and self._overlap_round
         self._overlap_round = False
         if overlapped:
@@ -460,21 +448,6 @@ class FedModel:
         a = self.args
         return (getattr(a, "client_dropout", 0.0) > 0 or bool(getattr(a, "skip_nonfinite", 0))
                 or getattr(a, "inject_nonfinite_round", -1) >= 0)
-
-    def _train_graph(self, gkey, rb, order, starts, my_slots, counts, W, B, clients):
-        """The merged round through the captured HIP graphs (parallel/graph.py)."""
-        pos, slot_per_ex = self._merged_positions(order, starts, my_slots, counts)
-        n_res = self._n_metrics
-        payload = self.graphs.compute(gkey, rb, pos, slot_per_ex, counts, W, B, n_res)
-        dist.all_reduce_(payload)
-        G = payload[:self.main_numel]  # scaled by 1/B inside the server graph
-        metrics = payload[self.main_numel:].view(n_res, W).clone()
-        dl, ul = self.accountant.round(clients, self.round_idx)
-        self._pending = (G, clients, True, 1.0)
-        self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
-                           "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel()),
-                           "graph": True}
-        return [metrics[i] for i in range(n_res)] + [dl, ul]
 
     @staticmethod
     def _merged_positions(order, starts, my_slots, counts):
@@ -515,8 +488,7 @@ class FedModel:
 
     def _merged_body(self, get_data, slots_t, n_t, n_local: int, W: int, payload: torch.Tensor,
                      capture: bool = False):
-        """Whole merged-client round up to the all-reduce, on device inputs only
-        (captured into a HIP graph by parallel/graph.py)."""
+        """Whole merged-client round up to the all-reduce, on device inputs only."""
         self.flat.zero_grad()
         data = get_data()
         inputs, targets = data[:-1], data[-1]
@@ -537,10 +509,10 @@ class FedModel:
         n_local = len(pos)
         self.flat.zero_grad()
         packed = None
-        if rb.graph_index is not None and self.device.type == "cuda":
+        if rb.device_index is not None and self.device.type == "cuda":
             # every per-round host array in ONE pinned H2D copy: (rows, keys),
             # client slots, client sizes, accounting meta
-            idx2 = rb.graph_index(pos)
+            idx2 = rb.device_index(pos)
             meta = self.accountant.round_meta(clients)
             host = np.concatenate([idx2.reshape(-1), slot_per_ex, counts.astype(np.int64), meta])
             dev = dist.h2d(host, self.device)
@@ -550,7 +522,7 @@ class FedModel:
                 parts.append(dev[o:o + n])
                 o += n
             packed = parts
-            data = rb.graph_gather(parts[0].view(2, n_local))
+            data = rb.device_gather(parts[0].view(2, n_local))
             self._acct_meta = parts[3]
         else:
             data = rb.take(pos)
@@ -964,19 +936,13 @@ class FedModel:
             self.fedavg_lr = float(lr)
         if self._pending is None:
             return  # e.g. the reference's "HACK STEP" before the first round
-        G, clients, via_graph, gscale = self._pending
+        G, clients, gscale = self._pending
         self._pending = None
         if getattr(self.args, "skip_nonfinite", 0) and not bool(torch.isfinite(G).all()):
             # failure detection: a NaN/Inf in the aggregate (a diverged or faulty
             # client) would poison V, E and the weights for good -> drop the round
             self.skipped_rounds += 1
             self.last_round["skipped_nonfinite"] = True
-            self.round_idx += 1
-            return
-        if via_graph:
-            if self.accountant.hist_for(self.round_idx).data_ptr() != self.graphs.hist_ptr:
-                self.graphs.invalidate_server()  # histogram grew: recapture
-            self.graphs.server(G, float(lr), self.round_idx)
             self.round_idx += 1
             return
         with self.timer.phase("server"):

@@ -97,14 +97,13 @@ class ServerState:
         self.noise_round = 0
 
     def update(self, G: torch.Tensor, lr, w: torch.Tensor, last_mod: torch.Tensor, round_idx: int,
-               client_state=None, participating=None, step: Optional[torch.Tensor] = None,
-               hist: Optional[torch.Tensor] = None, gscale: float = 1.0):
+               client_state=None, participating=None, hist: Optional[torch.Tensor] = None,
+               gscale: float = 1.0):
         """Apply one server step.  ``gscale * G`` is the summed transmit / B
-        (the scale is folded into the momentum kernel).  ``step`` (device int32 [2] = lr bits, round) replaces the
-        scalar lr / round_idx when the update runs inside a captured HIP
-        graph (parallel/graph.py); ``hist`` is the accountant's change histogram,
-        updated with the stamps.  Returns (idx, vals) for sparse modes (the
-        un-scaled update), else None."""
+        (the scale is folded into the momentum kernel); ``hist`` is the
+        accountant's change histogram, updated with the stamps.  Returns
+        (idx, vals) for sparse modes (the un-scaled update), else None."""
+        step = None  # device-side lr / round (ops' graph-capture form): unused
         a = self.args
         rho = float(a.virtual_momentum)
         lr_s, lr_v = (lr, None) if not torch.is_tensor(lr) else (0.0, lr)
@@ -113,8 +112,6 @@ class ServerState:
         # here on, unless the step is sparse (then the k changed coordinates
         # are patched into them)
         img_sync = weights_begin_update(w)
-        if step is not None:  # captured graph step: no Python bookkeeping at replay
-            img_sync = []
         if mode == "sketch":
             et = a.error_type
             if et == "virtual":
@@ -125,8 +122,7 @@ class ServerState:
                 src = self.V
             sk = self.sketch.like(src)
             ctx = dist.ctx()
-            if (ctx.world_size > 1 and step is None
-                    and getattr(a, "shard_unsketch", "on") == "on"):
+            if ctx.world_size > 1 and getattr(a, "shard_unsketch", "on") == "on":
                 # every rank estimates 1/N of the coordinates and the k-lists
                 # are merged (bitwise the replicated result, ops/sketch.py)
                 idx, vals = sk.unsketch_sparse_sharded(a.k, ctx.rank, ctx.world_size,

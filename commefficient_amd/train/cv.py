@@ -40,9 +40,11 @@ def get_datasets(args):
     name = args.dataset_name or "CIFAR10"
     args.dataset_name = name
     if args.synthetic:
+        hard = getattr(args, "synthetic_difficulty", "easy") == "hard"
         tr = make_synthetic(name, train=True, do_iid=args.do_iid, num_clients=args.num_clients,
-                            size=args.synthetic_size, seed=args.seed)
-        te = make_synthetic(name, train=False, size=args.synthetic_size, seed=args.seed)
+                            size=args.synthetic_size, seed=args.seed, hard=hard)
+        te = make_synthetic(name, train=False, size=args.synthetic_size, seed=args.seed,
+                            hard=hard)
         return tr, te
     cls = DATASETS[name]
     tr = cls(args.dataset_dir, name, None, args.do_iid, args.num_clients, train=True,

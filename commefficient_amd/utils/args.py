@@ -128,6 +128,10 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="use synthetic data shaped like --dataset_name (no files needed)")
     g.add_argument("--synthetic_size", type=int, default=None,
                    help="number of synthetic training examples (default: real dataset size)")
+    g.add_argument("--synthetic_difficulty", choices=["easy", "hard"], default="easy",
+                   help="synthetic images: 'easy' = class pattern + small noise; 'hard' = "
+                        "weaker class pattern + a distractor class pattern + strong noise "
+                        "(not separable by eye; convergence runs)")
     g.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
                    help="compute dtype of forward/backward (master weights stay fp32)")
     g.add_argument("--merge_clients", choices=["auto", "on", "off"], default="auto",
@@ -206,10 +210,6 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="native GPT-2 path: token-wise ops (embeddings, GEMMs, LayerNorm/"
                         "GELU junctions) on the real tokens only, attention on the padded "
                         "layout (exact: right padding never reaches a real token)")
-    g.add_argument("--graph", choices=["auto", "on", "off"], default="off",
-                   help="replay merged-client rounds from captured HIP graphs "
-                        "(parallel/graph.py) once a round geometry repeats (auto/on: "
-                        "eligible configurations; measured throughput-neutral for ResNet-9)")
     g.add_argument("--gpt2_size", choices=["small", "mini", "tiny"], default="small",
                    help="GPT-2 architecture: 'small' = 124M GPT-2 (reference); 'mini' (2 x 256, "
                         "4 heads: native kernels) and 'tiny' (2 x 64) for tests")
@@ -269,7 +269,4 @@ def finalize_args(args, probe_port: bool = True):
         while is_port_in_use(args.port):
             args.port += int(rng.randint(1, 1000))
     validate_args(args)
-    if getattr(args, "graph", "off") != "off" and args.device != "cpu":
-        from .. import request_graph_replay
-        request_graph_replay()  # before the HIP runtime initialises
     return args

@@ -619,7 +619,7 @@ def test_kept_conv_images_match_fresh_prep(mode):
                             "--mode", mode, "--local_momentum", "0", "--virtual_momentum", "0.9",
                             "--k", "3000", "--num_rows", "5", "--num_cols", "50000",
                             "--num_clients", "40", "--num_workers", "8", "--local_batch_size", "-1",
-                            "--device", "cuda", "--graph", "off"] + extra, probe_port=False)
+                            "--device", "cuda"] + extra, probe_port=False)
     ds = make_synthetic("CIFAR10", train=True, num_clients=40, size=400, seed=0)
     loader = DeviceFedLoader(ds, 8, -1, "cuda", seed=0)
     model = models.build_model(args, 10)

@@ -134,8 +134,9 @@ def test_bench_two_ranks_one_gpu():
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
            "--clients-per-gpu", "20", "--num-clients", "2000"]
-    out = subprocess.run(cmd, env=env, check=True, timeout=300, capture_output=True, text=True,
-                         cwd=root).stdout
+    res = subprocess.run(cmd, env=env, timeout=300, capture_output=True, text=True, cwd=root)
+    assert res.returncode == 0, res.stderr[-4000:]
+    out = res.stdout
     lines = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
     assert len(lines) == 1, out
     r = lines[0]

@@ -429,8 +429,7 @@ def test_bf16_replica_follows_sparse_server_steps_gpu(mode):
              if mode == "sketch" else [])
     args = parse_args(argv=["--mode", mode, "--local_momentum", "0", "--virtual_momentum", "0.9",
                             "--num_workers", "2", "--local_batch_size", "2", "--device", "cuda",
-                            "--dtype", "bf16", "--num_clients", "2", "--weight_cast", "once",
-                            "--graph", "off"] + extra, probe_port=False)
+                            "--dtype", "bf16", "--num_clients", "2", "--weight_cast", "once"] + extra, probe_port=False)
     fed = FedModel(model, gpt2_loss_train, args, num_clients=2)
     opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), args, fed)
     flat = fed.flat
