@@ -1,0 +1,66 @@
+"""GPT-2-size dense planned encode / query with coordinate windows
+(COMMEFF_CS_WINDOW_MB, COMMEFF_CS_Q1_SPLITS); one subprocess per setting.
+Checks the windowed encode is deterministic and close to the unwindowed one."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+CHILD = r'''
+import sys, json, torch
+sys.path.insert(0, %r)
+from commefficient_amd.ops import CSVec
+def timeit(fn, n=10):
+    for _ in range(2): fn()
+    ts = []
+    for _ in range(n):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(); fn(); b.record(); b.synchronize(); ts.append(a.elapsed_time(b) * 1e3)
+    ts.sort(); return ts[len(ts) // 2]
+d, r, c = 124444417, 5, 500000
+g = torch.Generator(device="cuda").manual_seed(0)
+v = torch.randn(d, device="cuda", generator=g)
+w = torch.randn(d, device="cuda", generator=g)
+sk = CSVec(d, c, r, device="cuda", numBlocks=20, kernel="planned")
+sk.accumulateVec(v, 1.0, w, 1e-3, overwrite=True)
+t1 = sk.table.clone()
+sk.accumulateVec(v, 1.0, w, 1e-3, overwrite=True)
+det = bool(torch.equal(t1, sk.table))
+enc = timeit(lambda: sk.accumulateVec(v, 1.0, w, 1e-3, overwrite=True))
+est = sk.query()
+qry = timeit(lambda: sk.query())
+torch.save({"table": sk.table.cpu(), "est": est[:5000000].cpu()}, sys.argv[1])
+print(json.dumps({"encode_us": enc, "query_us": qry, "deterministic": det}))
+''' % ROOT
+
+
+def main():
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    settings = [("0", "0"), ("48", "1"), ("96", "1"), ("96", "2"), ("160", "1"), ("160", "4"),
+                ("256", "2")]
+    ref = None
+    for mb, sp in settings:
+        env = dict(os.environ, COMMEFF_CS_WINDOW_MB=mb, COMMEFF_CS_Q1_SPLITS=sp)
+        f = os.path.join(out, f"cw_{mb}_{sp}.pt")
+        res = subprocess.run([sys.executable, "-c", CHILD, f], env=env, capture_output=True,
+                             text=True, timeout=300)
+        line = [x for x in res.stdout.splitlines() if x.startswith("{")]
+        if res.returncode != 0 or not line:
+            print("FAIL", mb, sp, res.stderr[-2000:])
+            sys.exit(1)
+        r = json.loads(line[0])
+        import torch
+        t = torch.load(f, weights_only=True)
+        if ref is None:
+            ref = t
+        rel = float((t["table"] - ref["table"]).norm() / ref["table"].norm())
+        r.update(window_mb=mb, q1_splits=sp, table_rel_vs_first=rel,
+                 est_equal_first=bool(torch.equal(t["est"], ref["est"])))
+        os.remove(f)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
