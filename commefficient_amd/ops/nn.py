@@ -30,8 +30,30 @@ class _ReluMaxPool(torch.autograd.Function):
         return _ops().relu_maxpool_backward(gy.to(torch.bfloat16), idx, ctx.k), None
 
 
+# ``stock_ops()``: every model op takes its plain PyTorch composition (no
+# native kernels, no flat-buffer gradient sinks) -- for torch.func transforms
+# (vmap over per-client weight copies in the batched FedAvg local SGD,
+# parallel/fed_model.py), which the native autograd Functions do not support
+_STOCK = [False]
+
+
+class stock_ops:
+    def __enter__(self):
+        self.prev = _STOCK[0]
+        _STOCK[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _STOCK[0] = self.prev
+        return False
+
+
+def stock_active() -> bool:
+    return _STOCK[0]
+
+
 def fused_ok(x: torch.Tensor, k: int) -> bool:
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and k in (2, 4)
+    return (not _STOCK[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and k in (2, 4)
             and x.shape[1] % 8 == 0 and x.shape[2] % k == 0 and x.shape[3] % k == 0
             and x.is_contiguous(memory_format=torch.channels_last))
 
@@ -147,7 +169,7 @@ class prepared_conv_weights:
         self.keys = []
 
     def __enter__(self):
-        if self.weights and _CONV_BACKEND[0] == "native":
+        if self.weights and _CONV_BACKEND[0] == "native" and not _STOCK[0]:
             ws = [w.detach() for w in self.weights]
             capturing = torch.cuda.is_current_stream_capturing() or not _IMAGE_CACHE_ON[0]
             ck = tuple(w.data_ptr() for w in ws)
@@ -382,7 +404,8 @@ def residual_unit(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> torch.
 
 
 def conv3x3_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    return (_CONV_BACKEND[0] == "native" and x.is_cuda and x.dtype == torch.bfloat16
+    return (_CONV_BACKEND[0] == "native" and not _STOCK[0] and x.is_cuda
+            and x.dtype == torch.bfloat16
             and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
             and weight.dtype == torch.float32 and weight.dim() == 4
             and tuple(weight.shape[2:]) == (3, 3) and weight.shape[1] == x.shape[1]
@@ -433,7 +456,8 @@ class _InputConv(torch.autograd.Function):
 def input_conv_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
     """The augmentation kernel's 3-channel bf16 batch (4-channel pixel stride)
     into a [64, 3, 3, 3] conv."""
-    if not (_CONV_BACKEND[0] == "native" and x.is_cuda and x.dtype == torch.bfloat16
+    if not (_CONV_BACKEND[0] == "native" and not _STOCK[0] and x.is_cuda
+            and x.dtype == torch.bfloat16
             and x.dim() == 4 and x.shape[1] == 3 and not x.requires_grad
             and weight.dtype == torch.float32 and tuple(weight.shape) == (64, 3, 3, 3)):
         return False
@@ -478,7 +502,7 @@ class _FusedHead(torch.autograd.Function):
 
 
 def head_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+    return (not _STOCK[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 8 == 0
             and x.shape[2] * x.shape[3] <= 255 and weight.dtype == torch.float32
             and weight.dim() == 2 and weight.shape[1] == x.shape[1] and weight.shape[0] <= 128)
@@ -541,7 +565,7 @@ class _GhostBN(torch.autograd.Function):
 
 
 def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+    return (not _STOCK[0] and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and x.is_contiguous(memory_format=torch.channels_last)
             and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
             and (weight is None or weight.dtype == torch.float32))
@@ -580,7 +604,7 @@ class _FusedCE(torch.autograd.Function):
 
 def cross_entropy_correct(logits: torch.Tensor, targets: torch.Tensor):
     """(per-example CE loss f32, top-1 correct f32) of ``logits`` [B, C]."""
-    if (logits.is_cuda and logits.dim() == 2 and targets.dtype == torch.int64
+    if (not _STOCK[0] and logits.is_cuda and logits.dim() == 2 and targets.dtype == torch.int64
             and logits.dtype in (torch.bfloat16, torch.float32)):
         return _FusedCE.apply(logits, targets)
     per_ex = F.cross_entropy(logits.float(), targets, reduction="none")
@@ -830,7 +854,7 @@ def _gpu_bf16_nhwc(x: torch.Tensor) -> bool:
 def conv2d_native_kind(x: torch.Tensor, weight: torch.Tensor, stride, padding, dilation,
                        groups) -> str:
     """Which native path serves this convolution: "1x1", "3x3" or "" (MIOpen)."""
-    if _CONV_BACKEND[0] != "native" or groups != 1 or not _gpu_bf16_nhwc(x):
+    if _CONV_BACKEND[0] != "native" or _STOCK[0] or groups != 1 or not _gpu_bf16_nhwc(x):
         return ""
     if weight.dtype != torch.float32 or weight.dim() != 4 or weight.shape[1] != x.shape[1]:
         return ""

@@ -362,6 +362,9 @@ def native_ok(tr, input_ids: torch.Tensor) -> bool:
     cfg = getattr(tr, "config", None)
     if cfg is None or getattr(cfg, "model_type", "") != "gpt2" or not hasattr(tr, "h"):
         return False
+    from .nn import stock_active
+    if stock_active():  # torch.func transforms: the HF modules
+        return False
     H = cfg.n_embd
     return (tr.wte.weight.dtype == torch.bfloat16
             and (not input_ids.is_cuda or _native_hidden_size(H))

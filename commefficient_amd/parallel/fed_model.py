@@ -659,6 +659,8 @@ class FedModel:
         with (self._autocast() if shared_w else nullcontext()), prep:
             if shared_w and self._grouped_ok(counts[my_slots]):
                 msum = self._grouped_loop(rb, order, starts, my_slots, mine, counts, W, out)
+            elif a.mode == "fedavg" and self._fedavg_batched_ok(counts[my_slots]):
+                msum = self._fedavg_batched(rb, order, starts, my_slots, mine, counts, W, out)
             else:
                 msum = self._per_client_loop(rb, order, starts, my_slots, mine, counts, W, out)
         if msum is None:  # no clients on this rank this round
@@ -894,6 +896,114 @@ class FedModel:
         new.index_add_(0, idx, vals)
         self.client_state.put("weights", c, new)
         return new
+
+    # ------------------------------------------------ batched FedAvg clients
+    def _fedavg_batched_ok(self, sizes: np.ndarray) -> bool:
+        """Local SGD of this rank's clients in lockstep (``_fedavg_batched``):
+        equal client sizes (one vmapped batch shape per step), no worker-side
+        DP (its noise stream is per client and sequential), no bf16 replica."""
+        a = self.args
+        mode = getattr(a, "fedavg_batched", "auto")
+        if mode == "off" or a.do_test or len(sizes) < 2 or a.do_dp or self._shadow is not None:
+            return False
+        ok = bool(np.all(sizes == sizes[0])) and int(sizes[0]) > 0
+        if mode == "on" and not ok:
+            raise ValueError("--fedavg_batched on needs equal client sizes and no --dp")
+        return ok
+
+    def _fedavg_batched(self, rb, order, starts, my_slots, mine, counts, W, out):
+        """FedAvg local SGD (fed_worker.py:61-113) of G clients at once.
+
+        Every client starts from the server weights and takes the same number
+        of local steps on its own batches, so the G trajectories run in
+        lockstep: one [G, d] stack of per-client weights, and per step ONE
+        ``torch.func.vmap(grad(loss))`` over (weights, BatchNorm buffers,
+        batch) -- the G forward/backward passes become single batched kernels
+        (grouped convolutions, batched GEMMs) instead of G launch-bound passes
+        of a few images each.  The client tail of every step is applied row
+        by row in closed form: clipping to max_grad_norm, weight decay
+        (wd / W) at the client's current weights (utils.py:257-258,
+        fed_worker.py:288-292), then w_c -= lr * decay^step * g_c.  The upload
+        is sum_c n (w_0 - w_c).  The model's ops run their plain PyTorch
+        composition here (``ops.nn.stock_ops``).  BatchNorm: each client
+        normalises with its own batch statistics and updates its own copy of
+        the running statistics; the model keeps their mean afterwards (the
+        reference's worker model accumulated them client after client)."""
+        from torch.func import grad, vmap
+        from torch.nn.utils.stateless import _reparametrize_module
+        from ..ops.nn import stock_ops
+        a = self.args
+        n = int(counts[my_slots[0]])
+        bs = a.fedavg_batch_size if a.fedavg_batch_size != -1 else n
+        lr = self.fedavg_lr
+        # per-client weights + gradients + vmapped activations
+        cap = max(2, int(a.grouped_gb * 2 ** 30) // (12 * self.d))
+        per_pass = max(1, min(cap, len(mine)))
+        fl = self.flat
+        names = [nm for nm, p in self.model.named_parameters() if p.requires_grad]
+        frozen = {nm: p.detach() for nm, p in self.model.named_parameters() if not p.requires_grad}
+        bufs0 = dict(self.model.named_buffers())
+        model, loss_fn, args = self.model, self.compute_loss_train, a
+
+        def client_loss(params, buffers, *xy):
+            inputs, targets = xy[:-1], xy[-1]
+            # (torch.func.functional_call's reparametrisation, around the loss
+            # function: compute_loss calls the model itself)
+            with _reparametrize_module(model, {**params, **frozen, **buffers}):
+                per_ex, mets = loss_fn(model, tuple(inputs), targets, args)
+            per_ex = per_ex.float()
+            return per_ex.mean(), (per_ex.detach().mean(),
+                                   tuple(m.detach().float().mean() for m in mets))
+
+        gfn = vmap(grad(client_loss, has_aux=True))
+        loss_rows, met_rows, slot_rows = [], [], []
+        for p0 in range(0, len(mine), per_pass):
+            slots = my_slots[p0:p0 + per_pass]
+            Gp = len(slots)
+            pos = np.concatenate([order[starts[s]:starts[s + 1]] for s in slots])
+            data = rb.take(pos)
+            xs = [t.reshape((Gp, n) + tuple(t.shape[1:])) for t in data]
+            Wg = self.w.unsqueeze(0).repeat(Gp, 1)
+            bufs = {k: b.detach().unsqueeze(0).repeat((Gp,) + (1,) * b.dim()).clone()
+                    for k, b in bufs0.items()}
+            step = 0
+            ls, ms = [], None
+            with stock_ops(), self._autocast(cache=False):
+                for _ in range(a.num_fedavg_epochs):
+                    for s0 in range(0, n, bs):
+                        s1 = min(n, s0 + bs)
+                        params = {nm: Wg[:, o:o + k].view((Gp,) + tuple(shp))
+                                  for nm, o, k, shp in zip(names, fl.offsets, fl.numels, fl.shapes)}
+                        g, (l, mets) = gfn(params, bufs, *[x[:, s0:s1] for x in xs])
+                        Gg = torch.cat([g[nm].float().reshape(Gp, -1) for nm in names], dim=1)
+                        if a.max_grad_norm is not None:
+                            nrm = Gg.norm(dim=1, keepdim=True)
+                            Gg.mul_(torch.where(nrm > a.max_grad_norm,
+                                                a.max_grad_norm / nrm, torch.ones_like(nrm)))
+                        if a.weight_decay != 0:
+                            Gg.add_(Wg, alpha=a.weight_decay / a.num_workers)
+                        Wg.add_(Gg, alpha=-lr * (a.fedavg_lr_decay ** step))
+                        ls.append(l)
+                        ms = list(mets) if ms is None else [x + y for x, y in zip(ms, mets)]
+                        step += 1
+            # upload: sum_c n (w_0 - w_c)
+            out.add_(self.w, alpha=float(n * Gp))
+            out.sub_(Wg.sum(dim=0), alpha=float(n))
+            with torch.no_grad():  # running statistics: the clients' mean
+                for k, b in bufs0.items():
+                    if b.is_floating_point():
+                        b.copy_(bufs[k].mean(dim=0))
+                    else:
+                        b.copy_(bufs[k].max(dim=0).values)
+            loss_rows.append(torch.stack(ls).mean(dim=0))
+            met_rows.append([m / step for m in ms])
+            slot_rows.append(slots)
+        msum = torch.zeros(1 + len(met_rows[0]), W, device=self.device)
+        slots_t = torch.from_numpy(np.concatenate(slot_rows).astype(np.int64)).to(self.device)
+        msum[0].index_copy_(0, slots_t, torch.cat(loss_rows))
+        for i in range(len(met_rows[0])):
+            msum[1 + i].index_copy_(0, slots_t, torch.cat([m[i] for m in met_rows]))
+        return msum
 
     def _fedavg_client(self, inputs, targets, n):
         """Local SGD on one client's data (fed_worker.py:61-113)."""

@@ -79,6 +79,11 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     p.add_argument("--num_fedavg_epochs", type=int, default=1)
     p.add_argument("--fedavg_batch_size", type=int, default=-1)
     p.add_argument("--fedavg_lr_decay", type=float, default=1)
+    p.add_argument("--fedavg_batched", choices=["auto", "on", "off"], default="auto",
+                   help="multi-step FedAvg local SGD of a rank's clients at once (torch.func.vmap "
+                        "over per-client weight copies, parallel/fed_model.py) instead of one "
+                        "client after another; auto: when the clients have equal sizes and no "
+                        "worker-side DP is on")
     p.add_argument("--error_type", choices=ERROR_TYPES, default="none")
     p.add_argument("--lr_scale", type=float, default=default_lr)
     p.add_argument("--pivot_epoch", type=float, default=5)

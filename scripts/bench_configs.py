@@ -46,13 +46,22 @@ def cfg_args(name, N, b):
                    "--virtual_momentum", "0.9", "--num_clients", "10000", "--num_workers", str(W),
                    "--local_batch_size", "-1", "--fedavg_batch_size", "-1",
                    "--num_fedavg_epochs", "1", "--batchnorm"]
+    if name == "cifar100_fedavg_local":
+        # multi-step local SGD: 5 local epochs of full-batch steps per client
+        W = b.clients or 100 * N
+        return W, ["--dataset_name", "CIFAR100", "--synthetic", "--model", "ResNet18",
+                   "--mode", "fedavg", "--error_type", "none", "--local_momentum", "0",
+                   "--virtual_momentum", "0.9", "--num_clients", "10000", "--num_workers", str(W),
+                   "--local_batch_size", "-1", "--fedavg_batch_size", "-1",
+                   "--num_fedavg_epochs", "5", "--batchnorm"]
     raise ValueError(name)
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--config", required=True,
-                   choices=["imagenet_local_topk", "gpt2_sketch", "cifar100_fedavg"])
+                   choices=["imagenet_local_topk", "gpt2_sketch", "cifar100_fedavg",
+                            "cifar100_fedavg_local"])
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--clients", type=int, default=0, help="clients per round (total)")
