@@ -793,6 +793,43 @@ at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
   return conv3x3_fwd_impl(x, w, relu, mask, addend, nullptr);
 }
 
+// y = conv3x3(x, w) and y_dual = y where dual_mask > 0 else 0 (two outputs of
+// one epilogue: a dgrad and the relu backward of its consumer's other input)
+std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_dual_hip(const at::Tensor& x, const at::Tensor& w,
+                                                        const at::Tensor& dual_mask) {
+  check_nhwc_bf16(x, "conv3x3_dual: x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 &&
+                  w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C,
+              "conv3x3_dual: w must be contiguous bf16 [K, 3, 3, C]");
+  const int64_t K = w.size(0);
+  TORCH_CHECK(conv3x3_supported(static_cast<int>(C), static_cast<int>(K)),
+              "conv3x3_dual: C and K must be multiples of 64");
+  TORCH_CHECK(N * H * W < (1ll << 31), "conv3x3_dual: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, K, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto yd = at::empty_like(y, y.options().memory_format(at::MemoryFormat::ChannelsLast));
+  ConvFwdArgs a{};
+  a.x = bf16_ptr(x);
+  a.w = bf16_ptr(w);
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.mask = nullptr;
+  a.addend = nullptr;
+  a.y_pre = nullptr;
+  a.pool_idx = nullptr;
+  a.dual_mask = opt_like(c10::optional<at::Tensor>(dual_mask), y, "conv3x3_dual: dual_mask");
+  a.y_dual = reinterpret_cast<uint16_t*>(yd.data_ptr());
+  a.P = static_cast<int>(N * H * W);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.relu = 0;
+  a.pool = 0;
+  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  return {y, yd};
+}
+
 // dgrad with the relu + 2x2 max-pool backward of the layer below fused into
 // the epilogue: y [N, K, 2H, 2W] (channels_last) = unpool(conv3x3(x, w) +
 // addend) with idx [N, K, H, W] the pool's window codes (conv3x3_fwd_pool2)
@@ -1634,6 +1671,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("relu_maxpool_backward(Tensor gy, Tensor idx, int k) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool relu, Tensor? mask=None, Tensor? addend=None) -> Tensor");
   m.def("conv3x3_fwd_unpool(Tensor x, Tensor w, Tensor? addend, Tensor idx) -> Tensor");
+  m.def("conv3x3_fwd_dual(Tensor x, Tensor w, Tensor dual_mask) -> (Tensor, Tensor)");
   m.def("conv3x3_fwd_pool2(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def("head_fwd(Tensor x, Tensor w, Tensor targets, float scale) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("head_bwd(Tensor gl, Tensor gunit, Tensor w, Tensor pooled, Tensor codes, int H, int W, float scale, "
@@ -1736,6 +1774,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("relu_maxpool_backward", &relu_maxpool_backward_hip);
   m.impl("conv3x3_fwd", &conv3x3_fwd_hip);
   m.impl("conv3x3_fwd_unpool", &conv3x3_fwd_unpool_hip);
+  m.impl("conv3x3_fwd_dual", &conv3x3_fwd_dual_hip);
   m.impl("conv3x3_fwd_pool2", &conv3x3_fwd_pool2_hip);
   m.impl("head_fwd", &head_fwd_hip);
   m.impl("head_bwd", &head_bwd_hip);

@@ -216,6 +216,18 @@ __device__ __forceinline__ void conv_fwd_epilogue(const ConvFwdArgs& a, f32x16_t
       continue;
     }
     *reinterpret_cast<v4u*>(a.y + o) = out;
+    if (a.y_dual != nullptr) {
+      const v4u m = *reinterpret_cast<const v4u*>(a.dual_mask + o);
+      v4u od;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const uint32_t lo = m[h] & 0xffffu, hi = m[h] >> 16;
+        // keep where mask > 0: sign bit clear and not +0 (csrc relu_mask)
+        od[h] = (((lo & 0x8000u) == 0u && lo != 0u) ? (out[h] & 0xffffu) : 0u) |
+                (((hi & 0x8000u) == 0u && hi != 0u) ? (out[h] & 0xffff0000u) : 0u);
+      }
+      *reinterpret_cast<v4u*>(a.y_dual + o) = od;
+    }
   }
   }  // pass
 }

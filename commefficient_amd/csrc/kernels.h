@@ -185,6 +185,11 @@ struct ConvFwdArgs {
   // un-pooled tensor, each value routed to its code's window position (zeros
   // elsewhere) -- the relu + max-pool backward fused into the dgrad epilogue
   const uint8_t* unpool_idx = nullptr;
+  // optional [P, K]: also write y_dual = y where dual_mask > 0 else 0 (the
+  // relu backward of the layer that produced this conv's input, for the
+  // consumer of that layer's other input gradient -- ops/nn.py _MaskLink)
+  const uint16_t* dual_mask = nullptr;
+  uint16_t* y_dual = nullptr;
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]

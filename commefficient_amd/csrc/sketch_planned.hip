@@ -43,6 +43,15 @@ namespace {
 
 constexpr int kLdsBytes = 160 * 1024;
 
+// Logical block order for the run-gathering passes: blocks are dealt
+// round-robin over the 8 XCDs, so neighbouring tiles (encode P2) or chunks
+// (query Q2) -- whose runs share 128-byte lines -- would read those lines
+// through different L2s; remapped, logical blocks l and l+1 run on one XCD.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t bid, uint32_t nwg) {
+  const uint32_t xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 __device__ __forceinline__ float signed_v(float v, uint32_t info) {
   return (info & 0x8000u) ? -v : v;
 }
@@ -208,7 +217,8 @@ enc_p2_dense_fx_kernel(float* __restrict__ table, long long* __restrict__ slab,
                        uint32_t num_chunks, uint32_t splits, bool overwrite) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* T = reinterpret_cast<unsigned long long*>(smem);
-  const uint32_t t = blockIdx.x / splits, s = blockIdx.x - t * splits;
+  const uint32_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const uint32_t t = lb / splits, s = lb - t * splits;
   const uint32_t nt = blockDim.x;
   const float m = gmax[0];
   const bool finite = fx_finite(m);
@@ -311,7 +321,7 @@ enc_p2_kernel(float* __restrict__ table, const float* __restrict__ vals,
   float* S = reinterpret_cast<float*>(smem);
   int32_t* msrc = reinterpret_cast<int32_t*>(S + kPlanSegCap);
   int32_t* mpos = msrc + num_chunks;
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = xcd_block(blockIdx.x, gridDim.x);
   const uint32_t nt = blockDim.x;
   const int32_t* psrc = p2_src + static_cast<size_t>(t) * num_chunks;
   const int32_t* ppos = p2_pos + static_cast<size_t>(t) * (num_chunks + 1);
@@ -392,7 +402,8 @@ enc_p2_dense_kernel(float* __restrict__ table, const float* __restrict__ vals,
                     uint32_t num_chunks, uint32_t splits, bool overwrite) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* T = reinterpret_cast<float*>(smem);
-  const uint32_t t = blockIdx.x / splits, s = blockIdx.x - t * splits;
+  const uint32_t lb = xcd_block(blockIdx.x, gridDim.x);
+  const uint32_t t = lb / splits, s = lb - t * splits;
   const uint32_t nt = blockDim.x;
   for (uint32_t b = threadIdx.x; b < tile; b += nt) T[b] = 0.f;
   __syncthreads();
@@ -553,7 +564,7 @@ qry_q2_kernel(const float* __restrict__ vals, uint32_t d, uint32_t r_rt, uint32_
               float* __restrict__ est, bool vec16, uint32_t c0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t r = R > 0 ? static_cast<uint32_t>(R) : r_rt;
-  const uint32_t cb = blockIdx.x + c0;  // coordinate chunk of this block
+  const uint32_t cb = xcd_block(blockIdx.x, gridDim.x) + c0;  // coordinate chunk of this block
   const uint32_t i0 = cb * chunk;
   const uint32_t i1 = min(d, i0 + chunk);
   float* stage = reinterpret_cast<float*>(smem);

@@ -278,6 +278,30 @@ class _UnpoolLink:
         return full + _ops().relu_maxpool_backward(g, self.idx, 2)
 
 
+class _MaskLink:
+    """Hand-off between a native residual unit (its output's relu mask ``y2``)
+    and the native conv that consumes that output (ResNet-9: res1 ->
+    layer2): the consumer's dgrad epilogue also writes the gradient masked by
+    ``y2`` (``conv3x3_fwd_dual``), which the residual unit's backward takes
+    instead of a separate relu-mask pass -- when the gradient it receives is
+    exactly that dgrad (one consumer; otherwise it masks what it got)."""
+
+    __slots__ = ("mask", "src", "masked", "claimed")
+
+    def __init__(self, mask):
+        self.mask = mask
+        self.src = self.masked = None
+        self.claimed = False
+
+    def take(self, g):
+        src, masked = self.src, self.masked
+        self.src = self.masked = None
+        if masked is not None and g.data_ptr() == src.data_ptr() and g.shape == src.shape \
+                and g.stride() == src.stride():
+            return masked
+        return None
+
+
 _UNPOOL_ON = [True]
 _ZERO: dict = {}
 
@@ -286,6 +310,15 @@ def set_fused_unpool(on: bool) -> None:
     """Fuse the relu + max-pool backward into the consumer's dgrad epilogue
     (default on; off = the separate csrc/pool.hip backward kernel)."""
     _UNPOOL_ON[0] = bool(on)
+
+
+def _mask_link_of(x: torch.Tensor):
+    link = getattr(x, "_commeff_mask", None)
+    if not (_UNPOOL_ON[0] and link is not None and not link.claimed and link.mask.shape == x.shape
+            and torch.is_grad_enabled() and x.requires_grad):
+        return None
+    link.claimed = True
+    return link
 
 
 def _link_of(x: torch.Tensor):
@@ -310,9 +343,10 @@ class _Conv3x3Act(torch.autograd.Function):
     last_out_link = None  # forward -> conv3x3_relu_pool side channel (no autograd state)
 
     @staticmethod
-    def forward(ctx, x, weight, pool_k, in_link=None):
+    def forward(ctx, x, weight, pool_k, in_link=None, in_mask=None):
         wf, wt = _prep(weight)
         ctx.in_link = in_link
+        ctx.in_mask = in_mask
         ctx.out_link = None
         if pool_k == 2 and _pool_fusable(x, weight):
             # relu + 2x2 max-pool in the conv epilogue: the full-resolution
@@ -348,10 +382,13 @@ class _Conv3x3Act(torch.autograd.Function):
             link = ctx.in_link
             if link is not None:  # the input's relu + max-pool backward in the epilogue
                 gx = link.park(_ops().conv3x3_fwd_unpool(g, wt, None, link.idx), x)
+            elif ctx.in_mask is not None:  # + the producer's relu-masked copy
+                gx, gxm = _ops().conv3x3_fwd_dual(g, wt, ctx.in_mask.mask)
+                ctx.in_mask.src, ctx.in_mask.masked = gx, gxm
             else:
                 gx = _ops().conv3x3_fwd(g, wt, False)
         gw = _wgrad_to(g, x, ctx.weight) if ctx.needs_input_grad[1] else None
-        return gx, gw, None, None
+        return gx, gw, None, None, None
 
 
 class _ResidualUnit(torch.autograd.Function):
@@ -366,6 +403,8 @@ class _ResidualUnit(torch.autograd.Function):
     than the per-op composition.
     """
 
+    last_mask_link = None  # forward -> residual_unit side channel (no autograd state)
+
     @staticmethod
     def forward(ctx, x, w1, w2, in_link=None):
         w1f, w1t = _prep(w1)
@@ -375,13 +414,17 @@ class _ResidualUnit(torch.autograd.Function):
         ctx.save_for_backward(x, y1, y2, w1t, w2t)
         ctx.w1, ctx.w2 = w1, w2
         ctx.in_link = in_link
+        ctx.out_mask = _MaskLink(y2)
+        _ResidualUnit.last_mask_link = ctx.out_mask
         return out
 
     @staticmethod
     def backward(ctx, g):
         x, y1, y2, w1t, w2t = ctx.saved_tensors
         g = g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        g2 = _ops().relu_mask(g, y2)
+        g2 = ctx.out_mask.take(g)  # masked by the consumer's dgrad epilogue
+        if g2 is None:
+            g2 = _ops().relu_mask(g, y2)
         g1 = _ops().conv3x3_fwd(g2, w2t, False, y1)  # masked by relu(conv1) > 0
         dw2 = _wgrad_to(g2, y1, ctx.w2) if ctx.needs_input_grad[2] else None
         gx = None
@@ -398,7 +441,11 @@ class _ResidualUnit(torch.autograd.Function):
 def residual_unit(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
     """``x + relu(conv2(relu(conv1(x))))`` (3x3, pad 1, no bias)."""
     if conv3x3_native_ok(x, w1) and conv3x3_native_ok(x, w2) and w1.shape[0] == x.shape[1]:
-        return _ResidualUnit.apply(x, w1, w2, _link_of(x))
+        out = _ResidualUnit.apply(x, w1, w2, _link_of(x))
+        if _ResidualUnit.last_mask_link is not None and out.requires_grad:
+            out._commeff_mask = _ResidualUnit.last_mask_link
+        _ResidualUnit.last_mask_link = None
+        return out
     y = F.relu(F.conv2d(x, w1, padding=1))
     return x + F.relu(F.conv2d(y, w2, padding=1))
 
@@ -418,7 +465,7 @@ def conv3x3_relu_pool(x: torch.Tensor, weight: torch.Tensor, pool_k: int = 0) ->
     else the PyTorch (MIOpen) composition."""
     if conv3x3_native_ok(x, weight) and (
             pool_k == 0 or (x.shape[2] % pool_k == 0 and x.shape[3] % pool_k == 0)):
-        out = _Conv3x3Act.apply(x, weight, int(pool_k), _link_of(x))
+        out = _Conv3x3Act.apply(x, weight, int(pool_k), _link_of(x), _mask_link_of(x))
         link = _Conv3x3Act.last_out_link
         if link is not None:
             out._commeff_unpool = link

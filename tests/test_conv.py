@@ -561,7 +561,7 @@ def test_conv1x1_passthrough_sums_identity_grad():
     _close(x.grad, xr.grad)
 
 
-@pytest.mark.parametrize("chain", ["pool_res", "pool_pool", "two_consumers"])
+@pytest.mark.parametrize("chain", ["pool_res", "pool_pool", "two_consumers", "pool_res_pool"])
 def test_fused_unpool_backward_bitwise(chain):
     """The relu + 2x2 max-pool backward fused into the consumer's dgrad
     epilogue (ops/nn.py _UnpoolLink, conv3x3_fwd_unpool) gives bitwise the
@@ -582,6 +582,8 @@ def test_fused_unpool_backward_bitwise(chain):
             y = cnn.conv3x3_relu_pool(x, ws[0], 2)
             if chain == "pool_res":
                 out = cnn.residual_unit(y, ws[1], ws[2])
+            elif chain == "pool_res_pool":  # ResNet-9 layer1 -> res1 -> layer2 (both links)
+                out = cnn.conv3x3_relu_pool(cnn.residual_unit(y, ws[1], ws[2]), ws[1], 2)
             elif chain == "pool_pool":
                 out = cnn.conv3x3_relu_pool(y, ws[1], 2) * 1.0 + ws[2].sum() * 0
             else:
