@@ -402,45 +402,52 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
 // ============================================================ long sequences
 // Flash-style kernels for sequences longer than LM (up to DS = 1024 tokens,
 // GPT-2's n_positions): a workgroup owns 128 rows of one (sequence, head) --
-// 32 per wave -- and streams the other operand through LDS in 64-row tiles
-// with an online softmax, so LDS no longer bounds the length.
+// 32 per wave -- and streams the other operand through a double-buffered LDS
+// ring in 64-row tiles (the next tile's global loads are in flight while the
+// current one is used; one block barrier per tile), with an online softmax.
 //   forward   (query rows):  S = Q K^T per 64-key tile into a per-wave fp32
-//             tile, row max / rescale / exp / dropout by 2 threads per row,
-//             O = alpha O + P_drop V on the MFMA; O / l and LSE at the end;
-//   backward  dQ kernel (query rows): S, dP = dO V^T per 64-key tile, dS in
-//             registers -> per-wave LDS, dQ += dS K;  it also writes
-//             D_i = dO_i . O_i for the second kernel;
-//             dK/dV kernel (key rows): S^T = K Q^T, dP^T = V dO^T per 64-query
-//             tile, dV += P_drop^T dO, dK += dS^T Q.
-// Every output element is written once by one workgroup: deterministic, no
-// atomics.  Dropout masks use the same (seq, head, i, j) hash as the short
-// kernels, so the two families are interchangeable.
+//             tile, row max / rescale / exp / dropout by 2 threads per row
+//             (P_drop written over the row's S), O = alpha O + P_drop V;
+//             O / l and LSE at the end;
+//   backward  dQ kernel (query rows): S, dP = dO V^T per 64-key tile, dS
+//             straight from the accumulators into a per-wave transposed
+//             image, dQ += dS K; it also writes D_i = dO_i . O_i;
+//             dK/dV kernel (key rows): S^T = K Q^T, dP^T = V dO^T per
+//             64-query tile, dV += P_drop^T dO, dK += dS^T Q.
+// Every operand that an MFMA needs transposed (V for P V, K for dS K, Q and
+// dO for the key-row products, dS / P_drop as A operands) is read with the
+// gfx950 transposing LDS read ds_read_b64_tr_b16 from the row-major tile (or
+// from 8-byte stores of the accumulator columns): no scalar transposing
+// stores.  Every output element is written once by one workgroup:
+// deterministic, no atomics.  Dropout masks use the same (seq, head, i, j)
+// hash as the short kernels, so the two families are interchangeable.
 constexpr int QB = 128;  // rows per workgroup
 constexpr int TT = 64;   // streamed tile rows
-constexpr int T2 = 72;   // bf16 row stride of [64][64] tiles (and per-wave [32][64])
-constexpr int F2 = 68;   // fp32 row stride of per-wave [32][64] tiles
+constexpr int T2 = 72;   // bf16 row stride of [64][64] tiles
+constexpr int F2 = 68;   // fp32 row stride of the per-wave [32][64] score tile
+constexpr int TI = 36;   // bf16 row stride of per-wave transposed images [64][32]
 
-// 64 rows x 64 columns (bf16) of a row block starting at token row r0 + t0
-// (column offset col) into LDS row-major [64][T2] and/or transposed [64][T2];
-// rows >= L are zero.  256 threads, two 16-byte pieces each.
-__device__ __forceinline__ void tile_load(uint16_t* dst, uint16_t* dstT, const uint16_t* base,
-                                          int64_t ld, int64_t r0, int t0, int L, int tid) {
+// global pieces of one 64 x 64 bf16 tile (rows t0 + i of a row block at
+// token row r0; rows >= L are zero): two 16-byte pieces per thread
+struct TilePieces {
   v4u v[2];
+};
+__device__ __forceinline__ TilePieces tile_fetch(const uint16_t* base, int64_t ld, int64_t r0, int t0,
+                                                 int L, int tid) {
+  TilePieces p;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u, i = c >> 3, ch = c & 7;
-    v[u] = v4u{0u, 0u, 0u, 0u};
-    if (t0 + i < L) v[u] = *reinterpret_cast<const v4u*>(base + (r0 + t0 + i) * ld + ch * 8);
+    p.v[u] = v4u{0u, 0u, 0u, 0u};
+    if (t0 + i < L) p.v[u] = *reinterpret_cast<const v4u*>(base + (r0 + t0 + i) * ld + ch * 8);
   }
+  return p;
+}
+__device__ __forceinline__ void tile_store(uint16_t* dst, const TilePieces& p, int tid) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = tid + 256 * u, i = c >> 3, ch = c & 7;
-    if (dst) *reinterpret_cast<v4u*>(dst + i * T2 + ch * 8) = v[u];
-    if (dstT) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        dstT[(ch * 8 + e) * T2 + i] = static_cast<uint16_t>((v[u][e >> 1] >> (16 * (e & 1))) & 0xffffu);
-    }
+    *reinterpret_cast<v4u*>(dst + i * T2 + ch * 8) = p.v[u];
   }
 }
 
@@ -456,8 +463,37 @@ __device__ __forceinline__ void frag_load(bf16x8_t f[4], const uint16_t* base, i
   }
 }
 
-// 32 rows x 64 columns staged bf16 in a per-wave [32][T2] tile -> token rows
-// r0 + g0 + row (< L) of a [M, ld] bf16 matrix at column offset col
+// Transposing-read operand (cdna_hip_programming.md T10): 32 columns
+// [cb, cb + 32) x 16 rows [16 ks, 16 ks + 16) of a bf16 image with row
+// stride LD elements, as the MFMA operand whose lane holds column
+// cb + (lane & 31) and k = 8 (lane >> 5) + j.  Lane 4q + p of each 16-lane
+// group addresses row q (+4 for the second read), columns 4p .. 4p + 3.
+template <int LD>
+__device__ __forceinline__ bf16x8_t tr_op(const uint16_t* img, int cb, int ks, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = cb + 16 * (g & 1) + 4 * p;
+  const int row = 16 * ks + 8 * (g >> 1) + q;
+  const unsigned char* b = reinterpret_cast<const unsigned char*>(img);
+  return tr_read(b + (row * LD + col) * 2, b + ((row + 4) * LD + col) * 2);
+}
+
+// accumulator values v[e] (row crow(e, hi), column lr of a 32 x 32 tile)
+// stored TRANSPOSED into an image [column][row] (stride TI): the four rows
+// (e & 3) of a group are consecutive there -> one 8-byte store per group
+__device__ __forceinline__ void store_t(uint16_t* img, const float (&v)[16], int col, int hi) {
+#pragma unroll
+  for (int grp = 0; grp < 4; ++grp) {
+    const int r0 = 8 * grp + 4 * hi;
+    uint2 w;
+    w.x = pack_bf16(v[4 * grp], v[4 * grp + 1]);
+    w.y = pack_bf16(v[4 * grp + 2], v[4 * grp + 3]);
+    *reinterpret_cast<uint2*>(img + col * TI + r0) = w;
+  }
+}
+
+// 32 rows x 64 columns staged bf16 in a per-wave [32][stride] tile -> token
+// rows r0 + g0 + row (< L) of a [M, ld] bf16 matrix
+template <int STRIDE>
 __device__ __forceinline__ void rows_store(uint16_t* out, int64_t ld, int64_t r0, int g0, int L,
                                            const uint16_t* stage, int lane) {
 #pragma unroll
@@ -465,10 +501,11 @@ __device__ __forceinline__ void rows_store(uint16_t* out, int64_t ld, int64_t r0
     const int c = lane + 64 * u, row = c >> 3, ch = c & 7;
     if (g0 + row < L)
       *reinterpret_cast<v4u*>(out + (r0 + g0 + row) * ld + ch * 8) =
-          *reinterpret_cast<const v4u*>(stage + row * T2 + ch * 8);
+          *reinterpret_cast<const v4u*>(stage + row * STRIDE + ch * 8);
   }
 }
 
+template <int STRIDE>
 __device__ __forceinline__ void stage_acc(uint16_t* stage, const f32x16_t acc[2], int hi, int lr,
                                           const float* rowscale) {
 #pragma unroll
@@ -477,22 +514,23 @@ __device__ __forceinline__ void stage_acc(uint16_t* stage, const f32x16_t acc[2]
     for (int e = 0; e < 16; ++e) {
       const int row = crow(e, hi);
       const float v = rowscale ? acc[ct][e] * rowscale[row] : acc[ct][e];
-      stage[row * T2 + 32 * ct + lr] = bfbits(v);
+      stage[row * STRIDE + 32 * ct + lr] = bfbits(v);
     }
 }
 
-// LDS: K [64][T2], V^T [64][T2], per wave: S fp32 [32][F2], P bf16 [32][T2],
-// alpha [32]  (~72 KB: 2 workgroups per CU)
-__global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// LDS: K, V [2][64][T2] ring, per wave: S fp32 [32][F2] (P_drop bf16 written
+// over its rows), alpha [32]  (~72 KB: 2 workgroups per CU)
+__global__ void __launch_bounds__(256, 2) attn_long_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sVt = sK + TT * T2;
+  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);   // [2][TT][T2]
+  uint16_t* sV = sK + 2 * TT * T2;                     // [2][TT][T2]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
-  float* sS = reinterpret_cast<float*>(sVt + TT * T2) + w * 32 * F2;
-  uint16_t* sP = reinterpret_cast<uint16_t*>(reinterpret_cast<float*>(sVt + TT * T2) + 4 * 32 * F2) +
-                 w * 32 * T2;
-  float* sA = reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(
-                  reinterpret_cast<float*>(sVt + TT * T2) + 4 * 32 * F2) + 4 * 32 * T2) + w * 32;
+  float* sS = reinterpret_cast<float*>(sV + 2 * TT * T2) + w * 32 * F2;
+  uint16_t* sP = reinterpret_cast<uint16_t*>(sS);  // row i at the start of S row i (stride 2*F2)
+  constexpr int PS = 2 * F2;                        // bf16 row stride of P
+  float* sA = reinterpret_cast<float*>(sV + 2 * TT * T2) + 4 * 32 * F2 + w * 32;
   const int tiles = a.lse_ld / QB;
   const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
   const int n = bh / a.nh, h = bh - n * a.nh;
@@ -503,6 +541,8 @@ __global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
   const int64_t ld3 = 3 * static_cast<int64_t>(H);
   const int wq0 = q0 + 32 * w;
   const bool wvalid = wq0 < L;
+  const uint16_t* kbase = a.qkv + H + h * HD;
+  const uint16_t* vbase = a.qkv + 2 * H + h * HD;
   bf16x8_t qf[4];
   frag_load(qf, a.qkv + h * HD, ld3, r0 + wq0 + lr, wq0 + lr < L, hi);
   f32x16_t o[2] = {zero16(), zero16()};
@@ -510,11 +550,22 @@ __global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
   const int srow = lane >> 1, half = lane & 1, gi = wq0 + srow;
   float m_run = -__builtin_huge_valf(), l_run = 0.f;
   const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
+  {
+    const TilePieces pk = tile_fetch(kbase, ld3, r0, 0, L, tid);
+    const TilePieces pv = tile_fetch(vbase, ld3, r0, 0, L, tid);
+    tile_store(sK, pk, tid);
+    tile_store(sV, pv, tid);
+  }
+  __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
-    __syncthreads();  // every wave is done with the previous K / V tile
-    tile_load(sK, nullptr, a.qkv + H + h * HD, ld3, r0, kt * TT, L, tid);
-    tile_load(nullptr, sVt, a.qkv + 2 * H + h * HD, ld3, r0, kt * TT, L, tid);
-    __syncthreads();
+    const uint16_t* cK = sK + (kt & 1) * TT * T2;
+    const uint16_t* cV = sV + (kt & 1) * TT * T2;
+    TilePieces pk, pv;
+    const bool more = kt + 1 < nkt;
+    if (more) {  // next tile's loads in flight during this tile's math
+      pk = tile_fetch(kbase, ld3, r0, (kt + 1) * TT, L, tid);
+      pv = tile_fetch(vbase, ld3, r0, (kt + 1) * TT, L, tid);
+    }
     const bool act = wvalid && kt * TT <= wq0 + 31;
     if (act) {
 #pragma unroll
@@ -522,7 +573,7 @@ __global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
         f32x16_t acc = zero16();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sK + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
+          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(cK + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[ks], bf, acc, 0, 0, 0);
         }
 #pragma unroll
@@ -532,9 +583,7 @@ __global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
           sS[row * F2 + col] = (j <= i && i < L) ? acc[e] * a.scale : -__builtin_huge_valf();
         }
       }
-    }
-    __syncthreads();
-    if (act) {
+      wave_lds_sync();
       float p[32];
       float mt = -__builtin_huge_valf();
 #pragma unroll
@@ -555,6 +604,7 @@ __global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
       l_run = l_run * alpha + sum;
       m_run = live ? m_new : m_run;
       const uint64_t ib = (static_cast<uint64_t>(bh) * DS + gi) * DS + kt * TT + half * 32;
+      wave_lds_sync();  // every lane holds its S values: P may overwrite the rows
 #pragma unroll
       for (int t = 0; t < 32; t += 2) {
         float v0 = p[t], v1 = p[t + 1];
@@ -562,56 +612,51 @@ __global__ void __launch_bounds__(256) attn_long_fwd_kernel(AttnArgs a) {
           v0 = akeep(ib + t, a.seed, a.thresh) ? v0 * a.dscale : 0.f;
           v1 = akeep(ib + t + 1, a.seed, a.thresh) ? v1 * a.dscale : 0.f;
         }
-        *reinterpret_cast<uint32_t*>(sP + srow * T2 + half * 32 + t) =
+        *reinterpret_cast<uint32_t*>(sP + srow * PS + half * 32 + t) =
             static_cast<uint32_t>(bfbits(v0)) | (static_cast<uint32_t>(bfbits(v1)) << 16);
       }
       if (half == 0) sA[srow] = alpha;
-    }
-    __syncthreads();
-    if (act) {
+      wave_lds_sync();
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int e = 0; e < 16; ++e) o[ct][e] *= sA[crow(e, hi)];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sP + lr * T2 + 16 * ks + 8 * hi);
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sP + lr * PS + 16 * ks + 8 * hi);
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sVt + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
-          o[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, o[ct], 0, 0, 0);
-        }
+        for (int ct = 0; ct < 2; ++ct)
+          o[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_op<T2>(cV, 32 * ct, ks, lane), o[ct], 0, 0, 0);
       }
     }
+    if (more) {  // the other buffer was last read before the previous barrier
+      tile_store(sK + ((kt + 1) & 1) * TT * T2, pk, tid);
+      tile_store(sV + ((kt + 1) & 1) * TT * T2, pv, tid);
+    }
+    __syncthreads();
   }
-  const float l = l_run + __shfl_xor(l_run, 1, 64);
-  __syncthreads();
   if (wvalid) {
+    const float l = l_run + __shfl_xor(l_run, 1, 64);
     if (half == 0) {
       sA[srow] = gi < L ? 1.f / l : 0.f;
       if (gi < L) a.lse[static_cast<int64_t>(bh) * a.lse_ld + gi] = m_run + __logf(l);
     }
-  }
-  __syncthreads();
-  if (wvalid) {
-    stage_acc(sP, o, hi, lr, sA);
-    __syncthreads();
-    rows_store(a.o + h * HD, H, r0, wq0, L, sP, lane);
-  } else {
-    __syncthreads();
+    wave_lds_sync();
+    stage_acc<PS>(sP, o, hi, lr, sA);
+    wave_lds_sync();
+    rows_store<PS>(a.o + h * HD, H, r0, wq0, L, sP, lane);
   }
 }
 
-// dQ (+ D): LDS K, V [64][T2], K^T [64][T2], per wave dS bf16 [32][T2],
-// D / LSE [32]  (~46 KB)
-__global__ void __launch_bounds__(256) attn_long_dq_kernel(AttnArgs a) {
+// dQ (+ D): LDS K, V [2][64][T2] ring, per wave: dS^T image [64][TI] bf16,
+// D / LSE [32]  (~56 KB)
+__global__ void __launch_bounds__(256, 2) attn_long_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sV = sK + TT * T2;
-  uint16_t* sKt = sV + TT * T2;
+  uint16_t* sV = sK + 2 * TT * T2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
-  uint16_t* sdS = sKt + TT * T2 + w * 32 * T2;
-  float* sDr = reinterpret_cast<float*>(sKt + TT * T2 + 4 * 32 * T2) + w * 64;
+  uint16_t* sdSt = sV + 2 * TT * T2 + w * TT * TI;  // [key][query]
+  float* sDr = reinterpret_cast<float*>(sV + 2 * TT * T2 + 4 * TT * TI) + w * 64;
   float* sLr = sDr + 32;
   const int tiles = a.lse_ld / QB;
   const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
@@ -623,6 +668,8 @@ __global__ void __launch_bounds__(256) attn_long_dq_kernel(AttnArgs a) {
   const int64_t ld3 = 3 * static_cast<int64_t>(H);
   const int wq0 = q0 + 32 * w;
   const bool wvalid = wq0 < L;
+  const uint16_t* kbase = a.qkv + H + h * HD;
+  const uint16_t* vbase = a.qkv + 2 * H + h * HD;
   bf16x8_t qf[4], gf[4];
   frag_load(qf, a.qkv + h * HD, ld3, r0 + wq0 + lr, wq0 + lr < L, hi);
   frag_load(gf, a.dout + h * HD, H, r0 + wq0 + lr, wq0 + lr < L, hi);
@@ -653,11 +700,22 @@ __global__ void __launch_bounds__(256) attn_long_dq_kernel(AttnArgs a) {
   }
   f32x16_t gq[2] = {zero16(), zero16()};
   const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
+  {
+    const TilePieces pk = tile_fetch(kbase, ld3, r0, 0, L, tid);
+    const TilePieces pv = tile_fetch(vbase, ld3, r0, 0, L, tid);
+    tile_store(sK, pk, tid);
+    tile_store(sV, pv, tid);
+  }
+  __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
-    __syncthreads();
-    tile_load(sK, sKt, a.qkv + H + h * HD, ld3, r0, kt * TT, L, tid);
-    tile_load(sV, nullptr, a.qkv + 2 * H + h * HD, ld3, r0, kt * TT, L, tid);
-    __syncthreads();
+    const uint16_t* cK = sK + (kt & 1) * TT * T2;
+    const uint16_t* cV = sV + (kt & 1) * TT * T2;
+    TilePieces pk, pv;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      pk = tile_fetch(kbase, ld3, r0, (kt + 1) * TT, L, tid);
+      pv = tile_fetch(vbase, ld3, r0, (kt + 1) * TT, L, tid);
+    }
     const bool act = wvalid && kt * TT <= wq0 + 31;
     if (act) {
 #pragma unroll
@@ -666,9 +724,10 @@ __global__ void __launch_bounds__(256) attn_long_dq_kernel(AttnArgs a) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const int ko = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[ks], *reinterpret_cast<const bf16x8_t*>(sK + ko), s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[ks], *reinterpret_cast<const bf16x8_t*>(sV + ko), dp, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[ks], *reinterpret_cast<const bf16x8_t*>(cK + ko), s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[ks], *reinterpret_cast<const bf16x8_t*>(cV + ko), dp, 0, 0, 0);
         }
+        float ds[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int row = crow(e, hi), col = 32 * ct + lr;
@@ -678,46 +737,44 @@ __global__ void __launch_bounds__(256) attn_long_dq_kernel(AttnArgs a) {
           bool keep = true;
           if (a.thresh != 0u) keep = akeep((static_cast<uint64_t>(bh) * DS + i) * DS + j, a.seed, a.thresh);
           const float dP = keep ? dp[e] * a.dscale : 0.f;
-          sdS[row * T2 + col] = bfbits(P * (dP - sDr[row]) * a.scale);
+          ds[e] = P * (dP - sDr[row]) * a.scale;
         }
+        store_t(sdSt, ds, 32 * ct + lr, hi);  // [key][query]
       }
+      wave_lds_sync();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {  // keys 16 ks ..
+        const bf16x8_t af = tr_op<TI>(sdSt, 0, ks, lane);  // A[query][key]
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+          gq[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_op<T2>(cK, 32 * ct, ks, lane), gq[ct], 0, 0, 0);
+      }
+    }
+    if (more) {
+      tile_store(sK + ((kt + 1) & 1) * TT * T2, pk, tid);
+      tile_store(sV + ((kt + 1) & 1) * TT * T2, pv, tid);
     }
     __syncthreads();
-    if (act) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sdS + lr * T2 + 16 * ks + 8 * hi);
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(sKt + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
-          gq[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, gq[ct], 0, 0, 0);
-        }
-      }
-    }
   }
-  __syncthreads();
   if (wvalid) {
-    stage_acc(sdS, gq, hi, lr, nullptr);
-    __syncthreads();
-    rows_store(a.dqkv + h * HD, ld3, r0, wq0, L, sdS, lane);
-  } else {
-    __syncthreads();
+    uint16_t* stage = sdSt;  // 32 rows x 64 columns (stride T2 fits in the 64 x TI image)
+    stage_acc<T2>(stage, gq, hi, lr, nullptr);
+    wave_lds_sync();
+    rows_store<T2>(a.dqkv + h * HD, ld3, r0, wq0, L, stage, lane);
   }
 }
 
-// dK, dV: LDS Q, dO [64][T2], Q^T, dO^T [64][T2], LSE / D [64], per wave
-// P_drop^T, dS^T bf16 [32][T2] (~74 KB)
-__global__ void __launch_bounds__(256) attn_long_dkdv_kernel(AttnArgs a) {
+// dK, dV: LDS Q, dO [2][64][T2] ring, LSE / D [2][64], per wave P_drop and dS
+// images [64 queries][TI] (~75 KB)
+__global__ void __launch_bounds__(256, 2) attn_long_dkdv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sG = sQ + TT * T2;
-  uint16_t* sQt = sG + TT * T2;
-  uint16_t* sGt = sQt + TT * T2;
-  float* sL = reinterpret_cast<float*>(sGt + TT * T2);
-  float* sD = sL + TT;
+  uint16_t* sG = sQ + 2 * TT * T2;
+  float* sL = reinterpret_cast<float*>(sG + 2 * TT * T2);  // [2][TT]
+  float* sD = sL + 2 * TT;                                  // [2][TT]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
-  uint16_t* sPt = reinterpret_cast<uint16_t*>(sD + TT) + w * 2 * 32 * T2;
-  uint16_t* sSt = sPt + 32 * T2;
+  uint16_t* sPd = reinterpret_cast<uint16_t*>(sD + 2 * TT) + w * 2 * TT * TI;  // [query][key]
+  uint16_t* sdS = sPd + TT * TI;
   const int tiles = a.lse_ld / QB;
   const int bh = blockIdx.x / tiles, k0 = (blockIdx.x - bh * tiles) * QB;
   const int n = bh / a.nh, h = bh - n * a.nh;
@@ -728,77 +785,112 @@ __global__ void __launch_bounds__(256) attn_long_dkdv_kernel(AttnArgs a) {
   const int64_t ld3 = 3 * static_cast<int64_t>(H);
   const int wk0 = k0 + 32 * w;
   const bool wvalid = wk0 < L;
+  const uint16_t* qbase = a.qkv + h * HD;
+  const uint16_t* gbase = a.dout + h * HD;
+  const float* lrow = a.lse + static_cast<int64_t>(bh) * a.lse_ld;
+  const float* drow = a.dbuf + static_cast<int64_t>(bh) * a.lse_ld;
   bf16x8_t kf[4], vf[4];
   frag_load(kf, a.qkv + H + h * HD, ld3, r0 + wk0 + lr, wk0 + lr < L, hi);
   frag_load(vf, a.qkv + 2 * H + h * HD, ld3, r0 + wk0 + lr, wk0 + lr < L, hi);
   f32x16_t gk[2] = {zero16(), zero16()}, gv[2] = {zero16(), zero16()};
-  for (int qs = k0; qs < L; qs += TT) {
-    __syncthreads();
-    tile_load(sQ, sQt, a.qkv + h * HD, ld3, r0, qs, L, tid);
-    tile_load(sG, sGt, a.dout + h * HD, H, r0, qs, L, tid);
+  {
+    const TilePieces pq = tile_fetch(qbase, ld3, r0, k0, L, tid);
+    const TilePieces pg = tile_fetch(gbase, H, r0, k0, L, tid);
+    tile_store(sQ, pq, tid);
+    tile_store(sG, pg, tid);
     if (tid < TT) {
-      const int i = qs + tid;
-      sL[tid] = i < L ? a.lse[static_cast<int64_t>(bh) * a.lse_ld + i] : 0.f;
-      sD[tid] = i < L ? a.dbuf[static_cast<int64_t>(bh) * a.lse_ld + i] : 0.f;
+      const int i = k0 + tid;
+      sL[tid] = i < L ? lrow[i] : 0.f;
+      sD[tid] = i < L ? drow[i] : 0.f;
     }
-    __syncthreads();
+  }
+  __syncthreads();
+  for (int qs = k0, it = 0; qs < L; qs += TT, ++it) {
+    const int b = it & 1;
+    const uint16_t* cQ = sQ + b * TT * T2;
+    const uint16_t* cG = sG + b * TT * T2;
+    const float* cL = sL + b * TT;
+    const float* cD = sD + b * TT;
+    TilePieces pq, pg;
+    float nl = 0.f, nd = 0.f;
+    const bool more = qs + TT < L;
+    if (more) {
+      pq = tile_fetch(qbase, ld3, r0, qs + TT, L, tid);
+      pg = tile_fetch(gbase, H, r0, qs + TT, L, tid);
+      if (tid < TT) {
+        const int i = qs + TT + tid;
+        nl = i < L ? lrow[i] : 0.f;
+        nd = i < L ? drow[i] : 0.f;
+      }
+    }
     const bool act = wvalid && qs + TT - 1 >= wk0;
     if (act) {
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
+      for (int ct = 0; ct < 2; ++ct) {  // queries 32 ct ..
         f32x16_t s = zero16(), dp = zero16();
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const int ko = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], *reinterpret_cast<const bf16x8_t*>(sQ + ko), s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks], *reinterpret_cast<const bf16x8_t*>(sG + ko), dp, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], *reinterpret_cast<const bf16x8_t*>(cQ + ko), s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks], *reinterpret_cast<const bf16x8_t*>(cG + ko), dp, 0, 0, 0);
         }
+        float pd[16], ds[16];
+        const int col = 32 * ct + lr, i = qs + col;  // query
+        const float Li = cL[col], Di = cD[col];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int row = crow(e, hi), col = 32 * ct + lr;  // row: key, col: query
-          const int j = wk0 + row, i = qs + col;
+          const int j = wk0 + crow(e, hi);  // key
           const bool valid = j <= i && i < L;
-          const float P = valid ? __expf(s[e] * a.scale - sL[col]) : 0.f;
+          const float P = valid ? __expf(s[e] * a.scale - Li) : 0.f;
           bool keep = true;
           if (a.thresh != 0u) keep = akeep((static_cast<uint64_t>(bh) * DS + i) * DS + j, a.seed, a.thresh);
           const float dP = keep ? dp[e] * a.dscale : 0.f;
-          sPt[row * T2 + col] = bfbits(keep ? P * a.dscale : 0.f);
-          sSt[row * T2 + col] = bfbits(P * (dP - sD[col]) * a.scale);
+          pd[e] = keep ? P * a.dscale : 0.f;
+          ds[e] = P * (dP - Di) * a.scale;
         }
+        store_t(sPd, pd, col, hi);  // [query][key]
+        store_t(sdS, ds, col, hi);
       }
-    }
-    __syncthreads();
-    if (act) {
+      wave_lds_sync();
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int ao = lr * T2 + 16 * ks + 8 * hi;
-        const bf16x8_t pa = *reinterpret_cast<const bf16x8_t*>(sPt + ao);
-        const bf16x8_t sa = *reinterpret_cast<const bf16x8_t*>(sSt + ao);
+      for (int ks = 0; ks < 4; ++ks) {  // queries 16 ks ..
+        const bf16x8_t pa = tr_op<TI>(sPd, 0, ks, lane);  // A[key][query]
+        const bf16x8_t sa = tr_op<TI>(sdS, 0, ks, lane);
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
-          const int bo = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
-          gv[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, *reinterpret_cast<const bf16x8_t*>(sGt + bo), gv[ct], 0, 0, 0);
-          gk[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, *reinterpret_cast<const bf16x8_t*>(sQt + bo), gk[ct], 0, 0, 0);
+          gv[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, tr_op<T2>(cG, 32 * ct, ks, lane), gv[ct], 0, 0, 0);
+          gk[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, tr_op<T2>(cQ, 32 * ct, ks, lane), gk[ct], 0, 0, 0);
         }
       }
     }
+    if (more) {
+      tile_store(sQ + (b ^ 1) * TT * T2, pq, tid);
+      tile_store(sG + (b ^ 1) * TT * T2, pg, tid);
+      if (tid < TT) {
+        sL[(b ^ 1) * TT + tid] = nl;
+        sD[(b ^ 1) * TT + tid] = nd;
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (wvalid) {
-    stage_acc(sPt, gk, hi, lr, nullptr);
-    stage_acc(sSt, gv, hi, lr, nullptr);
-    __syncthreads();
-    rows_store(a.dqkv + H + h * HD, ld3, r0, wk0, L, sPt, lane);
-    rows_store(a.dqkv + 2 * H + h * HD, ld3, r0, wk0, L, sSt, lane);
-  } else {
-    __syncthreads();
+    stage_acc<T2>(sPd, gk, hi, lr, nullptr);  // 32 x 64 at stride T2 fits in 2 x 64 x TI
+    wave_lds_sync();
+    rows_store<T2>(a.dqkv + H + h * HD, ld3, r0, wk0, L, sPd, lane);
+    wave_lds_sync();
+    stage_acc<T2>(sPd, gv, hi, lr, nullptr);
+    wave_lds_sync();
+    rows_store<T2>(a.dqkv + 2 * H + h * HD, ld3, r0, wk0, L, sPd, lane);
   }
 }
 
-constexpr size_t kLongFwdLds = 2 * TT * T2 * 2 + 4 * 32 * F2 * 4 + 4 * 32 * T2 * 2 + 4 * 32 * 4;
-constexpr size_t kLongDqLds = 3 * TT * T2 * 2 + 4 * 32 * T2 * 2 + 4 * 64 * 4;
-constexpr size_t kLongDkdvLds = 4 * TT * T2 * 2 + 2 * TT * 4 + 4 * 2 * 32 * T2 * 2;
-static_assert(kLongDkdvLds <= 80 * 1024 && kLongFwdLds <= 80 * 1024, "2 workgroups per CU");
+constexpr size_t kLongFwdLds = 4 * TT * T2 * 2 + 4 * 32 * F2 * 4 + 4 * 32 * 4;
+constexpr size_t kLongDqLds = 4 * TT * T2 * 2 + 4 * TT * TI * 2 + 4 * 64 * 4;
+constexpr size_t kLongDkdvLds = 4 * TT * T2 * 2 + 4 * TT * 4 + 4 * 2 * TT * TI * 2;
+static_assert(kLongDkdvLds <= 80 * 1024 && kLongFwdLds <= 80 * 1024 && kLongDqLds <= 80 * 1024,
+              "2 workgroups per CU");
+static_assert(32 * T2 <= TT * TI, "dQ staging fits in the dS image");
+static_assert(2 * F2 >= TT, "P rows fit in the S rows");
 
 constexpr size_t kFwdLds = (2 * LM * RS + HD * TS) * 2 + LM * SS * 4;
 constexpr size_t kBwdLds = 3 * HD * TS * 2 + 2 * LM * 4 + 3 * LM * TS * 2;

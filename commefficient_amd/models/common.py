@@ -9,7 +9,8 @@ import torch.nn.functional as F
 
 from ..ops import grouped as _grouped
 from ..ops.nn import (_AffineGrouped, conv1x1_passthrough, conv2d_grouped, conv2d_native,
-                      conv2d_native_kind, ghost_batch_norm, ghost_bn_native_ok, linear_grouped)
+                      conv2d_native_kind, ghost_batch_norm, ghost_bn_native_ok, linear_grouped,
+                      stock_active)
 
 
 class Mul(nn.Module):
@@ -76,6 +77,8 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
 
     def _bn(self, x, addend=None):
         """(normalised x, whether the fused ReLU (and the addend) was applied)"""
+        if stock_active():
+            return self._bn_stock(x), False
         G = max(1, self.ghost_groups)
         gg = _grouped.active() if (self.training and self.affine) else None
         if gg is not None and gg.view(self.weight) is None:
@@ -115,6 +118,31 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
                 self.running_var.mul_(1 - m).add_(m * unb)
                 self.num_batches_tracked += 1
         return y.reshape(x.shape).to(x.dtype).contiguous(memory_format=_fmt(x)), False
+
+
+    def _bn_stock(self, x):
+        """Batch norm as a plain fp32 composition (``ops.nn.stock_ops``: under
+        torch.func.vmap each client's statistics and running-statistics
+        buffers are its own batched slices; MIOpen's batch norm rejects the
+        bf16 weights autocast + vmap hand it)."""
+        C = x.shape[1]
+        xf = x.float()
+        if self.training or not self.track_running_stats or self.running_mean is None:
+            mean = xf.mean(dim=(0, 2, 3))
+            var = xf.var(dim=(0, 2, 3), unbiased=False)
+            if self.training and self.track_running_stats and self.running_mean is not None:
+                with torch.no_grad():
+                    n = xf.numel() // C
+                    m = self.momentum if self.momentum is not None else 0.1
+                    self.running_mean.mul_(1 - m).add_(mean.detach() * m)
+                    self.running_var.mul_(1 - m).add_(var.detach() * (m * n / max(1, n - 1)))
+                    self.num_batches_tracked.add_(1)
+        else:
+            mean, var = self.running_mean, self.running_var
+        y = (xf - mean.view(1, C, 1, 1)) * torch.rsqrt(var.view(1, C, 1, 1) + self.eps)
+        if self.affine:
+            y = y * self.weight.view(1, C, 1, 1) + self.bias.view(1, C, 1, 1)
+        return y.to(x.dtype)
 
 
 def _fmt(x):
