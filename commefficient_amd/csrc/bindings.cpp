@@ -1575,6 +1575,50 @@ at::Tensor heads_to_rows_hip(at::TensorList srcs, const c10::optional<at::Tensor
   return out;
 }
 
+// sink (fp32 [M, N], row-contiguous) += a^T b for a [T, M], b [T, N] bf16
+// with unit column stride (gemm_tn.hip)
+void gemm_tn_acc_hip(at::Tensor sink, const at::Tensor& a, const at::Tensor& b) {
+  TORCH_CHECK(sink.scalar_type() == at::kFloat && sink.dim() == 2 && sink.stride(1) == 1,
+              "gemm_tn_acc: sink must be fp32 [M, N] with unit column stride");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
+                  b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1 && a.size(0) == b.size(0),
+              "gemm_tn_acc: a [T, M], b [T, N] bf16 with unit column stride");
+  const int64_t M = a.size(1), N = b.size(1), T = a.size(0);
+  TORCH_CHECK(sink.size(0) == M && sink.size(1) == N, "gemm_tn_acc: sink shape");
+  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(sink.data_ptr()) % 16 == 0 && sink.stride(0) % 4 == 0,
+              "gemm_tn_acc: M, N multiples of 256, 16-byte aligned rows");
+  TORCH_CHECK(T < (1ll << 31) && M * N < (1ll << 31), "gemm_tn_acc: size");
+  if (T == 0) return;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  int cus = 256;
+  {
+    hipDeviceProp_t prop;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      cus = prop.multiProcessorCount;
+  }
+  GemmTnArgs g{};
+  g.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  g.lda = a.stride(0);
+  g.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  g.ldb = b.stride(0);
+  g.C = sink.data_ptr<float>();
+  g.ldc = sink.stride(0);
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.T = static_cast<int>(T);
+  g.splits = gemm_tn_splits(g.M, g.N, g.T, cus);
+  at::Tensor slab;
+  if (g.splits > 1) {
+    slab = at::empty({static_cast<int64_t>(g.splits) * M * N}, sink.options());
+    g.slab = slab.data_ptr<float>();
+  }
+  launch_gemm_tn_acc(g, cur_stream());
+}
+
 void check_seqs(const at::Tensor& start, const at::Tensor& len) {
   TORCH_CHECK(start.scalar_type() == at::kInt && len.scalar_type() == at::kInt &&
                   start.is_contiguous() && len.is_contiguous() && start.numel() == len.numel(),
@@ -1735,6 +1779,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("attn_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, Tensor start, Tensor len, int nh, "
         "float p_drop, int seed, int max_len) -> Tensor");
   m.def("heads_to_rows(Tensor[] srcs, Tensor? tok, int Mr) -> Tensor");
+  m.def("gemm_tn_acc(Tensor(a!) sink, Tensor a, Tensor b) -> ()");
   m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu, Tensor(a!)? sbias=None) "
         "-> (Tensor, Tensor)");
 }
@@ -1814,6 +1859,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("bias_gelu_fwd", &bias_gelu_fwd_hip);
   m.impl("bias_act_bwd", &bias_act_bwd_hip);
   m.impl("pad_rows", &pad_rows_hip);
+  m.impl("gemm_tn_acc", &gemm_tn_acc_hip);
   m.impl("attn_fwd", &attn_fwd_hip);
   m.impl("attn_bwd", &attn_bwd_hip);
   m.impl("heads_to_rows", &heads_to_rows_hip);

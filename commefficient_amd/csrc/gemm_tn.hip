@@ -1,0 +1,217 @@
+// Weight-gradient GEMM for the GPT-2 linears: C[M][N] (fp32) += A^T B with
+// A [T][M] and B [T][N] bf16 row-major -- dW[in][out] += sum over the round's
+// token rows t of X[t][in] dY[t][out] (HF Conv1D layout), accumulated straight
+// into the flat fp32 gradient (ops/transformer.py grad sinks).
+//
+// Reference model: the GPT2DoubleHeadsModel backward of
+// /root/reference/CommEfficient/gpt2_train.py:55-99.
+// hipBLASLt runs these shapes (768 x 768 .. 3072 x 768 over ~10k tokens) at
+// 144-421 TF/s: 9-36 output tiles of 256 x 256 cannot fill 256 CUs.  Here:
+//   * the reduction runs over the ROW index of both operands, so both tiles
+//     are staged K-major by LDS DMA (global_load_lds, 16 bytes a lane) into
+//     XOR-swizzled [64 tokens][256] images and read with the gfx950
+//     transposing read ds_read_b64_tr_b16 in the 32x32x16 operand layout
+//     (the same images and reads as conv.hip's wide wgrad kernel);
+//   * 256 x 256 tile per 8-wave block (4 x 2 waves of 64 x 128), 64-token
+//     K-steps through a two-stage ring, one block per CU (128 KB LDS);
+//   * split-K over tokens so tiles x splits ~ one block per CU; each split
+//     writes its fp32 partial tile to a slab and a second kernel adds the
+//     slabs to C in a fixed order (bitwise deterministic); one split
+//     accumulates into C directly.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+#include "conv_common.h"
+
+namespace commeff {
+namespace {
+
+constexpr int GBK = 64;                    // tokens per K-step
+constexpr int GHALF = GBK * 128 * 2;       // one [64][128] bf16 image (16 KB)
+constexpr int GSTAGE = 4 * GHALF;          // A (2 halves) + B (2 halves)
+constexpr int kGemmLds = 2 * GSTAGE;       // two stages: 128 KB
+
+__device__ __attribute__((aligned(16))) uint32_t g_gemm_zero[4] = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ void gl16(const void* src, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntn = a.N / 256;
+  const int ntiles = (a.M / 256) * ntn;
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int pbeg = split * a.steps_per_split * GBK;
+  const int pend = min(a.T, pbeg + a.steps_per_split * GBK);
+  const int nsteps = pend > pbeg ? (pend - pbeg + GBK - 1) / GBK : 0;
+  const uint64_t zero = reinterpret_cast<uint64_t>(g_gemm_zero);
+
+  // piece i (0..3) of this thread: image half i >> 1, chunk slot (i & 1) * 512 + tid
+  uint64_t a_ptr[4], b_ptr[4];
+  int p_row[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int h = i >> 1, sp = (i & 1) * 512 + tid;
+    const int row = sp >> 4, lc = (sp & 15) ^ sw_tr256(row);
+    p_row[i] = pbeg + row;
+    a_ptr[i] = reinterpret_cast<uint64_t>(a.A + static_cast<int64_t>(pbeg + row) * a.lda + m0 + h * 128 + lc * 8);
+    b_ptr[i] = reinterpret_cast<uint64_t>(a.B + static_cast<int64_t>(pbeg + row) * a.ldb + n0 + h * 128 + lc * 8);
+  }
+  auto issue = [&](int stage) __attribute__((always_inline)) {
+    unsigned char* base = smem + stage * GSTAGE + wid * 1024;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = p_row[i] < pend;  // token rows past the split: zero page
+      gl16(reinterpret_cast<const void*>(ok ? a_ptr[i] : zero), base + (i >> 1) * GHALF + (i & 1) * 8192);
+      gl16(reinterpret_cast<const void*>(ok ? b_ptr[i] : zero),
+           base + 2 * GHALF + (i >> 1) * GHALF + (i & 1) * 8192);
+      p_row[i] += GBK;
+      a_ptr[i] += static_cast<uint64_t>(GBK) * a.lda * 2;
+      b_ptr[i] += static_cast<uint64_t>(GBK) * a.ldb * 2;
+    }
+  };
+
+  f32x16_t acc[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
+
+  if (nsteps > 0) issue(0);
+  // transposed-read offsets: A columns m = wr*64 + mi*32 live in half wr >> 1,
+  // B columns wc*128 + ni*32 in half wc
+  int toA[2][2], toB[4][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    tr_offsets<256>((wr & 1) * 64 + mi * 32, lane, toA[mi]);
+    toA[mi][0] += (wr >> 1) * GHALF;
+    toA[mi][1] += (wr >> 1) * GHALF;
+  }
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    tr_offsets<256>(ni * 32, lane, toB[ni]);
+    toB[ni][0] += 2 * GHALF + wc * GHALF;
+    toB[ni][1] += 2 * GHALF + wc * GHALF;
+  }
+  int rd = 0;
+  for (int st = 0; st < nsteps; ++st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + 1 < nsteps) issue(rd ^ 1);
+    const unsigned char* sb = smem + rd * GSTAGE;
+    bf16x8_t af[2][2], bfr[2][4];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) af[0][mi] = tr_read(sb + toA[mi][0], sb + toA[mi][1]);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) bfr[0][ni] = tr_read(sb + toB[ni][0], sb + toB[ni][1]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int cur = kk & 1, nxt = cur ^ 1;
+      if (kk + 1 < 4) {
+        const int dd = (kk + 1) * 16 * 256;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) af[nxt][mi] = tr_read(sb + toA[mi][0] + dd, sb + toA[mi][1] + dd);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) bfr[nxt][ni] = tr_read(sb + toB[ni][0] + dd, sb + toB[ni][1] + dd);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
+    }
+    rd ^= 1;
+  }
+
+  // C row m (lanes: 32 consecutive n) -- one split: accumulate into C; else
+  // this split's slab [M][N]
+  const int hi = lane >> 5, lr = lane & 31;
+  const bool direct = a.splits == 1;
+  float* out = direct ? a.C : a.slab + static_cast<size_t>(split) * a.M * a.N;
+  const int64_t ld = direct ? a.ldc : a.N;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wc * 128 + ni * 32 + lr;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        float* p = out + static_cast<int64_t>(m) * ld + n;
+        if (direct) *p += acc[mi][ni][e];
+        else *p = acc[mi][ni][e];
+      }
+    }
+}
+
+// C[m][n] += sum over s of slab[s][m][n], s in order (float4 per thread)
+__global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__ C, int64_t ldc,
+                                                             const float* __restrict__ slab, int M,
+                                                             int N, int splits) {
+  const int64_t n4 = static_cast<int64_t>(M) * N / 4;
+  const int64_t plane = static_cast<int64_t>(M) * N;
+  for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < n4;
+       q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t e = q * 4;
+    const int m = static_cast<int>(e / N), n = static_cast<int>(e - static_cast<int64_t>(m) * N);
+    float4 s = *reinterpret_cast<const float4*>(slab + e);
+    for (int k = 1; k < splits; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + k * plane + e);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    float4* c = reinterpret_cast<float4*>(C + static_cast<int64_t>(m) * ldc + n);
+    float4 cv = *c;
+    cv.x += s.x;
+    cv.y += s.y;
+    cv.z += s.z;
+    cv.w += s.w;
+    *c = cv;
+  }
+}
+
+}  // namespace
+
+int gemm_tn_splits(int M, int N, int T, int cus) {
+  const int tiles = (M / 256) * (N / 256);
+  const int steps = (T + GBK - 1) / GBK;
+  int s = (cus + tiles - 1) / tiles;  // ~ one block per CU
+  const int max_s = steps / 4 > 0 ? steps / 4 : 1;  // >= 4 K-steps per split
+  if (s > max_s) s = max_s;
+  if (s < 1) s = 1;
+  return s;
+}
+
+void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream) {
+  if (a.M == 0 || a.N == 0 || a.T == 0) return;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_tn_acc_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds);
+    attr = true;
+  }
+  const int steps = (a.T + GBK - 1) / GBK;
+  a.steps_per_split = (steps + a.splits - 1) / a.splits;
+  const int tiles = (a.M / 256) * (a.N / 256);
+  hipLaunchKernelGGL(gemm_tn_acc_kernel, dim3(static_cast<uint32_t>(tiles * a.splits)), dim3(512),
+                     kGemmLds, stream, a);
+  if (a.splits > 1) {
+    const int64_t n4 = static_cast<int64_t>(a.M) * a.N / 4;
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
+                       a.C, a.ldc, a.slab, a.M, a.N, a.splits);
+  }
+}
+
+}  // namespace commeff

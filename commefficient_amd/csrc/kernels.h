@@ -380,6 +380,23 @@ struct AttnArgs {
 };
 void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream);
 void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream);
+// C[M][N] (fp32, row stride ldc) += A^T B, A [T][lda] and B [T][ldb] bf16
+// (gemm_tn.hip; M, N multiples of 256, lda / ldb multiples of 8); split-K
+// over T with fp32 slabs [splits][M][N] summed into C in a fixed order
+struct GemmTnArgs {
+  const uint16_t* A;
+  int64_t lda;
+  const uint16_t* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  float* slab;
+  int M, N, T;
+  int splits;
+  int steps_per_split;  // set by the launcher
+};
+int gemm_tn_splits(int M, int N, int T, int cus);
+void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream);
 // out_q[c] = sum over b < G of part[b*stride + q*N + c], q < Q (fixed order)
 void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,
                          const ColsumOut& out, hipStream_t stream);

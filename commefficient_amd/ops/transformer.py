@@ -28,6 +28,8 @@ numerics oracle of tests/test_transformer.py.
 """
 from __future__ import annotations
 
+import os
+
 from contextlib import contextmanager
 from typing import Dict, Optional
 
@@ -197,9 +199,29 @@ def _sinks(*params):
     return tuple(_sink(p) for p in params)
 
 
+_WGRAD_GEMM = {"native": os.environ.get("COMMEFF_WGRAD_GEMM", "native") == "native"}
+
+
+def _gemm_tn_ok(sink: torch.Tensor, at: torch.Tensor, b: torch.Tensor) -> bool:
+    """csrc/gemm_tn.hip serves sink [M, N] += at^T b: bf16 [T, M] / [T, N]
+    operands with unit column stride, M and N multiples of 256."""
+    return (_WGRAD_GEMM["native"] and sink.dtype == torch.float32 and sink.dim() == 2
+            and sink.stride(1) == 1 and at.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and at.dim() == 2 and b.dim() == 2 and at.stride(1) == 1 and b.stride(1) == 1
+            and at.shape[1] % 256 == 0 and b.shape[1] % 256 == 0
+            and at.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and sink.stride(0) % 4 == 0
+            and at.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and sink.data_ptr() % 16 == 0)
+
+
 def _acc_mm(sink: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
-    """sink (fp32) += a @ b (bf16 operands, fp32 accumulation and output)."""
+    """sink (fp32) += a @ b (bf16 operands, fp32 accumulation and output).
+    The weight gradients (a = X^T, a view of the token rows) run on the
+    native split-K TN GEMM (csrc/gemm_tn.hip) when the shapes fit, else on
+    hipBLASLt (COMMEFF_WGRAD_GEMM=blas: always)."""
     if sink.is_cuda:
+        if _gemm_tn_ok(sink, a.t(), b):
+            _ops().gemm_tn_acc(sink, a.t(), b)
+            return
         torch.addmm(sink, a, b, out_dtype=torch.float32, out=sink)
     else:
         sink.add_(a.float() @ b.float())
