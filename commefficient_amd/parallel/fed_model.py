@@ -986,9 +986,11 @@ class FedModel:
                         ls.append(l)
                         ms = list(mets) if ms is None else [x + y for x, y in zip(ms, mets)]
                         step += 1
-            # upload: sum_c n (w_0 - w_c)
-            out.add_(self.w, alpha=float(n * Gp))
-            out.sub_(Wg.sum(dim=0), alpha=float(n))
+            # upload: sum_c n (w_0 - w_c); per-client differences first, so a
+            # coordinate no client moved contributes an exact 0 (download
+            # accounting counts exact changes)
+            Wg.neg_().add_(self.w)
+            out.add_(Wg.sum(dim=0), alpha=float(n))
             with torch.no_grad():  # running statistics: the clients' mean
                 for k, b in bufs0.items():
                     if b.is_floating_point():
