@@ -143,7 +143,8 @@ def main():
                           "unit": unit, "ms_per_round": round(el / b.steps * 1e3, 2),
                           "clients_per_round": W, "examples_per_round": ex / b.steps,
                           "grad_size": fed.d, "loss_last": float(out[0].mean().item()),
-                          "dtype": args.dtype, "data": "synthetic"}), flush=True)
+                          "dtype": args.dtype, "data": "synthetic",
+                          "extra_flags": [x for x in b.extra if x != "--"]}), flush=True)
     dist.shutdown()
 
 
