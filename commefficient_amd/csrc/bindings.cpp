@@ -730,6 +730,139 @@ at::Tensor relu_maxpool_backward_hip(const at::Tensor& gy, const at::Tensor& idx
   return gx;
 }
 
+// --------------------------------------------------------------- im2col
+const uint16_t* bf16_ptr(const at::Tensor& t);
+void check_nhwc_bf16(const at::Tensor& t, const char* name);
+
+int64_t conv_out_size(int64_t in, int64_t k, int64_t stride, int64_t pad) {
+  return (in + 2 * pad - k) / stride + 1;
+}
+
+// col [N*OH*OW, Kc] of x (bf16, channels innermost: x.stride(1) == 1, any
+// pixel stride -- the augmentation kernel's 4-channel layout included)
+at::Tensor im2col_hip(const at::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                      int64_t Kc) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.stride(1) == 1,
+              "im2col: x must be a bf16 NCHW tensor with channels innermost");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(R >= 1 && S >= 1 && stride >= 1 && pad >= 0 && pad < R && pad < S, "im2col: geometry");
+  const int64_t OH = conv_out_size(H, R, stride, pad), OW = conv_out_size(W, S, stride, pad);
+  TORCH_CHECK(OH > 0 && OW > 0, "im2col: empty output");
+  TORCH_CHECK(Kc % 8 == 0 && Kc >= R * S * C, "im2col: Kc must be a multiple of 8 and >= R*S*C");
+  const int64_t P = N * OH * OW;
+  TORCH_CHECK(P * (Kc / 8) < (int64_t(1) << 32) && P < (int64_t(1) << 31) &&
+                  x.stride(0) * N < (int64_t(1) << 31),
+              "im2col: 32-bit index range");
+  TORCH_CHECK(x.stride(2) >= 0 && x.stride(3) >= C, "im2col: pixel strides");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto col = at::empty({P, Kc}, x.options());
+  Im2colArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.col = reinterpret_cast<uint16_t*>(col.data_ptr());
+  a.N = static_cast<int>(N); a.H = static_cast<int>(H); a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C); a.OH = static_cast<int>(OH); a.OW = static_cast<int>(OW);
+  a.R = static_cast<int>(R); a.S = static_cast<int>(S);
+  a.stride = static_cast<int>(stride); a.pad = static_cast<int>(pad); a.Kc = static_cast<int>(Kc);
+  a.sN = x.stride(0); a.sH = x.stride(2); a.sW = x.stride(3);
+  a.vec = C % 8 == 0 && a.sN % 8 == 0 && a.sH % 8 == 0 && a.sW % 8 == 0 &&
+          reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0;
+  launch_im2col(a, cur_stream());
+  return col;
+}
+
+// gx [N, C, H, W] (channels_last) of the column-image gradient gcol [N*OH*OW, Kc]
+at::Tensor col2im_hip(const at::Tensor& gcol, int64_t N, int64_t H, int64_t W, int64_t C, int64_t R,
+                      int64_t S, int64_t stride, int64_t pad) {
+  TORCH_CHECK(gcol.is_cuda() && gcol.scalar_type() == at::kBFloat16 && gcol.dim() == 2 &&
+                  gcol.is_contiguous(),
+              "col2im: gcol must be a contiguous bf16 [P, Kc] tensor");
+  TORCH_CHECK(C % 8 == 0 && R >= 1 && S >= 1 && stride >= 1 && pad >= 0 && pad < R && pad < S,
+              "col2im: geometry (C % 8 == 0)");
+  const int64_t OH = conv_out_size(H, R, stride, pad), OW = conv_out_size(W, S, stride, pad);
+  const int64_t Kc = gcol.size(1);
+  TORCH_CHECK(gcol.size(0) == N * OH * OW && Kc % 8 == 0 && Kc >= R * S * C, "col2im: gcol shape");
+  TORCH_CHECK(N * H * W * C < (int64_t(1) << 34) && gcol.numel() < (int64_t(1) << 40) &&
+                  N * H * W * (C / 8) < (int64_t(1) << 32),
+              "col2im: index range");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gcol.device());
+  auto gx = at::empty({N, C, H, W}, gcol.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Im2colArgs a{};
+  a.N = static_cast<int>(N); a.H = static_cast<int>(H); a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C); a.OH = static_cast<int>(OH); a.OW = static_cast<int>(OW);
+  a.R = static_cast<int>(R); a.S = static_cast<int>(S);
+  a.stride = static_cast<int>(stride); a.pad = static_cast<int>(pad); a.Kc = static_cast<int>(Kc);
+  launch_col2im(a, reinterpret_cast<const uint16_t*>(gcol.data_ptr()),
+                reinterpret_cast<uint16_t*>(gx.data_ptr()), cur_stream());
+  return gx;
+}
+
+// bf16 [K, Kc] GEMM image of an fp32 [K, C, R, S] conv weight (column (r*S+s)*C + c)
+at::Tensor conv_weight_rsc_hip(const at::Tensor& w, int64_t Kc) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 4 && w.is_contiguous(),
+              "conv_weight_rsc: w must be a contiguous fp32 [K, C, R, S] tensor");
+  const int64_t K = w.size(0), C = w.size(1), RS = w.size(2) * w.size(3);
+  TORCH_CHECK(Kc % 8 == 0 && Kc >= RS * C, "conv_weight_rsc: Kc");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  auto out = at::empty({K, Kc}, w.options().dtype(at::kBFloat16));
+  launch_weight_rsc(w.data_ptr<float>(), reinterpret_cast<uint16_t*>(out.data_ptr()),
+                    static_cast<int>(K), static_cast<int>(C), static_cast<int>(RS),
+                    static_cast<int>(Kc), cur_stream());
+  return out;
+}
+
+// dst [G, K, C*RS] fp32 (rows may be strided) (+)= the (c, r, s)-ordered sum of
+// the split-K partial products src [G*splits, K, Kc] ((r, s, c) columns)
+void wgrad_rsc_add_hip(at::Tensor dst, const at::Tensor& src, int64_t splits, int64_t C, int64_t RS,
+                       bool accumulate) {
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.dim() == 3 && dst.stride(2) == 1 &&
+                  dst.stride(1) == dst.size(2) && dst.size(2) == C * RS,
+              "wgrad_rsc_add: dst must be fp32 [G, K, C*RS] with contiguous rows");
+  const int64_t G = dst.size(0), K = dst.size(1);
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kFloat && src.dim() == 3 && src.is_contiguous() &&
+                  src.size(0) == G * splits && src.size(1) == K && src.size(2) >= C * RS,
+              "wgrad_rsc_add: src must be contiguous fp32 [G*splits, K, Kc]");
+  TORCH_CHECK(K * C * RS < (int64_t(1) << 31), "wgrad_rsc_add: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
+  launch_wgrad_rsc_add(dst.data_ptr<float>(), G > 1 ? dst.stride(0) : 0, src.data_ptr<float>(),
+                       static_cast<int>(G), static_cast<int>(splits), static_cast<int>(K),
+                       static_cast<int>(C), static_cast<int>(RS), static_cast<int>(src.size(2)),
+                       accumulate, cur_stream());
+}
+
+std::tuple<at::Tensor, at::Tensor> maxpool_fwd_hip(const at::Tensor& x, int64_t k, int64_t s, int64_t p) {
+  check_nhwc_bf16(x, "maxpool: x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k, "maxpool: geometry");
+  const int64_t OH = conv_out_size(H, k, s, p), OW = conv_out_size(W, k, s, p);
+  TORCH_CHECK(OH > 0 && OW > 0 && N * OH * OW * (C / 8) < (int64_t(1) << 32), "maxpool: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto codes = at::empty({N, C, OH, OW},
+                         x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  launch_maxpool_fwd(bf16_ptr(x), reinterpret_cast<uint16_t*>(y.data_ptr()), codes.data_ptr<uint8_t>(),
+                     static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                     static_cast<int>(k), static_cast<int>(s), static_cast<int>(p), cur_stream());
+  return {y, codes};
+}
+
+at::Tensor maxpool_bwd_hip(const at::Tensor& gy, const at::Tensor& codes, int64_t H, int64_t W, int64_t k,
+                           int64_t s, int64_t p) {
+  TORCH_CHECK(gy.scalar_type() == at::kBFloat16 && codes.scalar_type() == at::kByte, "maxpool_bwd: dtypes");
+  auto g = gy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(codes.is_contiguous(at::MemoryFormat::ChannelsLast) && codes.sizes() == g.sizes(),
+              "maxpool_bwd: codes layout");
+  const int64_t N = g.size(0), C = g.size(1);
+  TORCH_CHECK(C % 8 == 0 && g.size(2) == conv_out_size(H, k, s, p) && g.size(3) == conv_out_size(W, k, s, p),
+              "maxpool_bwd: geometry");
+  TORCH_CHECK(N * H * W * (C / 8) < (int64_t(1) << 32), "maxpool_bwd: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gy.device());
+  auto gx = at::empty({N, C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_maxpool_bwd(bf16_ptr(g), codes.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(gx.data_ptr()),
+                     static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
+                     static_cast<int>(k), static_cast<int>(s), static_cast<int>(p), cur_stream());
+  return gx;
+}
+
 // --------------------------------------------------------------- conv3x3
 const uint16_t* bf16_ptr(const at::Tensor& t) {
   return reinterpret_cast<const uint16_t*>(t.data_ptr());
@@ -1780,6 +1913,12 @@ TORCH_LIBRARY(commeff, m) {
         "float p_drop, int seed, int max_len) -> Tensor");
   m.def("heads_to_rows(Tensor[] srcs, Tensor? tok, int Mr) -> Tensor");
   m.def("gemm_tn_acc(Tensor(a!) sink, Tensor a, Tensor b) -> ()");
+  m.def("im2col(Tensor x, int R, int S, int stride, int pad, int Kc) -> Tensor");
+  m.def("col2im(Tensor gcol, int N, int H, int W, int C, int R, int S, int stride, int pad) -> Tensor");
+  m.def("conv_weight_rsc(Tensor w, int Kc) -> Tensor");
+  m.def("wgrad_rsc_add(Tensor(a!) dst, Tensor src, int splits, int C, int RS, bool accumulate) -> ()");
+  m.def("maxpool_fwd(Tensor x, int k, int s, int p) -> (Tensor, Tensor)");
+  m.def("maxpool_bwd(Tensor gy, Tensor codes, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu, Tensor(a!)? sbias=None) "
         "-> (Tensor, Tensor)");
 }
@@ -1863,4 +2002,10 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("attn_fwd", &attn_fwd_hip);
   m.impl("attn_bwd", &attn_bwd_hip);
   m.impl("heads_to_rows", &heads_to_rows_hip);
+  m.impl("im2col", &im2col_hip);
+  m.impl("col2im", &col2im_hip);
+  m.impl("conv_weight_rsc", &conv_weight_rsc_hip);
+  m.impl("wgrad_rsc_add", &wgrad_rsc_add_hip);
+  m.impl("maxpool_fwd", &maxpool_fwd_hip);
+  m.impl("maxpool_bwd", &maxpool_bwd_hip);
 }

@@ -1,0 +1,397 @@
+// Explicit-GEMM convolutions and the overlapping max-pool of the ImageNet
+// ResNets (gfx950): the 7x7/s2 stem, the strided 3x3 of each stage's first
+// bottleneck, the strided 1x1 downsample and the 3x3/s2 max-pool.
+//
+// Reference model: torchvision-style ResNet-101 of
+// /root/reference/CommEfficient/models/resnets.py:140-230 (stem conv1 + maxpool,
+// Bottleneck conv2 with stride, downsample conv1x1 with stride).  These shapes
+// fall outside the stride-1 3x3 MFMA kernels of conv.hip; MIOpen served them
+// (igemm_fwd / igemm_bwd / igemm_wrw) and at::native the NHWC max-pool
+// (655 us per backward, profiles/r2_pmc_imagenet.txt).  Here every such conv
+// is an explicit GEMM over a bf16 column image:
+//   * im2col_kernel writes col[p][(r*S + s)*C + c] (zero outside the image
+//     and in the padding columns up to Kc); with C % 8 == 0 every thread moves
+//     one 16-byte chunk (8 channels of one tap), otherwise (the 3-channel
+//     stem input, any pixel stride) 8 single gathers;
+//   * the forward / dgrad GEMMs are plain hipBLASLt GEMMs on col and the
+//     [K][Kc] weight image (ops/nn.py);
+//   * col2im_kernel is the dgrad's gather: every input pixel sums the <=
+//     ceil(R/stride) x ceil(S/stride) column entries that read it, in fp32, in
+//     a fixed tap order (deterministic, no atomics, zeros written where no
+//     tap lands -- the strided 1x1 scatter in the same pass);
+//   * wgrad_rsc_add_kernel folds the split-K partial products of the weight
+//     gradient (fixed order), permutes (r, s, c) -> (c, r, s) and adds into
+//     the flat fp32 gradient (or the per-group rows of ops/grouped.py);
+//   * maxpool_fwd_kernel / maxpool_bwd_kernel: k x k max-pool with stride s and
+//     padding p, 1-byte window codes, and a gather backward (each input pixel
+//     collects the outputs whose code points at it).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+#include "sketch_hash.h"
+
+namespace commeff {
+namespace {
+
+typedef uint16_t bf16raw;
+
+struct alignas(16) V8 {
+  bf16raw h[8];
+};
+
+__device__ __forceinline__ float bf2f(bf16raw v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+
+__device__ __forceinline__ bf16raw f2bf(float f) {  // round to nearest even (NaN kept quiet)
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<bf16raw>((u >> 16) | 0x40u);
+  return static_cast<bf16raw>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+int blocks_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  return static_cast<int>(b < 32768 ? b : 32768);
+}
+
+// ---------------------------------------------------------------- im2col
+struct ColGeom {
+  int H, W, C, OH, OW, R, S, stride, pad, Kc, KC8;
+  int64_t sN, sH, sW;  // input strides in elements (channel stride 1)
+  uint32_t total;      // P * Kc / 8
+  FastDivU32 d_kc8, d_ow, d_oh, d_c8, d_s, d_c;
+};
+
+__device__ __forceinline__ void col_row(uint32_t p, const ColGeom& q, int& n, int& oh, int& ow) {
+  const uint32_t p2 = fdiv(p, q.d_ow);
+  ow = static_cast<int>(p - p2 * q.OW);
+  const uint32_t nn = fdiv(p2, q.d_oh);
+  oh = static_cast<int>(p2 - nn * q.OH);
+  n = static_cast<int>(nn);
+}
+
+// C % 8 == 0: one 16-byte tap chunk per thread
+__global__ void __launch_bounds__(256) im2col_vec_kernel(const bf16raw* __restrict__ x,
+                                                         bf16raw* __restrict__ col, ColGeom q) {
+  const uint32_t step = gridDim.x * blockDim.x;
+  const int taps = q.R * q.S;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
+    const uint32_t p = fdiv(g, q.d_kc8);
+    const uint32_t j8 = g - p * q.KC8;
+    const uint32_t tap = fdiv(j8, q.d_c8);
+    const uint32_t c8 = j8 - tap * (q.C / 8);
+    V8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v.h[e] = 0;
+    if (static_cast<int>(tap) < taps) {
+      int n, oh, ow;
+      col_row(p, q, n, oh, ow);
+      const uint32_t r = fdiv(tap, q.d_s);
+      const int s = static_cast<int>(tap - r * q.S);
+      const int ih = oh * q.stride - q.pad + static_cast<int>(r);
+      const int iw = ow * q.stride - q.pad + s;
+      if (ih >= 0 && ih < q.H && iw >= 0 && iw < q.W)
+        v = *reinterpret_cast<const V8*>(x + n * q.sN + ih * q.sH + iw * q.sW + c8 * 8);
+    }
+    *reinterpret_cast<V8*>(col + static_cast<size_t>(g) * 8) = v;
+  }
+}
+
+// any C / pixel stride (the 3-channel network input): 8 single gathers
+__global__ void __launch_bounds__(256) im2col_any_kernel(const bf16raw* __restrict__ x,
+                                                         bf16raw* __restrict__ col, ColGeom q) {
+  const uint32_t step = gridDim.x * blockDim.x;
+  const int rsc = q.R * q.S * q.C;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
+    const uint32_t p = fdiv(g, q.d_kc8);
+    const int j0 = static_cast<int>(g - p * q.KC8) * 8;
+    int n, oh, ow;
+    col_row(p, q, n, oh, ow);
+    const bf16raw* xn = x + n * q.sN;
+    V8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = j0 + e;
+      bf16raw val = 0;
+      if (j < rsc) {
+        const uint32_t tap = fdiv(static_cast<uint32_t>(j), q.d_c);
+        const int c = j - static_cast<int>(tap) * q.C;
+        const uint32_t r = fdiv(tap, q.d_s);
+        const int s = static_cast<int>(tap - r * q.S);
+        const int ih = oh * q.stride - q.pad + static_cast<int>(r);
+        const int iw = ow * q.stride - q.pad + s;
+        if (ih >= 0 && ih < q.H && iw >= 0 && iw < q.W) val = xn[ih * q.sH + iw * q.sW + c];
+      }
+      v.h[e] = val;
+    }
+    *reinterpret_cast<V8*>(col + static_cast<size_t>(g) * 8) = v;
+  }
+}
+
+// ---------------------------------------------------------------- col2im
+struct GatherGeom {
+  int H, W, C, OH, OW, R, S, stride, pad, Kc;
+  uint32_t total;  // N * H * W * C / 8
+  FastDivU32 d_c8, d_w, d_h;
+};
+
+// gx[n][h][w][c] = sum over taps (r, s) hitting (h, w) of gcol[p(oh, ow)][(r*S+s)*C + c]
+__global__ void __launch_bounds__(256) col2im_kernel(const bf16raw* __restrict__ gcol,
+                                                     bf16raw* __restrict__ gx, GatherGeom q) {
+  const uint32_t step = gridDim.x * blockDim.x;
+  const int C8 = q.C / 8;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
+    const uint32_t pix = fdiv(g, q.d_c8);
+    const int c8 = static_cast<int>(g - pix * C8);
+    const uint32_t p2 = fdiv(pix, q.d_w);
+    const int w = static_cast<int>(pix - p2 * q.W);
+    const uint32_t n = fdiv(p2, q.d_h);
+    const int h = static_cast<int>(p2 - n * q.H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int r = 0; r < q.R; ++r) {
+      const int th = h + q.pad - r;  // = oh * stride
+      if (th < 0 || th % q.stride) continue;
+      const int oh = th / q.stride;
+      if (oh >= q.OH) continue;
+      for (int s = 0; s < q.S; ++s) {
+        const int tw = w + q.pad - s;
+        if (tw < 0 || tw % q.stride) continue;
+        const int ow = tw / q.stride;
+        if (ow >= q.OW) continue;
+        const size_t p = (static_cast<size_t>(n) * q.OH + oh) * q.OW + ow;
+        const V8 v = *reinterpret_cast<const V8*>(gcol + p * q.Kc + (r * q.S + s) * q.C + c8 * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f(v.h[e]);
+      }
+    }
+    V8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.h[e] = f2bf(acc[e]);
+    *reinterpret_cast<V8*>(gx + static_cast<size_t>(g) * 8) = o;
+  }
+}
+
+// ---------------------------------------------------------------- weights
+// w fp32 [K][C][R][S] -> bf16 [K][Kc], column (r*S + s)*C + c, zero padding
+__global__ void __launch_bounds__(256) weight_rsc_kernel(const float* __restrict__ w,
+                                                         bf16raw* __restrict__ out, int K, int C,
+                                                         int RS, int Kc) {
+  const int64_t total = static_cast<int64_t>(K) * Kc;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int k = static_cast<int>(i / Kc), j = static_cast<int>(i - static_cast<int64_t>(k) * Kc);
+    bf16raw v = 0;
+    if (j < RS * C) {
+      const int tap = j / C, c = j - tap * C;
+      v = f2bf(w[(static_cast<int64_t>(k) * C + c) * RS + tap]);
+    }
+    out[i] = v;
+  }
+}
+
+// dst[g][k][c][t] (+)= sum_{u < splits} src[g*splits + u][k][t*C + c]   (u in order)
+__global__ void __launch_bounds__(256) wgrad_rsc_add_kernel(float* __restrict__ dst, int64_t dst_ld,
+                                                            const float* __restrict__ src, int G,
+                                                            int splits, int K, int C, int RS, int Kc,
+                                                            int accumulate) {
+  const int per = K * C * RS;
+  const int64_t total = static_cast<int64_t>(G) * per;
+  const int64_t plane = static_cast<int64_t>(K) * Kc;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i / per);
+    const int rem = static_cast<int>(i - static_cast<int64_t>(g) * per);
+    const int k = rem / (C * RS);
+    const int ct = rem - k * (C * RS);
+    const int c = ct / RS, t = ct - c * RS;
+    const float* s0 = src + static_cast<int64_t>(g) * splits * plane + static_cast<int64_t>(k) * Kc + t * C + c;
+    float acc = 0.f;
+    for (int u = 0; u < splits; ++u) acc += s0[u * plane];
+    float* d = dst + g * dst_ld + rem;
+    *d = accumulate ? *d + acc : acc;
+  }
+}
+
+// ---------------------------------------------------------------- max-pool
+struct MaxPoolGeom {
+  int H, W, C, OH, OW, k, s, p;
+  uint32_t total;
+  FastDivU32 d_c8, d_w, d_h;  // output (fwd) or input (bwd) grid
+};
+
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16raw* __restrict__ x,
+                                                          bf16raw* __restrict__ y,
+                                                          uint8_t* __restrict__ codes, MaxPoolGeom q) {
+  const uint32_t step = gridDim.x * blockDim.x;
+  const int C8 = q.C / 8;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
+    const uint32_t pix = fdiv(g, q.d_c8);
+    const int c8 = static_cast<int>(g - pix * C8);
+    const uint32_t p2 = fdiv(pix, q.d_w);
+    const int ow = static_cast<int>(pix - p2 * q.OW);
+    const uint32_t n = fdiv(p2, q.d_h);
+    const int oh = static_cast<int>(p2 - n * q.OH);
+    float best[8];
+    uint32_t arg[8];
+    bool first = true;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = 0.f;
+      arg[e] = 0;
+    }
+    const int h0 = oh * q.s - q.p, w0 = ow * q.s - q.p;
+    for (int dy = 0; dy < q.k; ++dy) {
+      const int ih = h0 + dy;
+      if (ih < 0 || ih >= q.H) continue;
+      for (int dx = 0; dx < q.k; ++dx) {
+        const int iw = w0 + dx;
+        if (iw < 0 || iw >= q.W) continue;
+        const V8 v = *reinterpret_cast<const V8*>(
+            x + ((static_cast<size_t>(n) * q.H + ih) * q.W + iw) * q.C + c8 * 8);
+        const uint32_t code = static_cast<uint32_t>(dy * q.k + dx);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = bf2f(v.h[e]);
+          // first maximum in window order; a NaN wins and stays (PyTorch's rule)
+          if (first || f > best[e] || (f != f && best[e] == best[e])) {
+            best[e] = f;
+            arg[e] = code;
+          }
+        }
+        first = false;
+      }
+    }
+    V8 o;
+    uint64_t cw = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o.h[e] = static_cast<bf16raw>(__float_as_uint(best[e]) >> 16);  // an input value: exact
+      cw |= static_cast<uint64_t>(arg[e]) << (8 * e);
+    }
+    *reinterpret_cast<V8*>(y + static_cast<size_t>(g) * 8) = o;
+    *reinterpret_cast<uint64_t*>(codes + static_cast<size_t>(g) * 8) = cw;
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16raw* __restrict__ gy,
+                                                          const uint8_t* __restrict__ codes,
+                                                          bf16raw* __restrict__ gx, MaxPoolGeom q) {
+  const uint32_t step = gridDim.x * blockDim.x;
+  const int C8 = q.C / 8;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
+    const uint32_t pix = fdiv(g, q.d_c8);
+    const int c8 = static_cast<int>(g - pix * C8);
+    const uint32_t p2 = fdiv(pix, q.d_w);
+    const int w = static_cast<int>(pix - p2 * q.W);
+    const uint32_t n = fdiv(p2, q.d_h);
+    const int h = static_cast<int>(p2 - n * q.H);
+    // outputs whose window [o*s - p, o*s - p + k) contains h
+    const int th = h + q.p, tw = w + q.p;
+    const int oh_lo = th - q.k + 1 > 0 ? (th - q.k + 1 + q.s - 1) / q.s : 0;
+    const int oh_hi = min(th / q.s, q.OH - 1);
+    const int ow_lo = tw - q.k + 1 > 0 ? (tw - q.k + 1 + q.s - 1) / q.s : 0;
+    const int ow_hi = min(tw / q.s, q.OW - 1);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const uint32_t want = static_cast<uint32_t>((th - oh * q.s) * q.k + (tw - ow * q.s));
+        const size_t o = ((static_cast<size_t>(n) * q.OH + oh) * q.OW + ow) * q.C + c8 * 8;
+        const uint64_t cw = *reinterpret_cast<const uint64_t*>(codes + o);
+        const V8 v = *reinterpret_cast<const V8*>(gy + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (((cw >> (8 * e)) & 0xffu) == want) acc[e] += bf2f(v.h[e]);
+      }
+    }
+    V8 out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out.h[e] = f2bf(acc[e]);
+    *reinterpret_cast<V8*>(gx + static_cast<size_t>(g) * 8) = out;
+  }
+}
+
+}  // namespace
+
+void launch_im2col(const Im2colArgs& a, hipStream_t stream) {
+  const int64_t P = static_cast<int64_t>(a.N) * a.OH * a.OW;
+  const int64_t total = P * (a.Kc / 8);
+  if (total == 0) return;
+  ColGeom q;
+  q.H = a.H; q.W = a.W; q.C = a.C; q.OH = a.OH; q.OW = a.OW; q.R = a.R; q.S = a.S;
+  q.stride = a.stride; q.pad = a.pad; q.Kc = a.Kc; q.KC8 = a.Kc / 8;
+  q.sN = a.sN; q.sH = a.sH; q.sW = a.sW;
+  q.total = static_cast<uint32_t>(total);
+  q.d_kc8 = make_fastdiv(q.KC8);
+  q.d_ow = make_fastdiv(a.OW);
+  q.d_oh = make_fastdiv(a.OH);
+  q.d_c8 = make_fastdiv(a.C % 8 == 0 ? a.C / 8 : 1);
+  q.d_s = make_fastdiv(a.S);
+  q.d_c = make_fastdiv(a.C);
+  if (a.vec)
+    hipLaunchKernelGGL(im2col_vec_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, a.x, a.col, q);
+  else
+    hipLaunchKernelGGL(im2col_any_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, a.x, a.col, q);
+}
+
+void launch_col2im(const Im2colArgs& a, const uint16_t* gcol, uint16_t* gx, hipStream_t stream) {
+  const int64_t total = static_cast<int64_t>(a.N) * a.H * a.W * (a.C / 8);
+  if (total == 0) return;
+  GatherGeom q;
+  q.H = a.H; q.W = a.W; q.C = a.C; q.OH = a.OH; q.OW = a.OW; q.R = a.R; q.S = a.S;
+  q.stride = a.stride; q.pad = a.pad; q.Kc = a.Kc;
+  q.total = static_cast<uint32_t>(total);
+  q.d_c8 = make_fastdiv(a.C / 8);
+  q.d_w = make_fastdiv(a.W);
+  q.d_h = make_fastdiv(a.H);
+  hipLaunchKernelGGL(col2im_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gcol, gx, q);
+}
+
+void launch_weight_rsc(const float* w, uint16_t* out, int K, int C, int RS, int Kc, hipStream_t stream) {
+  const int64_t total = static_cast<int64_t>(K) * Kc;
+  if (total == 0) return;
+  hipLaunchKernelGGL(weight_rsc_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, w, out, K, C, RS,
+                     Kc);
+}
+
+void launch_wgrad_rsc_add(float* dst, int64_t dst_ld, const float* src, int G, int splits, int K, int C,
+                          int RS, int Kc, bool accumulate, hipStream_t stream) {
+  const int64_t total = static_cast<int64_t>(G) * K * C * RS;
+  if (total == 0) return;
+  hipLaunchKernelGGL(wgrad_rsc_add_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, dst, dst_ld, src,
+                     G, splits, K, C, RS, Kc, accumulate ? 1 : 0);
+}
+
+void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* codes, int N, int H, int W, int C, int k,
+                        int s, int p, hipStream_t stream) {
+  MaxPoolGeom q;
+  q.H = H; q.W = W; q.C = C; q.k = k; q.s = s; q.p = p;
+  q.OH = (H + 2 * p - k) / s + 1;
+  q.OW = (W + 2 * p - k) / s + 1;
+  const int64_t total = static_cast<int64_t>(N) * q.OH * q.OW * (C / 8);
+  if (total == 0) return;
+  q.total = static_cast<uint32_t>(total);
+  q.d_c8 = make_fastdiv(C / 8);
+  q.d_w = make_fastdiv(q.OW);
+  q.d_h = make_fastdiv(q.OH);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, x, y, codes, q);
+}
+
+void launch_maxpool_bwd(const uint16_t* gy, const uint8_t* codes, uint16_t* gx, int N, int H, int W, int C,
+                        int k, int s, int p, hipStream_t stream) {
+  MaxPoolGeom q;
+  q.H = H; q.W = W; q.C = C; q.k = k; q.s = s; q.p = p;
+  q.OH = (H + 2 * p - k) / s + 1;
+  q.OW = (W + 2 * p - k) / s + 1;
+  const int64_t total = static_cast<int64_t>(N) * H * W * (C / 8);
+  if (total == 0) return;
+  q.total = static_cast<uint32_t>(total);
+  q.d_c8 = make_fastdiv(C / 8);
+  q.d_w = make_fastdiv(W);
+  q.d_h = make_fastdiv(H);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gy, codes, gx, q);
+}
+
+}  // namespace commeff

@@ -311,6 +311,31 @@ void launch_relu_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N
 void launch_relu_maxpool_bwd(const uint16_t* gy, const uint8_t* idx, uint16_t* gx, int N,
                              int H, int W, int C, int k, hipStream_t stream);
 
+// --------------------------------------------------------------- im2col --
+// explicit-GEMM convolutions (csrc/im2col.hip): col [N*OH*OW][Kc] bf16,
+// column (r*S + s)*C + c, zero outside the image and for columns >= R*S*C
+struct Im2colArgs {
+  const uint16_t* x;  // NHWC bf16, channel stride 1, strides sN / sH / sW
+  uint16_t* col;
+  int N, H, W, C, OH, OW, R, S, stride, pad, Kc;
+  int64_t sN, sH, sW;
+  bool vec;  // C % 8 == 0 and 16-byte aligned pixels: 16-byte moves
+};
+void launch_im2col(const Im2colArgs& a, hipStream_t stream);
+// gx NHWC [N][H][W][C] (C % 8 == 0) = the dgrad gather of gcol [N*OH*OW][Kc]
+void launch_col2im(const Im2colArgs& a, const uint16_t* gcol, uint16_t* gx, hipStream_t stream);
+// w fp32 [K][C][R*S] -> bf16 [K][Kc] in the column order above
+void launch_weight_rsc(const float* w, uint16_t* out, int K, int C, int RS, int Kc,
+                       hipStream_t stream);
+// dst[g][k][c][t] (+)= sum over the `splits` partial products src[g*splits+u][k][t*C+c]
+void launch_wgrad_rsc_add(float* dst, int64_t dst_ld, const float* src, int G, int splits,
+                          int K, int C, int RS, int Kc, bool accumulate, hipStream_t stream);
+// k x k / stride s / padding p max-pool on NHWC bf16 (C % 8 == 0), 1-byte codes
+void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* codes, int N, int H, int W,
+                        int C, int k, int s, int p, hipStream_t stream);
+void launch_maxpool_bwd(const uint16_t* gy, const uint8_t* codes, uint16_t* gx, int N, int H,
+                        int W, int C, int k, int s, int p, hipStream_t stream);
+
 // -------------------------------------------------------------- augment --
 // CIFAR-style augmentation of uint8 NHWC images into a bf16 NHWC
 // (channels_last) batch: reflect-pad `pad`, random crop, random h-flip,

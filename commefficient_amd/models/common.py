@@ -10,7 +10,7 @@ import torch.nn.functional as F
 from ..ops import grouped as _grouped
 from ..ops.nn import (_AffineGrouped, conv1x1_passthrough, conv2d_grouped, conv2d_native,
                       conv2d_native_kind, ghost_batch_norm, ghost_bn_native_ok, linear_grouped,
-                      stock_active)
+                      max_pool2d, stock_active)
 
 
 class Mul(nn.Module):
@@ -168,10 +168,12 @@ def has_batchnorm(model: nn.Module) -> bool:
 
 
 class NativeConv2d(nn.Conv2d):
-    """``nn.Conv2d`` (same parameters / state_dict keys) whose bias-free 1x1
-    and stride-1 3x3 convolutions of bf16 channels_last activations run on
-    hipBLASLt GEMMs / the native MFMA kernels (ops/nn.py ``conv2d_native``);
-    every other case is the stock (MIOpen) convolution."""
+    """``nn.Conv2d`` (same parameters / state_dict keys) whose bias-free,
+    ungrouped convolutions of bf16 channels-innermost activations run native
+    (ops/nn.py ``conv2d_native``): 1x1 as hipBLASLt GEMMs, stride-1 3x3 on the
+    MFMA kernels of csrc/conv.hip, anything else (7x7 stems, strided 3x3) as
+    column-image GEMMs (csrc/im2col.hip); grouped / dilated convs are the stock
+    (MIOpen) convolution."""
 
     def forward(self, x):
         gg = _grouped.active() if self.weight.requires_grad else None
@@ -181,7 +183,7 @@ class NativeConv2d(nn.Conv2d):
             kind = conv2d_native_kind(x, self.weight, self.stride, self.padding, self.dilation,
                                       self.groups)
             if kind:
-                return conv2d_native(x, self.weight, kind, self.stride[0], gg)
+                return conv2d_native(x, self.weight, kind, self.stride[0], gg, self.padding[0])
             if gg is not None:
                 return conv2d_grouped(x, self.weight, self.stride, self.padding, self.dilation,
                                       self.groups, gg)
@@ -200,6 +202,18 @@ class NativeConv2d(nn.Conv2d):
                 and tuple(self.stride) == (1, 1)):
             return conv1x1_passthrough(x, self.weight, gg)
         return self(x), x
+
+
+class NativeMaxPool2d(nn.MaxPool2d):
+    """``nn.MaxPool2d`` whose bf16 channels_last case runs the native
+    max-pool (csrc/im2col.hip: window codes + gather backward)."""
+
+    def forward(self, x):
+        k, s, p = (self.kernel_size, self.stride, self.padding)
+        if (isinstance(k, int) and isinstance(s, int) and isinstance(p, int)
+                and self.dilation == 1 and not self.ceil_mode and not self.return_indices):
+            return max_pool2d(x, k, s, p)
+        return super().forward(x)
 
 
 class NativeLinear(nn.Linear):

@@ -22,8 +22,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .common import (GhostBatchNorm2d, NativeConv2d, NativeLinear, ScalarBias, ScalarScale, conv1x1,
-                     conv3x3)
+from .common import (GhostBatchNorm2d, NativeConv2d, NativeLinear, NativeMaxPool2d, ScalarBias,
+                     ScalarScale, conv1x1, conv3x3)
 
 __all__ = ["FixupResNet9", "FixupResNet18", "ResNet18", "FixupResNet50"]
 
@@ -238,7 +238,7 @@ class FixupResNet(nn.Module):
         self.inplanes = 64
         self.conv1 = NativeConv2d(initial_channels, 64, kernel_size=7, stride=2, padding=3, bias=False)
         self.bias1 = nn.Parameter(torch.zeros(1))
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.maxpool = NativeMaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

@@ -17,7 +17,8 @@ import math
 import torch
 import torch.nn as nn
 
-from .common import GhostBatchNorm2d, NativeConv2d, NativeLinear, conv1x1, conv3x3
+from .common import (GhostBatchNorm2d, NativeConv2d, NativeLinear, NativeMaxPool2d, conv1x1,
+                     conv3x3)
 
 __all__ = ["ResNet", "ResNet101", "resnet18", "resnet34", "resnet50", "resnet101", "resnet152",
            "resnext50_32x4d", "resnext101_32x8d", "wide_resnet50_2", "wide_resnet101_2"]
@@ -114,7 +115,7 @@ class ResNet(nn.Module):
         hw = (input_hw + 2 * 3 - 7) // 2 + 1
         self.bn1 = _norm(norm, 64, hw, relu=True)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.maxpool = NativeMaxPool2d(kernel_size=3, stride=2, padding=1)
         hw = (hw + 2 - 3) // 2 + 1
         self.layer1, hw = self._make_layer(block, 64, layers[0], hw)
         self.layer2, hw = self._make_layer(block, 128, layers[1], hw, stride=2)

@@ -669,8 +669,14 @@ def cross_entropy_correct(logits: torch.Tensor, targets: torch.Tensor):
 #     accumulates straight into the flat fp32 gradient view;
 #   * stride-1 3x3 convs with C % 64 == 0 and K % 64 == 0 run on the native
 #     MFMA kernels of csrc/conv.hip (forward, dgrad on the flipped weights,
-#     wgrad accumulating into the flat gradient when K % 128 == 0);
-#   * everything else (7x7 stems, strided 3x3) stays on MIOpen.
+#     wgrad accumulating into the flat gradient when K % 128 == 0, else the
+#     column-image wgrad below);
+#   * every other bias-free, ungrouped conv of a bf16 channels-innermost
+#     activation (the 7x7/s2 stem, strided 3x3, odd kernel sizes) is an
+#     explicit GEMM over a bf16 column image (csrc/im2col.hip): im2col ->
+#     hipBLASLt GEMM forward, GEMM + native col2im gather for dgrad, split-K
+#     GEMM + native permute-add into the flat gradient for wgrad;
+#   * grouped / dilated convs stay on MIOpen.
 # Under ``ops.grouped.grouped_grads`` every path writes per-group weight
 # gradients instead (see ops/grouped.py).
 def _grad_view(weight: torch.Tensor, shape):
@@ -689,6 +695,28 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
 
 
+def _wgrad_splits(Pg: int, K: int, C: int, G: int) -> int:
+    """Split-K factor of a [K, C] weight-gradient GEMM over G groups of Pg rows."""
+    tiles = max(1, (K // 128) * (C // 128))
+    S = 1
+    while S < 64 and Pg % (2 * S) == 0 and Pg // (2 * S) >= 256 and G * S * tiles < 1024:
+        S *= 2
+    return S
+
+
+def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
+    """(parts [G*S, K, C] fp32, S): the split-K partial products of
+    g2d^T x2d for each group of P/G rows, unsummed."""
+    P, K = g2d.shape
+    C = x2d.shape[1]
+    Pg = P // G
+    S = _wgrad_splits(Pg, K, C, G)
+    if G * S == 1:
+        return torch.mm(g2d.t(), x2d, out_dtype=torch.float32).unsqueeze(0), 1
+    return torch.bmm(g2d.view(G * S, Pg // S, K).transpose(1, 2), x2d.view(G * S, Pg // S, C),
+                     out_dtype=torch.float32), S
+
+
 def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> torch.Tensor:
     """dW (+)= g2d^T x2d, a reduction over the P rows, per group of P/G rows.
 
@@ -703,10 +731,7 @@ def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> 
     P, K = g2d.shape
     C = x2d.shape[1]
     Pg = P // G
-    tiles = max(1, (K // 128) * (C // 128))
-    S = 1
-    while S < 64 and Pg % (2 * S) == 0 and Pg // (2 * S) >= 256 and G * S * tiles < 1024:
-        S *= 2
+    S = _wgrad_splits(Pg, K, C, G)
     if G == 1 and S == 1:
         if into is not None:
             return torch.addmm(into, g2d.t(), x2d, out_dtype=torch.float32, out=into)
@@ -722,43 +747,49 @@ def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> 
 
 
 class _Conv1x1(torch.autograd.Function):
+    """1x1 conv as a GEMM on the NHWC image; with stride s the subsampled
+    input is a 1x1 column image (csrc/im2col.hip) and the input gradient
+    comes back through the col2im gather (zeros off the stride grid), both
+    single native passes."""
+
     @staticmethod
     def forward(ctx, x, weight, stride, gg):
-        ctx.in_hw = (x.shape[2], x.shape[3])
-        if stride > 1:
-            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
-        n, c, h, w = x.shape
+        n, c, H, W = x.shape
         k = weight.shape[0]
+        if stride > 1:
+            x2d = _ops().im2col(x, 1, 1, stride, 0, c)
+            h, w = (H - 1) // stride + 1, (W - 1) // stride + 1
+        else:
+            x2d, h, w = _nhwc2d(x), H, W
         wb = weight.detach().view(k, c).to(torch.bfloat16)
-        y2d = torch.mm(_nhwc2d(x), wb.t())
-        ctx.save_for_backward(x, wb)
+        y2d = torch.mm(x2d, wb.t())
+        ctx.save_for_backward(x2d, wb)
         ctx.weight, ctx.stride, ctx.gg = weight, stride, gg
+        ctx.dims = (n, c, H, W, h, w)
         return y2d.view(n, h, w, k).permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, gy):
-        x, wb = ctx.saved_tensors
-        n, c, h, w = x.shape
+        x2d, wb = ctx.saved_tensors
+        n, c, H, W, h, w = ctx.dims
         k = wb.shape[0]
         g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
         gx = None
         if ctx.needs_input_grad[0]:
-            gsub = torch.mm(g2d, wb).view(n, h, w, c).permute(0, 3, 1, 2)
+            gsub = torch.mm(g2d, wb)
             s = ctx.stride
             if s > 1:
-                H, W = ctx.in_hw
-                gx = torch.zeros(n, H, W, c, dtype=gsub.dtype, device=gsub.device).permute(0, 3, 1, 2)
-                gx[:, :, ::s, ::s] = gsub
+                gx = _ops().col2im(gsub, n, H, W, c, 1, 1, s, 0)
             else:
-                gx = gsub
+                gx = gsub.view(n, h, w, c).permute(0, 3, 1, 2)
         gw = None
         if ctx.needs_input_grad[1]:
             if ctx.gg is not None:
                 G = ctx.gg.G
-                _wgrad_gemm(g2d, _nhwc2d(x), ctx.gg.view(ctx.weight).view(G, k, c), G)
+                _wgrad_gemm(g2d, x2d, ctx.gg.view(ctx.weight).view(G, k, c), G)
             else:
                 into = _grad_view(ctx.weight, (k, c))
-                gw = _wgrad_gemm(g2d, _nhwc2d(x), into)
+                gw = _wgrad_gemm(g2d, x2d, into)
                 gw = None if into is not None else gw.view(k, c, 1, 1)
         return gx, gw, None, None
 
@@ -844,24 +875,114 @@ class _Conv3x3(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             w = ctx.weight
             native = w.shape[0] % 128 == 0  # the native wgrad tiles need K % 128 == 0
-
-            def one(gs, xs, dst):
-                if native:
-                    _ops().conv3x3_wgrad_into(gs, xs, dst)
-                else:
-                    dst.add_(_wgrad_mopen(gs, xs, w, (1, 1), (1, 1), (1, 1), 1))
-
-            if ctx.gg is not None and native:
+            if native and ctx.gg is not None:
                 # every group's split-K slabs in one launch + a per-group reduction
                 gv = ctx.gg.view(w)
                 _ops().conv3x3_wgrad_grouped(g, x, gv.shape[0], gv.view(gv.shape[0], -1))
-            elif ctx.gg is not None:
-                _grouped_wgrad_slices(g, x, ctx.gg.view(w), one)
             elif native:
                 gw = _wgrad_to(g, x, w)
-            else:
-                gw = _wgrad_mopen(g, x, w, (1, 1), (1, 1), (1, 1), 1)
+            else:  # K % 128 != 0: column-image GEMM (csrc/im2col.hip)
+                col = _ops().im2col(x, 3, 3, 1, 1, 9 * x.shape[1])
+                gw = _col_wgrad(_nhwc2d(g), col, w, ctx.gg)
         return gx, gw, None
+
+
+def _col_width(C: int, R: int, S: int) -> int:
+    """Column-image row length: R*S*C rounded up to 8 (16-byte rows)."""
+    return -(-C * R * S // 8) * 8
+
+
+def _col_image(weight: torch.Tensor, Kc: int) -> torch.Tensor:
+    """bf16 [K, Kc] GEMM image of ``weight`` with (r, s, c) columns -- for a
+    3x3 with C % 64 == 0 the forward image of ``prepared_conv_weights`` when
+    this pass prepared it (same layout), else one conversion kernel."""
+    K, C, R, S = weight.shape
+    if (R, S) == (3, 3) and Kc == 9 * C:
+        hit = _PREP.get((weight.data_ptr(), weight._version))
+        if hit is not None:
+            return hit[0].view(K, Kc)
+    return _ops().conv_weight_rsc(weight.detach().contiguous(), Kc)
+
+
+def _col_wgrad(g2d: torch.Tensor, col: torch.Tensor, weight: torch.Tensor, gg):
+    """dW of a column-image conv: split-K GEMMs of g2d^T col, then one native
+    pass that sums the splits in order, permutes (r, s, c) -> (c, r, s) and
+    accumulates into the flat fp32 gradient (or the per-group rows of
+    ``gg``).  Returns the gradient for autograd, None when accumulated."""
+    K, C, R, S = weight.shape
+    G = gg.G if gg is not None else 1
+    parts, splits = _wgrad_parts(g2d, col, G)
+    if gg is not None:
+        _ops().wgrad_rsc_add(gg.view(weight).view(G, K, C * R * S), parts, splits, C, R * S, True)
+        return None
+    into = _grad_view(weight, (1, K, C * R * S))
+    dst = into if into is not None else torch.empty(1, K, C * R * S, dtype=torch.float32,
+                                                     device=g2d.device)
+    _ops().wgrad_rsc_add(dst, parts, splits, C, R * S, into is not None)
+    return None if into is not None else dst.view(weight.shape)
+
+
+class _ConvCol(torch.autograd.Function):
+    """Bias-free, ungrouped conv of a bf16 channels-innermost activation as an
+    explicit GEMM over its bf16 column image (csrc/im2col.hip): the 7x7/s2
+    stem (3 channels, any pixel stride: no dgrad, the input is data), the
+    strided 3x3 of each ResNet stage's first bottleneck, any other kernel size.
+    The column image is kept for the weight gradient instead of the input."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad, gg):
+        K, C, R, S = weight.shape
+        N, _, H, W = x.shape
+        Kc = _col_width(C, R, S)
+        col = _ops().im2col(x, R, S, stride, pad, Kc)
+        wt = _col_image(weight, Kc)
+        OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+        y2d = torch.mm(col, wt.t())
+        ctx.save_for_backward(col, wt)
+        ctx.geo = (N, C, H, W, R, S, stride, pad)
+        ctx.weight, ctx.gg = weight, gg
+        return y2d.view(N, OH, OW, K).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        col, wt = ctx.saved_tensors
+        N, C, H, W, R, S, stride, pad = ctx.geo
+        g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = _ops().col2im(torch.mm(g2d, wt), N, H, W, C, R, S, stride, pad)
+        gw = _col_wgrad(g2d, col, ctx.weight, ctx.gg) if ctx.needs_input_grad[1] else None
+        return gx, gw, None, None, None
+
+
+class _MaxPool(torch.autograd.Function):
+    """k x k / stride s / padding p max-pool on NHWC bf16 (csrc/im2col.hip):
+    1-byte window codes forward, a gather backward (no atomics, no zero fill)."""
+
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, codes = _ops().maxpool_fwd(x, k, s, p)
+        ctx.save_for_backward(codes)
+        ctx.conf = (x.shape[2], x.shape[3], k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (codes,) = ctx.saved_tensors
+        H, W, k, s, p = ctx.conf
+        return _ops().maxpool_bwd(gy.to(torch.bfloat16), codes, H, W, k, s, p), None, None, None
+
+
+def maxpool_native_ok(x: torch.Tensor, k: int, s: int, p: int) -> bool:
+    return (not _STOCK[0] and _gpu_bf16_nhwc(x) and x.shape[1] % 8 == 0 and 1 <= k <= 15
+            and s >= 1 and 0 <= 2 * p <= k)
+
+
+def max_pool2d(x: torch.Tensor, k: int, s: int, p: int = 0) -> torch.Tensor:
+    """``F.max_pool2d(x, k, s, p)`` on the native kernels when they apply."""
+    if maxpool_native_ok(x, k, s, p):
+        return _MaxPool.apply(x, int(k), int(s), int(p))
+    return F.max_pool2d(x, k, s, p)
 
 
 class _ConvGrouped(torch.autograd.Function):
@@ -900,8 +1021,11 @@ def _gpu_bf16_nhwc(x: torch.Tensor) -> bool:
 
 def conv2d_native_kind(x: torch.Tensor, weight: torch.Tensor, stride, padding, dilation,
                        groups) -> str:
-    """Which native path serves this convolution: "1x1", "3x3" or "" (MIOpen)."""
-    if _CONV_BACKEND[0] != "native" or _STOCK[0] or groups != 1 or not _gpu_bf16_nhwc(x):
+    """Which native path serves this convolution: "1x1", "3x3", "col" (column
+    image) or "" (MIOpen)."""
+    if _CONV_BACKEND[0] != "native" or _STOCK[0] or groups != 1:
+        return ""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.stride(1) == 1):
         return ""
     if weight.dtype != torch.float32 or weight.dim() != 4 or weight.shape[1] != x.shape[1]:
         return ""
@@ -910,20 +1034,27 @@ def conv2d_native_kind(x: torch.Tensor, weight: torch.Tensor, stride, padding, d
     p = padding if isinstance(padding, int) else (padding[0] if padding[0] == padding[1] else -1)
     dl = dilation if isinstance(dilation, int) else (dilation[0] if dilation[0] == dilation[1]
                                                      else -1)
-    if dl != 1:
+    if dl != 1 or s < 1 or p < 0:
         return ""
-    if (kh, kw) == (1, 1) and p == 0 and s >= 1 and x.shape[1] % 8 == 0 \
-            and weight.shape[0] % 8 == 0:
+    C, K = x.shape[1], weight.shape[0]
+    dense = x.is_contiguous(memory_format=torch.channels_last)
+    if dense and (kh, kw) == (1, 1) and p == 0 and C % 8 == 0 and K % 8 == 0:
         return "1x1"
-    if ((kh, kw) == (3, 3) and s == 1 and p == 1 and x.shape[1] % 64 == 0
-            and weight.shape[0] % 64 == 0):
+    if dense and (kh, kw) == (3, 3) and s == 1 and p == 1 and C % 64 == 0 and K % 64 == 0:
         return "3x3"
+    if K % 8 == 0 and p < kh and p < kw and x.stride(3) >= C and (
+            (dense and C % 8 == 0) or not x.requires_grad):
+        # the col2im dgrad gather needs C % 8 == 0; a data input needs none
+        return "col"
     return ""
 
 
-def conv2d_native(x: torch.Tensor, weight: torch.Tensor, kind: str, stride: int = 1, gg=None):
+def conv2d_native(x: torch.Tensor, weight: torch.Tensor, kind: str, stride: int = 1, gg=None,
+                  padding: int = 0):
     if kind == "1x1":
         return _Conv1x1.apply(x, weight, int(stride), gg)
+    if kind == "col":
+        return _ConvCol.apply(x, weight, int(stride), int(padding), gg)
     return _Conv3x3.apply(x, weight, gg)
 
 

@@ -129,9 +129,12 @@ class FedModel:
         if self.device.type == "cuda":
             find = bool(getattr(args, "miopen_find", 0))
             # the reference: cudnn.deterministic = True, benchmark = False
-            # (cv_train.py:323-326, gpt2_train.py:361-364)
+            # (cv_train.py:323-326, gpt2_train.py:361-364).  MIOpen's
+            # deterministic mode means its naive direct kernels, so it is opt-in
+            # (--miopen_deterministic); every native conv path is deterministic
             torch.backends.cudnn.benchmark = find
-            torch.backends.cudnn.deterministic = not find
+            torch.backends.cudnn.deterministic = (
+                bool(getattr(args, "miopen_deterministic", 0)) and not find)
         from ..ops.nn import set_conv_backend
         set_conv_backend(getattr(args, "conv", "native"))
         self.flat = FlatParams(self.model, self.device)

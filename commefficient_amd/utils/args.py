@@ -195,8 +195,13 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--miopen_find", type=int, default=0,
                    help="1: MIOpen exhaustive kernel search per conv shape (cudnn.benchmark; "
                         "algorithm choice may differ run to run).  Default 0 = the reference's "
-                        "cudnn.deterministic=True, benchmark=False (cv_train.py:325-326); "
-                        "only convs outside the native kernels reach MIOpen")
+                        "benchmark=False (cv_train.py:325-326); only convs outside the native "
+                        "kernels reach MIOpen")
+    g.add_argument("--miopen_deterministic", type=int, default=0,
+                   help="1: cudnn.deterministic=True as the reference sets it "
+                        "(cv_train.py:325).  Off by default: MIOpen serves it with its naive "
+                        "direct-convolution kernels (measured 60x slower on the ImageNet round); "
+                        "the native conv paths are deterministic either way")
     g.add_argument("--conv", choices=["native", "miopen"], default="native",
                    help="3x3 conv(+relu+pool) units: native MFMA kernels (csrc/conv.hip) "
                         "where shapes fit, or MIOpen everywhere")
