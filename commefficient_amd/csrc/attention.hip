@@ -57,9 +57,18 @@ __device__ __forceinline__ uint32_t amix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-__device__ __forceinline__ bool akeep(uint64_t idx, uint32_t seed, uint32_t thresh) {
-  const uint32_t hi = amix32(static_cast<uint32_t>(idx >> 32) + seed);
-  return amix32(static_cast<uint32_t>(idx) ^ hi) >= thresh;
+// dropout keep(idx) = amix32(lo32(idx) ^ amix32(hi32(idx) + seed)) >= thresh
+// (ops/transformer.py _ref_attn), evaluated with the high word hoisted out of
+// the element loops: with DS*DS = 2^20, idx = ((bh*DS + i)*DS + j) has high
+// word bh >> 12 and low word (bh << 20) + (i << 10) + j (mod 2^32)
+__device__ __forceinline__ uint32_t akeep_hs(int bh, uint32_t seed) {
+  return amix32((static_cast<uint32_t>(bh) >> 12) + seed);
+}
+__device__ __forceinline__ uint32_t akeep_lo(int bh, int i, int j) {
+  return (static_cast<uint32_t>(bh) << 20) + (static_cast<uint32_t>(i) << 10) + static_cast<uint32_t>(j);
+}
+__device__ __forceinline__ bool akeep_fast(uint32_t lo, uint32_t hs, uint32_t thresh) {
+  return amix32(lo ^ hs) >= thresh;
 }
 
 __device__ __forceinline__ int crow(int e, int hi) { return (e & 3) + 8 * (e >> 2) + 4 * hi; }
@@ -159,13 +168,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
     sum += __shfl_xor(sum, 1, 64);
     if (i < L && half == 0) a.lse[static_cast<int64_t>(bh) * LM + i] = m + __logf(sum);
     const float inv = 1.f / sum;
-    const uint64_t ib = (static_cast<uint64_t>(bh) * DS + i) * DS + half * 64;
+    const uint32_t hs = akeep_hs(bh, a.seed), ib = akeep_lo(bh, i, half * 64);
 #pragma unroll
     for (int t = 0; t < 64; t += 2) {
       float v0 = p[t] * inv, v1 = p[t + 1] * inv;
       if (a.thresh != 0u) {
-        v0 = akeep(ib + t, a.seed, a.thresh) ? v0 * a.dscale : 0.f;
-        v1 = akeep(ib + t + 1, a.seed, a.thresh) ? v1 * a.dscale : 0.f;
+        v0 = akeep_fast(ib + t, hs, a.thresh) ? v0 * a.dscale : 0.f;
+        v1 = akeep_fast(ib + t + 1, hs, a.thresh) ? v1 * a.dscale : 0.f;
       }
       *reinterpret_cast<uint32_t*>(sP + i * TS + half * 64 + t) =
           static_cast<uint32_t>(bfbits(v0)) | (static_cast<uint32_t>(bfbits(v1)) << 16);
@@ -318,7 +327,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
         const float P = valid ? __expf(s[e] * a.scale - sL[row]) : 0.f;
         bool keep = true;
         if (a.thresh != 0u)
-          keep = akeep((static_cast<uint64_t>(bh) * DS + row) * DS + col, a.seed, a.thresh);
+          keep = akeep_fast(akeep_lo(bh, row, col), akeep_hs(bh, a.seed), a.thresh);
         const float dP = keep ? dp[e] * a.dscale : 0.f;
         pd[ct][e] = keep ? P * a.dscale : 0.f;
         ds[ct][e] = P * (dP - sD[row]) * a.scale;
@@ -603,14 +612,14 @@ __global__ void __launch_bounds__(256, 2) attn_long_fwd_kernel(AttnArgs a) {
       }
       l_run = l_run * alpha + sum;
       m_run = live ? m_new : m_run;
-      const uint64_t ib = (static_cast<uint64_t>(bh) * DS + gi) * DS + kt * TT + half * 32;
+      const uint32_t hs = akeep_hs(bh, a.seed), ib = akeep_lo(bh, gi, kt * TT + half * 32);
       wave_lds_sync();  // every lane holds its S values: P may overwrite the rows
 #pragma unroll
       for (int t = 0; t < 32; t += 2) {
         float v0 = p[t], v1 = p[t + 1];
         if (a.thresh != 0u) {
-          v0 = akeep(ib + t, a.seed, a.thresh) ? v0 * a.dscale : 0.f;
-          v1 = akeep(ib + t + 1, a.seed, a.thresh) ? v1 * a.dscale : 0.f;
+          v0 = akeep_fast(ib + t, hs, a.thresh) ? v0 * a.dscale : 0.f;
+          v1 = akeep_fast(ib + t + 1, hs, a.thresh) ? v1 * a.dscale : 0.f;
         }
         *reinterpret_cast<uint32_t*>(sP + srow * PS + half * 32 + t) =
             static_cast<uint32_t>(bfbits(v0)) | (static_cast<uint32_t>(bfbits(v1)) << 16);
@@ -735,7 +744,7 @@ __global__ void __launch_bounds__(256, 2) attn_long_dq_kernel(AttnArgs a) {
           const bool valid = j <= i && i < L;
           const float P = valid ? __expf(s[e] * a.scale - sLr[row]) : 0.f;
           bool keep = true;
-          if (a.thresh != 0u) keep = akeep((static_cast<uint64_t>(bh) * DS + i) * DS + j, a.seed, a.thresh);
+          if (a.thresh != 0u) keep = akeep_fast(akeep_lo(bh, i, j), akeep_hs(bh, a.seed), a.thresh);
           const float dP = keep ? dp[e] * a.dscale : 0.f;
           ds[e] = P * (dP - sDr[row]) * a.scale;
         }
@@ -843,7 +852,7 @@ __global__ void __launch_bounds__(256, 2) attn_long_dkdv_kernel(AttnArgs a) {
           const bool valid = j <= i && i < L;
           const float P = valid ? __expf(s[e] * a.scale - Li) : 0.f;
           bool keep = true;
-          if (a.thresh != 0u) keep = akeep((static_cast<uint64_t>(bh) * DS + i) * DS + j, a.seed, a.thresh);
+          if (a.thresh != 0u) keep = akeep_fast(akeep_lo(bh, i, j), akeep_hs(bh, a.seed), a.thresh);
           const float dP = keep ? dp[e] * a.dscale : 0.f;
           pd[e] = keep ? P * a.dscale : 0.f;
           ds[e] = P * (dP - Di) * a.scale;

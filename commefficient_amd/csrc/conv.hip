@@ -386,7 +386,22 @@ struct HaloGeom {
   // stacked with ONE shared zero row between them: G * (Rg + 1) + 1), window
   // rows (padded rows x padded width)
   int G, Rg, PW, PR, NPW;
+  // window swizzle (halo_swizzle): 16-byte chunk c of padded row (pr, pc) sits
+  // at slot c ^ (((pc >> 1) + swa * pr + swb * (pr >> 2)) & 7)
+  int swa, swb;
 };
+
+// The A fragments' ds_read_b128 lane groups ({0-3,12-15,20-27}, ...) read
+// window rows that jump by the padding columns at every image row of the
+// tile, so the chunk swizzle must depend on the padded (row, column), not on
+// the flat window row: with the flat-row swizzle (row >> 1) & 7 a 16x16 layer
+// reads its A fragments in 8 LDS cycles instead of 4, an 8x8 layer in 12
+// (a lane-exact model of the four lane groups over every tap, wave and
+// sub-step).  Per width the (swa, swb) below make 32/16/8-wide tiles
+// conflict-free and 4-wide ones 6 cycles (flat swizzle: 8).
+__device__ __forceinline__ int sw_halo(int pr, int pc, const HaloGeom& g) {
+  return ((pc >> 1) + g.swa * pr + g.swb * (pr >> 2)) & 7;
+}
 // TBM = 128 (4 waves, window <= 288 rows) or 256 (8 waves, <= 384 rows:
 // 48 KB + B ring 32 KB = 80 KB, still 2 blocks/CU; the B tile then feeds 256
 // pixels, halving its pieces per MFMA once more)
@@ -439,10 +454,11 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
 #pragma unroll
   for (int i = 0; i < kHaloWinLd; ++i) {
     const int sl = i * NT + tid;
-    const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
+    const int row = sl >> 3;
     int off = -1;
     if (row < hg.NPW) {
       const int pr = row / hg.PW, pc = row - pr * hg.PW, w = pc - 1;
+      const int lc = (sl & 7) ^ sw_halo(pr, pc, hg);
       // padded row pr: G == 1 -> image row h0 + pr - 1 (zero outside the
       // image); else pr = g (Rg + 1) + 1 + h, separators (pr % (Rg+1) == 0) zero
       int img = img0, h = h0 + pr - 1;
@@ -481,13 +497,14 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
 
   // this lane's output pixels (rows of the A fragments) -> padded window rows
   const int hi = lane >> 5, lr = lane & 31;
-  int pb[2];
+  int pbr[2], pbc[2];  // padded (row, column) of the tap-(1, 1) window row
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
     const int m = wr * 64 + mi * 32 + lr;
     const int g = m / (hg.Rg * W), rem = m - g * hg.Rg * W;
     const int r = rem / W, w = rem - r * W;
-    pb[mi] = (g * (hg.Rg + 1) + r + 1) * hg.PW + (w + 1);
+    pbr[mi] = g * (hg.Rg + 1) + r + 1;
+    pbc[mi] = w + 1;
   }
   int offB[4][NI];
 #pragma unroll
@@ -523,14 +540,14 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (s + 1 < s_end) issue_b(s + 1);
-    const int dsh = (tap / 3 - 1) * hg.PW + (tap % 3 - 1);
+    const int dr = tap / 3 - 1, dc = tap % 3 - 1;
     int offA[2];
     int swA[2];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
-      const int row = pb[mi] + dsh;
-      offA[mi] = row * 128;
-      swA[mi] = sw_rd128(row);
+      const int pr = pbr[mi] + dr, pc = pbc[mi] + dc;
+      offA[mi] = (pr * hg.PW + pc) * 128;
+      swA[mi] = sw_halo(pr, pc, hg);
     }
     const unsigned char* sB = smem + kHaloWinBytes + (s & 1) * (BN * 128);
     bf16x8_t af[2][2], bfr[2][NI];
@@ -1349,6 +1366,17 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g, int BN = 128) {
   g->PW = W + 2;
   g->PR = g->G * (g->Rg + 1) + 1;
   g->NPW = g->PR * g->PW;
+  // window swizzle per tile width (see sw_halo); other widths: the flat-row
+  // swizzle (row >> 1) & 7, which is swa = PW / 2 for an even PW
+  static const bool sw_on = [] {  // COMMEFF_HALO_SWIZZLE=0: flat-row swizzle everywhere
+    const char* e = getenv("COMMEFF_HALO_SWIZZLE");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  g->swa = (g->PW / 2) & 7;
+  g->swb = 0;
+  if (sw_on && W == 16) g->swa = 0;
+  if (sw_on && W == 8) g->swa = 4;
+  if (sw_on && W == 4) { g->swa = 2; g->swb = 4; }
   // (ResNet-9 res3, W = 4: 288 padded rows for 128 pixels -- slower alone in
   // scripts/bench_conv.py, but faster inside the round: bench 222-223k with a
   // 256-row cap vs 224-227k with 288, profiles/r1_experiments.md)

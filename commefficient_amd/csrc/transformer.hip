@@ -283,7 +283,7 @@ __device__ __forceinline__ void bias_act_row(const V8& gv, const V8& uv, const f
 }
 
 // one thread per 8-column vector (blockDim = NV), rows strided by the grid,
-// two rows per step (both rows' loads issued before either is used);
+// four rows per step (their loads issued before any is used);
 // part: [gridDim.x][N] fp32 column partials of du
 template <bool GELU>
 __global__ void __launch_bounds__(1024)
@@ -302,18 +302,19 @@ bias_act_bwd_kernel(const V8* __restrict__ gf, const V8* __restrict__ u, const V
     for (int e = 0; e < 8; ++e) bv[e] = 0.f;
   }
   int64_t row = blockIdx.x;
-  for (; row + G < M; row += 2 * G) {
-    const int64_t i0 = row * NV + cv, i1 = (row + G) * NV + cv;
-    const V8 g0 = gf[i0], g1 = gf[i1];
-    V8 u0 = g0, u1 = g1;
-    if (GELU) {
-      u0 = u[i0];
-      u1 = u[i1];
+  constexpr int kR = 4;  // rows per step, every load issued before any is used
+  for (; row + (kR - 1) * G < M; row += kR * G) {
+    V8 gv[kR], uv[kR];
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      const int64_t i = (row + k * G) * NV + cv;
+      gv[k] = gf[i];
+      uv[k] = GELU ? u[i] : gv[k];
     }
-    bias_act_row<GELU>(g0, u0, bv, du, i0, acc);
-    bias_act_row<GELU>(g1, u1, bv, du, i1, acc);
+#pragma unroll
+    for (int k = 0; k < kR; ++k) bias_act_row<GELU>(gv[k], uv[k], bv, du, (row + k * G) * NV + cv, acc);
   }
-  if (row < M) {
+  for (; row < M; row += G) {
     const int64_t i0 = row * NV + cv;
     const V8 g0 = gf[i0];
     bias_act_row<GELU>(g0, GELU ? u[i0] : g0, bv, du, i0, acc);
@@ -323,38 +324,46 @@ bias_act_bwd_kernel(const V8* __restrict__ gf, const V8* __restrict__ u, const V
   *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
-// out_q[c] = sum_b part[b*stride + q*N + c]: 64 columns per 1024-thread
-// block; wave w sums its contiguous share of the partials with 4 independent
-// accumulators (loads in flight), the 16 wave sums are combined in wave order
-// through LDS -- a fixed summation order, so the result is deterministic
+// out_q[c] = sum_b part[b*stride + q*N + c]: 16 columns per 1024-thread
+// block (Q*N/16 blocks: ~150-200 for GPT-2, the kernel is latency-bound);
+// lane l of wave w reads column l % 16 of rows w*per + l/16 + 4i (every load
+// of the lane in flight at once), sums them in row order, then the 4 row
+// phases (xor-shuffles 16, 32) and the 16 waves (LDS, wave order) combine in a
+// fixed order -- the result is deterministic
 __global__ void __launch_bounds__(1024)
 colsum_final_kernel(const float* __restrict__ part, int G, int Q, int64_t N, int64_t stride,
                     ColsumOut out) {
-  __shared__ float red[16][64];
+  __shared__ float red[16][16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t col = static_cast<int64_t>(blockIdx.x) * 64 + lane;  // over Q*N
+  const int cl = lane & 15, ph = lane >> 4;
+  const int64_t col = static_cast<int64_t>(blockIdx.x) * 16 + cl;  // over Q*N
   const bool ok = col < Q * N;
   const int per = (G + 15) / 16;
   const int b0 = w * per;
   const int b1 = b0 + per < G ? b0 + per : G;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  float acc = 0.f;
   if (ok) {
     const float* src = part + col;
-    int b = b0;
-    for (; b + 3 < b1; b += 4) {
-      a0 += src[static_cast<int64_t>(b) * stride];
-      a1 += src[static_cast<int64_t>(b + 1) * stride];
-      a2 += src[static_cast<int64_t>(b + 2) * stride];
-      a3 += src[static_cast<int64_t>(b + 3) * stride];
+    constexpr int kU = 16;
+    for (int b = b0 + ph; b < b1; b += 4 * kU) {
+      float t[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int bb = b + 4 * u;
+        t[u] = bb < b1 ? src[static_cast<int64_t>(bb) * stride] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc += t[u];
     }
-    for (; b < b1; ++b) a0 += src[static_cast<int64_t>(b) * stride];
   }
-  red[w][lane] = (a0 + a1) + (a2 + a3);
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  if (ph == 0) red[w][cl] = acc;
   __syncthreads();
-  if (w == 0 && ok) {
+  if (w == 0 && ph == 0 && ok) {
     float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][lane];
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
     const int q = static_cast<int>(col / N);
     const int64_t c = col - q * N;
     void* o = q == 0 ? out.p[0] : (q == 1 ? out.p[1] : out.p[2]);
@@ -376,6 +385,8 @@ uint32_t drop_threshold(float p) {
   return t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t);
 }
 
+// LN backward blocks (= column-partial rows for colsum_final); 1536 blocks
+// measured slower than 512 for a GPT-2 round (658 vs 589 us / 25 calls)
 int ln_grid(int64_t M) {
   const int64_t b = (M + 7) / 8;
   return static_cast<int>(b < 512 ? (b > 0 ? b : 1) : 512);
@@ -467,7 +478,7 @@ void launch_bias_act_bwd(const void* gf, const void* u, const void* b, void* du,
 void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,
                          const ColsumOut& out, hipStream_t stream) {
   const int64_t cols = Q * N;
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(static_cast<uint32_t>((cols + 63) / 64)),
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(static_cast<uint32_t>((cols + 15) / 16)),
                      dim3(1024), 0, stream, part, G, Q, N, stride, out);
 }
 
