@@ -657,6 +657,140 @@ __global__ void __launch_bounds__(256, 2) attn_long_fwd_kernel(AttnArgs a) {
   }
 }
 
+// Forward, transposed formulation: the same tiles and online softmax with the
+// scores computed as S^T = K Q^T, so the accumulator lane (query lr, half hi)
+// holds 16 keys of ITS query: the row max / sum are lane-local plus one
+// xor-shuffle with lane ^ 32, P never leaves the registers (it is the B
+// operand of O^T += V^T P^T: an accumulator's keys 8 (ks & 1) .. + 7 are the
+// operand's k slots, and the V^T operand is read with the SAME key order --
+// transposing reads of rows kb + 4 hi + 0..3 and kb + 8 + 4 hi + 0..3), and the
+// O rescale by alpha and the final 1 / l are lane-local.  No per-wave S / P /
+// alpha images: 37 KB of LDS (the K / V ring) and no wave-level LDS round
+// trips between the two MFMA phases.
+template <int LD>
+__device__ __forceinline__ bf16x8_t tr_op_perm(const uint16_t* img, int cb, int kb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = cb + 16 * (g & 1) + 4 * p;
+  const int row = kb + 4 * (g >> 1) + q;
+  const unsigned char* b = reinterpret_cast<const unsigned char*>(img);
+  return tr_read(b + (row * LD + col) * 2, b + ((row + 8) * LD + col) * 2);
+}
+
+__global__ void __launch_bounds__(256, 3) attn_long_fwd_t_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);   // [2][TT][T2]
+  uint16_t* sV = sK + 2 * TT * T2;                     // [2][TT][T2]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
+  const int tiles = a.lse_ld / QB;
+  const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
+  const int n = bh / a.nh, h = bh - n * a.nh;
+  const int L = min(a.len[n], a.lse_ld);
+  if (q0 >= L) return;
+  const int64_t r0 = a.start[n];
+  const int H = a.nh * HD;
+  const int64_t ld3 = 3 * static_cast<int64_t>(H);
+  const int wq0 = q0 + 32 * w;
+  const bool wvalid = wq0 < L;
+  const int qi = wq0 + lr;  // this lane's query
+  const uint16_t* kbase = a.qkv + H + h * HD;
+  const uint16_t* vbase = a.qkv + 2 * H + h * HD;
+  bf16x8_t qf[4];  // B operand: query lr, dims 16 ks + 8 hi ..
+  frag_load(qf, a.qkv + h * HD, ld3, r0 + qi, qi < L, hi);
+  f32x16_t o[2] = {zero16(), zero16()};  // O^T: dims 32 dt + crow(e, hi), query lr
+  float m_run = -__builtin_huge_valf(), l_run = 0.f;
+  const uint32_t hs = akeep_hs(bh, a.seed);
+  const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
+  {
+    const TilePieces pk = tile_fetch(kbase, ld3, r0, 0, L, tid);
+    const TilePieces pv = tile_fetch(vbase, ld3, r0, 0, L, tid);
+    tile_store(sK, pk, tid);
+    tile_store(sV, pv, tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const uint16_t* cK = sK + (kt & 1) * TT * T2;
+    const uint16_t* cV = sV + (kt & 1) * TT * T2;
+    TilePieces pk, pv;
+    const bool more = kt + 1 < nkt;
+    if (more) {  // next tile's loads in flight during this tile's math
+      pk = tile_fetch(kbase, ld3, r0, (kt + 1) * TT, L, tid);
+      pv = tile_fetch(vbase, ld3, r0, (kt + 1) * TT, L, tid);
+    }
+    if (wvalid && kt * TT <= wq0 + 31) {
+      f32x16_t s[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {  // keys 32 ct ..
+        s[ct] = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(cK + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
+          s[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[ct], 0, 0, 0);
+        }
+      }
+      float mt = -__builtin_huge_valf();
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int j = kt * TT + 32 * ct + crow(e, hi);
+          const float v = (j <= qi && qi < L) ? s[ct][e] * a.scale : -__builtin_huge_valf();
+          s[ct][e] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_run, mt);
+      const bool live = m_new > -__builtin_huge_valf();
+      const float alpha = live ? __expf(m_run - m_new) : 1.f;
+      float sum = 0.f;
+      bf16x8_t pf[4];  // B operand of O^T: keys of k-step ks = accumulator ct = ks >> 1, e = 8 (ks & 1) ..
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float p = live ? __expf(s[ct][e] - m_new) : 0.f;
+          sum += p;
+          if (a.thresh != 0u) {
+            const int j = kt * TT + 32 * ct + crow(e, hi);
+            p = akeep_fast(akeep_lo(bh, qi, j), hs, a.thresh) ? p * a.dscale : 0.f;
+          }
+          pf[2 * ct + (e >> 3)][e & 7] = static_cast<__bf16>(p);
+        }
+      l_run = l_run * alpha + sum;
+      m_run = live ? m_new : m_run;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_op_perm<T2>(cV, 32 * dt, 16 * ks, lane), pf[ks],
+                                                          o[dt], 0, 0, 0);
+    }
+    if (more) {  // the other buffer was last read before the previous barrier
+      tile_store(sK + ((kt + 1) & 1) * TT * T2, pk, tid);
+      tile_store(sV + ((kt + 1) & 1) * TT * T2, pv, tid);
+    }
+    __syncthreads();
+  }
+  if (wvalid && qi < L) {
+    const float l = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = 1.f / l;
+    if (hi == 0) a.lse[static_cast<int64_t>(bh) * a.lse_ld + qi] = m_run + __logf(l);
+    uint16_t* orow = a.o + (r0 + qi) * H + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {  // dims 32 dt + 8 grp + 4 hi .. + 3
+        uint2 v;
+        v.x = pack_bf16(o[dt][4 * grp] * inv, o[dt][4 * grp + 1] * inv);
+        v.y = pack_bf16(o[dt][4 * grp + 2] * inv, o[dt][4 * grp + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * grp + 4 * hi) = v;
+      }
+  }
+}
+
 // dQ (+ D): LDS K, V [2][64][T2] ring, per wave: dS^T image [64][TI] bf16,
 // D / LSE [32]  (~56 KB)
 __global__ void __launch_bounds__(256, 2) attn_long_dq_kernel(AttnArgs a) {
@@ -894,6 +1028,7 @@ __global__ void __launch_bounds__(256, 2) attn_long_dkdv_kernel(AttnArgs a) {
 }
 
 constexpr size_t kLongFwdLds = 4 * TT * T2 * 2 + 4 * 32 * F2 * 4 + 4 * 32 * 4;
+constexpr size_t kLongFwdTLds = 4 * TT * T2 * 2;  // the K / V ring only
 constexpr size_t kLongDqLds = 4 * TT * T2 * 2 + 4 * TT * TI * 2 + 4 * 64 * 4;
 constexpr size_t kLongDkdvLds = 4 * TT * T2 * 2 + 4 * TT * 4 + 4 * 2 * TT * TI * 2;
 static_assert(kLongDkdvLds <= 80 * 1024 && kLongFwdLds <= 80 * 1024 && kLongDqLds <= 80 * 1024,
@@ -919,16 +1054,25 @@ uint32_t attn_thresh(float p) {
 void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream) {
   if (nseq == 0) return;
   if (a.lse_ld > LM) {  // long sequences: flash-style kernel
+    static const bool transposed = [] {  // COMMEFF_ATTN_FWD_T=0: the S-image forward
+      const char* e = getenv("COMMEFF_ATTN_FWD_T");
+      return !(e != nullptr && e[0] == '0');
+    }();
     static bool lattr = false;
     if (!lattr) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_fwd_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongFwdLds));
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_fwd_t_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongFwdTLds));
       lattr = true;
     }
     a.thresh = attn_thresh(p_drop);
     a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-    hipLaunchKernelGGL(attn_long_fwd_kernel, dim3(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB))),
-                       dim3(256), kLongFwdLds, stream, a);
+    const dim3 grid(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB)));
+    if (transposed)
+      hipLaunchKernelGGL(attn_long_fwd_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
+    else
+      hipLaunchKernelGGL(attn_long_fwd_kernel, grid, dim3(256), kLongFwdLds, stream, a);
     return;
   }
   static bool attr = false;
