@@ -174,7 +174,7 @@ enc_p1_kernel(const float* __restrict__ vec, const float* __restrict__ wvec, flo
 
 // ----------------------------------------------- encode P2 (dense, fixed point)
 // gfx950 retires LDS float atomics at ~0.33 lanes/clk/CU but 64-bit integer
-// ones at ~5.9 (scripts/dev/lds_atomic_bench.hip, measured), so the dense P2
+// ones at ~5.9 (scripts/experiments/lds_atomic_bench.hip, measured), so the dense P2
 // accumulates in 64-bit fixed point: every value is scaled by the same power
 // of two 2^shift with max|v| * 2^shift < 2^46 (18 bits of headroom: buckets of
 // up to 65536 entries, checked when the plan is built), rounded to an integer

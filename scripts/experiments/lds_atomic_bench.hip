@@ -1,6 +1,6 @@
 // LDS atomic-add throughput on gfx950: f32 vs u32 vs u64 (fixed point) at
 // random addresses in an 8192-entry tile (the dense sketch encode P2 pattern).
-// hipcc -O3 --offload-arch=gfx950 scripts/dev/lds_atomic_bench.hip -o /tmp/lab
+// hipcc -O3 --offload-arch=gfx950 scripts/experiments/lds_atomic_bench.hip -o /tmp/lab
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
