@@ -98,7 +98,8 @@ def test_gloo_two_ranks_match_single_process(mode):
 def test_two_ranks_one_gpu(mode):
     """The multi-rank GPU path (device tensors, native kernels, replicated
     server update) with two ranks sharing cuda:0 over gloo (RCCL refuses
-    duplicate devices): replicas bit-identical, losses close to one rank."""
+    duplicate devices): replicas bit-identical, round-0 losses equal to the
+    single-rank run, weights equal up to rare top-k near-tie flips."""
     import subprocess
     import sys
     worker = os.path.join(os.path.dirname(__file__), "dist_gpu_worker.py")
@@ -115,9 +116,23 @@ def test_two_ranks_one_gpu(mode):
         s = torch.load(os.path.join(d, "r0_w1.pt"), weights_only=True)
     assert torch.equal(r0["w"], r1["w"]), "replicas diverged"
     assert torch.isfinite(r0["loss"]).all()
-    # bf16 forward/backward over a different per-rank batch split: close, not equal
-    torch.testing.assert_close(r0["loss"], s["loss"], rtol=2e-2, atol=2e-2)
-    assert (r0["w"] - s["w"]).abs().max() < 0.05
+    dw = (r0["w"] - s["w"]).abs()
+    print(f"round-0 loss max diff {(r0['loss'][0] - s['loss'][0]).abs().max().item():.3e}; "
+          f"later rounds {(r0['loss'] - s['loss']).abs().max().item():.3e}; "
+          f"|dw| max {dw.max().item():.3e}, frac > 1e-4 {(dw > 1e-4).float().mean().item():.3e}, "
+          f"frac > 0 {(dw > 0).float().mean().item():.3e}")
+    # round 0 runs at identical weights, and every example's forward is
+    # computed the same way whatever the per-rank batch split (per-pixel
+    # MFMA accumulation order, per-example head): identical per-client losses
+    torch.testing.assert_close(r0["loss"][0], s["loss"][0], rtol=1e-6, atol=1e-7)
+    # the weight gradient sums over a rank's examples first (fp32 reassociation,
+    # ~1e-7 relative), so a top-k near-tie can flip: of the k = 5,000
+    # coordinates updated per round, only a few may differ afterwards
+    # (measured: 0-7.6e-5 of the coordinates beyond 1e-4, max |dw| 1.6e-4;
+    # later-round losses 4-7e-6 apart)
+    assert (dw > 1e-4).float().mean() < 5e-4, dw
+    assert dw.max() < 1e-3, dw.max()
+    torch.testing.assert_close(r0["loss"], s["loss"], rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.gpu

@@ -165,11 +165,14 @@ def test_engine_grouped_matches_per_client_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("G", [2, 8])
 def test_native_layers_per_group_grads_gpu(G):
-    """GPU bf16 layers (native 1x1/3x3, ghost BN kernel, MIOpen stem and
-    strided conv, batched-GEMM linear): the grouped rows vs the same bf16
-    model run one group at a time into the flat gradient.  (vs fp32 autograd
-    both are ~0.5 off: 4-pixel BN groups at layer 4 amplify bf16 rounding --
-    the comparison that isolates the grouping is against bf16 per group.)"""
+    """GPU bf16 layers (native 1x1/3x3, ghost BN kernel, column-image stem
+    and strided convs, native max-pool, batched-GEMM linear): the grouped rows
+    vs the same bf16 model run one group at a time into the flat gradient.
+    (vs fp32 autograd both are ~0.5 off: small BN groups at layer 4 amplify
+    bf16 rounding -- the comparison that isolates the grouping is against bf16
+    per group.)  The two bf16 runs differ by 0.4-1.0 % (measured): the 1x1
+    GEMMs tile a 4- and a 4G-image batch differently and the split-K weight
+    gradients sum in a different order, each rounding its bf16 outputs."""
     torch.manual_seed(0)
     # random-init logits are large enough to saturate the softmax, where bf16
     # rounding of the logits flips the loss gradient (both bf16 paths were
@@ -198,6 +201,6 @@ def test_native_layers_per_group_grads_gpu(G):
         per_ex = F.cross_entropy(model(x).float(), y, reduction="none")
         (per_ex.sum() / n).backward()
     assert flat.g.abs().max() == 0
+    errs = [((buf[g] - rows[g]).norm() / rows[g].norm()).item() for g in range(G)]
     for g in range(G):
-        err = (buf[g] - rows[g]).norm() / rows[g].norm()
-        assert err < 0.1, (g, err.item())
+        assert errs[g] < 0.03, (g, errs[g])
