@@ -791,6 +791,122 @@ __global__ void __launch_bounds__(256, 3) attn_long_fwd_t_kernel(AttnArgs a) {
   }
 }
 
+// dQ (+ D), transposed formulation (as attn_long_fwd_t_kernel): S^T = K Q^T
+// and dP^T = V dO^T put one query per lane, so LSE_i and D_i are lane-local,
+// dS^T = P^T (dP^T - D) never leaves the registers, and dQ^T += K^T dS^T reads
+// K^T with the permuted key order of the register operand.  LDS: the K / V
+// ring only.
+__global__ void __launch_bounds__(256, 3) attn_long_dq_t_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sV = sK + 2 * TT * T2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
+  const int tiles = a.lse_ld / QB;
+  const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
+  const int n = bh / a.nh, h = bh - n * a.nh;
+  const int L = min(a.len[n], a.lse_ld);
+  if (q0 >= L) return;
+  const int64_t r0 = a.start[n];
+  const int H = a.nh * HD;
+  const int64_t ld3 = 3 * static_cast<int64_t>(H);
+  const int wq0 = q0 + 32 * w;
+  const bool wvalid = wq0 < L;
+  const int qi = wq0 + lr;
+  const bool qok = qi < L;
+  const uint16_t* kbase = a.qkv + H + h * HD;
+  const uint16_t* vbase = a.qkv + 2 * H + h * HD;
+  bf16x8_t qf[4], gf[4];  // B operands: query lr, dims 16 ks + 8 hi ..
+  frag_load(qf, a.qkv + h * HD, ld3, r0 + qi, qok, hi);
+  frag_load(gf, a.dout + h * HD, H, r0 + qi, qok, hi);
+  float Di = 0.f, Li = 0.f;
+  {  // D_i = dO_i . O_i (lanes lr and lr + 32: 32 dims each) and LSE_i
+    if (qok) {
+      const uint16_t* orow = a.o + (r0 + qi) * H + h * HD + hi * 32;
+      const uint16_t* grow = a.dout + (r0 + qi) * H + h * HD + hi * 32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const v4u ov = *reinterpret_cast<const v4u*>(orow + 8 * q);
+        const v4u gv = *reinterpret_cast<const v4u*>(grow + 8 * q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int sh = 16 * (e & 1);
+          Di += bfval(static_cast<uint16_t>((ov[e >> 1] >> sh) & 0xffffu)) *
+                bfval(static_cast<uint16_t>((gv[e >> 1] >> sh) & 0xffffu));
+        }
+      }
+      Li = a.lse[static_cast<int64_t>(bh) * a.lse_ld + qi];
+    }
+    Di += __shfl_xor(Di, 32, 64);
+    if (qok && hi == 0) a.dbuf[static_cast<int64_t>(bh) * a.lse_ld + qi] = Di;
+  }
+  const uint32_t hs = akeep_hs(bh, a.seed);
+  f32x16_t gq[2] = {zero16(), zero16()};  // dQ^T: dims 32 dt + crow(e, hi), query lr
+  const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
+  {
+    const TilePieces pk = tile_fetch(kbase, ld3, r0, 0, L, tid);
+    const TilePieces pv = tile_fetch(vbase, ld3, r0, 0, L, tid);
+    tile_store(sK, pk, tid);
+    tile_store(sV, pv, tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const uint16_t* cK = sK + (kt & 1) * TT * T2;
+    const uint16_t* cV = sV + (kt & 1) * TT * T2;
+    TilePieces pk, pv;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      pk = tile_fetch(kbase, ld3, r0, (kt + 1) * TT, L, tid);
+      pv = tile_fetch(vbase, ld3, r0, (kt + 1) * TT, L, tid);
+    }
+    if (wvalid && kt * TT <= wq0 + 31) {
+      bf16x8_t df[4];  // dS^T as the B operand of k-step ks (permuted key order)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {  // keys 32 ct ..
+        f32x16_t s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int ko = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t*>(cK + ko), qf[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t*>(cV + ko), gf[ks], dp, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int j = kt * TT + 32 * ct + crow(e, hi);
+          const bool valid = j <= qi && qok;
+          const float P = valid ? __expf(s[e] * a.scale - Li) : 0.f;
+          bool keep = true;
+          if (a.thresh != 0u) keep = akeep_fast(akeep_lo(bh, qi, j), hs, a.thresh);
+          const float dP = keep ? dp[e] * a.dscale : 0.f;
+          df[2 * ct + (e >> 3)][e & 7] = static_cast<__bf16>(P * (dP - Di) * a.scale);
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          gq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_op_perm<T2>(cK, 32 * dt, 16 * ks, lane), df[ks],
+                                                           gq[dt], 0, 0, 0);
+    }
+    if (more) {
+      tile_store(sK + ((kt + 1) & 1) * TT * T2, pk, tid);
+      tile_store(sV + ((kt + 1) & 1) * TT * T2, pv, tid);
+    }
+    __syncthreads();
+  }
+  if (wvalid && qok) {
+    uint16_t* drow = a.dqkv + (r0 + qi) * ld3 + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {  // dims 32 dt + 8 grp + 4 hi .. + 3
+        uint2 v;
+        v.x = pack_bf16(gq[dt][4 * grp], gq[dt][4 * grp + 1]);
+        v.y = pack_bf16(gq[dt][4 * grp + 2], gq[dt][4 * grp + 3]);
+        *reinterpret_cast<uint2*>(drow + 32 * dt + 8 * grp + 4 * hi) = v;
+      }
+  }
+}
+
 // dQ (+ D): LDS K, V [2][64][T2] ring, per wave: dS^T image [64][TI] bf16,
 // D / LSE [32]  (~56 KB)
 __global__ void __launch_bounds__(256, 2) attn_long_dq_kernel(AttnArgs a) {
@@ -1027,8 +1143,141 @@ __global__ void __launch_bounds__(256, 2) attn_long_dkdv_kernel(AttnArgs a) {
   }
 }
 
+// dK, dV with the scores in query-row form: S = Q K^T and dP = dO V^T put one
+// KEY per lane (column lr), so P_drop and dS are, as they come out of the
+// accumulators, the B operands of dV^T += dO^T P_drop and dK^T += Q^T dS (key
+// n = lane, query k in the accumulator's permuted order; dO^T / Q^T read with
+// the same order).  LSE / D per query row come from the staged [2][64] rows.
+// LDS: the Q / dO ring + LSE / D (38 KB), no per-wave P / dS images.
+__global__ void __launch_bounds__(256, 2) attn_long_dkdv_s_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sG = sQ + 2 * TT * T2;
+  float* sL = reinterpret_cast<float*>(sG + 2 * TT * T2);  // [2][TT]
+  float* sD = sL + 2 * TT;                                  // [2][TT]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
+  const int tiles = a.lse_ld / QB;
+  const int bh = blockIdx.x / tiles, k0 = (blockIdx.x - bh * tiles) * QB;
+  const int n = bh / a.nh, h = bh - n * a.nh;
+  const int L = min(a.len[n], a.lse_ld);
+  if (k0 >= L) return;
+  const int64_t r0 = a.start[n];
+  const int H = a.nh * HD;
+  const int64_t ld3 = 3 * static_cast<int64_t>(H);
+  const int wk0 = k0 + 32 * w;
+  const bool wvalid = wk0 < L;
+  const int kj = wk0 + lr;  // this lane's key
+  const uint16_t* qbase = a.qkv + h * HD;
+  const uint16_t* gbase = a.dout + h * HD;
+  const float* lrow = a.lse + static_cast<int64_t>(bh) * a.lse_ld;
+  const float* drow = a.dbuf + static_cast<int64_t>(bh) * a.lse_ld;
+  bf16x8_t kf[4], vf[4];  // B operands: key lr, dims 16 ks + 8 hi ..
+  frag_load(kf, a.qkv + H + h * HD, ld3, r0 + kj, kj < L, hi);
+  frag_load(vf, a.qkv + 2 * H + h * HD, ld3, r0 + kj, kj < L, hi);
+  const uint32_t hs = akeep_hs(bh, a.seed);
+  f32x16_t gk[2] = {zero16(), zero16()}, gv[2] = {zero16(), zero16()};  // dims 32 dt + crow, key lr
+  {
+    const TilePieces pq = tile_fetch(qbase, ld3, r0, k0, L, tid);
+    const TilePieces pg = tile_fetch(gbase, H, r0, k0, L, tid);
+    tile_store(sQ, pq, tid);
+    tile_store(sG, pg, tid);
+    if (tid < TT) {
+      const int i = k0 + tid;
+      sL[tid] = i < L ? lrow[i] : 0.f;
+      sD[tid] = i < L ? drow[i] : 0.f;
+    }
+  }
+  __syncthreads();
+  for (int qs = k0, it = 0; qs < L; qs += TT, ++it) {
+    const int b = it & 1;
+    const uint16_t* cQ = sQ + b * TT * T2;
+    const uint16_t* cG = sG + b * TT * T2;
+    const float* cL = sL + b * TT;
+    const float* cD = sD + b * TT;
+    TilePieces pq, pg;
+    float nl = 0.f, nd = 0.f;
+    const bool more = qs + TT < L;
+    if (more) {
+      pq = tile_fetch(qbase, ld3, r0, qs + TT, L, tid);
+      pg = tile_fetch(gbase, H, r0, qs + TT, L, tid);
+      if (tid < TT) {
+        const int i = qs + TT + tid;
+        nl = i < L ? lrow[i] : 0.f;
+        nd = i < L ? drow[i] : 0.f;
+      }
+    }
+    if (wvalid && qs + TT - 1 >= wk0) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {  // queries 32 ct .. : k-steps 2 ct, 2 ct + 1
+        f32x16_t s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int qo = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t*>(cQ + qo), kf[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8_t*>(cG + qo), vf[ks], dp, 0, 0, 0);
+        }
+        bf16x8_t pfr[2], sfr[2];  // P_drop / dS as B operands (permuted query order)
+#pragma unroll
+        for (int grp = 0; grp < 4; ++grp) {
+          const int qr = 32 * ct + 8 * grp + 4 * hi;  // tile rows qr .. qr + 3 (e = 4 grp ..)
+          const float4 l4 = *reinterpret_cast<const float4*>(cL + qr);
+          const float4 d4 = *reinterpret_cast<const float4*>(cD + qr);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e = 4 * grp + t;
+            const int i = qs + qr + t;  // query
+            const bool valid = kj <= i && i < L;
+            const float P = valid ? __expf(s[e] * a.scale - lv[t]) : 0.f;
+            bool keep = true;
+            if (a.thresh != 0u) keep = akeep_fast(akeep_lo(bh, i, kj), hs, a.thresh);
+            const float dP = keep ? dp[e] * a.dscale : 0.f;
+            pfr[e >> 3][e & 7] = static_cast<__bf16>(keep ? P * a.dscale : 0.f);
+            sfr[e >> 3][e & 7] = static_cast<__bf16>(P * (dP - dv[t]) * a.scale);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int kb = 32 * ct + 16 * u;
+            gv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_op_perm<T2>(cG, 32 * dt, kb, lane), pfr[u],
+                                                             gv[dt], 0, 0, 0);
+            gk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_op_perm<T2>(cQ, 32 * dt, kb, lane), sfr[u],
+                                                             gk[dt], 0, 0, 0);
+          }
+      }
+    }
+    if (more) {
+      tile_store(sQ + (b ^ 1) * TT * T2, pq, tid);
+      tile_store(sG + (b ^ 1) * TT * T2, pg, tid);
+      if (tid < TT) {
+        sL[(b ^ 1) * TT + tid] = nl;
+        sD[(b ^ 1) * TT + tid] = nd;
+      }
+    }
+    __syncthreads();
+  }
+  if (wvalid && kj < L) {
+    uint16_t* krow = a.dqkv + (r0 + kj) * ld3 + H + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int grp = 0; grp < 4; ++grp) {  // dims 32 dt + 8 grp + 4 hi .. + 3
+        uint2 k2, v2;
+        k2.x = pack_bf16(gk[dt][4 * grp], gk[dt][4 * grp + 1]);
+        k2.y = pack_bf16(gk[dt][4 * grp + 2], gk[dt][4 * grp + 3]);
+        v2.x = pack_bf16(gv[dt][4 * grp], gv[dt][4 * grp + 1]);
+        v2.y = pack_bf16(gv[dt][4 * grp + 2], gv[dt][4 * grp + 3]);
+        *reinterpret_cast<uint2*>(krow + 32 * dt + 8 * grp + 4 * hi) = k2;
+        *reinterpret_cast<uint2*>(krow + H + 32 * dt + 8 * grp + 4 * hi) = v2;
+      }
+  }
+}
+
 constexpr size_t kLongFwdLds = 4 * TT * T2 * 2 + 4 * 32 * F2 * 4 + 4 * 32 * 4;
 constexpr size_t kLongFwdTLds = 4 * TT * T2 * 2;  // the K / V ring only
+constexpr size_t kLongDkdvSLds = 4 * TT * T2 * 2 + 4 * TT * 4;  // Q / dO ring + LSE / D
 constexpr size_t kLongDqLds = 4 * TT * T2 * 2 + 4 * TT * TI * 2 + 4 * 64 * 4;
 constexpr size_t kLongDkdvLds = 4 * TT * T2 * 2 + 4 * TT * 4 + 4 * 2 * TT * TI * 2;
 static_assert(kLongDkdvLds <= 80 * 1024 && kLongFwdLds <= 80 * 1024 && kLongDqLds <= 80 * 1024,
@@ -1098,11 +1347,38 @@ void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongDkdvLds));
       lattr = true;
     }
+    static const bool dq_t = [] {  // COMMEFF_ATTN_DQ_T=0: the dS-image dQ kernel
+      const char* e = getenv("COMMEFF_ATTN_DQ_T");
+      return !(e != nullptr && e[0] == '0');
+    }();
+    static bool tattr = false;
+    if (!tattr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dq_t_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongFwdTLds));
+      tattr = true;
+    }
     a.thresh = attn_thresh(p_drop);
     a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     const dim3 grid(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB)));
-    hipLaunchKernelGGL(attn_long_dq_kernel, grid, dim3(256), kLongDqLds, stream, a);
-    hipLaunchKernelGGL(attn_long_dkdv_kernel, grid, dim3(256), kLongDkdvLds, stream, a);
+    if (dq_t)
+      hipLaunchKernelGGL(attn_long_dq_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
+    else
+      hipLaunchKernelGGL(attn_long_dq_kernel, grid, dim3(256), kLongDqLds, stream, a);
+    static const bool dkdv_s = [] {  // COMMEFF_ATTN_DKDV_S=0: the P / dS-image dK dV kernel
+      const char* e = getenv("COMMEFF_ATTN_DKDV_S");
+      return !(e != nullptr && e[0] == '0');
+    }();
+    if (dkdv_s) {
+      static bool sattr = false;
+      if (!sattr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dkdv_s_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongDkdvSLds));
+        sattr = true;
+      }
+      hipLaunchKernelGGL(attn_long_dkdv_s_kernel, grid, dim3(256), kLongDkdvSLds, stream, a);
+    } else {
+      hipLaunchKernelGGL(attn_long_dkdv_kernel, grid, dim3(256), kLongDkdvLds, stream, a);
+    }
     return;
   }
   static bool attr = false;
