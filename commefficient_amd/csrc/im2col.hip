@@ -22,6 +22,8 @@
 //   * wgrad_rsc_add_kernel folds the split-K partial products of the weight
 //     gradient (fixed order), permutes (r, s, c) -> (c, r, s) and adds into
 //     the flat fp32 gradient (or the per-group rows of ops/grouped.py);
+//     wgrad_split_add4_kernel is its 1x1 case (no permutation: float4 moves,
+//     8 split loads in flight), also used by the 1x1 GEMM convs' split-K;
 //   * maxpool_fwd_kernel / maxpool_bwd_kernel: k x k max-pool with stride s and
 //     padding p, 1-byte window codes, and a gather backward (each input pixel
 //     collects the outputs whose code points at it).
@@ -213,6 +215,47 @@ __global__ void __launch_bounds__(256) wgrad_rsc_add_kernel(float* __restrict__ 
   }
 }
 
+// RS == 1 (1x1 convs): dst[g][k][c..c+3] (+)= sum_u src[g*splits + u][k][c..c+3],
+// float4 per thread, 8 split loads in flight, summed in split order
+__global__ void __launch_bounds__(256) wgrad_split_add4_kernel(float* __restrict__ dst, int64_t dst_ld,
+                                                              const float* __restrict__ src, int G,
+                                                              int splits, int KC, int accumulate) {
+  const int per4 = KC / 4;
+  const int64_t total = static_cast<int64_t>(G) * per4;
+  const int64_t plane = KC;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int g = static_cast<int>(i / per4);
+    const int e = static_cast<int>(i - static_cast<int64_t>(g) * per4) * 4;
+    const float* s0 = src + static_cast<int64_t>(g) * splits * plane + e;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int kU = 8;
+    for (int u0 = 0; u0 < splits; u0 += kU) {
+      float4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        v[u] = u0 + u < splits ? *reinterpret_cast<const float4*>(s0 + (u0 + u) * plane)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        acc.x += v[u].x;
+        acc.y += v[u].y;
+        acc.z += v[u].z;
+        acc.w += v[u].w;
+      }
+    }
+    float4* d = reinterpret_cast<float4*>(dst + g * dst_ld + e);
+    if (accumulate) {
+      const float4 o = *d;
+      acc.x += o.x;
+      acc.y += o.y;
+      acc.z += o.z;
+      acc.w += o.w;
+    }
+    *d = acc;
+  }
+}
+
 // ---------------------------------------------------------------- max-pool
 struct MaxPoolGeom {
   int H, W, C, OH, OW, k, s, p;
@@ -360,6 +403,13 @@ void launch_wgrad_rsc_add(float* dst, int64_t dst_ld, const float* src, int G, i
                           int RS, int Kc, bool accumulate, hipStream_t stream) {
   const int64_t total = static_cast<int64_t>(G) * K * C * RS;
   if (total == 0) return;
+  const bool al16 = reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                    (G == 1 || dst_ld % 4 == 0);
+  if (RS == 1 && Kc == C && (K * C) % 4 == 0 && al16) {
+    hipLaunchKernelGGL(wgrad_split_add4_kernel, dim3(blocks_for(total / 4)), dim3(256), 0, stream, dst, dst_ld,
+                       src, G, splits, K * C, accumulate ? 1 : 0);
+    return;
+  }
   hipLaunchKernelGGL(wgrad_rsc_add_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, dst, dst_ld, src,
                      G, splits, K, C, RS, Kc, accumulate ? 1 : 0);
 }

@@ -738,6 +738,11 @@ def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> 
         return torch.mm(g2d.t(), x2d, out_dtype=torch.float32)
     part = torch.bmm(g2d.view(G * S, Pg // S, K).transpose(1, 2), x2d.view(G * S, Pg // S, C),
                      out_dtype=torch.float32)
+    if into is not None and part.is_cuda and into.stride(-1) == 1 and into.stride(-2) == C:
+        # one native pass: the splits summed in order and added into the flat
+        # (or per-group) gradient (csrc/im2col.hip; was a reduce + an add kernel)
+        _ops().wgrad_rsc_add(into.view(G, K, C), part, S, C, 1, True)
+        return into
     if S > 1:
         part = part.view(G, S, K, C).sum(1)
     part = part.view(G, K, C) if G > 1 else part.view(K, C)
@@ -819,8 +824,12 @@ class _Conv1x1Pass(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             if gid is not None:
+                # the identity gradient is this node's own input (the residual
+                # BN backward's fresh dadd): accumulate into it in place (an
+                # out-of-place addmm first copies it: ~36 us per block of a
+                # ResNet-101 round)
                 gi = _nhwc2d(gid.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
-                gx2d = torch.addmm(gi, g2d, wb)
+                gx2d = torch.addmm(gi, g2d, wb, out=gi)
             else:
                 gx2d = torch.mm(g2d, wb)
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
