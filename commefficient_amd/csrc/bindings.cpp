@@ -1087,8 +1087,10 @@ at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at:
 }
 
 // ghost batch norm: x [N, C, H, W] bf16 channels_last, G | N groups.
-// returns (y, stat [G, 2, C] = mean, rstd); running stats updated in place
-std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c10::optional<at::Tensor>& w,
+// returns (y, stat [G, 2, C] = mean, rstd, relu_bits [N*H*W*C/8] uint8: bit
+// c % 8 of byte (pixel*C + c) / 8 set where y > 0 -- empty without relu);
+// running stats updated in place
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c10::optional<at::Tensor>& w,
                                                     const c10::optional<at::Tensor>& b, int64_t G, double eps,
                                                     double momentum, const c10::optional<at::Tensor>& run_mean,
                                                     const c10::optional<at::Tensor>& run_var, bool relu,
@@ -1127,12 +1129,13 @@ std::tuple<at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor& x, const c
   auto stat = at::empty({G, 2, C}, fo);
   auto ab = at::empty({G, 2, C}, fo);
   auto y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto bits = at::empty({relu ? x.numel() / 8 : 0}, x.options().dtype(at::kByte));
   launch_bn_fwd(bf16_ptr(x), wp, bp, static_cast<int>(G), static_cast<int>(M), static_cast<int>(C),
                 static_cast<float>(eps), static_cast<float>(momentum), rm, rv, part.data_ptr<float>(),
                 stat.data_ptr<float>(), ab.data_ptr<float>(), relu, nb,
                 reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream(),
-                has_add ? bf16_ptr(*addend) : nullptr);
-  return {y, stat};
+                has_add ? bf16_ptr(*addend) : nullptr, relu ? bits.data_ptr<uint8_t>() : nullptr);
+  return {y, stat, bits};
 }
 
 // returns (dx, dweight, dbias) (dweight / dbias undefined without affine, or
@@ -1150,9 +1153,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
   check_nhwc_bf16(dy, "ghost_bn_bwd: dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "ghost_bn_bwd: dy shape");
   const bool fused_relu = y_relu.has_value() && y_relu->defined();
-  if (fused_relu) {
-    check_nhwc_bf16(*y_relu, "ghost_bn_bwd: y");
-    TORCH_CHECK(y_relu->sizes() == x.sizes(), "ghost_bn_bwd: y shape");
+  if (fused_relu) {  // the forward's 1-bit ReLU mask
+    TORCH_CHECK(y_relu->is_cuda() && y_relu->scalar_type() == at::kByte && y_relu->is_contiguous() &&
+                    y_relu->numel() == x.numel() / 8,
+                "ghost_bn_bwd: y_relu must be the forward's uint8 [numel / 8] ReLU bits");
   }
   if (dadd.has_value() && dadd->defined()) {  // receives the ReLU-masked dy
     check_nhwc_bf16(*dadd, "ghost_bn_bwd: dadd");
@@ -1193,7 +1197,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_bwd_hip(const at::Tensor
   float* dwp = into ? gw->data_ptr<float>() : (affine && !grouped ? dw.data_ptr<float>() : nullptr);
   float* dbp = into ? gb->data_ptr<float>() : (affine && !grouped ? db.data_ptr<float>() : nullptr);
   auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  launch_bn_bwd(bf16_ptr(x), bf16_ptr(dy), fused_relu ? bf16_ptr(*y_relu) : nullptr, stat.data_ptr<float>(),
+  launch_bn_bwd(bf16_ptr(x), bf16_ptr(dy), fused_relu ? y_relu->data_ptr<uint8_t>() : nullptr, stat.data_ptr<float>(),
                 affine ? w->data_ptr<float>() : nullptr, static_cast<int>(G), static_cast<int>(M),
                 static_cast<int>(C), part.data_ptr<float>(), coef.data_ptr<float>(), dwp, dbp,
                 into ? 1.f : 0.f, reinterpret_cast<uint16_t*>(dx.data_ptr()), cur_stream(),
@@ -1858,7 +1862,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
         "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None, Tensor? addend=None) "
-        "-> (Tensor, Tensor)");
+        "-> (Tensor, Tensor, Tensor)");
   m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None, "
         "Tensor(a!)? gw=None, Tensor(b!)? gb=None, Tensor(c!)? ggw=None, Tensor(d!)? ggb=None, "
         "Tensor(e!)? dadd=None) -> (Tensor, Tensor, Tensor)");

@@ -43,16 +43,26 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, t);
 }
 
-// keep the bf16 lanes of d where the bf16 lanes of y are > 0
-__device__ __forceinline__ u4 relu_mask8(u4 d, const u4 y) {
+// keep the bf16 lanes of d whose bit in the 1-bit ReLU mask m is set
+__device__ __forceinline__ u4 relu_bits8(u4 d, uint32_t m) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t lo = y[q] & 0xffffu, hi = y[q] >> 16;
-    const uint32_t keep = ((lo & 0x8000u) == 0u && lo != 0u ? 0x0000ffffu : 0u) |
-                          ((hi & 0x8000u) == 0u && hi != 0u ? 0xffff0000u : 0u);
+    const uint32_t keep = (((m >> (2 * q)) & 1u) ? 0x0000ffffu : 0u) | (((m >> (2 * q + 1)) & 1u) ? 0xffff0000u : 0u);
     d[q] &= keep;
   }
   return d;
+}
+
+// bit j set: bf16 lane j of the packed y is > 0 (what relu_mask8 keeps)
+__device__ __forceinline__ uint32_t pos_bits8(const u4 y) {
+  uint32_t m = 0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t lo = y[q] & 0xffffu, hi = y[q] >> 16;
+    m |= ((lo & 0x8000u) == 0u && lo != 0u ? 1u : 0u) << (2 * q);
+    m |= ((hi & 0x8000u) == 0u && hi != 0u ? 1u : 0u) << (2 * q + 1);
+  }
+  return m;
 }
 
 // thread layout of the partial-sum kernels: CL = C/8 chunk lanes (16 bytes =
@@ -61,7 +71,7 @@ __device__ __forceinline__ u4 relu_mask8(u4 d, const u4 y) {
 template <bool BWD>
 __global__ void __launch_bounds__(256)
 bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                  const uint16_t* __restrict__ ymask, const float* __restrict__ stat, int C, int M,
+                  const uint8_t* __restrict__ ybits, const float* __restrict__ stat, int C, int M,
                   int S, float* __restrict__ part) {
   // part[(g*S + s)*2*C + {0: sum, C: sum2}][c]
   __shared__ float red[2][256][8];
@@ -118,9 +128,9 @@ bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
       const u4 x1 = two ? *reinterpret_cast<const u4*>(x + o1) : x0;
       u4 d0 = *reinterpret_cast<const u4*>(dy + o0), d1 = {0u, 0u, 0u, 0u};
       if (two) d1 = *reinterpret_cast<const u4*>(dy + o1);
-      if (ymask != nullptr) {  // fused ReLU: dy where y > 0
-        d0 = relu_mask8(d0, *reinterpret_cast<const u4*>(ymask + o0));
-        if (two) d1 = relu_mask8(d1, *reinterpret_cast<const u4*>(ymask + o1));
+      if (ybits != nullptr) {  // fused ReLU: dy where y > 0 (1 bit per element)
+        d0 = relu_bits8(d0, ybits[o0 >> 3]);
+        if (two) d1 = relu_bits8(d1, ybits[o1 >> 3]);
       }
       float f0[8], f1[8], e0[8], e1[8];
       unpack8(x0, f0);
@@ -450,9 +460,9 @@ __device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
 template <bool BWD>
 __global__ void __launch_bounds__(256)
 bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                const uint16_t* __restrict__ ymask, const float* __restrict__ coef, int C, int M,
+                const uint8_t* __restrict__ ybits, const float* __restrict__ coef, int C, int M,
                 uint32_t nchunks, bool relu, uint16_t* __restrict__ out,
-                uint16_t* __restrict__ aux) {
+                uint16_t* __restrict__ aux, uint8_t* __restrict__ bits_out) {
   const uint32_t CL = static_cast<uint32_t>(C) >> 3;
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nchunks; i += gridDim.x * 256u) {
     const uint32_t p = i / CL;
@@ -479,7 +489,7 @@ bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
     } else {
       float d[8], R[8];
       u4 dv = *reinterpret_cast<const u4*>(dy + static_cast<size_t>(i) * 8);
-      if (ymask != nullptr) dv = relu_mask8(dv, *reinterpret_cast<const u4*>(ymask + static_cast<size_t>(i) * 8));
+      if (ybits != nullptr) dv = relu_bits8(dv, ybits[i]);
       if (aux != nullptr) *reinterpret_cast<u4*>(aux + static_cast<size_t>(i) * 8) = dv;
       unpack8(dv, d);
       load8f(k + 2 * C, R);
@@ -488,6 +498,7 @@ bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
     }
     const u4 v = {pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
     *reinterpret_cast<u4*>(out + static_cast<size_t>(i) * 8) = v;
+    if (!BWD && bits_out != nullptr) bits_out[i] = static_cast<uint8_t>(pos_bits8(v));
   }
 }
 
@@ -516,7 +527,7 @@ int bn_slabs(int G, int M) {
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C,
                    float eps, float momentum, float* run_mean, float* run_var, float* part,
                    float* stat, float* ab, bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream,
-                   const uint16_t* addend) {
+                   const uint16_t* addend, uint8_t* relu_bits) {
   const int S = bn_slabs(G, M);
   hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
                      nullptr, C, M, S, part);
@@ -534,10 +545,10 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                      nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
-                     const_cast<uint16_t*>(addend));
+                     const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr);
 }
 
-void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
+void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw, float* gdb,
                    int64_t gstride, uint16_t* dadd) {
@@ -559,7 +570,7 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu
   }
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
-                     coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd);
+                     coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd, nullptr);
 }
 
 }  // namespace commeff

@@ -287,8 +287,9 @@ int64_t bn_scratch_floats(int G, int M, int C);
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C, float eps,
                    float momentum, float* run_mean, float* run_var, float* part, float* stat, float* ab,
                    bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream,
-                   const uint16_t* addend = nullptr);
-void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint16_t* y_relu, const float* stat,
+                   const uint16_t* addend = nullptr, uint8_t* relu_bits = nullptr);
+// y_relu: the forward's 1-bit ReLU mask (one byte per 8 channels of a pixel)
+void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw = nullptr,
                    float* gdb = nullptr, int64_t gstride = 0, uint16_t* dadd = nullptr);

@@ -571,9 +571,10 @@ class _GhostBN(torch.autograd.Function):
                 gg=None, addend=None):
         if addend is not None:  # y = relu(bn(x) + addend): a residual block's tail
             addend = addend.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        y, stat = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
-                                      running_mean, running_var, bool(relu), nbt, addend)
-        ctx.save_for_backward(x, stat, weight, y if relu else None)
+        y, stat, bits = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
+                                            running_mean, running_var, bool(relu), nbt, addend)
+        # the backward's ReLU gate: 1 bit per element (y itself is 16)
+        ctx.save_for_backward(x, stat, weight, bits if relu else None)
         ctx.groups = int(groups)
         ctx.params = (weight, bias)
         ctx.gg = gg
