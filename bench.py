@@ -41,7 +41,8 @@ def main():
     p.add_argument("--clients-per-gpu", type=int, default=100)
     p.add_argument("--client-size", type=int, default=5)
     p.add_argument("--num-clients", type=int, default=10000)
-    p.add_argument("--encode", default="planned", choices=["planned", "binned", "direct"])
+    p.add_argument("--encode", default="region", choices=["region", "planned", "binned", "direct"],
+                   help="sketch hash family / kernels (utils/args.py --encode)")
     p.add_argument("--conv", default="native", choices=["native", "miopen"],
                    help="3x3 conv units on the native MFMA kernels or on MIOpen")
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")

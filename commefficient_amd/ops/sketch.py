@@ -52,6 +52,11 @@ def make_hashes(r: int, c: int, num_blocks: int = 1, seed: int = 42):
 
 
 
+def _rg():
+    from . import sketch_region
+    return sketch_region
+
+
 def _topk_hint(tag, device):
     from . import topk_hint
     return topk_hint(tag, device)
@@ -70,7 +75,9 @@ class CSVec:
         self.seed = seed
         # GPU encode/query kernels: "planned" (precomputed permutation, atomic
         # free, deterministic), "binned" (LDS atomics) or "direct" (global
-        # atomics / random gathers)
+        # atomics / random gathers) on the multiply-shift family below, or
+        # "region": the region-permutation family of ops/sketch_region.py
+        # (its own hashes; CPU and GPU)
         self.kernel = kernel
         if _hashes is None:
             h, bo, bs = make_hashes(self.r, self.c, self.numBlocks, seed)
@@ -85,6 +92,12 @@ class CSVec:
         # mapping is data-independent) and shared by every sketch derived
         # with like()
         self._scratch = _scratch if _scratch is not None else {}
+        self.region = None
+        if kernel == "region":
+            if "region" not in self._scratch:
+                from .sketch_region import RegionHash
+                self._scratch["region"] = RegionHash(self.d, self.c, self.r, seed)
+            self.region = self._scratch["region"]
 
     # -- construction helpers -------------------------------------------------
     def like(self, table: Optional[torch.Tensor] = None) -> "CSVec":
@@ -130,6 +143,9 @@ class CSVec:
         no separate zeroing pass on the planned path).  ``dense=False`` uses
         the direct-atomic kernel (best for sparse vectors)."""
         assert vec.numel() == self.d, (vec.numel(), self.d)
+        if self.region is not None:
+            _rg().encode(self.region, self.table, vec, scale, wvec, wscale, overwrite)
+            return
         if dense and self._use_plan():
             ops().cs_encode_planned(self.table, vec.reshape(-1), float(scale), wvec,
                                     float(wscale), self.c, self._plan(), bool(overwrite))
@@ -145,6 +161,8 @@ class CSVec:
 
     def query(self) -> torch.Tensor:
         """Median-of-rows estimate of every coordinate (dense, length d)."""
+        if self.region is not None:
+            return _rg().query(self.region, self.table)
         if self._use_plan():
             return ops().cs_query_planned(self.table, self.d, self._plan())
         if self.device.type == "cuda" and self.kernel != "direct":
@@ -164,6 +182,9 @@ class CSVec:
         """Coordinate shard boundaries [b_0 = 0, ..., b_world = d] at plan-chunk
         granularity (shard q = chunks [nch*q//world, nch*(q+1)//world)), or
         None when the query is not planned (no chunk structure)."""
+        if self.region is not None:
+            m = self.region.m
+            return [min(self.d, q * m) for q in self.region.chunk_bounds(world)]
         if not self._use_plan():
             return None
         geom = ops().plan_geometry(self.d, self.r, self.c)
@@ -192,10 +213,14 @@ class CSVec:
         """This rank's candidates: [2, k] int64 = (global indices, fp32 bits of
         the estimates) of its shard's top-k."""
         b = bounds if bounds is not None else self.shard_bounds(world)
-        nch = int(ops().plan_geometry(self.d, self.r, self.c)[3])
         lo, hi = b[rank], b[rank + 1]
-        est = ops().cs_query_planned(self.table, self.d, self._plan(), nch * rank // world,
-                                     nch * (rank + 1) // world)
+        if self.region is not None:
+            qb = self.region.chunk_bounds(world)
+            est = _rg().query(self.region, self.table, qb[rank], qb[rank + 1])
+        else:
+            nch = int(ops().plan_geometry(self.d, self.r, self.c)[3])
+            est = ops().cs_query_planned(self.table, self.d, self._plan(), nch * rank // world,
+                                         nch * (rank + 1) // world)
         li, lv = ops().topk_abs(est[lo:hi], k, _topk_hint(("unsketch_shard", self.d, k, rank, world),
                                                          est.device))
         pack = torch.empty(2, k, dtype=torch.int64, device=self.device)
@@ -221,6 +246,9 @@ class CSVec:
         """Zero cells (j, h_j(i)) of this table (and ``other``) for recovered
         coordinates i with nonzero value -- the reference's
         ``nz = S(delta).nonzero(); table[nz] = 0``."""
+        if self.region is not None:
+            _rg().zero_buckets(self.region, self.table, other, idx, vals)
+            return
         ops().cs_zero_buckets(self.table, other, idx, vals, self.hashes, self.blk_off,
                               self.blk_sign, self.numBlocks, self.d)
 

@@ -173,10 +173,12 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
     g.add_argument("--inject_nonfinite_round", type=int, default=-1,
                    help="fault injection: corrupt the aggregated upload of this round with a NaN")
     g.add_argument("--sketch_seed", type=int, default=42, help="Count-Sketch hash seed")
-    g.add_argument("--encode", choices=["planned", "binned", "direct"], default="planned",
-                   help="GPU Count-Sketch encode/query kernels: planned (precomputed "
-                        "permutation, atomic free), binned (LDS atomics) or direct "
-                        "(global atomics)")
+    g.add_argument("--encode", choices=["region", "planned", "binned", "direct"], default="region",
+                   help="Count-Sketch hash family + GPU kernels: region (region-permutation "
+                        "family, ops/sketch_region.py: LDS-local encode and query, no plan) or "
+                        "the csvec-layout multiply-shift family (numBlocks) with planned "
+                        "(precomputed permutation, atomic free), binned (LDS atomics) or "
+                        "direct (global atomics) kernels")
     g.add_argument("--client_state_device", choices=["auto", "gpu", "cpu"], default="auto",
                    help="where per-client momentum/error/weights live")
     g.add_argument("--resume", type=str, default=None,

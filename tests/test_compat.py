@@ -62,7 +62,7 @@ def test_get_server_update_matches_engine(mode, extra):
     args.grad_size = d
     lr = 1.0 if mode == "fedavg" else 0.3
     sk = CSVec(d, args.num_cols, args.num_rows, "cpu", args.num_blocks,
-               seed=args.sketch_seed) if mode == "sketch" else None
+               seed=args.sketch_seed, kernel=args.encode) if mode == "sketch" else None
     eng = ServerState(args, d, "cpu", sk)
     shape = eng.V.shape
     V, E = torch.zeros(shape), torch.zeros(shape)

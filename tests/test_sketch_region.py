@@ -1,0 +1,177 @@
+"""Region-permutation Count Sketch (ops/sketch_region.py, csrc/sketch_region.hip).
+
+CPU: the family's structure (bijective inside a chunk, ~1/c pairwise collision
+rate per row, one coordinate of each chunk per bucket of its region), CSVec
+API semantics on the CPU implementation, and heavy-hitter recovery no worse
+than the multiply-shift csvec family.  GPU: the HIP encode / query / zeroing
+against the CPU implementation (query and zeroing bitwise, encode to fp32
+summation order), bitwise run-to-run determinism, chunk-range (sharded)
+queries, and the sharded unsketch equal to the replicated one."""
+import numpy as np
+import pytest
+import torch
+
+from commefficient_amd.ops import CSVec
+from commefficient_amd.ops import sketch_region
+from commefficient_amd.ops.sketch_region import RegionHash, collision_rate, region_size
+
+GEOMS = [(1000, 100, 5), (20000, 3000, 5), (50001, 5000, 3), (7, 10, 1), (123457, 20000, 4)]
+
+
+@pytest.mark.parametrize("d,c,r", GEOMS)
+def test_region_structure(d, c, r):
+    h = RegionHash(d, c, r, seed=3)
+    b, s = h.dense()
+    assert b.shape == (r, d) and int(b.min()) >= 0 and int(b.max()) < h.R * h.m <= c
+    assert set(np.unique(s.numpy())) <= {-1.0, 1.0}
+    for q in range(h.nch):
+        lo, hi = q * h.m, min(d, (q + 1) * h.m)
+        for j in range(r):
+            bq = b[j, lo:hi]
+            assert bq.unique().numel() == hi - lo  # bijective inside a chunk
+            assert int(bq.min()) // h.m == int(bq.max()) // h.m == int(h.region[j, q])
+    # regions get the chunks dealt evenly
+    for j in range(r):
+        cnt = np.bincount(h.region[j], minlength=h.R)
+        assert cnt.max() - cnt.min() <= 1
+
+
+def test_region_size_choices():
+    assert region_size(500000, 5) == 500000 // 245
+    assert region_size(100, 5) == 100
+    m = region_size(10 ** 6, 16)
+    assert 16 * m * 4 <= 160 * 1024
+
+
+def test_collision_rate_is_uniform_like():
+    d, c, r = 200000, 20000, 5
+    h = RegionHash(d, c, r, seed=1)
+    rate = collision_rate(h, pairs=400000)
+    assert abs(rate - 1.0 / c) < 0.3 / c, (rate, 1.0 / c)
+
+
+def test_csvec_region_linearity_and_exact_recovery():
+    d, c, r = 30000, 4000, 5
+    torch.manual_seed(0)
+    a, b = torch.randn(d), torch.randn(d)
+    s1 = CSVec(d, c, r, kernel="region")
+    s2 = s1.like()
+    s12 = s1.like()
+    s1.accumulateVec(a)
+    s2.accumulateVec(b)
+    s12.accumulateVec(a, 1.0, b, 1.0)
+    torch.testing.assert_close(s12.table, s1.table + s2.table, rtol=1e-5, atol=1e-5)
+    # a sparse vector is recovered exactly unless two of its entries collide in
+    # >= 3 of 5 rows (they cannot inside one chunk)
+    v = torch.zeros(d)
+    hot = torch.tensor([5, 17, 999, 2047, 2048, 29999])
+    v[hot] = torch.tensor([3.0, -2.0, 1.5, 7.0, -4.0, 0.5])
+    sk = CSVec(d, c, r, kernel="region")
+    sk.accumulateVec(v)
+    est = sk.query()
+    torch.testing.assert_close(est[hot], v[hot])
+    idx, vals = sk.unsketch_sparse(4)
+    assert sorted(idx.tolist()) == [5, 17, 2047, 2048]
+
+
+def test_csvec_region_overwrite_and_zero():
+    d, c, r = 9000, 1000, 3
+    sk = CSVec(d, c, r, kernel="region")
+    sk.table.fill_(123.0)
+    v = torch.randn(d)
+    sk.accumulateVec(v, overwrite=True)
+    ref = CSVec(d, c, r, kernel="region")
+    ref.accumulateVec(v)
+    assert torch.equal(sk.table, ref.table)
+    other = ref.table.clone() + 1.0
+    idx = torch.tensor([0, 4000, 8999])
+    vals = torch.tensor([1.0, 0.0, -2.0])
+    ref.zero_heavy_hitters(idx, vals, other)
+    b = ref.region.buckets_of(idx)
+    for j in range(r):
+        for t in (0, 2):  # the nonzero entries' cells, in both tables
+            assert ref.table[j, b[j, t]] == 0 and other[j, b[j, t]] == 0
+
+
+def test_heavy_hitter_recall_matches_csvec_family():
+    # heavy-tailed vector: top-k recall of the region family within a few
+    # points of the multiply-shift (csvec layout) family at the same geometry
+    d, c, r, k = 200000, 20000, 5, 1000
+    g = torch.Generator().manual_seed(7)
+    v = torch.randn(d, generator=g) * 0.01
+    hot = torch.randperm(d, generator=g)[:k]
+    v[hot] += torch.randn(k, generator=g).sign() * (0.5 + torch.rand(k, generator=g))
+    true = set(torch.topk(v.abs(), k).indices.tolist())
+    recall = {}
+    for kern in ("region", "planned"):
+        sk = CSVec(d, c, r, kernel=kern, numBlocks=20)
+        sk.accumulateVec(v)
+        idx, _ = sk.unsketch_sparse(k)
+        recall[kern] = len(true & set(idx.tolist())) / k
+    assert recall["region"] >= recall["planned"] - 0.02, recall
+    assert recall["region"] > 0.95, recall
+
+
+# ------------------------------------------------------------------ GPU
+GPU_GEOMS = [(1000, 100, 5), (6568640, 500000, 5), (50001, 5000, 3), (123457, 20000, 4),
+             (2000003, 500000, 5)]
+
+
+def _pair(d, c, r, seed=11):
+    cpu = CSVec(d, c, r, kernel="region", seed=seed)
+    gpu = CSVec(d, c, r, device="cuda", kernel="region", seed=seed)
+    return cpu, gpu
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,c,r", GPU_GEOMS)
+def test_region_gpu_encode_query_zero_match_cpu(d, c, r):
+    torch.manual_seed(d % 1000)
+    v = torch.randn(d)
+    w = torch.randn(d)
+    cpu, gpu = _pair(d, c, r)
+    cpu.accumulateVec(v, 0.5, w, 0.01)
+    gpu.table.fill_(7.0)  # overwrite ignores stale contents, incl. the unused tail
+    gpu.accumulateVec(v.cuda(), 0.5, w.cuda(), 0.01, overwrite=True)
+    torch.testing.assert_close(gpu.table.cpu(), cpu.table, rtol=1e-5, atol=1e-5)
+    gpu.accumulateVec(v.cuda())  # accumulate (+=)
+    cpu.accumulateVec(v)
+    torch.testing.assert_close(gpu.table.cpu(), cpu.table, rtol=1e-5, atol=1e-5)
+    # query / zeroing of one shared table: bitwise
+    gpu.table.copy_(cpu.table)
+    assert torch.equal(gpu.query().cpu(), cpu.query())
+    k = min(1000, d // 3)
+    idx = torch.randperm(d)[:k].sort().values
+    vals = torch.randn(k)
+    vals[::4] = 0
+    other_c = cpu.table.clone()
+    other_g = other_c.cuda()
+    cpu.zero_heavy_hitters(idx, vals, other_c)
+    gpu.zero_heavy_hitters(idx.cuda(), vals.cuda(), other_g)
+    assert torch.equal(gpu.table.cpu(), cpu.table)
+    assert torch.equal(other_g.cpu(), other_c)
+
+
+@pytest.mark.gpu
+def test_region_gpu_deterministic_and_sharded():
+    d, c, r = 6568640, 500000, 5
+    v = torch.randn(d, device="cuda")
+    w = torch.randn(d, device="cuda")
+    a = CSVec(d, c, r, device="cuda", kernel="region")
+    b = a.like()
+    a.accumulateVec(v, 0.3, w, 1e-3, overwrite=True)
+    b.accumulateVec(v, 0.3, w, 1e-3, overwrite=True)
+    assert torch.equal(a.table, b.table)
+    full = a.query()
+    k = 50000
+    ref_idx, ref_vals = a.unsketch_sparse(k)
+    for world in (2, 3, 8):
+        bounds = a.shard_bounds(world)
+        packs = [a.unsketch_shard(k, q, world, bounds) for q in range(world)]
+        for q in range(world):
+            lo, hi = bounds[q], bounds[q + 1]
+            qb = a.region.chunk_bounds(world)
+            est = sketch_region.query(a.region, a.table, qb[q], qb[q + 1])
+            assert torch.equal(est[lo:hi], full[lo:hi])
+        idx, vals = CSVec.merge_shards(torch.stack(packs).view(world, 2 * k), world, k)
+        assert torch.equal(idx, ref_idx) and torch.equal(vals, ref_vals)
