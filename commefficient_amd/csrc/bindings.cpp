@@ -342,75 +342,78 @@ void cs_zero_buckets_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2,
                          cur_stream());
 }
 
-// ---- region-permutation sketch (sketch_region.hip)
+// ---- region sketch (sketch_region.hip)
 struct RegionParams {
-  int64_t r, c, m, R, nch;
+  int64_t r, c, m, g, G, W, nch;
 };
 
-RegionParams check_region(const at::Tensor& table, int64_t d, int64_t m, const at::Tensor& perm,
-                          const at::Tensor& cinfo) {
+RegionParams check_region(const at::Tensor& table, int64_t d, int64_t m, int64_t g, int64_t W,
+                          const at::Tensor& perm, const at::Tensor& cinfo, const at::Tensor* lists,
+                          const at::Tensor* goffs) {
   check_f32(table, "table");
   RegionParams p;
   p.c = table.size(-1);
   p.r = table.numel() / p.c;
   p.m = m;
-  TORCH_CHECK(m >= 1 && p.r >= 1 && p.r <= kMaxRows, "region sketch: bad geometry");
-  p.R = p.c / m;
+  p.g = g;
+  p.W = W;
   p.nch = (d + m - 1) / m;
-  TORCH_CHECK(p.R >= 1 && d >= 1 && d < (int64_t(1) << 32), "region sketch: m > c or d out of range");
-  TORCH_CHECK(perm.scalar_type() == at::kInt && perm.is_contiguous() && perm.numel() == p.r * m &&
-                  perm.device() == table.device(), "region sketch: perm must be int32 [r, m] on the table's device");
-  TORCH_CHECK(cinfo.scalar_type() == at::kInt && cinfo.is_contiguous() && cinfo.numel() == p.r * p.nch * 2 &&
-                  cinfo.device() == table.device(), "region sketch: cinfo must be int32 [r, nch, 2]");
+  p.G = p.c / (g * m);
+  TORCH_CHECK(region_geometry_supported(p.r, m, g, W) && p.G >= 1 && d >= 1 && d < (int64_t(1) << 32) &&
+                  p.G * g < (int64_t(1) << 24),
+              "region sketch: unsupported geometry (r <= 16, m <= 64, W <= min(16, g), r*g*m floats in LDS)");
+  auto i32 = [&](const at::Tensor& t, int64_t n, const char* what) {
+    TORCH_CHECK(t.scalar_type() == at::kInt && t.is_contiguous() && t.numel() == n && t.device() == table.device(),
+                "region sketch: ", what, " must be int32 with ", n, " elements on the table's device");
+  };
+  i32(perm, p.r * m, "perm [r, m]");
+  i32(cinfo, p.r * p.nch, "cinfo [r, nch] / [nch, r]");
+  if (lists != nullptr) i32(*lists, p.nch, "lists [nch]");
+  if (goffs != nullptr) i32(*goffs, p.G + 1, "goffs [G + 1]");
   return p;
 }
 
 void cs_region_encode_hip(at::Tensor table, const at::Tensor& vec, double scale,
-                          const c10::optional<at::Tensor>& wvec, double wscale, int64_t m,
+                          const c10::optional<at::Tensor>& wvec, double wscale, int64_t m, int64_t g, int64_t W,
                           const at::Tensor& perm, const at::Tensor& cinfo, const at::Tensor& lists,
-                          const at::Tensor& offs, bool overwrite) {
+                          const at::Tensor& goffs, bool overwrite) {
   check_f32(vec, "vec");
   const int64_t d = vec.numel();
-  const RegionParams p = check_region(table, d, m, perm, cinfo);
+  const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
   if (wvec.has_value() && wvec->defined()) {
     check_f32(*wvec, "wvec");
     TORCH_CHECK(wvec->numel() == d && wvec->device() == vec.device(), "wvec must match vec");
   }
   TORCH_CHECK(vec.device() == table.device(), "region sketch: vec on another device");
-  TORCH_CHECK(lists.scalar_type() == at::kInt && lists.is_contiguous() && lists.numel() == p.r * p.nch &&
-                  offs.scalar_type() == at::kInt && offs.is_contiguous() && offs.numel() == p.r * (p.R + 1) &&
-                  lists.device() == table.device() && offs.device() == table.device(),
-              "region sketch: lists int32 [r, nch], offs int32 [r, R + 1]");
-  TORCH_CHECK(region_encode_waves(m) > 0, "region sketch: m too large for the LDS encode");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   launch_cs_region_encode(table.data_ptr<float>(), vec.data_ptr<float>(), fptr(wvec),
-                          static_cast<float>(scale), static_cast<float>(wscale), d,
-                          static_cast<int>(p.r), p.c, m, p.R, p.nch,
-                          reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
-                          cinfo.data_ptr<int32_t>(), lists.data_ptr<int32_t>(), offs.data_ptr<int32_t>(),
-                          overwrite, cur_stream());
+                          static_cast<float>(scale), static_cast<float>(wscale), d, static_cast<int>(p.r), p.c,
+                          m, g, p.G, W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+                          reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
+                          goffs.data_ptr<int32_t>(), overwrite, cur_stream());
 }
 
 // est [d]; with q0 < q1 only the coordinates of chunks [q0, q1) are computed
 // (a rank's shard of the unsketch; the rest of est is left unset)
-at::Tensor cs_region_query_hip(const at::Tensor& table, int64_t d, int64_t m, const at::Tensor& perm,
-                               const at::Tensor& cinfo, int64_t q0, int64_t q1) {
-  const RegionParams p = check_region(table, d, m, perm, cinfo);
+at::Tensor cs_region_query_hip(const at::Tensor& table, int64_t d, int64_t m, int64_t g, int64_t W,
+                               const at::Tensor& perm, const at::Tensor& cinfo, const at::Tensor& lists,
+                               const at::Tensor& goffs, int64_t q0, int64_t q1) {
+  const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
   if (q1 < 0) q1 = p.nch;
   TORCH_CHECK(q0 >= 0 && q0 <= q1 && q1 <= p.nch, "cs_region_query: chunk range out of bounds");
-  TORCH_CHECK(p.r * m * 4 <= 160 * 1024, "cs_region_query: r * m floats must fit in LDS");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   auto est = at::empty({d}, table.options());
-  launch_cs_region_query(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(p.r), p.c, m,
-                         p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
-                         cinfo.data_ptr<int32_t>(), q0, q1, cur_stream());
+  launch_cs_region_query(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(p.r), p.c, m, g, p.G,
+                         W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+                         reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
+                         goffs.data_ptr<int32_t>(), q0, q1, cur_stream());
   return est;
 }
 
 void cs_region_zero_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2, const at::Tensor& idx,
-                        const c10::optional<at::Tensor>& vals, int64_t d, int64_t m, const at::Tensor& perm,
-                        const at::Tensor& cinfo) {
-  const RegionParams p = check_region(t1, d, m, perm, cinfo);
+                        const c10::optional<at::Tensor>& vals, int64_t d, int64_t m, int64_t g,
+                        const at::Tensor& perm, const at::Tensor& cinfo) {
+  const RegionParams p = check_region(t1, d, m, g, 1, perm, cinfo, nullptr, nullptr);
   TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous() && idx.device() == t1.device(),
               "cs_region_zero: idx must be int64 on the table's device");
   if (t2.has_value() && t2->defined())
@@ -420,10 +423,9 @@ void cs_region_zero_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2, cons
     TORCH_CHECK(vals->numel() == idx.numel() && vals->scalar_type() == at::kFloat && vals->is_contiguous(),
                 "cs_region_zero: vals must be f32 like idx");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(t1.device());
-  launch_cs_region_zero(t1.data_ptr<float>(), fptr(t2), idx.data_ptr<int64_t>(), fptr(vals), idx.numel(),
-                        d, static_cast<int>(p.r), p.c, m, p.nch,
-                        reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()), cinfo.data_ptr<int32_t>(),
-                        cur_stream());
+  launch_cs_region_zero(t1.data_ptr<float>(), fptr(t2), idx.data_ptr<int64_t>(), fptr(vals), idx.numel(), d,
+                        static_cast<int>(p.r), p.c, m, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+                        reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), cur_stream());
 }
 
 at::Tensor cs_l2estimate_hip(const at::Tensor& table) {
@@ -1970,10 +1972,11 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor blk_off, Tensor blk_sign, int num_blocks, int d) -> ()");
   m.def("cs_l2estimate(Tensor table) -> Tensor");
   m.def("cs_region_encode(Tensor(a!) table, Tensor vec, float scale, Tensor? wvec, float wscale, int m, "
-        "Tensor perm, Tensor cinfo, Tensor lists, Tensor offs, bool overwrite=False) -> ()");
-  m.def("cs_region_query(Tensor table, int d, int m, Tensor perm, Tensor cinfo, int q0=0, int q1=-1) -> Tensor");
-  m.def("cs_region_zero(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, int d, int m, Tensor perm, "
-        "Tensor cinfo) -> ()");
+        "int g, int W, Tensor perm, Tensor cinfo, Tensor lists, Tensor goffs, bool overwrite=False) -> ()");
+  m.def("cs_region_query(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
+        "Tensor goffs, int q0=0, int q1=-1) -> Tensor");
+  m.def("cs_region_zero(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, int d, int m, int g, "
+        "Tensor perm, Tensor cinfo) -> ()");
   m.def("topk_abs(Tensor x, int k, Tensor? hint=None) -> (Tensor, Tensor)");
   m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
   m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "

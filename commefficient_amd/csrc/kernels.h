@@ -97,23 +97,23 @@ void launch_cs_zero_buckets(float* t1, float* t2, const int64_t* idx,
                             const float* vals, int64_t k, const RowHashes& h,
                             const SketchGeom& g, const int32_t* blk_off,
                             const float* blk_sign, hipStream_t stream);
-// Region-permutation sketch (sketch_region.hip, ops/sketch_region.py):
-// perm [r, m] u32 = P_j(o) | S_j(o) << 31; cinfo [r, nch] (region base,
-// shift | sigma << 31); lists [r, nch] chunks ordered by (region, chunk),
-// offs [r, R + 1] region starts in lists.
-int region_encode_waves(int64_t m);  // 0: m too large for the LDS copies
+// Region sketch (sketch_region.hip, ops/sketch_region.py): perm [r, m] u32 =
+// P_j(o) | S_j(o) << 31; cinfo [r, nch] u32 = region | shift << 24 | sigma << 31;
+// lists [nch] chunks grouped (group-major, batches of W), goffs [G + 1].
+bool region_geometry_supported(int64_t r, int64_t m, int64_t g, int64_t W);
 void launch_cs_region_encode(float* table, const float* vec, const float* wvec, float scale,
-                             float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t R,
-                             int64_t nch, const uint32_t* perm, const int32_t* cinfo,
-                             const int32_t* lists, const int32_t* offs, bool overwrite,
+                             float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t g, int64_t G,
+                             int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
+                             const int32_t* lists, const int32_t* goffs, bool overwrite,
                              hipStream_t stream);
 // est[i] for the coordinates of chunks [q0, q1)
-void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m,
-                            int64_t nch, const uint32_t* perm, const int32_t* cinfo, int64_t q0,
-                            int64_t q1, hipStream_t stream);
+void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
+                            int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
+                            const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
+                            hipStream_t stream);
 void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float* vals, int64_t k,
                            int64_t d, int r, int64_t c, int64_t m, int64_t nch, const uint32_t* perm,
-                           const int32_t* cinfo, hipStream_t stream);
+                           const uint32_t* cinfo, hipStream_t stream);
 // out[0] = sqrt(lower-median_j sum_c table[j,c]^2); partial: >= r*256 floats
 void launch_cs_l2estimate(const float* table, int r, int64_t c, float* partial,
                           float* out, hipStream_t stream);

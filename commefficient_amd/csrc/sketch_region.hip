@@ -1,33 +1,36 @@
-// Region-permutation Count Sketch for gfx950: encode, median query and
-// heavy-hitter zeroing with no plan arrays, no atomics and no r*d
-// intermediate.  Bitwise deterministic.
+// Region Count Sketch for gfx950: encode, median query and heavy-hitter
+// zeroing with no atomics and no r*d intermediate; bitwise deterministic.
 //
 // Hash family (ops/sketch_region.py builds the parameters from the seed):
-// the d coordinates are cut into chunks of m consecutive coordinates and each
-// table row into R regions of m buckets (R = c // m; the <= R - 1 leftover
-// buckets of a row are never used).  In row j, chunk q goes to region
-// rho_j(q) (chunks dealt evenly over the regions in a random order) and its
-// coordinate o lands on bucket
-//     rho_j(q) * m + (P_j(o) + shift_j(q)) mod m,   sign S_j(o) ^ sigma_j(q)
-// with P_j a random permutation of [m].  Inside one chunk the map is a
-// bijection (chunk-mates never collide); two coordinates of different chunks
-// collide with probability (1/R) * (1/m) ~= 1/c per row, independently per
-// row -- the pairwise behaviour the Count-Sketch estimates rest on, with each
-// bucket receiving exactly one coordinate from each chunk of its region.
-// This replaces the reference CSVec's hashed numBlocks layout
+// the d coordinates are cut into chunks of m = 64 consecutive coordinates
+// (one wavefront) and each table row into regions of m buckets, g = 32
+// regions per GROUP (G = c // (g m) groups; leftover buckets unused).  Chunks
+// are dealt to groups (random balanced order); inside its group a chunk sits
+// in a batch of W = 32 chunks, and in row j the batch's chunks take W distinct
+// regions of the group (a random injection per (row, batch); W = 32 when
+// g >= 32: two chunks per wave per batch).  Coordinate o
+// of chunk q lands in row j on bucket
+//     region_j(q) * m + (P_j(o) + shift_j(q)) mod m,   sign S_j(o) ^ sigma_j(q)
+// with P_j a random permutation of [m].  Inside a chunk the map is a
+// bijection; two coordinates of one group collide in row j with probability
+// G/c, independently across rows, of different groups never: ~1/c per row,
+// like uniform hashing.  A chunk of large values (a "hot" layer) meets a
+// different random 1/g of its group in every row, so the median filters it.
+// Replaces the reference CSVec's hashed numBlocks layout
 // (/root/reference/CommEfficient/fed_aggregator.py:464-467 builds the CSVec,
-// fed_worker.py:313-320 encodes, fed_aggregator.py:584-595 unsketches): the
-// per-chunk structure turns the encode scatter and the query gather into
-// region-local LDS work.
+// fed_worker.py:313-320 encodes, fed_aggregator.py:584-595 unsketches).
 //
-// Encode (block per (region, row), W waves): each wave owns an LDS copy of
-// the region and adds its share of the region's chunks into it -- within a
-// chunk every lane writes a distinct bucket, and a wave's LDS accesses are
-// processed in order, so plain read-add-write needs no atomics or barriers;
-// the W copies are summed in a fixed order into the table.
-// Query (block per chunk): the chunk's r regions -> LDS (r * m floats, 16-byte
-// loads), then every coordinate gathers its r signed cells and stores the
-// lower median.
+// Encode (block per group, one wave per chunk of a batch): the group's r x g
+// regions accumulate in LDS (40 KB); every chunk is read once; a batch's
+// chunks own distinct regions in every row and a chunk's lanes distinct
+// buckets, so plain read-add-writes need no atomics; one barrier separates
+// batches (a fixed order: deterministic).  Several batches' values are in
+// flight at once.
+// Query (block per group): the group's r x g regions -> LDS once, then one wave
+// per chunk gathers each lane's r signed cells and stores the lower median.
+// cinfo word of (row, chunk): region (bits 0-23) | shift << 24 | sigma << 31;
+// the encode and query read them in list order ([list position][row]: one
+// contiguous 4r-byte run per chunk), the zeroing by chunk ([row][chunk]).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "kernels.h"
@@ -36,73 +39,126 @@ namespace commeff {
 namespace {
 
 constexpr uint32_t kSignBit = 0x80000000u;
+constexpr uint32_t kRegionMask = 0x00ffffffu;
 
-// (per-coordinate permutation word, chunk shift word) -> in-region bucket, negate?
-__device__ __forceinline__ uint32_t region_bucket(uint32_t pw, uint32_t shift, uint32_t m) {
-  uint32_t b = (pw & ~kSignBit) + (shift & ~kSignBit);
+__device__ __forceinline__ uint32_t ci_region(uint32_t w) { return w & kRegionMask; }
+__device__ __forceinline__ uint32_t ci_shift(uint32_t w) { return (w >> 24) & 0x3fu; }
+
+// in-region bucket of lane word pw (P_j(o) | S_j(o) << 31) under chunk word w
+__device__ __forceinline__ uint32_t in_region(uint32_t pw, uint32_t w, uint32_t m) {
+  uint32_t b = (pw & ~kSignBit) + ci_shift(w);
   return b >= m ? b - m : b;
 }
-__device__ __forceinline__ bool region_neg(uint32_t pw, uint32_t shift) {
-  return ((pw ^ shift) & kSignBit) != 0u;
-}
+__device__ __forceinline__ bool neg_of(uint32_t pw, uint32_t w) { return ((pw ^ w) & kSignBit) != 0u; }
 
-template <int W>
-__global__ void __launch_bounds__(W * 64)
+// RT rows (0: runtime r <= kMaxRows), SL = chunk slots per wave per pipelined
+// group, K slots per batch (batch = K * W chunks, W = blockDim / 64 waves:
+// one barrier per K chunks per wave), HW: a weight-decay operand
+template <int RT, int SL, int K, bool HW>
+__global__ void __launch_bounds__(1024)
 cs_region_encode_kernel(float* __restrict__ table, const float* __restrict__ vec,
                         const float* __restrict__ wvec, float scale, float wscale, uint32_t d,
-                        uint32_t c, uint32_t m, uint32_t R, uint32_t nch,
-                        const uint32_t* __restrict__ perm, const uint2* __restrict__ cinfo,
-                        const int32_t* __restrict__ lists, const int32_t* __restrict__ offs,
+                        uint32_t c, uint32_t m, uint32_t g, uint32_t G, uint32_t nch, uint32_t r_rt,
+                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
+                        const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
                         int overwrite) {
-  extern __shared__ __attribute__((aligned(16))) float acc[];  // [W][m]
-  const uint32_t rho = blockIdx.x, j = blockIdx.y;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (uint32_t e = tid; e < W * m; e += W * 64) acc[e] = 0.f;
+  constexpr int NR = RT > 0 ? RT : kMaxRows;
+  extern __shared__ __attribute__((aligned(16))) float acc[];  // [r][g * m]
+  const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
+  const uint32_t grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t W = blockDim.x >> 6, gm = g * m, rbase = grp * g;
+  for (uint32_t e = tid; e < r * gm; e += blockDim.x) acc[e] = 0.f;
+  uint32_t pw[NR];  // this lane's permutation words, the same in every chunk
+#pragma unroll
+  for (int j = 0; j < NR; ++j) pw[j] = (j < static_cast<int>(r) && lane < m) ? perm[j * m + lane] : 0u;
+  const int32_t l0 = goffs[grp], l1 = goffs[grp + 1];
+  const int32_t step = static_cast<int32_t>(SL * W);
+  // software pipeline over groups of SL / K batches: while group k is added into
+  // LDS, the values and chunk words of group k + 1 and the chunk ids of group
+  // k + 2 are in flight.  Every load is unconditional (indices clamped into
+  // range, validity applied at use): a load under a lane or list-end branch
+  // is waited for inside the branch.  The chunk words are VECTOR loads (lane
+  // j < r fetches row j's word, broadcast with readlane): a scalar load's
+  // wait would also wait for the LDS traffic.
+  uint32_t q1[SL], q2[SL], word[SL], wordn[SL];
+  float x[SL], xn[SL], y[SL], yn[SL];
+  const int32_t llast = l1 > l0 ? l1 - 1 : l0;
+  const uint32_t lr = lane < r ? lane : r - 1;
+  auto ids = [&](int32_t lb, uint32_t (&q)[SL]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < SL; ++u) q[u] = static_cast<uint32_t>(lists[min(lb + static_cast<int32_t>(u * W + w), llast)]);
+  };
+  auto values = [&](int32_t lb, const uint32_t (&q)[SL], float (&xx)[SL], float (&yy)[SL], uint32_t (&ww)[SL])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < SL; ++u) {
+      ww[u] = cinfo[static_cast<size_t>(min(lb + static_cast<int32_t>(u * W + w), llast)) * r + lr];
+      const size_t i = static_cast<size_t>(q[u]) * m + min(lane, d - q[u] * m - 1);
+      xx[u] = vec[i];
+      if constexpr (HW) yy[u] = wvec[i];
+    }
+  };
+  if (l1 > l0) {
+    ids(l0, q1);
+    values(l0, q1, x, y, word);
+    ids(l0 + step, q2);
+  }
   __syncthreads();
-  float* mine = acc + w * m;
-  const uint32_t* pj = perm + static_cast<size_t>(j) * m;
-  const int32_t* lj = lists + static_cast<size_t>(j) * nch;
-  const int32_t l0 = offs[j * (R + 1) + rho], l1 = offs[j * (R + 1) + rho + 1];
-  constexpr uint32_t U = 8;  // elements per lane in flight
-  for (int32_t li = l0 + static_cast<int32_t>(w); li < l1; li += W) {
-    const uint32_t q = static_cast<uint32_t>(lj[li]);
-    const uint32_t shift = cinfo[static_cast<size_t>(j) * nch + q].y;
-    const size_t i0 = static_cast<size_t>(q) * m;
-    const uint32_t len = min(m, d - static_cast<uint32_t>(i0));
-    for (uint32_t ob = lane; ob < len; ob += 64 * U) {
-      float v[U];
-      uint32_t pw[U];
+  for (int32_t lb = l0; lb < l1; lb += step) {
+    uint32_t qc[SL];
 #pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t o = ob + 64 * u;
-        v[u] = 0.f;
-        pw[u] = 0u;
-        if (o < len) {
-          v[u] = scale * vec[i0 + o];
-          if (wvec != nullptr) v[u] += wscale * wvec[i0 + o];
-          pw[u] = pj[o];
-        }
-      }
+    for (int u = 0; u < SL; ++u) qc[u] = q1[u];
+    // (unconditional even past the end -- clamped loads: a load under a
+    // branch is waited for where the branch joins)
+    values(lb + step, q2, xn, yn, wordn);
 #pragma unroll
-      for (uint32_t u = 0; u < U; ++u) {
-        if (ob + 64 * u < len) {
-          const uint32_t b = region_bucket(pw[u], shift, m);
-          mine[b] += region_neg(pw[u], shift) ? -v[u] : v[u];
-        }
+    for (int u = 0; u < SL; ++u) q1[u] = q2[u];
+    ids(lb + 2 * step, q2);
+#pragma unroll
+    for (int u = 0; u < SL; ++u) {
+      const bool live = lb + static_cast<int32_t>(u * W + w) < l1 && lane < min(m, d - qc[u] * m);
+      float v = scale * x[u];
+      if constexpr (HW) v += wscale * y[u];
+      uint32_t cw[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) cw[j] = j < static_cast<int>(r) ? __builtin_amdgcn_readlane(word[u], j) : 0u;
+      // the previous batch's read-add-writes are done (LDS only: the loads of
+      // the groups ahead stay in flight -- __syncthreads would drain them)
+      if (u % K == 0) {  // a new batch
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
       }
+      if (live) {
+        uint32_t b[NR];
+        float a[NR];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {  // distinct cells: every read before the writes
+          b[j] = 0u;
+          a[j] = 0.f;
+          if (j < static_cast<int>(r)) {
+            b[j] = j * gm + (ci_region(cw[j]) - rbase) * m + in_region(pw[j], cw[j], m);
+            a[j] = acc[b[j]];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          if (j < static_cast<int>(r)) acc[b[j]] = a[j] + (neg_of(pw[j], cw[j]) ? -v : v);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SL; ++u) {
+      x[u] = xn[u];
+      if constexpr (HW) y[u] = yn[u];
+      word[u] = wordn[u];
     }
   }
   __syncthreads();
-  float* trow = table + static_cast<size_t>(j) * c;
-  const uint32_t base = rho * m;
-  for (uint32_t e = tid; e < m; e += W * 64) {
-    float s = acc[e];
-#pragma unroll
-    for (int k = 1; k < W; ++k) s += acc[k * m + e];  // fixed order
-    trow[base + e] = overwrite ? s : trow[base + e] + s;
+  for (uint32_t j = 0; j < r; ++j) {
+    float* trow = table + static_cast<size_t>(j) * c + static_cast<size_t>(grp) * gm;
+    for (uint32_t e = tid; e < gm; e += blockDim.x) trow[e] = overwrite ? acc[j * gm + e] : trow[e] + acc[j * gm + e];
+    if (overwrite && grp == 0)  // the unused buckets past G*g*m stay zero
+      for (uint32_t e = G * gm + tid; e < c; e += blockDim.x) table[static_cast<size_t>(j) * c + e] = 0.f;
   }
-  if (overwrite && rho == 0)  // the unused buckets past R*m stay zero
-    for (uint32_t e = R * m + tid; e < c; e += W * 64) trow[e] = 0.f;
 }
 
 template <int RT>
@@ -131,49 +187,83 @@ __device__ __forceinline__ float lower_median(float (&v)[kMaxRows], int r) {
   return res;
 }
 
+// est for the chunks of group blockIdx.x inside [q0, q1); blockDim = 64 * W
 template <int RT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 cs_region_query_kernel(const float* __restrict__ table, float* __restrict__ est, uint32_t d,
-                       uint32_t c, uint32_t m, uint32_t nch, uint32_t r_rt,
-                       const uint32_t* __restrict__ perm, const uint2* __restrict__ cinfo,
-                       uint32_t q0, int vec4) {
-  extern __shared__ __attribute__((aligned(16))) float reg[];  // [r][m]
+                       uint32_t c, uint32_t m, uint32_t g, uint32_t nch, uint32_t r_rt,
+                       const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
+                       const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
+                       uint32_t q0, uint32_t q1, int vec4) {
+  constexpr int NR = RT > 0 ? RT : kMaxRows;
+  extern __shared__ __attribute__((aligned(16))) float reg[];  // [r][g * m]
   const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
-  const uint32_t q = q0 + blockIdx.x;
-  const uint32_t tid = threadIdx.x;
-  __shared__ uint32_t sh[kMaxRows];
-  if (tid < r) sh[tid] = cinfo[static_cast<size_t>(tid) * nch + q].y;
-  // stage the chunk's region of every row (coalesced; 16-byte when aligned)
+  const uint32_t grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t W = blockDim.x >> 6, gm = g * m, rbase = grp * g;
   for (uint32_t j = 0; j < r; ++j) {
-    const uint32_t base = cinfo[static_cast<size_t>(j) * nch + q].x;
-    const float* src = table + static_cast<size_t>(j) * c + base;
-    float* dst = reg + j * m;
+    const float* src = table + static_cast<size_t>(j) * c + static_cast<size_t>(grp) * gm;
+    float* dst = reg + j * gm;
     if (vec4) {
-      const float4* s4 = reinterpret_cast<const float4*>(src);
-      float4* d4 = reinterpret_cast<float4*>(dst);
-      for (uint32_t e = tid; e < (m >> 2); e += 256) d4[e] = s4[e];
+      for (uint32_t e = tid; e < (gm >> 2); e += blockDim.x)
+        reinterpret_cast<float4*>(dst)[e] = reinterpret_cast<const float4*>(src)[e];
     } else {
-      for (uint32_t e = tid; e < m; e += 256) dst[e] = src[e];
+      for (uint32_t e = tid; e < gm; e += blockDim.x) dst[e] = src[e];
     }
   }
+  uint32_t pw[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) pw[j] = (j < static_cast<int>(r) && lane < m) ? perm[j * m + lane] : 0u;
   __syncthreads();
-  const size_t i0 = static_cast<size_t>(q) * m;
-  const uint32_t len = min(m, d - static_cast<uint32_t>(i0));
   const int rr = static_cast<int>(r);
-  for (uint32_t o = tid; o < len; o += 256) {
-    float v[kMaxRows];
-    uint32_t pw[kMaxRows];
+  const int32_t l0 = goffs[grp], l1 = goffs[grp + 1];
+  // chunk ids and words of the next UQ chunks of this wave are in flight
+  // while the current UQ are gathered (VECTOR loads for the words: lane j < r
+  // fetches row j's word, readlane broadcasts -- a scalar load's wait would
+  // also wait for the LDS gathers)
+  constexpr int UQ = 8;
+  const int32_t step = static_cast<int32_t>(UQ * W);
+  uint32_t q[UQ], word[UQ], qn[UQ], wn[UQ];
+  // (unconditional loads at clamped positions: a load under a branch is
+  // waited for inside the branch)
+  const int32_t llast = l1 > l0 ? l1 - 1 : l0;
+  const uint32_t lr = lane < r ? lane : r - 1;
+  auto fetch = [&](int32_t lb, uint32_t (&qq)[UQ], uint32_t (&ww)[UQ]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < (RT > 0 ? RT : kMaxRows); ++j) pw[j] = j < rr ? perm[static_cast<size_t>(j) * m + o] : 0u;
+    for (int u = 0; u < UQ; ++u) {
+      const int32_t li = min(lb + static_cast<int32_t>(u * W + w), llast);
+      qq[u] = static_cast<uint32_t>(lists[li]);
+      ww[u] = cinfo[static_cast<size_t>(li) * r + lr];
+    }
+  };
+  if (l1 > l0) fetch(l0, q, word);
+  for (int32_t lb = l0; lb < l1; lb += step) {
+    fetch(lb + step, qn, wn);  // (unconditional, clamped: see the encode)
 #pragma unroll
-    for (int j = 0; j < (RT > 0 ? RT : kMaxRows); ++j) {
-      v[j] = 0.f;
-      if (j < rr) {
-        const float x = reg[j * m + region_bucket(pw[j], sh[j], m)];
-        v[j] = region_neg(pw[j], sh[j]) ? -x : x;
+    for (int u = 0; u < UQ; ++u) {
+      // (wave-uniform) past the list end / another rank's shard
+      if (lb + static_cast<int32_t>(u * W + w) >= l1 || q[u] < q0 || q[u] >= q1) continue;
+      const uint32_t len = min(m, d - q[u] * m);
+      uint32_t cw[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) cw[j] = j < rr ? __builtin_amdgcn_readlane(word[u], j) : 0u;
+      if (lane < len) {
+        float v[kMaxRows];
+#pragma unroll
+        for (int j = 0; j < kMaxRows; ++j) {
+          v[j] = 0.f;
+          if (j < NR && j < rr) {
+            const float x = reg[j * gm + (ci_region(cw[j]) - rbase) * m + in_region(pw[j], cw[j], m)];
+            v[j] = neg_of(pw[j], cw[j]) ? -x : x;
+          }
+        }
+        est[static_cast<size_t>(q[u]) * m + lane] = lower_median<RT>(v, rr);
       }
     }
-    est[i0 + o] = lower_median<RT>(v, rr);
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      q[u] = qn[u];
+      word[u] = wn[u];
+    }
   }
 }
 
@@ -182,7 +272,7 @@ __global__ void __launch_bounds__(256)
 cs_region_zero_kernel(float* __restrict__ t1, float* __restrict__ t2, const int64_t* __restrict__ idx,
                       const float* __restrict__ vals, int64_t k, uint64_t d, uint32_t r, uint32_t c,
                       uint32_t m, uint32_t nch, const uint32_t* __restrict__ perm,
-                      const uint2* __restrict__ cinfo) {
+                      const uint32_t* __restrict__ cinfo) {
   const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (e >= k * r) return;
   const int64_t t = e / r;
@@ -191,8 +281,9 @@ cs_region_zero_kernel(float* __restrict__ t1, float* __restrict__ t2, const int6
   const uint64_t i = static_cast<uint64_t>(idx[t]);
   if (i >= d) return;  // (top-k indices are always in range)
   const uint32_t q = static_cast<uint32_t>(i / m), o = static_cast<uint32_t>(i - static_cast<uint64_t>(q) * m);
-  const uint2 ci = cinfo[static_cast<size_t>(j) * nch + q];
-  const size_t cell = static_cast<size_t>(j) * c + ci.x + region_bucket(perm[static_cast<size_t>(j) * m + o], ci.y, m);
+  const uint32_t cw = cinfo[static_cast<size_t>(j) * nch + q];
+  const size_t cell = static_cast<size_t>(j) * c + static_cast<size_t>(ci_region(cw)) * m +
+                      in_region(perm[j * m + o], cw, m);
   t1[cell] = 0.f;
   if (t2 != nullptr) t2[cell] = 0.f;
 }
@@ -208,68 +299,77 @@ void set_lds_once(F* fn, int bytes, int* done) {
 
 }  // namespace
 
-int region_encode_waves(int64_t m) {
-  // W LDS copies of the region: 8 waves while they fit 2 blocks per CU
-  return m * 4 * 8 <= 80 * 1024 ? 8 : (m * 4 * 4 <= 160 * 1024 ? 4 : (m * 4 * 2 <= 160 * 1024 ? 2 : 0));
+// W = chunks per batch: one wave per chunk up to 16, two per wave at 32
+bool region_geometry_supported(int64_t r, int64_t m, int64_t g, int64_t W) {
+  return r >= 1 && r <= kMaxRows && m >= 1 && m <= 64 && g >= 1 && W >= 1 && (W <= 16 || W == 32) &&
+         W <= g && r * g * m * 4 <= 160 * 1024;
 }
 
 void launch_cs_region_encode(float* table, const float* vec, const float* wvec, float scale,
-                             float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t R,
-                             int64_t nch, const uint32_t* perm, const int32_t* cinfo,
-                             const int32_t* lists, const int32_t* offs, bool overwrite,
+                             float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t g, int64_t G,
+                             int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
+                             const int32_t* lists, const int32_t* goffs, bool overwrite,
                              hipStream_t stream) {
-  const int W = region_encode_waves(m);
-  const int lds = static_cast<int>(W * m * 4);
-  const dim3 grid(static_cast<uint32_t>(R), static_cast<uint32_t>(r));
-  const uint2* ci = reinterpret_cast<const uint2*>(cinfo);
-#define COMMEFF_REGION_ENC(WW)                                                                       \
-  do {                                                                                                \
-    static int done = 0;                                                                              \
-    set_lds_once(cs_region_encode_kernel<WW>, lds, &done);                                            \
-    hipLaunchKernelGGL(cs_region_encode_kernel<WW>, grid, dim3(WW * 64), lds, stream, table, vec, wvec, \
-                       scale, wscale, static_cast<uint32_t>(d), static_cast<uint32_t>(c),             \
-                       static_cast<uint32_t>(m), static_cast<uint32_t>(R), static_cast<uint32_t>(nch), \
-                       perm, ci, lists, offs, overwrite ? 1 : 0);                                     \
+  const int lds = static_cast<int>(r * g * m * 4);
+  const int nw = W > 16 ? 16 : static_cast<int>(W);
+  const dim3 grid(static_cast<uint32_t>(G)), block(static_cast<uint32_t>(64 * nw));
+#define COMMEFF_REGION_ENC(RR, SS, KK, HH)                                                               \
+  do {                                                                                                   \
+    static int done = 0;                                                                                 \
+    set_lds_once(cs_region_encode_kernel<RR, SS, KK, HH>, lds, &done);                                   \
+    hipLaunchKernelGGL((cs_region_encode_kernel<RR, SS, KK, HH>), grid, block, lds, stream, table, vec, wvec, \
+                       scale, wscale, static_cast<uint32_t>(d), static_cast<uint32_t>(c),                \
+                       static_cast<uint32_t>(m), static_cast<uint32_t>(g), static_cast<uint32_t>(G),     \
+                       static_cast<uint32_t>(nch), static_cast<uint32_t>(r), perm, cinfo, lists, goffs,  \
+                       overwrite ? 1 : 0);                                                               \
   } while (0)
-  if (W == 8) COMMEFF_REGION_ENC(8);
-  else if (W == 4) COMMEFF_REGION_ENC(4);
-  else COMMEFF_REGION_ENC(2);
+  const bool hw = wvec != nullptr && wscale != 0.f;
+  if (W == 32) {  // two chunks per wave per batch
+    if (r == 5 && hw) COMMEFF_REGION_ENC(5, 8, 2, true);
+    else if (r == 5) COMMEFF_REGION_ENC(5, 8, 2, false);
+    else if (hw) COMMEFF_REGION_ENC(0, 2, 2, true);
+    else COMMEFF_REGION_ENC(0, 2, 2, false);
+  } else {
+    if (r == 5 && hw) COMMEFF_REGION_ENC(5, 8, 1, true);
+    else if (r == 5) COMMEFF_REGION_ENC(5, 8, 1, false);
+    else if (hw) COMMEFF_REGION_ENC(0, 2, 1, true);
+    else COMMEFF_REGION_ENC(0, 2, 1, false);
+  }
 #undef COMMEFF_REGION_ENC
 }
 
-void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m,
-                            int64_t nch, const uint32_t* perm, const int32_t* cinfo, int64_t q0,
-                            int64_t q1, hipStream_t stream) {
+void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
+                            int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
+                            const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
+                            hipStream_t stream) {
   if (q1 <= q0) return;
-  const int lds = static_cast<int>(r * m * 4);
-  const int vec4 = (m % 4 == 0 && c % 4 == 0) ? 1 : 0;
-  const uint2* ci = reinterpret_cast<const uint2*>(cinfo);
-  const dim3 grid(static_cast<uint32_t>(q1 - q0));
-  if (r == 5) {
-    static int done = 0;
-    set_lds_once(cs_region_query_kernel<5>, lds, &done);
-    hipLaunchKernelGGL(cs_region_query_kernel<5>, grid, dim3(256), lds, stream, table, est,
-                       static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),
-                       static_cast<uint32_t>(nch), 5u, perm, ci, static_cast<uint32_t>(q0), vec4);
-  } else {
-    static int done = 0;
-    set_lds_once(cs_region_query_kernel<0>, lds, &done);
-    hipLaunchKernelGGL(cs_region_query_kernel<0>, grid, dim3(256), lds, stream, table, est,
-                       static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),
-                       static_cast<uint32_t>(nch), static_cast<uint32_t>(r), perm, ci,
-                       static_cast<uint32_t>(q0), vec4);
-  }
+  const int lds = static_cast<int>(r * g * m * 4);
+  const int vec4 = ((g * m) % 4 == 0 && c % 4 == 0) ? 1 : 0;
+  const dim3 grid(static_cast<uint32_t>(G)), block(static_cast<uint32_t>(64 * (W > 16 ? 16 : W)));
+#define COMMEFF_REGION_QRY(RR)                                                                           \
+  do {                                                                                                   \
+    static int done = 0;                                                                                 \
+    set_lds_once(cs_region_query_kernel<RR>, lds, &done);                                                \
+    hipLaunchKernelGGL((cs_region_query_kernel<RR>), grid, block, lds, stream, table, est,               \
+                       static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),     \
+                       static_cast<uint32_t>(g), static_cast<uint32_t>(nch), static_cast<uint32_t>(r),   \
+                       perm, cinfo, lists, goffs, static_cast<uint32_t>(q0), static_cast<uint32_t>(q1),  \
+                       vec4);                                                                            \
+  } while (0)
+  if (r == 5) COMMEFF_REGION_QRY(5);
+  else COMMEFF_REGION_QRY(0);
+#undef COMMEFF_REGION_QRY
 }
 
 void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float* vals, int64_t k,
                            int64_t d, int r, int64_t c, int64_t m, int64_t nch, const uint32_t* perm,
-                           const int32_t* cinfo, hipStream_t stream) {
+                           const uint32_t* cinfo, hipStream_t stream) {
   const int64_t n = k * r;
   if (n <= 0) return;
   hipLaunchKernelGGL(cs_region_zero_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0,
-                     stream, t1, t2, idx, vals, k, static_cast<uint64_t>(d), static_cast<uint32_t>(r), static_cast<uint32_t>(c),
-                     static_cast<uint32_t>(m), static_cast<uint32_t>(nch), perm,
-                     reinterpret_cast<const uint2*>(cinfo));
+                     stream, t1, t2, idx, vals, k, static_cast<uint64_t>(d), static_cast<uint32_t>(r),
+                     static_cast<uint32_t>(c), static_cast<uint32_t>(m), static_cast<uint32_t>(nch), perm,
+                     cinfo);
 }
 
 }  // namespace commeff

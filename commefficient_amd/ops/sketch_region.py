@@ -1,26 +1,43 @@
-"""Region-permutation Count-Sketch hash family (``--encode region``, default).
+"""Region Count-Sketch hash family (``--encode region``, the default).
 
-The coordinates are cut into chunks of ``m`` consecutive coordinates and each
-table row into ``R = c // m`` regions of ``m`` buckets.  In row ``j`` chunk
-``q`` is dealt to region ``rho_j(q)`` (a random order, dealt evenly) and its
-coordinate ``o`` goes to bucket ``rho_j(q)*m + (P_j(o) + shift_j(q)) mod m``
-with sign ``S_j(o) * sigma_j(q)``, where ``P_j`` is a random permutation of
-``[m]``.  Chunk-mates never collide (a bijection inside the chunk); two
-coordinates of different chunks collide with probability ``1/(R*m) ~= 1/c`` per
-row, independently across rows -- the pairwise property the Count-Sketch
-unbiasedness and variance bounds use (csvec's own ``numBlocks`` layout also
-reuses one hash per block with a per-block offset and sign:
-/root/reference/CommEfficient/fed_aggregator.py:464-467 builds it).
+The coordinates are cut into chunks of ``m = 64`` consecutive coordinates and
+each table row into regions of ``m`` buckets, ``g = 32`` regions per group
+(``G = c // (g*m)`` groups; the few leftover buckets of a row are unused).
+Chunks are dealt to the groups (random balanced order).  Inside its group a
+chunk sits in a batch of ``W = 32`` chunks, and in row ``j`` the batch's chunks
+take ``W`` distinct regions of the group (a random injection per (row,
+batch)).  Coordinate ``o`` of chunk ``q`` goes in row ``j`` to bucket
+``region_j(q)*m + (P_j(o) + shift_j(q)) mod m`` with sign
+``S_j(o) * sigma_j(q)``, where ``P_j`` is a random permutation of ``[m]`` and
+``shift_j``, ``sigma_j`` are random per (row, chunk).
 
-Why this family on MI355X: the encode becomes "add each chunk into its region"
-(region-sized LDS accumulators, no atomics, no plan arrays, no r*d
-intermediate) and the median query "stage the chunk's r regions in LDS and
-gather" (csrc/sketch_region.hip).  The parameters are a few hundred KB built
-once from the seed with numpy, identical on every rank.
+Collisions.  Chunk-mates never collide (a bijection inside the chunk).  Two
+coordinates of one group collide in row ``j`` with probability ``~G/c``,
+independently across rows; of different groups never: ``~1/c`` per row, like
+uniform hashing, every bucket receiving one coordinate from each chunk of its
+region.  Because the region a chunk takes is drawn independently per row, a
+"hot" chunk (part of a layer with large gradients) meets a different random
+``1/g`` of its group in every row and the median filters it
+(tests/test_sketch_region.py checks this against the csvec layout).  (A
+first version shared one region assignment across all rows so that the
+encode would read each chunk once: then a hot chunk pollutes the same
+region-mates in every row, and ResNet-9 training stalled -- bench loss after
+250 rounds 0.9994 vs 0.0005, profiles/r3_experiments.md.)  The reference's
+CSVec also reuses one hash per block with a per-block offset and sign
+(numBlocks, /root/reference/CommEfficient/fed_aggregator.py:464-467 builds it).
+
+Why this family on MI355X: a group's ``r x g`` regions (40 KB) fit in LDS, so
+the encode is one block per group reading each of its chunks once (one
+wavefront per chunk; the batch structure makes a batch's updates
+conflict-free, so no atomics) and the query one block per group staging its
+regions once and gathering for all its chunks (csrc/sketch_region.hip): no
+plan arrays, no ``r*d`` intermediate.  The parameters (a 4-byte word per
+(row, chunk), the permutations, the grouped chunk list) are built once from
+the seed with numpy, identical on every rank.
 
 The CPU implementation below (dense bucket / sign arrays, ``index_add_``,
-``torch.median`` = lower median) defines the same family for CPU runs and
-serves as the reference the GPU kernels are tested against.
+``torch.median`` = lower median) defines the same family for CPU runs and is
+the reference the GPU kernels are tested against.
 """
 from __future__ import annotations
 
@@ -32,39 +49,53 @@ import torch
 from .._ext import ops
 
 
-def region_size(c: int, r: int, target: int = 2048) -> int:
-    """Chunk / region size m for a c-column, r-row table: about ``target``
-    (one 8 KB LDS copy per wave in the encode), r regions in LDS for the query
-    (r*m*4 <= 160 KB), and c // m regions (at most R - 1 buckets unused)."""
-    target = max(1, min(int(target), (160 * 1024) // (4 * max(1, r))))
-    if c <= target:
-        return int(c)
-    R = -(-c // target)
-    return int(c // R)
+def region_geometry(c: int, r: int, m: int = 64, g: int = 32, W: int = 32):
+    """(m, g, G, W): chunk / region size m (<= 64: one wavefront per chunk),
+    g regions per group (r*g*m floats fit in LDS), G = c // (g*m) groups, W
+    chunks per batch (<= g; 16 wavefronts per block, two chunks per wavefront
+    at W = 32: one barrier per two chunks)."""
+    m = max(1, min(int(m), int(c)))
+    g = max(1, min(int(g), int(c) // m, (160 * 1024) // (4 * m * max(1, int(r)))))
+    W = max(1, min(int(W), g))
+    if 16 < W < 32:
+        W = 16
+    return m, g, int(c) // (g * m), W
 
 
 class RegionHash:
     """Parameters of one (d, c, r, seed) region sketch.
 
     Host arrays (numpy): ``P`` [r, m] permutation, ``S`` [r, m] sign bit,
-    ``region`` [r, nch], ``shift`` [r, nch], ``sigma`` [r, nch] sign bit.
-    Device tensors (``tensors(device)``): perm / cinfo / lists / offs as the
+    ``group`` [nch], ``region`` [r, nch] (global region index), ``shift``
+    [r, nch], ``sigma`` [r, nch] sign bit, ``lists`` / ``goffs`` the chunks
+    group by group in batch order.  Device tensors (``tensors(device)``):
+    perm / cinfo (by chunk) / cinfo_l (in list order) / lists / goffs as the
     kernels read them (csrc/kernels.h)."""
 
-    def __init__(self, d: int, c: int, r: int, seed: int = 42, m: Optional[int] = None):
+    def __init__(self, d: int, c: int, r: int, seed: int = 42, **geom):
         self.d, self.c, self.r = int(d), int(c), int(r)
-        self.m = int(m) if m else region_size(self.c, self.r)
-        assert 1 <= self.m <= self.c
-        self.R = self.c // self.m
-        self.nch = -(-self.d // self.m)
-        rng = np.random.default_rng([int(seed), 0x5E610, self.d, self.c, self.r])
-        r_, m_, nch, R = self.r, self.m, self.nch, self.R
+        self.m, self.g, self.G, self.W = region_geometry(self.c, self.r, **geom)
+        m_, g_, G, W, r_ = self.m, self.g, self.G, self.W, self.r
+        self.R = G * g_
+        nch = self.nch = -(-self.d // m_)
+        rng = np.random.default_rng([int(seed), 0x5E611, self.d, self.c, self.r])
         self.P = np.stack([rng.permutation(m_) for _ in range(r_)]).astype(np.int64)
         self.S = rng.integers(0, 2, size=(r_, m_), dtype=np.int64)
+        order = rng.permutation(nch)
+        group = np.empty(nch, dtype=np.int64)
+        within = np.empty(nch, dtype=np.int64)
+        group[order] = np.arange(nch) % G      # dealt evenly
+        within[order] = np.arange(nch) // G    # position inside the group's list
+        self.group = group
+        self.lists = np.concatenate([order[x::G] for x in range(G)]).astype(np.int32)
+        self.goffs = np.concatenate([[0], np.cumsum([len(order[x::G]) for x in range(G)])]).astype(np.int32)
+        batch, slot = within // W, within % W
+        nbatch = int(batch.max()) + 1
         region = np.empty((r_, nch), dtype=np.int64)
         for j in range(r_):
-            order = rng.permutation(nch)
-            region[j, order] = np.arange(nch) % R  # dealt evenly
+            # per (group, batch): the batch's W chunks take W distinct regions
+            inj = np.argsort(rng.random((G, nbatch, g_)), axis=-1)[..., :W]
+            region[j] = group * g_ + inj[group, batch, slot]
         self.region = region
         self.shift = rng.integers(0, m_, size=(r_, nch), dtype=np.int64)
         self.sigma = rng.integers(0, 2, size=(r_, nch), dtype=np.int64)
@@ -76,20 +107,13 @@ class RegionHash:
         device = torch.device(device)
         key = str(device)
         if key not in self._dev:
-            r_, m_, nch, R = self.r, self.m, self.nch, self.R
             perm = (self.P | (self.S << 31)).astype(np.uint32).view(np.int32)
-            cinfo = np.empty((r_, nch, 2), dtype=np.uint32)
-            cinfo[..., 0] = (self.region * m_).astype(np.uint32)
-            cinfo[..., 1] = (self.shift | (self.sigma << 31)).astype(np.uint32)
-            lists = np.empty((r_, nch), dtype=np.int32)
-            offs = np.empty((r_, R + 1), dtype=np.int32)
-            for j in range(r_):
-                order = np.lexsort((np.arange(nch), self.region[j]))  # by region, then chunk
-                lists[j] = order
-                offs[j] = np.searchsorted(self.region[j][order], np.arange(R + 1))
+            cinfo = (self.region | (self.shift << 24) | (self.sigma << 31)).astype(np.uint32).view(np.int32)
             t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
-            self._dev[key] = {"perm": t(perm), "cinfo": t(cinfo.view(np.int32)),
-                              "lists": t(lists), "offs": t(offs)}
+            self._dev[key] = {"perm": t(perm), "cinfo": t(cinfo), "lists": t(self.lists),
+                              "goffs": t(self.goffs),
+                              # list order, rows innermost: the encode / query stream it
+                              "cinfo_l": t(cinfo[:, self.lists].T)}
         return self._dev[key]
 
     def chunk_bounds(self, world: int) -> list:
@@ -123,8 +147,8 @@ def encode(h: RegionHash, table: torch.Tensor, vec: torch.Tensor, scale: float =
     if table.is_cuda:
         t = h.tensors(table.device)
         ops().cs_region_encode(table, v, float(scale), wvec.reshape(-1) if wvec is not None else None,
-                               float(wscale), h.m, t["perm"], t["cinfo"], t["lists"], t["offs"],
-                               bool(overwrite))
+                               float(wscale), h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
+                               t["goffs"], bool(overwrite))
         return
     x = v.float() * scale
     if wvec is not None and wscale != 0.0:
@@ -142,7 +166,8 @@ def query(h: RegionHash, table: torch.Tensor, q0: int = 0, q1: int = -1) -> torc
     chunks [q0, q1) when given, the rest left unset on the GPU)."""
     if table.is_cuda:
         t = h.tensors(table.device)
-        return ops().cs_region_query(table, h.d, h.m, t["perm"], t["cinfo"], int(q0), int(q1))
+        return ops().cs_region_query(table, h.d, h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
+                                     t["goffs"], int(q0), int(q1))
     b, s = h.dense()
     tv = table.view(h.r, h.c)
     vals = torch.stack([s[j] * tv[j][b[j]] for j in range(h.r)])
@@ -156,7 +181,7 @@ def zero_buckets(h: RegionHash, t1: torch.Tensor, t2: Optional[torch.Tensor], id
     if t1.is_cuda:
         t = h.tensors(t1.device)
         ops().cs_region_zero(t1, t2, idx.contiguous(), vals.contiguous() if vals is not None else None,
-                             h.d, h.m, t["perm"], t["cinfo"])
+                             h.d, h.m, h.g, t["perm"], t["cinfo"])
         return
     sel = idx if vals is None else idx[vals != 0]
     if sel.numel() == 0:
@@ -181,4 +206,4 @@ def collision_rate(h: RegionHash, pairs: int = 200000, seed: int = 0) -> float:
     return float((b[:, a[keep]] == b[:, c[keep]]).float().mean())
 
 
-__all__ = ["RegionHash", "region_size", "encode", "query", "zero_buckets", "collision_rate"]
+__all__ = ["RegionHash", "region_geometry", "encode", "query", "zero_buckets", "collision_rate"]
