@@ -410,6 +410,41 @@ at::Tensor cs_region_query_hip(const at::Tensor& table, int64_t d, int64_t m, in
   return est;
 }
 
+// the unsketch of a chunk range in one go: median query fused with the top-k's
+// first histogram, then the remaining top-k passes over est[q0*m, q1*m);
+// returns (idx relative to q0*m, vals)
+std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(const at::Tensor& table, int64_t d, int64_t m, int64_t g,
+                                                      int64_t W, const at::Tensor& perm, const at::Tensor& cinfo,
+                                                      const at::Tensor& lists, const at::Tensor& goffs, int64_t k,
+                                                      const c10::optional<at::Tensor>& hint, int64_t q0,
+                                                      int64_t q1) {
+  const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
+  if (q1 < 0) q1 = p.nch;
+  TORCH_CHECK(q0 >= 0 && q0 < q1 && q1 <= p.nch, "cs_region_topk: chunk range out of bounds");
+  const int64_t lo = q0 * m, hi = std::min(d, q1 * m), n = hi - lo;
+  TORCH_CHECK(k >= 1 && k < n, "cs_region_topk: need 1 <= k < shard size");
+  uint32_t* hp = nullptr;
+  if (hint.has_value() && hint->defined()) {
+    TORCH_CHECK(hint->scalar_type() == at::kInt && hint->numel() >= 1 && hint->device() == table.device(),
+                "cs_region_topk: hint must be an int32 device tensor");
+    hp = reinterpret_cast<uint32_t*>(hint->data_ptr<int32_t>());
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  auto est = at::empty({d}, table.options());
+  auto ws = at::empty({topk_workspace_bytes(n)}, table.options().dtype(at::kByte));
+  auto idx = at::empty({k}, table.options().dtype(at::kLong));
+  auto vals = at::empty({k}, table.options());
+  topk_prepare(ws.data_ptr(), cur_stream());
+  launch_cs_region_query(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(p.r), p.c, m, g, p.G,
+                         W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+                         reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
+                         goffs.data_ptr<int32_t>(), q0, q1, cur_stream(), hp,
+                         reinterpret_cast<uint32_t*>(ws.data_ptr()));
+  launch_topk_abs_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                       ws.data_ptr(), cur_stream(), hp);
+  return {idx, vals};
+}
+
 void cs_region_zero_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2, const at::Tensor& idx,
                         const c10::optional<at::Tensor>& vals, int64_t d, int64_t m, int64_t g,
                         const at::Tensor& perm, const at::Tensor& cinfo) {
@@ -1975,6 +2010,8 @@ TORCH_LIBRARY(commeff, m) {
         "int g, int W, Tensor perm, Tensor cinfo, Tensor lists, Tensor goffs, bool overwrite=False) -> ()");
   m.def("cs_region_query(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
         "Tensor goffs, int q0=0, int q1=-1) -> Tensor");
+  m.def("cs_region_topk(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
+        "Tensor goffs, int k, Tensor? hint=None, int q0=0, int q1=-1) -> (Tensor, Tensor)");
   m.def("cs_region_zero(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, int d, int m, int g, "
         "Tensor perm, Tensor cinfo) -> ()");
   m.def("topk_abs(Tensor x, int k, Tensor? hint=None) -> (Tensor, Tensor)");
@@ -2078,6 +2115,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("cs_region_encode", &cs_region_encode_hip);
   m.impl("cs_region_query", &cs_region_query_hip);
   m.impl("cs_region_zero", &cs_region_zero_hip);
+  m.impl("cs_region_topk", &cs_region_topk_hip);
   m.impl("topk_abs", &topk_abs_hip);
   m.impl("momentum_ef", &momentum_ef_hip);
   m.impl("sparse_apply", &sparse_apply_hip);

@@ -106,11 +106,12 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
                              int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                              const int32_t* lists, const int32_t* goffs, bool overwrite,
                              hipStream_t stream);
-// est[i] for the coordinates of chunks [q0, q1)
+// est[i] for the coordinates of chunks [q0, q1); hist0 != nullptr: also the
+// top-k's first histogram of est (see topk_prepare)
 void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
                             int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
-                            hipStream_t stream);
+                            hipStream_t stream, const uint32_t* hint = nullptr, uint32_t* hist0 = nullptr);
 void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float* vals, int64_t k,
                            int64_t d, int r, int64_t c, int64_t m, int64_t nch, const uint32_t* perm,
                            const uint32_t* cinfo, hipStream_t stream);
@@ -129,6 +130,12 @@ int64_t topk_workspace_bytes(int64_t n);
 void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx,
                      float* vals, void* workspace, hipStream_t stream,
                      uint32_t* hint = nullptr);
+// the same selection split at the first histogram: topk_prepare zeroes the
+// histograms, a producer builds hist[0] (uint32 [2048] at the workspace
+// start: keys = bits & 0x7fffffff >= hint[0], bin key >> 20), then the rest
+void topk_prepare(void* workspace, hipStream_t stream);
+void launch_topk_abs_rest(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,
+                          void* workspace, hipStream_t stream, uint32_t* hint);
 
 // ----------------------------------------------------------- elementwise --
 // V = rho*V + gscale*G ; mode 1: E += V ; mode 2: E = V

@@ -187,14 +187,22 @@ __device__ __forceinline__ float lower_median(float (&v)[kMaxRows], int r) {
   return res;
 }
 
-// est for the chunks of group blockIdx.x inside [q0, q1); blockDim = 64 * W
-template <int RT>
+// est for the chunks of group blockIdx.x inside [q0, q1); blockDim = 64 * W.
+// HIST: also the top-k's first histogram of the estimates (csrc/topk.hip
+// pass 0: keys = bits & 0x7fffffff >= hint[0], bin = key >> 20) -- LDS
+// privatised, non-empty bins added to hist0: integer counts, deterministic
+template <int RT, bool HIST>
 __global__ void __launch_bounds__(1024)
 cs_region_query_kernel(const float* __restrict__ table, float* __restrict__ est, uint32_t d,
                        uint32_t c, uint32_t m, uint32_t g, uint32_t nch, uint32_t r_rt,
                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
                        const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
-                       uint32_t q0, uint32_t q1, int vec4) {
+                       uint32_t q0, uint32_t q1, int vec4, const uint32_t* __restrict__ hint,
+                       uint32_t* __restrict__ hist0) {
+  __shared__ uint32_t hh[HIST ? 2048 : 1];
+  if constexpr (HIST)
+    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) hh[b] = 0u;
+  const uint32_t hlb = (HIST && hint != nullptr) ? hint[0] : 0u;
   constexpr int NR = RT > 0 ? RT : kMaxRows;
   extern __shared__ __attribute__((aligned(16))) float reg[];  // [r][g * m]
   const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
@@ -256,7 +264,12 @@ cs_region_query_kernel(const float* __restrict__ table, float* __restrict__ est,
             v[j] = neg_of(pw[j], cw[j]) ? -x : x;
           }
         }
-        est[static_cast<size_t>(q[u]) * m + lane] = lower_median<RT>(v, rr);
+        const float e = lower_median<RT>(v, rr);
+        est[static_cast<size_t>(q[u]) * m + lane] = e;
+        if constexpr (HIST) {
+          const uint32_t key = __float_as_uint(e) & 0x7fffffffu;
+          if (key >= hlb) atomicAdd(hh + (key >> 20), 1u);
+        }
       }
     }
 #pragma unroll
@@ -264,6 +277,11 @@ cs_region_query_kernel(const float* __restrict__ table, float* __restrict__ est,
       q[u] = qn[u];
       word[u] = wn[u];
     }
+  }
+  if constexpr (HIST) {
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x)
+      if (hh[b] != 0u) atomicAdd(hist0 + b, hh[b]);
   }
 }
 
@@ -341,23 +359,28 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
 void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
                             int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
-                            hipStream_t stream) {
+                            hipStream_t stream, const uint32_t* hint, uint32_t* hist0) {
   if (q1 <= q0) return;
   const int lds = static_cast<int>(r * g * m * 4);
   const int vec4 = ((g * m) % 4 == 0 && c % 4 == 0) ? 1 : 0;
   const dim3 grid(static_cast<uint32_t>(G)), block(static_cast<uint32_t>(64 * (W > 16 ? 16 : W)));
-#define COMMEFF_REGION_QRY(RR)                                                                           \
+#define COMMEFF_REGION_QRY(RR, HH)                                                                       \
   do {                                                                                                   \
     static int done = 0;                                                                                 \
-    set_lds_once(cs_region_query_kernel<RR>, lds, &done);                                                \
-    hipLaunchKernelGGL((cs_region_query_kernel<RR>), grid, block, lds, stream, table, est,               \
+    set_lds_once(cs_region_query_kernel<RR, HH>, lds, &done);                                            \
+    hipLaunchKernelGGL((cs_region_query_kernel<RR, HH>), grid, block, lds, stream, table, est,           \
                        static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),     \
                        static_cast<uint32_t>(g), static_cast<uint32_t>(nch), static_cast<uint32_t>(r),   \
                        perm, cinfo, lists, goffs, static_cast<uint32_t>(q0), static_cast<uint32_t>(q1),  \
-                       vec4);                                                                            \
+                       vec4, hint, hist0);                                                               \
   } while (0)
-  if (r == 5) COMMEFF_REGION_QRY(5);
-  else COMMEFF_REGION_QRY(0);
+  if (hist0 != nullptr) {
+    if (r == 5) COMMEFF_REGION_QRY(5, true);
+    else COMMEFF_REGION_QRY(0, true);
+  } else {
+    if (r == 5) COMMEFF_REGION_QRY(5, false);
+    else COMMEFF_REGION_QRY(0, false);
+  }
 #undef COMMEFF_REGION_QRY
 }
 

@@ -385,13 +385,32 @@ int64_t topk_workspace_bytes(int64_t) {
 void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,
                      void* workspace, hipStream_t stream, uint32_t* hint) {
   if (k <= 0 || n <= 0) return;
+  topk_prepare(workspace, stream);
   WS w = carve(workspace);
-  (void)hipMemsetAsync(w.hist[0], 0, 4 * kBins * 4, stream);
   int hb = static_cast<int>((n + 1023) / 1024);
   if (hb > 1024) hb = 1024;
   if (hb < 1) hb = 1;
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
   hipLaunchKernelGGL(hist_kernel<0>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
+  launch_topk_abs_rest(x, n, k, idx, vals, workspace, stream, hint);
+}
+
+void topk_prepare(void* workspace, hipStream_t stream) {
+  WS w = carve(workspace);
+  (void)hipMemsetAsync(w.hist[0], 0, 4 * kBins * 4, stream);
+}
+
+// the passes after the first histogram (hist[0] at the workspace start: keys
+// >= hint[0] counted by their top 11 bits -- hist_kernel<0> or a producer
+// kernel that saw every element, e.g. the region sketch query)
+void launch_topk_abs_rest(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,
+                          void* workspace, hipStream_t stream, uint32_t* hint) {
+  if (k <= 0 || n <= 0) return;
+  WS w = carve(workspace);
+  int hb = static_cast<int>((n + 1023) / 1024);
+  if (hb > 1024) hb = 1024;
+  if (hb < 1) hb = 1;
+  const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
   if (hint != nullptr)
     hipLaunchKernelGGL(hist_kernel<3>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
   hipLaunchKernelGGL(hist_kernel<1>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);

@@ -175,6 +175,9 @@ class CSVec:
                               self.numBlocks, self.d)
 
     def unsketch_sparse(self, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.region is not None:
+            return _rg().topk(self.region, self.table, int(k),
+                              _topk_hint(("unsketch", self.d, int(k)), self.table.device))
         est = self.query()
         return ops().topk_abs(est, int(k), _topk_hint(("unsketch", self.d, int(k)), est.device))
 
@@ -214,15 +217,15 @@ class CSVec:
         the estimates) of its shard's top-k."""
         b = bounds if bounds is not None else self.shard_bounds(world)
         lo, hi = b[rank], b[rank + 1]
+        hint = _topk_hint(("unsketch_shard", self.d, k, rank, world), self.table.device)
         if self.region is not None:
             qb = self.region.chunk_bounds(world)
-            est = _rg().query(self.region, self.table, qb[rank], qb[rank + 1])
+            li, lv = _rg().topk(self.region, self.table, k, hint, qb[rank], qb[rank + 1])
         else:
             nch = int(ops().plan_geometry(self.d, self.r, self.c)[3])
             est = ops().cs_query_planned(self.table, self.d, self._plan(), nch * rank // world,
                                          nch * (rank + 1) // world)
-        li, lv = ops().topk_abs(est[lo:hi], k, _topk_hint(("unsketch_shard", self.d, k, rank, world),
-                                                         est.device))
+            li, lv = ops().topk_abs(est[lo:hi], k, hint)
         pack = torch.empty(2, k, dtype=torch.int64, device=self.device)
         pack[0] = li + lo
         pack[1] = lv.view(torch.int32)

@@ -174,6 +174,22 @@ def query(h: RegionHash, table: torch.Tensor, q0: int = 0, q1: int = -1) -> torc
     return vals.median(dim=0).values
 
 
+def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor] = None,
+         q0: int = 0, q1: int = -1):
+    """(idx, vals): the k largest-magnitude median estimates of the
+    coordinates of chunks [q0, q1) (idx relative to q0*m, ascending; ties ->
+    lower index).  GPU: one fused launch sequence -- the query also builds the
+    selection's first histogram (csrc/topk.hip, no extra pass over est)."""
+    q1 = h.nch if q1 < 0 else q1
+    lo, hi = q0 * h.m, min(h.d, q1 * h.m)
+    if table.is_cuda and 1 <= k < hi - lo:
+        t = h.tensors(table.device)
+        return ops().cs_region_topk(table, h.d, h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
+                                    t["goffs"], int(k), hint, int(q0), int(q1))
+    est = query(h, table, q0, q1)
+    return ops().topk_abs(est[lo:hi].contiguous(), int(k), hint)
+
+
 def zero_buckets(h: RegionHash, t1: torch.Tensor, t2: Optional[torch.Tensor], idx: torch.Tensor,
                  vals: Optional[torch.Tensor]):
     """Zero cells (j, bucket_j(i)) of t1 (and t2) of the coordinates in idx
@@ -206,4 +222,4 @@ def collision_rate(h: RegionHash, pairs: int = 200000, seed: int = 0) -> float:
     return float((b[:, a[keep]] == b[:, c[keep]]).float().mean())
 
 
-__all__ = ["RegionHash", "region_geometry", "encode", "query", "zero_buckets", "collision_rate"]
+__all__ = ["RegionHash", "region_geometry", "encode", "query", "topk", "zero_buckets", "collision_rate"]

@@ -211,3 +211,25 @@ def test_hot_chunks_are_filtered_by_the_median():
         sk.accumulateVec(v)
         err[kern] = float((sk.query()[heavy] - v[heavy]).abs().median())
     assert err["region"] <= 2 * err["planned"] + 0.005, err
+
+
+@pytest.mark.gpu
+def test_region_fused_topk_matches_query_then_topk():
+    # the fused unsketch (query + first top-k histogram in one kernel) selects
+    # bitwise what query() followed by the standalone top-k selects, with and
+    # without a (stale, too high, too low) hint, on full and chunk ranges
+    from commefficient_amd import ops as O
+    d, c, r, k = 6568640, 500000, 5, 50000
+    sk = CSVec(d, c, r, device="cuda", kernel="region")
+    sk.accumulateVec(torch.randn(d, device="cuda") * torch.rand(d, device="cuda") ** 4, overwrite=True)
+    est = sk.query()
+    ref = O.topk_abs(est, k)
+    for hv in (None, 0, 0x3f000000, 0x7f000000):
+        hint = None if hv is None else torch.full((1,), hv, dtype=torch.int32, device="cuda")
+        idx, vals = sketch_region.topk(sk.region, sk.table, k, hint)
+        assert torch.equal(idx, ref[0]) and torch.equal(vals, ref[1])
+    qb = sk.region.chunk_bounds(4)
+    lo, hi = qb[1] * sk.region.m, qb[2] * sk.region.m
+    ref2 = O.topk_abs(est[lo:hi].contiguous(), k)
+    idx, vals = sketch_region.topk(sk.region, sk.table, k, None, qb[1], qb[2])
+    assert torch.equal(idx, ref2[0]) and torch.equal(vals, ref2[1])
