@@ -376,7 +376,7 @@ RegionParams check_region(const at::Tensor& table, int64_t d, int64_t m, int64_t
 void cs_region_encode_hip(at::Tensor table, const at::Tensor& vec, double scale,
                           const c10::optional<at::Tensor>& wvec, double wscale, int64_t m, int64_t g, int64_t W,
                           const at::Tensor& perm, const at::Tensor& cinfo, const at::Tensor& lists,
-                          const at::Tensor& goffs, bool overwrite) {
+                          const at::Tensor& goffs, bool overwrite, bool zero_vec) {
   check_f32(vec, "vec");
   const int64_t d = vec.numel();
   const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
@@ -390,7 +390,8 @@ void cs_region_encode_hip(at::Tensor table, const at::Tensor& vec, double scale,
                           static_cast<float>(scale), static_cast<float>(wscale), d, static_cast<int>(p.r), p.c,
                           m, g, p.G, W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                           reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
-                          goffs.data_ptr<int32_t>(), overwrite, cur_stream());
+                          goffs.data_ptr<int32_t>(), overwrite, cur_stream(),
+                          zero_vec ? const_cast<float*>(vec.data_ptr<float>()) : nullptr);
 }
 
 // est [d]; with q0 < q1 only the coordinates of chunks [q0, q1) are computed
@@ -2007,7 +2008,8 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor blk_off, Tensor blk_sign, int num_blocks, int d) -> ()");
   m.def("cs_l2estimate(Tensor table) -> Tensor");
   m.def("cs_region_encode(Tensor(a!) table, Tensor vec, float scale, Tensor? wvec, float wscale, int m, "
-        "int g, int W, Tensor perm, Tensor cinfo, Tensor lists, Tensor goffs, bool overwrite=False) -> ()");
+        "int g, int W, Tensor perm, Tensor cinfo, Tensor lists, Tensor goffs, bool overwrite=False, "
+        "bool zero_vec=False) -> ()");
   m.def("cs_region_query(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
         "Tensor goffs, int q0=0, int q1=-1) -> Tensor");
   m.def("cs_region_topk(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "

@@ -159,36 +159,65 @@ __global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
 
 // Weight gradient.  LDS images (64 rows of 128 B, sw_tr128 swizzle):
 // A = g[px][k] (masked gy), B = im2col[px][4 tap + c] (taps 9..15 zero).
-struct PrepWgStage {
-  v4u g[2];  // 16-byte chunks of g: rows (tid + 256 i) >> 3, chunk (tid + 256 i) & 7
-  v4u xb[2]; // 16-byte chunks of im2col: two taps each
+// Raw operands of one 64-pixel step as loaded: every load unconditional (a
+// clamped in-range address, validity kept as bits and applied when the step
+// is staged in LDS) -- a load under a branch is waited for inside it, which
+// had left the "prefetched" step serialised behind the MFMAs
+struct PrepWgRaw {
+  v4u g[2];   // gy chunks (rows (tid + 256 i) >> 3, chunk (tid + 256 i) & 7)
+  v2u mw[2];  // the rows' ReLU-mask words
+  v2u t[2][2];  // the two taps of the im2col chunk
+  uint32_t ok;  // bit 3i: row valid, 3i+1 / 3i+2: tap 0 / 1 inside the image
 };
 
-__device__ __forceinline__ void prep_wg_load(const ConvPrepArgs& a, int step, int tid, PrepWgStage& st) {
+__device__ __forceinline__ void prep_wg_load_raw(const ConvPrepArgs& a, int step, int tid, PrepWgRaw& st) {
+  st.ok = 0u;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int id = tid + 256 * i, row = id >> 3, cc = id & 7;
-    const PrepPix x = prep_pix(a, step * 64 + row);
-    v4u g = {0u, 0u, 0u, 0u};
-    if (x.valid) {
-      g = *reinterpret_cast<const v4u*>(a.gy + static_cast<size_t>(x.p) * kPrepK + 8 * cc);
-      const v2u mw = *reinterpret_cast<const v2u*>(a.mask_in + 2 * x.p);
-      // channels 8cc + j: word j >> 2, bit 16 (cc >> 2) + 4 (cc & 3) + (j & 3)
-      const int sh = 16 * (cc >> 2) + 4 * (cc & 3);
-      const uint32_t m0 = mw[0] >> sh, m1 = mw[1] >> sh;
+    const PrepPix x = prep_pix(a, step * 64 + row);  // x.p = 0 when invalid
+    st.g[i] = *reinterpret_cast<const v4u*>(a.gy + static_cast<size_t>(x.p) * kPrepK + 8 * cc);
+    st.mw[i] = *reinterpret_cast<const v2u*>(a.mask_in + 2 * x.p);
+    st.ok |= (x.valid ? 1u : 0u) << (3 * i);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t bits = q < 2 ? m0 : m1;  // element pair q covers channels 2q, 2q+1
-        const int j0 = (2 * q) & 3;
-        const uint32_t keep = (((bits >> j0) & 1u) ? 0x0000ffffu : 0u) |
-                              (((bits >> (j0 + 1)) & 1u) ? 0xffff0000u : 0u);
-        g[q] &= keep;
-      }
+    for (int h = 0; h < 2; ++h) {
+      const int tap = 2 * cc + h;
+      const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+      const bool ok = tap < 9 && x.valid && static_cast<unsigned>(x.h + dr) < static_cast<unsigned>(a.H) &&
+                      static_cast<unsigned>(x.w + ds) < static_cast<unsigned>(a.W);
+      const int src = ok ? x.p + dr * a.W + ds : x.p;
+      st.t[i][h] = *reinterpret_cast<const v2u*>(a.x + static_cast<size_t>(src) * 4);
+      st.ok |= (ok ? 1u : 0u) << (3 * i + 1 + h);
     }
-    st.g[i] = g;
-    const v2u t0 = prep_tap(a, x, 2 * cc), t1 = prep_tap(a, x, 2 * cc + 1);
-    st.xb[i] = v4u{t0[0], t0[1], t1[0], t1[1]};
   }
+}
+
+// masked gy chunk / im2col chunk of row i of a raw step
+__device__ __forceinline__ void prep_wg_finish(const ConvPrepArgs& a, const PrepWgRaw& st, int i, int cc,
+                                               v4u* g, v4u* xb) {
+  v4u gg = {0u, 0u, 0u, 0u};
+  if ((st.ok >> (3 * i)) & 1u) {
+    gg = st.g[i];
+    // channels 8cc + j: word j >> 2, bit 16 (cc >> 2) + 4 (cc & 3) + (j & 3)
+    const int sh = 16 * (cc >> 2) + 4 * (cc & 3);
+    const uint32_t m0 = st.mw[i][0] >> sh, m1 = st.mw[i][1] >> sh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t bits = q < 2 ? m0 : m1;  // element pair q covers channels 2q, 2q+1
+      const int j0 = (2 * q) & 3;
+      const uint32_t keep = (((bits >> j0) & 1u) ? 0x0000ffffu : 0u) |
+                            (((bits >> (j0 + 1)) & 1u) ? 0xffff0000u : 0u);
+      gg[q] &= keep;
+    }
+  }
+  *g = gg;
+  v2u t0 = ((st.ok >> (3 * i + 1)) & 1u) ? st.t[i][0] : v2u{0u, 0u};
+  v2u t1 = ((st.ok >> (3 * i + 2)) & 1u) ? st.t[i][1] : v2u{0u, 0u};
+  if (a.Cin <= 3) {
+    t0[1] &= 0xffffu;
+    t1[1] &= 0xffffu;
+  }
+  *xb = v4u{t0[0], t0[1], t1[0], t1[1]};
 }
 
 __global__ void __launch_bounds__(256) prep_wgrad_kernel(ConvPrepArgs a, int steps_per_block) {
@@ -197,31 +226,48 @@ __global__ void __launch_bounds__(256) prep_wgrad_kernel(ConvPrepArgs a, int ste
   const int mi = wid >> 1, ni = wid & 1;
   const int nsteps = (a.P + 63) / 64;
   const int s0 = blockIdx.x * steps_per_block, s1 = min(nsteps, s0 + steps_per_block);
+  if (s0 >= s1) return;  // (block-uniform)
   int toA[2], toB[2];
   tr_offsets<128>(mi * 32, lane, toA);
   tr_offsets<128>(ni * 32, lane, toB);
   f32x16_t acc;
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-  PrepWgStage st;
-  if (s0 < s1) prep_wg_load(a, s0, tid, st);
-  for (int step = s0; step < s1; ++step) {
-    __syncthreads();  // the previous step's operand reads are done
+  // two raw stages: the loads of step s + 2 are in flight during the MFMAs
+  // of steps s and s + 1 (step indices past the block clamp to its last step)
+  PrepWgRaw sa, sb;
+  prep_wg_load_raw(a, s0, tid, sa);
+  prep_wg_load_raw(a, min(s0 + 1, s1 - 1), tid, sb);
+  auto process = [&](const PrepWgRaw& st) __attribute__((always_inline)) {
+    // the previous step's operand reads are done (LDS only: the raw stages
+    // ahead stay in flight -- __syncthreads would drain them)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int id = tid + 256 * i, row = id >> 3, cc = id & 7;
       const int off = row * 128 + ((cc ^ sw_tr128(row)) << 4);
-      *reinterpret_cast<v4u*>(sm + off) = st.g[i];
-      *reinterpret_cast<v4u*>(sm + 8192 + off) = st.xb[i];
+      v4u g, xb;
+      prep_wg_finish(a, st, i, cc, &g, &xb);
+      *reinterpret_cast<v4u*>(sm + off) = g;
+      *reinterpret_cast<v4u*>(sm + 8192 + off) = xb;
     }
-    __syncthreads();
-    if (step + 1 < s1) prep_wg_load(a, step + 1, tid, st);  // lands during the MFMAs
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int d = kk * 16 * 128;
       const bf16x8_t af = tr_read(sm + toA[0] + d, sm + toA[1] + d);
       const bf16x8_t bf = tr_read(sm + 8192 + toB[0] + d, sm + 8192 + toB[1] + d);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+    }
+  };
+  for (int step = s0; step < s1; step += 2) {
+    process(sa);
+    prep_wg_load_raw(a, min(step + 2, s1 - 1), tid, sa);
+    if (step + 1 < s1) {  // (block-uniform)
+      process(sb);
+      prep_wg_load_raw(a, min(step + 3, s1 - 1), tid, sb);
     }
   }
   // partial[block][k][n], n = 4 tap + c

@@ -105,7 +105,7 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
                              float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t g, int64_t G,
                              int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                              const int32_t* lists, const int32_t* goffs, bool overwrite,
-                             hipStream_t stream);
+                             hipStream_t stream, float* zero_vec = nullptr);  // zero_vec: vec, cleared
 // est[i] for the coordinates of chunks [q0, q1); hist0 != nullptr: also the
 // top-k's first histogram of est (see topk_prepare)
 void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,

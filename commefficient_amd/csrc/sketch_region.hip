@@ -61,7 +61,7 @@ cs_region_encode_kernel(float* __restrict__ table, const float* __restrict__ vec
                         uint32_t c, uint32_t m, uint32_t g, uint32_t G, uint32_t nch, uint32_t r_rt,
                         const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
                         const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
-                        int overwrite) {
+                        int overwrite, float* __restrict__ zero_vec) {
   constexpr int NR = RT > 0 ? RT : kMaxRows;
   extern __shared__ __attribute__((aligned(16))) float acc[];  // [r][g * m]
   const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
@@ -129,6 +129,9 @@ cs_region_encode_kernel(float* __restrict__ table, const float* __restrict__ vec
         __builtin_amdgcn_s_barrier();
       }
       if (live) {
+        // zero_vec (== vec): the encode is the vector's last reader -- clear
+        // it for the next accumulation (each element is read exactly once)
+        if (zero_vec != nullptr) zero_vec[static_cast<size_t>(qc[u]) * m + lane] = 0.f;
         uint32_t b[NR];
         float a[NR];
 #pragma unroll
@@ -327,7 +330,7 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
                              float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t g, int64_t G,
                              int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                              const int32_t* lists, const int32_t* goffs, bool overwrite,
-                             hipStream_t stream) {
+                             hipStream_t stream, float* zero_vec) {
   const int lds = static_cast<int>(r * g * m * 4);
   const int nw = W > 16 ? 16 : static_cast<int>(W);
   const dim3 grid(static_cast<uint32_t>(G)), block(static_cast<uint32_t>(64 * nw));
@@ -339,7 +342,7 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
                        scale, wscale, static_cast<uint32_t>(d), static_cast<uint32_t>(c),                \
                        static_cast<uint32_t>(m), static_cast<uint32_t>(g), static_cast<uint32_t>(G),     \
                        static_cast<uint32_t>(nch), static_cast<uint32_t>(r), perm, cinfo, lists, goffs,  \
-                       overwrite ? 1 : 0);                                                               \
+                       overwrite ? 1 : 0, zero_vec);                                                     \
   } while (0)
   const bool hw = wvec != nullptr && wscale != 0.f;
   if (W == 32) {  // two chunks per wave per batch

@@ -533,10 +533,13 @@ class _FusedHead(torch.autograd.Function):
         ctx.save_for_backward(gunit, pooled, codes)
         ctx.weight, ctx.scale, ctx.hw = weight, float(scale), (x.shape[2], x.shape[3])
         ctx.mark_non_differentiable(correct)
+        ctx.set_materialize_grads(False)  # no zeros fill for the unused gradient of `correct`
         return loss, correct
 
     @staticmethod
     def backward(ctx, gl, gc):
+        if gl is None:  # (grads are not materialised) the loss got no gradient
+            return None, None, None, None
         gunit, pooled, codes = ctx.saved_tensors
         w = ctx.weight
         gr = w.grad

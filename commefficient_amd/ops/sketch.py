@@ -138,23 +138,25 @@ class CSVec:
 
     def accumulateVec(self, vec: torch.Tensor, scale: float = 1.0,
                       wvec: Optional[torch.Tensor] = None, wscale: float = 0.0,
-                      dense: bool = True, overwrite: bool = False):
+                      dense: bool = True, overwrite: bool = False, zero_vec: bool = False) -> bool:
         """table += S(scale*vec + wscale*wvec) (``overwrite``: table = S(...),
         no separate zeroing pass on the planned path).  ``dense=False`` uses
-        the direct-atomic kernel (best for sparse vectors)."""
+        the direct-atomic kernel (best for sparse vectors).  ``zero_vec``: the
+        region GPU encode may clear vec behind its reads; returns True if it
+        did (the caller then skips its own zeroing of vec)."""
         assert vec.numel() == self.d, (vec.numel(), self.d)
         if self.region is not None:
-            _rg().encode(self.region, self.table, vec, scale, wvec, wscale, overwrite)
-            return
+            return _rg().encode(self.region, self.table, vec, scale, wvec, wscale, overwrite, zero_vec)
         if dense and self._use_plan():
             ops().cs_encode_planned(self.table, vec.reshape(-1), float(scale), wvec,
                                     float(wscale), self.c, self._plan(), bool(overwrite))
-            return
+            return False
         if overwrite:
             self.table.zero_()
         layout = self._binned_layout() if (dense and self.kernel != "direct") else []
         ops().cs_encode(self.table, vec.reshape(-1), self.hashes, self.blk_off, self.blk_sign,
                         self.numBlocks, float(scale), wvec, float(wscale), layout)
+        return False
 
     def accumulateTable(self, table: torch.Tensor):
         self.table.add_(table.view(self.r, self.c))

@@ -141,15 +141,19 @@ class RegionHash:
 
 
 def encode(h: RegionHash, table: torch.Tensor, vec: torch.Tensor, scale: float = 1.0,
-           wvec: Optional[torch.Tensor] = None, wscale: float = 0.0, overwrite: bool = False):
-    """table (+)= S(scale*vec + wscale*wvec)."""
+           wvec: Optional[torch.Tensor] = None, wscale: float = 0.0, overwrite: bool = False,
+           zero_vec: bool = False) -> bool:
+    """table (+)= S(scale*vec + wscale*wvec).  ``zero_vec``: also clear vec
+    (the GPU encode reads every element once and stores a zero behind it --
+    no separate fill kernel for the next accumulation); returns whether it did."""
     v = vec.reshape(-1)
     if table.is_cuda:
         t = h.tensors(table.device)
+        zero_vec = bool(zero_vec) and v.data_ptr() == vec.data_ptr() and v.is_contiguous()
         ops().cs_region_encode(table, v, float(scale), wvec.reshape(-1) if wvec is not None else None,
                                float(wscale), h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
-                               t["goffs"], bool(overwrite))
-        return
+                               t["goffs"], bool(overwrite), zero_vec)
+        return zero_vec
     x = v.float() * scale
     if wvec is not None and wscale != 0.0:
         x = x + wscale * wvec.reshape(-1).float()
@@ -159,6 +163,7 @@ def encode(h: RegionHash, table: torch.Tensor, vec: torch.Tensor, scale: float =
     tv = table.view(h.r, h.c)
     for j in range(h.r):
         tv[j].index_add_(0, b[j], s[j] * x)
+    return False
 
 
 def query(h: RegionHash, table: torch.Tensor, q0: int = 0, q1: int = -1) -> torch.Tensor:

@@ -482,8 +482,12 @@ class FedModel:
         wscale = a.weight_decay / a.num_workers * n_local
         if a.mode == "sketch":
             sk = self.sketch.like(out.view(a.num_rows, a.num_cols))
-            sk.accumulateVec(self.flat.g, 1.0, self.w if wscale != 0 else None, wscale,
-                             dense=a.encode != "direct", overwrite=True)
+            # the encode is the flat gradient's last reader this round: the
+            # region kernel clears it behind its reads (the next zero_grad
+            # then skips its fill)
+            self.flat.g_zeroed = sk.accumulateVec(self.flat.g, 1.0, self.w if wscale != 0 else None,
+                                                  wscale, dense=a.encode != "direct", overwrite=True,
+                                                  zero_vec=True)
         else:
             # fedavg (single local step): sum_i (w - (w - lr g_i)) n_i = lr * transmit
             s = self.fedavg_lr if a.mode == "fedavg" else 1.0

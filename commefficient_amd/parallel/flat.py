@@ -44,6 +44,7 @@ class FlatParams:
         self.device = torch.device(device)
         self.w = torch.empty(self.d, dtype=torch.float32, device=self.device)
         self.g = torch.zeros(self.d, dtype=torch.float32, device=self.device)
+        self.g_zeroed = False  # g already all-zero (cleared by the sketch encode)
         with torch.no_grad():
             for p, o, n in zip(self.params, self.offsets, self.numels):
                 self.w[o:o + n].copy_(p.detach().reshape(-1).to(self.device, torch.float32))
@@ -70,7 +71,10 @@ class FlatParams:
             p.grad = self.g[o:o + n].view(s)
 
     def zero_grad(self):
-        self.g.zero_()
+        if self.g_zeroed:
+            self.g_zeroed = False  # the sketch encode already cleared g (fed_model._encode_merged)
+        else:
+            self.g.zero_()
         # autograd may have replaced .grad (e.g. set_to_none elsewhere)
         for p, o, n in zip(self.params, self.offsets, self.numels):
             if p.grad is None or p.grad.data_ptr() != self.g[o:o + n].data_ptr():

@@ -233,3 +233,16 @@ def test_region_fused_topk_matches_query_then_topk():
     ref2 = O.topk_abs(est[lo:hi].contiguous(), k)
     idx, vals = sketch_region.topk(sk.region, sk.table, k, None, qb[1], qb[2])
     assert torch.equal(idx, ref2[0]) and torch.equal(vals, ref2[1])
+
+
+@pytest.mark.gpu
+def test_region_encode_zero_vec_clears_the_vector():
+    d, c, r = 2000003, 500000, 5
+    v = torch.randn(d, device="cuda")
+    w = torch.randn(d, device="cuda")
+    a = CSVec(d, c, r, device="cuda", kernel="region")
+    b = a.like()
+    vv = v.clone()
+    a.accumulateVec(v, 0.5, w, 1e-3, overwrite=True)
+    assert b.accumulateVec(vv, 0.5, w, 1e-3, overwrite=True, zero_vec=True)
+    assert torch.equal(a.table, b.table) and int(vv.count_nonzero()) == 0
