@@ -404,8 +404,8 @@ at::Tensor cs_region_query_hip(const at::Tensor& table, int64_t d, int64_t m, in
   TORCH_CHECK(q0 >= 0 && q0 <= q1 && q1 <= p.nch, "cs_region_query: chunk range out of bounds");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   auto est = at::empty({d}, table.options());
-  launch_cs_region_query(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(p.r), p.c, m, g, p.G,
-                         W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+  launch_cs_region_query(const_cast<float*>(table.data_ptr<float>()), est.data_ptr<float>(), d, static_cast<int>(p.r),
+                         p.c, m, g, p.G, W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                          reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
                          goffs.data_ptr<int32_t>(), q0, q1, cur_stream());
   return est;
@@ -414,12 +414,32 @@ at::Tensor cs_region_query_hip(const at::Tensor& table, int64_t d, int64_t m, in
 // the unsketch of a chunk range in one go: median query fused with the top-k's
 // first histogram, then the remaining top-k passes over est[q0*m, q1*m);
 // returns (idx relative to q0*m, vals)
-std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(const at::Tensor& table, int64_t d, int64_t m, int64_t g,
+// mom_mode 1 / 2 (momV, momG given): the server momentum fused into the
+// query's staging of the table (1: table = E, V = rho V + gscale G, E += V;
+// 2: table = V = rho V + gscale G)
+std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t d, int64_t m, int64_t g,
                                                       int64_t W, const at::Tensor& perm, const at::Tensor& cinfo,
                                                       const at::Tensor& lists, const at::Tensor& goffs, int64_t k,
                                                       const c10::optional<at::Tensor>& hint, int64_t q0,
-                                                      int64_t q1) {
+                                                      int64_t q1, const c10::optional<at::Tensor>& momV,
+                                                      const c10::optional<at::Tensor>& momG, double rho,
+                                                      double gscale, int64_t mom_mode) {
   const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
+  float* mv = nullptr;
+  const float* mg = nullptr;
+  if (mom_mode != 0) {
+    TORCH_CHECK((mom_mode == 1 || mom_mode == 2) && momG.has_value() && momG->defined(),
+                "cs_region_topk: mom_mode 1 / 2 needs momG (and momV for 1)");
+    TORCH_CHECK(momG->sizes() == table.sizes() && momG->scalar_type() == at::kFloat && momG->is_contiguous() &&
+                    momG->device() == table.device(), "cs_region_topk: momG must match the table");
+    mg = momG->data_ptr<float>();
+    if (mom_mode == 1) {
+      TORCH_CHECK(momV.has_value() && momV->defined() && momV->sizes() == table.sizes() &&
+                      momV->scalar_type() == at::kFloat && momV->is_contiguous() && momV->device() == table.device(),
+                  "cs_region_topk: momV must match the table");
+      mv = momV->data_ptr<float>();
+    }
+  }
   if (q1 < 0) q1 = p.nch;
   TORCH_CHECK(q0 >= 0 && q0 < q1 && q1 <= p.nch, "cs_region_topk: chunk range out of bounds");
   const int64_t lo = q0 * m, hi = std::min(d, q1 * m), n = hi - lo;
@@ -440,7 +460,8 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(const at::Tensor& table, i
                          W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                          reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
                          goffs.data_ptr<int32_t>(), q0, q1, cur_stream(), hp,
-                         reinterpret_cast<uint32_t*>(ws.data_ptr()));
+                         reinterpret_cast<uint32_t*>(ws.data_ptr()), mv, mg, static_cast<float>(rho),
+                         static_cast<float>(gscale), static_cast<int>(mom_mode));
   launch_topk_abs_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                        ws.data_ptr(), cur_stream(), hp);
   return {idx, vals};
@@ -2012,8 +2033,9 @@ TORCH_LIBRARY(commeff, m) {
         "bool zero_vec=False) -> ()");
   m.def("cs_region_query(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
         "Tensor goffs, int q0=0, int q1=-1) -> Tensor");
-  m.def("cs_region_topk(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
-        "Tensor goffs, int k, Tensor? hint=None, int q0=0, int q1=-1) -> (Tensor, Tensor)");
+  m.def("cs_region_topk(Tensor(a!) table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
+        "Tensor goffs, int k, Tensor? hint=None, int q0=0, int q1=-1, Tensor(b!)? momV=None, Tensor? momG=None, "
+        "float rho=0.0, float gscale=0.0, int mom_mode=0) -> (Tensor, Tensor)");
   m.def("cs_region_zero(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, int d, int m, int g, "
         "Tensor perm, Tensor cinfo) -> ()");
   m.def("topk_abs(Tensor x, int k, Tensor? hint=None) -> (Tensor, Tensor)");

@@ -36,10 +36,12 @@ momentum_ef_kernel(float4* __restrict__ V, float4* __restrict__ E, const float4*
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n4; i += stride) {
     float4 v = V[i], g = G[i];
-    v.x = rho * v.x + gscale * g.x;
-    v.y = rho * v.y + gscale * g.y;
-    v.z = rho * v.z + gscale * g.z;
-    v.w = rho * v.w + gscale * g.w;
+    // explicit fmaf: the region query's fused momentum (sketch_region.hip)
+    // must round identically
+    v.x = fmaf(rho, v.x, gscale * g.x);
+    v.y = fmaf(rho, v.y, gscale * g.y);
+    v.z = fmaf(rho, v.z, gscale * g.z);
+    v.w = fmaf(rho, v.w, gscale * g.w);
     V[i] = v;
     if (mode == 1) {
       float4 e = E[i];
@@ -55,7 +57,7 @@ __global__ void momentum_ef_tail(float* V, float* E, const float* G, int64_t sta
                                  float rho, float gscale, int mode) {
   int64_t i = start + blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   if (i >= n) return;
-  float v = rho * V[i] + gscale * G[i];
+  float v = fmaf(rho, V[i], gscale * G[i]);
   V[i] = v;
   if (mode == 1) E[i] += v;
   else if (mode == 2) E[i] = v;

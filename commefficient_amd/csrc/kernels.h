@@ -108,10 +108,15 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
                              hipStream_t stream, float* zero_vec = nullptr);  // zero_vec: vec, cleared
 // est[i] for the coordinates of chunks [q0, q1); hist0 != nullptr: also the
 // top-k's first histogram of est (see topk_prepare)
-void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
+// mom_mode 1 / 2: the server momentum on the table first (1: V = rho V +
+// gscale G, table = E += V; 2: table = V = rho V + gscale G), see
+// sketch_region.hip RegionMom
+void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
                             int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
-                            hipStream_t stream, const uint32_t* hint = nullptr, uint32_t* hist0 = nullptr);
+                            hipStream_t stream, const uint32_t* hint = nullptr, uint32_t* hist0 = nullptr,
+                            float* momV = nullptr, const float* momG = nullptr, float rho = 0.f,
+                            float gscale = 0.f, int mom_mode = 0);
 void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float* vals, int64_t k,
                            int64_t d, int r, int64_t c, int64_t m, int64_t nch, const uint32_t* perm,
                            const uint32_t* cinfo, hipStream_t stream);

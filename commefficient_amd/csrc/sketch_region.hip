@@ -194,14 +194,27 @@ __device__ __forceinline__ float lower_median(float (&v)[kMaxRows], int r) {
 // HIST: also the top-k's first histogram of the estimates (csrc/topk.hip
 // pass 0: keys = bits & 0x7fffffff >= hint[0], bin = key >> 20) -- LDS
 // privatised, non-empty bins added to hist0: integer counts, deterministic
+// Server momentum fused into the staging (MOM, csrc/elementwise.hip
+// momentum_ef semantics on this group's regions, which no other block
+// touches): 1 = virtual error feedback, V = rho V + gscale G, E += V, the
+// query reads E (= table); 2 = V = rho V + gscale G, the query reads V (=
+// table).  The regions of every group are staged (and updated) even when the
+// query covers only a chunk range; the unused tail buckets stay zero.
+struct RegionMom {
+  float* V;
+  const float* G;
+  float rho, gscale;
+  int mode;
+};
+
 template <int RT, bool HIST>
 __global__ void __launch_bounds__(1024)
-cs_region_query_kernel(const float* __restrict__ table, float* __restrict__ est, uint32_t d,
+cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint32_t d,
                        uint32_t c, uint32_t m, uint32_t g, uint32_t nch, uint32_t r_rt,
                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
                        const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
                        uint32_t q0, uint32_t q1, int vec4, const uint32_t* __restrict__ hint,
-                       uint32_t* __restrict__ hist0) {
+                       uint32_t* __restrict__ hist0, RegionMom mom) {
   __shared__ uint32_t hh[HIST ? 2048 : 1];
   if constexpr (HIST)
     for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) hh[b] = 0u;
@@ -212,13 +225,45 @@ cs_region_query_kernel(const float* __restrict__ table, float* __restrict__ est,
   const uint32_t grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t W = blockDim.x >> 6, gm = g * m, rbase = grp * g;
   for (uint32_t j = 0; j < r; ++j) {
-    const float* src = table + static_cast<size_t>(j) * c + static_cast<size_t>(grp) * gm;
+    const size_t o = static_cast<size_t>(j) * c + static_cast<size_t>(grp) * gm;
+    float* src = table + o;
     float* dst = reg + j * gm;
     if (vec4) {
-      for (uint32_t e = tid; e < (gm >> 2); e += blockDim.x)
-        reinterpret_cast<float4*>(dst)[e] = reinterpret_cast<const float4*>(src)[e];
+      for (uint32_t e = tid; e < (gm >> 2); e += blockDim.x) {
+        float4 t = reinterpret_cast<const float4*>(src)[e];
+        if (mom.mode != 0) {
+          const float4 gg = reinterpret_cast<const float4*>(mom.G + o)[e];
+          float4 v = mom.mode == 1 ? reinterpret_cast<const float4*>(mom.V + o)[e] : t;
+          // (explicit fmaf, as in momentum_ef: identical rounding)
+          v.x = fmaf(mom.rho, v.x, mom.gscale * gg.x);
+          v.y = fmaf(mom.rho, v.y, mom.gscale * gg.y);
+          v.z = fmaf(mom.rho, v.z, mom.gscale * gg.z);
+          v.w = fmaf(mom.rho, v.w, mom.gscale * gg.w);
+          if (mom.mode == 1) {
+            reinterpret_cast<float4*>(mom.V + o)[e] = v;
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+          } else {
+            t = v;
+          }
+          reinterpret_cast<float4*>(src)[e] = t;
+        }
+        reinterpret_cast<float4*>(dst)[e] = t;
+      }
     } else {
-      for (uint32_t e = tid; e < gm; e += blockDim.x) dst[e] = src[e];
+      for (uint32_t e = tid; e < gm; e += blockDim.x) {
+        float t = src[e];
+        if (mom.mode != 0) {
+          float v = fmaf(mom.rho, mom.mode == 1 ? mom.V[o + e] : t, mom.gscale * mom.G[o + e]);
+          if (mom.mode == 1) {
+            mom.V[o + e] = v;
+            t += v;
+          } else {
+            t = v;
+          }
+          src[e] = t;
+        }
+        dst[e] = t;
+      }
     }
   }
   uint32_t pw[NR];
@@ -359,10 +404,12 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
 #undef COMMEFF_REGION_ENC
 }
 
-void launch_cs_region_query(const float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
+void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
                             int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
-                            hipStream_t stream, const uint32_t* hint, uint32_t* hist0) {
+                            hipStream_t stream, const uint32_t* hint, uint32_t* hist0, float* momV,
+                            const float* momG, float rho, float gscale, int mom_mode) {
+  const RegionMom mom{momV, momG, rho, gscale, mom_mode};
   if (q1 <= q0) return;
   const int lds = static_cast<int>(r * g * m * 4);
   const int vec4 = ((g * m) % 4 == 0 && c % 4 == 0) ? 1 : 0;
@@ -375,7 +422,7 @@ void launch_cs_region_query(const float* table, float* est, int64_t d, int r, in
                        static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),     \
                        static_cast<uint32_t>(g), static_cast<uint32_t>(nch), static_cast<uint32_t>(r),   \
                        perm, cinfo, lists, goffs, static_cast<uint32_t>(q0), static_cast<uint32_t>(q1),  \
-                       vec4, hint, hist0);                                                               \
+                       vec4, hint, hist0, mom);                                                          \
   } while (0)
   if (hist0 != nullptr) {
     if (r == 5) COMMEFF_REGION_QRY(5, true);

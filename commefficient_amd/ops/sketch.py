@@ -176,10 +176,14 @@ class CSVec:
         return ops().cs_query(self.table, self.hashes, self.blk_off, self.blk_sign,
                               self.numBlocks, self.d)
 
-    def unsketch_sparse(self, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    def unsketch_sparse(self, k: int, mom=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """``mom = (V, G, rho, gscale, error_type)``: apply the server momentum
+        to the table first (ops.momentum_ef; fused into the query on the GPU
+        region path)."""
         if self.region is not None:
             return _rg().topk(self.region, self.table, int(k),
-                              _topk_hint(("unsketch", self.d, int(k)), self.table.device))
+                              _topk_hint(("unsketch", self.d, int(k)), self.table.device), mom=mom)
+        self._momentum(mom)
         est = self.query()
         return ops().topk_abs(est, int(k), _topk_hint(("unsketch", self.d, int(k)), est.device))
 
@@ -196,7 +200,14 @@ class CSVec:
         chunk, nch = int(geom[2]), int(geom[3])
         return [min(self.d, (nch * q // world) * chunk) for q in range(world + 1)]
 
-    def unsketch_sparse_sharded(self, k: int, rank: int, world: int, all_gather_rows):
+    def _momentum(self, mom):
+        if mom is not None:
+            from . import momentum_ef
+            V, G, rho, gs, et = mom
+            momentum_ef(V.view(-1), self.table.view(-1) if et == "virtual" else None, G.view(-1), rho,
+                        gs, et)
+
+    def unsketch_sparse_sharded(self, k: int, rank: int, world: int, all_gather_rows, mom=None):
         """``unsketch_sparse`` with the median query and the top-k split over
         ``world`` ranks: rank r estimates only its coordinate shard, selects
         the shard's k largest |estimates| (ties -> lower index), the k-lists
@@ -210,11 +221,11 @@ class CSVec:
         k = int(k)
         b = self.shard_bounds(world) if world > 1 else None
         if b is None or min(b[q + 1] - b[q] for q in range(world)) < k:
-            return self.unsketch_sparse(k)
-        pack = self.unsketch_shard(k, rank, world, b)
+            return self.unsketch_sparse(k, mom=mom)
+        pack = self.unsketch_shard(k, rank, world, b, mom=mom)
         return self.merge_shards(all_gather_rows(pack.view(1, 2 * k)), world, k)
 
-    def unsketch_shard(self, k: int, rank: int, world: int, bounds=None) -> torch.Tensor:
+    def unsketch_shard(self, k: int, rank: int, world: int, bounds=None, mom=None) -> torch.Tensor:
         """This rank's candidates: [2, k] int64 = (global indices, fp32 bits of
         the estimates) of its shard's top-k."""
         b = bounds if bounds is not None else self.shard_bounds(world)
@@ -222,8 +233,9 @@ class CSVec:
         hint = _topk_hint(("unsketch_shard", self.d, k, rank, world), self.table.device)
         if self.region is not None:
             qb = self.region.chunk_bounds(world)
-            li, lv = _rg().topk(self.region, self.table, k, hint, qb[rank], qb[rank + 1])
+            li, lv = _rg().topk(self.region, self.table, k, hint, qb[rank], qb[rank + 1], mom=mom)
         else:
+            self._momentum(mom)
             nch = int(ops().plan_geometry(self.d, self.r, self.c)[3])
             est = ops().cs_query_planned(self.table, self.d, self._plan(), nch * rank // world,
                                          nch * (rank + 1) // world)

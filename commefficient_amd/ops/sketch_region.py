@@ -179,18 +179,37 @@ def query(h: RegionHash, table: torch.Tensor, q0: int = 0, q1: int = -1) -> torc
     return vals.median(dim=0).values
 
 
+MOM_MODE = {"virtual": 1, "none": 2}
+
+
 def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor] = None,
-         q0: int = 0, q1: int = -1):
+         q0: int = 0, q1: int = -1, mom=None):
     """(idx, vals): the k largest-magnitude median estimates of the
     coordinates of chunks [q0, q1) (idx relative to q0*m, ascending; ties ->
     lower index).  GPU: one fused launch sequence -- the query also builds the
-    selection's first histogram (csrc/topk.hip, no extra pass over est)."""
+    selection's first histogram (csrc/topk.hip, no extra pass over est).
+    ``mom = (V, G, rho, gscale, error_type)``: first the server momentum of
+    ops.momentum_ef on the table (error_type "virtual": table is E, V = rho V +
+    gscale G, E += V; "none": table is V = rho V + gscale G), on the GPU
+    inside the query's staging of the table (every region, whatever the range)."""
     q1 = h.nch if q1 < 0 else q1
     lo, hi = q0 * h.m, min(h.d, q1 * h.m)
     if table.is_cuda and 1 <= k < hi - lo:
         t = h.tensors(table.device)
+        mv = mg = None
+        rho = gs = 0.0
+        mode = 0
+        if mom is not None:
+            V, G, rho, gs, et = mom
+            mode = MOM_MODE[et]
+            mv, mg = (V.view(table.shape) if mode == 1 else None), G.view(table.shape)
         return ops().cs_region_topk(table, h.d, h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
-                                    t["goffs"], int(k), hint, int(q0), int(q1))
+                                    t["goffs"], int(k), hint, int(q0), int(q1), mv, mg, float(rho),
+                                    float(gs), mode)
+    if mom is not None:
+        from . import momentum_ef
+        V, G, rho, gs, et = mom
+        momentum_ef(V.view(-1), table.view(-1) if et == "virtual" else None, G.view(-1), rho, gs, et)
     est = query(h, table, q0, q1)
     return ops().topk_abs(est[lo:hi].contiguous(), int(k), hint)
 

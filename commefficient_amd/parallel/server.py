@@ -114,21 +114,20 @@ class ServerState:
         img_sync = weights_begin_update(w)
         if mode == "sketch":
             et = a.error_type
-            if et == "virtual":
-                ops.momentum_ef(self.V.view(-1), self.E.view(-1), G.view(-1), rho, gscale, "virtual")
-                src = self.E
-            else:  # local / none: un-sketch V itself (see module docstring)
-                ops.momentum_ef(self.V.view(-1), None, G.view(-1), rho, gscale, "none")
-                src = self.V
+            virt = et == "virtual"
+            src = self.E if virt else self.V  # local / none: un-sketch V itself (module docstring)
+            # the momentum step (V = rho V + G/B; virtual: E += V) goes with the
+            # unsketch: the region GPU query applies it while staging the table
+            mom = (self.V, G, rho, gscale, "virtual" if virt else "none")
             sk = self.sketch.like(src)
             ctx = dist.ctx()
             if ctx.world_size > 1 and getattr(a, "shard_unsketch", "on") == "on":
                 # every rank estimates 1/N of the coordinates and the k-lists
                 # are merged (bitwise the replicated result, ops/sketch.py)
                 idx, vals = sk.unsketch_sparse_sharded(a.k, ctx.rank, ctx.world_size,
-                                                       dist.all_gather_rows)
+                                                       dist.all_gather_rows, mom=mom)
             else:
-                idx, vals = sk.unsketch_sparse(a.k)
+                idx, vals = sk.unsketch_sparse(a.k, mom=mom)
             # error feedback (virtual) + momentum-factor masking in sketch space
             sk.zero_heavy_hitters(idx, vals, self.V if et == "virtual" else None)
             ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)

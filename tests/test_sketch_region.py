@@ -246,3 +246,27 @@ def test_region_encode_zero_vec_clears_the_vector():
     a.accumulateVec(v, 0.5, w, 1e-3, overwrite=True)
     assert b.accumulateVec(vv, 0.5, w, 1e-3, overwrite=True, zero_vec=True)
     assert torch.equal(a.table, b.table) and int(vv.count_nonzero()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("et", ["virtual", "none"])
+def test_region_fused_momentum_matches_separate(et):
+    # the server momentum applied inside the query's staging == momentum_ef
+    # then the unsketch: selection, V and E bitwise, also for a chunk range
+    # (the momentum still covers every region)
+    from commefficient_amd import ops as O
+    d, c, r, k = 6568640, 500000, 5, 50000
+    base = CSVec(d, c, r, device="cuda", kernel="region")
+    torch.manual_seed(5)
+    V0, E0, G = (torch.randn(r, c, device="cuda") for _ in range(3))
+    for q0, q1 in ((0, -1), tuple(base.region.chunk_bounds(3)[1:3])):
+        V1, E1 = V0.clone(), E0.clone()
+        O.momentum_ef(V1.view(-1), E1.view(-1) if et == "virtual" else None, G.view(-1), 0.9, 0.01, et)
+        src1 = E1 if et == "virtual" else V1
+        ref = sketch_region.topk(base.region, src1, k, None, q0, q1)
+        V2, E2 = V0.clone(), E0.clone()
+        src2 = E2 if et == "virtual" else V2
+        got = sketch_region.topk(base.region, src2, k, None, q0, q1, mom=(V2, G, 0.9, 0.01, et))
+        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+        m = base.region.G * base.region.g * base.region.m  # the unused tail is never touched
+        assert torch.equal(V2[:, :m], V1[:, :m]) and torch.equal(E2[:, :m], E1[:, :m])
