@@ -1,7 +1,10 @@
 """Round loaders for the PersonaChat datasets: the host builds token records
 only for the rows this rank computes, pads them to the selection's max length
-and ships one pinned H2D copy (non_blocking) per tensor."""
+and ships the round's int64 tensors in ONE pinned H2D copy (non_blocking),
+split into views on the device."""
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -12,8 +15,20 @@ from .fed_persona import collate, label_positions
 
 
 def _to_dev(ts, device):
+    """Host tensors -> device tensors of the same shapes: one packed H2D copy
+    when they are all int64 on a GPU (a copy per tensor cost a pinned-ring
+    round trip each at the start of every GPT-2 round, where the GPU waits)."""
     from ..parallel.dist import h2d
-    return [h2d(t, device) if torch.device(device).type == "cuda" else t for t in ts]
+    if torch.device(device).type != "cuda":
+        return list(ts)
+    if not all(t.dtype == torch.int64 for t in ts) or os.environ.get("COMMEFF_PERSONA_PACK") == "0":
+        return [h2d(t, device) for t in ts]
+    flat = h2d(np.concatenate([t.numpy().reshape(-1) for t in ts]), device)
+    out, o = [], 0
+    for t in ts:
+        out.append(flat[o:o + t.numel()].view(t.shape))
+        o += t.numel()
+    return out
 
 
 class PersonaFedLoader:

@@ -130,19 +130,38 @@ def main():
         warnings.showwarning = _show
         warnings.simplefilter("always")
         torch.cuda.set_sync_debug_mode("warn")
+    allocs0 = torch.cuda.memory_stats().get("num_device_alloc", 0)
     t0 = time.perf_counter()
+    host = 0.0  # host time spent enqueueing (the GPU idles when this is the bound)
     for i in range(b.warmup, b.warmup + b.steps):
+        h0 = time.perf_counter()
         out = fed(batches[i])
         fopt.step()
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
     dist.barrier()
     el = dist.max_over_ranks(time.perf_counter() - t0)
+    tp = os.environ.get("COMMEFF_TORCH_PROFILE")
+    if tp:  # 3 more rounds under torch.profiler (host launch vs GPU start: scripts/launch_lag.py)
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for i in range(b.warmup, b.warmup + min(3, b.steps)):
+                fed(batches[i])
+                fopt.step()
+            torch.cuda.synchronize()
+        if ctx.is_main:
+            os.makedirs(tp, exist_ok=True)
+            prof.export_chrome_trace(os.path.join(tp, "trace.json"))
     ex = sum(n_ex[b.warmup:])
     if ctx.is_main:
         print(json.dumps({"config": b.config, "n_gpus": N, "value": round(ex / el, 1),
                           "unit": unit, "ms_per_round": round(el / b.steps * 1e3, 2),
                           "clients_per_round": W, "examples_per_round": ex / b.steps,
                           "grad_size": fed.d, "loss_last": float(out[0].mean().item()),
+                          "host_ms_per_round": round(host / b.steps * 1e3, 2),
+                          # device allocations (hipMalloc) inside the timed rounds: each
+                          # can synchronise the device
+                          "device_allocs": torch.cuda.memory_stats().get("num_device_alloc", 0) - allocs0,
                           "dtype": args.dtype, "data": "synthetic",
                           "extra_flags": [x for x in b.extra if x != "--"]}), flush=True)
     dist.shutdown()

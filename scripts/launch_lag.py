@@ -16,6 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--marker", default="enc_p1")
+    ap.add_argument("--quiet", action="store_true", help="summary lines only")
     args = ap.parse_args()
     ev = json.load(open(args.trace))["traceEvents"]
     launches, kernels = {}, []
@@ -35,7 +36,8 @@ def main():
         return
     a, b = starts[-2], starts[-1]
     t0 = kernels[a]["ts"]
-    print("# gpu_t(us)  host_t(us)  lag(us)  dur(us)  kernel  <- runtime call")
+    if not args.quiet:
+        print("# gpu_t(us)  host_t(us)  lag(us)  dur(us)  kernel  <- runtime call")
     lags = []
     for k in kernels[a:b]:
         l = launches.get(k["args"]["correlation"])
@@ -43,9 +45,24 @@ def main():
             continue
         lag = k["ts"] - (l["ts"] + l.get("dur", 0))
         lags.append(lag)
-        print("%9.1f %10.1f %8.1f %8.1f  %-60s <- %s" % (k["ts"] - t0, l["ts"] - t0, lag, k.get("dur", 0),
-                                                      k["name"][:60], l["name"]))
+        if not args.quiet:
+            print("%9.1f %10.1f %8.1f %8.1f  %-60s <- %s" % (k["ts"] - t0, l["ts"] - t0, lag, k.get("dur", 0),
+                                                          k["name"][:60], l["name"]))
     print("# kernels %d  min lag %.1f  mean lag %.1f" % (len(lags), min(lags), sum(lags) / len(lags)))
+    # GPU idle stretches of the round (union over streams) with the lag of the
+    # kernel that ended each: lag ~ 0 there = the host had not launched it yet
+    ks = sorted(kernels[a:b], key=lambda k: k["ts"])
+    end, idle, host_idle = ks[0]["ts"], 0.0, 0.0
+    for k in ks:
+        if k["ts"] > end:
+            gap = k["ts"] - end
+            idle += gap
+            l = launches.get(k["args"]["correlation"])
+            if l is not None and k["ts"] - (l["ts"] + l.get("dur", 0)) < 50:
+                host_idle += gap
+        end = max(end, k["ts"] + k.get("dur", 0))
+    print("# round %.1f us, GPU idle %.1f us, of which waiting on a late launch %.1f us"
+          % (end - ks[0]["ts"], idle, host_idle))
 
 
 if __name__ == "__main__":

@@ -1,18 +1,19 @@
 """Deterministic replay: the whole GPU FetchSGD round at the
-headline sketch geometry (5 x 500,000, where the atomic-free planned sketch
-applies) -- native convs with fixed-order split-K reductions, planned encode
-and query, radix-select top-k, fused head/loss -- is a pure function of its
-inputs: two runs from the same seed end with bit-identical weights and server
-state.  (Geometries the plan does not fit, e.g. GPT-2's, fall back to the
-binned encode whose LDS float atomics are not bitwise reproducible run to run;
-ranks still agree, since every rank applies the same all-reduced table.)"""
+headline sketch geometry (5 x 500,000) -- native convs with fixed-order split-K
+reductions, the region sketch (default; no atomics, any geometry incl. GPT-2's:
+tests/test_sketch_region.py) or the planned csvec-layout sketch, radix-select
+top-k, fused head/loss -- is a pure function of its inputs: two runs from the
+same seed end with bit-identical weights and server state.  (The csvec
+layout's binned fallback uses LDS float atomics and is not bitwise
+reproducible run to run; ranks still agree, since every rank applies the same
+all-reduced table.)"""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-def _run(rounds: int):
+def _run(rounds: int, encode: str):
     from commefficient_amd import models
     from commefficient_amd.data import make_synthetic
     from commefficient_amd.data.device_loader import DeviceFedLoader
@@ -27,7 +28,7 @@ def _run(rounds: int):
                             "--virtual_momentum", "0.9", "--k", "50000", "--num_rows", "5",
                             "--num_cols", "500000", "--num_clients", "80", "--num_workers", "16",
                             "--local_batch_size", "-1", "--weight_decay", "5e-4",
-                            "--device", "cuda"], probe_port=False)
+                            "--device", "cuda", "--encode", encode], probe_port=False)
     torch.manual_seed(0)
     ds = make_synthetic("CIFAR10", train=True, num_clients=80, size=800, seed=1)
     loader = DeviceFedLoader(ds, 16, -1, "cuda", seed=2, augment=True, out_bf16=True)
@@ -39,13 +40,17 @@ def _run(rounds: int):
         fed(next(it))
         opt.step()
     torch.cuda.synchronize()
-    assert fed.sketch._use_plan(), "expected the planned (atomic-free) sketch kernels"
+    if encode == "region":
+        assert fed.sketch.region is not None, "expected the region sketch kernels"
+    else:
+        assert fed.sketch._use_plan(), "expected the planned (atomic-free) sketch kernels"
     return fed.w.clone(), fed.server.V.clone(), fed.server.E.clone()
 
 
-def test_fetchsgd_rounds_replay_bitwise():
-    a = _run(3)
-    b = _run(3)
+@pytest.mark.parametrize("encode", ["region", "planned"])
+def test_fetchsgd_rounds_replay_bitwise(encode):
+    a = _run(3, encode)
+    b = _run(3, encode)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     assert torch.isfinite(a[0]).all()
