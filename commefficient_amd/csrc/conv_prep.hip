@@ -78,7 +78,45 @@ __device__ __forceinline__ void prep_load_b(const ConvPrepArgs& a, int tile, int
   }
 }
 
-__global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
+// The same B fragments as raw loads: every tap loaded unconditionally from a
+// clamped in-range pixel, validity kept as bits (bit 2s+h: tap 4s+2hi+h) and
+// applied by prep_finish_b just before the MFMAs -- a load under a branch is
+// waited for inside it, which had serialised the "in flight" next tile
+struct PrepRawB {
+  v2u t[3][2];
+  uint32_t ok;
+};
+__device__ __forceinline__ void prep_load_b_raw(const ConvPrepArgs& a, int tile, int lr, int hi, PrepRawB& rb) {
+  const PrepPix x = prep_pix(a, tile * 32 + lr);
+  rb.ok = 0u;
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int tap = 4 * s + 2 * hi + h;
+      const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+      const bool ok = tap < 9 && x.valid && static_cast<unsigned>(x.h + dr) < static_cast<unsigned>(a.H) &&
+                      static_cast<unsigned>(x.w + ds) < static_cast<unsigned>(a.W);
+      const int src = ok ? x.p + dr * a.W + ds : x.p;
+      rb.t[s][h] = *reinterpret_cast<const v2u*>(a.x + static_cast<size_t>(src) * 4);
+      rb.ok |= (ok ? 1u : 0u) << (2 * s + h);
+    }
+}
+__device__ __forceinline__ void prep_finish_b(const ConvPrepArgs& a, const PrepRawB& rb, bf16x8_t (&b)[3]) {
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    v2u t0 = ((rb.ok >> (2 * s)) & 1u) ? rb.t[s][0] : v2u{0u, 0u};
+    v2u t1 = ((rb.ok >> (2 * s + 1)) & 1u) ? rb.t[s][1] : v2u{0u, 0u};
+    if (a.Cin <= 3) {
+      t0[1] &= 0xffffu;
+      t1[1] &= 0xffffu;
+    }
+    const v4u v = {t0[0], t0[1], t1[0], t1[1]};
+    b[s] = __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) prep_fwd_kernel(ConvPrepArgs a) {
   // weight fragments (row m = 32 mt + lr, GEMM k = 16 s + 8 hi + j -> tap k/4,
   // channel k%4), built once per block in LDS
   __shared__ bf16x8_t wsm[2][3][64];
@@ -86,14 +124,24 @@ __global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
   // (16-byte aligned, 2-way bank aliasing for the 8-byte fragment writes)
   constexpr int kPitch = 144;
   __shared__ __attribute__((aligned(16))) unsigned char ysm[4][32 * kPitch];
-  for (int e = threadIdx.x; e < 2 * 3 * 64 * 8; e += 256) {
+  // all 12 loads of a thread in flight together (unrolled, unconditional at a
+  // clamped index): a per-element load-wait loop here was a serial prologue
+  // of ~12 memory latencies per block
+  float wv[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int e = threadIdx.x + 256 * i;
     const int j = e & 7, ln = (e >> 3) & 63, ms = e >> 9;  // ms = mt*3 + s
     const int mt = ms / 3, s = ms - 3 * mt;
     const int kk = 16 * s + 8 * (ln >> 5) + j, tap = kk >> 2, c = kk & 3;
     const int m = 32 * mt + (ln & 31);
-    reinterpret_cast<__bf16*>(&wsm[0][0][0])[e] =
-        static_cast<__bf16>((tap < 9 && c < a.Cin) ? a.w[(m * a.Cin + c) * 9 + tap] : 0.f);
+    const bool ok = tap < 9 && c < a.Cin;
+    wv[i] = a.w[ok ? (m * a.Cin + c) * 9 + tap : 0];
+    wv[i] = ok ? wv[i] : 0.f;
   }
+#pragma unroll
+  for (int i = 0; i < 12; ++i)
+    reinterpret_cast<__bf16*>(&wsm[0][0][0])[threadIdx.x + 256 * i] = static_cast<__bf16>(wv[i]);
   __syncthreads();
   const int lane = threadIdx.x & 63, lr = lane & 31, hi = lane >> 5;
   bf16x8_t wa[2][3];
@@ -105,12 +153,14 @@ __global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
   const int nwaves = (gridDim.x * 256) >> 6;
   int tile = (blockIdx.x * 256 + threadIdx.x) >> 6;
   if (tile >= ntiles) return;
-  bf16x8_t b[3];
-  prep_load_b(a, tile, lr, hi, b);
-  while (true) {
-    const int next = tile + nwaves;
-    bf16x8_t bn[3];
-    if (next < ntiles) prep_load_b(a, next, lr, hi, bn);  // in flight during this tile's work
+  // the next tile's loads in flight during this tile's work (measured: two
+  // tiles ahead was no faster); past the end they re-read the current tile
+  unsigned char* ys = ysm[threadIdx.x >> 6];
+  auto body = [&](PrepRawB& rb, int t) {
+    bf16x8_t b[3];
+    prep_finish_b(a, rb, b);
+    const int ahead = t + nwaves;
+    prep_load_b_raw(a, ahead < ntiles ? ahead : t, lr, hi, rb);
     f32x16_t acc[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -120,11 +170,10 @@ __global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
       for (int s = 0; s < 3; ++s)
         acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[mt][s], b[s], acc[mt], 0, 0, 0);
     }
-    const int p = tile * 32 + lr;
+    const int p = t * 32 + lr;
     // lane (pixel p, hi) holds channels 32 mt + 8 g + 4 hi + (0..3) in
     // acc[mt][4 g ..]: ReLU + bf16 into the wave's LDS rows, then whole
     // 128-byte output rows leave with 16-byte stores (8 rows per instruction)
-    unsigned char* ys = ysm[threadIdx.x >> 6];
     uint32_t mbits = 0;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -146,14 +195,17 @@ __global__ void __launch_bounds__(256) prep_fwd_kernel(ConvPrepArgs a) {
     for (int q = 0; q < 4; ++q) {
       const int c = q * 64 + lane, row = c >> 3, col = c & 7;
       const v4u o = *reinterpret_cast<const v4u*>(ys + row * kPitch + col * 16);
-      if (tile * 32 + row < a.P)
-        *reinterpret_cast<v4u*>(a.y + static_cast<size_t>(tile * 32 + row) * kPrepK + col * 8) = o;
+      if (t * 32 + row < a.P)
+        *reinterpret_cast<v4u*>(a.y + static_cast<size_t>(t * 32 + row) * kPrepK + col * 8) = o;
     }
     __builtin_amdgcn_wave_barrier();  // rows read before the next tile overwrites them
-    if (next >= ntiles) break;
-    tile = next;
-#pragma unroll
-    for (int s = 0; s < 3; ++s) b[s] = bn[s];
+  };
+  PrepRawB rb;
+  prep_load_b_raw(a, tile, lr, hi, rb);
+  while (true) {
+    body(rb, tile);
+    tile += nwaves;
+    if (tile >= ntiles) break;
   }
 }
 
@@ -320,7 +372,7 @@ void launch_conv_prep_fwd(ConvPrepArgs a, hipStream_t stream) {
   const int ntiles = (a.P + 31) / 32;
   static const int tpw = [] {  // tiles per wave (weights are set up once per block); tuning knob
     const char* e = std::getenv("COMMEFF_PREP_TPW");
-    const int v = e != nullptr ? std::atoi(e) : 8;
+    const int v = e != nullptr ? std::atoi(e) : 4;  // scripts/bench_prep.py sweep: 4 best
     return v < 1 ? 1 : v;
   }();
   int blocks = (ntiles + 4 * tpw - 1) / (4 * tpw);
