@@ -45,6 +45,8 @@ def main():
                    help="sketch hash family / kernels (utils/args.py --encode)")
     p.add_argument("--conv", default="native", choices=["native", "miopen"],
                    help="3x3 conv units on the native MFMA kernels or on MIOpen")
+    p.add_argument("--wgrad-stream", default="on", choices=["on", "off"],
+                   help="weight gradients on a side stream (utils/args.py --wgrad_stream)")
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
     p.add_argument("--torch-profile", default=None,
                    help="after the timed steps, trace 5 more with torch.profiler into this dir")
@@ -79,7 +81,7 @@ def main():
             "--num_blocks", "20", "--num_clients", str(b.num_clients), "--num_workers", str(W),
             "--local_batch_size", "-1", "--weight_decay", "5e-4", "--dtype", "bf16",
             "--device", "cuda", "--encode", b.encode, "--seed", "21",
-            "--miopen_find", str(b.miopen_find), "--conv", b.conv]
+            "--miopen_find", str(b.miopen_find), "--conv", b.conv, "--wgrad_stream", b.wgrad_stream]
     if b.profile:
         argv += ["--profile_dir", "gpurun_out/bench_profile"]
     args = parse_args(argv=argv, probe_port=False)
