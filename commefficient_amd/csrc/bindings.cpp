@@ -9,6 +9,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -451,19 +452,45 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
     hp = reinterpret_cast<uint32_t*>(hint->data_ptr<int32_t>());
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
+  // candidate-list top-k (COMMEFF_TOPK_CAND=0: the full-vector passes)
+  static const bool cand_on = [] {
+    const char* e = std::getenv("COMMEFF_TOPK_CAND");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  const bool cand = cand_on && m == 64 && topk_cand_supported(n);
   auto est = at::empty({d}, table.options());
-  auto ws = at::empty({topk_workspace_bytes(n)}, table.options().dtype(at::kByte));
+  auto ws = at::empty({cand ? topk_cand_workspace_bytes(n) : topk_workspace_bytes(n)},
+                      table.options().dtype(at::kByte));
   auto idx = at::empty({k}, table.options().dtype(at::kLong));
   auto vals = at::empty({k}, table.options());
-  topk_prepare(ws.data_ptr(), cur_stream());
+  uint64_t* ballots = nullptr;
+  uint32_t* seg = nullptr;
+  if (cand) {
+    topk_cand_prepare(ws.data_ptr(), cur_stream());
+    topk_cand_ptrs(ws.data_ptr(), n, &ballots, &seg);
+  } else {
+    topk_prepare(ws.data_ptr(), cur_stream());
+  }
   launch_cs_region_query(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(p.r), p.c, m, g, p.G,
                          W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                          reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
                          goffs.data_ptr<int32_t>(), q0, q1, cur_stream(), hp,
                          reinterpret_cast<uint32_t*>(ws.data_ptr()), mv, mg, static_cast<float>(rho),
-                         static_cast<float>(gscale), static_cast<int>(mom_mode));
-  launch_topk_abs_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
-                       ws.data_ptr(), cur_stream(), hp);
+                         static_cast<float>(gscale), static_cast<int>(mom_mode), ballots, seg);
+  if (cand) {
+    launch_topk_cand_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                          ws.data_ptr(), cur_stream(), hp);
+    static const bool stats = std::getenv("COMMEFF_TOPK_CAND_STATS") != nullptr;  // debug: host sync
+    if (stats) {
+      const int64_t off = (4 * 2048 * 4 + 2 * 4096 * 4 + 2048 * 4) / 4;
+      auto ctl = ws.view(at::kInt).slice(0, off, off + 2).cpu();
+      fprintf(stderr, "[topk_cand] n=%lld k=%lld use=%d M=%d\n", static_cast<long long>(n),
+              static_cast<long long>(k), ctl[0].item<int>(), ctl[1].item<int>());
+    }
+  }
+  else
+    launch_topk_abs_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                         ws.data_ptr(), cur_stream(), hp);
   return {idx, vals};
 }
 

@@ -116,7 +116,8 @@ void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t 
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
                             hipStream_t stream, const uint32_t* hint = nullptr, uint32_t* hist0 = nullptr,
                             float* momV = nullptr, const float* momG = nullptr, float rho = 0.f,
-                            float gscale = 0.f, int mom_mode = 0);
+                            float gscale = 0.f, int mom_mode = 0, uint64_t* ballots = nullptr,
+                            uint32_t* segtot = nullptr);
 void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float* vals, int64_t k,
                            int64_t d, int r, int64_t c, int64_t m, int64_t nch, const uint32_t* perm,
                            const uint32_t* cinfo, hipStream_t stream);
@@ -141,6 +142,16 @@ void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx,
 void topk_prepare(void* workspace, hipStream_t stream);
 void launch_topk_abs_rest(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,
                           void* workspace, hipStream_t stream, uint32_t* hint);
+// candidate-list variant (csrc/topk.hip cand_compact_kernel): the producer of
+// hist[0] also writes the per-64-element-chunk masks of keys >= hint and the
+// per-segment popcounts (topk_cand_ptrs); topk_cand_prepare zeroes the
+// histograms and segment totals.  Same result as launch_topk_abs_rest.
+bool topk_cand_supported(int64_t n);
+int64_t topk_cand_workspace_bytes(int64_t n);
+void topk_cand_prepare(void* workspace, hipStream_t stream);
+void topk_cand_ptrs(void* workspace, int64_t n, uint64_t** ballots, uint32_t** seg);
+void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals, void* workspace,
+                           hipStream_t stream, uint32_t* hint);
 
 // ----------------------------------------------------------- elementwise --
 // V = rho*V + gscale*G ; mode 1: E += V ; mode 2: E = V

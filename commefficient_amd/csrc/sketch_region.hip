@@ -214,10 +214,18 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
                        const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
                        uint32_t q0, uint32_t q1, int vec4, const uint32_t* __restrict__ hint,
-                       uint32_t* __restrict__ hist0, RegionMom mom) {
+                       uint32_t* __restrict__ hist0, RegionMom mom, uint64_t* __restrict__ ballots,
+                       uint32_t* __restrict__ segtot) {
+  // ballots (m == 64): per chunk of est the mask of keys >= hint, and the
+  // per-segment (1,024 chunks) popcount totals: the top-k's candidate list
+  // (csrc/topk.hip cand_compact_kernel)
   __shared__ uint32_t hh[HIST ? 2048 : 1];
+  __shared__ uint32_t sh[HIST ? 2048 : 1];
   if constexpr (HIST)
-    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) hh[b] = 0u;
+    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) {
+      hh[b] = 0u;
+      sh[b] = 0u;
+    }
   const uint32_t hlb = (HIST && hint != nullptr) ? hint[0] : 0u;
   constexpr int NR = RT > 0 ? RT : kMaxRows;
   extern __shared__ __attribute__((aligned(16))) float reg[];  // [r][g * m]
@@ -302,6 +310,7 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
       uint32_t cw[NR];
 #pragma unroll
       for (int j = 0; j < NR; ++j) cw[j] = j < rr ? __builtin_amdgcn_readlane(word[u], j) : 0u;
+      bool cand = false;
       if (lane < len) {
         float v[kMaxRows];
 #pragma unroll
@@ -316,7 +325,17 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
         est[static_cast<size_t>(q[u]) * m + lane] = e;
         if constexpr (HIST) {
           const uint32_t key = __float_as_uint(e) & 0x7fffffffu;
-          if (key >= hlb) atomicAdd(hh + (key >> 20), 1u);
+          cand = key >= hlb;
+          if (cand) atomicAdd(hh + (key >> 20), 1u);
+        }
+      }
+      if constexpr (HIST) {
+        if (ballots != nullptr) {
+          const uint64_t bal = __ballot(cand);
+          if (lane == 0) {
+            ballots[q[u] - q0] = bal;
+            atomicAdd(sh + ((q[u] - q0) >> 10), static_cast<uint32_t>(__popcll(bal)));
+          }
         }
       }
     }
@@ -328,8 +347,10 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
   }
   if constexpr (HIST) {
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x)
+    for (uint32_t b = threadIdx.x; b < 2048; b += blockDim.x) {
       if (hh[b] != 0u) atomicAdd(hist0 + b, hh[b]);
+      if (ballots != nullptr && sh[b] != 0u) atomicAdd(segtot + b, sh[b]);
+    }
   }
 }
 
@@ -408,8 +429,10 @@ void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t 
                             int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
                             hipStream_t stream, const uint32_t* hint, uint32_t* hist0, float* momV,
-                            const float* momG, float rho, float gscale, int mom_mode) {
+                            const float* momG, float rho, float gscale, int mom_mode, uint64_t* ballots,
+                            uint32_t* segtot) {
   const RegionMom mom{momV, momG, rho, gscale, mom_mode};
+  if (m != 64 || hist0 == nullptr) ballots = nullptr;
   if (q1 <= q0) return;
   const int lds = static_cast<int>(r * g * m * 4);
   const int vec4 = ((g * m) % 4 == 0 && c % 4 == 0) ? 1 : 0;
@@ -422,7 +445,7 @@ void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t 
                        static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),     \
                        static_cast<uint32_t>(g), static_cast<uint32_t>(nch), static_cast<uint32_t>(r),   \
                        perm, cinfo, lists, goffs, static_cast<uint32_t>(q0), static_cast<uint32_t>(q1),  \
-                       vec4, hint, hist0, mom);                                                          \
+                       vec4, hint, hist0, mom, ballots, segtot);                                         \
   } while (0)
   if (hist0 != nullptr) {
     if (r == 5) COMMEFF_REGION_QRY(5, true);

@@ -21,6 +21,7 @@
 //   privatised in LDS; only non-empty bins are flushed with atomics.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include "kernels.h"
 
@@ -143,11 +144,25 @@ __device__ Walk walk(const WS& w, uint32_t k, uint32_t* tot, uint32_t* res) {
 // L's bin then hold exact counts of every key >= L, which is all the top-down
 // walk reads whenever >= k keys are >= L; otherwise the fill-in makes the
 // histogram exact.  Deterministic either way (integer counts).
-template <int PASS>
+// Candidate mode (CAND): the passes read the compacted candidate list of
+// cand_compact_kernel (ctl[0] = 1: values cval[0, ctl[1]), their indices
+// cidx) instead of x[0, n) when the list is in use (see launch_topk_cand_rest)
+struct Cand {
+  const uint32_t* ctl;
+  const float* val;
+  const int32_t* idx;
+};
+
+template <int PASS, bool CAND = false>
 __global__ void __launch_bounds__(256)
-hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk, const uint32_t* __restrict__ hint) {
+hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk, const uint32_t* __restrict__ hint,
+            Cand cd = Cand{}) {
   __shared__ uint32_t h[kBins];
   __shared__ uint32_t tot[4], res[2];
+  if (CAND && cd.ctl[0] != 0u) {
+    x = cd.val;
+    n = cd.ctl[1];
+  }
   for (int b = threadIdx.x; b < kBins; b += blockDim.x) h[b] = 0;
   const uint32_t lb = hint != nullptr ? hint[0] : 0u;
   if constexpr (PASS == 3) {
@@ -213,9 +228,23 @@ hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk, const ui
   }
 }
 
+// candidate mode: a block's span from the device-side length
+__device__ __forceinline__ int64_t cand_span(int64_t n) {
+  const int64_t sp = (n + gridDim.x - 1) / gridDim.x;
+  return ((sp + 1023) / 1024) * 1024;
+}
+
+template <bool CAND = false>
 __global__ void __launch_bounds__(256)
-count_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32_t kk) {
+count_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32_t kk, Cand cd = Cand{}) {
   __shared__ uint32_t tot[4], res[2];
+  if constexpr (CAND) {
+    if (cd.ctl[0] != 0u) {
+      x = cd.val;
+      n = cd.ctl[1];
+    }
+    span = cand_span(n);
+  }
   const uint32_t thr = walk<3>(ws, kk, tot, res).prefix;
   const int64_t i0 = blockIdx.x * span;
   const int64_t i1 = min(n, i0 + span);
@@ -293,16 +322,27 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wt, ui
 // per iteration each thread takes 4 consecutive elements (one 16-byte load),
 // tie ranks and output slots come from two block-wide exclusive scans
 // (elements stay in ascending order)
+template <bool CAND = false>
 __global__ void __launch_bounds__(256)
 write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32_t kk,
-             int64_t* __restrict__ idx, float* __restrict__ vals, uint32_t* __restrict__ hint) {
+             int64_t* __restrict__ idx, float* __restrict__ vals, uint32_t* __restrict__ hint, Cand cd = Cand{},
+             float hint_frac = 0.5f) {
   __shared__ uint32_t tot[4], res[2];
   __shared__ uint32_t wt_eq[4], wt_sel[4];
+  const int32_t* cmap = nullptr;  // candidate -> index (ascending)
+  if constexpr (CAND) {
+    if (cd.ctl[0] != 0u) {
+      x = cd.val;
+      n = cd.ctl[1];
+      cmap = cd.idx;
+    }
+    span = cand_span(n);
+  }
   const Walk wk = walk<3>(ws, kk, tot, res);
   const uint32_t thr = wk.prefix, ties = wk.remaining;
-  // next call's lower bound: half this threshold (finite thresholds only)
+  // next call's lower bound: hint_frac x this threshold (finite thresholds only)
   if (hint != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-    hint[0] = thr < 0x7f800000u ? __float_as_uint(__uint_as_float(thr) * 0.5f) : 0u;
+    hint[0] = thr < 0x7f800000u ? __float_as_uint(__uint_as_float(thr) * hint_frac) : 0u;
   // counts of the blocks before this one
   uint32_t g = 0, e = 0;
   for (int b = threadIdx.x; b < static_cast<int>(blockIdx.x); b += 256) {
@@ -364,7 +404,7 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if ((selm >> t) & 1u) {
-          idx[pos] = i + t;
+          idx[pos] = (CAND && cmap != nullptr) ? static_cast<int64_t>(cmap[i + t]) : i + t;
           vals[pos] = vv[u][t];
           ++pos;
         }
@@ -376,10 +416,183 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
   }
 }
 
+// ---- candidate lists (the region sketch query's top-k) ----
+// The producer of hist[0] (keys >= hint) also writes one 64-bit mask per
+// 64-element chunk of x (bit l: key(x[64 q + l]) >= hint) and the per-segment
+// popcount totals (segments of kSegC chunks, LDS-aggregated integer atomics).
+// cand_compact_kernel then copies the keys >= hint -- for a hint of half the
+// previous threshold a few times k, not n -- into an ascending-index list,
+// and the four radix passes run over that list on 256 blocks: each pass's
+// cost had been its 1,024-block prologue and the n-element stream, not the
+// selection.  Exact fallbacks decided on the device (same result bitwise):
+// fewer than k keys >= hint -> the compaction blocks add the fill-in
+// histogram of the keys < hint (hist[3]) and the passes read x; more than
+// `cap` candidates -> the passes read x.
+constexpr int kSegC = 1024;    // chunks per segment (= compaction block)
+constexpr int kSegMax = 2048;  // segments (n <= 2048 * 65536)
+
+struct CandWS {
+  uint32_t* seg;       // kSegMax popcount totals
+  uint32_t* ctl;       // [0] list in use, [1] its length
+  uint64_t* ballots;   // one mask per chunk
+  int32_t* cidx;       // cap
+  float* cval;         // cap
+};
+
+int64_t cand_cap(int64_t n) {
+  const int64_t c = n / 8;
+  return c < 4096 ? (n < 4096 ? n : 4096) : c;
+}
+
+CandWS carve_cand(void* base, int64_t n) {
+  char* p = reinterpret_cast<char*>(base) + 4 * kBins * 4 + 2 * kNB * 4;
+  CandWS c;
+  c.seg = reinterpret_cast<uint32_t*>(p); p += kSegMax * 4;
+  c.ctl = reinterpret_cast<uint32_t*>(p); p += 16;
+  const int64_t nch = (n + 63) / 64;
+  c.ballots = reinterpret_cast<uint64_t*>(p); p += nch * 8;
+  const int64_t cap = cand_cap(n);
+  c.cidx = reinterpret_cast<int32_t*>(p); p += ((cap * 4 + 15) / 16) * 16;
+  c.cval = reinterpret_cast<float*>(p);
+  return c;
+}
+
+// block = kSub chunks (4,096 elements) of one segment, 256 threads of 16
+// consecutive elements (four 16-byte loads, all in flight at once); a
+// thread's output slot is the candidates before its segment (segment
+// totals), before its sub-range inside the segment (ballot popcounts) and
+// before it inside the block (one scan)
+constexpr int kSub = 64;
+__global__ void __launch_bounds__(256)
+cand_compact_kernel(const float* __restrict__ x, int64_t n, WS ws, CandWS cw, uint32_t kk,
+                    const uint32_t* __restrict__ hint, int64_t cap) {
+  __shared__ uint32_t h[kBins];
+  __shared__ uint32_t wt[4], wt2[4], wt3[4];
+  const int tid = threadIdx.x;
+  const uint32_t lb = hint != nullptr ? hint[0] : 0u;
+  const int nseg = static_cast<int>((n + 64 * kSegC - 1) / (64 * kSegC));
+  const int64_t nch = (n + 63) / 64;
+  const int64_t cb0 = static_cast<int64_t>(blockIdx.x) * kSub;  // first chunk of the block
+  const int seg = static_cast<int>(cb0 / kSegC);
+  const int64_t sc0 = static_cast<int64_t>(seg) * kSegC;        // first chunk of its segment
+  // every block decides the mode from the same integer totals
+  uint32_t ht = 0, mt = 0, mb = 0;
+#pragma unroll
+  for (int q = 0; q < kBins / 256; ++q) ht += ws.hist[0][tid + 256 * q];
+  for (int s2 = tid; s2 < nseg; s2 += 256) {
+    const uint32_t v = cw.seg[s2];
+    mt += v;
+    mb += s2 < seg ? v : 0u;
+  }
+  // chunks of the segment before this block (< kSegC - kSub of them)
+  for (int64_t ch = sc0 + tid; ch < cb0; ch += 256) mb += static_cast<uint32_t>(__popcll(cw.ballots[ch]));
+  uint32_t hist_total, m_total, before;
+  (void)block_excl_scan(ht, wt, hist_total);
+  (void)block_excl_scan(mt, wt2, m_total);
+  (void)block_excl_scan(mb, wt3, before);
+  const bool fill = hist_total < kk;
+  const bool use = !fill && static_cast<int64_t>(m_total) <= cap;
+  if (blockIdx.x == 0 && tid == 0) {
+    cw.ctl[0] = use ? 1u : 0u;
+    cw.ctl[1] = m_total;
+  }
+  if (!fill && !use) return;
+  // this thread's 16 elements (clamped loads; validity applied at use)
+  const int64_t e0 = cb0 * 64 + 16 * tid;
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0;
+  float v[16];
+  if (al) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = min(e0 + 4 * u, n - 4);
+      const float4 q = *reinterpret_cast<const float4*>(x + i);
+      v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) v[t] = x[min(e0 + t, n - 1)];
+  }
+  if (fill) {  // hist[3]: the keys < hint of this block's elements
+    for (int b = tid; b < kBins; b += 256) h[b] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t k = key_of(v[t]);
+      if (e0 + t < n && k < lb) atomicAdd(h + (k >> 20), 1u);
+    }
+    __syncthreads();
+    for (int b = tid; b < kBins; b += 256)
+      if (h[b] != 0u) atomicAdd(ws.hist[3] + b, h[b]);
+    return;
+  }
+  const int64_t ch = cb0 + (tid >> 2);
+  const uint64_t bal = cw.ballots[ch < nch ? ch : nch - 1];
+  const uint32_t bits = (ch < nch) ? static_cast<uint32_t>(bal >> (16 * (tid & 3))) & 0xffffu : 0u;
+  uint32_t blk_tot;
+  uint32_t pos = before + block_excl_scan(static_cast<uint32_t>(__popc(bits)), wt, blk_tot);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    if ((bits >> t) & 1u) {
+      cw.cidx[pos] = static_cast<int32_t>(e0 + t);
+      cw.cval[pos] = v[t];
+      ++pos;
+    }
+  }
+}
+
 }  // namespace
 
 int64_t topk_workspace_bytes(int64_t) {
   return 4 * kBins * 4 + 2 * kNB * 4;
+}
+
+bool topk_cand_supported(int64_t n) {
+  return n >= 64 && n <= static_cast<int64_t>(kSegMax) * 64 * kSegC && n < (int64_t{1} << 31);
+}
+
+int64_t topk_cand_workspace_bytes(int64_t n) {
+  const int64_t cap = cand_cap(n);
+  return 4 * kBins * 4 + 2 * kNB * 4 + kSegMax * 4 + 16 + ((n + 63) / 64) * 8 + ((cap * 4 + 15) / 16) * 16 +
+         cap * 4;
+}
+
+void topk_cand_prepare(void* workspace, hipStream_t stream) {
+  // histograms, block counts and segment totals (contiguous)
+  (void)hipMemsetAsync(workspace, 0, 4 * kBins * 4 + 2 * kNB * 4 + kSegMax * 4, stream);
+}
+
+void topk_cand_ptrs(void* workspace, int64_t n, uint64_t** ballots, uint32_t** seg) {
+  const CandWS c = carve_cand(workspace, n);
+  *ballots = c.ballots;
+  *seg = c.seg;
+}
+
+void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals, void* workspace,
+                           hipStream_t stream, uint32_t* hint) {
+  if (k <= 0 || n <= 0) return;
+  WS w = carve(workspace);
+  const CandWS cw = carve_cand(workspace, n);
+  const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
+  const int nblk = static_cast<int>(((n + 63) / 64 + kSub - 1) / kSub);
+  hipLaunchKernelGGL(cand_compact_kernel, dim3(nblk), dim3(256), 0, stream, x, n, w, cw, kk, hint,
+                     cand_cap(n));
+  const Cand cd{cw.ctl, cw.cval, cw.cidx};
+  constexpr int nb = 256;  // candidate passes (the fallbacks stream x on these too)
+  hipLaunchKernelGGL((hist_kernel<1, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
+  hipLaunchKernelGGL((hist_kernel<2, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
+  hipLaunchKernelGGL(count_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, cd);
+  // the candidate list holds the keys >= hint: a tighter bound than the
+  // full-vector passes' 0.5 (COMMEFF_TOPK_HINT_FRAC; a threshold that drops
+  // below it between calls takes the exact fill-in fallback).  ResNet-9
+  // FetchSGD round (k = 50,000 of 6.57M): 0.5 -> ~815k candidates, 0.75 ->
+  // ~340k, 0.85 -> ~200k, fallbacks only in the first two rounds for all three
+  static const float frac = [] {
+    const char* e = std::getenv("COMMEFF_TOPK_HINT_FRAC");
+    const float f = e != nullptr ? static_cast<float>(std::atof(e)) : 0.85f;
+    return f > 0.f && f < 1.f ? f : 0.85f;
+  }();
+  hipLaunchKernelGGL(write_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, idx, vals,
+                     hint, cd, frac);
 }
 
 void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,
@@ -391,7 +604,7 @@ void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* 
   if (hb > 1024) hb = 1024;
   if (hb < 1) hb = 1;
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
-  hipLaunchKernelGGL(hist_kernel<0>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
+  hipLaunchKernelGGL((hist_kernel<0, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
   launch_topk_abs_rest(x, n, k, idx, vals, workspace, stream, hint);
 }
 
@@ -412,9 +625,9 @@ void launch_topk_abs_rest(const float* x, int64_t n, int64_t k, int64_t* idx, fl
   if (hb < 1) hb = 1;
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
   if (hint != nullptr)
-    hipLaunchKernelGGL(hist_kernel<3>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
-  hipLaunchKernelGGL(hist_kernel<1>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
-  hipLaunchKernelGGL(hist_kernel<2>, dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint);
+    hipLaunchKernelGGL((hist_kernel<3, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
+  hipLaunchKernelGGL((hist_kernel<1, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
+  hipLaunchKernelGGL((hist_kernel<2, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
   // compaction blocks: 1,024 (every block's prologue sums the counts of the
   // blocks before it), up to kNB for very long vectors (>= 32 K elements a
   // block: GPT-2 size 151 -> 128 us for the ordered write pass)
@@ -424,8 +637,9 @@ void launch_topk_abs_rest(const float* x, int64_t n, int64_t k, int64_t* idx, fl
   int64_t span = (n + nb - 1) / nb;
   span = ((span + 1023) / 1024) * 1024;  // write_kernel: 1024 elements per block step
   nb = static_cast<int>((n + span - 1) / span);
-  hipLaunchKernelGGL(count_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk);
-  hipLaunchKernelGGL(write_kernel, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, idx, vals, hint);
+  hipLaunchKernelGGL(count_kernel<false>, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, Cand{});
+  hipLaunchKernelGGL(write_kernel<false>, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, idx, vals, hint,
+                     Cand{});
 }
 
 }  // namespace commeff
