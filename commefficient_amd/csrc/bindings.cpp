@@ -482,7 +482,7 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
                           ws.data_ptr(), cur_stream(), hp);
     static const bool stats = std::getenv("COMMEFF_TOPK_CAND_STATS") != nullptr;  // debug: host sync
     if (stats) {
-      const int64_t off = (4 * 2048 * 4 + 2 * 4096 * 4 + 2048 * 4) / 4;
+      const int64_t off = (4 * 2048 * 4 + 2 * 4096 * 4 + 64 + 2048 * 4) / 4;  // topk.hip carve_cand: ctl
       auto ctl = ws.view(at::kInt).slice(0, off, off + 2).cpu();
       fprintf(stderr, "[topk_cand] n=%lld k=%lld use=%d M=%d\n", static_cast<long long>(n),
               static_cast<long long>(k), ctl[0].item<int>(), ctl[1].item<int>());

@@ -35,6 +35,7 @@ struct WS {
   uint32_t* hist[4];  // kBins each (pass 2 uses 512; [3]: pass-0 fill-in below the hint)
   uint32_t* cnt_gt;   // kNB
   uint32_t* cnt_eq;   // kNB
+  uint32_t* wk;       // 16: the digit walk after pass p (prefix, remaining) at [2p - 2, 2p - 1]
 };
 
 WS carve(void* base) {
@@ -46,6 +47,7 @@ WS carve(void* base) {
   }
   w.cnt_gt = reinterpret_cast<uint32_t*>(p); p += kNB * 4;
   w.cnt_eq = reinterpret_cast<uint32_t*>(p); p += kNB * 4;
+  w.wk = reinterpret_cast<uint32_t*>(p); p += 64;
   return w;
 }
 
@@ -133,6 +135,35 @@ __device__ Walk walk(const WS& w, uint32_t k, uint32_t* tot, uint32_t* res) {
   return s;
 }
 
+// The walk after PASSES selections with the earlier ones taken from ws.wk
+// (written by block 0 of the previous pass -- every block computes the same
+// integers, the stream orders the passes): one select_bin per pass instead
+// of PASSES; block 0 stores this pass's result for the next
+template <int PASSES>
+__device__ Walk walk_cached(const WS& w, uint32_t k, uint32_t* tot, uint32_t* res) {
+  Walk s = {0u, k};
+  if constexpr (PASSES == 1) {
+    const Sel a = select_bin<2048>(w.hist[0], s.remaining, tot, res, w.hist[3]);
+    s.prefix = a.bin;
+    s.remaining -= a.above;
+  } else if constexpr (PASSES == 2) {
+    s = Walk{w.wk[0], w.wk[1]};
+    const Sel a = select_bin<2048>(w.hist[1], s.remaining, tot, res);
+    s.prefix = (s.prefix << 11) | a.bin;
+    s.remaining -= a.above;
+  } else if constexpr (PASSES == 3) {
+    s = Walk{w.wk[2], w.wk[3]};
+    const Sel a = select_bin<512>(w.hist[2], s.remaining, tot, res);
+    s.prefix = (s.prefix << 9) | a.bin;
+    s.remaining -= a.above;
+  }
+  if (PASSES >= 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+    w.wk[2 * PASSES - 2] = s.prefix;
+    w.wk[2 * PASSES - 1] = s.remaining;
+  }
+  return s;
+}
+
 // PASS 0: digit = key >> 20 (11 bits)
 // PASS 1: digit = (key >> 9) & 0x7ff, needs (key >> 20) == prefix
 // PASS 2: digit = key & 0x1ff,         needs (key >> 9)  == prefix
@@ -175,7 +206,7 @@ hist_kernel(const float* __restrict__ x, int64_t n, WS ws, uint32_t kk, const ui
     if (tot[0] + tot[1] + tot[2] + tot[3] >= kk) return;
     __syncthreads();
   }
-  const uint32_t prefix = PASS == 3 ? 0u : walk<PASS>(ws, kk, tot, res).prefix;
+  const uint32_t prefix = PASS == 3 ? 0u : walk_cached<PASS == 3 ? 0 : PASS>(ws, kk, tot, res).prefix;
   __syncthreads();  // h zeroed before any atomic
   // (LDS atomics retire ~0.4 lanes/clk/CU and bound pass 0; per-wave
   // sub-histograms measured no faster, wave-aggregated atomics 4x slower:
@@ -245,7 +276,7 @@ count_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
     }
     span = cand_span(n);
   }
-  const uint32_t thr = walk<3>(ws, kk, tot, res).prefix;
+  const uint32_t thr = walk_cached<3>(ws, kk, tot, res).prefix;
   const int64_t i0 = blockIdx.x * span;
   const int64_t i1 = min(n, i0 + span);
   uint32_t gt = 0, eq = 0;
@@ -338,7 +369,7 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
     }
     span = cand_span(n);
   }
-  const Walk wk = walk<3>(ws, kk, tot, res);
+  const Walk wk = {ws.wk[4], ws.wk[5]};  // count_kernel's walk
   const uint32_t thr = wk.prefix, ties = wk.remaining;
   // next call's lower bound: hint_frac x this threshold (finite thresholds only)
   if (hint != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
@@ -445,7 +476,7 @@ int64_t cand_cap(int64_t n) {
 }
 
 CandWS carve_cand(void* base, int64_t n) {
-  char* p = reinterpret_cast<char*>(base) + 4 * kBins * 4 + 2 * kNB * 4;
+  char* p = reinterpret_cast<char*>(base) + 4 * kBins * 4 + 2 * kNB * 4 + 64;
   CandWS c;
   c.seg = reinterpret_cast<uint32_t*>(p); p += kSegMax * 4;
   c.ctl = reinterpret_cast<uint32_t*>(p); p += 16;
@@ -543,7 +574,7 @@ cand_compact_kernel(const float* __restrict__ x, int64_t n, WS ws, CandWS cw, ui
 }  // namespace
 
 int64_t topk_workspace_bytes(int64_t) {
-  return 4 * kBins * 4 + 2 * kNB * 4;
+  return 4 * kBins * 4 + 2 * kNB * 4 + 64;
 }
 
 bool topk_cand_supported(int64_t n) {
@@ -552,13 +583,13 @@ bool topk_cand_supported(int64_t n) {
 
 int64_t topk_cand_workspace_bytes(int64_t n) {
   const int64_t cap = cand_cap(n);
-  return 4 * kBins * 4 + 2 * kNB * 4 + kSegMax * 4 + 16 + ((n + 63) / 64) * 8 + ((cap * 4 + 15) / 16) * 16 +
+  return 4 * kBins * 4 + 2 * kNB * 4 + 64 + kSegMax * 4 + 16 + ((n + 63) / 64) * 8 + ((cap * 4 + 15) / 16) * 16 +
          cap * 4;
 }
 
 void topk_cand_prepare(void* workspace, hipStream_t stream) {
   // histograms, block counts and segment totals (contiguous)
-  (void)hipMemsetAsync(workspace, 0, 4 * kBins * 4 + 2 * kNB * 4 + kSegMax * 4, stream);
+  (void)hipMemsetAsync(workspace, 0, 4 * kBins * 4 + 2 * kNB * 4 + 64 + kSegMax * 4, stream);
 }
 
 void topk_cand_ptrs(void* workspace, int64_t n, uint64_t** ballots, uint32_t** seg) {
