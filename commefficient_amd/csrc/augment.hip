@@ -45,9 +45,15 @@ __global__ void __launch_bounds__(256)
 augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx, int64_t B,
                int H, int W, int C, int pad, int flip, const float* __restrict__ mean,
                const float* __restrict__ inv_std, uint64_t seed, const int64_t* __restrict__ keys,
-               uint16_t* __restrict__ out, int CS) {
+               uint16_t* __restrict__ out, int CS, const int64_t* __restrict__ targets,
+               int64_t* __restrict__ yout) {
   const int64_t npix = B * H * W;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  // the batch's labels too (one launch fewer than a separate gather)
+  if (targets != nullptr) {
+    const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+    if (t < B) yout[t] = targets[idx[t]];
+  }
   float m[4], s[4];
   for (int ch = 0; ch < C; ++ch) {
     m[ch] = mean[ch];
@@ -84,14 +90,14 @@ augment_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ idx
 void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx, int64_t B, int H, int W,
                             int C, int pad, int flip, const float* mean, const float* inv_std,
                             uint64_t seed, const int64_t* keys, uint16_t* out_bf16,
-                            int out_cstride, hipStream_t stream) {
+                            int out_cstride, hipStream_t stream, const int64_t* targets, int64_t* yout) {
   if (B <= 0) return;
   int64_t npix = B * H * W;
   int64_t blocks = (npix + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(augment_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
                      data, idx, B, H, W, C, pad, flip, mean, inv_std, seed, keys, out_bf16,
-                     out_cstride);
+                     out_cstride, targets, yout);
 }
 
 }  // namespace commeff

@@ -424,7 +424,8 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
                                                       const c10::optional<at::Tensor>& hint, int64_t q0,
                                                       int64_t q1, const c10::optional<at::Tensor>& momV,
                                                       const c10::optional<at::Tensor>& momG, double rho,
-                                                      double gscale, int64_t mom_mode) {
+                                                      double gscale, int64_t mom_mode,
+                                                      const c10::optional<at::Tensor>& ws_keep) {
   const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
   float* mv = nullptr;
   const float* mg = nullptr;
@@ -459,14 +460,22 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
   }();
   const bool cand = cand_on && m == 64 && topk_cand_supported(n);
   auto est = at::empty({d}, table.options());
-  auto ws = at::empty({cand ? topk_cand_workspace_bytes(n) : topk_workspace_bytes(n)},
-                      table.options().dtype(at::kByte));
+  // a caller-kept workspace (zeroed once, see cs_region_topk_ws_bytes) is
+  // left zeroed by the passes: no memset per call
+  const bool keep = cand && ws_keep.has_value() && ws_keep->defined();
+  if (keep)
+    TORCH_CHECK(ws_keep->scalar_type() == at::kByte && ws_keep->is_contiguous() &&
+                    ws_keep->device() == table.device() && ws_keep->numel() >= topk_cand_workspace_bytes(n),
+                "cs_region_topk: ws must be a contiguous uint8 tensor of cs_region_topk_ws_bytes bytes");
+  auto ws = keep ? *ws_keep
+                 : at::empty({cand ? topk_cand_workspace_bytes(n) : topk_workspace_bytes(n)},
+                             table.options().dtype(at::kByte));
   auto idx = at::empty({k}, table.options().dtype(at::kLong));
   auto vals = at::empty({k}, table.options());
   uint64_t* ballots = nullptr;
   uint32_t* seg = nullptr;
   if (cand) {
-    topk_cand_prepare(ws.data_ptr(), cur_stream());
+    if (!keep) topk_cand_prepare(ws.data_ptr(), cur_stream());
     topk_cand_ptrs(ws.data_ptr(), n, &ballots, &seg);
   } else {
     topk_prepare(ws.data_ptr(), cur_stream());
@@ -479,7 +488,7 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
                          static_cast<float>(gscale), static_cast<int>(mom_mode), ballots, seg);
   if (cand) {
     launch_topk_cand_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
-                          ws.data_ptr(), cur_stream(), hp);
+                          ws.data_ptr(), cur_stream(), hp, keep);
     static const bool stats = std::getenv("COMMEFF_TOPK_CAND_STATS") != nullptr;  // debug: host sync
     if (stats) {
       const int64_t off = (4 * 2048 * 4 + 2 * 4096 * 4 + 64 + 2048 * 4) / 4;  // topk.hip carve_cand: ctl
@@ -492,6 +501,15 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
     launch_topk_abs_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                          ws.data_ptr(), cur_stream(), hp);
   return {idx, vals};
+}
+
+// bytes of a kept cs_region_topk workspace for the chunk range [q0, q1)
+// (0: the call sizes its own -- candidate lists unsupported or disabled)
+int64_t cs_region_topk_ws_bytes(int64_t d, int64_t m, int64_t q0, int64_t q1) {
+  const int64_t lo = q0 * m, hi = std::min(d, q1 * m), n = hi - lo;
+  const char* e = std::getenv("COMMEFF_TOPK_CAND");
+  if ((e != nullptr && e[0] == '0') || m != 64 || !topk_cand_supported(n)) return 0;
+  return topk_cand_workspace_bytes(n);
 }
 
 void cs_region_zero_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2, const at::Tensor& idx,
@@ -703,9 +721,10 @@ at::Tensor scatter_dense_hip(const at::Tensor& idx, const at::Tensor& vals, int6
   return out;
 }
 
-at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pad, bool flip,
+at::Tensor augment_run(const at::Tensor& data, const at::Tensor& idx, int64_t pad, bool flip,
                        const at::Tensor& mean, const at::Tensor& inv_std, int64_t seed,
-                       bool out_bf16, const c10::optional<at::Tensor>& keys) {
+                       bool out_bf16, const c10::optional<at::Tensor>& keys, const at::Tensor* targets,
+                       at::Tensor* y) {
   TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.is_contiguous(),
               "data must be uint8 [N,H,W,C] contiguous");
   TORCH_CHECK(data.size(3) <= 4, "at most 4 channels");
@@ -718,14 +737,40 @@ at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pa
   auto mc = mean.to(data.device(), at::kFloat).contiguous();
   auto sc = inv_std.to(data.device(), at::kFloat).contiguous();
   auto ic = idx.contiguous();
+  const int64_t* tp = nullptr;
+  int64_t* yp = nullptr;
+  if (targets != nullptr) {
+    TORCH_CHECK(targets->scalar_type() == at::kLong && targets->dim() == 1 && targets->is_contiguous() &&
+                    targets->device() == data.device() && targets->size(0) == data.size(0),
+                "augment: targets must be a contiguous int64 [N] on the data's device");
+    *y = at::empty({B}, targets->options());
+    tp = targets->data_ptr<int64_t>();
+    yp = y->data_ptr<int64_t>();
+  }
   launch_augment_u8_nhwc(data.data_ptr<uint8_t>(), ic.data_ptr<int64_t>(), B,
                          static_cast<int>(H), static_cast<int>(W), static_cast<int>(C),
                          static_cast<int>(pad), flip ? 1 : 0, mc.data_ptr<float>(),
                          sc.data_ptr<float>(), static_cast<uint64_t>(seed), key_ptr(keys, B),
                          reinterpret_cast<uint16_t*>(out.data_ptr()), static_cast<int>(CS),
-                         cur_stream());
+                         cur_stream(), tp, yp);
   auto o = out.narrow(3, 0, C).permute({0, 3, 1, 2});
   return out_bf16 ? o : o.to(at::kFloat);
+}
+
+at::Tensor augment_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pad, bool flip,
+                       const at::Tensor& mean, const at::Tensor& inv_std, int64_t seed,
+                       bool out_bf16, const c10::optional<at::Tensor>& keys) {
+  return augment_run(data, idx, pad, flip, mean, inv_std, seed, out_bf16, keys, nullptr, nullptr);
+}
+
+// the augmented batch and its labels targets[idx] from one kernel
+std::tuple<at::Tensor, at::Tensor> augment_y_hip(const at::Tensor& data, const at::Tensor& idx, int64_t pad,
+                                                 bool flip, const at::Tensor& mean, const at::Tensor& inv_std,
+                                                 int64_t seed, bool out_bf16, const c10::optional<at::Tensor>& keys,
+                                                 const at::Tensor& targets) {
+  at::Tensor y;
+  auto x = augment_run(data, idx, pad, flip, mean, inv_std, seed, out_bf16, keys, &targets, &y);
+  return {x, y};
 }
 
 // ------------------------------------------------------- planned sketch ops
@@ -2062,7 +2107,8 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor goffs, int q0=0, int q1=-1) -> Tensor");
   m.def("cs_region_topk(Tensor(a!) table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
         "Tensor goffs, int k, Tensor? hint=None, int q0=0, int q1=-1, Tensor(b!)? momV=None, Tensor? momG=None, "
-        "float rho=0.0, float gscale=0.0, int mom_mode=0) -> (Tensor, Tensor)");
+        "float rho=0.0, float gscale=0.0, int mom_mode=0, Tensor(c!)? ws=None) -> (Tensor, Tensor)");
+  m.def("cs_region_topk_ws_bytes(int d, int m, int q0, int q1) -> int", &commeff::cs_region_topk_ws_bytes);
   m.def("cs_region_zero(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, int d, int m, int g, "
         "Tensor perm, Tensor cinfo) -> ()");
   m.def("topk_abs(Tensor x, int k, Tensor? hint=None) -> (Tensor, Tensor)");
@@ -2082,6 +2128,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("scatter_dense(Tensor idx, Tensor vals, int n) -> Tensor");
   m.def("augment_u8_nhwc(Tensor data, Tensor idx, int pad, bool flip, Tensor mean, Tensor inv_std, "
         "int seed, bool out_bf16, Tensor? keys=None) -> Tensor");
+  m.def("augment_u8_nhwc_y(Tensor data, Tensor idx, int pad, bool flip, Tensor mean, Tensor inv_std, "
+        "int seed, bool out_bf16, Tensor? keys, Tensor targets) -> (Tensor, Tensor)");
   m.def("binned_scratch_bytes(int d, int r, int c, int num_blocks) -> int",
         &commeff::binned_scratch_bytes);
   m.def("resid_ln_fwd(Tensor x, Tensor? p, Tensor? bias, Tensor gamma, Tensor beta, float p_drop, "
@@ -2181,6 +2229,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("zero_at", &zero_at_hip);
   m.impl("scatter_dense", &scatter_dense_hip);
   m.impl("augment_u8_nhwc", &augment_hip);
+  m.impl("augment_u8_nhwc_y", &augment_y_hip);
   m.impl("resid_ln_fwd", &resid_ln_fwd_hip);
   m.impl("resid_ln_bwd", &resid_ln_bwd_hip);
   m.impl("bias_gelu_fwd", &bias_gelu_fwd_hip);

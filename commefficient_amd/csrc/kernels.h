@@ -150,8 +150,11 @@ bool topk_cand_supported(int64_t n);
 int64_t topk_cand_workspace_bytes(int64_t n);
 void topk_cand_prepare(void* workspace, hipStream_t stream);
 void topk_cand_ptrs(void* workspace, int64_t n, uint64_t** ballots, uint32_t** seg);
+// persistent: the workspace is reused across calls (zeroed once by the
+// caller): the last pass re-zeroes the histograms / segment totals, so no
+// topk_cand_prepare is needed before the next call
 void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals, void* workspace,
-                           hipStream_t stream, uint32_t* hint);
+                           hipStream_t stream, uint32_t* hint, bool persistent = false);
 
 // ----------------------------------------------------------- elementwise --
 // V = rho*V + gscale*G ; mode 1: E += V ; mode 2: E = V
@@ -386,7 +389,8 @@ void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx,
                             int64_t B, int H, int W, int C, int pad,
                             int flip, const float* mean, const float* inv_std,
                             uint64_t seed, const int64_t* keys, uint16_t* out_bf16,
-                            int out_cstride, hipStream_t stream);
+                            int out_cstride, hipStream_t stream,
+                            const int64_t* targets = nullptr, int64_t* yout = nullptr);
 
 // ---------------------------------------------------------- transformer --
 // GPT-2 block junctions on bf16 [M, H] rows (transformer.hip, ops/transformer.py).

@@ -30,6 +30,8 @@ namespace {
 
 constexpr int kBins = 2048;
 constexpr int kNB = 4096;  // blocks for count/write passes (upper bound)
+constexpr int kSegC = 1024;    // candidate lists: chunks per segment
+constexpr int kSegMax = 2048;  // segments (n <= 2048 * 65536)
 
 struct WS {
   uint32_t* hist[4];  // kBins each (pass 2 uses 512; [3]: pass-0 fill-in below the hint)
@@ -357,7 +359,7 @@ template <bool CAND = false>
 __global__ void __launch_bounds__(256)
 write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32_t kk,
              int64_t* __restrict__ idx, float* __restrict__ vals, uint32_t* __restrict__ hint, Cand cd = Cand{},
-             float hint_frac = 0.5f) {
+             float hint_frac = 0.5f, uint32_t* __restrict__ clean_seg = nullptr) {
   __shared__ uint32_t tot[4], res[2];
   __shared__ uint32_t wt_eq[4], wt_sel[4];
   const int32_t* cmap = nullptr;  // candidate -> index (ascending)
@@ -370,6 +372,13 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
     span = cand_span(n);
   }
   const Walk wk = {ws.wk[4], ws.wk[5]};  // count_kernel's walk
+  if (clean_seg != nullptr) {
+    // persistent workspace: leave the histograms and segment totals zeroed
+    // for the next call (nothing after count_kernel reads them)
+    const int nt = static_cast<int>(gridDim.x) * 256, t0 = static_cast<int>(blockIdx.x) * 256 + threadIdx.x;
+    for (int e = t0; e < 4 * kBins; e += nt) ws.hist[0][e] = 0u;  // hist[0..3] are contiguous
+    for (int e = t0; e < kSegMax; e += nt) clean_seg[e] = 0u;
+  }
   const uint32_t thr = wk.prefix, ties = wk.remaining;
   // next call's lower bound: hint_frac x this threshold (finite thresholds only)
   if (hint != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
@@ -459,8 +468,6 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
 // fewer than k keys >= hint -> the compaction blocks add the fill-in
 // histogram of the keys < hint (hist[3]) and the passes read x; more than
 // `cap` candidates -> the passes read x.
-constexpr int kSegC = 1024;    // chunks per segment (= compaction block)
-constexpr int kSegMax = 2048;  // segments (n <= 2048 * 65536)
 
 struct CandWS {
   uint32_t* seg;       // kSegMax popcount totals
@@ -599,7 +606,7 @@ void topk_cand_ptrs(void* workspace, int64_t n, uint64_t** ballots, uint32_t** s
 }
 
 void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals, void* workspace,
-                           hipStream_t stream, uint32_t* hint) {
+                           hipStream_t stream, uint32_t* hint, bool persistent) {
   if (k <= 0 || n <= 0) return;
   WS w = carve(workspace);
   const CandWS cw = carve_cand(workspace, n);
@@ -623,7 +630,7 @@ void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, f
     return f > 0.f && f < 1.f ? f : 0.85f;
   }();
   hipLaunchKernelGGL(write_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, idx, vals,
-                     hint, cd, frac);
+                     hint, cd, frac, persistent ? cw.seg : nullptr);
 }
 
 void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* vals,

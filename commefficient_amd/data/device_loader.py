@@ -54,6 +54,9 @@ class DeviceImageSource:
         if self.device.type == "cuda":
             t = h2d(t, self.device)
         idx, kt = (t[0], t[1]) if keys is not None else (t, None)
+        if self.device.type == "cuda":  # labels gathered by the same kernel
+            return ops.augment_u8_nhwc_y(self.data, idx, self.pad, self.flip, self.mean,
+                                         self.inv_std, seed, self.out_bf16, kt, self.targets)
         x = ops.augment_u8_nhwc(self.data, idx, self.pad, self.flip, self.mean, self.inv_std,
                                 seed, self.out_bf16, kt)
         y = self.targets[idx]
@@ -64,6 +67,9 @@ class DeviceImageSource:
         0 -- the same pixels as ``gather(rows, seed, keys)`` when
         ``keys' = seed * 0x9E3779B97F4A7C15 + keys`` (mod 2^64), so the rows and
         keys ride in the round's one packed H2D copy."""
+        if self.device.type == "cuda":  # labels gathered by the same kernel
+            return ops.augment_u8_nhwc_y(self.data, idx2[0], self.pad, self.flip, self.mean,
+                                         self.inv_std, 0, self.out_bf16, idx2[1], self.targets)
         x = ops.augment_u8_nhwc(self.data, idx2[0], self.pad, self.flip, self.mean,
                                 self.inv_std, 0, self.out_bf16, idx2[1])
         return x, self.targets[idx2[0]]

@@ -12,7 +12,8 @@ from .sketch import CSVec, make_hashes
 
 __all__ = ["CSVec", "make_hashes", "topk_abs", "topk_dense", "momentum_ef", "sparse_apply",
            "dense_apply", "count_ge", "axpby", "l2norm", "clip_noise", "client_state",
-           "zero_at", "scatter_dense", "augment_u8_nhwc", "account_round", "account_hist"]
+           "zero_at", "scatter_dense", "augment_u8_nhwc", "augment_u8_nhwc_y", "account_round",
+           "account_hist"]
 
 ERROR_MODE = {"none": 0, "virtual": 1, "local": 2}
 
@@ -114,6 +115,12 @@ def scatter_dense(idx, vals, n):
 def augment_u8_nhwc(data, idx, pad, flip, mean, inv_std, seed, out_bf16=True, keys=None):
     return _ops().augment_u8_nhwc(data, idx, int(pad), bool(flip), mean, inv_std, int(seed),
                                   bool(out_bf16), keys)
+
+
+def augment_u8_nhwc_y(data, idx, pad, flip, mean, inv_std, seed, out_bf16, keys, targets):
+    """augment_u8_nhwc and the labels targets[idx] from one kernel (GPU)."""
+    return _ops().augment_u8_nhwc_y(data, idx, int(pad), bool(flip), mean, inv_std, int(seed),
+                                    bool(out_bf16), keys, targets)
 
 
 # ------------------------------------------------------------ conv3x3 (MFMA)

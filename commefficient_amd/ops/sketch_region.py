@@ -182,6 +182,19 @@ def query(h: RegionHash, table: torch.Tensor, q0: int = 0, q1: int = -1) -> torc
 MOM_MODE = {"virtual": 1, "none": 2}
 
 
+def _topk_ws(h: RegionHash, device, q0: int, q1: int) -> Optional[torch.Tensor]:
+    """The candidate-list top-k workspace of this hash and chunk range, kept
+    across calls (zeroed once; the kernels leave it zeroed): no memset per
+    call.  None when the op sizes its own."""
+    cache = h.__dict__.setdefault("_topk_ws", {})
+    key = (str(device), int(q0), int(q1))
+    ws = cache.get(key)
+    if ws is None:
+        nb = int(ops().cs_region_topk_ws_bytes(h.d, h.m, int(q0), int(q1)))
+        ws = cache[key] = torch.zeros(nb, dtype=torch.uint8, device=device) if nb > 0 else False
+    return ws if ws is not False else None
+
+
 def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor] = None,
          q0: int = 0, q1: int = -1, mom=None):
     """(idx, vals): the k largest-magnitude median estimates of the
@@ -205,7 +218,7 @@ def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor
             mv, mg = (V.view(table.shape) if mode == 1 else None), G.view(table.shape)
         return ops().cs_region_topk(table, h.d, h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
                                     t["goffs"], int(k), hint, int(q0), int(q1), mv, mg, float(rho),
-                                    float(gs), mode)
+                                    float(gs), mode, _topk_ws(h, table.device, q0, q1))
     if mom is not None:
         from . import momentum_ef
         V, G, rho, gs, et = mom

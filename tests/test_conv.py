@@ -334,6 +334,22 @@ def test_augment_writes_padded_pixels():
     assert torch.all(pad == 0)
 
 
+def test_augment_with_labels_matches_separate_gather():
+    """augment_u8_nhwc_y: the same pixels as augment_u8_nhwc plus targets[idx]."""
+    from commefficient_amd import ops as cops
+    g = torch.Generator().manual_seed(3)
+    data = torch.randint(0, 256, (40, 32, 32, 3), dtype=torch.uint8, generator=g).cuda()
+    targets = torch.randint(0, 10, (40,), generator=g).cuda()
+    idx = torch.randint(0, 40, (300,), generator=g).cuda()
+    keys = torch.arange(300, device="cuda") * 7
+    mean = torch.tensor([0.5, 0.4, 0.3], device="cuda")
+    inv = torch.tensor([2.0, 3.0, 4.0], device="cuda")
+    x0 = cops.augment_u8_nhwc(data, idx, 4, True, mean, inv, 11, True, keys)
+    x1, y1 = cops.augment_u8_nhwc_y(data, idx, 4, True, mean, inv, 11, True, keys, targets)
+    assert torch.equal(x0, x1) and x1.stride() == x0.stride()
+    assert torch.equal(y1, targets[idx])
+
+
 @pytest.mark.parametrize("N, C, H, K", [(3, 64, 32, 128), (5, 128, 16, 256), (7, 256, 8, 512),
                                         (2, 64, 4, 128),
                                         # batches big enough for the 256 x 256 tile
