@@ -361,8 +361,13 @@ __global__ void __launch_bounds__(256) prep_wgrad_reduce_kernel(const float* __r
 }  // namespace
 
 int conv_prep_wgrad_blocks(int P) {
+  static const int per = [] {  // pixel steps per block (tuning knob COMMEFF_PREP_WG_STEPS)
+    const char* e = std::getenv("COMMEFF_PREP_WG_STEPS");
+    const int v = e != nullptr ? std::atoi(e) : 8;
+    return v < 1 ? 1 : v;
+  }();
   const int steps = (P + 63) / 64;
-  int b = (steps + 7) / 8;  // >= 8 pixel steps per block
+  int b = (steps + per - 1) / per;
   return b < 1024 ? (b < 1 ? 1 : b) : 1024;
 }
 

@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Input-convolution (conv_prep) micro-benchmark at the headline batch
 (500 x 3 x 32 x 32): forward and weight-gradient medians (HIP events).  The
-tiles-per-wave knob COMMEFF_PREP_TPW is read once per process, so a sweep runs
-this script once per value:
+tiles-per-wave knob COMMEFF_PREP_TPW (and the weight gradient's COMMEFF_PREP_WG_STEPS) is read
+once per process, so a sweep runs this script once per value:
 
     for t in 2 4 8; do COMMEFF_PREP_TPW=$t python scripts/bench_prep.py; done
 """
@@ -43,6 +43,9 @@ def main():
     r["fwd_us"] = timeit(lambda: ops.conv_prep_fwd(x, w))
     out_bytes = y.numel() * 2 + mask.numel() * 4 + B * H * W * 8
     r["fwd_TBps"] = out_bytes / r["fwd_us"] / 1e6
+    gy = torch.randn_like(y, dtype=torch.float32).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dw = torch.zeros(64, 3, 3, 3, device="cuda")
+    r["wgrad_us"] = timeit(lambda: ops.conv_prep_wgrad_into(gy, mask, x, dw))
     r["fill_y_us"] = timeit(lambda: y.fill_(0))  # write roofline at this size
     r["fill_TBps"] = y.numel() * 2 / r["fill_y_us"] / 1e6
     print(json.dumps(r), flush=True)
