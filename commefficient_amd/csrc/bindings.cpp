@@ -594,6 +594,36 @@ void sparse_apply_hip(at::Tensor w, const at::Tensor& idx, const at::Tensor& val
                       static_cast<int32_t>(round), step_ptr(step), hist_ptr(hist), cur_stream());
 }
 
+// sparse_apply + cs_region_zero of the same (idx, vals) in one kernel
+void cs_region_zero_apply_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2, const at::Tensor& idx,
+                              const at::Tensor& vals, int64_t d, int64_t m, int64_t g, const at::Tensor& perm,
+                              const at::Tensor& cinfo, at::Tensor w, double lr,
+                              const c10::optional<at::Tensor>& lr_vec, const c10::optional<at::Tensor>& last_mod,
+                              int64_t round, const c10::optional<at::Tensor>& hist) {
+  const RegionParams p = check_region(t1, d, m, g, 1, perm, cinfo, nullptr, nullptr);
+  check_f32(w, "w");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous() && idx.device() == t1.device(),
+              "cs_region_zero_apply: idx must be int64 on the table's device");
+  TORCH_CHECK(vals.numel() == idx.numel() && vals.scalar_type() == at::kFloat && vals.is_contiguous(),
+              "cs_region_zero_apply: vals must match idx");
+  TORCH_CHECK(w.device() == t1.device() && w.numel() == d, "cs_region_zero_apply: w must hold the d weights");
+  TORCH_CHECK(p.r >= 1 && p.r <= 8, "cs_region_zero_apply: at most 8 rows (rh::kZeroRows)");
+  float* t2p = nullptr;
+  if (t2.has_value() && t2->defined()) {
+    TORCH_CHECK(t2->sizes() == t1.sizes() && t2->scalar_type() == at::kFloat && t2->is_contiguous(),
+                "cs_region_zero_apply: t2 must match t1");
+    t2p = t2->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
+  launch_sparse_apply_region_zero(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
+                                  idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
+                                  static_cast<int32_t>(round), nullptr, hist_ptr(hist), t1.data_ptr<float>(), t2p,
+                                  reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+                                  reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()),
+                                  static_cast<int>(p.r), p.c, m, p.nch, d, cur_stream());
+}
+
 void dense_apply_hip(at::Tensor w, const at::Tensor& delta, double lr,
                      const c10::optional<at::Tensor>& lr_vec,
                      const c10::optional<at::Tensor>& last_mod, int64_t round,
@@ -2115,6 +2145,9 @@ TORCH_LIBRARY(commeff, m) {
   m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
   m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "
         "Tensor(b!)? last_mod, int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");
+  m.def("cs_region_zero_apply(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor vals, int d, int m, int g, "
+        "Tensor perm, Tensor cinfo, Tensor(c!) w, float lr, Tensor? lr_vec, Tensor(d!)? last_mod, int round, "
+        "Tensor(e!)? hist=None) -> ()");
   m.def("dense_apply(Tensor(a!) w, Tensor delta, float lr, Tensor? lr_vec, Tensor(b!)? last_mod, "
         "int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");
   m.def("account_hist(Tensor hist, Tensor meta, int W, Tensor(a!) client_dl, Tensor(b!) client_ul, "
@@ -2215,6 +2248,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("cs_region_query", &cs_region_query_hip);
   m.impl("cs_region_zero", &cs_region_zero_hip);
   m.impl("cs_region_topk", &cs_region_topk_hip);
+  m.impl("cs_region_zero_apply", &cs_region_zero_apply_hip);
   m.impl("topk_abs", &topk_abs_hip);
   m.impl("momentum_ef", &momentum_ef_hip);
   m.impl("sparse_apply", &sparse_apply_hip);

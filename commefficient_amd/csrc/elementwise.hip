@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "kernels.h"
+#include "region_hash.h"
 
 namespace commeff {
 namespace {
@@ -126,11 +127,16 @@ __device__ __forceinline__ void hist_flush(const HistWin& hw, int32_t* hist) {
 
 constexpr int kApplyBlock = 1024;
 
+// ZERO: also the region sketch's heavy-hitter zeroing of the same list
+// (cs_region_zero_kernel semantics: the r cells of every coordinate with a
+// nonzero value, in t1 and t2) -- one launch fewer per server step
+template <bool ZERO = false>
 __global__ void __launch_bounds__(kApplyBlock)
 sparse_apply_kernel(float* __restrict__ w, const int64_t* __restrict__ idx,
                     const float* __restrict__ vals, int64_t k, float lr,
                     const float* __restrict__ lr_vec, int32_t* __restrict__ last_mod,
-                    int32_t round, const int32_t* __restrict__ step, int32_t* __restrict__ hist) {
+                    int32_t round, const int32_t* __restrict__ step, int32_t* __restrict__ hist,
+                    rh::RegionZero rz = rh::RegionZero{}) {
   __shared__ int32_t lh[kHistWin + 1];
   const int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   if (step != nullptr) {  // graph replay: [lr bits, round] from device memory
@@ -145,8 +151,33 @@ sparse_apply_kernel(float* __restrict__ w, const int64_t* __restrict__ idx,
     const int64_t i = idx[q];
     const float l = lr_vec != nullptr ? lr_vec[i] : lr;
     const float old = w[i];
-    const float nw = old - l * vals[q];
+    const float vq = vals[q];
+    const float nw = old - l * vq;
     w[i] = nw;
+    if constexpr (ZERO) {
+      // the rows' hash words loaded together (unconditional, clamped row):
+      // one dependent-load latency per coordinate, not one per row
+      const uint64_t ic = static_cast<uint64_t>(i) < rz.d ? static_cast<uint64_t>(i) : 0u;
+      const uint32_t qc = static_cast<uint32_t>(ic / rz.m), o = static_cast<uint32_t>(ic - static_cast<uint64_t>(qc) * rz.m);
+      uint32_t cw[rh::kZeroRows], pw[rh::kZeroRows];
+#pragma unroll
+      for (int j = 0; j < rh::kZeroRows; ++j) {
+        const uint32_t jj = static_cast<uint32_t>(j) < rz.r ? static_cast<uint32_t>(j) : rz.r - 1;
+        cw[j] = rz.cinfo[static_cast<size_t>(jj) * rz.nch + qc];
+        pw[j] = rz.perm[jj * rz.m + o];
+      }
+      if (vq != 0.f && static_cast<uint64_t>(i) < rz.d) {
+#pragma unroll
+        for (int j = 0; j < rh::kZeroRows; ++j) {
+          if (static_cast<uint32_t>(j) < rz.r) {
+            const size_t cell = static_cast<size_t>(j) * rz.c + static_cast<size_t>(rh::ci_region(cw[j])) * rz.m +
+                                rh::in_region(pw[j], cw[j], rz.m);
+            rz.t1[cell] = 0.f;
+            if (rz.t2 != nullptr) rz.t2[cell] = 0.f;
+          }
+        }
+      }
+    }
     if (last_mod != nullptr && nw != old) {
       from = last_mod[i];
       last_mod[i] = round;
@@ -507,8 +538,21 @@ void launch_sparse_apply(float* w, const int64_t* idx, const float* vals, int64_
                          const float* lr_vec, int32_t* last_mod, int32_t round,
                          const int32_t* step, int32_t* hist, hipStream_t stream) {
   if (k <= 0) return;
-  hipLaunchKernelGGL(sparse_apply_kernel, dim3((k + kApplyBlock - 1) / kApplyBlock), dim3(kApplyBlock),
-                     0, stream, w, idx, vals, k, lr, lr_vec, last_mod, round, step, hist);
+  hipLaunchKernelGGL(sparse_apply_kernel<false>, dim3((k + kApplyBlock - 1) / kApplyBlock), dim3(kApplyBlock),
+                     0, stream, w, idx, vals, k, lr, lr_vec, last_mod, round, step, hist, rh::RegionZero{});
+}
+
+void launch_sparse_apply_region_zero(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
+                                     const float* lr_vec, int32_t* last_mod, int32_t round, const int32_t* step,
+                                     int32_t* hist, float* t1, float* t2, const uint32_t* perm,
+                                     const uint32_t* cinfo, int r, int64_t c, int64_t m, int64_t nch, int64_t d,
+                                     hipStream_t stream) {
+  if (k <= 0) return;
+  const rh::RegionZero rz{t1, t2, perm, cinfo, static_cast<uint32_t>(r), static_cast<uint32_t>(c),
+                          static_cast<uint32_t>(m), static_cast<uint32_t>(nch), static_cast<uint64_t>(d)};
+  // 256-thread blocks: 4x the blocks of the plain apply for the scattered zeroing
+  hipLaunchKernelGGL(sparse_apply_kernel<true>, dim3((k + 255) / 256), dim3(256), 0, stream, w, idx, vals, k, lr,
+                     lr_vec, last_mod, round, step, hist, rz);
 }
 
 void launch_dense_apply(float* w, const float* delta, int64_t n, float lr, const float* lr_vec,

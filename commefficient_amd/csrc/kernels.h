@@ -165,6 +165,13 @@ void launch_sparse_apply(float* w, const int64_t* idx, const float* vals,
                          int64_t k, float lr, const float* lr_vec,
                          int32_t* last_mod, int32_t round, const int32_t* step,
                          int32_t* hist, hipStream_t stream);
+// the same plus the region sketch's heavy-hitter zeroing of the list (cells of
+// coordinates with nonzero vals in t1 and t2; cs_region_zero semantics)
+void launch_sparse_apply_region_zero(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
+                                     const float* lr_vec, int32_t* last_mod, int32_t round, const int32_t* step,
+                                     int32_t* hist, float* t1, float* t2, const uint32_t* perm,
+                                     const uint32_t* cinfo, int r, int64_t c, int64_t m, int64_t nch, int64_t d,
+                                     hipStream_t stream);
 // w -= lr(i) * delta ; last_mod[i] = round where w changed
 // (step != nullptr: lr = bits of step[0], round = step[1], read on the device
 // so a captured HIP graph replays with the current round's values)

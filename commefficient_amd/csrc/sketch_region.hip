@@ -34,22 +34,17 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "kernels.h"
+#include "region_hash.h"
 
 namespace commeff {
 namespace {
 
-constexpr uint32_t kSignBit = 0x80000000u;
-constexpr uint32_t kRegionMask = 0x00ffffffu;
-
-__device__ __forceinline__ uint32_t ci_region(uint32_t w) { return w & kRegionMask; }
-__device__ __forceinline__ uint32_t ci_shift(uint32_t w) { return (w >> 24) & 0x3fu; }
-
-// in-region bucket of lane word pw (P_j(o) | S_j(o) << 31) under chunk word w
-__device__ __forceinline__ uint32_t in_region(uint32_t pw, uint32_t w, uint32_t m) {
-  uint32_t b = (pw & ~kSignBit) + ci_shift(w);
-  return b >= m ? b - m : b;
-}
-__device__ __forceinline__ bool neg_of(uint32_t pw, uint32_t w) { return ((pw ^ w) & kSignBit) != 0u; }
+using rh::ci_region;
+using rh::ci_shift;
+using rh::in_region;
+using rh::kRegionMask;
+using rh::kSignBit;
+using rh::neg_of;
 
 // RT rows (0: runtime r <= kMaxRows), SL = chunk slots per wave per pipelined
 // group, K slots per batch (batch = K * W chunks, W = blockDim / 64 waves:
@@ -367,10 +362,7 @@ cs_region_zero_kernel(float* __restrict__ t1, float* __restrict__ t2, const int6
   if (vals != nullptr && vals[t] == 0.f) return;
   const uint64_t i = static_cast<uint64_t>(idx[t]);
   if (i >= d) return;  // (top-k indices are always in range)
-  const uint32_t q = static_cast<uint32_t>(i / m), o = static_cast<uint32_t>(i - static_cast<uint64_t>(q) * m);
-  const uint32_t cw = cinfo[static_cast<size_t>(j) * nch + q];
-  const size_t cell = static_cast<size_t>(j) * c + static_cast<size_t>(ci_region(cw)) * m +
-                      in_region(perm[j * m + o], cw, m);
+  const size_t cell = rh::cell_of(i, j, c, m, nch, perm, cinfo);
   t1[cell] = 0.f;
   if (t2 != nullptr) t2[cell] = 0.f;
 }

@@ -269,6 +269,19 @@ class CSVec:
         ops().cs_zero_buckets(self.table, other, idx, vals, self.hashes, self.blk_off,
                               self.blk_sign, self.numBlocks, self.d)
 
+    def zero_heavy_hitters_apply(self, idx: torch.Tensor, vals: torch.Tensor, other: Optional[torch.Tensor],
+                                 w: torch.Tensor, lr: float, lr_vec, last_mod, round_idx: int, hist) -> bool:
+        """zero_heavy_hitters + ops.sparse_apply(w, idx, vals, ...) in one GPU
+        kernel (region family).  Returns False (nothing done) where the fused
+        kernel does not apply; the caller then runs the two steps."""
+        if self.region is None or not self.table.is_cuda or w.numel() != self.d or self.r > 8:
+            return False
+        t = self.region.tensors(self.table.device)
+        ops().cs_region_zero_apply(self.table, other, idx.contiguous(), vals.contiguous(), self.d,
+                                   self.region.m, self.region.g, t["perm"], t["cinfo"], w, float(lr),
+                                   lr_vec, last_mod, int(round_idx), hist)
+        return True
+
     def l2estimate(self) -> torch.Tensor:
         return ops().cs_l2estimate(self.table)
 

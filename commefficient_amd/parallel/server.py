@@ -128,9 +128,13 @@ class ServerState:
                                                        dist.all_gather_rows, mom=mom)
             else:
                 idx, vals = sk.unsketch_sparse(a.k, mom=mom)
-            # error feedback (virtual) + momentum-factor masking in sketch space
-            sk.zero_heavy_hitters(idx, vals, self.V if et == "virtual" else None)
-            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
+            # error feedback (virtual) + momentum-factor masking in sketch space,
+            # and the weight step (one kernel for the region family)
+            other = self.V if et == "virtual" else None
+            if step is not None or not sk.zero_heavy_hitters_apply(idx, vals, other, w, lr_s, lr_v, last_mod,
+                                                                    round_idx, hist):
+                sk.zero_heavy_hitters(idx, vals, other)
+                ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
             weights_end_update(img_sync, w, idx)
             return idx, vals
         if mode == "true_topk":

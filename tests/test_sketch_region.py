@@ -270,3 +270,33 @@ def test_region_fused_momentum_matches_separate(et):
         assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
         m = base.region.G * base.region.g * base.region.m  # the unused tail is never touched
         assert torch.equal(V2[:, :m], V1[:, :m]) and torch.equal(E2[:, :m], E1[:, :m])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,c,r", GPU_GEOMS)
+def test_region_zero_apply_matches_separate_steps(d, c, r):
+    """cs_region_zero_apply = zero_heavy_hitters + sparse_apply (bitwise),
+    incl. the last-changed stamps and the change histogram."""
+    from commefficient_amd import ops as cops
+    torch.manual_seed(d % 997)
+    _, gpu = _pair(d, c, r)
+    gpu.table.copy_(torch.randn(gpu.table.shape))
+    other = torch.randn(gpu.table.shape, device="cuda")
+    k = min(1000, d // 3)
+    idx = torch.randperm(d)[:k].sort().values.cuda()
+    vals = torch.randn(k, device="cuda")
+    vals[::4] = 0
+    w = torch.randn(d, device="cuda")
+    last_mod = torch.randint(-1, 3, (d,), dtype=torch.int32, device="cuda")
+    hist = torch.zeros(64, dtype=torch.int32, device="cuda")
+    lr_vec = torch.rand(d, device="cuda")
+    for lrv in (None, lr_vec):
+        t1, t2, w1, lm1, h1 = gpu.table.clone(), other.clone(), w.clone(), last_mod.clone(), hist.clone()
+        sep = gpu.like(t1)
+        sep.zero_heavy_hitters(idx, vals, t2)
+        cops.sparse_apply(w1, idx, vals, 0.3, lrv, lm1, 5, None, h1)
+        t3, t4, w2, lm2, h2 = gpu.table.clone(), other.clone(), w.clone(), last_mod.clone(), hist.clone()
+        fused = gpu.like(t3)
+        assert fused.zero_heavy_hitters_apply(idx, vals, t4, w2, 0.3, lrv, lm2, 5, h2)
+        for a, b in ((t1, t3), (t2, t4), (w1, w2), (lm1, lm2), (h1, h2)):
+            assert torch.equal(a, b)
