@@ -1310,9 +1310,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> head_fwd_
 }
 
 // returns dx [B, C, h, w] (channels_last bf16); dw = beta * dw + dW
-at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at::Tensor& w,
+at::Tensor head_bwd_run(const at::Tensor& gl, const at::Tensor& gunit, const at::Tensor& w,
                         const at::Tensor& pooled, const at::Tensor& codes, int64_t H, int64_t W,
-                        double scale, at::Tensor dw, double beta) {
+                        double scale, at::Tensor dw, double beta, const at::Tensor* ymask, at::Tensor* dxm) {
   check_f32(w, "head: w");
   const int64_t B = pooled.size(0), C = pooled.size(1), K = w.size(0);
   TORCH_CHECK(gunit.is_contiguous() && gunit.size(0) == B && gunit.size(1) == K && codes.is_contiguous() &&
@@ -1323,12 +1323,38 @@ at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at:
   auto dx = at::empty({B, C, H, W}, pooled.options().memory_format(at::MemoryFormat::ChannelsLast));
   check_f32(dw, "head_bwd: dw");
   TORCH_CHECK(dw.sizes() == w.sizes(), "head_bwd: dw shape");
+  const uint16_t* ym = nullptr;
+  uint16_t* dm = nullptr;
+  if (ymask != nullptr) {
+    TORCH_CHECK(ymask->scalar_type() == at::kBFloat16 && ymask->sizes() == dx.sizes() &&
+                    ymask->is_contiguous(at::MemoryFormat::ChannelsLast) && ymask->device() == dx.device(),
+                "head_bwd_dual: ymask must be bf16 channels_last like x");
+    *dxm = at::empty_like(dx);
+    ym = reinterpret_cast<const uint16_t*>(ymask->data_ptr());
+    dm = reinterpret_cast<uint16_t*>(dxm->data_ptr());
+  }
   launch_head_bwd(g.data_ptr<float>(), gunit.data_ptr<float>(), w.data_ptr<float>(),
                   reinterpret_cast<const uint16_t*>(pooled.data_ptr()), codes.data_ptr<uint8_t>(),
                   static_cast<int>(B), static_cast<int>(C), static_cast<int>(H * W), static_cast<int>(K),
                   static_cast<float>(scale), reinterpret_cast<uint16_t*>(dx.data_ptr()), dw.data_ptr<float>(),
-                  static_cast<float>(beta), cur_stream());
+                  static_cast<float>(beta), cur_stream(), ym, dm);
   return dx;
+}
+
+at::Tensor head_bwd_hip(const at::Tensor& gl, const at::Tensor& gunit, const at::Tensor& w,
+                        const at::Tensor& pooled, const at::Tensor& codes, int64_t H, int64_t W,
+                        double scale, at::Tensor dw, double beta) {
+  return head_bwd_run(gl, gunit, w, pooled, codes, H, W, scale, dw, beta, nullptr, nullptr);
+}
+
+// dx and dx masked by ymask > 0 (the producer's ReLU backward) from one kernel
+std::tuple<at::Tensor, at::Tensor> head_bwd_dual_hip(const at::Tensor& gl, const at::Tensor& gunit,
+                                                     const at::Tensor& w, const at::Tensor& pooled,
+                                                     const at::Tensor& codes, int64_t H, int64_t W, double scale,
+                                                     at::Tensor dw, double beta, const at::Tensor& ymask) {
+  at::Tensor dxm;
+  auto dx = head_bwd_run(gl, gunit, w, pooled, codes, H, W, scale, dw, beta, &ymask, &dxm);
+  return {dx, dxm};
 }
 
 // ghost batch norm: x [N, C, H, W] bf16 channels_last, G | N groups.
@@ -2102,6 +2128,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("head_fwd(Tensor x, Tensor w, Tensor targets, float scale) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("head_bwd(Tensor gl, Tensor gunit, Tensor w, Tensor pooled, Tensor codes, int H, int W, float scale, "
         "Tensor(a!) dw, float beta) -> Tensor");
+  m.def("head_bwd_dual(Tensor gl, Tensor gunit, Tensor w, Tensor pooled, Tensor codes, int H, int W, "
+        "float scale, Tensor(a!) dw, float beta, Tensor ymask) -> (Tensor, Tensor)");
   m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
@@ -2227,6 +2255,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("conv3x3_fwd_pool2", &conv3x3_fwd_pool2_hip);
   m.impl("head_fwd", &head_fwd_hip);
   m.impl("head_bwd", &head_bwd_hip);
+  m.impl("head_bwd_dual", &head_bwd_dual_hip);
   m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
   m.impl("ce_fwd", &ce_fwd_hip);
   m.impl("client_means", &client_means_hip);

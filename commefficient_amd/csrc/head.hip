@@ -163,7 +163,10 @@ __global__ void __launch_bounds__(256)
 head_bwd_kernel(const float* __restrict__ gl, const float* __restrict__ gunit, const float* __restrict__ w,
                 const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ codes, int B, int C,
                 int NPIX, int NCLS, float scale, int nrow_blocks, uint16_t* __restrict__ dx,
-                float* __restrict__ dw, float beta) {
+                float* __restrict__ dw, float beta, const uint16_t* __restrict__ ymask,
+                uint16_t* __restrict__ dxm) {
+  // ymask / dxm (optional): also dx masked by ymask > 0 -- the producing
+  // residual unit's ReLU backward (nn.py _MaskLink), one pass fewer
   const int lane = threadIdx.x & 63;
   if (static_cast<int>(blockIdx.x) < nrow_blocks) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -190,7 +193,16 @@ head_bwd_kernel(const float* __restrict__ gl, const float* __restrict__ gunit, c
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           o.h[j] = ((cd >> (8 * j)) & 0xffu) == static_cast<uint64_t>(p) ? hv[j] : static_cast<uint16_t>(0);
-        *reinterpret_cast<H8*>(dx + (static_cast<size_t>(b) * NPIX + p) * C + ch) = o;
+        const size_t off = (static_cast<size_t>(b) * NPIX + p) * C + ch;
+        *reinterpret_cast<H8*>(dx + off) = o;
+        if (ymask != nullptr) {
+          const H8 y = *reinterpret_cast<const H8*>(ymask + off);
+          H8 om;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            om.h[j] = (!(y.h[j] & 0x8000u) && y.h[j] != 0u) ? o.h[j] : static_cast<uint16_t>(0);
+          *reinterpret_cast<H8*>(dxm + off) = om;
+        }
       }
     }
     return;
@@ -241,12 +253,12 @@ void launch_head_fwd(const uint16_t* x, const float* w, const int64_t* tgt, int 
 
 void launch_head_bwd(const float* gl, const float* gunit, const float* w, const uint16_t* pooled,
                      const uint8_t* codes, int B, int C, int NPIX, int NCLS, float scale, uint16_t* dx,
-                     float* dw, float beta, hipStream_t stream) {
+                     float* dw, float beta, hipStream_t stream, const uint16_t* ymask, uint16_t* dxm) {
   const int nrow = (B + 3) / 4;
   const int nw = NCLS * ((C + 63) / 64);
   if (nrow + nw <= 0) return;
   hipLaunchKernelGGL(head_bwd_kernel, dim3(nrow + nw), dim3(256), 0, stream, gl, gunit, w, pooled, codes, B, C,
-                     NPIX, NCLS, scale, nrow, dx, dw, beta);
+                     NPIX, NCLS, scale, nrow, dx, dw, beta, ymask, dxm);
 }
 
 }  // namespace commeff

@@ -328,7 +328,8 @@ void launch_head_fwd(const uint16_t* x, const float* w, const int64_t* tgt, int 
                      hipStream_t stream);
 void launch_head_bwd(const float* gl, const float* gunit, const float* w, const uint16_t* pooled,
                      const uint8_t* codes, int B, int C, int NPIX, int NCLS, float scale, uint16_t* dx,
-                     float* dw, float beta, hipStream_t stream);
+                     float* dw, float beta, hipStream_t stream, const uint16_t* ymask = nullptr,
+                     uint16_t* dxm = nullptr);
 // ghost batch norm (bn.hip): x NHWC bf16, G groups of M pixels, C % 8 == 0,
 // C <= 2048; part = bn_scratch_floats(G, M, C) floats, stat = ab = 2GC, coef = 3GC
 int bn_slabs(int G, int M);

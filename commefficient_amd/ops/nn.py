@@ -527,11 +527,15 @@ class _FusedHead(torch.autograd.Function):
     accumulates straight into an existing flat-buffer ``.grad``."""
 
     @staticmethod
-    def forward(ctx, x, weight, targets, scale):
+    def forward(ctx, x, weight, targets, scale, in_mask=None):
         loss, correct, gunit, pooled, codes = _ops().head_fwd(x, weight.detach(), targets,
                                                               float(scale))
         ctx.save_for_backward(gunit, pooled, codes)
         ctx.weight, ctx.scale, ctx.hw = weight, float(scale), (x.shape[2], x.shape[3])
+        # a native residual unit's output (link taken by fused_head_loss: grad
+        # mode is off in here): the backward also writes the gradient masked
+        # by its ReLU (dual output, no relu_mask pass)
+        ctx.in_mask = in_mask
         ctx.mark_non_differentiable(correct)
         ctx.set_materialize_grads(False)  # no zeros fill for the unused gradient of `correct`
         return loss, correct
@@ -539,16 +543,21 @@ class _FusedHead(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gl, gc):
         if gl is None:  # (grads are not materialised) the loss got no gradient
-            return None, None, None, None
+            return None, None, None, None, None
         gunit, pooled, codes = ctx.saved_tensors
         w = ctx.weight
         gr = w.grad
         into = (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
                 and gr.shape == w.shape and gr.device == w.device)
         dw = gr if into else torch.empty_like(w, dtype=torch.float32)
-        dx = _ops().head_bwd(gl.contiguous(), gunit, w.detach(), pooled, codes, ctx.hw[0],
-                             ctx.hw[1], ctx.scale, dw, 1.0 if into else 0.0)
-        return dx, (None if into else dw), None, None
+        if ctx.in_mask is not None:
+            dx, dxm = _ops().head_bwd_dual(gl.contiguous(), gunit, w.detach(), pooled, codes, ctx.hw[0],
+                                           ctx.hw[1], ctx.scale, dw, 1.0 if into else 0.0, ctx.in_mask.mask)
+            ctx.in_mask.src, ctx.in_mask.masked = dx, dxm
+        else:
+            dx = _ops().head_bwd(gl.contiguous(), gunit, w.detach(), pooled, codes, ctx.hw[0],
+                                 ctx.hw[1], ctx.scale, dw, 1.0 if into else 0.0)
+        return dx, (None if into else dw), None, None, None
 
 
 def head_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -560,7 +569,11 @@ def head_native_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
 
 def fused_head_loss(x, weight, targets, scale: float):
     """(per-example CE loss, correct) of ``scale * maxpool_all(relu(x)) @ weight.T``."""
-    return _FusedHead.apply(x, weight, targets.contiguous(), float(scale))
+    link = _mask_link_of(x)
+    if link is not None and not (link.mask.dtype == torch.bfloat16
+                                 and link.mask.is_contiguous(memory_format=torch.channels_last)):
+        link = None
+    return _FusedHead.apply(x, weight, targets.contiguous(), float(scale), link)
 
 
 # ------------------------------------------------------------ ghost batch norm

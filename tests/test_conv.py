@@ -615,6 +615,40 @@ def test_fused_unpool_backward_bitwise(chain):
         assert torch.equal(ga, gb)
 
 
+def test_residual_into_fused_head_dual_backward_matches_unfused():
+    """ResNet-9 res3 -> head: the head backward's masked second output
+    (head_bwd_dual, the residual unit's ReLU backward) gives the same
+    gradients, bitwise, as the separate relu_mask pass."""
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x0 = torch.randn(16, 512, 4, 4, device="cuda", generator=g).relu().to(torch.bfloat16)
+    x0 = x0.contiguous(memory_format=torch.channels_last)
+    w1 = torch.randn(512, 512, 3, 3, device="cuda", generator=g) * 0.02
+    w2 = torch.randn(512, 512, 3, 3, device="cuda", generator=g) * 0.02
+    wl = torch.randn(10, 512, device="cuda", generator=g) * 0.05
+    tg = torch.randint(0, 10, (16,), device="cuda", generator=g)
+
+    def run(fused):
+        cnn.set_fused_unpool(fused)
+        try:
+            x = x0.clone().requires_grad_(True)
+            ws = [w.clone().requires_grad_(True) for w in (w1, w2, wl)]
+            f = cnn.residual_unit(x, ws[0], ws[1])
+            loss, _ = cnn.fused_head_loss(f, ws[2], tg, 0.125)
+            with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+                loss.sum().backward()
+                torch.cuda.synchronize()
+            n_mask = sum("relu_mask" in e.name for e in prof.events()
+                         if e.device_type == torch.autograd.DeviceType.CUDA)
+            return [x.grad] + [w.grad for w in ws], n_mask
+        finally:
+            cnn.set_fused_unpool(True)
+
+    (a, na), (b, nb) = run(True), run(False)
+    assert na == 0 and nb == 1  # the dual output replaced the relu_mask pass
+    for ga, gb in zip(a, b):
+        assert torch.equal(ga, gb)
+
+
 @pytest.mark.parametrize("mode", ["sketch", "true_topk", "uncompressed"])
 def test_kept_conv_images_match_fresh_prep(mode):
     """ResNet-9 rounds through FedModel: the bf16 conv-weight images kept
