@@ -48,6 +48,8 @@ def main():
     p.add_argument("--wgrad-stream", default="on", choices=["on", "off"],
                    help="weight gradients on a side stream (utils/args.py --wgrad_stream)")
     p.add_argument("--profile", action="store_true", help="per-phase HIP event timings")
+    p.add_argument("--round-times", action="store_true",
+                   help="HIP event per timed round; adds round_ms (GPU ms per round) to the JSON")
     p.add_argument("--torch-profile", default=None,
                    help="after the timed steps, trace 5 more with torch.profiler into this dir")
     p.add_argument("--miopen-find", type=int, default=int(os.environ.get("COMMEFF_MIOPEN_FIND", "0")),
@@ -139,10 +141,17 @@ def main():
         fed.timer.counts.clear()
     t0 = time.perf_counter()
     host_s = 0.0  # host time spent enqueueing (no syncs inside a round)
+    evs = []
+    if b.round_times:
+        evs.append(torch.cuda.Event(enable_timing=True))
+        evs[-1].record()
     for i in range(b.warmup, b.warmup + b.steps):
         h0 = time.perf_counter()
         out = step(i)
         host_s += time.perf_counter() - h0
+        if b.round_times:
+            evs.append(torch.cuda.Event(enable_timing=True))
+            evs[-1].record()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -200,6 +209,8 @@ def main():
             "backend": ctx.backend, "weights_checksum": checksum,
             **({"rehearsal": "gloo, ranks sharing one GPU"} if rehearsal and N > 1 else {}),
             "host_enqueue_ms_per_step": round(host_s / b.steps * 1000.0, 3),
+            **({"round_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(evs) - 1)]}
+               if evs else {}),
         }), flush=True)
     dist.barrier()
     dist.shutdown()

@@ -1319,9 +1319,9 @@ void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
     a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     const dim3 grid(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB)));
     if (transposed)
-      hipLaunchKernelGGL(attn_long_fwd_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
+      COMMEFF_LAUNCH(attn_long_fwd_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
     else
-      hipLaunchKernelGGL(attn_long_fwd_kernel, grid, dim3(256), kLongFwdLds, stream, a);
+      COMMEFF_LAUNCH(attn_long_fwd_kernel, grid, dim3(256), kLongFwdLds, stream, a);
     return;
   }
   static bool attr = false;
@@ -1332,7 +1332,7 @@ void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
   }
   a.thresh = attn_thresh(p_drop);
   a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(static_cast<uint32_t>(nseq * a.nh)), dim3(256), kFwdLds,
+  COMMEFF_LAUNCH(attn_fwd_kernel, dim3(static_cast<uint32_t>(nseq * a.nh)), dim3(256), kFwdLds,
                      stream, a);
 }
 
@@ -1361,9 +1361,9 @@ void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
     a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     const dim3 grid(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB)));
     if (dq_t)
-      hipLaunchKernelGGL(attn_long_dq_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
+      COMMEFF_LAUNCH(attn_long_dq_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
     else
-      hipLaunchKernelGGL(attn_long_dq_kernel, grid, dim3(256), kLongDqLds, stream, a);
+      COMMEFF_LAUNCH(attn_long_dq_kernel, grid, dim3(256), kLongDqLds, stream, a);
     static const bool dkdv_s = [] {  // COMMEFF_ATTN_DKDV_S=0: the P / dS-image dK dV kernel
       const char* e = getenv("COMMEFF_ATTN_DKDV_S");
       return !(e != nullptr && e[0] == '0');
@@ -1375,9 +1375,9 @@ void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongDkdvSLds));
         sattr = true;
       }
-      hipLaunchKernelGGL(attn_long_dkdv_s_kernel, grid, dim3(256), kLongDkdvSLds, stream, a);
+      COMMEFF_LAUNCH(attn_long_dkdv_s_kernel, grid, dim3(256), kLongDkdvSLds, stream, a);
     } else {
-      hipLaunchKernelGGL(attn_long_dkdv_kernel, grid, dim3(256), kLongDkdvLds, stream, a);
+      COMMEFF_LAUNCH(attn_long_dkdv_kernel, grid, dim3(256), kLongDkdvLds, stream, a);
     }
     return;
   }
@@ -1389,7 +1389,7 @@ void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
   }
   a.thresh = attn_thresh(p_drop);
   a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(static_cast<uint32_t>(nseq * a.nh)), dim3(256), kBwdLds,
+  COMMEFF_LAUNCH(attn_bwd_kernel, dim3(static_cast<uint32_t>(nseq * a.nh)), dim3(256), kBwdLds,
                      stream, a);
 }
 

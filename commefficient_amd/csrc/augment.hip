@@ -95,7 +95,7 @@ void launch_augment_u8_nhwc(const uint8_t* data, const int64_t* idx, int64_t B, 
   int64_t npix = B * H * W;
   int64_t blocks = (npix + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(augment_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
+  COMMEFF_LAUNCH(augment_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
                      data, idx, B, H, W, C, pad, flip, mean, inv_std, seed, keys, out_bf16,
                      out_cstride, targets, yout);
 }

@@ -2158,18 +2158,18 @@ TORCH_LIBRARY(commeff, m) {
   m.def("cs_zero_buckets(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, Tensor hashes, "
         "Tensor blk_off, Tensor blk_sign, int num_blocks, int d) -> ()");
   m.def("cs_l2estimate(Tensor table) -> Tensor");
-  m.def("cs_region_encode(Tensor(a!) table, Tensor vec, float scale, Tensor? wvec, float wscale, int m, "
+  m.def("cs_region_encode(Tensor(a!) table, Tensor(b!) vec, float scale, Tensor? wvec, float wscale, int m, "
         "int g, int W, Tensor perm, Tensor cinfo, Tensor lists, Tensor goffs, bool overwrite=False, "
         "bool zero_vec=False) -> ()");
   m.def("cs_region_query(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
         "Tensor goffs, int q0=0, int q1=-1) -> Tensor");
   m.def("cs_region_topk(Tensor(a!) table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
-        "Tensor goffs, int k, Tensor? hint=None, int q0=0, int q1=-1, Tensor(b!)? momV=None, Tensor? momG=None, "
+        "Tensor goffs, int k, Tensor(d!)? hint=None, int q0=0, int q1=-1, Tensor(b!)? momV=None, Tensor? momG=None, "
         "float rho=0.0, float gscale=0.0, int mom_mode=0, Tensor(c!)? ws=None) -> (Tensor, Tensor)");
   m.def("cs_region_topk_ws_bytes(int d, int m, int q0, int q1) -> int", &commeff::cs_region_topk_ws_bytes);
   m.def("cs_region_zero(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, int d, int m, int g, "
         "Tensor perm, Tensor cinfo) -> ()");
-  m.def("topk_abs(Tensor x, int k, Tensor? hint=None) -> (Tensor, Tensor)");
+  m.def("topk_abs(Tensor x, int k, Tensor(a!)? hint=None) -> (Tensor, Tensor)");
   m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
   m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "
         "Tensor(b!)? last_mod, int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");

@@ -529,21 +529,21 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
                    float* stat, float* ab, bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream,
                    const uint16_t* addend, uint8_t* relu_bits) {
   const int S = bn_slabs(G, M);
-  hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
+  COMMEFF_LAUNCH(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
                      nullptr, C, M, S, part);
   if (G >= 2 && G < kGL) {
     // per-group mean / var behind the partial sums (bn_scratch_floats)
     float* gmv = part + static_cast<size_t>(G) * S * 2 * C;
-    hipLaunchKernelGGL(bn_fwd_finalize_group_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
+    COMMEFF_LAUNCH(bn_fwd_finalize_group_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
                        x, part, w, b, C, M, S, eps, stat, ab, gmv);
-    hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gmv, C, M, G,
+    COMMEFF_LAUNCH(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gmv, C, M, G,
                        momentum, run_mean, run_var, nbt);
   } else {
-    hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part,
+    COMMEFF_LAUNCH(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part,
                        w, b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var, nbt);
   }
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
-  hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
+  COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                      nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
                      const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr);
 }
@@ -553,23 +553,23 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw, float* gdb,
                    int64_t gstride, uint16_t* dadd) {
   const int S = bn_slabs(G, M);
-  hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
+  COMMEFF_LAUNCH(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
                      S, part);
   if (G >= 2 && G < kGL) {
     float* gsum = part + static_cast<size_t>(G) * S * 2 * C;  // see bn_scratch_floats
     const bool grouped = gdw != nullptr;
-    hipLaunchKernelGGL(bn_bwd_finalize_group_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
+    COMMEFF_LAUNCH(bn_bwd_finalize_group_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
                        part, stat, w, C, M, S, coef, gdw, gdb, gstride,
                        (!grouped && (dw != nullptr || db != nullptr)) ? gsum : nullptr);
     if (!grouped && (dw != nullptr || db != nullptr))
-      hipLaunchKernelGGL(bn_dwdb_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gsum, C, G, dw, db,
+      COMMEFF_LAUNCH(bn_dwdb_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gsum, C, G, dw, db,
                          beta);
   } else {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat,
+    COMMEFF_LAUNCH(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat,
                        w, C, M, S, G, coef, dw, db, beta, gdw, gdb, gstride);
   }
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
-  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
+  COMMEFF_LAUNCH(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
                      coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd, nullptr);
 }
 

@@ -1190,10 +1190,10 @@ void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits,
                          int64_t gstride, int groups, hipStream_t stream) {
   const dim3 grid(K * (C / 64), groups);
   if (splits >= 32)
-    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
+    COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
                        beta, gstride);
   else
-    hipLaunchKernelGGL(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
+    COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
                        beta, gstride);
 }
 
@@ -1320,7 +1320,7 @@ void launch_fwd(const ConvFwdArgs& a, hipStream_t stream) {
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  hipLaunchKernelGGL((conv_fwd_kernel<TBM, BN, NSTAGE, POOL>), dim3(mt * (a.K / BN)), dim3(TBM * 2),
+  COMMEFF_LAUNCH((conv_fwd_kernel<TBM, BN, NSTAGE, POOL>), dim3(mt * (a.K / BN)), dim3(TBM * 2),
                      lds, stream, a);
 }
 
@@ -1333,7 +1333,7 @@ void launch_wgrad(const ConvWgradArgs& a, hipStream_t stream) {
     init = true;
   }
   const int tiles = wgrad_tiles(a.K, a.C);
-  hipLaunchKernelGGL((conv_wgrad_kernel<BN, NSTAGE, ROWSTEP, PAIR>), dim3(tiles * a.splits), dim3(256),
+  COMMEFF_LAUNCH((conv_wgrad_kernel<BN, NSTAGE, ROWSTEP, PAIR>), dim3(tiles * a.splits), dim3(256),
                      lds, stream, a);
 }
 
@@ -1397,7 +1397,7 @@ void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t strea
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  hipLaunchKernelGGL((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), dim3(mt * (a.K / BN)),
+  COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), dim3(mt * (a.K / BN)),
                      dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
 }
 
@@ -1513,14 +1513,14 @@ void launch_wgrad_wide(const ConvWgradArgs& a, hipStream_t stream) {
       set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 2>), lds);
       init = true;
     }
-    hipLaunchKernelGGL((conv_wgrad_wide_kernel<ROWSTEP, 2>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 2>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
   } else {
     static bool init = false;
     if (!init) {
       set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 1>), lds);
       init = true;
     }
-    hipLaunchKernelGGL((conv_wgrad_wide_kernel<ROWSTEP, 1>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 1>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
   }
 }
 
@@ -1581,9 +1581,9 @@ void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_
       init = true;
     }
     if (stages == 3)
-      hipLaunchKernelGGL(conv_wgrad_halo_kernel<3>, dim3(tiles * a.splits), dim3(256), 3 * stage_bytes, stream, a);
+      COMMEFF_LAUNCH(conv_wgrad_halo_kernel<3>, dim3(tiles * a.splits), dim3(256), 3 * stage_bytes, stream, a);
     else
-      hipLaunchKernelGGL(conv_wgrad_halo_kernel<2>, dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
+      COMMEFF_LAUNCH(conv_wgrad_halo_kernel<2>, dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
   } else if (wgrad_wide(a.K, a.C)) {
     if (rowstep) launch_wgrad_wide<true>(a, stream); else launch_wgrad_wide<false>(a, stream);
   } else if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)
@@ -1642,7 +1642,7 @@ __global__ void __launch_bounds__(256) conv_images_patch_kernel(ConvPatchBatch b
 void launch_conv_images_patch(const ConvPatchBatch& b, const int64_t* idx, int64_t k,
                               hipStream_t stream) {
   if (k <= 0 || b.n <= 0) return;
-  hipLaunchKernelGGL(conv_images_patch_kernel, dim3(static_cast<uint32_t>((k + 255) / 256)), dim3(256), 0,
+  COMMEFF_LAUNCH(conv_images_patch_kernel, dim3(static_cast<uint32_t>((k + 255) / 256)), dim3(256), 0,
                      stream, b, idx, k);
 }
 
@@ -1653,13 +1653,13 @@ void launch_conv_weight_prep(ConvPrepBatch b, hipStream_t stream) {
     blocks += ((b.t[i].K + kPT - 1) / kPT) * ((b.t[i].C + kPT - 1) / kPT);
   }
   if (blocks == 0) return;
-  hipLaunchKernelGGL(conv_weight_prep_kernel, dim3(blocks), dim3(256), 0, stream, b);
+  COMMEFF_LAUNCH(conv_weight_prep_kernel, dim3(blocks), dim3(256), 0, stream, b);
 }
 
 void launch_relu_mask(const uint16_t* gy, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream) {
   const int64_t n8 = n / 8;
-  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(n8, 256)), dim3(256), 0, stream,
+  COMMEFF_LAUNCH(relu_mask_kernel, dim3(grid_for(n8, 256)), dim3(256), 0, stream,
                      reinterpret_cast<const v4u*>(gy), reinterpret_cast<const v4u*>(y),
                      reinterpret_cast<v4u*>(g), n8);
 }

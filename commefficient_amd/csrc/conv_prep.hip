@@ -382,7 +382,7 @@ void launch_conv_prep_fwd(ConvPrepArgs a, hipStream_t stream) {
   }();
   int blocks = (ntiles + 4 * tpw - 1) / (4 * tpw);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(prep_fwd_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, stream, a);
+  COMMEFF_LAUNCH(prep_fwd_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, stream, a);
 }
 
 void launch_conv_prep_wgrad(ConvPrepArgs a, float* dw, float beta, hipStream_t stream) {
@@ -391,8 +391,8 @@ void launch_conv_prep_wgrad(ConvPrepArgs a, float* dw, float beta, hipStream_t s
   const int nb = conv_prep_wgrad_blocks(a.P);
   const int steps = (a.P + 63) / 64;
   const int spb = (steps + nb - 1) / nb;
-  hipLaunchKernelGGL(prep_wgrad_kernel, dim3(nb), dim3(256), 0, stream, a, spb);
-  hipLaunchKernelGGL(prep_wgrad_reduce_kernel, dim3((kPrepK * 27 + 15) / 16), dim3(256), 0, stream,
+  COMMEFF_LAUNCH(prep_wgrad_kernel, dim3(nb), dim3(256), 0, stream, a, spb);
+  COMMEFF_LAUNCH(prep_wgrad_reduce_kernel, dim3((kPrepK * 27 + 15) / 16), dim3(256), 0, stream,
                      a.partial, nb, a.Cin, dw, beta);
 }
 

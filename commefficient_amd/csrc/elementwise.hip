@@ -525,12 +525,12 @@ void launch_momentum_ef(float* V, float* E, const float* G, int64_t n, float rho
   if (n <= 0) return;
   int64_t n4 = (aligned16(V) && aligned16(E) && aligned16(G)) ? n / 4 : 0;
   if (n4 > 0)
-    hipLaunchKernelGGL(momentum_ef_kernel, dim3(grid_for(n4)), dim3(kBlock), 0, stream,
+    COMMEFF_LAUNCH(momentum_ef_kernel, dim3(grid_for(n4)), dim3(kBlock), 0, stream,
                        reinterpret_cast<float4*>(V), reinterpret_cast<float4*>(E),
                        reinterpret_cast<const float4*>(G), n4, rho, gscale, mode);
   int64_t start = n4 * 4;
   if (start < n)
-    hipLaunchKernelGGL(momentum_ef_tail, dim3((n - start + kBlock - 1) / kBlock), dim3(kBlock), 0,
+    COMMEFF_LAUNCH(momentum_ef_tail, dim3((n - start + kBlock - 1) / kBlock), dim3(kBlock), 0,
                        stream, V, E, G, start, n, rho, gscale, mode);
 }
 
@@ -538,7 +538,7 @@ void launch_sparse_apply(float* w, const int64_t* idx, const float* vals, int64_
                          const float* lr_vec, int32_t* last_mod, int32_t round,
                          const int32_t* step, int32_t* hist, hipStream_t stream) {
   if (k <= 0) return;
-  hipLaunchKernelGGL(sparse_apply_kernel<false>, dim3((k + kApplyBlock - 1) / kApplyBlock), dim3(kApplyBlock),
+  COMMEFF_LAUNCH(sparse_apply_kernel<false>, dim3((k + kApplyBlock - 1) / kApplyBlock), dim3(kApplyBlock),
                      0, stream, w, idx, vals, k, lr, lr_vec, last_mod, round, step, hist, rh::RegionZero{});
 }
 
@@ -551,7 +551,7 @@ void launch_sparse_apply_region_zero(float* w, const int64_t* idx, const float* 
   const rh::RegionZero rz{t1, t2, perm, cinfo, static_cast<uint32_t>(r), static_cast<uint32_t>(c),
                           static_cast<uint32_t>(m), static_cast<uint32_t>(nch), static_cast<uint64_t>(d)};
   // 256-thread blocks: 4x the blocks of the plain apply for the scattered zeroing
-  hipLaunchKernelGGL(sparse_apply_kernel<true>, dim3((k + 255) / 256), dim3(256), 0, stream, w, idx, vals, k, lr,
+  COMMEFF_LAUNCH(sparse_apply_kernel<true>, dim3((k + 255) / 256), dim3(256), 0, stream, w, idx, vals, k, lr,
                      lr_vec, last_mod, round, step, hist, rz);
 }
 
@@ -561,7 +561,7 @@ void launch_dense_apply(float* w, const float* delta, int64_t n, float lr, const
   if (n <= 0) return;
   int64_t nb = (n + kApplyBlock - 1) / kApplyBlock;
   if (nb > 512) nb = 512;  // each block flushes its LDS histogram window once
-  hipLaunchKernelGGL(dense_apply_kernel, dim3(static_cast<int>(nb)), dim3(kApplyBlock), 0, stream, w,
+  COMMEFF_LAUNCH(dense_apply_kernel, dim3(static_cast<int>(nb)), dim3(kApplyBlock), 0, stream, w,
                      delta, n, lr, lr_vec, last_mod, round, step, hist);
 }
 
@@ -569,7 +569,7 @@ void launch_account_hist(const int32_t* hist, int nbins, const int64_t* meta, in
                          double* client_dl, double* client_ul, double upc, double* dl,
                          hipStream_t stream) {
   if (W <= 0) return;
-  hipLaunchKernelGGL(account_hist_kernel, dim3(1), dim3(1024), 0, stream, hist, nbins, meta, W,
+  COMMEFF_LAUNCH(account_hist_kernel, dim3(1), dim3(1024), 0, stream, hist, nbins, meta, W,
                      client_dl, client_ul, upc, dl);
 }
 
@@ -578,10 +578,10 @@ void launch_count_ge(const int32_t* last_mod, int64_t n, const int32_t* thr, int
   // counts must hold 2*(T+1) int64: [0, T+1) scratch bins, [T+1, 2T+1) output
   if (T <= 0) return;
   unsigned long long* bins = reinterpret_cast<unsigned long long*>(counts);
-  (void)hipMemsetAsync(bins, 0, (T + 1) * sizeof(unsigned long long), stream);
-  hipLaunchKernelGGL(count_ge_kernel, dim3(grid_for(n, 1024)), dim3(kBlock), 0, stream, last_mod,
+  tape_memset(bins, 0, (T + 1) * sizeof(unsigned long long), stream);
+  COMMEFF_LAUNCH(count_ge_kernel, dim3(grid_for(n, 1024)), dim3(kBlock), 0, stream, last_mod,
                      n, thr, T, bins);
-  hipLaunchKernelGGL(count_ge_finish, dim3(1), dim3(64), 0, stream, bins, T, counts + T + 1);
+  COMMEFF_LAUNCH(count_ge_finish, dim3(1), dim3(64), 0, stream, bins, T, counts + T + 1);
 }
 
 int account_round_blocks(int64_t n) { return grid_for(n, 256); }
@@ -591,51 +591,51 @@ void launch_account_round(const int32_t* last_mod, int64_t n, const int64_t* met
                           double* dl, hipStream_t stream) {
   const int nb = account_round_blocks(n);
   if (T > 0)
-    hipLaunchKernelGGL(count_partial_kernel, dim3(nb), dim3(kBlock), 0, stream, last_mod, n, meta, T,
+    COMMEFF_LAUNCH(count_partial_kernel, dim3(nb), dim3(kBlock), 0, stream, last_mod, n, meta, T,
                        partial);
-  hipLaunchKernelGGL(account_finish_kernel, dim3(1), dim3(1024), 0, stream, partial, T > 0 ? nb : 0, T,
+  COMMEFF_LAUNCH(account_finish_kernel, dim3(1), dim3(1024), 0, stream, partial, T > 0 ? nb : 0, T,
                      meta, W, client_dl, client_ul, upc, dl);
 }
 
 void launch_axpby(float* out, const float* a, float alpha, const float* b, float beta, int64_t n,
                   hipStream_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, out, a, alpha, b,
+  COMMEFF_LAUNCH(axpby_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, out, a, alpha, b,
                      beta, n);
 }
 
 void launch_l2norm(const float* x, int64_t n, float* partial, float* out, hipStream_t stream) {
   int nb = grid_for(n, 1024);
-  hipLaunchKernelGGL(sqsum_kernel, dim3(nb), dim3(kBlock), 0, stream, x, n, partial);
-  hipLaunchKernelGGL(sqrt_sum_kernel, dim3(1), dim3(1024), 0, stream, partial, nb, out);
+  COMMEFF_LAUNCH(sqsum_kernel, dim3(nb), dim3(kBlock), 0, stream, x, n, partial);
+  COMMEFF_LAUNCH(sqrt_sum_kernel, dim3(1), dim3(1024), 0, stream, partial, nb, out);
 }
 
 void launch_clip_noise(float* x, int64_t n, const float* norm, float clip, float noise_std,
                        uint64_t seed, uint64_t offset, hipStream_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(clip_noise_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, x, n, norm,
+  COMMEFF_LAUNCH(clip_noise_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, x, n, norm,
                      clip, noise_std, seed, offset);
 }
 
 void launch_client_state(const float* g, float* u, float* e, int64_t n, float rho,
                          hipStream_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(client_state_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, u, e, n,
+  COMMEFF_LAUNCH(client_state_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, g, u, e, n,
                      rho);
 }
 
 void launch_zero_at(float* a, float* b, float* c, const int64_t* idx, int64_t k,
                     hipStream_t stream) {
   if (k <= 0) return;
-  hipLaunchKernelGGL(zero_at_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, a,
+  COMMEFF_LAUNCH(zero_at_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, a,
                      b, c, idx, k);
 }
 
 void launch_scatter_dense(float* out, int64_t n, const int64_t* idx, const float* vals, int64_t k,
                           hipStream_t stream) {
-  (void)hipMemsetAsync(out, 0, n * sizeof(float), stream);
+  tape_memset(out, 0, n * sizeof(float), stream);
   if (k <= 0) return;
-  hipLaunchKernelGGL(scatter_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out,
+  COMMEFF_LAUNCH(scatter_kernel, dim3((k + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, out,
                      idx, vals, k);
 }
 

@@ -203,13 +203,13 @@ void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream) {
   const int steps = (a.T + GBK - 1) / GBK;
   a.steps_per_split = (steps + a.splits - 1) / a.splits;
   const int tiles = (a.M / 256) * (a.N / 256);
-  hipLaunchKernelGGL(gemm_tn_acc_kernel, dim3(static_cast<uint32_t>(tiles * a.splits)), dim3(512),
+  COMMEFF_LAUNCH(gemm_tn_acc_kernel, dim3(static_cast<uint32_t>(tiles * a.splits)), dim3(512),
                      kGemmLds, stream, a);
   if (a.splits > 1) {
     const int64_t n4 = static_cast<int64_t>(a.M) * a.N / 4;
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
+    COMMEFF_LAUNCH(gemm_tn_reduce_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
                        a.C, a.ldc, a.slab, a.M, a.N, a.splits);
   }
 }

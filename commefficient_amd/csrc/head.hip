@@ -247,7 +247,7 @@ void launch_head_fwd(const uint16_t* x, const float* w, const int64_t* tgt, int 
                      hipStream_t stream) {
   if (B <= 0) return;
   // two waves (examples) per block: 250 blocks for B = 500 fill the 256 CUs
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 1) / 2), dim3(128), 0, stream, x, w, tgt, B, C, NPIX, NCLS,
+  COMMEFF_LAUNCH(head_fwd_kernel, dim3((B + 1) / 2), dim3(128), 0, stream, x, w, tgt, B, C, NPIX, NCLS,
                      scale, loss, correct, gunit, pooled, codes);
 }
 
@@ -257,7 +257,7 @@ void launch_head_bwd(const float* gl, const float* gunit, const float* w, const 
   const int nrow = (B + 3) / 4;
   const int nw = NCLS * ((C + 63) / 64);
   if (nrow + nw <= 0) return;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(nrow + nw), dim3(256), 0, stream, gl, gunit, w, pooled, codes, B, C,
+  COMMEFF_LAUNCH(head_bwd_kernel, dim3(nrow + nw), dim3(256), 0, stream, gl, gunit, w, pooled, codes, B, C,
                      NPIX, NCLS, scale, nrow, dx, dw, beta, ymask, dxm);
 }
 

@@ -374,9 +374,9 @@ void launch_im2col(const Im2colArgs& a, hipStream_t stream) {
   q.d_s = make_fastdiv(a.S);
   q.d_c = make_fastdiv(a.C);
   if (a.vec)
-    hipLaunchKernelGGL(im2col_vec_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, a.x, a.col, q);
+    COMMEFF_LAUNCH(im2col_vec_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, a.x, a.col, q);
   else
-    hipLaunchKernelGGL(im2col_any_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, a.x, a.col, q);
+    COMMEFF_LAUNCH(im2col_any_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, a.x, a.col, q);
 }
 
 void launch_col2im(const Im2colArgs& a, const uint16_t* gcol, uint16_t* gx, hipStream_t stream) {
@@ -389,13 +389,13 @@ void launch_col2im(const Im2colArgs& a, const uint16_t* gcol, uint16_t* gx, hipS
   q.d_c8 = make_fastdiv(a.C / 8);
   q.d_w = make_fastdiv(a.W);
   q.d_h = make_fastdiv(a.H);
-  hipLaunchKernelGGL(col2im_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gcol, gx, q);
+  COMMEFF_LAUNCH(col2im_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gcol, gx, q);
 }
 
 void launch_weight_rsc(const float* w, uint16_t* out, int K, int C, int RS, int Kc, hipStream_t stream) {
   const int64_t total = static_cast<int64_t>(K) * Kc;
   if (total == 0) return;
-  hipLaunchKernelGGL(weight_rsc_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, w, out, K, C, RS,
+  COMMEFF_LAUNCH(weight_rsc_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, w, out, K, C, RS,
                      Kc);
 }
 
@@ -406,11 +406,11 @@ void launch_wgrad_rsc_add(float* dst, int64_t dst_ld, const float* src, int G, i
   const bool al16 = reinterpret_cast<uintptr_t>(dst) % 16 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
                     (G == 1 || dst_ld % 4 == 0);
   if (RS == 1 && Kc == C && (K * C) % 4 == 0 && al16) {
-    hipLaunchKernelGGL(wgrad_split_add4_kernel, dim3(blocks_for(total / 4)), dim3(256), 0, stream, dst, dst_ld,
+    COMMEFF_LAUNCH(wgrad_split_add4_kernel, dim3(blocks_for(total / 4)), dim3(256), 0, stream, dst, dst_ld,
                        src, G, splits, K * C, accumulate ? 1 : 0);
     return;
   }
-  hipLaunchKernelGGL(wgrad_rsc_add_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, dst, dst_ld, src,
+  COMMEFF_LAUNCH(wgrad_rsc_add_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, dst, dst_ld, src,
                      G, splits, K, C, RS, Kc, accumulate ? 1 : 0);
 }
 
@@ -426,7 +426,7 @@ void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* codes, int N, i
   q.d_c8 = make_fastdiv(C / 8);
   q.d_w = make_fastdiv(q.OW);
   q.d_h = make_fastdiv(q.OH);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, x, y, codes, q);
+  COMMEFF_LAUNCH(maxpool_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, x, y, codes, q);
 }
 
 void launch_maxpool_bwd(const uint16_t* gy, const uint8_t* codes, uint16_t* gx, int N, int H, int W, int C,
@@ -441,7 +441,7 @@ void launch_maxpool_bwd(const uint16_t* gy, const uint8_t* codes, uint16_t* gx, 
   q.d_c8 = make_fastdiv(C / 8);
   q.d_w = make_fastdiv(W);
   q.d_h = make_fastdiv(H);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gy, codes, gx, q);
+  COMMEFF_LAUNCH(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gy, codes, gx, q);
 }
 
 }  // namespace commeff

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime_api.h>
 #include <cstdint>
 #include "sketch_hash.h"
+#include "launch.h"
 
 namespace commeff {
 

@@ -1,0 +1,69 @@
+// Kernel launches of the native extension, with an optional launch tape.
+//
+// Every launcher in csrc/*.hip launches through COMMEFF_LAUNCH (and clears
+// memory through tape_memset).  Normally that is a plain hipLaunchKernel.
+// While a launch tape is recording (tape_begin .. tape_end, driven by
+// parallel/tape.py), each launch is also appended to the tape as a closure
+// holding a by-value copy of the kernel's arguments (device pointers, scalars,
+// argument structs), its grid, block and dynamic LDS size.  Replaying the tape
+// re-issues exactly those launches, in recording order, on the caller's
+// stream: a whole federated round (~45 kernels) costs the host ~45
+// hipLaunchKernel calls instead of a Python pass through autograd, the
+// dispatcher and the engine's bookkeeping.
+//
+// A tape is only valid while every buffer it points at stays where it was at
+// recording time; parallel/tape.py records under a PyTorch graph-capture
+// private memory pool (so intermediates keep their addresses) and checks that
+// the captured HIP graph holds exactly as many kernel / memset nodes as the
+// tape (no launch that bypassed COMMEFF_LAUNCH, e.g. a PyTorch kernel).
+// Per-round scalars (learning rate, round index) must therefore reach the
+// recorded kernels through device memory, never as launch arguments.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+#include <functional>
+#include <tuple>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+namespace commeff {
+
+struct LaunchTape {
+  std::vector<std::function<void(hipStream_t)>> ops;
+};
+
+// non-null while a tape records (set/cleared by the bindings, tape.cpp)
+LaunchTape* tape_active();
+
+template <typename F, typename T, size_t... I>
+inline void launch_from_tuple(F k, dim3 g, dim3 b, uint32_t sh, hipStream_t s, T& args,
+                              std::index_sequence<I...>) {
+  void* argv[sizeof...(I) > 0 ? sizeof...(I) : 1] = {static_cast<void*>(&std::get<I>(args))...};
+  (void)hipLaunchKernel(reinterpret_cast<const void*>(k), g, b, argv, sh, s);
+}
+
+template <typename... P, typename... A>
+inline void tape_launch(void (*k)(P...), dim3 g, dim3 b, uint32_t sh, hipStream_t s, A&&... a) {
+  static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+  using Tup = std::tuple<std::decay_t<P>...>;
+  Tup args(static_cast<std::decay_t<P>>(std::forward<A>(a))...);
+  if (LaunchTape* t = tape_active()) {
+    t->ops.emplace_back([k, g, b, sh, args](hipStream_t st) mutable {
+      launch_from_tuple(k, g, b, sh, st, args, std::index_sequence_for<P...>{});
+    });
+  }
+  launch_from_tuple(k, g, b, sh, s, args, std::index_sequence_for<P...>{});
+}
+
+inline void tape_memset(void* p, int v, size_t n, hipStream_t s) {
+  if (LaunchTape* t = tape_active()) {
+    t->ops.emplace_back([p, v, n](hipStream_t st) { (void)hipMemsetAsync(p, v, n, st); });
+  }
+  (void)hipMemsetAsync(p, v, n, s);
+}
+
+}  // namespace commeff
+
+#define COMMEFF_LAUNCH(kernel, grid, block, shmem, stream, ...) \
+  ::commeff::tape_launch(kernel, grid, block, shmem, stream, ##__VA_ARGS__)

@@ -86,11 +86,11 @@ void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int 
   if (B == 0) return;
   const dim3 grid(static_cast<uint32_t>((B + 3) / 4));
   if (bf16)
-    hipLaunchKernelGGL(ce_fwd_kernel<uint16_t>, grid, dim3(256), 0, stream,
+    COMMEFF_LAUNCH(ce_fwd_kernel<uint16_t>, grid, dim3(256), 0, stream,
                        static_cast<const uint16_t*>(x), tgt, B, C, loss, correct,
                        static_cast<uint16_t*>(grad));
   else
-    hipLaunchKernelGGL(ce_fwd_kernel<float>, grid, dim3(256), 0, stream,
+    COMMEFF_LAUNCH(ce_fwd_kernel<float>, grid, dim3(256), 0, stream,
                        static_cast<const float*>(x), tgt, B, C, loss, correct,
                        static_cast<float*>(grad));
 }
@@ -128,7 +128,7 @@ void launch_client_means(const ClientMeanRows& rows, const int64_t* slot, int n,
                          bool counts_f32, int W, float* out, hipStream_t stream) {
   const int total = rows.m * W;
   if (total <= 0) return;
-  hipLaunchKernelGGL(client_means_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, rows, slot,
+  COMMEFF_LAUNCH(client_means_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, rows, slot,
                      n, counts, counts_f32, W, out);
 }
 

@@ -148,10 +148,10 @@ void launch_relu_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* idx, int N
   if (total == 0) return;
   const PoolGeom q = make_pool_geom(N, H, W, C, k);
   if (k == 2)
-    hipLaunchKernelGGL(relu_maxpool_fwd_kernel<2>, dim3(grid_for(total)), dim3(256), 0, stream, x,
+    COMMEFF_LAUNCH(relu_maxpool_fwd_kernel<2>, dim3(grid_for(total)), dim3(256), 0, stream, x,
                        y, idx, q);
   else
-    hipLaunchKernelGGL(relu_maxpool_fwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, stream, x,
+    COMMEFF_LAUNCH(relu_maxpool_fwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, stream, x,
                        y, idx, q);
 }
 
@@ -161,10 +161,10 @@ void launch_relu_maxpool_bwd(const uint16_t* gy, const uint8_t* idx, uint16_t* g
   if (total == 0) return;
   const PoolGeom q = make_pool_geom(N, H, W, C, k);
   if (k == 2)
-    hipLaunchKernelGGL(relu_maxpool_bwd_kernel<2>, dim3(grid_for(total)), dim3(256), 0, stream,
+    COMMEFF_LAUNCH(relu_maxpool_bwd_kernel<2>, dim3(grid_for(total)), dim3(256), 0, stream,
                        gy, idx, gx, q);
   else
-    hipLaunchKernelGGL(relu_maxpool_bwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, stream,
+    COMMEFF_LAUNCH(relu_maxpool_bwd_kernel<4>, dim3(grid_for(total)), dim3(256), 0, stream,
                        gy, idx, gx, q);
 }
 

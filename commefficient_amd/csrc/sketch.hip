@@ -429,7 +429,7 @@ void launch_cs_encode(float* table, const float* vec, const float* wvec, float s
                       float wscale, const RowHashes& h, const SketchGeom& g,
                       const int32_t* blk_off, const float* blk_sign, hipStream_t stream) {
   if (g.d == 0) return;
-  hipLaunchKernelGGL(cs_encode_direct_kernel, dim3(grid_for(g.d, 256, 8192)), dim3(256), 0,
+  COMMEFF_LAUNCH(cs_encode_direct_kernel, dim3(grid_for(g.d, 256, 8192)), dim3(256), 0,
                      stream, table, vec, wvec, scale, wscale, to_args(h, g), g, blk_off,
                      blk_sign);
 }
@@ -460,7 +460,7 @@ void launch_cs_layout(const RowHashes& h, const SketchGeom& g, const int32_t* bl
                       hipStream_t stream) {
   if (g.d == 0) return;
   size_t lds = p.num_tiles * sizeof(uint32_t);
-  hipLaunchKernelGGL(cs_layout_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256), lds,
+  COMMEFF_LAUNCH(cs_layout_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256), lds,
                      stream, to_args(h, g), g, blk_off, blk_sign, counts,
                      static_cast<uint32_t>(p.num_tiles), static_cast<uint32_t>(p.chunk));
 }
@@ -478,7 +478,7 @@ void launch_cs_encode_binned(float* table, const float* vec, const float* wvec, 
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(cs_bin_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256),
+  COMMEFF_LAUNCH(cs_bin_kernel, dim3(static_cast<uint32_t>(p.num_chunks)), dim3(256),
                      bin_lds_bytes(p), stream, vec, wvec, scale, wscale, to_args(h, g), g,
                      blk_off, blk_sign, counts, base, entries,
                      static_cast<uint32_t>(p.num_tiles), static_cast<uint32_t>(p.chunk));
@@ -486,7 +486,7 @@ void launch_cs_encode_binned(float* table, const float* vec, const float* wvec, 
   uint32_t splits = static_cast<uint32_t>((512 + p.num_tiles - 1) / p.num_tiles);
   if (splits < 1) splits = 1;
   if (splits > 8) splits = 8;
-  hipLaunchKernelGGL(cs_accum_kernel, dim3(static_cast<uint32_t>(p.num_tiles) * splits),
+  COMMEFF_LAUNCH(cs_accum_kernel, dim3(static_cast<uint32_t>(p.num_tiles) * splits),
                      dim3(1024), 0, stream, table, seg, entries,
                      static_cast<uint32_t>(static_cast<int64_t>(g.r) * g.c), splits);
 }
@@ -497,11 +497,11 @@ void launch_cs_query(const float* table, float* est, const RowHashes& h, const S
   dim3 grid(grid_for(g.d, 256, 16384));
   HashArgs a = to_args(h, g);
   switch (g.r) {
-    case 1: hipLaunchKernelGGL(cs_query_kernel<1>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
-    case 3: hipLaunchKernelGGL(cs_query_kernel<3>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
-    case 5: hipLaunchKernelGGL(cs_query_kernel<5>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
-    case 7: hipLaunchKernelGGL(cs_query_kernel<7>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
-    default: hipLaunchKernelGGL(cs_query_kernel<0>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    case 1: COMMEFF_LAUNCH(cs_query_kernel<1>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    case 3: COMMEFF_LAUNCH(cs_query_kernel<3>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    case 5: COMMEFF_LAUNCH(cs_query_kernel<5>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    case 7: COMMEFF_LAUNCH(cs_query_kernel<7>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
+    default: COMMEFF_LAUNCH(cs_query_kernel<0>, grid, dim3(256), 0, stream, table, est, a, g, blk_off, blk_sign); break;
   }
 }
 
@@ -512,14 +512,14 @@ void launch_cs_query_rows(const float* table, float* vals, float* est, const Row
   HashArgs a = to_args(h, g);
   const dim3 grid(grid_for(g.d, 1024, 8192));
   for (uint32_t j = 0; j < g.r; ++j)
-    hipLaunchKernelGGL(cs_query_row_kernel, grid, dim3(256), 0, stream, table + static_cast<size_t>(j) * g.c,
+    COMMEFF_LAUNCH(cs_query_row_kernel, grid, dim3(256), 0, stream, table + static_cast<size_t>(j) * g.c,
                        vals + static_cast<size_t>(j) * g.d, a, g, blk_off, blk_sign, j);
   const dim3 g2(grid_for(g.d, 256, 16384));
   switch (g.r) {
-    case 5: hipLaunchKernelGGL(cs_median_rows_kernel<5>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
-    case 3: hipLaunchKernelGGL(cs_median_rows_kernel<3>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
-    case 1: hipLaunchKernelGGL(cs_median_rows_kernel<1>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
-    default: hipLaunchKernelGGL(cs_median_rows_kernel<0>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
+    case 5: COMMEFF_LAUNCH(cs_median_rows_kernel<5>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
+    case 3: COMMEFF_LAUNCH(cs_median_rows_kernel<3>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
+    case 1: COMMEFF_LAUNCH(cs_median_rows_kernel<1>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
+    default: COMMEFF_LAUNCH(cs_median_rows_kernel<0>, g2, dim3(256), 0, stream, vals, est, g.d, g.r); break;
   }
 }
 
@@ -527,15 +527,15 @@ void launch_cs_zero_buckets(float* t1, float* t2, const int64_t* idx, const floa
                             int64_t k, const RowHashes& h, const SketchGeom& g,
                             const int32_t* blk_off, const float* blk_sign, hipStream_t stream) {
   if (k <= 0) return;
-  hipLaunchKernelGGL(cs_zero_kernel, dim3((k + 255) / 256), dim3(256), 0, stream, t1, t2, idx,
+  COMMEFF_LAUNCH(cs_zero_kernel, dim3((k + 255) / 256), dim3(256), 0, stream, t1, t2, idx,
                      vals, k, to_args(h, g), g, blk_off, blk_sign);
 }
 
 void launch_cs_l2estimate(const float* table, int r, int64_t c, float* partial, float* out,
                           hipStream_t stream) {
   const int nb = 256;
-  hipLaunchKernelGGL(row_sqsum_kernel, dim3(nb, r), dim3(256), 0, stream, table, c, partial);
-  hipLaunchKernelGGL(l2est_final_kernel, dim3(1), dim3(64), 0, stream, partial, r, nb, out);
+  COMMEFF_LAUNCH(row_sqsum_kernel, dim3(nb, r), dim3(256), 0, stream, table, c, partial);
+  COMMEFF_LAUNCH(l2est_final_kernel, dim3(1), dim3(64), 0, stream, partial, r, nb, out);
 }
 
 }  // namespace commeff

@@ -760,7 +760,7 @@ void launch_cs_hash_all(const RowHashes& h, const SketchGeom& g, const int32_t* 
   if (g.d == 0) return;
   int64_t blocks = (static_cast<int64_t>(g.d) + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(hash_all_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
+  COMMEFF_LAUNCH(hash_all_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
                      h, g, blk_off, blk_sign, out);
 }
 
@@ -787,23 +787,23 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
                    (reinterpret_cast<uintptr_t>(a.src_info) % 16 == 0) && ch % 8 == 0;
   const bool fxp = p.dense && a.fx != nullptr;  // fixed-point dense P2
   switch (r) {
-    case 5: hipLaunchKernelGGL(enc_p1_kernel<5>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
-    case 3: hipLaunchKernelGGL(enc_p1_kernel<3>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
-    case 1: hipLaunchKernelGGL(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
-    default: hipLaunchKernelGGL(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+    case 5: COMMEFF_LAUNCH(enc_p1_kernel<5>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+    case 3: COMMEFF_LAUNCH(enc_p1_kernel<3>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+    case 1: COMMEFF_LAUNCH(enc_p1_kernel<1>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
+    default: COMMEFF_LAUNCH(enc_p1_kernel<0>, g1, dim3(1024), l1, stream, vec, wvec, scale, wscale, dd, rr, ch, a.src_info, a.vals, v16, fxp ? a.bmax : nullptr); break;
   }
   if (fxp) {
     const uint32_t splits = static_cast<uint32_t>(p.p2_splits);
     const uint32_t total = static_cast<uint32_t>(r * c);
-    hipLaunchKernelGGL(fx_max_kernel, dim3(1), dim3(1024), 0, stream, a.bmax,
+    COMMEFF_LAUNCH(fx_max_kernel, dim3(1), dim3(1024), 0, stream, a.bmax,
                        static_cast<uint32_t>(p.num_chunks), a.gmax);
-    hipLaunchKernelGGL(enc_p2_dense_fx_kernel, dim3(nt * splits), dim3(1024), p.tile * 8, stream,
+    COMMEFF_LAUNCH(enc_p2_dense_fx_kernel, dim3(nt * splits), dim3(1024), p.tile * 8, stream,
                        table, reinterpret_cast<long long*>(a.fx), a.gmax, a.vals, a.perm, a.p2_src,
                        a.p2_pos, static_cast<uint32_t>(p.tile), total,
                        static_cast<uint32_t>(p.num_chunks), splits, overwrite);
     if (splits > 1) {
       const uint32_t blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
-      hipLaunchKernelGGL(enc_fx_reduce_kernel, dim3(blocks), dim3(256), 0, stream, table,
+      COMMEFF_LAUNCH(enc_fx_reduce_kernel, dim3(blocks), dim3(256), 0, stream, table,
                          reinterpret_cast<const long long*>(a.fx), a.gmax, total,
                          static_cast<size_t>(p.num_tiles) * p.tile, splits, overwrite);
     }
@@ -813,16 +813,16 @@ void launch_cs_encode_planned(float* table, const float* vec, const float* wvec,
     // enough blocks for every CU: split each tile's chunk range
     uint32_t splits = static_cast<uint32_t>(p.p2_splits);
     if (overwrite && splits > 1) {
-      (void)hipMemsetAsync(table, 0, static_cast<size_t>(r) * c * sizeof(float), stream);
+      tape_memset(table, 0, static_cast<size_t>(r) * c * sizeof(float), stream);
     }
-    hipLaunchKernelGGL(enc_p2_dense_kernel, dim3(nt * splits), dim3(1024), p.tile * 4, stream, table,
+    COMMEFF_LAUNCH(enc_p2_dense_kernel, dim3(nt * splits), dim3(1024), p.tile * 4, stream, table,
                        a.vals, a.perm, a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
                        static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks), splits,
                        overwrite);
     return;
   }
   const size_t l2 = static_cast<size_t>(kPlanSegCap) * 4 + (2 * p.num_chunks + 1) * 4;
-  hipLaunchKernelGGL(enc_p2_kernel, dim3(nt), dim3(1024), l2, stream, table, a.vals, a.perm,
+  COMMEFF_LAUNCH(enc_p2_kernel, dim3(nt), dim3(1024), l2, stream, table, a.vals, a.perm,
                      a.csr, a.seg, a.p2_src, a.p2_pos, static_cast<uint32_t>(p.tile),
                      static_cast<uint32_t>(r * c), static_cast<uint32_t>(p.num_chunks), overwrite);
 }
@@ -848,7 +848,7 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
   // >= 8 blocks per CU (dense plans have few, long tiles)
   uint32_t splits = 4;
   while (nt * splits < 8 * static_cast<uint32_t>(device_cus()) && splits < 64) splits *= 2;
-  hipLaunchKernelGGL(qry_q1_kernel, dim3(nt * splits), dim3(256), p.tile * 4, stream, table,
+  COMMEFF_LAUNCH(qry_q1_kernel, dim3(nt * splits), dim3(256), p.tile * 4, stream, table,
                      a.ent_info, a.seg, a.vals, static_cast<uint32_t>(p.tile),
                      static_cast<uint32_t>(r * c), splits, a.base, nt, static_cast<uint32_t>(c0),
                      static_cast<uint32_t>(c1), static_cast<uint32_t>(p.num_chunks));
@@ -859,15 +859,15 @@ void launch_cs_query_planned(const float* table, float* est, int64_t d, int r, i
   const bool v16 = (reinterpret_cast<uintptr_t>(est) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(a.src_info) % 16 == 0) && ch % 8 == 0;
   if (p.dense) {
-    if (r == 5) hipLaunchKernelGGL((qry_q2_kernel<5, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0);
-    else hipLaunchKernelGGL((qry_q2_kernel<0, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0);
+    if (r == 5) COMMEFF_LAUNCH((qry_q2_kernel<5, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0);
+    else COMMEFF_LAUNCH((qry_q2_kernel<0, 4>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0);
     return;
   }
   switch (r) {
-    case 5: hipLaunchKernelGGL((qry_q2_kernel<5, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
-    case 3: hipLaunchKernelGGL((qry_q2_kernel<3, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
-    case 1: hipLaunchKernelGGL((qry_q2_kernel<1, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
-    default: hipLaunchKernelGGL((qry_q2_kernel<0, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
+    case 5: COMMEFF_LAUNCH((qry_q2_kernel<5, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
+    case 3: COMMEFF_LAUNCH((qry_q2_kernel<3, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
+    case 1: COMMEFF_LAUNCH((qry_q2_kernel<1, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
+    default: COMMEFF_LAUNCH((qry_q2_kernel<0, 2>), g2, dim3(1024), l2, stream, a.vals, dd, rr, ch, nt, a.src_info, a.base, a.off, est, v16, cc0); break;
   }
 }
 

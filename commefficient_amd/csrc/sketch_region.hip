@@ -396,7 +396,7 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
   do {                                                                                                   \
     static int done = 0;                                                                                 \
     set_lds_once(cs_region_encode_kernel<RR, SS, KK, HH>, lds, &done);                                   \
-    hipLaunchKernelGGL((cs_region_encode_kernel<RR, SS, KK, HH>), grid, block, lds, stream, table, vec, wvec, \
+    COMMEFF_LAUNCH((cs_region_encode_kernel<RR, SS, KK, HH>), grid, block, lds, stream, table, vec, wvec, \
                        scale, wscale, static_cast<uint32_t>(d), static_cast<uint32_t>(c),                \
                        static_cast<uint32_t>(m), static_cast<uint32_t>(g), static_cast<uint32_t>(G),     \
                        static_cast<uint32_t>(nch), static_cast<uint32_t>(r), perm, cinfo, lists, goffs,  \
@@ -433,7 +433,7 @@ void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t 
   do {                                                                                                   \
     static int done = 0;                                                                                 \
     set_lds_once(cs_region_query_kernel<RR, HH>, lds, &done);                                            \
-    hipLaunchKernelGGL((cs_region_query_kernel<RR, HH>), grid, block, lds, stream, table, est,           \
+    COMMEFF_LAUNCH((cs_region_query_kernel<RR, HH>), grid, block, lds, stream, table, est,           \
                        static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),     \
                        static_cast<uint32_t>(g), static_cast<uint32_t>(nch), static_cast<uint32_t>(r),   \
                        perm, cinfo, lists, goffs, static_cast<uint32_t>(q0), static_cast<uint32_t>(q1),  \
@@ -454,7 +454,7 @@ void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float
                            const uint32_t* cinfo, hipStream_t stream) {
   const int64_t n = k * r;
   if (n <= 0) return;
-  hipLaunchKernelGGL(cs_region_zero_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0,
+  COMMEFF_LAUNCH(cs_region_zero_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0,
                      stream, t1, t2, idx, vals, k, static_cast<uint64_t>(d), static_cast<uint32_t>(r),
                      static_cast<uint32_t>(c), static_cast<uint32_t>(m), static_cast<uint32_t>(nch), perm,
                      cinfo);

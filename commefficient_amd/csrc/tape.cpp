@@ -1,0 +1,120 @@
+// Launch tapes (csrc/launch.h): record the native kernel launches of one
+// federated round and replay them from C++ (parallel/tape.py drives this).
+//
+//   tape_begin()             start recording (every COMMEFF_LAUNCH / tape_memset
+//                            is appended to a new tape; launches still execute,
+//                            or are captured when the stream is capturing)
+//   tape_end() -> id         stop recording, keep the tape
+//   tape_replay(id)          re-issue the recorded launches on the current stream
+//   tape_size(id), tape_free(id)
+//   graph_node_counts(g)     [kernel, memcpy, memset, other] nodes of a captured
+//                            hipGraph_t (torch.cuda.CUDAGraph.raw_cuda_graph()):
+//                            the completeness check of a tape recorded under
+//                            stream capture
+//
+// Replaces the per-round Python enqueue of the reference's worker loop
+// (/root/reference/CommEfficient/fed_worker.py:26-138) and server step
+// (fed_aggregator.py:429-613) for rounds of fixed geometry.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hip/hip_runtime_api.h>
+#include <torch/library.h>
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "launch.h"
+
+namespace commeff {
+
+namespace {
+std::atomic<LaunchTape*> g_active{nullptr};
+std::mutex g_mu;
+std::map<int64_t, std::unique_ptr<LaunchTape>> g_tapes;
+int64_t g_next = 1;
+std::unique_ptr<LaunchTape> g_recording;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+}  // namespace
+
+LaunchTape* tape_active() { return g_active.load(std::memory_order_acquire); }
+
+namespace {
+
+void tape_begin() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(!g_recording, "tape_begin: a tape is already recording");
+  g_recording = std::make_unique<LaunchTape>();
+  g_active.store(g_recording.get(), std::memory_order_release);
+}
+
+int64_t tape_end() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  TORCH_CHECK(g_recording, "tape_end: no tape is recording");
+  g_active.store(nullptr, std::memory_order_release);
+  const int64_t id = g_next++;
+  g_tapes[id] = std::move(g_recording);
+  return id;
+}
+
+LaunchTape* get(int64_t id) {
+  auto it = g_tapes.find(id);
+  TORCH_CHECK(it != g_tapes.end(), "unknown launch tape ", id);
+  return it->second.get();
+}
+
+void tape_replay(int64_t id) {
+  LaunchTape* t;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    t = get(id);
+  }
+  const hipStream_t s = cur_stream();
+  for (auto& op : t->ops) op(s);
+}
+
+int64_t tape_size(int64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return static_cast<int64_t>(get(id)->ops.size());
+}
+
+void tape_free(int64_t id) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_tapes.erase(id);
+}
+
+std::vector<int64_t> graph_node_counts(int64_t graph) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(static_cast<intptr_t>(graph));
+  size_t n = 0;
+  TORCH_CHECK(hipGraphGetNodes(g, nullptr, &n) == hipSuccess, "hipGraphGetNodes failed");
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n > 0) TORCH_CHECK(hipGraphGetNodes(g, nodes.data(), &n) == hipSuccess, "hipGraphGetNodes failed");
+  std::vector<int64_t> cnt(4, 0);
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType ty;
+    TORCH_CHECK(hipGraphNodeGetType(nodes[i], &ty) == hipSuccess, "hipGraphNodeGetType failed");
+    switch (ty) {
+      case hipGraphNodeTypeKernel: ++cnt[0]; break;
+      case hipGraphNodeTypeMemcpy: ++cnt[1]; break;
+      case hipGraphNodeTypeMemset: ++cnt[2]; break;
+      case hipGraphNodeTypeEmpty: break;  // capture joins / forks
+      default: ++cnt[3]; break;
+    }
+  }
+  return cnt;
+}
+
+}  // namespace
+}  // namespace commeff
+
+TORCH_LIBRARY_FRAGMENT(commeff, m) {
+  m.def("tape_begin() -> ()", &commeff::tape_begin);
+  m.def("tape_end() -> int", &commeff::tape_end);
+  m.def("tape_replay(int id) -> ()", &commeff::tape_replay);
+  m.def("tape_size(int id) -> int", &commeff::tape_size);
+  m.def("tape_free(int id) -> ()", &commeff::tape_free);
+  m.def("graph_node_counts(int graph) -> int[]", &commeff::graph_node_counts);
+}

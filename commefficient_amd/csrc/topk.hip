@@ -596,7 +596,7 @@ int64_t topk_cand_workspace_bytes(int64_t n) {
 
 void topk_cand_prepare(void* workspace, hipStream_t stream) {
   // histograms, block counts and segment totals (contiguous)
-  (void)hipMemsetAsync(workspace, 0, 4 * kBins * 4 + 2 * kNB * 4 + 64 + kSegMax * 4, stream);
+  tape_memset(workspace, 0, 4 * kBins * 4 + 2 * kNB * 4 + 64 + kSegMax * 4, stream);
 }
 
 void topk_cand_ptrs(void* workspace, int64_t n, uint64_t** ballots, uint32_t** seg) {
@@ -612,13 +612,13 @@ void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, f
   const CandWS cw = carve_cand(workspace, n);
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
   const int nblk = static_cast<int>(((n + 63) / 64 + kSub - 1) / kSub);
-  hipLaunchKernelGGL(cand_compact_kernel, dim3(nblk), dim3(256), 0, stream, x, n, w, cw, kk, hint,
+  COMMEFF_LAUNCH(cand_compact_kernel, dim3(nblk), dim3(256), 0, stream, x, n, w, cw, kk, hint,
                      cand_cap(n));
   const Cand cd{cw.ctl, cw.cval, cw.cidx};
   constexpr int nb = 256;  // candidate passes (the fallbacks stream x on these too)
-  hipLaunchKernelGGL((hist_kernel<1, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
-  hipLaunchKernelGGL((hist_kernel<2, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
-  hipLaunchKernelGGL(count_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, cd);
+  COMMEFF_LAUNCH((hist_kernel<1, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
+  COMMEFF_LAUNCH((hist_kernel<2, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
+  COMMEFF_LAUNCH(count_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, cd);
   // the candidate list holds the keys >= hint: a tighter bound than the
   // full-vector passes' 0.5 (COMMEFF_TOPK_HINT_FRAC; a threshold that drops
   // below it between calls takes the exact fill-in fallback).  ResNet-9
@@ -629,7 +629,7 @@ void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, f
     const float f = e != nullptr ? static_cast<float>(std::atof(e)) : 0.85f;
     return f > 0.f && f < 1.f ? f : 0.85f;
   }();
-  hipLaunchKernelGGL(write_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, idx, vals,
+  COMMEFF_LAUNCH(write_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, idx, vals,
                      hint, cd, frac, persistent ? cw.seg : nullptr);
 }
 
@@ -642,13 +642,13 @@ void launch_topk_abs(const float* x, int64_t n, int64_t k, int64_t* idx, float* 
   if (hb > 1024) hb = 1024;
   if (hb < 1) hb = 1;
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
-  hipLaunchKernelGGL((hist_kernel<0, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
+  COMMEFF_LAUNCH((hist_kernel<0, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
   launch_topk_abs_rest(x, n, k, idx, vals, workspace, stream, hint);
 }
 
 void topk_prepare(void* workspace, hipStream_t stream) {
   WS w = carve(workspace);
-  (void)hipMemsetAsync(w.hist[0], 0, 4 * kBins * 4, stream);
+  tape_memset(w.hist[0], 0, 4 * kBins * 4, stream);
 }
 
 // the passes after the first histogram (hist[0] at the workspace start: keys
@@ -663,9 +663,9 @@ void launch_topk_abs_rest(const float* x, int64_t n, int64_t k, int64_t* idx, fl
   if (hb < 1) hb = 1;
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
   if (hint != nullptr)
-    hipLaunchKernelGGL((hist_kernel<3, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
-  hipLaunchKernelGGL((hist_kernel<1, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
-  hipLaunchKernelGGL((hist_kernel<2, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
+    COMMEFF_LAUNCH((hist_kernel<3, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
+  COMMEFF_LAUNCH((hist_kernel<1, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
+  COMMEFF_LAUNCH((hist_kernel<2, false>), dim3(hb), dim3(256), 0, stream, x, n, w, kk, hint, Cand{});
   // compaction blocks: 1,024 (every block's prologue sums the counts of the
   // blocks before it), up to kNB for very long vectors (>= 32 K elements a
   // block: GPT-2 size 151 -> 128 us for the ordered write pass)
@@ -675,9 +675,9 @@ void launch_topk_abs_rest(const float* x, int64_t n, int64_t k, int64_t* idx, fl
   int64_t span = (n + nb - 1) / nb;
   span = ((span + 1023) / 1024) * 1024;  // write_kernel: 1024 elements per block step
   nb = static_cast<int>((n + span - 1) / span);
-  hipLaunchKernelGGL(count_kernel<false>, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, Cand{});
-  hipLaunchKernelGGL(write_kernel<false>, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, idx, vals, hint,
-                     Cand{});
+  COMMEFF_LAUNCH(count_kernel<false>, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, Cand{});
+  COMMEFF_LAUNCH(write_kernel<false>, dim3(nb), dim3(256), 0, stream, x, n, span, w, kk, idx, vals, hint,
+                 Cand{}, 0.5f, static_cast<uint32_t*>(nullptr));
 }
 
 }  // namespace commeff

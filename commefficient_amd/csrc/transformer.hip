@@ -405,7 +405,7 @@ void launch_resid_ln_fwd(const void* x, const void* p, const void* bias, const v
   const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   const dim3 grid(static_cast<uint32_t>((M + 7) / 8));
 #define RLN_FWD(VV)                                                                              \
-  hipLaunchKernelGGL(resid_ln_fwd_kernel<VV>, grid, dim3(256), 0, stream,                        \
+  COMMEFF_LAUNCH(resid_ln_fwd_kernel<VV>, grid, dim3(256), 0, stream,                        \
                      static_cast<const V8*>(x), static_cast<const V8*>(p),                       \
                      static_cast<const V8*>(bias), static_cast<const V8*>(gamma),                \
                      static_cast<const V8*>(beta), static_cast<V8*>(h_out),                      \
@@ -432,7 +432,7 @@ void launch_resid_ln_bwd(const void* gy, const void* gh, const void* h, const fl
   const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   const dim3 grid(static_cast<uint32_t>(ln_grid(M)));
 #define RLN_BWD(VV)                                                                              \
-  hipLaunchKernelGGL(resid_ln_bwd_kernel<VV>, grid, dim3(256), 0, stream,                        \
+  COMMEFF_LAUNCH(resid_ln_bwd_kernel<VV>, grid, dim3(256), 0, stream,                        \
                      static_cast<const V8*>(gy), static_cast<const V8*>(gh),                     \
                      static_cast<const V8*>(h), mean, rstd, static_cast<const V8*>(gamma),       \
                      static_cast<V8*>(dh_out), static_cast<V8*>(dp_out), part, M, th, scale,     \
@@ -453,7 +453,7 @@ void launch_bias_gelu_fwd(const void* u, const void* b, void* f, int64_t M, int6
                           hipStream_t stream) {
   const int64_t nvec = M * N / 8;
   if (nvec == 0) return;
-  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3(static_cast<uint32_t>((nvec + 255) / 256)),
+  COMMEFF_LAUNCH(bias_gelu_fwd_kernel, dim3(static_cast<uint32_t>((nvec + 255) / 256)),
                      dim3(256), 0, stream, static_cast<const V8*>(u), static_cast<const V8*>(b),
                      static_cast<V8*>(f), nvec, static_cast<int>(N / 8));
 }
@@ -467,18 +467,18 @@ void launch_bias_act_bwd(const void* gf, const void* u, const void* b, void* du,
   const dim3 grid(static_cast<uint32_t>(bias_act_bwd_blocks(M)));
   const int NV = static_cast<int>(N / 8);
   if (gelu)
-    hipLaunchKernelGGL(bias_act_bwd_kernel<true>, grid, dim3(NV), 0, stream,
+    COMMEFF_LAUNCH(bias_act_bwd_kernel<true>, grid, dim3(NV), 0, stream,
                        static_cast<const V8*>(gf), static_cast<const V8*>(u),
                        static_cast<const V8*>(b), static_cast<V8*>(du), part, M, NV);
   else
-    hipLaunchKernelGGL(bias_act_bwd_kernel<false>, grid, dim3(NV), 0, stream,
+    COMMEFF_LAUNCH(bias_act_bwd_kernel<false>, grid, dim3(NV), 0, stream,
                        static_cast<const V8*>(gf), nullptr, nullptr, nullptr, part, M, NV);
 }
 
 void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,
                          const ColsumOut& out, hipStream_t stream) {
   const int64_t cols = Q * N;
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(static_cast<uint32_t>((cols + 15) / 16)),
+  COMMEFF_LAUNCH(colsum_final_kernel, dim3(static_cast<uint32_t>((cols + 15) / 16)),
                      dim3(1024), 0, stream, part, G, Q, N, stride, out);
 }
 
@@ -534,7 +534,7 @@ heads_to_rows_kernel(HeadSrcs src, int P, int H8, int hd8, int64_t L,
 void launch_pad_rows(const void* src, int64_t src_ld, int64_t K, const int32_t* inv, int64_t rows,
                      void* out, hipStream_t stream) {
   if (rows == 0) return;
-  hipLaunchKernelGGL(pad_rows_kernel, dim3(static_cast<uint32_t>(rows)), dim3(256), 0, stream,
+  COMMEFF_LAUNCH(pad_rows_kernel, dim3(static_cast<uint32_t>(rows)), dim3(256), 0, stream,
                      static_cast<const V8*>(src), src_ld / 8, static_cast<int>(K / 8), inv,
                      static_cast<V8*>(out));
 }
@@ -542,7 +542,7 @@ void launch_pad_rows(const void* src, int64_t src_ld, int64_t K, const int32_t* 
 void launch_heads_to_rows(const HeadSrcs& src, int P, int64_t H, int64_t hd, int64_t L,
                           const int32_t* tok, int64_t Mr, void* out, hipStream_t stream) {
   if (Mr == 0) return;
-  hipLaunchKernelGGL(heads_to_rows_kernel, dim3(static_cast<uint32_t>(Mr)), dim3(256), 0, stream,
+  COMMEFF_LAUNCH(heads_to_rows_kernel, dim3(static_cast<uint32_t>(Mr)), dim3(256), 0, stream,
                      src, P, static_cast<int>(H / 8), static_cast<int>(hd / 8), L, tok,
                      static_cast<V8*>(out));
 }

@@ -112,11 +112,12 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
         if self.track_running_stats and self.running_mean is not None:
             with torch.no_grad():
                 n = xf.shape[1] * xf.shape[3]
-                m = self.momentum if self.momentum is not None else 0.1
+                self.num_batches_tracked += 1
+                m = (self.momentum if self.momentum is not None
+                     else 1.0 / float(self.num_batches_tracked.item()))
                 self.running_mean.mul_(1 - m).add_(m * mean.mean(dim=0).view(C))
                 unb = var.mean(dim=0).view(C) * (n / max(1, n - 1))
                 self.running_var.mul_(1 - m).add_(m * unb)
-                self.num_batches_tracked += 1
         return y.reshape(x.shape).to(x.dtype).contiguous(memory_format=_fmt(x)), False
 
 
@@ -133,10 +134,12 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
             if self.training and self.track_running_stats and self.running_mean is not None:
                 with torch.no_grad():
                     n = xf.numel() // C
-                    m = self.momentum if self.momentum is not None else 0.1
+                    self.num_batches_tracked.add_(1)
+                    # momentum None: cumulative average (PyTorch's factor 1/num_batches_tracked)
+                    m = (self.momentum if self.momentum is not None
+                         else 1.0 / self.num_batches_tracked.double())
                     self.running_mean.mul_(1 - m).add_(mean.detach() * m)
                     self.running_var.mul_(1 - m).add_(var.detach() * (m * n / max(1, n - 1)))
-                    self.num_batches_tracked.add_(1)
         else:
             mean, var = self.running_mean, self.running_var
         y = (xf - mean.view(1, C, 1, 1)) * torch.rsqrt(var.view(1, C, 1, 1) + self.eps)

@@ -69,6 +69,30 @@ def relu_maxpool(x: torch.Tensor, k: int) -> torch.Tensor:
 # (csrc/conv.hip): "native" (default) or "miopen" (torch.nn.functional.conv2d).
 _CONV_BACKEND = ["native"]
 
+# Listeners told when a native backward has written a parameter's gradient
+# straight into its flat-buffer ``.grad`` (and handed autograd None, so no
+# AccumulateGrad node and no post-accumulate hook runs for it): the dense
+# modes' overlapped bucket all-reduce (parallel/overlap.py) counts these as
+# "gradient ready".  Called on the stream that wrote the gradient.
+_GRAD_READY = []
+
+
+def add_grad_ready_listener(fn):
+    _GRAD_READY.append(fn)
+
+
+def remove_grad_ready_listener(fn):
+    if fn in _GRAD_READY:
+        _GRAD_READY.remove(fn)
+
+
+def _grad_written(*params):
+    if _GRAD_READY:
+        for p in params:
+            if p is not None:
+                for fn in _GRAD_READY:
+                    fn(p)
+
 
 def set_conv_backend(name: str) -> None:
     if name not in ("native", "miopen"):
@@ -225,6 +249,7 @@ def _wgrad_to(g: torch.Tensor, x: torch.Tensor, weight: torch.Tensor):
     if (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
             and gr.device == g.device and tuple(gr.shape) == tuple(weight.shape)):
         _ops().conv3x3_wgrad_into(g, x, gr)
+        _grad_written(weight)
         return None
     return _ops().conv3x3_wgrad(g, x)
 
@@ -496,6 +521,7 @@ class _InputConv(torch.autograd.Function):
         if (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
                 and gr.device == gy.device and gr.shape == ctx.weight.shape):
             _ops().conv_prep_wgrad_into(gy, mask, x, gr)
+            _grad_written(ctx.weight)
             return None, None
         return None, _ops().conv_prep_wgrad(gy, mask, x)
 
@@ -557,6 +583,8 @@ class _FusedHead(torch.autograd.Function):
         else:
             dx = _ops().head_bwd(gl.contiguous(), gunit, w.detach(), pooled, codes, ctx.hw[0],
                                  ctx.hw[1], ctx.scale, dw, 1.0 if into else 0.0)
+        if into:
+            _grad_written(w)
         return dx, (None if into else dw), None, None, None
 
 
@@ -607,6 +635,10 @@ class _GhostBN(torch.autograd.Function):
         # the residual addend's gradient: the ReLU-masked dy, written by the
         # backward apply kernel
         dadd = torch.empty_like(dy) if ctx.has_add else None
+        if dadd is not None:
+            # a fresh buffer that only the residual branch consumes: its
+            # consumer may accumulate into it in place (_Conv1x1Pass)
+            dadd._commeff_fresh = True
         if ctx.gg is not None and pw is not None:
             # grouped (per-client) dweight / dbias rows, ops/grouped.py; the
             # BN groups are the gradient groups
@@ -625,6 +657,8 @@ class _GhostBN(torch.autograd.Function):
                                          dadd)
         if weight is None or into:
             dw = db = None
+        if into:
+            _grad_written(pw, pb)
         return dx, dw, db, None, None, None, None, None, None, None, None, dadd
 
 
@@ -813,6 +847,8 @@ class _Conv1x1(torch.autograd.Function):
                 into = _grad_view(ctx.weight, (k, c))
                 gw = _wgrad_gemm(g2d, x2d, into)
                 gw = None if into is not None else gw.view(k, c, 1, 1)
+                if into is not None:
+                    _grad_written(ctx.weight)
         return gx, gw, None, None
 
 
@@ -841,12 +877,17 @@ class _Conv1x1Pass(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             if gid is not None:
-                # the identity gradient is this node's own input (the residual
-                # BN backward's fresh dadd): accumulate into it in place (an
-                # out-of-place addmm first copies it: ~36 us per block of a
-                # ResNet-101 round)
                 gi = _nhwc2d(gid.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
-                gx2d = torch.addmm(gi, g2d, wb, out=gi)
+                if getattr(gid, "_commeff_fresh", False) and gi.data_ptr() == gid.data_ptr():
+                    # the identity gradient is the residual BN backward's fresh
+                    # dadd, consumed only here: accumulate into it in place (an
+                    # out-of-place addmm first copies it: ~36 us per block of a
+                    # ResNet-101 round)
+                    gx2d = torch.addmm(gi, g2d, wb, out=gi)
+                else:
+                    # autograd may hand the same tensor to another consumer
+                    # (unfused relu(y + addend) path): never write into it
+                    gx2d = torch.addmm(gi, g2d, wb)
             else:
                 gx2d = torch.mm(g2d, wb)
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
@@ -859,6 +900,8 @@ class _Conv1x1Pass(torch.autograd.Function):
                 into = _grad_view(ctx.weight, (k, c))
                 gw = _wgrad_gemm(g2d, _nhwc2d(x), into)
                 gw = None if into is not None else gw.view(k, c, 1, 1)
+                if into is not None:
+                    _grad_written(ctx.weight)
         return gx, gw, None
 
 
@@ -945,7 +988,10 @@ def _col_wgrad(g2d: torch.Tensor, col: torch.Tensor, weight: torch.Tensor, gg):
     dst = into if into is not None else torch.empty(1, K, C * R * S, dtype=torch.float32,
                                                      device=g2d.device)
     _ops().wgrad_rsc_add(dst, parts, splits, C, R * S, into is not None)
-    return None if into is not None else dst.view(weight.shape)
+    if into is not None:
+        _grad_written(weight)
+        return None
+    return dst.view(weight.shape)
 
 
 class _ConvCol(torch.autograd.Function):

@@ -46,24 +46,23 @@ def ctx() -> DistCtx:
     return _CTX
 
 
-# RCCL defaults for one MI355X node (8 GPUs, each with 7 point-to-point xGMI
+# RCCL settings for one MI355X node (8 GPUs, each with 7 point-to-point xGMI
 # links to the others).  Set only when the user has not set them:
 # * TORCH_NCCL_HIGH_PRIORITY=1 -- RCCL kernels on a high-priority HIP stream, so
 #   the bucketed gradient all-reduces issued during the backward
 #   (parallel/overlap.py) are not queued behind the compute kernels;
 # * TORCH_NCCL_AVOID_RECORD_STREAMS=1 -- no record_stream on the payload, whose
-#   buffer is reused round after round (no allocator retention);
-# * NCCL_MIN_NCHANNELS=16 -- at least 16 channels (rings) for the 10 MB sketch
-#   all-reduce, so every one of the 7 links carries traffic (the default channel
-#   search can settle on fewer for medium messages; a ring is link-bound on xGMI);
-# * RCCL_MSCCL_ENABLE=1 -- RCCL's MSCCL single-node all-reduce schedules for the
-#   fully connected xGMI mesh (used where RCCL finds them faster than rings).
+#   buffer is reused round after round (no allocator retention).
+# Channel counts and algorithm/protocol choices stay with RCCL's own tuning
+# tables for the xGMI mesh: no multi-GPU box was available to measure an
+# override against them (round 3 forced NCCL_MIN_NCHANNELS=16 and
+# RCCL_MSCCL_ENABLE=1 without a measurement; both were dropped).
+# HSA_ENABLE_IPC_MODE_LEGACY=0 (dmabuf IPC) must be in the LAUNCHER's
+# environment: the HSA runtime reads it once, before this module runs.
 # Override any of them from the environment; COMMEFF_RCCL_DEFAULTS=0 sets none.
 RCCL_DEFAULTS = {
     "TORCH_NCCL_HIGH_PRIORITY": "1",
     "TORCH_NCCL_AVOID_RECORD_STREAMS": "1",
-    "NCCL_MIN_NCHANNELS": "16",
-    "RCCL_MSCCL_ENABLE": "1",
 }
 
 
@@ -73,7 +72,6 @@ def apply_rccl_defaults(env=None) -> dict:
     env = os.environ if env is None else env
     if env.get("COMMEFF_RCCL_DEFAULTS", "1") == "0":
         return {}
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
     out = {}
     for k, v in RCCL_DEFAULTS.items():
         if k not in env:

@@ -950,6 +950,11 @@ class FedModel:
         names = [nm for nm, p in self.model.named_parameters() if p.requires_grad]
         frozen = {nm: p.detach() for nm, p in self.model.named_parameters() if not p.requires_grad}
         bufs0 = dict(self.model.named_buffers())
+        # every pass starts from the round's buffers; the running statistics
+        # written back are the mean over ALL clients (equal weight each),
+        # independent of how many clients fit in one vmap pass
+        bufs_init = {k: b.detach().clone() for k, b in bufs0.items()}
+        buf_acc = {}
         model, loss_fn, args = self.model, self.compute_loss_train, a
 
         def client_loss(params, buffers, *xy):
@@ -971,8 +976,8 @@ class FedModel:
             data = rb.take(pos)
             xs = [t.reshape((Gp, n) + tuple(t.shape[1:])) for t in data]
             Wg = self.w.unsqueeze(0).repeat(Gp, 1)
-            bufs = {k: b.detach().unsqueeze(0).repeat((Gp,) + (1,) * b.dim()).clone()
-                    for k, b in bufs0.items()}
+            bufs = {k: b.unsqueeze(0).repeat((Gp,) + (1,) * b.dim()).clone()
+                    for k, b in bufs_init.items()}
             step = 0
             ls, ms = [], None
             with stock_ops(), self._autocast(cache=False):
@@ -998,15 +1003,23 @@ class FedModel:
             # accounting counts exact changes)
             Wg.neg_().add_(self.w)
             out.add_(Wg.sum(dim=0), alpha=float(n))
-            with torch.no_grad():  # running statistics: the clients' mean
-                for k, b in bufs0.items():
+            with torch.no_grad():  # running statistics: summed over this pass's clients
+                for k, b in bufs.items():
                     if b.is_floating_point():
-                        b.copy_(bufs[k].mean(dim=0))
+                        v = b.double().sum(dim=0)
+                        buf_acc[k] = v if k not in buf_acc else buf_acc[k] + v
                     else:
-                        b.copy_(bufs[k].max(dim=0).values)
+                        v = b.max(dim=0).values
+                        buf_acc[k] = v if k not in buf_acc else torch.maximum(buf_acc[k], v)
             loss_rows.append(torch.stack(ls).mean(dim=0))
             met_rows.append([m / step for m in ms])
             slot_rows.append(slots)
+        with torch.no_grad():  # the clients' mean, written once
+            for k, b in bufs0.items():
+                if b.is_floating_point():
+                    b.copy_((buf_acc[k] / len(mine)).to(b.dtype))
+                else:
+                    b.copy_(buf_acc[k])
         msum = torch.zeros(1 + len(met_rows[0]), W, device=self.device)
         slots_t = torch.from_numpy(np.concatenate(slot_rows).astype(np.int64)).to(self.device)
         msum[0].index_copy_(0, slots_t, torch.cat(loss_rows))

@@ -9,11 +9,14 @@ SURVEY.md §5.8).  Here the flat gradient is cut into buckets of contiguous
 parameters in backward order; as soon as every parameter of a bucket has its
 gradient (a post-accumulate-grad hook), the bucket's RCCL all-reduce is issued
 asynchronously and runs on the process group's stream while the backward of
-the earlier layers continues.  After the backward any bucket not yet issued
-(parameters whose gradients native kernels write straight into the flat
-buffer never fire the hook) is issued, all are waited for, and the weight
-decay term -- identical on every rank -- is added once to the reduced sum
-(``sum_r (g_r + c_r w) = sum_r g_r + (sum_r c_r) w``).
+the earlier layers continues.  Native backward kernels that accumulate a
+weight gradient straight into the flat buffer hand autograd None, so no
+AccumulateGrad node (and no hook) runs for that parameter: they announce the
+write instead (``ops.nn._grad_written``, called on the stream that wrote it,
+which the all-reduce then waits for), and count as ready the same way.  After
+the backward any bucket not yet issued is issued, all are waited for, and the
+weight decay term -- identical on every rank -- is added once to the reduced
+sum (``sum_r (g_r + c_r w) = sum_r g_r + (sum_r c_r) w``).
 
 Every rank must issue the same collectives in the same order: buckets complete
 in backward order, which is the same on every rank for the same model and
@@ -66,8 +69,14 @@ class OverlapReducer:
         self.works: List[Optional[object]] = [None] * len(self.buckets)
         self.issued_early = 0
         self._handles = []
+        self._index = {}
         for i, p in enumerate(params):
             self._handles.append(p.register_post_accumulate_grad_hook(self._hook(i)))
+            self._index[id(p)] = i
+        # native in-place gradient writes (no hook fires for those)
+        from ..ops import nn as _nn
+        self._nn = _nn
+        _nn.add_grad_ready_listener(self._written)
 
     def _hook(self, i: int):
         def fn(p):
@@ -78,13 +87,22 @@ class OverlapReducer:
                 o, n = f.offsets[i], f.numels[i]
                 f.g[o:o + n].add_(p.grad.reshape(-1))
                 p.grad = None
-            self.done_param[i] = True
-            b = self.bucket_of[i]
-            self.pending[b] -= 1
-            if self.pending[b] == 0:
-                self._issue(b)
-                self.issued_early += 1
+            self._ready(i)
         return fn
+
+    def _written(self, p):
+        i = self._index.get(id(p))
+        if i is None or not self.armed or self.done_param[i] or self.shadow:
+            return
+        self._ready(i)
+
+    def _ready(self, i: int):
+        self.done_param[i] = True
+        b = self.bucket_of[i]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._issue(b)
+            self.issued_early += 1
 
     def _issue(self, b: int):
         lo, hi = self.ranges[b]
@@ -120,3 +138,4 @@ class OverlapReducer:
         for h in self._handles:
             h.remove()
         self._handles = []
+        self._nn.remove_grad_ready_listener(self._written)

@@ -103,7 +103,6 @@ class ServerState:
         (the scale is folded into the momentum kernel); ``hist`` is the
         accountant's change histogram, updated with the stamps.  Returns
         (idx, vals) for sparse modes (the un-scaled update), else None."""
-        step = None  # device-side lr / round (ops' graph-capture form): unused
         a = self.args
         rho = float(a.virtual_momentum)
         lr_s, lr_v = (lr, None) if not torch.is_tensor(lr) else (0.0, lr)
@@ -131,10 +130,10 @@ class ServerState:
             # error feedback (virtual) + momentum-factor masking in sketch space,
             # and the weight step (one kernel for the region family)
             other = self.V if et == "virtual" else None
-            if step is not None or not sk.zero_heavy_hitters_apply(idx, vals, other, w, lr_s, lr_v, last_mod,
-                                                                    round_idx, hist):
+            # (region family: one fused kernel; csvec layout: zeroing, then the apply)
+            if not sk.zero_heavy_hitters_apply(idx, vals, other, w, lr_s, lr_v, last_mod, round_idx, hist):
                 sk.zero_heavy_hitters(idx, vals, other)
-                ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
+                ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, hist=hist)
             weights_end_update(img_sync, w, idx)
             return idx, vals
         if mode == "true_topk":
@@ -143,7 +142,7 @@ class ServerState:
             if client_state is not None and participating is not None:
                 client_state.zero_velocity_at(participating, idx)
             ops.zero_at(idx, self.E, self.V)
-            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
+            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, hist=hist)
             weights_end_update(img_sync, w, idx)
             return idx, vals
         if mode in ("local_topk", "uncompressed"):
@@ -155,11 +154,11 @@ class ServerState:
                 ops.clip_noise(self.V, None, 0.0, a.noise_multiplier, seed=a.seed * 7919 + 17,
                                offset=self.noise_round * self.d)
                 self.noise_round += 1
-            ops.dense_apply(w, self.V, lr_s, lr_v, last_mod, round_idx, step, hist)
+            ops.dense_apply(w, self.V, lr_s, lr_v, last_mod, round_idx, hist=hist)
             return None
         if mode == "fedavg":
             ops.momentum_ef(self.V, None, G, rho, gscale, "none")
-            ops.dense_apply(w, self.V, 1.0, None, last_mod, round_idx, step, hist)
+            ops.dense_apply(w, self.V, 1.0, None, last_mod, round_idx, hist=hist)
             return None
         raise ValueError(mode)
 

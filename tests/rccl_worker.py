@@ -83,6 +83,9 @@ def main(out_dir, mode, rounds, device):
             assert info.get("sparse_allgather"), info
         if mode == "uncompressed_overlap":
             assert info.get("overlapped_buckets", 0) >= 2, info
+            # the native wgrad kernels announce their in-place writes
+            # (ops.nn._grad_written): buckets go out during the backward
+            assert info.get("buckets_during_backward", 0) >= 1, info
     torch.save({"w": fed.w.cpu(), "loss": torch.stack(losses).cpu(), "checksum": checksum,
                 "dl": fed.accountant.client_download.cpu()},
                os.path.join(out_dir, f"{mode}_r{ctx.rank}_w{ctx.world_size}.pt"))

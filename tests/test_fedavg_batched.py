@@ -161,3 +161,46 @@ def test_batched_local_sgd_gpu_bf16():
     assert rel < 2 * bf_noise + 1e-2, (rel, bf_noise)
     assert ((up_a - up_f).norm() / up_f.norm()).item() < 2 * bf_noise + 1e-2
     torch.testing.assert_close(l_a, l_b, rtol=2e-2, atol=2e-2)
+
+
+def test_batched_running_stats_do_not_depend_on_pass_size():
+    """BatchNorm running statistics after a batched FedAvg round are the mean
+    over ALL clients, each client starting from the round's buffers: splitting
+    the clients over several vmap passes (a small --grouped_gb) gives the same
+    buffers and upload as one pass."""
+    torch.manual_seed(0)
+    base = ResNet(BasicBlock, [1, 1, 1, 1], num_classes=10, input_hw=16)
+    res = {}
+    for gb in ("4", "1e-9"):  # one pass of 4 clients / two passes of 2
+        model = copy.deepcopy(base)
+        fed, opt = _engine("on", ["--fedavg_batch_size", "3", "--grouped_gb", gb], model)
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(24, 3, 16, 16, generator=g)
+        y = torch.randint(0, 10, (24,), generator=g)
+        # lr 0: the clients' weights stay put, so their statistics differ only
+        # by conv rounding across vmap widths (a random-init BN net amplifies
+        # any weight difference ~1e4-fold, test_vmapped_batchnorm_steps_exact_in_fp64)
+        fed.fedavg_lr = 0.0
+        fed((torch.arange(4).repeat_interleave(6), x, y))
+        res[gb] = {k: b.clone() for k, b in model.named_buffers()}
+    for k, b in res["4"].items():
+        # rounding: ~1e-6; the old pass-order dependence (pass 2 started from
+        # pass 1's mean and overwrote it) moved them by ~1e-2
+        torch.testing.assert_close(res["1e-9"][k], b, rtol=1e-5, atol=1e-5)
+
+
+def test_bn_stock_cumulative_average_when_momentum_none():
+    """momentum=None: PyTorch's cumulative moving average (factor
+    1/num_batches_tracked), also in the vmap-friendly stock composition."""
+    from commefficient_amd.models.common import GhostBatchNorm2d
+    from commefficient_amd.ops.nn import stock_ops
+    torch.manual_seed(0)
+    ref = torch.nn.BatchNorm2d(5, momentum=None)
+    ours = GhostBatchNorm2d(5, momentum=None)
+    for _ in range(3):
+        x = torch.randn(6, 5, 4, 4)
+        ref(x)
+        with stock_ops():
+            ours(x)
+    torch.testing.assert_close(ours.running_mean, ref.running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(ours.running_var, ref.running_var, rtol=1e-5, atol=1e-6)
