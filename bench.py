@@ -188,7 +188,9 @@ def main():
     value = imgs_per_step * b.steps / elapsed
     up_ref = fed.accountant.upload_per_client * W
     payload = fed.last_round.get("payload_bytes", 0)
-    wire = fed.accountant.wire_bytes_per_rank(payload // 4)
+    # ring-algorithm bytes each rank sends per round (all-reduce, or with the
+    # sharded server reduce-scatter + metric all-reduce + k-list all-gather)
+    wire = fed.last_round.get("wire_bytes", fed.accountant.wire_bytes_per_rank(payload // 4))
     if ctx.is_main:
         print(json.dumps({
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
@@ -197,9 +199,14 @@ def main():
             "data": "synthetic (CIFAR-10 shape, random-init ResNet-9)",
             "config": {"model": "ResNet9", "global_batch": imgs_per_step, "seq_len": None,
                        "image_hw": 32, "parallelism": f"dp{N}", "mode": "sketch",
-                       "k": 50000, "num_rows": 5, "num_cols": 500000, "num_blocks": 20,
+                       "k": 50000, "num_rows": 5, "num_cols": 500000,
+                       # numBlocks only shapes the csvec-layout hashes (--encode
+                       # planned|binned|direct); the region family has no blocks
+                       **({"num_blocks": 20} if b.encode != "region" else {}),
                        "clients_per_round": W, "client_size": b.client_size,
-                       "num_clients": b.num_clients, "encode": b.encode},
+                       "num_clients": b.num_clients, "encode": b.encode,
+                       "server": ("sharded" if fed.shard_server else "replicated"),
+                       "round_tape": bool(fed.last_round.get("taped"))},
             "bytes_per_step": {"upload_ref_accounting": up_ref,
                                "download_ref_accounting": dl,
                                "allreduce_payload_per_rank": payload,

@@ -346,20 +346,38 @@ void cs_zero_buckets_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2,
 // ---- region sketch (sketch_region.hip)
 struct RegionParams {
   int64_t r, c, m, g, G, W, nch;
+  RegionLayout L;
 };
 
+// The table's shape gives its layout (kernels.h RegionLayout):
+//   [r, c]          row-major, every group (g0 must be 0);
+//   [Gs, r, g*m]    group-major, groups [g0, g0 + Gs) (the sharded server's
+//                   per-rank state, or the padded payload with g0 = 0).
 RegionParams check_region(const at::Tensor& table, int64_t d, int64_t m, int64_t g, int64_t W,
                           const at::Tensor& perm, const at::Tensor& cinfo, const at::Tensor* lists,
-                          const at::Tensor* goffs) {
+                          const at::Tensor* goffs, int64_t g0 = 0) {
   check_f32(table, "table");
   RegionParams p;
-  p.c = table.size(-1);
-  p.r = table.numel() / p.c;
   p.m = m;
   p.g = g;
   p.W = W;
   p.nch = (d + m - 1) / m;
-  p.G = p.c / (g * m);
+  const int64_t gm = g * m;
+  if (table.dim() == 3) {
+    TORCH_CHECK(table.size(2) == gm && g0 >= 0, "region sketch: group-major table must be [groups, r, g*m]");
+    p.r = table.size(1);
+    p.c = 0;
+    p.G = goffs != nullptr ? goffs->numel() - 1 : g0 + table.size(0);
+    const int64_t g1 = std::min(p.G, g0 + table.size(0));
+    p.L = RegionLayout{static_cast<uint32_t>(p.r * gm), static_cast<uint32_t>(gm), static_cast<uint32_t>(g0),
+                       static_cast<uint32_t>(std::max(g0, g1))};
+  } else {
+    TORCH_CHECK(g0 == 0, "region sketch: a row-major table holds every group (g0 = 0)");
+    p.c = table.size(-1);
+    p.r = table.numel() / p.c;
+    p.G = p.c / gm;
+    p.L = RegionLayout{static_cast<uint32_t>(gm), static_cast<uint32_t>(p.c), 0u, static_cast<uint32_t>(p.G)};
+  }
   TORCH_CHECK(region_geometry_supported(p.r, m, g, W) && p.G >= 1 && d >= 1 && d < (int64_t(1) << 32) &&
                   p.G * g < (int64_t(1) << 24),
               "region sketch: unsupported geometry (r <= 16, m <= 64, W <= min(16, g), r*g*m floats in LDS)");
@@ -370,7 +388,7 @@ RegionParams check_region(const at::Tensor& table, int64_t d, int64_t m, int64_t
   i32(perm, p.r * m, "perm [r, m]");
   i32(cinfo, p.r * p.nch, "cinfo [r, nch] / [nch, r]");
   if (lists != nullptr) i32(*lists, p.nch, "lists [nch]");
-  if (goffs != nullptr) i32(*goffs, p.G + 1, "goffs [G + 1]");
+  if (goffs != nullptr && table.dim() != 3) i32(*goffs, p.G + 1, "goffs [G + 1]");
   return p;
 }
 
@@ -381,6 +399,7 @@ void cs_region_encode_hip(at::Tensor table, const at::Tensor& vec, double scale,
   check_f32(vec, "vec");
   const int64_t d = vec.numel();
   const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
+  TORCH_CHECK(table.dim() != 3 || table.size(0) >= p.G, "cs_region_encode: a group-major table needs every group");
   if (wvec.has_value() && wvec->defined()) {
     check_f32(*wvec, "wvec");
     TORCH_CHECK(wvec->numel() == d && wvec->device() == vec.device(), "wvec must match vec");
@@ -391,7 +410,7 @@ void cs_region_encode_hip(at::Tensor table, const at::Tensor& vec, double scale,
                           static_cast<float>(scale), static_cast<float>(wscale), d, static_cast<int>(p.r), p.c,
                           m, g, p.G, W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                           reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
-                          goffs.data_ptr<int32_t>(), overwrite, cur_stream(),
+                          goffs.data_ptr<int32_t>(), overwrite, p.L, cur_stream(),
                           zero_vec ? const_cast<float*>(vec.data_ptr<float>()) : nullptr);
 }
 
@@ -399,16 +418,16 @@ void cs_region_encode_hip(at::Tensor table, const at::Tensor& vec, double scale,
 // (a rank's shard of the unsketch; the rest of est is left unset)
 at::Tensor cs_region_query_hip(const at::Tensor& table, int64_t d, int64_t m, int64_t g, int64_t W,
                                const at::Tensor& perm, const at::Tensor& cinfo, const at::Tensor& lists,
-                               const at::Tensor& goffs, int64_t q0, int64_t q1) {
-  const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
+                               const at::Tensor& goffs, int64_t q0, int64_t q1, int64_t g0) {
+  const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs, g0);
   if (q1 < 0) q1 = p.nch;
   TORCH_CHECK(q0 >= 0 && q0 <= q1 && q1 <= p.nch, "cs_region_query: chunk range out of bounds");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
   auto est = at::empty({d}, table.options());
   launch_cs_region_query(const_cast<float*>(table.data_ptr<float>()), est.data_ptr<float>(), d, static_cast<int>(p.r),
-                         p.c, m, g, p.G, W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+                         m, g, W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                          reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
-                         goffs.data_ptr<int32_t>(), q0, q1, cur_stream());
+                         goffs.data_ptr<int32_t>(), q0, q1, p.L, cur_stream());
   return est;
 }
 
@@ -425,8 +444,18 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
                                                       int64_t q1, const c10::optional<at::Tensor>& momV,
                                                       const c10::optional<at::Tensor>& momG, double rho,
                                                       double gscale, int64_t mom_mode,
-                                                      const c10::optional<at::Tensor>& ws_keep) {
-  const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs);
+                                                      const c10::optional<at::Tensor>& ws_keep, int64_t g0,
+                                                      const c10::optional<at::Tensor>& cpos, int64_t ncoord) {
+  const RegionParams p = check_region(table, d, m, g, W, perm, cinfo, &lists, &goffs, g0);
+  const int32_t* cp = nullptr;
+  if (cpos.has_value() && cpos->defined()) {
+    // a group-major shard's query: est holds the shard's ncoord coordinates
+    // at compact positions (chunks ascending), idx are compact positions
+    TORCH_CHECK(cpos->scalar_type() == at::kInt && cpos->is_contiguous() && cpos->numel() == p.nch &&
+                    cpos->device() == table.device() && ncoord >= 1 && ncoord <= d && q0 == 0,
+                "cs_region_topk: cpos must be int32 [nch] with 1 <= ncoord <= d");
+    cp = cpos->data_ptr<int32_t>();
+  }
   float* mv = nullptr;
   const float* mg = nullptr;
   if (mom_mode != 0) {
@@ -444,7 +473,7 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
   }
   if (q1 < 0) q1 = p.nch;
   TORCH_CHECK(q0 >= 0 && q0 < q1 && q1 <= p.nch, "cs_region_topk: chunk range out of bounds");
-  const int64_t lo = q0 * m, hi = std::min(d, q1 * m), n = hi - lo;
+  const int64_t lo = cp != nullptr ? 0 : q0 * m, hi = cp != nullptr ? ncoord : std::min(d, q1 * m), n = hi - lo;
   TORCH_CHECK(k >= 1 && k < n, "cs_region_topk: need 1 <= k < shard size");
   uint32_t* hp = nullptr;
   if (hint.has_value() && hint->defined()) {
@@ -480,12 +509,12 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
   } else {
     topk_prepare(ws.data_ptr(), cur_stream());
   }
-  launch_cs_region_query(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(p.r), p.c, m, g, p.G,
+  launch_cs_region_query(table.data_ptr<float>(), est.data_ptr<float>(), d, static_cast<int>(p.r), m, g,
                          W, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                          reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), lists.data_ptr<int32_t>(),
-                         goffs.data_ptr<int32_t>(), q0, q1, cur_stream(), hp,
+                         goffs.data_ptr<int32_t>(), q0, q1, p.L, cur_stream(), hp,
                          reinterpret_cast<uint32_t*>(ws.data_ptr()), mv, mg, static_cast<float>(rho),
-                         static_cast<float>(gscale), static_cast<int>(mom_mode), ballots, seg);
+                         static_cast<float>(gscale), static_cast<int>(mom_mode), ballots, seg, cp);
   if (cand) {
     launch_topk_cand_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                           ws.data_ptr(), cur_stream(), hp, keep);
@@ -514,8 +543,8 @@ int64_t cs_region_topk_ws_bytes(int64_t d, int64_t m, int64_t q0, int64_t q1) {
 
 void cs_region_zero_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2, const at::Tensor& idx,
                         const c10::optional<at::Tensor>& vals, int64_t d, int64_t m, int64_t g,
-                        const at::Tensor& perm, const at::Tensor& cinfo) {
-  const RegionParams p = check_region(t1, d, m, g, 1, perm, cinfo, nullptr, nullptr);
+                        const at::Tensor& perm, const at::Tensor& cinfo, int64_t g0) {
+  const RegionParams p = check_region(t1, d, m, g, 1, perm, cinfo, nullptr, nullptr, g0);
   TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous() && idx.device() == t1.device(),
               "cs_region_zero: idx must be int64 on the table's device");
   if (t2.has_value() && t2->defined())
@@ -526,8 +555,8 @@ void cs_region_zero_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2, cons
                 "cs_region_zero: vals must be f32 like idx");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(t1.device());
   launch_cs_region_zero(t1.data_ptr<float>(), fptr(t2), idx.data_ptr<int64_t>(), fptr(vals), idx.numel(), d,
-                        static_cast<int>(p.r), p.c, m, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
-                        reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), cur_stream());
+                        static_cast<int>(p.r), g, m, p.nch, reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
+                        reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()), p.L, cur_stream());
 }
 
 at::Tensor cs_l2estimate_hip(const at::Tensor& table) {
@@ -599,8 +628,9 @@ void cs_region_zero_apply_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2
                               const at::Tensor& vals, int64_t d, int64_t m, int64_t g, const at::Tensor& perm,
                               const at::Tensor& cinfo, at::Tensor w, double lr,
                               const c10::optional<at::Tensor>& lr_vec, const c10::optional<at::Tensor>& last_mod,
-                              int64_t round, const c10::optional<at::Tensor>& hist) {
-  const RegionParams p = check_region(t1, d, m, g, 1, perm, cinfo, nullptr, nullptr);
+                              int64_t round, const c10::optional<at::Tensor>& hist,
+                              const c10::optional<at::Tensor>& step, int64_t g0) {
+  const RegionParams p = check_region(t1, d, m, g, 1, perm, cinfo, nullptr, nullptr, g0);
   check_f32(w, "w");
   TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous() && idx.device() == t1.device(),
               "cs_region_zero_apply: idx must be int64 on the table's device");
@@ -618,10 +648,10 @@ void cs_region_zero_apply_hip(at::Tensor t1, const c10::optional<at::Tensor>& t2
   int32_t* lm = last_mod.has_value() && last_mod->defined() ? last_mod->data_ptr<int32_t>() : nullptr;
   launch_sparse_apply_region_zero(w.data_ptr<float>(), idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                                   idx.numel(), static_cast<float>(lr), fptr(lr_vec), lm,
-                                  static_cast<int32_t>(round), nullptr, hist_ptr(hist), t1.data_ptr<float>(), t2p,
+                                  static_cast<int32_t>(round), step_ptr(step), hist_ptr(hist), t1.data_ptr<float>(), t2p,
                                   reinterpret_cast<const uint32_t*>(perm.data_ptr<int32_t>()),
                                   reinterpret_cast<const uint32_t*>(cinfo.data_ptr<int32_t>()),
-                                  static_cast<int>(p.r), p.c, m, p.nch, d, cur_stream());
+                                  static_cast<int>(p.r), g, m, p.nch, d, p.L, cur_stream());
 }
 
 void dense_apply_hip(at::Tensor w, const at::Tensor& delta, double lr,
@@ -2162,20 +2192,21 @@ TORCH_LIBRARY(commeff, m) {
         "int g, int W, Tensor perm, Tensor cinfo, Tensor lists, Tensor goffs, bool overwrite=False, "
         "bool zero_vec=False) -> ()");
   m.def("cs_region_query(Tensor table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
-        "Tensor goffs, int q0=0, int q1=-1) -> Tensor");
+        "Tensor goffs, int q0=0, int q1=-1, int g0=0) -> Tensor");
   m.def("cs_region_topk(Tensor(a!) table, int d, int m, int g, int W, Tensor perm, Tensor cinfo, Tensor lists, "
         "Tensor goffs, int k, Tensor(d!)? hint=None, int q0=0, int q1=-1, Tensor(b!)? momV=None, Tensor? momG=None, "
-        "float rho=0.0, float gscale=0.0, int mom_mode=0, Tensor(c!)? ws=None) -> (Tensor, Tensor)");
+        "float rho=0.0, float gscale=0.0, int mom_mode=0, Tensor(c!)? ws=None, int g0=0, Tensor? cpos=None, "
+        "int ncoord=-1) -> (Tensor, Tensor)");
   m.def("cs_region_topk_ws_bytes(int d, int m, int q0, int q1) -> int", &commeff::cs_region_topk_ws_bytes);
   m.def("cs_region_zero(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor? vals, int d, int m, int g, "
-        "Tensor perm, Tensor cinfo) -> ()");
+        "Tensor perm, Tensor cinfo, int g0=0) -> ()");
   m.def("topk_abs(Tensor x, int k, Tensor(a!)? hint=None) -> (Tensor, Tensor)");
   m.def("momentum_ef(Tensor(a!) V, Tensor(b!)? E, Tensor G, float rho, float gscale, int mode) -> ()");
   m.def("sparse_apply(Tensor(a!) w, Tensor idx, Tensor vals, float lr, Tensor? lr_vec, "
         "Tensor(b!)? last_mod, int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");
   m.def("cs_region_zero_apply(Tensor(a!) t1, Tensor(b!)? t2, Tensor idx, Tensor vals, int d, int m, int g, "
         "Tensor perm, Tensor cinfo, Tensor(c!) w, float lr, Tensor? lr_vec, Tensor(d!)? last_mod, int round, "
-        "Tensor(e!)? hist=None) -> ()");
+        "Tensor(e!)? hist=None, Tensor? step=None, int g0=0) -> ()");
   m.def("dense_apply(Tensor(a!) w, Tensor delta, float lr, Tensor? lr_vec, Tensor(b!)? last_mod, "
         "int round, Tensor? step=None, Tensor(c!)? hist=None) -> ()");
   m.def("account_hist(Tensor hist, Tensor meta, int W, Tensor(a!) client_dl, Tensor(b!) client_ul, "

@@ -170,10 +170,12 @@ sparse_apply_kernel(float* __restrict__ w, const int64_t* __restrict__ idx,
 #pragma unroll
         for (int j = 0; j < rh::kZeroRows; ++j) {
           if (static_cast<uint32_t>(j) < rz.r) {
-            const size_t cell = static_cast<size_t>(j) * rz.c + static_cast<size_t>(rh::ci_region(cw[j])) * rz.m +
-                                rh::in_region(pw[j], cw[j], rz.m);
-            rz.t1[cell] = 0.f;
-            if (rz.t2 != nullptr) rz.t2[cell] = 0.f;
+            const uint32_t region = rh::ci_region(cw[j]), grp = region / rz.g;
+            if (grp >= rz.L.g0 && grp < rz.L.g1) {  // (sharded server: this rank's groups only)
+              const size_t cell = rh::cell_at(region, rh::in_region(pw[j], cw[j], rz.m), j, rz.g, rz.m, rz.L);
+              rz.t1[cell] = 0.f;
+              if (rz.t2 != nullptr) rz.t2[cell] = 0.f;
+            }
           }
         }
       }
@@ -545,14 +547,14 @@ void launch_sparse_apply(float* w, const int64_t* idx, const float* vals, int64_
 void launch_sparse_apply_region_zero(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
                                      const float* lr_vec, int32_t* last_mod, int32_t round, const int32_t* step,
                                      int32_t* hist, float* t1, float* t2, const uint32_t* perm,
-                                     const uint32_t* cinfo, int r, int64_t c, int64_t m, int64_t nch, int64_t d,
-                                     hipStream_t stream) {
+                                     const uint32_t* cinfo, int r, int64_t g, int64_t m, int64_t nch, int64_t d,
+                                     RegionLayout L, hipStream_t stream) {
   if (k <= 0) return;
-  const rh::RegionZero rz{t1, t2, perm, cinfo, static_cast<uint32_t>(r), static_cast<uint32_t>(c),
-                          static_cast<uint32_t>(m), static_cast<uint32_t>(nch), static_cast<uint64_t>(d)};
+  const rh::RegionZero rz{t1, t2, perm, cinfo, static_cast<uint32_t>(r), static_cast<uint32_t>(g),
+                          static_cast<uint32_t>(m), static_cast<uint32_t>(nch), static_cast<uint64_t>(d), L};
   // 256-thread blocks: 4x the blocks of the plain apply for the scattered zeroing
   COMMEFF_LAUNCH(sparse_apply_kernel<true>, dim3((k + 255) / 256), dim3(256), 0, stream, w, idx, vals, k, lr,
-                     lr_vec, last_mod, round, step, hist, rz);
+                 lr_vec, last_mod, round, step, hist, rz);
 }
 
 void launch_dense_apply(float* w, const float* delta, int64_t n, float lr, const float* lr_vec,

@@ -102,26 +102,44 @@ void launch_cs_zero_buckets(float* t1, float* t2, const int64_t* idx,
 // P_j(o) | S_j(o) << 31; cinfo [r, nch] u32 = region | shift << 24 | sigma << 31;
 // lists [nch] chunks grouped (group-major, batches of W), goffs [G + 1].
 bool region_geometry_supported(int64_t r, int64_t m, int64_t g, int64_t W);
+// Table layout of a region sketch: cell (group grp, row j, bucket t of the
+// group) at (grp - g0) * gs + j * rs + t for grp in [g0, g1).  Row-major
+// [r][c]: {g*m, c, 0, G}; group-major [G'][r][g*m] (sharded server): {r*g*m,
+// g*m, g0, g1} with the tensor starting at group g0.
+struct RegionLayout {
+  uint32_t gs, rs, g0, g1;
+};
+// c: buckets per row (row-major: the unused tail past G*g*m is zeroed on overwrite)
 void launch_cs_region_encode(float* table, const float* vec, const float* wvec, float scale,
                              float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t g, int64_t G,
                              int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
-                             const int32_t* lists, const int32_t* goffs, bool overwrite,
+                             const int32_t* lists, const int32_t* goffs, bool overwrite, RegionLayout L,
                              hipStream_t stream, float* zero_vec = nullptr);  // zero_vec: vec, cleared
-// est[i] for the coordinates of chunks [q0, q1); hist0 != nullptr: also the
-// top-k's first histogram of est (see topk_prepare)
+// est[i] for the coordinates of chunks [q0, q1) whose group is in [L.g0, L.g1)
+// (one block per such group; the others are left unset); hist0 != nullptr:
+// also the top-k's first histogram of est (see topk_prepare)
 // mom_mode 1 / 2: the server momentum on the table first (1: V = rho V +
 // gscale G, table = E += V; 2: table = V = rho V + gscale G), see
-// sketch_region.hip RegionMom
-void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
-                            int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
+// sketch_region.hip RegionMom (V, G in the table's layout)
+void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t m, int64_t g,
+                            int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
-                            hipStream_t stream, const uint32_t* hint = nullptr, uint32_t* hist0 = nullptr,
-                            float* momV = nullptr, const float* momG = nullptr, float rho = 0.f,
-                            float gscale = 0.f, int mom_mode = 0, uint64_t* ballots = nullptr,
-                            uint32_t* segtot = nullptr);
+                            RegionLayout L, hipStream_t stream, const uint32_t* hint = nullptr,
+                            uint32_t* hist0 = nullptr, float* momV = nullptr, const float* momG = nullptr,
+                            float rho = 0.f, float gscale = 0.f, int mom_mode = 0,
+                            uint64_t* ballots = nullptr, uint32_t* segtot = nullptr,
+                            const int32_t* cpos = nullptr);  // cpos: est / ballots at compact chunk slots
+// zero the cells of idx (vals != 0) whose group is in [L.g0, L.g1)
 void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float* vals, int64_t k,
-                           int64_t d, int r, int64_t c, int64_t m, int64_t nch, const uint32_t* perm,
-                           const uint32_t* cinfo, hipStream_t stream);
+                           int64_t d, int r, int64_t g, int64_t m, int64_t nch, const uint32_t* perm,
+                           const uint32_t* cinfo, RegionLayout L, hipStream_t stream);
+// sharded-server k-list helpers (shard.hip)
+bool merge_packed_supported(int nl);
+// cmap (optional): idx are compact shard positions, global = cmap[idx / m] * m + idx % m
+void launch_topk_pack(const int64_t* idx, const float* vals, int64_t k, const int32_t* cmap, int64_t m,
+                      int64_t* out, hipStream_t stream);
+void launch_merge_packed(const int64_t* allp, int nl, int64_t k, float* vals, int64_t* idx, hipStream_t stream);
+void launch_gather_i64(const int64_t* src, const int64_t* pos, int64_t n, int64_t* out, hipStream_t stream);
 // out[0] = sqrt(lower-median_j sum_c table[j,c]^2); partial: >= r*256 floats
 void launch_cs_l2estimate(const float* table, int r, int64_t c, float* partial,
                           float* out, hipStream_t stream);
@@ -171,8 +189,8 @@ void launch_sparse_apply(float* w, const int64_t* idx, const float* vals,
 void launch_sparse_apply_region_zero(float* w, const int64_t* idx, const float* vals, int64_t k, float lr,
                                      const float* lr_vec, int32_t* last_mod, int32_t round, const int32_t* step,
                                      int32_t* hist, float* t1, float* t2, const uint32_t* perm,
-                                     const uint32_t* cinfo, int r, int64_t c, int64_t m, int64_t nch, int64_t d,
-                                     hipStream_t stream);
+                                     const uint32_t* cinfo, int r, int64_t g, int64_t m, int64_t nch, int64_t d,
+                                     RegionLayout L, hipStream_t stream);
 // w -= lr(i) * delta ; last_mod[i] = round where w changed
 // (step != nullptr: lr = bits of step[0], round = step[1], read on the device
 // so a captured HIP graph replays with the current round's values)

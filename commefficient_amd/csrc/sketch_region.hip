@@ -56,7 +56,7 @@ cs_region_encode_kernel(float* __restrict__ table, const float* __restrict__ vec
                         uint32_t c, uint32_t m, uint32_t g, uint32_t G, uint32_t nch, uint32_t r_rt,
                         const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
                         const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
-                        int overwrite, float* __restrict__ zero_vec) {
+                        int overwrite, float* __restrict__ zero_vec, RegionLayout L) {
   constexpr int NR = RT > 0 ? RT : kMaxRows;
   extern __shared__ __attribute__((aligned(16))) float acc[];  // [r][g * m]
   const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
@@ -152,9 +152,9 @@ cs_region_encode_kernel(float* __restrict__ table, const float* __restrict__ vec
   }
   __syncthreads();
   for (uint32_t j = 0; j < r; ++j) {
-    float* trow = table + static_cast<size_t>(j) * c + static_cast<size_t>(grp) * gm;
+    float* trow = table + static_cast<size_t>(grp - L.g0) * L.gs + static_cast<size_t>(j) * L.rs;
     for (uint32_t e = tid; e < gm; e += blockDim.x) trow[e] = overwrite ? acc[j * gm + e] : trow[e] + acc[j * gm + e];
-    if (overwrite && grp == 0)  // the unused buckets past G*g*m stay zero
+    if (overwrite && grp == 0 && L.rs == c)  // row-major: the unused buckets past G*g*m stay zero
       for (uint32_t e = G * gm + tid; e < c; e += blockDim.x) table[static_cast<size_t>(j) * c + e] = 0.f;
   }
 }
@@ -205,12 +205,12 @@ struct RegionMom {
 template <int RT, bool HIST>
 __global__ void __launch_bounds__(1024)
 cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint32_t d,
-                       uint32_t c, uint32_t m, uint32_t g, uint32_t nch, uint32_t r_rt,
+                       RegionLayout L, uint32_t m, uint32_t g, uint32_t nch, uint32_t r_rt,
                        const uint32_t* __restrict__ perm, const uint32_t* __restrict__ cinfo,
                        const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
                        uint32_t q0, uint32_t q1, int vec4, const uint32_t* __restrict__ hint,
                        uint32_t* __restrict__ hist0, RegionMom mom, uint64_t* __restrict__ ballots,
-                       uint32_t* __restrict__ segtot) {
+                       uint32_t* __restrict__ segtot, const int32_t* __restrict__ cpos) {
   // ballots (m == 64): per chunk of est the mask of keys >= hint, and the
   // per-segment (1,024 chunks) popcount totals: the top-k's candidate list
   // (csrc/topk.hip cand_compact_kernel)
@@ -225,10 +225,10 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
   constexpr int NR = RT > 0 ? RT : kMaxRows;
   extern __shared__ __attribute__((aligned(16))) float reg[];  // [r][g * m]
   const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
-  const uint32_t grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t grp = blockIdx.x + L.g0, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t W = blockDim.x >> 6, gm = g * m, rbase = grp * g;
   for (uint32_t j = 0; j < r; ++j) {
-    const size_t o = static_cast<size_t>(j) * c + static_cast<size_t>(grp) * gm;
+    const size_t o = static_cast<size_t>(blockIdx.x) * L.gs + static_cast<size_t>(j) * L.rs;
     float* src = table + o;
     float* dst = reg + j * gm;
     if (vec4) {
@@ -317,7 +317,9 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
           }
         }
         const float e = lower_median<RT>(v, rr);
-        est[static_cast<size_t>(q[u]) * m + lane] = e;
+        // (cpos: a sharded query's compact chunk positions, ascending in q)
+        const uint32_t qo = cpos != nullptr ? static_cast<uint32_t>(cpos[q[u]]) : q[u];
+        est[static_cast<size_t>(qo) * m + lane] = e;
         if constexpr (HIST) {
           const uint32_t key = __float_as_uint(e) & 0x7fffffffu;
           cand = key >= hlb;
@@ -328,8 +330,9 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
         if (ballots != nullptr) {
           const uint64_t bal = __ballot(cand);
           if (lane == 0) {
-            ballots[q[u] - q0] = bal;
-            atomicAdd(sh + ((q[u] - q0) >> 10), static_cast<uint32_t>(__popcll(bal)));
+            const uint32_t qb = (cpos != nullptr ? static_cast<uint32_t>(cpos[q[u]]) : q[u]) - q0;
+            ballots[qb] = bal;
+            atomicAdd(sh + (qb >> 10), static_cast<uint32_t>(__popcll(bal)));
           }
         }
       }
@@ -352,9 +355,9 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
 // zero cells (j, bucket_j(idx[t])) of t1 (and t2) where vals[t] != 0 (or always)
 __global__ void __launch_bounds__(256)
 cs_region_zero_kernel(float* __restrict__ t1, float* __restrict__ t2, const int64_t* __restrict__ idx,
-                      const float* __restrict__ vals, int64_t k, uint64_t d, uint32_t r, uint32_t c,
+                      const float* __restrict__ vals, int64_t k, uint64_t d, uint32_t r, uint32_t g,
                       uint32_t m, uint32_t nch, const uint32_t* __restrict__ perm,
-                      const uint32_t* __restrict__ cinfo) {
+                      const uint32_t* __restrict__ cinfo, RegionLayout L) {
   const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (e >= k * r) return;
   const int64_t t = e / r;
@@ -362,7 +365,8 @@ cs_region_zero_kernel(float* __restrict__ t1, float* __restrict__ t2, const int6
   if (vals != nullptr && vals[t] == 0.f) return;
   const uint64_t i = static_cast<uint64_t>(idx[t]);
   if (i >= d) return;  // (top-k indices are always in range)
-  const size_t cell = rh::cell_of(i, j, c, m, nch, perm, cinfo);
+  const size_t cell = rh::cell_of(i, j, g, m, nch, perm, cinfo, L);
+  if (cell == ~static_cast<size_t>(0)) return;  // another rank's group (sharded server)
   t1[cell] = 0.f;
   if (t2 != nullptr) t2[cell] = 0.f;
 }
@@ -387,7 +391,7 @@ bool region_geometry_supported(int64_t r, int64_t m, int64_t g, int64_t W) {
 void launch_cs_region_encode(float* table, const float* vec, const float* wvec, float scale,
                              float wscale, int64_t d, int r, int64_t c, int64_t m, int64_t g, int64_t G,
                              int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
-                             const int32_t* lists, const int32_t* goffs, bool overwrite,
+                             const int32_t* lists, const int32_t* goffs, bool overwrite, RegionLayout L,
                              hipStream_t stream, float* zero_vec) {
   const int lds = static_cast<int>(r * g * m * 4);
   const int nw = W > 16 ? 16 : static_cast<int>(W);
@@ -400,7 +404,7 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
                        scale, wscale, static_cast<uint32_t>(d), static_cast<uint32_t>(c),                \
                        static_cast<uint32_t>(m), static_cast<uint32_t>(g), static_cast<uint32_t>(G),     \
                        static_cast<uint32_t>(nch), static_cast<uint32_t>(r), perm, cinfo, lists, goffs,  \
-                       overwrite ? 1 : 0, zero_vec);                                                     \
+                       overwrite ? 1 : 0, zero_vec, L);                                                  \
   } while (0)
   const bool hw = wvec != nullptr && wscale != 0.f;
   if (W == 32) {  // two chunks per wave per batch
@@ -417,27 +421,27 @@ void launch_cs_region_encode(float* table, const float* vec, const float* wvec, 
 #undef COMMEFF_REGION_ENC
 }
 
-void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t c, int64_t m, int64_t g,
-                            int64_t G, int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
+void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t m, int64_t g,
+                            int64_t W, int64_t nch, const uint32_t* perm, const uint32_t* cinfo,
                             const int32_t* lists, const int32_t* goffs, int64_t q0, int64_t q1,
-                            hipStream_t stream, const uint32_t* hint, uint32_t* hist0, float* momV,
-                            const float* momG, float rho, float gscale, int mom_mode, uint64_t* ballots,
-                            uint32_t* segtot) {
+                            RegionLayout L, hipStream_t stream, const uint32_t* hint, uint32_t* hist0,
+                            float* momV, const float* momG, float rho, float gscale, int mom_mode,
+                            uint64_t* ballots, uint32_t* segtot, const int32_t* cpos) {
   const RegionMom mom{momV, momG, rho, gscale, mom_mode};
   if (m != 64 || hist0 == nullptr) ballots = nullptr;
-  if (q1 <= q0) return;
+  if (q1 <= q0 || L.g1 <= L.g0) return;
   const int lds = static_cast<int>(r * g * m * 4);
-  const int vec4 = ((g * m) % 4 == 0 && c % 4 == 0) ? 1 : 0;
-  const dim3 grid(static_cast<uint32_t>(G)), block(static_cast<uint32_t>(64 * (W > 16 ? 16 : W)));
+  const int vec4 = ((g * m) % 4 == 0 && L.gs % 4 == 0 && L.rs % 4 == 0) ? 1 : 0;
+  const dim3 grid(L.g1 - L.g0), block(static_cast<uint32_t>(64 * (W > 16 ? 16 : W)));
 #define COMMEFF_REGION_QRY(RR, HH)                                                                       \
   do {                                                                                                   \
     static int done = 0;                                                                                 \
     set_lds_once(cs_region_query_kernel<RR, HH>, lds, &done);                                            \
     COMMEFF_LAUNCH((cs_region_query_kernel<RR, HH>), grid, block, lds, stream, table, est,           \
-                       static_cast<uint32_t>(d), static_cast<uint32_t>(c), static_cast<uint32_t>(m),     \
+                       static_cast<uint32_t>(d), L, static_cast<uint32_t>(m),                            \
                        static_cast<uint32_t>(g), static_cast<uint32_t>(nch), static_cast<uint32_t>(r),   \
                        perm, cinfo, lists, goffs, static_cast<uint32_t>(q0), static_cast<uint32_t>(q1),  \
-                       vec4, hint, hist0, mom, ballots, segtot);                                         \
+                       vec4, hint, hist0, mom, ballots, segtot, cpos);                                   \
   } while (0)
   if (hist0 != nullptr) {
     if (r == 5) COMMEFF_REGION_QRY(5, true);
@@ -450,14 +454,14 @@ void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t 
 }
 
 void launch_cs_region_zero(float* t1, float* t2, const int64_t* idx, const float* vals, int64_t k,
-                           int64_t d, int r, int64_t c, int64_t m, int64_t nch, const uint32_t* perm,
-                           const uint32_t* cinfo, hipStream_t stream) {
+                           int64_t d, int r, int64_t g, int64_t m, int64_t nch, const uint32_t* perm,
+                           const uint32_t* cinfo, RegionLayout L, hipStream_t stream) {
   const int64_t n = k * r;
   if (n <= 0) return;
   COMMEFF_LAUNCH(cs_region_zero_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0,
-                     stream, t1, t2, idx, vals, k, static_cast<uint64_t>(d), static_cast<uint32_t>(r),
-                     static_cast<uint32_t>(c), static_cast<uint32_t>(m), static_cast<uint32_t>(nch), perm,
-                     cinfo);
+                 stream, t1, t2, idx, vals, k, static_cast<uint64_t>(d), static_cast<uint32_t>(r),
+                 static_cast<uint32_t>(g), static_cast<uint32_t>(m), static_cast<uint32_t>(nch), perm, cinfo,
+                 L);
 }
 
 }  // namespace commeff

@@ -107,10 +107,22 @@ std::vector<int64_t> graph_node_counts(int64_t graph) {
   return cnt;
 }
 
+// t.zero_() through the tape (a recorded round may clear buffers)
+void zero_(at::Tensor t) {
+  TORCH_CHECK(t.is_contiguous(), "zero_: contiguous tensors only");
+  if (t.numel() == 0) return;
+  if (t.is_cuda()) {
+    tape_memset(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream());
+  } else {
+    t.zero_();
+  }
+}
+
 }  // namespace
 }  // namespace commeff
 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
+  m.def("zero_(Tensor(a!) t) -> ()", &commeff::zero_);
   m.def("tape_begin() -> ()", &commeff::tape_begin);
   m.def("tape_end() -> int", &commeff::tape_end);
   m.def("tape_replay(int id) -> ()", &commeff::tape_replay);

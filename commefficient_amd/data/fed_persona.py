@@ -234,9 +234,25 @@ class SyntheticPersona(FedDataset):
     with max_history 2 the model input is ~70..240 tokens -- past the
     128-token short attention kernels, as real PersonaChat inputs are."""
 
+    TEXTS = ("uniform", "bigram")
+    BIGRAM_VOCAB, BIGRAM_FANOUT = 1024, 4
+
     def __init__(self, num_personalities=1000, dialogs_per_client=2, utterances_per_dialog=7,
                  num_candidates=2, max_history=2, vocab=50257, train=True, do_iid=False,
-                 num_clients=None, seed=0, sent_len=(8, 20), n_val=500, persona_sents=5):
+                 num_clients=None, seed=0, sent_len=(8, 20), n_val=500, persona_sents=5,
+                 text="uniform"):
+        """``text``: "uniform" -- i.i.d. uniform tokens (the throughput
+        benches: nothing to learn beyond the special tokens); "bigram" -- a
+        learnable language, the same for train and validation: 1,024 of the
+        vocabulary's tokens, each followed by one of 4 fixed successors chosen
+        uniformly (LM loss from ~ln 50257 = 10.8 at init down to ln 4 = 1.39
+        once the chain is learnt; tests/test_drivers.py)."""
+        assert text in self.TEXTS, text
+        self.text = text
+        if text == "bigram":
+            lang = np.random.RandomState(seed * 7919 + 0xB16)
+            self._sub = np.sort(lang.choice(vocab, self.BIGRAM_VOCAB, replace=False)).astype(np.int64)
+            self._succ = lang.randint(0, self.BIGRAM_VOCAB, size=(self.BIGRAM_VOCAB, self.BIGRAM_FANOUT))
         self.num_candidates, self.max_history, self.vocab = num_candidates, max_history, vocab
         self._np, self._dpc, self._upd = num_personalities, dialogs_per_client, utterances_per_dialog
         self._n_val = n_val
@@ -253,8 +269,25 @@ class SyntheticPersona(FedDataset):
         self.images_per_client = np.full(self._np, self._dpc * self._upd)
         self.num_val_images = self._n_val
 
+    def _walk(self, lens, start, choice):
+        """Bigram sentences: sentence i starts at sub-vocabulary token start[i]
+        and takes successor choice[i, t] at step t; returns token id lists."""
+        L = int(max(lens))
+        cur = np.asarray(start, dtype=np.int64) % self.BIGRAM_VOCAB
+        seq = np.empty((len(lens), L), dtype=np.int64)
+        seq[:, 0] = cur
+        for t in range(1, L):
+            cur = self._succ[cur, choice[:, t] % self.BIGRAM_FANOUT]
+            seq[:, t] = cur
+        ids = self._sub[seq]
+        return [ids[i, :n].tolist() for i, n in enumerate(lens)]
+
     def _sents(self, n):
         lo, hi = self._sent_len
+        if self.text == "bigram":
+            lens = [self._rng.randint(lo, hi) for _ in range(n)]
+            return self._walk(lens, self._rng.randint(0, self.BIGRAM_VOCAB, size=n),
+                              self._rng.randint(0, self.BIGRAM_FANOUT, size=(n, hi)))
         return [self._rng.randint(0, self.vocab, size=self._rng.randint(lo, hi)).tolist()
                 for _ in range(n)]
 
@@ -267,12 +300,17 @@ class SyntheticPersona(FedDataset):
         n_hist = min(2 * int(u) + 1, 2 * self.max_history + 1)
         n_sent = n_hist + max(2, self.num_candidates)
         lens = lo + (_hash64(key, np.arange(1, n_sent + 1)) % np.uint64(hi - lo)).astype(np.int64)
-        toks = (_hash64(key, np.arange(1000, 1000 + int(lens.sum()))) % np.uint64(self.vocab))
-        toks = toks.astype(np.int64).tolist()
-        sents, o = [], 0
-        for n in lens.tolist():
-            sents.append(toks[o:o + n])
-            o += n
+        if self.text == "bigram":
+            start = _hash64(key, np.arange(500, 500 + n_sent)).astype(np.int64) & 0xffff
+            choice = (_hash64(key, np.arange(1000, 1000 + n_sent * hi)) % np.uint64(self.BIGRAM_FANOUT))
+            sents = self._walk(lens.tolist(), start, choice.astype(np.int64).reshape(n_sent, hi))
+        else:
+            toks = (_hash64(key, np.arange(1000, 1000 + int(lens.sum()))) % np.uint64(self.vocab))
+            toks = toks.astype(np.int64).tolist()
+            sents, o = [], 0
+            for n in lens.tolist():
+                sents.append(toks[o:o + n])
+                o += n
         return utterance_to_inputs(persona, sents[:n_hist], sents[n_hist:], self.special_ids,
                                    self.num_candidates, self.max_history, train)
 

@@ -35,6 +35,29 @@ def topk_hint(tag, device) -> Optional[torch.Tensor]:
     return h
 
 
+def pack_topk(idx: torch.Tensor, vals: torch.Tensor, cmap: Optional[torch.Tensor] = None,
+              m: int = 1) -> torch.Tensor:
+    """int64 words idx << 32 | bits(vals) (``cmap``: idx are compact shard
+    positions, global = cmap[idx // m] * m + idx % m) -- csrc/shard.hip."""
+    return _ops().topk_pack(idx.contiguous(), vals.contiguous(), cmap, int(m))
+
+
+def merge_packed(allp: torch.Tensor, nl: int, k: int):
+    """(vals f32, idx int64) of nl packed k-lists (each ascending by index,
+    disjoint) in ascending index order."""
+    return _ops().merge_packed(allp.contiguous(), int(nl), int(k))
+
+
+def gather_i64(src: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+    return _ops().gather_i64(src.contiguous(), pos.contiguous())
+
+
+def zero_(t: torch.Tensor) -> None:
+    """``t.zero_()`` as a native memset (recordable by a launch tape,
+    parallel/tape.py); t contiguous."""
+    _ops().zero_(t)
+
+
 def topk_abs(x: torch.Tensor, k: int, hint: Optional[torch.Tensor] = None
              ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Deterministic magnitude top-k: (idx ascending int64, vals=x[idx]); ties -> lower index.

@@ -85,7 +85,8 @@ class CSVec:
             bs = bs.to(self.device)
             _hashes = (h, bo, bs)
         self.hashes, self.blk_off, self.blk_sign = _hashes
-        if table is None:
+        fresh = table is None
+        if fresh:
             table = torch.zeros(self.r, self.c, device=self.device, dtype=torch.float32)
         self.table = table
         # GPU encode/query plans, built once per geometry (the hash -> tile
@@ -98,6 +99,8 @@ class CSVec:
                 from .sketch_region import RegionHash
                 self._scratch["region"] = RegionHash(self.d, self.c, self.r, seed)
             self.region = self._scratch["region"]
+            if fresh and self._scratch.get("layout_world", 1) > 1:
+                self.table = self.new_table()
 
     # -- construction helpers -------------------------------------------------
     def like(self, table: Optional[torch.Tensor] = None) -> "CSVec":
@@ -270,19 +273,56 @@ class CSVec:
                               self.blk_sign, self.numBlocks, self.d)
 
     def zero_heavy_hitters_apply(self, idx: torch.Tensor, vals: torch.Tensor, other: Optional[torch.Tensor],
-                                 w: torch.Tensor, lr: float, lr_vec, last_mod, round_idx: int, hist) -> bool:
+                                 w: torch.Tensor, lr: float, lr_vec, last_mod, round_idx: int, hist,
+                                 step: Optional[torch.Tensor] = None, g0: int = 0) -> bool:
         """zero_heavy_hitters + ops.sparse_apply(w, idx, vals, ...) in one GPU
-        kernel (region family).  Returns False (nothing done) where the fused
-        kernel does not apply; the caller then runs the two steps."""
+        kernel (region family; ``g0``: a group-major shard's first group).
+        Returns False (nothing done) where the fused kernel does not apply;
+        the caller then runs the two steps."""
         if self.region is None or not self.table.is_cuda or w.numel() != self.d or self.r > 8:
             return False
         t = self.region.tensors(self.table.device)
         ops().cs_region_zero_apply(self.table, other, idx.contiguous(), vals.contiguous(), self.d,
                                    self.region.m, self.region.g, t["perm"], t["cinfo"], w, float(lr),
-                                   lr_vec, last_mod, int(round_idx), hist)
+                                   lr_vec, last_mod, int(round_idx), hist, step, int(g0))
         return True
 
+    # -- group-major tables (sharded server, parallel/server.py) -------------
+    def layout_world(self) -> int:
+        return getattr(self, "_layout_world", 1)
+
+    def set_group_layout(self, world: int):
+        """Tables of this sketch (and of ``like``/``new_table``) become the
+        padded group-major [world * Gp, r, g*m] of the region family, so a
+        reduce-scatter hands every rank a contiguous slice of whole groups."""
+        assert self.region is not None, "group layout: region family only"
+        self._layout_world = int(world)
+        self._scratch["layout_world"] = int(world)
+        self.table = self.new_table()
+
+    def table_shape(self):
+        w = self._scratch.get("layout_world", 1)
+        if self.region is None or w <= 1:
+            return (self.r, self.c)
+        h = self.region
+        return (w * h.shard_groups(w), self.r, h.g * h.m)
+
+    def table_numel(self) -> int:
+        n = 1
+        for x in self.table_shape():
+            n *= x
+        return n
+
+    def new_table(self) -> torch.Tensor:
+        return torch.zeros(self.table_shape(), device=self.device, dtype=torch.float32)
+
+    def table_view(self, flat: torch.Tensor) -> torch.Tensor:
+        return flat.view(self.table_shape())
+
     def l2estimate(self) -> torch.Tensor:
+        if self.table.dim() == 3:  # group-major: row sums over the groups
+            rs = self.table.double().square().sum(dim=(0, 2))
+            return rs.median().sqrt().float()
         return ops().cs_l2estimate(self.table)
 
     def __truediv__(self, other):

@@ -132,6 +132,77 @@ class RegionHash:
             self._cpu = (torch.from_numpy(b), torch.from_numpy(s))
         return self._cpu
 
+    # ---------------------------------------------------- table layouts
+    # A table is row-major [r, c] (every group) or group-major [Gs, r, g*m]
+    # holding groups [g0, g0 + Gs) -- the sharded server's per-rank state and
+    # its padded payload (csrc/kernels.h RegionLayout).
+    def shard_groups(self, world: int) -> int:
+        """Groups per rank of the sharded server (the payload pads G to
+        world * this)."""
+        return -(-self.G // int(world))
+
+    def cells(self, table: torch.Tensor, g0: int = 0):
+        """(cell [r, d] int64 flat index into ``table``, valid [d] bool: the
+        coordinate's group lies in the table) for the table's layout."""
+        key = (tuple(table.shape), int(g0))
+        cache = self.__dict__.setdefault("_cells", {})
+        if key not in cache:
+            b, _ = self.dense()
+            gm = self.g * self.m
+            grp = b // gm
+            if table.dim() == 3:
+                Gs = table.shape[0]
+                cell = (grp - g0) * (self.r * gm) + torch.arange(self.r).view(-1, 1) * gm + (b - grp * gm)
+                valid = (grp[0] >= g0) & (grp[0] < g0 + Gs)  # (a chunk's group is the same in every row)
+            else:
+                cell = torch.arange(self.r).view(-1, 1) * self.c + b
+                valid = torch.ones(self.d, dtype=torch.bool)
+            cache[key] = (torch.where(valid.view(1, -1), cell, torch.zeros_like(cell)), valid)
+        return cache[key]
+
+    def shard_ok(self, world: int, k: int) -> bool:
+        """Every rank's groups hold more than k coordinates (the sharded
+        server's per-rank top-k needs k < shard size)."""
+        Gp = self.shard_groups(world)
+        for r in range(world):
+            mine = int(np.sum((self.group >= r * Gp) & (self.group < (r + 1) * Gp)))
+            if mine * self.m - (self.nch * self.m - self.d) <= k:
+                return False
+        return True
+
+    def shard_maps(self, g0: int, g1: int, device):
+        """(cpos [nch] int32: compact position of every chunk of groups
+        [g0, g1), -1 elsewhere; cmap [nsh] int32: the shard's chunks ascending;
+        ncoord: its coordinates) -- the sharded query writes the shard's
+        estimates compactly, in ascending coordinate order."""
+        key = (int(g0), int(g1), str(torch.device(device)))
+        cache = self.__dict__.setdefault("_shard_maps", {})
+        if key not in cache:
+            mine = np.nonzero((self.group >= g0) & (self.group < g1))[0]
+            cpos = np.full(self.nch, -1, dtype=np.int32)
+            cpos[mine] = np.arange(len(mine), dtype=np.int32)
+            ncoord = len(mine) * self.m
+            if len(mine) and mine[-1] == self.nch - 1:  # the last chunk may be partial
+                ncoord -= self.nch * self.m - self.d
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+            cache[key] = (t(cpos), t(mine.astype(np.int32)), int(ncoord))
+        return cache[key]
+
+    def group_major(self, rm: torch.Tensor, world: int) -> torch.Tensor:
+        """Row-major [r, c] -> the padded group-major [world * Gp, r, g*m]."""
+        gm, Gp = self.g * self.m, self.shard_groups(world)
+        out = torch.zeros(world * Gp, self.r, gm, dtype=rm.dtype, device=rm.device)
+        out[:self.G] = rm.view(self.r, self.c)[:, :self.G * gm].reshape(self.r, self.G, gm).permute(1, 0, 2)
+        return out
+
+    def row_major(self, gmj: torch.Tensor, g0: int = 0) -> torch.Tensor:
+        """Group-major groups [g0, g0 + Gs) -> row-major [r, c] (zeros elsewhere)."""
+        gm = self.g * self.m
+        out = torch.zeros(self.r, self.c, dtype=gmj.dtype, device=gmj.device)
+        n = max(0, min(gmj.shape[0], self.G - g0))
+        out[:, g0 * gm:(g0 + n) * gm] = gmj[:n].permute(1, 0, 2).reshape(self.r, n * gm)
+        return out
+
     def buckets_of(self, idx: torch.Tensor) -> torch.Tensor:
         """[r, k] buckets of coordinates ``idx`` (host computation)."""
         i = idx.detach().cpu().numpy().astype(np.int64)
@@ -157,37 +228,42 @@ def encode(h: RegionHash, table: torch.Tensor, vec: torch.Tensor, scale: float =
     x = v.float() * scale
     if wvec is not None and wscale != 0.0:
         x = x + wscale * wvec.reshape(-1).float()
-    b, s = h.dense()
+    _, s = h.dense()
+    cell, valid = h.cells(table)
+    assert bool(valid.all()), "region encode: the table must hold every group"
     if overwrite:
         table.zero_()
-    tv = table.view(h.r, h.c)
+    tf = table.view(-1)
     for j in range(h.r):
-        tv[j].index_add_(0, b[j], s[j] * x)
+        tf.index_add_(0, cell[j], s[j] * x)
     return False
 
 
-def query(h: RegionHash, table: torch.Tensor, q0: int = 0, q1: int = -1) -> torch.Tensor:
+def query(h: RegionHash, table: torch.Tensor, q0: int = 0, q1: int = -1, g0: int = 0) -> torch.Tensor:
     """Lower median over rows of the signed cells of every coordinate (only
-    chunks [q0, q1) when given, the rest left unset on the GPU)."""
+    chunks [q0, q1) -- and, for a group-major shard, the coordinates of its
+    groups -- when given; the rest left unset on the GPU, 0 on the CPU)."""
     if table.is_cuda:
         t = h.tensors(table.device)
         return ops().cs_region_query(table, h.d, h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
-                                     t["goffs"], int(q0), int(q1))
-    b, s = h.dense()
-    tv = table.view(h.r, h.c)
-    vals = torch.stack([s[j] * tv[j][b[j]] for j in range(h.r)])
-    return vals.median(dim=0).values
+                                     t["goffs"], int(q0), int(q1), int(g0))
+    _, s = h.dense()
+    cell, valid = h.cells(table, g0)
+    tf = table.reshape(-1)
+    vals = torch.stack([s[j] * tf[cell[j]] for j in range(h.r)])
+    return torch.where(valid, vals.median(dim=0).values, torch.zeros((), dtype=vals.dtype))
 
 
 MOM_MODE = {"virtual": 1, "none": 2}
 
 
-def _topk_ws(h: RegionHash, device, q0: int, q1: int) -> Optional[torch.Tensor]:
+def _topk_ws(h: RegionHash, device, q0: int, q1: int, tag=None) -> Optional[torch.Tensor]:
     """The candidate-list top-k workspace of this hash and chunk range, kept
     across calls (zeroed once; the kernels leave it zeroed): no memset per
     call.  None when the op sizes its own."""
+    q1 = h.nch if q1 < 0 else q1
     cache = h.__dict__.setdefault("_topk_ws", {})
-    key = (str(device), int(q0), int(q1))
+    key = (str(device), int(q0), int(q1), tag)
     ws = cache.get(key)
     if ws is None:
         nb = int(ops().cs_region_topk_ws_bytes(h.d, h.m, int(q0), int(q1)))
@@ -196,7 +272,7 @@ def _topk_ws(h: RegionHash, device, q0: int, q1: int) -> Optional[torch.Tensor]:
 
 
 def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor] = None,
-         q0: int = 0, q1: int = -1, mom=None):
+         q0: int = 0, q1: int = -1, mom=None, g0: int = 0):
     """(idx, vals): the k largest-magnitude median estimates of the
     coordinates of chunks [q0, q1) (idx relative to q0*m, ascending; ties ->
     lower index).  GPU: one fused launch sequence -- the query also builds the
@@ -204,7 +280,9 @@ def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor
     ``mom = (V, G, rho, gscale, error_type)``: first the server momentum of
     ops.momentum_ef on the table (error_type "virtual": table is E, V = rho V +
     gscale G, E += V; "none": table is V = rho V + gscale G), on the GPU
-    inside the query's staging of the table (every region, whatever the range)."""
+    inside the query's staging of the table (every region, whatever the range).
+    A group-major shard (table [Gs, r, g*m] of groups [g0, g0 + Gs)): only
+    its groups' coordinates are candidates; idx are global and ascending."""
     q1 = h.nch if q1 < 0 else q1
     lo, hi = q0 * h.m, min(h.d, q1 * h.m)
     if table.is_cuda and 1 <= k < hi - lo:
@@ -216,6 +294,13 @@ def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor
             V, G, rho, gs, et = mom
             mode = MOM_MODE[et]
             mv, mg = (V.view(table.shape) if mode == 1 else None), G.view(table.shape)
+        if table.dim() == 3:  # a group-major shard: compact estimates, global idx
+            cpos, cmap, ncoord = h.shard_maps(g0, g0 + table.shape[0], table.device)
+            li, lv = ops().cs_region_topk(table, h.d, h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
+                                          t["goffs"], int(k), hint, 0, -1, mv, mg, float(rho), float(gs),
+                                          mode, _topk_ws(h, table.device, 0, -1, ("shard", g0)), int(g0),
+                                          cpos, ncoord)
+            return li, lv, cmap
         return ops().cs_region_topk(table, h.d, h.m, h.g, h.W, t["perm"], t["cinfo_l"], t["lists"],
                                     t["goffs"], int(k), hint, int(q0), int(q1), mv, mg, float(rho),
                                     float(gs), mode, _topk_ws(h, table.device, q0, q1))
@@ -223,29 +308,36 @@ def topk(h: RegionHash, table: torch.Tensor, k: int, hint: Optional[torch.Tensor
         from . import momentum_ef
         V, G, rho, gs, et = mom
         momentum_ef(V.view(-1), table.view(-1) if et == "virtual" else None, G.view(-1), rho, gs, et)
-    est = query(h, table, q0, q1)
+    est = query(h, table, q0, q1, g0)
+    if table.dim() == 3:  # candidates: the shard's coordinates only (ascending), global idx
+        _, valid = h.cells(table, g0)
+        cand = torch.nonzero(valid).view(-1)
+        p, v = ops().topk_abs(est[cand].contiguous(), int(k), hint)
+        return cand[p], v, None
     return ops().topk_abs(est[lo:hi].contiguous(), int(k), hint)
 
 
 def zero_buckets(h: RegionHash, t1: torch.Tensor, t2: Optional[torch.Tensor], idx: torch.Tensor,
-                 vals: Optional[torch.Tensor]):
+                 vals: Optional[torch.Tensor], g0: int = 0):
     """Zero cells (j, bucket_j(i)) of t1 (and t2) of the coordinates in idx
-    with nonzero vals (all of idx when vals is None)."""
+    with nonzero vals (all of idx when vals is None) -- for a group-major
+    shard only those of its groups."""
     if t1.is_cuda:
         t = h.tensors(t1.device)
         ops().cs_region_zero(t1, t2, idx.contiguous(), vals.contiguous() if vals is not None else None,
-                             h.d, h.m, h.g, t["perm"], t["cinfo"])
+                             h.d, h.m, h.g, t["perm"], t["cinfo"], int(g0))
         return
     sel = idx if vals is None else idx[vals != 0]
+    cell, valid = h.cells(t1, g0)
+    sel = sel[valid[sel]]
     if sel.numel() == 0:
         return
-    b = h.buckets_of(sel)
     for t in (t1, t2):
         if t is None:
             continue
-        tv = t.view(h.r, h.c)
+        tf = t.view(-1)
         for j in range(h.r):
-            tv[j, b[j]] = 0.0
+            tf[cell[j][sel]] = 0.0
 
 
 def collision_rate(h: RegionHash, pairs: int = 200000, seed: int = 0) -> float:

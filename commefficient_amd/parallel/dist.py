@@ -184,11 +184,36 @@ def h2d_into(out: torch.Tensor, x) -> torch.Tensor:
 
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:
     if _CTX.distributed:
+        from . import tape
+        if tape.eager_step(lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM)):
+            return t  # recorded round (parallel/tape.py): runs at replay
         if t.is_cuda and _CTX.backend == "gloo":
             # gloo reads device memory without ordering against the stream
             torch.cuda.current_stream().synchronize()
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
+
+
+def reduce_scatter_(out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+    """out (this rank's 1/N of t, summed over ranks) = reduce-scatter of the
+    contiguous ``t`` (rank r gets elements [r n, (r+1) n), n = out.numel()).
+    gloo has no reduce-scatter: all-reduce + slice (same sums)."""
+    if not _CTX.distributed:
+        out.copy_(t.view(out.shape))
+        return out
+    from . import tape
+    if tape.eager_step(lambda: dist.reduce_scatter_tensor(out.view(-1), t.view(-1))):
+        return out  # recorded round (parallel/tape.py): runs at replay
+    if _CTX.backend == "gloo":
+        if t.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        full = t.clone()
+        dist.all_reduce(full, op=dist.ReduceOp.SUM)
+        n = out.numel()
+        out.view(-1).copy_(full.view(-1)[_CTX.rank * n:(_CTX.rank + 1) * n])
+        return out
+    dist.reduce_scatter_tensor(out.view(-1), t.view(-1))
+    return out
 
 
 def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
@@ -198,6 +223,9 @@ def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
         return t
     out = torch.empty((_CTX.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                       device=t.device)
+    from . import tape
+    if tape.eager_step(lambda: dist.all_gather_into_tensor(out, t.contiguous())):
+        return out  # recorded round (parallel/tape.py): runs at replay
     if t.is_cuda and _CTX.backend == "gloo":
         torch.cuda.current_stream().synchronize()
         chunks = list(out.chunk(_CTX.world_size))

@@ -149,11 +149,21 @@ class FedModel:
             self.sketch = CSVec(self.d, args.num_cols, args.num_rows, device=self.device,
                                 numBlocks=args.num_blocks, seed=args.sketch_seed,
                                 kernel=args.encode)
-        self.server = ServerState(args, self.d, self.device, self.sketch)
+        # sharded FetchSGD server (server.py ServerState): region family on > 1
+        # rank -- the tables are reduce-scattered by region group
+        N = self.ctx.world_size
+        self.shard_server = (args.mode == "sketch" and self.sketch.region is not None and N > 1
+                             and getattr(args, "shard_unsketch", "on") == "on"
+                             and self.sketch.region.shard_ok(N, args.k))
+        if self.shard_server:
+            self.sketch.set_group_layout(N)
+            self._shard_G = self.sketch.region.shard_groups(N)
+        self.server = ServerState(args, self.d, self.device, self.sketch,
+                                  shard=(self.ctx.rank, N) if self.shard_server else None)
         self.client_state = ClientStateStore(args, self.d, self.num_clients, self.device,
                                              self.ctx.rank, self.ctx.world_size,
                                              init_weights=self.w)
-        main_numel = args.num_rows * args.num_cols if args.mode == "sketch" else self.d
+        main_numel = self.sketch.table_numel() if args.mode == "sketch" else self.d
         self.main_numel = main_numel
         self.accountant = ByteAccountant(args, self.d, self.num_clients, self.device,
                                          self.ctx.world_size, main_numel)
@@ -191,6 +201,15 @@ class FedModel:
         self._overlap = None  # bucketed all-reduce overlapped with backward (overlap.py)
         self._overlap_armed = False
         self._overlap_round = False
+        # recorded rounds replayed from C++ (parallel/tape.py)
+        self._tapes = None
+        if (self.device.type == "cuda" and getattr(args, "round_tape", "auto") != "off"
+                and os.environ.get("COMMEFF_TAPE", "1") != "0"):
+            from .tape import RoundTapes
+            self._tapes = RoundTapes(self.device)
+            self._tapes.call_ctx = lambda: self.timer.phase("allreduce")
+        self._tape_entries = {}
+        self._n_metrics = None
 
     # ------------------------------------------------------------------ API
     def attach_optimizer(self, opt):
@@ -276,7 +295,9 @@ class FedModel:
     def _payload_buf(self, n_metric_slots: int) -> torch.Tensor:
         n = self.main_numel + n_metric_slots
         if self._payload is None or self._payload.numel() < n:
-            self._payload = torch.empty(max(n, self.main_numel + 4096), device=self.device)
+            # zeros: the padding groups of a group-major payload (sharded server)
+            # are never written and must stay 0
+            self._payload = torch.zeros(max(n, self.main_numel + 4096), device=self.device)
         return self._payload[:n]
 
     def _assign(self, clients: np.ndarray) -> np.ndarray:
@@ -384,6 +405,12 @@ class FedModel:
             mbs = a.microbatch_size if a.microbatch_size and a.microbatch_size > 0 else 0
             if merged and 0 < mbs < int(sizes.sum()) and mbs % int(sizes[0]) != 0:
                 merged = False
+        if merged and self._tapes is not None and not self._fault_handling():
+            e = self._tape_entry(rb, int(counts[my_slots].sum()), W, B)
+            if e is not None:
+                out = self._train_taped(e, rb, order, starts, my_slots, counts, W, B, clients)
+                if out is not None:
+                    return out
         # metric slots: [n_metrics, W] appended to the payload; allocate after
         # we know n_metrics -> run compute first into a local list
         with self.timer.phase("compute"):
@@ -399,6 +426,7 @@ class FedModel:
         if metric_sums.data_ptr() != tail.data_ptr():
             tail.copy_(metric_sums.reshape(-1))
         sparse_bytes = None
+        G = None
         if merged and self._overlap_round:
             # the gradient buckets were all-reduced during the backward
             with self.timer.phase("allreduce"):
@@ -416,10 +444,11 @@ class FedModel:
             elif main is None:
                 payload[:self.main_numel].zero_()
             with self.timer.phase("allreduce"):
-                dist.all_reduce_(payload)
+                G = self._aggregate(payload)
+        if G is None:
+            G = payload[:self.main_numel]
         # G = summed transmit / B  (fed_aggregator.py:332); the division is
         # folded into the server's momentum kernel (gscale) -> keep a view
-        G = payload[:self.main_numel]
         if self.round_idx == getattr(a, "inject_nonfinite_round", -1):
             G[:1].fill_(float("nan"))  # fault injection: a corrupted aggregate
         # clone: the payload buffer is reused by the next round
@@ -442,10 +471,145 @@ class FedModel:
                                "sparse_allgather": True}
         else:
             self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
-                               "wire_bytes": self.accountant.wire_bytes_per_rank(payload.numel())}
+                               "wire_bytes": self._wire_bytes(payload.numel())}
+            if self.shard_server:
+                self.last_round["sharded_server"] = True
         if dropped:
             self.last_round["dropped_clients"] = dropped
         return [metrics[i] for i in range(n_res)] + [dl, ul]
+
+    # ------------------------------------------------------- recorded rounds
+    def _tape_entry(self, rb, n_local: int, W: int, B: int):
+        """The recorded-round entry for this geometry when the round can be
+        replayed from a launch tape (parallel/tape.py): merged clients whose
+        inputs come from the device loader, one microbatch, one LR group, no
+        BatchNorm (its running-statistics counter is a PyTorch op), no bf16
+        replica (GPT-2's GEMMs are hipBLASLt), no full phase timer, no overlapped
+        bucket reducer.  A geometry is first run eagerly (lazy initialisation),
+        recorded the second time and replayed from then on."""
+        a = self.args
+        if (rb.device_index is None or n_local == 0 or self.has_bn
+                or (self.timer.enabled and self.timer.only is None)
+                or self._shadow is not None or a.mode not in ("sketch", "uncompressed", "true_topk")
+                or (a.microbatch_size and 0 < a.microbatch_size < n_local)
+                or self.optimizer is None or len(self.optimizer.param_groups) != 1
+                or self._n_metrics is None
+                or (self.ctx.world_size > 1 and a.mode != "sketch")):
+            return None
+        key = (id(getattr(rb.device_gather, "__self__", rb.device_gather)), n_local, W, B)
+        if key in self._tapes.failed:
+            return None
+        e = self._tape_entries.get(key)
+        if e is None:
+            self._tape_entries[key] = e = {"key": key, "seen": 0, "compute": None, "server": None}
+        e["seen"] += 1
+        return e if e["seen"] >= 2 else None
+
+    def _train_taped(self, e, rb, order, starts, my_slots, counts, W, B, clients):
+        """A merged round through its launch tape: stage the round's host
+        arrays into the entry's static device buffer, replay (recording on
+        first use), account, and leave the server step pending."""
+        pos, slot_per_ex = self._merged_positions(order, starts, my_slots, counts)
+        n_local = len(pos)
+        n_res = self._n_metrics
+        idx2 = rb.device_index(pos)
+        meta = self.accountant.round_meta(clients)
+        host = np.concatenate([idx2.reshape(-1), slot_per_ex, counts.astype(np.int64), meta])
+        if e.get("packed") is None or e["packed"].numel() != host.size:
+            e["packed"] = torch.empty(host.size, dtype=torch.int64, device=self.device)
+            e["compute"] = e["server"] = None
+        dist.h2d_into(e["packed"], host)
+        parts, o = [], 0
+        for n in (2 * n_local, n_local, W, len(meta)):
+            parts.append(e["packed"][o:o + n])
+            o += n
+        payload = self._payload_buf(n_res * W)
+        if e.get("payload_ptr") != payload.data_ptr():
+            e["compute"] = e["server"] = None
+        if e["compute"] is None:
+            self._tape_free(e)
+
+            def body():
+                self.flat.zero_grad()
+                data = rb.device_gather(parts[0].view(2, n_local))
+                with prepared_conv_weights(self._native_3x3_weights()):
+                    pe, ms = self._fwd_bwd(data[:-1], data[-1], None, groups=1,
+                                           ex_groups=parts[1] if self._loss_groups else None)
+                tail = payload[self.main_numel:].view(n_res, W)
+                self._metric_sums([pe] + ms, parts[1], parts[2], W, out=tail)
+                self._encode_merged(payload[:self.main_numel], n_local)
+                return self._aggregate(payload)
+            e["compute"] = self._tapes.record(e["key"], body)
+            e["payload_ptr"] = payload.data_ptr()
+            if e["compute"] is None:  # incomplete tape: this geometry stays eager
+                self._tape_entries.pop(e["key"], None)
+                return None
+        with self.timer.phase("compute"):
+            self._tapes.replay(e["compute"])
+        G = e["compute"].result if e["compute"].result is not None else payload[:self.main_numel]
+        metrics = payload[self.main_numel:].view(n_res, W).clone()
+        dl, ul = self.accountant.round(clients, self.round_idx, meta=parts[3])
+        self._pending = (G, clients, 1.0 / B, e)
+        self.last_round = {"clients": W, "examples": B, "payload_bytes": payload.numel() * 4,
+                           "wire_bytes": self._wire_bytes(payload.numel()), "taped": True}
+        if self.shard_server:
+            self.last_round["sharded_server"] = True
+        return [metrics[i] for i in range(n_res)] + [dl, ul]
+
+    def _server_taped(self, e, G, gscale, lr):
+        """The server step of a recorded round: lr / round index through the
+        device step buffer, replay (recording on first use)."""
+        t = self._tapes
+        hist = self.accountant.hist_for(self.round_idx)
+        if e.get("step") is None:
+            e["step"] = torch.zeros(2, dtype=torch.int32, device=self.device)
+        lr_bits = int(np.array([lr], dtype=np.float32).view(np.int32)[0])
+        dist.h2d_into(e["step"], np.array([lr_bits, self.round_idx], dtype=np.int32))
+        if e["server"] is not None and e.get("hist_ptr") != (hist.data_ptr(), hist.numel()):
+            e["server"].free()
+            e["server"] = None
+        if e["server"] is None:
+            step = e["step"]
+            e["server"] = t.record(e["key"] + ("server",), lambda: self.server.update(
+                G, 0.0, self.w, self.accountant.last_mod, 0, None, None, hist=hist, gscale=gscale,
+                step=step))
+            e["hist_ptr"] = (hist.data_ptr(), hist.numel())
+            if e["server"] is None:
+                return False
+        t.replay(e["server"])
+        return True
+
+    def _tape_free(self, e):
+        for part in ("compute", "server"):
+            if e.get(part) is not None:
+                e[part].free()
+                e[part] = None
+
+    def _aggregate(self, payload: torch.Tensor):
+        """The round's one collective: all-reduce of the payload, or (sharded
+        server) reduce-scatter of the group-major tables + all-reduce of the
+        metric tail.  Returns this rank's G (the shard), or None (the payload)."""
+        if not self.shard_server:
+            dist.all_reduce_(payload)
+            return None
+        buf = getattr(self, "_shard_buf", None)
+        if buf is None:
+            self._shard_buf = buf = torch.empty(self.server.V.shape, device=self.device)
+        dist.reduce_scatter_(buf, payload[:self.main_numel])
+        dist.all_reduce_(payload[self.main_numel:])
+        return buf
+
+    def _wire_bytes(self, numel: int) -> float:
+        """Bytes one rank sends per round for the payload collectives (ring
+        algorithms): all-reduce 2 (N-1)/N 4n; sharded server: reduce-scatter
+        (N-1)/N of the table + all-reduce of the metrics + all-gather of the
+        packed k-lists ((N-1) 8k)."""
+        if not self.shard_server:
+            return self.accountant.wire_bytes_per_rank(numel)
+        N = self.ctx.world_size
+        tail = numel - self.main_numel
+        return ((N - 1) / N * 4.0 * self.main_numel + self.accountant.wire_bytes_per_rank(tail)
+                + (N - 1) * 8.0 * int(self.args.k))
 
     def _fault_handling(self) -> bool:
         a = self.args
@@ -481,7 +645,7 @@ class FedModel:
         a = self.args
         wscale = a.weight_decay / a.num_workers * n_local
         if a.mode == "sketch":
-            sk = self.sketch.like(out.view(a.num_rows, a.num_cols))
+            sk = self.sketch.like(self.sketch.table_view(out))
             # the encode is the flat gradient's last reader this round: the
             # region kernel clears it behind its reads (the next zero_grad
             # then skips its fill)
@@ -775,7 +939,7 @@ class FedModel:
                 self.flat.g.fill_(1.0)
                 transmit = self.flat.g
                 if a.mode == "sketch":
-                    sk = self.sketch.like(torch.zeros(a.num_rows, a.num_cols, device=self.device))
+                    sk = self.sketch.like(self.sketch.new_table())
                     sk.accumulateVec(self.flat.g)
                     transmit = sk.table.view(-1)
                 elif a.mode == "local_topk":
@@ -853,14 +1017,26 @@ class FedModel:
         k, wmax = sp["k"], sp["wmax"]
         allb = dist.all_gather_rows(sp["buf"])
         G.zero_()
-        for r, cnt in enumerate(sp["counts"]):
-            for j in range(cnt):
-                row = allb[r * wmax + j]
-                G.index_add_(0, row[:k].long(), row[k:].view(torch.float32))
+        rows = torch.from_numpy(np.concatenate(
+            [np.arange(r * wmax, r * wmax + cnt) for r, cnt in enumerate(sp["counts"])]).astype(np.int64))
+        if rows.numel():
+            # every list's (index, value) pairs in (rank, client) order, summed
+            # per index in that order: a stable sort by index keeps it, so
+            # duplicates across lists add up exactly as the sequential
+            # per-list accumulation did -- one sort + one segmented sum instead
+            # of a launch per list, and no atomics (bitwise equal on every rank)
+            sel = allb.index_select(0, rows.to(allb.device))
+            idx = sel[:, :k].reshape(-1).long()
+            val = sel[:, k:].reshape(-1).view(torch.float32)
+            idx, order = torch.sort(idx, stable=True)
+            val = val[order]
+            uniq, counts = torch.unique_consecutive(idx, return_counts=True)
+            G[uniq] = torch.segment_reduce(val, "sum", lengths=counts)
         return int(sp["buf"].numel() * 4)
 
     def _n_metrics_guess(self):
-        return getattr(self, "_n_metrics", 2)
+        n = getattr(self, "_n_metrics", None)
+        return n if n is not None else 2
 
     def _finish_client(self, c: int, n: int, g: Optional[torch.Tensor] = None):
         """fed_worker.py:184-230 local_step after the gradient ``g`` (default:
@@ -869,8 +1045,13 @@ class FedModel:
         a = self.args
         g = self.flat.g if g is None else g
         if a.mode == "sketch":
-            sk = self.sketch.like(torch.zeros(a.num_rows, a.num_cols, device=self.device))
-            sk.accumulateVec(g, float(n), dense=a.encode != "direct")
+            # one client table reused for every client (overwritten by the
+            # encode; the transmit is added to the upload before the next client)
+            tab = getattr(self, "_client_table", None)
+            if tab is None or tab.shape != self.sketch.table_shape():
+                self._client_table = tab = self.sketch.new_table()
+            sk = self.sketch.like(tab)
+            sk.accumulateVec(g, float(n), dense=a.encode != "direct", overwrite=True)
             if a.max_grad_norm is not None:
                 est = sk.l2estimate()
                 ops.clip_noise(sk.table.view(-1), est, a.max_grad_norm * n, 0.0)
@@ -1068,8 +1249,15 @@ class FedModel:
             self.fedavg_lr = float(lr)
         if self._pending is None:
             return  # e.g. the reference's "HACK STEP" before the first round
-        G, clients, gscale = self._pending
+        G, clients, gscale = self._pending[:3]
+        taped = self._pending[3] if len(self._pending) > 3 else None
         self._pending = None
+        if taped is not None and not torch.is_tensor(lr):
+            with self.timer.phase("server"):
+                ok = self._server_taped(taped, G, gscale, float(lr))
+            if ok:
+                self.round_idx += 1
+                return
         if getattr(self.args, "skip_nonfinite", 0) and not bool(torch.isfinite(G).all()):
             # failure detection: a NaN/Inf in the aggregate (a diverged or faulty
             # client) would poison V, E and the weights for good -> drop the round

@@ -16,6 +16,8 @@ from typing import List, Tuple
 import torch
 import torch.nn as nn
 
+from .. import ops
+
 
 def trainable_params(model: nn.Module) -> List[nn.Parameter]:
     return [p for p in model.parameters() if p.requires_grad]
@@ -73,6 +75,8 @@ class FlatParams:
     def zero_grad(self):
         if self.g_zeroed:
             self.g_zeroed = False  # the sketch encode already cleared g (fed_model._encode_merged)
+        elif self.g.is_cuda:
+            ops.zero_(self.g)  # (a memset a recorded round can replay, parallel/tape.py)
         else:
             self.g.zero_()
         # autograd may have replaced .grad (e.g. set_to_none elsewhere)

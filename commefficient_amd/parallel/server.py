@@ -85,23 +85,42 @@ class FedOptimizer(torch.optim.Optimizer):
 class ServerState:
     """Replicated server state + the mode-specific update."""
 
-    def __init__(self, args, d: int, device, sketch: Optional[CSVec]):
+    def __init__(self, args, d: int, device, sketch: Optional[CSVec], shard=None):
+        """``shard = (rank, world)``: the sharded FetchSGD server (region
+        family on > 1 rank).  The round's sketch tables are reduce-scattered
+        by region group (group-major layout, ``CSVec.set_group_layout``), and
+        rank r keeps only its groups [r Gp, (r+1) Gp) of V and E: the momentum /
+        error feedback, the median query and the top-k of its groups'
+        coordinates run on 1/N of the table, the k-lists are all-gathered as
+        packed words and merged in ascending coordinate order (csrc/shard.hip),
+        so the global top-k -- ties to the lower index -- is bitwise the
+        replicated one; each rank then zeroes the heavy hitters' buckets of
+        its own groups and applies the (replicated) weight step."""
         self.args = args
         self.d = d
         self.device = device
         self.sketch = sketch
+        self.shard = None
         mode = args.mode
         shape = (args.num_rows, args.num_cols) if mode == "sketch" else (d,)
+        if shard is not None and mode == "sketch":
+            rank, world = shard
+            h = sketch.region
+            Gp = h.shard_groups(world)
+            self.shard = (int(rank), int(world), rank * Gp, Gp)
+            shape = (Gp, args.num_rows, h.g * h.m)
         self.V = torch.zeros(shape, device=device)
         self.E = torch.zeros(shape, device=device)
         self.noise_round = 0
 
     def update(self, G: torch.Tensor, lr, w: torch.Tensor, last_mod: torch.Tensor, round_idx: int,
                client_state=None, participating=None, hist: Optional[torch.Tensor] = None,
-               gscale: float = 1.0):
+               gscale: float = 1.0, step: Optional[torch.Tensor] = None):
         """Apply one server step.  ``gscale * G`` is the summed transmit / B
         (the scale is folded into the momentum kernel); ``hist`` is the
-        accountant's change histogram, updated with the stamps.  Returns
+        accountant's change histogram, updated with the stamps.  ``step``
+        (device int32 [2] = lr bits, round) replaces the scalar lr / round_idx
+        in the apply kernels of a recorded round (parallel/tape.py).  Returns
         (idx, vals) for sparse modes (the un-scaled update), else None."""
         a = self.args
         rho = float(a.virtual_momentum)
@@ -111,6 +130,10 @@ class ServerState:
         # here on, unless the step is sparse (then the k changed coordinates
         # are patched into them)
         img_sync = weights_begin_update(w)
+        if mode == "sketch" and self.shard is not None:
+            idx, vals = self._sketch_sharded(G, rho, gscale, w, lr_s, lr_v, last_mod, round_idx, hist, step)
+            weights_end_update(img_sync, w, idx)
+            return idx, vals
         if mode == "sketch":
             et = a.error_type
             virt = et == "virtual"
@@ -120,7 +143,7 @@ class ServerState:
             mom = (self.V, G, rho, gscale, "virtual" if virt else "none")
             sk = self.sketch.like(src)
             ctx = dist.ctx()
-            if ctx.world_size > 1 and getattr(a, "shard_unsketch", "on") == "on":
+            if ctx.world_size > 1 and getattr(a, "shard_unsketch", "on") in ("on", "query"):
                 # every rank estimates 1/N of the coordinates and the k-lists
                 # are merged (bitwise the replicated result, ops/sketch.py)
                 idx, vals = sk.unsketch_sparse_sharded(a.k, ctx.rank, ctx.world_size,
@@ -131,9 +154,10 @@ class ServerState:
             # and the weight step (one kernel for the region family)
             other = self.V if et == "virtual" else None
             # (region family: one fused kernel; csvec layout: zeroing, then the apply)
-            if not sk.zero_heavy_hitters_apply(idx, vals, other, w, lr_s, lr_v, last_mod, round_idx, hist):
+            if not sk.zero_heavy_hitters_apply(idx, vals, other, w, lr_s, lr_v, last_mod, round_idx, hist,
+                                               step):
                 sk.zero_heavy_hitters(idx, vals, other)
-                ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, hist=hist)
+                ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
             weights_end_update(img_sync, w, idx)
             return idx, vals
         if mode == "true_topk":
@@ -142,7 +166,7 @@ class ServerState:
             if client_state is not None and participating is not None:
                 client_state.zero_velocity_at(participating, idx)
             ops.zero_at(idx, self.E, self.V)
-            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, hist=hist)
+            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
             weights_end_update(img_sync, w, idx)
             return idx, vals
         if mode in ("local_topk", "uncompressed"):
@@ -154,18 +178,54 @@ class ServerState:
                 ops.clip_noise(self.V, None, 0.0, a.noise_multiplier, seed=a.seed * 7919 + 17,
                                offset=self.noise_round * self.d)
                 self.noise_round += 1
-            ops.dense_apply(w, self.V, lr_s, lr_v, last_mod, round_idx, hist=hist)
+            ops.dense_apply(w, self.V, lr_s, lr_v, last_mod, round_idx, step, hist)
             return None
         if mode == "fedavg":
             ops.momentum_ef(self.V, None, G, rho, gscale, "none")
-            ops.dense_apply(w, self.V, 1.0, None, last_mod, round_idx, hist=hist)
+            ops.dense_apply(w, self.V, 1.0, None, last_mod, round_idx, step, hist)
             return None
         raise ValueError(mode)
 
+    def _sketch_sharded(self, G, rho, gscale, w, lr_s, lr_v, last_mod, round_idx, hist, step):
+        from ..ops import sketch_region as _rg
+        a = self.args
+        rank, world, g0, Gp = self.shard
+        k = int(a.k)
+        h = self.sketch.region
+        virt = a.error_type == "virtual"
+        src = self.E if virt else self.V
+        mom = (self.V, G.view(self.V.shape), rho, gscale, "virtual" if virt else "none")
+        hint = ops.topk_hint(("unsketch_groups", self.d, k, rank, world), self.device)
+        li, lv, cmap = _rg.topk(h, src, k, hint, mom=mom, g0=g0)
+        pack = ops.pack_topk(li, lv, cmap, h.m)
+        allp = dist.all_gather_rows(pack.view(1, k))
+        vm, im = ops.merge_packed(allp.view(-1), world, k)
+        pos, vals = ops.topk_abs(vm, k, ops.topk_hint(("merge_groups", self.d, k, world), self.device))
+        idx = ops.gather_i64(im, pos)
+        sk = self.sketch.like(src)
+        other = self.V if virt else None
+        if not sk.zero_heavy_hitters_apply(idx, vals, other, w, lr_s, lr_v, last_mod, round_idx, hist,
+                                           step, g0=g0):
+            _rg.zero_buckets(h, src, other, idx, vals, g0=g0)
+            ops.sparse_apply(w, idx, vals, lr_s, lr_v, last_mod, round_idx, step, hist)
+        return idx, vals
+
     def state_dict(self):
+        if self.shard is not None:  # every rank's groups, in the row-major [r, c] format
+            h = self.sketch.region
+            rank, world, g0, Gp = self.shard
+            V = h.row_major(dist.all_gather_rows(self.V.contiguous()))
+            E = h.row_major(dist.all_gather_rows(self.E.contiguous()))
+            return {"V": V.cpu(), "E": E.cpu(), "noise_round": self.noise_round}
         return {"V": self.V.cpu(), "E": self.E.cpu(), "noise_round": self.noise_round}
 
     def load_state_dict(self, sd):
-        self.V.copy_(sd["V"])
-        self.E.copy_(sd["E"])
+        if self.shard is not None:
+            h = self.sketch.region
+            rank, world, g0, Gp = self.shard
+            self.V.copy_(h.group_major(sd["V"].to(self.device), world)[g0:g0 + Gp])
+            self.E.copy_(h.group_major(sd["E"].to(self.device), world)[g0:g0 + Gp])
+        else:
+            self.V.copy_(sd["V"])
+            self.E.copy_(sd["E"])
         self.noise_round = int(sd.get("noise_round", 0))

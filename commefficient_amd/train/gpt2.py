@@ -34,12 +34,13 @@ from .cv import restore_driver_state, save_checkpoint
 def get_data_loaders(args, device, tokenizer=None):
     if args.synthetic:
         n_pers = args.num_clients or 1000
+        text = getattr(args, "synthetic_text", "uniform")
         tr = SyntheticPersona(num_personalities=n_pers, num_candidates=args.num_candidates,
                               max_history=args.max_history, train=True, do_iid=args.do_iid,
-                              num_clients=args.num_clients, seed=args.seed)
+                              num_clients=args.num_clients, seed=args.seed, text=text)
         te = SyntheticPersona(num_personalities=n_pers, num_candidates=args.num_candidates,
                               max_history=args.max_history, train=False, seed=args.seed,
-                              n_val=max(args.valid_batch_size * args.num_workers, 200))
+                              n_val=max(args.valid_batch_size * args.num_workers, 200), text=text)
     else:
         tr = FedPERSONA(tokenizer, args.num_candidates, args.max_history,
                         args.personality_permutations, args.dataset_dir, "PERSONA", None,

@@ -211,10 +211,18 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="GPT-2 blocks: native junction kernels (csrc/transformer.hip: fused "
                         "residual+dropout+LayerNorm, bias+GELU, bias gradients) around "
                         "hipBLASLt GEMMs and SDPA, or the HF module forward")
-    g.add_argument("--shard_unsketch", choices=["on", "off"], default="on",
-                   help="sketch mode on >1 rank: each rank runs the median query + top-k on "
-                        "its 1/N of the coordinates, the k-lists are all-gathered and merged "
-                        "(bitwise the replicated result; one all-gather of 2k int64 per rank)")
+    g.add_argument("--shard_unsketch", choices=["on", "query", "off"], default="on",
+                   help="sketch mode on >1 rank.  on: the sharded server -- region family: the "
+                        "tables are reduce-scattered by region group and each rank keeps V/E, "
+                        "runs the momentum, median query and top-k for its 1/N of the groups "
+                        "(csvec layout: as 'query'); query: all-reduce of the whole table, each "
+                        "rank queries 1/N of the coordinates; in both the k-lists are "
+                        "all-gathered and merged (bitwise the replicated result); off: every "
+                        "rank runs the whole server step")
+    g.add_argument("--round_tape", choices=["auto", "off"], default="auto",
+                   help="record a merged round of fixed geometry once and replay its native "
+                        "kernel launches from C++ afterwards (parallel/tape.py); off: every "
+                        "round is enqueued from Python")
     g.add_argument("--wgrad_stream", choices=["on", "off"], default="on",
                    help="native GPT-2 path: weight-gradient GEMMs on a side HIP stream, "
                         "overlapping the rest of the backward")
@@ -222,6 +230,9 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                    help="native GPT-2 path: token-wise ops (embeddings, GEMMs, LayerNorm/"
                         "GELU junctions) on the real tokens only, attention on the padded "
                         "layout (exact: right padding never reaches a real token)")
+    g.add_argument("--synthetic_text", choices=["uniform", "bigram"], default="uniform",
+                   help="--synthetic PersonaChat tokens: uniform i.i.d. (throughput benches) or a "
+                        "learnable bigram language over 1,024 tokens (learning tests)")
     g.add_argument("--gpt2_size", choices=["small", "mini", "tiny"], default="small",
                    help="GPT-2 architecture: 'small' = 124M GPT-2 (reference); 'mini' (2 x 256, "
                         "4 heads: native kernels) and 'tiny' (2 x 64) for tests")

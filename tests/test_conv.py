@@ -689,3 +689,35 @@ def test_kept_conv_images_match_fresh_prep(mode):
                 assert torch.equal(a, b)
     if mode != "uncompressed":
         assert any(c.fresh() for c in cnn._IMAGES.values())
+
+
+@pytest.mark.parametrize("N,C,H,K", [(500, 64, 32, 128), (500, 128, 16, 128), (500, 128, 16, 256),
+                                     (500, 256, 8, 512), (500, 256, 16, 128), (300, 512, 8, 256)])
+@pytest.mark.parametrize("epi", ["plain", "relu", "mask_add", "pool"])
+def test_persistent_halo_kernel_bench_batches(N, C, H, K, epi):
+    """The persistent pipelined halo kernel (``conv_fwd_pipe_kernel``: one
+    8-wave block per CU walking several 256-pixel tiles, next window and two
+    weight tiles in flight) at the ResNet-9 bench batch, where it is the one
+    the dispatcher picks, for every fused epilogue; (300, 512, 8, 256) has
+    fewer tiles than CUs (one tile per block, window double-buffering only)."""
+    x, w = _inputs(N, C, H, H, K, seed=N + C)
+    wf, _ = ops.conv_weight_prep(w)
+    ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
+    if epi == "pool":
+        if 128 % (2 * H) != 0:
+            pytest.skip("pool epilogue needs whole row pairs")
+        p, i = torch.ops.commeff.conv3x3_fwd_pool2(x, wf)
+        _close(p, F.max_pool2d(ref.relu(), 2))
+        y_ref = ops.conv3x3_fwd(x, wf, False)
+        p_ref, i_ref = torch.ops.commeff.relu_maxpool(y_ref, 2)
+        assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16)) and torch.equal(i, i_ref)
+        return
+    if epi == "mask_add":
+        g = torch.Generator(device="cuda").manual_seed(1)
+        mask = _nhwc(torch.randn(N, K, H, H, device="cuda", generator=g).to(torch.bfloat16))
+        add = _nhwc(torch.randn(N, K, H, H, device="cuda", generator=g).to(torch.bfloat16))
+        y = ops.conv3x3_fwd(x, wf, False, mask, add)
+        _close(y, torch.where(mask.float() > 0, ref, torch.zeros_like(ref)) + add.float())
+        return
+    y = ops.conv3x3_fwd(x, wf, epi == "relu")
+    _close(y, ref.relu() if epi == "relu" else ref)

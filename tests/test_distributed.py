@@ -40,6 +40,14 @@ def _run(rank, world, port, mode, out_dir, rounds):
                                    "300", "--sparse_allgather", "on"],
              "fedavg": ["--local_momentum", "0", "--virtual_momentum", "0.5",
                         "--fedavg_batch_size", "2"],
+             # the sharded server (reduce-scatter by region group) vs the
+             # query-sharded one on a table of 9 groups
+             "sketch_sharded": ["--error_type", "virtual", "--local_momentum", "0",
+                                "--virtual_momentum", "0.9", "--k", "300", "--num_rows", "3",
+                                "--num_cols", "20000", "--shard_unsketch", "on"],
+             "sketch_query": ["--error_type", "virtual", "--local_momentum", "0",
+                              "--virtual_momentum", "0.9", "--k", "300", "--num_rows", "3",
+                              "--num_cols", "20000", "--shard_unsketch", "query"],
              # simulated client failures (same draw on every rank)
              "sketch_dropout": ["--error_type", "virtual", "--local_momentum", "0",
                                 "--virtual_momentum", "0.9", "--k", "300", "--num_rows", "3",
@@ -48,7 +56,7 @@ def _run(rank, world, port, mode, out_dir, rounds):
              "uncompressed_dropout": ["--local_momentum", "0", "--virtual_momentum", "0.9",
                                       "--client_dropout", "0.95"]}[mode]
     lbs = "-1"
-    base = mode.replace("_sparse", "").replace("_dropout", "")
+    base = mode.replace("_sparse", "").replace("_dropout", "").replace("_sharded", "").replace("_query", "")
     args = parse_args(argv=["--mode", base, "--device", "cpu", "--dtype", "fp32",
                             "--num_clients", "40", "--num_workers", "6", "--local_batch_size", lbs,
                             "--dataset_name", "CIFAR10", "--synthetic"] + extra, probe_port=False)
@@ -66,11 +74,15 @@ def _run(rank, world, port, mode, out_dir, rounds):
         losses.append(loss.clone())
     if mode.endswith("_sparse"):
         assert fed.last_round.get("sparse_allgather"), fed.last_round
+    if mode == "sketch_sharded" and world > 1:
+        assert fed.last_round.get("sharded_server"), fed.last_round
+        assert fed.server.V.shape[0] == -(-9 // world)  # this rank's groups only
     if mode == "uncompressed" and world > 1:  # gradient buckets reduced during the backward
         assert fed.last_round.get("overlapped_buckets", 0) >= 2, fed.last_round
         assert fed.last_round.get("buckets_during_backward", 0) >= 1, fed.last_round
+    sd = fed.server.state_dict()  # (sharded: gathered into the row-major format)
     torch.save({"w": fed.w.clone(), "loss": torch.cat([l.reshape(-1) for l in losses]),
-                "dl": fed.accountant.client_download.clone()},
+                "dl": fed.accountant.client_download.clone(), "V": sd["V"], "E": sd["E"]},
                os.path.join(out_dir, f"r{rank}_w{world}.pt"))
     dist.shutdown()
 
@@ -91,6 +103,48 @@ def test_gloo_two_ranks_match_single_process(mode):
     torch.testing.assert_close(r0["w"], s["w"], rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(r0["loss"], s["loss"], rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(r0["dl"], s["dl"])
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_server_bitwise_equals_query_sharded(world):
+    """The sharded FetchSGD server (tables reduce-scattered by region group,
+    V / E / query / top-k per rank, packed k-lists merged in coordinate
+    order) against the all-reduce + query-sharded server on the same 2 gloo
+    ranks: the same sums, so bitwise the same weights, losses, accounting
+    and server state (gathered back into the row-major format)."""
+    rounds = 4
+    with tempfile.TemporaryDirectory() as d:
+        res = {}
+        for mode in ("sketch_sharded", "sketch_query"):
+            mp.start_processes(_run, args=(world, _free_port(), mode, d, rounds), nprocs=world,
+                               start_method="spawn", join=True)
+            res[mode] = [torch.load(os.path.join(d, f"r{r}_w{world}.pt"), weights_only=True)
+                         for r in range(world)]
+    a, b = res["sketch_sharded"], res["sketch_query"]
+    for r in range(world):
+        for key in ("w", "loss", "dl", "V", "E"):
+            assert torch.equal(a[r][key], b[r][key]), (r, key)
+
+
+def test_sharded_server_three_ranks_match_single_process():
+    """3 ranks (9 groups, 3 per rank): replicas bitwise identical, and the
+    same run as one process up to the collective's summation order (a ring
+    all-reduce / reduce-scatter of 3 ranks adds in a position-dependent
+    order, and the group-major payload puts a cell at another position than
+    the row-major one -- so unlike 2 ranks, not bitwise the query path)."""
+    rounds = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_run, args=(3, _free_port(), "sketch_sharded", d, rounds), nprocs=3,
+                           start_method="spawn", join=True)
+        mp.start_processes(_run, args=(1, _free_port(), "sketch_sharded", d, rounds), nprocs=1,
+                           start_method="spawn", join=True)
+        rs = [torch.load(os.path.join(d, f"r{r}_w3.pt"), weights_only=True) for r in range(3)]
+        s = torch.load(os.path.join(d, "r0_w1.pt"), weights_only=True)
+    for r in (1, 2):
+        assert torch.equal(rs[0]["w"], rs[r]["w"]) and torch.equal(rs[0]["V"], rs[r]["V"])
+    torch.testing.assert_close(rs[0]["w"], s["w"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rs[0]["loss"], s["loss"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rs[0]["V"], s["V"], rtol=1e-3, atol=1e-5)
 
 
 @pytest.mark.gpu

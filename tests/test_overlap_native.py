@@ -46,7 +46,7 @@ def test_native_backward_marks_buckets_ready():
     ovl._issue = record
     assert len(ovl.buckets) >= 4, len(ovl.buckets)
     fed.flat.zero_grad()
-    _, x, y = batch
+    x, y = batch.take(np.arange(len(batch)))
     ovl.arm()
     with fed._autocast(cache=False):
         per_ex, _ = cv_loss(fed.model, fed._prep((x,)), y, args)
@@ -80,7 +80,7 @@ def test_native_backward_grad_ready_follows_backward_order():
         ovl._issue = lambda b: issued_at.append((b, len(order)))
         ovl.works = [None] * len(ovl.buckets)
         fed.flat.zero_grad()
-        _, x, y = batch
+        x, y = batch.take(np.arange(len(batch)))
         ovl.arm()
         with fed._autocast(cache=False):
             per_ex, _ = cv_loss(fed.model, fed._prep((x,)), y, args)

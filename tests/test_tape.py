@@ -1,0 +1,95 @@
+"""Launch tapes (parallel/tape.py, csrc/launch.h, csrc/tape.cpp): a recorded
+round replayed from C++ must give bitwise the eager round's results, and a
+recording that contains a launch outside the tape must be refused."""
+import numpy as np
+import pytest
+import torch
+
+
+@pytest.mark.gpu
+def test_tape_records_native_launches_and_refuses_foreign_kernels():
+    from commefficient_amd import ops
+    from commefficient_amd.parallel.tape import RoundTapes
+    dev = torch.device("cuda", 0)
+    t = torch.ones(1000, device=dev)
+    u = torch.ones(10, device=dev)
+    tapes = RoundTapes(dev)
+    rep = tapes.record("native", lambda: ops.zero_(t))
+    assert rep is not None
+    torch.cuda.synchronize()
+    assert t.sum().item() == 1000  # nothing executed while recording
+    tapes.replay(rep)
+    torch.cuda.synchronize()
+    assert t.abs().sum().item() == 0
+    t.fill_(2.0)
+    tapes.replay(rep)
+    torch.cuda.synchronize()
+    assert t.abs().sum().item() == 0
+    with pytest.warns(UserWarning, match="incomplete"):
+        bad = tapes.record("foreign", lambda: (ops.zero_(t), u.add_(1.0)))
+    assert bad is None and "foreign" in tapes.failed
+
+
+def _bench_engine(mode: str, tape: str, W: int = 40, n: int = 5):
+    from commefficient_amd import models
+    from commefficient_amd.data import make_synthetic
+    from commefficient_amd.data.device_loader import DeviceFedLoader
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd.train.losses import cv_loss
+    from commefficient_amd.utils.args import parse_args
+    dist.init("cuda")
+    extra = {"sketch": ["--error_type", "virtual", "--local_momentum", "0", "--virtual_momentum",
+                        "0.9", "--k", "20000", "--num_rows", "5", "--num_cols", "200000"],
+             "true_topk": ["--error_type", "virtual", "--local_momentum", "0",
+                           "--virtual_momentum", "0.9", "--k", "20000"],
+             "uncompressed": ["--local_momentum", "0", "--virtual_momentum", "0.9"]}[mode]
+    args = parse_args(argv=["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", "2000",
+                            "--mode", mode, "--num_clients", "400", "--num_workers", str(W),
+                            "--local_batch_size", "-1", "--weight_decay", "5e-4", "--dtype", "bf16",
+                            "--device", "cuda", "--seed", "21", "--round_tape", tape] + extra,
+                      probe_port=False)
+    torch.manual_seed(args.seed)
+    np.random.seed(args.seed)
+    ds = make_synthetic("CIFAR10", train=True, num_clients=400, size=2000, seed=args.seed)
+    loader = DeviceFedLoader(ds, W, -1, "cuda", seed=args.seed, augment=True, out_bf16=True)
+    model = models.build_model(args, 10)
+    fed = FedModel(model, cv_loss, args, num_clients=400)
+    opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), args, fed)
+    return fed, opt, loader, ds, W
+
+
+def _run(fed, opt, loader, ds, W, rounds):
+    losses, dls = [], []
+    it = iter(loader.sampler)
+    done = 0
+    while done < rounds:
+        r = next(it)
+        cids = ds.client_of(r)
+        if len(np.unique(cids)) < W:
+            continue
+        out = fed(loader.make_batch(cids, ds.data_index(r)))
+        opt.param_groups[0]["lr"] = 0.1 * (1 + done % 3)  # a changing LR reaches the replay
+        opt.step()
+        losses.append(out[0].clone())
+        dls.append(out[2].clone())
+        done += 1
+    torch.cuda.synchronize()
+    return torch.stack(losses), torch.stack(dls)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["sketch", "true_topk", "uncompressed"])
+def test_taped_rounds_bitwise_equal_eager(mode):
+    rounds = 7
+    res = {}
+    for tape in ("off", "auto"):
+        fed, opt, loader, ds, W = _bench_engine(mode, tape)
+        losses, dls = _run(fed, opt, loader, ds, W, rounds)
+        res[tape] = (fed.w.clone(), losses, dls, fed.accountant.last_mod.clone(), fed.server.V.clone())
+        if tape == "auto":
+            assert fed.last_round.get("taped"), fed.last_round
+            assert fed._tapes.replays >= 2 * (rounds - 2), fed._tapes.replays
+    for a, b in zip(res["off"], res["auto"]):
+        assert torch.equal(a, b), (a - b).abs().max()
