@@ -1652,7 +1652,7 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   // CU at least one (ResNet-9: all but res3, whose 8 K-step windows per tile
   // keep the split kernel below)
   // (COMMEFF_CONV_PIPE=2: whenever the geometry fits, for tests at small batches)
-  if (halo_on && pipe_on && a.unpool_idx == nullptr && halo_geom(a.H, a.W, a.K, 256, &hg) &&
+  if (halo_on && pipe_on && halo_geom(a.H, a.W, a.K, 256, &hg) &&
       (pipe_on == 2 || static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) >= cu_count())) {
     if (a.pool == 2) launch_fwd_pipe<true, 128>(a, hg, stream); else launch_fwd_pipe<false, 128>(a, hg, stream);
     return;

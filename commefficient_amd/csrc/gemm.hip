@@ -1,0 +1,274 @@
+// Dense bf16 GEMMs of the model layers on the gfx950 MFMA:
+//
+//   C[M][N] = act(A[M][K] . op(B) + bias[N]) (+ beta * C)      fp32 accumulation
+//     NT: B stored [N][K] (K contiguous)  -- Linear forward with the weight as
+//         [out][in], 1x1-conv forward ([K_out][C_in]), GPT-2 input gradients
+//         (dY [T][out] . W[in][out]^T), the tied LM head (hid . wte^T);
+//     NN: B stored [K][N] (N contiguous)  -- HF Conv1D forward (X . W[in][out]),
+//         1x1-conv input gradients (dY . W[K_out][C_in]).
+//   act: none or tanh-GELU (GPT-2 MLP; the pre-activation is stored too).
+//
+// Replaces the hipBLASLt (Cijk_*) GEMMs of the GPT-2 blocks (reference model:
+// /root/reference/CommEfficient/gpt2_train.py:262-273, HF GPT2DoubleHeads) and
+// of the ResNet bottlenecks' 1x1 convs (models/resnets.py:76-130).
+//
+// Tile: BM = 128 rows x BN (128 or 64) columns per 4-wave block (waves 2 x 2,
+// 64 x BN/2 each, 32x32x16 MFMAs), 64-deep K-steps through a two-stage LDS
+// ring filled by LDS DMA (global_load_lds, 16 bytes a lane, no staging
+// registers), one raw s_barrier per K-step, two blocks per CU (the measured
+// best trade of ring depth for occupancy on the conv kernels, conv.hip).  A
+// (and B for NT) is staged [rows][64 k] with the XOR swizzle applied on the
+// SOURCE address (the DMA writes lane-linearly) and read with ds_read_b128;
+// B for NN is staged K-major [64 k][BN] and read with the transposing
+// ds_read_b64_tr_b16.  Rows past M load a zero page and are not stored.
+// Tile -> block mapping is XCD-aware.  The epilogue stages the fp32 tile
+// through LDS and writes 16-byte rows.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+#include "conv_common.h"
+
+namespace commeff {
+namespace {
+
+constexpr int GK = 64;  // K-step
+
+__device__ __attribute__((aligned(16))) uint32_t g_mm_zero[4] = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ void mm_glds16(const void* src, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+template <int BN, bool NN>
+struct MmCfg {
+  static constexpr int BM = 128, NT = 256;
+  static constexpr int A_BYTES = BM * GK * 2;          // [128 rows][64 k]
+  static constexpr int B_BYTES = BN * GK * 2;          // NT: [BN rows][64 k]; NN: [64 k][BN]
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int ALD = A_BYTES / 16 / NT;        // 4
+  static constexpr int BLD = B_BYTES / 16 / NT;        // 4 or 2
+  static constexpr int LD = BN + 4;                    // epilogue fp32 row stride
+  static constexpr int EPI = BM * LD * 4;
+  static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+};
+
+template <int BN, bool NN, int ACT, bool F32>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
+  using Cfg = MmCfg<BN, NN>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NI = BN / 64, ALD = Cfg::ALD, BLD = Cfg::BLD;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, hi = lane >> 5, lr = lane & 31;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntn = a.N / BN;
+  const int m0 = (bid / ntn) * Cfg::BM, n0 = (bid % ntn) * BN;
+  const int KT = a.K / GK;
+  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_mm_zero);
+
+  // A pieces: slot s = i*256 + tid -> (row s >> 3, swizzled chunk)
+  const uint16_t* a_ptr[ALD];
+#pragma unroll
+  for (int i = 0; i < ALD; ++i) {
+    const int s = i * 256 + tid, row = s >> 3, lc = (s & 7) ^ sw_rd128(row);
+    a_ptr[i] = m0 + row < a.M ? a.A + static_cast<int64_t>(m0 + row) * a.lda + lc * 8 : nullptr;
+  }
+  const uint16_t* b_ptr[BLD];
+#pragma unroll
+  for (int j = 0; j < BLD; ++j) {
+    const int s = j * 256 + tid;
+    if constexpr (NN) {  // [64 k][BN]: rows of BN/8 chunks, transposed-read swizzle
+      constexpr int CPR = BN / 8;
+      const int row = s / CPR, ch = s % CPR;
+      const int lc = BN == 128 ? (ch ^ sw_tr256(row)) : (ch ^ sw_tr128(row));
+      b_ptr[j] = a.B + static_cast<int64_t>(row) * a.ldb + n0 + lc * 8;
+    } else {
+      const int row = s >> 3, lc = (s & 7) ^ sw_rd128(row);
+      b_ptr[j] = a.B + static_cast<int64_t>(n0 + row) * a.ldb + lc * 8;
+    }
+  }
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+    unsigned char* base = smem + stage * Cfg::STAGE + wid * 1024;
+#pragma unroll
+    for (int i = 0; i < ALD; ++i) mm_glds16(a_ptr[i] != nullptr ? a_ptr[i] + kt * GK : zero, base + i * 4096);
+#pragma unroll
+    for (int j = 0; j < BLD; ++j) {
+      const uint16_t* src = NN ? b_ptr[j] + static_cast<int64_t>(kt) * GK * a.ldb : b_ptr[j] + kt * GK;
+      mm_glds16(src, base + Cfg::A_BYTES + j * 4096);
+    }
+  };
+
+  // fragment offsets (bytes inside a stage)
+  int offA[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int row = wr * 64 + mi * 32 + lr, chk = 2 * kk + hi;
+      offA[kk][mi] = row * 128 + ((chk ^ sw_rd128(row)) << 4);
+    }
+  int offB[4][NI];   // NT
+  int toB[NI][2];    // NN: transposed reads, +kk*16 rows
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    if constexpr (NN) {
+      if constexpr (BN == 128) tr_offsets<256>(wc * (BN / 2) + ni * 32, lane, toB[ni]);
+      else tr_offsets<128>(wc * (BN / 2) + ni * 32, lane, toB[ni]);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int row = wc * (BN / 2) + ni * 32 + lr, chk = 2 * kk + hi;
+        offB[kk][ni] = row * 128 + ((chk ^ sw_rd128(row)) << 4);
+      }
+    }
+  }
+  constexpr int BROW = BN * 2;  // NN image row bytes
+
+  f32x16_t acc[2][NI];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
+
+  if (KT > 0) issue(0, 0);
+  for (int kt = 0; kt < KT; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < KT) issue((kt + 1) & 1, kt + 1);
+    const unsigned char* sA = smem + (kt & 1) * Cfg::STAGE;
+    const unsigned char* sB = sA + Cfg::A_BYTES;
+    bf16x8_t af[2][2], bfr[2][NI];
+    auto load = [&](int kk, int buf) __attribute__((always_inline)) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) af[buf][mi] = *reinterpret_cast<const bf16x8_t*>(sA + offA[kk][mi]);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        if constexpr (NN) {
+          const int dd = kk * 16 * BROW;
+          bfr[buf][ni] = tr_read(sB + toB[ni][0] + dd, sB + toB[ni][1] + dd);
+        } else {
+          bfr[buf][ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[kk][ni]);
+        }
+      }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int cur = kk & 1;
+      if (kk + 1 < 4) load(kk + 1, cur ^ 1);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // ---- epilogue: fp32 tile through LDS -> bias / beta / act -> 16-byte rows
+  float* ct = reinterpret_cast<float*>(smem);
+  constexpr int LD = Cfg::LD;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        ct[row * LD + wc * (BN / 2) + ni * 32 + lr] = acc[mi][ni][e];
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int e = tid; e < Cfg::BM * CPR; e += 256) {
+    const int row = e / CPR, cc = e - row * CPR, m = m0 + row;
+    if (m >= a.M) continue;
+    const int n = n0 + cc * 8;
+    const float4 lo = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8);
+    const float4 up = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8 + 4);
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, up.x, up.y, up.z, up.w};
+    if (a.bias != nullptr) {
+      const float4 b0 = *reinterpret_cast<const float4*>(a.bias + n);
+      const float4 b1 = *reinterpret_cast<const float4*>(a.bias + n + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
+    const int64_t o = static_cast<int64_t>(m) * a.ldc + n;
+    if constexpr (F32) {
+      float* c = reinterpret_cast<float*>(a.C) + o;
+      if (a.beta != 0.f) {
+        const float4 c0 = *reinterpret_cast<const float4*>(c), c1 = *reinterpret_cast<const float4*>(c + 4);
+        v[0] += a.beta * c0.x; v[1] += a.beta * c0.y; v[2] += a.beta * c0.z; v[3] += a.beta * c0.w;
+        v[4] += a.beta * c1.x; v[5] += a.beta * c1.y; v[6] += a.beta * c1.z; v[7] += a.beta * c1.w;
+      }
+      *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      uint16_t* c = reinterpret_cast<uint16_t*>(a.C) + o;
+      if (a.beta != 0.f) {
+        const v4u old = *reinterpret_cast<const v4u*>(c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += a.beta * bf2f((old[j >> 1] >> (16 * (j & 1))) & 0xffffu);
+      }
+      if constexpr (ACT == 1) {  // tanh-GELU; the pre-activation goes to C2
+        v4u pre;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pre[j] = pack_bf16(v[2 * j], v[2 * j + 1]);
+        *reinterpret_cast<v4u*>(reinterpret_cast<uint16_t*>(a.C2) + o) = pre;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(bf2f((pre[j >> 1] >> (16 * (j & 1))) & 0xffffu));
+      }
+      v4u out;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[j] = pack_bf16(v[2 * j], v[2 * j + 1]);
+      *reinterpret_cast<v4u*>(c) = out;
+    }
+  }
+}
+
+template <int BN, bool NN, int ACT, bool F32>
+void launch_gemm_t(const GemmArgs& a, hipStream_t stream) {
+  constexpr int lds = MmCfg<BN, NN>::LDS;
+  static bool init = false;
+  if (!init) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<BN, NN, ACT, F32>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    init = true;
+  }
+  const int tiles = ((a.M + 127) / 128) * (a.N / BN);
+  COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32>), dim3(tiles), dim3(256), lds, stream, a);
+}
+
+}  // namespace
+
+bool gemm_supported(int M, int N, int K, bool nn) {
+  (void)nn;
+  return M >= 1 && N >= 64 && N % 64 == 0 && K >= 64 && K % 64 == 0;
+}
+
+void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream) {
+  if (a.M <= 0) return;
+  // 128-wide column tiles when they still give ~every resident slot (2 per CU) a block
+  const bool wide = a.N % 128 == 0 && static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) >= 384;
+  if (act == 1) {
+    if (wide) { if (nn) launch_gemm_t<128, true, 1, false>(a, stream); else launch_gemm_t<128, false, 1, false>(a, stream); }
+    else { if (nn) launch_gemm_t<64, true, 1, false>(a, stream); else launch_gemm_t<64, false, 1, false>(a, stream); }
+    return;
+  }
+  if (f32) {
+    if (wide) { if (nn) launch_gemm_t<128, true, 0, true>(a, stream); else launch_gemm_t<128, false, 0, true>(a, stream); }
+    else { if (nn) launch_gemm_t<64, true, 0, true>(a, stream); else launch_gemm_t<64, false, 0, true>(a, stream); }
+    return;
+  }
+  if (wide) { if (nn) launch_gemm_t<128, true, 0, false>(a, stream); else launch_gemm_t<128, false, 0, false>(a, stream); }
+  else { if (nn) launch_gemm_t<64, true, 0, false>(a, stream); else launch_gemm_t<64, false, 0, false>(a, stream); }
+}
+
+}  // namespace commeff

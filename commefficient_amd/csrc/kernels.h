@@ -480,6 +480,23 @@ void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
 // C[M][N] (fp32, row stride ldc) += A^T B, A [T][lda] and B [T][ldb] bf16
 // (gemm_tn.hip; M, N multiples of 256, lda / ldb multiples of 8); split-K
 // over T with fp32 slabs [splits][M][N] summed into C in a fixed order
+// C[M][N] = act(A[M][K] . op(B) + bias) (+ beta C); NT: B [N][K], NN: B [K][N]
+// (gemm.hip).  bf16 operands / output (f32: fp32 output), act 1: tanh-GELU with
+// the pre-activation written to C2.  N % 64 == 0, K % 64 == 0.
+struct GemmArgs {
+  const uint16_t* A;
+  int64_t lda;
+  const uint16_t* B;
+  int64_t ldb;
+  void* C;
+  int64_t ldc;
+  void* C2;
+  const float* bias;
+  int M, N, K;
+  float beta;
+};
+bool gemm_supported(int M, int N, int K, bool nn);
+void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);
 struct GemmTnArgs {
   const uint16_t* A;
   int64_t lda;

@@ -740,6 +740,39 @@ def _grad_view(weight: torch.Tensor, shape):
     return None
 
 
+# forward / input-gradient GEMMs of the 1x1 and column-image convs on the
+# native MFMA kernels (csrc/gemm.hip); COMMEFF_GEMM=blas: hipBLASLt
+_GEMM_NATIVE = [__import__("os").environ.get("COMMEFF_GEMM", "native") == "native"]
+
+
+def _gemm_ok(a: torch.Tensor, b: torch.Tensor, n: int) -> bool:
+    return (_GEMM_NATIVE[0] and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and a.dim() == 2 and b.dim() == 2 and a.stride(1) == 1 and b.stride(1) == 1
+            and n % 64 == 0 and a.shape[1] % 64 == 0 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def _mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ b^T with b [N, K] (a conv forward: rows of pixels x weight rows)."""
+    if _gemm_ok(a, b, b.shape[0]):
+        return _ops().mm_nt(a, b)
+    return torch.mm(a, b.t())
+
+
+def _mm_nn(a: torch.Tensor, b: torch.Tensor, acc: torch.Tensor = None, in_place: bool = False):
+    """a @ b with b [K, N] (a conv input gradient), + ``acc`` (in place into
+    it when ``in_place``)."""
+    if _gemm_ok(a, b, b.shape[1]) and (acc is None or (acc.dtype == torch.bfloat16 and acc.stride(1) == 1
+                                                        and acc.stride(0) % 8 == 0)):
+        if acc is None:
+            return _ops().mm_nn(a, b)
+        out = acc if in_place else acc.clone()
+        return _ops().mm_nn(a, b, None, out, 1.0)
+    if acc is None:
+        return torch.mm(a, b)
+    return torch.addmm(acc, a, b, out=acc) if in_place else torch.addmm(acc, a, b)
+
+
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     """[N, C, H, W] channels_last -> its [N*H*W, C] row-major image (a view)."""
     n, c, h, w = t.shape
@@ -818,7 +851,7 @@ class _Conv1x1(torch.autograd.Function):
         else:
             x2d, h, w = _nhwc2d(x), H, W
         wb = weight.detach().view(k, c).to(torch.bfloat16)
-        y2d = torch.mm(x2d, wb.t())
+        y2d = _mm_nt(x2d, wb)
         ctx.save_for_backward(x2d, wb)
         ctx.weight, ctx.stride, ctx.gg = weight, stride, gg
         ctx.dims = (n, c, H, W, h, w)
@@ -832,7 +865,7 @@ class _Conv1x1(torch.autograd.Function):
         g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
         gx = None
         if ctx.needs_input_grad[0]:
-            gsub = torch.mm(g2d, wb)
+            gsub = _mm_nn(g2d, wb)
             s = ctx.stride
             if s > 1:
                 gx = _ops().col2im(gsub, n, H, W, c, 1, 1, s, 0)
@@ -863,7 +896,7 @@ class _Conv1x1Pass(torch.autograd.Function):
         n, c, h, w = x.shape
         k = weight.shape[0]
         wb = weight.detach().view(k, c).to(torch.bfloat16)
-        y2d = torch.mm(_nhwc2d(x), wb.t())
+        y2d = _mm_nt(_nhwc2d(x), wb)
         ctx.save_for_backward(x, wb)
         ctx.weight, ctx.gg = weight, gg
         return y2d.view(n, h, w, k).permute(0, 3, 1, 2), x.view_as(x)
@@ -883,13 +916,13 @@ class _Conv1x1Pass(torch.autograd.Function):
                     # dadd, consumed only here: accumulate into it in place (an
                     # out-of-place addmm first copies it: ~36 us per block of a
                     # ResNet-101 round)
-                    gx2d = torch.addmm(gi, g2d, wb, out=gi)
+                    gx2d = _mm_nn(g2d, wb, gi, in_place=True)
                 else:
                     # autograd may hand the same tensor to another consumer
                     # (unfused relu(y + addend) path): never write into it
-                    gx2d = torch.addmm(gi, g2d, wb)
+                    gx2d = _mm_nn(g2d, wb, gi)
             else:
-                gx2d = torch.mm(g2d, wb)
+                gx2d = _mm_nn(g2d, wb)
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
         gw = None
         if ctx.needs_input_grad[1]:
@@ -1009,7 +1042,7 @@ class _ConvCol(torch.autograd.Function):
         col = _ops().im2col(x, R, S, stride, pad, Kc)
         wt = _col_image(weight, Kc)
         OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
-        y2d = torch.mm(col, wt.t())
+        y2d = _mm_nt(col, wt)
         ctx.save_for_backward(col, wt)
         ctx.geo = (N, C, H, W, R, S, stride, pad)
         ctx.weight, ctx.gg = weight, gg
@@ -1022,7 +1055,7 @@ class _ConvCol(torch.autograd.Function):
         g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = _ops().col2im(torch.mm(g2d, wt), N, H, W, C, R, S, stride, pad)
+            gx = _ops().col2im(_mm_nn(g2d, wt), N, H, W, C, R, S, stride, pad)
         gw = _col_wgrad(g2d, col, ctx.weight, ctx.gg) if ctx.needs_input_grad[1] else None
         return gx, gw, None, None, None
 

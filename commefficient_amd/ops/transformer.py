@@ -15,7 +15,9 @@ junction (csrc/transformer.hip):
       f   = gelu_tanh(y @ W_fc + b_fc)                              _FcGelu
       h, y = h + drop(f @ W_mproj + b_mproj), LN1_next|LN_f(h)      _ResidLN
 
-GEMMs stay on hipBLASLt (``torch.mm``).  Backward of each junction is one
+The forward and input-gradient GEMMs run on the native MFMA kernels of
+csrc/gemm.hip (``_mm`` / ``_mm_t``; COMMEFF_GEMM=blas: hipBLASLt), the
+weight gradients on csrc/gemm_tn.hip.  Backward of each junction is one
 kernel (LN backward + residual gradient + dropout backward + column partials
 of dgamma/dbeta/dbias) plus one fixed-order column reduction, so every
 gradient is deterministic for a given dropout seed.  Dropout masks are a
@@ -200,6 +202,30 @@ def _sinks(*params):
 
 
 _WGRAD_GEMM = {"native": os.environ.get("COMMEFF_WGRAD_GEMM", "native") == "native"}
+# forward / input-gradient GEMMs on the native MFMA kernels (csrc/gemm.hip);
+# COMMEFF_GEMM=blas: hipBLASLt (torch.mm)
+_GEMM = {"native": os.environ.get("COMMEFF_GEMM", "native") == "native"}
+
+
+def _native_mm_ok(a: torch.Tensor, b: torch.Tensor, n: int) -> bool:
+    return (_GEMM["native"] and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and a.dim() == 2 and b.dim() == 2 and a.stride(1) == 1 and b.stride(1) == 1
+            and n % 64 == 0 and a.shape[1] % 64 == 0 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def _mm(a: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a @ W (+ bias): the HF Conv1D forward, W [in, out] (native NN GEMM)."""
+    if _native_mm_ok(a, W, W.shape[1]):
+        return _ops().mm_nn(a, W, bias.float() if bias is not None else None)
+    return torch.addmm(bias, a, W) if bias is not None else torch.mm(a, W)
+
+
+def _mm_t(dy: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """dy @ W^T: the input gradient of a Conv1D, W [in, out] (native NT GEMM)."""
+    if _native_mm_ok(dy, W, W.shape[0]):
+        return _ops().mm_nt(dy, W)
+    return torch.mm(dy, W.t())
 
 
 def _gemm_tn_ok(sink: torch.Tensor, at: torch.Tensor, b: torch.Tensor) -> bool:
@@ -303,7 +329,7 @@ class _ResidLN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, o, W, b, gamma, beta, p_drop, seed, eps):
-        p = torch.mm(o, W)
+        p = _mm(o, W)
         h, y, mean, rstd = _Impl.resid_ln_fwd(x, p, b, gamma, beta, p_drop, seed, eps, True)
         ctx.save_for_backward(o, W, h, mean, rstd, gamma)
         ctx.cfg = (p_drop, seed)
@@ -318,7 +344,7 @@ class _ResidLN(torch.autograd.Function):
         gy = torch.zeros_like(h) if gy is None else gy.contiguous()
         dh, dp, dgamma, dbeta, dbias = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma,
                                                           p_drop, seed, True, True, sg, sbe, sb)
-        do = torch.mm(dp, W.t()) if ctx.needs_input_grad[1] else None
+        do = _mm_t(dp, W) if ctx.needs_input_grad[1] else None
         dW = _wgrad(sW, o.t(), dp) if ctx.needs_input_grad[2] else None
         return (dh, do, dW, None if sb is not None else dbias,
                 None if sg is not None else dgamma, None if sbe is not None else dbeta,
@@ -330,7 +356,7 @@ class _FcGelu(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, a, W, b):
-        u = torch.mm(a, W)
+        u = _mm(a, W)
         f = _Impl.bias_gelu_fwd(u, b)
         ctx.save_for_backward(a, W, u, b)
         ctx.sinks = _sinks(W, b)
@@ -341,7 +367,7 @@ class _FcGelu(torch.autograd.Function):
         a, W, u, b = ctx.saved_tensors
         sW, sb = ctx.sinks
         du, db = _Impl.bias_act_bwd(gf.contiguous(), u, b, True, sb)
-        da = torch.mm(du, W.t()) if ctx.needs_input_grad[0] else None
+        da = _mm_t(du, W) if ctx.needs_input_grad[0] else None
         dW = _wgrad(sW, a.t(), du) if ctx.needs_input_grad[1] else None
         return da, dW, None if sb is not None else db
 
@@ -353,7 +379,7 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, a, W, b):
         ctx.save_for_backward(a, W, b)
         ctx.sinks = _sinks(W, b)
-        return torch.addmm(b, a, W)
+        return _mm(a, W, b)
 
     @staticmethod
     def backward(ctx, gy):
@@ -361,7 +387,7 @@ class _Linear(torch.autograd.Function):
         sW, sb = ctx.sinks
         gy = gy.contiguous()
         _, db = _Impl.bias_act_bwd(gy, None, b, False, sb)
-        da = torch.mm(gy, W.t()) if ctx.needs_input_grad[0] else None
+        da = _mm_t(gy, W) if ctx.needs_input_grad[0] else None
         dW = _wgrad(sW, a.t(), gy) if ctx.needs_input_grad[1] else None
         return da, dW, None if sb is not None else db
 

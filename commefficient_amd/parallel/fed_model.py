@@ -819,6 +819,8 @@ class FedModel:
         if self._sparse is None:
             out.zero_()
         self._dp_ctr = getattr(self, "_dp_ctr", 0)
+        if self.client_state.active:
+            self.client_state.begin_round(mine)  # host-tier rows: prefetch ahead
         # every client computes at the same weights (except FedAvg's local
         # steps and per-client top-k-down weights): one autocast context
         # around the loop lets the clients share the bf16 weight casts

@@ -57,6 +57,48 @@ class ClientStateStore:
         self.rows: Dict[str, Dict[int, torch.Tensor]] = {k: {} for k in self.kinds}
         self.init_weights = init_weights.detach().clone().to(self.store_device) \
             if (init_weights is not None and "weights" in self.kinds) else None
+        # host-tier rows: the round's next clients are copied ahead on a side
+        # stream (``begin_round``), so a client's H2D copy overlaps the previous
+        # clients' compute instead of sitting in front of its own
+        self.prefetch_depth = int(getattr(args, "client_prefetch", 4))
+        self._order: list = []
+        self._next = 0
+        self._staged: Dict[tuple, tuple] = {}
+        self._copy_stream = None
+
+    @property
+    def host_tier(self) -> bool:
+        return self.store_device.type == "cpu" and self.compute_device.type == "cuda"
+
+    def begin_round(self, clients: Iterable[int]):
+        """The order in which this rank will ``get`` the round's clients:
+        starts the first ``prefetch_depth`` host -> device copies."""
+        self._staged.clear()
+        self._order = [int(c) for c in clients]
+        self._next = 0
+        if self.host_tier and self.prefetch_depth > 0:
+            self._advance()
+
+    def _advance(self):
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.compute_device)
+        cur = torch.cuda.current_stream(self.compute_device)
+        while self._next < len(self._order) and \
+                len({c for (_, c) in self._staged}) < self.prefetch_depth:
+            c = self._order[self._next]
+            self._next += 1
+            for kind in self.kinds:
+                row = self.rows[kind].get(c)
+                if row is None:
+                    continue  # first participation: created on the device side by get()
+                dev = torch.empty(self.d, device=self.compute_device)
+                # (the row's previous write-back, on the compute stream, lands first)
+                self._copy_stream.wait_stream(cur)
+                with torch.cuda.stream(self._copy_stream):
+                    dev.copy_(row, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._copy_stream)
+                self._staged[(kind, c)] = (dev, ev)
 
     @property
     def active(self) -> bool:
@@ -82,7 +124,18 @@ class ClientStateStore:
                                       self.compute_device.type == "cuda")
         t = rows[c]
         if t.device != self.compute_device:
-            return t.to(self.compute_device, non_blocking=True)
+            hit = self._staged.pop((kind, c), None)
+            if hit is not None:
+                dev, ev = hit
+                torch.cuda.current_stream(self.compute_device).wait_event(ev)
+                dev.record_stream(torch.cuda.current_stream(self.compute_device))
+                if self.host_tier:
+                    self._advance()
+                return dev
+            out = t.to(self.compute_device, non_blocking=True)
+            if self.host_tier and self._order:
+                self._advance()
+            return out
         return t
 
     def put(self, kind: str, client: int, value: torch.Tensor):

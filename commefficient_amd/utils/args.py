@@ -181,6 +181,9 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                         "direct (global atomics) kernels")
     g.add_argument("--client_state_device", choices=["auto", "gpu", "cpu"], default="auto",
                    help="where per-client momentum/error/weights live")
+    g.add_argument("--client_prefetch", type=int, default=4,
+                   help="host-tier client state: rows of the next N clients of the round copied "
+                        "to the GPU ahead on a side stream (parallel/state.py)")
     g.add_argument("--resume", type=str, default=None,
                    help="resume from a *.fedstate.pt sidecar written with --checkpoint")
     g.add_argument("--checkpoint_every", type=int, default=0,

@@ -387,3 +387,41 @@ def test_reference_oracle_two_workers_top1():
     e2[j] -= lr * est[j]
     np.testing.assert_allclose(w1, e1, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(w2, e2, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_host_tier_client_state_prefetch_matches_device_tier():
+    """Per-client state in host memory (--client_state_device cpu) with the
+    round's next clients prefetched on a side stream gives bitwise the
+    device-resident run (local momentum + local error, local top-k)."""
+    import copy
+    from commefficient_amd import models
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd.train.losses import cv_loss
+    from commefficient_amd.utils.args import parse_args
+    dist.init("cuda")
+    torch.manual_seed(0)
+    base = models.ResNet9(channels={"prep": 16, "layer1": 32, "layer2": 32, "layer3": 64})
+    res = {}
+    for where in ("gpu", "cpu"):
+        args = parse_args(argv=["--dataset_name", "CIFAR10", "--mode", "local_topk", "--error_type", "local",
+                                "--local_momentum", "0.9", "--virtual_momentum", "0", "--k", "500",
+                                "--num_workers", "6", "--num_clients", "12", "--local_batch_size", "-1",
+                                "--device", "cuda", "--dtype", "fp32", "--client_state_device", where,
+                                "--client_prefetch", "2"], probe_port=False)
+        model = copy.deepcopy(base).cuda()
+        fed = FedModel(model, cv_loss, args, num_clients=12)
+        assert fed.client_state.host_tier == (where == "cpu")
+        opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05), args, fed)
+        g = torch.Generator().manual_seed(3)
+        for r in range(4):
+            x = torch.randn(24, 3, 32, 32, generator=g).cuda()
+            y = torch.randint(0, 10, (24,), generator=g).cuda()
+            cids = torch.arange(6).repeat_interleave(4) + 6 * (r % 2)
+            fed((cids, x, y))
+            opt.step()
+        torch.cuda.synchronize()
+        res[where] = fed.w.clone()
+    assert torch.equal(res["gpu"], res["cpu"])
