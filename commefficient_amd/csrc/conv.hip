@@ -1635,9 +1635,12 @@ void launch_fwd_pipe(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t strea
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
-  static const int pipe_on = [] {  // COMMEFF_CONV_PIPE=0: the one-tile-per-block halo kernels
+  // COMMEFF_CONV_PIPE=1: the persistent pipelined kernel (off by default: one
+  // 8-wave block per CU lost to two co-resident one-tile blocks, 1.91 vs 1.68
+  // ms per ResNet-9 round -- profiles/r4_experiments.md)
+  static const int pipe_on = [] {
     const char* e = getenv("COMMEFF_CONV_PIPE");
-    return e != nullptr ? atoi(e) : 1;
+    return e != nullptr ? atoi(e) : 0;
   }();
   static const bool halo_on = [] {  // COMMEFF_CONV_HALO=0: the per-tap tile kernel
     const char* e = getenv("COMMEFF_CONV_HALO");

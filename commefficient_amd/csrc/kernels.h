@@ -140,6 +140,8 @@ void launch_topk_pack(const int64_t* idx, const float* vals, int64_t k, const in
                       int64_t* out, hipStream_t stream);
 void launch_merge_packed(const int64_t* allp, int nl, int64_t k, float* vals, int64_t* idx, hipStream_t stream);
 void launch_gather_i64(const int64_t* src, const int64_t* pos, int64_t n, int64_t* out, hipStream_t stream);
+// dst (device) = n bytes read by a kernel from pinned host memory (its device mapping)
+void launch_host_read_copy(const void* host_src, void* dst, int64_t n, hipStream_t stream);
 // out[0] = sqrt(lower-median_j sum_c table[j,c]^2); partial: >= r*256 floats
 void launch_cs_l2estimate(const float* table, int r, int64_t c, float* partial,
                           float* out, hipStream_t stream);

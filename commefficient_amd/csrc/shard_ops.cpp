@@ -1,6 +1,7 @@
 // torch.ops.commeff registrations of the sharded-server k-list helpers
 // (csrc/shard.hip): topk_pack, merge_packed, gather_i64 -- HIP kernels on the
-// GPU, the same semantics in plain ATen on the CPU (the gloo rehearsal).
+// GPU, the same semantics in plain ATen on the CPU (the gloo rehearsal) -- and
+// the per-round host staging copy host_read_copy (csrc/hostcopy.hip).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -85,10 +86,31 @@ at::Tensor gather_i64_hip(const at::Tensor& src, const at::Tensor& pos) {
   return out;
 }
 
+// dst (device) <- src (pinned host), read by a kernel on the current stream
+// (csrc/hostcopy.hip); alignment or an unpinned source: a stream-ordered copy
+void host_read_copy_hip(at::Tensor dst, const at::Tensor& src) {
+  TORCH_CHECK(dst.is_cuda() && !src.is_cuda() && dst.is_contiguous() && src.is_contiguous() &&
+                  dst.nbytes() == src.nbytes(),
+              "host_read_copy: contiguous device dst and host src of one size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
+  void* dptr = nullptr;
+  const bool mapped = src.is_pinned() &&
+                      hipHostGetDevicePointer(&dptr, const_cast<void*>(src.data_ptr()), 0) == hipSuccess &&
+                      dptr != nullptr;
+  if (!mapped || reinterpret_cast<uintptr_t>(dptr) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 != 0) {
+    (void)hipGetLastError();
+    dst.copy_(src, /*non_blocking=*/true);
+    return;
+  }
+  launch_host_read_copy(dptr, dst.data_ptr(), static_cast<int64_t>(dst.nbytes()), stream_now());
+}
+
 }  // namespace
 }  // namespace commeff
 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
+  m.def("host_read_copy(Tensor(a!) dst, Tensor src) -> ()");
   m.def("topk_pack(Tensor idx, Tensor vals, Tensor? cmap=None, int m=1) -> Tensor");
   m.def("merge_packed(Tensor allp, int nl, int k) -> (Tensor, Tensor)");
   m.def("gather_i64(Tensor src, Tensor pos) -> Tensor");
@@ -98,10 +120,12 @@ TORCH_LIBRARY_IMPL(commeff, CPU, m) {
   m.impl("topk_pack", &commeff::topk_pack_cpu);
   m.impl("merge_packed", &commeff::merge_packed_cpu);
   m.impl("gather_i64", &commeff::gather_i64_cpu);
+  m.impl("host_read_copy", [](at::Tensor dst, const at::Tensor& src) { dst.copy_(src); });
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("topk_pack", &commeff::topk_pack_hip);
   m.impl("merge_packed", &commeff::merge_packed_hip);
   m.impl("gather_i64", &commeff::gather_i64_hip);
+  m.impl("host_read_copy", &commeff::host_read_copy_hip);
 }

@@ -10,7 +10,8 @@
 //   graph_node_counts(g)     [kernel, memcpy, memset, other] nodes of a captured
 //                            hipGraph_t (torch.cuda.CUDAGraph.raw_cuda_graph()):
 //                            the completeness check of a tape recorded under
-//                            stream capture
+//                            stream capture; then [roots, max dependencies,
+//                            max dependents] (a single chain: <= 1 each)
 //
 // Replaces the per-round Python enqueue of the reference's worker loop
 // (/root/reference/CommEfficient/fed_worker.py:26-138) and server step
@@ -20,6 +21,7 @@
 #include <hip/hip_runtime_api.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -104,6 +106,24 @@ std::vector<int64_t> graph_node_counts(int64_t graph) {
       default: ++cnt[3]; break;
     }
   }
+  // the dependency shape: a tape replays its launches in order on the streams
+  // they were recorded on, without cross-stream waits, so only a single chain
+  // (one root, no node with two dependencies or two dependents) replays the
+  // captured order exactly
+  int64_t roots = 0, max_in = 0, max_out = 0;
+  for (size_t i = 0; i < n; ++i) {
+    size_t din = 0, dout = 0;
+    TORCH_CHECK(hipGraphNodeGetDependencies(nodes[i], nullptr, &din) == hipSuccess,
+                "hipGraphNodeGetDependencies failed");
+    TORCH_CHECK(hipGraphNodeGetDependentNodes(nodes[i], nullptr, &dout) == hipSuccess,
+                "hipGraphNodeGetDependentNodes failed");
+    roots += din == 0;
+    max_in = std::max<int64_t>(max_in, static_cast<int64_t>(din));
+    max_out = std::max<int64_t>(max_out, static_cast<int64_t>(dout));
+  }
+  cnt.push_back(roots);
+  cnt.push_back(max_in);
+  cnt.push_back(max_out);
   return cnt;
 }
 

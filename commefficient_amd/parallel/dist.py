@@ -112,6 +112,10 @@ def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> 
     return _CTX
 
 
+# COMMEFF_H2D=blit: stage with hipMemcpyAsync instead of the host-read kernel
+_H2D_KERNEL = os.environ.get("COMMEFF_H2D", "kernel") != "blit"
+
+
 class _PinnedRing:
     """Persistent pinned staging buffers for small per-round H2D copies.
 
@@ -147,7 +151,15 @@ class _PinnedRing:
             self.events[k].synchronize()
         stage = self.bufs[k][:nbytes].view(t.dtype).view(t.shape)
         stage.copy_(t)
-        out.copy_(stage, non_blocking=True)
+        from . import tape
+        if _H2D_KERNEL and out.is_contiguous() and not tape.recording():
+            # a kernel of this stream reads the pinned slot (csrc/hostcopy.hip):
+            # no runtime blit with its queue drain and cache maintenance.  (Never
+            # inside a recorded round: the replay would re-read this slot.)
+            from .._ext import ops as _ops
+            _ops().host_read_copy(out, stage)
+        else:
+            out.copy_(stage, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self.events[k] = ev

@@ -21,9 +21,11 @@ A round of fixed geometry is therefore recorded ONCE and replayed:
   recording into segments: tape, collective, tape, ...; a replay re-issues
   the tapes from C++ and runs the collectives eagerly on the same buffers;
 * completeness check: the captured HIP graph must hold exactly as many
-  kernel + memset nodes as the tapes and nothing else -- a launch that
-  bypassed the tape (a PyTorch kernel, a copy) makes the geometry fall back
-  to the eager path for good (with a one-line warning naming the counts).
+  kernel + memset nodes as the tapes and nothing else, in a single chain of
+  dependencies -- a launch that bypassed the tape (a PyTorch kernel, a copy)
+  or work forked onto a second stream (a replay issues no cross-stream
+  waits) makes the geometry fall back to the eager path for good (with a
+  one-line warning naming the counts).
 
 The HIP graph itself is never launched (ROCm 7.2's graph packet capture
 faulted on the second replay of this round in round 1 and was throughput-
@@ -111,6 +113,7 @@ class RoundTapes:
         self.pool = None
         self.failed = set()
         self.replays = 0
+        self.last_counts = None
         # context around the eager steps (collectives) of a replay, e.g. a phase timer
         self.call_ctx = None
 
@@ -145,12 +148,16 @@ class RoundTapes:
         cur.wait_stream(self.stream)
         self.pool = g.pool()
         counts = [int(c) for c in _ops().graph_node_counts(g.raw_cuda_graph())]
+        self.last_counts = counts
         n_tape = sum(int(_ops().tape_size(x)) for kind, x in rec.segments if kind == "tape")
         rep = Replay(rec.segments, g, result)
-        if counts[1] or counts[3] or counts[0] + counts[2] != n_tape:
+        chain = len(counts) < 7 or (counts[4] <= 1 and counts[5] <= 1 and counts[6] <= 1)
+        if counts[1] or counts[3] or counts[0] + counts[2] != n_tape or not chain:
             warnings.warn(f"launch tape for {key!r} incomplete (graph nodes: {counts[0]} kernels, "
                           f"{counts[1]} copies, {counts[2]} memsets, {counts[3]} other; tape: "
-                          f"{n_tape} launches): this round geometry stays eager")
+                          f"{n_tape} launches; roots / max deps / max dependents: "
+                          f"{counts[4:7]}): this round "
+                          f"geometry stays eager")
             rep.free()
             self.failed.add(key)
             return None

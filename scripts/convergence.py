@@ -34,6 +34,11 @@ MODES = {
     "sketch": ["--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
                "--virtual_momentum", "0.9", "--k", "50000", "--num_rows", "5",
                "--num_cols", "500000", "--num_blocks", "20"],
+    # the same sketch in the reference's CSVec hash layout (numBlocks = 20
+    # multiply-shift hashes; --encode planned) instead of the region family
+    "sketch_planned": ["--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
+                       "--virtual_momentum", "0.9", "--k", "50000", "--num_rows", "5",
+                       "--num_cols", "500000", "--num_blocks", "20", "--encode", "planned"],
     "true_topk": ["--mode", "true_topk", "--error_type", "virtual", "--local_momentum", "0",
                   "--virtual_momentum", "0.9", "--k", "50000"],
     "uncompressed": ["--mode", "uncompressed", "--error_type", "none", "--local_momentum", "0",
@@ -109,14 +114,16 @@ def main():
             lrs[k] = float(v)
         else:
             lrs["*"] = float(part)
-    for mode in b.modes.split(","):
-        lr = lrs.get(mode, lrs.get("*", 0.4))
+    for spec in b.modes.split(","):
+        # "mode" (LR from --lr_scale) or "mode@lr" (matched / best-LR grids in one call)
+        mode, _, lr_s = spec.partition("@")
+        lr = float(lr_s) if lr_s else lrs.get(mode, lrs.get("*", 0.4))
         rows, fed, wall = run(mode, b.epochs, b.pivot, lr, b.device, b.dtype, b.out,
                               b.size, difficulty=b.difficulty)
         last = rows[-1] if rows else {}
-        summary[mode] = {"test_acc": last.get("test_acc"), "test_loss": last.get("test_loss"),
+        summary[spec] = {"test_acc": last.get("test_acc"), "test_loss": last.get("test_loss"),
                          "rounds": fed.round_idx, "wall_s": round(wall, 1), "lr_scale": lr}
-        print("CONVERGENCE", mode, json.dumps(summary[mode]), flush=True)
+        print("CONVERGENCE", spec, json.dumps(summary[spec]), flush=True)
     print("SUMMARY", json.dumps(summary))
 
 

@@ -28,6 +28,12 @@ def main():
     ap.add_argument("--marker", default="enc_p1_kernel")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--per-round", type=int, default=0,
+                    help="also print every round's wall / busy / idle and the PER_ROUND "
+                         "largest kernels' times, from the first marker on")
+    ap.add_argument("--gaps", type=int, default=0,
+                    help="print the GAPS largest idle gaps per round, by (previous kernel -> "
+                         "next kernel), averaged over the selected rounds")
     ap.add_argument("--tail-ms", type=float, default=0.0,
                     help="no marker: take the kernels of the trace's last TAIL_MS ms "
                          "(e.g. rounds * ms_per_round of the timed steps)")
@@ -46,6 +52,8 @@ def main():
             raise SystemExit(f"only {len(starts)} marker kernels")
         lo, hi = starts[-a.rounds - 1], starts[-1]
         sel = rows[lo:hi]
+    if a.per_round and a.tail_ms <= 0:
+        per_round(rows, starts, a.per_round)
     n = a.rounds
     wall = (sel[-1][1] - sel[0][0]) / n
     busy = collections.Counter()
@@ -59,11 +67,45 @@ def main():
         busy[short(k)] += e - s
         calls[short(k)] += 1
     tot = sum(busy.values())
+    if a.gaps:
+        gap = collections.Counter()
+        prev, end = None, sel[0][0]
+        for s, e, k in sel:
+            if prev is not None and s > end:
+                gap[(short(prev)[:40], short(k)[:40])] += s - end
+            if e >= end:
+                end, prev = e, k
+        print(f"# largest idle gaps (us/round): previous kernel -> next kernel")
+        for (p0, k0), v in gap.most_common(a.gaps):
+            print(f"{v / n / 1e3:9.1f}  {p0} -> {k0}")
     print(f"# rounds={n} wall/round={wall / 1e3:.1f}us busy/round={tot / n / 1e3:.1f}us "
           f"idle/round={idle / n / 1e3:.1f}us kernels/round={len(sel) / n:.1f}")
     print("# us/round  calls/round  kernel")
     for k, v in busy.most_common(a.top):
         print(f"{v / n / 1e3:9.1f} {calls[k] / n:6.1f}  {k}")
+
+
+def per_round(rows, starts, top):
+    """Round-by-round split: does a round's time change because the GPU waits
+    (idle) or because kernels run longer (and which)?"""
+    spans = [rows[starts[i]:starts[i + 1]] for i in range(len(starts) - 1)]
+    tot = collections.Counter()
+    for sp in spans:
+        for s, e, k in sp:
+            tot[short(k)] += e - s
+    names = [k for k, _ in tot.most_common(top)]
+    print("# round  wall_us  busy_us  idle_us  " + "  ".join(n[:28] for n in names))
+    for i, sp in enumerate(spans):
+        wall = sp[-1][1] - sp[0][0]
+        busy = collections.Counter()
+        idle, end = 0, sp[0][0]
+        for s, e, k in sp:
+            if s > end:
+                idle += s - end
+            end = max(end, e)
+            busy[short(k)] += e - s
+        print(f"{i:7d} {wall / 1e3:8.1f} {sum(busy.values()) / 1e3:8.1f} {idle / 1e3:8.1f}  "
+              + "  ".join(f"{busy[n] / 1e3:28.1f}" for n in names))
 
 
 if __name__ == "__main__":

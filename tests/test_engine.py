@@ -392,8 +392,11 @@ def test_reference_oracle_two_workers_top1():
 @pytest.mark.gpu
 def test_host_tier_client_state_prefetch_matches_device_tier():
     """Per-client state in host memory (--client_state_device cpu) with the
-    round's next clients prefetched on a side stream gives bitwise the
-    device-resident run (local momentum + local error, local top-k)."""
+    round's next clients prefetched on a side stream gives the device-resident
+    run (local momentum + local error, local top-k).  The fp32 convolutions
+    are not bitwise reproducible run to run (MIOpen algorithm choice), so the
+    tiers are compared at a tolerance far below what one stale prefetched row
+    (a client's state missing its previous round) moves the weights by."""
     import copy
     from commefficient_amd import models
     from commefficient_amd.parallel import dist
@@ -424,4 +427,4 @@ def test_host_tier_client_state_prefetch_matches_device_tier():
             opt.step()
         torch.cuda.synchronize()
         res[where] = fed.w.clone()
-    assert torch.equal(res["gpu"], res["cpu"])
+    torch.testing.assert_close(res["cpu"], res["gpu"], rtol=1e-4, atol=2e-6)

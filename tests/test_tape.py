@@ -89,7 +89,7 @@ def test_taped_rounds_bitwise_equal_eager(mode):
         losses, dls = _run(fed, opt, loader, ds, W, rounds)
         res[tape] = (fed.w.clone(), losses, dls, fed.accountant.last_mod.clone(), fed.server.V.clone())
         if tape == "auto":
-            assert fed.last_round.get("taped"), fed.last_round
+            assert fed.last_round.get("taped"), (fed.last_round, fed._tapes.last_counts)
             assert fed._tapes.replays >= 2 * (rounds - 2), fed._tapes.replays
     for a, b in zip(res["off"], res["auto"]):
         assert torch.equal(a, b), (a - b).abs().max()
