@@ -1565,7 +1565,45 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_relu_add_hip(const at::Tensor& x, con
 
 // dw [K][C][3][3] fp32 = sum_p dy[p, k] x[p + (r-1, s-1), c]
 void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits, at::Tensor& dw,
-                       float beta);
+                       float beta, bool may_defer = false);
+
+// Deferred split-K reductions (ops/nn.py deferred_wgrad): while on, the
+// accumulate-into convs of a backward pass write only their slabs, which are
+// kept alive here, and wgrad_flush reduces them all in one batched launch
+struct PendingReduce {
+  at::Tensor slab, dw;
+  int K, C, splits;
+  float beta;
+};
+bool g_wgrad_defer = false;
+std::vector<PendingReduce> g_wgrad_pending;
+
+void wgrad_flush() {
+  size_t i = 0;
+  while (i < g_wgrad_pending.size()) {
+    WgradReduceBatch b{};
+    b.n = 0;
+    for (; i < g_wgrad_pending.size() && b.n < kWgradBatch; ++i, ++b.n) {
+      const auto& r = g_wgrad_pending[i];
+      b.slab[b.n] = r.slab.data_ptr<float>();
+      b.dw[b.n] = r.dw.data_ptr<float>();
+      b.K[b.n] = r.K;
+      b.C[b.n] = r.C;
+      b.splits[b.n] = r.splits;
+      b.beta[b.n] = r.beta;
+    }
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(g_wgrad_pending[i - 1].dw.device());
+    launch_wgrad_reduce_batch(b, cur_stream());
+  }
+  // (the slabs go back to the caching allocator stream-ordered: reused only
+  // by work queued after the reduction)
+  g_wgrad_pending.clear();
+}
+
+void wgrad_defer(bool on) {
+  if (!on) wgrad_flush();
+  g_wgrad_defer = on;
+}
 
 at::Tensor conv3x3_wgrad_hip(const at::Tensor& dy, const at::Tensor& x, int64_t splits) {
   auto dw = at::empty({dy.size(1), x.size(1), 3, 3},
@@ -1582,7 +1620,7 @@ void conv3x3_wgrad_into_hip(const at::Tensor& dy, const at::Tensor& x, at::Tenso
   TORCH_CHECK(dw.dim() == 4 && dw.size(0) == dy.size(1) && dw.size(1) == x.size(1) &&
                   dw.size(2) == 3 && dw.size(3) == 3,
               "conv3x3_wgrad_into: dw must be [K, C, 3, 3]");
-  conv3x3_wgrad_run(dy, x, splits, dw, 1.f);
+  conv3x3_wgrad_run(dy, x, splits, dw, 1.f, /*may_defer=*/true);
 }
 
 // grouped (per-client) weight gradients: dw [G, K*C*9] fp32 rows (any row
@@ -1624,7 +1662,7 @@ void conv3x3_wgrad_grouped_hip(const at::Tensor& dy, const at::Tensor& x, int64_
 }
 
 void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits, at::Tensor& dw,
-                       float beta) {
+                       float beta, bool may_defer) {
   check_nhwc_bf16(dy, "conv3x3_wgrad: dy");
   check_nhwc_bf16(x, "conv3x3_wgrad: x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
@@ -1645,6 +1683,18 @@ void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits
   a.C = static_cast<int>(C);
   a.K = static_cast<int>(K);
   a.splits = static_cast<int>(splits);
+  if (may_defer && g_wgrad_defer && dw.is_contiguous()) {
+    // a second gradient into the same dw (a conv applied twice in one pass):
+    // the earlier reductions go first, one batched launch must not hold both
+    for (const auto& r : g_wgrad_pending)
+      if (r.dw.data_ptr() == dw.data_ptr()) {
+        wgrad_flush();
+        break;
+      }
+    launch_conv3x3_wgrad_slabs(a, cur_stream());
+    g_wgrad_pending.push_back({slab, dw, a.K, a.C, a.splits, beta});
+    return;
+  }
   launch_conv3x3_wgrad(a, dw.data_ptr<float>(), beta, cur_stream());
 }
 
@@ -2171,6 +2221,8 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor(e!)? dadd=None) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
+  m.def("wgrad_defer(bool on) -> ()", &commeff::wgrad_defer);
+  m.def("wgrad_flush() -> ()", &commeff::wgrad_flush);
   m.def("conv3x3_wgrad_grouped(Tensor dy, Tensor x, int G, Tensor(a!) dw) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("conv_weight_prep_multi(Tensor[] ws) -> Tensor[]");

@@ -530,17 +530,19 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
   issue_b(s_beg);
   for (int s = s_beg; s < s_end; ++s) {
     const int tap = s % 9, cb = s / 9;
-    if (tap == 0 && s > s_beg) {  // every wave is past the old window's reads
+    if (tap == 0 && s > s_beg && !(a.ablate & 2)) {  // every wave is past the old window's reads
       // (staging the next window behind the last tap's MFMAs instead needs
       // all A fragments in registers: 220 VGPRs, measured 6 % slower)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       issue_window(cb);
     }
-    wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + 1 < s_end) issue_b(s + 1);
+    if (!(a.ablate & 4) || s == s_beg) {
+      wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (s + 1 < s_end && (!(a.ablate & 1) || s == s_beg)) issue_b(s + 1);
     const int dr = tap / 3 - 1, dc = tap % 3 - 1;
     int offA[2];
     int swA[2];
@@ -1391,6 +1393,62 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
   }
 }
 
+// Batched form: the split-K reductions of up to kWgradBatch convs of a
+// backward pass in ONE launch (their slabs are kept until the end of the
+// pass, ops/nn.py deferred_wgrad).  Seven per-layer reductions of ResNet-9
+// are 85 us per round of mostly latency-bound blocks (128-2048 per launch);
+// one launch keeps every block of every layer in flight.  Each block finds its
+// conv by compile-time-indexed compares (a dynamically indexed by-value
+// argument array would be copied to scratch); 8 split partitions per block,
+// summed in fixed order (deterministic).
+__global__ void __launch_bounds__(512) conv_wgrad_reduce_batch_kernel(WgradReduceBatch b) {
+  __shared__ float t[8][64 * 9];
+  int item = 0;
+#pragma unroll
+  for (int i = 1; i < kWgradBatch; ++i)
+    if (i < b.n && static_cast<int>(blockIdx.x) >= b.block0[i]) item = i;
+  const float* slab = b.slab[0];
+  float* dw = b.dw[0];
+  int C = b.C[0], K = b.K[0], splits = b.splits[0], blk0 = b.block0[0];
+  float beta = b.beta[0];
+#pragma unroll
+  for (int i = 1; i < kWgradBatch; ++i)
+    if (i == item) {
+      slab = b.slab[i];
+      dw = b.dw[i];
+      C = b.C[i];
+      K = b.K[i];
+      splits = b.splits[i];
+      beta = b.beta[i];
+      blk0 = b.block0[i];
+    }
+  const int blk = static_cast<int>(blockIdx.x) - blk0;
+  const int ncb = C >> 6;
+  const int k = blk / ncb, c0 = (blk - k * ncb) * 64;
+  const int cc = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const size_t sstride = static_cast<size_t>(K) * 9 * C;
+  const float* src = slab + static_cast<size_t>(k) * 9 * C + c0 + cc;
+  float acc[9];
+#pragma unroll
+  for (int rs = 0; rs < 9; ++rs) acc[rs] = 0.f;
+#pragma unroll 2
+  for (int sp = part; sp < splits; sp += 8) {
+    const float* p = src + sp * sstride;
+#pragma unroll
+    for (int rs = 0; rs < 9; ++rs) acc[rs] += p[rs * C];
+  }
+#pragma unroll
+  for (int rs = 0; rs < 9; ++rs) t[part][cc * 9 + rs] = acc[rs];
+  __syncthreads();
+  float* o = dw + (static_cast<size_t>(k) * C + c0) * 9;
+  for (int e = threadIdx.x; e < 576; e += 512) {
+    float v = t[0][e];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v += t[q][e];
+    o[e] = beta != 0.f ? beta * o[e] + v : v;
+  }
+}
+
 void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
                          int64_t gstride, int groups, hipStream_t stream) {
   const dim3 grid(K * (C / 64), groups);
@@ -1635,6 +1693,11 @@ void launch_fwd_pipe(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t strea
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
+  static const int ablate = [] {
+    const char* e = getenv("COMMEFF_CONV_ABLATE");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  a.ablate = ablate;
   // COMMEFF_CONV_PIPE=1: the persistent pipelined kernel (off by default: one
   // 8-wave block per CU lost to two co-resident one-tile blocks, 1.91 vs 1.68
   // ms per ResNet-9 round -- profiles/r4_experiments.md)
@@ -1793,6 +1856,23 @@ int conv3x3_wgrad_splits(int P, int H, int W, int K, int C) {
 }
 
 void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_t stream);
+
+void launch_wgrad_reduce_batch(WgradReduceBatch b, hipStream_t stream) {
+  if (b.n <= 0) return;
+  int total = 0;
+  for (int i = 0; i < b.n; ++i) {
+    b.block0[i] = total;
+    total += b.K[i] * (b.C[i] / 64);
+  }
+  COMMEFF_LAUNCH(conv_wgrad_reduce_batch_kernel, dim3(total), dim3(512), 0, stream, b);
+}
+
+// the split-K slabs only (the reduction deferred to launch_wgrad_reduce_batch)
+void launch_conv3x3_wgrad_slabs(ConvWgradArgs a, hipStream_t stream) {
+  const int steps = (a.P + BK - 1) / BK;
+  a.group_px = 0;
+  launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
+}
 
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream) {
   const int steps = (a.P + BK - 1) / BK;

@@ -261,6 +261,10 @@ struct ConvFwdArgs {
   // consumer of that layer's other input gradient -- ops/nn.py _MaskLink)
   const uint16_t* dual_mask = nullptr;
   uint16_t* y_dual = nullptr;
+  // timing experiments only (COMMEFF_CONV_ABLATE, results are wrong): bit 0 =
+  // no weight-tile loads after the first two K-steps, bit 1 = no window reload
+  // per channel block, bit 2 = no per-K-step wait / barrier
+  int ablate = 0;
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]
@@ -282,6 +286,17 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
+// split-K slabs only; their reductions batched across convs by launch_wgrad_reduce_batch
+void launch_conv3x3_wgrad_slabs(ConvWgradArgs a, hipStream_t stream);
+constexpr int kWgradBatch = 16;
+struct WgradReduceBatch {
+  int n;
+  const float* slab[kWgradBatch];
+  float* dw[kWgradBatch];  // [K][C][3][3] fp32: dw = beta * dw + sum of the splits
+  int K[kWgradBatch], C[kWgradBatch], splits[kWgradBatch], block0[kWgradBatch];
+  float beta[kWgradBatch];
+};
+void launch_wgrad_reduce_batch(WgradReduceBatch b, hipStream_t stream);
 // per-group dw_g [K][C][3][3] (+)= the wgrad of group g's pixels, dw_g at
 // dw + g * gstride floats (a.splits = G x splits_per_group, set by the caller)
 void launch_conv3x3_wgrad_grouped(ConvWgradArgs a, int G, float* dw, int64_t gstride, float beta,

@@ -8,6 +8,7 @@ composition (CPU runs, fp32 runs, odd shapes).
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
@@ -94,6 +95,39 @@ def _grad_written(*params):
                     fn(p)
 
 
+class deferred_wgrad:
+    """``with deferred_wgrad(): loss.backward()`` -- the native 3x3 convs that
+    accumulate their weight gradient into an existing fp32 ``.grad`` write
+    only their split-K slabs during the pass; one batched launch reduces all
+    of them at exit (csrc/conv.hip conv_wgrad_reduce_batch_kernel) instead of
+    one latency-bound reduction per layer.  Off while gradient-ready
+    listeners are registered (the overlapped bucket all-reduce needs each
+    gradient when its layer's backward returns).  Opt-in (COMMEFF_WGRAD_DEFER=1):
+    the reductions are bound by their slab bytes, not by launch latency -- the
+    batched launch took 99 us per ResNet-9 round against 85 us for the seven
+    per-layer ones (profiles/r4_experiments.md)."""
+
+    _depth = 0
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = (enabled and not _GRAD_READY and _CONV_BACKEND[0] == "native"
+                        and not _STOCK[0] and os.environ.get("COMMEFF_WGRAD_DEFER", "0") == "1")
+        self.active = False
+
+    def __enter__(self):
+        if self.enabled and deferred_wgrad._depth == 0:
+            _ops().wgrad_defer(True)
+            self.active = True
+        deferred_wgrad._depth += 1
+        return self
+
+    def __exit__(self, *exc):
+        deferred_wgrad._depth -= 1
+        if self.active:
+            _ops().wgrad_defer(False)  # launches the batched reductions
+        return False
+
+
 def set_conv_backend(name: str) -> None:
     if name not in ("native", "miopen"):
         raise ValueError(f"unknown conv backend {name!r}")
@@ -136,9 +170,12 @@ class _ImageCache:
     # weight-mirror protocol (weights_begin_update / weights_end_update)
     def begin(self, w_flat: torch.Tensor) -> bool:
         lo, hi = w_flat.data_ptr(), w_flat.data_ptr() + 4 * w_flat.numel()
-        ok = ((self.valid or self.synced) and self._unchanged() and len(self.weights) <= 16
+        usable = self.valid or self.synced
+        ok = (usable and self._unchanged() and len(self.weights) <= 16
               and all(lo <= w.data_ptr() < hi for w in self.weights))
         self.valid = self.synced = False
+        if usable and not ok:
+            _IMG_GEN[0] += 1  # in sync until now, stale from here on: recorded readers re-record
         return ok
 
     def patch(self, w_flat: torch.Tensor, idx: torch.Tensor) -> None:
@@ -148,6 +185,13 @@ class _ImageCache:
 
 
 _IMAGES: dict = {}  # key: weight data pointers -> _ImageCache (one model at a time)
+# bumped whenever the kept images are replaced or dropped: recorded rounds
+# that read them (parallel/tape.py) are recorded again
+_IMG_GEN = [0]
+
+
+def image_generation() -> int:
+    return _IMG_GEN[0]
 # other derived copies of the flat weights (parallel/flat.py bf16 replica),
 # weakly held: a torn-down FedModel's replica is not kept alive or updated
 _MIRRORS = weakref.WeakSet()
@@ -159,6 +203,7 @@ def set_conv_image_cache(on: bool) -> None:
     passes; COMMEFF_WEIGHT_MIRRORS=0 turns this off (re-derive every pass)."""
     _IMAGE_CACHE_ON[0] = bool(on)
     _IMAGES.clear()
+    _IMG_GEN[0] += 1
 
 
 def register_weight_mirror(m) -> None:
@@ -176,6 +221,7 @@ def invalidate_conv_images() -> None:
     kept derived copies must be rebuilt."""
     for c in list(_IMAGES.values()) + list(_MIRRORS):
         c.begin(torch.empty(0))
+    _IMG_GEN[0] += 1
 
 
 class prepared_conv_weights:
@@ -195,16 +241,21 @@ class prepared_conv_weights:
     def __enter__(self):
         if self.weights and _CONV_BACKEND[0] == "native" and not _STOCK[0]:
             ws = [w.detach() for w in self.weights]
-            capturing = torch.cuda.is_current_stream_capturing() or not _IMAGE_CACHE_ON[0]
+            capturing = torch.cuda.is_current_stream_capturing()
             ck = tuple(w.data_ptr() for w in ws)
-            cache = None if capturing else _IMAGES.get(ck)
+            cache = _IMAGES.get(ck) if _IMAGE_CACHE_ON[0] else None
             if cache is not None and cache.fresh():
+                # (also while a round is recorded, parallel/tape.py: the replays
+                # read these images, which the recorded server step keeps
+                # patched; a replaced cache bumps image_generation() and the
+                # engine records its rounds again)
                 out = cache.images
             else:
                 out = _ops().conv_weight_prep_multi(ws)
-                if not capturing:
+                if not capturing and _IMAGE_CACHE_ON[0]:
                     _IMAGES.clear()
                     _IMAGES[ck] = _ImageCache(ws, out)
+                    _IMG_GEN[0] += 1
             for i, w in enumerate(self.weights):
                 key = (w.data_ptr(), w._version)
                 _PREP[key] = (out[2 * i], out[2 * i + 1])

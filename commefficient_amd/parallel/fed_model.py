@@ -40,7 +40,8 @@ import torch.nn as nn
 from .. import ops
 from ..models.common import NativeConv2d, ghost_batchnorm, groupable, has_batchnorm
 from ..ops.grouped import GroupedGrads, grouped_grads
-from ..ops.nn import invalidate_conv_images, prepared_conv_weights, set_conv_image_cache
+from ..ops.nn import (deferred_wgrad, image_generation, invalidate_conv_images,
+                      prepared_conv_weights, set_conv_image_cache)
 from ..ops import CSVec
 from ..ops import transformer as _tx
 from ..utils.logging import PhaseTimer
@@ -341,15 +342,18 @@ class FedModel:
                     per_ex, metrics = self.compute_loss_val(model, self._prep(inputs),
                                                             targets, self.args)
         if want_grad:
-            if (loss_weight is None and not capture and per_ex.dtype == torch.float32
-                    and per_ex.dim() == 1):
-                # d(sum)/d(per_ex) = 1: a cached ones vector (no sum / fill kernels)
-                torch.autograd.backward(per_ex, grad_tensors=self._ones(per_ex))
-            else:
-                total = per_ex.float().sum()
-                if loss_weight is not None:
-                    total = total * loss_weight
-                total.backward()
+            # the native conv wgrad split-K reductions: one batched launch at the
+            # end of the pass (ops/nn.py deferred_wgrad)
+            with deferred_wgrad(self.device.type == "cuda"):
+                if (loss_weight is None and not capture and per_ex.dtype == torch.float32
+                        and per_ex.dim() == 1):
+                    # d(sum)/d(per_ex) = 1: a cached ones vector (no sum / fill kernels)
+                    torch.autograd.backward(per_ex, grad_tensors=self._ones(per_ex))
+                else:
+                    total = per_ex.float().sum()
+                    if loss_weight is not None:
+                        total = total * loss_weight
+                    total.backward()
             if sinks is not None:
                 _tx.join_wgrad_stream()  # side-stream weight gradients into flat.g
             if shadow is not None and not self._overlap_armed:
@@ -516,16 +520,18 @@ class FedModel:
         meta = self.accountant.round_meta(clients)
         host = np.concatenate([idx2.reshape(-1), slot_per_ex, counts.astype(np.int64), meta])
         if e.get("packed") is None or e["packed"].numel() != host.size:
+            self._tape_free(e)
             e["packed"] = torch.empty(host.size, dtype=torch.int64, device=self.device)
-            e["compute"] = e["server"] = None
         dist.h2d_into(e["packed"], host)
         parts, o = [], 0
         for n in (2 * n_local, n_local, W, len(meta)):
             parts.append(e["packed"][o:o + n])
             o += n
         payload = self._payload_buf(n_res * W)
-        if e.get("payload_ptr") != payload.data_ptr():
-            e["compute"] = e["server"] = None
+        if e.get("payload_ptr") != payload.data_ptr() or e.get("img_gen") != image_generation():
+            # a new payload buffer, or the kept conv weight images the tapes
+            # read (and the server tape patches) were replaced: record again
+            self._tape_free(e)
         if e["compute"] is None:
             self._tape_free(e)
 
@@ -539,8 +545,10 @@ class FedModel:
                 self._metric_sums([pe] + ms, parts[1], parts[2], W, out=tail)
                 self._encode_merged(payload[:self.main_numel], n_local)
                 return self._aggregate(payload)
+            gen = image_generation()
             e["compute"] = self._tapes.record(e["key"], body)
             e["payload_ptr"] = payload.data_ptr()
+            e["img_gen"] = gen
             if e["compute"] is None:  # incomplete tape: this geometry stays eager
                 self._tape_entries.pop(e["key"], None)
                 return None

@@ -114,6 +114,7 @@ class RoundTapes:
         self.failed = set()
         self.replays = 0
         self.last_counts = None
+        self._live: List[Replay] = []
         # context around the eager steps (collectives) of a replay, e.g. a phase timer
         self.call_ctx = None
 
@@ -123,6 +124,11 @@ class RoundTapes:
         global _REC
         if key in self.failed:
             return None
+        self._live = [r for r in self._live if r.valid]
+        if not self._live:
+            # every graph of the shared pool was freed: PyTorch released the
+            # pool with the last one, so the next capture starts a new pool
+            self.pool = None
         cur = torch.cuda.current_stream(self.device)
         cur.synchronize()
         self.stream.wait_stream(cur)
@@ -151,6 +157,7 @@ class RoundTapes:
         self.last_counts = counts
         n_tape = sum(int(_ops().tape_size(x)) for kind, x in rec.segments if kind == "tape")
         rep = Replay(rec.segments, g, result)
+        self._live.append(rep)
         chain = len(counts) < 7 or (counts[4] <= 1 and counts[5] <= 1 and counts[6] <= 1)
         if counts[1] or counts[3] or counts[0] + counts[2] != n_tape or not chain:
             warnings.warn(f"launch tape for {key!r} incomplete (graph nodes: {counts[0]} kernels, "

@@ -33,3 +33,31 @@ def test_fetchsgd_reaches_uncompressed_accuracy_gpu():
     assert acc["sketch"] >= 0.87, acc
     # FetchSGD within a few points of uncompressed SGD (FetchSGD paper, Fig. 3)
     assert abs(acc["sketch"] - acc["uncompressed"]) <= 0.03, acc
+
+
+def _final_acc(path):
+    import json
+    last = {}
+    for line in open(path):
+        r = json.loads(line)
+        last[(r["mode"], r["lr_scale"])] = r
+    return last
+
+
+def test_region_sketch_converges_like_csvec_layout():
+    """Training-level parity pin of the default hash family (--encode region,
+    ops/sketch_region.py) against the reference's CSVec layout (--encode
+    planned, numBlocks = 20 multiply-shift hashes; fed_aggregator.py:464-467,
+    584-595): the committed 24-epoch curves of scripts/convergence.py
+    (profiles/r4_convergence.jsonl, same config, seed and LR per pair) end
+    within 1 point of test accuracy of each other at every LR measured."""
+    path = os.path.join(ROOT, "profiles", "r4_convergence.jsonl")
+    if not os.path.exists(path):
+        pytest.skip("profiles/r4_convergence.jsonl not recorded")
+    last = _final_acc(path)
+    pairs = [(lr, last[("sketch", lr)]["test_acc"], last[("sketch_planned", lr)]["test_acc"])
+             for (m, lr) in last if m == "sketch" and ("sketch_planned", lr) in last]
+    assert pairs, "no (region, planned) pair at a common LR"
+    for lr, region, planned in pairs:
+        assert last[("sketch", lr)]["epoch"] == last[("sketch_planned", lr)]["epoch"] == 24
+        assert abs(region - planned) <= 0.01, (lr, region, planned)
