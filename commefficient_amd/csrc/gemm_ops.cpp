@@ -28,14 +28,16 @@ at::Tensor mm_impl(const at::Tensor& a, const at::Tensor& b, bool nn, const c10:
                     (f32 || out->scalar_type() == at::kBFloat16),
                 "mm: out must be [M, N] bf16 / fp32 with unit column stride");
   if (bias.has_value() && bias->defined())
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N, "mm: bias f32 [N]");
+    TORCH_CHECK((bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16) &&
+                    bias->is_contiguous() && bias->numel() == N,
+                "mm: bias f32 / bf16 [N]");
   TORCH_CHECK(act == 0 || (act == 1 && !f32 && pre.has_value() && pre->defined() && pre->sizes() == at::IntArrayRef({M, N}) &&
                            pre->is_contiguous() && pre->scalar_type() == at::kBFloat16),
               "mm: act 1 (GELU) needs a bf16 [M, N] pre tensor and a bf16 output");
   at::Tensor C = has_out ? *out : at::empty({M, N}, a.options());
   if (!a.is_cuda()) {  // fp32 reference: one rounding at the end, as the kernel
     auto r = nn ? at::mm(a.to(at::kFloat), b.to(at::kFloat)) : at::mm(a.to(at::kFloat), b.to(at::kFloat).t());
-    if (bias.has_value() && bias->defined()) r = r + *bias;
+    if (bias.has_value() && bias->defined()) r = r + bias->to(at::kFloat);
     if (beta != 0.0) r = r + beta * C.to(at::kFloat);
     if (act == 1) {
       auto p = r.to(at::kBFloat16);
@@ -47,6 +49,11 @@ at::Tensor mm_impl(const at::Tensor& a, const at::Tensor& b, bool nn, const c10:
   }
   TORCH_CHECK(gemm_supported(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), nn),
               "mm: native GEMM needs N % 64 == 0 and K % 64 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
+                  a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(C.data_ptr()) % 16 == 0 && C.stride(0) % 8 == 0 &&
+                  (!bias.has_value() || !bias->defined() || reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0),
+              "mm: 16-byte aligned operands and row strides");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   GemmArgs g;
   g.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
@@ -56,7 +63,9 @@ at::Tensor mm_impl(const at::Tensor& a, const at::Tensor& b, bool nn, const c10:
   g.C = C.data_ptr();
   g.ldc = C.stride(0);
   g.C2 = act == 1 ? pre->data_ptr() : nullptr;
-  g.bias = bias.has_value() && bias->defined() ? bias->data_ptr<float>() : nullptr;
+  const bool hb = bias.has_value() && bias->defined();
+  g.bias = hb && bias->scalar_type() == at::kFloat ? bias->data_ptr<float>() : nullptr;
+  g.bias16 = hb && bias->scalar_type() == at::kBFloat16 ? reinterpret_cast<const uint16_t*>(bias->data_ptr()) : nullptr;
   g.M = static_cast<int>(M);
   g.N = static_cast<int>(N);
   g.K = static_cast<int>(K);

@@ -509,6 +509,7 @@ struct GemmArgs {
   int64_t ldc;
   void* C2;
   const float* bias;
+  const uint16_t* bias16 = nullptr;  // bf16 bias (instead of the fp32 one)
   int M, N, K;
   float beta;
 };

@@ -208,16 +208,20 @@ _GEMM = {"native": os.environ.get("COMMEFF_GEMM", "native") == "native"}
 
 
 def _native_mm_ok(a: torch.Tensor, b: torch.Tensor, n: int) -> bool:
-    return (_GEMM["native"] and a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
-            and a.dim() == 2 and b.dim() == 2 and a.stride(1) == 1 and b.stride(1) == 1
-            and n % 64 == 0 and a.shape[1] % 64 == 0 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+    # (bf16 CUDA operands are checked by the op itself; this keeps the shapes
+    # it serves: one Python test per call instead of a dozen attribute reads)
+    sa, sb = a.stride(), b.stride()
+    return (_GEMM["native"] and a.is_cuda and n % 64 == 0 and a.shape[1] % 64 == 0
+            and sa[1] == 1 and sb[1] == 1 and sa[0] % 8 == 0 and sb[0] % 8 == 0
+            and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
             and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
 
 
 def _mm(a: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """a @ W (+ bias): the HF Conv1D forward, W [in, out] (native NN GEMM)."""
+    """a @ W (+ bias): the HF Conv1D forward, W [in, out] (native NN GEMM, the
+    bf16 bias added in its epilogue)."""
     if _native_mm_ok(a, W, W.shape[1]):
-        return _ops().mm_nn(a, W, bias.float() if bias is not None else None)
+        return _ops().mm_nn(a, W, bias)
     return torch.addmm(bias, a, W) if bias is not None else torch.mm(a, W)
 
 

@@ -131,6 +131,11 @@ def main():
         warnings.simplefilter("always")
         torch.cuda.set_sync_debug_mode("warn")
     allocs0 = torch.cuda.memory_stats().get("num_device_alloc", 0)
+    prof_out = os.environ.get("COMMEFF_PROFILE_ROUNDS")
+    if prof_out:  # cProfile of the timed rounds only (host cost per call site)
+        import cProfile
+        cprof = cProfile.Profile()
+        cprof.enable()
     t0 = time.perf_counter()
     host = 0.0  # host time spent enqueueing (the GPU idles when this is the bound)
     for i in range(b.warmup, b.warmup + b.steps):
@@ -139,6 +144,13 @@ def main():
         fopt.step()
         host += time.perf_counter() - h0
     torch.cuda.synchronize()
+    if prof_out:
+        cprof.disable()
+        import pstats
+        with open(prof_out, "w") as f:
+            st = pstats.Stats(cprof, stream=f)
+            st.sort_stats("tottime").print_stats(50)
+            st.sort_stats("cumtime").print_stats(80)
     dist.barrier()
     el = dist.max_over_ranks(time.perf_counter() - t0)
     tp = os.environ.get("COMMEFF_TORCH_PROFILE")

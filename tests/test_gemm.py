@@ -14,6 +14,8 @@ SHAPES = [  # M, N, K
     (9600, 3072, 768),   # MLP up
     (9600, 768, 3072),   # MLP down
     (25088, 256, 1024),  # ResNet-101 bottleneck 1x1 (8 x 56 x 56 px)
+    (9500, 768, 3072),   # 256-row tiles with a row tail (9500 % 256 = 28)
+    (9500, 2304, 768),   # 256 x 256 tiles with a row tail
     (777, 128, 256),     # row tail
     (130, 64, 64),       # 64-wide tiles, tiny
 ]
@@ -50,6 +52,9 @@ def test_gemm_matches_fp32(M, N, K, layout):
     assert _rel(y, ref) < 1e-2
     yb = _ops().mm_nt(a, b, bias) if layout == "nt" else _ops().mm_nn(a, b.t().contiguous(), bias)
     assert _rel(yb, ref + bias) < 1e-2
+    b16 = bias.to(torch.bfloat16)  # bf16 bias (the GPT-2 Conv1D biases), added in the epilogue
+    yh = _ops().mm_nt(a, b, b16) if layout == "nt" else _ops().mm_nn(a, b.t().contiguous(), b16)
+    assert _rel(yh, ref + b16.float()) < 1e-2
 
 
 @pytest.mark.gpu
