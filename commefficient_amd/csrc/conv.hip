@@ -428,8 +428,20 @@ struct HaloCfg {
 template <int TBM, int BN>
 constexpr int halo_lds() { return HaloCfg<TBM>::kWinBytes + 2 * BN * 128; }
 
-template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
-__global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
+// DB: double-buffered operand fragments.  Without it the compiler (at the
+// 128-VGPR budget of 4 waves/SIMD) gives the next sub-step's fragments the
+// registers of the current ones, so every 4-MFMA group waits for its own LDS
+// reads (s_waitcnt lgkmcnt(0) right before it, disassembly) -- ~45 % of the
+// MFMA rate with every global load, barrier and the epilogue removed
+// (COMMEFF_CONV_ABLATE=15).  With it the fragment offsets are one register per
+// operand row (sub-step kk flips chunk bits 5-6), the reads of sub-step kk+1
+// are pinned above the MFMAs of kk (sched_barrier), and the step's barrier
+// sits before the last sub-step's MFMAs, which overlap the next step's first
+// reads.
+template <int TBM, bool POOL, bool SPLIT = false, int BN = 128, bool DB = true>
+__global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1))
+__attribute__((amdgpu_waves_per_eu((TBM == 256 && !SPLIT) ? 4 : 1)))  // two 8-wave blocks per CU
+conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   static_assert(BN == 128 || (BN == 64 && !SPLIT && !POOL), "halo tile width");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
   // group g (split-K half) of this block: its own window + B ring
@@ -472,12 +484,12 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
     }
     win_off[i] = off;
   }
-  const uint16_t* b_ptr[BLD];
+  int b_off[BLD];  // element offsets into a.w (< K * 9 * C)
 #pragma unroll
   for (int j = 0; j < BLD; ++j) {
     const int sl = j * NT + tid;
     const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
-    b_ptr[j] = a.w + static_cast<size_t>(n0 + row) * 9 * C + lc * 8;
+    b_off[j] = (n0 + row) * 9 * C + lc * 8;
   }
   auto issue_window = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
@@ -493,7 +505,7 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
     unsigned char* base = smem + kHaloWinBytes + (step & 1) * (BN * 128) + wid * 1024;
     const int boff = (step % 9) * C + (step / 9) * 64;
 #pragma unroll
-    for (int j = 0; j < BLD; ++j) glds16(b_ptr[j] + boff, base + j * NT * 16);
+    for (int j = 0; j < BLD; ++j) glds16(a.w + (b_off[j] + boff), base + j * NT * 16);
   };
 
   // this lane's output pixels (rows of the A fragments) -> padded window rows
@@ -526,6 +538,88 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
 
+  if constexpr (DB) {
+    int bB[NI];  // sub-step 0 B offsets; sub-step kk: ^ (kk << 5)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int row = wc * (BN / 2) + ni * 32 + lr;
+      bB[ni] = row * 128 + ((hi ^ sw_rd128(row)) << 4);
+    }
+    auto a_base = [&](int st, int (&bA)[2]) __attribute__((always_inline)) {
+      const int tap = st % 9, dr = tap / 3 - 1, dc = tap % 3 - 1;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int pr = pbr[mi] + dr, pc = pbc[mi] + dc;
+        bA[mi] = (pr * hg.PW + pc) * 128 + ((hi ^ sw_halo(pr, pc, hg)) << 4);
+      }
+    };
+    auto load = [&](int st, int kk, const int (&bA)[2], bf16x8_t (&fa)[2], bf16x8_t (&fb)[NI])
+        __attribute__((always_inline)) {
+      const unsigned char* sB = smem + kHaloWinBytes + (st & 1) * (BN * 128);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) fa[mi] = *reinterpret_cast<const bf16x8_t*>(smem + (bA[mi] ^ (kk << 5)));
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) fb[ni] = *reinterpret_cast<const bf16x8_t*>(sB + (bB[ni] ^ (kk << 5)));
+    };
+    auto mma = [&](const bf16x8_t (&fa)[2], const bf16x8_t (&fb)[NI]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+    };
+    issue_window(s_beg / 9);
+    issue_b(s_beg);
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s_beg + 1 < s_end) issue_b(s_beg + 1);
+    int bA[2];
+    a_base(s_beg, bA);
+    bf16x8_t fa0[2], fb0[NI], fa1[2], fb1[NI];
+    load(s_beg, 0, bA, fa0, fb0);
+    // MFMAs of one buffer interleaved one-for-one with the reads of the other
+    // (an MFMA gap takes 2 ds_read_b128 at no cost, MI355X_MICROARCH.md §LDS):
+    // the reads are in flight under the MFMAs that precede their use
+    auto interleave = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+      }
+    };
+    for (int s = s_beg; s < s_end; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      mma(fa0, fb0);
+      load(s, 1, bA, fa1, fb1);
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+      mma(fa1, fb1);
+      load(s, 2, bA, fa0, fb0);
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+      mma(fa0, fb0);
+      load(s, 3, bA, fa1, fb1);
+      interleave();
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < s_end) {
+        // this wave's reads of step s are done; at a channel-block boundary every
+        // wave's are (barrier) before the next window overwrites the old one
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if ((s + 1) % 9 == 0) {
+          __builtin_amdgcn_s_barrier();
+          issue_window((s + 1) / 9);
+        }
+        wait_vmcnt<0>();  // B(s + 1) (and the new window) landed for this wave ...
+        __builtin_amdgcn_s_barrier();  // ... and for every wave; slot s & 1 is free
+        if (s + 2 < s_end) issue_b(s + 2);
+        a_base(s + 1, bA);
+        load(s + 1, 0, bA, fa0, fb0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma(fa1, fb1);
+    }
+  } else {
   issue_window(s_beg / 9);
   issue_b(s_beg);
   for (int s = s_beg; s < s_end; ++s) {
@@ -578,6 +672,7 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
     }
   }
+  }  // DB
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr (SPLIT) {
@@ -606,6 +701,15 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1)) conv_fwd_halo_kerne
     conv_fwd_epilogue<TBM, BN, POOL, TBM * 4>(a, acc, smem_base, m0, n0, threadIdx.x, wr, wc, hi, lr,
                                               half == 0);
   } else {
+    if (a.ablate & 8) {  // timing experiment: no epilogue (one value per lane keeps the MFMAs)
+      float t = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) t += acc[mi][ni][0];
+      if (t == 12345.f) a.y[tid] = 1;
+      return;
+    }
     conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, m0, n0, tid, wr, wc, hi, lr);
   }
 }
@@ -1667,14 +1771,24 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g, int BN = 128) {
 template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
 void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
   constexpr int lds = halo_lds<TBM, BN>() * (SPLIT ? 2 : 1);
+  // COMMEFF_CONV_DB=0: the single-buffered fragment loop (A/B experiments)
+  static const bool db = [] {
+    const char* e = getenv("COMMEFF_CONV_DB");
+    return !(e != nullptr && e[0] == '0');
+  }();
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, true>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, false>), lds);
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), dim3(mt * (a.K / BN)),
-                     dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
+  if (db)
+    COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, true>), dim3(mt * (a.K / BN)),
+                   dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
+  else
+    COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, false>), dim3(mt * (a.K / BN)),
+                   dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
 }
 
 template <bool POOL, int BN>

@@ -523,12 +523,15 @@ bool gemm_supported(int M, int N, int K, bool nn) {
 
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream) {
   if (a.M <= 0) return;
-  // 256-row tiles with a 4-stage ring (one block per CU) when they still give
-  // most CUs a tile; 256 columns when that is still >= ~200 tiles
-  // (COMMEFF_GEMM_BIG=0: the 128-row kernel only)
+  // COMMEFF_GEMM_BIG=1: 256-row tiles with a 4-stage ring (one block per CU)
+  // when they still give most CUs a tile.  Off by default: on the GPT-2 and
+  // ResNet-101 shapes it measured equal or slower than the 128-row kernel
+  // (e.g. 9400 x 768 x 3072 NN 84.9 vs 62.3 us; profiles/r4_gemm_native_vs_hipblaslt.jsonl):
+  // these GEMMs are one wave of tiles whose load / store phases, not the
+  // K-loop latency, set the time
   static const bool big_on = [] {
     const char* e = getenv("COMMEFF_GEMM_BIG");
-    return !(e != nullptr && e[0] == '0');
+    return e != nullptr && e[0] == '1';
   }();
   const int64_t mt = (a.M + 255) / 256;
   if (big_on && a.K % GK2 == 0 && a.N % 128 == 0) {

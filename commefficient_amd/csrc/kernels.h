@@ -263,7 +263,7 @@ struct ConvFwdArgs {
   uint16_t* y_dual = nullptr;
   // timing experiments only (COMMEFF_CONV_ABLATE, results are wrong): bit 0 =
   // no weight-tile loads after the first two K-steps, bit 1 = no window reload
-  // per channel block, bit 2 = no per-K-step wait / barrier
+  // per channel block, bit 2 = no per-K-step wait / barrier, bit 3 = no epilogue
   int ablate = 0;
 };
 struct ConvWgradArgs {
