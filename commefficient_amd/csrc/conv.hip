@@ -872,37 +872,50 @@ __global__ void __launch_bounds__(512) conv_fwd_pipe_kernel(ConvFwdArgs a, HaloG
     const unsigned char* sW = win_buf(wn & 1);
     const unsigned char* sB = ring + (g % 3) * (BN * 128);
     const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-    int offA[2], swA[2];
+    int bA[2];  // sub-step 0 A offsets; sub-step kk: ^ (kk << 5) (chunk bits 5-6)
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
       const int pr = pbr[mi] + dr, pc = pbc[mi] + dc;
-      offA[mi] = (pr * hg.PW + pc) * 128;
-      swA[mi] = sw_halo(pr, pc, hg);
+      bA[mi] = (pr * hg.PW + pc) * 128 + ((hi ^ sw_halo(pr, pc, hg)) << 4);
     }
-    bf16x8_t af[2][2], bfr[2][NI];
+    // double-buffered fragments, MFMAs interleaved one-for-one with the next
+    // sub-step's reads (as the halo kernel's DB loop)
+    bf16x8_t fa0[2], fb0[NI], fa1[2], fb1[NI];
+    auto load = [&](int kk, bf16x8_t (&fa)[2], bf16x8_t (&fb)[NI]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-      af[0][mi] = *reinterpret_cast<const bf16x8_t*>(sW + offA[mi] + ((hi ^ swA[mi]) << 4));
+      for (int mi = 0; mi < 2; ++mi) fa[mi] = *reinterpret_cast<const bf16x8_t*>(sW + (bA[mi] ^ (kk << 5)));
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) bfr[0][ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[0][ni]);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int cur = kk & 1, nxt = cur ^ 1;
-      if (kk + 1 < 4) {
-        const int chk = 2 * (kk + 1) + hi;
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-          af[nxt][mi] = *reinterpret_cast<const bf16x8_t*>(sW + offA[mi] + ((chk ^ swA[mi]) << 4));
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          bfr[nxt][ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[kk + 1][ni]);
-      }
+      for (int ni = 0; ni < NI; ++ni) fb[ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[kk][ni]);
+    };
+    auto mma = [&](const bf16x8_t (&fa)[2], const bf16x8_t (&fb)[NI]) __attribute__((always_inline)) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
-    }
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
+    };
+    auto interleave = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    };
+    load(0, fa0, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fa0, fb0);
+    load(1, fa1, fb1);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fa1, fb1);
+    load(2, fa0, fb0);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fa0, fb0);
+    load(3, fa1, fb1);
+    interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    mma(fa1, fb1);
     if (tap == 8) {
       if (cb + 1 == CB) {
         // tile done: stage through the window just finished (every wave is
@@ -1127,7 +1140,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(ConvWgradArgs a) {
 // operand images are pairs of the 128-wide [64 px][128] images of the small
 // kernel (same swizzle and transposed reads), one block per CU (128 KB LDS);
 // split-K over pixels fills the chip, slabs as in conv_wgrad_kernel.
-template <bool ROWSTEP, int TPG>
+template <bool ROWSTEP, int TPG, bool IL = true>
 __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int HALF = BK * 128 * 2;           // one [64 px][128] image, 16 KB
@@ -1247,20 +1260,47 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int cur = kk & 1, nxt = cur ^ 1;
-      if (kk + 1 < 4) {
-        const int dd = (kk + 1) * 16 * 256;
+      if constexpr (IL) {
+        // the 8 MFMAs of kk interleaved with the 12 transposed reads of kk + 1
+        // (as the halo wgrad kernel)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
-          af[nxt][mi] = tr_read(sb + toA[mi][0] + dd, sb + toA[mi][1] + dd);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          bfr[nxt][ni] = tr_read(sb + toB[ni][0] + dd, sb + toB[ni][1] + dd);
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
+        if (kk + 1 < 4) {
+          const int dd = (kk + 1) * 16 * 256;
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+            af[nxt][mi] = tr_read(sb + toA[mi][0] + dd, sb + toA[mi][1] + dd);
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            bfr[nxt][ni] = tr_read(sb + toB[ni][0] + dd, sb + toB[ni][1] + dd);
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        if (kk + 1 < 4) {
+          const int dd = (kk + 1) * 16 * 256;
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+            af[nxt][mi] = tr_read(sb + toA[mi][0] + dd, sb + toA[mi][1] + dd);
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            bfr[nxt][ni] = tr_read(sb + toB[ni][0] + dd, sb + toB[ni][1] + dd);
+        }
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
       }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
     }
     rd ^= 1;
   }
@@ -1300,7 +1340,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
 // for waves whose pieces start inside the window (wave-uniform), so a stage
 // holds 72 window rows and every wave has >= ALD + 2 DMA loads per stage.
 constexpr int kHaloWRows = 72;  // window rows staged per K-step (>= R * (W + 2) > 64)
-template <int NSTAGE>
+template <int NSTAGE, bool IL = true>
 __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int A_BYTES = BK * WBM * 2;         // [64 px][128 k], 256-byte rows
@@ -1418,6 +1458,16 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int cur = kk & 1, nxt = cur ^ 1;
+      // the 6 MFMAs of sub-step kk interleaved with the 10 transposed reads of
+      // kk + 1 (two per MFMA gap; the fragments are double-buffered), so the
+      // reads are in flight under the MFMAs instead of waited for in front of
+      // each (the compiler's own order: disassembly, profiles/r4_experiments.md)
+      if constexpr (IL) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 3; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
       if (kk + 1 < 4) {
         const int da = (kk + 1) * 16 * 256;
 #pragma unroll
@@ -1426,12 +1476,16 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
 #pragma unroll
         for (int ni = 0; ni < 3; ++ni)
           bfr[nxt][ni] = tr_read(sb + offB[kk + 1][ni][0], sb + offB[kk + 1][ni][1]);
+        if constexpr (IL) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
       }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 3; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
+      if constexpr (IL) __builtin_amdgcn_sched_barrier(0);
     }
     rd = rd + 1 == NSTAGE ? 0 : rd + 1;
     wrs = wrs + 1 == NSTAGE ? 0 : wrs + 1;
@@ -1931,20 +1985,34 @@ template <bool ROWSTEP>
 void launch_wgrad_wide(const ConvWgradArgs& a, hipStream_t stream) {
   constexpr int lds = 2 * 4 * BK * 128 * 2;
   const int tiles = wgrad_tiles(a.K, a.C);
+  // COMMEFF_WGRAD_WIDE_IL=1: the MFMA / read interleave of the halo wgrad
+  // kernel here too (off: res3 60.8 -> 65.4 us, layer 3 equal; r4 log)
+  static const bool il = [] {
+    const char* e = getenv("COMMEFF_WGRAD_WIDE_IL");
+    return e != nullptr && e[0] == '1';
+  }();
   if (a.C == 128) {
     static bool init = false;
     if (!init) {
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 2>), lds);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 2, true>), lds);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 2, false>), lds);
       init = true;
     }
-    COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 2>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    if (il)
+      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 2, true>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    else
+      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 2, false>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
   } else {
     static bool init = false;
     if (!init) {
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 1>), lds);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 1, true>), lds);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 1, false>), lds);
       init = true;
     }
-    COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 1>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    if (il)
+      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 1, true>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    else
+      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 1, false>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
   }
 }
 
@@ -2015,16 +2083,25 @@ void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_
     }();
     const int tiles = (a.K / WBM) * 3 * (a.C / 64);
     constexpr int stage_bytes = BK * WBM * 2 + kHaloWRows * 128;
+    // COMMEFF_WGRAD_IL=0: the compiler's own read / MFMA order (A/B experiments)
+    static const bool il = [] {
+      const char* e = getenv("COMMEFF_WGRAD_IL");
+      return !(e != nullptr && e[0] == '0');
+    }();
     static bool init = false;
     if (!init) {
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2>), 2 * stage_bytes);
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<3>), 3 * stage_bytes);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2, true>), 2 * stage_bytes);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<3, true>), 3 * stage_bytes);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2, false>), 2 * stage_bytes);
       init = true;
     }
     if (stages == 3)
-      COMMEFF_LAUNCH(conv_wgrad_halo_kernel<3>, dim3(tiles * a.splits), dim3(256), 3 * stage_bytes, stream, a);
+      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<3, true>), dim3(tiles * a.splits), dim3(256), 3 * stage_bytes, stream, a);
+    else if (il)
+      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2, true>), dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
     else
-      COMMEFF_LAUNCH(conv_wgrad_halo_kernel<2>, dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
+      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2, false>), dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream,
+                     a);
   } else if (wgrad_wide(a.K, a.C)) {
     if (rowstep) launch_wgrad_wide<true>(a, stream); else launch_wgrad_wide<false>(a, stream);
   } else if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)

@@ -29,9 +29,10 @@ def main():
         flops = 2.0 * N * H * H * K * C * 9
         f = timeit(lambda: ops.conv3x3_fwd(x, wf, True), n=40)
         d = timeit(lambda: ops.conv3x3_fwd(dy, wt, False), n=40)
+        wg = timeit(lambda: ops.conv3x3_wgrad(dy, x), n=40)
         print(json.dumps({"ablate": ab, "layer": name, "fwd_us": round(f, 1),
                           "fwd_tflops": round(flops / f / 1e6, 1),
-                          "dgrad_us": round(d, 1)}), flush=True)
+                          "dgrad_us": round(d, 1), "wgrad_us": round(wg, 1)}), flush=True)
 
 
 if __name__ == "__main__":
