@@ -58,10 +58,29 @@ def _compare(d, mode, n, bitwise_single: bool, tol):
         torch.testing.assert_close(res[0]["w"], s["w"], rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(res[0]["loss"], s["loss"], rtol=1e-4, atol=1e-5)
     else:
-        torch.testing.assert_close(res[0]["loss"], s["loss"], rtol=tol, atol=tol)
+        torch.testing.assert_close(res[0]["loss"], s["loss"], rtol=tol["loss"], atol=tol["loss"])
         w0 = s["w"]
         moved = (w0 - res[0]["w"]).abs().max()
-        assert moved < 0.05, moved
+        assert moved < tol["w"], moved
+
+
+# Tolerances of the N-GPU vs 1-GPU comparison (bf16 compute), derived:
+# * every example's forward is the same computation in both runs (merged
+#   clients, no BatchNorm; the native conv kernels sum each output pixel over
+#   the same K order whatever the batch), so round 1's loss is bitwise equal
+#   and the runs differ only through the gradient SUMS: the per-rank split
+#   changes the fp32 summation order of the split-K weight gradients and the
+#   cross-rank all-reduce (relative ~1e-6 of the gradient).
+# * dense server step (uncompressed): after 3 rounds at lr 0.05 the weights
+#   differ by ~1e-6 x lr x |g| -- far below 1e-3; the later rounds' losses move
+#   only where a bf16 activation rounds the other way (<< 5e-3 relative).
+# * selecting modes (sketch / true / local top-k): an order-level difference can
+#   flip a near-tie coordinate in or out of the k selected; such a coordinate
+#   moves by lr x |its momentum-accumulated value| per round, <= 3 x 0.05 x
+#   ~0.3 = 0.045 over 3 rounds for this ResNet-9's gradients (< 0.05), and the
+#   loss of the next round by a few 1e-3 relative (3e-2 bound).
+TOLS = {"uncompressed_overlap": {"loss": 5e-3, "w": 1e-3}}
+TOL_SELECT = {"loss": 3e-2, "w": 0.05}
 
 
 def _visible():
@@ -91,4 +110,4 @@ def test_rccl_multi_gpu(mode, n):
     with tempfile.TemporaryDirectory() as d:
         _launch(n, d, mode, 3, "cuda", 600)
         _launch(1, d, mode, 3, "cuda", 600)
-        _compare(d, mode, n, bitwise_single=False, tol=3e-2)
+        _compare(d, mode, n, bitwise_single=False, tol=TOLS.get(mode, TOL_SELECT))
