@@ -2010,6 +2010,76 @@ std::tuple<at::Tensor, at::Tensor> bias_act_bwd_hip(const at::Tensor& gf,
   return {du, db};
 }
 
+// The same backward passes with the column sums deferred: they return the
+// block partials instead, and colsum_into reduces them into fp32 gradient
+// sinks later -- on the weight-gradient side stream (ops/transformer.py), so
+// the ~40 us of latency-bound column sums per junction leave the input-
+// gradient critical path
+std::tuple<at::Tensor, at::Tensor, at::Tensor> resid_ln_bwd_part_hip(
+    const at::Tensor& gy, const c10::optional<at::Tensor>& gh, const at::Tensor& h,
+    const at::Tensor& mean, const at::Tensor& rstd, const at::Tensor& gamma, double p_drop,
+    int64_t seed, bool want_dp) {
+  TORCH_CHECK(h.dim() == 2, "resid_ln_bwd_part: h must be [M, H]");
+  const int64_t M = h.size(0), H = h.size(1);
+  TORCH_CHECK(resid_ln_supported(H), "resid_ln_bwd_part: unsupported H ", H);
+  check_rows_bf16(h, M, H, "resid_ln_bwd_part: h");
+  check_rows_bf16(gy, M, H, "resid_ln_bwd_part: gy");
+  if (gh.has_value() && gh->defined()) check_rows_bf16(*gh, M, H, "resid_ln_bwd_part: gh");
+  check_vec_bf16(gamma, H, "resid_ln_bwd_part: gamma");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == M && rstd.numel() == M &&
+                  rstd.scalar_type() == at::kFloat,
+              "resid_ln_bwd_part: mean/rstd must be float32 [M]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(h.device());
+  auto dh = at::empty_like(h);
+  auto dp = want_dp ? at::empty_like(h) : at::empty({0}, h.options());
+  const int G = resid_ln_bwd_blocks(M);
+  auto part = at::empty({G, 3, H}, h.options().dtype(at::kFloat));
+  launch_resid_ln_bwd(gy.data_ptr(), opt_ptr(gh), h.data_ptr(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), gamma.data_ptr(), dh.data_ptr(),
+                      want_dp ? dp.data_ptr() : nullptr, part.data_ptr<float>(), M, H,
+                      static_cast<float>(p_drop), static_cast<uint32_t>(seed), cur_stream());
+  return {dh, dp, part};
+}
+
+std::tuple<at::Tensor, at::Tensor> bias_act_bwd_part_hip(const at::Tensor& gf,
+                                                         const c10::optional<at::Tensor>& u,
+                                                         const at::Tensor& b, bool gelu) {
+  TORCH_CHECK(gf.dim() == 2 && gf.size(1) % 8 == 0 && gf.size(1) / 8 <= 1024,
+              "bias_act_bwd_part: gf must be [M, N], N % 8 == 0, N <= 8192");
+  const int64_t M = gf.size(0), N = gf.size(1);
+  TORCH_CHECK(M > 0, "bias_act_bwd_part: no rows");
+  check_rows_bf16(gf, M, N, "bias_act_bwd_part: gf");
+  check_vec_bf16(b, N, "bias_act_bwd_part: b");
+  if (gelu) {
+    TORCH_CHECK(u.has_value() && u->defined(), "bias_act_bwd_part: gelu needs u");
+    check_rows_bf16(*u, M, N, "bias_act_bwd_part: u");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gf.device());
+  auto du = gelu ? at::empty_like(gf) : at::empty({0}, gf.options());
+  const int G = bias_act_bwd_blocks(M);
+  auto part = at::empty({G, N}, gf.options().dtype(at::kFloat));
+  launch_bias_act_bwd(gf.data_ptr(), gelu ? u->data_ptr() : nullptr, b.data_ptr(),
+                      gelu ? du.data_ptr() : nullptr, part.data_ptr<float>(), M, N, gelu,
+                      cur_stream());
+  return {du, part};
+}
+
+// sink_q (fp32 [N]) += sum over the G blocks of part[g, q, :] (q < Q, part
+// [G, Q*N] rows), fixed order (deterministic); a missing sink skips its q
+void colsum_into_hip(const at::Tensor& part, int64_t Q, const c10::optional<at::Tensor>& s0,
+                     const c10::optional<at::Tensor>& s1, const c10::optional<at::Tensor>& s2) {
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() >= 2 && Q >= 1 && Q <= 3 &&
+                  part.numel() % (part.size(0) * Q) == 0,
+              "colsum_into: part must be contiguous fp32 [G, Q, N]");
+  const int64_t G = part.size(0), N = part.numel() / (G * Q);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
+  void* p0 = sink_ptr(s0, N, "colsum_into: s0");
+  void* p1 = Q > 1 ? sink_ptr(s1, N, "colsum_into: s1") : nullptr;
+  void* p2 = Q > 2 ? sink_ptr(s2, N, "colsum_into: s2") : nullptr;
+  ColsumOut out{{p0, p1, p2}, {2, 2, 2}};
+  launch_colsum_final(part.data_ptr<float>(), static_cast<int>(G), static_cast<int>(Q), N, Q * N, out, cur_stream());
+}
+
 at::Tensor pad_rows_hip(const at::Tensor& src, const c10::optional<at::Tensor>& inv, int64_t rows) {
   TORCH_CHECK(src.scalar_type() == at::kBFloat16 && src.dim() == 2 && src.stride(1) == 1 &&
                   src.size(1) % 8 == 0 && src.stride(0) % 8 == 0 &&
@@ -2297,6 +2367,10 @@ TORCH_LIBRARY(commeff, m) {
   m.def("maxpool_bwd(Tensor gy, Tensor codes, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bias_act_bwd(Tensor gf, Tensor? u, Tensor b, bool gelu, Tensor(a!)? sbias=None) "
         "-> (Tensor, Tensor)");
+  m.def("resid_ln_bwd_part(Tensor gy, Tensor? gh, Tensor h, Tensor mean, Tensor rstd, Tensor gamma, "
+        "float p_drop, int seed, bool want_dp) -> (Tensor, Tensor, Tensor)");
+  m.def("bias_act_bwd_part(Tensor gf, Tensor? u, Tensor b, bool gelu) -> (Tensor, Tensor)");
+  m.def("colsum_into(Tensor part, int Q, Tensor(a!)? s0=None, Tensor(b!)? s1=None, Tensor(c!)? s2=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CPU, m) {
@@ -2380,6 +2454,9 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("resid_ln_bwd", &resid_ln_bwd_hip);
   m.impl("bias_gelu_fwd", &bias_gelu_fwd_hip);
   m.impl("bias_act_bwd", &bias_act_bwd_hip);
+  m.impl("resid_ln_bwd_part", &resid_ln_bwd_part_hip);
+  m.impl("bias_act_bwd_part", &bias_act_bwd_part_hip);
+  m.impl("colsum_into", &colsum_into_hip);
   m.impl("pad_rows", &pad_rows_hip);
   m.impl("gemm_tn_acc", &gemm_tn_acc_hip);
   m.impl("attn_fwd", &attn_fwd_hip);

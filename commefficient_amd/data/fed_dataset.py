@@ -117,7 +117,10 @@ class FedDataset(torch.utils.data.Dataset):
             orig_idx = idx
             row = int(self.data_index(np.array([idx]))[0])
             nat = int(self.natural_client_of_row(np.array([row]))[0])
-            start = int(np.concatenate([[0], np.cumsum(self.images_per_client)])[nat])
+            offs = getattr(self, "_client_offsets", None)
+            if offs is None or len(offs) != len(self.images_per_client) + 1:
+                offs = self._client_offsets = np.concatenate([[0], np.cumsum(self.images_per_client)])
+            start = int(offs[nat])
             inputs = self._get_train_item(nat, row - start)
             client_id = int(self.client_of(np.array([orig_idx]))[0])
         else:

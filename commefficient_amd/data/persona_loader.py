@@ -31,19 +31,80 @@ def _to_dev(ts, device):
     return out
 
 
+# --train_dataloader_workers: the records of the next rounds are built in
+# worker processes while the current round runs (the reference's DataLoader
+# workers, gpt2_train.py:155-166).  Forked, not spawned: the children inherit
+# the dataset and never touch the GPU (as PyTorch DataLoader workers), and no
+# process that initialised the GPU execs another program.
+_WORKER_DS = None
+
+
+def _build_records(idx):
+    """Worker: the records of dataset items ``idx``, token lists as int32
+    arrays (pickled compactly; collate pads them like lists)."""
+    out = []
+    for i in idx:
+        rec = _WORKER_DS[int(i)][1]
+        out.append({"input_ids": [np.asarray(x, dtype=np.int32) for x in rec["input_ids"]],
+                    "token_type_ids": [np.asarray(x, dtype=np.int32) for x in rec["token_type_ids"]],
+                    "lm_labels": [np.asarray(x, dtype=np.int32) for x in rec["lm_labels"]],
+                    "mc_token_ids": list(rec["mc_token_ids"]), "mc_labels": rec["mc_labels"]})
+    return out
+
+
 class PersonaFedLoader:
-    def __init__(self, dataset, num_workers, local_batch_size, device, seed):
+    def __init__(self, dataset, num_workers, local_batch_size, device, seed, workers=0, prefetch=2):
         self.dataset = dataset
         self.sampler = FedSampler(dataset, num_workers, local_batch_size, seed=seed)
         self.device = device
+        self.workers = int(workers)
+        self.prefetch = max(1, int(prefetch))
+        self._pool = None
+
+    def _executor(self):
+        if self._pool is None:
+            import multiprocessing as mp
+            from concurrent.futures import ProcessPoolExecutor
+            global _WORKER_DS
+            _WORKER_DS = self.dataset
+            self._pool = ProcessPoolExecutor(max_workers=self.workers, mp_context=mp.get_context("fork"))
+        return self._pool
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=False, cancel_futures=True)
+            self._pool = None
 
     def __len__(self):
         return len(self.dataset)
 
     def __iter__(self):
         self.epoch = getattr(self, "epoch", 0) + 1
-        for r in self.sampler:
-            yield self.make_batch(r)
+        if self.workers <= 0:
+            for r in self.sampler:
+                yield self.make_batch(r)
+            return
+        # the next ``prefetch`` rounds' records are built in the workers while
+        # this one is consumed (each round's items split across the workers)
+        from collections import deque
+        ex = self._executor()
+        ahead = deque()
+
+        def submit(r):
+            parts = np.array_split(np.asarray(r), min(self.workers, len(r)))
+            return r, [ex.submit(_build_records, p) for p in parts if len(p)]
+
+        it = iter(self.sampler)
+        for r in it:
+            ahead.append(submit(r))
+            if len(ahead) > self.prefetch:
+                break
+        while ahead:
+            r, futs = ahead.popleft()
+            nxt = next(it, None)
+            if nxt is not None:
+                ahead.append(submit(nxt))
+            yield self.make_batch(r, futs)
 
     def state_dict(self, pos=None):
         """Sampler position (resume mid-epoch) -- the records themselves are a
@@ -54,12 +115,19 @@ class PersonaFedLoader:
         self.sampler.load_state_dict(sd["sampler"])
         self.epoch = int(sd.get("epoch", 0))
 
-    def make_batch(self, r):
+    def make_batch(self, r, futures=None):
         ds, dev = self.dataset, self.device
         cids = ds.client_of(r)
+        built = []
 
         def take(pos, r=r):
-            recs = [ds[int(i)][1] for i in r[pos]]
+            if futures is not None:
+                if not built:
+                    for f in futures:
+                        built.extend(f.result())
+                recs = [built[int(i)] for i in np.asarray(pos).reshape(-1)]
+            else:
+                recs = [ds[int(i)][1] for i in r[pos]]
             host = collate(recs)
             ids, mc, lab, mcl, tt, lp = _to_dev(list(host) + [label_positions(host[2])], dev)
             # sequence lengths stay on the host (mc token = last real token):

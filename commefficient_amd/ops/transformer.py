@@ -283,14 +283,44 @@ def set_fused_attention(enabled: bool) -> None:
     _ATTN["enabled"] = bool(enabled)
 
 
+def _side_stream(device) -> "torch.cuda.Stream":
+    if _SIDE["stream"] is None:
+        _SIDE["stream"] = torch.cuda.Stream(device=device)
+    return _SIDE["stream"]
+
+
+# The junction backward's column sums (LayerNorm dgamma / dbeta, the branch
+# bias gradients) go to the same side stream when all their outputs are fp32
+# sinks: ~40 us each of latency-bound reductions that otherwise sit in the
+# input-gradient chain behind the side stream's GEMM blocks (1.9 ms per GPT-2
+# round, profiles/r4_gpt2_native_gemm_round_kernels.txt).  COMMEFF_COLSUM_SIDE=0:
+# summed in place on the main stream.
+_COLSUM_SIDE = os.environ.get("COMMEFF_COLSUM_SIDE", "1") != "0"
+
+
+def _colsum_deferred(t: torch.Tensor, *sinks) -> bool:
+    return (_COLSUM_SIDE and _SIDE["enabled"] and t.is_cuda
+            and all(x is not None for x in sinks))
+
+
+def _side_colsum(part: torch.Tensor, q: int, sinks) -> None:
+    """sinks[i] += column sums of the block partials ``part`` (quantity i),
+    on the weight-gradient side stream after the producing kernel."""
+    main = torch.cuda.current_stream()
+    side = _side_stream(part.device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        _ops().colsum_into(part, q, *sinks)
+    part.record_stream(side)
+    _SIDE["pending"] = True
+
+
 def _wgrad(sink, a, b):
     if sink is None:
         return torch.mm(a, b)
     if sink.is_cuda and _SIDE["enabled"]:
         main = torch.cuda.current_stream()
-        if _SIDE["stream"] is None:
-            _SIDE["stream"] = torch.cuda.Stream(device=sink.device)
-        side = _SIDE["stream"]
+        side = _side_stream(sink.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             _acc_mm(sink, a, b)
@@ -322,6 +352,10 @@ class _EmbedLN(torch.autograd.Function):
         p_drop, seed = ctx.cfg
         sg, sb = ctx.sinks
         gy = torch.zeros_like(h) if gy is None else gy.contiguous()
+        if _colsum_deferred(gy, sg, sb):
+            _, dx, part = _ops().resid_ln_bwd_part(gy, _c(gh), h, mean, rstd, gamma, p_drop, seed, True)
+            _side_colsum(part, 3, (sg, sb, None))
+            return dx, None, None, None, None, None
         _, dx, dgamma, dbeta, _ = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma, p_drop,
                                                      seed, True, False, sg, sb, None)
         return (dx, None if sg is not None else dgamma, None if sb is not None else dbeta,
@@ -346,8 +380,13 @@ class _ResidLN(torch.autograd.Function):
         p_drop, seed = ctx.cfg
         sW, sb, sg, sbe = ctx.sinks
         gy = torch.zeros_like(h) if gy is None else gy.contiguous()
-        dh, dp, dgamma, dbeta, dbias = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma,
-                                                          p_drop, seed, True, True, sg, sbe, sb)
+        if _colsum_deferred(gy, sg, sbe, sb):
+            dh, dp, part = _ops().resid_ln_bwd_part(gy, _c(gh), h, mean, rstd, gamma, p_drop, seed, True)
+            _side_colsum(part, 3, (sg, sbe, sb))
+            dgamma = dbeta = dbias = None
+        else:
+            dh, dp, dgamma, dbeta, dbias = _Impl.resid_ln_bwd(gy, _c(gh), h, mean, rstd, gamma,
+                                                              p_drop, seed, True, True, sg, sbe, sb)
         do = _mm_t(dp, W) if ctx.needs_input_grad[1] else None
         dW = _wgrad(sW, o.t(), dp) if ctx.needs_input_grad[2] else None
         return (dh, do, dW, None if sb is not None else dbias,
@@ -370,7 +409,13 @@ class _FcGelu(torch.autograd.Function):
     def backward(ctx, gf):
         a, W, u, b = ctx.saved_tensors
         sW, sb = ctx.sinks
-        du, db = _Impl.bias_act_bwd(gf.contiguous(), u, b, True, sb)
+        gf = gf.contiguous()
+        if _colsum_deferred(gf, sb) and gf.shape[0] > 0:
+            du, part = _ops().bias_act_bwd_part(gf, u, b, True)
+            _side_colsum(part, 1, (sb, None, None))
+            db = None
+        else:
+            du, db = _Impl.bias_act_bwd(gf, u, b, True, sb)
         da = _mm_t(du, W) if ctx.needs_input_grad[0] else None
         dW = _wgrad(sW, a.t(), du) if ctx.needs_input_grad[1] else None
         return da, dW, None if sb is not None else db
@@ -390,7 +435,12 @@ class _Linear(torch.autograd.Function):
         a, W, b = ctx.saved_tensors
         sW, sb = ctx.sinks
         gy = gy.contiguous()
-        _, db = _Impl.bias_act_bwd(gy, None, b, False, sb)
+        if _colsum_deferred(gy, sb) and gy.shape[0] > 0:
+            _, part = _ops().bias_act_bwd_part(gy, None, b, False)
+            _side_colsum(part, 1, (sb, None, None))
+            db = None
+        else:
+            _, db = _Impl.bias_act_bwd(gy, None, b, False, sb)
         da = _mm_t(gy, W) if ctx.needs_input_grad[0] else None
         dW = _wgrad(sW, a.t(), gy) if ctx.needs_input_grad[1] else None
         return da, dW, None if sb is not None else db

@@ -47,7 +47,8 @@ def get_data_loaders(args, device, tokenizer=None):
                         args.do_iid, args.num_clients, train=True, download=True, seed=args.seed)
         te = FedPERSONA(tokenizer, -1, args.max_history, 1, args.dataset_dir, "PERSONA",
                         None, train=False)
-    train = PersonaFedLoader(tr, args.num_workers, args.local_batch_size, device, args.seed)
+    train = PersonaFedLoader(tr, args.num_workers, args.local_batch_size, device, args.seed,
+                             workers=getattr(args, "train_dataloader_workers", 0))
     test = PersonaValLoader(te, args.valid_batch_size * args.num_workers, device)
     return train, test
 
@@ -184,6 +185,7 @@ def main(args):
         if args.max_rounds and fed.round_idx >= args.max_rounds:
             break
     profiler.close(fed.timer)
+    train_loader.close()  # the record worker processes, if any
     fed.finalize()
     if args.do_checkpoint:
         save_checkpoint(fed, args, progress)

@@ -38,7 +38,11 @@ def cfg_args(name, N, b):
                     "--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
                     "--virtual_momentum", "0.9", "--k", "50000", "--num_rows", "5",
                     "--num_cols", "500000", "--num_clients", "17568", "--num_workers", str(W),
-                    "--local_batch_size", "8", "--num_candidates", "2", "--max_history", "2"]
+                    "--local_batch_size", "8", "--num_candidates", "2", "--max_history", "2",
+                    # the next rounds' records built in 2 worker processes (the
+                    # reference's DataLoader workers); the timed loop then pulls
+                    # each round from the loader itself
+                    "--train_dataloader_workers", "2"]
     if name == "cifar100_fedavg":
         W = b.clients or 100 * N
         return W, ["--dataset_name", "CIFAR100", "--synthetic", "--model", "ResNet18",
@@ -100,19 +104,32 @@ def main():
     opt = torch.optim.SGD(model.parameters(), lr=0.01 if b.config == "cifar100_fedavg" else 0.05)
     fed = FedModel(model, loss, args, vloss, num_clients=args.num_clients)
     fopt = FedOptimizer(opt, args, fed)
-    batches = []
     it = iter(loader)
-    while len(batches) < b.warmup + b.steps:
-        try:
-            rb = next(it)
-        except StopIteration:
-            it = iter(loader)
-            continue
-        if len(np.unique(rb.client_ids)) == W:
-            batches.append(rb)
-    n_ex = [len(x) for x in batches]
+
+    def next_batch():
+        nonlocal it
+        while True:
+            try:
+                rb = next(it)
+            except StopIteration:
+                it = iter(loader)
+                continue
+            if len(np.unique(rb.client_ids)) == W:
+                return rb
+
+    # with loader workers the rounds are pulled inside the timed loop (the
+    # workers build the next rounds meanwhile); else built lazily from
+    # pre-drawn batches (the records are assembled inside the timed rounds)
+    streamed = getattr(args, "train_dataloader_workers", 0) > 0
+    batches = [] if streamed else [next_batch() for _ in range(b.warmup + b.steps)]
+
+    class _Batches:
+        def __getitem__(self, i):
+            return next_batch() if streamed else batches[i]
+    batches_at = _Batches()
+    n_ex = []
     for i in range(b.warmup):
-        fed(batches[i])
+        fed(batches_at[i])
         fopt.step()
     torch.cuda.synchronize()
     dist.barrier()
@@ -140,7 +157,9 @@ def main():
     host = 0.0  # host time spent enqueueing (the GPU idles when this is the bound)
     for i in range(b.warmup, b.warmup + b.steps):
         h0 = time.perf_counter()
-        out = fed(batches[i])
+        rb = batches_at[i]
+        n_ex.append(len(rb))
+        out = fed(rb)
         fopt.step()
         host += time.perf_counter() - h0
     torch.cuda.synchronize()
@@ -158,13 +177,13 @@ def main():
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
             for i in range(b.warmup, b.warmup + min(3, b.steps)):
-                fed(batches[i])
+                fed(batches_at[i])
                 fopt.step()
             torch.cuda.synchronize()
         if ctx.is_main:
             os.makedirs(tp, exist_ok=True)
             prof.export_chrome_trace(os.path.join(tp, "trace.json"))
-    ex = sum(n_ex[b.warmup:])
+    ex = sum(n_ex)
     if ctx.is_main:
         print(json.dumps({"config": b.config, "n_gpus": N, "value": round(ex / el, 1),
                           "unit": unit, "ms_per_round": round(el / b.steps * 1e3, 2),
@@ -176,6 +195,8 @@ def main():
                           "device_allocs": torch.cuda.memory_stats().get("num_device_alloc", 0) - allocs0,
                           "dtype": args.dtype, "data": "synthetic",
                           "extra_flags": [x for x in b.extra if x != "--"]}), flush=True)
+    if hasattr(loader, "close"):
+        loader.close()
     dist.shutdown()
 
 

@@ -199,3 +199,31 @@ def test_prepare_femnist_from_leaf_json(tmp_path):
     assert len(ds.images_per_client) == 3 and int(np.sum(ds.images_per_client)) == len(y)
     te = FedEMNIST(str(tmp_path), "EMNIST", None, False, None, train=False)
     assert len(te.arrays()[1]) == ds.num_val_images
+
+
+def test_persona_loader_workers_match_inline():
+    """--train_dataloader_workers: the rounds built in forked worker
+    processes (prefetched ahead) are the rounds built inline, tensor for
+    tensor, in the same order."""
+    from commefficient_amd.data.persona_loader import PersonaFedLoader
+    ds = SyntheticPersona(num_personalities=40, num_candidates=2, max_history=2, train=True,
+                          num_clients=40, seed=3)
+    outs = {}
+    for workers in (0, 2):
+        ld = PersonaFedLoader(ds, 4, 3, "cpu", seed=7, workers=workers)
+        rounds = []
+        for i, rb in enumerate(ld):
+            if i >= 5:
+                break
+            pos = np.arange(len(rb))[::-1].copy()  # a permuted selection
+            rounds.append((rb.client_ids.copy(), rb.take(pos)))
+        ld.close()
+        outs[workers] = rounds
+    assert len(outs[0]) == len(outs[2]) == 5
+    for (c0, t0), (c2, t2) in zip(outs[0], outs[2]):
+        assert np.array_equal(c0, c2)
+        for a, b in zip(t0, t2):
+            if torch.is_tensor(a):
+                assert torch.equal(a, b)
+            else:
+                assert np.array_equal(np.asarray(a), np.asarray(b))

@@ -216,6 +216,32 @@ def test_grad_sinks_match_collected_grads_gpu():
 
 
 @pytest.mark.gpu
+def test_side_stream_column_sums_bitwise_gpu(monkeypatch):
+    """The junctions' column sums queued on the weight-gradient side stream
+    (colsum_into after resid_ln_bwd_part / bias_act_bwd_part) give the flat
+    gradient bitwise equal to the in-line sums (same kernel, same order)."""
+    from commefficient_amd.parallel.flat import FlatParams
+    ids, tt = _inputs(device="cuda")
+    res = []
+    for side in (True, False):
+        monkeypatch.setattr(tx, "_COLSUM_SIDE", side)
+        torch.manual_seed(0)
+        m = _tiny_gpt2().to("cuda").eval()
+        flat = FlatParams(m, "cuda")
+        sh = flat.make_bf16_shadow()
+        flat.refresh_shadow()
+        flat.zero_grad()
+        for rep in range(2):
+            with tx.grad_sinks(flat.grad_sink_map()):
+                h = tx.gpt2_hidden(sh.transformer, ids[:, :, rep:], tt[:, :, rep:])
+            h.float().square().mean().backward()
+            tx.join_wgrad_stream()
+        torch.cuda.synchronize()
+        res.append(flat.g.clone())
+    assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
 def test_fedmodel_native_transformer_matches_hf_gpu():
     """One FetchSGD-free (uncompressed) round of a GPT-2 double-heads model
     through FedModel: native junctions + fp32 gradient sinks vs HF modules."""
