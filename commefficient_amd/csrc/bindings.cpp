@@ -1195,6 +1195,80 @@ at::Tensor conv3x3_fwd_impl(const at::Tensor& x, const at::Tensor& w, bool relu,
   return y;
 }
 
+// Grouped 3x3 conv (stride 1, pad 1) on channel-stacked images, batched
+// FedAvg (ops/nn.py _GConv3x3): x [N, G*C, H, W] channels_last bf16, w the
+// [G*kg, 3, 3, C] bf16 image of G per-group weights [kg, C, 3, 3]; output
+// channel group g reads input channels [g C, (g+1) C).  An empty tensor when
+// the halo kernels have no tiling for the shape (the caller falls back).
+at::Tensor conv3x3_fwd_grouped_hip(const at::Tensor& x, const at::Tensor& w, int64_t G) {
+  check_nhwc_bf16(x, "conv3x3_fwd_grouped: x");
+  const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(G >= 1 && GC % G == 0, "conv3x3_fwd_grouped: channels not a multiple of G");
+  const int64_t C = GC / G;
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 4 &&
+                  w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C && w.size(0) % G == 0,
+              "conv3x3_fwd_grouped: w must be contiguous bf16 [G*kg, 3, 3, C]");
+  const int64_t K = w.size(0), kg = K / G;
+  TORCH_CHECK(N * H * W * std::max(GC, K) < (1ll << 31), "conv3x3_fwd_grouped: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, K, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  ConvFwdArgs a;
+  a.x = bf16_ptr(x);
+  a.w = bf16_ptr(w);
+  a.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  a.mask = nullptr;
+  a.addend = nullptr;
+  a.y_pre = nullptr;
+  a.pool_idx = nullptr;
+  a.pool = 0;
+  a.relu = 0;
+  a.P = static_cast<int>(N * H * W);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.x_stride = static_cast<int>(GC);
+  a.kg = static_cast<int>(kg);
+  if (a.P == 0) return y;
+  if (!launch_conv3x3_fwd_grouped(a, cur_stream())) return at::empty({0}, x.options());
+  return y;
+}
+
+// dW [G*kg, C, 3, 3] fp32 of the grouped conv above (dy [N, G*kg, H, W], x
+// [N, G*C, H, W], channels_last bf16); empty when unsupported
+at::Tensor conv3x3_wgrad_grouped_ch_hip(const at::Tensor& dy, const at::Tensor& x, int64_t G) {
+  check_nhwc_bf16(dy, "conv3x3_wgrad_grouped_ch: dy");
+  check_nhwc_bf16(x, "conv3x3_wgrad_grouped_ch: x");
+  const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W && G >= 1 && GC % G == 0 && K % G == 0,
+              "conv3x3_wgrad_grouped_ch: shapes");
+  const int64_t C = GC / G, kg = K / G;
+  if (!conv3x3_wgrad_grouped_supported(static_cast<int>(H), static_cast<int>(W), static_cast<int>(K),
+                                       static_cast<int>(C), static_cast<int>(kg)))
+    return at::empty({0}, x.options().dtype(at::kFloat));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto dw = at::empty({K, C, 3, 3}, x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous));
+  const int P = static_cast<int>(N * H * W);
+  const int splits = conv3x3_wgrad_splits(P, static_cast<int>(H), static_cast<int>(W), static_cast<int>(K),
+                                          static_cast<int>(C));
+  auto slab = at::empty({splits * K * 9 * C}, dw.options());
+  ConvWgradArgs a;
+  a.dy = bf16_ptr(dy);
+  a.x = bf16_ptr(x);
+  a.slab = slab.data_ptr<float>();
+  a.P = P;
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.splits = splits;
+  a.x_stride = static_cast<int>(GC);
+  a.kg = static_cast<int>(kg);
+  if (P > 0) launch_conv3x3_wgrad(a, dw.data_ptr<float>(), 0.f, cur_stream());
+  else dw.zero_();
+  return dw;
+}
+
 at::Tensor conv3x3_fwd_hip(const at::Tensor& x, const at::Tensor& w, bool relu,
                            const c10::optional<at::Tensor>& mask,
                            const c10::optional<at::Tensor>& addend) {
@@ -2292,6 +2366,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
   m.def("wgrad_defer(bool on) -> ()", &commeff::wgrad_defer);
+  m.def("conv3x3_fwd_grouped(Tensor x, Tensor w, int G) -> Tensor");
+  m.def("conv3x3_wgrad_grouped_ch(Tensor dy, Tensor x, int G) -> Tensor");
   m.def("wgrad_flush() -> ()", &commeff::wgrad_flush);
   m.def("conv3x3_wgrad_grouped(Tensor dy, Tensor x, int G, Tensor(a!) dw) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
@@ -2420,6 +2496,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("ghost_bn_bwd", &ghost_bn_bwd_hip);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad_hip);
   m.impl("conv3x3_wgrad_into", &conv3x3_wgrad_into_hip);
+  m.impl("conv3x3_fwd_grouped", &conv3x3_fwd_grouped_hip);
+  m.impl("conv3x3_wgrad_grouped_ch", &conv3x3_wgrad_grouped_ch_hip);
   m.impl("conv3x3_wgrad_grouped", &conv3x3_wgrad_grouped_hip);
   m.impl("conv_weight_prep", &conv_weight_prep_hip);
   m.impl("conv_weight_prep_multi", &conv_weight_prep_multi_hip);

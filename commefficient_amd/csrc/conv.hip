@@ -459,6 +459,9 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   const int KT = 9 * (C >> 6);
   const int s_beg = SPLIT ? half * (KT / 2) : 0, s_end = SPLIT ? s_beg + KT / 2 : KT;
   const int img0 = m0 / HW, h0 = (m0 - img0 * HW) / W;  // first image / row of the tile
+  // grouped (channel-stacked) images: row stride and this tile's channel group
+  const int xs = a.x_stride > 0 ? a.x_stride : C;
+  const int cofs = a.kg > 0 ? (n0 / a.kg) * C : 0;
   const int nimg = a.P / HW;
   const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_conv_zero);
 
@@ -480,7 +483,7 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
         img = img0 + q;
         h = rr - 1;  // -1 on a separator row
       }
-      if (img < nimg && h >= 0 && h < H && w >= 0 && w < W) off = ((img * H + h) * W + w) * C + lc * 8;
+      if (img < nimg && h >= 0 && h < H && w >= 0 && w < W) off = ((img * H + h) * W + w) * xs + cofs + lc * 8;
     }
     win_off[i] = off;
   }
@@ -1358,6 +1361,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
   const int tc = tile % ntc, r = (tile / ntc) % 3, tk = tile / (3 * ntc);
   const int k0 = tk * WBM, c0 = tc * 64, dr = r - 1;
   const int R = BK / W, PW = W + 2, NROW = R * PW;
+  // grouped (channel-stacked) x: row stride and this tile's channel group
+  const int xs = a.x_stride > 0 ? a.x_stride : C;
+  const int cofs = a.kg > 0 ? (k0 / a.kg) * C : 0;
   int pbeg, pend;
   wgrad_split_range(a, split, &pbeg, &pend);
   const int nsteps = pend > pbeg ? (pend - pbeg) / BK : 0;  // whole K-steps (host-checked)
@@ -1383,7 +1389,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
     b_jj[i] = j + dr;
     b_rel[i] = (j + dr) * W + w;
     if (row < NROW && w >= 0 && w < W) b_ok |= 1u << i;
-    b_rel[i] = b_rel[i] * C + c0 + lc * 8;  // element offset from pixel p0's row start
+    b_rel[i] = b_rel[i] * xs + cofs + c0 + lc * 8;  // element offset from pixel p0's row start
   }
 
   auto issue = [&](int stage, int p0) __attribute__((always_inline)) {
@@ -1394,12 +1400,12 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
       a_ptr[i] += static_cast<uint64_t>(BK) * K * 2;
     }
     const int h0 = (p0 % HW) / W;  // first image row of the step (uniform)
-    const uint16_t* xs = a.x + static_cast<size_t>(p0) * C;
+    const uint16_t* xrow = a.x + static_cast<size_t>(p0) * xs;
 #pragma unroll
     for (int i = 0; i < BLD; ++i) {
       if (i < 2 || i * 256 + wid * 64 < NROW * 8) {
         const bool ok = ((b_ok >> i) & 1u) && static_cast<unsigned>(h0 + b_jj[i]) < static_cast<unsigned>(H);
-        glds16(ok ? reinterpret_cast<const void*>(xs + b_rel[i]) : reinterpret_cast<const void*>(zero),
+        glds16(ok ? reinterpret_cast<const void*>(xrow + b_rel[i]) : reinterpret_cast<const void*>(zero),
                base + A_BYTES + i * 4096);
       }
     }
@@ -1719,6 +1725,7 @@ bool wgrad_halo(int H, int W, int K, int C) {
          (BK / W) * (W + 2) <= kHaloWRows;
 }
 
+
 // (k, c) x tap-group tiles of one wgrad: 64-channel inputs pair taps (PAIR)
 int wgrad_tiles(int K, int C) {
   if (wgrad_wide(K, C)) return (K / 256) * (C == 128 ? 5 : 9 * (C / 256));
@@ -1759,6 +1766,12 @@ void launch_wgrad(const ConvWgradArgs& a, hipStream_t stream) {
 }
 
 }  // namespace
+
+// channel-stacked grouped wgrad: the halo kernel with its tile's input-channel
+// group (output tiles of WBM = 128 rows never straddle a group)
+bool conv3x3_wgrad_grouped_supported(int H, int W, int K, int C, int kg) {
+  return kg > 0 && kg % WBM == 0 && K % kg == 0 && C % 64 == 0 && wgrad_halo(H, W, K, C);
+}
 
 static int wgrad_slots();
 
@@ -1856,6 +1869,29 @@ void launch_fwd_pipe(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t strea
   const int ntiles = ((a.P + 255) / 256) * (a.K / BN);
   const int grid = ntiles < cu_count() ? ntiles : cu_count();
   COMMEFF_LAUNCH((conv_fwd_pipe_kernel<POOL, BN>), dim3(grid), dim3(512), lds, stream, a, hg, ntiles);
+}
+
+// Grouped conv on channel-stacked images (a.kg, a.x_stride set): the halo
+// kernels only, no fused epilogue.  Returns false when the geometry has no
+// halo tiling (the caller falls back to a stock grouped convolution).
+bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream) {
+  if (a.kg <= 0 || a.pool != 0 || a.relu != 0 || a.mask != nullptr || a.addend != nullptr ||
+      a.unpool_idx != nullptr || a.dual_mask != nullptr || a.C % 64 != 0 || a.K % a.kg != 0)
+    return false;
+  a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
+  a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
+  a.ablate = 0;
+  HaloGeom hg;
+  if (a.kg % 128 == 0) {
+    if (halo_geom(a.H, a.W, a.K, 256, &hg)) { launch_fwd_halo<256, false>(a, hg, stream); return true; }
+    if (halo_geom(a.H, a.W, a.K, 128, &hg)) { launch_fwd_halo<128, false>(a, hg, stream); return true; }
+    return false;
+  }
+  if (a.kg % 64 == 0 && halo_geom(a.H, a.W, a.K, 256, &hg, 64)) {
+    launch_fwd_halo<256, false, false, 64>(a, hg, stream);
+    return true;
+  }
+  return false;
 }
 
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {

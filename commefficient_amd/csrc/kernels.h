@@ -265,10 +265,21 @@ struct ConvFwdArgs {
   // no weight-tile loads after the first two K-steps, bit 1 = no window reload
   // per channel block, bit 2 = no per-K-step wait / barrier, bit 3 = no epilogue
   int ablate = 0;
+  // grouped conv on channel-stacked images (batched FedAvg, ops/nn.py
+  // _GConv3x3): x rows hold x_stride channels, output channels come in groups
+  // of kg that read only input channels [g C, (g+1) C) (C = a.C, per group) and
+  // weight rows g kg .. (g+1) kg of a [G kg][3][3][C] image.  0 = ungrouped.
+  int x_stride = 0;
+  int kg = 0;
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]
   const uint16_t* x;   // [P, C]
+  // grouped (channel-stacked) wgrad: x rows of x_stride channels, dy rows of
+  // K (= G kg) channels; output channel k reads input channels [g C, (g+1) C)
+  // of its group g = k / kg (C = per-group channels).  0 = ungrouped.
+  int x_stride = 0;
+  int kg = 0;
   float* slab;         // [splits, K, 9, C] scratch
   int P, H, W, C, K;
   int splits;
@@ -286,6 +297,10 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
+// grouped convs on channel-stacked images (a.kg / a.x_stride set): false when
+// the geometry has no halo tiling (the caller falls back)
+bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream);
+bool conv3x3_wgrad_grouped_supported(int H, int W, int K, int C, int kg);
 // split-K slabs only; their reductions batched across convs by launch_wgrad_reduce_batch
 void launch_conv3x3_wgrad_slabs(ConvWgradArgs a, hipStream_t stream);
 constexpr int kWgradBatch = 16;

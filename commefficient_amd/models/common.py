@@ -8,6 +8,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import grouped as _grouped
+from ..ops import nn as _nn
 from ..ops.nn import (_AffineGrouped, conv1x1_passthrough, conv2d_grouped, conv2d_native,
                       conv2d_native_kind, ghost_batch_norm, ghost_bn_native_ok, linear_grouped,
                       max_pool2d, stock_active)
@@ -179,6 +180,14 @@ class NativeConv2d(nn.Conv2d):
     (MIOpen) convolution."""
 
     def forward(self, x):
+        if (_nn.vmap_native_active() and self.bias is None and self.groups == 1
+                and self.in_channels % 64 == 0 and self.out_channels % 64 == 0
+                and tuple(self.kernel_size) == (3, 3) and tuple(self.stride) == (1, 1)
+                and tuple(self.padding) == (1, 1) and tuple(self.dilation) == (1, 1)
+                and self.padding_mode == "zeros"):
+            # batched FedAvg under vmap: clients stacked along channels on the
+            # grouped native kernels (ops/nn.py vmap_native_convs)
+            return _nn.gconv3x3(x, self.weight)
         gg = _grouped.active() if self.weight.requires_grad else None
         if gg is not None and gg.view(self.weight) is None:
             gg = None

@@ -1290,3 +1290,163 @@ class _AffineGrouped(torch.autograd.Function):
         ctx.gg.view(w).add_(gw)
         ctx.gg.view(b).add_(gb)
         return gy * weight.view(shape).to(gy.dtype), None, None, None
+
+
+# ------------------------------------------------------------------------
+# Batched FedAvg: per-client 3x3 convolutions on native kernels under vmap.
+#
+# The lockstep local SGD of a rank's G clients (parallel/fed_model.py
+# _fedavg_batched) runs ONE torch.func.vmap(grad(loss)) per local step over a
+# [G, d] stack of client weights; the model's ops take their stock PyTorch
+# form there (stock_ops), and vmap turns every conv into a grouped MIOpen
+# convolution (column images + GEMMs: ~90 of the 169 ms of a ResNet-18
+# CIFAR-100 round of 100 clients x 5 local steps, profiles/r4_experiments.md).
+# Inside ``vmap_native_convs()`` the stride-1 3x3 convs instead go through
+# _GConv3x3, whose vmap rule stacks the clients along channels -- x [n, G C,
+# H, W], weight [G kg, C, 3, 3] -- and runs the grouped halo kernels
+# (csrc/conv.hip: each output-channel tile reads its own group's input
+# channels and weight rows): forward, input gradient (the same kernel on the
+# per-group flipped weights) and, where the halo wgrad tiles fit, the weight
+# gradient; other shapes fall back to the grouped stock convolution.
+_VMAP_NATIVE = [False]
+
+
+class vmap_native_convs:
+    """Opt-in (COMMEFF_GCONV=1): measured 174.8 vs 165.8 ms per ResNet-18
+    CIFAR-100 FedAvg round (100 clients x 5 local steps) -- the grouped halo
+    kernels replace ~45 ms of MIOpen column-image convolutions, but the round
+    is bound by vmap's host time (GPU idle ~40 ms/round), the stock
+    BatchNorm / elementwise work between the convs, the layout copies into the
+    channel-stacked form, and the weight gradients of the 64-channel and
+    8x8 / 4x4 layers, which have no grouped halo wgrad tiling yet and take the
+    grouped stock path (profiles/r4_experiments.md)."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = bool(enabled) and os.environ.get("COMMEFF_GCONV", "0") == "1"
+
+    def __enter__(self):
+        self.prev = _VMAP_NATIVE[0]
+        _VMAP_NATIVE[0] = self.enabled
+        return self
+
+    def __exit__(self, *exc):
+        _VMAP_NATIVE[0] = self.prev
+        return False
+
+
+def vmap_native_active() -> bool:
+    return _VMAP_NATIVE[0]
+
+
+def _bstack(t, bdim, B):
+    return t.movedim(bdim, 0) if bdim is not None else t.unsqueeze(0).expand(B, *t.shape)
+
+
+def _chan_stack(X):
+    """[B, n, C, H, W] -> [n, B C, H, W] with channels_last memory (clients
+    along channels): ONE copy into the kernels' [n, H, W, B C] layout."""
+    B, n, C, H, W = X.shape
+    return X.permute(1, 3, 4, 0, 2).contiguous().view(n, H, W, B * C).permute(0, 3, 1, 2)
+
+
+def _chan_unstack(y, B):
+    """[n, B K, H, W] (channels_last) -> [B, n, K, H, W] contiguous: one copy,
+    so the stock ops between the convs (BatchNorm, ReLU, residual adds) run on
+    dense per-client tensors instead of strided ones (their non-vectorised
+    kernels cost more than the copy, r4 log)."""
+    n, BK, H, W = y.shape
+    return y.view(n, B, BK // B, H, W).transpose(0, 1).contiguous()
+
+
+def _gconv_native_ok(x, G, C, kg) -> bool:
+    return (x.is_cuda and _CONV_BACKEND[0] == "native" and C % 64 == 0 and kg % 64 == 0)
+
+
+def _gconv_fwd(x, w, G):
+    """y = grouped 3x3 conv (stride 1, pad 1) of x [n, G C, H, W] with w
+    [G kg, C, 3, 3]: the grouped native kernel or the stock grouped conv."""
+    C, kg = x.shape[1] // G, w.shape[0] // G
+    if _gconv_native_ok(x, G, C, kg):
+        xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wf = w.detach().to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()  # [G kg, 3, 3, C]
+        y = _ops().conv3x3_fwd_grouped(xb, wf, G)
+        if y.numel() or xb.numel() == 0:
+            return y
+    return F.conv2d(x, w.to(x.dtype), padding=1, groups=G)
+
+
+class _GConv3x3Bwd(torch.autograd.Function):
+    """(dx, dw) of _GConv3x3 (its own Function so vmap can stack it too)."""
+
+    @staticmethod
+    def forward(gy, x, w, G):
+        C, kg = x.shape[1] // G, w.shape[0] // G
+        if _gconv_native_ok(gy, G, C, kg):
+            gyb = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            # per-group flipped, transposed weights [G C, 3, 3, kg]: the bf16
+            # cast, then one flip of the permuted view (a contiguous result)
+            wt = (w.detach().to(torch.bfloat16).view(G, kg, C, 3, 3).permute(0, 2, 3, 4, 1)
+                  .flip(2, 3).reshape(G * C, 3, 3, kg))
+            gx = _ops().conv3x3_fwd_grouped(gyb, wt, G)
+            if gx.numel() == 0 and gyb.numel():
+                gx = torch.nn.grad.conv2d_input(x.shape, w.to(gy.dtype), gy, padding=1, groups=G)
+            gw = _ops().conv3x3_wgrad_grouped_ch(gyb, xb, G)
+            if gw.numel() == 0 and xb.numel():
+                gw = torch.nn.grad.conv2d_weight(xb, w.shape, gyb, padding=1, groups=G)
+            return gx.to(x.dtype), gw.to(w.dtype)
+        gx = torch.nn.grad.conv2d_input(x.shape, w.to(gy.dtype), gy, padding=1, groups=G)
+        gw = torch.nn.grad.conv2d_weight(x.to(gy.dtype), w.shape, gy, padding=1, groups=G)
+        return gx.to(x.dtype), gw.to(w.dtype)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        pass
+
+    @staticmethod
+    def backward(ctx, ggx, ggw):
+        raise RuntimeError("_GConv3x3: no double backward")
+
+    @staticmethod
+    def vmap(info, in_dims, gy, x, w, G):
+        B = info.batch_size
+        bg, bx, bw, _ = in_dims
+        GY, X, Wt = _bstack(gy, bg, B), _bstack(x, bx, B), _bstack(w, bw, B)
+        gx, gw = _GConv3x3Bwd.apply(_chan_stack(GY), _chan_stack(X),
+                                    Wt.reshape(B * Wt.shape[1], *Wt.shape[2:]), B * G)
+        return (_chan_unstack(gx, B), gw.view(B, -1, *gw.shape[1:])), (0, 0)
+
+
+class _GConv3x3(torch.autograd.Function):
+    """Grouped stride-1 3x3 conv (G groups) whose vmap rule folds the vmapped
+    dimension into the groups (clients stacked along channels)."""
+
+    @staticmethod
+    def forward(x, w, G):
+        return _gconv_fwd(x, w, G)
+
+    @staticmethod
+    def setup_context(ctx, inputs, output):
+        x, w, G = inputs
+        ctx.save_for_backward(x, w)
+        ctx.G = G
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx, gw = _GConv3x3Bwd.apply(gy, x, w, ctx.G)
+        return gx, gw, None
+
+    @staticmethod
+    def vmap(info, in_dims, x, w, G):
+        bx, bw, _ = in_dims
+        B = info.batch_size
+        X, Wt = _bstack(x, bx, B), _bstack(w, bw, B)
+        y = _GConv3x3.apply(_chan_stack(X), Wt.reshape(B * Wt.shape[1], *Wt.shape[2:]), B * G)
+        return _chan_unstack(y, B), 0
+
+
+def gconv3x3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """A stride-1, pad-1, bias-free 3x3 conv that becomes the grouped native
+    kernel when vmapped over clients (see vmap_native_convs)."""
+    return _GConv3x3.apply(x, weight, 1)

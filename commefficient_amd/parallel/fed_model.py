@@ -1144,7 +1144,7 @@ class FedModel:
         reference's worker model accumulated them client after client)."""
         from torch.func import grad, vmap
         from torch.nn.utils.stateless import _reparametrize_module
-        from ..ops.nn import stock_ops
+        from ..ops.nn import stock_ops, vmap_native_convs
         a = self.args
         n = int(counts[my_slots[0]])
         bs = a.fedavg_batch_size if a.fedavg_batch_size != -1 else n
@@ -1186,7 +1186,7 @@ class FedModel:
                     for k, b in bufs_init.items()}
             step = 0
             ls, ms = [], None
-            with stock_ops(), self._autocast(cache=False):
+            with stock_ops(), vmap_native_convs(), self._autocast(cache=False):
                 for _ in range(a.num_fedavg_epochs):
                     for s0 in range(0, n, bs):
                         s1 = min(n, s0 + bs)

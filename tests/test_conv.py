@@ -750,3 +750,50 @@ def test_persistent_halo_kernel_bench_batches(N, C, H, K, epi):
         return
     y = ops.conv3x3_fwd(x, wf, epi == "relu")
     _close(y, ref.relu() if epi == "relu" else ref)
+
+
+@pytest.mark.parametrize("G,C,kg,H,n", [(3, 64, 64, 32, 5), (3, 128, 128, 16, 5), (2, 256, 256, 8, 5),
+                                          (3, 256, 256, 4, 5), (2, 64, 128, 16, 3)])
+def test_grouped_channel_stacked_conv_matches_fp32(G, C, kg, H, n):
+    """csrc/conv.hip grouped halo kernels on channel-stacked clients (batched
+    FedAvg, ops/nn.py _GConv3x3): forward, input gradient and weight gradient
+    vs the fp32 grouped convolution of the same bf16 operands."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = _nhwc(torch.randn(n, G * C, H, H, device="cuda", generator=g).to(torch.bfloat16))
+    w = torch.randn(G * kg, C, 3, 3, device="cuda", generator=g) * (9 * C) ** -0.5
+    wb = w.to(torch.bfloat16)
+    y = cnn._gconv_fwd(x, w, G)
+    ref = F.conv2d(x.float(), wb.float(), padding=1, groups=G)
+    assert y.shape == ref.shape
+    _close(y, ref)
+    gy = _nhwc(torch.randn(ref.shape, device="cuda", generator=g).to(torch.bfloat16))
+    gx, gw = cnn._GConv3x3Bwd.apply(gy, x, w, G)
+    rgx = torch.nn.grad.conv2d_input(x.shape, wb.float(), gy.float(), padding=1, groups=G)
+    rgw = torch.nn.grad.conv2d_weight(x.float(), w.shape, gy.float(), padding=1, groups=G)
+    _close(gx, rgx)
+    # (kg % 128 != 0 or no halo wgrad tiling: the stock grouped wgrad, whose
+    # bf16 output is rounded: 2^-8 relative)
+    _close(gw, rgw, rel=1e-3 if (kg % 128 == 0 and H >= 16) else 1e-2)
+
+
+def test_grouped_conv_vmap_grad_matches_per_client(monkeypatch):
+    """vmap(grad) over clients through the grouped native kernels == each
+    client's own gradient (bf16 operands, fp32 accumulation)."""
+    from torch.func import grad, vmap
+    g = torch.Generator(device="cuda").manual_seed(6)
+    B, n, C, K = 4, 5, 128, 128
+    x = torch.randn(B, n, C, 16, 16, device="cuda", generator=g).to(torch.bfloat16)
+    w = torch.randn(B, K, C, 3, 3, device="cuda", generator=g) * (9 * C) ** -0.5
+
+    def loss(w1, x1):
+        return cnn.gconv3x3(x1, w1).float().square().sum()
+
+    monkeypatch.setenv("COMMEFF_GCONV", "1")
+    with cnn.vmap_native_convs() as ctx:
+        assert ctx.enabled
+        gw = vmap(grad(loss))(w, x)
+    for i in range(B):
+        wi = w[i].to(torch.bfloat16).float().requires_grad_()
+        ref = torch.autograd.grad(F.conv2d(x[i].float(), wi, padding=1).square().sum(), wi)[0]
+        rel = (gw[i] - ref).norm() / ref.norm()
+        assert rel < 2e-2, (i, float(rel))
