@@ -2207,28 +2207,31 @@ at::Tensor heads_to_rows_hip(at::TensorList srcs, const c10::optional<at::Tensor
   return out;
 }
 
-// sink (fp32 [M, N], row-contiguous) += a^T b for a [T, M], b [T, N] bf16
-// with unit column stride (gemm_tn.hip)
-void gemm_tn_acc_hip(at::Tensor sink, const at::Tensor& a, const at::Tensor& b) {
-  TORCH_CHECK(sink.scalar_type() == at::kFloat && sink.dim() == 2 && sink.stride(1) == 1,
-              "gemm_tn_acc: sink must be fp32 [M, N] with unit column stride");
+// sink_g (fp32 [M, N], row-contiguous) += a_g^T b_g for each of G groups of
+// T rows: a [G T, M], b [G T, N] bf16 with unit column stride (gemm_tn.hip)
+// slab_only: C is unused; returns the [G * splits, M, N] fp32 split products
+// unsummed (a column-image weight gradient's parts, summed and permuted by
+// wgrad_rsc_add)
+static at::Tensor gemm_tn_run(float* sink, int64_t ldc, int64_t cg, const at::Tensor& a, const at::Tensor& b, int64_t G,
+                       bool slab_only = false) {
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
                   b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1 && a.size(0) == b.size(0),
               "gemm_tn_acc: a [T, M], b [T, N] bf16 with unit column stride");
-  const int64_t M = a.size(1), N = b.size(1), T = a.size(0);
-  TORCH_CHECK(sink.size(0) == M && sink.size(1) == N, "gemm_tn_acc: sink shape");
-  TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+  TORCH_CHECK(G >= 1 && a.size(0) % G == 0, "gemm_tn_acc: G must divide the rows");
+  const int64_t M = a.size(1), N = b.size(1), T = a.size(0) / G;
+  TORCH_CHECK(M % 64 == 0 && N % 64 == 0 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(sink.data_ptr()) % 16 == 0 && sink.stride(0) % 4 == 0,
-              "gemm_tn_acc: M, N multiples of 256, 16-byte aligned rows");
-  TORCH_CHECK(T < (1ll << 31) && M * N < (1ll << 31), "gemm_tn_acc: size");
-  if (T == 0) return;
+                  reinterpret_cast<uintptr_t>(sink) % 16 == 0 && ldc % 4 == 0 && cg % 4 == 0,
+              "gemm_tn_acc: M, N multiples of 64, 16-byte aligned rows");
+  TORCH_CHECK(a.size(0) < (1ll << 31) && M * N < (1ll << 31), "gemm_tn_acc: size");
+  if (T == 0) return at::Tensor();
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  int cus = 256;
-  {
+  static int cus = 0;
+  if (cus == 0) {
     hipDeviceProp_t prop;
     int dev = 0;
+    cus = 256;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
       cus = prop.multiProcessorCount;
   }
@@ -2237,18 +2240,50 @@ void gemm_tn_acc_hip(at::Tensor sink, const at::Tensor& a, const at::Tensor& b) 
   g.lda = a.stride(0);
   g.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
   g.ldb = b.stride(0);
-  g.C = sink.data_ptr<float>();
-  g.ldc = sink.stride(0);
+  g.C = sink;
+  g.ldc = ldc;
   g.M = static_cast<int>(M);
   g.N = static_cast<int>(N);
   g.T = static_cast<int>(T);
-  g.splits = gemm_tn_splits(g.M, g.N, g.T, cus);
+  g.G = static_cast<int>(G);
+  g.cg = cg;
+  // ~ one block per CU over all groups
+  g.splits = gemm_tn_splits(g.M, g.N, g.T, cus / g.G > 0 ? cus / g.G : 1);
+  g.slab_only = slab_only ? 1 : 0;
   at::Tensor slab;
-  if (g.splits > 1) {
-    slab = at::empty({static_cast<int64_t>(g.splits) * M * N}, sink.options());
+  if (g.splits > 1 || slab_only) {
+    slab = at::empty({G * g.splits, M, N}, a.options().dtype(at::kFloat));
     g.slab = slab.data_ptr<float>();
   }
   launch_gemm_tn_acc(g, cur_stream());
+  return slab;
+}
+
+void gemm_tn_acc_hip(at::Tensor sink, const at::Tensor& a, const at::Tensor& b) {
+  TORCH_CHECK(sink.scalar_type() == at::kFloat && sink.dim() == 2 && sink.stride(1) == 1 && sink.is_cuda(),
+              "gemm_tn_acc: sink must be fp32 [M, N] with unit column stride");
+  TORCH_CHECK(sink.size(0) == a.size(1) && sink.size(1) == b.size(1), "gemm_tn_acc: sink shape");
+  gemm_tn_run(sink.data_ptr<float>(), sink.stride(0), 0, a, b, 1);
+}
+
+// grouped: sink [G, M, N] (unit column stride), a [G T, M], b [G T, N]
+void gemm_tn_acc_grouped_hip(at::Tensor sink, const at::Tensor& a, const at::Tensor& b, int64_t G) {
+  TORCH_CHECK(sink.scalar_type() == at::kFloat && sink.dim() == 3 && sink.stride(2) == 1 && sink.is_cuda(),
+              "gemm_tn_acc_grouped: sink must be fp32 [G, M, N] with unit column stride");
+  TORCH_CHECK(sink.size(0) == G && sink.size(1) == a.size(1) && sink.size(2) == b.size(1),
+              "gemm_tn_acc_grouped: sink shape");
+  gemm_tn_run(sink.data_ptr<float>(), sink.stride(1), sink.stride(0), a, b, G);
+}
+
+// (parts [G * S, M, N] fp32, S): the S split-K products of each group's
+// a_g^T b_g, unsummed
+std::tuple<at::Tensor, int64_t> gemm_tn_parts_hip(const at::Tensor& a, const at::Tensor& b, int64_t G) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm_tn_parts: device tensors");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  // slab-only: the sink argument is never written (a's aligned address passes the checks)
+  auto parts = gemm_tn_run(reinterpret_cast<float*>(a.data_ptr()), 4, 0, a, b, G, true);
+  TORCH_CHECK(parts.defined(), "gemm_tn_parts: empty operands");
+  return {parts, parts.size(0) / G};
 }
 
 void check_seqs(const at::Tensor& start, const at::Tensor& len) {
@@ -2435,6 +2470,8 @@ TORCH_LIBRARY(commeff, m) {
         "float p_drop, int seed, int max_len) -> Tensor");
   m.def("heads_to_rows(Tensor[] srcs, Tensor? tok, int Mr) -> Tensor");
   m.def("gemm_tn_acc(Tensor(a!) sink, Tensor a, Tensor b) -> ()");
+  m.def("gemm_tn_acc_grouped(Tensor(a!) sink, Tensor a, Tensor b, int G) -> ()");
+  m.def("gemm_tn_parts(Tensor a, Tensor b, int G) -> (Tensor, int)");
   m.def("im2col(Tensor x, int R, int S, int stride, int pad, int Kc) -> Tensor");
   m.def("col2im(Tensor gcol, int N, int H, int W, int C, int R, int S, int stride, int pad) -> Tensor");
   m.def("conv_weight_rsc(Tensor w, int Kc) -> Tensor");
@@ -2537,6 +2574,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("colsum_into", &colsum_into_hip);
   m.impl("pad_rows", &pad_rows_hip);
   m.impl("gemm_tn_acc", &gemm_tn_acc_hip);
+  m.impl("gemm_tn_acc_grouped", &gemm_tn_acc_grouped_hip);
+  m.impl("gemm_tn_parts", &gemm_tn_parts_hip);
   m.impl("attn_fwd", &attn_fwd_hip);
   m.impl("attn_bwd", &attn_bwd_hip);
   m.impl("heads_to_rows", &heads_to_rows_hip);

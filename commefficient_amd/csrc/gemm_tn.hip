@@ -42,33 +42,43 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntn = a.N / 256;
-  const int ntiles = (a.M / 256) * ntn;
-  const int tile = bid % ntiles, split = bid / ntiles;
+  // M, N multiples of 64: a partial edge tile loads zeros past M / N and
+  // stores only its valid part
+  const int ntn = (a.N + 255) / 256;
+  const int ntiles = ((a.M + 255) / 256) * ntn;
+  const int per_g = ntiles * a.splits;
+  const int grp = bid / per_g, rem = bid - grp * per_g;
+  const int tile = rem % ntiles, split = rem / ntiles;
   const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
   const int pbeg = split * a.steps_per_split * GBK;
   const int pend = min(a.T, pbeg + a.steps_per_split * GBK);
+  // group grp: its own T operand rows and its own C (grouped weight gradients)
+  const uint16_t* __restrict__ gA = a.A + static_cast<int64_t>(grp) * a.T * a.lda;
+  const uint16_t* __restrict__ gB = a.B + static_cast<int64_t>(grp) * a.T * a.ldb;
   const int nsteps = pend > pbeg ? (pend - pbeg + GBK - 1) / GBK : 0;
   const uint64_t zero = reinterpret_cast<uint64_t>(g_gemm_zero);
 
   // piece i (0..3) of this thread: image half i >> 1, chunk slot (i & 1) * 512 + tid
   uint64_t a_ptr[4], b_ptr[4];
   int p_row[4];
+  bool a_in[4], b_in[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int h = i >> 1, sp = (i & 1) * 512 + tid;
     const int row = sp >> 4, lc = (sp & 15) ^ sw_tr256(row);
     p_row[i] = pbeg + row;
-    a_ptr[i] = reinterpret_cast<uint64_t>(a.A + static_cast<int64_t>(pbeg + row) * a.lda + m0 + h * 128 + lc * 8);
-    b_ptr[i] = reinterpret_cast<uint64_t>(a.B + static_cast<int64_t>(pbeg + row) * a.ldb + n0 + h * 128 + lc * 8);
+    a_in[i] = m0 + h * 128 + lc * 8 < a.M;
+    b_in[i] = n0 + h * 128 + lc * 8 < a.N;
+    a_ptr[i] = reinterpret_cast<uint64_t>(gA + static_cast<int64_t>(pbeg + row) * a.lda + m0 + h * 128 + lc * 8);
+    b_ptr[i] = reinterpret_cast<uint64_t>(gB + static_cast<int64_t>(pbeg + row) * a.ldb + n0 + h * 128 + lc * 8);
   }
   auto issue = [&](int stage) __attribute__((always_inline)) {
     unsigned char* base = smem + stage * GSTAGE + wid * 1024;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool ok = p_row[i] < pend;  // token rows past the split: zero page
-      gl16(reinterpret_cast<const void*>(ok ? a_ptr[i] : zero), base + (i >> 1) * GHALF + (i & 1) * 8192);
-      gl16(reinterpret_cast<const void*>(ok ? b_ptr[i] : zero),
+      gl16(reinterpret_cast<const void*>(ok && a_in[i] ? a_ptr[i] : zero), base + (i >> 1) * GHALF + (i & 1) * 8192);
+      gl16(reinterpret_cast<const void*>(ok && b_in[i] ? b_ptr[i] : zero),
            base + 2 * GHALF + (i >> 1) * GHALF + (i & 1) * 8192);
       p_row[i] += GBK;
       a_ptr[i] += static_cast<uint64_t>(GBK) * a.lda * 2;
@@ -134,14 +144,16 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
   // C row m (lanes: 32 consecutive n) -- one split: accumulate into C; else
   // this split's slab [M][N]
   const int hi = lane >> 5, lr = lane & 31;
-  const bool direct = a.splits == 1;
-  float* out = direct ? a.C : a.slab + static_cast<size_t>(split) * a.M * a.N;
+  const bool direct = a.splits == 1 && !a.slab_only;
+  float* out = direct ? a.C + static_cast<int64_t>(grp) * a.cg
+                      : a.slab + static_cast<size_t>(grp * a.splits + split) * a.M * a.N;
   const int64_t ld = direct ? a.ldc : a.N;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       const int n = n0 + wc * 128 + ni * 32 + lr;
+      if (n >= a.N || m0 + wr * 64 + mi * 32 >= a.M) continue;  // padding of an edge tile
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
@@ -152,25 +164,28 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
     }
 }
 
-// C[m][n] += sum over s of slab[s][m][n], s in order (float4 per thread)
+// C_g[m][n] += sum over s of slab[g][s][m][n], s in order (float4 per thread)
 __global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__ C, int64_t ldc,
                                                              const float* __restrict__ slab, int M,
-                                                             int N, int splits) {
-  const int64_t n4 = static_cast<int64_t>(M) * N / 4;
+                                                             int N, int splits, int G, int64_t cg) {
   const int64_t plane = static_cast<int64_t>(M) * N;
+  const int64_t n4 = G * plane / 4;
   for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < n4;
        q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t e = q * 4;
+    const int64_t eg = q * 4;
+    const int g = static_cast<int>(eg / plane);
+    const int64_t e = eg - g * plane;
     const int m = static_cast<int>(e / N), n = static_cast<int>(e - static_cast<int64_t>(m) * N);
-    float4 s = *reinterpret_cast<const float4*>(slab + e);
+    const float* sg = slab + static_cast<int64_t>(g) * splits * plane + e;
+    float4 s = *reinterpret_cast<const float4*>(sg);
     for (int k = 1; k < splits; ++k) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + k * plane + e);
+      const float4 v = *reinterpret_cast<const float4*>(sg + k * plane);
       s.x += v.x;
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
     }
-    float4* c = reinterpret_cast<float4*>(C + static_cast<int64_t>(m) * ldc + n);
+    float4* c = reinterpret_cast<float4*>(C + g * cg + static_cast<int64_t>(m) * ldc + n);
     float4 cv = *c;
     cv.x += s.x;
     cv.y += s.y;
@@ -183,7 +198,7 @@ __global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__
 }  // namespace
 
 int gemm_tn_splits(int M, int N, int T, int cus) {
-  const int tiles = (M / 256) * (N / 256);
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int steps = (T + GBK - 1) / GBK;
   int s = (cus + tiles - 1) / tiles;  // ~ one block per CU
   const int max_s = steps / 4 > 0 ? steps / 4 : 1;  // >= 4 K-steps per split
@@ -202,15 +217,16 @@ void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream) {
   }
   const int steps = (a.T + GBK - 1) / GBK;
   a.steps_per_split = (steps + a.splits - 1) / a.splits;
-  const int tiles = (a.M / 256) * (a.N / 256);
-  COMMEFF_LAUNCH(gemm_tn_acc_kernel, dim3(static_cast<uint32_t>(tiles * a.splits)), dim3(512),
+  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  if (a.G < 1) a.G = 1;
+  COMMEFF_LAUNCH(gemm_tn_acc_kernel, dim3(static_cast<uint32_t>(tiles * a.splits * a.G)), dim3(512),
                      kGemmLds, stream, a);
-  if (a.splits > 1) {
-    const int64_t n4 = static_cast<int64_t>(a.M) * a.N / 4;
+  if (a.splits > 1 && !a.slab_only) {
+    const int64_t n4 = static_cast<int64_t>(a.G) * a.M * a.N / 4;
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     COMMEFF_LAUNCH(gemm_tn_reduce_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
-                       a.C, a.ldc, a.slab, a.M, a.N, a.splits);
+                       a.C, a.ldc, a.slab, a.M, a.N, a.splits, a.G, a.cg);
   }
 }
 

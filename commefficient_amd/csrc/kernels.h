@@ -538,9 +538,12 @@ struct GemmTnArgs {
   float* C;
   int64_t ldc;
   float* slab;
-  int M, N, T;
+  int M, N, T;  // T: rows of each group
   int splits;
   int steps_per_split;  // set by the launcher
+  int G = 1;            // groups: A / B rows [g T, (g + 1) T) -> C + g cg
+  int64_t cg = 0;
+  int slab_only = 0;    // write every split's product to the slabs, no reduction into C
 };
 int gemm_tn_splits(int M, int N, int T, int cus);
 void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream);

@@ -845,11 +845,46 @@ def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
     P, K = g2d.shape
     C = x2d.shape[1]
     Pg = P // G
+    if _TN_PARTS and _wgrad_tn_ok(g2d, x2d, None, G, pad=True):
+        # native split-K TN GEMM writing its split products (csrc/gemm_tn.hip)
+        parts, S = _ops().gemm_tn_parts(g2d, x2d, G)
+        return parts, int(S)
     S = _wgrad_splits(Pg, K, C, G)
     if G * S == 1:
         return torch.mm(g2d.t(), x2d, out_dtype=torch.float32).unsqueeze(0), 1
     return torch.bmm(g2d.view(G * S, Pg // S, K).transpose(1, 2), x2d.view(G * S, Pg // S, C),
                      out_dtype=torch.float32), S
+
+
+# column-image weight-gradient parts on the native TN GEMM: measured slower
+# than hipBLASLt's batched GEMM at the ResNet-101 shapes (1.2-1.9x,
+# scripts/bench_wgrad_tn.py), opt-in
+_TN_PARTS = os.environ.get("COMMEFF_WGRAD_TN_PARTS", "0") == "1"
+# 1x1 weight gradients with both sides multiples of 256 on the native TN GEMM
+# (default; COMMEFF_WGRAD_TN=0: hipBLASLt batched GEMM + split reduction)
+_TN_1X1 = os.environ.get("COMMEFF_WGRAD_TN", "1") != "0"
+
+
+def _wgrad_tn_ok(g2d: torch.Tensor, x2d: torch.Tensor, into, G: int, pad: bool = False) -> bool:
+    """csrc/gemm_tn.hip serves the weight gradient: both sides multiples of
+    256 (its tile; with ``pad`` multiples of 64, the edge tiles zero-padded --
+    measured slower than hipBLASLt's 64-wide tiles at the ResNet-101 64 / 128
+    channel shapes), bf16 rows with unit column stride, 16-byte aligned;
+    ``into`` fp32 with 16-byte aligned rows (or absent)."""
+    P, K = g2d.shape
+    C = x2d.shape[1]
+    q = 64 if pad else 256
+    if not (_GEMM_NATIVE[0] and g2d.is_cuda and K % q == 0 and C % q == 0 and P % G == 0
+            and g2d.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16
+            and g2d.stride(1) == 1 and x2d.stride(1) == 1 and g2d.stride(0) % 8 == 0
+            and x2d.stride(0) % 8 == 0 and g2d.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0):
+        return False
+    if into is None:
+        return True
+    if into.dtype != torch.float32 or into.device != g2d.device or into.data_ptr() % 16 != 0:
+        return False
+    v = into.view(G, K, C) if (G > 1 or into.dim() == 3) else into.view(K, C)
+    return v.stride(-1) == 1 and v.stride(-2) % 4 == 0 and (v.dim() == 2 or v.stride(0) % 4 == 0)
 
 
 def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> torch.Tensor:
@@ -866,6 +901,16 @@ def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> 
     P, K = g2d.shape
     C = x2d.shape[1]
     Pg = P // G
+    if _TN_1X1 and _wgrad_tn_ok(g2d, x2d, into, G):
+        # native split-K TN GEMM (csrc/gemm_tn.hip), all groups in one launch,
+        # splits summed in a fixed order into the flat (or per-group) gradient
+        sink = into if into is not None else torch.zeros(
+            (G, K, C) if G > 1 else (K, C), dtype=torch.float32, device=g2d.device)
+        if G > 1:
+            _ops().gemm_tn_acc_grouped(sink.view(G, K, C), g2d, x2d, G)
+        else:
+            _ops().gemm_tn_acc(sink.view(K, C), g2d, x2d)
+        return sink
     S = _wgrad_splits(Pg, K, C, G)
     if G == 1 and S == 1:
         if into is not None:

@@ -89,3 +89,63 @@ def test_gemm_cpu_reference_semantics():
     g = _ops().mm_nn(a, b.t().contiguous(), bias, None, 0.0, 1, pre)
     torch.testing.assert_close(pre, (a.float() @ b.float().t() + bias).to(torch.bfloat16))
     torch.testing.assert_close(g, F.gelu(pre.float(), approximate="tanh").to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,T,M,N", [(3, 640, 256, 512), (8, 1568, 512, 256), (1, 6272, 1024, 256),
+                                     (2, 130, 256, 256), (4, 3136, 64, 256), (2, 700, 64, 64),
+                                     (1, 900, 320, 128)])
+def test_gemm_tn_grouped_vs_fp32(G, T, M, N):
+    """csrc/gemm_tn.hip with G groups of T rows in one launch: sink[g] +=
+    a_g^T b_g (the per-client 1x1-conv weight gradients), group rows strided
+    like the per-group gradient rows of ops/grouped.py."""
+    g = torch.Generator().manual_seed(G * T)
+    a = torch.randn(G * T, M, generator=g).to(torch.bfloat16).cuda()
+    b = torch.randn(G * T, N, generator=g).to(torch.bfloat16).cuda()
+    big = torch.randn(G, M * N + 64, generator=g).cuda()  # padded group rows
+    sink = big[:, :M * N].view(G, M, N)
+    s0, pad = sink.clone(), big[:, M * N:].clone()
+    _ops().gemm_tn_acc_grouped(sink, a, b, G)
+    assert torch.equal(big[:, M * N:], pad)  # nothing written past a group's rows
+    ref = s0 + torch.bmm(a.float().view(G, T, M).transpose(1, 2), b.float().view(G, T, N))
+    torch.testing.assert_close(sink, ref, rtol=1e-4, atol=1e-3 * (T ** 0.5) / 10)
+    # deterministic
+    sink2 = s0.clone()
+    _ops().gemm_tn_acc_grouped(sink2, a, b, G)
+    assert torch.equal(sink, sink2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 4])
+def test_1x1_wgrad_native_route(G):
+    """ops/nn.py _wgrad_gemm: 256-multiple 1x1 weight gradients run on the
+    native TN GEMM (into a flat gradient view, or per-group rows) and match
+    the fp32 product."""
+    from commefficient_amd.ops import nn as onn
+    P, K, C = 4 * 1568, 512, 256
+    g = torch.Generator().manual_seed(7)
+    g2d = torch.randn(P, K, generator=g).to(torch.bfloat16).cuda()
+    x2d = torch.randn(P, C, generator=g).to(torch.bfloat16).cuda()
+    assert onn._wgrad_tn_ok(g2d, x2d, None, G)
+    ref = torch.bmm(g2d.float().view(G, P // G, K).transpose(1, 2), x2d.float().view(G, P // G, C))
+    into = torch.randn(G, K, C, device="cuda")
+    want = into + ref
+    onn._wgrad_gemm(g2d, x2d, into if G > 1 else into.view(K, C), G)
+    torch.testing.assert_close(into, want, rtol=1e-4, atol=1e-2)
+    out = onn._wgrad_gemm(g2d, x2d, None, G)
+    torch.testing.assert_close(out.view(G, K, C), ref, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,T,M,N", [(8, 784, 128, 1152), (1, 3000, 64, 576), (2, 196, 512, 4608)])
+def test_gemm_tn_parts_sum_to_product(G, T, M, N):
+    """gemm_tn_parts: the unsummed split products of each group (the column-
+    image weight gradients' parts, ops/nn.py _wgrad_parts) add up to a_g^T b_g."""
+    g = torch.Generator().manual_seed(T + M)
+    a = torch.randn(G * T, M, generator=g).to(torch.bfloat16).cuda()
+    b = torch.randn(G * T, N, generator=g).to(torch.bfloat16).cuda()
+    parts, S = _ops().gemm_tn_parts(a, b, G)
+    assert parts.shape == (G * S, M, N)
+    got = parts.view(G, S, M, N).sum(1)
+    ref = torch.bmm(a.float().view(G, T, M).transpose(1, 2), b.float().view(G, T, N))
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3 * (T ** 0.5) / 10)
