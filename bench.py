@@ -131,15 +131,19 @@ def main():
         if b.check_every and N > 1 and (i + 1) % b.check_every == 0:
             dist.check_replicas(fed.w)
     torch.cuda.synchronize()
+    # host-side bookkeeping BEFORE the barrier, so the timed rounds start right
+    # after it (the GPU idles through whatever runs between)
     first_loss = float(out[0].mean().item())
-    dist.barrier()
-    torch.cuda.synchronize()
     dl_before = float(fed.accountant.client_download.sum().item())
     if fed.timer.enabled:
         fed.timer.summary()
         fed.timer.totals.clear()
         fed.timer.counts.clear()
+    g0 = time.perf_counter()
+    dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
+    gap_ms = (t0 - g0) * 1000.0
     host_s = 0.0  # host time spent enqueueing (no syncs inside a round)
     evs = []
     if b.round_times:
@@ -216,6 +220,7 @@ def main():
             "backend": ctx.backend, "weights_checksum": checksum,
             **({"rehearsal": "gloo, ranks sharing one GPU"} if rehearsal and N > 1 else {}),
             "host_enqueue_ms_per_step": round(host_s / b.steps * 1000.0, 3),
+            "barrier_before_timed_ms": round(gap_ms, 3),
             **({"round_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(evs) - 1)]}
                if evs else {}),
         }), flush=True)
