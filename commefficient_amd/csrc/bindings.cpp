@@ -1470,7 +1470,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor
                                                     double momentum, const c10::optional<at::Tensor>& run_mean,
                                                     const c10::optional<at::Tensor>& run_var, bool relu,
                                                     const c10::optional<at::Tensor>& nbt,
-                                                    const c10::optional<at::Tensor>& addend) {
+                                                    const c10::optional<at::Tensor>& addend,
+                                                    const c10::optional<at::Tensor>& tstats) {
   check_nhwc_bf16(x, "ghost_bn: x");
   const bool has_add = addend.has_value() && addend->defined();
   if (has_add) {
@@ -1497,6 +1498,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor
     TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->numel() == 1, "ghost_bn: num_batches_tracked int64 []");
     nb = nbt->data_ptr<int64_t>();
   }
+  const bool has_ts = tstats.has_value() && tstats->defined();
+  if (has_ts) {  // per-128-row-tile moments from the producing GEMM (mm_nt_bnstats)
+    TORCH_CHECK(tstats->is_cuda() && tstats->scalar_type() == at::kFloat && tstats->is_contiguous() &&
+                    tstats->numel() == (G * M + kBnStatTile - 1) / kBnStatTile * 4 * C && M >= kBnStatTile,
+                "ghost_bn: tile statistics must be fp32 [ceil(N*H*W / 128), 4, C] with >= 128 rows per group");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int S = bn_slabs(static_cast<int>(G), static_cast<int>(M));
   auto fo = x.options().dtype(at::kFloat);
@@ -1509,7 +1516,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ghost_bn_fwd_hip(const at::Tensor
                 static_cast<float>(eps), static_cast<float>(momentum), rm, rv, part.data_ptr<float>(),
                 stat.data_ptr<float>(), ab.data_ptr<float>(), relu, nb,
                 reinterpret_cast<uint16_t*>(y.data_ptr()), cur_stream(),
-                has_add ? bf16_ptr(*addend) : nullptr, relu ? bits.data_ptr<uint8_t>() : nullptr);
+                has_add ? bf16_ptr(*addend) : nullptr, relu ? bits.data_ptr<uint8_t>() : nullptr,
+                has_ts ? tstats->data_ptr<float>() : nullptr);
   return {y, stat, bits};
 }
 
@@ -2393,8 +2401,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
-        "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None, Tensor? addend=None) "
-        "-> (Tensor, Tensor, Tensor)");
+        "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None, Tensor? addend=None, "
+        "Tensor? tstats=None) -> (Tensor, Tensor, Tensor)");
   m.def("ghost_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor? w, int G, Tensor? y_relu=None, "
         "Tensor(a!)? gw=None, Tensor(b!)? gb=None, Tensor(c!)? ggw=None, Tensor(d!)? ggb=None, "
         "Tensor(e!)? dadd=None) -> (Tensor, Tensor, Tensor)");

@@ -387,6 +387,57 @@ bn_fwd_finalize_group_kernel(const uint16_t* __restrict__ x, const float* __rest
   gmv[o + C] = var;
 }
 
+// grid (C/64, G): group g's mean / var from the moments its producing GEMM
+// wrote per 128-row tile (GemmArgs::stats: [tile][slot][mean | M2][C]; slot 0
+// = the group of the tile's first row), merged with Chan's parallel formula in
+// tile order (16 lanes over strided tiles, then the lanes in order:
+// deterministic).  Outputs as bn_fwd_finalize_group_kernel.
+__global__ void __launch_bounds__(1024)
+bn_fwd_finalize_tiles_kernel(const float* __restrict__ ts, const float* __restrict__ w,
+                             const float* __restrict__ bias, int C, int Mtot, int M, float eps,
+                             float* __restrict__ stat, float* __restrict__ ab,
+                             float* __restrict__ gmv) {
+  __shared__ float red[3][kGL][64];
+  const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc, g = blockIdx.y;
+  const int lo = g * M, hi = lo + M;
+  const int b0 = lo / kBnStatTile, b1 = (hi - 1) / kBnStatTile;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  auto merge = [&](float nb, float mb, float qb) __attribute__((always_inline)) {
+    if (nb <= 0.f) return;
+    const float nn = n + nb, d = mb - mean;
+    mean += d * (nb / nn);
+    m2 += qb + d * d * (n * nb / nn);
+    n = nn;
+  };
+  if (c < C) {
+    for (int b = b0 + gl; b <= b1; b += kGL) {
+      const int r0 = b * kBnStatTile, r1 = min(r0 + kBnStatTile, Mtot);
+      const int slot = r0 / M == g ? 0 : 1;
+      const int nb = min(r1, hi) - max(r0, lo);
+      const float* o = ts + static_cast<size_t>(b) * 4 * C + 2 * slot * C;
+      merge(static_cast<float>(nb), o[c], o[C + c]);
+    }
+  }
+  red[0][gl][cc] = n;
+  red[1][gl][cc] = mean;
+  red[2][gl][cc] = m2;
+  __syncthreads();
+  if (gl != 0 || c >= C) return;
+  n = mean = m2 = 0.f;
+  for (int q = 0; q < kGL; ++q) merge(red[0][q][cc], red[1][q][cc], red[2][q][cc]);
+  const float wc = w != nullptr ? w[c] : 1.f, bc = w != nullptr ? bias[c] : 0.f;
+  const float var = fmaxf(m2 / static_cast<float>(M), 0.f);
+  const float rstd = rsqrtf(var + eps);
+  const size_t o = static_cast<size_t>(g) * 2 * C + c;
+  stat[o] = mean;
+  stat[o + C] = rstd;
+  ab[o] = wc * rstd;
+  ab[o + C] = bc - mean * wc * rstd;
+  gmv[o] = mean;
+  gmv[o + C] = var;
+}
+
 // running statistics from the group-averaged moments (fixed group order)
 __global__ void __launch_bounds__(256)
 bn_running_kernel(const float* __restrict__ gmv, int C, int M, int G, float momentum,
@@ -527,8 +578,21 @@ int bn_slabs(int G, int M) {
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C,
                    float eps, float momentum, float* run_mean, float* run_var, float* part,
                    float* stat, float* ab, bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream,
-                   const uint16_t* addend, uint8_t* relu_bits) {
+                   const uint16_t* addend, uint8_t* relu_bits, const float* tile_stats) {
   const int S = bn_slabs(G, M);
+  const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
+  if (tile_stats != nullptr) {
+    // the producing GEMM wrote per-tile moments: no partial pass over x
+    float* gmv = part + static_cast<size_t>(G) * S * 2 * C;
+    COMMEFF_LAUNCH(bn_fwd_finalize_tiles_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
+                   tile_stats, w, b, C, G * M, M, eps, stat, ab, gmv);
+    COMMEFF_LAUNCH(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gmv, C, M, G,
+                   momentum, run_mean, run_var, nbt);
+    COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
+                   nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
+                   const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr);
+    return;
+  }
   COMMEFF_LAUNCH(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
                      nullptr, C, M, S, part);
   if (G >= 2 && G < kGL) {
@@ -542,7 +606,6 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
     COMMEFF_LAUNCH(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part,
                        w, b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var, nbt);
   }
-  const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                      nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
                      const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr);

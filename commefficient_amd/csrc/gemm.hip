@@ -71,7 +71,7 @@ struct MmCfg {
   static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
 };
 
-template <int BN, bool NN, int ACT, bool F32>
+template <int BN, bool NN, int ACT, bool F32, bool ST = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   using Cfg = MmCfg<BN, NN>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -201,6 +201,25 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
       }
   __syncthreads();
   constexpr int CPR = BN / 8;
+  // batch-norm moments of the stored (bf16-rounded) tile (GemmArgs::stats),
+  // accumulated in registers by the store loop: this thread's 8 columns
+  // (cc = tid % CPR is fixed) over its rows, shifted by the tile's first row
+  // (sums of x - K and (x - K)^2), split at a group boundary inside the tile
+  constexpr bool kStatsOk = ST && !F32 && ACT == 0;
+  const bool st_on = kStatsOk && a.stats != nullptr;
+  const int rend = min(Cfg::BM, a.M - m0);
+  int rb = rend;
+  float K8[8], s1a[8], s2a[8], s1b[8], s2b[8];
+  if (st_on) {
+    const int g0 = m0 / a.stats_mg;
+    rb = min(rend, (g0 + 1) * a.stats_mg - m0);
+    const int c8 = (tid % CPR) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      K8[j] = bf2f(pack_bf16(ct[c8 + j], 0.f) & 0xffffu);
+      s1a[j] = s2a[j] = s1b[j] = s2b[j] = 0.f;
+    }
+  }
   for (int e = tid; e < Cfg::BM * CPR; e += 256) {
     const int row = e / CPR, cc = e - row * CPR, m = m0 + row;
     if (m >= a.M) continue;
@@ -238,6 +257,49 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) out[j] = pack_bf16(v[2 * j], v[2 * j + 1]);
       *reinterpret_cast<v4u*>(c) = out;
+      if (kStatsOk && st_on) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf2f((out[j >> 1] >> (16 * (j & 1))) & 0xffffu) - K8[j];
+          if (row < rb) { s1a[j] += d; s2a[j] = fmaf(d, d, s2a[j]); }
+          else { s1b[j] += d; s2b[j] = fmaf(d, d, s2b[j]); }
+        }
+      }
+    }
+  }
+  if constexpr (kStatsOk) {
+    if (st_on) {
+      // fixed-order combine of the RG row groups through LDS (the tile is no
+      // longer needed), then mean = K + S1/n, M2 = S2 - S1^2/n per slot
+      static_assert(Cfg::BM == kBnStatTile, "statistics tile rows");
+      constexpr int RG = 256 / CPR;
+      static_assert(RG * 4 * BN + BN <= Cfg::BM * Cfg::LD, "statistics scratch fits the tile");
+      __syncthreads();
+      const int rg = tid / CPR, c8 = (tid % CPR) * 8;
+      float* red = ct;                  // [RG][4][BN]: S1a, S2a, S1b, S2b
+      float* kk = ct + RG * 4 * BN;     // [BN]
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(rg * 4 + 0) * BN + c8 + j] = s1a[j];
+        red[(rg * 4 + 1) * BN + c8 + j] = s2a[j];
+        red[(rg * 4 + 2) * BN + c8 + j] = s1b[j];
+        red[(rg * 4 + 3) * BN + c8 + j] = s2b[j];
+        if (rg == 0) kk[c8 + j] = K8[j];
+      }
+      __syncthreads();
+      if (tid < BN) {
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int q = 0; q < RG; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) t[u] += red[(q * 4 + u) * BN + tid];
+        const float k0 = kk[tid];
+        const float na = static_cast<float>(rb), nb = static_cast<float>(rend - rb);
+        float* o = a.stats + static_cast<int64_t>(m0 / Cfg::BM) * 4 * a.N + n0 + tid;
+        o[0] = na > 0.f ? k0 + t[0] / na : 0.f;
+        o[a.N] = na > 0.f ? fmaxf(t[1] - t[0] * t[0] / na, 0.f) : 0.f;
+        o[2 * a.N] = nb > 0.f ? k0 + t[2] / nb : 0.f;
+        o[3 * a.N] = nb > 0.f ? fmaxf(t[3] - t[2] * t[2] / nb, 0.f) : 0.f;
+      }
     }
   }
 }
@@ -501,17 +563,17 @@ void launch_gemm_big(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t 
   }
 }
 
-template <int BN, bool NN, int ACT, bool F32>
+template <int BN, bool NN, int ACT, bool F32, bool ST = false>
 void launch_gemm_t(const GemmArgs& a, hipStream_t stream) {
   constexpr int lds = MmCfg<BN, NN>::LDS;
   static bool init = false;
   if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<BN, NN, ACT, F32>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<BN, NN, ACT, F32, ST>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     init = true;
   }
   const int tiles = ((a.M + 127) / 128) * (a.N / BN);
-  COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32>), dim3(tiles), dim3(256), lds, stream, a);
+  COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32, ST>), dim3(tiles), dim3(256), lds, stream, a);
 }
 
 }  // namespace
@@ -540,6 +602,11 @@ void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stre
   }
   // 128-wide column tiles when they still give ~every resident slot (2 per CU) a block
   const bool wide = a.N % 128 == 0 && static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) >= 384;
+  if (a.stats != nullptr && !nn && act == 0 && !f32) {  // BN moments in the epilogue (mm_nt_bnstats)
+    if (wide) launch_gemm_t<128, false, 0, false, true>(a, stream);
+    else launch_gemm_t<64, false, 0, false, true>(a, stream);
+    return;
+  }
   if (act == 1) {
     if (wide) { if (nn) launch_gemm_t<128, true, 1, false>(a, stream); else launch_gemm_t<128, false, 1, false>(a, stream); }
     else { if (nn) launch_gemm_t<64, true, 1, false>(a, stream); else launch_gemm_t<64, false, 1, false>(a, stream); }

@@ -8,6 +8,8 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace commeff {
@@ -84,6 +86,66 @@ at::Tensor mm_nn(const at::Tensor& a, const at::Tensor& b, const c10::optional<a
   return mm_impl(a, b, true, bias, out, beta, act, pre);
 }
 
+// (a b^T bf16 [M, N], tile moments fp32 [ceil(M / 128), 4, N]): the forward
+// of a conv feeding a ghost batch norm of G groups of M / G rows, with the
+// norm's per-128-row-tile mean / M2 (split at group boundaries) written by the
+// GEMM epilogue (GemmArgs::stats).  CPU: the same quantities from the fp32
+// reference's bf16-rounded output.
+std::tuple<at::Tensor, at::Tensor> mm_nt_bnstats(const at::Tensor& a, const at::Tensor& b, int64_t G) {
+  const int64_t M = a.size(0), N = b.size(0);
+  TORCH_CHECK(G >= 1 && M % G == 0 && M / G >= kBnStatTile, "mm_nt_bnstats: G | M with >= 128 rows per group");
+  const int64_t Mg = M / G, T = (M + kBnStatTile - 1) / kBnStatTile;
+  // every tile writes all four rows of its statistics (slot 1 zero when it
+  // holds one group)
+  auto stats = a.is_cuda() ? at::empty({T, 4, N}, a.options().dtype(at::kFloat))
+                           : at::zeros({T, 4, N}, a.options().dtype(at::kFloat));
+  if (!a.is_cuda()) {
+    auto y = mm_impl(a, b, false, c10::nullopt, c10::nullopt, 0.0, 0, c10::nullopt);
+    auto yf = y.to(at::kFloat);
+    for (int64_t t = 0; t < T; ++t) {
+      const int64_t r0 = t * kBnStatTile, r1 = std::min(M, r0 + kBnStatTile);
+      const int64_t rb = std::min(r1, (r0 / Mg + 1) * Mg);
+      const int64_t bounds[3] = {r0, rb, r1};
+      for (int slot = 0; slot < 2; ++slot) {
+        if (bounds[slot + 1] <= bounds[slot]) continue;
+        auto blk = yf.slice(0, bounds[slot], bounds[slot + 1]);
+        auto mean = blk.mean(0);
+        stats[t][2 * slot].copy_(mean);
+        stats[t][2 * slot + 1].copy_((blk - mean).pow(2).sum(0));
+      }
+    }
+    return {y, stats};
+  }
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+                  a.stride(1) == 1 && b.stride(1) == 1 && b.size(1) == a.size(1),
+              "mm_nt_bnstats: bf16 [M, K] x [N, K] with unit column stride");
+  const int64_t K = a.size(1);
+  TORCH_CHECK(gemm_supported(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), false),
+              "mm_nt_bnstats: native GEMM needs N % 64 == 0 and K % 64 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
+                  a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0,
+              "mm_nt_bnstats: 16-byte aligned operands and row strides");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto C = at::empty({M, N}, a.options());
+  GemmArgs g;
+  g.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  g.lda = a.stride(0);
+  g.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  g.ldb = b.stride(0);
+  g.C = C.data_ptr();
+  g.ldc = C.stride(0);
+  g.C2 = nullptr;
+  g.bias = nullptr;
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.K = static_cast<int>(K);
+  g.beta = 0.f;
+  g.stats = stats.data_ptr<float>();
+  g.stats_mg = static_cast<int>(Mg);
+  launch_gemm(g, false, 0, false, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  return {C, stats};
+}
+
 }  // namespace
 }  // namespace commeff
 
@@ -92,14 +154,17 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
         "Tensor(d!)? pre=None) -> Tensor");
   m.def("mm_nn(Tensor a, Tensor b, Tensor? bias=None, Tensor(c!)? out=None, float beta=0.0, int act=0, "
         "Tensor(d!)? pre=None) -> Tensor");
+  m.def("mm_nt_bnstats(Tensor a, Tensor b, int G) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CPU, m) {
   m.impl("mm_nt", &commeff::mm_nt);
   m.impl("mm_nn", &commeff::mm_nn);
+  m.impl("mm_nt_bnstats", &commeff::mm_nt_bnstats);
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("mm_nt", &commeff::mm_nt);
   m.impl("mm_nn", &commeff::mm_nn);
+  m.impl("mm_nt_bnstats", &commeff::mm_nt_bnstats);
 }

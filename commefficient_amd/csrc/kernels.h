@@ -389,7 +389,10 @@ int64_t bn_scratch_floats(int G, int M, int C);
 void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int M, int C, float eps,
                    float momentum, float* run_mean, float* run_var, float* part, float* stat, float* ab,
                    bool relu, int64_t* nbt, uint16_t* y, hipStream_t stream,
-                   const uint16_t* addend = nullptr, uint8_t* relu_bits = nullptr);
+                   const uint16_t* addend = nullptr, uint8_t* relu_bits = nullptr,
+                   const float* tile_stats = nullptr);
+// rows per tile of the GEMM-epilogue batch-norm moments (GemmArgs::stats)
+constexpr int kBnStatTile = 128;
 // y_relu: the forward's 1-bit ReLU mask (one byte per 8 channels of a pixel)
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
@@ -527,6 +530,12 @@ struct GemmArgs {
   const uint16_t* bias16 = nullptr;  // bf16 bias (instead of the fp32 one)
   int M, N, K;
   float beta;
+  // batch-norm statistics of the (bf16-rounded) output, per 128-row tile and
+  // group slot: stats[tile][slot][mean | M2][N], rows split at multiples of
+  // stats_mg (>= 128: a tile spans at most two groups; slot 0 = the group of
+  // the tile's first row).  bf16 output without activation only.
+  float* stats = nullptr;
+  int stats_mg = 0;
 };
 bool gemm_supported(int M, int N, int K, bool nn);
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);

@@ -96,7 +96,8 @@ class GhostBatchNorm2d(nn.BatchNorm2d):
                                  self.running_var if track else None,
                                  relu=fused_add or (self.fuse_relu and addend is None),
                                  num_batches_tracked=self.num_batches_tracked if track else None,
-                                 gg=gg, addend=addend if fused_add else None)
+                                 gg=gg, addend=addend if fused_add else None,
+                                 tstats=_nn.take_bnstats(x, G))
             return y, (fused_add or self.fuse_relu) if addend is None or fused_add else False
         if gg is None and (not self.training or G <= 1):
             return super().forward(x), False
@@ -160,9 +161,14 @@ def ghost_batchnorm(model: nn.Module, groups: int):
     mods = [m for m in model.modules() if isinstance(m, GhostBatchNorm2d)]
     for m in mods:
         m.ghost_groups = groups
+    # the native conv forwards also write their outputs' BN moments for these
+    # groups (ops/nn.py _mm_nt_conv)
+    prev = _nn._EPI["G"]
+    _nn._EPI["G"] = groups if (mods and model.training) else 0
     try:
         yield
     finally:
+        _nn._EPI["G"] = prev
         for m in mods:
             m.ghost_groups = 1
 

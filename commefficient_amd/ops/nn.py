@@ -663,11 +663,11 @@ class _GhostBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, groups, eps, momentum, running_mean, running_var, relu, nbt,
-                gg=None, addend=None):
+                gg=None, addend=None, tstats=None):
         if addend is not None:  # y = relu(bn(x) + addend): a residual block's tail
             addend = addend.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         y, stat, bits = _ops().ghost_bn_fwd(x, weight, bias, int(groups), float(eps), float(momentum),
-                                            running_mean, running_var, bool(relu), nbt, addend)
+                                            running_mean, running_var, bool(relu), nbt, addend, tstats)
         # the backward's ReLU gate: 1 bit per element (y itself is 16)
         ctx.save_for_backward(x, stat, weight, bits if relu else None)
         ctx.groups = int(groups)
@@ -696,7 +696,7 @@ class _GhostBN(torch.autograd.Function):
             assert ctx.gg.G == ctx.groups, "grouped grads need ghost-BN groups == gradient groups"
             dx, _, _ = _ops().ghost_bn_bwd(dy, x, stat, weight, ctx.groups, y, None, None,
                                            ctx.gg.view(pw), ctx.gg.view(pb), dadd)
-            return dx, None, None, None, None, None, None, None, None, None, None, dadd
+            return dx, None, None, None, None, None, None, None, None, None, None, dadd, None
         gw = pw.grad if pw is not None else None
         gb = pb.grad if pb is not None else None
         into = (gw is not None and gb is not None and gw.dtype == torch.float32
@@ -710,7 +710,7 @@ class _GhostBN(torch.autograd.Function):
             dw = db = None
         if into:
             _grad_written(pw, pb)
-        return dx, dw, db, None, None, None, None, None, None, None, None, dadd
+        return dx, dw, db, None, None, None, None, None, None, None, None, dadd, None
 
 
 def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
@@ -722,14 +722,14 @@ def ghost_bn_native_ok(x: torch.Tensor, weight) -> bool:
 
 def ghost_batch_norm(x, weight, bias, groups: int, eps: float, momentum: float,
                      running_mean=None, running_var=None, relu: bool = False,
-                     num_batches_tracked=None, gg=None, addend=None):
+                     num_batches_tracked=None, gg=None, addend=None, tstats=None):
     """Per-group batch norm (+ ReLU when ``relu``) on the native kernels; the
     running statistics and ``num_batches_tracked`` are updated on the device.
     ``gg``: per-group weight gradients (ops/grouped.py).  ``addend``: y =
     relu(bn(x) + addend) in the same pass (needs ``relu``)."""
     assert addend is None or relu, "the fused residual add is followed by the ReLU"
     return _GhostBN.apply(x, weight, bias, groups, eps, momentum, running_mean, running_var, relu,
-                          num_batches_tracked, gg, addend)
+                          num_batches_tracked, gg, addend, tstats)
 
 
 # ------------------------------------------------------------ loss
@@ -808,6 +808,51 @@ def _mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     if _gemm_ok(a, b, b.shape[0]):
         return _ops().mm_nt(a, b)
     return torch.mm(a, b.t())
+
+
+# Ghost-BN statistics from the producing GEMM's epilogue: inside a merged
+# BatchNorm forward (models/common.py ghost_batchnorm sets "G"), the native
+# 1x1 / column-image conv forwards also write the per-128-row-tile moments of
+# their output (csrc/gemm.hip GemmArgs::stats) and hand them to the consuming
+# GhostBatchNorm2d on the output tensor (``_commeff_bnstats``), which then
+# skips its statistics pass over x (csrc/bn.hip bn_fwd_finalize_tiles_kernel).
+# Opt-in (COMMEFF_BN_EPI=1): on the ResNet-101 round the epilogue cost
+# (+~20 us per forward GEMM: the 1x1 GEMMs run many waves of short-K tiles)
+# outweighed the statistics pass it removes (profiles/r4_experiments.md).
+_EPI = {"G": 0, "on": os.environ.get("COMMEFF_BN_EPI", "0") == "1", "last": None}
+
+
+def _mm_nt_conv(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """_mm_nt for a conv forward; leaves the output's tile moments in
+    ``_EPI["last"]`` when a ghost BN of G groups will consume it."""
+    G = _EPI["G"]
+    M = a.shape[0]
+    if _EPI["on"] and G >= 1 and M % G == 0 and M // G >= 128 and _gemm_ok(a, b, b.shape[0]):
+        y, st = _ops().mm_nt_bnstats(a, b, G)
+        _EPI["last"] = (st, G)
+        return y
+    return _mm_nt(a, b)
+
+
+def _with_bnstats(out: torch.Tensor) -> torch.Tensor:
+    """Attach the moments the conv forward just computed to its output."""
+    hit, _EPI["last"] = _EPI["last"], None
+    if hit is not None:
+        out._commeff_bnstats = (hit[0], hit[1], out._version)
+    return out
+
+
+def take_bnstats(x: torch.Tensor, G: int):
+    """The producing GEMM's tile moments of ``x`` for a ghost BN of G groups,
+    or None (not a fresh native conv output, modified in place since, or other
+    groups)."""
+    hit = getattr(x, "_commeff_bnstats", None)
+    if hit is None:
+        return None
+    x._commeff_bnstats = None  # consumed once (and not kept alive with x)
+    if hit[1] != G or hit[2] != x._version:
+        return None
+    return hit[0]
 
 
 def _mm_nn(a: torch.Tensor, b: torch.Tensor, acc: torch.Tensor = None, in_place: bool = False):
@@ -947,7 +992,7 @@ class _Conv1x1(torch.autograd.Function):
         else:
             x2d, h, w = _nhwc2d(x), H, W
         wb = weight.detach().view(k, c).to(torch.bfloat16)
-        y2d = _mm_nt(x2d, wb)
+        y2d = _mm_nt_conv(x2d, wb)
         ctx.save_for_backward(x2d, wb)
         ctx.weight, ctx.stride, ctx.gg = weight, stride, gg
         ctx.dims = (n, c, H, W, h, w)
@@ -992,7 +1037,7 @@ class _Conv1x1Pass(torch.autograd.Function):
         n, c, h, w = x.shape
         k = weight.shape[0]
         wb = weight.detach().view(k, c).to(torch.bfloat16)
-        y2d = _mm_nt(_nhwc2d(x), wb)
+        y2d = _mm_nt_conv(_nhwc2d(x), wb)
         ctx.save_for_backward(x, wb)
         ctx.weight, ctx.gg = weight, gg
         return y2d.view(n, h, w, k).permute(0, 3, 1, 2), x.view_as(x)
@@ -1036,7 +1081,9 @@ class _Conv1x1Pass(torch.autograd.Function):
 
 def conv1x1_passthrough(x, weight, gg=None):
     """(conv1x1(x, weight), x) with the two input gradients summed in one GEMM."""
-    return _Conv1x1Pass.apply(x, weight, gg)
+    _EPI["last"] = None
+    y, xi = _Conv1x1Pass.apply(x, weight, gg)
+    return _with_bnstats(y), xi
 
 
 def _wgrad_mopen(g, x, weight, stride, padding, dilation, groups):
@@ -1138,7 +1185,7 @@ class _ConvCol(torch.autograd.Function):
         col = _ops().im2col(x, R, S, stride, pad, Kc)
         wt = _col_image(weight, Kc)
         OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
-        y2d = _mm_nt(col, wt)
+        y2d = _mm_nt_conv(col, wt)
         ctx.save_for_backward(col, wt)
         ctx.geo = (N, C, H, W, R, S, stride, pad)
         ctx.weight, ctx.gg = weight, gg
@@ -1252,10 +1299,11 @@ def conv2d_native_kind(x: torch.Tensor, weight: torch.Tensor, stride, padding, d
 
 def conv2d_native(x: torch.Tensor, weight: torch.Tensor, kind: str, stride: int = 1, gg=None,
                   padding: int = 0):
+    _EPI["last"] = None
     if kind == "1x1":
-        return _Conv1x1.apply(x, weight, int(stride), gg)
+        return _with_bnstats(_Conv1x1.apply(x, weight, int(stride), gg))
     if kind == "col":
-        return _ConvCol.apply(x, weight, int(stride), int(padding), gg)
+        return _with_bnstats(_ConvCol.apply(x, weight, int(stride), int(padding), gg))
     return _Conv3x3.apply(x, weight, gg)
 
 
