@@ -1,5 +1,5 @@
 import sys, os, torch
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from commefficient_amd import _ext
 _ext.load()
 from commefficient_amd.models.common import ghost_batchnorm, GhostBatchNorm2d
