@@ -157,6 +157,7 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        if (m >= a.M) continue;  // M not a multiple of 32 (the LM head's vocabulary)
         float* p = out + static_cast<int64_t>(m) * ld + n;
         if (direct) *p += acc[mi][ni][e];
         else *p = acc[mi][ni][e];

@@ -234,11 +234,13 @@ def _mm_t(dy: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
 
 def _gemm_tn_ok(sink: torch.Tensor, at: torch.Tensor, b: torch.Tensor) -> bool:
     """csrc/gemm_tn.hip serves sink [M, N] += at^T b: bf16 [T, M] / [T, N]
-    operands with unit column stride, M and N multiples of 256."""
+    operands with unit column stride, M and N multiples of 256 (M also when
+    at's rows hold the 8-column chunk past M: the padded LM-head gradient)."""
+    M = at.shape[1] if at.dim() == 2 else 0
     return (_WGRAD_GEMM["native"] and sink.dtype == torch.float32 and sink.dim() == 2
             and sink.stride(1) == 1 and at.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
             and at.dim() == 2 and b.dim() == 2 and at.stride(1) == 1 and b.stride(1) == 1
-            and at.shape[1] % 256 == 0 and b.shape[1] % 256 == 0
+            and (M % 256 == 0 or at.stride(0) >= -(-M // 8) * 8) and b.shape[1] % 256 == 0
             and at.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and sink.stride(0) % 4 == 0
             and at.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and sink.data_ptr() % 16 == 0)
 
@@ -444,6 +446,75 @@ class _Linear(torch.autograd.Function):
         da = _mm_t(gy, W) if ctx.needs_input_grad[0] else None
         dW = _wgrad(sW, a.t(), gy) if ctx.needs_input_grad[1] else None
         return da, dW, None if sb is not None else db
+
+
+class _LMHead(torch.autograd.Function):
+    """logits = h W^T of the tied LM head, W [V, H] bf16 (V = 50,257: no tile
+    multiple).  Native NT GEMM against a zero-padded copy of W [ceil128(V), H]
+    (one copy per call), the logits a [T, V] view of the padded product;
+    backward: dh on the native NN GEMM over the zero-padded gradient, dW
+    accumulated into the weight's fp32 gradient sink by the split-K TN GEMM on
+    the weight-gradient side stream (replaces three hipBLASLt GEMMs; reference
+    model: gpt2_train.py:262-273, HF GPT2DoubleHeadsModel.lm_head)."""
+
+    @staticmethod
+    def forward(ctx, h, W):
+        V, H = W.shape
+        Vp = -(-V // 128) * 128
+        Wp = torch.empty(Vp, H, dtype=W.dtype, device=W.device)
+        Wp[:V].copy_(W)
+        Wp[V:].zero_()
+        ctx.save_for_backward(h, Wp, W)
+        ctx.sink = _sink(W)
+        return _ops().mm_nt(h, Wp)[:, :V]
+
+    @staticmethod
+    def backward(ctx, g):
+        h, Wp, W = ctx.saved_tensors
+        V = W.shape[0]
+        T = g.shape[0]
+        g16 = torch.empty(T, Wp.shape[0], dtype=torch.bfloat16, device=g.device)
+        g16[:, :V].copy_(g)
+        g16[:, V:].zero_()
+        dh = None
+        if ctx.needs_input_grad[0]:
+            # dh = g Wp reduces over the 50k vocabulary rows with only T x H
+            # outputs (~60 tiles): the split-K TN GEMM over the transposed
+            # gradient [Vp, T] keeps every CU busy (the NN GEMM took 0.7 ms)
+            Tp = -(-T // 8) * 8
+            gt = torch.empty(Wp.shape[0], Tp, dtype=torch.bfloat16, device=g.device)
+            gt[:, :T].copy_(g16.t())
+            dh32 = torch.zeros(T, h.shape[1], dtype=torch.float32, device=g.device)
+            _ops().gemm_tn_acc(dh32, gt[:, :T], Wp)
+            dh = dh32.to(torch.bfloat16)
+        dW = None
+        if ctx.needs_input_grad[1]:
+            if ctx.sink is not None:
+                _wgrad(ctx.sink, g16[:, :V].t(), h)
+            else:
+                dW = torch.mm(g16[:, :V].t(), h, out_dtype=torch.float32).to(W.dtype)
+        return dh, dW
+
+
+# The native LM head is opt-in (COMMEFF_LM_HEAD=native): isolated, its forward
+# + backward took 699 vs 377 us for hipBLASLt at 560 tokens
+# (scripts/bench_lmhead.py; the padded weight copy, the transposed gradient and
+# the fp32 read-modify-write of the 50,257 x 768 gradient sink), with the
+# GPT-2 round's wall time unchanged (host-bound).
+_LM_NATIVE = os.environ.get("COMMEFF_LM_HEAD", "blas") == "native"
+
+
+def lm_head(m, h: torch.Tensor) -> torch.Tensor:
+    """The (tied) LM head of an HF double-heads model on h [..., H]: native
+    (``_LMHead``, opt-in) for bf16 CUDA operands, else the module itself."""
+    W = m.lm_head.weight
+    H = h.shape[-1]
+    h2 = h.reshape(-1, H)
+    if (_LM_NATIVE and _GEMM["native"] and h.is_cuda and h.dtype == torch.bfloat16 and W.dtype == torch.bfloat16
+            and getattr(m.lm_head, "bias", None) is None and H % 64 == 0
+            and h2.is_contiguous() and h2.data_ptr() % 16 == 0):
+        return _LMHead.apply(h2, W).view(h.shape[:-1] + (W.shape[0],))
+    return m.lm_head(h)
 
 
 # ------------------------------------------------------------------ model

@@ -127,7 +127,7 @@ def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos,
     valid = lm_pos >= 0
     p = lm_pos.clamp_min(0)
     h = torch.gather(hid.reshape(B, C * L, H), 1, p.unsqueeze(-1).expand(-1, -1, H))
-    logits = m.lm_head(h)                                                # [B, R, V]
+    logits = _tx.lm_head(m, h)                                           # [B, R, V]
     tgt = torch.gather(lm_labels.reshape(B, C * L), 1, (p + 1).clamp_max(C * L - 1))
     tgt = torch.where(valid, tgt, torch.full_like(tgt, -100))
     tok = F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), tgt.reshape(-1),

@@ -497,3 +497,44 @@ def test_gemm_tn_wgrad_vs_fp32_reference_gpu(shape):
     view = big[:, :N]
     tx._acc_mm(view, a.t(), b)
     torch.testing.assert_close(view, ref - sink0, rtol=1e-4, atol=1e-3 * (T ** 0.5) / 10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sinked", [False, True])
+def test_lm_head_native_vs_fp32_gpu(sinked, monkeypatch):
+    """The tied LM head (vocabulary 50,257, no tile multiple) on the native
+    GEMMs (ops/transformer.py _LMHead): logits, dh and dW (returned, or
+    accumulated into an fp32 gradient sink on the side stream by the split-K
+    TN GEMM with a partial edge tile) vs the fp32 products of the same bf16
+    operands."""
+    V, H, T = 50257, 768, 600
+    monkeypatch.setattr(tx, "_LM_NATIVE", True)  # opt-in path (COMMEFF_LM_HEAD=native)
+    g = torch.Generator().manual_seed(5)
+    head = torch.nn.Linear(H, V, bias=False).to(torch.bfloat16).cuda()
+    with torch.no_grad():
+        head.weight.copy_((torch.randn(V, H, generator=g) * 0.05).to(torch.bfloat16))
+    m = type("M", (), {})()
+    m.lm_head = head
+    h = torch.randn(T, H, generator=g).to(torch.bfloat16).cuda().requires_grad_(True)
+    gy = torch.randn(T, V, generator=g).to(torch.bfloat16).cuda()
+    W = head.weight
+    sink0 = torch.randn(V, H, generator=g).cuda()
+    sink = sink0.clone()
+    with tx.grad_sinks({id(W): sink} if sinked else None):
+        logits = tx.lm_head(m, h)
+        assert logits.shape == (T, V) and logits.grad_fn is not None
+        fns = [logits.grad_fn] + [f for f, _ in logits.grad_fn.next_functions if f is not None]
+        assert any(type(f).__name__.startswith("_LMHead") for f in fns)
+        logits.backward(gy)
+    tx.join_wgrad_stream()
+    torch.cuda.synchronize()
+    ref = h.detach().float() @ W.detach().float().t()
+    rel = lambda a, b: ((a.float() - b).abs().max() / b.abs().max()).item()  # noqa: E731
+    assert rel(logits.detach(), ref) < 1e-2
+    assert rel(h.grad, gy.float() @ W.detach().float()) < 1e-2
+    dw_ref = gy.float().t() @ h.detach().float()
+    if sinked:
+        assert W.grad is None
+        torch.testing.assert_close(sink - sink0, dw_ref, rtol=1e-3, atol=2e-2)
+    else:
+        assert rel(W.grad, dw_ref) < 1e-2
