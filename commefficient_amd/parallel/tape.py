@@ -36,6 +36,7 @@ device buffers filled by stream-ordered H2D copies before each replay.
 """
 from __future__ import annotations
 
+import gc
 import warnings
 from typing import Callable, List, Optional
 
@@ -138,19 +139,30 @@ class RoundTapes:
             g = torch.cuda.CUDAGraph()
         rec = None
         result = None
-        with torch.cuda.stream(self.stream):
-            if self.pool is None:
-                g.capture_begin()
-            else:
-                g.capture_begin(pool=self.pool)
-            try:
-                rec = _REC = _Recording()
-                result = body()
-            finally:
-                _REC = None
-                if rec is not None:
-                    rec.close()
-                g.capture_end()
+        # no garbage collection inside the capture: a collected object whose
+        # finaliser calls the runtime (an unreachable engine's graphs, events
+        # or side-stream tensor frees) aborts a capturing process -- collect
+        # first, as torch.cuda.graph does, and hold the collector off
+        gc.collect()
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.stream(self.stream):
+                if self.pool is None:
+                    g.capture_begin()
+                else:
+                    g.capture_begin(pool=self.pool)
+                try:
+                    rec = _REC = _Recording()
+                    result = body()
+                finally:
+                    _REC = None
+                    if rec is not None:
+                        rec.close()
+                    g.capture_end()
+        finally:
+            if gc_was:
+                gc.enable()
         cur.wait_stream(self.stream)
         self.pool = g.pool()
         counts = [int(c) for c in _ops().graph_node_counts(g.raw_cuda_graph())]
