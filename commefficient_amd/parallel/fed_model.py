@@ -54,11 +54,19 @@ DEFAULT_NUM_CLIENTS = {"EMNIST": 3500, "PERSONA": 17568}
 
 
 def _set_training(module: torch.nn.Module, mode: bool) -> None:
-    """module.train(mode) only when some submodule is in the other mode: the
-    recursive walk costs ~0.7 ms per call on a GPT-2 (HF) module tree, paid
-    twice per round otherwise."""
-    if module.training != mode or any(m.training != mode for m in module.modules()):
-        module.train(mode)
+    """module.train(mode) only when some submodule is in the other mode.  The
+    check runs over a flat list of the submodules kept on the module (the
+    engine's module trees do not change shape): ``module.modules()`` itself
+    is a recursive generator walk, ~0.35 ms per call on the GPT-2 (HF) tree,
+    and ``train`` another ~0.7 ms, twice per round otherwise."""
+    mods = module.__dict__.get("_commeff_submodules")
+    if mods is None:
+        mods = list(module.modules())
+        module.__dict__["_commeff_submodules"] = mods
+    for m in mods:
+        if m.training != mode:
+            module.train(mode)
+            return
 
 
 class RoundBatch:

@@ -79,9 +79,13 @@ class FlatParams:
             ops.zero_(self.g)  # (a memset a recorded round can replay, parallel/tape.py)
         else:
             self.g.zero_()
-        # autograd may have replaced .grad (e.g. set_to_none elsewhere)
+        # autograd may have replaced .grad (e.g. set_to_none elsewhere); the
+        # expected address is computed, not sliced (a view per parameter per
+        # round was ~0.4 ms of host time on GPT-2)
+        base, es = self.g.data_ptr(), self.g.element_size()
         for p, o, n in zip(self.params, self.offsets, self.numels):
-            if p.grad is None or p.grad.data_ptr() != self.g[o:o + n].data_ptr():
+            gr = p.grad
+            if gr is None or gr.data_ptr() != base + o * es:
                 p.grad = self.g[o:o + n].view(p.shape)
 
     # ----------------------------------------------------- bf16 compute copy
