@@ -34,7 +34,19 @@ __global__ void __launch_bounds__(256) host_read_copy_kernel(const unsigned char
   if (t0 < tail) dst[(nw << 4) + t0] = src[(nw << 4) + t0];
 }
 
+// launch-status probe: writes its dynamic LDS size (checked launches, launch.h)
+__global__ void __launch_bounds__(64) launch_probe_kernel(int32_t* out) {
+  extern __shared__ int32_t probe_lds[];
+  probe_lds[threadIdx.x] = static_cast<int32_t>(threadIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = probe_lds[63] + 1;
+}
+
 }  // namespace
+
+void launch_probe(int32_t* out, uint32_t lds_bytes, hipStream_t stream) {
+  COMMEFF_LAUNCH(launch_probe_kernel, dim3(1), dim3(64), lds_bytes, stream, out);
+}
 
 void launch_host_read_copy(const void* host_src, void* dst, int64_t n, hipStream_t stream) {
   if (n <= 0) return;

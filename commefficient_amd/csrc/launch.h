@@ -18,10 +18,19 @@
 // tape (no launch that bypassed COMMEFF_LAUNCH, e.g. a PyTorch kernel).
 // Per-round scalars (learning rate, round index) must therefore reach the
 // recorded kernels through device memory, never as launch arguments.
+//
+// Every launch and memset status is checked (eager, recorded and replayed
+// alike): a failure raises (std::runtime_error -> Python RuntimeError through
+// the op bindings) naming the kernel, its grid, block and dynamic LDS bytes,
+// instead of leaving the outputs unwritten.  hipLaunchKernel's return value
+// costs nothing extra; the sticky error is also cleared so a later PyTorch
+// check does not report it against an unrelated op.
 #pragma once
 #include <hip/hip_runtime_api.h>
 #include <cstdint>
+#include <cstdio>
 #include <functional>
+#include <stdexcept>
 #include <tuple>
 #include <type_traits>
 #include <utility>
@@ -36,34 +45,57 @@ struct LaunchTape {
 // non-null while a tape records (set/cleared by the bindings, tape.cpp)
 LaunchTape* tape_active();
 
+[[noreturn]] inline void launch_failed(const char* name, hipError_t e, dim3 g, dim3 b, uint32_t sh) {
+  (void)hipGetLastError();  // clear the sticky status
+  char msg[512];
+  std::snprintf(msg, sizeof(msg),
+                "commeff: launch of %s failed: %s (%d); grid (%u, %u, %u), block (%u, %u, %u), "
+                "dynamic LDS %u bytes",
+                name, hipGetErrorString(e), static_cast<int>(e), g.x, g.y, g.z, b.x, b.y, b.z, sh);
+  throw std::runtime_error(msg);
+}
+
 template <typename F, typename T, size_t... I>
-inline void launch_from_tuple(F k, dim3 g, dim3 b, uint32_t sh, hipStream_t s, T& args,
-                              std::index_sequence<I...>) {
+inline void launch_from_tuple(const char* name, F k, dim3 g, dim3 b, uint32_t sh, hipStream_t s,
+                              T& args, std::index_sequence<I...>) {
   void* argv[sizeof...(I) > 0 ? sizeof...(I) : 1] = {static_cast<void*>(&std::get<I>(args))...};
-  (void)hipLaunchKernel(reinterpret_cast<const void*>(k), g, b, argv, sh, s);
+  const hipError_t e = hipLaunchKernel(reinterpret_cast<const void*>(k), g, b, argv, sh, s);
+  if (e != hipSuccess) launch_failed(name, e, g, b, sh);
 }
 
 template <typename... P, typename... A>
-inline void tape_launch(void (*k)(P...), dim3 g, dim3 b, uint32_t sh, hipStream_t s, A&&... a) {
+inline void tape_launch(const char* name, void (*k)(P...), dim3 g, dim3 b, uint32_t sh,
+                        hipStream_t s, A&&... a) {
   static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
   using Tup = std::tuple<std::decay_t<P>...>;
   Tup args(static_cast<std::decay_t<P>>(std::forward<A>(a))...);
   if (LaunchTape* t = tape_active()) {
-    t->ops.emplace_back([k, g, b, sh, args](hipStream_t st) mutable {
-      launch_from_tuple(k, g, b, sh, st, args, std::index_sequence_for<P...>{});
+    t->ops.emplace_back([name, k, g, b, sh, args](hipStream_t st) mutable {
+      launch_from_tuple(name, k, g, b, sh, st, args, std::index_sequence_for<P...>{});
     });
   }
-  launch_from_tuple(k, g, b, sh, s, args, std::index_sequence_for<P...>{});
+  launch_from_tuple(name, k, g, b, sh, s, args, std::index_sequence_for<P...>{});
+}
+
+inline void memset_checked(void* p, int v, size_t n, hipStream_t s) {
+  const hipError_t e = hipMemsetAsync(p, v, n, s);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    char msg[256];
+    std::snprintf(msg, sizeof(msg), "commeff: hipMemsetAsync of %zu bytes at %p failed: %s (%d)", n,
+                  p, hipGetErrorString(e), static_cast<int>(e));
+    throw std::runtime_error(msg);
+  }
 }
 
 inline void tape_memset(void* p, int v, size_t n, hipStream_t s) {
   if (LaunchTape* t = tape_active()) {
-    t->ops.emplace_back([p, v, n](hipStream_t st) { (void)hipMemsetAsync(p, v, n, st); });
+    t->ops.emplace_back([p, v, n](hipStream_t st) { memset_checked(p, v, n, st); });
   }
-  (void)hipMemsetAsync(p, v, n, s);
+  memset_checked(p, v, n, s);
 }
 
 }  // namespace commeff
 
 #define COMMEFF_LAUNCH(kernel, grid, block, shmem, stream, ...) \
-  ::commeff::tape_launch(kernel, grid, block, shmem, stream, ##__VA_ARGS__)
+  ::commeff::tape_launch(#kernel, kernel, grid, block, shmem, stream, ##__VA_ARGS__)

@@ -106,10 +106,29 @@ void host_read_copy_hip(at::Tensor dst, const at::Tensor& src) {
   launch_host_read_copy(dptr, dst.data_ptr(), static_cast<int64_t>(dst.nbytes()), stream_now());
 }
 
+// launch-status probe (launch.h): a launch the runtime rejects -- here more
+// dynamic LDS than a CU has -- raises a RuntimeError naming the kernel, grid,
+// block and LDS bytes
+void launch_probe_hip(at::Tensor out, int64_t lds_bytes) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 1, "launch_probe: int32 device out");
+  launch_probe(out.data_ptr<int32_t>(), static_cast<uint32_t>(lds_bytes), stream_now());
+}
+
+// CPU tensor: only on a machine without a HIP device, where the launch itself
+// must fail -- the same checked path, observable in the CPU test suite
+void launch_probe_cpu(at::Tensor out, int64_t lds_bytes) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  (void)hipGetLastError();
+  TORCH_CHECK(n == 0, "launch_probe: pass a device tensor on a machine with a GPU");
+  launch_probe(nullptr, static_cast<uint32_t>(lds_bytes), nullptr);
+}
+
 }  // namespace
 }  // namespace commeff
 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
+  m.def("launch_probe(Tensor(a!) out, int lds_bytes) -> ()");
   m.def("host_read_copy(Tensor(a!) dst, Tensor src) -> ()");
   m.def("topk_pack(Tensor idx, Tensor vals, Tensor? cmap=None, int m=1) -> Tensor");
   m.def("merge_packed(Tensor allp, int nl, int k) -> (Tensor, Tensor)");
@@ -121,6 +140,7 @@ TORCH_LIBRARY_IMPL(commeff, CPU, m) {
   m.impl("merge_packed", &commeff::merge_packed_cpu);
   m.impl("gather_i64", &commeff::gather_i64_cpu);
   m.impl("host_read_copy", [](at::Tensor dst, const at::Tensor& src) { dst.copy_(src); });
+  m.impl("launch_probe", &commeff::launch_probe_cpu);
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
@@ -128,4 +148,5 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("merge_packed", &commeff::merge_packed_hip);
   m.impl("gather_i64", &commeff::gather_i64_hip);
   m.impl("host_read_copy", &commeff::host_read_copy_hip);
+  m.impl("launch_probe", &commeff::launch_probe_hip);
 }

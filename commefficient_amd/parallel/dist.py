@@ -194,38 +194,54 @@ def h2d_into(out: torch.Tensor, x) -> torch.Tensor:
     return _RING.copy_into(t, out)
 
 
+def _all_reduce_impl(t: torch.Tensor):
+    if t.is_cuda and _CTX.backend == "gloo":
+        # gloo reads device memory without ordering against the stream
+        torch.cuda.current_stream().synchronize()
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+
 def all_reduce_(t: torch.Tensor) -> torch.Tensor:
     if _CTX.distributed:
         from . import tape
-        if tape.eager_step(lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM)):
-            return t  # recorded round (parallel/tape.py): runs at replay
-        if t.is_cuda and _CTX.backend == "gloo":
-            # gloo reads device memory without ordering against the stream
-            torch.cuda.current_stream().synchronize()
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        # a recorded round (parallel/tape.py) defers the SAME backend-aware
+        # call to its replay
+        if not tape.eager_step(lambda: _all_reduce_impl(t)):
+            _all_reduce_impl(t)
     return t
 
 
-def reduce_scatter_(out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
-    """out (this rank's 1/N of t, summed over ranks) = reduce-scatter of the
-    contiguous ``t`` (rank r gets elements [r n, (r+1) n), n = out.numel()).
-    gloo has no reduce-scatter: all-reduce + slice (same sums)."""
-    if not _CTX.distributed:
-        out.copy_(t.view(out.shape))
-        return out
-    from . import tape
-    if tape.eager_step(lambda: dist.reduce_scatter_tensor(out.view(-1), t.view(-1))):
-        return out  # recorded round (parallel/tape.py): runs at replay
+def _reduce_scatter_impl(out: torch.Tensor, t: torch.Tensor):
     if _CTX.backend == "gloo":
+        # gloo has no reduce-scatter: all-reduce + slice (same sums)
         if t.is_cuda:
             torch.cuda.current_stream().synchronize()
         full = t.clone()
         dist.all_reduce(full, op=dist.ReduceOp.SUM)
         n = out.numel()
         out.view(-1).copy_(full.view(-1)[_CTX.rank * n:(_CTX.rank + 1) * n])
-        return out
+        return
     dist.reduce_scatter_tensor(out.view(-1), t.view(-1))
+
+
+def reduce_scatter_(out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+    """out (this rank's 1/N of t, summed over ranks) = reduce-scatter of the
+    contiguous ``t`` (rank r gets elements [r n, (r+1) n), n = out.numel())."""
+    if not _CTX.distributed:
+        out.copy_(t.view(out.shape))
+        return out
+    from . import tape
+    if not tape.eager_step(lambda: _reduce_scatter_impl(out, t)):
+        _reduce_scatter_impl(out, t)
     return out
+
+
+def _all_gather_impl(out: torch.Tensor, t: torch.Tensor):
+    if t.is_cuda and _CTX.backend == "gloo":
+        torch.cuda.current_stream().synchronize()
+        dist.all_gather(list(out.chunk(_CTX.world_size)), t.contiguous())
+        return
+    dist.all_gather_into_tensor(out, t.contiguous())
 
 
 def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
@@ -236,14 +252,30 @@ def all_gather_rows(t: torch.Tensor) -> torch.Tensor:
     out = torch.empty((_CTX.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                       device=t.device)
     from . import tape
-    if tape.eager_step(lambda: dist.all_gather_into_tensor(out, t.contiguous())):
-        return out  # recorded round (parallel/tape.py): runs at replay
-    if t.is_cuda and _CTX.backend == "gloo":
-        torch.cuda.current_stream().synchronize()
-        chunks = list(out.chunk(_CTX.world_size))
-        dist.all_gather(chunks, t.contiguous())
-        return out
-    dist.all_gather_into_tensor(out, t.contiguous())
+    if not tape.eager_step(lambda: _all_gather_impl(out, t)):
+        _all_gather_impl(out, t)
+    return out
+
+
+def all_reduce_flag(bad: bool) -> bool:
+    """True on every rank when ``bad`` is True on any rank (a collective: a
+    decision that changes which collectives follow must be the same on all
+    ranks)."""
+    if not _CTX.distributed:
+        return bool(bad)
+    t = torch.tensor([1.0 if bad else 0.0],
+                     device=_CTX.device if _CTX.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item() > 0)
+
+
+def gather_objects(obj):
+    """Every rank's ``obj`` (a picklable, e.g. dict of CPU tensors), in rank
+    order, on rank 0 (None elsewhere).  A collective: every rank calls it."""
+    if not _CTX.distributed:
+        return [obj]
+    out = [None] * _CTX.world_size if _CTX.rank == 0 else None
+    dist.gather_object(obj, out, dst=0)
     return out
 
 

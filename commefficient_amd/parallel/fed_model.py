@@ -323,7 +323,8 @@ class FedModel:
         if N == 1:
             return clients
         if self.client_state.active:
-            return clients[clients % N == R]
+            # rows live on their owners: balanced ownership (state.py assign)
+            return self.client_state.assign(clients)
         W = len(clients)
         return clients[R * W // N:(R + 1) * W // N]
 
@@ -496,6 +497,7 @@ class FedModel:
                 self.last_round["sharded_server"] = True
         if dropped:
             self.last_round["dropped_clients"] = dropped
+        self.last_round["local_clients"] = len(mine)
         return [metrics[i] for i in range(n_res)] + [dl, ul]
 
     # ------------------------------------------------------- recorded rounds
@@ -516,12 +518,16 @@ class FedModel:
                 or self._n_metrics is None
                 or (self.ctx.world_size > 1 and a.mode != "sketch")):
             return None
-        key = (id(getattr(rb.device_gather, "__self__", rb.device_gather)), n_local, W, B)
+        src = getattr(rb.device_gather, "__self__", rb.device_gather)
+        key = (id(src), n_local, W, B)
         if key in self._tapes.failed:
             return None
         e = self._tape_entries.get(key)
         if e is None:
-            self._tape_entries[key] = e = {"key": key, "seen": 0, "compute": None, "server": None}
+            # the entry holds the source: its id (and the dataset buffers the
+            # tape's raw pointers name) cannot be reused while the tape lives
+            self._tape_entries[key] = e = {"key": key, "seen": 0, "compute": None, "server": None,
+                                           "src": src}
         e["seen"] += 1
         return e if e["seen"] >= 2 else None
 
@@ -1015,9 +1021,9 @@ class FedModel:
             out.add_(transmit.view(-1))
 
     def _assign_counts(self, clients: np.ndarray):
+        # (the balanced client-state ownership gives every rank the same count
+        # as the contiguous split: state.py assign)
         N = self.ctx.world_size
-        if self.client_state.active:
-            return [int(np.sum(clients % N == r)) for r in range(N)]
         W = len(clients)
         return [(r + 1) * W // N - r * W // N for r in range(N)]
 
@@ -1271,6 +1277,16 @@ class FedModel:
         return loss, mets, delta
 
     # -------------------------------------------------------------- server
+    def _nonfinite(self, G: torch.Tensor) -> bool:
+        """Whether the round's aggregate holds a NaN / Inf.  With the sharded
+        server each rank holds only its reduce-scattered groups of the table,
+        so the decision is all-reduced: a rank that skipped while the others
+        entered the server's all-gather would pair the collectives wrongly."""
+        bad = not bool(torch.isfinite(G).all())
+        if self.shard_server:
+            bad = dist.all_reduce_flag(bad)
+        return bad
+
     def server_step(self, lr):
         if self.args.mode == "fedavg":
             # FedOptimizer.step writes g_lr before anything else
@@ -1291,7 +1307,7 @@ class FedModel:
             if ok:
                 self.round_idx += 1
                 return
-        if getattr(self.args, "skip_nonfinite", 0) and not bool(torch.isfinite(G).all()):
+        if getattr(self.args, "skip_nonfinite", 0) and self._nonfinite(G):
             # failure detection: a NaN/Inf in the aggregate (a diverged or faulty
             # client) would poison V, E and the weights for good -> drop the round
             self.skipped_rounds += 1
@@ -1347,6 +1363,9 @@ class FedModel:
         return out
 
     def fed_state_dict(self):
+        """The resumable engine state.  A collective on > 1 rank (the sharded
+        server's V / E and the per-client rows are gathered): every rank calls
+        it; only rank 0's result is complete."""
         return {"round_idx": self.round_idx, "fedavg_lr": self.fedavg_lr,
                 "server": self.server.state_dict(), "accountant": self.accountant.state_dict(),
                 "client_state": self.client_state.state_dict(), "w": self.w.cpu(),

@@ -6,8 +6,13 @@ Reference: client state lives in host shared memory as ``[C, d]`` arrays
 worker updates are made on ``.to(device)`` *copies* and lost
 (fed_worker.py:169-174).  Here rows are written
 back, live in HBM when they fit (288 GB per MI355X) and are allocated lazily
-on first participation, each row owned by rank ``client % world_size`` (the
-engine assigns a client's work to its owner whenever client state exists).
+on first participation on the rank that owns the client.  Ownership is
+balanced per round (``assign``): every client has a home rank (initially
+``client % world``); when a round's clients would load the ranks unevenly,
+the surplus clients of the fuller ranks move to the emptier ones -- clients
+without state first -- and the moved clients' rows travel with them (one
+batched point-to-point exchange), so per-rank work differs by at most one
+client, as with the reference's even chunking (fed_aggregator.py:230-237).
 
 Byte accounting reproduces fed_aggregator.py:170-299 exactly in both of the
 reference's regimes with one mechanism: a per-coordinate ``last_mod`` round
@@ -65,6 +70,11 @@ class ClientStateStore:
         self._next = 0
         self._staged: Dict[tuple, tuple] = {}
         self._copy_stream = None
+        # replicated on every rank (identical updates): home rank of every client
+        # that was ever assigned, and the clients that hold rows
+        self.home: Dict[int, int] = {}
+        self.seen: set = set()
+        self.migrated = 0  # rows moved between ranks so far (diagnostics)
 
     @property
     def host_tier(self) -> bool:
@@ -91,10 +101,13 @@ class ClientStateStore:
                 row = self.rows[kind].get(c)
                 if row is None:
                     continue  # first participation: created on the device side by get()
-                dev = torch.empty(self.d, device=self.compute_device)
                 # (the row's previous write-back, on the compute stream, lands first)
                 self._copy_stream.wait_stream(cur)
                 with torch.cuda.stream(self._copy_stream):
+                    # allocated on the copy stream: a staged copy dropped before
+                    # get() (begin_round's clear) returns its block to THIS
+                    # stream's pool, ordered behind the copy still writing it
+                    dev = torch.empty(self.d, device=self.compute_device)
                     dev.copy_(row, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self._copy_stream)
@@ -105,7 +118,83 @@ class ClientStateStore:
         return bool(self.kinds)
 
     def owner(self, client: int) -> int:
-        return int(client) % self.world
+        c = int(client)
+        return self.home.get(c, c % self.world)
+
+    def assign(self, clients) -> np.ndarray:
+        """This rank's share of the round's ``clients`` (sorted unique,
+        identical on every rank).  Per-rank counts differ by at most one.  A
+        collective when rows have to move: every rank calls it once per round."""
+        clients = np.asarray(clients, dtype=np.int64)
+        N, R = self.world, self.rank
+        if N == 1:
+            self.seen.update(int(c) for c in clients)
+            return clients
+        W = len(clients)
+        target = [(r + 1) * W // N - r * W // N for r in range(N)]  # = the stateless split
+        by_rank = [[] for _ in range(N)]
+        for c in clients:
+            by_rank[self.owner(c)].append(int(c))
+        surplus = []
+        for r in range(N):
+            extra = len(by_rank[r]) - target[r]
+            if extra > 0:
+                # release clients without state first (nothing to move), then the
+                # highest ids; deterministic on every rank
+                cand = sorted(by_rank[r], key=lambda c: (c in self.seen, -c))
+                out = cand[:extra]
+                by_rank[r] = [c for c in by_rank[r] if c not in set(out)]
+                surplus += [(c, r) for c in out]
+        moves = []  # (client, src, dst) of clients that hold rows
+        si = 0
+        for r in range(N):
+            while len(by_rank[r]) < target[r]:
+                c, src = surplus[si]
+                si += 1
+                by_rank[r].append(c)
+                self.home[c] = r
+                if c in self.seen:
+                    moves.append((c, src, r))
+        for r in range(N):
+            for c in by_rank[r]:
+                self.home.setdefault(c, r)
+        if moves:
+            self._migrate(moves)
+        self.seen.update(int(c) for c in clients)
+        return np.array(sorted(by_rank[R]), dtype=np.int64)
+
+    def _migrate(self, moves):
+        """Send the rows of the moved clients from their old to their new home
+        (one batched isend / irecv exchange; RCCL needs device buffers)."""
+        import torch.distributed as tdist
+        from . import dist as _dist
+        ctx = _dist.ctx()
+        dev = self.compute_device if ctx.backend == "nccl" else torch.device("cpu")
+        p2p, recv = [], []
+        for (c, src, dst) in moves:
+            for kind in self.kinds:
+                if self.rank == src:
+                    row = self.rows[kind].pop(c, None)
+                    if row is None:  # (seen but never materialised: zeros)
+                        row = self.init_weights if kind == "weights" else torch.zeros(self.d)
+                    buf = row.to(dev)
+                    p2p.append(tdist.P2POp(tdist.isend, buf.contiguous(), dst))
+                elif self.rank == dst:
+                    buf = torch.empty(self.d, device=dev)
+                    p2p.append(tdist.P2POp(tdist.irecv, buf, src))
+                    recv.append((kind, c, buf))
+        self.migrated += len(moves)
+        if not p2p:
+            return
+        if dev.type == "cuda" and ctx.backend == "gloo":
+            torch.cuda.current_stream().synchronize()
+        for req in tdist.batch_isend_irecv(p2p):
+            req.wait()
+        for kind, c, buf in recv:
+            pin = self.store_device.type == "cpu" and self.compute_device.type == "cuda"
+            row = torch.empty(self.d, device=self.store_device, pin_memory=pin)
+            row.copy_(buf)
+            self.rows[kind][c] = row
 
     def get(self, kind: str, client: int) -> Optional[torch.Tensor]:
         """Device tensor for the row (created on first use).  For CPU-resident
@@ -128,6 +217,7 @@ class ClientStateStore:
             if hit is not None:
                 dev, ev = hit
                 torch.cuda.current_stream(self.compute_device).wait_event(ev)
+                # the compute stream uses a copy-stream block from here on
                 dev.record_stream(torch.cuda.current_stream(self.compute_device))
                 if self.host_tier:
                     self._advance()
@@ -161,12 +251,31 @@ class ClientStateStore:
                 row[idx.to(row.device)] = 0
 
     def state_dict(self):
-        return {k: {c: t.cpu() for c, t in v.items()} for k, v in self.rows.items()}
+        """Every rank's rows (a collective on > 1 rank: the rows live on their
+        owners; rank 0 receives the union, the other ranks None)."""
+        from . import dist as _dist
+        own = {k: {c: t.cpu() for c, t in v.items()} for k, v in self.rows.items()}
+        if self.world == 1:
+            return own
+        parts = _dist.gather_objects(own)
+        if parts is None:
+            return None
+        out = {k: {} for k in self.rows}
+        for p in parts:
+            for k, v in p.items():
+                out.setdefault(k, {}).update(v)
+        return out
 
     def load_state_dict(self, sd):
+        """Keep the rows this rank owns (home ``client % world`` after a resume:
+        any world size can resume any checkpoint)."""
+        self.home = {}
+        self.seen = set()
         for k, v in sd.items():
             if k in self.rows:
-                self.rows[k] = {int(c): t.to(self.store_device) for c, t in v.items()}
+                self.seen.update(int(c) for c in v)
+                self.rows[k] = {int(c): t.to(self.store_device) for c, t in v.items()
+                                if self.owner(int(c)) == self.rank}
 
 
 class ByteAccountant:

@@ -296,6 +296,9 @@ def restore_driver_state(sd: dict, loader, sched) -> dict:
 
 
 def save_checkpoint(model: FedModel, args, progress=None):
+    # every rank joins the gathers of the sharded server state and the
+    # per-client rows; rank 0 writes
+    fs = model.fed_state_dict()
     if not dist.ctx().is_main:
         return
     path = args.checkpoint_path + args.model + ".pt"
@@ -303,7 +306,6 @@ def save_checkpoint(model: FedModel, args, progress=None):
     if d:
         os.makedirs(d, exist_ok=True)
     torch.save(model.state_dict(), path)
-    fs = model.fed_state_dict()
     fs["driver"] = driver_state(progress)
     torch.save(fs, args.checkpoint_path + args.model + ".fedstate.pt")
     print("saved", path)

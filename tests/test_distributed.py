@@ -68,10 +68,17 @@ def _run(rank, world, port, mode, out_dir, rounds):
     opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05), args, fed)
     it = iter(loader)
     losses = []
+    local = []
     for _ in range(rounds):
-        loss, acc, dl, ul = fed(next(it))
+        try:
+            b = next(it)
+        except StopIteration:  # next epoch
+            it = iter(loader)
+            b = next(it)
+        loss, acc, dl, ul = fed(b)
         opt.step()
         losses.append(loss.clone())
+        local.append(fed.last_round["local_clients"])
     if mode.endswith("_sparse"):
         assert fed.last_round.get("sparse_allgather"), fed.last_round
     if mode == "sketch_sharded" and world > 1:
@@ -82,7 +89,8 @@ def _run(rank, world, port, mode, out_dir, rounds):
         assert fed.last_round.get("buckets_during_backward", 0) >= 1, fed.last_round
     sd = fed.server.state_dict()  # (sharded: gathered into the row-major format)
     torch.save({"w": fed.w.clone(), "loss": torch.cat([l.reshape(-1) for l in losses]),
-                "dl": fed.accountant.client_download.clone(), "V": sd["V"], "E": sd["E"]},
+                "dl": fed.accountant.client_download.clone(), "V": sd["V"], "E": sd["E"],
+                "local": torch.tensor(local), "migrated": fed.client_state.migrated},
                os.path.join(out_dir, f"r{rank}_w{world}.pt"))
     dist.shutdown()
 
@@ -257,3 +265,96 @@ def test_overlap_reducer_moves_replica_grads():
         a, b = torch.load(os.path.join(d, "ovl.pt"), weights_only=True)
     assert a.abs().sum() > 0
     torch.testing.assert_close(a, b)
+
+
+def test_client_state_ownership_balanced_three_ranks():
+    """Per-client state (local error + momentum) on 3 gloo ranks: every round
+    gives each rank W/3 +- 1 clients (balanced ownership, state.py assign; the
+    reference chunks clients evenly, fed_aggregator.py:230-237), the moved
+    clients' rows travel with them, and the run equals the single process."""
+    rounds = 14  # 84 participations of 40 clients: returning clients must move
+    mode = "local_topk"
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_run, args=(3, _free_port(), mode, d, rounds), nprocs=3,
+                           start_method="spawn", join=True)
+        mp.start_processes(_run, args=(1, _free_port(), mode, d, rounds), nprocs=1,
+                           start_method="spawn", join=True)
+        rs = [torch.load(os.path.join(d, f"r{r}_w3.pt"), weights_only=True) for r in range(3)]
+        s = torch.load(os.path.join(d, "r0_w1.pt"), weights_only=True)
+    counts = torch.stack([r["local"] for r in rs])  # [rank, round]
+    assert (counts.max(0).values - counts.min(0).values <= 1).all(), counts
+    assert rs[0]["migrated"] > 0, "the sampled rounds never needed a move (test too weak)"
+    for r in rs[1:]:
+        assert torch.equal(rs[0]["w"], r["w"]), "replicas diverged"
+    torch.testing.assert_close(rs[0]["w"], s["w"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rs[0]["loss"], s["loss"], rtol=1e-4, atol=1e-5)
+
+
+def _ckpt_worker(rank, world, port, out_dir, what):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(2)
+    from commefficient_amd import models
+    from commefficient_amd.data import make_synthetic
+    from commefficient_amd.data.device_loader import DeviceFedLoader
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.parallel.server import FedOptimizer
+    from commefficient_amd.train.cv import save_checkpoint
+    from commefficient_amd.train.losses import cv_loss
+    from commefficient_amd.utils.args import parse_args
+    dist.init("cpu")
+    argv = ["--mode", "sketch", "--device", "cpu", "--dtype", "fp32", "--num_clients", "40",
+            "--num_workers", "6", "--local_batch_size", "-1", "--dataset_name", "CIFAR10",
+            "--synthetic", "--error_type", "virtual", "--local_momentum", "0",
+            "--virtual_momentum", "0.9", "--k", "300", "--num_rows", "3", "--num_cols", "20000",
+            "--shard_unsketch", "on", "--checkpoint_path", os.path.join(out_dir, "ck_"),
+            "--skip_nonfinite", "1"]
+    args = parse_args(argv=argv, probe_port=False)
+    torch.manual_seed(0)
+    model = models.ResNet9(channels={"prep": 4, "layer1": 8, "layer2": 8, "layer3": 16})
+    ds = make_synthetic("CIFAR10", train=True, num_clients=40, size=160, seed=3)
+    loader = DeviceFedLoader(ds, 6, -1, "cpu", seed=5, augment=True)
+    fed = FedModel(model, cv_loss, args, num_clients=40)
+    opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05), args, fed)
+    assert fed.shard_server
+    it = iter(loader)
+    for r in range(3):
+        fed(next(it))
+        if what == "nonfinite" and r == 1 and rank == 1:
+            # a NaN that lands in ONE rank's reduce-scattered groups only
+            fed._pending[0].view(-1)[-1] = float("nan")
+        opt.step()
+    if what == "nonfinite":
+        assert fed.skipped_rounds == 1, fed.skipped_rounds  # on EVERY rank
+    else:
+        save_checkpoint(fed, args, {"epoch": 0, "iter": 3})  # every rank calls it
+    torch.save({"w": fed.w.clone(), "V": fed.server.state_dict()["V"]},
+               os.path.join(out_dir, f"{what}_r{rank}.pt"))
+    dist.shutdown()
+
+
+def test_checkpoint_sharded_server_two_ranks():
+    """save_checkpoint with the sharded server on 2 ranks: the gathers of V / E
+    run on every rank (no hang) and the file holds the full row-major state."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ckpt_worker, args=(2, _free_port(), d, "ckpt"), nprocs=2,
+                           start_method="spawn", join=True)
+        ck = torch.load(os.path.join(d, "ck_ResNet9.fedstate.pt"), weights_only=True)
+        r0 = torch.load(os.path.join(d, "ckpt_r0.pt"), weights_only=True)
+    assert ck["server"]["V"].shape == (3, 20000)
+    assert torch.equal(ck["server"]["V"], r0["V"])
+    assert torch.equal(ck["w"], r0["w"])
+
+
+def test_skip_nonfinite_decided_globally_two_ranks():
+    """A NaN in one rank's shard of the sharded server's table makes EVERY
+    rank skip the round (an all-reduced flag), so the collectives stay paired
+    and the replicas stay identical."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ckpt_worker, args=(2, _free_port(), d, "nonfinite"), nprocs=2,
+                           start_method="spawn", join=True)
+        r0 = torch.load(os.path.join(d, "nonfinite_r0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "nonfinite_r1.pt"), weights_only=True)
+    assert torch.equal(r0["w"], r1["w"])
+    assert torch.isfinite(r0["w"]).all()
