@@ -142,6 +142,9 @@ void launch_merge_packed(const int64_t* allp, int nl, int64_t k, float* vals, in
 void launch_gather_i64(const int64_t* src, const int64_t* pos, int64_t n, int64_t* out, hipStream_t stream);
 // dst (device) = n bytes read by a kernel from pinned host memory (its device mapping)
 void launch_host_read_copy(const void* host_src, void* dst, int64_t n, hipStream_t stream);
+// one-block kernel launched with ``lds_bytes`` of dynamic LDS (writes 64 to
+// out[0]): exercises the launch status check (launch.h)
+void launch_probe(int32_t* out, uint32_t lds_bytes, hipStream_t stream);
 // out[0] = sqrt(lower-median_j sum_c table[j,c]^2); partial: >= r*256 floats
 void launch_cs_l2estimate(const float* table, int r, int64_t c, float* partial,
                           float* out, hipStream_t stream);
@@ -294,6 +297,9 @@ struct ConvWgradArgs {
 bool conv3x3_supported(int C, int K);
 bool conv3x3_pool_supported(int H, int W, int K);
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
+// the streamed forward / dgrad kernel (conv_stream.hip); false when the shape
+// is not one it serves
+bool launch_conv3x3_stream(const ConvFwdArgs& a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
