@@ -717,223 +717,6 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   }
 }
 
-// ------------------------------------------- fwd / dgrad, persistent halo
-// The halo kernel above runs one 256-pixel tile per block, two blocks per
-// CU, and the whole grid is ONE wave of tiles at the ResNet-9 bench batch
-// (500 tiles for 512 slots): every block loads its first window, computes,
-// reloads the next channel block's window (the wait fully exposed) and
-// stores its tile at the same moment as every other block, so the HBM /
-// L2 phases never overlap the MFMA phases (bench_conv.py: res1 forward 843
-// TF/s at 500 images vs 957 at 2,000, where later tile waves are staggered).
-//
-// Here one 8-wave block per CU (144 KB LDS: two 48 KB windows + a 3-slot
-// weight ring) walks a static list of tiles (tile = block + i * grid) as one
-// continuous K-step stream:
-//   * the NEXT window (the next channel block of this tile, or the next
-//     tile's first) is staged into the other window buffer while the current
-//     one is read, 9 K-steps ahead of its use;
-//   * weight tiles B(g) go through a 3-slot ring issued two K-steps ahead,
-//     across tile boundaries; a K-step waits only for its own B(g) (counted
-//     vmcnt, raw s_barrier: the later loads stay in flight);
-//   * the epilogue stages the fp32 tile through the window buffer it has just
-//     finished reading, in 64-row passes, while the next tile's window and
-//     first weight tiles are already in flight.
-// One barrier per K-step orders the LDS-DMA data for every wave (each wave
-// waits for its own pieces first) and retires the ring slot / window buffer
-// that the step's new loads overwrite (last read one step, or one window,
-// earlier).
-template <int BN>
-struct PipeCfg {
-  static constexpr int TBM = 256, NT = 512, WIN = HaloCfg<256>::kWinBytes;
-  static constexpr int WLD = HaloCfg<256>::kWinLd;        // window pieces per thread (6)
-  static constexpr int RING = 3 * BN * 128;               // 3 weight slots
-  static constexpr int LDS = 2 * WIN + RING;              // [win0][ring][win1]
-  static constexpr int BLD = BN * 8 / NT;                 // weight pieces per thread per K-step
-};
-
-template <bool POOL, int BN>
-__global__ void __launch_bounds__(512) conv_fwd_pipe_kernel(ConvFwdArgs a, HaloGeom hg, int ntiles) {
-  using Cfg = PipeCfg<BN>;
-  constexpr int NT = Cfg::NT, NI = BN / 64, BLD = Cfg::BLD, WLD = Cfg::WLD;
-  static_assert(BLD >= 1, "weight pieces");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // window buffer b: smem + b * (WIN + RING)
-  auto win_buf = [&](int b) __attribute__((always_inline)) { return smem + b * (Cfg::WIN + Cfg::RING); };
-  unsigned char* const ring = smem + Cfg::WIN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1, hi = lane >> 5, lr = lane & 31;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int grid = gridDim.x;
-  const int my_tiles = bid < ntiles ? (ntiles - 1 - bid) / grid + 1 : 0;
-  const int C = a.C, H = a.H, W = a.W, HW = H * W;
-  const int CB = C >> 6, NS = 9 * CB;
-  const int ntn = a.K / BN;
-  const int nimg = a.P / HW;
-  const int total = my_tiles * NS;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_conv_zero);
-
-  // window (tile ti (local index), channel block cb) -> window buffer wbuf
-  auto issue_window = [&](int ti, int cb, unsigned char* wbuf) __attribute__((always_inline)) {
-    const int t = bid + ti * grid;
-    const int m0 = (t / ntn) * Cfg::TBM;
-    const int img0 = m0 / HW, h0 = (m0 - img0 * HW) / W;
-#pragma unroll
-    for (int i = 0; i < WLD; ++i) {
-      const int sl = i * NT + tid;
-      const int row = sl >> 3;
-      const uint16_t* src = zero;
-      if (row < hg.NPW) {
-        const int pr = row / hg.PW, pc = row - pr * hg.PW, w = pc - 1;
-        const int lc = (sl & 7) ^ sw_halo(pr, pc, hg);
-        int img = img0, h = h0 + pr - 1;
-        if (hg.G > 1) {
-          const int q = pr / (hg.Rg + 1), rr = pr - q * (hg.Rg + 1);
-          img = img0 + q;
-          h = rr - 1;
-        }
-        if (img < nimg && h >= 0 && h < H && w >= 0 && w < W)
-          src = a.x + static_cast<size_t>((img * H + h) * W + w) * C + cb * 64 + lc * 8;
-      }
-      // pieces past the window land in the buffer's unused tail (every wave
-      // issues WLD pieces: a constant vmcnt count)
-      glds16(src, wbuf + i * NT * 16 + wid * 1024);
-    }
-  };
-  // weight tile of global K-step g -> ring slot g % 3
-  auto issue_b = [&](int g) __attribute__((always_inline)) {
-    const int ti = g / NS, ls = g - ti * NS;
-    const int t = bid + ti * grid;
-    const int n0 = (t % ntn) * BN;
-    const int cb = ls / 9, tap = ls - cb * 9;
-    unsigned char* base = ring + (g % 3) * (BN * 128) + wid * 1024;
-#pragma unroll
-    for (int j = 0; j < BLD; ++j) {
-      const int sl = j * NT + tid;
-      const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
-      glds16(a.w + static_cast<size_t>(n0 + row) * 9 * C + tap * C + cb * 64 + lc * 8, base + j * NT * 16);
-    }
-  };
-
-  int offB[4][NI];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const int chk = 2 * kk + hi;
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int row = wc * (BN / 2) + ni * 32 + lr;
-      offB[kk][ni] = row * 128 + ((chk ^ sw_rd128(row)) << 4);
-    }
-  }
-  // this lane's output pixels -> padded window rows (same in every tile: the
-  // tile is whole image rows)
-  int pbr[2], pbc[2];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi) {
-    const int m = wr * 64 + mi * 32 + lr;
-    const int g = m / (hg.Rg * W), rem = m - g * hg.Rg * W;
-    const int r = rem / W, w = rem - r * W;
-    pbr[mi] = g * (hg.Rg + 1) + r + 1;
-    pbc[mi] = w + 1;
-  }
-
-  if (total > 0) {
-    issue_window(0, 0, win_buf(0));
-    issue_b(0);
-    if (total > 1) issue_b(1);
-  }
-  f32x16_t acc[2][NI];
-  int wn = 0;  // window counter (buffer wn & 1)
-  for (int g = 0; g < total; ++g) {
-    const int ti = g / NS, ls = g - ti * NS;
-    const int cb = ls / 9, tap = ls - cb * 9;
-    if (ls == 0) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
-    }
-    // B(g) and the current window landed: everything issued after B(g) may
-    // stay in flight -- the window of step g-1 (if it staged one) and B(g+1)
-    const bool more = g + 1 < total;
-    const bool win_prev = tap == 1 && (cb + 1 < CB || ti + 1 < my_tiles);
-    if (ls == 0) wait_vmcnt<0>();
-    else if (win_prev && more) wait_vmcnt<WLD + BLD>();
-    else if (win_prev) wait_vmcnt<WLD>();
-    else if (more) wait_vmcnt<BLD>();
-    else wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (tap == 0) {
-      // the next window goes into the buffer read one window ago (or staged
-      // the previous tile's epilogue): retired by this barrier
-      if (cb + 1 < CB) issue_window(ti, cb + 1, win_buf((wn + 1) & 1));
-      else if (ti + 1 < my_tiles) issue_window(ti + 1, 0, win_buf((wn + 1) & 1));
-    }
-    if (g + 2 < total) issue_b(g + 2);
-    const unsigned char* sW = win_buf(wn & 1);
-    const unsigned char* sB = ring + (g % 3) * (BN * 128);
-    const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-    int bA[2];  // sub-step 0 A offsets; sub-step kk: ^ (kk << 5) (chunk bits 5-6)
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int pr = pbr[mi] + dr, pc = pbc[mi] + dc;
-      bA[mi] = (pr * hg.PW + pc) * 128 + ((hi ^ sw_halo(pr, pc, hg)) << 4);
-    }
-    // double-buffered fragments, MFMAs interleaved one-for-one with the next
-    // sub-step's reads (as the halo kernel's DB loop)
-    bf16x8_t fa0[2], fb0[NI], fa1[2], fb1[NI];
-    auto load = [&](int kk, bf16x8_t (&fa)[2], bf16x8_t (&fb)[NI]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) fa[mi] = *reinterpret_cast<const bf16x8_t*>(sW + (bA[mi] ^ (kk << 5)));
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) fb[ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[kk][ni]);
-    };
-    auto mma = [&](const bf16x8_t (&fa)[2], const bf16x8_t (&fb)[NI]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi], fb[ni], acc[mi][ni], 0, 0, 0);
-    };
-    auto interleave = [&]() __attribute__((always_inline)) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-    };
-    load(0, fa0, fb0);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fa0, fb0);
-    load(1, fa1, fb1);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fa1, fb1);
-    load(2, fa0, fb0);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fa0, fb0);
-    load(3, fa1, fb1);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    mma(fa1, fb1);
-    if (tap == 8) {
-      if (cb + 1 == CB) {
-        // tile done: stage through the window just finished (every wave is
-        // past its reads after this barrier)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        const int t = bid + ti * grid;
-        conv_fwd_epilogue<256, BN, POOL, NT, 64>(a, acc, win_buf(wn & 1), (t / ntn) * Cfg::TBM,
-                                                 (t % ntn) * BN, tid, wr, wc, hi, lr);
-      }
-      ++wn;
-    }
-  }
-}
-
 // ------------------------------------------------------------------ wgrad
 // pixel range [pbeg, pend) of one split: consecutive steps_per_split * BK
 // pixels, or (grouped) the split's share of its group's pixels -- rows past
@@ -1858,19 +1641,6 @@ void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t strea
                    dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
 }
 
-template <bool POOL, int BN>
-void launch_fwd_pipe(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
-  constexpr int lds = PipeCfg<BN>::LDS;
-  static bool init = false;
-  if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_pipe_kernel<POOL, BN>), lds);
-    init = true;
-  }
-  const int ntiles = ((a.P + 255) / 256) * (a.K / BN);
-  const int grid = ntiles < cu_count() ? ntiles : cu_count();
-  COMMEFF_LAUNCH((conv_fwd_pipe_kernel<POOL, BN>), dim3(grid), dim3(512), lds, stream, a, hg, ntiles);
-}
-
 // Grouped conv on channel-stacked images (a.kg, a.x_stride set): the halo
 // kernels only, no fused epilogue.  Returns false when the geometry has no
 // halo tiling (the caller falls back to a stock grouped convolution).
@@ -1902,13 +1672,11 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
     return e != nullptr ? atoi(e) : 0;
   }();
   a.ablate = ablate;
-  // COMMEFF_CONV_PIPE=1: the persistent pipelined kernel (off by default: one
-  // 8-wave block per CU lost to two co-resident one-tile blocks, 1.91 vs 1.68
-  // ms per ResNet-9 round -- profiles/r4_experiments.md)
-  static const int pipe_on = [] {
-    const char* e = getenv("COMMEFF_CONV_PIPE");
-    return e != nullptr ? atoi(e) : 0;
+  static const bool stream_on = [] {  // COMMEFF_CONV_STREAM=0: the per-tile halo kernels below
+    const char* e = getenv("COMMEFF_CONV_STREAM");
+    return !(e != nullptr && e[0] == '0');
   }();
+  if (stream_on && launch_conv3x3_stream(a, stream)) return;
   static const bool halo_on = [] {  // COMMEFF_CONV_HALO=0: the per-tap tile kernel
     const char* e = getenv("COMMEFF_CONV_HALO");
     return !(e != nullptr && e[0] == '0');
@@ -1918,15 +1686,6 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
     return e != nullptr ? atoi(e) : 256;
   }();
   HaloGeom hg;
-  // persistent pipelined halo kernel: whenever the 256-pixel tiles give every
-  // CU at least one (ResNet-9: all but res3, whose 8 K-step windows per tile
-  // keep the split kernel below)
-  // (COMMEFF_CONV_PIPE=2: whenever the geometry fits, for tests at small batches)
-  if (halo_on && pipe_on && halo_geom(a.H, a.W, a.K, 256, &hg) &&
-      (pipe_on == 2 || static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) >= cu_count())) {
-    if (a.pool == 2) launch_fwd_pipe<true, 128>(a, hg, stream); else launch_fwd_pipe<false, 128>(a, hg, stream);
-    return;
-  }
   // 256-pixel tiles when they still give ~every resident slot (2 per CU) a block
   if (halo_on && halo_tbm == 256 && halo_geom(a.H, a.W, a.K, 256, &hg) &&
       static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) * 10 >= wgrad_slots() * 9) {

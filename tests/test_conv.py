@@ -723,12 +723,12 @@ def test_kept_conv_images_match_fresh_prep(mode):
 @pytest.mark.parametrize("N,C,H,K", [(500, 64, 32, 128), (500, 128, 16, 128), (500, 128, 16, 256),
                                      (500, 256, 8, 512), (500, 256, 16, 128), (300, 512, 8, 256)])
 @pytest.mark.parametrize("epi", ["plain", "relu", "mask_add", "pool"])
-def test_persistent_halo_kernel_bench_batches(N, C, H, K, epi):
-    """The persistent pipelined halo kernel (``conv_fwd_pipe_kernel``: one
-    8-wave block per CU walking several 256-pixel tiles, next window and two
-    weight tiles in flight) at the ResNet-9 bench batch, where it is the one
-    the dispatcher picks, for every fused epilogue; (300, 512, 8, 256) has
-    fewer tiles than CUs (one tile per block, window double-buffering only)."""
+def test_stream_kernel_bench_batches(N, C, H, K, epi):
+    """The streamed conv kernel (``conv_stream_kernel``: workgroups walking
+    several 256-pixel tiles as one K-step stream, next window and weight
+    tiles in flight, register epilogue) at the ResNet-9 bench batch, where the
+    dispatcher picks it, for every fused epilogue; (300, 512, 8, 256) has
+    fewer tiles than slots (one tile per workgroup)."""
     x, w = _inputs(N, C, H, H, K, seed=N + C)
     wf, _ = ops.conv_weight_prep(w)
     ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
