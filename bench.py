@@ -130,15 +130,16 @@ def main():
         out = step(i)
         if b.check_every and N > 1 and (i + 1) % b.check_every == 0:
             dist.check_replicas(fed.w)
-    torch.cuda.synchronize()
-    # host-side bookkeeping BEFORE the barrier, so the timed rounds start right
-    # after it (the GPU idles through whatever runs between)
-    first_loss = float(out[0].mean().item())
-    dl_before = float(fed.accountant.client_download.sum().item())
+    # no host bookkeeping between the warmup and the timed rounds: the values
+    # read afterwards are device snapshots taken here (no sync), so the GPU
+    # idles only for the synchronize / barrier round trip (an idle GPU drops
+    # its clock, and the first timed rounds then run slower)
+    tw = time.perf_counter()  # end of the warmup enqueue
+    first_loss_t = out[0].mean().clone()
+    dl_before_t = fed.accountant.client_download.sum().clone()
     if fed.timer.enabled:
-        fed.timer.summary()
-        fed.timer.totals.clear()
-        fed.timer.counts.clear()
+        fed.timer.discard()
+    torch.cuda.synchronize()
     g0 = time.perf_counter()
     dist.barrier()
     torch.cuda.synchronize()
@@ -166,8 +167,9 @@ def main():
     if b.check_every:
         # the replicated weights must be bitwise identical on every rank
         checksum = dist.check_replicas(fed.w)
+    first_loss = float(first_loss_t.item())
     last_loss = float(out[0].mean().item())
-    dl = (float(fed.accountant.client_download.sum().item()) - dl_before) / b.steps
+    dl = (float(fed.accountant.client_download.sum().item()) - float(dl_before_t.item())) / b.steps
     if b.torch_profile:
         from torch.profiler import ProfilerActivity, profile
         stack = bool(os.environ.get("COMMEFF_PROF_STACK"))
@@ -221,6 +223,9 @@ def main():
             **({"rehearsal": "gloo, ranks sharing one GPU"} if rehearsal and N > 1 else {}),
             "host_enqueue_ms_per_step": round(host_s / b.steps * 1000.0, 3),
             "barrier_before_timed_ms": round(gap_ms, 3),
+            # host time from the last warmup enqueue to the first timed one
+            # (includes the GPU draining the queued warmup rounds)
+            "warmup_to_timed_ms": round((t0 - tw) * 1000.0, 3),
             **({"round_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(evs) - 1)]}
                if evs else {}),
         }), flush=True)

@@ -1672,11 +1672,6 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
     return e != nullptr ? atoi(e) : 0;
   }();
   a.ablate = ablate;
-  static const bool stream_on = [] {  // COMMEFF_CONV_STREAM=0: the per-tile halo kernels below
-    const char* e = getenv("COMMEFF_CONV_STREAM");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  if (stream_on && launch_conv3x3_stream(a, stream)) return;
   static const bool halo_on = [] {  // COMMEFF_CONV_HALO=0: the per-tap tile kernel
     const char* e = getenv("COMMEFF_CONV_HALO");
     return !(e != nullptr && e[0] == '0');

@@ -297,9 +297,6 @@ struct ConvWgradArgs {
 bool conv3x3_supported(int C, int K);
 bool conv3x3_pool_supported(int H, int W, int K);
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
-// the streamed forward / dgrad kernel (conv_stream.hip); false when the shape
-// is not one it serves
-bool launch_conv3x3_stream(const ConvFwdArgs& a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);

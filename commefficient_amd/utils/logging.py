@@ -129,6 +129,12 @@ class PhaseTimer:
             self.enabled = True
             self.only = set(names)
 
+    def discard(self) -> None:
+        """Drop the recorded (unresolved) events and the totals, without a sync."""
+        self._pending.clear()
+        self.totals.clear()
+        self.counts.clear()
+
     def summary(self) -> Dict[str, float]:
         import torch
         if not self.enabled:

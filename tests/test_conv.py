@@ -723,12 +723,10 @@ def test_kept_conv_images_match_fresh_prep(mode):
 @pytest.mark.parametrize("N,C,H,K", [(500, 64, 32, 128), (500, 128, 16, 128), (500, 128, 16, 256),
                                      (500, 256, 8, 512), (500, 256, 16, 128), (300, 512, 8, 256)])
 @pytest.mark.parametrize("epi", ["plain", "relu", "mask_add", "pool"])
-def test_stream_kernel_bench_batches(N, C, H, K, epi):
-    """The streamed conv kernel (``conv_stream_kernel``: workgroups walking
-    several 256-pixel tiles as one K-step stream, next window and weight
-    tiles in flight, register epilogue) at the ResNet-9 bench batch, where the
-    dispatcher picks it, for every fused epilogue; (300, 512, 8, 256) has
-    fewer tiles than slots (one tile per workgroup)."""
+def test_fwd_bench_batches_every_epilogue(N, C, H, K, epi):
+    """The halo forward kernels at the ResNet-9 bench batch (one wave of
+    256-pixel tiles) for every fused epilogue; (300, 512, 8, 256) has fewer
+    tiles than resident slots."""
     x, w = _inputs(N, C, H, H, K, seed=N + C)
     wf, _ = ops.conv_weight_prep(w)
     ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
