@@ -37,7 +37,8 @@ namespace {
 
 constexpr int HD = 64;       // head dim
 constexpr int LM = 128;      // max sequence length of the short (all-in-LDS) kernels
-constexpr int DS = 1024;     // dropout index stride: idx = ((seq*heads + h)*DS + i)*DS + j
+// dropout index: idx = ((seq*heads + h)*DS + i)*DS + j with DS = 1024 (the
+// maximum sequence length)
 constexpr int RS = HD + 8;   // row stride (elements) of [LM][HD] bf16 tiles
 constexpr int TS = LM + 8;   // row stride of [HD][LM] and [LM][LM] bf16 tiles
 constexpr int SS = LM + 4;   // row stride of the fp32 score tile
@@ -433,8 +434,6 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a) {
 constexpr int QB = 128;  // rows per workgroup
 constexpr int TT = 64;   // streamed tile rows
 constexpr int T2 = 72;   // bf16 row stride of [64][64] tiles
-constexpr int F2 = 68;   // fp32 row stride of the per-wave [32][64] score tile
-constexpr int TI = 36;   // bf16 row stride of per-wave transposed images [64][32]
 
 // global pieces of one 64 x 64 bf16 tile (rows t0 + i of a row block at
 // token row r0; rows >= L are zero): two 16-byte pieces per thread
@@ -486,20 +485,6 @@ __device__ __forceinline__ bf16x8_t tr_op(const uint16_t* img, int cb, int ks, i
   return tr_read(b + (row * LD + col) * 2, b + ((row + 4) * LD + col) * 2);
 }
 
-// accumulator values v[e] (row crow(e, hi), column lr of a 32 x 32 tile)
-// stored TRANSPOSED into an image [column][row] (stride TI): the four rows
-// (e & 3) of a group are consecutive there -> one 8-byte store per group
-__device__ __forceinline__ void store_t(uint16_t* img, const float (&v)[16], int col, int hi) {
-#pragma unroll
-  for (int grp = 0; grp < 4; ++grp) {
-    const int r0 = 8 * grp + 4 * hi;
-    uint2 w;
-    w.x = pack_bf16(v[4 * grp], v[4 * grp + 1]);
-    w.y = pack_bf16(v[4 * grp + 2], v[4 * grp + 3]);
-    *reinterpret_cast<uint2*>(img + col * TI + r0) = w;
-  }
-}
-
 // 32 rows x 64 columns staged bf16 in a per-wave [32][stride] tile -> token
 // rows r0 + g0 + row (< L) of a [M, ld] bf16 matrix
 template <int STRIDE>
@@ -527,135 +512,7 @@ __device__ __forceinline__ void stage_acc(uint16_t* stage, const f32x16_t acc[2]
     }
 }
 
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// LDS: K, V [2][64][T2] ring, per wave: S fp32 [32][F2] (P_drop bf16 written
-// over its rows), alpha [32]  (~72 KB: 2 workgroups per CU)
-__global__ void __launch_bounds__(256, 2) attn_long_fwd_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);   // [2][TT][T2]
-  uint16_t* sV = sK + 2 * TT * T2;                     // [2][TT][T2]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
-  float* sS = reinterpret_cast<float*>(sV + 2 * TT * T2) + w * 32 * F2;
-  uint16_t* sP = reinterpret_cast<uint16_t*>(sS);  // row i at the start of S row i (stride 2*F2)
-  constexpr int PS = 2 * F2;                        // bf16 row stride of P
-  float* sA = reinterpret_cast<float*>(sV + 2 * TT * T2) + 4 * 32 * F2 + w * 32;
-  const int tiles = a.lse_ld / QB;
-  const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
-  const int n = bh / a.nh, h = bh - n * a.nh;
-  const int L = min(a.len[n], a.lse_ld);
-  if (q0 >= L) return;
-  const int64_t r0 = a.start[n];
-  const int H = a.nh * HD;
-  const int64_t ld3 = 3 * static_cast<int64_t>(H);
-  const int wq0 = q0 + 32 * w;
-  const bool wvalid = wq0 < L;
-  const uint16_t* kbase = a.qkv + H + h * HD;
-  const uint16_t* vbase = a.qkv + 2 * H + h * HD;
-  bf16x8_t qf[4];
-  frag_load(qf, a.qkv + h * HD, ld3, r0 + wq0 + lr, wq0 + lr < L, hi);
-  f32x16_t o[2] = {zero16(), zero16()};
-  // softmax state of row (lane >> 1) of this wave, columns half*32 ..
-  const int srow = lane >> 1, half = lane & 1, gi = wq0 + srow;
-  float m_run = -__builtin_huge_valf(), l_run = 0.f;
-  const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
-  {
-    const TilePieces pk = tile_fetch(kbase, ld3, r0, 0, L, tid);
-    const TilePieces pv = tile_fetch(vbase, ld3, r0, 0, L, tid);
-    tile_store(sK, pk, tid);
-    tile_store(sV, pv, tid);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const uint16_t* cK = sK + (kt & 1) * TT * T2;
-    const uint16_t* cV = sV + (kt & 1) * TT * T2;
-    TilePieces pk, pv;
-    const bool more = kt + 1 < nkt;
-    if (more) {  // next tile's loads in flight during this tile's math
-      pk = tile_fetch(kbase, ld3, r0, (kt + 1) * TT, L, tid);
-      pv = tile_fetch(vbase, ld3, r0, (kt + 1) * TT, L, tid);
-    }
-    const bool act = wvalid && kt * TT <= wq0 + 31;
-    if (act) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        f32x16_t acc = zero16();
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8_t bf = *reinterpret_cast<const bf16x8_t*>(cK + (32 * ct + lr) * T2 + 16 * ks + 8 * hi);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[ks], bf, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = crow(e, hi), col = 32 * ct + lr;
-          const int i = wq0 + row, j = kt * TT + col;
-          sS[row * F2 + col] = (j <= i && i < L) ? acc[e] * a.scale : -__builtin_huge_valf();
-        }
-      }
-      wave_lds_sync();
-      float p[32];
-      float mt = -__builtin_huge_valf();
-#pragma unroll
-      for (int t = 0; t < 32; ++t) {
-        p[t] = sS[srow * F2 + half * 32 + t];
-        mt = fmaxf(mt, p[t]);
-      }
-      mt = fmaxf(mt, __shfl_xor(mt, 1, 64));
-      const float m_new = fmaxf(m_run, mt);
-      const bool live = gi < L && m_new > -__builtin_huge_valf();
-      const float alpha = live ? __expf(m_run - m_new) : 1.f;
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < 32; ++t) {
-        p[t] = live ? __expf(p[t] - m_new) : 0.f;
-        sum += p[t];
-      }
-      l_run = l_run * alpha + sum;
-      m_run = live ? m_new : m_run;
-      const uint32_t hs = akeep_hs(bh, a.seed), ib = akeep_lo(bh, gi, kt * TT + half * 32);
-      wave_lds_sync();  // every lane holds its S values: P may overwrite the rows
-#pragma unroll
-      for (int t = 0; t < 32; t += 2) {
-        float v0 = p[t], v1 = p[t + 1];
-        if (a.thresh != 0u) {
-          v0 = akeep_fast(ib + t, hs, a.thresh) ? v0 * a.dscale : 0.f;
-          v1 = akeep_fast(ib + t + 1, hs, a.thresh) ? v1 * a.dscale : 0.f;
-        }
-        *reinterpret_cast<uint32_t*>(sP + srow * PS + half * 32 + t) =
-            static_cast<uint32_t>(bfbits(v0)) | (static_cast<uint32_t>(bfbits(v1)) << 16);
-      }
-      if (half == 0) sA[srow] = alpha;
-      wave_lds_sync();
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[ct][e] *= sA[crow(e, hi)];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(sP + lr * PS + 16 * ks + 8 * hi);
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-          o[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_op<T2>(cV, 32 * ct, ks, lane), o[ct], 0, 0, 0);
-      }
-    }
-    if (more) {  // the other buffer was last read before the previous barrier
-      tile_store(sK + ((kt + 1) & 1) * TT * T2, pk, tid);
-      tile_store(sV + ((kt + 1) & 1) * TT * T2, pv, tid);
-    }
-    __syncthreads();
-  }
-  if (wvalid) {
-    const float l = l_run + __shfl_xor(l_run, 1, 64);
-    if (half == 0) {
-      sA[srow] = gi < L ? 1.f / l : 0.f;
-      if (gi < L) a.lse[static_cast<int64_t>(bh) * a.lse_ld + gi] = m_run + __logf(l);
-    }
-    wave_lds_sync();
-    stage_acc<PS>(sP, o, hi, lr, sA);
-    wave_lds_sync();
-    rows_store<PS>(a.o + h * HD, H, r0, wq0, L, sP, lane);
-  }
-}
 
 // Forward, transposed formulation: the same tiles and online softmax with the
 // scores computed as S^T = K Q^T, so the accumulator lane (query lr, half hi)
@@ -907,241 +764,7 @@ __global__ void __launch_bounds__(256, 3) attn_long_dq_t_kernel(AttnArgs a) {
   }
 }
 
-// dQ (+ D): LDS K, V [2][64][T2] ring, per wave: dS^T image [64][TI] bf16,
-// D / LSE [32]  (~56 KB)
-__global__ void __launch_bounds__(256, 2) attn_long_dq_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sV = sK + 2 * TT * T2;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
-  uint16_t* sdSt = sV + 2 * TT * T2 + w * TT * TI;  // [key][query]
-  float* sDr = reinterpret_cast<float*>(sV + 2 * TT * T2 + 4 * TT * TI) + w * 64;
-  float* sLr = sDr + 32;
-  const int tiles = a.lse_ld / QB;
-  const int bh = blockIdx.x / tiles, q0 = (blockIdx.x - bh * tiles) * QB;
-  const int n = bh / a.nh, h = bh - n * a.nh;
-  const int L = min(a.len[n], a.lse_ld);
-  if (q0 >= L) return;
-  const int64_t r0 = a.start[n];
-  const int H = a.nh * HD;
-  const int64_t ld3 = 3 * static_cast<int64_t>(H);
-  const int wq0 = q0 + 32 * w;
-  const bool wvalid = wq0 < L;
-  const uint16_t* kbase = a.qkv + H + h * HD;
-  const uint16_t* vbase = a.qkv + 2 * H + h * HD;
-  bf16x8_t qf[4], gf[4];
-  frag_load(qf, a.qkv + h * HD, ld3, r0 + wq0 + lr, wq0 + lr < L, hi);
-  frag_load(gf, a.dout + h * HD, H, r0 + wq0 + lr, wq0 + lr < L, hi);
-  {  // D_i = dO_i . O_i and LSE_i of this wave's rows (2 threads per row)
-    const int srow = lane >> 1, half = lane & 1, i = wq0 + srow;
-    float s = 0.f;
-    if (i < L) {
-      const uint16_t* orow = a.o + (r0 + i) * H + h * HD + half * 32;
-      const uint16_t* grow = a.dout + (r0 + i) * H + h * HD + half * 32;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const v4u ov = *reinterpret_cast<const v4u*>(orow + 8 * q);
-        const v4u gv = *reinterpret_cast<const v4u*>(grow + 8 * q);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int sh = 16 * (e & 1);
-          s += bfval(static_cast<uint16_t>((ov[e >> 1] >> sh) & 0xffffu)) *
-               bfval(static_cast<uint16_t>((gv[e >> 1] >> sh) & 0xffffu));
-        }
-      }
-    }
-    s += __shfl_xor(s, 1, 64);
-    if (half == 0) {
-      sDr[srow] = s;
-      sLr[srow] = i < L ? a.lse[static_cast<int64_t>(bh) * a.lse_ld + i] : 0.f;
-      if (i < L) a.dbuf[static_cast<int64_t>(bh) * a.lse_ld + i] = s;
-    }
-  }
-  f32x16_t gq[2] = {zero16(), zero16()};
-  const int nkt = (min(q0 + QB, L) - 1) / TT + 1;
-  {
-    const TilePieces pk = tile_fetch(kbase, ld3, r0, 0, L, tid);
-    const TilePieces pv = tile_fetch(vbase, ld3, r0, 0, L, tid);
-    tile_store(sK, pk, tid);
-    tile_store(sV, pv, tid);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const uint16_t* cK = sK + (kt & 1) * TT * T2;
-    const uint16_t* cV = sV + (kt & 1) * TT * T2;
-    TilePieces pk, pv;
-    const bool more = kt + 1 < nkt;
-    if (more) {
-      pk = tile_fetch(kbase, ld3, r0, (kt + 1) * TT, L, tid);
-      pv = tile_fetch(vbase, ld3, r0, (kt + 1) * TT, L, tid);
-    }
-    const bool act = wvalid && kt * TT <= wq0 + 31;
-    if (act) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        f32x16_t s = zero16(), dp = zero16();
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int ko = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qf[ks], *reinterpret_cast<const bf16x8_t*>(cK + ko), s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[ks], *reinterpret_cast<const bf16x8_t*>(cV + ko), dp, 0, 0, 0);
-        }
-        float ds[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = crow(e, hi), col = 32 * ct + lr;
-          const int i = wq0 + row, j = kt * TT + col;
-          const bool valid = j <= i && i < L;
-          const float P = valid ? __expf(s[e] * a.scale - sLr[row]) : 0.f;
-          bool keep = true;
-          if (a.thresh != 0u) keep = akeep_fast(akeep_lo(bh, i, j), akeep_hs(bh, a.seed), a.thresh);
-          const float dP = keep ? dp[e] * a.dscale : 0.f;
-          ds[e] = P * (dP - sDr[row]) * a.scale;
-        }
-        store_t(sdSt, ds, 32 * ct + lr, hi);  // [key][query]
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {  // keys 16 ks ..
-        const bf16x8_t af = tr_op<TI>(sdSt, 0, ks, lane);  // A[query][key]
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-          gq[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, tr_op<T2>(cK, 32 * ct, ks, lane), gq[ct], 0, 0, 0);
-      }
-    }
-    if (more) {
-      tile_store(sK + ((kt + 1) & 1) * TT * T2, pk, tid);
-      tile_store(sV + ((kt + 1) & 1) * TT * T2, pv, tid);
-    }
-    __syncthreads();
-  }
-  if (wvalid) {
-    uint16_t* stage = sdSt;  // 32 rows x 64 columns (stride T2 fits in the 64 x TI image)
-    stage_acc<T2>(stage, gq, hi, lr, nullptr);
-    wave_lds_sync();
-    rows_store<T2>(a.dqkv + h * HD, ld3, r0, wq0, L, stage, lane);
-  }
-}
 
-// dK, dV: LDS Q, dO [2][64][T2] ring, LSE / D [2][64], per wave P_drop and dS
-// images [64 queries][TI] (~75 KB)
-__global__ void __launch_bounds__(256, 2) attn_long_dkdv_kernel(AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sG = sQ + 2 * TT * T2;
-  float* sL = reinterpret_cast<float*>(sG + 2 * TT * T2);  // [2][TT]
-  float* sD = sL + 2 * TT;                                  // [2][TT]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, lr = lane & 31;
-  uint16_t* sPd = reinterpret_cast<uint16_t*>(sD + 2 * TT) + w * 2 * TT * TI;  // [query][key]
-  uint16_t* sdS = sPd + TT * TI;
-  const int tiles = a.lse_ld / QB;
-  const int bh = blockIdx.x / tiles, k0 = (blockIdx.x - bh * tiles) * QB;
-  const int n = bh / a.nh, h = bh - n * a.nh;
-  const int L = min(a.len[n], a.lse_ld);
-  if (k0 >= L) return;
-  const int64_t r0 = a.start[n];
-  const int H = a.nh * HD;
-  const int64_t ld3 = 3 * static_cast<int64_t>(H);
-  const int wk0 = k0 + 32 * w;
-  const bool wvalid = wk0 < L;
-  const uint16_t* qbase = a.qkv + h * HD;
-  const uint16_t* gbase = a.dout + h * HD;
-  const float* lrow = a.lse + static_cast<int64_t>(bh) * a.lse_ld;
-  const float* drow = a.dbuf + static_cast<int64_t>(bh) * a.lse_ld;
-  bf16x8_t kf[4], vf[4];
-  frag_load(kf, a.qkv + H + h * HD, ld3, r0 + wk0 + lr, wk0 + lr < L, hi);
-  frag_load(vf, a.qkv + 2 * H + h * HD, ld3, r0 + wk0 + lr, wk0 + lr < L, hi);
-  f32x16_t gk[2] = {zero16(), zero16()}, gv[2] = {zero16(), zero16()};
-  {
-    const TilePieces pq = tile_fetch(qbase, ld3, r0, k0, L, tid);
-    const TilePieces pg = tile_fetch(gbase, H, r0, k0, L, tid);
-    tile_store(sQ, pq, tid);
-    tile_store(sG, pg, tid);
-    if (tid < TT) {
-      const int i = k0 + tid;
-      sL[tid] = i < L ? lrow[i] : 0.f;
-      sD[tid] = i < L ? drow[i] : 0.f;
-    }
-  }
-  __syncthreads();
-  for (int qs = k0, it = 0; qs < L; qs += TT, ++it) {
-    const int b = it & 1;
-    const uint16_t* cQ = sQ + b * TT * T2;
-    const uint16_t* cG = sG + b * TT * T2;
-    const float* cL = sL + b * TT;
-    const float* cD = sD + b * TT;
-    TilePieces pq, pg;
-    float nl = 0.f, nd = 0.f;
-    const bool more = qs + TT < L;
-    if (more) {
-      pq = tile_fetch(qbase, ld3, r0, qs + TT, L, tid);
-      pg = tile_fetch(gbase, H, r0, qs + TT, L, tid);
-      if (tid < TT) {
-        const int i = qs + TT + tid;
-        nl = i < L ? lrow[i] : 0.f;
-        nd = i < L ? drow[i] : 0.f;
-      }
-    }
-    const bool act = wvalid && qs + TT - 1 >= wk0;
-    if (act) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {  // queries 32 ct ..
-        f32x16_t s = zero16(), dp = zero16();
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int ko = (32 * ct + lr) * T2 + 16 * ks + 8 * hi;
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks], *reinterpret_cast<const bf16x8_t*>(cQ + ko), s, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks], *reinterpret_cast<const bf16x8_t*>(cG + ko), dp, 0, 0, 0);
-        }
-        float pd[16], ds[16];
-        const int col = 32 * ct + lr, i = qs + col;  // query
-        const float Li = cL[col], Di = cD[col];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int j = wk0 + crow(e, hi);  // key
-          const bool valid = j <= i && i < L;
-          const float P = valid ? __expf(s[e] * a.scale - Li) : 0.f;
-          bool keep = true;
-          if (a.thresh != 0u) keep = akeep_fast(akeep_lo(bh, i, j), akeep_hs(bh, a.seed), a.thresh);
-          const float dP = keep ? dp[e] * a.dscale : 0.f;
-          pd[e] = keep ? P * a.dscale : 0.f;
-          ds[e] = P * (dP - Di) * a.scale;
-        }
-        store_t(sPd, pd, col, hi);  // [query][key]
-        store_t(sdS, ds, col, hi);
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {  // queries 16 ks ..
-        const bf16x8_t pa = tr_op<TI>(sPd, 0, ks, lane);  // A[key][query]
-        const bf16x8_t sa = tr_op<TI>(sdS, 0, ks, lane);
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          gv[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, tr_op<T2>(cG, 32 * ct, ks, lane), gv[ct], 0, 0, 0);
-          gk[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, tr_op<T2>(cQ, 32 * ct, ks, lane), gk[ct], 0, 0, 0);
-        }
-      }
-    }
-    if (more) {
-      tile_store(sQ + (b ^ 1) * TT * T2, pq, tid);
-      tile_store(sG + (b ^ 1) * TT * T2, pg, tid);
-      if (tid < TT) {
-        sL[(b ^ 1) * TT + tid] = nl;
-        sD[(b ^ 1) * TT + tid] = nd;
-      }
-    }
-    __syncthreads();
-  }
-  if (wvalid) {
-    stage_acc<T2>(sPd, gk, hi, lr, nullptr);  // 32 x 64 at stride T2 fits in 2 x 64 x TI
-    wave_lds_sync();
-    rows_store<T2>(a.dqkv + H + h * HD, ld3, r0, wk0, L, sPd, lane);
-    wave_lds_sync();
-    stage_acc<T2>(sPd, gv, hi, lr, nullptr);
-    wave_lds_sync();
-    rows_store<T2>(a.dqkv + 2 * H + h * HD, ld3, r0, wk0, L, sPd, lane);
-  }
-}
 
 // dK, dV with the scores in query-row form: S = Q K^T and dP = dO V^T put one
 // KEY per lane (column lr), so P_drop and dS are, as they come out of the
@@ -1275,15 +898,9 @@ __global__ void __launch_bounds__(256, 2) attn_long_dkdv_s_kernel(AttnArgs a) {
   }
 }
 
-constexpr size_t kLongFwdLds = 4 * TT * T2 * 2 + 4 * 32 * F2 * 4 + 4 * 32 * 4;
 constexpr size_t kLongFwdTLds = 4 * TT * T2 * 2;  // the K / V ring only
 constexpr size_t kLongDkdvSLds = 4 * TT * T2 * 2 + 4 * TT * 4;  // Q / dO ring + LSE / D
-constexpr size_t kLongDqLds = 4 * TT * T2 * 2 + 4 * TT * TI * 2 + 4 * 64 * 4;
-constexpr size_t kLongDkdvLds = 4 * TT * T2 * 2 + 4 * TT * 4 + 4 * 2 * TT * TI * 2;
-static_assert(kLongDkdvLds <= 80 * 1024 && kLongFwdLds <= 80 * 1024 && kLongDqLds <= 80 * 1024,
-              "2 workgroups per CU");
-static_assert(32 * T2 <= TT * TI, "dQ staging fits in the dS image");
-static_assert(2 * F2 >= TT, "P rows fit in the S rows");
+static_assert(kLongDkdvSLds <= 80 * 1024 && kLongFwdTLds <= 80 * 1024, "2 workgroups per CU");
 
 constexpr size_t kFwdLds = (2 * LM * RS + HD * TS) * 2 + LM * SS * 4;
 constexpr size_t kBwdLds = 3 * HD * TS * 2 + 2 * LM * 4 + 3 * LM * TS * 2;
@@ -1303,14 +920,8 @@ uint32_t attn_thresh(float p) {
 void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream) {
   if (nseq == 0) return;
   if (a.lse_ld > LM) {  // long sequences: flash-style kernel
-    static const bool transposed = [] {  // COMMEFF_ATTN_FWD_T=0: the S-image forward
-      const char* e = getenv("COMMEFF_ATTN_FWD_T");
-      return !(e != nullptr && e[0] == '0');
-    }();
     static bool lattr = false;
     if (!lattr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_fwd_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongFwdLds));
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_fwd_t_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongFwdTLds));
       lattr = true;
@@ -1318,10 +929,7 @@ void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
     a.thresh = attn_thresh(p_drop);
     a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     const dim3 grid(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB)));
-    if (transposed)
-      COMMEFF_LAUNCH(attn_long_fwd_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
-    else
-      COMMEFF_LAUNCH(attn_long_fwd_kernel, grid, dim3(256), kLongFwdLds, stream, a);
+    COMMEFF_LAUNCH(attn_long_fwd_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
     return;
   }
   static bool attr = false;
@@ -1339,18 +947,6 @@ void launch_attn_fwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
 void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream) {
   if (nseq == 0) return;
   if (a.lse_ld > LM) {  // long sequences: dQ (+ D) kernel, then dK / dV kernel
-    static bool lattr = false;
-    if (!lattr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dq_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongDqLds));
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dkdv_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLongDkdvLds));
-      lattr = true;
-    }
-    static const bool dq_t = [] {  // COMMEFF_ATTN_DQ_T=0: the dS-image dQ kernel
-      const char* e = getenv("COMMEFF_ATTN_DQ_T");
-      return !(e != nullptr && e[0] == '0');
-    }();
     static bool tattr = false;
     if (!tattr) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dq_t_kernel),
@@ -1360,15 +956,8 @@ void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
     a.thresh = attn_thresh(p_drop);
     a.dscale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     const dim3 grid(static_cast<uint32_t>(nseq * a.nh * (a.lse_ld / QB)));
-    if (dq_t)
-      COMMEFF_LAUNCH(attn_long_dq_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
-    else
-      COMMEFF_LAUNCH(attn_long_dq_kernel, grid, dim3(256), kLongDqLds, stream, a);
-    static const bool dkdv_s = [] {  // COMMEFF_ATTN_DKDV_S=0: the P / dS-image dK dV kernel
-      const char* e = getenv("COMMEFF_ATTN_DKDV_S");
-      return !(e != nullptr && e[0] == '0');
-    }();
-    if (dkdv_s) {
+    COMMEFF_LAUNCH(attn_long_dq_t_kernel, grid, dim3(256), kLongFwdTLds, stream, a);
+    {
       static bool sattr = false;
       if (!sattr) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_dkdv_s_kernel),
@@ -1376,8 +965,6 @@ void launch_attn_bwd(AttnArgs a, int64_t nseq, float p_drop, hipStream_t stream)
         sattr = true;
       }
       COMMEFF_LAUNCH(attn_long_dkdv_s_kernel, grid, dim3(256), kLongDkdvSLds, stream, a);
-    } else {
-      COMMEFF_LAUNCH(attn_long_dkdv_kernel, grid, dim3(256), kLongDkdvLds, stream, a);
     }
     return;
   }

@@ -482,12 +482,8 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
     hp = reinterpret_cast<uint32_t*>(hint->data_ptr<int32_t>());
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(table.device());
-  // candidate-list top-k (COMMEFF_TOPK_CAND=0: the full-vector passes)
-  static const bool cand_on = [] {
-    const char* e = std::getenv("COMMEFF_TOPK_CAND");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  const bool cand = cand_on && m == 64 && topk_cand_supported(n);
+  // candidate-list top-k (else the full-vector passes)
+  const bool cand = m == 64 && topk_cand_supported(n);
   auto est = at::empty({d}, table.options());
   // a caller-kept workspace (zeroed once, see cs_region_topk_ws_bytes) is
   // left zeroed by the passes: no memset per call
@@ -518,13 +514,6 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
   if (cand) {
     launch_topk_cand_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
                           ws.data_ptr(), cur_stream(), hp, keep);
-    static const bool stats = std::getenv("COMMEFF_TOPK_CAND_STATS") != nullptr;  // debug: host sync
-    if (stats) {
-      const int64_t off = (4 * 2048 * 4 + 2 * 4096 * 4 + 64 + 2048 * 4) / 4;  // topk.hip carve_cand: ctl
-      auto ctl = ws.view(at::kInt).slice(0, off, off + 2).cpu();
-      fprintf(stderr, "[topk_cand] n=%lld k=%lld use=%d M=%d\n", static_cast<long long>(n),
-              static_cast<long long>(k), ctl[0].item<int>(), ctl[1].item<int>());
-    }
   }
   else
     launch_topk_abs_rest(est.data_ptr<float>() + lo, n, k, idx.data_ptr<int64_t>(), vals.data_ptr<float>(),
@@ -536,8 +525,7 @@ std::tuple<at::Tensor, at::Tensor> cs_region_topk_hip(at::Tensor table, int64_t 
 // (0: the call sizes its own -- candidate lists unsupported or disabled)
 int64_t cs_region_topk_ws_bytes(int64_t d, int64_t m, int64_t q0, int64_t q1) {
   const int64_t lo = q0 * m, hi = std::min(d, q1 * m), n = hi - lo;
-  const char* e = std::getenv("COMMEFF_TOPK_CAND");
-  if ((e != nullptr && e[0] == '0') || m != 64 || !topk_cand_supported(n)) return 0;
+  if (m != 64 || !topk_cand_supported(n)) return 0;
   return topk_cand_workspace_bytes(n);
 }
 
@@ -873,9 +861,6 @@ at::Tensor cs_hash_all_cpu(const at::Tensor& hashes, const at::Tensor& blk_off,
 
 // the exact (atomic-free) plan when its LDS segment fits, else the dense one
 bool any_plan_geometry(int64_t d, int64_t r, int64_t c, PlanGeom* p) {
-  // COMMEFF_SKETCH_PLAN=dense forces the fixed-point dense plan (measurement)
-  const char* force = std::getenv("COMMEFF_SKETCH_PLAN");
-  if (force != nullptr && std::string(force) == "dense") return planned_geometry_dense(d, r, c, p);
   return planned_geometry(d, r, c, p) || planned_geometry_dense(d, r, c, p);
 }
 
@@ -1647,45 +1632,7 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_relu_add_hip(const at::Tensor& x, con
 
 // dw [K][C][3][3] fp32 = sum_p dy[p, k] x[p + (r-1, s-1), c]
 void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits, at::Tensor& dw,
-                       float beta, bool may_defer = false);
-
-// Deferred split-K reductions (ops/nn.py deferred_wgrad): while on, the
-// accumulate-into convs of a backward pass write only their slabs, which are
-// kept alive here, and wgrad_flush reduces them all in one batched launch
-struct PendingReduce {
-  at::Tensor slab, dw;
-  int K, C, splits;
-  float beta;
-};
-bool g_wgrad_defer = false;
-std::vector<PendingReduce> g_wgrad_pending;
-
-void wgrad_flush() {
-  size_t i = 0;
-  while (i < g_wgrad_pending.size()) {
-    WgradReduceBatch b{};
-    b.n = 0;
-    for (; i < g_wgrad_pending.size() && b.n < kWgradBatch; ++i, ++b.n) {
-      const auto& r = g_wgrad_pending[i];
-      b.slab[b.n] = r.slab.data_ptr<float>();
-      b.dw[b.n] = r.dw.data_ptr<float>();
-      b.K[b.n] = r.K;
-      b.C[b.n] = r.C;
-      b.splits[b.n] = r.splits;
-      b.beta[b.n] = r.beta;
-    }
-    c10::hip::HIPGuardMasqueradingAsCUDA guard(g_wgrad_pending[i - 1].dw.device());
-    launch_wgrad_reduce_batch(b, cur_stream());
-  }
-  // (the slabs go back to the caching allocator stream-ordered: reused only
-  // by work queued after the reduction)
-  g_wgrad_pending.clear();
-}
-
-void wgrad_defer(bool on) {
-  if (!on) wgrad_flush();
-  g_wgrad_defer = on;
-}
+                       float beta);
 
 at::Tensor conv3x3_wgrad_hip(const at::Tensor& dy, const at::Tensor& x, int64_t splits) {
   auto dw = at::empty({dy.size(1), x.size(1), 3, 3},
@@ -1702,7 +1649,7 @@ void conv3x3_wgrad_into_hip(const at::Tensor& dy, const at::Tensor& x, at::Tenso
   TORCH_CHECK(dw.dim() == 4 && dw.size(0) == dy.size(1) && dw.size(1) == x.size(1) &&
                   dw.size(2) == 3 && dw.size(3) == 3,
               "conv3x3_wgrad_into: dw must be [K, C, 3, 3]");
-  conv3x3_wgrad_run(dy, x, splits, dw, 1.f, /*may_defer=*/true);
+  conv3x3_wgrad_run(dy, x, splits, dw, 1.f);
 }
 
 // grouped (per-client) weight gradients: dw [G, K*C*9] fp32 rows (any row
@@ -1744,7 +1691,7 @@ void conv3x3_wgrad_grouped_hip(const at::Tensor& dy, const at::Tensor& x, int64_
 }
 
 void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits, at::Tensor& dw,
-                       float beta, bool may_defer) {
+                       float beta) {
   check_nhwc_bf16(dy, "conv3x3_wgrad: dy");
   check_nhwc_bf16(x, "conv3x3_wgrad: x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
@@ -1765,18 +1712,6 @@ void conv3x3_wgrad_run(const at::Tensor& dy, const at::Tensor& x, int64_t splits
   a.C = static_cast<int>(C);
   a.K = static_cast<int>(K);
   a.splits = static_cast<int>(splits);
-  if (may_defer && g_wgrad_defer && dw.is_contiguous()) {
-    // a second gradient into the same dw (a conv applied twice in one pass):
-    // the earlier reductions go first, one batched launch must not hold both
-    for (const auto& r : g_wgrad_pending)
-      if (r.dw.data_ptr() == dw.data_ptr()) {
-        wgrad_flush();
-        break;
-      }
-    launch_conv3x3_wgrad_slabs(a, cur_stream());
-    g_wgrad_pending.push_back({slab, dw, a.K, a.C, a.splits, beta});
-    return;
-  }
   launch_conv3x3_wgrad(a, dw.data_ptr<float>(), beta, cur_stream());
 }
 
@@ -2411,10 +2346,8 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor(e!)? dadd=None) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
-  m.def("wgrad_defer(bool on) -> ()", &commeff::wgrad_defer);
   m.def("conv3x3_fwd_grouped(Tensor x, Tensor w, int G) -> Tensor");
   m.def("conv3x3_wgrad_grouped_ch(Tensor dy, Tensor x, int G) -> Tensor");
-  m.def("wgrad_flush() -> ()", &commeff::wgrad_flush);
   m.def("conv3x3_wgrad_grouped(Tensor dy, Tensor x, int G, Tensor(a!) dw) -> ()");
   m.def("conv_weight_prep(Tensor w) -> (Tensor, Tensor)");
   m.def("conv_weight_prep_multi(Tensor[] ws) -> Tensor[]");

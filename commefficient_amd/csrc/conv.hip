@@ -428,17 +428,17 @@ struct HaloCfg {
 template <int TBM, int BN>
 constexpr int halo_lds() { return HaloCfg<TBM>::kWinBytes + 2 * BN * 128; }
 
-// DB: double-buffered operand fragments.  Without it the compiler (at the
-// 128-VGPR budget of 4 waves/SIMD) gives the next sub-step's fragments the
-// registers of the current ones, so every 4-MFMA group waits for its own LDS
+// Double-buffered operand fragments.  Without them the compiler (at the
+// 128-VGPR budget of 4 waves/SIMD) gave the next sub-step's fragments the
+// registers of the current ones, so every 4-MFMA group waited for its own LDS
 // reads (s_waitcnt lgkmcnt(0) right before it, disassembly) -- ~45 % of the
 // MFMA rate with every global load, barrier and the epilogue removed
-// (COMMEFF_CONV_ABLATE=15).  With it the fragment offsets are one register per
+// (profiles/r4_experiments.md).  The fragment offsets are one register per
 // operand row (sub-step kk flips chunk bits 5-6), the reads of sub-step kk+1
 // are pinned above the MFMAs of kk (sched_barrier), and the step's barrier
 // sits before the last sub-step's MFMAs, which overlap the next step's first
 // reads.
-template <int TBM, bool POOL, bool SPLIT = false, int BN = 128, bool DB = true>
+template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
 __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1))
 __attribute__((amdgpu_waves_per_eu((TBM == 256 && !SPLIT) ? 4 : 1)))  // two 8-wave blocks per CU
 conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
@@ -522,17 +522,6 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
     pbr[mi] = g * (hg.Rg + 1) + r + 1;
     pbc[mi] = w + 1;
   }
-  int offB[4][NI];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const int chk = 2 * kk + hi;
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int row = wc * (BN / 2) + ni * 32 + lr;
-      offB[kk][ni] = row * 128 + ((chk ^ sw_rd128(row)) << 4);
-    }
-  }
-
   f32x16_t acc[2][NI];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -541,7 +530,6 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
 
-  if constexpr (DB) {
     int bB[NI];  // sub-step 0 B offsets; sub-step kk: ^ (kk << 5)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
@@ -622,60 +610,6 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
       __builtin_amdgcn_sched_barrier(0);
       mma(fa1, fb1);
     }
-  } else {
-  issue_window(s_beg / 9);
-  issue_b(s_beg);
-  for (int s = s_beg; s < s_end; ++s) {
-    const int tap = s % 9, cb = s / 9;
-    if (tap == 0 && s > s_beg && !(a.ablate & 2)) {  // every wave is past the old window's reads
-      // (staging the next window behind the last tap's MFMAs instead needs
-      // all A fragments in registers: 220 VGPRs, measured 6 % slower)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      issue_window(cb);
-    }
-    if (!(a.ablate & 4) || s == s_beg) {
-      wait_vmcnt<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    if (s + 1 < s_end && (!(a.ablate & 1) || s == s_beg)) issue_b(s + 1);
-    const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-    int offA[2];
-    int swA[2];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int pr = pbr[mi] + dr, pc = pbc[mi] + dc;
-      offA[mi] = (pr * hg.PW + pc) * 128;
-      swA[mi] = sw_halo(pr, pc, hg);
-    }
-    const unsigned char* sB = smem + kHaloWinBytes + (s & 1) * (BN * 128);
-    bf16x8_t af[2][2], bfr[2][NI];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-      af[0][mi] = *reinterpret_cast<const bf16x8_t*>(smem + offA[mi] + ((hi ^ swA[mi]) << 4));
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) bfr[0][ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[0][ni]);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int cur = kk & 1, nxt = cur ^ 1;
-      if (kk + 1 < 4) {
-        const int chk = 2 * (kk + 1) + hi;
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-          af[nxt][mi] = *reinterpret_cast<const bf16x8_t*>(smem + offA[mi] + ((chk ^ swA[mi]) << 4));
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          bfr[nxt][ni] = *reinterpret_cast<const bf16x8_t*>(sB + offB[kk + 1][ni]);
-      }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
-    }
-  }
-  }  // DB
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr (SPLIT) {
@@ -704,15 +638,6 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
     conv_fwd_epilogue<TBM, BN, POOL, TBM * 4>(a, acc, smem_base, m0, n0, threadIdx.x, wr, wc, hi, lr,
                                               half == 0);
   } else {
-    if (a.ablate & 8) {  // timing experiment: no epilogue (one value per lane keeps the MFMAs)
-      float t = 0.f;
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) t += acc[mi][ni][0];
-      if (t == 12345.f) a.y[tid] = 1;
-      return;
-    }
     conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, m0, n0, tid, wr, wc, hi, lr);
   }
 }
@@ -931,7 +856,6 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int HALF = BK * 128 * 2;           // one [64 px][128] image, 16 KB
   constexpr int A_BYTES = 2 * HALF, STAGE = 4 * HALF;
-  constexpr int NLD = 8;
   constexpr int NTAPG = TPG == 2 ? 5 : 9;
   constexpr int CPT = 256 / TPG;               // input channels per tap in a tile
 
@@ -1340,61 +1264,6 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
   }
 }
 
-// Batched form: the split-K reductions of up to kWgradBatch convs of a
-// backward pass in ONE launch (their slabs are kept until the end of the
-// pass, ops/nn.py deferred_wgrad).  Seven per-layer reductions of ResNet-9
-// are 85 us per round of mostly latency-bound blocks (128-2048 per launch);
-// one launch keeps every block of every layer in flight.  Each block finds its
-// conv by compile-time-indexed compares (a dynamically indexed by-value
-// argument array would be copied to scratch); 8 split partitions per block,
-// summed in fixed order (deterministic).
-__global__ void __launch_bounds__(512) conv_wgrad_reduce_batch_kernel(WgradReduceBatch b) {
-  __shared__ float t[8][64 * 9];
-  int item = 0;
-#pragma unroll
-  for (int i = 1; i < kWgradBatch; ++i)
-    if (i < b.n && static_cast<int>(blockIdx.x) >= b.block0[i]) item = i;
-  const float* slab = b.slab[0];
-  float* dw = b.dw[0];
-  int C = b.C[0], K = b.K[0], splits = b.splits[0], blk0 = b.block0[0];
-  float beta = b.beta[0];
-#pragma unroll
-  for (int i = 1; i < kWgradBatch; ++i)
-    if (i == item) {
-      slab = b.slab[i];
-      dw = b.dw[i];
-      C = b.C[i];
-      K = b.K[i];
-      splits = b.splits[i];
-      beta = b.beta[i];
-      blk0 = b.block0[i];
-    }
-  const int blk = static_cast<int>(blockIdx.x) - blk0;
-  const int ncb = C >> 6;
-  const int k = blk / ncb, c0 = (blk - k * ncb) * 64;
-  const int cc = threadIdx.x & 63, part = threadIdx.x >> 6;
-  const size_t sstride = static_cast<size_t>(K) * 9 * C;
-  const float* src = slab + static_cast<size_t>(k) * 9 * C + c0 + cc;
-  float acc[9];
-#pragma unroll
-  for (int rs = 0; rs < 9; ++rs) acc[rs] = 0.f;
-#pragma unroll 2
-  for (int sp = part; sp < splits; sp += 8) {
-    const float* p = src + sp * sstride;
-#pragma unroll
-    for (int rs = 0; rs < 9; ++rs) acc[rs] += p[rs * C];
-  }
-#pragma unroll
-  for (int rs = 0; rs < 9; ++rs) t[part][cc * 9 + rs] = acc[rs];
-  __syncthreads();
-  float* o = dw + (static_cast<size_t>(k) * C + c0) * 9;
-  for (int e = threadIdx.x; e < 576; e += 512) {
-    float v = t[0][e];
-#pragma unroll
-    for (int q = 1; q < 8; ++q) v += t[q][e];
-    o[e] = beta != 0.f ? beta * o[e] + v : v;
-  }
-}
 
 void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
                          int64_t gstride, int groups, hipStream_t stream) {
@@ -1489,22 +1358,12 @@ int grid_for(int64_t n, int per_block) {
 
 // the wide (256 x 256) wgrad kernel: K a multiple of 256, C = 128 (tap pairs)
 // or a multiple of 256
-bool wgrad_wide(int K, int C) {
-  static const bool off = [] {
-    const char* e = getenv("COMMEFF_WGRAD_WIDE");
-    return e != nullptr && e[0] == '0';
-  }();
-  return !off && K % 256 == 0 && (C == 128 || C % 256 == 0);
-}
+bool wgrad_wide(int K, int C) { return K % 256 == 0 && (C == 128 || C % 256 == 0); }
 
 // the halo wgrad kernel (three taps of a kernel row per block): 16 | W,
-// 64 % W == 0 and whole K-steps per image (COMMEFF_WGRAD_HALO=0: off)
+// 64 % W == 0 and whole K-steps per image
 bool wgrad_halo(int H, int W, int K, int C) {
-  static const bool off = [] {
-    const char* e = getenv("COMMEFF_WGRAD_HALO");
-    return e != nullptr && e[0] == '0';
-  }();
-  return !off && W % 16 == 0 && BK % W == 0 && (H * W) % BK == 0 && K % WBM == 0 && C % 64 == 0 &&
+  return W % 16 == 0 && BK % W == 0 && (H * W) % BK == 0 && K % WBM == 0 && C % 64 == 0 &&
          (BK / W) * (W + 2) <= kHaloWRows;
 }
 
@@ -1558,18 +1417,6 @@ bool conv3x3_wgrad_grouped_supported(int H, int W, int K, int C, int kg) {
 
 static int wgrad_slots();
 
-static int cu_count() {
-  static const int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess) {
-      hipDeviceProp_t prop;
-      if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-        n = prop.multiProcessorCount;
-    }
-    return n;
-  }();
-  return cus;
-}
 
 bool conv3x3_supported(int C, int K) { return C % 64 == 0 && K % 64 == 0 && C >= 64 && K >= 64; }
 
@@ -1598,47 +1445,28 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g, int BN = 128) {
   g->NPW = g->PR * g->PW;
   // window swizzle per tile width (see sw_halo); other widths: the flat-row
   // swizzle (row >> 1) & 7, which is swa = PW / 2 for an even PW
-  static const bool sw_on = [] {  // COMMEFF_HALO_SWIZZLE=0: flat-row swizzle everywhere
-    const char* e = getenv("COMMEFF_HALO_SWIZZLE");
-    return !(e != nullptr && e[0] == '0');
-  }();
   g->swa = (g->PW / 2) & 7;
   g->swb = 0;
-  if (sw_on && W == 16) g->swa = 0;
-  if (sw_on && W == 8) g->swa = 4;
-  if (sw_on && W == 4) { g->swa = 2; g->swb = 4; }
+  if (W == 16) g->swa = 0;
+  if (W == 8) g->swa = 4;
+  if (W == 4) { g->swa = 2; g->swb = 4; }
   // (ResNet-9 res3, W = 4: 288 padded rows for 128 pixels -- slower alone in
   // scripts/bench_conv.py, but faster inside the round: bench 222-223k with a
   // 256-row cap vs 224-227k with 288, profiles/r1_experiments.md)
-  static const int cap = [] {  // tuning knob: COMMEFF_HALO_MAXROWS (<= 288)
-    const char* e = getenv("COMMEFF_HALO_MAXROWS");
-    const int v = e != nullptr ? atoi(e) : 288;
-    return v > 288 ? 288 : v;
-  }();
-  return g->NPW <= (TBM == 256 ? HaloCfg<256>::kMaxRows : cap);
+  return g->NPW <= (TBM == 256 ? HaloCfg<256>::kMaxRows : HaloCfg<128>::kMaxRows);
 }
 
 template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
 void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
   constexpr int lds = halo_lds<TBM, BN>() * (SPLIT ? 2 : 1);
-  // COMMEFF_CONV_DB=0: the single-buffered fragment loop (A/B experiments)
-  static const bool db = [] {
-    const char* e = getenv("COMMEFF_CONV_DB");
-    return !(e != nullptr && e[0] == '0');
-  }();
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, true>), lds);
-    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, false>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), lds);
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  if (db)
-    COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, true>), dim3(mt * (a.K / BN)),
-                   dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
-  else
-    COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, false>), dim3(mt * (a.K / BN)),
-                   dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
+  COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), dim3(mt * (a.K / BN)),
+                 dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
 }
 
 // Grouped conv on channel-stacked images (a.kg, a.x_stride set): the halo
@@ -1650,7 +1478,6 @@ bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream) {
     return false;
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
-  a.ablate = 0;
   HaloGeom hg;
   if (a.kg % 128 == 0) {
     if (halo_geom(a.H, a.W, a.K, 256, &hg)) { launch_fwd_halo<256, false>(a, hg, stream); return true; }
@@ -1667,33 +1494,16 @@ bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream) {
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
-  static const int ablate = [] {
-    const char* e = getenv("COMMEFF_CONV_ABLATE");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  a.ablate = ablate;
-  static const bool halo_on = [] {  // COMMEFF_CONV_HALO=0: the per-tap tile kernel
-    const char* e = getenv("COMMEFF_CONV_HALO");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  static const int halo_tbm = [] {  // COMMEFF_CONV_HALO_TBM=128: only the 4-wave tile
-    const char* e = getenv("COMMEFF_CONV_HALO_TBM");
-    return e != nullptr ? atoi(e) : 256;
-  }();
   HaloGeom hg;
   // 256-pixel tiles when they still give ~every resident slot (2 per CU) a block
-  if (halo_on && halo_tbm == 256 && halo_geom(a.H, a.W, a.K, 256, &hg) &&
+  if (halo_geom(a.H, a.W, a.K, 256, &hg) &&
       static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) * 10 >= wgrad_slots() * 9) {
     if (a.pool == 2) launch_fwd_halo<256, true>(a, hg, stream); else launch_fwd_halo<256, false>(a, hg, stream);
     return;
   }
-  if (halo_on && halo_geom(a.H, a.W, a.K, 128, &hg)) {
-    static const bool split_on = [] {  // COMMEFF_CONV_SPLIT=0: one block per tile always
-      const char* e = getenv("COMMEFF_CONV_SPLIT");
-      return !(e != nullptr && e[0] == '0');
-    }();
+  if (halo_geom(a.H, a.W, a.K, 128, &hg)) {
     const int64_t tiles = static_cast<int64_t>((a.P + 127) / 128) * (a.K / 128);
-    if (split_on && (a.C / 64) % 2 == 0 && tiles * 2 <= wgrad_slots()) {
+    if ((a.C / 64) % 2 == 0 && tiles * 2 <= wgrad_slots()) {
       if (a.pool == 2) launch_fwd_halo<128, true, true>(a, hg, stream); else launch_fwd_halo<128, false, true>(a, hg, stream);
       return;
     }
@@ -1703,54 +1513,24 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   // 64-wide outputs of big layers (ResNet-9 layer-1 dgrad): the halo window
   // replaces 9 staged 256 x 64 A tiles per channel block (the per-tap kernel
   // streams ~3x the L2 bytes per MFMA)
-  static const bool halo64_on = [] {  // COMMEFF_CONV_HALO64=0: per-tap kernel
-    const char* e = getenv("COMMEFF_CONV_HALO64");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  if (halo_on && halo64_on && a.pool == 0 && a.K % 128 != 0 &&
+  if (a.pool == 0 && a.K % 128 != 0 &&
       halo_geom(a.H, a.W, a.K, 256, &hg, 64) &&
       static_cast<int64_t>((a.P + 255) / 256) * (a.K / 64) >= 512) {
     launch_fwd_halo<256, false, false, 64>(a, hg, stream);
     return;
   }
   if (a.pool == 2) {  // caller checked conv3x3_pool_supported
-    // opt-in (COMMEFF_CONV_WIDE=1): 256 x 256 tiles (8 waves of 64 x 128, half
-    // the LDS-DMA pieces per MFMA) when they still give every CU a block --
-    // measured throughput-neutral on ResNet-9 (profiles/r1_experiments.md),
-    // unlike the wide wgrad
-    static const bool wide_on = [] {
-      const char* e = getenv("COMMEFF_CONV_WIDE");
-      return e != nullptr && e[0] == '1';
-    }();
-    const int64_t wide_blocks = static_cast<int64_t>((a.P + 255) / 256) * (a.K / 256);
-    if (wide_on && a.K % 256 == 0 && wide_blocks * 10 >= static_cast<int64_t>(wgrad_slots()) / 2 * 9)
-      launch_fwd<256, 256, 2, true>(a, stream);
-    else
-      launch_fwd<128, 128, 2, true>(a, stream);
+    launch_fwd<128, 128, 2, true>(a, stream);
     return;
   }
   const bool wide = a.K % 128 == 0;
   const int bn = wide ? 128 : 64;
-  // tile override for tuning experiments: COMMEFF_CONV_CFG = 256_3 | 256_2 | 128_3 | 128_2
-  static const int cfg = [] {
-    const char* e = getenv("COMMEFF_CONV_CFG");
-    if (e == nullptr) return 0;
-    return atoi(e) * 10 + (e[3] == '_' ? atoi(e + 4) : 0);
-  }();
-  if (cfg != 0) {
-    switch (cfg) {
-      case 2563: if (wide) launch_fwd<256, 128, 3>(a, stream); else launch_fwd<256, 64, 3>(a, stream); return;
-      case 2562: if (wide) launch_fwd<256, 128, 2>(a, stream); else launch_fwd<256, 64, 2>(a, stream); return;
-      case 1283: if (wide) launch_fwd<128, 128, 3>(a, stream); else launch_fwd<128, 64, 3>(a, stream); return;
-      default: break;
-    }
-  }
   // measured (scripts/bench_conv.py sweep, profiles/r1_conv_tile_sweep.txt):
   // occupancy beats ring depth -- 128-pixel tiles with a 2-stage ring (2
   // blocks/CU) everywhere, except 64-wide outputs of big layers, where 256
   // pixels x 64 (8 waves, 2 stages) amortises the A operand better
   const bool big = static_cast<int64_t>((a.P + 255) / 256) * (a.K / bn) >= 512;
-  if (!wide && big && cfg != 1282) {
+  if (!wide && big) {
     launch_fwd<256, 64, 2>(a, stream);
   } else {
     if (wide) launch_fwd<128, 128, 2>(a, stream); else launch_fwd<128, 64, 2>(a, stream);
@@ -1775,34 +1555,22 @@ template <bool ROWSTEP>
 void launch_wgrad_wide(const ConvWgradArgs& a, hipStream_t stream) {
   constexpr int lds = 2 * 4 * BK * 128 * 2;
   const int tiles = wgrad_tiles(a.K, a.C);
-  // COMMEFF_WGRAD_WIDE_IL=1: the MFMA / read interleave of the halo wgrad
-  // kernel here too (off: res3 60.8 -> 65.4 us, layer 3 equal; r4 log)
-  static const bool il = [] {
-    const char* e = getenv("COMMEFF_WGRAD_WIDE_IL");
-    return e != nullptr && e[0] == '1';
-  }();
+  // (the halo wgrad's MFMA / read interleave measured slower here: res3
+  // 60.8 -> 65.4 us, layer 3 equal; profiles/r4_experiments.md)
   if (a.C == 128) {
     static bool init = false;
     if (!init) {
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 2, true>), lds);
       set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 2, false>), lds);
       init = true;
     }
-    if (il)
-      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 2, true>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
-    else
-      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 2, false>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 2, false>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
   } else {
     static bool init = false;
     if (!init) {
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 1, true>), lds);
       set_lds(reinterpret_cast<const void*>(conv_wgrad_wide_kernel<ROWSTEP, 1, false>), lds);
       init = true;
     }
-    if (il)
-      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 1, true>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
-    else
-      COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 1, false>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
+    COMMEFF_LAUNCH((conv_wgrad_wide_kernel<ROWSTEP, 1, false>), dim3(tiles * a.splits), dim3(512), lds, stream, a);
   }
 }
 
@@ -1829,22 +1597,7 @@ int conv3x3_wgrad_splits(int P, int H, int W, int K, int C) {
 
 void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_t stream);
 
-void launch_wgrad_reduce_batch(WgradReduceBatch b, hipStream_t stream) {
-  if (b.n <= 0) return;
-  int total = 0;
-  for (int i = 0; i < b.n; ++i) {
-    b.block0[i] = total;
-    total += b.K[i] * (b.C[i] / 64);
-  }
-  COMMEFF_LAUNCH(conv_wgrad_reduce_batch_kernel, dim3(total), dim3(512), 0, stream, b);
-}
 
-// the split-K slabs only (the reduction deferred to launch_wgrad_reduce_batch)
-void launch_conv3x3_wgrad_slabs(ConvWgradArgs a, hipStream_t stream) {
-  const int steps = (a.P + BK - 1) / BK;
-  a.group_px = 0;
-  launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
-}
 
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream) {
   const int steps = (a.P + BK - 1) / BK;
@@ -1858,46 +1611,23 @@ void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_
   a.steps_per_split = steps_per_split;
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
-  static const bool three = [] {  // tuning experiment: COMMEFF_WGRAD_STAGES=3
-    const char* e = getenv("COMMEFF_WGRAD_STAGES");
-    return e != nullptr && e[0] == '3';
-  }();
   const bool rowstep = BK % a.W == 0;
   const bool wide = a.C % 128 == 0;
   if (wgrad_halo(a.H, a.W, a.K, a.C) && (a.group_px == 0 || a.group_px % BK == 0)) {
-    // ring depth (COMMEFF_WGRAD_HALO_STAGES = 2 | 3; 3 x 25 KB still fits 2 blocks/CU,
-    // measured equal to 2 in the ResNet-9 round)
-    static const int stages = [] {
-      const char* e = getenv("COMMEFF_WGRAD_HALO_STAGES");
-      return e != nullptr && e[0] == '3' ? 3 : 2;
-    }();
+    // (a 3-stage ring -- 3 x 25 KB still fits 2 blocks/CU -- measured equal to
+    // 2 in the ResNet-9 round)
     const int tiles = (a.K / WBM) * 3 * (a.C / 64);
     constexpr int stage_bytes = BK * WBM * 2 + kHaloWRows * 128;
-    // COMMEFF_WGRAD_IL=0: the compiler's own read / MFMA order (A/B experiments)
-    static const bool il = [] {
-      const char* e = getenv("COMMEFF_WGRAD_IL");
-      return !(e != nullptr && e[0] == '0');
-    }();
     static bool init = false;
     if (!init) {
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2, true>), 2 * stage_bytes);
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<3, true>), 3 * stage_bytes);
-      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2, false>), 2 * stage_bytes);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2>), 2 * stage_bytes);
       init = true;
     }
-    if (stages == 3)
-      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<3, true>), dim3(tiles * a.splits), dim3(256), 3 * stage_bytes, stream, a);
-    else if (il)
-      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2, true>), dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
-    else
-      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2, false>), dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream,
-                     a);
+    COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2>), dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
   } else if (wgrad_wide(a.K, a.C)) {
     if (rowstep) launch_wgrad_wide<true>(a, stream); else launch_wgrad_wide<false>(a, stream);
   } else if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)
     if (rowstep) launch_wgrad<128, 2, true, true>(a, stream); else launch_wgrad<128, 2, false, true>(a, stream);
-  } else if (three && rowstep) {
-    if (wide) launch_wgrad<128, 3, true>(a, stream); else launch_wgrad<64, 3, true>(a, stream);
   } else if (rowstep) {
     if (wide) launch_wgrad<128, 2, true>(a, stream); else launch_wgrad<64, 2, true>(a, stream);
   } else {

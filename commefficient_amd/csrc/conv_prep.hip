@@ -361,11 +361,7 @@ __global__ void __launch_bounds__(256) prep_wgrad_reduce_kernel(const float* __r
 }  // namespace
 
 int conv_prep_wgrad_blocks(int P) {
-  static const int per = [] {  // pixel steps per block (tuning knob COMMEFF_PREP_WG_STEPS)
-    const char* e = std::getenv("COMMEFF_PREP_WG_STEPS");
-    const int v = e != nullptr ? std::atoi(e) : 8;
-    return v < 1 ? 1 : v;
-  }();
+  constexpr int per = 8;  // pixel steps per block (scripts/bench_prep.py sweep)
   const int steps = (P + 63) / 64;
   int b = (steps + per - 1) / per;
   return b < 1024 ? (b < 1 ? 1 : b) : 1024;
@@ -375,11 +371,7 @@ void launch_conv_prep_fwd(ConvPrepArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   const int ntiles = (a.P + 31) / 32;
-  static const int tpw = [] {  // tiles per wave (weights are set up once per block); tuning knob
-    const char* e = std::getenv("COMMEFF_PREP_TPW");
-    const int v = e != nullptr ? std::atoi(e) : 4;  // scripts/bench_prep.py sweep: 4 best
-    return v < 1 ? 1 : v;
-  }();
+  constexpr int tpw = 4;  // tiles per wave (weights set up once per block; bench_prep.py sweep: 4 best)
   int blocks = (ntiles + 4 * tpw - 1) / (4 * tpw);
   if (blocks > 4096) blocks = 4096;
   COMMEFF_LAUNCH(prep_fwd_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, stream, a);

@@ -304,265 +304,6 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ big tiles
-// 256 x BN (BN = 256 or 128) tiles, one 8-wave block per CU (waves 2 (M) x 4
-// (N), 128 x BN/4 each), 32-deep K-steps through a FOUR-stage LDS ring: three
-// stages of A/B stay in flight while one is consumed.  The 128 x 128 kernel
-// above waits after every K-step for loads issued one step earlier -- an HBM
-// round trip per 16 MFMAs, measured ~600 TF/s on the GPT-2 GEMMs, against
-// hipBLASLt's 256 x 256 x 32 tiles.  Per K-step: the fragments of the first
-// 16-k sub-step were read before the barrier's wave released the step, the
-// second sub-step's reads overlap the first's MFMAs, and the next step's first
-// reads overlap the second's MFMAs (issued right after the one barrier).
-// LDS images: A (and NT B) [rows][32 k] as 64-byte rows of four 16-byte
-// chunks, chunk c of row r at slot c ^ ((r >> 2) & 3) (every ds_read_b128
-// lane group of a fragment hits 16 distinct 4-bank slots); NN B as BN/128
-// halves [32 k][128 cols] of 256-byte rows read transposed (T10 swizzle).
-constexpr int GK2 = 32;
-
-template <int BN, bool NN>
-struct BigCfg {
-  static constexpr int BM = 256, NT = 512, NSTAGE = 4;
-  static constexpr int A_BYTES = BM * GK2 * 2;           // 16 KB
-  static constexpr int B_BYTES = BN * GK2 * 2;           // 16 / 8 KB
-  static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int APC = A_BYTES / 16 / NT;          // 2 pieces per thread
-  static constexpr int BPC = B_BYTES / 16 / NT;          // 2 / 1
-  static constexpr int P = APC + BPC;                    // DMA pieces per thread per stage
-  static constexpr int LD = BN + 4;                      // epilogue fp32 row stride
-  static constexpr int EPI = 128 * LD * 4;               // one 128-row pass
-  static constexpr int LDS = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
-};
-
-__device__ __forceinline__ int sw64(int row) { return (row >> 2) & 3; }
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int BN, bool NN, int ACT, bool F32>
-__global__ void __launch_bounds__(512) gemm_big_kernel(GemmArgs a) {
-  using Cfg = BigCfg<BN, NN>;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NI = BN / 128, P = Cfg::P;
-  constexpr int WN = BN / 4;                              // wave tile columns
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3, hi = lane >> 5, lr = lane & 31;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntn = a.N / BN;
-  const int m0 = (bid / ntn) * Cfg::BM, n0 = (bid % ntn) * BN;
-  const int KT = a.K / GK2;
-  const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_mm_zero);
-
-  // DMA sources (k offset added per stage); piece q of a stage lands at q * 16
-  const uint16_t* a_src[Cfg::APC];
-#pragma unroll
-  for (int i = 0; i < Cfg::APC; ++i) {
-    const int q = i * 512 + tid, row = q >> 2, c = (q & 3) ^ sw64(row);
-    a_src[i] = m0 + row < a.M ? a.A + static_cast<int64_t>(m0 + row) * a.lda + c * 8 : nullptr;
-  }
-  const uint16_t* b_src[Cfg::BPC];
-#pragma unroll
-  for (int j = 0; j < Cfg::BPC; ++j) {
-    const int q = j * 512 + tid;
-    if constexpr (NN) {  // half h: [32 k][128 cols], 16 chunks per row
-      const int h = q >> 9, r = (q & 511) >> 4, ch = (q & 15) ^ sw_tr256(r);
-      b_src[j] = a.B + static_cast<int64_t>(r) * a.ldb + n0 + h * 128 + ch * 8;
-    } else {
-      const int row = q >> 2, c = (q & 3) ^ sw64(row);
-      b_src[j] = a.B + static_cast<int64_t>(n0 + row) * a.ldb + c * 8;
-    }
-  }
-  auto issue = [&](int kt) __attribute__((always_inline)) {
-    unsigned char* base = smem + (kt & 3) * Cfg::STAGE + wid * 1024;
-    const int k0 = kt * GK2;
-#pragma unroll
-    for (int i = 0; i < Cfg::APC; ++i) mm_glds16(a_src[i] != nullptr ? a_src[i] + k0 : zero, base + i * 8192);
-#pragma unroll
-    for (int j = 0; j < Cfg::BPC; ++j) {
-      const uint16_t* src = NN ? b_src[j] + static_cast<int64_t>(k0) * a.ldb : b_src[j] + k0;
-      mm_glds16(src, base + Cfg::A_BYTES + j * 8192);
-    }
-  };
-
-  // fragment byte offsets inside a stage
-  int offA[2][4];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int row = wr * 128 + mi * 32 + lr, c = 2 * kk + hi;
-      offA[kk][mi] = row * 64 + ((c ^ sw64(row)) << 4);
-    }
-  int offB[2][NI];
-#pragma unroll
-  for (int ni = 0; ni < NI; ++ni) {
-    const int col = wc * WN + ni * 32;
-    if constexpr (NN) {
-      int t[2];
-      tr_offsets<256>(col & 127, lane, t);
-      offB[0][ni] = Cfg::A_BYTES + (col >> 7) * 8192 + t[0];
-      offB[1][ni] = Cfg::A_BYTES + (col >> 7) * 8192 + t[1];
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int row = col + lr, c = 2 * kk + hi;
-        offB[kk][ni] = Cfg::A_BYTES + row * 64 + ((c ^ sw64(row)) << 4);
-      }
-    }
-  }
-
-  f32x16_t acc[4][NI];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
-
-  bf16x8_t af[2][4], bfr[2][NI];
-  auto load = [&](int kt, int kk, int buf) __attribute__((always_inline)) {
-    const unsigned char* st = smem + (kt & 3) * Cfg::STAGE;
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) af[buf][mi] = *reinterpret_cast<const bf16x8_t*>(st + offA[kk][mi]);
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      if constexpr (NN) {
-        const int dd = kk * 16 * 256;
-        bfr[buf][ni] = tr_read(st + offB[0][ni] + dd, st + offB[1][ni] + dd);
-      } else {
-        bfr[buf][ni] = *reinterpret_cast<const bf16x8_t*>(st + offB[kk][ni]);
-      }
-    }
-  };
-  auto mfma = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[buf][mi], bfr[buf][ni], acc[mi][ni], 0, 0, 0);
-  };
-  // wait until stage `s` has landed: the stages issued after it may stay in flight
-  auto wait_stage = [&](int s) __attribute__((always_inline)) {
-    const int last = KT - 1 < s + 2 ? KT - 1 : s + 2;  // the last stage issued so far
-    const int after = last - s;
-    if (after >= 2) wait_vm<2 * P>();
-    else if (after == 1) wait_vm<P>();
-    else wait_vm<0>();
-  };
-
-  if (KT > 0) {
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-      if (s < KT) issue(s);
-    wait_stage(0);
-    __builtin_amdgcn_s_barrier();
-    load(0, 0, 0);
-  }
-  for (int kt = 0; kt < KT; ++kt) {
-    // every wave has finished reading stage kt - 1: its slot takes stage kt + 3
-    if (kt + 3 < KT) issue(kt + 3);
-    load(kt, 1, 1);
-    mfma(0);
-    if (kt + 1 < KT) {
-      // stage kt + 1 landed for this wave (counted: later stages stay in flight)
-      // and this wave's reads of stage kt are done; the barrier makes both
-      // true for every wave
-      wait_stage(kt + 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      load(kt + 1, 0, 0);
-    }
-    mfma(1);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  // ---- epilogue: two 128-row passes (wave row 0, then 1) through LDS
-  float* ct = reinterpret_cast<float*>(smem);
-  constexpr int LD = Cfg::LD, CPR = BN / 8;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    if (wr == pass) {
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int row = mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-            ct[row * LD + wc * WN + ni * 32 + lr] = acc[mi][ni][e];
-          }
-    }
-    __syncthreads();
-    for (int e = tid; e < 128 * CPR; e += 512) {
-      const int row = e / CPR, cc = e - row * CPR, m = m0 + pass * 128 + row;
-      if (m >= a.M) continue;
-      const int n = n0 + cc * 8;
-      const float4 lo = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8);
-      const float4 up = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8 + 4);
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, up.x, up.y, up.z, up.w};
-      add_bias(a, n, v);
-      const int64_t o = static_cast<int64_t>(m) * a.ldc + n;
-      if constexpr (F32) {
-        float* c = reinterpret_cast<float*>(a.C) + o;
-        if (a.beta != 0.f) {
-          const float4 c0 = *reinterpret_cast<const float4*>(c), c1 = *reinterpret_cast<const float4*>(c + 4);
-          v[0] += a.beta * c0.x; v[1] += a.beta * c0.y; v[2] += a.beta * c0.z; v[3] += a.beta * c0.w;
-          v[4] += a.beta * c1.x; v[5] += a.beta * c1.y; v[6] += a.beta * c1.z; v[7] += a.beta * c1.w;
-        }
-        *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      } else {
-        uint16_t* c = reinterpret_cast<uint16_t*>(a.C) + o;
-        if (a.beta != 0.f) {
-          const v4u old = *reinterpret_cast<const v4u*>(c);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += a.beta * bf2f((old[j >> 1] >> (16 * (j & 1))) & 0xffffu);
-        }
-        if constexpr (ACT == 1) {
-          v4u pre;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pre[j] = pack_bf16(v[2 * j], v[2 * j + 1]);
-          *reinterpret_cast<v4u*>(reinterpret_cast<uint16_t*>(a.C2) + o) = pre;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(bf2f((pre[j >> 1] >> (16 * (j & 1))) & 0xffffu));
-        }
-        v4u out;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) out[j] = pack_bf16(v[2 * j], v[2 * j + 1]);
-        *reinterpret_cast<v4u*>(c) = out;
-      }
-    }
-    __syncthreads();  // the next pass overwrites the staging rows
-  }
-}
-
-template <int BN, bool NN, int ACT, bool F32>
-void launch_gemm_big_t(const GemmArgs& a, hipStream_t stream) {
-  constexpr int lds = BigCfg<BN, NN>::LDS;
-  static bool init = false;
-  if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_big_kernel<BN, NN, ACT, F32>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    init = true;
-  }
-  const int tiles = ((a.M + 255) / 256) * (a.N / BN);
-  COMMEFF_LAUNCH((gemm_big_kernel<BN, NN, ACT, F32>), dim3(tiles), dim3(512), lds, stream, a);
-}
-
-template <int BN>
-void launch_gemm_big(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream) {
-  if (act == 1) {
-    if (nn) launch_gemm_big_t<BN, true, 1, false>(a, stream); else launch_gemm_big_t<BN, false, 1, false>(a, stream);
-  } else if (f32) {
-    if (nn) launch_gemm_big_t<BN, true, 0, true>(a, stream); else launch_gemm_big_t<BN, false, 0, true>(a, stream);
-  } else {
-    if (nn) launch_gemm_big_t<BN, true, 0, false>(a, stream); else launch_gemm_big_t<BN, false, 0, false>(a, stream);
-  }
-}
-
 template <int BN, bool NN, int ACT, bool F32, bool ST = false>
 void launch_gemm_t(const GemmArgs& a, hipStream_t stream) {
   constexpr int lds = MmCfg<BN, NN>::LDS;
@@ -585,21 +326,9 @@ bool gemm_supported(int M, int N, int K, bool nn) {
 
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream) {
   if (a.M <= 0) return;
-  // COMMEFF_GEMM_BIG=1: 256-row tiles with a 4-stage ring (one block per CU)
-  // when they still give most CUs a tile.  Off by default: on the GPT-2 and
-  // ResNet-101 shapes it measured equal or slower than the 128-row kernel
-  // (e.g. 9400 x 768 x 3072 NN 84.9 vs 62.3 us; profiles/r4_gemm_native_vs_hipblaslt.jsonl):
-  // these GEMMs are one wave of tiles whose load / store phases, not the
-  // K-loop latency, set the time
-  static const bool big_on = [] {
-    const char* e = getenv("COMMEFF_GEMM_BIG");
-    return e != nullptr && e[0] == '1';
-  }();
-  const int64_t mt = (a.M + 255) / 256;
-  if (big_on && a.K % GK2 == 0 && a.N % 128 == 0) {
-    if (a.N % 256 == 0 && mt * (a.N / 256) >= 200) { launch_gemm_big<256>(a, nn, act, f32, stream); return; }
-    if (mt * (a.N / 128) >= 160) { launch_gemm_big<128>(a, nn, act, f32, stream); return; }
-  }
+  // (256-row tiles with a 4-stage ring, one block per CU, measured equal or
+  // slower on the GPT-2 and ResNet-101 shapes: these GEMMs are one wave of
+  // tiles whose load / store phases set the time; profiles/r4_experiments.md)
   // 128-wide column tiles when they still give ~every resident slot (2 per CU) a block
   const bool wide = a.N % 128 == 0 && static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) >= 384;
   if (a.stats != nullptr && !nn && act == 0 && !f32) {  // BN moments in the epilogue (mm_nt_bnstats)

@@ -264,10 +264,6 @@ struct ConvFwdArgs {
   // consumer of that layer's other input gradient -- ops/nn.py _MaskLink)
   const uint16_t* dual_mask = nullptr;
   uint16_t* y_dual = nullptr;
-  // timing experiments only (COMMEFF_CONV_ABLATE, results are wrong): bit 0 =
-  // no weight-tile loads after the first two K-steps, bit 1 = no window reload
-  // per channel block, bit 2 = no per-K-step wait / barrier, bit 3 = no epilogue
-  int ablate = 0;
   // grouped conv on channel-stacked images (batched FedAvg, ops/nn.py
   // _GConv3x3): x rows hold x_stride channels, output channels come in groups
   // of kg that read only input channels [g C, (g+1) C) (C = a.C, per group) and
@@ -304,17 +300,6 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 // the geometry has no halo tiling (the caller falls back)
 bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream);
 bool conv3x3_wgrad_grouped_supported(int H, int W, int K, int C, int kg);
-// split-K slabs only; their reductions batched across convs by launch_wgrad_reduce_batch
-void launch_conv3x3_wgrad_slabs(ConvWgradArgs a, hipStream_t stream);
-constexpr int kWgradBatch = 16;
-struct WgradReduceBatch {
-  int n;
-  const float* slab[kWgradBatch];
-  float* dw[kWgradBatch];  // [K][C][3][3] fp32: dw = beta * dw + sum of the splits
-  int K[kWgradBatch], C[kWgradBatch], splits[kWgradBatch], block0[kWgradBatch];
-  float beta[kWgradBatch];
-};
-void launch_wgrad_reduce_batch(WgradReduceBatch b, hipStream_t stream);
 // per-group dw_g [K][C][3][3] (+)= the wgrad of group g's pixels, dw_g at
 // dw + g * gstride floats (a.splits = G x splits_per_group, set by the caller)
 void launch_conv3x3_wgrad_grouped(ConvWgradArgs a, int G, float* dw, int64_t gstride, float beta,

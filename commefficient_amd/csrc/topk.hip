@@ -620,15 +620,11 @@ void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, f
   COMMEFF_LAUNCH((hist_kernel<2, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
   COMMEFF_LAUNCH(count_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, cd);
   // the candidate list holds the keys >= hint: a tighter bound than the
-  // full-vector passes' 0.5 (COMMEFF_TOPK_HINT_FRAC; a threshold that drops
-  // below it between calls takes the exact fill-in fallback).  ResNet-9
-  // FetchSGD round (k = 50,000 of 6.57M): 0.5 -> ~815k candidates, 0.75 ->
-  // ~340k, 0.85 -> ~200k, fallbacks only in the first two rounds for all three
-  static const float frac = [] {
-    const char* e = std::getenv("COMMEFF_TOPK_HINT_FRAC");
-    const float f = e != nullptr ? static_cast<float>(std::atof(e)) : 0.85f;
-    return f > 0.f && f < 1.f ? f : 0.85f;
-  }();
+  // full-vector passes' 0.5 (a threshold that drops below it between calls
+  // takes the exact fill-in fallback).  ResNet-9 FetchSGD round (k = 50,000 of
+  // 6.57M): 0.5 -> ~815k candidates, 0.75 -> ~340k, 0.85 -> ~200k, fallbacks
+  // only in the first two rounds for all three
+  constexpr float frac = 0.85f;
   COMMEFF_LAUNCH(write_kernel<true>, dim3(nb), dim3(256), 0, stream, x, n, int64_t{0}, w, kk, idx, vals,
                      hint, cd, frac, persistent ? cw.seg : nullptr);
 }

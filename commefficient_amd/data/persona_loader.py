@@ -4,7 +4,6 @@ and ships the round's int64 tensors in ONE pinned H2D copy (non_blocking),
 split into views on the device."""
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -21,7 +20,7 @@ def _to_dev(ts, device):
     from ..parallel.dist import h2d
     if torch.device(device).type != "cuda":
         return list(ts)
-    if not all(t.dtype == torch.int64 for t in ts) or os.environ.get("COMMEFF_PERSONA_PACK") == "0":
+    if not all(t.dtype == torch.int64 for t in ts):
         return [h2d(t, device) for t in ts]
     flat = h2d(np.concatenate([t.numpy().reshape(-1) for t in ts]), device)
     out, o = [], 0

@@ -95,39 +95,6 @@ def _grad_written(*params):
                     fn(p)
 
 
-class deferred_wgrad:
-    """``with deferred_wgrad(): loss.backward()`` -- the native 3x3 convs that
-    accumulate their weight gradient into an existing fp32 ``.grad`` write
-    only their split-K slabs during the pass; one batched launch reduces all
-    of them at exit (csrc/conv.hip conv_wgrad_reduce_batch_kernel) instead of
-    one latency-bound reduction per layer.  Off while gradient-ready
-    listeners are registered (the overlapped bucket all-reduce needs each
-    gradient when its layer's backward returns).  Opt-in (COMMEFF_WGRAD_DEFER=1):
-    the reductions are bound by their slab bytes, not by launch latency -- the
-    batched launch took 99 us per ResNet-9 round against 85 us for the seven
-    per-layer ones (profiles/r4_experiments.md)."""
-
-    _depth = 0
-
-    def __init__(self, enabled: bool = True):
-        self.enabled = (enabled and not _GRAD_READY and _CONV_BACKEND[0] == "native"
-                        and not _STOCK[0] and os.environ.get("COMMEFF_WGRAD_DEFER", "0") == "1")
-        self.active = False
-
-    def __enter__(self):
-        if self.enabled and deferred_wgrad._depth == 0:
-            _ops().wgrad_defer(True)
-            self.active = True
-        deferred_wgrad._depth += 1
-        return self
-
-    def __exit__(self, *exc):
-        deferred_wgrad._depth -= 1
-        if self.active:
-            _ops().wgrad_defer(False)  # launches the batched reductions
-        return False
-
-
 def set_conv_backend(name: str) -> None:
     if name not in ("native", "miopen"):
         raise ValueError(f"unknown conv backend {name!r}")
@@ -890,10 +857,6 @@ def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
     P, K = g2d.shape
     C = x2d.shape[1]
     Pg = P // G
-    if _TN_PARTS and _wgrad_tn_ok(g2d, x2d, None, G, pad=True):
-        # native split-K TN GEMM writing its split products (csrc/gemm_tn.hip)
-        parts, S = _ops().gemm_tn_parts(g2d, x2d, G)
-        return parts, int(S)
     S = _wgrad_splits(Pg, K, C, G)
     if G * S == 1:
         return torch.mm(g2d.t(), x2d, out_dtype=torch.float32).unsqueeze(0), 1
@@ -901,13 +864,10 @@ def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
                      out_dtype=torch.float32), S
 
 
-# column-image weight-gradient parts on the native TN GEMM: measured slower
-# than hipBLASLt's batched GEMM at the ResNet-101 shapes (1.2-1.9x,
-# scripts/bench_wgrad_tn.py), opt-in
-_TN_PARTS = os.environ.get("COMMEFF_WGRAD_TN_PARTS", "0") == "1"
 # 1x1 weight gradients with both sides multiples of 256 on the native TN GEMM
-# (default; COMMEFF_WGRAD_TN=0: hipBLASLt batched GEMM + split reduction)
-_TN_1X1 = os.environ.get("COMMEFF_WGRAD_TN", "1") != "0"
+# (the column-image parts stay on hipBLASLt's batched GEMM: the native split
+# products measured 1.2-1.9x slower there, profiles/r4_experiments.md)
+_TN_1X1 = True
 
 
 def _wgrad_tn_ok(g2d: torch.Tensor, x2d: torch.Tensor, into, G: int, pad: bool = False) -> bool:

@@ -201,10 +201,10 @@ def _sinks(*params):
     return tuple(_sink(p) for p in params)
 
 
-_WGRAD_GEMM = {"native": os.environ.get("COMMEFF_WGRAD_GEMM", "native") == "native"}
-# forward / input-gradient GEMMs on the native MFMA kernels (csrc/gemm.hip);
-# COMMEFF_GEMM=blas: hipBLASLt (torch.mm)
+# forward / input-gradient / weight-gradient GEMMs on the native MFMA kernels
+# (csrc/gemm.hip, gemm_tn.hip); COMMEFF_GEMM=blas: hipBLASLt (torch.mm)
 _GEMM = {"native": os.environ.get("COMMEFF_GEMM", "native") == "native"}
+_WGRAD_GEMM = _GEMM
 
 
 def _native_mm_ok(a: torch.Tensor, b: torch.Tensor, n: int) -> bool:
@@ -249,7 +249,7 @@ def _acc_mm(sink: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
     """sink (fp32) += a @ b (bf16 operands, fp32 accumulation and output).
     The weight gradients (a = X^T, a view of the token rows) run on the
     native split-K TN GEMM (csrc/gemm_tn.hip) when the shapes fit, else on
-    hipBLASLt (COMMEFF_WGRAD_GEMM=blas: always)."""
+    hipBLASLt (COMMEFF_GEMM=blas: always)."""
     if sink.is_cuda:
         if _gemm_tn_ok(sink, a.t(), b):
             _ops().gemm_tn_acc(sink, a.t(), b)
@@ -295,9 +295,8 @@ def _side_stream(device) -> "torch.cuda.Stream":
 # bias gradients) go to the same side stream when all their outputs are fp32
 # sinks: ~40 us each of latency-bound reductions that otherwise sit in the
 # input-gradient chain behind the side stream's GEMM blocks (1.9 ms per GPT-2
-# round, profiles/r4_gpt2_native_gemm_round_kernels.txt).  COMMEFF_COLSUM_SIDE=0:
-# summed in place on the main stream.
-_COLSUM_SIDE = os.environ.get("COMMEFF_COLSUM_SIDE", "1") != "0"
+# round, profiles/r4_gpt2_native_gemm_round_kernels.txt).
+_COLSUM_SIDE = True
 
 
 def _colsum_deferred(t: torch.Tensor, *sinks) -> bool:

@@ -112,8 +112,9 @@ def init(device_type: str = "cuda", port: int = None, timeout_s: int = 1800) -> 
     return _CTX
 
 
-# COMMEFF_H2D=blit: stage with hipMemcpyAsync instead of the host-read kernel
-_H2D_KERNEL = os.environ.get("COMMEFF_H2D", "kernel") != "blit"
+# stage through the host-read kernel (csrc/hostcopy.hip), not a hipMemcpyAsync
+# blit (GPU idle 56 -> 13 us per round, profiles/r4_experiments.md)
+_H2D_KERNEL = True
 
 
 class _PinnedRing:

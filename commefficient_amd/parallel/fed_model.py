@@ -40,7 +40,7 @@ import torch.nn as nn
 from .. import ops
 from ..models.common import NativeConv2d, ghost_batchnorm, groupable, has_batchnorm
 from ..ops.grouped import GroupedGrads, grouped_grads
-from ..ops.nn import (deferred_wgrad, image_generation, invalidate_conv_images,
+from ..ops.nn import (image_generation, invalidate_conv_images,
                       prepared_conv_weights, set_conv_image_cache)
 from ..ops import CSVec
 from ..ops import transformer as _tx
@@ -359,18 +359,15 @@ class FedModel:
                     per_ex, metrics = self.compute_loss_val(model, self._prep(inputs),
                                                             targets, self.args)
         if want_grad:
-            # the native conv wgrad split-K reductions: one batched launch at the
-            # end of the pass (ops/nn.py deferred_wgrad)
-            with deferred_wgrad(self.device.type == "cuda"):
-                if (loss_weight is None and not capture and per_ex.dtype == torch.float32
-                        and per_ex.dim() == 1):
-                    # d(sum)/d(per_ex) = 1: a cached ones vector (no sum / fill kernels)
-                    torch.autograd.backward(per_ex, grad_tensors=self._ones(per_ex))
-                else:
-                    total = per_ex.float().sum()
-                    if loss_weight is not None:
-                        total = total * loss_weight
-                    total.backward()
+            if (loss_weight is None and not capture and per_ex.dtype == torch.float32
+                    and per_ex.dim() == 1):
+                # d(sum)/d(per_ex) = 1: a cached ones vector (no sum / fill kernels)
+                torch.autograd.backward(per_ex, grad_tensors=self._ones(per_ex))
+            else:
+                total = per_ex.float().sum()
+                if loss_weight is not None:
+                    total = total * loss_weight
+                total.backward()
             if sinks is not None:
                 _tx.join_wgrad_stream()  # side-stream weight gradients into flat.g
             if shadow is not None and not self._overlap_armed:
@@ -862,7 +859,7 @@ class FedModel:
         # steps and per-client top-k-down weights): one autocast context
         # around the loop lets the clients share the bf16 weight casts
         shared_w = (a.mode != "fedavg" and "weights" not in self.client_state.kinds
-                    and not a.do_test and os.environ.get("COMMEFF_SHARED_CASTS", "1") != "0")
+                    and not a.do_test)
         # ... and the native 3x3 convs share one batched bf16 weight preparation
         prep = (prepared_conv_weights(self._native_3x3_weights())
                 if shared_w and self.device.type == "cuda" else nullcontext())

@@ -194,35 +194,6 @@ def test_wgrad_accumulates_into_existing_grad():
     torch.testing.assert_close(w.grad, 0.5 + w2.grad, rtol=1e-5, atol=1e-5)
 
 
-def test_deferred_wgrad_reductions_match_immediate(monkeypatch):
-    """ops/nn.py deferred_wgrad: the split-K slabs of several convs (and two
-    gradients into one dw) reduced by ONE batched launch at exit give the
-    per-conv reductions (fp32 sums of the same slabs, 8-way instead of 4/16-way
-    partitioned: equal to rounding)."""
-    shapes = [(8, 128, 16, 16, 128), (8, 128, 16, 16, 256), (8, 256, 8, 8, 512), (8, 512, 4, 4, 512)]
-    cases = []
-    g = torch.Generator(device="cuda").manual_seed(11)
-    for (N, C, H, W, K) in shapes:
-        x, _ = _inputs(N, C, H, W, K)
-        dy = _nhwc(torch.randn(N, K, H, W, device="cuda", generator=g).to(torch.bfloat16))
-        cases.append((dy, x, torch.randn(K, C, 3, 3, device="cuda", generator=g)))
-    into = torch.ops.commeff.conv3x3_wgrad_into
-    ref = [d0.clone() for (_, _, d0) in cases]
-    for (dy, x, _), r in zip(cases, ref):
-        into(dy, x, r)
-    dy0, x0, _ = cases[0]
-    into(dy0, x0, ref[0])  # a second gradient into the first dw
-    out = [d0.clone() for (_, _, d0) in cases]
-    monkeypatch.setenv("COMMEFF_WGRAD_DEFER", "1")
-    with cnn.deferred_wgrad() as d:
-        assert d.active
-        for (dy, x, _), o in zip(cases, out):
-            into(dy, x, o)
-        into(dy0, x0, out[0])
-    for o, r in zip(out, ref):
-        torch.testing.assert_close(o, r, rtol=1e-5, atol=1e-4)
-
-
 @pytest.mark.parametrize("N,C,H", [(4, 128, 16), (3, 512, 4)])
 def test_residual_unit_matches_fp32(N, C, H):
     x, w1 = _inputs(N, C, H, H, C)
