@@ -235,6 +235,36 @@ void client_state_cpu(const at::Tensor& g, const c10::optional<at::Tensor>& u,
   cpu::client_state(g.data_ptr<float>(), fptr(u), fptr(e), g.numel(), static_cast<float>(rho));
 }
 
+void client_tail_check(const at::Tensor& g, const c10::optional<at::Tensor>& w,
+                       const c10::optional<at::Tensor>& u, const c10::optional<at::Tensor>& e) {
+  check_f32(g, "g");
+  for (const auto* t : {&w, &u, &e})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() && (*t)->numel() == g.numel() &&
+                      (*t)->device() == g.device(),
+                  "client_tail: contiguous fp32 operands of g's size and device");
+}
+
+void client_tail_cpu(at::Tensor g, const c10::optional<at::Tensor>& w, double wd, double scale,
+                     const c10::optional<at::Tensor>& u, const c10::optional<at::Tensor>& e, double rho) {
+  client_tail_check(g, w, u, e);
+  float* gp = g.data_ptr<float>();
+  const float* wp = fptr(w);
+  float *up = fptr(u), *ep = fptr(e);
+  const float fwd = static_cast<float>(wd), fs = static_cast<float>(scale), fr = static_cast<float>(rho);
+  for (int64_t i = 0; i < g.numel(); ++i) {
+    float t = gp[i];
+    if (wp) t += fwd * wp[i];
+    t *= fs;
+    if (up) {
+      t = fr * up[i] + t;
+      up[i] = t;
+    }
+    if (ep) ep[i] += t;
+    if (!up && !ep) gp[i] = t;
+  }
+}
+
 void zero_at_cpu(const c10::optional<at::Tensor>& a, const c10::optional<at::Tensor>& b,
                  const c10::optional<at::Tensor>& c, const at::Tensor& idx) {
   const int64_t* ip = idx.data_ptr<int64_t>();
@@ -753,6 +783,25 @@ void client_state_hip(const at::Tensor& g, const c10::optional<at::Tensor>& u,
   c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
   launch_client_state(g.data_ptr<float>(), fptr(u), fptr(e), g.numel(), static_cast<float>(rho),
                       cur_stream());
+}
+
+void client_tail_hip(at::Tensor g, const c10::optional<at::Tensor>& w, double wd, double scale,
+                     const c10::optional<at::Tensor>& u, const c10::optional<at::Tensor>& e, double rho) {
+  client_tail_check(g, w, u, e);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  const int64_t n = g.numel();
+  bool vec = n % 4 == 0;
+  for (const void* p : {static_cast<const void*>(g.data_ptr<float>()), static_cast<const void*>(fptr(w)),
+                        static_cast<const void*>(fptr(u)), static_cast<const void*>(fptr(e))})
+    vec = vec && reinterpret_cast<uintptr_t>(p) % 16 == 0;
+  if (!vec) {  // (never on the flat buffers) the unfused sequence on device
+    if (w.has_value() && w->defined()) g.add_(*w, wd);
+    g.mul_(scale);
+    launch_client_state(g.data_ptr<float>(), fptr(u), fptr(e), n, static_cast<float>(rho), cur_stream());
+    return;
+  }
+  launch_client_tail(g.data_ptr<float>(), fptr(w), static_cast<float>(wd), static_cast<float>(scale), fptr(u),
+                     fptr(e), static_cast<float>(rho), n, cur_stream());
 }
 
 void zero_at_hip(const c10::optional<at::Tensor>& a, const c10::optional<at::Tensor>& b,
@@ -2393,6 +2442,8 @@ TORCH_LIBRARY(commeff, m) {
   m.def("l2norm(Tensor x) -> Tensor");
   m.def("clip_noise(Tensor(a!) x, Tensor? norm, float clip, float noise_std, int seed, int offset) -> ()");
   m.def("client_state(Tensor g, Tensor(a!)? u, Tensor(b!)? e, float rho) -> ()");
+  m.def("client_tail(Tensor(a!) g, Tensor? w, float wd, float scale, Tensor(b!)? u, Tensor(c!)? e, "
+        "float rho) -> ()");
   m.def("zero_at(Tensor(a!)? a, Tensor(b!)? b, Tensor(c!)? c, Tensor idx) -> ()");
   m.def("scatter_dense(Tensor idx, Tensor vals, int n) -> Tensor");
   m.def("augment_u8_nhwc(Tensor data, Tensor idx, int pad, bool flip, Tensor mean, Tensor inv_std, "
@@ -2446,6 +2497,7 @@ TORCH_LIBRARY_IMPL(commeff, CPU, m) {
   m.impl("l2norm", &l2norm_cpu);
   m.impl("clip_noise", &clip_noise_cpu);
   m.impl("client_state", &client_state_cpu);
+  m.impl("client_tail", &client_tail_cpu);
   m.impl("zero_at", &zero_at_cpu);
   m.impl("scatter_dense", &scatter_dense_cpu);
   m.impl("augment_u8_nhwc", &augment_cpu);
@@ -2505,6 +2557,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("l2norm", &l2norm_hip);
   m.impl("clip_noise", &clip_noise_hip);
   m.impl("client_state", &client_state_hip);
+  m.impl("client_tail", &client_tail_hip);
   m.impl("zero_at", &zero_at_hip);
   m.impl("scatter_dense", &scatter_dense_hip);
   m.impl("augment_u8_nhwc", &augment_hip);

@@ -231,6 +231,10 @@ void launch_clip_noise(float* x, int64_t n, const float* norm, float clip,
                        float noise_std, uint64_t seed, uint64_t offset,
                        hipStream_t stream);
 // u = rho*u + g (if u) ; e += (u ? u : g) (if e)
+// fused client transmit tail: t = scale (g + wd w); u = rho u + t (t = u); e += t;
+// g = t when u and e are both null.  n % 4 == 0, 16-byte aligned.
+void launch_client_tail(float* g, const float* w, float wd, float scale, float* u, float* e, float rho,
+                        int64_t n, hipStream_t stream);
 void launch_client_state(const float* g, float* u, float* e, int64_t n,
                          float rho, hipStream_t stream);
 // x[idx[t]] = 0 for t < k  (up to 3 arrays)

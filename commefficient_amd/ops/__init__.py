@@ -11,7 +11,7 @@ from .._ext import ops as _ops
 from .sketch import CSVec, make_hashes
 
 __all__ = ["CSVec", "make_hashes", "topk_abs", "topk_dense", "momentum_ef", "sparse_apply",
-           "dense_apply", "count_ge", "axpby", "l2norm", "clip_noise", "client_state",
+           "dense_apply", "count_ge", "axpby", "l2norm", "clip_noise", "client_state", "client_tail",
            "zero_at", "scatter_dense", "augment_u8_nhwc", "augment_u8_nhwc_y", "account_round",
            "account_hist"]
 
@@ -125,6 +125,12 @@ def clip_noise(x, norm=None, clip=0.0, noise_std=0.0, seed=0, offset=0):
 
 def client_state(g, u=None, e=None, rho=0.0):
     _ops().client_state(g, u, e, float(rho))
+
+
+def client_tail(g, w=None, wd=0.0, scale=1.0, u=None, e=None, rho=0.0):
+    """t = scale (g + wd w); u = rho u + t (t = u); e += t; g = t when there is
+    neither u nor e -- one pass (csrc/elementwise.hip client_tail_kernel)."""
+    _ops().client_tail(g, w, float(wd), float(scale), u, e, float(rho))
 
 
 def zero_at(idx, a=None, b=None, c=None):

@@ -807,7 +807,7 @@ class FedModel:
             per_ex_all.append(pe)
             metrics_all.append(ms)
 
-    def _client_grad(self, inputs, targets, n: int, work: torch.Tensor):
+    def _client_grad(self, inputs, targets, n: int, work: torch.Tensor, defer_wd: bool = False):
         """Mean gradient of one client's batch + the reference's client-side
         processing up to the transmit (fed_worker.py:249-335).  Result is in
         ``self.flat.g``.  Returns (mean loss, mean metrics) device scalars."""
@@ -826,10 +826,10 @@ class FedModel:
             pm.append(ms)
         loss = torch.cat(pl).mean()
         mets = [torch.cat([m[i] for m in pm]).mean() for i in range(len(pm[0]))]
-        self._client_tail(self.flat.g, work)
+        self._client_tail(self.flat.g, work, defer_wd)
         return loss, mets
 
-    def _client_tail(self, g: torch.Tensor, work: torch.Tensor):
+    def _client_tail(self, g: torch.Tensor, work: torch.Tensor, defer_wd: bool = False):
         """Client-side processing of one client's mean gradient ``g`` (in
         place) before the transmit: clipping, weight decay at the client's
         weights ``work``, worker-side DP (fed_worker.py:288-309, utils.py:257-258)."""
@@ -837,8 +837,13 @@ class FedModel:
         if a.max_grad_norm is not None and a.mode != "sketch":
             nrm = ops.l2norm(g)
             ops.clip_noise(g, nrm, a.max_grad_norm, 0.0)
+        self._wd_pending = None
         if a.weight_decay != 0:
-            ops.axpby(g, g, 1.0, work, a.weight_decay / a.num_workers)
+            if a.do_dp or not defer_wd:
+                ops.axpby(g, g, 1.0, work, a.weight_decay / a.num_workers)
+            else:
+                # folded into the client's fused transmit tail (_finish_client)
+                self._wd_pending = (work, a.weight_decay / a.num_workers)
         if a.do_dp:
             nrm = ops.l2norm(g)
             std = a.noise_multiplier * math.sqrt(a.num_workers) if a.dp_mode == "worker" else 0.0
@@ -951,7 +956,7 @@ class FedModel:
             slots_all.append(np.repeat(slots, n))
             for j, c in enumerate(cl):
                 g = buf[j]
-                self._client_tail(g, self.w)
+                self._client_tail(g, self.w, defer_wd=True)
                 self._emit(out, self._finish_client(int(c), n, g))
         rows = [torch.cat([r[i] for r in rows_all]) for i in range(len(rows_all[0]))]
         slots_t = dist.h2d(np.concatenate(slots_all).astype(np.int64), self.device)
@@ -987,7 +992,7 @@ class FedModel:
                 if "weights" in self.client_state.kinds:
                     work = self._topk_down_weights(c)
                     self.flat.bind(work)
-                loss, mets = self._client_grad(inputs, targets, n, work)
+                loss, mets = self._client_grad(inputs, targets, n, work, defer_wd=True)
                 if work is not self.w:
                     self.flat.bind(self.w)
                 transmit = self._finish_client(c, n)
@@ -1080,6 +1085,11 @@ class FedModel:
         local top-k + masking."""
         a = self.args
         g = self.flat.g if g is None else g
+        wd = getattr(self, "_wd_pending", None)
+        self._wd_pending = None
+        if wd is not None and a.mode == "sketch":
+            ops.axpby(g, g, 1.0, wd[0], wd[1])
+            wd = None
         if a.mode == "sketch":
             # one client table reused for every client (overwritten by the
             # encode; the transmit is added to the upload before the next client)
@@ -1092,11 +1102,12 @@ class FedModel:
                 est = sk.l2estimate()
                 ops.clip_noise(sk.table.view(-1), est, a.max_grad_norm * n, 0.0)
             return sk.table.view(-1)
-        g.mul_(float(n))
         u = self.client_state.get("velocity", c)
         e = self.client_state.get("error", c)
-        if u is not None or e is not None:
-            ops.client_state(g, u, e, a.local_momentum)
+        # weight decay, the n_i scale (fed_worker.py:190) and the local momentum /
+        # error update in one pass over g
+        ops.client_tail(g, wd[0] if wd is not None else None, wd[1] if wd is not None else 0.0,
+                        float(n), u, e, a.local_momentum)
         to_send = e if e is not None else (u if u is not None else g)
         if a.mode == "local_topk":
             idx, vals = ops.topk_abs(to_send, a.k)

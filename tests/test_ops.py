@@ -449,3 +449,32 @@ def test_topk_hint_never_changes_the_result():
         b = ops.topk_abs(x.cuda(), k, hint)
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     assert int(hint.item()) != 0
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("has_w,has_u,has_e", [(True, True, True), (True, False, True), (False, True, False),
+                                               (True, False, False), (False, False, False)])
+def test_client_tail_matches_composition(device, has_w, has_u, has_e):
+    """ops.client_tail == weight decay (axpby) + the n_i scale + client_state
+    (fed_worker.py:184-230 after utils.py:257-258)."""
+    from commefficient_amd import ops
+    torch.manual_seed(3)
+    n = 4096 + 8
+    g = torch.randn(n, device=device)
+    w = torch.randn(n, device=device) if has_w else None
+    u = torch.randn(n, device=device) if has_u else None
+    e = torch.randn(n, device=device) if has_e else None
+    wd, scale, rho = 5e-4, 7.0, 0.9
+    ref_g = g.double() + (wd * w.double() if has_w else 0.0)
+    ref_g = ref_g * scale
+    ref_u = rho * u.double() + ref_g if has_u else None
+    t = ref_u if has_u else ref_g
+    ref_e = e.double() + t if has_e else None
+    g2, u2, e2 = g.clone(), (u.clone() if has_u else None), (e.clone() if has_e else None)
+    ops.client_tail(g2, w, wd, scale, u2, e2, rho)
+    if has_u:
+        torch.testing.assert_close(u2.double(), ref_u, rtol=1e-6, atol=1e-5)
+    if has_e:
+        torch.testing.assert_close(e2.double(), ref_e, rtol=1e-6, atol=1e-5)
+    if not has_u and not has_e:
+        torch.testing.assert_close(g2.double(), ref_g, rtol=1e-6, atol=1e-5)
