@@ -72,11 +72,20 @@ template <bool BWD>
 __global__ void __launch_bounds__(256)
 bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                   const uint8_t* __restrict__ ybits, const float* __restrict__ stat, int C, int M,
-                  int S, float* __restrict__ part) {
-  // part[(g*S + s)*2*C + {0: sum, C: sum2}][c]
+                  int S, float* __restrict__ part, int CB) {
+  // part[(g*S + s)*2*C + {0: sum, C: sum2}][c]; blockIdx.y: a block of CB
+  // channels (CB = C up to 2048 channels; the channel-stacked clients of
+  // parallel/fedavg_native.py have G*C of them)
   __shared__ float red[2][256][8];
   const int g = blockIdx.x / S, s = blockIdx.x - g * S;
-  const int CL = C >> 3, PL = 256 / CL;
+  const int cb0 = blockIdx.y * CB;
+  x += cb0;
+  if (BWD) {
+    dy += cb0;
+    stat += cb0;
+  }
+  part += cb0;
+  const int CL = CB >> 3, PL = 256 / CL;
   const int cl = threadIdx.x % CL, pl = threadIdx.x / CL;
   const bool active = pl < PL;
   const int per = (M + S - 1) / S;
@@ -134,7 +143,7 @@ bn_partial_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ d
         const bool in = pq < p1;
         xv[q] = in ? *reinterpret_cast<const u4*>(x + o) : u4{0u, 0u, 0u, 0u};
         dv[q] = in ? *reinterpret_cast<const u4*>(dy + o) : u4{0u, 0u, 0u, 0u};
-        mb[q] = (in && ybits != nullptr) ? ybits[o >> 3] : 0xffu;
+        mb[q] = (in && ybits != nullptr) ? ybits[(o + cb0) >> 3] : 0xffu;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -561,6 +570,88 @@ bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
   }
 }
 
+
+// ---- channel-stacked clients (parallel/fedavg_native.py): one "group" of M
+// pixels whose C = G * cg channels are G clients' cg channels side by side.
+// Statistics are per channel, i.e. per (client, channel); the affine
+// parameters of channel c are client c / cg's, read from its fp32 parameter
+// row (w[(c / cg) * ld + c % cg]); the weight / bias gradients go straight into
+// the clients' gradient rows.  The lanes of a block split the slabs (the
+// one-group branch of the kernels above), combined in a fixed order.
+__device__ __forceinline__ void cs_slab_sums(const float* __restrict__ part, int C, int S, int c, int cc,
+                                             int gl, float (&red)[2][kGL][64], float* t1, float* t2) {
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C) {
+    for (int s = gl; s < S; s += kGL) {
+      const float* p = part + static_cast<size_t>(s) * 2 * C;
+      s1 += p[c];
+      s2 += p[C + c];
+    }
+  }
+  red[0][gl][cc] = s1;
+  red[1][gl][cc] = s2;
+  __syncthreads();
+  float a = 0.f, b = 0.f;
+  for (int q = 0; q < kGL; ++q) {
+    a += red[0][q][cc];
+    b += red[1][q][cc];
+  }
+  *t1 = a;
+  *t2 = b;
+}
+
+__global__ void __launch_bounds__(1024)
+bn_cs_fwd_finalize_kernel(const uint16_t* __restrict__ x, const float* __restrict__ part,
+                          const float* __restrict__ prm, int64_t ld, int64_t woff, int64_t boff, int cg,
+                          int C, int M, int S, float eps, float momentum, float* __restrict__ stat,
+                          float* __restrict__ ab, float* __restrict__ run_mean,
+                          float* __restrict__ run_var, int64_t* __restrict__ nbt) {
+  __shared__ float red[2][kGL][64];
+  if (nbt != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+  const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc;
+  float t1, t2;
+  cs_slab_sums(part, C, S, c, cc, gl, red, &t1, &t2);
+  if (gl != 0 || c >= C) return;
+  const int64_t row = static_cast<int64_t>(c / cg) * ld + c % cg;
+  const float wc = prm[row + woff], bc = prm[row + boff];
+  const float kk = __uint_as_float(static_cast<uint32_t>(x[c]) << 16);
+  const float dd = t1 / M;
+  const float var = fmaxf(t2 / M - dd * dd, 0.f);
+  const float mean = kk + dd, rstd = rsqrtf(var + eps);
+  stat[c] = mean;
+  stat[C + c] = rstd;
+  ab[c] = wc * rstd;
+  ab[C + c] = bc - mean * wc * rstd;
+  if (run_mean != nullptr) {  // each client's own running statistics
+    const float unb = M > 1 ? static_cast<float>(M) / static_cast<float>(M - 1) : 1.f;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * unb;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+bn_cs_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__ stat,
+                          const float* __restrict__ prm, int64_t ld, int64_t woff, int cg, int C, int M,
+                          int S, float* __restrict__ coef, float* __restrict__ grad, int64_t gld,
+                          int64_t gwoff, int64_t gboff) {
+  __shared__ float red[2][kGL][64];
+  const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cc;
+  float s1, s2;
+  cs_slab_sums(part, C, S, c, cc, gl, red, &s1, &s2);
+  if (gl != 0 || c >= C) return;
+  const float wc = prm[static_cast<int64_t>(c / cg) * ld + c % cg + woff];
+  const float mean = stat[c], rstd = stat[C + c];
+  const float k0 = wc * rstd, k1 = s1 / M, k2 = s2 / M;
+  coef[c] = k0;
+  coef[C + c] = -k0 * k2 * rstd;
+  coef[2 * C + c] = -k0 * k1 + k0 * k2 * rstd * mean;
+  float* gr = grad + static_cast<int64_t>(c / cg) * gld + c % cg;
+  gr[gwoff] = s2;  // dweight = sum(dy xhat)
+  gr[gboff] = s1;  // dbias = sum(dy)
+}
+
 int apply_grid(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -602,7 +693,7 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
     return;
   }
   COMMEFF_LAUNCH(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
-                     nullptr, C, M, S, part);
+                     nullptr, C, M, S, part, C);
   if (G >= 2 && G < kGL) {
     // per-group mean / var behind the partial sums (bn_scratch_floats)
     float* gmv = part + static_cast<size_t>(G) * S * 2 * C;
@@ -625,7 +716,7 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu,
                    int64_t gstride, uint16_t* dadd) {
   const int S = bn_slabs(G, M);
   COMMEFF_LAUNCH(bn_partial_kernel<true>, dim3(G * S), dim3(256), 0, stream, x, dy, y_relu, stat, C, M,
-                     S, part);
+                     S, part, C);
   if (G >= 2 && G < kGL) {
     float* gsum = part + static_cast<size_t>(G) * S * 2 * C;  // see bn_scratch_floats
     const bool grouped = gdw != nullptr;
@@ -642,6 +733,44 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu,
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   COMMEFF_LAUNCH(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
                      coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd, nullptr);
+}
+
+// channel block of the partial kernels: the largest power-of-two multiple of
+// 8 dividing C, at most 2048 (C / 8 lanes of 16 bytes x 256 / (C / 8) pixels)
+static int cs_channel_block(int C) {
+  int cb = 8;
+  while (cb * 2 <= 2048 && C % (cb * 2) == 0) cb *= 2;
+  return cb;
+}
+
+int64_t bn_cs_scratch_floats(int M, int C) { return static_cast<int64_t>(bn_slabs(1, M)) * 2 * C; }
+
+void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t woff, int64_t boff, int cg,
+                      int M, int C, float eps, float momentum, float* run_mean, float* run_var,
+                      int64_t* nbt, float* part, float* stat, float* ab, uint16_t* y, uint8_t* relu_bits,
+                      hipStream_t stream) {
+  const int S = bn_slabs(1, M), CB = cs_channel_block(C);
+  COMMEFF_LAUNCH(bn_partial_kernel<false>, dim3(S, C / CB), dim3(256), 0, stream, x, nullptr, nullptr,
+                 nullptr, C, M, S, part, CB);
+  COMMEFF_LAUNCH(bn_cs_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part, prm,
+                 ld, woff, boff, cg, C, M, S, eps, momentum, stat, ab, run_mean, run_var, nbt);
+  const int64_t nchunks = static_cast<int64_t>(M) * (C / 8);
+  COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
+                 nullptr, ab, C, M, static_cast<uint32_t>(nchunks), true, y, nullptr, relu_bits);
+}
+
+void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
+                      const float* prm, int64_t ld, int64_t woff, int cg, int M, int C, float* part,
+                      float* coef, float* grad, int64_t gld, int64_t gwoff, int64_t gboff, uint16_t* dx,
+                      hipStream_t stream) {
+  const int S = bn_slabs(1, M), CB = cs_channel_block(C);
+  COMMEFF_LAUNCH(bn_partial_kernel<true>, dim3(S, C / CB), dim3(256), 0, stream, x, dy, y_relu, stat, C,
+                 M, S, part, CB);
+  COMMEFF_LAUNCH(bn_cs_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat, prm,
+                 ld, woff, cg, C, M, S, coef, grad, gld, gwoff, gboff);
+  const int64_t nchunks = static_cast<int64_t>(M) * (C / 8);
+  COMMEFF_LAUNCH(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
+                 coef, C, M, static_cast<uint32_t>(nchunks), false, dx, nullptr, nullptr);
 }
 
 }  // namespace commeff

@@ -1234,7 +1234,7 @@ template <int PARTS>
 __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const float* __restrict__ slab,
                                                                        float* __restrict__ dw, int K, int C,
                                                                        int splits, float beta,
-                                                                       int64_t gstride) {
+                                                                       int64_t gstride, int kg, int64_t ld) {
   __shared__ float t[PARTS][64 * 9];
   const int ncb = C >> 6;
   const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
@@ -1255,7 +1255,10 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
 #pragma unroll
   for (int rs = 0; rs < 9; ++rs) t[part][cc * 9 + rs] = acc[rs];
   __syncthreads();
-  float* o = dw + (static_cast<size_t>(k) * C + c0) * 9;
+  // kg > 0: output channel k is row k % kg of group k / kg's weight, groups
+  // ld floats apart (the per-client gradient rows of parallel/fedavg_native.py)
+  float* o = kg > 0 ? dw + static_cast<size_t>(k / kg) * ld + (static_cast<size_t>(k % kg) * C + c0) * 9
+                    : dw + (static_cast<size_t>(k) * C + c0) * 9;
   for (int e = threadIdx.x; e < 576; e += 64 * PARTS) {
     float v = t[0][e];
 #pragma unroll
@@ -1266,14 +1269,14 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
 
 
 void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
-                         int64_t gstride, int groups, hipStream_t stream) {
+                         int64_t gstride, int groups, hipStream_t stream, int kg = 0, int64_t ld = 0) {
   const dim3 grid(K * (C / 64), groups);
   if (splits >= 32)
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride);
+                       beta, gstride, kg, ld);
   else
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride);
+                       beta, gstride, kg, ld);
 }
 
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16
@@ -1604,6 +1607,15 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
   a.group_px = 0;
   launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
   launch_wgrad_reduce(a.slab, dw, a.K, a.C, a.splits, beta, int64_t{0}, 1, stream);
+}
+
+// channel-stacked grouped wgrad written straight into per-group rows: output
+// channel k of group k / kg at dst + (k / kg) * ld + (k % kg) * 9 C
+void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, hipStream_t stream) {
+  const int steps = (a.P + BK - 1) / BK;
+  a.group_px = 0;
+  launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
+  launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, 0.f, int64_t{0}, 1, stream, kg, ld);
 }
 
 // the wgrad GEMM kernels (slabs only) with a given split length

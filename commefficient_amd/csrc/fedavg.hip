@@ -1,0 +1,266 @@
+// Batched FedAvg local SGD (parallel/fedavg_native.py) for gfx950: the
+// elementwise / layout kernels around the convolutions of G clients trained
+// side by side.
+//
+// Reference: /root/reference/CommEfficient/fed_worker.py:61-113 (local SGD of
+// one client at a time: every client copies the server weights, takes its
+// local steps -- clip, weight decay, SGD -- and uploads n (w0 - w)).  Here the
+// G clients of a round are one program: their weights are the rows of one fp32
+// [G, ld] matrix, their activations are channel-stacked ([pixels][G*C]: each
+// client's channels side by side, the grouped halo convolutions of conv.hip),
+// and the per-client tails below run over all rows in one launch each:
+//   * weight_image_kernel: per-step bf16 images of every client's conv weight
+//     (halo forward [G K][3][3][C], flipped halo dgrad [G C][3][3][K], column
+//     GEMM [G][K][Kc]) straight from the fp32 rows;
+//   * row_sumsq_kernel + row_sgd_kernel: per-client gradient norm (fixed-order
+//     partials), then clip + weight decay + SGD of every row in one pass;
+//   * upload_kernel: out += n sum_g (w0 - w_g), clients in order;
+//   * avgmax_head_*: the ResNet-18 head's avg || max pool of the channel-stacked
+//     4x4 maps into per-client [n][2C] features, and its gather backward;
+//   * ew_bf16_kernel: residual adds / the stem ReLU (16-byte moves).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "kernels.h"
+
+namespace commeff {
+namespace {
+
+typedef uint16_t bf16raw;
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(bf16raw v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+
+__device__ __forceinline__ bf16raw f2bf(float f) {  // round to nearest even (NaN kept quiet)
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<bf16raw>((u >> 16) | 0x40u);
+  return static_cast<bf16raw>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+int grid_for(int64_t n, int64_t cap = 16384) {
+  int64_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  return static_cast<int>(b < cap ? b : cap);
+}
+
+// ------------------------------------------------------------ weight images
+// source element of (client g, out k, in c, tap t): W[g*ld + (k*C + c)*RS + t]
+// kind 0: dst[((g*K + k)*RS + t)*C + c]                (halo forward)
+// kind 1: dst[((g*C + c)*RS + t)*K + k] = tap RS-1-t   (halo dgrad: flipped, transposed)
+// kind 2: dst[(g*K + k)*Kc + t*C + c], zero past RS*C  (column-GEMM image)
+__global__ void __launch_bounds__(256) weight_image_kernel(const float* __restrict__ W, int64_t ld, int G,
+                                                           int K, int C, int RS, int Kc, int kind,
+                                                           bf16raw* __restrict__ dst) {
+  const int64_t per = kind == 2 ? static_cast<int64_t>(K) * Kc : static_cast<int64_t>(K) * C * RS;
+  const int64_t total = per * G;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int g = static_cast<int>(i / per);
+    const int64_t r = i - g * per;
+    int k, c, t;
+    bool pad = false;
+    if (kind == 0) {
+      c = static_cast<int>(r % C);
+      const int64_t kt = r / C;
+      t = static_cast<int>(kt % RS);
+      k = static_cast<int>(kt / RS);
+    } else if (kind == 1) {
+      k = static_cast<int>(r % K);
+      const int64_t ct = r / K;
+      t = RS - 1 - static_cast<int>(ct % RS);
+      c = static_cast<int>(ct / RS);
+    } else {
+      const int j = static_cast<int>(r % Kc);
+      k = static_cast<int>(r / Kc);
+      pad = j >= RS * C;
+      t = pad ? 0 : j / C;
+      c = pad ? 0 : j - t * C;
+    }
+    dst[i] = pad ? bf16raw(0) : f2bf(W[g * ld + (static_cast<int64_t>(k) * C + c) * RS + t]);
+  }
+}
+
+// ------------------------------------------------------------- per-row SGD
+constexpr int kRowParts = 64;  // partial sums per row (fixed order)
+
+// part[g*kRowParts + b] = sum of squares of block b's share of row g
+__global__ void __launch_bounds__(256) row_sumsq_kernel(const float* __restrict__ Gr, int64_t ld, int64_t d4,
+                                                        float* __restrict__ part) {
+  __shared__ float red[256];
+  const int g = blockIdx.y, b = blockIdx.x;
+  const float4* row = reinterpret_cast<const float4*>(Gr + g * ld);
+  float acc = 0.f;
+  for (int64_t i = b * 256ll + threadIdx.x; i < d4; i += kRowParts * 256ll) {
+    const float4 v = row[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[g * kRowParts + b] = red[0];
+}
+
+// W[g] = S[g] - lr * (scale_g * G[g] + wd * S[g]),  scale_g = clip / |G[g]| when
+// that is < 1 (clip > 0), else 1.  S = W (in place) or the broadcast w0 (sld 0)
+__global__ void __launch_bounds__(256) row_sgd_kernel(float* __restrict__ W, int64_t ld,
+                                                      const float* __restrict__ Src, int64_t sld,
+                                                      const float* __restrict__ Gr, int64_t gld, int64_t d4,
+                                                      const float* __restrict__ part, float clip, float lr,
+                                                      float wd) {
+  const int g = blockIdx.y;
+  float scale = 1.f;
+  if (clip > 0.f) {
+    float s = 0.f;
+    for (int b = 0; b < kRowParts; ++b) s += part[g * kRowParts + b];
+    const float nrm = sqrtf(s);
+    if (nrm > clip) scale = clip / nrm;
+  }
+  const float a = -lr * scale, c = 1.f - lr * wd;
+  float4* w = reinterpret_cast<float4*>(W + g * ld);
+  const float4* src = reinterpret_cast<const float4*>(Src + g * sld);
+  const float4* gr = reinterpret_cast<const float4*>(Gr + g * gld);
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < d4; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const float4 s = src[i], q = gr[i];
+    w[i] = make_float4(c * s.x + a * q.x, c * s.y + a * q.y, c * s.z + a * q.z, c * s.w + a * q.w);
+  }
+}
+
+// out[j] += n * sum_g (w0[j] - W[g][j]), clients in order (exact zeros where no
+// client moved a coordinate)
+__global__ void __launch_bounds__(256) upload_kernel(float* __restrict__ out, const float* __restrict__ w0,
+                                                     const float* __restrict__ W, int64_t ld, int G, int64_t d,
+                                                     float n) {
+  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < d; j += static_cast<int64_t>(gridDim.x) * 256) {
+    const float w = w0[j];
+    float acc = 0.f;
+    for (int g = 0; g < G; ++g) acc += w - W[g * ld + j];
+    out[j] += n * acc;
+  }
+}
+
+// ------------------------------------------------------------------ head
+// x [n][HW][G*C] bf16 -> feat [G][n][2C] fp32 (mean | max over HW), codes
+// [n][G*C] (first argmax)
+__global__ void __launch_bounds__(256) avgmax_head_fwd_kernel(const bf16raw* __restrict__ x, int n, int HW,
+                                                              int G, int C, float* __restrict__ feat,
+                                                              uint8_t* __restrict__ codes) {
+  const int GC = G * C;
+  const int64_t total = static_cast<int64_t>(n) * GC;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int e = static_cast<int>(i / GC), gc = static_cast<int>(i - static_cast<int64_t>(e) * GC);
+    const bf16raw* p = x + static_cast<int64_t>(e) * HW * GC + gc;
+    float s = 0.f, m = bf2f(p[0]);
+    int am = 0;
+    for (int h = 0; h < HW; ++h) {
+      const float v = bf2f(p[static_cast<int64_t>(h) * GC]);
+      s += v;
+      if (v > m) {
+        m = v;
+        am = h;
+      }
+    }
+    const int g = gc / C, c = gc - g * C;
+    float* f = feat + (static_cast<int64_t>(g) * n + e) * 2 * C;
+    f[c] = s / HW;
+    f[C + c] = m;
+    codes[i] = static_cast<uint8_t>(am);
+  }
+}
+
+// dx[e][h][g*C + c] = df[g][e][c] / HW + (h == code ? df[g][e][C + c] : 0)
+__global__ void __launch_bounds__(256) avgmax_head_bwd_kernel(const float* __restrict__ df,
+                                                              const uint8_t* __restrict__ codes, int n, int HW,
+                                                              int G, int C, bf16raw* __restrict__ dx) {
+  const int GC = G * C;
+  const int64_t total = static_cast<int64_t>(n) * HW * GC;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int gc = static_cast<int>(i % GC);
+    const int64_t eh = i / GC;
+    const int h = static_cast<int>(eh % HW), e = static_cast<int>(eh / HW);
+    const int g = gc / C, c = gc - g * C;
+    const float* f = df + (static_cast<int64_t>(g) * n + e) * 2 * C;
+    float v = f[c] / HW;
+    if (codes[static_cast<int64_t>(e) * GC + gc] == h) v += f[C + c];
+    dx[i] = f2bf(v);
+  }
+}
+
+// ------------------------------------------------------------ elementwise
+// mode 0: y = a + b;  mode 1: y = relu(a)   (n8 chunks of 8 bf16)
+__global__ void __launch_bounds__(256) ew_bf16_kernel(const bf16raw* __restrict__ a, const bf16raw* __restrict__ b,
+                                                      bf16raw* __restrict__ y, int64_t n8, int mode) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n8; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const u4 va = reinterpret_cast<const u4*>(a)[i];
+    u4 o;
+    if (mode == 0) {
+      const u4 vb = reinterpret_cast<const u4*>(b)[i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = bf2f(static_cast<bf16raw>(va[q] & 0xffffu)) + bf2f(static_cast<bf16raw>(vb[q] & 0xffffu));
+        const float hi = bf2f(static_cast<bf16raw>(va[q] >> 16)) + bf2f(static_cast<bf16raw>(vb[q] >> 16));
+        o[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t lo = va[q] & 0xffffu, hi = va[q] >> 16;
+        o[q] = ((lo & 0x8000u) ? 0u : lo) | (((hi & 0x8000u) ? 0u : hi) << 16);
+      }
+    }
+    reinterpret_cast<u4*>(y)[i] = o;
+  }
+}
+
+}  // namespace
+
+void launch_weight_image(const float* W, int64_t ld, int G, int K, int C, int RS, int Kc, int kind,
+                         uint16_t* dst, hipStream_t stream) {
+  const int64_t per = kind == 2 ? static_cast<int64_t>(K) * Kc : static_cast<int64_t>(K) * C * RS;
+  if (per * G == 0) return;
+  COMMEFF_LAUNCH(weight_image_kernel, dim3(grid_for(per * G)), dim3(256), 0, stream, W, ld, G, K, C, RS, Kc,
+                 kind, dst);
+}
+
+void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const float* Gr, int64_t gld, int G,
+                    int64_t d4, float clip, float lr, float wd, float* part, hipStream_t stream) {
+  if (G == 0 || d4 == 0) return;
+  if (clip > 0.f)
+    COMMEFF_LAUNCH(row_sumsq_kernel, dim3(kRowParts, G), dim3(256), 0, stream, Gr, gld, d4, part);
+  int bx = static_cast<int>((d4 + 255) / 256);
+  const int cap = (8192 + G - 1) / G;
+  if (bx > cap) bx = cap;
+  COMMEFF_LAUNCH(row_sgd_kernel, dim3(bx < 1 ? 1 : bx, G), dim3(256), 0, stream, W, ld, src, sld, Gr, gld, d4,
+                 part, clip, lr, wd);
+}
+
+int row_sgd_parts() { return kRowParts; }
+
+void launch_fedavg_upload(float* out, const float* w0, const float* W, int64_t ld, int G, int64_t d, float n,
+                          hipStream_t stream) {
+  if (d == 0) return;
+  COMMEFF_LAUNCH(upload_kernel, dim3(grid_for(d)), dim3(256), 0, stream, out, w0, W, ld, G, d, n);
+}
+
+void launch_avgmax_head_fwd(const uint16_t* x, int n, int HW, int G, int C, float* feat, uint8_t* codes,
+                            hipStream_t stream) {
+  const int64_t total = static_cast<int64_t>(n) * G * C;
+  if (total == 0) return;
+  COMMEFF_LAUNCH(avgmax_head_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, stream, x, n, HW, G, C, feat,
+                 codes);
+}
+
+void launch_avgmax_head_bwd(const float* df, const uint8_t* codes, int n, int HW, int G, int C, uint16_t* dx,
+                            hipStream_t stream) {
+  const int64_t total = static_cast<int64_t>(n) * HW * G * C;
+  if (total == 0) return;
+  COMMEFF_LAUNCH(avgmax_head_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, stream, df, codes, n, HW, G, C,
+                 dx);
+}
+
+void launch_ew_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n8, int mode, hipStream_t stream) {
+  if (n8 == 0) return;
+  COMMEFF_LAUNCH(ew_bf16_kernel, dim3(grid_for(n8)), dim3(256), 0, stream, a, b, y, n8, mode);
+}
+
+}  // namespace commeff

@@ -1,0 +1,363 @@
+// torch.ops.commeff registrations of the batched FedAvg engine
+// (parallel/fedavg_native.py): grouped column images, channel-stacked batch
+// norm, per-client weight images / gradient rows, the per-row SGD tail and the
+// upload (csrc/fedavg.hip, csrc/im2col.hip, csrc/bn.hip, csrc/conv.hip).
+// GPU only: the engine runs when the extension is loaded on a GPU; the CPU
+// path of batched FedAvg is the vmap composition in parallel/fed_model.py.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include "kernels.h"
+
+namespace commeff {
+
+void launch_weight_image(const float* W, int64_t ld, int G, int K, int C, int RS, int Kc, int kind,
+                         uint16_t* dst, hipStream_t stream);
+void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const float* Gr, int64_t gld, int G,
+                    int64_t d4, float clip, float lr, float wd, float* part, hipStream_t stream);
+int row_sgd_parts();
+void launch_fedavg_upload(float* out, const float* w0, const float* W, int64_t ld, int G, int64_t d, float n,
+                          hipStream_t stream);
+void launch_avgmax_head_fwd(const uint16_t* x, int n, int HW, int G, int C, float* feat, uint8_t* codes,
+                            hipStream_t stream);
+void launch_avgmax_head_bwd(const float* df, const uint8_t* codes, int n, int HW, int G, int C, uint16_t* dx,
+                            hipStream_t stream);
+void launch_ew_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n8, int mode, hipStream_t stream);
+
+namespace {
+
+hipStream_t stream_now() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void check_cl_bf16(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4 &&
+                  t.is_contiguous(at::MemoryFormat::ChannelsLast),
+              name, " must be a bf16 NCHW tensor with channels_last memory");
+}
+
+const uint16_t* bf(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bfw(at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+// fp32 parameter / gradient rows: a contiguous [rows, ld] (or flat) tensor
+// holding `rows` rows of ld floats; [off, off + span) must lie inside a row
+// (ld 0: one row shared by every group -- the server weights of the first local step)
+void check_rows(const at::Tensor& t, int64_t ld, int64_t rows, int64_t off, int64_t span, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), name,
+              " must be a contiguous fp32 device tensor");
+  TORCH_CHECK(rows >= 1 && off >= 0 && span >= 0 && ld >= 0 && (ld == 0 || off + span <= ld) &&
+                  (rows - 1) * ld + off + span <= t.numel(),
+              name, ": [", off, ", ", off + span, ") of ", rows, " rows of ", ld, " floats exceeds ", t.numel());
+}
+
+int64_t out_size(int64_t in, int64_t k, int64_t stride, int64_t pad) { return (in + 2 * pad - k) / stride + 1; }
+
+// per-client bf16 images of conv weights held in fp32 rows W[g*ld + off + (k*C + c)*RS + t]:
+// kind 0 -> [G*K, R, S, C] (halo forward), 1 -> [G*C, R, S, K] (flipped, halo dgrad),
+// 2 -> [G, K, Kc] (column-GEMM image, (r, s, c) columns, zero padding)
+at::Tensor fa_weight_image(const at::Tensor& W, int64_t ld, int64_t G, int64_t off, int64_t K, int64_t C,
+                           int64_t R, int64_t Kc, int64_t kind) {
+  const int64_t RS = R * R;
+  check_rows(W, ld, G, off, K * C * RS, "fa_weight_image: W");
+  TORCH_CHECK(kind >= 0 && kind <= 2 && K >= 1 && C >= 1 && R >= 1, "fa_weight_image: kind / shape");
+  TORCH_CHECK(kind != 2 || (Kc % 8 == 0 && Kc >= RS * C), "fa_weight_image: Kc");
+  TORCH_CHECK(G * K * std::max(Kc, C * RS) < (int64_t{1} << 40), "fa_weight_image: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  auto o = W.options().dtype(at::kBFloat16);
+  at::Tensor dst = kind == 0 ? at::empty({G * K, R, R, C}, o)
+                   : kind == 1 ? at::empty({G * C, R, R, K}, o)
+                               : at::empty({G, K, Kc}, o);
+  launch_weight_image(W.data_ptr<float>() + off, ld, static_cast<int>(G), static_cast<int>(K),
+                      static_cast<int>(C), static_cast<int>(RS), static_cast<int>(Kc), static_cast<int>(kind),
+                      bfw(dst), stream_now());
+  return dst;
+}
+
+// W[g] = src[g] - lr (scale_g G[g] + wd src[g]) for g < rows (src ld 0: one
+// broadcast row); scale_g = min(1, clip / |G[g]|) when clip > 0
+void fa_row_sgd(at::Tensor W, int64_t ld, const at::Tensor& src, int64_t sld, const at::Tensor& Gr, int64_t gld,
+                int64_t rows, int64_t d, double clip, double lr, double wd) {
+  const int64_t d4 = (d + 3) / 4;
+  TORCH_CHECK(ld % 4 == 0 && sld % 4 == 0 && gld % 4 == 0 && d4 * 4 <= std::min(ld, gld),
+              "fa_row_sgd: row strides must be multiples of 4 holding d");
+  check_rows(W, ld, rows, 0, d4 * 4, "fa_row_sgd: W");
+  check_rows(Gr, gld, rows, 0, d4 * 4, "fa_row_sgd: G");
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kFloat && src.is_contiguous() &&
+                  src.numel() >= (sld == 0 ? d4 * 4 : rows * sld) && (sld == 0 || sld >= d4 * 4),
+              "fa_row_sgd: src rows");
+  for (const at::Tensor* t : {static_cast<const at::Tensor*>(&W), &src, &Gr})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "fa_row_sgd: 16-byte aligned rows");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  at::Tensor part;
+  if (clip > 0) part = at::empty({rows * row_sgd_parts()}, W.options());
+  launch_row_sgd(W.data_ptr<float>(), ld, src.data_ptr<float>(), sld, Gr.data_ptr<float>(), gld,
+                 static_cast<int>(rows), d4, static_cast<float>(clip), static_cast<float>(lr),
+                 static_cast<float>(wd), clip > 0 ? part.data_ptr<float>() : nullptr, stream_now());
+}
+
+// out[j] += n sum_g (w0[j] - W[g*ld + j]), j < d
+void fa_upload(at::Tensor out, const at::Tensor& w0, const at::Tensor& W, int64_t ld, int64_t rows, double n) {
+  const int64_t d = out.numel();
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && w0.numel() == d &&
+                  w0.scalar_type() == at::kFloat && w0.is_contiguous(),
+              "fa_upload: out / w0 fp32 [d]");
+  check_rows(W, ld, rows, 0, d, "fa_upload: W");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
+  launch_fedavg_upload(out.data_ptr<float>(), w0.data_ptr<float>(), W.data_ptr<float>(), ld,
+                       static_cast<int>(rows), d, static_cast<float>(n), stream_now());
+}
+
+// x [n, G*C, h, w] channels_last -> (feat fp32 [G, n, 2C] = mean | max, codes uint8 [n, G*C])
+std::tuple<at::Tensor, at::Tensor> fa_head_fwd(const at::Tensor& x, int64_t G) {
+  check_cl_bf16(x, "fa_head_fwd: x");
+  const int64_t n = x.size(0), GC = x.size(1), HW = x.size(2) * x.size(3);
+  TORCH_CHECK(G >= 1 && GC % G == 0 && HW >= 1 && HW <= 256, "fa_head_fwd: G | channels, <= 256 pixels");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t C = GC / G;
+  auto feat = at::empty({G, n, 2 * C}, x.options().dtype(at::kFloat));
+  auto codes = at::empty({n, GC}, x.options().dtype(at::kByte));
+  launch_avgmax_head_fwd(bf(x), static_cast<int>(n), static_cast<int>(HW), static_cast<int>(G),
+                         static_cast<int>(C), feat.data_ptr<float>(), codes.data_ptr<uint8_t>(), stream_now());
+  return {feat, codes};
+}
+
+at::Tensor fa_head_bwd(const at::Tensor& df, const at::Tensor& codes, int64_t H, int64_t W) {
+  TORCH_CHECK(df.is_cuda() && df.scalar_type() == at::kFloat && df.is_contiguous() && df.dim() == 3 &&
+                  df.size(2) % 2 == 0,
+              "fa_head_bwd: df fp32 [G, n, 2C]");
+  const int64_t G = df.size(0), n = df.size(1), C = df.size(2) / 2;
+  TORCH_CHECK(codes.scalar_type() == at::kByte && codes.is_contiguous() && codes.dim() == 2 &&
+                  codes.size(0) == n && codes.size(1) == G * C && H * W >= 1 && H * W <= 256,
+              "fa_head_bwd: codes uint8 [n, G*C]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(df.device());
+  auto dx = at::empty({n, G * C, H, W}, df.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+  launch_avgmax_head_bwd(df.data_ptr<float>(), codes.data_ptr<uint8_t>(), static_cast<int>(n),
+                         static_cast<int>(H * W), static_cast<int>(G), static_cast<int>(C), bfw(dx), stream_now());
+  return dx;
+}
+
+// mode 0: a + b, mode 1: relu(a) (bf16 channels_last, 8-element multiples)
+at::Tensor fa_ew(const at::Tensor& a, const c10::optional<at::Tensor>& b, int64_t mode) {
+  check_cl_bf16(a, "fa_ew: a");
+  TORCH_CHECK(a.numel() % 8 == 0 && (mode == 0 || mode == 1), "fa_ew: numel % 8, mode 0 / 1");
+  if (mode == 0) {
+    TORCH_CHECK(b.has_value() && b->defined(), "fa_ew: add needs b");
+    check_cl_bf16(*b, "fa_ew: b");
+    TORCH_CHECK(b->sizes() == a.sizes(), "fa_ew: b shape");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto y = at::empty_like(a, a.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_ew_bf16(bf(a), mode == 0 ? bf(*b) : nullptr, bfw(y), a.numel() / 8, static_cast<int>(mode), stream_now());
+  return y;
+}
+
+// grouped column image [P, G, Kc] (P = n*OH*OW): channel-stacked x [n, G*C, H, W]
+// (client_major false) or client-major x [G*n, C, H, W] (true), channels_last
+at::Tensor im2col_grouped(const at::Tensor& x, int64_t G, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                          int64_t Kc, bool client_major) {
+  if (client_major) {  // the augmentation kernel's images: channels innermost, any pixel stride
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.stride(1) == 1 &&
+                    x.stride(3) >= x.size(1) && x.stride(2) >= x.stride(3) * x.size(3) &&
+                    x.stride(0) >= x.stride(2) * x.size(2),
+                "im2col_grouped: client-major x must be bf16 NCHW with channels innermost");
+  } else {
+    check_cl_bf16(x, "im2col_grouped: x");
+  }
+  const int64_t H = x.size(2), W = x.size(3);
+  TORCH_CHECK(G >= 1, "im2col_grouped: G");
+  const int64_t n = client_major ? x.size(0) / G : x.size(0);
+  const int64_t C = client_major ? x.size(1) : x.size(1) / G;
+  TORCH_CHECK(client_major ? x.size(0) % G == 0 : x.size(1) % G == 0, "im2col_grouped: G does not divide");
+  TORCH_CHECK(R >= 1 && S >= 1 && stride >= 1 && pad >= 0 && pad < R && pad < S, "im2col_grouped: geometry");
+  const int64_t OH = out_size(H, R, stride, pad), OW = out_size(W, S, stride, pad);
+  TORCH_CHECK(OH > 0 && OW > 0 && Kc % 8 == 0 && Kc >= R * S * C, "im2col_grouped: Kc / output");
+  const int64_t P = n * OH * OW;
+  TORCH_CHECK(P * G * (Kc / 8) < (int64_t{1} << 32) && x.size(0) * x.stride(0) < (int64_t{1} << 40),
+              "im2col_grouped: 32-bit range");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto col = at::empty({P, G, Kc}, x.options());
+  Im2colArgs a{};
+  a.x = bf(x);
+  a.col = bfw(col);
+  a.N = static_cast<int>(n); a.H = static_cast<int>(H); a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C); a.OH = static_cast<int>(OH); a.OW = static_cast<int>(OW);
+  a.R = static_cast<int>(R); a.S = static_cast<int>(S);
+  a.stride = static_cast<int>(stride); a.pad = static_cast<int>(pad); a.Kc = static_cast<int>(Kc);
+  a.sN = x.stride(0); a.sH = x.stride(2); a.sW = x.stride(3);
+  a.G = static_cast<int>(G);
+  a.sG = client_major ? n * x.stride(0) : C;
+  a.vec = C % 8 == 0 && a.sW % 8 == 0 && a.sH % 8 == 0 && a.sN % 8 == 0 && a.sG % 8 == 0 &&
+          reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0;
+  launch_im2col(a, stream_now());
+  return col;
+}
+
+// gx [n, G*C, H, W] (channels_last, channel-stacked) of gcol [P, G, Kc]
+at::Tensor col2im_grouped(const at::Tensor& gcol, int64_t G, int64_t n, int64_t H, int64_t W, int64_t C,
+                          int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  TORCH_CHECK(gcol.is_cuda() && gcol.scalar_type() == at::kBFloat16 && gcol.dim() == 3 && gcol.is_contiguous(),
+              "col2im_grouped: gcol must be a contiguous bf16 [P, G, Kc] tensor");
+  TORCH_CHECK(C % 8 == 0 && R >= 1 && S >= 1 && stride >= 1 && pad >= 0 && pad < R && pad < S,
+              "col2im_grouped: geometry (C % 8 == 0)");
+  const int64_t OH = out_size(H, R, stride, pad), OW = out_size(W, S, stride, pad);
+  const int64_t Kc = gcol.size(2);
+  TORCH_CHECK(gcol.size(0) == n * OH * OW && gcol.size(1) == G && Kc % 8 == 0 && Kc >= R * S * C,
+              "col2im_grouped: gcol shape");
+  TORCH_CHECK(n * H * W * G * (C / 8) < (int64_t{1} << 32) && gcol.numel() < (int64_t{1} << 40),
+              "col2im_grouped: index range");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gcol.device());
+  auto gx = at::empty({n, G * C, H, W}, gcol.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Im2colArgs a{};
+  a.N = static_cast<int>(n); a.H = static_cast<int>(H); a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C); a.OH = static_cast<int>(OH); a.OW = static_cast<int>(OW);
+  a.R = static_cast<int>(R); a.S = static_cast<int>(S);
+  a.stride = static_cast<int>(stride); a.pad = static_cast<int>(pad); a.Kc = static_cast<int>(Kc);
+  a.G = static_cast<int>(G);
+  launch_col2im(a, bf(gcol), bfw(gx), stream_now());
+  return gx;
+}
+
+// channel-stacked batch norm + ReLU: x [n, G*cg, h, w]; statistics per
+// (client, channel) over the n*h*w pixels; affine parameters from the fp32
+// rows prm[g*ld + woff / boff + c]; running statistics [G*cg] per client
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cs_bn_fwd(const at::Tensor& x, const at::Tensor& prm, int64_t ld,
+                                                         int64_t woff, int64_t boff, int64_t G, double eps,
+                                                         double momentum,
+                                                         const c10::optional<at::Tensor>& run_mean,
+                                                         const c10::optional<at::Tensor>& run_var,
+                                                         const c10::optional<at::Tensor>& nbt) {
+  check_cl_bf16(x, "cs_bn_fwd: x");
+  const int64_t C = x.size(1), M = x.size(0) * x.size(2) * x.size(3);
+  TORCH_CHECK(G >= 1 && C % G == 0 && (C / G) % 8 == 0 && M >= 1, "cs_bn_fwd: G | channels, 8 | channels per client");
+  const int64_t cg = C / G;
+  check_rows(prm, ld, G, std::min(woff, boff), std::max(woff, boff) - std::min(woff, boff) + cg, "cs_bn_fwd: prm");
+  TORCH_CHECK(M * C / 8 < (int64_t{1} << 32), "cs_bn_fwd: tensor too large");
+  float* rm = nullptr;
+  float* rv = nullptr;
+  if (run_mean.has_value() && run_mean->defined()) {
+    TORCH_CHECK(run_var.has_value() && run_var->defined(), "cs_bn_fwd: running stats together");
+    for (const auto* t : {&*run_mean, &*run_var})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C,
+                  "cs_bn_fwd: running stats fp32 [G*cg]");
+    rm = run_mean->data_ptr<float>();
+    rv = run_var->data_ptr<float>();
+  }
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->is_cuda() && nbt->scalar_type() == at::kLong && nbt->numel() == 1, "cs_bn_fwd: nbt int64 []");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto part = at::empty({bn_cs_scratch_floats(static_cast<int>(M), static_cast<int>(C))}, fo);
+  auto stat = at::empty({2, C}, fo);
+  auto ab = at::empty({2, C}, fo);
+  auto y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto bits = at::empty({x.numel() / 8}, x.options().dtype(at::kByte));
+  launch_bn_cs_fwd(bf(x), prm.data_ptr<float>(), ld, woff, boff, static_cast<int>(cg), static_cast<int>(M),
+                   static_cast<int>(C), static_cast<float>(eps), static_cast<float>(momentum), rm, rv, nb,
+                   part.data_ptr<float>(), stat.data_ptr<float>(), ab.data_ptr<float>(), bfw(y),
+                   bits.data_ptr<uint8_t>(), stream_now());
+  return {y, stat, bits};
+}
+
+// backward of cs_bn_fwd (ReLU through the forward's bits): returns dx; the
+// per-client weight / bias gradients are written to grad[g*gld + gwoff / gboff + c]
+at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stat, const at::Tensor& bits,
+                     const at::Tensor& prm, int64_t ld, int64_t woff, int64_t G, at::Tensor grad, int64_t gld,
+                     int64_t gwoff, int64_t gboff) {
+  check_cl_bf16(x, "cs_bn_bwd: x");
+  check_cl_bf16(dy, "cs_bn_bwd: dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "cs_bn_bwd: dy shape");
+  const int64_t C = x.size(1), M = x.size(0) * x.size(2) * x.size(3);
+  TORCH_CHECK(G >= 1 && C % G == 0 && (C / G) % 8 == 0, "cs_bn_bwd: G");
+  const int64_t cg = C / G;
+  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.is_contiguous() && stat.numel() == 2 * C,
+              "cs_bn_bwd: stat fp32 [2, C]");
+  TORCH_CHECK(bits.is_cuda() && bits.scalar_type() == at::kByte && bits.is_contiguous() && bits.numel() == x.numel() / 8,
+              "cs_bn_bwd: bits uint8 [numel / 8]");
+  check_rows(prm, ld, G, woff, cg, "cs_bn_bwd: prm");
+  check_rows(grad, gld, G, std::min(gwoff, gboff), std::max(gwoff, gboff) - std::min(gwoff, gboff) + cg,
+             "cs_bn_bwd: grad");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto part = at::empty({bn_cs_scratch_floats(static_cast<int>(M), static_cast<int>(C))}, fo);
+  auto coef = at::empty({3 * C}, fo);
+  auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  launch_bn_cs_bwd(bf(x), bf(dy), bits.data_ptr<uint8_t>(), stat.data_ptr<float>(), prm.data_ptr<float>(), ld,
+                   woff, static_cast<int>(cg), static_cast<int>(M), static_cast<int>(C), part.data_ptr<float>(),
+                   coef.data_ptr<float>(), grad.data_ptr<float>(), gld, gwoff, gboff, bfw(dx), stream_now());
+  return dx;
+}
+
+// channel-stacked grouped 3x3 wgrad (halo kernel) written into the per-client
+// gradient rows dst[g*ld + off + (k*C + c)*9 + t]; false (nothing written)
+// where the geometry has no grouped halo tiling
+bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at::Tensor dst, int64_t ld,
+                        int64_t off) {
+  check_cl_bf16(dy, "conv3x3_wgrad_rows: dy");
+  check_cl_bf16(x, "conv3x3_wgrad_rows: x");
+  const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W && G >= 1 && GC % G == 0 && K % G == 0,
+              "conv3x3_wgrad_rows: shapes");
+  const int64_t C = GC / G, kg = K / G;
+  if (!conv3x3_wgrad_grouped_supported(static_cast<int>(H), static_cast<int>(W), static_cast<int>(K),
+                                       static_cast<int>(C), static_cast<int>(kg)))
+    return false;
+  check_rows(dst, ld, G, off, kg * C * 9, "conv3x3_wgrad_rows: dst");
+  TORCH_CHECK(N * H * W * std::max(GC, K) < (int64_t{1} << 31), "conv3x3_wgrad_rows: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int P = static_cast<int>(N * H * W);
+  const int splits = conv3x3_wgrad_splits(P, static_cast<int>(H), static_cast<int>(W), static_cast<int>(K),
+                                          static_cast<int>(C));
+  auto slab = at::empty({splits * K * 9 * C}, x.options().dtype(at::kFloat));
+  ConvWgradArgs a;
+  a.dy = bf(dy);
+  a.x = bf(x);
+  a.slab = slab.data_ptr<float>();
+  a.P = P;
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.splits = splits;
+  a.x_stride = static_cast<int>(GC);
+  a.kg = static_cast<int>(kg);
+  launch_conv3x3_wgrad_rows(a, dst.data_ptr<float>() + off, static_cast<int>(kg), ld, stream_now());
+  return true;
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(commeff, m) {
+  m.def("fa_weight_image(Tensor W, int ld, int G, int off, int K, int C, int R, int Kc, int kind) -> Tensor");
+  m.def("fa_row_sgd(Tensor(a!) W, int ld, Tensor src, int sld, Tensor G, int gld, int rows, int d, float clip, "
+        "float lr, float wd) -> ()");
+  m.def("fa_upload(Tensor(a!) out, Tensor w0, Tensor W, int ld, int rows, float n) -> ()");
+  m.def("fa_head_fwd(Tensor x, int G) -> (Tensor, Tensor)");
+  m.def("fa_head_bwd(Tensor df, Tensor codes, int H, int W) -> Tensor");
+  m.def("fa_ew(Tensor a, Tensor? b, int mode) -> Tensor");
+  m.def("im2col_grouped(Tensor x, int G, int R, int S, int stride, int pad, int Kc, bool client_major) -> Tensor");
+  m.def("col2im_grouped(Tensor gcol, int G, int n, int H, int W, int C, int R, int S, int stride, int pad) -> Tensor");
+  m.def("cs_bn_fwd(Tensor x, Tensor prm, int ld, int woff, int boff, int G, float eps, float momentum, "
+        "Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt) -> (Tensor, Tensor, Tensor)");
+  m.def("cs_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor bits, Tensor prm, int ld, int woff, int G, "
+        "Tensor(a!) grad, int gld, int gwoff, int gboff) -> Tensor");
+  m.def("conv3x3_wgrad_rows(Tensor dy, Tensor x, int G, Tensor(a!) dst, int ld, int off) -> bool");
+}
+
+TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
+  m.impl("fa_weight_image", &fa_weight_image);
+  m.impl("fa_row_sgd", &fa_row_sgd);
+  m.impl("fa_upload", &fa_upload);
+  m.impl("fa_head_fwd", &fa_head_fwd);
+  m.impl("fa_head_bwd", &fa_head_bwd);
+  m.impl("fa_ew", &fa_ew);
+  m.impl("im2col_grouped", &im2col_grouped);
+  m.impl("col2im_grouped", &col2im_grouped);
+  m.impl("cs_bn_fwd", &cs_bn_fwd);
+  m.impl("cs_bn_bwd", &cs_bn_bwd);
+  m.impl("conv3x3_wgrad_rows", &conv3x3_wgrad_rows);
+}
+
+}  // namespace commeff

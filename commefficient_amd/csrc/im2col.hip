@@ -59,8 +59,9 @@ int blocks_for(int64_t n) {
 struct ColGeom {
   int H, W, C, OH, OW, R, S, stride, pad, Kc, KC8;
   int64_t sN, sH, sW;  // input strides in elements (channel stride 1)
-  uint32_t total;      // P * Kc / 8
-  FastDivU32 d_kc8, d_ow, d_oh, d_c8, d_s, d_c;
+  int64_t sG;          // grouped: input offset of group g's channels / images
+  uint32_t total;      // P * G * Kc / 8
+  FastDivU32 d_kc8, d_ow, d_oh, d_c8, d_s, d_c, d_g;
 };
 
 __device__ __forceinline__ void col_row(uint32_t p, const ColGeom& q, int& n, int& oh, int& ow) {
@@ -77,8 +78,10 @@ __global__ void __launch_bounds__(256) im2col_vec_kernel(const bf16raw* __restri
   const uint32_t step = gridDim.x * blockDim.x;
   const int taps = q.R * q.S;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
-    const uint32_t p = fdiv(g, q.d_kc8);
-    const uint32_t j8 = g - p * q.KC8;
+    const uint32_t pg = fdiv(g, q.d_kc8);  // (pixel, group) row of the [P][G][Kc] image
+    const uint32_t j8 = g - pg * q.KC8;
+    const uint32_t p = fdiv(pg, q.d_g);
+    const bf16raw* xg = x + static_cast<int64_t>(pg - p * static_cast<uint32_t>(q.d_g.d)) * q.sG;
     const uint32_t tap = fdiv(j8, q.d_c8);
     const uint32_t c8 = j8 - tap * (q.C / 8);
     V8 v;
@@ -92,7 +95,7 @@ __global__ void __launch_bounds__(256) im2col_vec_kernel(const bf16raw* __restri
       const int ih = oh * q.stride - q.pad + static_cast<int>(r);
       const int iw = ow * q.stride - q.pad + s;
       if (ih >= 0 && ih < q.H && iw >= 0 && iw < q.W)
-        v = *reinterpret_cast<const V8*>(x + n * q.sN + ih * q.sH + iw * q.sW + c8 * 8);
+        v = *reinterpret_cast<const V8*>(xg + n * q.sN + ih * q.sH + iw * q.sW + c8 * 8);
     }
     *reinterpret_cast<V8*>(col + static_cast<size_t>(g) * 8) = v;
   }
@@ -104,11 +107,12 @@ __global__ void __launch_bounds__(256) im2col_any_kernel(const bf16raw* __restri
   const uint32_t step = gridDim.x * blockDim.x;
   const int rsc = q.R * q.S * q.C;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
-    const uint32_t p = fdiv(g, q.d_kc8);
-    const int j0 = static_cast<int>(g - p * q.KC8) * 8;
+    const uint32_t pg = fdiv(g, q.d_kc8);
+    const int j0 = static_cast<int>(g - pg * q.KC8) * 8;
+    const uint32_t p = fdiv(pg, q.d_g);
     int n, oh, ow;
     col_row(p, q, n, oh, ow);
-    const bf16raw* xn = x + n * q.sN;
+    const bf16raw* xn = x + static_cast<int64_t>(pg - p * static_cast<uint32_t>(q.d_g.d)) * q.sG + n * q.sN;
     V8 v;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -131,19 +135,22 @@ __global__ void __launch_bounds__(256) im2col_any_kernel(const bf16raw* __restri
 
 // ---------------------------------------------------------------- col2im
 struct GatherGeom {
-  int H, W, C, OH, OW, R, S, stride, pad, Kc;
-  uint32_t total;  // N * H * W * C / 8
-  FastDivU32 d_c8, d_w, d_h;
+  int H, W, C, OH, OW, R, S, stride, pad, Kc, G;  // C per group; gcol [P][G][Kc]
+  uint32_t total;  // N * H * W * G * C / 8
+  FastDivU32 d_c8, d_w, d_h, d_gc8;  // d_c8: G*C/8 per pixel, d_gc8: C/8 per group
 };
 
 // gx[n][h][w][c] = sum over taps (r, s) hitting (h, w) of gcol[p(oh, ow)][(r*S+s)*C + c]
 __global__ void __launch_bounds__(256) col2im_kernel(const bf16raw* __restrict__ gcol,
                                                      bf16raw* __restrict__ gx, GatherGeom q) {
   const uint32_t step = gridDim.x * blockDim.x;
-  const int C8 = q.C / 8;
+  const int C8 = q.G * q.C / 8;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
     const uint32_t pix = fdiv(g, q.d_c8);
-    const int c8 = static_cast<int>(g - pix * C8);
+    const int gc8 = static_cast<int>(g - pix * C8);
+    const int grp = static_cast<int>(fdiv(static_cast<uint32_t>(gc8), q.d_gc8));
+    const int c8 = gc8 - grp * (q.C / 8);
+    const bf16raw* gsrc = gcol + static_cast<size_t>(grp) * q.Kc;
     const uint32_t p2 = fdiv(pix, q.d_w);
     const int w = static_cast<int>(pix - p2 * q.W);
     const uint32_t n = fdiv(p2, q.d_h);
@@ -162,7 +169,7 @@ __global__ void __launch_bounds__(256) col2im_kernel(const bf16raw* __restrict__
         const int ow = tw / q.stride;
         if (ow >= q.OW) continue;
         const size_t p = (static_cast<size_t>(n) * q.OH + oh) * q.OW + ow;
-        const V8 v = *reinterpret_cast<const V8*>(gcol + p * q.Kc + (r * q.S + s) * q.C + c8 * 8);
+        const V8 v = *reinterpret_cast<const V8*>(gsrc + p * q.G * q.Kc + (r * q.S + s) * q.C + c8 * 8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += bf2f(v.h[e]);
       }
@@ -359,14 +366,17 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16raw* __restr
 }  // namespace
 
 void launch_im2col(const Im2colArgs& a, hipStream_t stream) {
+  const int G = a.G > 1 ? a.G : 1;
   const int64_t P = static_cast<int64_t>(a.N) * a.OH * a.OW;
-  const int64_t total = P * (a.Kc / 8);
+  const int64_t total = P * G * (a.Kc / 8);
   if (total == 0) return;
   ColGeom q;
   q.H = a.H; q.W = a.W; q.C = a.C; q.OH = a.OH; q.OW = a.OW; q.R = a.R; q.S = a.S;
   q.stride = a.stride; q.pad = a.pad; q.Kc = a.Kc; q.KC8 = a.Kc / 8;
   q.sN = a.sN; q.sH = a.sH; q.sW = a.sW;
+  q.sG = a.sG;
   q.total = static_cast<uint32_t>(total);
+  q.d_g = make_fastdiv(G);
   q.d_kc8 = make_fastdiv(q.KC8);
   q.d_ow = make_fastdiv(a.OW);
   q.d_oh = make_fastdiv(a.OH);
@@ -380,13 +390,15 @@ void launch_im2col(const Im2colArgs& a, hipStream_t stream) {
 }
 
 void launch_col2im(const Im2colArgs& a, const uint16_t* gcol, uint16_t* gx, hipStream_t stream) {
-  const int64_t total = static_cast<int64_t>(a.N) * a.H * a.W * (a.C / 8);
+  const int G = a.G > 1 ? a.G : 1;
+  const int64_t total = static_cast<int64_t>(a.N) * a.H * a.W * G * (a.C / 8);
   if (total == 0) return;
   GatherGeom q;
   q.H = a.H; q.W = a.W; q.C = a.C; q.OH = a.OH; q.OW = a.OW; q.R = a.R; q.S = a.S;
-  q.stride = a.stride; q.pad = a.pad; q.Kc = a.Kc;
+  q.stride = a.stride; q.pad = a.pad; q.Kc = a.Kc; q.G = G;
   q.total = static_cast<uint32_t>(total);
-  q.d_c8 = make_fastdiv(a.C / 8);
+  q.d_c8 = make_fastdiv(G * a.C / 8);
+  q.d_gc8 = make_fastdiv(a.C / 8);
   q.d_w = make_fastdiv(a.W);
   q.d_h = make_fastdiv(a.H);
   COMMEFF_LAUNCH(col2im_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gcol, gx, q);

@@ -300,6 +300,8 @@ void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
 int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
+// grouped (a.kg, a.x_stride set) wgrad into per-group fp32 rows ld apart
+void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, hipStream_t stream);
 // grouped convs on channel-stacked images (a.kg / a.x_stride set): false when
 // the geometry has no halo tiling (the caller falls back)
 bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream);
@@ -386,6 +388,19 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
 // rows per tile of the GEMM-epilogue batch-norm moments (GemmArgs::stats)
 constexpr int kBnStatTile = 128;
 // y_relu: the forward's 1-bit ReLU mask (one byte per 8 channels of a pixel)
+// channel-stacked clients (C = G * cg channels, one pixel group of M rows):
+// per-channel statistics, affine parameters from per-client fp32 rows
+// (prm[(c / cg) * ld + off + c % cg]), fused ReLU (bits), weight / bias
+// gradients into the per-client gradient rows (grad[(c / cg) * gld + off + c % cg])
+int64_t bn_cs_scratch_floats(int M, int C);
+void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t woff, int64_t boff, int cg,
+                      int M, int C, float eps, float momentum, float* run_mean, float* run_var,
+                      int64_t* nbt, float* part, float* stat, float* ab, uint16_t* y, uint8_t* relu_bits,
+                      hipStream_t stream);
+void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
+                      const float* prm, int64_t ld, int64_t woff, int cg, int M, int C, float* part,
+                      float* coef, float* grad, int64_t gld, int64_t gwoff, int64_t gboff, uint16_t* dx,
+                      hipStream_t stream);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw = nullptr,
@@ -418,6 +433,11 @@ struct Im2colArgs {
   int N, H, W, C, OH, OW, R, S, stride, pad, Kc;
   int64_t sN, sH, sW;
   bool vec;  // C % 8 == 0 and 16-byte aligned pixels: 16-byte moves
+  // grouped column images (batched FedAvg, parallel/fedavg_native.py): G
+  // groups of C channels, group g's input at x + g * sG, col [P][G][Kc]; the
+  // col2im gather then writes gx [N][H][W][G*C].  0 / 0 = one group.
+  int G;
+  int64_t sG;
 };
 void launch_im2col(const Im2colArgs& a, hipStream_t stream);
 // gx NHWC [N][H][W][C] (C % 8 == 0) = the dgrad gather of gcol [N*OH*OW][Kc]

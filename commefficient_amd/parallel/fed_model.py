@@ -195,6 +195,7 @@ class FedModel:
         self.timer = PhaseTimer(bool(getattr(args, "profile_dir", None)), self.device)
         self._payload = None
         self._work = None  # separate work buffer for topk_down / fedavg
+        self._fa_native = None  # parallel/fedavg_native.py engine (built on first use)
         self.last_round = {}
         # bf16 conv-weight images kept across rounds and patched by sparse server
         # steps (ops/nn.py); COMMEFF_WEIGHT_MIRRORS=0: re-derive them every pass
@@ -1164,6 +1165,9 @@ class FedModel:
         normalises with its own batch statistics and updates its own copy of
         the running statistics; the model keeps their mean afterwards (the
         reference's worker model accumulated them client after client)."""
+        eng = self._fedavg_native_engine()
+        if eng is not None:
+            return self._fedavg_native(eng, rb, order, starts, my_slots, mine, counts, W, out)
         from torch.func import grad, vmap
         from torch.nn.utils.stateless import _reparametrize_module
         from ..ops.nn import stock_ops, vmap_native_convs
@@ -1253,6 +1257,70 @@ class FedModel:
         msum[0].index_copy_(0, slots_t, torch.cat(loss_rows))
         for i in range(len(met_rows[0])):
             msum[1 + i].index_copy_(0, slots_t, torch.cat([m[i] for m in met_rows]))
+        return msum
+
+    def _fedavg_native_engine(self):
+        """The explicit G-client program (parallel/fedavg_native.py) when this
+        model / configuration runs there, else None (the vmap composition)."""
+        mode = getattr(self.args, "fedavg_engine", "auto")
+        if mode == "vmap" or self.device.type != "cuda":
+            if mode == "native":
+                raise ValueError("--fedavg_engine native needs a GPU")
+            return None
+        if self._fa_native is None:
+            from .fedavg_native import ResNet18FedAvg
+            ok, why = ResNet18FedAvg.supported(self.model, self.args)
+            if not ok:
+                if mode == "native":
+                    raise ValueError(f"--fedavg_engine native: {why}")
+                self._fa_native = False
+            else:
+                names = [nm for nm, p in self.model.named_parameters() if p.requires_grad]
+                self._fa_native = ResNet18FedAvg(self.model, self.flat, names)
+        return self._fa_native or None
+
+    def _fedavg_native(self, eng, rb, order, starts, my_slots, mine, counts, W, out):
+        """``_fedavg_batched`` on the explicit G-client program: same
+        semantics (per-client BatchNorm statistics, the clients' mean of the
+        running statistics afterwards), no vmap."""
+        a = self.args
+        n = int(counts[my_slots[0]])
+        bs = a.fedavg_batch_size if a.fedavg_batch_size != -1 else n
+        cap = max(2, int(a.grouped_gb * 2 ** 30) // (12 * self.d))
+        per_pass = max(1, min(cap, len(mine)))
+        loss_rows, acc_rows, slot_rows, acc_bufs = [], [], [], None
+        for p0 in range(0, len(mine), per_pass):
+            slots = my_slots[p0:p0 + per_pass]
+            Gp = len(slots)
+            pos = np.concatenate([order[starts[s]:starts[s + 1]] for s in slots])
+            x, y = rb.take(pos)[:2]
+            if not (x.dtype == torch.bfloat16 and x.stride(1) == 1):
+                x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            lm, am, sums = eng.run(self.w, x, y, Gp, n, bs, a.num_fedavg_epochs, self.fedavg_lr,
+                                   a.fedavg_lr_decay, a.weight_decay / a.num_workers,
+                                   a.max_grad_norm, out, first_pass=p0 == 0)
+            acc_bufs = sums if acc_bufs is None else [tuple(u + v for u, v in zip(p, q))
+                                                      for p, q in zip(acc_bufs, sums)]
+            loss_rows.append(lm)
+            acc_rows.append(am)
+            slot_rows.append(slots)
+        with torch.no_grad():  # the clients' mean running statistics, written once
+            for b, (m1, m2, v1, v2) in zip(eng.blocks, acc_bufs):
+                b.m1.running_mean.copy_((m1 / len(mine)).to(b.m1.running_mean.dtype))
+                b.m2.running_mean.copy_((m2 / len(mine)).to(b.m2.running_mean.dtype))
+                b.m1.running_var.copy_((v1 / len(mine)).to(b.m1.running_var.dtype))
+                b.m2.running_var.copy_((v2 / len(mine)).to(b.m2.running_var.dtype))
+            # num_batches_tracked: every BatchNorm layer counts the local steps
+            # (the engine advanced the first layer's counter)
+            nbt0 = eng.blocks[0].m1.num_batches_tracked
+            for b in eng.blocks:
+                for m in (b.m1, b.m2):
+                    if m.num_batches_tracked is not nbt0:
+                        m.num_batches_tracked.copy_(nbt0)
+        msum = torch.zeros(2, W, device=self.device)
+        slots_t = torch.from_numpy(np.concatenate(slot_rows).astype(np.int64)).to(self.device)
+        msum[0].index_copy_(0, slots_t, torch.cat(loss_rows))
+        msum[1].index_copy_(0, slots_t, torch.cat(acc_rows))
         return msum
 
     def _fedavg_client(self, inputs, targets, n):

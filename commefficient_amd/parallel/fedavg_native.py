@@ -1,0 +1,304 @@
+"""Native batched FedAvg local SGD of a ResNet-18 round: G clients as ONE
+explicit program (no vmap, no MIOpen, no stock elementwise ops in the loop).
+
+Reference semantics: /root/reference/CommEfficient/fed_worker.py:61-113 --
+every client copies the server weights, takes ``num_fedavg_epochs`` passes of
+local SGD over its own data (gradient clipping to ``max_grad_norm``, weight
+decay ``wd / num_workers`` at the client's current weights, step
+``lr * decay**step``; utils.py:257-258, fed_worker.py:288-292) and uploads
+``n (w0 - w)``.  Model: /root/reference/CommEfficient/models/fixup_resnet18.py
+(the ResNet18 of models/fixup.py with --batchnorm): stem conv3x3 + ReLU,
+PreActBlocks ``relu(bn1(conv1 x)) -> relu(bn2(conv2 .)) + shortcut(x)``, head
+``linear(avg(x) || max(x))``.
+
+Layout (MI355X-first):
+
+* The G clients' weights are the rows of one fp32 [G, ld] matrix ``Wg``; their
+  gradients the rows of ``Gg``.  Every kernel reads / writes its client's
+  parameters in place -- weight gradients land in their rows directly (no
+  per-parameter concatenation), one per-row clip + weight-decay + SGD kernel
+  updates every client (csrc/fedavg.hip), and the first local step reads the
+  server weights as a broadcast row (no G-fold copy).
+* Activations are channel-stacked: [n, G*C, H, W] channels_last, i.e. each
+  pixel row holds the G clients' C channels side by side.  The stride-1 3x3
+  convolutions are the grouped halo MFMA kernels of csrc/conv.hip (forward,
+  and the input gradient on per-client flipped weights; the weight gradient
+  where a grouped halo tiling exists); batch norm is per channel, i.e. per
+  (client, channel) -- each client normalises with its own batch statistics
+  and keeps its own running statistics (csrc/bn.hip, channel-stacked path);
+  the strided convolutions and 1x1 shortcuts are grouped column images
+  (csrc/im2col.hip) times per-client weight images in strided-batched
+  library GEMMs (the shortcut reads the column image's centre tap, which IS
+  the stride-2 subsampled input, and its input gradient is added into that
+  tap before the one col2im gather).
+* The head pools the 4x4 maps of all clients in one kernel into per-client
+  [n, 512] fp32 features; the classifier is a batched fp32 GEMM on the
+  weight rows themselves.
+
+``supported(model, args)`` says whether a model / configuration runs here;
+FedModel falls back to the vmap composition otherwise.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .. import _ext
+
+
+def _ops():
+    return _ext.ops()
+
+
+def _gview(t: torch.Tensor, G: int) -> torch.Tensor:
+    """[n, G*K, H, W] channels_last -> [G, n*H*W, K] strided view (per-client
+    GEMM operand / output: batch stride K, row stride G*K)."""
+    n, GK, H, W = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * H * W, G, GK // G).transpose(0, 1)
+
+
+class _Block:
+    __slots__ = ("cin", "cout", "stride", "bn1w", "bn1b", "conv1", "bn2w", "bn2b", "conv2", "sc",
+                 "m1", "m2")
+
+
+class ResNet18FedAvg:
+    """Explicit G-client forward / backward / local SGD of models.fixup.ResNet18
+    (BatchNorm variant).  Construct once per FedModel; ``round(...)`` runs one
+    pass of clients."""
+
+    @staticmethod
+    def supported(model, args) -> Tuple[bool, str]:
+        from ..models.common import GhostBatchNorm2d
+        from ..models.fixup import ResNet18
+        if not isinstance(model, ResNet18):
+            return False, "not the ResNet18 of models/fixup.py"
+        if getattr(args, "dtype", "bf16") != "bf16":
+            return False, "bf16 compute only"
+        for m in model.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+                if not (isinstance(m, GhostBatchNorm2d) and m.affine and m.track_running_stats
+                        and m.momentum is not None and m.fuse_relu):
+                    return False, "BatchNorm layers must be affine GhostBatchNorm2d with ReLU"
+        for p in model.parameters():
+            if not p.requires_grad:
+                return False, "frozen parameters"
+        return True, ""
+
+    def __init__(self, model, flat, names: List[str]):
+        self.model = model
+        off = {nm: int(o) for nm, o in zip(names, flat.offsets)}
+        self.d = int(flat.d) if hasattr(flat, "d") else int(sum(flat.numels))
+        self.off = off
+        self.prep = off["prep.0.weight"]
+        self.blocks: List[_Block] = []
+        for li, layer in enumerate(model.layers):
+            for bi, blk in enumerate(layer):
+                p = f"layers.{li}.{bi}."
+                b = _Block()
+                b.cin, b.cout = blk.conv1.in_channels, blk.conv1.out_channels
+                b.stride = blk.conv1.stride[0]
+                b.bn1w, b.bn1b = off[p + "bn1.weight"], off[p + "bn1.bias"]
+                b.bn2w, b.bn2b = off[p + "bn2.weight"], off[p + "bn2.bias"]
+                b.conv1, b.conv2 = off[p + "conv1.weight"], off[p + "conv2.weight"]
+                b.sc = off.get(p + "shortcut.0.weight")
+                b.m1, b.m2 = blk.bn1, blk.bn2
+                if b.sc is None and (b.stride != 1 or b.cin != b.cout):
+                    raise ValueError("ResNet18FedAvg: block without a shortcut changes shape")
+                if b.sc is not None and b.stride != 2:
+                    raise ValueError("ResNet18FedAvg: stride-1 projection shortcuts are not wired")
+                self.blocks.append(b)
+        self.fc_w, self.fc_b = off["classifier.weight"], off["classifier.bias"]
+        self.ncls = model.classifier.out_features
+        self.feat = model.classifier.in_features
+        self.c0 = model.prep[0].out_channels
+        self.cin0 = model.prep[0].in_channels
+
+    # ----------------------------------------------------------- helpers
+    def _img(self, cache: Dict, W: torch.Tensor, ld: int, G: int, off: int, K: int, C: int, R: int,
+             kind: int) -> torch.Tensor:
+        key = (off, kind)
+        t = cache.get(key)
+        if t is None:
+            Kc = (R * R * C + 7) // 8 * 8
+            t = _ops().fa_weight_image(W, ld, G, off, K, C, R, Kc, kind)
+            cache[key] = t
+        return t
+
+    def _conv3(self, x, cache, W, ld, G, off, K, C):
+        """stride-1 3x3 conv of channel-stacked x with the clients' weights"""
+        y = _ops().conv3x3_fwd_grouped(x, self._img(cache, W, ld, G, off, K, C, 3, 0), G)
+        if y.numel() == 0 and x.numel():
+            col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
+            n, _, H, Wd = x.shape
+            y = torch.empty((n, G * K, H, Wd), device=x.device, dtype=torch.bfloat16,
+                            memory_format=torch.channels_last)
+            torch.bmm(col.transpose(0, 1), self._img(cache, W, ld, G, off, K, C, 3, 2).transpose(1, 2),
+                      out=_gview(y, G))
+        return y
+
+    def _conv3_dgrad(self, dy, cache, W, ld, G, off, K, C):
+        dx = _ops().conv3x3_fwd_grouped(dy, self._img(cache, W, ld, G, off, K, C, 3, 1), G)
+        if dx.numel() == 0 and dy.numel():
+            n, _, H, Wd = dy.shape
+            dcol = torch.empty((n * H * Wd, G, 9 * C), device=dy.device, dtype=torch.bfloat16)
+            torch.bmm(_gview(dy, G), self._img(cache, W, ld, G, off, K, C, 3, 2),
+                      out=dcol.transpose(0, 1))
+            dx = _ops().col2im_grouped(dcol, G, n, H, Wd, C, 3, 3, 1, 1)
+        return dx
+
+    def _conv3_wgrad(self, dy, x, G, Gg, gld, off, K, C):
+        if _ops().conv3x3_wgrad_rows(dy, x, G, Gg, gld, off):
+            return
+        col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
+        part = torch.bmm(_gview(dy, G).transpose(1, 2), col.transpose(0, 1), out_dtype=torch.float32)
+        dst = Gg[:, off:off + K * C * 9].view(G, K, C * 9)
+        _ops().wgrad_rsc_add(dst, part, 1, C, 9, False)
+
+    # ------------------------------------------------------------- round
+    def run(self, w0: torch.Tensor, x: torch.Tensor, y: torch.Tensor, G: int, n: int, bs: int,
+            epochs: int, lr: float, decay: float, wd: float, clip: Optional[float],
+            out: torch.Tensor, first_pass: bool):
+        """Local SGD of G clients (client-major batch x [G*n, 3, H, W], labels
+        y [G*n]); adds sum_g n (w0 - w_g) to ``out``.  Returns (per-client mean
+        loss [G], per-client mean accuracy [G]) over the local steps."""
+        ops = _ops()
+        dev = w0.device
+        d = self.d
+        ld = (d + 63) // 64 * 64
+        Wg = torch.empty((G, ld), device=dev, dtype=torch.float32)
+        Gg = torch.zeros((G, ld), device=dev, dtype=torch.float32)
+        # per-client running statistics (the model keeps their mean)
+        run = []
+        for b in self.blocks:
+            run.append(tuple(m.running_mean.detach().float().repeat(G).contiguous() for m in (b.m1, b.m2))
+                       + tuple(m.running_var.detach().float().repeat(G).contiguous() for m in (b.m1, b.m2)))
+        nbt = self.blocks[0].m1.num_batches_tracked if first_pass else None
+        loss_acc = torch.zeros(G, device=dev)
+        acc_acc = torch.zeros(G, device=dev)
+        ones = torch.ones((G, max(n, bs), 1), device=dev)
+        steps = 0
+        xv = x.view(G, n, *x.shape[1:]) if bs < n else None
+        for _ in range(epochs):
+            for s0 in range(0, n, bs):
+                s1 = min(n, s0 + bs)
+                if bs < n:
+                    xb = xv[:, s0:s1].reshape(G * (s1 - s0), *x.shape[1:]).contiguous(
+                        memory_format=torch.channels_last)
+                    yb = y.view(G, n)[:, s0:s1].reshape(-1).contiguous()
+                else:
+                    xb, yb = x, y
+                src, sld = (w0, 0) if steps == 0 else (Wg, ld)
+                l, c = self._step(xb, yb, G, s1 - s0, src, sld, Gg, ld, run,
+                                  nbt, ones)
+                loss_acc += l
+                acc_acc += c
+                ops.fa_row_sgd(Wg, ld, src, sld, Gg, ld, G, d, float(clip or 0.0),
+                               float(lr * decay ** steps), float(wd))
+                steps += 1
+        ops.fa_upload(out, w0, Wg, ld, G, float(n))
+        # running statistics: per-client copies summed for the caller's mean
+        sums = []
+        for b, (rm1, rm2, rv1, rv2) in zip(self.blocks, run):
+            sums.append((rm1.view(G, -1).double().sum(0), rm2.view(G, -1).double().sum(0),
+                         rv1.view(G, -1).double().sum(0), rv2.view(G, -1).double().sum(0)))
+        return loss_acc / steps, acc_acc / steps, sums
+
+    def _step(self, x, y, G, n, W, ld, Gg, gld, run, nbt, ones):
+        """One local step of every client: forward, backward into Gg."""
+        ops = _ops()
+        cache: Dict = {}
+        # ---- stem: grouped column image of the client-major input
+        C0, K0 = self.cin0, self.c0
+        Kc0 = (9 * C0 + 7) // 8 * 8
+        col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        H, Wd = x.shape[2], x.shape[3]
+        y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
+                         memory_format=torch.channels_last)
+        torch.bmm(col0.transpose(0, 1), self._img(cache, W, ld, G, self.prep, K0, C0, 3, 2).transpose(1, 2),
+                  out=_gview(y0, G))
+        a = ops.fa_ew(y0, None, 1)
+        a0 = a
+        saved = []
+        eps_m = [(b.m1.eps, b.m1.momentum, b.m2.eps, b.m2.momentum) for b in self.blocks]
+        for bi, b in enumerate(self.blocks):
+            xin = a
+            rm1, rm2, rv1, rv2 = run[bi]
+            e1, mo1, e2, mo2 = eps_m[bi]
+            colx = None
+            if b.stride == 1:
+                h1 = self._conv3(xin, cache, W, ld, G, b.conv1, b.cout, b.cin)
+                sc = xin
+            else:
+                colx = ops.im2col_grouped(xin, G, 3, 3, 2, 1, 9 * b.cin, False)
+                nn_, _, Hi, Wi = xin.shape
+                Ho, Wo = (Hi - 1) // 2 + 1, (Wi - 1) // 2 + 1
+                h1 = torch.empty((nn_, G * b.cout, Ho, Wo), device=x.device, dtype=torch.bfloat16,
+                                 memory_format=torch.channels_last)
+                cg = colx.transpose(0, 1)
+                torch.bmm(cg, self._img(cache, W, ld, G, b.conv1, b.cout, b.cin, 3, 2).transpose(1, 2),
+                          out=_gview(h1, G))
+                sc = torch.empty_like(h1)
+                ctr = cg[:, :, 4 * b.cin:5 * b.cin]
+                torch.bmm(ctr, self._img(cache, W, ld, G, b.sc, b.cout, b.cin, 1, 2).transpose(1, 2),
+                          out=_gview(sc, G))
+            a1, st1, bits1 = ops.cs_bn_fwd(h1, W, ld, b.bn1w, b.bn1b, G, e1, mo1, rm1, rv1,
+                                           nbt if bi == 0 else None)
+            h2 = self._conv3(a1, cache, W, ld, G, b.conv2, b.cout, b.cout)
+            a2, st2, bits2 = ops.cs_bn_fwd(h2, W, ld, b.bn2w, b.bn2b, G, e2, mo2, rm2, rv2, None)
+            a = ops.fa_ew(a2, sc, 0)
+            saved.append((xin, colx, h1, st1, bits1, a1, h2, st2, bits2))
+        # ---- head: avg || max pool -> per-client linear -> cross entropy
+        feat, codes = ops.fa_head_fwd(a, G)
+        # classifier rows of every client (the first step: the server row, batch stride 0)
+        Wr = W if ld else W.unsqueeze(0).expand(G, -1)
+        Wfc = Wr[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
+        bfc = Wr[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
+        logits = torch.bmm(feat, Wfc.transpose(1, 2))
+        logits.baddbmm_(ones[:, :n], bfc)
+        loss, correct, gl = ops.ce_fwd(logits.view(G * n, self.ncls), y)
+        gl = gl.view(G, n, self.ncls)
+        inv = 1.0 / n
+        gW = Gg[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
+        torch.baddbmm(gW, gl.transpose(1, 2), feat, beta=0.0, alpha=inv, out=gW)
+        gb = Gg[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
+        torch.baddbmm(gb, ones[:, :n].transpose(1, 2), gl, beta=0.0, alpha=inv, out=gb)
+        dfeat = torch.empty_like(feat)
+        torch.baddbmm(dfeat, gl, Wfc, beta=0.0, alpha=inv, out=dfeat)
+        da = ops.fa_head_bwd(dfeat, codes, a.shape[2], a.shape[3])
+        # ---- blocks, last to first
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            b = self.blocks[bi]
+            xin, colx, h1, st1, bits1, a1, h2, st2, bits2 = saved[bi]
+            dh2 = ops.cs_bn_bwd(da, h2, st2, bits2, W, ld, b.bn2w, G, Gg, gld, b.bn2w, b.bn2b)
+            da1 = self._conv3_dgrad(dh2, cache, W, ld, G, b.conv2, b.cout, b.cout)
+            self._conv3_wgrad(dh2, a1, G, Gg, gld, b.conv2, b.cout, b.cout)
+            dh1 = ops.cs_bn_bwd(da1, h1, st1, bits1, W, ld, b.bn1w, G, Gg, gld, b.bn1w, b.bn1b)
+            if b.stride == 1:
+                dx = self._conv3_dgrad(dh1, cache, W, ld, G, b.conv1, b.cout, b.cin)
+                self._conv3_wgrad(dh1, xin, G, Gg, gld, b.conv1, b.cout, b.cin)
+                da = ops.fa_ew(dx, da, 0)
+            else:
+                nn_, _, Hi, Wi = xin.shape
+                Kc = 9 * b.cin
+                dcol = torch.empty((colx.shape[0], G, Kc), device=x.device, dtype=torch.bfloat16)
+                dcg = dcol.transpose(0, 1)
+                torch.bmm(_gview(dh1, G), self._img(cache, W, ld, G, b.conv1, b.cout, b.cin, 3, 2), out=dcg)
+                dctr = dcg[:, :, 4 * b.cin:5 * b.cin]
+                torch.baddbmm(dctr, _gview(da, G), self._img(cache, W, ld, G, b.sc, b.cout, b.cin, 1, 2),
+                              out=dctr)
+                cg = colx.transpose(0, 1)
+                part = torch.bmm(_gview(dh1, G).transpose(1, 2), cg, out_dtype=torch.float32)
+                ops.wgrad_rsc_add(Gg[:, b.conv1:b.conv1 + b.cout * b.cin * 9].view(G, b.cout, b.cin * 9),
+                                  part, 1, b.cin, 9, False)
+                psc = torch.bmm(_gview(da, G).transpose(1, 2), cg[:, :, 4 * b.cin:5 * b.cin],
+                                out_dtype=torch.float32)
+                ops.wgrad_rsc_add(Gg[:, b.sc:b.sc + b.cout * b.cin].view(G, b.cout, b.cin), psc, 1,
+                                  b.cin, 1, False)
+                da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
+        # ---- stem weight gradient (ReLU backward through its output)
+        dy0 = ops.relu_mask(da, a0)
+        part = torch.bmm(_gview(dy0, G).transpose(1, 2), col0.transpose(0, 1), out_dtype=torch.float32)
+        ops.wgrad_rsc_add(Gg[:, self.prep:self.prep + K0 * C0 * 9].view(G, K0, C0 * 9), part, 1, C0, 9, False)
+        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)

@@ -84,6 +84,11 @@ def build_parser(default_lr: Optional[float] = None) -> argparse.ArgumentParser:
                         "over per-client weight copies, parallel/fed_model.py) instead of one "
                         "client after another; auto: when the clients have equal sizes and no "
                         "worker-side DP is on")
+    p.add_argument("--fedavg_engine", choices=["auto", "native", "vmap"], default="auto",
+                   help="batched FedAvg program: native = the explicit G-client ResNet-18 of "
+                        "parallel/fedavg_native.py (grouped MFMA convs, channel-stacked batch "
+                        "norm, per-row SGD kernels); vmap = torch.func.vmap over the model's "
+                        "stock ops; auto: native where supported (GPU, ResNet18 + BatchNorm)")
     p.add_argument("--error_type", choices=ERROR_TYPES, default="none")
     p.add_argument("--lr_scale", type=float, default=default_lr)
     p.add_argument("--pivot_epoch", type=float, default=5)

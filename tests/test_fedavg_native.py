@@ -1,0 +1,293 @@
+"""Native batched FedAvg (parallel/fedavg_native.py): every kernel of the
+explicit G-client ResNet-18 program against a plain PyTorch fp32 reference of
+the same op, and the whole local-SGD round against the vmap composition and
+the fp32 sequential path (fed_worker.py:61-113 semantics)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from commefficient_amd import _ext
+from commefficient_amd.models.fixup import ResNet18
+from commefficient_amd.parallel.fedavg_native import ResNet18FedAvg
+from commefficient_amd.utils.args import parse_args
+
+
+def _ops():
+    return _ext.ops()
+
+
+def _args(extra=()):
+    return parse_args(argv=["--dataset_name", "CIFAR100", "--mode", "fedavg", "--batchnorm",
+                            "--local_batch_size", "-1", "--local_momentum", "0", "--error_type", "none"]
+                      + list(extra), probe_port=False)
+
+
+def test_supported_models():
+    ok, _ = ResNet18FedAvg.supported(ResNet18(num_classes=100), _args())
+    assert ok
+    from commefficient_amd import models
+    assert not ResNet18FedAvg.supported(models.ResNet9(), _args())[0]
+    assert not ResNet18FedAvg.supported(ResNet18(num_classes=10), _args(["--dtype", "fp32"]))[0]
+
+
+def test_engine_layout_matches_parameter_order():
+    """Offsets of every parameter the program reads come from the flat layout
+    (FedModel's named_parameters order)."""
+    m = ResNet18(num_classes=100)
+    names = [nm for nm, p in m.named_parameters()]
+
+    class _Flat:
+        offsets, numels = [], []
+    o = 0
+    for p in m.parameters():
+        _Flat.offsets.append(o)
+        _Flat.numels.append(p.numel())
+        o += p.numel()
+    eng = ResNet18FedAvg(m, _Flat, names)
+    assert eng.d == o
+    assert [b.stride for b in eng.blocks] == [1, 1, 2, 1, 2, 1, 2, 1]
+    assert sum(b.sc is not None for b in eng.blocks) == 3
+    assert eng.feat == 512 and eng.ncls == 100
+
+
+# ----------------------------------------------------------------- kernels
+def _cs(t, G):
+    """[G, n, C, H, W] fp32 -> channel-stacked bf16 [n, G*C, H, W] channels_last"""
+    Gq, n, C, H, W = t.shape
+    return (t.permute(1, 0, 2, 3, 4).reshape(n, G * C, H, W).to(torch.bfloat16)
+            .contiguous(memory_format=torch.channels_last))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [3, 1])
+def test_weight_images(R):
+    torch.manual_seed(0)
+    G, K, C, off, ld = 3, 64, 16, 40, 64 * 16 * R * R + 104
+    W = torch.randn(G, ld, device="cuda")
+    w = W[:, off:off + K * C * R * R].view(G, K, C, R, R)
+    Kc = (R * R * C + 7) // 8 * 8
+    ops = _ops()
+    if R == 3:
+        i0 = ops.fa_weight_image(W, ld, G, off, K, C, R, Kc, 0)
+        torch.testing.assert_close(i0.float(), w.permute(0, 1, 3, 4, 2).reshape(G * K, R, R, C).bfloat16().float())
+        i1 = ops.fa_weight_image(W, ld, G, off, K, C, R, Kc, 1)
+        ref = w.flip(3, 4).permute(0, 2, 3, 4, 1).reshape(G * C, R, R, K)
+        torch.testing.assert_close(i1.float(), ref.bfloat16().float())
+    i2 = ops.fa_weight_image(W, ld, G, off, K, C, R, Kc, 2)
+    ref = torch.zeros(G, K, Kc, device="cuda")
+    ref[:, :, :R * R * C] = w.permute(0, 1, 3, 4, 2).reshape(G, K, R * R * C)
+    torch.testing.assert_close(i2.float(), ref.bfloat16().float())
+    # ld 0: one broadcast row
+    b = ops.fa_weight_image(W[0].contiguous(), 0, G, off, K, C, R, Kc, 2)
+    torch.testing.assert_close(b.float(), ref[:1].expand(G, -1, -1).bfloat16().float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,C", [(1, 64), (2, 64), (2, 16)])
+def test_im2col_col2im_grouped_match_per_client(stride, C):
+    torch.manual_seed(0)
+    G, n, H = 3, 2, 8
+    X = torch.randn(G, n, C, H, H, device="cuda")
+    x = _cs(X, G)
+    ops = _ops()
+    col = ops.im2col_grouped(x, G, 3, 3, stride, 1, 9 * C, False)
+    gcol = torch.randn_like(col, dtype=torch.float32).bfloat16()
+    gx = ops.col2im_grouped(gcol, G, n, H, H, C, 3, 3, stride, 1)
+    for g in range(G):
+        xg = X[g].bfloat16().contiguous(memory_format=torch.channels_last)
+        torch.testing.assert_close(col[:, g], ops.im2col(xg, 3, 3, stride, 1, 9 * C), rtol=0, atol=0)
+        ref = ops.col2im(gcol[:, g].contiguous(), n, H, H, C, 3, 3, stride, 1)
+        torch.testing.assert_close(gx[:, g * C:(g + 1) * C].float(), ref.float(), rtol=0, atol=0)
+    # client-major input (the data loader's [G*n, C, H, W] batch)
+    xc = X.reshape(G * n, C, H, H).bfloat16().contiguous(memory_format=torch.channels_last)
+    colc = ops.im2col_grouped(xc, G, 3, 3, stride, 1, 9 * C, True)
+    torch.testing.assert_close(colc, col, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_im2col_grouped_three_channel_stem():
+    torch.manual_seed(0)
+    G, n = 4, 3
+    X = torch.randn(G * n, 3, 32, 32, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    col = _ops().im2col_grouped(X, G, 3, 3, 1, 1, 32, True)
+    for g in range(G):
+        ref = _ops().im2col(X[g * n:(g + 1) * n], 3, 3, 1, 1, 32)
+        torch.testing.assert_close(col[:, g], ref, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,C,H", [(4, 64, 8), (100, 64, 4), (3, 256, 4)])
+def test_cs_bn_forward_backward(G, C, H):
+    torch.manual_seed(0)
+    n = 5
+    X = torch.randn(G, n, C, H, H, device="cuda") * 2 + 0.5
+    x = _cs(X, G)
+    ld, woff, boff = 2 * C + 32, 8, C + 16
+    P = torch.randn(G, ld, device="cuda")
+    rm = torch.randn(G * C, device="cuda")
+    rv = torch.rand(G * C, device="cuda") + 0.5
+    rm0, rv0 = rm.clone(), rv.clone()
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    ops = _ops()
+    y, stat, bits = ops.cs_bn_fwd(x, P, ld, woff, boff, G, 1e-5, 0.1, rm, rv, nbt)
+    xf = x.float().view(n, G, C, H, H).transpose(0, 1)  # [G, n, C, H, W]
+    w = P[:, woff:woff + C].view(G, 1, C, 1, 1)
+    b = P[:, boff:boff + C].view(G, 1, C, 1, 1)
+    xr = xf.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    mean = xr.mean(dim=(1, 3, 4), keepdim=True)
+    var = xr.var(dim=(1, 3, 4), unbiased=False, keepdim=True)
+    yr = F.relu((xr - mean) * torch.rsqrt(var + 1e-5) * wr + br)
+    torch.testing.assert_close(y.float().view(n, G, C, H, H).transpose(0, 1), yr.detach(), rtol=2e-2, atol=2e-2)
+    M = n * H * H
+    torch.testing.assert_close(rm.view(G, C), 0.9 * rm0.view(G, C) + 0.1 * mean.view(G, C), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rv.view(G, C), 0.9 * rv0.view(G, C) + 0.1 * var.view(G, C) * M / (M - 1),
+                               rtol=1e-3, atol=1e-3)
+    assert int(nbt) == 1
+    DY = torch.randn(G, n, C, H, H, device="cuda")
+    dy = _cs(DY, G)
+    yr.backward(dy.float().view(n, G, C, H, H).transpose(0, 1))
+    Gg = torch.zeros(G, ld, device="cuda")
+    dx = ops.cs_bn_bwd(dy, x, stat, bits, P, ld, woff, G, Gg, ld, woff, boff)
+    scale = xr.grad.abs().max()
+    torch.testing.assert_close(dx.float().view(n, G, C, H, H).transpose(0, 1) / scale, xr.grad / scale,
+                               rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(Gg[:, woff:woff + C], wr.grad.view(G, C), rtol=2e-2, atol=2e-2 * M ** 0.5)
+    torch.testing.assert_close(Gg[:, boff:boff + C], br.grad.view(G, C), rtol=2e-2, atol=2e-2 * M ** 0.5)
+
+
+@pytest.mark.gpu
+def test_head_pool_forward_backward():
+    torch.manual_seed(0)
+    G, n, C = 5, 3, 256
+    X = torch.randn(G, n, C, 4, 4, device="cuda")
+    x = _cs(X, G)
+    feat, codes = _ops().fa_head_fwd(x, G)
+    xf = x.float().view(n, G, C, 4, 4).transpose(0, 1).requires_grad_(True)
+    # (adaptive max-pool routes a tied maximum's gradient to one position, as the kernel does)
+    mx = F.adaptive_max_pool2d(xf.reshape(G * n, C, 4, 4), 1).view(G, n, C)
+    ref = torch.cat([xf.mean(dim=(3, 4)), mx], dim=2)  # [G, n, 2C]
+    torch.testing.assert_close(feat, ref.detach(), rtol=1e-5, atol=1e-5)
+    df = torch.randn_like(feat)
+    ref.backward(df)
+    dx = _ops().fa_head_bwd(df, codes, 4, 4)
+    torch.testing.assert_close(dx.float().view(n, G, C, 4, 4).transpose(0, 1), xf.grad, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("clip", [0.0, 0.5])
+def test_row_sgd_and_upload(clip):
+    torch.manual_seed(0)
+    G, d = 5, 1003
+    ld = 1024
+    W = torch.randn(G, ld, device="cuda")
+    Gr = torch.zeros(G, ld, device="cuda")
+    Gr[:, :d] = torch.randn(G, d, device="cuda")
+    w0 = torch.randn(d, device="cuda")
+    w0p = torch.zeros(ld, device="cuda")
+    w0p[:d] = w0
+    ops = _ops()
+    # first step: the broadcast server row
+    out = torch.zeros(G, ld, device="cuda")
+    ops.fa_row_sgd(out, ld, w0p, 0, Gr, ld, G, d, clip, 0.1, 0.01)
+    g = Gr[:, :d]
+    nrm = g.norm(dim=1, keepdim=True)
+    sc = torch.where(nrm > clip, clip / nrm, torch.ones_like(nrm)) if clip > 0 else torch.ones_like(nrm)
+    ref = w0 - 0.1 * (sc * g + 0.01 * w0)
+    torch.testing.assert_close(out[:, :d], ref, rtol=1e-5, atol=1e-6)
+    # in place
+    W2 = W.clone()
+    ops.fa_row_sgd(W2, ld, W2, ld, Gr, ld, G, d, clip, 0.1, 0.01)
+    torch.testing.assert_close(W2[:, :d], W[:, :d] - 0.1 * (sc * g + 0.01 * W[:, :d]), rtol=1e-5, atol=1e-6)
+    up = torch.ones(d, device="cuda")
+    ops.fa_upload(up, w0, W, ld, G, 5.0)
+    torch.testing.assert_close(up, 1 + 5 * (w0 - W[:, :d]).sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_conv3x3_wgrad_rows_matches_grouped_conv():
+    torch.manual_seed(0)
+    G, n, C, K, H = 3, 5, 128, 128, 16
+    x = _cs(torch.randn(G, n, C, H, H, device="cuda"), G)
+    dy = _cs(torch.randn(G, n, K, H, H, device="cuda"), G)
+    ld, off = K * C * 9 + 64, 32
+    dst = torch.zeros(G, ld, device="cuda")
+    assert _ops().conv3x3_wgrad_rows(dy, x, G, dst, ld, off)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (G * K, C, 3, 3), dy.float(), padding=1, groups=G)
+    got = dst[:, off:off + K * C * 9].reshape(G * K, C, 3, 3)
+    scale = ref.abs().max()
+    torch.testing.assert_close(got / scale, ref / scale, rtol=1e-2, atol=1e-2)
+    assert dst[:, :off].abs().max() == 0 and dst[:, off + K * C * 9:].abs().max() == 0
+
+
+@pytest.mark.gpu
+def test_ew_add_relu():
+    a = torch.randn(2, 64, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    b = torch.randn_like(a)
+    torch.testing.assert_close(_ops().fa_ew(a, b, 0).float(), (a.float() + b.float()).bfloat16().float())
+    torch.testing.assert_close(_ops().fa_ew(a, None, 1).float(), a.float().clamp_min(0))
+
+
+# ---------------------------------------------------------------- engine
+def _round(base, engine, dtype, G, n, extra, lr=0.05):
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.train.losses import cv_loss
+    dist.init("cuda")
+    args = parse_args(argv=["--dataset_name", "CIFAR100", "--mode", "fedavg", "--error_type", "none",
+                            "--local_momentum", "0", "--virtual_momentum", "0", "--num_workers", str(G),
+                            "--num_clients", str(G), "--local_batch_size", "-1", "--device", "cuda",
+                            "--dtype", dtype, "--batchnorm", "--fedavg_engine", engine] + extra,
+                      probe_port=False)
+    model = copy.deepcopy(base).cuda()
+    if dtype == "bf16":
+        model = model.to(memory_format=torch.channels_last)
+    fed = FedModel(model, cv_loss, args, num_clients=G)
+    fed.fedavg_lr = lr
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(G * n, 3, 32, 32, generator=g).cuda()
+    if dtype == "bf16":
+        x = x.bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 100, (G * n,), generator=g).cuda()
+    out = fed((torch.arange(G).repeat_interleave(n), x, y))
+    torch.cuda.synchronize()
+    bufs = {k: b.detach().float().clone() for k, b in model.named_buffers()}
+    return fed._payload[:fed.d].clone(), out[0].clone(), bufs, fed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [
+    ["--fedavg_batch_size", "-1", "--num_fedavg_epochs", "2"],
+    ["--fedavg_batch_size", "-1", "--num_fedavg_epochs", "3", "--weight_decay", "5e-4",
+     "--max_grad_norm", "2.0", "--fedavg_lr_decay", "0.9"],
+    ["--fedavg_batch_size", "2", "--num_fedavg_epochs", "1"],
+])
+def test_native_round_matches_vmap_and_fp32(extra):
+    """Upload and per-client losses of the native program vs the vmap
+    composition (bf16) and the fp32 sequential path: the native round must be
+    as close to fp32 as the bf16 vmap round is."""
+    torch.manual_seed(0)
+    base = ResNet18(num_classes=100)
+    G, n = 6, 5
+    up_n, l_n, b_n, fed = _round(base, "native", "bf16", G, n, extra)
+    assert fed._fa_native, "native engine did not run"
+    up_v, l_v, b_v, _ = _round(base, "vmap", "bf16", G, n, extra)
+    up_f, l_f, b_f, _ = _round(base, "vmap", "fp32", G, n, extra + ["--fedavg_batched", "off"])
+    noise = ((up_v - up_f).norm() / up_f.norm()).item()
+    rel = ((up_n - up_f).norm() / up_f.norm()).item()
+    assert rel < 2 * noise + 2e-2, (rel, noise)
+    lnoise = (l_v - l_f).abs().max().item()
+    assert (l_n - l_f).abs().max().item() <= 2 * lnoise + 3e-2 * l_f.abs().max().item(), (l_n, l_v, l_f)
+    # running statistics: the clients' mean (the batched semantics -- the
+    # sequential path accumulates them client after client on one model), so
+    # against the fp32 vmap round, within twice the bf16 vmap round's distance
+    _, _, b_vf, _ = _round(base, "vmap", "fp32", G, n, extra)
+    for k in b_v:
+        if "running" in k:
+            bn_noise = (b_v[k] - b_vf[k]).abs().max().item()
+            err = (b_n[k] - b_vf[k]).abs().max().item()
+            assert err <= 2 * bn_noise + 1e-2 * b_vf[k].abs().max().item() + 1e-3, (k, err, bn_noise)
+        elif "num_batches" in k:
+            assert b_n[k] == b_v[k], k
