@@ -487,6 +487,14 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
     }
     win_off[i] = off;
   }
+  // grouped weights not stored as one [G kg][3][3][C] image (a.w_gs != 0):
+  // this tile's group (n0 / kg, block-uniform since kg % BN == 0) reads its
+  // own rows w_gs elements apart (> 0), or every group the same rows (< 0)
+  const uint16_t* wsrc = a.w;
+  if (a.kg > 0 && a.w_gs != 0) {
+    const int64_t g = n0 / a.kg;
+    wsrc += (a.w_gs > 0 ? g * a.w_gs : int64_t{0}) - g * a.kg * 9 * static_cast<int64_t>(C);
+  }
   int b_off[BLD];  // element offsets into a.w (< K * 9 * C)
 #pragma unroll
   for (int j = 0; j < BLD; ++j) {
@@ -508,7 +516,7 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
     unsigned char* base = smem + kHaloWinBytes + (step & 1) * (BN * 128) + wid * 1024;
     const int boff = (step % 9) * C + (step / 9) * 64;
 #pragma unroll
-    for (int j = 0; j < BLD; ++j) glds16(a.w + (b_off[j] + boff), base + j * NT * 16);
+    for (int j = 0; j < BLD; ++j) glds16(wsrc + (b_off[j] + boff), base + j * NT * 16);
   };
 
   // this lane's output pixels (rows of the A fragments) -> padded window rows
@@ -1234,7 +1242,8 @@ template <int PARTS>
 __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const float* __restrict__ slab,
                                                                        float* __restrict__ dw, int K, int C,
                                                                        int splits, float beta,
-                                                                       int64_t gstride, int kg, int64_t ld) {
+                                                                       int64_t gstride, int kg, int64_t ld,
+                                                                       int rsc) {
   __shared__ float t[PARTS][64 * 9];
   const int ncb = C >> 6;
   const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
@@ -1257,26 +1266,30 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
   __syncthreads();
   // kg > 0: output channel k is row k % kg of group k / kg's weight, groups
   // ld floats apart (the per-client gradient rows of parallel/fedavg_native.py)
-  float* o = kg > 0 ? dw + static_cast<size_t>(k / kg) * ld + (static_cast<size_t>(k % kg) * C + c0) * 9
-                    : dw + (static_cast<size_t>(k) * C + c0) * 9;
+  // rsc: the row in (r, s, c) order ([kg][3][3][C], the engine's layout)
+  float* o = kg > 0 ? dw + static_cast<size_t>(k / kg) * ld + static_cast<size_t>(k % kg) * C * 9
+                    : dw + static_cast<size_t>(k) * C * 9;
   for (int e = threadIdx.x; e < 576; e += 64 * PARTS) {
-    float v = t[0][e];
+    const int src = rsc ? (e & 63) * 9 + (e >> 6) : e;
+    float v = t[0][src];
 #pragma unroll
-    for (int q = 1; q < PARTS; ++q) v += t[q][e];  // fixed order: deterministic
-    o[e] = beta != 0.f ? beta * o[e] + v : v;
+    for (int q = 1; q < PARTS; ++q) v += t[q][src];  // fixed order: deterministic
+    float* oe = rsc ? o + (e >> 6) * C + c0 + (e & 63) : o + c0 * 9 + e;
+    *oe = beta != 0.f ? beta * *oe + v : v;
   }
 }
 
 
 void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
-                         int64_t gstride, int groups, hipStream_t stream, int kg = 0, int64_t ld = 0) {
+                         int64_t gstride, int groups, hipStream_t stream, int kg = 0, int64_t ld = 0,
+                         bool rsc = false) {
   const dim3 grid(K * (C / 64), groups);
   if (splits >= 32)
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld);
+                       beta, gstride, kg, ld, rsc ? 1 : 0);
   else
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld);
+                       beta, gstride, kg, ld, rsc ? 1 : 0);
 }
 
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16
@@ -1611,11 +1624,11 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 
 // channel-stacked grouped wgrad written straight into per-group rows: output
 // channel k of group k / kg at dst + (k / kg) * ld + (k % kg) * 9 C
-void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, hipStream_t stream) {
+void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream) {
   const int steps = (a.P + BK - 1) / BK;
   a.group_px = 0;
   launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
-  launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, 0.f, int64_t{0}, 1, stream, kg, ld);
+  launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, 0.f, int64_t{0}, 1, stream, kg, ld, rsc);
 }
 
 // the wgrad GEMM kernels (slabs only) with a given split length

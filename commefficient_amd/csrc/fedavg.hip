@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) row_sgd_kernel(float* __restrict__ W, int
                                                       const float* __restrict__ Src, int64_t sld,
                                                       const float* __restrict__ Gr, int64_t gld, int64_t d4,
                                                       const float* __restrict__ part, float clip, float lr,
-                                                      float wd) {
+                                                      float wd, bf16raw* __restrict__ Wb) {
   const int g = blockIdx.y;
   float scale = 1.f;
   if (clip > 0.f) {
@@ -120,23 +120,60 @@ __global__ void __launch_bounds__(256) row_sgd_kernel(float* __restrict__ W, int
   float4* w = reinterpret_cast<float4*>(W + g * ld);
   const float4* src = reinterpret_cast<const float4*>(Src + g * sld);
   const float4* gr = reinterpret_cast<const float4*>(Gr + g * gld);
+  uint2* wb = Wb != nullptr ? reinterpret_cast<uint2*>(Wb + g * ld) : nullptr;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < d4; i += static_cast<int64_t>(gridDim.x) * 256) {
     const float4 s = src[i], q = gr[i];
-    w[i] = make_float4(c * s.x + a * q.x, c * s.y + a * q.y, c * s.z + a * q.z, c * s.w + a * q.w);
+    const float4 o = make_float4(c * s.x + a * q.x, c * s.y + a * q.y, c * s.z + a * q.z, c * s.w + a * q.w);
+    w[i] = o;
+    // the bf16 mirror the next step's convolutions read (same row layout)
+    if (wb != nullptr)
+      wb[i] = make_uint2(static_cast<uint32_t>(f2bf(o.x)) | (static_cast<uint32_t>(f2bf(o.y)) << 16),
+                         static_cast<uint32_t>(f2bf(o.z)) | (static_cast<uint32_t>(f2bf(o.w)) << 16));
   }
 }
 
 // out[j] += n * sum_g (w0[j] - W[g][j]), clients in order (exact zeros where no
 // client moved a coordinate)
+// (perm: the rows hold the engine's layout, element j of a row is coordinate
+// perm[j] of the flat vector; a bijection, so the scattered adds never collide)
 __global__ void __launch_bounds__(256) upload_kernel(float* __restrict__ out, const float* __restrict__ w0,
                                                      const float* __restrict__ W, int64_t ld, int G, int64_t d,
-                                                     float n) {
+                                                     float n, const int32_t* __restrict__ perm) {
   for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < d; j += static_cast<int64_t>(gridDim.x) * 256) {
     const float w = w0[j];
     float acc = 0.f;
     for (int g = 0; g < G; ++g) acc += w - W[g * ld + j];
-    out[j] += n * acc;
+    out[perm != nullptr ? perm[j] : j] += n * acc;
   }
+}
+
+// dst[j] = src[perm[j]] (the server weights in the engine's layout) and its bf16 copy
+__global__ void __launch_bounds__(256) gather_rows_kernel(float* __restrict__ dst, bf16raw* __restrict__ dstb,
+                                                          const float* __restrict__ src,
+                                                          const int32_t* __restrict__ perm, int64_t d) {
+  for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < d; j += static_cast<int64_t>(gridDim.x) * 256) {
+    const float v = src[perm[j]];
+    dst[j] = v;
+    dstb[j] = f2bf(v);
+  }
+}
+
+// flipped, transposed dgrad image of 3x3 weights held as bf16 (r, s, c) rows:
+// src[g*ld + (k*9 + t)*C + c] -> dst[((g*C + c)*9 + 8 - t)*K + k].  Per client
+// a [K][9C] -> [9C][K] transpose in 64 x 64 tiles through LDS (reads along c,
+// writes along k: both coalesced).  grid (9C/64, K/64, G)
+__global__ void __launch_bounds__(256) dgrad_image_kernel(const bf16raw* __restrict__ src, int64_t ld, int K,
+                                                          int C, bf16raw* __restrict__ dst) {
+  __shared__ bf16raw t[64][66];
+  const int g = blockIdx.z, j0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const bf16raw* s = src + g * ld;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) t[r][tx] = s[static_cast<int64_t>(k0 + r) * 9 * C + j0 + tx];
+  __syncthreads();
+  const int tap = j0 / C, c0 = j0 - tap * C;  // 64 | C: one tap per tile
+  bf16raw* d = dst + static_cast<int64_t>(g) * C * 9 * K;
+  for (int r = ty; r < 64; r += 4)  // tile column r = channel c0 + r
+    d[(static_cast<int64_t>(c0 + r) * 9 + 8 - tap) * K + k0 + tx] = t[tx][r];
 }
 
 // ------------------------------------------------------------------ head
@@ -223,7 +260,7 @@ void launch_weight_image(const float* W, int64_t ld, int G, int K, int C, int RS
 }
 
 void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const float* Gr, int64_t gld, int G,
-                    int64_t d4, float clip, float lr, float wd, float* part, hipStream_t stream) {
+                    int64_t d4, float clip, float lr, float wd, float* part, uint16_t* Wb, hipStream_t stream) {
   if (G == 0 || d4 == 0) return;
   if (clip > 0.f)
     COMMEFF_LAUNCH(row_sumsq_kernel, dim3(kRowParts, G), dim3(256), 0, stream, Gr, gld, d4, part);
@@ -231,15 +268,26 @@ void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const f
   const int cap = (8192 + G - 1) / G;
   if (bx > cap) bx = cap;
   COMMEFF_LAUNCH(row_sgd_kernel, dim3(bx < 1 ? 1 : bx, G), dim3(256), 0, stream, W, ld, src, sld, Gr, gld, d4,
-                 part, clip, lr, wd);
+                 part, clip, lr, wd, Wb);
 }
 
 int row_sgd_parts() { return kRowParts; }
 
 void launch_fedavg_upload(float* out, const float* w0, const float* W, int64_t ld, int G, int64_t d, float n,
-                          hipStream_t stream) {
+                          const int32_t* perm, hipStream_t stream) {
   if (d == 0) return;
-  COMMEFF_LAUNCH(upload_kernel, dim3(grid_for(d)), dim3(256), 0, stream, out, w0, W, ld, G, d, n);
+  COMMEFF_LAUNCH(upload_kernel, dim3(grid_for(d)), dim3(256), 0, stream, out, w0, W, ld, G, d, n, perm);
+}
+
+void launch_gather_rows(float* dst, uint16_t* dstb, const float* src, const int32_t* perm, int64_t d,
+                        hipStream_t stream) {
+  if (d == 0) return;
+  COMMEFF_LAUNCH(gather_rows_kernel, dim3(grid_for(d)), dim3(256), 0, stream, dst, dstb, src, perm, d);
+}
+
+void launch_dgrad_image(const uint16_t* src, int64_t ld, int G, int K, int C, uint16_t* dst, hipStream_t stream) {
+  if (G == 0) return;
+  COMMEFF_LAUNCH(dgrad_image_kernel, dim3(9 * C / 64, K / 64, G), dim3(256), 0, stream, src, ld, K, C, dst);
 }
 
 void launch_avgmax_head_fwd(const uint16_t* x, int n, int HW, int G, int C, float* feat, uint8_t* codes,

@@ -16,10 +16,13 @@ namespace commeff {
 void launch_weight_image(const float* W, int64_t ld, int G, int K, int C, int RS, int Kc, int kind,
                          uint16_t* dst, hipStream_t stream);
 void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const float* Gr, int64_t gld, int G,
-                    int64_t d4, float clip, float lr, float wd, float* part, hipStream_t stream);
+                    int64_t d4, float clip, float lr, float wd, float* part, uint16_t* Wb, hipStream_t stream);
 int row_sgd_parts();
 void launch_fedavg_upload(float* out, const float* w0, const float* W, int64_t ld, int G, int64_t d, float n,
-                          hipStream_t stream);
+                          const int32_t* perm, hipStream_t stream);
+void launch_gather_rows(float* dst, uint16_t* dstb, const float* src, const int32_t* perm, int64_t d,
+                        hipStream_t stream);
+void launch_dgrad_image(const uint16_t* src, int64_t ld, int G, int K, int C, uint16_t* dst, hipStream_t stream);
 void launch_avgmax_head_fwd(const uint16_t* x, int n, int HW, int G, int C, float* feat, uint8_t* codes,
                             hipStream_t stream);
 void launch_avgmax_head_bwd(const float* df, const uint8_t* codes, int n, int HW, int G, int C, uint16_t* dx,
@@ -76,7 +79,7 @@ at::Tensor fa_weight_image(const at::Tensor& W, int64_t ld, int64_t G, int64_t o
 // W[g] = src[g] - lr (scale_g G[g] + wd src[g]) for g < rows (src ld 0: one
 // broadcast row); scale_g = min(1, clip / |G[g]|) when clip > 0
 void fa_row_sgd(at::Tensor W, int64_t ld, const at::Tensor& src, int64_t sld, const at::Tensor& Gr, int64_t gld,
-                int64_t rows, int64_t d, double clip, double lr, double wd) {
+                int64_t rows, int64_t d, double clip, double lr, double wd, const c10::optional<at::Tensor>& Wb) {
   const int64_t d4 = (d + 3) / 4;
   TORCH_CHECK(ld % 4 == 0 && sld % 4 == 0 && gld % 4 == 0 && d4 * 4 <= std::min(ld, gld),
               "fa_row_sgd: row strides must be multiples of 4 holding d");
@@ -87,24 +90,104 @@ void fa_row_sgd(at::Tensor W, int64_t ld, const at::Tensor& src, int64_t sld, co
               "fa_row_sgd: src rows");
   for (const at::Tensor* t : {static_cast<const at::Tensor*>(&W), &src, &Gr})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "fa_row_sgd: 16-byte aligned rows");
+  uint16_t* wb = nullptr;
+  if (Wb.has_value() && Wb->defined()) {  // bf16 mirror rows of the same layout
+    TORCH_CHECK(Wb->is_cuda() && Wb->scalar_type() == at::kBFloat16 && Wb->is_contiguous() &&
+                    Wb->numel() >= rows * ld && reinterpret_cast<uintptr_t>(Wb->data_ptr()) % 8 == 0,
+                "fa_row_sgd: Wb must be contiguous bf16 [rows, ld]");
+    wb = reinterpret_cast<uint16_t*>(Wb->data_ptr());
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
   at::Tensor part;
   if (clip > 0) part = at::empty({rows * row_sgd_parts()}, W.options());
   launch_row_sgd(W.data_ptr<float>(), ld, src.data_ptr<float>(), sld, Gr.data_ptr<float>(), gld,
                  static_cast<int>(rows), d4, static_cast<float>(clip), static_cast<float>(lr),
-                 static_cast<float>(wd), clip > 0 ? part.data_ptr<float>() : nullptr, stream_now());
+                 static_cast<float>(wd), clip > 0 ? part.data_ptr<float>() : nullptr, wb, stream_now());
 }
 
 // out[j] += n sum_g (w0[j] - W[g*ld + j]), j < d
-void fa_upload(at::Tensor out, const at::Tensor& w0, const at::Tensor& W, int64_t ld, int64_t rows, double n) {
+// (perm: rows / w0 in the engine's layout, element j -> coordinate perm[j] of out)
+void fa_upload(at::Tensor out, const at::Tensor& w0, const at::Tensor& W, int64_t ld, int64_t rows, double n,
+               const c10::optional<at::Tensor>& perm) {
   const int64_t d = out.numel();
-  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && w0.numel() == d &&
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && w0.numel() >= d &&
                   w0.scalar_type() == at::kFloat && w0.is_contiguous(),
               "fa_upload: out / w0 fp32 [d]");
   check_rows(W, ld, rows, 0, d, "fa_upload: W");
+  const int32_t* pp = nullptr;
+  if (perm.has_value() && perm->defined()) {
+    TORCH_CHECK(perm->is_cuda() && perm->scalar_type() == at::kInt && perm->is_contiguous() && perm->numel() == d,
+                "fa_upload: perm int32 [d]");
+    pp = perm->data_ptr<int32_t>();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
   launch_fedavg_upload(out.data_ptr<float>(), w0.data_ptr<float>(), W.data_ptr<float>(), ld,
-                       static_cast<int>(rows), d, static_cast<float>(n), stream_now());
+                       static_cast<int>(rows), d, static_cast<float>(n), pp, stream_now());
+}
+
+// dst[j] = src[perm[j]], dstb = bf16(dst): the server weights in the engine's layout
+void fa_gather_rows(at::Tensor dst, at::Tensor dstb, const at::Tensor& src, const at::Tensor& perm) {
+  const int64_t d = perm.numel();
+  TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.is_contiguous(), "fa_gather_rows: perm int32");
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous() && dst.numel() >= d &&
+                  dstb.scalar_type() == at::kBFloat16 && dstb.is_contiguous() && dstb.numel() >= d &&
+                  src.scalar_type() == at::kFloat && src.is_contiguous() && src.numel() == d,
+              "fa_gather_rows: dst fp32, dstb bf16 >= d, src fp32 [d]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
+  launch_gather_rows(dst.data_ptr<float>(), bfw(dstb), src.data_ptr<float>(), perm.data_ptr<int32_t>(), d,
+                     stream_now());
+}
+
+// [G*C, 3, 3, K] flipped / transposed dgrad image of 3x3 weights held as bf16
+// (r, s, c)-ordered rows Wb[g*ld + off + (k*9 + t)*C + c] (ld 0: one image)
+at::Tensor fa_dgrad_image(const at::Tensor& Wb, int64_t ld, int64_t G, int64_t off, int64_t K, int64_t C) {
+  TORCH_CHECK(Wb.is_cuda() && Wb.scalar_type() == at::kBFloat16 && Wb.is_contiguous(), "fa_dgrad_image: Wb bf16");
+  TORCH_CHECK(K % 64 == 0 && C % 64 == 0 && G >= 1 && off >= 0 && (ld == 0 || off + K * 9 * C <= ld) &&
+                  (ld == 0 ? 0 : G - 1) * ld + off + K * 9 * C <= Wb.numel(),
+              "fa_dgrad_image: 64 | K, C; rows in range");
+  const int64_t Gi = ld == 0 ? 1 : G;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(Wb.device());
+  auto dst = at::empty({Gi * C, 3, 3, K}, Wb.options());
+  launch_dgrad_image(bf(Wb) + off, ld, static_cast<int>(Gi), static_cast<int>(K), static_cast<int>(C), bfw(dst),
+                     stream_now());
+  return dst;
+}
+
+// grouped stride-1 3x3 conv of channel-stacked x whose group-g weights are the
+// kg rows [kg][3][3][C] at w + off + g * ld (ld 0: every group the same rows)
+at::Tensor conv3x3_fwd_rows(const at::Tensor& x, const at::Tensor& w, int64_t G, int64_t off, int64_t ld,
+                            int64_t kg) {
+  check_cl_bf16(x, "conv3x3_fwd_rows: x");
+  const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(G >= 1 && GC % G == 0 && kg >= 1, "conv3x3_fwd_rows: channels not a multiple of G");
+  const int64_t C = GC / G, K = G * kg;
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && off >= 0 && ld >= 0 &&
+                  (ld == 0 || off + kg * 9 * C <= ld) && (ld == 0 ? 0 : G - 1) * ld + off + kg * 9 * C <= w.numel(),
+              "conv3x3_fwd_rows: weight rows out of range");
+  TORCH_CHECK(N * H * W * std::max(GC, K) < (int64_t{1} << 31), "conv3x3_fwd_rows: size");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({N, K, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  ConvFwdArgs a;
+  a.x = bf(x);
+  a.w = bf(w) + off;
+  a.y = bfw(y);
+  a.mask = nullptr;
+  a.addend = nullptr;
+  a.y_pre = nullptr;
+  a.pool_idx = nullptr;
+  a.pool = 0;
+  a.relu = 0;
+  a.P = static_cast<int>(N * H * W);
+  a.H = static_cast<int>(H);
+  a.W = static_cast<int>(W);
+  a.C = static_cast<int>(C);
+  a.K = static_cast<int>(K);
+  a.x_stride = static_cast<int>(GC);
+  a.kg = static_cast<int>(kg);
+  a.w_gs = ld > 0 ? ld : -1;
+  if (a.P == 0) return y;
+  if (!launch_conv3x3_fwd_grouped(a, stream_now())) return at::empty({0}, x.options());
+  return y;
 }
 
 // x [n, G*C, h, w] channels_last -> (feat fp32 [G, n, 2C] = mean | max, codes uint8 [n, G*C])
@@ -294,7 +377,7 @@ at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor
 // gradient rows dst[g*ld + off + (k*C + c)*9 + t]; false (nothing written)
 // where the geometry has no grouped halo tiling
 bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at::Tensor dst, int64_t ld,
-                        int64_t off) {
+                        int64_t off, bool rsc) {
   check_cl_bf16(dy, "conv3x3_wgrad_rows: dy");
   check_cl_bf16(x, "conv3x3_wgrad_rows: x");
   const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
@@ -323,7 +406,7 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
   a.splits = splits;
   a.x_stride = static_cast<int>(GC);
   a.kg = static_cast<int>(kg);
-  launch_conv3x3_wgrad_rows(a, dst.data_ptr<float>() + off, static_cast<int>(kg), ld, stream_now());
+  launch_conv3x3_wgrad_rows(a, dst.data_ptr<float>() + off, static_cast<int>(kg), ld, rsc, stream_now());
   return true;
 }
 
@@ -332,8 +415,11 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_weight_image(Tensor W, int ld, int G, int off, int K, int C, int R, int Kc, int kind) -> Tensor");
   m.def("fa_row_sgd(Tensor(a!) W, int ld, Tensor src, int sld, Tensor G, int gld, int rows, int d, float clip, "
-        "float lr, float wd) -> ()");
-  m.def("fa_upload(Tensor(a!) out, Tensor w0, Tensor W, int ld, int rows, float n) -> ()");
+        "float lr, float wd, Tensor(b!)? Wb=None) -> ()");
+  m.def("fa_upload(Tensor(a!) out, Tensor w0, Tensor W, int ld, int rows, float n, Tensor? perm=None) -> ()");
+  m.def("fa_gather_rows(Tensor(a!) dst, Tensor(b!) dstb, Tensor src, Tensor perm) -> ()");
+  m.def("fa_dgrad_image(Tensor Wb, int ld, int G, int off, int K, int C) -> Tensor");
+  m.def("conv3x3_fwd_rows(Tensor x, Tensor w, int G, int off, int ld, int kg) -> Tensor");
   m.def("fa_head_fwd(Tensor x, int G) -> (Tensor, Tensor)");
   m.def("fa_head_bwd(Tensor df, Tensor codes, int H, int W) -> Tensor");
   m.def("fa_ew(Tensor a, Tensor? b, int mode) -> Tensor");
@@ -343,13 +429,16 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt) -> (Tensor, Tensor, Tensor)");
   m.def("cs_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor bits, Tensor prm, int ld, int woff, int G, "
         "Tensor(a!) grad, int gld, int gwoff, int gboff) -> Tensor");
-  m.def("conv3x3_wgrad_rows(Tensor dy, Tensor x, int G, Tensor(a!) dst, int ld, int off) -> bool");
+  m.def("conv3x3_wgrad_rows(Tensor dy, Tensor x, int G, Tensor(a!) dst, int ld, int off, bool rsc=False) -> bool");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("fa_weight_image", &fa_weight_image);
   m.impl("fa_row_sgd", &fa_row_sgd);
   m.impl("fa_upload", &fa_upload);
+  m.impl("fa_gather_rows", &fa_gather_rows);
+  m.impl("fa_dgrad_image", &fa_dgrad_image);
+  m.impl("conv3x3_fwd_rows", &conv3x3_fwd_rows);
   m.impl("fa_head_fwd", &fa_head_fwd);
   m.impl("fa_head_bwd", &fa_head_bwd);
   m.impl("fa_ew", &fa_ew);

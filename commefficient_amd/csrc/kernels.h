@@ -274,6 +274,10 @@ struct ConvFwdArgs {
   // weight rows g kg .. (g+1) kg of a [G kg][3][3][C] image.  0 = ungrouped.
   int x_stride = 0;
   int kg = 0;
+  // grouped weights: 0 = one contiguous [G kg][3][3][C] image; > 0 = group g's
+  // kg rows start at w + g * w_gs (per-client bf16 weight rows,
+  // parallel/fedavg_native.py); < 0 = every group reads the same kg rows
+  int64_t w_gs = 0;
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]
@@ -301,7 +305,8 @@ int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
 // grouped (a.kg, a.x_stride set) wgrad into per-group fp32 rows ld apart
-void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, hipStream_t stream);
+// (rsc: rows in (r, s, c) order instead of PyTorch's (c, r, s))
+void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream);
 // grouped convs on channel-stacked images (a.kg / a.x_stride set): false when
 // the geometry has no halo tiling (the caller falls back)
 bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream);

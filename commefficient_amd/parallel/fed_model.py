@@ -1253,7 +1253,7 @@ class FedModel:
                 else:
                     b.copy_(buf_acc[k])
         msum = torch.zeros(1 + len(met_rows[0]), W, device=self.device)
-        slots_t = torch.from_numpy(np.concatenate(slot_rows).astype(np.int64)).to(self.device)
+        slots_t = dist.h2d(np.concatenate(slot_rows).astype(np.int64), self.device)
         msum[0].index_copy_(0, slots_t, torch.cat(loss_rows))
         for i in range(len(met_rows[0])):
             msum[1 + i].index_copy_(0, slots_t, torch.cat([m[i] for m in met_rows]))
@@ -1318,7 +1318,8 @@ class FedModel:
                     if m.num_batches_tracked is not nbt0:
                         m.num_batches_tracked.copy_(nbt0)
         msum = torch.zeros(2, W, device=self.device)
-        slots_t = torch.from_numpy(np.concatenate(slot_rows).astype(np.int64)).to(self.device)
+        # (through the pinned ring: a pageable copy would wait for the whole round)
+        slots_t = dist.h2d(np.concatenate(slot_rows).astype(np.int64), self.device)
         msum[0].index_copy_(0, slots_t, torch.cat(loss_rows))
         msum[1].index_copy_(0, slots_t, torch.cat(acc_rows))
         return msum

@@ -115,46 +115,69 @@ class ResNet18FedAvg:
         self.c0 = model.prep[0].out_channels
         self.cin0 = model.prep[0].in_channels
 
-    # ----------------------------------------------------------- helpers
-    def _img(self, cache: Dict, W: torch.Tensor, ld: int, G: int, off: int, K: int, C: int, R: int,
-             kind: int) -> torch.Tensor:
-        key = (off, kind)
-        t = cache.get(key)
-        if t is None:
-            Kc = (R * R * C + 7) // 8 * 8
-            t = _ops().fa_weight_image(W, ld, G, off, K, C, R, Kc, kind)
-            cache[key] = t
-        return t
+    # ------------------------------------------------------------ layout
+    def _perm(self, device) -> torch.Tensor:
+        """int32 [d]: element j of a client row is flat coordinate perm[j].  The
+        rows keep every 3x3 conv weight (except the 3-channel stem) in the
+        kernels' (k, r, s, c) order -- the bf16 mirror then IS the grouped conv
+        kernels' forward image and the column-GEMM image, and the weight
+        gradients come out of the MFMA / GEMM reductions in that order -- and
+        everything else in PyTorch's order."""
+        if getattr(self, "_perm_t", None) is None or self._perm_t.device != device:
+            import numpy as np
+            perm = np.arange(self.d, dtype=np.int64)
+            for b in self.blocks:
+                for off, K, C in ((b.conv1, b.cout, b.cin), (b.conv2, b.cout, b.cout)):
+                    # internal (k, t, c) <- PyTorch (k, c, t)
+                    k, t, c = np.meshgrid(np.arange(K), np.arange(9), np.arange(C), indexing="ij")
+                    perm[off:off + K * 9 * C] = off + ((k * C + c) * 9 + t).reshape(-1)
+            self._perm_t = torch.from_numpy(perm.astype(np.int32)).to(device)
+        return self._perm_t
 
-    def _conv3(self, x, cache, W, ld, G, off, K, C):
+    @staticmethod
+    def _rows(Wt: torch.Tensor, ld: int, G: int, off: int, K: int, n: int) -> torch.Tensor:
+        """[G, K, n] view of every client's [K][n] block at ``off`` (ld 0: the
+        shared server row, batch stride 0)"""
+        if ld:
+            return Wt[:, off:off + K * n].view(G, K, n)
+        return Wt[off:off + K * n].view(1, K, n).expand(G, K, n)
+
+    # ----------------------------------------------------------- convs
+    def _conv3(self, x, Wb, ldb, G, off, K, C):
         """stride-1 3x3 conv of channel-stacked x with the clients' weights"""
-        y = _ops().conv3x3_fwd_grouped(x, self._img(cache, W, ld, G, off, K, C, 3, 0), G)
-        if y.numel() == 0 and x.numel():
+        y = _ops().conv3x3_fwd_rows(x, Wb, G, off, ldb, K)
+        if y.numel() == 0 and x.numel():  # no halo tiling: column image x weight rows
             col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
             n, _, H, Wd = x.shape
             y = torch.empty((n, G * K, H, Wd), device=x.device, dtype=torch.bfloat16,
                             memory_format=torch.channels_last)
-            torch.bmm(col.transpose(0, 1), self._img(cache, W, ld, G, off, K, C, 3, 2).transpose(1, 2),
+            torch.bmm(col.transpose(0, 1), self._rows(Wb, ldb, G, off, K, 9 * C).transpose(1, 2),
                       out=_gview(y, G))
         return y
 
-    def _conv3_dgrad(self, dy, cache, W, ld, G, off, K, C):
-        dx = _ops().conv3x3_fwd_grouped(dy, self._img(cache, W, ld, G, off, K, C, 3, 1), G)
+    def _conv3_dgrad(self, dy, Wb, ldb, G, off, K, C):
+        img = _ops().fa_dgrad_image(Wb, ldb, G, off, K, C)
+        dx = _ops().conv3x3_fwd_rows(dy, img, G, 0, C * 9 * K if ldb else 0, C)
         if dx.numel() == 0 and dy.numel():
             n, _, H, Wd = dy.shape
             dcol = torch.empty((n * H * Wd, G, 9 * C), device=dy.device, dtype=torch.bfloat16)
-            torch.bmm(_gview(dy, G), self._img(cache, W, ld, G, off, K, C, 3, 2),
-                      out=dcol.transpose(0, 1))
+            torch.bmm(_gview(dy, G), self._rows(Wb, ldb, G, off, K, 9 * C), out=dcol.transpose(0, 1))
             dx = _ops().col2im_grouped(dcol, G, n, H, Wd, C, 3, 3, 1, 1)
         return dx
 
+    @staticmethod
+    def _rows_store(Gg, off, part):
+        """part fp32 [G, K, n] -> the clients' gradient rows at ``off`` (a plain
+        vectorised copy: part is already in the rows' order)"""
+        G, K, n = part.shape
+        _ops().wgrad_rsc_add(Gg[:, off:off + K * n].view(G, K, n), part, 1, n, 1, False)
+
     def _conv3_wgrad(self, dy, x, G, Gg, gld, off, K, C):
-        if _ops().conv3x3_wgrad_rows(dy, x, G, Gg, gld, off):
+        if _ops().conv3x3_wgrad_rows(dy, x, G, Gg, gld, off, True):
             return
         col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
         part = torch.bmm(_gview(dy, G).transpose(1, 2), col.transpose(0, 1), out_dtype=torch.float32)
-        dst = Gg[:, off:off + K * C * 9].view(G, K, C * 9)
-        _ops().wgrad_rsc_add(dst, part, 1, C, 9, False)
+        self._rows_store(Gg, off, part)
 
     # ------------------------------------------------------------- round
     def run(self, w0: torch.Tensor, x: torch.Tensor, y: torch.Tensor, G: int, n: int, bs: int,
@@ -162,12 +185,20 @@ class ResNet18FedAvg:
             out: torch.Tensor, first_pass: bool):
         """Local SGD of G clients (client-major batch x [G*n, 3, H, W], labels
         y [G*n]); adds sum_g n (w0 - w_g) to ``out``.  Returns (per-client mean
-        loss [G], per-client mean accuracy [G]) over the local steps."""
+        loss [G], per-client mean accuracy [G], per-layer sums of the clients'
+        running statistics) over the local steps."""
         ops = _ops()
         dev = w0.device
         d = self.d
         ld = (d + 63) // 64 * 64
+        perm = self._perm(dev)
+        # the server weights in the rows' layout (+ bf16), read as a broadcast
+        # row by the first local step
+        w0i = torch.empty(ld, device=dev, dtype=torch.float32)
+        w0b = torch.empty(ld, device=dev, dtype=torch.bfloat16)
+        ops.fa_gather_rows(w0i, w0b, w0, perm)
         Wg = torch.empty((G, ld), device=dev, dtype=torch.float32)
+        Wb = torch.empty((G, ld), device=dev, dtype=torch.bfloat16)
         Gg = torch.zeros((G, ld), device=dev, dtype=torch.float32)
         # per-client running statistics (the model keeps their mean)
         run = []
@@ -189,15 +220,17 @@ class ResNet18FedAvg:
                     yb = y.view(G, n)[:, s0:s1].reshape(-1).contiguous()
                 else:
                     xb, yb = x, y
-                src, sld = (w0, 0) if steps == 0 else (Wg, ld)
-                l, c = self._step(xb, yb, G, s1 - s0, src, sld, Gg, ld, run,
-                                  nbt, ones)
+                if steps == 0:
+                    W, Wbf, sld = w0i, w0b, 0
+                else:
+                    W, Wbf, sld = Wg, Wb, ld
+                l, c = self._step(xb, yb, G, s1 - s0, W, Wbf, sld, Gg, ld, run, nbt, ones)
                 loss_acc += l
                 acc_acc += c
-                ops.fa_row_sgd(Wg, ld, src, sld, Gg, ld, G, d, float(clip or 0.0),
-                               float(lr * decay ** steps), float(wd))
+                ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip or 0.0),
+                               float(lr * decay ** steps), float(wd), Wb)
                 steps += 1
-        ops.fa_upload(out, w0, Wg, ld, G, float(n))
+        ops.fa_upload(out, w0i, Wg, ld, G, float(n), perm)
         # running statistics: per-client copies summed for the caller's mean
         sums = []
         for b, (rm1, rm2, rv1, rv2) in zip(self.blocks, run):
@@ -205,30 +238,29 @@ class ResNet18FedAvg:
                          rv1.view(G, -1).double().sum(0), rv2.view(G, -1).double().sum(0)))
         return loss_acc / steps, acc_acc / steps, sums
 
-    def _step(self, x, y, G, n, W, ld, Gg, gld, run, nbt, ones):
-        """One local step of every client: forward, backward into Gg."""
+    def _step(self, x, y, G, n, W, Wb, ld, Gg, gld, run, nbt, ones):
+        """One local step of every client (fp32 rows W, bf16 mirror Wb, both
+        ld apart; ld 0 = the shared server row): forward, backward into Gg."""
         ops = _ops()
-        cache: Dict = {}
-        # ---- stem: grouped column image of the client-major input
+        # ---- stem: grouped column image of the client-major input (its 3-channel
+        # weight stays in PyTorch's order: a small padded column image)
         C0, K0 = self.cin0, self.c0
         Kc0 = (9 * C0 + 7) // 8 * 8
         col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
         H, Wd = x.shape[2], x.shape[3]
         y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
                          memory_format=torch.channels_last)
-        torch.bmm(col0.transpose(0, 1), self._img(cache, W, ld, G, self.prep, K0, C0, 3, 2).transpose(1, 2),
-                  out=_gview(y0, G))
+        w0img = ops.fa_weight_image(W, ld, G, self.prep, K0, C0, 3, Kc0, 2)
+        torch.bmm(col0.transpose(0, 1), w0img.transpose(1, 2), out=_gview(y0, G))
         a = ops.fa_ew(y0, None, 1)
         a0 = a
         saved = []
-        eps_m = [(b.m1.eps, b.m1.momentum, b.m2.eps, b.m2.momentum) for b in self.blocks]
         for bi, b in enumerate(self.blocks):
             xin = a
             rm1, rm2, rv1, rv2 = run[bi]
-            e1, mo1, e2, mo2 = eps_m[bi]
             colx = None
             if b.stride == 1:
-                h1 = self._conv3(xin, cache, W, ld, G, b.conv1, b.cout, b.cin)
+                h1 = self._conv3(xin, Wb, ld, G, b.conv1, b.cout, b.cin)
                 sc = xin
             else:
                 colx = ops.im2col_grouped(xin, G, 3, 3, 2, 1, 9 * b.cin, False)
@@ -237,24 +269,24 @@ class ResNet18FedAvg:
                 h1 = torch.empty((nn_, G * b.cout, Ho, Wo), device=x.device, dtype=torch.bfloat16,
                                  memory_format=torch.channels_last)
                 cg = colx.transpose(0, 1)
-                torch.bmm(cg, self._img(cache, W, ld, G, b.conv1, b.cout, b.cin, 3, 2).transpose(1, 2),
+                torch.bmm(cg, self._rows(Wb, ld, G, b.conv1, b.cout, 9 * b.cin).transpose(1, 2),
                           out=_gview(h1, G))
+                # the 1x1 stride-2 shortcut reads the centre tap of the column image
                 sc = torch.empty_like(h1)
-                ctr = cg[:, :, 4 * b.cin:5 * b.cin]
-                torch.bmm(ctr, self._img(cache, W, ld, G, b.sc, b.cout, b.cin, 1, 2).transpose(1, 2),
-                          out=_gview(sc, G))
-            a1, st1, bits1 = ops.cs_bn_fwd(h1, W, ld, b.bn1w, b.bn1b, G, e1, mo1, rm1, rv1,
+                torch.bmm(cg[:, :, 4 * b.cin:5 * b.cin],
+                          self._rows(Wb, ld, G, b.sc, b.cout, b.cin).transpose(1, 2), out=_gview(sc, G))
+            a1, st1, bits1 = ops.cs_bn_fwd(h1, W, ld, b.bn1w, b.bn1b, G, b.m1.eps, b.m1.momentum, rm1, rv1,
                                            nbt if bi == 0 else None)
-            h2 = self._conv3(a1, cache, W, ld, G, b.conv2, b.cout, b.cout)
-            a2, st2, bits2 = ops.cs_bn_fwd(h2, W, ld, b.bn2w, b.bn2b, G, e2, mo2, rm2, rv2, None)
+            h2 = self._conv3(a1, Wb, ld, G, b.conv2, b.cout, b.cout)
+            a2, st2, bits2 = ops.cs_bn_fwd(h2, W, ld, b.bn2w, b.bn2b, G, b.m2.eps, b.m2.momentum, rm2, rv2,
+                                           None)
             a = ops.fa_ew(a2, sc, 0)
             saved.append((xin, colx, h1, st1, bits1, a1, h2, st2, bits2))
         # ---- head: avg || max pool -> per-client linear -> cross entropy
         feat, codes = ops.fa_head_fwd(a, G)
         # classifier rows of every client (the first step: the server row, batch stride 0)
-        Wr = W if ld else W.unsqueeze(0).expand(G, -1)
-        Wfc = Wr[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
-        bfc = Wr[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
+        Wfc = self._rows(W, ld, G, self.fc_w, self.ncls, self.feat)
+        bfc = self._rows(W, ld, G, self.fc_b, 1, self.ncls)
         logits = torch.bmm(feat, Wfc.transpose(1, 2))
         logits.baddbmm_(ones[:, :n], bfc)
         loss, correct, gl = ops.ce_fwd(logits.view(G * n, self.ncls), y)
@@ -272,30 +304,26 @@ class ResNet18FedAvg:
             b = self.blocks[bi]
             xin, colx, h1, st1, bits1, a1, h2, st2, bits2 = saved[bi]
             dh2 = ops.cs_bn_bwd(da, h2, st2, bits2, W, ld, b.bn2w, G, Gg, gld, b.bn2w, b.bn2b)
-            da1 = self._conv3_dgrad(dh2, cache, W, ld, G, b.conv2, b.cout, b.cout)
+            da1 = self._conv3_dgrad(dh2, Wb, ld, G, b.conv2, b.cout, b.cout)
             self._conv3_wgrad(dh2, a1, G, Gg, gld, b.conv2, b.cout, b.cout)
             dh1 = ops.cs_bn_bwd(da1, h1, st1, bits1, W, ld, b.bn1w, G, Gg, gld, b.bn1w, b.bn1b)
             if b.stride == 1:
-                dx = self._conv3_dgrad(dh1, cache, W, ld, G, b.conv1, b.cout, b.cin)
+                dx = self._conv3_dgrad(dh1, Wb, ld, G, b.conv1, b.cout, b.cin)
                 self._conv3_wgrad(dh1, xin, G, Gg, gld, b.conv1, b.cout, b.cin)
                 da = ops.fa_ew(dx, da, 0)
             else:
                 nn_, _, Hi, Wi = xin.shape
-                Kc = 9 * b.cin
-                dcol = torch.empty((colx.shape[0], G, Kc), device=x.device, dtype=torch.bfloat16)
+                dcol = torch.empty((colx.shape[0], G, 9 * b.cin), device=x.device, dtype=torch.bfloat16)
                 dcg = dcol.transpose(0, 1)
-                torch.bmm(_gview(dh1, G), self._img(cache, W, ld, G, b.conv1, b.cout, b.cin, 3, 2), out=dcg)
+                torch.bmm(_gview(dh1, G), self._rows(Wb, ld, G, b.conv1, b.cout, 9 * b.cin), out=dcg)
+                # the shortcut's input gradient joins the centre tap before the gather
                 dctr = dcg[:, :, 4 * b.cin:5 * b.cin]
-                torch.baddbmm(dctr, _gview(da, G), self._img(cache, W, ld, G, b.sc, b.cout, b.cin, 1, 2),
-                              out=dctr)
+                torch.baddbmm(dctr, _gview(da, G), self._rows(Wb, ld, G, b.sc, b.cout, b.cin), out=dctr)
                 cg = colx.transpose(0, 1)
-                part = torch.bmm(_gview(dh1, G).transpose(1, 2), cg, out_dtype=torch.float32)
-                ops.wgrad_rsc_add(Gg[:, b.conv1:b.conv1 + b.cout * b.cin * 9].view(G, b.cout, b.cin * 9),
-                                  part, 1, b.cin, 9, False)
-                psc = torch.bmm(_gview(da, G).transpose(1, 2), cg[:, :, 4 * b.cin:5 * b.cin],
-                                out_dtype=torch.float32)
-                ops.wgrad_rsc_add(Gg[:, b.sc:b.sc + b.cout * b.cin].view(G, b.cout, b.cin), psc, 1,
-                                  b.cin, 1, False)
+                self._rows_store(Gg, b.conv1, torch.bmm(_gview(dh1, G).transpose(1, 2), cg,
+                                                        out_dtype=torch.float32))
+                self._rows_store(Gg, b.sc, torch.bmm(_gview(da, G).transpose(1, 2),
+                                                     cg[:, :, 4 * b.cin:5 * b.cin], out_dtype=torch.float32))
                 da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)

@@ -223,6 +223,50 @@ def test_conv3x3_wgrad_rows_matches_grouped_conv():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("H,K,C", [(16, 128, 128), (8, 256, 128), (32, 64, 64)])
+def test_conv_rows_forward_and_dgrad_image(H, K, C):
+    """Grouped halo conv reading every client's bf16 (k, r, s, c) weight rows in
+    place (row stride ld, or one shared row), and the flipped / transposed
+    dgrad image built from those rows."""
+    torch.manual_seed(0)
+    G, n, off = 3, 2, 64
+    ld = off + K * 9 * C + 64
+    x = _cs(torch.randn(G, n, C, H, H, device="cuda"), G)
+    w = torch.randn(G, K, C, 3, 3, device="cuda") / (3 * C ** 0.5)  # PyTorch layout
+    Wb = torch.zeros(G, ld, device="cuda", dtype=torch.bfloat16)
+    Wb[:, off:off + K * 9 * C] = w.permute(0, 1, 3, 4, 2).reshape(G, -1).bfloat16()
+    ops = _ops()
+    y = ops.conv3x3_fwd_rows(x, Wb, G, off, ld, K)
+    ref = F.conv2d(x.float(), w.reshape(G * K, C, 3, 3).bfloat16().float(), padding=1, groups=G)
+    scale = ref.abs().max()
+    torch.testing.assert_close(y.float() / scale, ref / scale, rtol=2e-2, atol=2e-2)
+    # one shared row (the first local step)
+    y0 = ops.conv3x3_fwd_rows(x, Wb[0].contiguous(), G, off, 0, K)
+    ref0 = F.conv2d(x.float(), w[:1].expand(G, -1, -1, -1, -1).reshape(G * K, C, 3, 3).bfloat16().float(),
+                    padding=1, groups=G)
+    torch.testing.assert_close(y0.float() / scale, ref0 / scale, rtol=2e-2, atol=2e-2)
+    img = ops.fa_dgrad_image(Wb, ld, G, off, K, C)
+    refi = w.flip(3, 4).permute(0, 2, 3, 4, 1).reshape(G * C, 3, 3, K).bfloat16()
+    torch.testing.assert_close(img, refi, rtol=0, atol=0)
+    assert ops.fa_dgrad_image(Wb[1].contiguous(), 0, G, off, K, C).shape == (C, 3, 3, K)
+
+
+@pytest.mark.gpu
+def test_conv3x3_wgrad_rows_rsc_order():
+    torch.manual_seed(0)
+    G, n, C, K, H = 2, 5, 128, 128, 16
+    x = _cs(torch.randn(G, n, C, H, H, device="cuda"), G)
+    dy = _cs(torch.randn(G, n, K, H, H, device="cuda"), G)
+    ld, off = K * C * 9 + 64, 32
+    dst = torch.zeros(G, ld, device="cuda")
+    assert _ops().conv3x3_wgrad_rows(dy, x, G, dst, ld, off, True)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (G * K, C, 3, 3), dy.float(), padding=1, groups=G)
+    got = dst[:, off:off + K * C * 9].reshape(G * K, 3, 3, C).permute(0, 3, 1, 2)
+    scale = ref.abs().max()
+    torch.testing.assert_close(got / scale, ref / scale, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
 def test_ew_add_relu():
     a = torch.randn(2, 64, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     b = torch.randn_like(a)
