@@ -525,7 +525,10 @@ __device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
 // fwd: y = x A + B ;  bwd: dx = P dy + Q x + R  (per-(group, channel) coefficients)
 // ``aux``: forward -- a residual addend (y = act(x A + B + addend)); backward --
 // an output for the ReLU-masked dy (the addend's gradient)
-template <bool BWD>
+// POST (forward): y = relu(x A + B) + aux -- the residual add AFTER the ReLU
+// (models/fixup.py PreActBlock: relu(bn2(conv2 .)) + shortcut), the ReLU bits
+// of the pre-add value
+template <bool BWD, bool POST = false>
 __global__ void __launch_bounds__(256)
 bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                 const uint8_t* __restrict__ ybits, const float* __restrict__ coef, int C, int M,
@@ -544,7 +547,7 @@ bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
     if (!BWD) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f[j] * A[j] + B[j];
-      if (aux != nullptr) {  // fused residual add (before the ReLU)
+      if (!POST && aux != nullptr) {  // fused residual add (before the ReLU)
         float r8[8];
         unpack8(*reinterpret_cast<const u4*>(aux + static_cast<size_t>(i) * 8), r8);
 #pragma unroll
@@ -565,8 +568,17 @@ bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
       for (int j = 0; j < 8; ++j) o[j] = d[j] * A[j] + f[j] * B[j] + R[j];
     }
     const u4 v = {pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])};
-    *reinterpret_cast<u4*>(out + static_cast<size_t>(i) * 8) = v;
     if (!BWD && bits_out != nullptr) bits_out[i] = static_cast<uint8_t>(pos_bits8(v));
+    if (!BWD && POST) {  // residual add after the ReLU (on the bf16-rounded value)
+      float r8[8], q[8];
+      unpack8(*reinterpret_cast<const u4*>(aux + static_cast<size_t>(i) * 8), r8);
+      unpack8(v, q);
+      const u4 w = {pack2(q[0] + r8[0], q[1] + r8[1]), pack2(q[2] + r8[2], q[3] + r8[3]),
+                    pack2(q[4] + r8[4], q[5] + r8[5]), pack2(q[6] + r8[6], q[7] + r8[7])};
+      *reinterpret_cast<u4*>(out + static_cast<size_t>(i) * 8) = w;
+    } else {
+      *reinterpret_cast<u4*>(out + static_cast<size_t>(i) * 8) = v;
+    }
   }
 }
 
@@ -748,15 +760,20 @@ int64_t bn_cs_scratch_floats(int M, int C) { return static_cast<int64_t>(bn_slab
 void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t woff, int64_t boff, int cg,
                       int M, int C, float eps, float momentum, float* run_mean, float* run_var,
                       int64_t* nbt, float* part, float* stat, float* ab, uint16_t* y, uint8_t* relu_bits,
-                      hipStream_t stream) {
+                      const uint16_t* post_add, hipStream_t stream) {
   const int S = bn_slabs(1, M), CB = cs_channel_block(C);
   COMMEFF_LAUNCH(bn_partial_kernel<false>, dim3(S, C / CB), dim3(256), 0, stream, x, nullptr, nullptr,
                  nullptr, C, M, S, part, CB);
   COMMEFF_LAUNCH(bn_cs_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part, prm,
                  ld, woff, boff, cg, C, M, S, eps, momentum, stat, ab, run_mean, run_var, nbt);
   const int64_t nchunks = static_cast<int64_t>(M) * (C / 8);
-  COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
-                 nullptr, ab, C, M, static_cast<uint32_t>(nchunks), true, y, nullptr, relu_bits);
+  if (post_add != nullptr)
+    COMMEFF_LAUNCH((bn_apply_kernel<false, true>), dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
+                   nullptr, ab, C, M, static_cast<uint32_t>(nchunks), true, y, const_cast<uint16_t*>(post_add),
+                   relu_bits);
+  else
+    COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
+                   nullptr, ab, C, M, static_cast<uint32_t>(nchunks), true, y, nullptr, relu_bits);
 }
 
 void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,

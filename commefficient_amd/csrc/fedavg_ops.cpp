@@ -308,8 +308,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cs_bn_fwd(const at::Tensor& x, co
                                                          double momentum,
                                                          const c10::optional<at::Tensor>& run_mean,
                                                          const c10::optional<at::Tensor>& run_var,
-                                                         const c10::optional<at::Tensor>& nbt) {
+                                                         const c10::optional<at::Tensor>& nbt,
+                                                         const c10::optional<at::Tensor>& post_add) {
   check_cl_bf16(x, "cs_bn_fwd: x");
+  const uint16_t* pa = nullptr;
+  if (post_add.has_value() && post_add->defined()) {  // y = relu(bn(x)) + post_add
+    check_cl_bf16(*post_add, "cs_bn_fwd: post_add");
+    TORCH_CHECK(post_add->sizes() == x.sizes(), "cs_bn_fwd: post_add shape");
+    pa = bf(*post_add);
+  }
   const int64_t C = x.size(1), M = x.size(0) * x.size(2) * x.size(3);
   TORCH_CHECK(G >= 1 && C % G == 0 && (C / G) % 8 == 0 && M >= 1, "cs_bn_fwd: G | channels, 8 | channels per client");
   const int64_t cg = C / G;
@@ -340,7 +347,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cs_bn_fwd(const at::Tensor& x, co
   launch_bn_cs_fwd(bf(x), prm.data_ptr<float>(), ld, woff, boff, static_cast<int>(cg), static_cast<int>(M),
                    static_cast<int>(C), static_cast<float>(eps), static_cast<float>(momentum), rm, rv, nb,
                    part.data_ptr<float>(), stat.data_ptr<float>(), ab.data_ptr<float>(), bfw(y),
-                   bits.data_ptr<uint8_t>(), stream_now());
+                   bits.data_ptr<uint8_t>(), pa, stream_now());
   return {y, stat, bits};
 }
 
@@ -426,7 +433,8 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("im2col_grouped(Tensor x, int G, int R, int S, int stride, int pad, int Kc, bool client_major) -> Tensor");
   m.def("col2im_grouped(Tensor gcol, int G, int n, int H, int W, int C, int R, int S, int stride, int pad) -> Tensor");
   m.def("cs_bn_fwd(Tensor x, Tensor prm, int ld, int woff, int boff, int G, float eps, float momentum, "
-        "Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt) -> (Tensor, Tensor, Tensor)");
+        "Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt, Tensor? post_add=None) "
+        "-> (Tensor, Tensor, Tensor)");
   m.def("cs_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor bits, Tensor prm, int ld, int woff, int G, "
         "Tensor(a!) grad, int gld, int gwoff, int gboff) -> Tensor");
   m.def("conv3x3_wgrad_rows(Tensor dy, Tensor x, int G, Tensor(a!) dst, int ld, int off, bool rsc=False) -> bool");

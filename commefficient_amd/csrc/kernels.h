@@ -401,7 +401,7 @@ int64_t bn_cs_scratch_floats(int M, int C);
 void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t woff, int64_t boff, int cg,
                       int M, int C, float eps, float momentum, float* run_mean, float* run_var,
                       int64_t* nbt, float* part, float* stat, float* ab, uint16_t* y, uint8_t* relu_bits,
-                      hipStream_t stream);
+                      const uint16_t* post_add, hipStream_t stream);
 void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                       const float* prm, int64_t ld, int64_t woff, int cg, int M, int C, float* part,
                       float* coef, float* grad, int64_t gld, int64_t gwoff, int64_t gboff, uint16_t* dx,

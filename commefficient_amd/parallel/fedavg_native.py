@@ -165,19 +165,29 @@ class ResNet18FedAvg:
             dx = _ops().col2im_grouped(dcol, G, n, H, Wd, C, 3, 3, 1, 1)
         return dx
 
-    @staticmethod
-    def _rows_store(Gg, off, part):
-        """part fp32 [G, K, n] -> the clients' gradient rows at ``off`` (a plain
-        vectorised copy: part is already in the rows' order)"""
-        G, K, n = part.shape
-        _ops().wgrad_rsc_add(Gg[:, off:off + K * n].view(G, K, n), part, 1, n, 1, False)
+    _BMM_INTO = [True]
+
+    @classmethod
+    def _bmm_rows(cls, Gg, off, A, B):
+        """fp32 A_g @ B_g (bf16 operands) written straight into the clients'
+        gradient rows at ``off`` (they are in the product's order); else through
+        a temporary and a vectorised copy"""
+        G, K, n = A.shape[0], A.shape[1], B.shape[2]
+        dst = Gg[:, off:off + K * n].view(G, K, n)
+        if cls._BMM_INTO[0]:
+            try:
+                torch.bmm(A, B, out_dtype=torch.float32, out=dst)
+                return
+            except (RuntimeError, TypeError):
+                cls._BMM_INTO[0] = False
+        part = torch.bmm(A, B, out_dtype=torch.float32)
+        _ops().wgrad_rsc_add(dst, part, 1, n, 1, False)
 
     def _conv3_wgrad(self, dy, x, G, Gg, gld, off, K, C):
         if _ops().conv3x3_wgrad_rows(dy, x, G, Gg, gld, off, True):
             return
         col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
-        part = torch.bmm(_gview(dy, G).transpose(1, 2), col.transpose(0, 1), out_dtype=torch.float32)
-        self._rows_store(Gg, off, part)
+        self._bmm_rows(Gg, off, _gview(dy, G).transpose(1, 2), col.transpose(0, 1))
 
     # ------------------------------------------------------------- round
     def run(self, w0: torch.Tensor, x: torch.Tensor, y: torch.Tensor, G: int, n: int, bs: int,
@@ -278,9 +288,9 @@ class ResNet18FedAvg:
             a1, st1, bits1 = ops.cs_bn_fwd(h1, W, ld, b.bn1w, b.bn1b, G, b.m1.eps, b.m1.momentum, rm1, rv1,
                                            nbt if bi == 0 else None)
             h2 = self._conv3(a1, Wb, ld, G, b.conv2, b.cout, b.cout)
-            a2, st2, bits2 = ops.cs_bn_fwd(h2, W, ld, b.bn2w, b.bn2b, G, b.m2.eps, b.m2.momentum, rm2, rv2,
-                                           None)
-            a = ops.fa_ew(a2, sc, 0)
+            # relu(bn2) + shortcut in the BN's apply pass (the ReLU bits are the pre-add value's)
+            a, st2, bits2 = ops.cs_bn_fwd(h2, W, ld, b.bn2w, b.bn2b, G, b.m2.eps, b.m2.momentum, rm2, rv2,
+                                          None, sc)
             saved.append((xin, colx, h1, st1, bits1, a1, h2, st2, bits2))
         # ---- head: avg || max pool -> per-client linear -> cross entropy
         feat, codes = ops.fa_head_fwd(a, G)
@@ -320,10 +330,8 @@ class ResNet18FedAvg:
                 dctr = dcg[:, :, 4 * b.cin:5 * b.cin]
                 torch.baddbmm(dctr, _gview(da, G), self._rows(Wb, ld, G, b.sc, b.cout, b.cin), out=dctr)
                 cg = colx.transpose(0, 1)
-                self._rows_store(Gg, b.conv1, torch.bmm(_gview(dh1, G).transpose(1, 2), cg,
-                                                        out_dtype=torch.float32))
-                self._rows_store(Gg, b.sc, torch.bmm(_gview(da, G).transpose(1, 2),
-                                                     cg[:, :, 4 * b.cin:5 * b.cin], out_dtype=torch.float32))
+                self._bmm_rows(Gg, b.conv1, _gview(dh1, G).transpose(1, 2), cg)
+                self._bmm_rows(Gg, b.sc, _gview(da, G).transpose(1, 2), cg[:, :, 4 * b.cin:5 * b.cin])
                 da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)

@@ -146,6 +146,11 @@ def test_cs_bn_forward_backward(G, C, H):
     torch.testing.assert_close(rv.view(G, C), 0.9 * rv0.view(G, C) + 0.1 * var.view(G, C) * M / (M - 1),
                                rtol=1e-3, atol=1e-3)
     assert int(nbt) == 1
+    # the residual add after the ReLU (PreActBlock tail): same bits, y + r
+    r = torch.randn_like(y, dtype=torch.float32).bfloat16().contiguous(memory_format=torch.channels_last)
+    y2, _, bits2 = ops.cs_bn_fwd(x, P, ld, woff, boff, G, 1e-5, 0.1, rm.clone(), rv.clone(), None, r)
+    assert torch.equal(bits2, bits)
+    torch.testing.assert_close(y2.float(), (y.float() + r.float()).bfloat16().float(), rtol=0, atol=0)
     DY = torch.randn(G, n, C, H, H, device="cuda")
     dy = _cs(DY, G)
     yr.backward(dy.float().view(n, G, C, H, H).transpose(0, 1))
