@@ -1243,10 +1243,15 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
                                                                        float* __restrict__ dw, int K, int C,
                                                                        int splits, float beta,
                                                                        int64_t gstride, int kg, int64_t ld,
-                                                                       int rsc) {
+                                                                       int rsc, int sub) {
   __shared__ float t[PARTS][64 * 9];
   const int ncb = C >> 6;
   const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
+  // sub > 0: each kernel group of kg channels is kg / sub clients whose weights
+  // are the diagonal sub x sub blocks of the group's product (two 64-channel
+  // clients computed as one 128-channel group); other blocks are not written
+  const int half = sub > 0 ? (k % kg) / sub : 0;
+  if (sub > 0 && c0 / sub != half) return;  // block-uniform
   slab += static_cast<size_t>(blockIdx.y) * splits * K * 9 * C;
   dw += static_cast<size_t>(blockIdx.y) * gstride;
   const int cc = threadIdx.x & 63, part = threadIdx.x >> 6;
@@ -1267,14 +1272,17 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
   // kg > 0: output channel k is row k % kg of group k / kg's weight, groups
   // ld floats apart (the per-client gradient rows of parallel/fedavg_native.py)
   // rsc: the row in (r, s, c) order ([kg][3][3][C], the engine's layout)
-  float* o = kg > 0 ? dw + static_cast<size_t>(k / kg) * ld + static_cast<size_t>(k % kg) * C * 9
-                    : dw + static_cast<size_t>(k) * C * 9;
+  const int Cl = sub > 0 ? sub : C, c0l = c0 - half * sub;
+  float* o = sub > 0 ? dw + static_cast<size_t>((k / kg) * (kg / sub) + half) * ld +
+                           static_cast<size_t>((k % kg) % sub) * Cl * 9
+             : kg > 0 ? dw + static_cast<size_t>(k / kg) * ld + static_cast<size_t>(k % kg) * C * 9
+                      : dw + static_cast<size_t>(k) * C * 9;
   for (int e = threadIdx.x; e < 576; e += 64 * PARTS) {
     const int src = rsc ? (e & 63) * 9 + (e >> 6) : e;
     float v = t[0][src];
 #pragma unroll
     for (int q = 1; q < PARTS; ++q) v += t[q][src];  // fixed order: deterministic
-    float* oe = rsc ? o + (e >> 6) * C + c0 + (e & 63) : o + c0 * 9 + e;
+    float* oe = rsc ? o + (e >> 6) * Cl + c0l + (e & 63) : o + c0l * 9 + e;
     *oe = beta != 0.f ? beta * *oe + v : v;
   }
 }
@@ -1282,14 +1290,14 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
 
 void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
                          int64_t gstride, int groups, hipStream_t stream, int kg = 0, int64_t ld = 0,
-                         bool rsc = false) {
+                         bool rsc = false, int sub = 0) {
   const dim3 grid(K * (C / 64), groups);
   if (splits >= 32)
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld, rsc ? 1 : 0);
+                       beta, gstride, kg, ld, rsc ? 1 : 0, sub);
   else
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld, rsc ? 1 : 0);
+                       beta, gstride, kg, ld, rsc ? 1 : 0, sub);
 }
 
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16
@@ -1624,11 +1632,12 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 
 // channel-stacked grouped wgrad written straight into per-group rows: output
 // channel k of group k / kg at dst + (k / kg) * ld + (k % kg) * 9 C
-void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream) {
+void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream,
+                               int sub) {
   const int steps = (a.P + BK - 1) / BK;
   a.group_px = 0;
   launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
-  launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, 0.f, int64_t{0}, 1, stream, kg, ld, rsc);
+  launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, 0.f, int64_t{0}, 1, stream, kg, ld, rsc, sub);
 }
 
 // the wgrad GEMM kernels (slabs only) with a given split length

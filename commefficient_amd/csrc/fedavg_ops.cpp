@@ -391,16 +391,21 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W && G >= 1 && GC % G == 0 && K % G == 0,
               "conv3x3_wgrad_rows: shapes");
   const int64_t C = GC / G, kg = K / G;
+  // 64-channel clients (no 64-row grouped halo tiling): pairs of clients as
+  // one 128-channel group, whose diagonal 64 x 64 blocks are the two clients'
+  // weight gradients (twice the MFMA work, no column image)
+  const bool pairs = kg == 64 && C == 64 && G % 2 == 0;
+  const int64_t kC = pairs ? 128 : C, kK = pairs ? 128 : kg;
   if (!conv3x3_wgrad_grouped_supported(static_cast<int>(H), static_cast<int>(W), static_cast<int>(K),
-                                       static_cast<int>(C), static_cast<int>(kg)))
+                                       static_cast<int>(kC), static_cast<int>(kK)))
     return false;
   check_rows(dst, ld, G, off, kg * C * 9, "conv3x3_wgrad_rows: dst");
   TORCH_CHECK(N * H * W * std::max(GC, K) < (int64_t{1} << 31), "conv3x3_wgrad_rows: size");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int P = static_cast<int>(N * H * W);
   const int splits = conv3x3_wgrad_splits(P, static_cast<int>(H), static_cast<int>(W), static_cast<int>(K),
-                                          static_cast<int>(C));
-  auto slab = at::empty({splits * K * 9 * C}, x.options().dtype(at::kFloat));
+                                          static_cast<int>(kC));
+  auto slab = at::empty({splits * K * 9 * kC}, x.options().dtype(at::kFloat));
   ConvWgradArgs a;
   a.dy = bf(dy);
   a.x = bf(x);
@@ -408,12 +413,13 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
   a.P = P;
   a.H = static_cast<int>(H);
   a.W = static_cast<int>(W);
-  a.C = static_cast<int>(C);
+  a.C = static_cast<int>(kC);
   a.K = static_cast<int>(K);
   a.splits = splits;
   a.x_stride = static_cast<int>(GC);
-  a.kg = static_cast<int>(kg);
-  launch_conv3x3_wgrad_rows(a, dst.data_ptr<float>() + off, static_cast<int>(kg), ld, rsc, stream_now());
+  a.kg = static_cast<int>(kK);
+  launch_conv3x3_wgrad_rows(a, dst.data_ptr<float>() + off, static_cast<int>(kK), ld, rsc, stream_now(),
+                            pairs ? 64 : 0);
   return true;
 }
 

@@ -306,7 +306,10 @@ int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);
 // grouped (a.kg, a.x_stride set) wgrad into per-group fp32 rows ld apart
 // (rsc: rows in (r, s, c) order instead of PyTorch's (c, r, s))
-void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream);
+// (sub > 0: every kernel group of kg channels is kg / sub clients -- the
+// diagonal sub x sub blocks are written, each to its client's row)
+void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream,
+                               int sub = 0);
 // grouped convs on channel-stacked images (a.kg / a.x_stride set): false when
 // the geometry has no halo tiling (the caller falls back)
 bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream);

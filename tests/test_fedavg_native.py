@@ -257,9 +257,12 @@ def test_conv_rows_forward_and_dgrad_image(H, K, C):
 
 
 @pytest.mark.gpu
-def test_conv3x3_wgrad_rows_rsc_order():
+@pytest.mark.parametrize("G,C,K,H", [(2, 128, 128, 16), (4, 64, 64, 32)])
+def test_conv3x3_wgrad_rows_rsc_order(G, C, K, H):
+    """(64-channel clients: computed in pairs as 128-channel groups, the
+    diagonal blocks kept)"""
     torch.manual_seed(0)
-    G, n, C, K, H = 2, 5, 128, 128, 16
+    n = 5
     x = _cs(torch.randn(G, n, C, H, H, device="cuda"), G)
     dy = _cs(torch.randn(G, n, K, H, H, device="cuda"), G)
     ld, off = K * C * 9 + 64, 32
