@@ -1243,7 +1243,8 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
                                                                        float* __restrict__ dw, int K, int C,
                                                                        int splits, float beta,
                                                                        int64_t gstride, int kg, int64_t ld,
-                                                                       int rsc, int sub) {
+                                                                       int rsc, int sub, float alpha,
+                                                                       uint16_t* __restrict__ mirror) {
   __shared__ float t[PARTS][64 * 9];
   const int ncb = C >> 6;
   const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
@@ -1254,6 +1255,7 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
   if (sub > 0 && c0 / sub != half) return;  // block-uniform
   slab += static_cast<size_t>(blockIdx.y) * splits * K * 9 * C;
   dw += static_cast<size_t>(blockIdx.y) * gstride;
+  float* const dw_base = dw;
   const int cc = threadIdx.x & 63, part = threadIdx.x >> 6;
   const size_t sstride = static_cast<size_t>(K) * 9 * C;
   const float* src = slab + static_cast<size_t>(k) * 9 * C + c0 + cc;
@@ -1283,21 +1285,28 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
 #pragma unroll
     for (int q = 1; q < PARTS; ++q) v += t[q][src];  // fixed order: deterministic
     float* oe = rsc ? o + (e >> 6) * Cl + c0l + (e & 63) : o + c0l * 9 + e;
-    *oe = beta != 0.f ? beta * *oe + v : v;
+    // alpha / beta: the batched FedAvg clients' SGD step applied in place
+    // (w = (1 - lr wd) w - lr g), with the bf16 mirror of the new weight
+    const float r = beta != 0.f ? beta * *oe + alpha * v : alpha * v;
+    *oe = r;
+    if (mirror != nullptr) {
+      const uint32_t u = __float_as_uint(r);
+      mirror[oe - dw_base] = static_cast<uint16_t>((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
   }
 }
 
 
 void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
                          int64_t gstride, int groups, hipStream_t stream, int kg = 0, int64_t ld = 0,
-                         bool rsc = false, int sub = 0) {
+                         bool rsc = false, int sub = 0, float alpha = 1.f, uint16_t* mirror = nullptr) {
   const dim3 grid(K * (C / 64), groups);
   if (splits >= 32)
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld, rsc ? 1 : 0, sub);
+                       beta, gstride, kg, ld, rsc ? 1 : 0, sub, alpha, mirror);
   else
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld, rsc ? 1 : 0, sub);
+                       beta, gstride, kg, ld, rsc ? 1 : 0, sub, alpha, mirror);
 }
 
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16
@@ -1633,11 +1642,12 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 // channel-stacked grouped wgrad written straight into per-group rows: output
 // channel k of group k / kg at dst + (k / kg) * ld + (k % kg) * 9 C
 void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream,
-                               int sub) {
+                               int sub, float beta, float alpha, uint16_t* mirror) {
   const int steps = (a.P + BK - 1) / BK;
   a.group_px = 0;
   launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
-  launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, 0.f, int64_t{0}, 1, stream, kg, ld, rsc, sub);
+  launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, beta, int64_t{0}, 1, stream, kg, ld, rsc, sub, alpha,
+                      mirror);
 }
 
 // the wgrad GEMM kernels (slabs only) with a given split length

@@ -121,14 +121,31 @@ __global__ void __launch_bounds__(256) row_sgd_kernel(float* __restrict__ W, int
   const float4* src = reinterpret_cast<const float4*>(Src + g * sld);
   const float4* gr = reinterpret_cast<const float4*>(Gr + g * gld);
   uint2* wb = Wb != nullptr ? reinterpret_cast<uint2*>(Wb + g * ld) : nullptr;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < d4; i += static_cast<int64_t>(gridDim.x) * 256) {
-    const float4 s = src[i], q = gr[i];
-    const float4 o = make_float4(c * s.x + a * q.x, c * s.y + a * q.y, c * s.z + a * q.z, c * s.w + a * q.w);
-    w[i] = o;
-    // the bf16 mirror the next step's convolutions read (same row layout)
-    if (wb != nullptr)
-      wb[i] = make_uint2(static_cast<uint32_t>(f2bf(o.x)) | (static_cast<uint32_t>(f2bf(o.y)) << 16),
-                         static_cast<uint32_t>(f2bf(o.z)) | (static_cast<uint32_t>(f2bf(o.w)) << 16));
+  // 4 float4 of W and of G in flight per thread (one per pass: ~5.4 TB/s)
+  constexpr int U = 4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t i0 = blockIdx.x * 256ll + threadIdx.x; i0 < d4; i0 += U * stride) {
+    float4 sv[U], qv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < d4) {
+        sv[u] = src[i];
+        qv[u] = gr[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= d4) break;
+      const float4 s = sv[u], q = qv[u];
+      const float4 o = make_float4(c * s.x + a * q.x, c * s.y + a * q.y, c * s.z + a * q.z, c * s.w + a * q.w);
+      w[i] = o;
+      // the bf16 mirror the next step's convolutions read (same row layout)
+      if (wb != nullptr)
+        wb[i] = make_uint2(static_cast<uint32_t>(f2bf(o.x)) | (static_cast<uint32_t>(f2bf(o.y)) << 16),
+                           static_cast<uint32_t>(f2bf(o.z)) | (static_cast<uint32_t>(f2bf(o.w)) << 16));
+    }
   }
 }
 
@@ -145,6 +162,23 @@ __global__ void __launch_bounds__(256) upload_kernel(float* __restrict__ out, co
     for (int g = 0; g < G; ++g) acc += w - W[g * ld + j];
     out[perm != nullptr ? perm[j] : j] += n * acc;
   }
+}
+
+// W[g][j] = src[j] (every client row = the server row), float4
+__global__ void __launch_bounds__(256) bcast_rows_kernel(float* __restrict__ W, int64_t ld,
+                                                         const float* __restrict__ src, int64_t d4) {
+  float4* w = reinterpret_cast<float4*>(W + blockIdx.y * ld);
+  const float4* s = reinterpret_cast<const float4*>(src);
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < d4; i += static_cast<int64_t>(gridDim.x) * 256) w[i] = s[i];
+}
+
+// Wb[g*ld + off + j] = bf16(W[g*ld + off + j]), j < n (a segment's bf16 mirror)
+__global__ void __launch_bounds__(256) cast_rows_kernel(uint16_t* __restrict__ Wb, const float* __restrict__ W,
+                                                        int64_t ld, int64_t off, int64_t n) {
+  const float* w = W + blockIdx.y * ld + off;
+  uint16_t* b = Wb + blockIdx.y * ld + off;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256)
+    b[i] = f2bf(w[i]);
 }
 
 // dst[j] = src[perm[j]] (the server weights in the engine's layout) and its bf16 copy
@@ -264,7 +298,7 @@ void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const f
   if (G == 0 || d4 == 0) return;
   if (clip > 0.f)
     COMMEFF_LAUNCH(row_sumsq_kernel, dim3(kRowParts, G), dim3(256), 0, stream, Gr, gld, d4, part);
-  int bx = static_cast<int>((d4 + 255) / 256);
+  int bx = static_cast<int>((d4 + 1023) / 1024);
   const int cap = (8192 + G - 1) / G;
   if (bx > cap) bx = cap;
   COMMEFF_LAUNCH(row_sgd_kernel, dim3(bx < 1 ? 1 : bx, G), dim3(256), 0, stream, W, ld, src, sld, Gr, gld, d4,
@@ -283,6 +317,22 @@ void launch_gather_rows(float* dst, uint16_t* dstb, const float* src, const int3
                         hipStream_t stream) {
   if (d == 0) return;
   COMMEFF_LAUNCH(gather_rows_kernel, dim3(grid_for(d)), dim3(256), 0, stream, dst, dstb, src, perm, d);
+}
+
+void launch_bcast_rows(float* W, int64_t ld, const float* src, int G, int64_t d4, hipStream_t stream) {
+  if (G == 0 || d4 == 0) return;
+  int bx = static_cast<int>((d4 + 255) / 256);
+  const int cap = (8192 + G - 1) / G;
+  if (bx > cap) bx = cap;
+  COMMEFF_LAUNCH(bcast_rows_kernel, dim3(bx, G), dim3(256), 0, stream, W, ld, src, d4);
+}
+
+void launch_cast_rows(uint16_t* Wb, const float* W, int64_t ld, int G, int64_t off, int64_t n, hipStream_t stream) {
+  if (G == 0 || n == 0) return;
+  int bx = static_cast<int>((n + 255) / 256);
+  const int cap = (8192 + G - 1) / G;
+  if (bx > cap) bx = cap;
+  COMMEFF_LAUNCH(cast_rows_kernel, dim3(bx, G), dim3(256), 0, stream, Wb, W, ld, off, n);
 }
 
 void launch_dgrad_image(const uint16_t* src, int64_t ld, int G, int K, int C, uint16_t* dst, hipStream_t stream) {

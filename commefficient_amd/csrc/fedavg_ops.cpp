@@ -23,6 +23,8 @@ void launch_fedavg_upload(float* out, const float* w0, const float* W, int64_t l
 void launch_gather_rows(float* dst, uint16_t* dstb, const float* src, const int32_t* perm, int64_t d,
                         hipStream_t stream);
 void launch_dgrad_image(const uint16_t* src, int64_t ld, int G, int K, int C, uint16_t* dst, hipStream_t stream);
+void launch_bcast_rows(float* W, int64_t ld, const float* src, int G, int64_t d4, hipStream_t stream);
+void launch_cast_rows(uint16_t* Wb, const float* W, int64_t ld, int G, int64_t off, int64_t n, hipStream_t stream);
 void launch_avgmax_head_fwd(const uint16_t* x, int n, int HW, int G, int C, float* feat, uint8_t* codes,
                             hipStream_t stream);
 void launch_avgmax_head_bwd(const float* df, const uint8_t* codes, int n, int HW, int G, int C, uint16_t* dx,
@@ -136,6 +138,28 @@ void fa_gather_rows(at::Tensor dst, at::Tensor dstb, const at::Tensor& src, cons
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
   launch_gather_rows(dst.data_ptr<float>(), bfw(dstb), src.data_ptr<float>(), perm.data_ptr<int32_t>(), d,
                      stream_now());
+}
+
+// W[g] = src for every row g < rows (d floats, 16-byte aligned rows)
+void fa_bcast_rows(at::Tensor W, int64_t ld, const at::Tensor& src, int64_t rows, int64_t d) {
+  const int64_t d4 = (d + 3) / 4;
+  TORCH_CHECK(ld % 4 == 0 && d4 * 4 <= ld, "fa_bcast_rows: ld");
+  check_rows(W, ld, rows, 0, d4 * 4, "fa_bcast_rows: W");
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kFloat && src.is_contiguous() && src.numel() >= d4 * 4 &&
+                  reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0,
+              "fa_bcast_rows: src fp32 >= d (padded to 4), aligned");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  launch_bcast_rows(W.data_ptr<float>(), ld, src.data_ptr<float>(), static_cast<int>(rows), d4, stream_now());
+}
+
+// Wb[g, off:off+n] = bf16(W[g, off:off+n]) for every row
+void fa_cast_rows(at::Tensor Wb, const at::Tensor& W, int64_t ld, int64_t rows, int64_t off, int64_t n) {
+  check_rows(W, ld, rows, off, n, "fa_cast_rows: W");
+  TORCH_CHECK(Wb.is_cuda() && Wb.scalar_type() == at::kBFloat16 && Wb.is_contiguous() && Wb.numel() >= rows * ld,
+              "fa_cast_rows: Wb bf16 [rows, ld]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  launch_cast_rows(bfw(Wb), W.data_ptr<float>(), ld, static_cast<int>(rows), off, n, stream_now());
 }
 
 // [G*C, 3, 3, K] flipped / transposed dgrad image of 3x3 weights held as bf16
@@ -355,7 +379,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cs_bn_fwd(const at::Tensor& x, co
 // per-client weight / bias gradients are written to grad[g*gld + gwoff / gboff + c]
 at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stat, const at::Tensor& bits,
                      const at::Tensor& prm, int64_t ld, int64_t woff, int64_t G, at::Tensor grad, int64_t gld,
-                     int64_t gwoff, int64_t gboff) {
+                     int64_t gwoff, int64_t gboff, double beta, double alpha) {
   check_cl_bf16(x, "cs_bn_bwd: x");
   check_cl_bf16(dy, "cs_bn_bwd: dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "cs_bn_bwd: dy shape");
@@ -376,7 +400,8 @@ at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor
   auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   launch_bn_cs_bwd(bf(x), bf(dy), bits.data_ptr<uint8_t>(), stat.data_ptr<float>(), prm.data_ptr<float>(), ld,
                    woff, static_cast<int>(cg), static_cast<int>(M), static_cast<int>(C), part.data_ptr<float>(),
-                   coef.data_ptr<float>(), grad.data_ptr<float>(), gld, gwoff, gboff, bfw(dx), stream_now());
+                   coef.data_ptr<float>(), grad.data_ptr<float>(), gld, gwoff, gboff, bfw(dx), stream_now(),
+                   static_cast<float>(beta), static_cast<float>(alpha));
   return dx;
 }
 
@@ -384,7 +409,7 @@ at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor
 // gradient rows dst[g*ld + off + (k*C + c)*9 + t]; false (nothing written)
 // where the geometry has no grouped halo tiling
 bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at::Tensor dst, int64_t ld,
-                        int64_t off, bool rsc) {
+                        int64_t off, bool rsc, double beta, double alpha, const c10::optional<at::Tensor>& mirror) {
   check_cl_bf16(dy, "conv3x3_wgrad_rows: dy");
   check_cl_bf16(x, "conv3x3_wgrad_rows: x");
   const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
@@ -400,6 +425,13 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
                                        static_cast<int>(kC), static_cast<int>(kK)))
     return false;
   check_rows(dst, ld, G, off, kg * C * 9, "conv3x3_wgrad_rows: dst");
+  uint16_t* mp = nullptr;
+  if (mirror.has_value() && mirror->defined()) {  // bf16 rows of dst's layout
+    TORCH_CHECK(mirror->is_cuda() && mirror->scalar_type() == at::kBFloat16 && mirror->is_contiguous() &&
+                    mirror->numel() >= dst.numel(),
+                "conv3x3_wgrad_rows: mirror bf16 like dst");
+    mp = reinterpret_cast<uint16_t*>(mirror->data_ptr()) + off;
+  }
   TORCH_CHECK(N * H * W * std::max(GC, K) < (int64_t{1} << 31), "conv3x3_wgrad_rows: size");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int P = static_cast<int>(N * H * W);
@@ -419,7 +451,7 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
   a.x_stride = static_cast<int>(GC);
   a.kg = static_cast<int>(kK);
   launch_conv3x3_wgrad_rows(a, dst.data_ptr<float>() + off, static_cast<int>(kK), ld, rsc, stream_now(),
-                            pairs ? 64 : 0);
+                            pairs ? 64 : 0, static_cast<float>(beta), static_cast<float>(alpha), mp);
   return true;
 }
 
@@ -442,8 +474,11 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt, Tensor? post_add=None) "
         "-> (Tensor, Tensor, Tensor)");
   m.def("cs_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor bits, Tensor prm, int ld, int woff, int G, "
-        "Tensor(a!) grad, int gld, int gwoff, int gboff) -> Tensor");
-  m.def("conv3x3_wgrad_rows(Tensor dy, Tensor x, int G, Tensor(a!) dst, int ld, int off, bool rsc=False) -> bool");
+        "Tensor(a!) grad, int gld, int gwoff, int gboff, float beta=0., float alpha=1.) -> Tensor");
+  m.def("conv3x3_wgrad_rows(Tensor dy, Tensor x, int G, Tensor(a!) dst, int ld, int off, bool rsc=False, "
+        "float beta=0., float alpha=1., Tensor(b!)? mirror=None) -> bool");
+  m.def("fa_bcast_rows(Tensor(a!) W, int ld, Tensor src, int rows, int d) -> ()");
+  m.def("fa_cast_rows(Tensor(a!) Wb, Tensor W, int ld, int rows, int off, int n) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
@@ -451,6 +486,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("fa_row_sgd", &fa_row_sgd);
   m.impl("fa_upload", &fa_upload);
   m.impl("fa_gather_rows", &fa_gather_rows);
+  m.impl("fa_bcast_rows", &fa_bcast_rows);
+  m.impl("fa_cast_rows", &fa_cast_rows);
   m.impl("fa_dgrad_image", &fa_dgrad_image);
   m.impl("conv3x3_fwd_rows", &conv3x3_fwd_rows);
   m.impl("fa_head_fwd", &fa_head_fwd);

@@ -308,8 +308,10 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 // (rsc: rows in (r, s, c) order instead of PyTorch's (c, r, s))
 // (sub > 0: every kernel group of kg channels is kg / sub clients -- the
 // diagonal sub x sub blocks are written, each to its client's row)
+// (beta / alpha: dst = beta dst + alpha dW -- an SGD step in place -- and the
+// bf16 mirror of the result at the same offsets from `mirror`)
 void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream,
-                               int sub = 0);
+                               int sub = 0, float beta = 0.f, float alpha = 1.f, uint16_t* mirror = nullptr);
 // grouped convs on channel-stacked images (a.kg / a.x_stride set): false when
 // the geometry has no halo tiling (the caller falls back)
 bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream);
@@ -408,7 +410,7 @@ void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t w
 void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                       const float* prm, int64_t ld, int64_t woff, int cg, int M, int C, float* part,
                       float* coef, float* grad, int64_t gld, int64_t gwoff, int64_t gboff, uint16_t* dx,
-                      hipStream_t stream);
+                      hipStream_t stream, float beta = 0.f, float alpha = 1.f);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw = nullptr,

@@ -58,6 +58,18 @@ def _gview(t: torch.Tensor, G: int) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(n * H * W, G, GK // G).transpose(0, 1)
 
 
+class _Sink:
+    """Where one local step's weight gradients go: rows ``dst`` (ld apart)
+    receive ``beta * dst + alpha * grad`` -- the gradient rows (beta 0, alpha
+    1; a per-row SGD kernel follows, needed for clipping) or the weight rows
+    themselves (beta = 1 - lr wd, alpha = -lr: the SGD step fused into every
+    producer), with the bf16 ``mirror`` of the updated weights."""
+    __slots__ = ("dst", "ld", "beta", "alpha", "mirror")
+
+    def __init__(self, dst, ld, beta, alpha, mirror):
+        self.dst, self.ld, self.beta, self.alpha, self.mirror = dst, ld, float(beta), float(alpha), mirror
+
+
 class _Block:
     __slots__ = ("cin", "cout", "stride", "bn1w", "bn1b", "conv1", "bn2w", "bn2b", "conv2", "sc",
                  "m1", "m2")
@@ -118,19 +130,20 @@ class ResNet18FedAvg:
     # ------------------------------------------------------------ layout
     def _perm(self, device) -> torch.Tensor:
         """int32 [d]: element j of a client row is flat coordinate perm[j].  The
-        rows keep every 3x3 conv weight (except the 3-channel stem) in the
-        kernels' (k, r, s, c) order -- the bf16 mirror then IS the grouped conv
-        kernels' forward image and the column-GEMM image, and the weight
+        rows keep every 3x3 conv weight in the kernels' (k, r, s, c) order --
+        the bf16 mirror then IS the grouped conv kernels' forward image and the column-GEMM image, and the weight
         gradients come out of the MFMA / GEMM reductions in that order -- and
         everything else in PyTorch's order."""
         if getattr(self, "_perm_t", None) is None or self._perm_t.device != device:
             import numpy as np
             perm = np.arange(self.d, dtype=np.int64)
+            convs = [(self.prep, self.c0, self.cin0)]
             for b in self.blocks:
-                for off, K, C in ((b.conv1, b.cout, b.cin), (b.conv2, b.cout, b.cout)):
-                    # internal (k, t, c) <- PyTorch (k, c, t)
-                    k, t, c = np.meshgrid(np.arange(K), np.arange(9), np.arange(C), indexing="ij")
-                    perm[off:off + K * 9 * C] = off + ((k * C + c) * 9 + t).reshape(-1)
+                convs += [(b.conv1, b.cout, b.cin), (b.conv2, b.cout, b.cout)]
+            for off, K, C in convs:
+                # internal (k, t, c) <- PyTorch (k, c, t)
+                k, t, c = np.meshgrid(np.arange(K), np.arange(9), np.arange(C), indexing="ij")
+                perm[off:off + K * 9 * C] = off + ((k * C + c) * 9 + t).reshape(-1)
             self._perm_t = torch.from_numpy(perm.astype(np.int32)).to(device)
         return self._perm_t
 
@@ -168,26 +181,42 @@ class ResNet18FedAvg:
     _BMM_INTO = [True]
 
     @classmethod
-    def _bmm_rows(cls, Gg, off, A, B):
-        """fp32 A_g @ B_g (bf16 operands) written straight into the clients'
-        gradient rows at ``off`` (they are in the product's order); else through
-        a temporary and a vectorised copy"""
+    def _bmm_rows(cls, sink, off, A, B):
+        """fp32 A_g @ B_g (bf16 operands) into the sink's rows at ``off`` (they
+        are in the product's order): the gradient itself, or -- the fused SGD
+        step -- rows = beta rows + alpha A_g @ B_g in the GEMM's epilogue, then
+        the bf16 mirror of the updated segment"""
         G, K, n = A.shape[0], A.shape[1], B.shape[2]
-        dst = Gg[:, off:off + K * n].view(G, K, n)
+        dst = sink.dst[:, off:off + K * n].view(G, K, n)
         if cls._BMM_INTO[0]:
             try:
-                torch.bmm(A, B, out_dtype=torch.float32, out=dst)
+                if sink.beta == 0.0 and sink.alpha == 1.0:
+                    torch.bmm(A, B, out_dtype=torch.float32, out=dst)
+                else:
+                    torch.baddbmm(dst, A, B, out_dtype=torch.float32, beta=sink.beta, alpha=sink.alpha,
+                                  out=dst)
+                cls._mirror(sink, off, K * n)
                 return
             except (RuntimeError, TypeError):
                 cls._BMM_INTO[0] = False
         part = torch.bmm(A, B, out_dtype=torch.float32)
-        _ops().wgrad_rsc_add(dst, part, 1, n, 1, False)
+        if sink.beta == 0.0 and sink.alpha == 1.0:
+            _ops().wgrad_rsc_add(dst, part, 1, n, 1, False)
+        else:
+            dst.mul_(sink.beta).add_(part, alpha=sink.alpha)
+        cls._mirror(sink, off, K * n)
 
-    def _conv3_wgrad(self, dy, x, G, Gg, gld, off, K, C):
-        if _ops().conv3x3_wgrad_rows(dy, x, G, Gg, gld, off, True):
+    @staticmethod
+    def _mirror(sink, off, n):
+        if sink.mirror is not None:
+            _ops().fa_cast_rows(sink.mirror, sink.dst, sink.ld, sink.dst.shape[0], off, n)
+
+    def _conv3_wgrad(self, dy, x, G, sink, off, K, C):
+        if _ops().conv3x3_wgrad_rows(dy, x, G, sink.dst, sink.ld, off, True, sink.beta, sink.alpha,
+                                     sink.mirror):
             return
         col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
-        self._bmm_rows(Gg, off, _gview(dy, G).transpose(1, 2), col.transpose(0, 1))
+        self._bmm_rows(sink, off, _gview(dy, G).transpose(1, 2), col.transpose(0, 1))
 
     # ------------------------------------------------------------- round
     def run(self, w0: torch.Tensor, x: torch.Tensor, y: torch.Tensor, G: int, n: int, bs: int,
@@ -209,7 +238,15 @@ class ResNet18FedAvg:
         ops.fa_gather_rows(w0i, w0b, w0, perm)
         Wg = torch.empty((G, ld), device=dev, dtype=torch.float32)
         Wb = torch.empty((G, ld), device=dev, dtype=torch.bfloat16)
-        Gg = torch.zeros((G, ld), device=dev, dtype=torch.float32)
+        # without clipping every weight-gradient producer applies the SGD step
+        # to the client rows in place (no gradient rows, no separate update
+        # pass); clipping needs each client's whole gradient norm first
+        fused = not clip
+        if fused:
+            ops.fa_bcast_rows(Wg, ld, w0i, G, d)
+            Gg = None
+        else:
+            Gg = torch.zeros((G, ld), device=dev, dtype=torch.float32)
         # per-client running statistics (the model keeps their mean)
         run = []
         for b in self.blocks:
@@ -234,11 +271,14 @@ class ResNet18FedAvg:
                     W, Wbf, sld = w0i, w0b, 0
                 else:
                     W, Wbf, sld = Wg, Wb, ld
-                l, c = self._step(xb, yb, G, s1 - s0, W, Wbf, sld, Gg, ld, run, nbt, ones)
+                lr_t = float(lr * decay ** steps)
+                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, Wb) if fused
+                        else _Sink(Gg, ld, 0.0, 1.0, None))
+                l, c = self._step(xb, yb, G, s1 - s0, W, Wbf, sld, sink, run, nbt, ones)
                 loss_acc += l
                 acc_acc += c
-                ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip or 0.0),
-                               float(lr * decay ** steps), float(wd), Wb)
+                if not fused:
+                    ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip), lr_t, float(wd), Wb)
                 steps += 1
         ops.fa_upload(out, w0i, Wg, ld, G, float(n), perm)
         # running statistics: per-client copies summed for the caller's mean
@@ -248,20 +288,21 @@ class ResNet18FedAvg:
                          rv1.view(G, -1).double().sum(0), rv2.view(G, -1).double().sum(0)))
         return loss_acc / steps, acc_acc / steps, sums
 
-    def _step(self, x, y, G, n, W, Wb, ld, Gg, gld, run, nbt, ones):
+    def _step(self, x, y, G, n, W, Wb, ld, sink, run, nbt, ones):
         """One local step of every client (fp32 rows W, bf16 mirror Wb, both
-        ld apart; ld 0 = the shared server row): forward, backward into Gg."""
+        ld apart; ld 0 = the shared server row): forward, then backward into
+        the sink (gradient rows, or the in-place SGD step)."""
         ops = _ops()
-        # ---- stem: grouped column image of the client-major input (its 3-channel
-        # weight stays in PyTorch's order: a small padded column image)
+        # ---- stem: grouped column image of the client-major input (9 C0 = 27
+        # columns padded to 32; the GEMMs read the first 27)
         C0, K0 = self.cin0, self.c0
         Kc0 = (9 * C0 + 7) // 8 * 8
         col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        col0g = col0.transpose(0, 1)[:, :, :9 * C0]
         H, Wd = x.shape[2], x.shape[3]
         y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
                          memory_format=torch.channels_last)
-        w0img = ops.fa_weight_image(W, ld, G, self.prep, K0, C0, 3, Kc0, 2)
-        torch.bmm(col0.transpose(0, 1), w0img.transpose(1, 2), out=_gview(y0, G))
+        torch.bmm(col0g, self._rows(Wb, ld, G, self.prep, K0, 9 * C0).transpose(1, 2), out=_gview(y0, G))
         a = ops.fa_ew(y0, None, 1)
         a0 = a
         saved = []
@@ -302,24 +343,29 @@ class ResNet18FedAvg:
         loss, correct, gl = ops.ce_fwd(logits.view(G * n, self.ncls), y)
         gl = gl.view(G, n, self.ncls)
         inv = 1.0 / n
-        gW = Gg[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
-        torch.baddbmm(gW, gl.transpose(1, 2), feat, beta=0.0, alpha=inv, out=gW)
-        gb = Gg[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
-        torch.baddbmm(gb, ones[:, :n].transpose(1, 2), gl, beta=0.0, alpha=inv, out=gb)
+        # (the feature gradient first: the classifier rows may be updated in place next)
         dfeat = torch.empty_like(feat)
         torch.baddbmm(dfeat, gl, Wfc, beta=0.0, alpha=inv, out=dfeat)
+        gW = sink.dst[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
+        torch.baddbmm(gW, gl.transpose(1, 2), feat, beta=sink.beta, alpha=sink.alpha * inv, out=gW)
+        gb = sink.dst[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
+        torch.baddbmm(gb, ones[:, :n].transpose(1, 2), gl, beta=sink.beta, alpha=sink.alpha * inv, out=gb)
         da = ops.fa_head_bwd(dfeat, codes, a.shape[2], a.shape[3])
         # ---- blocks, last to first
         for bi in range(len(self.blocks) - 1, -1, -1):
             b = self.blocks[bi]
             xin, colx, h1, st1, bits1, a1, h2, st2, bits2 = saved[bi]
-            dh2 = ops.cs_bn_bwd(da, h2, st2, bits2, W, ld, b.bn2w, G, Gg, gld, b.bn2w, b.bn2b)
+            dh2 = ops.cs_bn_bwd(da, h2, st2, bits2, W, ld, b.bn2w, G, sink.dst, sink.ld, b.bn2w, b.bn2b,
+                                sink.beta, sink.alpha)
+            # (each conv's input gradient reads its weights before the weight
+            # gradient's producer may update them in place)
             da1 = self._conv3_dgrad(dh2, Wb, ld, G, b.conv2, b.cout, b.cout)
-            self._conv3_wgrad(dh2, a1, G, Gg, gld, b.conv2, b.cout, b.cout)
-            dh1 = ops.cs_bn_bwd(da1, h1, st1, bits1, W, ld, b.bn1w, G, Gg, gld, b.bn1w, b.bn1b)
+            self._conv3_wgrad(dh2, a1, G, sink, b.conv2, b.cout, b.cout)
+            dh1 = ops.cs_bn_bwd(da1, h1, st1, bits1, W, ld, b.bn1w, G, sink.dst, sink.ld, b.bn1w, b.bn1b,
+                                sink.beta, sink.alpha)
             if b.stride == 1:
                 dx = self._conv3_dgrad(dh1, Wb, ld, G, b.conv1, b.cout, b.cin)
-                self._conv3_wgrad(dh1, xin, G, Gg, gld, b.conv1, b.cout, b.cin)
+                self._conv3_wgrad(dh1, xin, G, sink, b.conv1, b.cout, b.cin)
                 da = ops.fa_ew(dx, da, 0)
             else:
                 nn_, _, Hi, Wi = xin.shape
@@ -330,11 +376,10 @@ class ResNet18FedAvg:
                 dctr = dcg[:, :, 4 * b.cin:5 * b.cin]
                 torch.baddbmm(dctr, _gview(da, G), self._rows(Wb, ld, G, b.sc, b.cout, b.cin), out=dctr)
                 cg = colx.transpose(0, 1)
-                self._bmm_rows(Gg, b.conv1, _gview(dh1, G).transpose(1, 2), cg)
-                self._bmm_rows(Gg, b.sc, _gview(da, G).transpose(1, 2), cg[:, :, 4 * b.cin:5 * b.cin])
+                self._bmm_rows(sink, b.conv1, _gview(dh1, G).transpose(1, 2), cg)
+                self._bmm_rows(sink, b.sc, _gview(da, G).transpose(1, 2), cg[:, :, 4 * b.cin:5 * b.cin])
                 da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)
-        part = torch.bmm(_gview(dy0, G).transpose(1, 2), col0.transpose(0, 1), out_dtype=torch.float32)
-        ops.wgrad_rsc_add(Gg[:, self.prep:self.prep + K0 * C0 * 9].view(G, K0, C0 * 9), part, 1, C0, 9, False)
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
