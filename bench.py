@@ -126,8 +126,11 @@ def main():
         fopt.step()
         return out
 
+    warm_host = []
     for i in range(b.warmup):
+        h0 = time.perf_counter()
         out = step(i)
+        warm_host.append(round((time.perf_counter() - h0) * 1000.0, 2))
         if b.check_every and N > 1 and (i + 1) % b.check_every == 0:
             dist.check_replicas(fed.w)
     # no host bookkeeping between the warmup and the timed rounds: the values
@@ -135,8 +138,11 @@ def main():
     # idles only for the synchronize / barrier round trip (an idle GPU drops
     # its clock, and the first timed rounds then run slower)
     tw = time.perf_counter()  # end of the warmup enqueue
-    first_loss_t = out[0].mean().clone()
-    dl_before_t = fed.accountant.client_download.sum().clone()
+    # (plain copies: a reduction kernel used for the first time here would be
+    # loaded from the code object now -- ~20 ms of GPU idle before the timed
+    # rounds; the means / sums are taken after the timed region)
+    first_loss_t = out[0].clone()
+    dl_before_t = fed.accountant.client_download.clone()
     if fed.timer.enabled:
         fed.timer.discard()
     torch.cuda.synchronize()
@@ -167,9 +173,9 @@ def main():
     if b.check_every:
         # the replicated weights must be bitwise identical on every rank
         checksum = dist.check_replicas(fed.w)
-    first_loss = float(first_loss_t.item())
+    first_loss = float(first_loss_t.mean().item())
     last_loss = float(out[0].mean().item())
-    dl = (float(fed.accountant.client_download.sum().item()) - float(dl_before_t.item())) / b.steps
+    dl = (float(fed.accountant.client_download.sum().item()) - float(dl_before_t.sum().item())) / b.steps
     if b.torch_profile:
         from torch.profiler import ProfilerActivity, profile
         stack = bool(os.environ.get("COMMEFF_PROF_STACK"))
@@ -226,6 +232,7 @@ def main():
             # host time from the last warmup enqueue to the first timed one
             # (includes the GPU draining the queued warmup rounds)
             "warmup_to_timed_ms": round((t0 - tw) * 1000.0, 3),
+            "warmup_host_ms": warm_host,
             **({"round_ms": [round(evs[i].elapsed_time(evs[i + 1]), 3) for i in range(len(evs) - 1)]}
                if evs else {}),
         }), flush=True)
