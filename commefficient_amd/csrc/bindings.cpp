@@ -1671,6 +1671,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ce_fwd_hip(const at::Tensor& logi
   return {loss, correct, grad};
 }
 
+// g [B, C] (bf16 / f32, contiguous) *= s [B] row by row, in place
+void scale_rows_hip(at::Tensor g, const at::Tensor& s) {
+  TORCH_CHECK(g.dim() == 2 && g.is_contiguous() &&
+                  (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat),
+              "scale_rows: g must be contiguous bf16/f32 [B, C]");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.is_contiguous() && s.numel() == g.size(0) &&
+                  s.device() == g.device(),
+              "scale_rows: s must be contiguous f32 [B]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  launch_scale_rows(g.data_ptr(), g.scalar_type() == at::kBFloat16, s.data_ptr<float>(), g.size(0),
+                    static_cast<int>(g.size(1)), cur_stream());
+}
+
 // residual unit tail: out = relu(conv3x3(x, w)) + addend, and pre = relu(conv3x3(x, w))
 std::tuple<at::Tensor, at::Tensor> conv3x3_relu_add_hip(const at::Tensor& x, const at::Tensor& w,
                                                         const at::Tensor& addend) {
@@ -2386,6 +2399,7 @@ TORCH_LIBRARY(commeff, m) {
         "float scale, Tensor(a!) dw, float beta, Tensor ymask) -> (Tensor, Tensor)");
   m.def("conv3x3_relu_add(Tensor x, Tensor w, Tensor addend) -> (Tensor, Tensor)");
   m.def("ce_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor, Tensor)");
+  m.def("scale_rows(Tensor(a!) g, Tensor s) -> ()");
   m.def("client_means(Tensor(a!) out, Tensor[] rows, Tensor slot, Tensor counts) -> ()");
   m.def("ghost_bn_fwd(Tensor x, Tensor? w, Tensor? b, int G, float eps, float momentum, Tensor(a!)? run_mean, "
         "Tensor(b!)? run_var, bool relu=False, Tensor(c!)? num_batches_tracked=None, Tensor? addend=None, "
@@ -2524,6 +2538,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("head_bwd_dual", &head_bwd_dual_hip);
   m.impl("conv3x3_relu_add", &conv3x3_relu_add_hip);
   m.impl("ce_fwd", &ce_fwd_hip);
+  m.impl("scale_rows", &scale_rows_hip);
   m.impl("client_means", &client_means_hip);
   m.impl("ghost_bn_fwd", &ghost_bn_fwd_hip);
   m.impl("ghost_bn_bwd", &ghost_bn_bwd_hip);

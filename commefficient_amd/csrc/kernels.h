@@ -423,6 +423,7 @@ struct ClientMeanRows {
 };
 void launch_client_means(const ClientMeanRows& rows, const int64_t* slot, int n, const void* counts,
                          bool counts_f32, int W, float* out, hipStream_t stream);
+void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, hipStream_t stream);
 void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
                    float* correct, void* grad, hipStream_t stream);
 

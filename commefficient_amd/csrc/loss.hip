@@ -3,7 +3,9 @@
 // its logits row, the per-example loss lse(x) - x[t], top-1 correctness
 // (argmax with ties to the lower index, like torch.argmax) and the unit
 // gradient softmax(x) - onehot(t) (scaled by dL/dloss in backward).  Replaces
-// log_softmax / nll / argmax / eq / cast kernels forward and backward.
+// log_softmax / nll / argmax / eq / cast kernels forward and backward.  Rows
+// whose target is outside [0, C) (the LM's ignore label -100) get zero loss and
+// gradient: the GPT-2 LM loss at the labelled positions (train/losses.py).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "kernels.h"
@@ -50,6 +52,15 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ x,
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
   const T* xr = x + row * C;
+  const int64_t t = tgt[row];
+  if (t < 0 || t >= C) {  // ignored row (label -100): zero loss and gradient
+    if (lane == 0) {
+      loss[row] = 0.f;
+      correct[row] = 0.f;
+    }
+    for (int j = lane; j < C; j += 64) st<T>(grad, row * C + j, 0.f);
+    return;
+  }
   // max and its first index
   float m = -__builtin_huge_valf();
   int mi = C;
@@ -67,7 +78,6 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ x,
   for (int j = lane; j < C; j += 64) s += __expf(ld<T>(xr, j) - m);
   s = wave_sum(s);
   const float lse = m + __logf(s);
-  const int64_t t = tgt[row];
   if (lane == 0) {
     loss[row] = lse - ld<T>(xr, t);
     correct[row] = mi == t ? 1.f : 0.f;
@@ -79,7 +89,29 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ x,
   }
 }
 
+// g[r][j] *= s[r] (the CE backward: the unit gradient scaled by dL/dloss), one
+// wave per row
+template <typename T>
+__global__ void __launch_bounds__(256) scale_rows_kernel(T* __restrict__ g, const float* __restrict__ s,
+                                                         int64_t B, int C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float f = s[row];
+  T* gr = g + row * C;
+  for (int j = lane; j < C; j += 64) st<T>(gr, j, ld<T>(gr, j) * f);
+}
+
 }  // namespace
+
+void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, hipStream_t stream) {
+  if (B == 0) return;
+  const dim3 grid(static_cast<uint32_t>((B + 3) / 4));
+  if (bf16)
+    COMMEFF_LAUNCH(scale_rows_kernel<uint16_t>, grid, dim3(256), 0, stream, static_cast<uint16_t*>(g), s, B, C);
+  else
+    COMMEFF_LAUNCH(scale_rows_kernel<float>, grid, dim3(256), 0, stream, static_cast<float*>(g), s, B, C);
+}
 
 void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
                    float* correct, void* grad, hipStream_t stream) {

@@ -715,7 +715,9 @@ class _FusedCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gl, gc):
         (gunit,) = ctx.saved_tensors
-        return gunit * gl.unsqueeze(1).to(gunit.dtype), None
+        # the saved unit gradient is scaled in place (backward runs once)
+        _ops().scale_rows(gunit, gl.float().contiguous())
+        return gunit, None
 
 
 def cross_entropy_correct(logits: torch.Tensor, targets: torch.Tensor):

@@ -130,8 +130,14 @@ def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos,
     logits = _tx.lm_head(m, h)                                           # [B, R, V]
     tgt = torch.gather(lm_labels.reshape(B, C * L), 1, (p + 1).clamp_max(C * L - 1))
     tgt = torch.where(valid, tgt, torch.full_like(tgt, -100))
-    tok = F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), tgt.reshape(-1),
-                          ignore_index=-100, reduction="none").view(B, -1)
+    if logits.is_cuda:
+        # one native pass over the bf16 logits: loss, and the unit gradient for
+        # backward (rows labelled -100: zero), no fp32 copy of the logits
+        tok = cross_entropy_correct(logits.reshape(-1, logits.shape[-1]),
+                                    tgt.reshape(-1).contiguous())[0].view(B, -1)
+    else:
+        tok = F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), tgt.reshape(-1),
+                              ignore_index=-100, reduction="none").view(B, -1)
     mask = (tgt != -100).float()
     return (tok * mask).sum(1), mask.sum(1), mc_logits
 

@@ -126,9 +126,9 @@ def _round0_rows(grouped: str, device: str, dtype: str):
     rows = []
     orig = FedModel._client_tail
 
-    def rec(self, g, work):
+    def rec(self, g, work, **kw):
         rows.append(g.detach().clone())
-        return orig(self, g, work)
+        return orig(self, g, work, **kw)
 
     FedModel._client_tail = rec
     try:

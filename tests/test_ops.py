@@ -2,6 +2,7 @@
 against the pure-torch oracles in tests/oracle.py."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 from commefficient_amd import ops
 from commefficient_amd.ops import CSVec, make_hashes
@@ -478,3 +479,27 @@ def test_client_tail_matches_composition(device, has_w, has_u, has_e):
         torch.testing.assert_close(e2.double(), ref_e, rtol=1e-6, atol=1e-5)
     if not has_u and not has_e:
         torch.testing.assert_close(g2.double(), ref_g, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_fused_ce_ignore_rows_and_backward(dtype):
+    """The GPT-2 LM loss at the labelled positions (train/losses.py): rows
+    labelled -100 get zero loss and gradient; backward scales the unit
+    gradient row by row in place (csrc/loss.hip scale_rows)."""
+    from commefficient_amd.ops.nn import cross_entropy_correct
+    torch.manual_seed(0)
+    V = 50257
+    logits = (torch.randn(7, V, device="cuda") * 3).to(dtype)
+    tgt = torch.tensor([5, -100, 50256, 0, -100, 123, 4000], device="cuda")
+    x = logits.clone().requires_grad_(True)
+    loss, _ = cross_entropy_correct(x, tgt)
+    w = torch.randn(7, device="cuda")
+    (loss * w).sum().backward()
+    xr = logits.float().clone().requires_grad_(True)
+    ref = F.cross_entropy(xr, tgt, ignore_index=-100, reduction="none")
+    (ref * w).sum().backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=tol, atol=tol * 1e-2)
+    assert x.grad[1].abs().max() == 0 and x.grad[4].abs().max() == 0
