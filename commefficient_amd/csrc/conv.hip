@@ -876,6 +876,10 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
   const int tile = bid % ntiles, split = bid / ntiles;
   const int tc = tile % ntc, rs = (tile / ntc) % NTAPG, tk = tile / (ntc * NTAPG);
   const int k0 = tk * 256, c0 = tc * CPT;
+  // grouped (channel-stacked) x: pixel row stride and this tile's channel
+  // group (kg % 256 == 0: a 256-row tile is one group's output channels)
+  const int xs = a.x_stride > 0 ? a.x_stride : C;
+  const int cofs = a.kg > 0 ? (k0 / a.kg) * C : 0;
   int pbeg, pend;
   wgrad_split_range(a, split, &pbeg, &pend);
   const int nsteps = pend > pbeg ? (pend - pbeg + BK - 1) / BK : 0;
@@ -903,7 +907,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
     const uint32_t q = fdiv(static_cast<uint32_t>(p), a.div_w);
     b_w[i] = p - static_cast<int>(q) * W;
     b_h[i] = static_cast<int>(q - fdiv(q, a.div_h) * H) + b_dr[i];
-    b_ptr[i] = reinterpret_cast<uint64_t>(a.x + static_cast<int64_t>(p + b_dr[i] * W + b_ds[i]) * C + cc);
+    b_ptr[i] = reinterpret_cast<uint64_t>(a.x + static_cast<int64_t>(p + b_dr[i] * W + b_ds[i]) * xs + cofs + cc);
     if (real && static_cast<unsigned>(b_w[i] + b_ds[i]) < static_cast<unsigned>(W)) b_ok |= 1u << i;
     if (!ROWSTEP && real) b_ok |= 16u << i;  // (recomputed per step below)
   }
@@ -927,7 +931,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
       glds16(reinterpret_cast<const void*>(ok ? b_ptr[i] : zero),
              base + A_BYTES + (i >> 1) * HALF + (i & 1) * 8192);
       b_row[i] += BK;
-      b_ptr[i] += static_cast<uint64_t>(BK) * C * 2;
+      b_ptr[i] += static_cast<uint64_t>(BK) * xs * 2;
       if constexpr (ROWSTEP) {
         const int nh = b_h[i] + dh;
         b_h[i] = nh - b_dr[i] >= H ? nh - H : nh;
@@ -1445,7 +1449,10 @@ void launch_wgrad(const ConvWgradArgs& a, hipStream_t stream) {
 // channel-stacked grouped wgrad: the halo kernel with its tile's input-channel
 // group (output tiles of WBM = 128 rows never straddle a group)
 bool conv3x3_wgrad_grouped_supported(int H, int W, int K, int C, int kg) {
-  return kg > 0 && kg % WBM == 0 && K % kg == 0 && C % 64 == 0 && wgrad_halo(H, W, K, C);
+  if (kg <= 0 || K % kg != 0 || C % 64 != 0) return false;
+  if (wgrad_halo(H, W, K, C)) return kg % WBM == 0;
+  // the wide kernel (any image width): its 256-row tiles must not straddle a group
+  return kg % 256 == 0 && wgrad_wide(K, C);
 }
 
 static int wgrad_slots();

@@ -827,7 +827,7 @@ class FedModel:
             pm.append(ms)
         loss = torch.cat(pl).mean()
         mets = [torch.cat([m[i] for m in pm]).mean() for i in range(len(pm[0]))]
-        self._client_tail(self.flat.g, work, defer_wd)
+        self._client_tail(self.flat.g, work, defer_wd=defer_wd)
         return loss, mets
 
     def _client_tail(self, g: torch.Tensor, work: torch.Tensor, defer_wd: bool = False):

@@ -257,10 +257,11 @@ def test_conv_rows_forward_and_dgrad_image(H, K, C):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G,C,K,H", [(2, 128, 128, 16), (4, 64, 64, 32)])
+@pytest.mark.parametrize("G,C,K,H", [(2, 128, 128, 16), (4, 64, 64, 32), (2, 256, 256, 8), (3, 256, 256, 4)])
 def test_conv3x3_wgrad_rows_rsc_order(G, C, K, H):
     """(64-channel clients: computed in pairs as 128-channel groups, the
-    diagonal blocks kept)"""
+    diagonal blocks kept; 8x8 / 4x4 images: the wide wgrad kernel with
+    channel-stacked groups)"""
     torch.manual_seed(0)
     n = 5
     x = _cs(torch.randn(G, n, C, H, H, device="cuda"), G)
