@@ -2227,11 +2227,11 @@ static at::Tensor gemm_tn_run(float* sink, int64_t ldc, int64_t cg, const at::Te
   // M: a multiple of 64, or any M whose A rows hold the 8-column chunk past
   // M (a padded buffer: the tied LM head's 50,257-row weight gradient)
   const bool m_ok = M % 64 == 0 || a.stride(0) >= (M + 7) / 8 * 8;
-  TORCH_CHECK(m_ok && N % 64 == 0 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+  TORCH_CHECK(m_ok && N % 8 == 0 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(sink) % 16 == 0 && ldc % 4 == 0 && cg % 4 == 0,
-              "gemm_tn_acc: M (or A's row stride) and N multiples of 64, 16-byte aligned rows");
+              "gemm_tn_acc: M (or A's row stride) a multiple of 64, N of 8, 16-byte aligned rows");
   TORCH_CHECK(a.size(0) < (1ll << 31) && M * N < (1ll << 31), "gemm_tn_acc: size");
   if (T == 0) return at::Tensor();
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());

@@ -37,19 +37,28 @@ __device__ __forceinline__ void gl16(const void* src, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-__global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
+// SMALL: a 128 x 128 tile per 4-wave block (2 x 2 waves of 64 x 64, one
+// [64][128] image per operand, 64 KB of LDS: two blocks per CU) for the
+// narrow weight gradients -- the ResNet-101 64 / 128-channel layers and the
+// 7x7 stem's [64 x 152] product -- whose 256 x 256 tiles would be mostly
+// padding; split-K over the (large) token / pixel count fills the chip.
+template <bool SMALL>
+__global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnArgs a) {
+  constexpr int NTH = SMALL ? 256 : 512, TILE = SMALL ? 128 : 256, NH = SMALL ? 1 : 2;
+  constexpr int NI = SMALL ? 2 : 4, WN = SMALL ? 64 : 128;  // wave tile: 64 x WN
+  constexpr int STG = 2 * NH * GHALF;                        // A + B images of one stage
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  // M, N multiples of 64: a partial edge tile loads zeros past M / N and
+  // M, N multiples of 8: a partial edge tile loads zeros past M / N and
   // stores only its valid part
-  const int ntn = (a.N + 255) / 256;
-  const int ntiles = ((a.M + 255) / 256) * ntn;
+  const int ntn = (a.N + TILE - 1) / TILE;
+  const int ntiles = ((a.M + TILE - 1) / TILE) * ntn;
   const int per_g = ntiles * a.splits;
   const int grp = bid / per_g, rem = bid - grp * per_g;
   const int tile = rem % ntiles, split = rem / ntiles;
-  const int m0 = (tile / ntn) * 256, n0 = (tile % ntn) * 256;
+  const int m0 = (tile / ntn) * TILE, n0 = (tile % ntn) * TILE;
   const int pbeg = split * a.steps_per_split * GBK;
   const int pend = min(a.T, pbeg + a.steps_per_split * GBK);
   // group grp: its own T operand rows and its own C (grouped weight gradients)
@@ -58,13 +67,13 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
   const int nsteps = pend > pbeg ? (pend - pbeg + GBK - 1) / GBK : 0;
   const uint64_t zero = reinterpret_cast<uint64_t>(g_gemm_zero);
 
-  // piece i (0..3) of this thread: image half i >> 1, chunk slot (i & 1) * 512 + tid
+  // piece i (0..3) of this thread: image half h, chunk slot sp of the half
   uint64_t a_ptr[4], b_ptr[4];
   int p_row[4];
   bool a_in[4], b_in[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int h = i >> 1, sp = (i & 1) * 512 + tid;
+    const int h = SMALL ? 0 : i >> 1, sp = SMALL ? i * NTH + tid : (i & 1) * 512 + tid;
     const int row = sp >> 4, lc = (sp & 15) ^ sw_tr256(row);
     p_row[i] = pbeg + row;
     a_in[i] = m0 + h * 128 + lc * 8 < a.M;
@@ -73,42 +82,43 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
     b_ptr[i] = reinterpret_cast<uint64_t>(gB + static_cast<int64_t>(pbeg + row) * a.ldb + n0 + h * 128 + lc * 8);
   }
   auto issue = [&](int stage) __attribute__((always_inline)) {
-    unsigned char* base = smem + stage * GSTAGE + wid * 1024;
+    unsigned char* base = smem + stage * STG + wid * 1024;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const bool ok = p_row[i] < pend;  // token rows past the split: zero page
-      gl16(reinterpret_cast<const void*>(ok && a_in[i] ? a_ptr[i] : zero), base + (i >> 1) * GHALF + (i & 1) * 8192);
-      gl16(reinterpret_cast<const void*>(ok && b_in[i] ? b_ptr[i] : zero),
-           base + 2 * GHALF + (i >> 1) * GHALF + (i & 1) * 8192);
+      // (lane-linear LDS destination of the wave's 64 chunks of slot sp)
+      const int dst = SMALL ? i * NTH * 16 : (i >> 1) * GHALF + (i & 1) * 8192;
+      gl16(reinterpret_cast<const void*>(ok && a_in[i] ? a_ptr[i] : zero), base + dst);
+      gl16(reinterpret_cast<const void*>(ok && b_in[i] ? b_ptr[i] : zero), base + NH * GHALF + dst);
       p_row[i] += GBK;
       a_ptr[i] += static_cast<uint64_t>(GBK) * a.lda * 2;
       b_ptr[i] += static_cast<uint64_t>(GBK) * a.ldb * 2;
     }
   };
 
-  f32x16_t acc[2][4];
+  f32x16_t acc[2][NI];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
 
   if (nsteps > 0) issue(0);
-  // transposed-read offsets: A columns m = wr*64 + mi*32 live in half wr >> 1,
-  // B columns wc*128 + ni*32 in half wc
-  int toA[2][2], toB[4][2];
+  // transposed-read offsets: A columns m = wr*64 + mi*32 (half wr >> 1 of the
+  // big tile), B columns wc*WN + ni*32 (half wc of the big tile)
+  int toA[2][2], toB[NI][2];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
-    tr_offsets<256>((wr & 1) * 64 + mi * 32, lane, toA[mi]);
-    toA[mi][0] += (wr >> 1) * GHALF;
-    toA[mi][1] += (wr >> 1) * GHALF;
+    tr_offsets<256>((SMALL ? wr : (wr & 1)) * 64 + mi * 32, lane, toA[mi]);
+    toA[mi][0] += (SMALL ? 0 : (wr >> 1)) * GHALF;
+    toA[mi][1] += (SMALL ? 0 : (wr >> 1)) * GHALF;
   }
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    tr_offsets<256>(ni * 32, lane, toB[ni]);
-    toB[ni][0] += 2 * GHALF + wc * GHALF;
-    toB[ni][1] += 2 * GHALF + wc * GHALF;
+  for (int ni = 0; ni < NI; ++ni) {
+    tr_offsets<256>((SMALL ? wc * 64 : 0) + ni * 32, lane, toB[ni]);
+    toB[ni][0] += NH * GHALF + (SMALL ? 0 : wc) * GHALF;
+    toB[ni][1] += NH * GHALF + (SMALL ? 0 : wc) * GHALF;
   }
   int rd = 0;
   for (int st = 0; st < nsteps; ++st) {
@@ -116,12 +126,12 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (st + 1 < nsteps) issue(rd ^ 1);
-    const unsigned char* sb = smem + rd * GSTAGE;
-    bf16x8_t af[2][2], bfr[2][4];
+    const unsigned char* sb = smem + rd * STG;
+    bf16x8_t af[2][2], bfr[2][NI];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) af[0][mi] = tr_read(sb + toA[mi][0], sb + toA[mi][1]);
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) bfr[0][ni] = tr_read(sb + toB[ni][0], sb + toB[ni][1]);
+    for (int ni = 0; ni < NI; ++ni) bfr[0][ni] = tr_read(sb + toB[ni][0], sb + toB[ni][1]);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int cur = kk & 1, nxt = cur ^ 1;
@@ -130,12 +140,12 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi) af[nxt][mi] = tr_read(sb + toA[mi][0] + dd, sb + toA[mi][1] + dd);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) bfr[nxt][ni] = tr_read(sb + toB[ni][0] + dd, sb + toB[ni][1] + dd);
+        for (int ni = 0; ni < NI; ++ni) bfr[nxt][ni] = tr_read(sb + toB[ni][0] + dd, sb + toB[ni][1] + dd);
       }
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
+        for (int ni = 0; ni < NI; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][mi], bfr[cur][ni], acc[mi][ni], 0, 0, 0);
     }
     rd ^= 1;
@@ -151,8 +161,8 @@ __global__ void __launch_bounds__(512) gemm_tn_acc_kernel(GemmTnArgs a) {
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + wc * 128 + ni * 32 + lr;
+    for (int ni = 0; ni < NI; ++ni) {
+      const int n = n0 + wc * WN + ni * 32 + lr;
       if (n >= a.N || m0 + wr * 64 + mi * 32 >= a.M) continue;  // padding of an edge tile
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -198,8 +208,13 @@ __global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__
 
 }  // namespace
 
+static bool tn_small(int M, int N) { return M % 256 != 0 || N % 256 != 0; }
+
 int gemm_tn_splits(int M, int N, int T, int cus) {
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  // (small tiles: two blocks per CU)
+  const int t = tn_small(M, N) ? 128 : 256;
+  if (t == 128) cus *= 2;
+  const int tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
   const int steps = (T + GBK - 1) / GBK;
   int s = (cus + tiles - 1) / tiles;  // ~ one block per CU
   const int max_s = steps / 4 > 0 ? steps / 4 : 1;  // >= 4 K-steps per split
@@ -212,16 +227,24 @@ void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream) {
   if (a.M == 0 || a.N == 0 || a.T == 0) return;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_tn_acc_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_tn_acc_kernel<false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_tn_acc_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds / 2);
     attr = true;
   }
   const int steps = (a.T + GBK - 1) / GBK;
   a.steps_per_split = (steps + a.splits - 1) / a.splits;
-  const int tiles = ((a.M + 255) / 256) * ((a.N + 255) / 256);
+  const bool small = tn_small(a.M, a.N);
+  const int t = small ? 128 : 256;
+  const int tiles = ((a.M + t - 1) / t) * ((a.N + t - 1) / t);
   if (a.G < 1) a.G = 1;
-  COMMEFF_LAUNCH(gemm_tn_acc_kernel, dim3(static_cast<uint32_t>(tiles * a.splits * a.G)), dim3(512),
-                     kGemmLds, stream, a);
+  if (small)
+    COMMEFF_LAUNCH(gemm_tn_acc_kernel<true>, dim3(static_cast<uint32_t>(tiles * a.splits * a.G)), dim3(256),
+                   kGemmLds / 2, stream, a);
+  else
+    COMMEFF_LAUNCH(gemm_tn_acc_kernel<false>, dim3(static_cast<uint32_t>(tiles * a.splits * a.G)), dim3(512),
+                   kGemmLds, stream, a);
   if (a.splits > 1 && !a.slab_only) {
     const int64_t n4 = static_cast<int64_t>(a.G) * a.M * a.N / 4;
     int64_t blocks = (n4 + 255) / 256;

@@ -859,6 +859,9 @@ def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
     P, K = g2d.shape
     C = x2d.shape[1]
     Pg = P // G
+    if _TN_1X1 and _wgrad_tn_ok(g2d, x2d, None, G):
+        # the native split-K TN GEMM's slabs (csrc/gemm_tn.hip, slab-only)
+        return _ops().gemm_tn_parts(g2d, x2d, G)
     S = _wgrad_splits(Pg, K, C, G)
     if G * S == 1:
         return torch.mm(g2d.t(), x2d, out_dtype=torch.float32).unsqueeze(0), 1
@@ -872,16 +875,15 @@ def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
 _TN_1X1 = True
 
 
-def _wgrad_tn_ok(g2d: torch.Tensor, x2d: torch.Tensor, into, G: int, pad: bool = False) -> bool:
-    """csrc/gemm_tn.hip serves the weight gradient: both sides multiples of
-    256 (its tile; with ``pad`` multiples of 64, the edge tiles zero-padded --
-    measured slower than hipBLASLt's 64-wide tiles at the ResNet-101 64 / 128
-    channel shapes), bf16 rows with unit column stride, 16-byte aligned;
-    ``into`` fp32 with 16-byte aligned rows (or absent)."""
+def _wgrad_tn_ok(g2d: torch.Tensor, x2d: torch.Tensor, into, G: int) -> bool:
+    """csrc/gemm_tn.hip serves the weight gradient: K a multiple of 64 and C
+    of 8 (256-multiples on its 256 x 256 tiles, the narrow 64 / 128-channel
+    layers and the stem's 152 column-image columns on its 128 x 128 tiles),
+    bf16 rows with unit column stride, 16-byte aligned; ``into`` fp32 with
+    16-byte aligned rows (or absent)."""
     P, K = g2d.shape
     C = x2d.shape[1]
-    q = 64 if pad else 256
-    if not (_GEMM_NATIVE[0] and g2d.is_cuda and K % q == 0 and C % q == 0 and P % G == 0
+    if not (_GEMM_NATIVE[0] and g2d.is_cuda and K % 64 == 0 and C % 8 == 0 and P % G == 0
             and g2d.dtype == torch.bfloat16 and x2d.dtype == torch.bfloat16
             and g2d.stride(1) == 1 and x2d.stride(1) == 1 and g2d.stride(0) % 8 == 0
             and x2d.stride(0) % 8 == 0 and g2d.data_ptr() % 16 == 0 and x2d.data_ptr() % 16 == 0):

@@ -94,7 +94,7 @@ def test_gemm_cpu_reference_semantics():
 @pytest.mark.gpu
 @pytest.mark.parametrize("G,T,M,N", [(3, 640, 256, 512), (8, 1568, 512, 256), (1, 6272, 1024, 256),
                                      (2, 130, 256, 256), (4, 3136, 64, 256), (2, 700, 64, 64),
-                                     (1, 900, 320, 128)])
+                                     (1, 900, 320, 128), (2, 5000, 64, 152), (3, 2000, 128, 72)])
 def test_gemm_tn_grouped_vs_fp32(G, T, M, N):
     """csrc/gemm_tn.hip with G groups of T rows in one launch: sink[g] +=
     a_g^T b_g (the per-client 1x1-conv weight gradients), group rows strided
@@ -137,7 +137,8 @@ def test_1x1_wgrad_native_route(G):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G,T,M,N", [(8, 784, 128, 1152), (1, 3000, 64, 576), (2, 196, 512, 4608)])
+@pytest.mark.parametrize("G,T,M,N", [(8, 784, 128, 1152), (1, 3000, 64, 576), (2, 196, 512, 4608),
+                                     (8, 12544, 64, 152)])
 def test_gemm_tn_parts_sum_to_product(G, T, M, N):
     """gemm_tn_parts: the unsummed split products of each group (the column-
     image weight gradients' parts, ops/nn.py _wgrad_parts) add up to a_g^T b_g."""
