@@ -89,6 +89,69 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ x,
   }
 }
 
+// Large vocabularies (the GPT-2 LM head, C = 50,257): one 256-thread block per
+// row, an online max / sum pass (running max with rescaled sum, first argmax)
+// reduced over the block in a fixed tree, then the gradient pass -- two passes
+// over the row instead of three, 4x the lanes of the one-wave kernel.
+template <typename T>
+__global__ void __launch_bounds__(256) ce_fwd_row_kernel(const T* __restrict__ x,
+                                                         const int64_t* __restrict__ tgt, int C,
+                                                         float* __restrict__ loss,
+                                                         float* __restrict__ correct,
+                                                         T* __restrict__ grad) {
+  __shared__ float sm[256], ss[256];
+  __shared__ int si[256];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const T* xr = x + row * C;
+  T* gr = grad + row * C;
+  const int64_t t = tgt[row];
+  if (t < 0 || t >= C) {  // ignored row (label -100): zero loss and gradient
+    if (tid == 0) {
+      loss[row] = 0.f;
+      correct[row] = 0.f;
+    }
+    for (int j = tid; j < C; j += 256) st<T>(gr, j, 0.f);
+    return;
+  }
+  float m = -__builtin_huge_valf(), sum = 0.f;
+  int mi = C;
+  for (int j = tid; j < C; j += 256) {
+    const float v = ld<T>(xr, j);
+    if (v > m) {
+      sum = sum * __expf(m - v) + 1.f;
+      m = v;
+      mi = j;
+    } else {
+      sum += __expf(v - m);
+    }
+  }
+  sm[tid] = m;
+  ss[tid] = sum;
+  si[tid] = mi;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const float m1 = sm[tid], m2 = sm[tid + o];
+      const float mm = fmaxf(m1, m2);
+      const float s1 = m1 == -__builtin_huge_valf() ? 0.f : ss[tid] * __expf(m1 - mm);
+      const float s2 = m2 == -__builtin_huge_valf() ? 0.f : ss[tid + o] * __expf(m2 - mm);
+      const int i1 = si[tid], i2 = si[tid + o];
+      si[tid] = (m2 > m1 || (m2 == m1 && i2 < i1)) ? i2 : i1;
+      sm[tid] = mm;
+      ss[tid] = s1 + s2;
+    }
+    __syncthreads();
+  }
+  const float mx = sm[0], tot = ss[0];
+  if (tid == 0) {
+    loss[row] = mx + __logf(tot) - ld<T>(xr, t);
+    correct[row] = si[0] == t ? 1.f : 0.f;
+  }
+  const float inv = 1.f / tot;
+  for (int j = tid; j < C; j += 256) st<T>(gr, j, __expf(ld<T>(xr, j) - mx) * inv - (j == t ? 1.f : 0.f));
+}
+
 // g[r][j] *= s[r] (the CE backward: the unit gradient scaled by dL/dloss), one
 // wave per row
 template <typename T>
@@ -102,10 +165,27 @@ __global__ void __launch_bounds__(256) scale_rows_kernel(T* __restrict__ g, cons
   for (int j = lane; j < C; j += 64) st<T>(gr, j, ld<T>(gr, j) * f);
 }
 
+template <typename T>
+__global__ void __launch_bounds__(256) scale_row_block_kernel(T* __restrict__ g, const float* __restrict__ s, int C) {
+  const int64_t row = blockIdx.x;
+  const float f = s[row];
+  T* gr = g + row * C;
+  for (int j = threadIdx.x; j < C; j += 256) st<T>(gr, j, ld<T>(gr, j) * f);
+}
+
 }  // namespace
 
 void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, hipStream_t stream) {
   if (B == 0) return;
+  if (C > 4096) {  // a block per (long) row
+    if (bf16)
+      COMMEFF_LAUNCH(scale_row_block_kernel<uint16_t>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
+                     static_cast<uint16_t*>(g), s, C);
+    else
+      COMMEFF_LAUNCH(scale_row_block_kernel<float>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
+                     static_cast<float*>(g), s, C);
+    return;
+  }
   const dim3 grid(static_cast<uint32_t>((B + 3) / 4));
   if (bf16)
     COMMEFF_LAUNCH(scale_rows_kernel<uint16_t>, grid, dim3(256), 0, stream, static_cast<uint16_t*>(g), s, B, C);
@@ -116,6 +196,15 @@ void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, hip
 void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
                    float* correct, void* grad, hipStream_t stream) {
   if (B == 0) return;
+  if (C > 4096) {
+    if (bf16)
+      COMMEFF_LAUNCH(ce_fwd_row_kernel<uint16_t>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
+                     static_cast<const uint16_t*>(x), tgt, C, loss, correct, static_cast<uint16_t*>(grad));
+    else
+      COMMEFF_LAUNCH(ce_fwd_row_kernel<float>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
+                     static_cast<const float*>(x), tgt, C, loss, correct, static_cast<float*>(grad));
+    return;
+  }
   const dim3 grid(static_cast<uint32_t>((B + 3) / 4));
   if (bf16)
     COMMEFF_LAUNCH(ce_fwd_kernel<uint16_t>, grid, dim3(256), 0, stream,

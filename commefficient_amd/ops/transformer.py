@@ -336,6 +336,61 @@ def _wgrad(sink, a, b):
 
 
 # ---------------------------------------------------------------- autograd
+_EMB_WS: Dict = {}  # (device, V, H) -> the embedding backward's fixed-point workspace
+
+
+def _emb_ws(device, V: int, H: int):
+    key = (str(device), V, H)
+    ws = _EMB_WS.get(key)
+    if ws is None:
+        # zero once; every backward leaves the rows it touched zeroed again
+        ws = (torch.zeros(V * H, dtype=torch.int64, device=device),
+              torch.zeros(V, dtype=torch.int32, device=device),
+              torch.zeros(V + 1, dtype=torch.int32, device=device))
+        _EMB_WS[key] = ws
+    return ws
+
+
+class _Embed(torch.autograd.Function):
+    """e = wte[ids] + wpe[pos] (+ wte[token types]) on the real token rows
+    (csrc/embed.hip): one gather-add kernel forward; backward scatters the row
+    gradients into the token and position tables' fp32 gradients with
+    fixed-point integer atomics -- order-independent, hence deterministic,
+    without PyTorch's sort + sum_and_scatter (HF GPT2Model.forward,
+    gpt2_train.py:55-99)."""
+
+    @staticmethod
+    def forward(ctx, wte, wpe, ids, tt, tok, L):
+        out = _ops().embed_fwd(ids, tt, tok, L, wte, wpe)
+        ctx.save_for_backward(ids, tt, tok)
+        ctx.L = L
+        ctx.params = (wte, wpe)
+        ctx.sinks = (_sink(wte), _sink(wpe))
+        return out
+
+    @staticmethod
+    def backward(ctx, de):
+        ids, tt, tok = ctx.saved_tensors
+        de = de.to(torch.bfloat16).contiguous()
+        grads = []
+        for i, (w, sink) in enumerate(zip(ctx.params, ctx.sinks)):
+            if not ctx.needs_input_grad[i]:
+                grads.append(None)
+                continue
+            V, H = w.shape
+            dst = sink if sink is not None else torch.zeros(V, H, dtype=torch.float32, device=de.device)
+            acc, cnt, lst = _emb_ws(de.device, V, H)
+            _ops().embed_bwd(de, ids, tt, tok, ctx.L, i == 1, acc, cnt, lst, dst)
+            grads.append(None if sink is not None else dst.to(w.dtype))
+        return grads[0], grads[1], None, None, None, None
+
+
+def _embed_native_ok(tr, ids) -> bool:
+    wte, wpe = tr.wte.weight, tr.wpe.weight
+    return (ids.is_cuda and wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16
+            and wte.is_contiguous() and wpe.is_contiguous() and ids.dtype == torch.int64)
+
+
 class _EmbedLN(torch.autograd.Function):
     """h = drop(x); y = LN(h)."""
 
@@ -788,7 +843,11 @@ def gpt2_hidden(tr, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tens
         from ..parallel.dist import h2d
         se = h2d(se, ids.device)
         sstart, slen = se[:Nn], se[Nn:]
-    if tok is None:
+    if _embed_native_ok(tr, ids):
+        # one native gather-add (real token rows only) and its sort-free backward
+        tt_flat = token_type_ids.reshape(M).contiguous() if token_type_ids is not None else None
+        e = _Embed.apply(tr.wte.weight, tr.wpe.weight, ids.reshape(M).contiguous(), tt_flat, tok, L)
+    elif tok is None:
         pos = torch.arange(L, device=ids.device)
         e = (tr.wte(ids) + tr.wpe(pos)).reshape(M, H)
         if token_type_ids is not None:

@@ -117,6 +117,9 @@ def _double_heads(m, input_ids, token_type_ids, mc_token_ids, args, last_only=Fa
     return (out.logits[:, -1] if last_only else out.logits), out.mc_logits
 
 
+_NATIVE_LM_CE = [True]  # (tests compare against the stock cross-entropy)
+
+
 def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos, args=None,
                   lengths=None):
     """(per-example sum of LM token losses, labelled-token count, mc logits)
@@ -130,7 +133,7 @@ def _lm_at_labels(m, input_ids, mc_token_ids, lm_labels, token_type_ids, lm_pos,
     logits = _tx.lm_head(m, h)                                           # [B, R, V]
     tgt = torch.gather(lm_labels.reshape(B, C * L), 1, (p + 1).clamp_max(C * L - 1))
     tgt = torch.where(valid, tgt, torch.full_like(tgt, -100))
-    if logits.is_cuda:
+    if logits.is_cuda and _NATIVE_LM_CE[0]:
         # one native pass over the bf16 logits: loss, and the unit gradient for
         # backward (rows labelled -100: zero), no fp32 copy of the logits
         tok = cross_entropy_correct(logits.reshape(-1, logits.shape[-1]),

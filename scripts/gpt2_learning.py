@@ -102,7 +102,14 @@ def main():
     p.add_argument("--mode", default="sketch", choices=["sketch", "uncompressed", "true_topk"])
     p.add_argument("--out", default=None)
     p.add_argument("--device", default="cuda")
+    p.add_argument("--stock", action="store_true",
+                   help="HF embedding + F.cross_entropy instead of the native ones (A/B)")
     b = p.parse_args()
+    if b.stock:
+        from commefficient_amd.ops import transformer as tx
+        from commefficient_amd.train import losses
+        tx._embed_native_ok = lambda tr, ids: False
+        losses._NATIVE_LM_CE[0] = False
     extra = ["--mode", b.mode, "--local_momentum", "0", "--virtual_momentum", "0.9",
              "--lr_scale", str(b.lr)]
     if b.mode == "sketch":

@@ -152,8 +152,9 @@ def test_gpt2_fetchsgd_learns_bigram_text():
     text (``--synthetic_text bigram``: 1,024 tokens with 4 successors each,
     LM nll ln 50262 = 10.8 at init, ln 4 = 1.39 at the optimum) a mini GPT-2
     (2 layers x 256) with a 5 x 500,000 sketch and k = 50,000 brings the
-    validation LM nll down by more than 3 nats in 120 rounds of 8 clients
-    (curve: profiles/r4_gpt2_learning.jsonl)."""
+    validation LM nll down by more than 3 nats within 200 rounds of 8 clients
+    (curves: profiles/r4_gpt2_learning.jsonl, gpurun_out/r5g2learn: native
+    embedding + CE and the stock ones track each other within the noise)."""
     import importlib.util
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
                         "gpt2_learning.py")
@@ -163,12 +164,14 @@ def test_gpt2_fetchsgd_learns_bigram_text():
     extra = ["--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
              "--virtual_momentum", "0.9", "--num_rows", "5", "--num_cols", "500000", "--k", "50000",
              "--lr_scale", "0.3"]
-    rows = mod.curve(120, 40, extra, "mini", log=print)
+    rows = mod.curve(200, 20, extra, "mini", log=print)
     # (the validation nll at this constant LR moves by ~1 nat between
-    # evaluations -- 7.6 / 7.1 / 7.3 at rounds 40 / 80 / 120 on MI355X, 8.45 at
-    # 100 -- so the bound is on the best evaluation, with a looser one on the last)
-    first, last = rows[0]["val_nll"], rows[-1]["val_nll"]
+    # evaluations -- e.g. 8.55 / 7.09 / 7.22 / 8.20 / 6.95 at rounds 40-120 on
+    # MI355X -- so the bound is on the best evaluation, with a looser one on
+    # the mean of the last three)
+    first = rows[0]["val_nll"]
+    last = sum(r["val_nll"] for r in rows[-3:]) / 3
     best = min(r["val_nll"] for r in rows[1:])
     assert best < first - 3.0, rows
-    assert last < first - 2.0, rows
+    assert last < first - 2.5, rows
     assert rows[-1]["train_loss"] < rows[1]["train_loss"], rows

@@ -538,3 +538,52 @@ def test_lm_head_native_vs_fp32_gpu(sinked, monkeypatch):
         torch.testing.assert_close(sink - sink0, dw_ref, rtol=1e-3, atol=2e-2)
     else:
         assert rel(W.grad, dw_ref) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_tt,with_tok,sink", [(True, True, True), (True, False, False), (False, True, False)])
+def test_native_embedding_vs_fp32(with_tt, with_tok, sink):
+    """csrc/embed.hip: e = wte[ids] + wpe[t % L] (+ wte[tt]) on the real token
+    rows, and the sort-free fixed-point backward into the fp32 table
+    gradients (or the returned gradients), vs an fp32 index_add reference;
+    bitwise deterministic across runs."""
+    from commefficient_amd.ops import transformer as tx
+    torch.manual_seed(0)
+    V, P, H, N, L = 50257, 1024, 768, 6, 40
+    wte = (torch.randn(V, H, device="cuda") * 0.02).bfloat16().requires_grad_(True)
+    wpe = (torch.randn(P, H, device="cuda") * 0.02).bfloat16().requires_grad_(True)
+    ids = torch.randint(0, V, (N * L,), device="cuda")
+    ids[::7] = 13  # repeated tokens
+    tt = torch.randint(50254, 50257, (N * L,), device="cuda") if with_tt else None
+    lengths = torch.tensor([40, 33, 7, 40, 1, 25])
+    tok = tx.real_token_index(lengths, L, "cuda")[0] if with_tok else None
+    rows = tok.long() if tok is not None else torch.arange(N * L, device="cuda")
+    de = (torch.randn(rows.numel(), H, device="cuda")).bfloat16()
+
+    def run():
+        sinks = None
+        if sink:
+            gw, gp = torch.zeros(V, H, device="cuda"), torch.zeros(P, H, device="cuda")
+            sinks = {id(wte): gw, id(wpe): gp}
+        wte.grad = wpe.grad = None
+        with tx.grad_sinks(sinks):
+            e = tx._Embed.apply(wte, wpe, ids, tt, tok, L)
+        e.backward(de)
+        if sink:
+            return e, gw, gp
+        return e, wte.grad.float(), wpe.grad.float()
+
+    e, gw, gp = run()
+    ref = wte.detach().float()[ids[rows]] + wpe.detach().float()[rows % L]
+    if tt is not None:
+        ref = ref + wte.detach().float()[tt[rows]]
+    torch.testing.assert_close(e.float(), ref.bfloat16().float(), rtol=1e-2, atol=1e-3)
+    rgw = torch.zeros(V, H, device="cuda").index_add_(0, ids[rows], de.float())
+    if tt is not None:
+        rgw.index_add_(0, tt[rows], de.float())
+    rgp = torch.zeros(P, H, device="cuda").index_add_(0, rows % L, de.float())
+    tol = 1e-5 if sink else 2e-2  # (returned gradients are bf16)
+    torch.testing.assert_close(gw, rgw, rtol=tol, atol=tol)
+    torch.testing.assert_close(gp, rgp, rtol=tol, atol=tol)
+    e2, gw2, gp2 = run()  # deterministic, and the workspace was left zeroed
+    assert torch.equal(gw, gw2) and torch.equal(gp, gp2)
