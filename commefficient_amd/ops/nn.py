@@ -1097,8 +1097,12 @@ class _Conv3x3(torch.autograd.Function):
 
 
 def _col_width(C: int, R: int, S: int) -> int:
-    """Column-image row length: R*S*C rounded up to 8 (16-byte rows)."""
-    return -(-C * R * S // 8) * 8
+    """Column-image row length: R*S*C rounded up to 64 on the native GEMMs (a
+    whole number of their 64-deep K-steps: the 7x7 stem's 147 columns -> 192,
+    its forward then the native NT GEMM instead of hipBLASLt), else to 8
+    (16-byte rows)."""
+    q = 64 if _GEMM_NATIVE[0] else 8
+    return -(-C * R * S // q) * q
 
 
 def _col_image(weight: torch.Tensor, Kc: int) -> torch.Tensor:
