@@ -158,6 +158,7 @@ class ResNet18FedAvg:
     # ----------------------------------------------------------- convs
     def _conv3(self, x, Wb, ldb, G, off, K, C):
         """stride-1 3x3 conv of channel-stacked x with the clients' weights"""
+        # (4x4 maps too: the column-image GEMM measured slower here, 36.2 vs 35.8 ms)
         y = _ops().conv3x3_fwd_rows(x, Wb, G, off, ldb, K)
         if y.numel() == 0 and x.numel():  # no halo tiling: column image x weight rows
             col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
