@@ -750,10 +750,14 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu,
 }
 
 // channel block of the partial kernels: the largest power-of-two multiple of
-// 8 dividing C, at most 2048 (C / 8 lanes of 16 bytes x 256 / (C / 8) pixels)
-static int cs_channel_block(int C) {
+// 8 dividing C, at most 2048 (C / 8 lanes of 16 bytes x 256 / (C / 8) pixels),
+// halved (down to 64) while the S x C / CB grid has fewer than 1024 blocks --
+// the small maps of the deep layers (S = 1..5 slabs) otherwise ran 25..125
+// blocks walking every pixel serially (17.8 us per backward partial at 4x4)
+static int cs_channel_block(int C, int S) {
   int cb = 8;
   while (cb * 2 <= 2048 && C % (cb * 2) == 0) cb *= 2;
+  while (cb > 64 && static_cast<int64_t>(S) * (C / cb) < 1024) cb /= 2;
   return cb;
 }
 
@@ -763,7 +767,7 @@ void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t w
                       int M, int C, float eps, float momentum, float* run_mean, float* run_var,
                       int64_t* nbt, float* part, float* stat, float* ab, uint16_t* y, uint8_t* relu_bits,
                       const uint16_t* post_add, hipStream_t stream) {
-  const int S = bn_slabs(1, M), CB = cs_channel_block(C);
+  const int S = bn_slabs(1, M), CB = cs_channel_block(C, S);
   COMMEFF_LAUNCH(bn_partial_kernel<false>, dim3(S, C / CB), dim3(256), 0, stream, x, nullptr, nullptr,
                  nullptr, C, M, S, part, CB);
   COMMEFF_LAUNCH(bn_cs_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part, prm,
@@ -782,7 +786,7 @@ void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_re
                       const float* prm, int64_t ld, int64_t woff, int cg, int M, int C, float* part,
                       float* coef, float* grad, int64_t gld, int64_t gwoff, int64_t gboff, uint16_t* dx,
                       hipStream_t stream, float beta, float alpha) {
-  const int S = bn_slabs(1, M), CB = cs_channel_block(C);
+  const int S = bn_slabs(1, M), CB = cs_channel_block(C, S);
   COMMEFF_LAUNCH(bn_partial_kernel<true>, dim3(S, C / CB), dim3(256), 0, stream, x, dy, y_relu, stat, C,
                  M, S, part, CB);
   COMMEFF_LAUNCH(bn_cs_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat, prm,

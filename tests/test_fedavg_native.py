@@ -118,10 +118,10 @@ def test_im2col_grouped_three_channel_stem():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G,C,H", [(4, 64, 8), (100, 64, 4), (3, 256, 4)])
-def test_cs_bn_forward_backward(G, C, H):
+@pytest.mark.parametrize("G,C,H,n", [(4, 64, 8, 5), (100, 64, 4, 5), (3, 256, 4, 5), (100, 64, 32, 5),
+                                     (6, 512, 4, 2), (6, 512, 4, 1)])
+def test_cs_bn_forward_backward(G, C, H, n):
     torch.manual_seed(0)
-    n = 5
     X = torch.randn(G, n, C, H, H, device="cuda") * 2 + 0.5
     x = _cs(X, G)
     ld, woff, boff = 2 * C + 32, 8, C + 16
@@ -336,11 +336,16 @@ def test_native_round_matches_vmap_and_fp32(extra):
     # running statistics: the clients' mean (the batched semantics -- the
     # sequential path accumulates them client after client on one model), so
     # against the fp32 vmap round, within twice the bf16 vmap round's distance
+    # (as norms: with 1-image batches (extra2: 16 values per channel at 4x4) a
+    # single channel's variance follows the bf16 rounding of the steps before
+    # it chaotically -- max-abs distances of 0.6 (vmap) to 1.3 between two
+    # summation orders of the same BN kernel)
     _, _, b_vf, _ = _round(base, "vmap", "fp32", G, n, extra)
     for k in b_v:
         if "running" in k:
-            bn_noise = (b_v[k] - b_vf[k]).abs().max().item()
-            err = (b_n[k] - b_vf[k]).abs().max().item()
-            assert err <= 2 * bn_noise + 1e-2 * b_vf[k].abs().max().item() + 1e-3, (k, err, bn_noise)
+            ref = b_vf[k].norm().item()
+            bn_noise = (b_v[k] - b_vf[k]).norm().item() / ref
+            err = (b_n[k] - b_vf[k]).norm().item() / ref
+            assert err <= 2 * bn_noise + 1e-2, (k, err, bn_noise)
         elif "num_batches" in k:
             assert b_n[k] == b_v[k], k
