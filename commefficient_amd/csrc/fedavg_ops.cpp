@@ -455,9 +455,66 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
   return true;
 }
 
+// rows_g[off + k*N + j] = beta rows_g + alpha sum_p A[g][k][p] B[g][p][j] with
+// A [G, K, P] (unit stride along K: the channel-stacked output gradient seen
+// as [G, K, P]) and B [G, P, N] (unit stride along N: a grouped column image)
+// on the TN MFMA GEMM (gemm_tn.hip), the bf16 mirror of the updated rows
+// written in its epilogue -- hipBLASLt's baddbmm + a cast pass re-reading the
+// rows otherwise.  false (nothing written): a layout the kernel cannot read.
+bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64_t ld, int64_t off, double beta,
+                 double alpha, const c10::optional<at::Tensor>& mirror, int64_t small) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
+                  A.dim() == 3 && B.dim() == 3 && A.size(0) == B.size(0) && A.size(2) == B.size(1),
+              "fa_bmm_rows: A [G, K, P], B [G, P, N] bf16");
+  const int64_t G = A.size(0), K = A.size(1), P = A.size(2), N = B.size(2);
+  const auto a16 = [](const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
+  if (A.stride(1) != 1 || B.stride(2) != 1 || K % 8 || N % 8 || A.stride(2) % 8 || A.stride(0) % 8 ||
+      B.stride(1) % 8 || B.stride(0) % 8 || !a16(A) || !a16(B) || ld % 4 || off % 4)
+    return false;
+  check_rows(dst, ld, G, off, K * N, "fa_bmm_rows: dst");
+  TORCH_CHECK(ld > 0, "fa_bmm_rows: per-client rows");
+  uint16_t* mp = nullptr;
+  if (mirror.has_value() && mirror->defined()) {
+    TORCH_CHECK(mirror->is_cuda() && mirror->scalar_type() == at::kBFloat16 && mirror->is_contiguous() &&
+                    mirror->numel() >= dst.numel(),
+                "fa_bmm_rows: mirror bf16 like dst");
+    mp = reinterpret_cast<uint16_t*>(mirror->data_ptr()) + off;
+  }
+  TORCH_CHECK(P < (int64_t{1} << 31) && K * N < (int64_t{1} << 31), "fa_bmm_rows: size");
+  if (G == 0 || K == 0 || N == 0) return true;
+  if (P == 0) return false;  // (the launcher skips T = 0: the decay alone is the caller's)
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  GemmTnArgs g{};
+  g.A = bf(A);
+  g.lda = A.stride(2);
+  g.sa = A.stride(0);
+  g.B = bf(B);
+  g.ldb = B.stride(1);
+  g.sb = B.stride(0);
+  g.C = dst.data_ptr<float>() + off;
+  g.ldc = N;
+  g.cg = ld;
+  g.M = static_cast<int>(K);
+  g.N = static_cast<int>(N);
+  g.T = static_cast<int>(P);
+  g.G = static_cast<int>(G);
+  g.splits = 1;  // G clients x tiles: the chip is full without split-K
+  g.beta = static_cast<float>(beta);
+  g.alpha = static_cast<float>(alpha);
+  g.mirror = mp;
+  g.mcg = ld;
+  g.small = static_cast<int>(small);
+  g.stage = (small == 1 || small == -2) ? 1 : 0;
+  if (small == -2) g.small = 1;
+  launch_gemm_tn_acc(g, stream_now());
+  return true;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
+  m.def("fa_bmm_rows(Tensor A, Tensor B, Tensor(a!) dst, int ld, int off, float beta=1., float alpha=1., "
+        "Tensor(b!)? mirror=None, int small=-1) -> bool");
   m.def("fa_weight_image(Tensor W, int ld, int G, int off, int K, int C, int R, int Kc, int kind) -> Tensor");
   m.def("fa_row_sgd(Tensor(a!) W, int ld, Tensor src, int sld, Tensor G, int gld, int rows, int d, float clip, "
         "float lr, float wd, Tensor(b!)? Wb=None) -> ()");
@@ -483,6 +540,7 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("fa_weight_image", &fa_weight_image);
+  m.impl("fa_bmm_rows", &fa_bmm_rows);
   m.impl("fa_row_sgd", &fa_row_sgd);
   m.impl("fa_upload", &fa_upload);
   m.impl("fa_gather_rows", &fa_gather_rows);

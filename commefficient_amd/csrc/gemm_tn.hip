@@ -62,8 +62,10 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
   const int pbeg = split * a.steps_per_split * GBK;
   const int pend = min(a.T, pbeg + a.steps_per_split * GBK);
   // group grp: its own T operand rows and its own C (grouped weight gradients)
-  const uint16_t* __restrict__ gA = a.A + static_cast<int64_t>(grp) * a.T * a.lda;
-  const uint16_t* __restrict__ gB = a.B + static_cast<int64_t>(grp) * a.T * a.ldb;
+  // (sa / sb: the channel-stacked clients of parallel/fedavg_native.py share
+  // the token rows, each its column block)
+  const uint16_t* __restrict__ gA = a.A + grp * (a.sa >= 0 ? a.sa : static_cast<int64_t>(a.T) * a.lda);
+  const uint16_t* __restrict__ gB = a.B + grp * (a.sb >= 0 ? a.sb : static_cast<int64_t>(a.T) * a.ldb);
   const int nsteps = pend > pbeg ? (pend - pbeg + GBK - 1) / GBK : 0;
   const uint64_t zero = reinterpret_cast<uint64_t>(g_gemm_zero);
 
@@ -151,34 +153,123 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
     rd ^= 1;
   }
 
+  const bool direct = a.splits == 1 && !a.slab_only;
+  if (SMALL && direct && a.stage) {
+    // the 128 x 128 fp32 tile through the (drained) LDS ring, then streamed
+    // row-wise: a wave reads / writes two 512-byte rows of C per instruction
+    // (16 bytes a lane) and 256-byte rows of the mirror -- the MFMA layout
+    // stores 128-byte pieces 4 bytes a lane, with 2-byte mirror stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    float* tl = reinterpret_cast<float*>(smem);
+    {
+      const int hi = lane >> 5, lr = lane & 31;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int r = wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+            tl[r * 128 + wc * WN + ni * 32 + lr] = acc[mi][ni][e];
+          }
+    }
+    __syncthreads();
+    float* cb = a.C + static_cast<int64_t>(grp) * a.cg;
+    uint16_t* mb = a.mirror != nullptr ? a.mirror + static_cast<int64_t>(grp) * a.mcg : nullptr;
+    const bool plain = a.beta == 1.f && a.alpha == 1.f, rdc = plain || a.beta != 0.f;
+    const int c4 = tid & 31, r0 = tid >> 5;  // 8 rows per pass, 16 passes
+    const int n = n0 + c4 * 4;
+#pragma unroll
+    for (int pb = 0; pb < 16; pb += 4) {
+      float4 o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = m0 + (pb + q) * 8 + r0;
+        o[q] = rdc && m < a.M && n < a.N ? *reinterpret_cast<const float4*>(cb + static_cast<int64_t>(m) * a.ldc + n)
+                                         : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = (pb + q) * 8 + r0, m = m0 + r;
+        if (m >= a.M || n >= a.N) continue;
+        const float4 t = *reinterpret_cast<const float4*>(tl + r * 128 + c4 * 4);
+        float4 v;
+        if (plain) {
+          v = float4{o[q].x + t.x, o[q].y + t.y, o[q].z + t.z, o[q].w + t.w};
+        } else {
+          v = float4{a.beta * o[q].x + a.alpha * t.x, a.beta * o[q].y + a.alpha * t.y,
+                     a.beta * o[q].z + a.alpha * t.z, a.beta * o[q].w + a.alpha * t.w};
+        }
+        *reinterpret_cast<float4*>(cb + static_cast<int64_t>(m) * a.ldc + n) = v;
+        if (mb != nullptr) {
+          uint2 h;
+          h.x = pack_bf16(v.x, v.y);
+          h.y = pack_bf16(v.z, v.w);
+          *reinterpret_cast<uint2*>(mb + static_cast<int64_t>(m) * a.ldc + n) = h;
+        }
+      }
+    }
+    return;
+  }
   // C row m (lanes: 32 consecutive n) -- one split: accumulate into C; else
   // this split's slab [M][N]
   const int hi = lane >> 5, lr = lane & 31;
-  const bool direct = a.splits == 1 && !a.slab_only;
   float* out = direct ? a.C + static_cast<int64_t>(grp) * a.cg
                       : a.slab + static_cast<size_t>(grp * a.splits + split) * a.M * a.N;
   const int64_t ld = direct ? a.ldc : a.N;
+  // direct + mirror: the fused SGD step of the FedAvg engine (C = the weight
+  // rows, beta = 1 - lr wd, alpha = -lr) and the rows' bf16 copy, written here
+  // instead of by a cast pass re-reading C
+  uint16_t* mir = direct && a.mirror != nullptr ? a.mirror + static_cast<int64_t>(grp) * a.mcg : nullptr;
+  const bool plain = a.beta == 1.f && a.alpha == 1.f;
+  const bool rdc = direct && (plain || a.beta != 0.f);
+  // (batches of NB column blocks: 32 more registers in the 256 x 256 variant
+  // -- all NI of them spilled)
+  constexpr int NB = SMALL ? NI : 2;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < 2; ++mi) {
+    if (m0 + wr * 64 + mi * 32 >= a.M) continue;  // padding of an edge tile
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int n = n0 + wc * WN + ni * 32 + lr;
-      if (n >= a.N || m0 + wr * 64 + mi * 32 >= a.M) continue;  // padding of an edge tile
+    for (int nb = 0; nb < NI; nb += NB) {
+      // every C value of this batch loaded before its first store: the mirror
+      // (another base) may alias C as far as the compiler knows, and
+      // interleaved load / store pairs ran one HBM round trip at a time (378 us
+      // per FedAvg layer-3 weight update)
+      float old[NB][16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-        if (m >= a.M) continue;  // M not a multiple of 32 (the LM head's vocabulary)
-        float* p = out + static_cast<int64_t>(m) * ld + n;
-        if (direct) *p += acc[mi][ni][e];
-        else *p = acc[mi][ni][e];
+      for (int q = 0; q < NB; ++q) {
+        const int n = n0 + wc * WN + (nb + q) * 32 + lr;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+          old[q][e] = rdc && n < a.N && m < a.M ? out[static_cast<int64_t>(m) * ld + n] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int n = n0 + wc * WN + (nb + q) * 32 + lr;
+        if (n >= a.N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+          if (m >= a.M) continue;  // M not a multiple of 32 (the LM head's vocabulary)
+          const float c = acc[mi][nb + q][e];
+          const float v = !direct ? c : plain ? old[q][e] + c : a.beta * old[q][e] + a.alpha * c;
+          out[static_cast<int64_t>(m) * ld + n] = v;
+          if (mir != nullptr) mir[static_cast<int64_t>(m) * ld + n] = static_cast<uint16_t>(pack_bf16(v, 0.f));
+        }
       }
     }
+  }
 }
 
 // C_g[m][n] += sum over s of slab[g][s][m][n], s in order (float4 per thread)
 __global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__ C, int64_t ldc,
                                                              const float* __restrict__ slab, int M,
-                                                             int N, int splits, int G, int64_t cg) {
+                                                             int N, int splits, int G, int64_t cg,
+                                                             float beta, float alpha,
+                                                             uint16_t* __restrict__ mirror, int64_t mcg) {
   const int64_t plane = static_cast<int64_t>(M) * N;
   const int64_t n4 = G * plane / 4;
   for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < n4;
@@ -198,21 +289,33 @@ __global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__
     }
     float4* c = reinterpret_cast<float4*>(C + g * cg + static_cast<int64_t>(m) * ldc + n);
     float4 cv = *c;
-    cv.x += s.x;
-    cv.y += s.y;
-    cv.z += s.z;
-    cv.w += s.w;
+    if (beta == 1.f && alpha == 1.f) {
+      cv.x += s.x;
+      cv.y += s.y;
+      cv.z += s.z;
+      cv.w += s.w;
+    } else {
+      cv.x = (beta != 0.f ? beta * cv.x : 0.f) + alpha * s.x;
+      cv.y = (beta != 0.f ? beta * cv.y : 0.f) + alpha * s.y;
+      cv.z = (beta != 0.f ? beta * cv.z : 0.f) + alpha * s.z;
+      cv.w = (beta != 0.f ? beta * cv.w : 0.f) + alpha * s.w;
+    }
     *c = cv;
+    if (mirror != nullptr) {
+      uint32_t* mp = reinterpret_cast<uint32_t*>(mirror + g * mcg + static_cast<int64_t>(m) * ldc + n);
+      mp[0] = pack_bf16(cv.x, cv.y);
+      mp[1] = pack_bf16(cv.z, cv.w);
+    }
   }
 }
 
 }  // namespace
 
-static bool tn_small(int M, int N) { return M % 256 != 0 || N % 256 != 0; }
+static bool tn_small(int M, int N, int force = -1) { return force >= 0 ? force != 0 : M % 256 != 0 || N % 256 != 0; }
 
-int gemm_tn_splits(int M, int N, int T, int cus) {
+int gemm_tn_splits(int M, int N, int T, int cus, int small) {
   // (small tiles: two blocks per CU)
-  const int t = tn_small(M, N) ? 128 : 256;
+  const int t = tn_small(M, N, small) ? 128 : 256;
   if (t == 128) cus *= 2;
   const int tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
   const int steps = (T + GBK - 1) / GBK;
@@ -235,7 +338,7 @@ void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream) {
   }
   const int steps = (a.T + GBK - 1) / GBK;
   a.steps_per_split = (steps + a.splits - 1) / a.splits;
-  const bool small = tn_small(a.M, a.N);
+  const bool small = tn_small(a.M, a.N, a.small);
   const int t = small ? 128 : 256;
   const int tiles = ((a.M + t - 1) / t) * ((a.N + t - 1) / t);
   if (a.G < 1) a.G = 1;
@@ -250,7 +353,7 @@ void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream) {
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     COMMEFF_LAUNCH(gemm_tn_reduce_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
-                       a.C, a.ldc, a.slab, a.M, a.N, a.splits, a.G, a.cg);
+                       a.C, a.ldc, a.slab, a.M, a.N, a.splits, a.G, a.cg, a.beta, a.alpha, a.mirror, a.mcg);
   }
 }
 

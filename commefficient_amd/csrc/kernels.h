@@ -576,8 +576,15 @@ struct GemmTnArgs {
   int G = 1;            // groups: A / B rows [g T, (g + 1) T) -> C + g cg
   int64_t cg = 0;
   int slab_only = 0;    // write every split's product to the slabs, no reduction into C
+  int64_t sa = -1, sb = -1;       // group strides of A / B in elements (< 0: T lda / T ldb)
+  float beta = 1.f, alpha = 1.f;  // C = beta C + alpha A^T B
+  uint16_t* mirror = nullptr;     // + bf16(C) at the same [m][n] (ldc), group stride mcg
+  int64_t mcg = 0;
+  int small = -1;                 // tile: -1 by shape, 0: 256 x 256, 1: 128 x 128
+  int stage = 0;                  // 128 x 128, one split: C updated through LDS, 16 bytes a lane
+                                  // (ldc, cg, mcg multiples of 4; C, mirror 16 / 8-byte aligned)
 };
-int gemm_tn_splits(int M, int N, int T, int cus);
+int gemm_tn_splits(int M, int N, int T, int cus, int small = -1);
 void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream);
 // out_q[c] = sum over b < G of part[b*stride + q*N + c], q < Q (fixed order)
 void launch_colsum_final(const float* part, int G, int Q, int64_t N, int64_t stride,

@@ -1,28 +1,12 @@
 cd "${GRAFT_REPO_ROOT}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r5ab4; mkdir -p $O
-cat > /tmp/rs.py <<'PY'
-import sys, torch
-sys.path.insert(0, "tests"); sys.path.insert(0, ".")
-import test_fedavg_native as t
-from commefficient_amd.models.fixup import ResNet18
-for extra in (["--fedavg_batch_size", "-1", "--num_fedavg_epochs", "2"], ["--fedavg_batch_size", "2", "--num_fedavg_epochs", "1"]):
-    torch.manual_seed(0)
-    base = ResNet18(num_classes=100)
-    G, n = 6, 5
-    _, _, b_n, _ = t._round(base, "native", "bf16", G, n, extra)
-    _, _, b_v, _ = t._round(base, "vmap", "bf16", G, n, extra)
-    _, _, b_vf, _ = t._round(base, "vmap", "fp32", G, n, extra)
-    worst = []
-    for k in b_v:
-        if "running" in k:
-            ref = b_vf[k].norm().item()
-            worst.append(((b_n[k] - b_vf[k]).norm().item() / ref, (b_v[k] - b_vf[k]).norm().item() / ref,
-                          (b_n[k] - b_vf[k]).abs().max().item(), (b_v[k] - b_vf[k]).abs().max().item(), k))
-    worst.sort(reverse=True)
-    for w in worst[:4]: print(extra[1], "rel_n %.4f rel_v %.4f max_n %.3f max_v %.3f %s" % w)
-PY
-for v in new old; do
-if [ $v = old ]; then export COMMEFF_BN_OLDCB=1; fi
-echo "== $v"; timeout -k 10 300 python -u /tmp/rs.py > $O/$v.log 2>&1; echo "rc=$?"; tail -8 $O/$v.log
+O=gpurun_out/r5tn3; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu tests/test_fedavg_native.py tests/test_gemm.py > $O/tests.log 2>&1 || { echo TESTS_FAILED; tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+for v in 1 -1 0 1 -1 0; do
+  if [ $v = 0 ]; then export COMMEFF_FA_TN=0; else export COMMEFF_FA_TN=1 COMMEFF_FA_TN_SMALL=$v; fi
+  timeout -k 10 300 python scripts/bench_configs.py --config cifar100_fedavg_local --steps 5 --warmup 2 > $O/tn$v.log 2>&1 || { tail -20 $O/tn$v.log; exit 1; }
+  echo "small=$v: $(tail -1 $O/tn$v.log | cut -c1-110)"
 done
+export COMMEFF_FA_TN=1 COMMEFF_FA_TN_SMALL=1
+timeout -k 10 400 rocprofv3 --kernel-trace -d $O/prof -o run -- python scripts/bench_configs.py --config cifar100_fedavg_local --steps 2 --warmup 1 > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }

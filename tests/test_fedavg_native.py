@@ -276,6 +276,38 @@ def test_conv3x3_wgrad_rows_rsc_order(G, C, K, H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K,N,Nfull,o,P,small", [(256, 2304, 2304, 0, 80, -1), (64, 64, 576, 256, 320, -1),
+                                                 (512, 2304, 2304, 0, 17, 1), (128, 1152, 1152, 0, 200, 0),
+                                                 (72, 136, 136, 0, 50, 1)])
+def test_fa_bmm_rows_sgd_and_mirror(K, N, Nfull, o, P, small):
+    """TN GEMM over channel-stacked operands into client rows: rows = beta rows
+    + alpha A_g B_g with the bf16 mirror from the epilogue (fp32 reference)"""
+    torch.manual_seed(0)
+    G, ld, off = 5, K * N + 96, 32
+    At = torch.randn(P, G, K, device="cuda").bfloat16()
+    col = torch.randn(P, G, Nfull, device="cuda").bfloat16()
+    A = At.permute(1, 2, 0)
+    B = col.transpose(0, 1)[:, :, o:o + N]
+    W = torch.randn(G, ld, device="cuda")
+    W0 = W.clone()
+    Wb = torch.zeros(G, ld, device="cuda", dtype=torch.bfloat16)
+    assert _ops().fa_bmm_rows(A, B, W, ld, off, 0.99, -0.1, Wb, small)
+    ref = 0.99 * W0[:, off:off + K * N].view(G, K, N) - 0.1 * torch.bmm(A.float(), B.float())
+    got = W[:, off:off + K * N].view(G, K, N)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(Wb[:, off:off + K * N].view(G, K, N), got.bfloat16(), rtol=0, atol=0)
+    # the rest of the rows untouched
+    assert torch.equal(W[:, :off], W0[:, :off]) and torch.equal(W[:, off + K * N:], W0[:, off + K * N:])
+    assert not Wb[:, :off].any() and not Wb[:, off + K * N:].any()
+    # plain accumulation (beta 1, alpha 1), no mirror
+    W2 = W0.clone()
+    assert _ops().fa_bmm_rows(A, B, W2, ld, off, 1.0, 1.0, None, small)
+    torch.testing.assert_close(W2[:, off:off + K * N].view(G, K, N),
+                               W0[:, off:off + K * N].view(G, K, N) + torch.bmm(A.float(), B.float()),
+                               rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
 def test_ew_add_relu():
     a = torch.randn(2, 64, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     b = torch.randn_like(a)
