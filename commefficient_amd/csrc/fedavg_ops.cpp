@@ -116,6 +116,9 @@ void fa_upload(at::Tensor out, const at::Tensor& w0, const at::Tensor& W, int64_
                   w0.scalar_type() == at::kFloat && w0.is_contiguous(),
               "fa_upload: out / w0 fp32 [d]");
   check_rows(W, ld, rows, 0, d, "fa_upload: W");
+  TORCH_CHECK(ld % 4 == 0 && reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(w0.data_ptr()) % 16 == 0,
+              "fa_upload: rows of a multiple of 4 floats, 16-byte aligned");
   const int32_t* pp = nullptr;
   if (perm.has_value() && perm->defined()) {
     TORCH_CHECK(perm->is_cuda() && perm->scalar_type() == at::kInt && perm->is_contiguous() && perm->numel() == d,

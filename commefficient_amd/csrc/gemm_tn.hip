@@ -181,16 +181,16 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
     const int c4 = tid & 31, r0 = tid >> 5;  // 8 rows per pass, 16 passes
     const int n = n0 + c4 * 4;
 #pragma unroll
-    for (int pb = 0; pb < 16; pb += 4) {
-      float4 o[4];
+    for (int pb = 0; pb < 16; pb += 8) {
+      float4 o[8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 8; ++q) {
         const int m = m0 + (pb + q) * 8 + r0;
         o[q] = rdc && m < a.M && n < a.N ? *reinterpret_cast<const float4*>(cb + static_cast<int64_t>(m) * a.ldc + n)
                                          : float4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < 8; ++q) {
         const int r = (pb + q) * 8 + r0, m = m0 + r;
         if (m >= a.M || n >= a.N) continue;
         const float4 t = *reinterpret_cast<const float4*>(tl + r * 128 + c4 * 4);
