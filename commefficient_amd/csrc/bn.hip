@@ -646,7 +646,8 @@ __global__ void __launch_bounds__(1024)
 bn_cs_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__ stat,
                           const float* __restrict__ prm, int64_t ld, int64_t woff, int cg, int C, int M,
                           int S, float* __restrict__ coef, float* __restrict__ grad, int64_t gld,
-                          int64_t gwoff, int64_t gboff, float beta, float alpha) {
+                          int64_t gwoff, int64_t gboff, float beta, float alpha,
+                          const float* __restrict__ wsrc, int64_t sld) {
   __shared__ float red[2][kGL][64];
   const int cc = threadIdx.x & 63, gl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cc;
@@ -662,8 +663,11 @@ bn_cs_bwd_finalize_kernel(const float* __restrict__ part, const float* __restric
   float* gr = grad + static_cast<int64_t>(c / cg) * gld + c % cg;
   // dweight = sum(dy xhat), dbias = sum(dy); beta / alpha: the SGD step applied
   // in place to the weight rows (read above, before this write)
-  gr[gwoff] = beta != 0.f ? beta * gr[gwoff] + alpha * s2 : alpha * s2;
-  gr[gboff] = beta != 0.f ? beta * gr[gboff] + alpha * s1 : alpha * s1;
+  // (wsrc: beta scales the current weights' rows, sld apart / 0 shared, at
+  // the same offsets -- the first local step's server row, not a copy in grad)
+  const float* sr = wsrc != nullptr ? wsrc + static_cast<int64_t>(c / cg) * sld + c % cg : gr;
+  gr[gwoff] = beta != 0.f ? beta * sr[gwoff] + alpha * s2 : alpha * s2;
+  gr[gboff] = beta != 0.f ? beta * sr[gboff] + alpha * s1 : alpha * s1;
 }
 
 int apply_grid(int64_t n) {
@@ -785,12 +789,12 @@ void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t w
 void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                       const float* prm, int64_t ld, int64_t woff, int cg, int M, int C, float* part,
                       float* coef, float* grad, int64_t gld, int64_t gwoff, int64_t gboff, uint16_t* dx,
-                      hipStream_t stream, float beta, float alpha) {
+                      hipStream_t stream, float beta, float alpha, const float* wsrc, int64_t sld) {
   const int S = bn_slabs(1, M), CB = cs_channel_block(C, S);
   COMMEFF_LAUNCH(bn_partial_kernel<true>, dim3(S, C / CB), dim3(256), 0, stream, x, dy, y_relu, stat, C,
                  M, S, part, CB);
   COMMEFF_LAUNCH(bn_cs_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, part, stat, prm,
-                 ld, woff, cg, C, M, S, coef, grad, gld, gwoff, gboff, beta, alpha);
+                 ld, woff, cg, C, M, S, coef, grad, gld, gwoff, gboff, beta, alpha, wsrc, sld);
   const int64_t nchunks = static_cast<int64_t>(M) * (C / 8);
   COMMEFF_LAUNCH(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
                  coef, C, M, static_cast<uint32_t>(nchunks), false, dx, nullptr, nullptr);

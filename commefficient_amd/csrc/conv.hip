@@ -1248,7 +1248,9 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
                                                                        int splits, float beta,
                                                                        int64_t gstride, int kg, int64_t ld,
                                                                        int rsc, int sub, float alpha,
-                                                                       uint16_t* __restrict__ mirror) {
+                                                                       uint16_t* __restrict__ mirror,
+                                                                       const float* __restrict__ wsrc,
+                                                                       int64_t sld) {
   __shared__ float t[PARTS][64 * 9];
   const int ncb = C >> 6;
   const int k = blockIdx.x / ncb, c0 = (blockIdx.x - k * ncb) * 64;
@@ -1283,6 +1285,10 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
                            static_cast<size_t>((k % kg) % sub) * Cl * 9
              : kg > 0 ? dw + static_cast<size_t>(k / kg) * ld + static_cast<size_t>(k % kg) * C * 9
                       : dw + static_cast<size_t>(k) * C * 9;
+  // wsrc: the same element of row `row` of the current weights (sld apart; 0:
+  // the server row every client starts from -- no broadcast copy into dw)
+  const int64_t row = sub > 0 ? static_cast<int64_t>((k / kg) * (kg / sub) + half) : kg > 0 ? k / kg : 0;
+  const float* so = wsrc != nullptr ? wsrc + row * sld + (o - (dw + row * ld)) : nullptr;
   for (int e = threadIdx.x; e < 576; e += 64 * PARTS) {
     const int src = rsc ? (e & 63) * 9 + (e >> 6) : e;
     float v = t[0][src];
@@ -1291,7 +1297,7 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
     float* oe = rsc ? o + (e >> 6) * Cl + c0l + (e & 63) : o + c0l * 9 + e;
     // alpha / beta: the batched FedAvg clients' SGD step applied in place
     // (w = (1 - lr wd) w - lr g), with the bf16 mirror of the new weight
-    const float r = beta != 0.f ? beta * *oe + alpha * v : alpha * v;
+    const float r = beta != 0.f ? beta * (so != nullptr ? so[oe - o] : *oe) + alpha * v : alpha * v;
     *oe = r;
     if (mirror != nullptr) {
       const uint32_t u = __float_as_uint(r);
@@ -1303,14 +1309,15 @@ __global__ void __launch_bounds__(64 * PARTS) conv_wgrad_reduce_kernel(const flo
 
 void launch_wgrad_reduce(const float* slab, float* dw, int K, int C, int splits, float beta,
                          int64_t gstride, int groups, hipStream_t stream, int kg = 0, int64_t ld = 0,
-                         bool rsc = false, int sub = 0, float alpha = 1.f, uint16_t* mirror = nullptr) {
+                         bool rsc = false, int sub = 0, float alpha = 1.f, uint16_t* mirror = nullptr,
+                         const float* wsrc = nullptr, int64_t sld = 0) {
   const dim3 grid(K * (C / 64), groups);
   if (splits >= 32)
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<16>, grid, dim3(1024), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld, rsc ? 1 : 0, sub, alpha, mirror);
+                       beta, gstride, kg, ld, rsc ? 1 : 0, sub, alpha, mirror, wsrc, sld);
   else
     COMMEFF_LAUNCH(conv_wgrad_reduce_kernel<4>, grid, dim3(256), 0, stream, slab, dw, K, C, splits,
-                       beta, gstride, kg, ld, rsc ? 1 : 0, sub, alpha, mirror);
+                       beta, gstride, kg, ld, rsc ? 1 : 0, sub, alpha, mirror, wsrc, sld);
 }
 
 // w [K][C][3][3] fp32 -> wf [K][3][3][C] bf16 and wt [C][3][3][K] bf16
@@ -1649,12 +1656,13 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 // channel-stacked grouped wgrad written straight into per-group rows: output
 // channel k of group k / kg at dst + (k / kg) * ld + (k % kg) * 9 C
 void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream,
-                               int sub, float beta, float alpha, uint16_t* mirror) {
+                               int sub, float beta, float alpha, uint16_t* mirror, const float* wsrc,
+                               int64_t sld) {
   const int steps = (a.P + BK - 1) / BK;
   a.group_px = 0;
   launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
   launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, beta, int64_t{0}, 1, stream, kg, ld, rsc, sub, alpha,
-                      mirror);
+                      mirror, wsrc, sld);
 }
 
 // the wgrad GEMM kernels (slabs only) with a given split length

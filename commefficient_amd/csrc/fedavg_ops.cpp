@@ -55,6 +55,15 @@ void check_rows(const at::Tensor& t, int64_t ld, int64_t rows, int64_t off, int6
               name, ": [", off, ", ", off + span, ") of ", rows, " rows of ", ld, " floats exceeds ", t.numel());
 }
 
+// the current weights a fused SGD step scales (beta): fp32 rows sld apart (0:
+// the shared server row of the first local step); none: the destination's own
+const float* src_rows(const c10::optional<at::Tensor>& src, int64_t sld, int64_t rows, int64_t off, int64_t span,
+                      const char* name) {
+  if (!src.has_value() || !src->defined()) return nullptr;
+  check_rows(*src, sld, rows, off, span, name);
+  return src->data_ptr<float>();
+}
+
 int64_t out_size(int64_t in, int64_t k, int64_t stride, int64_t pad) { return (in + 2 * pad - k) / stride + 1; }
 
 // per-client bf16 images of conv weights held in fp32 rows W[g*ld + off + (k*C + c)*RS + t]:
@@ -382,7 +391,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cs_bn_fwd(const at::Tensor& x, co
 // per-client weight / bias gradients are written to grad[g*gld + gwoff / gboff + c]
 at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stat, const at::Tensor& bits,
                      const at::Tensor& prm, int64_t ld, int64_t woff, int64_t G, at::Tensor grad, int64_t gld,
-                     int64_t gwoff, int64_t gboff, double beta, double alpha) {
+                     int64_t gwoff, int64_t gboff, double beta, double alpha,
+                     const c10::optional<at::Tensor>& src, int64_t sld) {
   check_cl_bf16(x, "cs_bn_bwd: x");
   check_cl_bf16(dy, "cs_bn_bwd: dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "cs_bn_bwd: dy shape");
@@ -396,6 +406,8 @@ at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor
   check_rows(prm, ld, G, woff, cg, "cs_bn_bwd: prm");
   check_rows(grad, gld, G, std::min(gwoff, gboff), std::max(gwoff, gboff) - std::min(gwoff, gboff) + cg,
              "cs_bn_bwd: grad");
+  const float* sp = src_rows(src, sld, G, std::min(gwoff, gboff),
+                             std::max(gwoff, gboff) - std::min(gwoff, gboff) + cg, "cs_bn_bwd: src");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto fo = x.options().dtype(at::kFloat);
   auto part = at::empty({bn_cs_scratch_floats(static_cast<int>(M), static_cast<int>(C))}, fo);
@@ -404,7 +416,7 @@ at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor
   launch_bn_cs_bwd(bf(x), bf(dy), bits.data_ptr<uint8_t>(), stat.data_ptr<float>(), prm.data_ptr<float>(), ld,
                    woff, static_cast<int>(cg), static_cast<int>(M), static_cast<int>(C), part.data_ptr<float>(),
                    coef.data_ptr<float>(), grad.data_ptr<float>(), gld, gwoff, gboff, bfw(dx), stream_now(),
-                   static_cast<float>(beta), static_cast<float>(alpha));
+                   static_cast<float>(beta), static_cast<float>(alpha), sp, sld);
   return dx;
 }
 
@@ -412,7 +424,8 @@ at::Tensor cs_bn_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor
 // gradient rows dst[g*ld + off + (k*C + c)*9 + t]; false (nothing written)
 // where the geometry has no grouped halo tiling
 bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at::Tensor dst, int64_t ld,
-                        int64_t off, bool rsc, double beta, double alpha, const c10::optional<at::Tensor>& mirror) {
+                        int64_t off, bool rsc, double beta, double alpha, const c10::optional<at::Tensor>& mirror,
+                        const c10::optional<at::Tensor>& src, int64_t sld) {
   check_cl_bf16(dy, "conv3x3_wgrad_rows: dy");
   check_cl_bf16(x, "conv3x3_wgrad_rows: x");
   const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3), K = dy.size(1);
@@ -428,6 +441,7 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
                                        static_cast<int>(kC), static_cast<int>(kK)))
     return false;
   check_rows(dst, ld, G, off, kg * C * 9, "conv3x3_wgrad_rows: dst");
+  const float* sp = src_rows(src, sld, G, off, kg * C * 9, "conv3x3_wgrad_rows: src");
   uint16_t* mp = nullptr;
   if (mirror.has_value() && mirror->defined()) {  // bf16 rows of dst's layout
     TORCH_CHECK(mirror->is_cuda() && mirror->scalar_type() == at::kBFloat16 && mirror->is_contiguous() &&
@@ -454,7 +468,8 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
   a.x_stride = static_cast<int>(GC);
   a.kg = static_cast<int>(kK);
   launch_conv3x3_wgrad_rows(a, dst.data_ptr<float>() + off, static_cast<int>(kK), ld, rsc, stream_now(),
-                            pairs ? 64 : 0, static_cast<float>(beta), static_cast<float>(alpha), mp);
+                            pairs ? 64 : 0, static_cast<float>(beta), static_cast<float>(alpha), mp,
+                            sp != nullptr ? sp + off : nullptr, sld);
   return true;
 }
 
@@ -465,7 +480,8 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
 // written in its epilogue -- hipBLASLt's baddbmm + a cast pass re-reading the
 // rows otherwise.  false (nothing written): a layout the kernel cannot read.
 bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64_t ld, int64_t off, double beta,
-                 double alpha, const c10::optional<at::Tensor>& mirror, int64_t small) {
+                 double alpha, const c10::optional<at::Tensor>& mirror, int64_t small,
+                 const c10::optional<at::Tensor>& src, int64_t sld) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
                   A.dim() == 3 && B.dim() == 3 && A.size(0) == B.size(0) && A.size(2) == B.size(1),
               "fa_bmm_rows: A [G, K, P], B [G, P, N] bf16");
@@ -476,6 +492,8 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
     return false;
   check_rows(dst, ld, G, off, K * N, "fa_bmm_rows: dst");
   TORCH_CHECK(ld > 0, "fa_bmm_rows: per-client rows");
+  const float* sp = src_rows(src, sld, G, off, K * N, "fa_bmm_rows: src");
+  if (sp != nullptr && (sld % 4 || reinterpret_cast<uintptr_t>(sp + off) % 16)) return false;
   uint16_t* mp = nullptr;
   if (mirror.has_value() && mirror->defined()) {
     TORCH_CHECK(mirror->is_cuda() && mirror->scalar_type() == at::kBFloat16 && mirror->is_contiguous() &&
@@ -506,6 +524,8 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
   g.alpha = static_cast<float>(alpha);
   g.mirror = mp;
   g.mcg = ld;
+  g.src = sp != nullptr ? sp + off : nullptr;
+  g.scg = sld;
   g.small = static_cast<int>(small);
   g.stage = (small == 1 || small == -2) ? 1 : 0;
   if (small == -2) g.small = 1;
@@ -517,7 +537,7 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_bmm_rows(Tensor A, Tensor B, Tensor(a!) dst, int ld, int off, float beta=1., float alpha=1., "
-        "Tensor(b!)? mirror=None, int small=-1) -> bool");
+        "Tensor(b!)? mirror=None, int small=-1, Tensor? src=None, int sld=0) -> bool");
   m.def("fa_weight_image(Tensor W, int ld, int G, int off, int K, int C, int R, int Kc, int kind) -> Tensor");
   m.def("fa_row_sgd(Tensor(a!) W, int ld, Tensor src, int sld, Tensor G, int gld, int rows, int d, float clip, "
         "float lr, float wd, Tensor(b!)? Wb=None) -> ()");
@@ -534,9 +554,10 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
         "Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt, Tensor? post_add=None) "
         "-> (Tensor, Tensor, Tensor)");
   m.def("cs_bn_bwd(Tensor dy, Tensor x, Tensor stat, Tensor bits, Tensor prm, int ld, int woff, int G, "
-        "Tensor(a!) grad, int gld, int gwoff, int gboff, float beta=0., float alpha=1.) -> Tensor");
+        "Tensor(a!) grad, int gld, int gwoff, int gboff, float beta=0., float alpha=1., Tensor? src=None, "
+        "int sld=0) -> Tensor");
   m.def("conv3x3_wgrad_rows(Tensor dy, Tensor x, int G, Tensor(a!) dst, int ld, int off, bool rsc=False, "
-        "float beta=0., float alpha=1., Tensor(b!)? mirror=None) -> bool");
+        "float beta=0., float alpha=1., Tensor(b!)? mirror=None, Tensor? src=None, int sld=0) -> bool");
   m.def("fa_bcast_rows(Tensor(a!) W, int ld, Tensor src, int rows, int d) -> ()");
   m.def("fa_cast_rows(Tensor(a!) Wb, Tensor W, int ld, int rows, int off, int n) -> ()");
 }

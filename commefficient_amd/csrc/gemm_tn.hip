@@ -178,6 +178,7 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
     float* cb = a.C + static_cast<int64_t>(grp) * a.cg;
     uint16_t* mb = a.mirror != nullptr ? a.mirror + static_cast<int64_t>(grp) * a.mcg : nullptr;
     const bool plain = a.beta == 1.f && a.alpha == 1.f, rdc = plain || a.beta != 0.f;
+    const float* sb = a.src != nullptr ? a.src + static_cast<int64_t>(grp) * a.scg : cb;
     const int c4 = tid & 31, r0 = tid >> 5;  // 8 rows per pass, 16 passes
     const int n = n0 + c4 * 4;
 #pragma unroll
@@ -186,7 +187,7 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int m = m0 + (pb + q) * 8 + r0;
-        o[q] = rdc && m < a.M && n < a.N ? *reinterpret_cast<const float4*>(cb + static_cast<int64_t>(m) * a.ldc + n)
+        o[q] = rdc && m < a.M && n < a.N ? *reinterpret_cast<const float4*>(sb + static_cast<int64_t>(m) * a.ldc + n)
                                          : float4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
@@ -224,6 +225,7 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
   uint16_t* mir = direct && a.mirror != nullptr ? a.mirror + static_cast<int64_t>(grp) * a.mcg : nullptr;
   const bool plain = a.beta == 1.f && a.alpha == 1.f;
   const bool rdc = direct && (plain || a.beta != 0.f);
+  const float* src = direct && a.src != nullptr ? a.src + static_cast<int64_t>(grp) * a.scg : out;
   // (batches of NB column blocks: 32 more registers in the 256 x 256 variant
   // -- all NI of them spilled)
   constexpr int NB = SMALL ? NI : 2;
@@ -243,7 +245,7 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
-          old[q][e] = rdc && n < a.N && m < a.M ? out[static_cast<int64_t>(m) * ld + n] : 0.f;
+          old[q][e] = rdc && n < a.N && m < a.M ? src[static_cast<int64_t>(m) * ld + n] : 0.f;
         }
       }
 #pragma unroll

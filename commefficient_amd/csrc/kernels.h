@@ -309,9 +309,11 @@ void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t st
 // (sub > 0: every kernel group of kg channels is kg / sub clients -- the
 // diagonal sub x sub blocks are written, each to its client's row)
 // (beta / alpha: dst = beta dst + alpha dW -- an SGD step in place -- and the
-// bf16 mirror of the result at the same offsets from `mirror`)
+// bf16 mirror of the result at the same offsets from `mirror`; wsrc: beta
+// scales wsrc's rows (sld apart, 0: one shared row) instead of dst's)
 void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, bool rsc, hipStream_t stream,
-                               int sub = 0, float beta = 0.f, float alpha = 1.f, uint16_t* mirror = nullptr);
+                               int sub = 0, float beta = 0.f, float alpha = 1.f, uint16_t* mirror = nullptr,
+                               const float* wsrc = nullptr, int64_t sld = 0);
 // grouped convs on channel-stacked images (a.kg / a.x_stride set): false when
 // the geometry has no halo tiling (the caller falls back)
 bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream);
@@ -410,7 +412,8 @@ void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t w
 void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                       const float* prm, int64_t ld, int64_t woff, int cg, int M, int C, float* part,
                       float* coef, float* grad, int64_t gld, int64_t gwoff, int64_t gboff, uint16_t* dx,
-                      hipStream_t stream, float beta = 0.f, float alpha = 1.f);
+                      hipStream_t stream, float beta = 0.f, float alpha = 1.f, const float* wsrc = nullptr,
+                      int64_t sld = 0);
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
                    const float* w, int G, int M, int C, float* part, float* coef, float* dw, float* db,
                    float beta, uint16_t* dx, hipStream_t stream, float* gdw = nullptr,
@@ -581,6 +584,8 @@ struct GemmTnArgs {
   uint16_t* mirror = nullptr;     // + bf16(C) at the same [m][n] (ldc), group stride mcg
   int64_t mcg = 0;
   int small = -1;                 // tile: -1 by shape, 0: 256 x 256, 1: 128 x 128
+  const float* src = nullptr;     // beta scales src (group stride scg, 0: shared) instead of C
+  int64_t scg = 0;
   int stage = 0;                  // 128 x 128, one split: C updated through LDS, 16 bytes a lane
                                   // (ldc, cg, mcg multiples of 4; C, mirror 16 / 8-byte aligned)
 };

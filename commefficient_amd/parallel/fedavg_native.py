@@ -63,11 +63,21 @@ class _Sink:
     receive ``beta * dst + alpha * grad`` -- the gradient rows (beta 0, alpha
     1; a per-row SGD kernel follows, needed for clipping) or the weight rows
     themselves (beta = 1 - lr wd, alpha = -lr: the SGD step fused into every
-    producer), with the bf16 ``mirror`` of the updated weights."""
-    __slots__ = ("dst", "ld", "beta", "alpha", "mirror")
+    producer), with the bf16 ``mirror`` of the updated weights.  ``src`` (sld
+    apart, 0: one shared row) holds the weights the step starts from -- the
+    first local step reads the server row there instead of a broadcast copy
+    of it in ``dst``."""
+    __slots__ = ("dst", "ld", "beta", "alpha", "mirror", "src", "sld")
 
-    def __init__(self, dst, ld, beta, alpha, mirror):
+    def __init__(self, dst, ld, beta, alpha, mirror, src=None, sld=0):
         self.dst, self.ld, self.beta, self.alpha, self.mirror = dst, ld, float(beta), float(alpha), mirror
+        self.src, self.sld = src, int(sld)
+
+    def src_rows(self, off, K, n):
+        """[G, K, n] view of the weights ``beta`` scales (``dst``'s own without src)"""
+        if self.src is None:
+            return self.dst[:, off:off + K * n].view(-1, K, n)
+        return ResNet18FedAvg._rows(self.src, self.sld, self.dst.shape[0], off, K, n)
 
 
 class _Block:
@@ -200,7 +210,7 @@ class ResNet18FedAvg:
         the bf16 mirror of the updated segment"""
         G, K, n = A.shape[0], A.shape[1], B.shape[2]
         if cls._TN[0] and _ops().fa_bmm_rows(A, B, sink.dst, sink.ld, off, sink.beta, sink.alpha, sink.mirror,
-                                             cls._TN[1]):
+                                             cls._TN[1], sink.src, sink.sld):
             return
         dst = sink.dst[:, off:off + K * n].view(G, K, n)
         if cls._BMM_INTO[0]:
@@ -208,8 +218,8 @@ class ResNet18FedAvg:
                 if sink.beta == 0.0 and sink.alpha == 1.0:
                     torch.bmm(A, B, out_dtype=torch.float32, out=dst)
                 else:
-                    torch.baddbmm(dst, A, B, out_dtype=torch.float32, beta=sink.beta, alpha=sink.alpha,
-                                  out=dst)
+                    torch.baddbmm(sink.src_rows(off, K, n), A, B, out_dtype=torch.float32, beta=sink.beta,
+                                  alpha=sink.alpha, out=dst)
                 cls._mirror(sink, off, K * n)
                 return
             except (RuntimeError, TypeError):
@@ -218,6 +228,8 @@ class ResNet18FedAvg:
         if sink.beta == 0.0 and sink.alpha == 1.0:
             _ops().wgrad_rsc_add(dst, part, 1, n, 1, False)
         else:
+            if sink.src is not None:
+                dst.copy_(sink.src_rows(off, K, n))
             dst.mul_(sink.beta).add_(part, alpha=sink.alpha)
         cls._mirror(sink, off, K * n)
 
@@ -230,7 +242,7 @@ class ResNet18FedAvg:
         # 8x8 / 4x4 maps: 5 or 2 K-steps of pixels per 256 x 256 wide-kernel
         # tile -- the column-image GEMM measured faster (36.5 vs 38.4 ms/round)
         if x.shape[3] >= 16 and _ops().conv3x3_wgrad_rows(dy, x, G, sink.dst, sink.ld, off, True, sink.beta,
-                                                          sink.alpha, sink.mirror):
+                                                          sink.alpha, sink.mirror, sink.src, sink.sld):
             return
         col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
         self._bmm_rows(sink, off, _gview(dy, G).transpose(1, 2), col.transpose(0, 1))
@@ -260,7 +272,8 @@ class ResNet18FedAvg:
         # pass); clipping needs each client's whole gradient norm first
         fused = not clip
         if fused:
-            ops.fa_bcast_rows(Wg, ld, w0i, G, d)
+            # (no broadcast of the server row into Wg: the first step's
+            # producers read it as their source row)
             Gg = None
         else:
             Gg = torch.zeros((G, ld), device=dev, dtype=torch.float32)
@@ -289,7 +302,7 @@ class ResNet18FedAvg:
                 else:
                     W, Wbf, sld = Wg, Wb, ld
                 lr_t = float(lr * decay ** steps)
-                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, Wb) if fused
+                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, Wb, W, sld) if fused
                         else _Sink(Gg, ld, 0.0, 1.0, None))
                 l, c = self._step(xb, yb, G, s1 - s0, W, Wbf, sld, sink, run, nbt, ones)
                 loss_acc += l
@@ -364,22 +377,24 @@ class ResNet18FedAvg:
         dfeat = torch.empty_like(feat)
         torch.baddbmm(dfeat, gl, Wfc, beta=0.0, alpha=inv, out=dfeat)
         gW = sink.dst[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
-        torch.baddbmm(gW, gl.transpose(1, 2), feat, beta=sink.beta, alpha=sink.alpha * inv, out=gW)
+        torch.baddbmm(sink.src_rows(self.fc_w, self.ncls, self.feat), gl.transpose(1, 2), feat, beta=sink.beta,
+                      alpha=sink.alpha * inv, out=gW)
         gb = sink.dst[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
-        torch.baddbmm(gb, ones[:, :n].transpose(1, 2), gl, beta=sink.beta, alpha=sink.alpha * inv, out=gb)
+        torch.baddbmm(sink.src_rows(self.fc_b, 1, self.ncls), ones[:, :n].transpose(1, 2), gl, beta=sink.beta,
+                      alpha=sink.alpha * inv, out=gb)
         da = ops.fa_head_bwd(dfeat, codes, a.shape[2], a.shape[3])
         # ---- blocks, last to first
         for bi in range(len(self.blocks) - 1, -1, -1):
             b = self.blocks[bi]
             xin, colx, h1, st1, bits1, a1, h2, st2, bits2 = saved[bi]
             dh2 = ops.cs_bn_bwd(da, h2, st2, bits2, W, ld, b.bn2w, G, sink.dst, sink.ld, b.bn2w, b.bn2b,
-                                sink.beta, sink.alpha)
+                                sink.beta, sink.alpha, sink.src, sink.sld)
             # (each conv's input gradient reads its weights before the weight
             # gradient's producer may update them in place)
             da1 = self._conv3_dgrad(dh2, Wb, ld, G, b.conv2, b.cout, b.cout)
             self._conv3_wgrad(dh2, a1, G, sink, b.conv2, b.cout, b.cout)
             dh1 = ops.cs_bn_bwd(da1, h1, st1, bits1, W, ld, b.bn1w, G, sink.dst, sink.ld, b.bn1w, b.bn1b,
-                                sink.beta, sink.alpha)
+                                sink.beta, sink.alpha, sink.src, sink.sld)
             if b.stride == 1:
                 dx = self._conv3_dgrad(dh1, Wb, ld, G, b.conv1, b.cout, b.cin)
                 self._conv3_wgrad(dh1, xin, G, sink, b.conv1, b.cout, b.cin)

@@ -299,6 +299,12 @@ def test_fa_bmm_rows_sgd_and_mirror(K, N, Nfull, o, P, small):
     # the rest of the rows untouched
     assert torch.equal(W[:, :off], W0[:, :off]) and torch.equal(W[:, off + K * N:], W0[:, off + K * N:])
     assert not Wb[:, :off].any() and not Wb[:, off + K * N:].any()
+    # the first local step: beta scales the shared server row (sld 0), not dst
+    w0 = torch.randn(ld, device="cuda")
+    W3 = torch.full((G, ld), float("nan"), device="cuda")
+    assert _ops().fa_bmm_rows(A, B, W3, ld, off, 0.99, -0.1, Wb, small, w0, 0)
+    ref3 = 0.99 * w0[off:off + K * N].view(1, K, N) - 0.1 * torch.bmm(A.float(), B.float())
+    torch.testing.assert_close(W3[:, off:off + K * N].view(G, K, N), ref3, rtol=1e-4, atol=1e-3)
     # plain accumulation (beta 1, alpha 1), no mirror
     W2 = W0.clone()
     assert _ops().fa_bmm_rows(A, B, W2, ld, off, 1.0, 1.0, None, small)
