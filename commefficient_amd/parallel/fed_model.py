@@ -1200,6 +1200,11 @@ class FedModel:
                                    tuple(m.detach().float().mean() for m in mets))
 
         gfn = vmap(grad(client_loss, has_aux=True))
+        # the client tail (clip, weight decay, SGD) as one row kernel on the GPU
+        # (rows of a multiple of 4 floats: every CV model here; max_grad_norm
+        # 0 means no clipping there, as None does here)
+        row_sgd = (self.device.type == "cuda" and self.d % 4 == 0
+                   and (a.max_grad_norm is None or a.max_grad_norm > 0))
         loss_rows, met_rows, slot_rows = [], [], []
         for p0 in range(0, len(mine), per_pass):
             slots = my_slots[p0:p0 + per_pass]
@@ -1220,13 +1225,21 @@ class FedModel:
                                   for nm, o, k, shp in zip(names, fl.offsets, fl.numels, fl.shapes)}
                         g, (l, mets) = gfn(params, bufs, *[x[:, s0:s1] for x in xs])
                         Gg = torch.cat([g[nm].float().reshape(Gp, -1) for nm in names], dim=1)
-                        if a.max_grad_norm is not None:
-                            nrm = Gg.norm(dim=1, keepdim=True)
-                            Gg.mul_(torch.where(nrm > a.max_grad_norm,
-                                                a.max_grad_norm / nrm, torch.ones_like(nrm)))
-                        if a.weight_decay != 0:
-                            Gg.add_(Wg, alpha=a.weight_decay / a.num_workers)
-                        Wg.add_(Gg, alpha=-lr * (a.fedavg_lr_decay ** step))
+                        lr_t = lr * (a.fedavg_lr_decay ** step)
+                        if row_sgd:
+                            # one kernel: per-row clip + weight decay + SGD (csrc/fedavg.hip)
+                            from .. import _ext
+                            _ext.ops().fa_row_sgd(Wg, self.d, Wg, self.d, Gg, self.d, Gp, self.d,
+                                                  float(a.max_grad_norm or 0.0), float(lr_t),
+                                                  float(a.weight_decay / a.num_workers))
+                        else:
+                            if a.max_grad_norm is not None:
+                                nrm = Gg.norm(dim=1, keepdim=True)
+                                Gg.mul_(torch.where(nrm > a.max_grad_norm,
+                                                    a.max_grad_norm / nrm, torch.ones_like(nrm)))
+                            if a.weight_decay != 0:
+                                Gg.add_(Wg, alpha=a.weight_decay / a.num_workers)
+                            Wg.add_(Gg, alpha=-lr_t)
                         ls.append(l)
                         ms = list(mets) if ms is None else [x + y for x, y in zip(ms, mets)]
                         step += 1

@@ -109,14 +109,14 @@ def test_batched_path_runs_with_batchnorm_and_updates_running_stats():
     assert fed._payload[:fed.d].abs().max() > 0
 
 
-def _gpu_round(base, dtype, batched, steps):
+def _gpu_round(base, dtype, batched, steps, extra=()):
     dist.init("cuda")
     args = parse_args(argv=["--dataset_name", "CIFAR10", "--mode", "fedavg", "--error_type", "none",
                             "--local_momentum", "0", "--virtual_momentum", "0.5", "--num_workers",
                             "8", "--num_clients", "8", "--local_batch_size", "-1", "--device", "cuda",
                             "--dtype", dtype, "--fedavg_batched", batched]
                       + (["--fedavg_batch_size", "4", "--num_fedavg_epochs", "2"] if steps == 4
-                         else ["--fedavg_batch_size", "8"]), probe_port=False)
+                         else ["--fedavg_batch_size", "8"]) + list(extra), probe_port=False)
     model = copy.deepcopy(base).cuda()
     if dtype == "bf16":
         model = model.to(memory_format=torch.channels_last)
@@ -141,6 +141,19 @@ def test_batched_local_sgd_gpu_fp32():
     base = models.ResNet9(channels={"prep": 64, "layer1": 128, "layer2": 128, "layer3": 256})
     up_a, l_a = _gpu_round(base, "fp32", "on", 4)
     up_b, l_b = _gpu_round(base, "fp32", "off", 4)
+    assert ((up_a - up_b).norm() / up_b.norm()).item() < 1e-3
+    torch.testing.assert_close(l_a, l_b, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_batched_local_sgd_gpu_fp32_clip_weight_decay():
+    """The vmap path's client tail on the row kernel (fa_row_sgd: per-client
+    clip + weight decay + SGD) vs the sequential path's stock tail"""
+    torch.manual_seed(0)
+    base = models.ResNet9(channels={"prep": 64, "layer1": 128, "layer2": 128, "layer3": 256})
+    extra = ["--max_grad_norm", "0.5", "--weight_decay", "5e-2", "--fedavg_lr_decay", "0.8"]
+    up_a, l_a = _gpu_round(base, "fp32", "on", 4, extra)
+    up_b, l_b = _gpu_round(base, "fp32", "off", 4, extra)
     assert ((up_a - up_b).norm() / up_b.norm()).item() < 1e-3
     torch.testing.assert_close(l_a, l_b, rtol=1e-3, atol=1e-3)
 
