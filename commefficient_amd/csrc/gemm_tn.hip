@@ -226,6 +226,22 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
   const bool plain = a.beta == 1.f && a.alpha == 1.f;
   const bool rdc = direct && (plain || a.beta != 0.f);
   const float* src = direct && a.src != nullptr ? a.src + static_cast<int64_t>(grp) * a.scg : out;
+  if (!direct) {  // a split's slab: plain stores
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int n = n0 + wc * WN + ni * 32 + lr;
+        if (n >= a.N || m0 + wr * 64 + mi * 32 >= a.M) continue;  // padding of an edge tile
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+          if (m >= a.M) continue;  // M not a multiple of 32 (the LM head's vocabulary)
+          out[static_cast<int64_t>(m) * ld + n] = acc[mi][ni][e];
+        }
+      }
+    return;
+  }
   // (batches of NB column blocks: 32 more registers in the 256 x 256 variant
   // -- all NI of them spilled)
   constexpr int NB = SMALL ? NI : 2;
@@ -257,7 +273,7 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
           const int m = m0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
           if (m >= a.M) continue;  // M not a multiple of 32 (the LM head's vocabulary)
           const float c = acc[mi][nb + q][e];
-          const float v = !direct ? c : plain ? old[q][e] + c : a.beta * old[q][e] + a.alpha * c;
+          const float v = plain ? old[q][e] + c : a.beta * old[q][e] + a.alpha * c;
           out[static_cast<int64_t>(m) * ld + n] = v;
           if (mir != nullptr) mir[static_cast<int64_t>(m) * ld + n] = static_cast<uint16_t>(pack_bf16(v, 0.f));
         }

@@ -1,5 +1,7 @@
 """Per-kernel PMC summary (dispatch-averaged) of rocprofv3 counter CSVs."""
-import collections, csv, glob, sys
+import collections, csv, glob, os, sys
+
+FILT = os.environ.get("PMC_FILTER", "conv")
 
 def load(d):
     f = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
@@ -8,7 +10,7 @@ def load(d):
     dur = collections.defaultdict(float)
     for r in csv.DictReader(open(f[0])):
         k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").replace("commeff::", "").split("(")[0]
-        if "conv" not in k:
+        if FILT not in k:
             continue
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         if r["Dispatch_Id"] not in disp[k]:
