@@ -1520,7 +1520,9 @@ void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t strea
 // kernels only, no fused epilogue.  Returns false when the geometry has no
 // halo tiling (the caller falls back to a stock grouped convolution).
 bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream) {
-  if (a.kg <= 0 || a.pool != 0 || a.relu != 0 || a.mask != nullptr || a.addend != nullptr ||
+  // (the residual addend epilogue reads [P, K] like the output: the batched
+  // FedAvg block's input gradient = dgrad + the identity shortcut's gradient)
+  if (a.kg <= 0 || a.pool != 0 || a.relu != 0 || a.mask != nullptr || a.y_pre != nullptr ||
       a.unpool_idx != nullptr || a.dual_mask != nullptr || a.C % 64 != 0 || a.K % a.kg != 0)
     return false;
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));

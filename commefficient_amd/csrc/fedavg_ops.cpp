@@ -192,7 +192,7 @@ at::Tensor fa_dgrad_image(const at::Tensor& Wb, int64_t ld, int64_t G, int64_t o
 // grouped stride-1 3x3 conv of channel-stacked x whose group-g weights are the
 // kg rows [kg][3][3][C] at w + off + g * ld (ld 0: every group the same rows)
 at::Tensor conv3x3_fwd_rows(const at::Tensor& x, const at::Tensor& w, int64_t G, int64_t off, int64_t ld,
-                            int64_t kg) {
+                            int64_t kg, const c10::optional<at::Tensor>& addend) {
   check_cl_bf16(x, "conv3x3_fwd_rows: x");
   const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3);
   TORCH_CHECK(G >= 1 && GC % G == 0 && kg >= 1, "conv3x3_fwd_rows: channels not a multiple of G");
@@ -203,12 +203,17 @@ at::Tensor conv3x3_fwd_rows(const at::Tensor& x, const at::Tensor& w, int64_t G,
   TORCH_CHECK(N * H * W * std::max(GC, K) < (int64_t{1} << 31), "conv3x3_fwd_rows: size");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto y = at::empty({N, K, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool add = addend.has_value() && addend->defined();
+  if (add) {  // y = conv + addend (fused in the epilogue)
+    check_cl_bf16(*addend, "conv3x3_fwd_rows: addend");
+    TORCH_CHECK(addend->sizes() == y.sizes(), "conv3x3_fwd_rows: addend shape");
+  }
   ConvFwdArgs a;
   a.x = bf(x);
   a.w = bf(w) + off;
   a.y = bfw(y);
   a.mask = nullptr;
-  a.addend = nullptr;
+  a.addend = add ? bf(*addend) : nullptr;
   a.y_pre = nullptr;
   a.pool_idx = nullptr;
   a.pool = 0;
@@ -544,7 +549,7 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_upload(Tensor(a!) out, Tensor w0, Tensor W, int ld, int rows, float n, Tensor? perm=None) -> ()");
   m.def("fa_gather_rows(Tensor(a!) dst, Tensor(b!) dstb, Tensor src, Tensor perm) -> ()");
   m.def("fa_dgrad_image(Tensor Wb, int ld, int G, int off, int K, int C) -> Tensor");
-  m.def("conv3x3_fwd_rows(Tensor x, Tensor w, int G, int off, int ld, int kg) -> Tensor");
+  m.def("conv3x3_fwd_rows(Tensor x, Tensor w, int G, int off, int ld, int kg, Tensor? addend=None) -> Tensor");
   m.def("fa_head_fwd(Tensor x, int G) -> (Tensor, Tensor)");
   m.def("fa_head_bwd(Tensor df, Tensor codes, int H, int W) -> Tensor");
   m.def("fa_ew(Tensor a, Tensor? b, int mode) -> Tensor");

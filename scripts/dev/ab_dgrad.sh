@@ -1,5 +1,7 @@
 cd "${GRAFT_REPO_ROOT}" || exit 1
 export TMPDIR=/tmp
-for v in -1 -1; do
-  echo "small=$v"; COMMEFF_TN_SMALL_AB=$v timeout -k 10 120 python3 scripts/bench_gemm_tn.py || exit 1
+O=gpurun_out/r5add2; mkdir -p $O
+for v in 1 0 1 0 1 0; do
+  AB_ADD=$v timeout -k 10 300 python scripts/bench_configs.py --config cifar100_fedavg_local --steps 8 --warmup 2 > $O/b$v.log 2>&1 || { tail -20 $O/b$v.log; exit 1; }
+  echo "add=$v: $(tail -1 $O/b$v.log | cut -c60-110)"
 done

@@ -250,6 +250,10 @@ def test_conv_rows_forward_and_dgrad_image(H, K, C):
     ref0 = F.conv2d(x.float(), w[:1].expand(G, -1, -1, -1, -1).reshape(G * K, C, 3, 3).bfloat16().float(),
                     padding=1, groups=G)
     torch.testing.assert_close(y0.float() / scale, ref0 / scale, rtol=2e-2, atol=2e-2)
+    # the residual addend epilogue: y + r (the shortcut gradient of the backward)
+    r = torch.randn_like(y, dtype=torch.float32).bfloat16().contiguous(memory_format=torch.channels_last)
+    ya = ops.conv3x3_fwd_rows(x, Wb, G, off, ld, K, r)
+    torch.testing.assert_close(ya.float(), (y.float() + r.float()).bfloat16().float(), rtol=1e-2, atol=2e-2)
     img = ops.fa_dgrad_image(Wb, ld, G, off, K, C)
     refi = w.flip(3, 4).permute(0, 2, 3, 4, 1).reshape(G * C, 3, 3, K).bfloat16()
     torch.testing.assert_close(img, refi, rtol=0, atol=0)
