@@ -492,8 +492,13 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
               "fa_bmm_rows: A [G, K, P], B [G, P, N] bf16");
   const int64_t G = A.size(0), K = A.size(1), P = A.size(2), N = B.size(2);
   const auto a16 = [](const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
-  if (A.stride(1) != 1 || B.stride(2) != 1 || K % 8 || N % 8 || A.stride(2) % 8 || A.stride(0) % 8 ||
-      B.stride(1) % 8 || B.stride(0) % 8 || !a16(A) || !a16(B) || ld % 4 || off % 4)
+  // N % 8 != 0 (the stem's 27 columns): the 16-byte chunk loads read up to
+  // round8(N) columns, which must stay inside the operand row (its padding:
+  // products of the columns past N are never stored)
+  const int64_t N8 = (N + 7) / 8 * 8;
+  if (A.stride(1) != 1 || B.stride(2) != 1 || K % 8 || A.stride(2) % 8 || A.stride(0) % 8 ||
+      B.stride(1) % 8 || B.stride(0) % 8 || !a16(A) || !a16(B) || ld % 4 || off % 4 ||
+      (N % 8 && (N8 > B.stride(1) || N8 > B.stride(0))))
     return false;
   check_rows(dst, ld, G, off, K * N, "fa_bmm_rows: dst");
   TORCH_CHECK(ld > 0, "fa_bmm_rows: per-client rows");
@@ -534,6 +539,10 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
   g.small = static_cast<int>(small);
   g.stage = (small == 1 || small == -2) ? 1 : 0;
   if (small == -2) g.small = 1;
+  if (N % 4) {  // the staged epilogue moves 16-byte row pieces: the MFMA-layout one
+    g.stage = 0;
+    g.small = 1;
+  }
   launch_gemm_tn_acc(g, stream_now());
   return true;
 }

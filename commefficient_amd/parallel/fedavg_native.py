@@ -215,7 +215,10 @@ class ResNet18FedAvg:
         step -- rows = beta rows + alpha A_g @ B_g in the GEMM's epilogue, then
         the bf16 mirror of the updated segment"""
         G, K, n = A.shape[0], A.shape[1], B.shape[2]
-        if cls._TN[0] and _ops().fa_bmm_rows(A, B, sink.dst, sink.ld, off, sink.beta, sink.alpha, sink.mirror,
+        # (the stem's 27 columns stay on hipBLASLt: its [64 x 27] products over
+        # 5,120 pixels are 100 one-tile blocks of 80 K-steps on the TN GEMM --
+        # 31.43 vs 31.15 ms per round, same-box A/B)
+        if cls._TN[0] and n % 8 == 0 and _ops().fa_bmm_rows(A, B, sink.dst, sink.ld, off, sink.beta, sink.alpha, sink.mirror,
                                              cls._TN[1], sink.src, sink.sld):
             return
         dst = sink.dst[:, off:off + K * n].view(G, K, n)
