@@ -1062,7 +1062,7 @@ __global__ void __launch_bounds__(512) conv_wgrad_wide_kernel(ConvWgradArgs a) {
 // for waves whose pieces start inside the window (wave-uniform), so a stage
 // holds 72 window rows and every wave has >= ALD + 2 DMA loads per stage.
 constexpr int kHaloWRows = 72;  // window rows staged per K-step (>= R * (W + 2) > 64)
-template <int NSTAGE, bool IL = true>
+template <int NSTAGE, bool IL = true, bool ROWS = false>
 __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int A_BYTES = BK * WBM * 2;         // [64 px][128 k], 256-byte rows
@@ -1216,8 +1216,54 @@ __global__ void __launch_bounds__(256) conv_wgrad_halo_kernel(ConvWgradArgs a) {
     wrs = wrs + 1 == NSTAGE ? 0 : wrs + 1;
   }
 
-  float* slab = a.slab + static_cast<size_t>(split) * K * 9 * C;
   const int hi = lane >> 5, lr = lane & 31;
+  if constexpr (ROWS) {
+    // the client rows directly (one split): output channel k is row k / kg's
+    // channel k % kg; with rows_sub (64-channel clients in pairs) the tile's
+    // 128 x 128 block holds two clients, and only the diagonal 64 x 64 blocks
+    // (input block tc == the wave's row half wr) are theirs -- wave-uniform.
+    // (A template variant of its own: the headline's slab epilogue keeps its
+    // register budget, 2 waves / SIMD.)
+    const int sb = a.rows_sub, kg = a.kg;
+    const int Cl = sb > 0 ? sb : C;
+    if (sb > 0 && tc != wr) return;
+    const int half = sb > 0 ? wr : 0;
+    const int64_t rowb = sb > 0 ? static_cast<int64_t>(k0 / kg) * (kg / sb) + half : -1;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 3; ++ni) {
+        const int n = wc * 96 + ni * 32 + lr;
+        const int tap = 3 * r + (n >> 6), c = c0 + (n & 63) - half * sb;
+#pragma unroll
+        for (int e0 = 0; e0 < 16; e0 += 4) {
+          // (the old values of a batch loaded before its stores: the mirror may
+          // alias the rows as far as the compiler knows)
+          float old[4];
+          int64_t o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = e0 + q;
+            const int k = k0 + wr * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+            const int kl = sb > 0 ? k % sb : k % kg;
+            const int64_t row = sb > 0 ? rowb : k / kg;
+            const int64_t in = (static_cast<int64_t>(kl) * 9 + tap) * Cl + c;
+            o[q] = row * a.rows_ld + in;
+            old[q] = a.rows_beta != 0.f
+                         ? (a.rows_src != nullptr ? a.rows_src[row * a.rows_sld + in] : a.rows[o[q]])
+                         : 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = a.rows_beta * old[q] + a.rows_alpha * acc[mi][ni][e0 + q];
+            a.rows[o[q]] = v;
+            if (a.rows_mirror != nullptr) a.rows_mirror[o[q]] = static_cast<uint16_t>(pack_bf16(v, 0.f));
+          }
+        }
+      }
+    return;
+  }
+  float* slab = a.slab + static_cast<size_t>(split) * K * 9 * C;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -1662,6 +1708,21 @@ void launch_conv3x3_wgrad_rows(ConvWgradArgs a, float* dst, int kg, int64_t ld, 
                                int64_t sld) {
   const int steps = (a.P + BK - 1) / BK;
   a.group_px = 0;
+  if (a.splits == 1 && rsc && wgrad_halo(a.H, a.W, a.K, a.C) && static_cast<int>(a.kg) == kg) {
+    // one split: the halo kernel's epilogue updates the rows (no slab, no
+    // reduction pass: 8 fewer bytes per weight; FedAvg round 31.46 -> 31.32 ms,
+    // same-box A/B)
+    a.rows = dst;
+    a.rows_ld = ld;
+    a.rows_sub = sub;
+    a.rows_beta = beta;
+    a.rows_alpha = alpha;
+    a.rows_mirror = mirror;
+    a.rows_src = wsrc;
+    a.rows_sld = sld;
+    launch_conv3x3_wgrad_steps(a, steps, stream);
+    return;
+  }
   launch_conv3x3_wgrad_steps(a, (steps + a.splits - 1) / a.splits, stream);
   launch_wgrad_reduce(a.slab, dst, a.K, a.C, a.splits, beta, int64_t{0}, 1, stream, kg, ld, rsc, sub, alpha,
                       mirror, wsrc, sld);
@@ -1682,9 +1743,13 @@ void launch_conv3x3_wgrad_steps(ConvWgradArgs a, int steps_per_split, hipStream_
     static bool init = false;
     if (!init) {
       set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2>), 2 * stage_bytes);
+      set_lds(reinterpret_cast<const void*>(conv_wgrad_halo_kernel<2, true, true>), 2 * stage_bytes);
       init = true;
     }
-    COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2>), dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
+    if (a.rows != nullptr)  // one split, the rows updated in the epilogue
+      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2, true, true>), dim3(tiles), dim3(256), 2 * stage_bytes, stream, a);
+    else
+      COMMEFF_LAUNCH((conv_wgrad_halo_kernel<2>), dim3(tiles * a.splits), dim3(256), 2 * stage_bytes, stream, a);
   } else if (wgrad_wide(a.K, a.C)) {
     if (rowstep) launch_wgrad_wide<true>(a, stream); else launch_wgrad_wide<false>(a, stream);
   } else if (a.C == 64) {  // tap pairs: 128-wide tiles (measured 158 -> see profiles/r1_experiments.md)

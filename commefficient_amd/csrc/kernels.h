@@ -297,6 +297,17 @@ struct ConvWgradArgs {
   // inside one group (0: ungrouped)
   int group_px = 0;
   int splits_per_group = 0;
+  // one split on the halo kernel (launch_conv3x3_wgrad_rows): the epilogue
+  // updates the client rows itself -- rows = beta src + alpha dW in (r, s, c)
+  // order, + the bf16 mirror -- instead of writing a slab for the reduction
+  // (rows_sub: the 64-channel clients' pairs, see conv_wgrad_reduce_kernel)
+  float* rows = nullptr;
+  int64_t rows_ld = 0;
+  int rows_sub = 0;
+  float rows_beta = 0.f, rows_alpha = 1.f;
+  uint16_t* rows_mirror = nullptr;
+  const float* rows_src = nullptr;
+  int64_t rows_sld = 0;
 };
 bool conv3x3_supported(int C, int K);
 bool conv3x3_pool_supported(int H, int W, int K);
