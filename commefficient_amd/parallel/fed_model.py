@@ -1312,17 +1312,17 @@ class FedModel:
             lm, am, sums = eng.run(self.w, x, y, Gp, n, bs, a.num_fedavg_epochs, self.fedavg_lr,
                                    a.fedavg_lr_decay, a.weight_decay / a.num_workers,
                                    a.max_grad_norm, out, first_pass=p0 == 0)
-            acc_bufs = sums if acc_bufs is None else [tuple(u + v for u, v in zip(p, q))
-                                                      for p, q in zip(acc_bufs, sums)]
+            acc_bufs = sums if acc_bufs is None else [p + q for p, q in zip(acc_bufs, sums)]
             loss_rows.append(lm)
             acc_rows.append(am)
             slot_rows.append(slots)
         with torch.no_grad():  # the clients' mean running statistics, written once
-            for b, (m1, m2, v1, v2) in zip(eng.blocks, acc_bufs):
-                b.m1.running_mean.copy_((m1 / len(mine)).to(b.m1.running_mean.dtype))
-                b.m2.running_mean.copy_((m2 / len(mine)).to(b.m2.running_mean.dtype))
-                b.m1.running_var.copy_((v1 / len(mine)).to(b.m1.running_var.dtype))
-                b.m2.running_var.copy_((v2 / len(mine)).to(b.m2.running_var.dtype))
+            for b, s4 in zip(eng.blocks, acc_bufs):
+                m1, m2, v1, v2 = (s4 / len(mine)).to(b.m1.running_mean.dtype).unbind(0)
+                b.m1.running_mean.copy_(m1)
+                b.m2.running_mean.copy_(m2)
+                b.m1.running_var.copy_(v1)
+                b.m2.running_var.copy_(v2)
             # num_batches_tracked: every BatchNorm layer counts the local steps
             # (the engine advanced the first layer's counter)
             nbt0 = eng.blocks[0].m1.num_batches_tracked

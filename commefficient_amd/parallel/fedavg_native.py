@@ -286,11 +286,17 @@ class ResNet18FedAvg:
             Gg = None
         else:
             Gg = torch.zeros((G, ld), device=dev, dtype=torch.float32)
-        # per-client running statistics (the model keeps their mean)
-        run = []
+        # per-client running statistics (the model keeps their mean): one
+        # [4, G, C] buffer per block (mean 1, mean 2, var 1, var 2), each slice
+        # a contiguous [G*C] copy per client -- one fill and one reduction per
+        # block instead of four of each
+        run, run_bufs = [], []
         for b in self.blocks:
-            run.append(tuple(m.running_mean.detach().float().repeat(G).contiguous() for m in (b.m1, b.m2))
-                       + tuple(m.running_var.detach().float().repeat(G).contiguous() for m in (b.m1, b.m2)))
+            src = torch.stack([b.m1.running_mean, b.m2.running_mean, b.m1.running_var,
+                               b.m2.running_var]).detach().float()
+            buf = src.unsqueeze(1).expand(4, G, src.shape[1]).contiguous()
+            run_bufs.append(buf)
+            run.append(tuple(buf[i].view(-1) for i in range(4)))
         nbt = self.blocks[0].m1.num_batches_tracked if first_pass else None
         loss_acc = torch.zeros(G, device=dev)
         acc_acc = torch.zeros(G, device=dev)
@@ -320,11 +326,9 @@ class ResNet18FedAvg:
                     ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip), lr_t, float(wd), Wb)
                 steps += 1
         ops.fa_upload(out, w0i, Wg, ld, G, float(n), perm)
-        # running statistics: per-client copies summed for the caller's mean
-        sums = []
-        for b, (rm1, rm2, rv1, rv2) in zip(self.blocks, run):
-            sums.append((rm1.view(G, -1).double().sum(0), rm2.view(G, -1).double().sum(0),
-                         rv1.view(G, -1).double().sum(0), rv2.view(G, -1).double().sum(0)))
+        # running statistics: per-client copies summed for the caller's mean,
+        # [4, C] fp64 per block (mean 1, mean 2, var 1, var 2)
+        sums = [torch.sum(buf, dim=1, dtype=torch.float64) for buf in run_bufs]
         return loss_acc / steps, acc_acc / steps, sums
 
     def _step(self, x, y, G, n, W, Wb, ld, sink, run, nbt, ones):
