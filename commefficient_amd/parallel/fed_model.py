@@ -1317,12 +1317,11 @@ class FedModel:
             acc_rows.append(am)
             slot_rows.append(slots)
         with torch.no_grad():  # the clients' mean running statistics, written once
+            dsts, srcs = [], []
             for b, s4 in zip(eng.blocks, acc_bufs):
-                m1, m2, v1, v2 = (s4 / len(mine)).to(b.m1.running_mean.dtype).unbind(0)
-                b.m1.running_mean.copy_(m1)
-                b.m2.running_mean.copy_(m2)
-                b.m1.running_var.copy_(v1)
-                b.m2.running_var.copy_(v2)
+                dsts += [b.m1.running_mean, b.m2.running_mean, b.m1.running_var, b.m2.running_var]
+                srcs += list((s4 / len(mine)).to(b.m1.running_mean.dtype).unbind(0))
+            torch._foreach_copy_(dsts, srcs)
             # num_batches_tracked: every BatchNorm layer counts the local steps
             # (the engine advanced the first layer's counter)
             nbt0 = eng.blocks[0].m1.num_batches_tracked
