@@ -279,11 +279,16 @@ struct MaxPoolGeom {
   FastDivU32 d_c8, d_w, d_h;  // output (fwd) or input (bwd) grid
 };
 
+// KK > 0: a compile-time k x k window whose KK*KK loads are all issued before
+// the first comparison (clamped addresses, validity applied at use; the
+// runtime-k loop waited for each load inside its bounds branch)
+template <int KK>
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16raw* __restrict__ x,
                                                           bf16raw* __restrict__ y,
                                                           uint8_t* __restrict__ codes, MaxPoolGeom q) {
   const uint32_t step = gridDim.x * blockDim.x;
   const int C8 = q.C / 8;
+  const int k = KK > 0 ? KK : q.k;
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < q.total; g += step) {
     const uint32_t pix = fdiv(g, q.d_c8);
     const int c8 = static_cast<int>(g - pix * C8);
@@ -300,25 +305,42 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16raw* __restr
       arg[e] = 0;
     }
     const int h0 = oh * q.s - q.p, w0 = ow * q.s - q.p;
-    for (int dy = 0; dy < q.k; ++dy) {
-      const int ih = h0 + dy;
-      if (ih < 0 || ih >= q.H) continue;
-      for (int dx = 0; dx < q.k; ++dx) {
-        const int iw = w0 + dx;
-        if (iw < 0 || iw >= q.W) continue;
-        const V8 v = *reinterpret_cast<const V8*>(
-            x + ((static_cast<size_t>(n) * q.H + ih) * q.W + iw) * q.C + c8 * 8);
-        const uint32_t code = static_cast<uint32_t>(dy * q.k + dx);
+    const bf16raw* xn = x + static_cast<size_t>(n) * q.H * q.W * q.C + c8 * 8;
+    auto take = [&](const V8& v, uint32_t code) __attribute__((always_inline)) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float f = bf2f(v.h[e]);
-          // first maximum in window order; a NaN wins and stays (PyTorch's rule)
-          if (first || f > best[e] || (f != f && best[e] == best[e])) {
-            best[e] = f;
-            arg[e] = code;
-          }
+      for (int e = 0; e < 8; ++e) {
+        const float f = bf2f(v.h[e]);
+        // first maximum in window order; a NaN wins and stays (PyTorch's rule)
+        if (first || f > best[e] || (f != f && best[e] == best[e])) {
+          best[e] = f;
+          arg[e] = code;
         }
-        first = false;
+      }
+      first = false;
+    };
+    if constexpr (KK > 0) {
+      V8 v[KK * KK];
+      bool ok[KK * KK];
+#pragma unroll
+      for (int t = 0; t < KK * KK; ++t) {
+        const int ih = h0 + t / KK, iw = w0 + t % KK;
+        ok[t] = ih >= 0 && ih < q.H && iw >= 0 && iw < q.W;
+        const int ihc = min(max(ih, 0), q.H - 1), iwc = min(max(iw, 0), q.W - 1);
+        v[t] = *reinterpret_cast<const V8*>(xn + (static_cast<size_t>(ihc) * q.W + iwc) * q.C);
+      }
+#pragma unroll
+      for (int t = 0; t < KK * KK; ++t)
+        if (ok[t]) take(v[t], static_cast<uint32_t>(t));
+    } else {
+      for (int dy = 0; dy < k; ++dy) {
+        const int ih = h0 + dy;
+        if (ih < 0 || ih >= q.H) continue;
+        for (int dx = 0; dx < k; ++dx) {
+          const int iw = w0 + dx;
+          if (iw < 0 || iw >= q.W) continue;
+          take(*reinterpret_cast<const V8*>(xn + (static_cast<size_t>(ih) * q.W + iw) * q.C),
+               static_cast<uint32_t>(dy * k + dx));
+        }
       }
     }
     V8 o;
@@ -333,6 +355,9 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16raw* __restr
   }
 }
 
+// NW > 0: at most NW x NW windows contain an input pixel (k = 3, s = 2: 2 x 2);
+// their code and gradient loads are all issued before the first use
+template <int NW>
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16raw* __restrict__ gy,
                                                           const uint8_t* __restrict__ codes,
                                                           bf16raw* __restrict__ gx, MaxPoolGeom q) {
@@ -354,15 +379,41 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16raw* __restr
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
-    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const uint32_t want = static_cast<uint32_t>((th - oh * q.s) * q.k + (tw - ow * q.s));
-        const size_t o = ((static_cast<size_t>(n) * q.OH + oh) * q.OW + ow) * q.C + c8 * 8;
-        const uint64_t cw = *reinterpret_cast<const uint64_t*>(codes + o);
-        const V8 v = *reinterpret_cast<const V8*>(gy + o);
+    const size_t nb = static_cast<size_t>(n) * q.OH * q.OW;
+    if constexpr (NW > 0) {
+      uint64_t cw[NW * NW];
+      V8 v[NW * NW];
+      bool ok[NW * NW];
+      uint32_t want[NW * NW];
+#pragma unroll
+      for (int t = 0; t < NW * NW; ++t) {
+        const int oh = oh_lo + t / NW, ow = ow_lo + t % NW;
+        ok[t] = oh <= oh_hi && ow <= ow_hi;
+        const int ohc = min(oh, q.OH - 1), owc = min(ow, q.OW - 1);
+        want[t] = static_cast<uint32_t>((th - oh * q.s) * q.k + (tw - ow * q.s));
+        const size_t o = (nb + static_cast<size_t>(ohc) * q.OW + owc) * q.C + c8 * 8;
+        cw[t] = *reinterpret_cast<const uint64_t*>(codes + o);
+        v[t] = *reinterpret_cast<const V8*>(gy + o);
+      }
+      // (window order, as the runtime loop: row-major over (oh, ow))
+#pragma unroll
+      for (int t = 0; t < NW * NW; ++t) {
+        if (!ok[t]) continue;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (((cw >> (8 * e)) & 0xffu) == want) acc[e] += bf2f(v.h[e]);
+          if (((cw[t] >> (8 * e)) & 0xffu) == want[t]) acc[e] += bf2f(v[t].h[e]);
+      }
+    } else {
+      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+          const uint32_t want = static_cast<uint32_t>((th - oh * q.s) * q.k + (tw - ow * q.s));
+          const size_t o = (nb + static_cast<size_t>(oh) * q.OW + ow) * q.C + c8 * 8;
+          const uint64_t cw = *reinterpret_cast<const uint64_t*>(codes + o);
+          const V8 v = *reinterpret_cast<const V8*>(gy + o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((cw >> (8 * e)) & 0xffu) == want) acc[e] += bf2f(v.h[e]);
+        }
       }
     }
     V8 out;
@@ -447,7 +498,10 @@ void launch_maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* codes, int N, i
   q.d_c8 = make_fastdiv(C / 8);
   q.d_w = make_fastdiv(q.OW);
   q.d_h = make_fastdiv(q.OH);
-  COMMEFF_LAUNCH(maxpool_fwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, x, y, codes, q);
+  if (k == 3)
+    COMMEFF_LAUNCH(maxpool_fwd_kernel<3>, dim3(blocks_for(total)), dim3(256), 0, stream, x, y, codes, q);
+  else
+    COMMEFF_LAUNCH(maxpool_fwd_kernel<0>, dim3(blocks_for(total)), dim3(256), 0, stream, x, y, codes, q);
 }
 
 void launch_maxpool_bwd(const uint16_t* gy, const uint8_t* codes, uint16_t* gx, int N, int H, int W, int C,
@@ -462,7 +516,10 @@ void launch_maxpool_bwd(const uint16_t* gy, const uint8_t* codes, uint16_t* gx, 
   q.d_c8 = make_fastdiv(C / 8);
   q.d_w = make_fastdiv(W);
   q.d_h = make_fastdiv(H);
-  COMMEFF_LAUNCH(maxpool_bwd_kernel, dim3(blocks_for(total)), dim3(256), 0, stream, gy, codes, gx, q);
+  if (k == 3 && s == 2)  // every input pixel in at most 2 x 2 windows
+    COMMEFF_LAUNCH(maxpool_bwd_kernel<2>, dim3(blocks_for(total)), dim3(256), 0, stream, gy, codes, gx, q);
+  else
+    COMMEFF_LAUNCH(maxpool_bwd_kernel<0>, dim3(blocks_for(total)), dim3(256), 0, stream, gy, codes, gx, q);
 }
 
 }  // namespace commeff

@@ -192,3 +192,22 @@ def test_resnet101_round_has_no_library_convs():
     assert not any("convolution" in n and "aten::" in n for n in names), sorted(
         n for n in names if "conv" in n)
     assert not any("max_pool" in n for n in names), sorted(n for n in names if "pool" in n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,s,p,H", [(3, 2, 1, 15), (3, 2, 1, 16), (2, 2, 0, 14), (3, 1, 1, 9)])
+def test_maxpool_fwd_bwd_match_torch(k, s, p, H):
+    """Native max-pool (k = 3 window loads all in flight; the runtime-k loop
+    otherwise) vs F.max_pool2d: values, and the gradient routed to the first
+    maximum of each window (PyTorch's rule)"""
+    ops = torch.ops.commeff
+    torch.manual_seed(0)
+    x = torch.randn(3, 64, H, H + 1, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y, codes = ops.maxpool_fwd(x, k, s, p)
+    xr = x.float().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(xr, k, s, p)
+    torch.testing.assert_close(y.float(), yr.detach(), rtol=0, atol=0)
+    gy = torch.randn_like(yr).bfloat16()
+    yr.backward(gy.float())
+    gx = ops.maxpool_bwd(gy.contiguous(memory_format=torch.channels_last), codes, H, H + 1, k, s, p)
+    torch.testing.assert_close(gx.float(), xr.grad, rtol=1e-2, atol=1e-2)
