@@ -127,10 +127,12 @@ def test_strided_1x1_native_subsample(N, C, H, W, K):
     assert torch.equal(x.grad[:, :, 1::2, :].float().abs().sum(), torch.tensor(0.0, device="cuda"))
 
 
-def test_im2col_layout():
+@pytest.mark.parametrize("H,W,data_input", [(11, 10, True), (150, 141, True), (37, 140, False)])
+def test_im2col_layout(H, W, data_input):
     """col[p][(r*S + s)*C + c] = x[n][c][oh*s - p + r][ow*s - p + s] (zero outside
-    and in the padding columns) -- against F.unfold."""
-    x, _ = _case_inputs(2, 3, 11, 10, 8, 7, True)
+    and in the padding columns) -- against F.unfold (4-channel and 3-channel
+    pixel strides, wide rows)."""
+    x, _ = _case_inputs(2, 3, H, W, 8, 7, data_input)
     col = cnn._ops().im2col(x, 7, 7, 2, 3, 152)
     u = F.unfold(x.float(), 7, padding=3, stride=2)  # [N, C*49, L] (c, r, s) order
     N, L = x.shape[0], u.shape[2]
