@@ -202,12 +202,15 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
           v = float4{a.beta * o[q].x + a.alpha * t.x, a.beta * o[q].y + a.alpha * t.y,
                      a.beta * o[q].z + a.alpha * t.z, a.beta * o[q].w + a.alpha * t.w};
         }
-        *reinterpret_cast<float4*>(cb + static_cast<int64_t>(m) * a.ldc + n) = v;
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+        f4v* cp = reinterpret_cast<f4v*>(cb + static_cast<int64_t>(m) * a.ldc + n);
+        const f4v vv = {v.x, v.y, v.z, v.w};
+        if (a.nt) __builtin_nontemporal_store(vv, cp); else *cp = vv;
         if (mb != nullptr) {
-          uint2 h;
-          h.x = pack_bf16(v.x, v.y);
-          h.y = pack_bf16(v.z, v.w);
-          *reinterpret_cast<uint2*>(mb + static_cast<int64_t>(m) * a.ldc + n) = h;
+          const u2v h = {pack_bf16(v.x, v.y), pack_bf16(v.z, v.w)};
+          u2v* mp = reinterpret_cast<u2v*>(mb + static_cast<int64_t>(m) * a.ldc + n);
+          if (a.nt) __builtin_nontemporal_store(h, mp); else *mp = h;
         }
       }
     }

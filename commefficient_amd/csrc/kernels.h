@@ -597,6 +597,7 @@ struct GemmTnArgs {
   int small = -1;                 // tile: -1 by shape, 0: 256 x 256, 1: 128 x 128
   const float* src = nullptr;     // beta scales src (group stride scg, 0: shared) instead of C
   int64_t scg = 0;
+  int nt = 0;                     // (staged epilogue) nontemporal stores
   int stage = 0;                  // 128 x 128, one split: C updated through LDS, 16 bytes a lane
                                   // (ldc, cg, mcg multiples of 4; C, mirror 16 / 8-byte aligned)
 };
