@@ -438,11 +438,18 @@ constexpr int halo_lds() { return HaloCfg<TBM>::kWinBytes + 2 * BN * 128; }
 // are pinned above the MFMAs of kk (sched_barrier), and the step's barrier
 // sits before the last sub-step's MFMAs, which overlap the next step's first
 // reads.
-template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
+// BT (grouped input gradient straight from the clients' weight rows,
+// parallel/fedavg_native.py): the weights are the CONV's rows [Kc][3][3][Cc]
+// per group (Kc = a.C, the dgrad's input channels; Cc = a.kg, its outputs),
+// read flipped: the B tile of (tap, 64-channel block) is staged k-major
+// ([64 k][128 c], 256-byte rows: the rows' own order) and its fragments come
+// from transposing LDS reads -- no transposed weight image per step.
+template <int TBM, bool POOL, bool SPLIT = false, int BN = 128, bool BT = false>
 __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1))
 __attribute__((amdgpu_waves_per_eu((TBM == 256 && !SPLIT) ? 4 : 1)))  // two 8-wave blocks per CU
 conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   static_assert(BN == 128 || (BN == 64 && !SPLIT && !POOL), "halo tile width");
+  static_assert(!BT || (BN == 128 && !SPLIT && !POOL), "transposed weight rows: 128-wide plain tiles");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
   // group g (split-K half) of this block: its own window + B ring
   const int half = SPLIT ? static_cast<int>(threadIdx.x) / (TBM * 2) : 0;
@@ -496,11 +503,23 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
     wsrc += (a.w_gs > 0 ? g * a.w_gs : int64_t{0}) - g * a.kg * 9 * static_cast<int64_t>(C);
   }
   int b_off[BLD];  // element offsets into a.w (< K * 9 * C)
+  const uint16_t* wbt = a.w;  // BT: this group's conv rows
+  int bt_c0 = 0;
 #pragma unroll
   for (int j = 0; j < BLD; ++j) {
     const int sl = j * NT + tid;
-    const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
-    b_off[j] = (n0 + row) * 9 * C + lc * 8;
+    if constexpr (BT) {  // [64 k rows][16 chunks of 8 c], transposed-read swizzle
+      const int row = sl >> 4, lc = (sl & 15) ^ sw_tr256(row);
+      b_off[j] = row * 9 * a.kg + lc * 8;
+    } else {
+      const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
+      b_off[j] = (n0 + row) * 9 * C + lc * 8;
+    }
+  }
+  if constexpr (BT) {
+    const int64_t g = n0 / a.kg;
+    wbt = a.w + (a.w_gs > 0 ? g * a.w_gs : int64_t{0});
+    bt_c0 = n0 - static_cast<int>(g) * a.kg;
   }
   auto issue_window = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
@@ -514,9 +533,16 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   // K-step s = cb * 9 + tap (channel block outer: one window per cb)
   auto issue_b = [&](int step) __attribute__((always_inline)) {
     unsigned char* base = smem + kHaloWinBytes + (step & 1) * (BN * 128) + wid * 1024;
-    const int boff = (step % 9) * C + (step / 9) * 64;
+    if constexpr (BT) {
+      // rows k = (step / 9) 64 + row, flipped tap 8 - step % 9, columns bt_c0..
+      const int64_t boff = static_cast<int64_t>(step / 9) * 64 * 9 * a.kg + (8 - step % 9) * a.kg + bt_c0;
 #pragma unroll
-    for (int j = 0; j < BLD; ++j) glds16(wsrc + (b_off[j] + boff), base + j * NT * 16);
+      for (int j = 0; j < BLD; ++j) glds16(wbt + (b_off[j] + boff), base + j * NT * 16);
+    } else {
+      const int boff = (step % 9) * C + (step / 9) * 64;
+#pragma unroll
+      for (int j = 0; j < BLD; ++j) glds16(wsrc + (b_off[j] + boff), base + j * NT * 16);
+    }
   };
 
   // this lane's output pixels (rows of the A fragments) -> padded window rows
@@ -539,10 +565,12 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
       for (int e = 0; e < 16; ++e) acc[mi][ni][e] = 0.f;
 
     int bB[NI];  // sub-step 0 B offsets; sub-step kk: ^ (kk << 5)
+    int tB[NI][2];  // BT: transposed-read offsets; sub-step kk: + kk 16 rows
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       const int row = wc * (BN / 2) + ni * 32 + lr;
       bB[ni] = row * 128 + ((hi ^ sw_rd128(row)) << 4);
+      if constexpr (BT) tr_offsets<256>(wc * (BN / 2) + ni * 32, lane, tB[ni]);
     }
     auto a_base = [&](int st, int (&bA)[2]) __attribute__((always_inline)) {
       const int tap = st % 9, dr = tap / 3 - 1, dc = tap % 3 - 1;
@@ -558,7 +586,12 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) fa[mi] = *reinterpret_cast<const bf16x8_t*>(smem + (bA[mi] ^ (kk << 5)));
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) fb[ni] = *reinterpret_cast<const bf16x8_t*>(sB + (bB[ni] ^ (kk << 5)));
+      for (int ni = 0; ni < NI; ++ni) {
+        if constexpr (BT)
+          fb[ni] = tr_read(sB + tB[ni][0] + kk * 16 * 256, sB + tB[ni][1] + kk * 16 * 256);
+        else
+          fb[ni] = *reinterpret_cast<const bf16x8_t*>(sB + (bB[ni] ^ (kk << 5)));
+      }
     };
     auto mma = [&](const bf16x8_t (&fa)[2], const bf16x8_t (&fb)[NI]) __attribute__((always_inline)) {
 #pragma unroll
@@ -1549,16 +1582,16 @@ bool halo_geom(int H, int W, int K, int TBM, HaloGeom* g, int BN = 128) {
   return g->NPW <= (TBM == 256 ? HaloCfg<256>::kMaxRows : HaloCfg<128>::kMaxRows);
 }
 
-template <int TBM, bool POOL, bool SPLIT = false, int BN = 128>
+template <int TBM, bool POOL, bool SPLIT = false, int BN = 128, bool BT = false>
 void launch_fwd_halo(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
   constexpr int lds = halo_lds<TBM, BN>() * (SPLIT ? 2 : 1);
   static bool init = false;
   if (!init) {
-    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, BT>), lds);
     init = true;
   }
   const int mt = (a.P + TBM - 1) / TBM;
-  COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN>), dim3(mt * (a.K / BN)),
+  COMMEFF_LAUNCH((conv_fwd_halo_kernel<TBM, POOL, SPLIT, BN, BT>), dim3(mt * (a.K / BN)),
                  dim3(TBM * 2 * (SPLIT ? 2 : 1)), lds, stream, a, hg);
 }
 
@@ -1574,6 +1607,12 @@ bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   HaloGeom hg;
+  if (a.w_bt) {  // input gradient from the conv's own weight rows (transposed B)
+    if (a.kg % 128 != 0 || a.w_gs == 0) return false;
+    if (halo_geom(a.H, a.W, a.K, 256, &hg)) { launch_fwd_halo<256, false, false, 128, true>(a, hg, stream); return true; }
+    if (halo_geom(a.H, a.W, a.K, 128, &hg)) { launch_fwd_halo<128, false, false, 128, true>(a, hg, stream); return true; }
+    return false;
+  }
   if (a.kg % 128 == 0) {
     if (halo_geom(a.H, a.W, a.K, 256, &hg)) { launch_fwd_halo<256, false>(a, hg, stream); return true; }
     if (halo_geom(a.H, a.W, a.K, 128, &hg)) { launch_fwd_halo<128, false>(a, hg, stream); return true; }

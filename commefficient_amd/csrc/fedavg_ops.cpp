@@ -192,11 +192,13 @@ at::Tensor fa_dgrad_image(const at::Tensor& Wb, int64_t ld, int64_t G, int64_t o
 // grouped stride-1 3x3 conv of channel-stacked x whose group-g weights are the
 // kg rows [kg][3][3][C] at w + off + g * ld (ld 0: every group the same rows)
 at::Tensor conv3x3_fwd_rows(const at::Tensor& x, const at::Tensor& w, int64_t G, int64_t off, int64_t ld,
-                            int64_t kg, const c10::optional<at::Tensor>& addend) {
+                            int64_t kg, const c10::optional<at::Tensor>& addend, bool bt) {
   check_cl_bf16(x, "conv3x3_fwd_rows: x");
   const int64_t N = x.size(0), GC = x.size(1), H = x.size(2), W = x.size(3);
   TORCH_CHECK(G >= 1 && GC % G == 0 && kg >= 1, "conv3x3_fwd_rows: channels not a multiple of G");
   const int64_t C = GC / G, K = G * kg;
+  // bt: x is a conv's output gradient and w that conv's rows [C][3][3][kg]
+  // (same element count per group as a [kg][3][3][C] image)
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && off >= 0 && ld >= 0 &&
                   (ld == 0 || off + kg * 9 * C <= ld) && (ld == 0 ? 0 : G - 1) * ld + off + kg * 9 * C <= w.numel(),
               "conv3x3_fwd_rows: weight rows out of range");
@@ -226,6 +228,7 @@ at::Tensor conv3x3_fwd_rows(const at::Tensor& x, const at::Tensor& w, int64_t G,
   a.x_stride = static_cast<int>(GC);
   a.kg = static_cast<int>(kg);
   a.w_gs = ld > 0 ? ld : -1;
+  a.w_bt = bt ? 1 : 0;
   if (a.P == 0) return y;
   if (!launch_conv3x3_fwd_grouped(a, stream_now())) return at::empty({0}, x.options());
   return y;
@@ -559,7 +562,8 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_upload(Tensor(a!) out, Tensor w0, Tensor W, int ld, int rows, float n, Tensor? perm=None) -> ()");
   m.def("fa_gather_rows(Tensor(a!) dst, Tensor(b!) dstb, Tensor src, Tensor perm) -> ()");
   m.def("fa_dgrad_image(Tensor Wb, int ld, int G, int off, int K, int C) -> Tensor");
-  m.def("conv3x3_fwd_rows(Tensor x, Tensor w, int G, int off, int ld, int kg, Tensor? addend=None) -> Tensor");
+  m.def("conv3x3_fwd_rows(Tensor x, Tensor w, int G, int off, int ld, int kg, Tensor? addend=None, "
+        "bool bt=False) -> Tensor");
   m.def("fa_head_fwd(Tensor x, int G) -> (Tensor, Tensor)");
   m.def("fa_head_bwd(Tensor df, Tensor codes, int H, int W) -> Tensor");
   m.def("fa_ew(Tensor a, Tensor? b, int mode) -> Tensor");

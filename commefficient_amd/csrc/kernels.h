@@ -278,6 +278,9 @@ struct ConvFwdArgs {
   // kg rows start at w + g * w_gs (per-client bf16 weight rows,
   // parallel/fedavg_native.py); < 0 = every group reads the same kg rows
   int64_t w_gs = 0;
+  // grouped input gradient (with w_gs != 0): w holds the CONV's weight rows
+  // [C][3][3][kg] per group, read flipped and transposed (conv_fwd_halo_kernel BT)
+  int w_bt = 0;
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]

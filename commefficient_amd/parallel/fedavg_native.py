@@ -188,6 +188,12 @@ class ResNet18FedAvg:
         # 2 x 118 MB of image per conv) measured 35.8 vs 36.3 ms per round
         # (8x8: 35.8 vs 35.9, kept on the halo kernel)
         if dy.shape[3] >= 8:
+            # 128-channel outputs: the halo kernel reads the conv's own rows
+            # through transposed B tiles (no flipped image per step)
+            if C % 128 == 0 and self._DGRAD_BT[0]:
+                dx = _ops().conv3x3_fwd_rows(dy, Wb, G, off, ldb, C, addend, True)
+                if dx.numel():
+                    return dx
             img = _ops().fa_dgrad_image(Wb, ldb, G, off, K, C)
             dx = _ops().conv3x3_fwd_rows(dy, img, G, 0, C * 9 * K if ldb else 0, C, addend)
             if dx.numel():
@@ -202,6 +208,9 @@ class ResNet18FedAvg:
         return dx
 
     _BMM_INTO = [True]
+    # (128-channel input gradients from the rows themselves: 29.72 vs 30.53 ms
+    # per round with the per-step flipped images, same-box A/B)
+    _DGRAD_BT = [True]
     # weight gradients / SGD updates on the native TN GEMM (gemm_tn.hip):
     # 128 x 128 tiles whose epilogue streams the updated rows and their bf16
     # mirror through LDS -- 32.4 ms per round vs 34.6 on hipBLASLt's baddbmm +

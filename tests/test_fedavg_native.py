@@ -258,6 +258,25 @@ def test_conv_rows_forward_and_dgrad_image(H, K, C):
     refi = w.flip(3, 4).permute(0, 2, 3, 4, 1).reshape(G * C, 3, 3, K).bfloat16()
     torch.testing.assert_close(img, refi, rtol=0, atol=0)
     assert ops.fa_dgrad_image(Wb[1].contiguous(), 0, G, off, K, C).shape == (C, 3, 3, K)
+    # the input gradient: through the image, and (C % 128 == 0) straight from
+    # the rows with the transposed B tiles -- vs the fp32 grouped dgrad
+    dy = _cs(torch.randn(G, n, K, H, H, device="cuda"), G)
+    gref = torch.nn.grad.conv2d_input(x.shape, w.reshape(G * K, C, 3, 3).bfloat16().float(), dy.float(),
+                                      padding=1, groups=G)
+    gs = gref.abs().max()
+    dx_img = ops.conv3x3_fwd_rows(dy, img, G, 0, C * 9 * K, C)
+    torch.testing.assert_close(dx_img.float() / gs, gref / gs, rtol=2e-2, atol=2e-2)
+    dx_bt = ops.conv3x3_fwd_rows(dy, Wb, G, off, ld, C, None, True)
+    if C % 128 == 0:
+        torch.testing.assert_close(dx_bt.float() / gs, gref / gs, rtol=2e-2, atol=2e-2)
+        assert torch.equal(dx_bt, dx_img)  # same products in the same order
+        # the first local step's shared row
+        dx0 = ops.conv3x3_fwd_rows(dy, Wb[0].contiguous(), G, off, 0, C, None, True)
+        g0 = torch.nn.grad.conv2d_input(x.shape, w[:1].expand(G, -1, -1, -1, -1).reshape(G * K, C, 3, 3)
+                                        .bfloat16().float(), dy.float(), padding=1, groups=G)
+        torch.testing.assert_close(dx0.float() / gs, g0 / gs, rtol=2e-2, atol=2e-2)
+    else:
+        assert dx_bt.numel() == 0  # (64-wide outputs: the image path)
 
 
 @pytest.mark.gpu
