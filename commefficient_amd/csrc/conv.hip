@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1))
 __attribute__((amdgpu_waves_per_eu((TBM == 256 && !SPLIT) ? 4 : 1)))  // two 8-wave blocks per CU
 conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   static_assert(BN == 128 || (BN == 64 && !SPLIT && !POOL), "halo tile width");
-  static_assert(!BT || (BN == 128 && !SPLIT && !POOL), "transposed weight rows: 128-wide plain tiles");
+  static_assert(!BT || (!SPLIT && !POOL), "transposed weight rows: plain tiles");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
   // group g (split-K half) of this block: its own window + B ring
   const int half = SPLIT ? static_cast<int>(threadIdx.x) / (TBM * 2) : 0;
@@ -508,8 +508,9 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
 #pragma unroll
   for (int j = 0; j < BLD; ++j) {
     const int sl = j * NT + tid;
-    if constexpr (BT) {  // [64 k rows][16 chunks of 8 c], transposed-read swizzle
-      const int row = sl >> 4, lc = (sl & 15) ^ sw_tr256(row);
+    if constexpr (BT) {  // [64 k rows][BN / 8 chunks of 8 c], transposed-read swizzle
+      const int row = BN == 128 ? sl >> 4 : sl >> 3;
+      const int lc = BN == 128 ? (sl & 15) ^ sw_tr256(row) : (sl & 7) ^ sw_tr128(row);
       b_off[j] = row * 9 * a.kg + lc * 8;
     } else {
       const int row = sl >> 3, lc = (sl & 7) ^ sw_rd128(row);
@@ -570,7 +571,7 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
     for (int ni = 0; ni < NI; ++ni) {
       const int row = wc * (BN / 2) + ni * 32 + lr;
       bB[ni] = row * 128 + ((hi ^ sw_rd128(row)) << 4);
-      if constexpr (BT) tr_offsets<256>(wc * (BN / 2) + ni * 32, lane, tB[ni]);
+      if constexpr (BT) tr_offsets<BN * 2>(wc * (BN / 2) + ni * 32, lane, tB[ni]);
     }
     auto a_base = [&](int st, int (&bA)[2]) __attribute__((always_inline)) {
       const int tap = st % 9, dr = tap / 3 - 1, dc = tap % 3 - 1;
@@ -588,7 +589,7 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         if constexpr (BT)
-          fb[ni] = tr_read(sB + tB[ni][0] + kk * 16 * 256, sB + tB[ni][1] + kk * 16 * 256);
+          fb[ni] = tr_read(sB + tB[ni][0] + kk * 16 * BN * 2, sB + tB[ni][1] + kk * 16 * BN * 2);
         else
           fb[ni] = *reinterpret_cast<const bf16x8_t*>(sB + (bB[ni] ^ (kk << 5)));
       }
@@ -1608,9 +1609,16 @@ bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream) {
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   HaloGeom hg;
   if (a.w_bt) {  // input gradient from the conv's own weight rows (transposed B)
-    if (a.kg % 128 != 0 || a.w_gs == 0) return false;
-    if (halo_geom(a.H, a.W, a.K, 256, &hg)) { launch_fwd_halo<256, false, false, 128, true>(a, hg, stream); return true; }
-    if (halo_geom(a.H, a.W, a.K, 128, &hg)) { launch_fwd_halo<128, false, false, 128, true>(a, hg, stream); return true; }
+    if (a.w_gs == 0) return false;
+    if (a.kg % 128 == 0) {
+      if (halo_geom(a.H, a.W, a.K, 256, &hg)) { launch_fwd_halo<256, false, false, 128, true>(a, hg, stream); return true; }
+      if (halo_geom(a.H, a.W, a.K, 128, &hg)) { launch_fwd_halo<128, false, false, 128, true>(a, hg, stream); return true; }
+      return false;
+    }
+    if (a.kg % 64 == 0 && halo_geom(a.H, a.W, a.K, 256, &hg, 64)) {
+      launch_fwd_halo<256, false, false, 64, true>(a, hg, stream);
+      return true;
+    }
     return false;
   }
   if (a.kg % 128 == 0) {

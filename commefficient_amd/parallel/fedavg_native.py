@@ -188,9 +188,9 @@ class ResNet18FedAvg:
         # 2 x 118 MB of image per conv) measured 35.8 vs 36.3 ms per round
         # (8x8: 35.8 vs 35.9, kept on the halo kernel)
         if dy.shape[3] >= 8:
-            # 128-channel outputs: the halo kernel reads the conv's own rows
-            # through transposed B tiles (no flipped image per step)
-            if C % 128 == 0 and self._DGRAD_BT[0]:
+            # the halo kernel reads the conv's own rows through transposed B
+            # tiles (no flipped image per step)
+            if C % 64 == 0 and self._DGRAD_BT[0]:
                 dx = _ops().conv3x3_fwd_rows(dy, Wb, G, off, ldb, C, addend, True)
                 if dx.numel():
                     return dx

@@ -267,7 +267,7 @@ def test_conv_rows_forward_and_dgrad_image(H, K, C):
     dx_img = ops.conv3x3_fwd_rows(dy, img, G, 0, C * 9 * K, C)
     torch.testing.assert_close(dx_img.float() / gs, gref / gs, rtol=2e-2, atol=2e-2)
     dx_bt = ops.conv3x3_fwd_rows(dy, Wb, G, off, ld, C, None, True)
-    if C % 128 == 0:
+    if C % 64 == 0:
         torch.testing.assert_close(dx_bt.float() / gs, gref / gs, rtol=2e-2, atol=2e-2)
         assert torch.equal(dx_bt, dx_img)  # same products in the same order
         # the first local step's shared row
@@ -275,8 +275,6 @@ def test_conv_rows_forward_and_dgrad_image(H, K, C):
         g0 = torch.nn.grad.conv2d_input(x.shape, w[:1].expand(G, -1, -1, -1, -1).reshape(G * K, C, 3, 3)
                                         .bfloat16().float(), dy.float(), padding=1, groups=G)
         torch.testing.assert_close(dx0.float() / gs, g0 / gs, rtol=2e-2, atol=2e-2)
-    else:
-        assert dx_bt.numel() == 0  # (64-wide outputs: the image path)
 
 
 @pytest.mark.gpu
