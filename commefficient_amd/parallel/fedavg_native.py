@@ -184,9 +184,8 @@ class ResNet18FedAvg:
         shortcut's gradient, fused into the halo kernel's epilogue)"""
         dx = torch.empty(0)
         # 4x4 maps: the column-image GEMM against the weight rows + col2im
-        # (no transposed weight image: 37 MB of column gradient instead of
-        # 2 x 118 MB of image per conv) measured 35.8 vs 36.3 ms per round
-        # (8x8: 35.8 vs 35.9, kept on the halo kernel)
+        # (35.8 vs 36.3 ms per round against the halo kernel on a flipped
+        # image; 29.69 vs 29.71 against the transposed-rows halo kernel)
         if dy.shape[3] >= 8:
             # the halo kernel reads the conv's own rows through transposed B
             # tiles (no flipped image per step)
