@@ -551,9 +551,53 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
   return true;
 }
 
+// out_g (bf16) = A_g op(B_g) (+ beta out_g) for the G clients on the native
+// MFMA GEMM (gemm.hip, group strides): A [G, M, K], B [G, N, K] (nt) or
+// [G, K, N] (nn), out [G, M, N], each with unit stride along its last dim (the
+// channel-stacked activations / column images and the weight rows as strided
+// views).  false (nothing written): a shape or layout the kernel does not take.
+bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, double beta) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && out.is_cuda() && A.scalar_type() == at::kBFloat16 &&
+                  B.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16 && A.dim() == 3 &&
+                  B.dim() == 3 && out.dim() == 3,
+              "fa_gemm: bf16 [G, ., .] operands");
+  const int64_t G = A.size(0), M = A.size(1), K = A.size(2), N = nn ? B.size(2) : B.size(1);
+  TORCH_CHECK(B.size(0) == G && out.size(0) == G && (nn ? B.size(1) : B.size(2)) == K && out.size(1) == M &&
+                  out.size(2) == N,
+              "fa_gemm: shapes");
+  const auto a16 = [](const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
+  if (A.stride(2) != 1 || B.stride(2) != 1 || out.stride(2) != 1 || !a16(A) || !a16(B) || !a16(out) ||
+      A.stride(1) % 8 || A.stride(0) % 8 || B.stride(1) % 8 || B.stride(0) % 8 || out.stride(1) % 8 ||
+      out.stride(0) % 8 || !gemm_supported(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), nn) ||
+      G * M * std::max(A.stride(1), out.stride(1)) >= (int64_t{1} << 31))
+    return false;
+  if (G == 0 || M == 0) return true;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  GemmArgs g{};
+  g.A = bf(A);
+  g.lda = A.stride(1);
+  g.B = bf(B);
+  g.ldb = B.stride(1);
+  g.C = out.data_ptr();
+  g.ldc = out.stride(1);
+  g.C2 = nullptr;
+  g.bias = nullptr;
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.K = static_cast<int>(K);
+  g.beta = static_cast<float>(beta);
+  g.G = static_cast<int>(G);
+  g.sa = A.stride(0);
+  g.sb = B.stride(0);
+  g.sc = out.stride(0);
+  launch_gemm(g, nn, 0, false, stream_now());
+  return true;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
+  m.def("fa_gemm(Tensor A, Tensor B, Tensor(a!) out, bool nn, float beta=0.) -> bool");
   m.def("fa_bmm_rows(Tensor A, Tensor B, Tensor(a!) dst, int ld, int off, float beta=1., float alpha=1., "
         "Tensor(b!)? mirror=None, int small=-1, Tensor? src=None, int sld=0) -> bool");
   m.def("fa_weight_image(Tensor W, int ld, int G, int off, int K, int C, int R, int Kc, int kind) -> Tensor");
@@ -584,6 +628,7 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("fa_weight_image", &fa_weight_image);
   m.impl("fa_bmm_rows", &fa_bmm_rows);
+  m.impl("fa_gemm", &fa_gemm);
   m.impl("fa_row_sgd", &fa_row_sgd);
   m.impl("fa_upload", &fa_upload);
   m.impl("fa_gather_rows", &fa_gather_rows);

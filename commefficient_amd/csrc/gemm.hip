@@ -72,14 +72,23 @@ struct MmCfg {
 };
 
 template <int BN, bool NN, int ACT, bool F32, bool ST = false>
-__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
   using Cfg = MmCfg<BN, NN>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NI = BN / 64, ALD = Cfg::ALD, BLD = Cfg::BLD;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, hi = lane >> 5, lr = lane & 31;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntn = a.N / BN;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntn = a0.N / BN;
+  GemmArgs a = a0;
+  if (a0.G > 1) {  // group of this block (its tiles are consecutive)
+    const int per_g = ((a0.M + Cfg::BM - 1) / Cfg::BM) * ntn;
+    const int grp = bid / per_g;
+    bid -= grp * per_g;
+    a.A += grp * a0.sa;
+    a.B += grp * a0.sb;
+    a.C = static_cast<unsigned char*>(a0.C) + grp * a0.sc * (F32 ? 4 : 2);
+  }
   const int m0 = (bid / ntn) * Cfg::BM, n0 = (bid % ntn) * BN;
   const int KT = a.K / GK;
   const uint16_t* zero = reinterpret_cast<const uint16_t*>(g_mm_zero);
@@ -313,7 +322,7 @@ void launch_gemm_t(const GemmArgs& a, hipStream_t stream) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     init = true;
   }
-  const int tiles = ((a.M + 127) / 128) * (a.N / BN);
+  const int tiles = ((a.M + 127) / 128) * (a.N / BN) * (a.G > 1 ? a.G : 1);
   COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32, ST>), dim3(tiles), dim3(256), lds, stream, a);
 }
 
@@ -330,7 +339,8 @@ void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stre
   // slower on the GPT-2 and ResNet-101 shapes: these GEMMs are one wave of
   // tiles whose load / store phases set the time; profiles/r4_experiments.md)
   // 128-wide column tiles when they still give ~every resident slot (2 per CU) a block
-  const bool wide = a.N % 128 == 0 && static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) >= 384;
+  const bool wide = a.N % 128 == 0 &&
+                    static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) * (a.G > 1 ? a.G : 1) >= 384;
   if (a.stats != nullptr && !nn && act == 0 && !f32) {  // BN moments in the epilogue (mm_nt_bnstats)
     if (wide) launch_gemm_t<128, false, 0, false, true>(a, stream);
     else launch_gemm_t<64, false, 0, false, true>(a, stream);

@@ -576,6 +576,10 @@ struct GemmArgs {
   // the tile's first row).  bf16 output without activation only.
   float* stats = nullptr;
   int stats_mg = 0;
+  // G independent products (the batched FedAvg clients' channel-stacked
+  // operands): group g reads A + g sa, B + g sb and writes C + g sc
+  int G = 1;
+  int64_t sa = 0, sb = 0, sc = 0;
 };
 bool gemm_supported(int M, int N, int K, bool nn);
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);

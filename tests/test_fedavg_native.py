@@ -335,6 +335,28 @@ def test_fa_bmm_rows_sgd_and_mirror(K, N, Nfull, o, P, small):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nn,M,N,K,shared", [(False, 320, 256, 1152, False), (False, 80, 128, 64, True),
+                                             (True, 1280, 576, 128, False), (True, 80, 2304, 256, True)])
+def test_fa_gemm_grouped(nn, M, N, K, shared):
+    """Grouped native GEMM over channel-stacked operands (strided views) vs
+    fp32 bmm, with beta accumulation and a shared (broadcast) weight row"""
+    torch.manual_seed(0)
+    G = 5
+    At = torch.randn(M, G, K, device="cuda").bfloat16()
+    A = At.transpose(0, 1)  # [G, M, K], strides (K, G K, 1)
+    shape = (G, K, N) if nn else (G, N, K)
+    B = torch.randn(1 if shared else G, *shape[1:], device="cuda").bfloat16()
+    B = B.expand(G, -1, -1) if shared else B
+    out_t = torch.randn(M, G, N, device="cuda").bfloat16()
+    out = out_t.transpose(0, 1)
+    old = out.float().clone()
+    assert _ops().fa_gemm(A, B, out, nn, 1.0)
+    ref = old + torch.bmm(A.float(), B.float() if nn else B.float().transpose(1, 2))
+    scale = ref.abs().max()
+    torch.testing.assert_close(out.float() / scale, ref / scale, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
 def test_ew_add_relu():
     a = torch.randn(2, 64, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     b = torch.randn_like(a)
