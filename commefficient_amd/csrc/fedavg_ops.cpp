@@ -489,7 +489,19 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
 // rows otherwise.  false (nothing written): a layout the kernel cannot read.
 bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64_t ld, int64_t off, double beta,
                  double alpha, const c10::optional<at::Tensor>& mirror, int64_t small,
-                 const c10::optional<at::Tensor>& src, int64_t sld) {
+                 const c10::optional<at::Tensor>& src, int64_t sld, const c10::optional<at::Tensor>& ximp) {
+  if (ximp.has_value() && ximp->defined()) {
+    // B = the implicit 3x3 / stride-1 / pad-1 column image of the
+    // channel-stacked ximp [n, G*C, H, W] (B itself is only a [G, P, 9C] shape
+    // carrier: any tensor of those sizes, e.g. an expanded view)
+    check_cl_bf16(*ximp, "fa_bmm_rows: ximp");
+    const int64_t G = A.size(0), C = ximp->size(1) / G, P = ximp->size(0) * ximp->size(2) * ximp->size(3);
+    TORCH_CHECK(ximp->size(1) == G * C && B.size(0) == G && B.size(1) == P && B.size(2) == 9 * C && A.size(2) == P,
+                "fa_bmm_rows: ximp shapes");
+    if (C % 8 || A.stride(1) != 1 || A.size(1) % 8 || A.stride(2) % 8 || A.stride(0) % 8 ||
+        reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 || ld % 4 || off % 4)
+      return false;
+  }
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 &&
                   A.dim() == 3 && B.dim() == 3 && A.size(0) == B.size(0) && A.size(2) == B.size(1),
               "fa_bmm_rows: A [G, K, P], B [G, P, N] bf16");
@@ -499,9 +511,10 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
   // round8(N) columns, which must stay inside the operand row (its padding:
   // products of the columns past N are never stored)
   const int64_t N8 = (N + 7) / 8 * 8;
-  if (A.stride(1) != 1 || B.stride(2) != 1 || K % 8 || A.stride(2) % 8 || A.stride(0) % 8 ||
-      B.stride(1) % 8 || B.stride(0) % 8 || !a16(A) || !a16(B) || ld % 4 || off % 4 ||
-      (N % 8 && (N8 > B.stride(1) || N8 > B.stride(0))))
+  const bool imp = ximp.has_value() && ximp->defined();
+  if (A.stride(1) != 1 || K % 8 || A.stride(2) % 8 || A.stride(0) % 8 || !a16(A) || ld % 4 || off % 4 ||
+      (!imp && (B.stride(2) != 1 || B.stride(1) % 8 || B.stride(0) % 8 || !a16(B) ||
+                (N % 8 && (N8 > B.stride(1) || N8 > B.stride(0))))))
     return false;
   check_rows(dst, ld, G, off, K * N, "fa_bmm_rows: dst");
   TORCH_CHECK(ld > 0, "fa_bmm_rows: per-client rows");
@@ -539,6 +552,14 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
   g.mcg = ld;
   g.src = sp != nullptr ? sp + off : nullptr;
   g.scg = sld;
+  if (ximp.has_value() && ximp->defined()) {
+    g.B = bf(*ximp);
+    g.ldb = ximp->size(1);  // G * C channels per pixel row
+    g.sb = ximp->size(1) / G;
+    g.imp_C = static_cast<int>(ximp->size(1) / G);
+    g.imp_H = static_cast<int>(ximp->size(2));
+    g.imp_W = static_cast<int>(ximp->size(3));
+  }
   g.small = static_cast<int>(small);
   g.stage = (small == 1 || small == -2) ? 1 : 0;
   if (small == -2) g.small = 1;
@@ -599,7 +620,7 @@ bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_gemm(Tensor A, Tensor B, Tensor(a!) out, bool nn, float beta=0.) -> bool");
   m.def("fa_bmm_rows(Tensor A, Tensor B, Tensor(a!) dst, int ld, int off, float beta=1., float alpha=1., "
-        "Tensor(b!)? mirror=None, int small=-1, Tensor? src=None, int sld=0) -> bool");
+        "Tensor(b!)? mirror=None, int small=-1, Tensor? src=None, int sld=0, Tensor? ximp=None) -> bool");
   m.def("fa_weight_image(Tensor W, int ld, int G, int off, int K, int C, int R, int Kc, int kind) -> Tensor");
   m.def("fa_row_sgd(Tensor(a!) W, int ld, Tensor src, int sld, Tensor G, int gld, int rows, int d, float clip, "
         "float lr, float wd, Tensor(b!)? Wb=None) -> ()");

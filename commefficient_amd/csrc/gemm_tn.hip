@@ -83,6 +83,20 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
     a_ptr[i] = reinterpret_cast<uint64_t>(gA + static_cast<int64_t>(pbeg + row) * a.lda + m0 + h * 128 + lc * 8);
     b_ptr[i] = reinterpret_cast<uint64_t>(gB + static_cast<int64_t>(pbeg + row) * a.ldb + n0 + h * 128 + lc * 8);
   }
+  // implicit column image: the chunk's tap (fixed: imp_C % 8 == 0) and its
+  // channel offset; the pixel shift is applied per step
+  int imp_dr[4], imp_dc[4], imp_co[4];
+  if (a.imp_C > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = SMALL ? 0 : i >> 1, sp = SMALL ? i * NTH + tid : (i & 1) * 512 + tid;
+      const int row = sp >> 4, lc = (sp & 15) ^ sw_tr256(row);
+      const int j = n0 + h * 128 + lc * 8, tap = j / a.imp_C;
+      imp_dr[i] = tap / 3 - 1;
+      imp_dc[i] = tap % 3 - 1;
+      imp_co[i] = j - tap * a.imp_C;
+    }
+  }
   auto issue = [&](int stage) __attribute__((always_inline)) {
     unsigned char* base = smem + stage * STG + wid * 1024;
 #pragma unroll
@@ -91,7 +105,16 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
       // (lane-linear LDS destination of the wave's 64 chunks of slot sp)
       const int dst = SMALL ? i * NTH * 16 : (i >> 1) * GHALF + (i & 1) * 8192;
       gl16(reinterpret_cast<const void*>(ok && a_in[i] ? a_ptr[i] : zero), base + dst);
-      gl16(reinterpret_cast<const void*>(ok && b_in[i] ? b_ptr[i] : zero), base + NH * GHALF + dst);
+      uint64_t bp = b_ptr[i];
+      bool bok = ok && b_in[i];
+      if (a.imp_C > 0) {
+        const int p = p_row[i], hw = a.imp_H * a.imp_W;
+        const int rem = p % hw, hh = rem / a.imp_W + imp_dr[i], ww = rem % a.imp_W + imp_dc[i];
+        bok = bok && hh >= 0 && hh < a.imp_H && ww >= 0 && ww < a.imp_W;
+        bp = reinterpret_cast<uint64_t>(gB + static_cast<int64_t>(p + imp_dr[i] * a.imp_W + imp_dc[i]) * a.ldb +
+                                        imp_co[i]);
+      }
+      gl16(reinterpret_cast<const void*>(bok ? bp : zero), base + NH * GHALF + dst);
       p_row[i] += GBK;
       a_ptr[i] += static_cast<uint64_t>(GBK) * a.lda * 2;
       b_ptr[i] += static_cast<uint64_t>(GBK) * a.ldb * 2;

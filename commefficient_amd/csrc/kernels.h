@@ -602,6 +602,11 @@ struct GemmTnArgs {
   uint16_t* mirror = nullptr;     // + bf16(C) at the same [m][n] (ldc), group stride mcg
   int64_t mcg = 0;
   int small = -1;                 // tile: -1 by shape, 0: 256 x 256, 1: 128 x 128
+  // imp_C > 0: B is the IMPLICIT 3x3 / stride-1 / pad-1 column image of the
+  // channel-stacked x (a.B; pixel rows ldb apart, group g at + g sb) of
+  // imp_H x imp_W images: column j = tap * imp_C + c reads pixel p shifted by
+  // the tap (zero outside the image) -- no column image in memory
+  int imp_C = 0, imp_H = 0, imp_W = 0;
   const float* src = nullptr;     // beta scales src (group stride scg, 0: shared) instead of C
   int64_t scg = 0;
   int nt = 0;                     // (staged epilogue) nontemporal stores

@@ -10,7 +10,7 @@ import torch.nn.functional as F
 
 from commefficient_amd import _ext
 from commefficient_amd.models.fixup import ResNet18
-from commefficient_amd.parallel.fedavg_native import ResNet18FedAvg
+from commefficient_amd.parallel.fedavg_native import ResNet18FedAvg, _gview
 from commefficient_amd.utils.args import parse_args
 
 
@@ -354,6 +354,30 @@ def test_fa_gemm_grouped(nn, M, N, K, shared):
     ref = old + torch.bmm(A.float(), B.float() if nn else B.float().transpose(1, 2))
     scale = ref.abs().max()
     torch.testing.assert_close(out.float() / scale, ref / scale, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,K,H,n", [(256, 256, 8, 5), (256, 256, 4, 5), (128, 256, 4, 2)])
+def test_fa_bmm_rows_implicit_column_image(C, K, H, n):
+    """The TN GEMM reading the 3x3 column image implicitly from the
+    channel-stacked x == the same update from the materialised im2col_grouped"""
+    torch.manual_seed(0)
+    G = 3
+    x = _cs(torch.randn(G, n, C, H, H, device="cuda"), G)
+    dy = _cs(torch.randn(G, n, K, H, H, device="cuda"), G)
+    ld, off = K * 9 * C + 64, 32
+    W0 = torch.randn(G, ld, device="cuda")
+    Wa, Wb_ = W0.clone(), W0.clone()
+    Ma = torch.zeros(G, ld, device="cuda", dtype=torch.bfloat16)
+    Mb = torch.zeros_like(Ma)
+    ops = _ops()
+    A = _gview(dy, G).transpose(1, 2)
+    col = ops.im2col_grouped(x, G, 3, 3, 1, 1, 9 * C, False)
+    assert ops.fa_bmm_rows(A, col.transpose(0, 1), Wa, ld, off, 0.99, -0.1, Ma, 1)
+    shape = torch.empty((1, 1, 1), device="cuda", dtype=torch.bfloat16).expand(G, n * H * H, 9 * C)
+    assert ops.fa_bmm_rows(A, shape, Wb_, ld, off, 0.99, -0.1, Mb, 1, None, 0, x)
+    torch.testing.assert_close(Wb_, Wa, rtol=1e-5, atol=1e-5)
+    assert torch.equal(Mb, Ma) or (Mb.float() - Ma.float()).abs().max() < 1e-2
 
 
 @pytest.mark.gpu
