@@ -275,9 +275,11 @@ class ResNet18FedAvg:
             _ops().fa_cast_rows(sink.mirror, sink.dst, sink.ld, sink.dst.shape[0], off, n)
 
     def _conv3_wgrad(self, dy, x, G, sink, off, K, C):
-        # 8x8 / 4x4 maps: 5 or 2 K-steps of pixels per 256 x 256 wide-kernel
-        # tile -- the column-image GEMM measured faster (36.5 vs 38.4 ms/round)
-        if x.shape[3] >= 16 and _ops().conv3x3_wgrad_rows(dy, x, G, sink.dst, sink.ld, off, True, sink.beta,
+        # 32x32 maps on the grouped halo wgrad; 16x16 and smaller on the TN
+        # GEMM over the implicit column image (27.59 vs 27.97 ms per round with
+        # the halo kernel on 16x16 too, 27.88 with the TN GEMM on 32x32 too;
+        # the wide wgrad kernel on 8x8 / 4x4 had measured 38.4 vs 36.5)
+        if x.shape[3] >= 32 and _ops().conv3x3_wgrad_rows(dy, x, G, sink.dst, sink.ld, off, True, sink.beta,
                                                           sink.alpha, sink.mirror, sink.src, sink.sld):
             return
         A = _gview(dy, G).transpose(1, 2)
