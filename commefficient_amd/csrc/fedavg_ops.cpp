@@ -590,7 +590,7 @@ bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, 
   if (A.stride(2) != 1 || B.stride(2) != 1 || out.stride(2) != 1 || !a16(A) || !a16(B) || !a16(out) ||
       A.stride(1) % 8 || A.stride(0) % 8 || B.stride(1) % 8 || B.stride(0) % 8 || out.stride(1) % 8 ||
       out.stride(0) % 8 || !gemm_supported(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), nn) ||
-      G * M * std::max(A.stride(1), out.stride(1)) >= (int64_t{1} << 31))
+      M >= (int64_t{1} << 31))  // (element offsets are 64-bit in the kernel)
     return false;
   if (G == 0 || M == 0) return true;
   c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());

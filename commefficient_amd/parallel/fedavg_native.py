@@ -378,15 +378,26 @@ class ResNet18FedAvg:
         the sink (gradient rows, or the in-place SGD step)."""
         ops = _ops()
         # ---- stem: grouped column image of the client-major input (9 C0 = 27
-        # columns padded to 32; the GEMMs read the first 27)
+        # columns zero-padded to 64: the forward is the native grouped GEMM
+        # against a 64-column copy of the weight rows; the weight update reads
+        # the first 27)
         C0, K0 = self.cin0, self.c0
-        Kc0 = (9 * C0 + 7) // 8 * 8
+        Kc0 = (9 * C0 + 63) // 64 * 64 if _NATIVE_GMM[0] else (9 * C0 + 7) // 8 * 8
         col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
         col0g = col0.transpose(0, 1)[:, :, :9 * C0]
         H, Wd = x.shape[2], x.shape[3]
         y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
                          memory_format=torch.channels_last)
-        torch.bmm(col0g, self._rows(Wb, ld, G, self.prep, K0, 9 * C0).transpose(1, 2), out=_gview(y0, G))
+        w0rows = self._rows(Wb, ld, G, self.prep, K0, 9 * C0)
+        done = False
+        if _NATIVE_GMM[0] and Kc0 % 64 == 0:
+            pad = getattr(self, "_stem_img", None)
+            if pad is None or pad.shape != (G, K0, Kc0) or pad.device != x.device:
+                pad = self._stem_img = torch.zeros((G, K0, Kc0), device=x.device, dtype=torch.bfloat16)
+            pad[:, :, :9 * C0].copy_(w0rows)  # (the padding columns stay zero)
+            done = ops.fa_gemm(col0.transpose(0, 1), pad, _gview(y0, G), False, 0.0)
+        if not done:
+            torch.bmm(col0g, w0rows.transpose(1, 2), out=_gview(y0, G))
         a = ops.fa_ew(y0, None, 1)
         a0 = a
         saved = []
