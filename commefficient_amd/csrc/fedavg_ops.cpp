@@ -489,14 +489,20 @@ bool conv3x3_wgrad_rows(const at::Tensor& dy, const at::Tensor& x, int64_t G, at
 // rows otherwise.  false (nothing written): a layout the kernel cannot read.
 bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64_t ld, int64_t off, double beta,
                  double alpha, const c10::optional<at::Tensor>& mirror, int64_t small,
-                 const c10::optional<at::Tensor>& src, int64_t sld, const c10::optional<at::Tensor>& ximp) {
+                 const c10::optional<at::Tensor>& src, int64_t sld, const c10::optional<at::Tensor>& ximp,
+                 int64_t R, int64_t stride, int64_t pad) {
+  int64_t OH = 0, OW = 0;
   if (ximp.has_value() && ximp->defined()) {
-    // B = the implicit 3x3 / stride-1 / pad-1 column image of the
-    // channel-stacked ximp [n, G*C, H, W] (B itself is only a [G, P, 9C] shape
-    // carrier: any tensor of those sizes, e.g. an expanded view)
+    // B = the implicit R x R / stride / pad column image of the
+    // channel-stacked ximp [n, G*C, H, W] (B itself is only a [G, P, R*R*C]
+    // shape carrier: any tensor of those sizes, e.g. an expanded view)
     check_cl_bf16(*ximp, "fa_bmm_rows: ximp");
-    const int64_t G = A.size(0), C = ximp->size(1) / G, P = ximp->size(0) * ximp->size(2) * ximp->size(3);
-    TORCH_CHECK(ximp->size(1) == G * C && B.size(0) == G && B.size(1) == P && B.size(2) == 9 * C && A.size(2) == P,
+    TORCH_CHECK(R >= 1 && stride >= 1 && pad >= 0, "fa_bmm_rows: geometry");
+    OH = (ximp->size(2) + 2 * pad - R) / stride + 1;
+    OW = (ximp->size(3) + 2 * pad - R) / stride + 1;
+    const int64_t G = A.size(0), C = ximp->size(1) / G, P = ximp->size(0) * OH * OW;
+    TORCH_CHECK(ximp->size(1) == G * C && B.size(0) == G && B.size(1) == P && B.size(2) == R * R * C &&
+                    A.size(2) == P,
                 "fa_bmm_rows: ximp shapes");
     if (C % 8 || A.stride(1) != 1 || A.size(1) % 8 || A.stride(2) % 8 || A.stride(0) % 8 ||
         reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 || ld % 4 || off % 4)
@@ -559,6 +565,11 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
     g.imp_C = static_cast<int>(ximp->size(1) / G);
     g.imp_H = static_cast<int>(ximp->size(2));
     g.imp_W = static_cast<int>(ximp->size(3));
+    g.imp_OH = static_cast<int>(OH);
+    g.imp_OW = static_cast<int>(OW);
+    g.imp_R = static_cast<int>(R);
+    g.imp_s = static_cast<int>(stride);
+    g.imp_pad = static_cast<int>(pad);
   }
   g.small = static_cast<int>(small);
   g.stage = (small == 1 || small == -2) ? 1 : 0;
@@ -577,7 +588,8 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
 // [G, K, N] (nn), out [G, M, N], each with unit stride along its last dim (the
 // channel-stacked activations / column images and the weight rows as strided
 // views).  false (nothing written): a shape or layout the kernel does not take.
-bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, double beta) {
+bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, double beta,
+             const c10::optional<at::Tensor>& ximp, int64_t R, int64_t stride, int64_t pad) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && out.is_cuda() && A.scalar_type() == at::kBFloat16 &&
                   B.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16 && A.dim() == 3 &&
                   B.dim() == 3 && out.dim() == 3,
@@ -587,8 +599,21 @@ bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, 
                   out.size(2) == N,
               "fa_gemm: shapes");
   const auto a16 = [](const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; };
-  if (A.stride(2) != 1 || B.stride(2) != 1 || out.stride(2) != 1 || !a16(A) || !a16(B) || !a16(out) ||
-      A.stride(1) % 8 || A.stride(0) % 8 || B.stride(1) % 8 || B.stride(0) % 8 || out.stride(1) % 8 ||
+  // ximp (NT only): A is the implicit R x R / stride / pad column image of the
+  // channel-stacked ximp [n, G*C, H, W] (A: a [G, M, R*R*C] shape carrier)
+  const bool imp = ximp.has_value() && ximp->defined();
+  int64_t iC = 0, iOH = 0, iOW = 0;
+  if (imp) {
+    check_cl_bf16(*ximp, "fa_gemm: ximp");
+    iC = ximp->size(1) / G;
+    iOH = (ximp->size(2) + 2 * pad - R) / stride + 1;
+    iOW = (ximp->size(3) + 2 * pad - R) / stride + 1;
+    TORCH_CHECK(!nn && ximp->size(1) == G * iC && K == R * R * iC && M == ximp->size(0) * iOH * iOW,
+                "fa_gemm: ximp geometry");
+    if (iC % 64 || !a16(*ximp)) return false;
+  }
+  if ((!imp && (A.stride(2) != 1 || !a16(A) || A.stride(1) % 8 || A.stride(0) % 8)) || B.stride(2) != 1 ||
+      out.stride(2) != 1 || !a16(B) || !a16(out) || B.stride(1) % 8 || B.stride(0) % 8 || out.stride(1) % 8 ||
       out.stride(0) % 8 || !gemm_supported(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), nn) ||
       M >= (int64_t{1} << 31))  // (element offsets are 64-bit in the kernel)
     return false;
@@ -611,6 +636,19 @@ bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, 
   g.sa = A.stride(0);
   g.sb = B.stride(0);
   g.sc = out.stride(0);
+  if (imp) {
+    g.A = bf(*ximp);
+    g.lda = ximp->size(1);  // pixel row: G * C channels
+    g.sa = iC;
+    g.imp_C = static_cast<int>(iC);
+    g.imp_H = static_cast<int>(ximp->size(2));
+    g.imp_W = static_cast<int>(ximp->size(3));
+    g.imp_OH = static_cast<int>(iOH);
+    g.imp_OW = static_cast<int>(iOW);
+    g.imp_R = static_cast<int>(R);
+    g.imp_s = static_cast<int>(stride);
+    g.imp_pad = static_cast<int>(pad);
+  }
   launch_gemm(g, nn, 0, false, stream_now());
   return true;
 }
@@ -618,9 +656,11 @@ bool fa_gemm(const at::Tensor& A, const at::Tensor& B, at::Tensor out, bool nn, 
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
-  m.def("fa_gemm(Tensor A, Tensor B, Tensor(a!) out, bool nn, float beta=0.) -> bool");
+  m.def("fa_gemm(Tensor A, Tensor B, Tensor(a!) out, bool nn, float beta=0., Tensor? ximp=None, int R=3, "
+        "int stride=1, int pad=1) -> bool");
   m.def("fa_bmm_rows(Tensor A, Tensor B, Tensor(a!) dst, int ld, int off, float beta=1., float alpha=1., "
-        "Tensor(b!)? mirror=None, int small=-1, Tensor? src=None, int sld=0, Tensor? ximp=None) -> bool");
+        "Tensor(b!)? mirror=None, int small=-1, Tensor? src=None, int sld=0, Tensor? ximp=None, int R=3, "
+        "int stride=1, int pad=1) -> bool");
   m.def("fa_weight_image(Tensor W, int ld, int G, int off, int K, int C, int R, int Kc, int kind) -> Tensor");
   m.def("fa_row_sgd(Tensor(a!) W, int ld, Tensor src, int sld, Tensor G, int gld, int rows, int d, float clip, "
         "float lr, float wd, Tensor(b!)? Wb=None) -> ()");

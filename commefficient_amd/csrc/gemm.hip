@@ -71,7 +71,7 @@ struct MmCfg {
   static constexpr int LDS = 2 * STAGE > EPI ? 2 * STAGE : EPI;
 };
 
-template <int BN, bool NN, int ACT, bool F32, bool ST = false>
+template <int BN, bool NN, int ACT, bool F32, bool ST = false, bool IMP = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
   using Cfg = MmCfg<BN, NN>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -95,10 +95,20 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
 
   // A pieces: slot s = i*256 + tid -> (row s >> 3, swizzled chunk)
   const uint16_t* a_ptr[ALD];
+  int imp_h0[ALD], imp_w0[ALD];  // IMP: the output pixel's input origin (oh s - pad, ow s - pad)
 #pragma unroll
   for (int i = 0; i < ALD; ++i) {
     const int s = i * 256 + tid, row = s >> 3, lc = (s & 7) ^ sw_rd128(row);
-    a_ptr[i] = m0 + row < a.M ? a.A + static_cast<int64_t>(m0 + row) * a.lda + lc * 8 : nullptr;
+    if constexpr (IMP) {
+      const int p = m0 + row, ohw = a.imp_OH * a.imp_OW;
+      const int n = p / ohw, rem = p - n * ohw, oh = rem / a.imp_OW, ow = rem - oh * a.imp_OW;
+      imp_h0[i] = oh * a.imp_s - a.imp_pad;
+      imp_w0[i] = ow * a.imp_s - a.imp_pad;
+      // image n's first pixel row (+ this lane's channel chunk)
+      a_ptr[i] = p < a.M ? a.A + static_cast<int64_t>(n) * a.imp_H * a.imp_W * a.lda + lc * 8 : nullptr;
+    } else {
+      a_ptr[i] = m0 + row < a.M ? a.A + static_cast<int64_t>(m0 + row) * a.lda + lc * 8 : nullptr;
+    }
   }
   const uint16_t* b_ptr[BLD];
 #pragma unroll
@@ -116,8 +126,19 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
   }
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
     unsigned char* base = smem + stage * Cfg::STAGE + wid * 1024;
+    if constexpr (IMP) {
+      const int k0 = kt * GK, tap = k0 / a.imp_C, c0 = k0 - tap * a.imp_C;
+      const int r = tap / a.imp_R, t = tap - r * a.imp_R;
 #pragma unroll
-    for (int i = 0; i < ALD; ++i) mm_glds16(a_ptr[i] != nullptr ? a_ptr[i] + kt * GK : zero, base + i * 4096);
+      for (int i = 0; i < ALD; ++i) {
+        const int ih = imp_h0[i] + r, iw = imp_w0[i] + t;
+        const bool ok = a_ptr[i] != nullptr && ih >= 0 && ih < a.imp_H && iw >= 0 && iw < a.imp_W;
+        mm_glds16(ok ? a_ptr[i] + (static_cast<int64_t>(ih) * a.imp_W + iw) * a.lda + c0 : zero, base + i * 4096);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < ALD; ++i) mm_glds16(a_ptr[i] != nullptr ? a_ptr[i] + kt * GK : zero, base + i * 4096);
+    }
 #pragma unroll
     for (int j = 0; j < BLD; ++j) {
       const uint16_t* src = NN ? b_ptr[j] + static_cast<int64_t>(kt) * GK * a.ldb : b_ptr[j] + kt * GK;
@@ -313,17 +334,17 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
   }
 }
 
-template <int BN, bool NN, int ACT, bool F32, bool ST = false>
+template <int BN, bool NN, int ACT, bool F32, bool ST = false, bool IMP = false>
 void launch_gemm_t(const GemmArgs& a, hipStream_t stream) {
   constexpr int lds = MmCfg<BN, NN>::LDS;
   static bool init = false;
   if (!init) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<BN, NN, ACT, F32, ST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_kernel<BN, NN, ACT, F32, ST, IMP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     init = true;
   }
   const int tiles = ((a.M + 127) / 128) * (a.N / BN) * (a.G > 1 ? a.G : 1);
-  COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32, ST>), dim3(tiles), dim3(256), lds, stream, a);
+  COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32, ST, IMP>), dim3(tiles), dim3(256), lds, stream, a);
 }
 
 }  // namespace
@@ -341,6 +362,11 @@ void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stre
   // 128-wide column tiles when they still give ~every resident slot (2 per CU) a block
   const bool wide = a.N % 128 == 0 &&
                     static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) * (a.G > 1 ? a.G : 1) >= 384;
+  if (a.imp_C > 0) {  // implicit column image A (NT, bf16 out, no activation)
+    if (wide) launch_gemm_t<128, false, 0, false, false, true>(a, stream);
+    else launch_gemm_t<64, false, 0, false, false, true>(a, stream);
+    return;
+  }
   if (a.stats != nullptr && !nn && act == 0 && !f32) {  // BN moments in the epilogue (mm_nt_bnstats)
     if (wide) launch_gemm_t<128, false, 0, false, true>(a, stream);
     else launch_gemm_t<64, false, 0, false, true>(a, stream);

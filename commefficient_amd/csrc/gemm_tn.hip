@@ -92,8 +92,8 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
       const int h = SMALL ? 0 : i >> 1, sp = SMALL ? i * NTH + tid : (i & 1) * 512 + tid;
       const int row = sp >> 4, lc = (sp & 15) ^ sw_tr256(row);
       const int j = n0 + h * 128 + lc * 8, tap = j / a.imp_C;
-      imp_dr[i] = tap / 3 - 1;
-      imp_dc[i] = tap % 3 - 1;
+      imp_dr[i] = tap / a.imp_R;  // kernel row / column of the tap
+      imp_dc[i] = tap % a.imp_R;
       imp_co[i] = j - tap * a.imp_C;
     }
   }
@@ -108,11 +108,15 @@ __global__ void __launch_bounds__(SMALL ? 256 : 512) gemm_tn_acc_kernel(GemmTnAr
       uint64_t bp = b_ptr[i];
       bool bok = ok && b_in[i];
       if (a.imp_C > 0) {
-        const int p = p_row[i], hw = a.imp_H * a.imp_W;
-        const int rem = p % hw, hh = rem / a.imp_W + imp_dr[i], ww = rem % a.imp_W + imp_dc[i];
+        // output pixel p -> input pixel (n, oh s - pad + r, ow s - pad + t)
+        const int OH = a.imp_OH > 0 ? a.imp_OH : a.imp_H, OW = a.imp_OW > 0 ? a.imp_OW : a.imp_W;
+        const int p = p_row[i], ohw = OH * OW;
+        const int n = p / ohw, rem = p - n * ohw, oh = rem / OW, ow = rem - oh * OW;
+        const int hh = oh * a.imp_s - a.imp_pad + imp_dr[i], ww = ow * a.imp_s - a.imp_pad + imp_dc[i];
         bok = bok && hh >= 0 && hh < a.imp_H && ww >= 0 && ww < a.imp_W;
-        bp = reinterpret_cast<uint64_t>(gB + static_cast<int64_t>(p + imp_dr[i] * a.imp_W + imp_dc[i]) * a.ldb +
-                                        imp_co[i]);
+        bp = reinterpret_cast<uint64_t>(
+            gB + (static_cast<int64_t>(n) * a.imp_H * a.imp_W + static_cast<int64_t>(hh) * a.imp_W + ww) * a.ldb +
+            imp_co[i]);
       }
       gl16(reinterpret_cast<const void*>(bok ? bp : zero), base + NH * GHALF + dst);
       p_row[i] += GBK;

@@ -580,6 +580,11 @@ struct GemmArgs {
   // operands): group g reads A + g sa, B + g sb and writes C + g sc
   int G = 1;
   int64_t sa = 0, sb = 0, sc = 0;
+  // imp_C > 0 (NT only): A is the IMPLICIT column image of the channels-last x
+  // (a.A; pixel rows lda apart, group offset sa) of imp_H x imp_W images, an
+  // imp_R x imp_R conv with stride imp_s / pad imp_pad onto imp_OH x imp_OW:
+  // column k = tap * imp_C + c (imp_C % 64 == 0: a K-step stays in one tap)
+  int imp_C = 0, imp_H = 0, imp_W = 0, imp_OH = 0, imp_OW = 0, imp_R = 3, imp_s = 1, imp_pad = 1;
 };
 bool gemm_supported(int M, int N, int K, bool nn);
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);
@@ -607,6 +612,9 @@ struct GemmTnArgs {
   // imp_H x imp_W images: column j = tap * imp_C + c reads pixel p shifted by
   // the tap (zero outside the image) -- no column image in memory
   int imp_C = 0, imp_H = 0, imp_W = 0;
+  // (output grid / conv geometry of the implicit image; 0: same as the input,
+  // 3x3, stride 1, pad 1)
+  int imp_OH = 0, imp_OW = 0, imp_R = 3, imp_s = 1, imp_pad = 1;
   const float* src = nullptr;     // beta scales src (group stride scg, 0: shared) instead of C
   int64_t scg = 0;
   int nt = 0;                     // (staged epilogue) nontemporal stores

@@ -77,6 +77,11 @@ def _gmm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, nn: bool, beta: fl
         torch.bmm(A, Bm, out=out)
 
 
+def _carrier(x: torch.Tensor, G: int, P: int, N: int) -> torch.Tensor:
+    """A [G, P, N] bf16 shape carrier (no storage) for an implicit column image"""
+    return torch.empty((1, 1, 1), device=x.device, dtype=torch.bfloat16).expand(G, P, N)
+
+
 class _Sink:
     """Where one local step's weight gradients go: rows ``dst`` (ld apart)
     receive ``beta * dst + alpha * grad`` -- the gradient rows (beta 0, alpha
@@ -296,6 +301,9 @@ class ResNet18FedAvg:
     # (8x8 / 4x4 weight updates reading the column image implicitly: 28.44 vs
     # 29.50 ms per round with im2col_grouped + the column-image TN GEMM, same-box A/B)
     _IMPLICIT = [True]
+    # (the stride-2 convs + shortcuts forward and weight updates over the
+    # implicit column image: 28.34 vs 28.60 ms per round with im2col, same-box A/B)
+    _IMP_STRIDED = [True]
 
     # ------------------------------------------------------------- round
     def run(self, w0: torch.Tensor, x: torch.Tensor, y: torch.Tensor, G: int, n: int, bs: int,
@@ -409,17 +417,24 @@ class ResNet18FedAvg:
                 h1 = self._conv3(xin, Wb, ld, G, b.conv1, b.cout, b.cin)
                 sc = xin
             else:
-                colx = ops.im2col_grouped(xin, G, 3, 3, 2, 1, 9 * b.cin, False)
                 nn_, _, Hi, Wi = xin.shape
                 Ho, Wo = (Hi - 1) // 2 + 1, (Wi - 1) // 2 + 1
                 h1 = torch.empty((nn_, G * b.cout, Ho, Wo), device=x.device, dtype=torch.bfloat16,
                                  memory_format=torch.channels_last)
-                cg = colx.transpose(0, 1)
-                _gmm(cg, self._rows(Wb, ld, G, b.conv1, b.cout, 9 * b.cin), _gview(h1, G), False)
-                # the 1x1 stride-2 shortcut reads the centre tap of the column image
                 sc = torch.empty_like(h1)
-                _gmm(cg[:, :, 4 * b.cin:5 * b.cin], self._rows(Wb, ld, G, b.sc, b.cout, b.cin), _gview(sc, G),
-                     False)
+                w1 = self._rows(Wb, ld, G, b.conv1, b.cout, 9 * b.cin)
+                wsc = self._rows(Wb, ld, G, b.sc, b.cout, b.cin)
+                P1 = nn_ * Ho * Wo
+                # the stride-2 conv and its 1x1 shortcut on the native GEMM over
+                # the IMPLICIT column image of xin (no im2col)
+                if not (self._IMP_STRIDED[0]
+                        and ops.fa_gemm(_carrier(xin, G, P1, 9 * b.cin), w1, _gview(h1, G), False, 0.0, xin, 3, 2, 1)
+                        and ops.fa_gemm(_carrier(xin, G, P1, b.cin), wsc, _gview(sc, G), False, 0.0, xin, 1, 2, 0)):
+                    colx = ops.im2col_grouped(xin, G, 3, 3, 2, 1, 9 * b.cin, False)
+                    cg = colx.transpose(0, 1)
+                    _gmm(cg, w1, _gview(h1, G), False)
+                    # the 1x1 stride-2 shortcut reads the centre tap of the column image
+                    _gmm(cg[:, :, 4 * b.cin:5 * b.cin], wsc, _gview(sc, G), False)
             a1, st1, bits1 = ops.cs_bn_fwd(h1, W, ld, b.bn1w, b.bn1b, G, b.m1.eps, b.m1.momentum, rm1, rv1,
                                            nbt if bi == 0 else None)
             h2 = self._conv3(a1, Wb, ld, G, b.conv2, b.cout, b.cout)
@@ -467,15 +482,24 @@ class ResNet18FedAvg:
                 da = dx
             else:
                 nn_, _, Hi, Wi = xin.shape
-                dcol = torch.empty((colx.shape[0], G, 9 * b.cin), device=x.device, dtype=torch.bfloat16)
+                P1 = nn_ * ((Hi - 1) // 2 + 1) * ((Wi - 1) // 2 + 1)
+                dcol = torch.empty((P1, G, 9 * b.cin), device=x.device, dtype=torch.bfloat16)
                 dcg = dcol.transpose(0, 1)
                 _gmm(_gview(dh1, G), self._rows(Wb, ld, G, b.conv1, b.cout, 9 * b.cin), dcg, True)
                 # the shortcut's input gradient joins the centre tap before the gather
                 dctr = dcg[:, :, 4 * b.cin:5 * b.cin]
                 _gmm(_gview(da, G), self._rows(Wb, ld, G, b.sc, b.cout, b.cin), dctr, True, 1.0)
-                cg = colx.transpose(0, 1)
-                self._bmm_rows(sink, b.conv1, _gview(dh1, G).transpose(1, 2), cg)
-                self._bmm_rows(sink, b.sc, _gview(da, G).transpose(1, 2), cg[:, :, 4 * b.cin:5 * b.cin])
+                A1, Asc = _gview(dh1, G).transpose(1, 2), _gview(da, G).transpose(1, 2)
+                if colx is None and not (
+                        ops.fa_bmm_rows(A1, _carrier(xin, G, P1, 9 * b.cin), sink.dst, sink.ld, b.conv1, sink.beta,
+                                        sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xin, 3, 2, 1)
+                        and ops.fa_bmm_rows(Asc, _carrier(xin, G, P1, b.cin), sink.dst, sink.ld, b.sc, sink.beta,
+                                            sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xin, 1, 2, 0)):
+                    raise RuntimeError("ResNet18FedAvg: implicit strided weight update refused after its forward")
+                if colx is not None:
+                    cg = colx.transpose(0, 1)
+                    self._bmm_rows(sink, b.conv1, A1, cg)
+                    self._bmm_rows(sink, b.sc, Asc, cg[:, :, 4 * b.cin:5 * b.cin])
                 da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)

@@ -381,6 +381,40 @@ def test_fa_bmm_rows_implicit_column_image(C, K, H, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("C,K,H,n", [(64, 128, 32, 2), (128, 256, 16, 3), (256, 256, 8, 5)])
+def test_implicit_strided_column_image(C, K, H, n):
+    """Stride-2 3x3 conv and its 1x1 stride-2 shortcut: forward on the native
+    GEMM over the implicit column image, and the TN weight update over it, ==
+    the same products over the materialised im2col_grouped image"""
+    torch.manual_seed(0)
+    G = 3
+    ops = _ops()
+    x = _cs(torch.randn(G, n, C, H, H, device="cuda"), G)
+    Ho = (H - 1) // 2 + 1
+    P = n * Ho * Ho
+    col = ops.im2col_grouped(x, G, 3, 3, 2, 1, 9 * C, False)
+    cg = col.transpose(0, 1)
+    w1 = torch.randn(G, K, 9 * C, device="cuda").bfloat16()
+    wsc = torch.randn(G, K, C, device="cuda").bfloat16()
+    carrier = torch.empty((1, 1, 1), device="cuda", dtype=torch.bfloat16)
+    for R, pad, N, w, ref_a in ((3, 1, 9 * C, w1, cg), (1, 0, C, wsc, cg[:, :, 4 * C:5 * C])):
+        out = torch.empty(P, G, K, device="cuda", dtype=torch.bfloat16)
+        ref = torch.empty_like(out)
+        assert ops.fa_gemm(ref_a, w, ref.transpose(0, 1), False, 0.0)
+        assert ops.fa_gemm(carrier.expand(G, P, N), w, out.transpose(0, 1), False, 0.0, x, R, 2, pad)
+        assert torch.equal(out, ref)
+        # the weight update over the same implicit image
+        dy = torch.randn(P, G, K, device="cuda").bfloat16()
+        A = dy.permute(1, 2, 0)  # [G, K, P]
+        ld, off = K * N + 64, 32
+        Wr = torch.randn(G, ld, device="cuda")
+        Wi = Wr.clone()
+        assert ops.fa_bmm_rows(A, ref_a, Wr, ld, off, 0.99, -0.1, None, 1)
+        assert ops.fa_bmm_rows(A, carrier.expand(G, P, N), Wi, ld, off, 0.99, -0.1, None, 1, None, 0, x, R, 2, pad)
+        torch.testing.assert_close(Wi, Wr, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_ew_add_relu():
     a = torch.randn(2, 64, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     b = torch.randn_like(a)
