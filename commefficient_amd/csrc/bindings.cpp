@@ -2217,17 +2217,32 @@ at::Tensor heads_to_rows_hip(at::TensorList srcs, const c10::optional<at::Tensor
 // slab_only: C is unused; returns the [G * splits, M, N] fp32 split products
 // unsummed (a column-image weight gradient's parts, summed and permuted by
 // wgrad_rsc_add)
+// imp_R > 0: b is a channels-last bf16 image x [n, C, H, W] and the B operand
+// its implicit imp_R x imp_R / imp_s / imp_pad column image [n OH OW, R R C]
+// (gathered per tap in the kernel: GemmTnArgs::imp_*); each group whole images
 static at::Tensor gemm_tn_run(float* sink, int64_t ldc, int64_t cg, const at::Tensor& a, const at::Tensor& b, int64_t G,
-                       bool slab_only = false) {
+                       bool slab_only = false, int64_t imp_R = 0, int64_t imp_s = 1, int64_t imp_pad = 0) {
+  const bool imp = imp_R > 0;
+  int64_t OH = 0, OW = 0;
+  if (imp) {
+    TORCH_CHECK(b.scalar_type() == at::kBFloat16 && b.dim() == 4 && b.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    b.size(1) % 8 == 0 && imp_s >= 1 && imp_pad >= 0 && imp_pad < imp_R,
+                "gemm_tn_parts_imp: channels-last bf16 image with C % 8 == 0");
+    OH = (b.size(2) + 2 * imp_pad - imp_R) / imp_s + 1;
+    OW = (b.size(3) + 2 * imp_pad - imp_R) / imp_s + 1;
+    TORCH_CHECK(a.dim() == 2 && a.size(0) == b.size(0) * OH * OW && G >= 1 && b.size(0) % G == 0,
+                "gemm_tn_parts_imp: a [n OH OW, M], G | n");
+  }
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
-                  b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1 && a.size(0) == b.size(0),
+                  (imp || (b.dim() == 2 && b.stride(1) == 1 && a.size(0) == b.size(0))) && a.stride(1) == 1,
               "gemm_tn_acc: a [T, M], b [T, N] bf16 with unit column stride");
   TORCH_CHECK(G >= 1 && a.size(0) % G == 0, "gemm_tn_acc: G must divide the rows");
-  const int64_t M = a.size(1), N = b.size(1), T = a.size(0) / G;
+  const int64_t M = a.size(1), N = imp ? imp_R * imp_R * b.size(1) : b.size(1), T = a.size(0) / G;
+  const int64_t ldb = imp ? b.size(1) : b.stride(0);
   // M: a multiple of 64, or any M whose A rows hold the 8-column chunk past
   // M (a padded buffer: the tied LM head's 50,257-row weight gradient)
   const bool m_ok = M % 64 == 0 || a.stride(0) >= (M + 7) / 8 * 8;
-  TORCH_CHECK(m_ok && N % 8 == 0 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+  TORCH_CHECK(m_ok && N % 8 == 0 && a.stride(0) % 8 == 0 && ldb % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(sink) % 16 == 0 && ldc % 4 == 0 && cg % 4 == 0,
@@ -2247,7 +2262,7 @@ static at::Tensor gemm_tn_run(float* sink, int64_t ldc, int64_t cg, const at::Te
   g.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
   g.lda = a.stride(0);
   g.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
-  g.ldb = b.stride(0);
+  g.ldb = ldb;
   g.C = sink;
   g.ldc = ldc;
   g.M = static_cast<int>(M);
@@ -2255,6 +2270,17 @@ static at::Tensor gemm_tn_run(float* sink, int64_t ldc, int64_t cg, const at::Te
   g.T = static_cast<int>(T);
   g.G = static_cast<int>(G);
   g.cg = cg;
+  if (imp) {
+    g.sb = b.size(0) / G * b.size(2) * b.size(3) * ldb;  // a group's images
+    g.imp_C = static_cast<int>(b.size(1));
+    g.imp_H = static_cast<int>(b.size(2));
+    g.imp_W = static_cast<int>(b.size(3));
+    g.imp_OH = static_cast<int>(OH);
+    g.imp_OW = static_cast<int>(OW);
+    g.imp_R = static_cast<int>(imp_R);
+    g.imp_s = static_cast<int>(imp_s);
+    g.imp_pad = static_cast<int>(imp_pad);
+  }
   // ~ one block per CU over all groups
   g.splits = gemm_tn_splits(g.M, g.N, g.T, cus / g.G > 0 ? cus / g.G : 1);
   g.slab_only = slab_only ? 1 : 0;
@@ -2291,6 +2317,17 @@ std::tuple<at::Tensor, int64_t> gemm_tn_parts_hip(const at::Tensor& a, const at:
   // slab-only: the sink argument is never written (a's aligned address passes the checks)
   auto parts = gemm_tn_run(reinterpret_cast<float*>(a.data_ptr()), 4, 0, a, b, G, true);
   TORCH_CHECK(parts.defined(), "gemm_tn_parts: empty operands");
+  return {parts, parts.size(0) / G};
+}
+
+// gemm_tn_parts with b the implicit R x R / stride / pad column image of the
+// channels-last image x (a strided conv's weight gradient without im2col)
+std::tuple<at::Tensor, int64_t> gemm_tn_parts_imp_hip(const at::Tensor& a, const at::Tensor& x, int64_t G, int64_t R,
+                                                      int64_t stride, int64_t pad) {
+  TORCH_CHECK(a.is_cuda() && x.is_cuda() && R >= 1, "gemm_tn_parts_imp: device tensors");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto parts = gemm_tn_run(reinterpret_cast<float*>(a.data_ptr()), 4, 0, a, x, G, true, R, stride, pad);
+  TORCH_CHECK(parts.defined(), "gemm_tn_parts_imp: empty operands");
   return {parts, parts.size(0) / G};
 }
 
@@ -2481,6 +2518,7 @@ TORCH_LIBRARY(commeff, m) {
   m.def("gemm_tn_acc(Tensor(a!) sink, Tensor a, Tensor b) -> ()");
   m.def("gemm_tn_acc_grouped(Tensor(a!) sink, Tensor a, Tensor b, int G) -> ()");
   m.def("gemm_tn_parts(Tensor a, Tensor b, int G) -> (Tensor, int)");
+  m.def("gemm_tn_parts_imp(Tensor a, Tensor x, int G, int R, int stride, int pad) -> (Tensor, int)");
   m.def("im2col(Tensor x, int R, int S, int stride, int pad, int Kc) -> Tensor");
   m.def("col2im(Tensor gcol, int N, int H, int W, int C, int R, int S, int stride, int pad) -> Tensor");
   m.def("conv_weight_rsc(Tensor w, int Kc) -> Tensor");
@@ -2588,6 +2626,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("gemm_tn_acc", &gemm_tn_acc_hip);
   m.impl("gemm_tn_acc_grouped", &gemm_tn_acc_grouped_hip);
   m.impl("gemm_tn_parts", &gemm_tn_parts_hip);
+  m.impl("gemm_tn_parts_imp", &gemm_tn_parts_imp_hip);
   m.impl("attn_fwd", &attn_fwd_hip);
   m.impl("attn_bwd", &attn_bwd_hip);
   m.impl("heads_to_rows", &heads_to_rows_hip);

@@ -363,6 +363,11 @@ void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stre
   const bool wide = a.N % 128 == 0 &&
                     static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) * (a.G > 1 ? a.G : 1) >= 384;
   if (a.imp_C > 0) {  // implicit column image A (NT, bf16 out, no activation)
+    if (a.stats != nullptr) {  // + BN moments (conv_nt_imp)
+      if (wide) launch_gemm_t<128, false, 0, false, true, true>(a, stream);
+      else launch_gemm_t<64, false, 0, false, true, true>(a, stream);
+      return;
+    }
     if (wide) launch_gemm_t<128, false, 0, false, false, true>(a, stream);
     else launch_gemm_t<64, false, 0, false, false, true>(a, stream);
     return;

@@ -146,6 +146,63 @@ std::tuple<at::Tensor, at::Tensor> mm_nt_bnstats(const at::Tensor& a, const at::
   return {C, stats};
 }
 
+// (y bf16 [n OH OW, K], tile moments fp32 [ceil(M / 128), 4, K] or empty when
+// G == 0): the R x R / stride / pad conv of the channels-last bf16 x [n, C, H,
+// W] against its (r, s, c) weight image w [K, R R C] as the native NT GEMM
+// with the column image gathered per tap from x (GemmArgs::imp_*, no im2col
+// pass), the BN moments of mm_nt_bnstats in the epilogue when G >= 1.
+std::tuple<at::Tensor, at::Tensor> conv_nt_imp(const at::Tensor& x, const at::Tensor& w, int64_t R, int64_t stride,
+                                               int64_t pad, int64_t G) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.dim() == 2 &&
+                  w.stride(1) == 1,
+              "conv_nt_imp: channels-last bf16 x, bf16 [K, R R C] w");
+  const int64_t n = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0);
+  TORCH_CHECK(R >= 1 && stride >= 1 && pad >= 0 && pad < R && C % 64 == 0 && w.size(1) == R * R * C,
+              "conv_nt_imp: geometry (C % 64 == 0, w [K, R R C])");
+  const int64_t OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - R) / stride + 1, M = n * OH * OW;
+  TORCH_CHECK(OH >= 1 && OW >= 1 && M < (int64_t{1} << 31), "conv_nt_imp: output size");
+  TORCH_CHECK(gemm_supported(static_cast<int>(M), static_cast<int>(K), static_cast<int>(R * R * C), false),
+              "conv_nt_imp: native GEMM needs K % 64 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+                  w.stride(0) % 8 == 0,
+              "conv_nt_imp: 16-byte aligned operands and row strides");
+  TORCH_CHECK(G == 0 || (M % G == 0 && M / G >= kBnStatTile), "conv_nt_imp: G | M with >= 128 rows per group");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto y = at::empty({M, K}, x.options());
+  at::Tensor stats;
+  GemmArgs g{};
+  g.A = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  g.lda = C;  // pixel row
+  g.B = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  g.ldb = w.stride(0);
+  g.C = y.data_ptr();
+  g.ldc = K;
+  g.C2 = nullptr;
+  g.bias = nullptr;
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(K);
+  g.K = static_cast<int>(R * R * C);
+  g.beta = 0.f;
+  g.imp_C = static_cast<int>(C);
+  g.imp_H = static_cast<int>(H);
+  g.imp_W = static_cast<int>(W);
+  g.imp_OH = static_cast<int>(OH);
+  g.imp_OW = static_cast<int>(OW);
+  g.imp_R = static_cast<int>(R);
+  g.imp_s = static_cast<int>(stride);
+  g.imp_pad = static_cast<int>(pad);
+  if (G >= 1) {
+    stats = at::empty({(M + kBnStatTile - 1) / kBnStatTile, 4, K}, x.options().dtype(at::kFloat));
+    g.stats = stats.data_ptr<float>();
+    g.stats_mg = static_cast<int>(M / G);
+  } else {
+    stats = at::empty({0}, x.options().dtype(at::kFloat));
+  }
+  launch_gemm(g, false, 0, false, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  return {y, stats};
+}
+
 }  // namespace
 }  // namespace commeff
 
@@ -155,6 +212,7 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("mm_nn(Tensor a, Tensor b, Tensor? bias=None, Tensor(c!)? out=None, float beta=0.0, int act=0, "
         "Tensor(d!)? pre=None) -> Tensor");
   m.def("mm_nt_bnstats(Tensor a, Tensor b, int G) -> (Tensor, Tensor)");
+  m.def("conv_nt_imp(Tensor x, Tensor w, int R, int stride, int pad, int G) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CPU, m) {
@@ -167,4 +225,5 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("mm_nt", &commeff::mm_nt);
   m.impl("mm_nn", &commeff::mm_nn);
   m.impl("mm_nt_bnstats", &commeff::mm_nt_bnstats);
+  m.impl("conv_nt_imp", &commeff::conv_nt_imp);
 }

@@ -1117,14 +1117,19 @@ def _col_image(weight: torch.Tensor, Kc: int) -> torch.Tensor:
     return _ops().conv_weight_rsc(weight.detach().contiguous(), Kc)
 
 
-def _col_wgrad(g2d: torch.Tensor, col: torch.Tensor, weight: torch.Tensor, gg):
+def _col_wgrad(g2d: torch.Tensor, col: torch.Tensor, weight: torch.Tensor, gg, imp=None):
     """dW of a column-image conv: split-K GEMMs of g2d^T col, then one native
     pass that sums the splits in order, permutes (r, s, c) -> (c, r, s) and
     accumulates into the flat fp32 gradient (or the per-group rows of
-    ``gg``).  Returns the gradient for autograd, None when accumulated."""
+    ``gg``).  Returns the gradient for autograd, None when accumulated.
+    ``imp`` (stride, pad): ``col`` is the conv's input image and the native TN
+    GEMM gathers its column image per tap (no im2col)."""
     K, C, R, S = weight.shape
     G = gg.G if gg is not None else 1
-    parts, splits = _wgrad_parts(g2d, col, G)
+    if imp is not None:
+        parts, splits = _ops().gemm_tn_parts_imp(g2d, col, G, R, imp[0], imp[1])
+    else:
+        parts, splits = _wgrad_parts(g2d, col, G)
     if gg is not None:
         _ops().wgrad_rsc_add(gg.view(weight).view(G, K, C * R * S), parts, splits, C, R * S, True)
         return None
@@ -1150,11 +1155,26 @@ class _ConvCol(torch.autograd.Function):
         K, C, R, S = weight.shape
         N, _, H, W = x.shape
         Kc = _col_width(C, R, S)
-        col = _ops().im2col(x, R, S, stride, pad, Kc)
         wt = _col_image(weight, Kc)
         OH, OW = (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
-        y2d = _mm_nt_conv(col, wt)
-        ctx.save_for_backward(col, wt)
+        # implicit column image (the strided 3x3 of each stage's first block):
+        # the native NT GEMM gathers it per tap from x, the weight gradient's
+        # TN GEMM likewise; x is kept instead of the 9x larger image
+        imp = (_IMP_COL[0] and _GEMM_NATIVE[0] and R == S and Kc == R * S * C and C % 64 == 0
+               and K % 64 == 0 and _gpu_bf16_nhwc(x) and x.data_ptr() % 16 == 0
+               and (gg is None or N % gg.G == 0))
+        if imp:
+            G, M = _EPI["G"], N * OH * OW
+            st_on = _EPI["on"] and G >= 1 and M % G == 0 and M // G >= 128
+            y2d, st = _ops().conv_nt_imp(x, wt, R, stride, pad, G if st_on else 0)
+            if st_on:
+                _EPI["last"] = (st, G)
+            ctx.save_for_backward(x, wt)
+        else:
+            col = _ops().im2col(x, R, S, stride, pad, Kc)
+            y2d = _mm_nt_conv(col, wt)
+            ctx.save_for_backward(col, wt)
+        ctx.imp = imp
         ctx.geo = (N, C, H, W, R, S, stride, pad)
         ctx.weight, ctx.gg = weight, gg
         return y2d.view(N, OH, OW, K).permute(0, 3, 1, 2)
@@ -1167,8 +1187,14 @@ class _ConvCol(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = _ops().col2im(_mm_nn(g2d, wt), N, H, W, C, R, S, stride, pad)
-        gw = _col_wgrad(g2d, col, ctx.weight, ctx.gg) if ctx.needs_input_grad[1] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gw = _col_wgrad(g2d, col, ctx.weight, ctx.gg, (stride, pad) if ctx.imp else None)
         return gx, gw, None, None, None
+
+
+# strided 3x3 convs on the implicit column image (False: im2col + GEMMs)
+_IMP_COL = [True]
 
 
 class _MaxPool(torch.autograd.Function):

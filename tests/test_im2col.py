@@ -70,6 +70,39 @@ def test_col_conv_matches_fp32(N, C, H, W, K, R, stride, pad, data_input):
         _close(x.grad, xr.grad)
 
 
+@pytest.mark.parametrize("N,C,H,W,K,bnstats", [(2, 128, 14, 14, 128, False), (3, 64, 15, 13, 64, False),
+                                                (2, 64, 32, 32, 128, True), (2, 128, 24, 23, 64, True)])
+def test_implicit_col_conv_matches_materialised(N, C, H, W, K, bnstats):
+    """The strided 3x3 on the implicit column image (conv_nt_imp forward,
+    gemm_tn_parts_imp weight gradient) == the im2col path bitwise: output,
+    epilogue BN moments, both gradients."""
+    x0, w0 = _case_inputs(N, C, H, W, K, 3, False, seed=3)
+    gy = None
+    outs = []
+    for imp in (True, False):
+        cnn._IMP_COL[0] = imp
+        saved = dict(cnn._EPI)
+        try:
+            cnn._EPI.update(on=bnstats, G=N if bnstats else 0)
+            x = x0.detach().clone().requires_grad_()
+            w = w0.detach().clone().requires_grad_()
+            y = cnn.conv2d_native(x, w, "col", 2, None, 1)
+            st = getattr(y, "_commeff_bnstats", None)
+            if gy is None:
+                gy = torch.randn(y.shape, device="cuda").to(torch.bfloat16)
+            y.backward(gy)
+            outs.append((y.detach(), None if st is None else st[0], x.grad, w.grad))
+        finally:
+            cnn._IMP_COL[0] = True
+            cnn._EPI.clear()
+            cnn._EPI.update(saved)
+    (yi, si, xi, wi), (ym, sm, xm, wm) = outs
+    assert torch.equal(yi, ym) and torch.equal(xi, xm) and torch.equal(wi, wm)
+    assert (si is None) == (sm is None) == (not bnstats)
+    if bnstats:
+        assert torch.equal(si, sm)
+
+
 def test_col_conv_wgrad_accumulates_into_existing_grad():
     x, w = _case_inputs(2, 128, 14, 14, 128, 3, False)
     w.grad = torch.full_like(w, 0.5)
