@@ -1090,7 +1090,11 @@ class _Conv3x3(torch.autograd.Function):
                 _ops().conv3x3_wgrad_grouped(g, x, gv.shape[0], gv.view(gv.shape[0], -1))
             elif native:
                 gw = _wgrad_to(g, x, w)
-            else:  # K % 128 != 0: column-image GEMM (csrc/im2col.hip)
+            elif (_IMP_COL[0] and _GEMM_NATIVE[0] and x.shape[1] % 8 == 0 and _gpu_bf16_nhwc(x)
+                  and x.data_ptr() % 16 == 0 and (ctx.gg is None or x.shape[0] % ctx.gg.G == 0)):
+                # K % 128 != 0: the TN GEMM over the implicit column image of x
+                gw = _col_wgrad(_nhwc2d(g), x, w, ctx.gg, (1, 1))
+            else:  # column-image GEMM (csrc/im2col.hip)
                 col = _ops().im2col(x, 3, 3, 1, 1, 9 * x.shape[1])
                 gw = _col_wgrad(_nhwc2d(g), col, w, ctx.gg)
         return gx, gw, None

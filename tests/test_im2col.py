@@ -103,6 +103,39 @@ def test_implicit_col_conv_matches_materialised(N, C, H, W, K, bnstats):
         assert torch.equal(si, sm)
 
 
+@pytest.mark.parametrize("grouped", [False, True])
+def test_narrow_3x3_wgrad_implicit_matches_materialised(grouped):
+    """The K = 64 stride-1 3x3 (ImageNet layer 1) weight gradient on the TN
+    GEMM over the implicit column image == the im2col path bitwise (returned
+    and per group)."""
+    G, n, C, H, K = 2, 2, 64, 20, 64
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x0 = _nhwc(torch.randn(G * n, C, H, H, device="cuda", generator=g).to(torch.bfloat16))
+    w0 = torch.randn(K, C, 3, 3, device="cuda", generator=g) * 0.05
+    assert cnn.conv2d_native_kind(x0, w0, 1, 1, 1, 1) == "3x3"
+    gy = torch.randn(G * n, K, H, H, device="cuda", generator=g).to(torch.bfloat16)
+    gy = _nhwc(gy)
+    outs = []
+    for imp in (True, False):
+        cnn._IMP_COL[0] = imp
+        try:
+            w = w0.detach().clone().requires_grad_()
+            if grouped:
+                buf = torch.zeros(G, w.numel() + 8, device="cuda")
+                gg = GroupedGrads(G, buf, {id(w): (8, w.shape)})
+                with grouped_grads(gg):
+                    y = cnn.conv2d_native(x0, w, "3x3", 1, gg, 1)
+                y.backward(gy)
+                outs.append(buf.clone())
+            else:
+                y = cnn.conv2d_native(x0, w, "3x3", 1, None, 1)
+                y.backward(gy)
+                outs.append(w.grad.clone())
+        finally:
+            cnn._IMP_COL[0] = True
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_col_conv_wgrad_accumulates_into_existing_grad():
     x, w = _case_inputs(2, 128, 14, 14, 128, 3, False)
     w.grad = torch.full_like(w, 0.5)
