@@ -9,12 +9,17 @@ all-reduce of the 10 MB table (+ metrics), and the replicated server update
 (momentum/error, median unsketch, top-k, heavy-hitter zeroing, weight apply,
 download accounting).  Nothing is skipped in the timed region.
 
-Weak scaling: every GPU runs --clients-per-gpu clients of --client-size
-images per round (default 100 x 5 = 500 images/GPU/round; 10,000 non-iid
-clients of 5 images each as in the FetchSGD CIFAR-10 setup).  Synthetic data
-of CIFAR shape, random-init weights.
+Weak scaling (default): every GPU runs --clients-per-gpu clients of
+--client-size images per round (default 100 x 5 = 500 images/GPU/round;
+10,000 non-iid clients of 5 images each as in the FetchSGD CIFAR-10 setup).
+Strong scaling (--clients-per-round W): a fixed round of W clients in total,
+split across the N ranks as the reference splits a round across its workers
+(/root/reference/CommEfficient/fed_aggregator.py:230-237; balanced here, each
+rank gets floor or ceil of W/N) -- the reference's own topology, e.g. W = 100
+at N = 8 is 12-13 clients per rank.  Synthetic data of CIFAR shape, random-init
+weights.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--clients-per-round W]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 import argparse
@@ -38,7 +43,11 @@ def main():
     # 250.4-250.5k img/s with 30 after 5 on one box (clocks and caches settle)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=50)
-    p.add_argument("--clients-per-gpu", type=int, default=100)
+    p.add_argument("--clients-per-gpu", type=int, default=100,
+                   help="weak scaling: clients per rank per round (round = this x N)")
+    p.add_argument("--clients-per-round", type=int, default=None,
+                   help="strong scaling: total clients per round, split across the ranks "
+                        "(fed_aggregator.py:230-237); overrides --clients-per-gpu")
     p.add_argument("--client-size", type=int, default=5)
     p.add_argument("--num-clients", type=int, default=10000)
     p.add_argument("--encode", default="region", choices=["region", "planned", "binned", "direct"],
@@ -75,7 +84,10 @@ def main():
         assert ctx.backend == "nccl", f"backend {ctx.backend!r}: the bench runs on RCCL"
         local = int(os.environ.get("LOCAL_WORLD_SIZE", str(N)))
         assert torch.cuda.device_count() >= local, "fewer visible GPUs than local ranks"
-    W = b.clients_per_gpu * N
+    strong = b.clients_per_round is not None
+    W = b.clients_per_round if strong else b.clients_per_gpu * N
+    if W < N:
+        sys.exit(f"{W} clients per round cannot feed {N} ranks")
     n_train = b.num_clients * b.client_size
     argv = ["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", str(n_train),
             "--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
@@ -207,7 +219,8 @@ def main():
         print(json.dumps({
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": N,
             "steps": b.steps, "warmup": b.warmup, "ms_per_step": round(ms, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "strong" if strong else "weak",
+            "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (CIFAR-10 shape, random-init ResNet-9)",
             "config": {"model": "ResNet9", "global_batch": imgs_per_step, "seq_len": None,
                        "image_hw": 32, "parallelism": f"dp{N}", "mode": "sketch",
@@ -215,7 +228,8 @@ def main():
                        # numBlocks only shapes the csvec-layout hashes (--encode
                        # planned|binned|direct); the region family has no blocks
                        **({"num_blocks": 20} if b.encode != "region" else {}),
-                       "clients_per_round": W, "client_size": b.client_size,
+                       "clients_per_round": W, "clients_per_rank_max": -(-W // N),
+                       "client_size": b.client_size,
                        "num_clients": b.num_clients, "encode": b.encode,
                        "server": ("sharded" if fed.shard_server else "replicated"),
                        "round_tape": bool(fed.last_round.get("taped"))},

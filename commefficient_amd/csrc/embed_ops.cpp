@@ -13,8 +13,8 @@ namespace commeff {
 void launch_embed_fwd(const int64_t* ids, const int64_t* tt, const int32_t* tok, int L, const uint16_t* wte,
                       const uint16_t* wpe, uint16_t* out, int Mr, int H, hipStream_t stream);
 void launch_embed_bwd(const uint16_t* de, const int64_t* ids, const int64_t* tt, const int32_t* tok, int L,
-                      int pos, unsigned long long* acc, int32_t* cnt, int32_t* lst, int V, int H, float* sink,
-                      int64_t ld, int Mr, hipStream_t stream);
+                      int pos, unsigned long long* acc, float* spill, int32_t* cnt, int32_t* lst, int V, int H,
+                      float* sink, int64_t ld, int Mr, hipStream_t stream);
 
 namespace {
 
@@ -59,12 +59,12 @@ at::Tensor embed_fwd(const at::Tensor& ids, const c10::optional<at::Tensor>& tt,
 }
 
 // sink [V, H] fp32 (row stride ld) += the table gradient of de [Mr, H]: keys
-// ids[t] (+ tt[t]) (pos false) or t % L (pos true).  acc int64 [V*H], cnt int32
-// [V], lst int32 [V + 1]: the persistent fixed-point workspace (zero on entry,
-// zero again on exit)
+// ids[t] (+ tt[t]) (pos false) or t % L (pos true).  acc int64 [V*H], spill fp32
+// [V*H], cnt int32 [V], lst int32 [V + 1]: the persistent fixed-point workspace
+// and its out-of-range / non-finite spill (zero on entry, zero again on exit)
 void embed_bwd(const at::Tensor& de, const at::Tensor& ids, const c10::optional<at::Tensor>& tt,
-               const c10::optional<at::Tensor>& tok, int64_t L, bool pos, at::Tensor acc, at::Tensor cnt,
-               at::Tensor lst, at::Tensor sink) {
+               const c10::optional<at::Tensor>& tok, int64_t L, bool pos, at::Tensor acc, at::Tensor spill,
+               at::Tensor cnt, at::Tensor lst, at::Tensor sink) {
   const int64_t M = ids.numel();
   check_ids(ids, M, "embed_bwd: ids");
   const bool has_tt = !pos && tt.has_value() && tt->defined();
@@ -80,14 +80,16 @@ void embed_bwd(const at::Tensor& de, const at::Tensor& ids, const c10::optional<
               "embed_bwd: sink fp32 [V, H] with unit column stride");
   const int64_t V = sink.size(0);
   TORCH_CHECK(acc.scalar_type() == at::kLong && acc.is_contiguous() && acc.numel() == V * H &&
+                  spill.scalar_type() == at::kFloat && spill.is_contiguous() && spill.numel() == V * H &&
                   cnt.scalar_type() == at::kInt && cnt.is_contiguous() && cnt.numel() == V &&
                   lst.scalar_type() == at::kInt && lst.is_contiguous() && lst.numel() == V + 1,
-              "embed_bwd: workspace acc int64 [V*H], cnt int32 [V], lst int32 [V+1]");
+              "embed_bwd: workspace acc int64 [V*H], spill fp32 [V*H], cnt int32 [V], lst int32 [V+1]");
   TORCH_CHECK(pos ? L >= 1 && L <= V : true, "embed_bwd: positions past the table");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(de.device());
   launch_embed_bwd(reinterpret_cast<const uint16_t*>(de.data_ptr()), ids.data_ptr<int64_t>(),
                    has_tt ? tt->data_ptr<int64_t>() : nullptr, tp, static_cast<int>(L), pos ? 1 : 0,
-                   reinterpret_cast<unsigned long long*>(acc.data_ptr<int64_t>()), cnt.data_ptr<int32_t>(),
+                   reinterpret_cast<unsigned long long*>(acc.data_ptr<int64_t>()), spill.data_ptr<float>(),
+                   cnt.data_ptr<int32_t>(),
                    lst.data_ptr<int32_t>(), static_cast<int>(V), static_cast<int>(H), sink.data_ptr<float>(),
                    sink.stride(0), static_cast<int>(Mr), stream_now());
 }
@@ -97,7 +99,7 @@ void embed_bwd(const at::Tensor& de, const at::Tensor& ids, const c10::optional<
 TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("embed_fwd(Tensor ids, Tensor? tt, Tensor? tok, int L, Tensor wte, Tensor wpe) -> Tensor");
   m.def("embed_bwd(Tensor de, Tensor ids, Tensor? tt, Tensor? tok, int L, bool pos, Tensor(a!) acc, "
-        "Tensor(b!) cnt, Tensor(c!) lst, Tensor(d!) sink) -> ()");
+        "Tensor(b!) spill, Tensor(c!) cnt, Tensor(d!) lst, Tensor(e!) sink) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {

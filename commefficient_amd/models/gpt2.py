@@ -34,10 +34,11 @@ def build_double_heads(model_checkpoint: str = "gpt2", n_special: int = 5, n_lay
                  ("n_positions", n_positions)):
         if v is not None:
             setattr(cfg, k, v)
-    try:
-        cfg._attn_implementation = "sdpa"
-    except Exception:
-        pass
+    if is_gpt2:  # (HF's OpenAI-GPT has no SDPA attention: it keeps the eager one)
+        try:
+            cfg._attn_implementation = "sdpa"
+        except Exception:
+            pass
     if is_gpt2 and cfg.activation_function == "gelu_new":
         # the same tanh-approximation GELU as one fused kernel each way
         # (torch's gelu(approximate="tanh")) instead of HF's ~8 elementwise ops

@@ -345,6 +345,7 @@ def _emb_ws(device, V: int, H: int):
     if ws is None:
         # zero once; every backward leaves the rows it touched zeroed again
         ws = (torch.zeros(V * H, dtype=torch.int64, device=device),
+              torch.zeros(V * H, dtype=torch.float32, device=device),  # out-of-range spill
               torch.zeros(V, dtype=torch.int32, device=device),
               torch.zeros(V + 1, dtype=torch.int32, device=device))
         _EMB_WS[key] = ws
@@ -379,8 +380,8 @@ class _Embed(torch.autograd.Function):
                 continue
             V, H = w.shape
             dst = sink if sink is not None else torch.zeros(V, H, dtype=torch.float32, device=de.device)
-            acc, cnt, lst = _emb_ws(de.device, V, H)
-            _ops().embed_bwd(de, ids, tt, tok, ctx.L, i == 1, acc, cnt, lst, dst)
+            acc, spill, cnt, lst = _emb_ws(de.device, V, H)
+            _ops().embed_bwd(de, ids, tt, tok, ctx.L, i == 1, acc, spill, cnt, lst, dst)
             grads.append(None if sink is not None else dst.to(w.dtype))
         return grads[0], grads[1], None, None, None, None
 

@@ -170,6 +170,11 @@ class ClientStateStore:
         from . import dist as _dist
         ctx = _dist.ctx()
         dev = self.compute_device if ctx.backend == "nccl" else torch.device("cpu")
+        if self.host_tier:
+            # a host-tier row's last write-back (``put``) is a non_blocking D2H copy on
+            # the compute stream; over gloo ``row.to(cpu)`` is the pinned row itself, so
+            # the send could ship it before that copy lands
+            torch.cuda.current_stream(self.compute_device).synchronize()
         p2p, recv = [], []
         for (c, src, dst) in moves:
             for kind in self.kinds:
@@ -186,8 +191,6 @@ class ClientStateStore:
         self.migrated += len(moves)
         if not p2p:
             return
-        if dev.type == "cuda" and ctx.backend == "gloo":
-            torch.cuda.current_stream().synchronize()
         for req in tdist.batch_isend_irecv(p2p):
             req.wait()
         for kind, c, buf in recv:

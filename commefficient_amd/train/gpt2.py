@@ -35,12 +35,17 @@ def get_data_loaders(args, device, tokenizer=None):
     if args.synthetic:
         n_pers = args.num_clients or 1000
         text = getattr(args, "synthetic_text", "uniform")
+        # the model's base vocabulary (GPT-2 50,257, OpenAI-GPT 40,478), before the
+        # 5 special tokens the synthetic records append
+        n_tok = getattr(args, "len_tokenizer", None)
+        vocab = n_tok - len(SPECIAL_TOKENS) if n_tok else 50257
         tr = SyntheticPersona(num_personalities=n_pers, num_candidates=args.num_candidates,
                               max_history=args.max_history, train=True, do_iid=args.do_iid,
-                              num_clients=args.num_clients, seed=args.seed, text=text)
+                              num_clients=args.num_clients, seed=args.seed, text=text, vocab=vocab)
         te = SyntheticPersona(num_personalities=n_pers, num_candidates=args.num_candidates,
                               max_history=args.max_history, train=False, seed=args.seed,
-                              n_val=max(args.valid_batch_size * args.num_workers, 200), text=text)
+                              n_val=max(args.valid_batch_size * args.num_workers, 200), text=text,
+                              vocab=vocab)
     else:
         tr = FedPERSONA(tokenizer, args.num_candidates, args.max_history,
                         args.personality_permutations, args.dataset_dir, "PERSONA", None,
@@ -125,7 +130,10 @@ def main(args):
     dims = {"tiny": {"n_layer": 2, "n_embd": 64, "n_head": 2},
             # smallest shape on the native junction + attention kernels
             "mini": {"n_layer": 2, "n_embd": 256, "n_head": 4}}.get(size, {})
-    model = GPT2DoubleHeads(args.model_checkpoint if not args.do_test else "gpt2", **dims)
+    # (--test: a random-init model of the checkpoint's family -- GPT-2 or
+    # OpenAI-GPT, gpt2_train.py:262-267 -- not the checkpoint itself)
+    family = "gpt2" if "gpt2" in args.model_checkpoint else "openai-gpt"
+    model = GPT2DoubleHeads(args.model_checkpoint if not args.do_test else family, **dims)
     if tokenizer is not None:
         model.model.resize_token_embeddings(len(tokenizer))
     args.len_tokenizer = model.model.config.vocab_size

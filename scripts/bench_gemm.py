@@ -1,7 +1,6 @@
 #!/usr/bin/env python
 """GEMM micro-benchmark at the GPT-2 and ResNet-101 shapes: the native MFMA
-kernels (csrc/gemm.hip; COMMEFF_GEMM_BIG=1 in the environment selects the
-256-row 4-stage kernel) vs hipBLASLt (torch.mm), HIP-event medians, one JSON line per
+kernels (csrc/gemm.hip) vs hipBLASLt (torch.mm), HIP-event medians, one JSON line per
 shape with TF/s and the max relative error against fp32."""
 import json
 import os
@@ -39,8 +38,7 @@ def main():
         fl = 2.0 * M * N * K
         print(json.dumps({"M": M, "N": N, "K": K, "layout": lay, "native_us": round(tn, 1),
                           "native_tflops": round(fl / tn / 1e6, 1), "blas_us": round(tl, 1),
-                          "blas_tflops": round(fl / tl / 1e6, 1), "rel_err": round(err, 5),
-                          "big": os.environ.get("COMMEFF_GEMM_BIG", "0")}), flush=True)
+                          "blas_tflops": round(fl / tl / 1e6, 1), "rel_err": round(err, 5)}), flush=True)
 
 
 if __name__ == "__main__":

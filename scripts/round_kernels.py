@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--tail-ms", type=float, default=0.0,
                     help="no marker: take the kernels of the trace's last TAIL_MS ms "
                          "(e.g. rounds * ms_per_round of the timed steps)")
+    ap.add_argument("--sequence", action="store_true",
+                    help="print the kernels of one round in launch order with their durations "
+                         "averaged over the selected rounds (needs a fixed kernel list per round)")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -54,6 +57,8 @@ def main():
         sel = rows[lo:hi]
     if a.per_round and a.tail_ms <= 0:
         per_round(rows, starts, a.per_round)
+    if a.sequence and a.tail_ms <= 0:
+        sequence(rows, starts[-a.rounds - 1:])
     n = a.rounds
     wall = (sel[-1][1] - sel[0][0]) / n
     busy = collections.Counter()
@@ -83,6 +88,18 @@ def main():
     print("# us/round  calls/round  kernel")
     for k, v in busy.most_common(a.top):
         print(f"{v / n / 1e3:9.1f} {calls[k] / n:6.1f}  {k}")
+
+
+def sequence(rows, starts):
+    spans = [rows[starts[i]:starts[i + 1]] for i in range(len(starts) - 1)]
+    n = min(len(sp) for sp in spans)
+    spans = [sp for sp in spans if len(sp) == n]
+    print(f"# launch order of one round ({len(spans)} rounds of {n} kernels averaged): "
+          "start offset us, duration us, kernel")
+    for j in range(n):
+        d = sum(sp[j][1] - sp[j][0] for sp in spans) / len(spans) / 1e3
+        t = sum(sp[j][0] - sp[0][0] for sp in spans) / len(spans) / 1e3
+        print(f"{t:9.1f} {d:8.1f}  {short(spans[0][j][2])}")
 
 
 def per_round(rows, starts, top):

@@ -100,7 +100,7 @@ def test_bottleneck_fwd_bwd_with_bn_epilogue_statistics_gpu(stride):
     their own passes: output, input gradient and weight gradients agree to
     bf16 rounding, and the fusion engaged.  (A whole random-init ResNet-50 is
     the wrong probe: its forward amplifies one-ulp differences of the first
-    norm, 4e-5, to ~1e-2 by layer 2 -- scripts/experiments/dbg_bnepi2.py.)"""
+    norm, 4e-5, to ~1e-2 by layer 2 -- measured in round 4, profiles/r4_experiments.md.)"""
     from commefficient_amd.models.common import conv1x1, ghost_batchnorm, GhostBatchNorm2d
     from commefficient_amd.models.resnets import Bottleneck
     from commefficient_amd.ops import nn as onn

@@ -226,7 +226,7 @@ def test_resnet9_native_as_accurate_as_miopen():
     """Whole ResNet-9 fwd+bwd: the native bf16 path must be as close to an
     fp32 run as MIOpen's bf16 path is (bf16 noise grows towards the input
     layers, ~15% on the prep conv for both; measured per-layer in
-    scripts/experiments/cmp_resnet9_grads.py)."""
+    a round-3 per-layer comparison script, in git history)."""
     from commefficient_amd.models import ResNet9
     torch.manual_seed(0)
     m = ResNet9().cuda()

@@ -17,9 +17,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(rank, world, port, mode, out_dir, rounds):
+def _run(rank, world, port, mode, out_dir, rounds, device="cpu"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    if device == "cuda":  # ranks sharing one GPU: gloo (RCCL refuses duplicate devices)
+        os.environ["COMMEFF_DIST_BACKEND"] = "gloo"
     torch.set_num_threads(2)
     from commefficient_amd import models
     from commefficient_amd.data import make_synthetic
@@ -29,7 +31,7 @@ def _run(rank, world, port, mode, out_dir, rounds):
     from commefficient_amd.parallel.server import FedOptimizer
     from commefficient_amd.train.losses import cv_loss
     from commefficient_amd.utils.args import parse_args
-    dist.init("cpu")
+    dist.init(device)
     extra = {"uncompressed": ["--local_momentum", "0", "--virtual_momentum", "0.9",
                               "--allreduce_bucket_mb", "0.01"],
              "sketch": ["--error_type", "virtual", "--local_momentum", "0", "--virtual_momentum",
@@ -57,13 +59,16 @@ def _run(rank, world, port, mode, out_dir, rounds):
                                       "--client_dropout", "0.95"]}[mode]
     lbs = "-1"
     base = mode.replace("_sparse", "").replace("_dropout", "").replace("_sharded", "").replace("_query", "")
-    args = parse_args(argv=["--mode", base, "--device", "cpu", "--dtype", "fp32",
+    if device == "cuda":  # client rows in pinned host memory, compute on the GPU
+        extra = extra + ["--client_state_device", "cpu"]
+    args = parse_args(argv=["--mode", base, "--device", device, "--dtype", "fp32",
                             "--num_clients", "40", "--num_workers", "6", "--local_batch_size", lbs,
                             "--dataset_name", "CIFAR10", "--synthetic"] + extra, probe_port=False)
     torch.manual_seed(0)
     model = models.ResNet9(channels={"prep": 4, "layer1": 8, "layer2": 8, "layer3": 16})
     ds = make_synthetic("CIFAR10", train=True, num_clients=40, size=160, seed=3)
-    loader = DeviceFedLoader(ds, 6, -1, "cpu", seed=5, augment=True)
+    loader = DeviceFedLoader(ds, 6, -1, device, seed=5, augment=True)
+    model = model.to(device)
     fed = FedModel(model, cv_loss, args, num_clients=40)
     opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05), args, fed)
     it = iter(loader)
@@ -87,9 +92,11 @@ def _run(rank, world, port, mode, out_dir, rounds):
     if mode == "uncompressed" and world > 1:  # gradient buckets reduced during the backward
         assert fed.last_round.get("overlapped_buckets", 0) >= 2, fed.last_round
         assert fed.last_round.get("buckets_during_backward", 0) >= 1, fed.last_round
+    if device == "cuda":
+        assert fed.client_state.host_tier, "expected pinned host-tier client rows"
     sd = fed.server.state_dict()  # (sharded: gathered into the row-major format)
-    torch.save({"w": fed.w.clone(), "loss": torch.cat([l.reshape(-1) for l in losses]),
-                "dl": fed.accountant.client_download.clone(), "V": sd["V"], "E": sd["E"],
+    torch.save({"w": fed.w.cpu(), "loss": torch.cat([l.reshape(-1) for l in losses]).cpu(),
+                "dl": fed.accountant.client_download.cpu(), "V": sd["V"], "E": sd["E"],
                 "local": torch.tensor(local), "migrated": fed.client_state.migrated},
                os.path.join(out_dir, f"r{rank}_w{world}.pt"))
     dist.shutdown()
@@ -198,28 +205,34 @@ def test_two_ranks_one_gpu(mode):
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_one_gpu():
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_bench_two_ranks_one_gpu(scaling):
     """bench.py's multi-rank path (the driver's N>1 scaling run) end to end:
     two ranks over gloo sharing cuda:0, one JSON line from rank 0 with the
-    whole-job throughput over both ranks' clients."""
+    whole-job throughput over both ranks' clients.  Strong scaling: a fixed
+    41-client round split 21 / 20 across the ranks (fed_aggregator.py:230-237)."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, COMMEFF_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    mode = ["--clients-per-gpu", "20"] if scaling == "weak" else ["--clients-per-round", "41"]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
-           "--clients-per-gpu", "20", "--num-clients", "2000"]
+           "--num-clients", "2000"] + mode
     res = subprocess.run(cmd, env=env, timeout=300, capture_output=True, text=True, cwd=root)
     assert res.returncode == 0, res.stderr[-4000:]
     out = res.stdout
     lines = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
     assert len(lines) == 1, out
     r = lines[0]
+    W = 40 if scaling == "weak" else 41
     assert r["n_gpus"] == 2 and r["steps"] == 3 and r["warmup"] == 2
-    assert r["config"]["global_batch"] == 2 * 20 * 5 and r["config"]["parallelism"] == "dp2"
-    assert r["value"] > 0 and abs(r["value"] - 200 * 1000 / r["ms_per_step"]) < 0.01 * r["value"]
+    assert r["scaling"] == scaling
+    assert r["config"]["global_batch"] == W * 5 and r["config"]["parallelism"] == "dp2"
+    assert r["config"]["clients_per_rank_max"] == (20 if scaling == "weak" else 21)
+    assert r["value"] > 0 and abs(r["value"] - W * 5 * 1000 / r["ms_per_step"]) < 0.01 * r["value"]
     assert r["bytes_per_step"]["allreduce_payload_per_rank"] > 0
 
 
@@ -288,6 +301,30 @@ def test_client_state_ownership_balanced_three_ranks():
         assert torch.equal(rs[0]["w"], r["w"]), "replicas diverged"
     torch.testing.assert_close(rs[0]["w"], s["w"], rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(rs[0]["loss"], s["loss"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_client_state_host_tier_migration_three_ranks_gpu():
+    """The same 3-rank ownership run with CUDA compute and the client rows in
+    pinned host memory (--client_state_device cpu) over gloo: a moved row is sent
+    only after its last write-back (a non_blocking D2H copy on the compute stream)
+    has landed (state.py _migrate), so the run equals the single GPU process."""
+    import torch.cuda
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    rounds, mode = 14, "local_topk"
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_run, args=(3, _free_port(), mode, d, rounds, "cuda"), nprocs=3,
+                           start_method="spawn", join=True)
+        mp.start_processes(_run, args=(1, _free_port(), mode, d, rounds, "cuda"), nprocs=1,
+                           start_method="spawn", join=True)
+        rs = [torch.load(os.path.join(d, f"r{r}_w3.pt"), weights_only=True) for r in range(3)]
+        s = torch.load(os.path.join(d, "r0_w1.pt"), weights_only=True)
+    assert rs[0]["migrated"] > 0, "the sampled rounds never needed a move (test too weak)"
+    for r in rs[1:]:
+        assert torch.equal(rs[0]["w"], r["w"]), "replicas diverged"
+    torch.testing.assert_close(rs[0]["w"], s["w"], rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rs[0]["loss"], s["loss"], rtol=1e-3, atol=1e-4)
 
 
 def _ckpt_worker(rank, world, port, out_dir, what):

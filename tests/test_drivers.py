@@ -76,6 +76,36 @@ def test_gpt2_driver_tiny_synthetic(tmp_path, monkeypatch):
     assert torch.isfinite(fed.w).all()
 
 
+def test_openai_gpt_double_heads_driver_tiny_synthetic(tmp_path, monkeypatch):
+    """OpenAI-GPT double heads (M9; the reference picks it for any checkpoint
+    name without "gpt2", gpt2_train.py:262-267) through the GPT-2 driver: a
+    tiny random-init OpenAIGPTDoubleHeadsModel (eager attention, its own 40,478
+    + 5 vocabulary) trains two FetchSGD rounds; validation nll starts at
+    ~ln(40,483)."""
+    import math
+    monkeypatch.chdir(tmp_path)
+    argv = ["--dataset_name", "PERSONA", "--model", "GPT2DoubleHeads", "--synthetic",
+            "--synthetic_size", "64", "--num_clients", "16", "--num_workers", "4",
+            "--local_batch_size", "2", "--valid_batch_size", "2", "--device", "cpu",
+            "--dtype", "fp32", "--gpt2_size", "tiny", "--mode", "sketch",
+            "--model_checkpoint", "openai-gpt",
+            "--error_type", "virtual", "--local_momentum", "0", "--virtual_momentum", "0.9",
+            "--num_rows", "3", "--num_cols", "2000", "--k", "200", "--num_epochs", "1",
+            "--max_rounds", "2", "--num_results_train", "1", "--port", "29614"]
+    fed = fed_train.main(argv)
+    m = fed.model.model
+    assert type(m).__name__ == "OpenAIGPTDoubleHeadsModel"
+    assert m.config.vocab_size == 40478 + 5
+    assert fed.round_idx == 2
+    assert torch.isfinite(fed.w).all()
+    from commefficient_amd.train.gpt2 import get_data_loaders
+    _, te = get_data_loaders(fed.args, torch.device("cpu"))
+    batch = next(iter(te))
+    fed.train(False)
+    nll = fed(batch)[0].mean().item()
+    assert abs(nll - math.log(40483)) < 1.0, nll
+
+
 @pytest.mark.parametrize("stop", [3, 5])
 def test_resume_reproduces_uninterrupted_run(stop, tmp_path, monkeypatch):
     """Checkpoint after ``stop`` rounds (mid-epoch: 3; epoch boundary: 5 of

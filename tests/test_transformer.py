@@ -587,3 +587,90 @@ def test_native_embedding_vs_fp32(with_tt, with_tok, sink):
     torch.testing.assert_close(gp, rgp, rtol=tol, atol=tol)
     e2, gw2, gp2 = run()  # deterministic, and the workspace was left zeroed
     assert torch.equal(gw, gw2) and torch.equal(gp, gp2)
+
+
+@pytest.mark.gpu
+def test_native_embedding_nonfinite_and_out_of_range():
+    """The fixed-point embedding backward (csrc/embed.hip) does not turn NaN /
+    Inf or huge gradients into finite garbage: values outside the exact range
+    go to the fp32 spill accumulator, so the table gradient matches
+    index_add's, NaN and Inf included; the next call is clean again."""
+    from commefficient_amd.ops import transformer as tx
+    torch.manual_seed(1)
+    V, P, H, N, L = 1000, 64, 256, 4, 32
+    wte = (torch.randn(V, H, device="cuda") * 0.02).bfloat16().requires_grad_(True)
+    wpe = (torch.randn(P, H, device="cuda") * 0.02).bfloat16().requires_grad_(True)
+    ids = torch.randint(0, V, (N * L,), device="cuda")
+    ids[5] = ids[9] = 77  # a poisoned key shared with finite rows
+    tt = torch.randint(997, 1000, (N * L,), device="cuda")
+    de = torch.randn(N * L, H, device="cuda").bfloat16()
+    de[5, 3] = float("nan")
+    de[9, 4] = float("inf")
+    de[9, 5] = 3.0e30  # finite, far past the fixed-point range
+    de[17, 6] = -65536.0
+
+    def run(d):
+        gw, gp = torch.zeros(V, H, device="cuda"), torch.zeros(P, H, device="cuda")
+        with tx.grad_sinks({id(wte): gw, id(wpe): gp}):
+            e = tx._Embed.apply(wte, wpe, ids, tt, None, L)
+        e.backward(d)
+        return gw, gp
+
+    gw, gp = run(de)
+    rows = torch.arange(N * L, device="cuda")
+    rgw = torch.zeros(V, H, device="cuda").index_add_(0, ids, de.float()).index_add_(0, tt, de.float())
+    rgp = torch.zeros(P, H, device="cuda").index_add_(0, rows % L, de.float())
+    assert torch.isnan(gw[77, 3]) and torch.isinf(gw[77, 4]) and gw[77, 4] > 0
+    torch.testing.assert_close(gw, rgw, rtol=1e-5, atol=1e-5, equal_nan=True)
+    torch.testing.assert_close(gp, rgp, rtol=1e-5, atol=1e-5, equal_nan=True)
+    # workspace (fixed-point accumulator, spill, flags) left zeroed
+    de2 = torch.randn(N * L, H, device="cuda").bfloat16()
+    gw2, _ = run(de2)
+    rgw2 = torch.zeros(V, H, device="cuda").index_add_(0, ids, de2.float()).index_add_(0, tt, de2.float())
+    assert torch.isfinite(gw2).all()
+    torch.testing.assert_close(gw2, rgw2, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpt2_nan_embedding_gradient_round_skipped(monkeypatch):
+    """A NaN in the embedding's input gradient reaches the round's aggregate
+    as a NaN (no integer-cast laundering in the native backward), so
+    --skip_nonfinite drops that round: the weights stay bitwise where they
+    were, and the next round trains again (mini GPT-2 under FetchSGD)."""
+    import importlib.util
+    import os
+    from commefficient_amd.ops import transformer as tx
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                        "gpt2_learning.py")
+    spec = importlib.util.spec_from_file_location("gpt2_learning", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    extra = ["--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
+             "--virtual_momentum", "0.9", "--num_rows", "5", "--num_cols", "500000", "--k", "50000",
+             "--lr_scale", "0.1", "--skip_nonfinite", "1", "--round_tape", "off"]
+    args, fed, opt, train_loader, _ = mod.build(extra, "mini")
+    poison = {"on": False, "hits": 0}
+    orig = tx._Embed.backward
+
+    def backward(ctx, de):
+        if poison["on"]:
+            de = de.clone()
+            de[0, 0] = float("nan")
+            poison["hits"] += 1
+        return orig(ctx, de)
+
+    monkeypatch.setattr(tx._Embed, "backward", staticmethod(backward))
+    ws = []
+    it = iter(train_loader)
+    for r in range(3):
+        batch = next(it)
+        poison["on"] = r == 1
+        fed(batch)
+        opt.step()
+        torch.cuda.synchronize()
+        ws.append(fed.w.detach().clone())
+    assert poison["hits"] >= 1, "the native embedding backward did not run"
+    assert fed.skipped_rounds == 1, fed.skipped_rounds
+    assert torch.isfinite(ws[2]).all()
+    assert torch.equal(ws[0], ws[1]), "the poisoned round changed the weights"
+    assert not torch.equal(ws[1], ws[2]), "training did not resume"
