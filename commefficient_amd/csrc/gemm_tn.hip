@@ -367,7 +367,10 @@ int gemm_tn_splits(int M, int N, int T, int cus, int small) {
   if (t == 128) cus *= 2;
   const int tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
   const int steps = (T + GBK - 1) / GBK;
-  int s = (cus + tiles - 1) / tiles;  // ~ one block per CU
+  // at most one block per resident slot: tiles x splits past the slot count
+  // leaves a second, nearly empty wave of blocks that costs a whole block time
+  // (GPT-2's 27 / 9 / 36-tile shapes ran 261-288 blocks on 256 CUs)
+  int s = cus / tiles;
   const int max_s = steps / 4 > 0 ? steps / 4 : 1;  // >= 4 K-steps per split
   if (s > max_s) s = max_s;
   if (s < 1) s = 1;

@@ -859,7 +859,7 @@ def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
     P, K = g2d.shape
     C = x2d.shape[1]
     Pg = P // G
-    if _TN_1X1 and _wgrad_tn_ok(g2d, x2d, None, G):
+    if _WGRAD_TN and _wgrad_tn_ok(g2d, x2d, None, G):
         # the native split-K TN GEMM's slabs (csrc/gemm_tn.hip, slab-only)
         return _ops().gemm_tn_parts(g2d, x2d, G)
     S = _wgrad_splits(Pg, K, C, G)
@@ -869,10 +869,12 @@ def _wgrad_parts(g2d: torch.Tensor, x2d: torch.Tensor, G: int = 1):
                      out_dtype=torch.float32), S
 
 
-# 1x1 weight gradients with both sides multiples of 256 on the native TN GEMM
-# (the column-image parts stay on hipBLASLt's batched GEMM: the native split
-# products measured 1.2-1.9x slower there, profiles/r4_experiments.md)
-_TN_1X1 = True
+# every weight gradient _wgrad_tn_ok accepts -- 1x1 convs, linears and the
+# (implicit or materialised) column images of the stems and strided convs -- on
+# the native split-K TN GEMM (256 x 256 tiles for 256-multiples, 128 x 128
+# otherwise; round 5: no slower than hipBLASLt's batched GEMMs on the narrow
+# shapes, profiles/r5_experiments.md); False routes them to hipBLASLt (A/B)
+_WGRAD_TN = True
 
 
 def _wgrad_tn_ok(g2d: torch.Tensor, x2d: torch.Tensor, into, G: int) -> bool:
@@ -910,7 +912,7 @@ def _wgrad_gemm(g2d: torch.Tensor, x2d: torch.Tensor, into=None, G: int = 1) -> 
     P, K = g2d.shape
     C = x2d.shape[1]
     Pg = P // G
-    if _TN_1X1 and _wgrad_tn_ok(g2d, x2d, into, G):
+    if _WGRAD_TN and _wgrad_tn_ok(g2d, x2d, into, G):
         # native split-K TN GEMM (csrc/gemm_tn.hip), all groups in one launch,
         # splits summed in a fixed order into the flat (or per-group) gradient
         sink = into if into is not None else torch.zeros(

@@ -1167,7 +1167,9 @@ class FedModel:
         reference's worker model accumulated them client after client)."""
         eng = self._fedavg_native_engine()
         if eng is not None:
-            return self._fedavg_native(eng, rb, order, starts, my_slots, mine, counts, W, out)
+            res = self._fedavg_native(eng, rb, order, starts, my_slots, mine, counts, W, out)
+            if res is not None:
+                return res
         from torch.func import grad, vmap
         from torch.nn.utils.stateless import _reparametrize_module
         from ..ops.nn import stock_ops, vmap_native_convs
@@ -1307,6 +1309,15 @@ class FedModel:
             Gp = len(slots)
             pos = np.concatenate([order[starts[s]:starts[s + 1]] for s in slots])
             x, y = rb.take(pos)[:2]
+            if p0 == 0:
+                # input geometry the engine's kernels cover (nothing has run yet):
+                # otherwise auto mode takes the vmap composition for good
+                ok, why = eng.accepts(tuple(x.shape))
+                if not ok:
+                    if getattr(a, "fedavg_engine", "auto") == "native":
+                        raise ValueError(f"--fedavg_engine native: {why}")
+                    self._fa_native = False
+                    return None
             if not (x.dtype == torch.bfloat16 and x.stride(1) == 1):
                 x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             lm, am, sums = eng.run(self.w, x, y, Gp, n, bs, a.num_fedavg_epochs, self.fedavg_lr,

@@ -132,6 +132,24 @@ class ResNet18FedAvg:
                 return False, "frozen parameters"
         return True, ""
 
+    def accepts(self, shape) -> Tuple[bool, str]:
+        """Whether a client batch of this NCHW ``shape`` runs on the engine's
+        kernels (checked before a round mutates anything): the input channels
+        of the model's stem, and a final feature map of at most 256 pixels for
+        the fused pooling head (fa_head_fwd / fa_head_bwd) -- e.g. 32 x 32
+        CIFAR or 28 x 28 EMNIST images, not 224 x 224 ImageNet ones."""
+        if len(shape) != 4:
+            return False, f"input of shape {tuple(shape)}: NCHW images expected"
+        _, c, h, w = shape
+        if c != self.cin0:
+            return False, f"{c} input channels, the stem takes {self.cin0}"
+        for b in self.blocks:
+            if b.stride == 2:
+                h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        if h * w > 256:
+            return False, f"final feature map {h}x{w} > 256 pixels (fused pooling head)"
+        return True, ""
+
     def __init__(self, model, flat, names: List[str]):
         self.model = model
         off = {nm: int(o) for nm, o in zip(names, flat.offsets)}

@@ -11,3 +11,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/rp -o tr --
 python scripts/round_kernels.py $O/rp/tr_kernel_trace.csv --marker augment_kernel --rounds 12 --sequence --top 60 > $O/seq.txt 2>&1
 rm -f $O/rp/tr_kernel_trace.csv
 head -70 $O/seq.txt
+timeout -k 10 200 python scripts/bench_gemm_tn.py > $O/tn.log 2>&1 || { tail -20 $O/tn.log; exit 1; }
+cat $O/tn.log

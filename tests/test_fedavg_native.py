@@ -52,6 +52,28 @@ def test_engine_layout_matches_parameter_order():
     assert eng.feat == 512 and eng.ncls == 100
 
 
+def test_engine_accepts_only_covered_geometry():
+    """auto mode must fall back to vmap (not fail mid-round) for inputs the
+    engine's kernels do not cover: the fused pooling head takes final maps of
+    <= 256 pixels, and the stem its own input channel count."""
+    m = ResNet18(num_classes=100)
+    names = [nm for nm, p in m.named_parameters()]
+
+    class _Flat:
+        offsets, numels = [], []
+    o = 0
+    for p in m.parameters():
+        _Flat.offsets.append(o)
+        _Flat.numels.append(p.numel())
+        o += p.numel()
+    eng = ResNet18FedAvg(m, _Flat, names)
+    assert eng.accepts((5, 3, 32, 32))[0]
+    assert eng.accepts((5, 3, 128, 128))[0]  # 16 x 16 final map
+    ok, why = eng.accepts((5, 3, 224, 224))
+    assert not ok and "256" in why
+    assert not eng.accepts((5, 1, 28, 28))[0]  # a 3-channel stem
+
+
 # ----------------------------------------------------------------- kernels
 def _cs(t, G):
     """[G, n, C, H, W] fp32 -> channel-stacked bf16 [n, G*C, H, W] channels_last"""
@@ -460,11 +482,38 @@ def test_native_round_matches_vmap_and_fp32(extra):
     """Upload and per-client losses of the native program vs the vmap
     composition (bf16) and the fp32 sequential path: the native round must be
     as close to fp32 as the bf16 vmap round is."""
+    _check_native_round(extra, 6, 5)
+
+
+@pytest.mark.gpu
+def test_native_round_multi_pass_uneven(monkeypatch):
+    """A --grouped_gb small enough for 3 clients per pass splits 7 clients
+    into passes of 3, 3 and 1: the running-statistic sums accumulate across
+    passes, num_batches_tracked advances once (first pass only), the stem's
+    padded weight image is re-made for the smaller last pass -- and the round
+    still matches the vmap and fp32 rounds."""
+    from commefficient_amd.parallel import fedavg_native as fa
+    d = sum(p.numel() for p in ResNet18(num_classes=100).parameters())
+    gb = 3.5 * 12 * d / 2 ** 30  # per pass: int(gb 2^30) // (12 d) = 3 clients
+    passes = []
+    orig = fa.ResNet18FedAvg.run
+
+    def run(self, *a, **kw):
+        passes.append(a[3])  # G of the pass
+        return orig(self, *a, **kw)
+
+    monkeypatch.setattr(fa.ResNet18FedAvg, "run", run)
+    _check_native_round(["--fedavg_batch_size", "-1", "--num_fedavg_epochs", "2", "--grouped_gb", str(gb)],
+                        7, 5, passes)
+
+
+def _check_native_round(extra, G, n, passes=None):
     torch.manual_seed(0)
     base = ResNet18(num_classes=100)
-    G, n = 6, 5
     up_n, l_n, b_n, fed = _round(base, "native", "bf16", G, n, extra)
     assert fed._fa_native, "native engine did not run"
+    if passes is not None:
+        assert passes == [3, 3, 1], passes
     up_v, l_v, b_v, _ = _round(base, "vmap", "bf16", G, n, extra)
     up_f, l_f, b_f, _ = _round(base, "vmap", "fp32", G, n, extra + ["--fedavg_batched", "off"])
     noise = ((up_v - up_f).norm() / up_f.norm()).item()
