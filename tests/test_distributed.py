@@ -67,7 +67,7 @@ def _run(rank, world, port, mode, out_dir, rounds, device="cpu"):
     torch.manual_seed(0)
     model = models.ResNet9(channels={"prep": 4, "layer1": 8, "layer2": 8, "layer3": 16})
     ds = make_synthetic("CIFAR10", train=True, num_clients=40, size=160, seed=3)
-    loader = DeviceFedLoader(ds, 6, -1, device, seed=5, augment=True)
+    loader = DeviceFedLoader(ds, 6, -1, device, seed=5, augment=True, out_bf16=False)
     model = model.to(device)
     fed = FedModel(model, cv_loss, args, num_clients=40)
     opt = FedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05), args, fed)
