@@ -13,6 +13,8 @@ import threading
 import torch
 
 _LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C.so")
+# A/B measurements only: load another build of the same sources instead
+_LIB = os.environ.get("COMMEFF_LIB") or _LIB
 _lock = threading.Lock()
 _loaded = False
 

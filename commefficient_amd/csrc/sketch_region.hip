@@ -227,32 +227,58 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
   const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
   const uint32_t grp = blockIdx.x + L.g0, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t W = blockDim.x >> 6, gm = g * m, rbase = grp * g;
+  if (vec4) {
+    // every row's staging loads of a pass issued before its stores (SU float4
+    // of table, G and V per thread in flight): one dependent HBM round trip per
+    // pass instead of one per row -- the rows' loads were serialised behind
+    // the previous row's stores (table / V may alias G as far as the compiler
+    // knows)
+    constexpr int SU = 4;
+    const uint32_t q4 = gm >> 2, n4 = r * q4;
+    for (uint32_t e0 = tid; e0 < n4; e0 += SU * blockDim.x) {
+      float4 t[SU], gg[SU], vv[SU];
+      size_t o[SU];
+      uint32_t di[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const uint32_t e = min(e0 + u * blockDim.x, n4 - 1);  // (clamped: loads unconditional)
+        const uint32_t j = e / q4, ee = e - j * q4;
+        o[u] = static_cast<size_t>(blockIdx.x) * L.gs + static_cast<size_t>(j) * L.rs + 4 * ee;
+        di[u] = j * gm + 4 * ee;
+        t[u] = *reinterpret_cast<const float4*>(table + o[u]);
+        if (mom.mode != 0) {
+          gg[u] = *reinterpret_cast<const float4*>(mom.G + o[u]);
+          vv[u] = mom.mode == 1 ? *reinterpret_cast<const float4*>(mom.V + o[u]) : t[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        if (e0 + u * blockDim.x >= n4) break;
+        float4 tt = t[u];
+        if (mom.mode != 0) {
+          float4 v = vv[u];
+          // (explicit fmaf, as in momentum_ef: identical rounding)
+          v.x = fmaf(mom.rho, v.x, mom.gscale * gg[u].x);
+          v.y = fmaf(mom.rho, v.y, mom.gscale * gg[u].y);
+          v.z = fmaf(mom.rho, v.z, mom.gscale * gg[u].z);
+          v.w = fmaf(mom.rho, v.w, mom.gscale * gg[u].w);
+          if (mom.mode == 1) {
+            *reinterpret_cast<float4*>(mom.V + o[u]) = v;
+            tt.x += v.x; tt.y += v.y; tt.z += v.z; tt.w += v.w;
+          } else {
+            tt = v;
+          }
+          *reinterpret_cast<float4*>(table + o[u]) = tt;
+        }
+        *reinterpret_cast<float4*>(reg + di[u]) = tt;
+      }
+    }
+  } else {
   for (uint32_t j = 0; j < r; ++j) {
     const size_t o = static_cast<size_t>(blockIdx.x) * L.gs + static_cast<size_t>(j) * L.rs;
     float* src = table + o;
     float* dst = reg + j * gm;
-    if (vec4) {
-      for (uint32_t e = tid; e < (gm >> 2); e += blockDim.x) {
-        float4 t = reinterpret_cast<const float4*>(src)[e];
-        if (mom.mode != 0) {
-          const float4 gg = reinterpret_cast<const float4*>(mom.G + o)[e];
-          float4 v = mom.mode == 1 ? reinterpret_cast<const float4*>(mom.V + o)[e] : t;
-          // (explicit fmaf, as in momentum_ef: identical rounding)
-          v.x = fmaf(mom.rho, v.x, mom.gscale * gg.x);
-          v.y = fmaf(mom.rho, v.y, mom.gscale * gg.y);
-          v.z = fmaf(mom.rho, v.z, mom.gscale * gg.z);
-          v.w = fmaf(mom.rho, v.w, mom.gscale * gg.w);
-          if (mom.mode == 1) {
-            reinterpret_cast<float4*>(mom.V + o)[e] = v;
-            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-          } else {
-            t = v;
-          }
-          reinterpret_cast<float4*>(src)[e] = t;
-        }
-        reinterpret_cast<float4*>(dst)[e] = t;
-      }
-    } else {
+    {
       for (uint32_t e = tid; e < gm; e += blockDim.x) {
         float t = src[e];
         if (mom.mode != 0) {
@@ -268,6 +294,7 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
         dst[e] = t;
       }
     }
+  }
   }
   uint32_t pw[NR];
 #pragma unroll

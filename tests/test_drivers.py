@@ -176,6 +176,34 @@ def test_gpt2_resume_reproduces_uninterrupted_run(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_gpt2_small_fetchsgd_learns_bigram_text():
+    """The full-size GPT-2 of the GPT-2 config (12 layers x 768, 124M
+    parameters) learns under FetchSGD (5 x 500,000 sketch, k = 50,000,
+    virtual momentum 0.9) on the learnable bigram text: validation LM nll
+    10.95 at init, 8.9 after 100 rounds at LR 0.05 on MI355X
+    (profiles/r6_gpt2_small_learning.jsonl: 7.97 at round 125; LR 0.02 / 0.1
+    reach 9.59 / 7.64 by round 150).  The first ~25 rounds' TRAINING loss
+    sits above the init value (momentum + error-feedback transient: 11.02
+    averaged over rounds 1-25 at LR 0.05) -- what the 13-round
+    bench_configs run shows as loss_last > ln 50257."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                        "gpt2_learning.py")
+    spec = importlib.util.spec_from_file_location("gpt2_learning", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    extra = ["--mode", "sketch", "--error_type", "virtual", "--local_momentum", "0",
+             "--virtual_momentum", "0.9", "--num_rows", "5", "--num_cols", "500000", "--k", "50000",
+             "--lr_scale", "0.05"]
+    rows = mod.curve(100, 25, extra, "small", log=print)
+    first = rows[0]["val_nll"]
+    best = min(r["val_nll"] for r in rows[1:])
+    assert first > 10.5, rows
+    assert best < first - 1.2, rows
+    assert rows[-1]["val_nll"] < rows[1]["val_nll"], rows
+
+
+@pytest.mark.gpu
 def test_gpt2_fetchsgd_learns_bigram_text():
     """GPT-2 under FetchSGD learns (reference objective gpt2_train.py:88-99,
     server fed_aggregator.py:568-613): on the learnable synthetic PersonaChat
