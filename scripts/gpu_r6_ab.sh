@@ -10,8 +10,8 @@ if [ -n "${TESTS-tests/test_conv.py}" ]; then
 fi
 for r in 1 2; do
   for v in $VALS; do
-    env $VAR=$v timeout -k 10 200 python scripts/dev/conv_lab.py > $O/lab_${v}_${r}.log 2>&1 || { tail -20 $O/lab_${v}_${r}.log; exit 1; }
-    echo "$VAR=$v lab: $(tail -1 $O/lab_${v}_${r}.log)"
+    env $VAR=$v timeout -k 10 200 python ${MICRO:-scripts/dev/conv_lab.py} > $O/lab_${v}_${r}.log 2>&1 || { tail -20 $O/lab_${v}_${r}.log; exit 1; }
+    echo "$VAR=$v lab: $(grep '^{' $O/lab_${v}_${r}.log | cut -c1-330)"
     env $VAR=$v timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/b_${v}_${r}.log 2>&1 || { tail -20 $O/b_${v}_${r}.log; exit 1; }
     python -c "import json; r=json.loads(open('$O/b_${v}_${r}.log').read().strip().splitlines()[-1]); print('$VAR=$v bench', r['value'], r['ms_per_step'])"
   done
