@@ -1190,6 +1190,20 @@ const uint16_t* opt_like(const c10::optional<at::Tensor>& t, const at::Tensor& y
   return bf16_ptr(*t);
 }
 
+// launch_conv3x3_fwd with its split-K workspace (if the launch wants one:
+// a grid of few tiles) from the caching allocator -- stream-ordered reuse,
+// and under a tape recording the capture's private pool keeps its address
+void run_conv3x3_fwd(ConvFwdArgs& a) {
+  const int64_t ws = conv3x3_fwd_split_floats(a);
+  at::Tensor part;
+  if (ws > 0) {
+    part = at::empty({ws}, at::TensorOptions().dtype(at::kFloat).device(
+                               at::Device(at::kCUDA, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().device_index())));
+    a.part = part.data_ptr<float>();
+  }
+  launch_conv3x3_fwd(a, cur_stream());
+}
+
 // y = act(conv3x3(x, w)) ; w bf16 [K][3][3][C] contiguous
 at::Tensor conv3x3_fwd_impl(const at::Tensor& x, const at::Tensor& w, bool relu,
                             const c10::optional<at::Tensor>& mask,
@@ -1225,7 +1239,7 @@ at::Tensor conv3x3_fwd_impl(const at::Tensor& x, const at::Tensor& w, bool relu,
     *pre = at::empty_like(y, y.options().memory_format(at::MemoryFormat::ChannelsLast));
     a.y_pre = reinterpret_cast<uint16_t*>(pre->data_ptr());
   }
-  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  if (a.P > 0) run_conv3x3_fwd(a);
   return y;
 }
 
@@ -1342,7 +1356,7 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_dual_hip(const at::Tensor& x, con
   a.K = static_cast<int>(K);
   a.relu = 0;
   a.pool = 0;
-  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  if (a.P > 0) run_conv3x3_fwd(a);
   return {y, yd};
 }
 
@@ -1383,7 +1397,7 @@ at::Tensor conv3x3_fwd_unpool_hip(const at::Tensor& x, const at::Tensor& w,
   a.K = static_cast<int>(K);
   a.relu = 0;
   a.pool = 0;
-  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  if (a.P > 0) run_conv3x3_fwd(a);
   return y;
 }
 
@@ -1419,7 +1433,7 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_pool2_hip(const at::Tensor& x, co
   a.K = static_cast<int>(K);
   a.relu = 1;
   a.pool = 2;
-  if (a.P > 0) launch_conv3x3_fwd(a, cur_stream());
+  if (a.P > 0) run_conv3x3_fwd(a);
   return {y, idx};
 }
 

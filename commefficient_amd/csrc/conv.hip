@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <stdexcept>
 #include "kernels.h"
 #include "conv_common.h"
 
@@ -444,12 +445,19 @@ constexpr int halo_lds() { return HaloCfg<TBM>::kWinBytes + 2 * BN * 128; }
 // read flipped: the B tile of (tap, 64-channel block) is staged k-major
 // ([64 k][128 c], 256-byte rows: the rows' own order) and its fragments come
 // from transposing LDS reads -- no transposed weight image per step.
-template <int TBM, bool POOL, bool SPLIT = false, int BN = 128, bool BT = false>
+// KS: split-K across blocks (a.ksplit blocks per output tile, each a whole
+// number of 64-channel blocks): the partial tile goes to a.part, and
+// conv_fwd_combine_kernel sums the splits in a fixed order and runs the
+// epilogue.  For grids of few tiles -- e.g. the per-rank round of a
+// strong-scaled W = 100 round at N = 8 (13 clients): res3's 4x4 maps are 36
+// tiles of 72 K-steps for 256 CUs.
+template <int TBM, bool POOL, bool SPLIT = false, int BN = 128, bool BT = false, bool KS = false>
 __global__ void __launch_bounds__(TBM * 2 * (SPLIT ? 2 : 1))
 __attribute__((amdgpu_waves_per_eu((TBM == 256 && !SPLIT) ? 4 : 1)))  // two 8-wave blocks per CU
 conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   static_assert(BN == 128 || (BN == 64 && !SPLIT && !POOL), "halo tile width");
   static_assert(!BT || (!SPLIT && !POOL), "transposed weight rows: plain tiles");
+  static_assert(!KS || (!SPLIT && !BT), "cross-block split-K: plain tiles");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
   // group g (split-K half) of this block: its own window + B ring
   const int half = SPLIT ? static_cast<int>(threadIdx.x) / (TBM * 2) : 0;
@@ -458,13 +466,18 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
   constexpr int kHaloWinBytes = HaloCfg<TBM>::kWinBytes, kHaloWinLd = HaloCfg<TBM>::kWinLd;
   const int tid = threadIdx.x & (NT - 1), lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int kspl = KS ? bid0 % a.ksplit : 0, bid = KS ? bid0 / a.ksplit : bid0;
   const int ntn = a.K / BN;
   const int tn = bid % ntn, tm = bid / ntn;
   const int m0 = tm * TBM, n0 = tn * BN;
   const int C = a.C, H = a.H, W = a.W, HW = H * W;
   const int KT = 9 * (C >> 6);
-  const int s_beg = SPLIT ? half * (KT / 2) : 0, s_end = SPLIT ? s_beg + KT / 2 : KT;
+  int s_beg = SPLIT ? half * (KT / 2) : 0, s_end = SPLIT ? s_beg + KT / 2 : KT;
+  if constexpr (KS) {
+    s_beg = kspl * (KT / a.ksplit);
+    s_end = s_beg + KT / a.ksplit;
+  }
   const int img0 = m0 / HW, h0 = (m0 - img0 * HW) / W;  // first image / row of the tile
   // grouped (channel-stacked) images: row stride and this tile's channel group
   const int xs = a.x_stride > 0 ? a.x_stride : C;
@@ -679,9 +692,69 @@ conv_fwd_halo_kernel(ConvFwdArgs a, HaloGeom hg) {
     __syncthreads();  // red is read before the epilogue overwrites the region
     conv_fwd_epilogue<TBM, BN, POOL, TBM * 4>(a, acc, smem_base, m0, n0, threadIdx.x, wr, wc, hi, lr,
                                               half == 0);
+  } else if constexpr (KS) {
+    // the partial tile, [tile][split][accumulator register][thread]: a wave's
+    // stores and the combine kernel's loads are 256-byte runs
+    float* pt = a.part + static_cast<size_t>(bid * a.ksplit + kspl) * (2 * NI * 16) * NT + tid;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pt[static_cast<size_t>((mi * NI + ni) * 16 + e) * NT] = acc[mi][ni][e];
   } else {
     conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, m0, n0, tid, wr, wc, hi, lr);
   }
+}
+
+// sum[t][i] = sum over s of part[t][s][i], s in order (deterministic), 16
+// bytes a thread: the splits' reduction spread over the whole chip (the
+// combine kernel below has only one block per tile)
+__global__ void __launch_bounds__(256) conv_fwd_psum_kernel(const float* __restrict__ part, float* __restrict__ sum,
+                                                            int tiles, int ks, int n4) {
+  const int q = blockIdx.x * 256 + threadIdx.x;  // float4 index over tiles x n4
+  if (q >= tiles * n4) return;
+  const int t = q / n4, i = q - t * n4;
+  const float4* p = reinterpret_cast<const float4*>(part) + static_cast<size_t>(t) * ks * n4 + i;
+  float4 a = p[0];
+  for (int s = 1; s < ks; ++s) {
+    const float4 b = p[static_cast<size_t>(s) * n4];
+    a.x += b.x;
+    a.y += b.y;
+    a.z += b.z;
+    a.w += b.w;
+  }
+  reinterpret_cast<float4*>(sum)[q] = a;
+}
+
+// sum of a tile's a.ksplit partials (split order: deterministic) in the
+// accumulator layout of conv_fwd_halo_kernel, then its epilogue
+template <int TBM, bool POOL, int BN>
+__global__ void __launch_bounds__(TBM * 2) conv_fwd_combine_kernel(ConvFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NI = BN / 64, NT = TBM * 2, NREG = 2 * NI * 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1, hi = lane >> 5, lr = lane & 31;
+  const int tile = blockIdx.x, ntn = a.K / BN;
+  const int m0 = (tile / ntn) * TBM, n0 = (tile % ntn) * BN;
+  f32x16_t acc[2][NI];
+  const float* pt = a.part + static_cast<size_t>(tile) * a.ksplit * NREG * NT + tid;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[mi][ni][e] = pt[static_cast<size_t>((mi * NI + ni) * 16 + e) * NT];
+  for (int s = 1; s < a.ksplit; ++s) {
+    const float* ps = pt + static_cast<size_t>(s) * NREG * NT;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mi][ni][e] += ps[static_cast<size_t>((mi * NI + ni) * 16 + e) * NT];
+  }
+  conv_fwd_epilogue<TBM, BN, POOL>(a, acc, smem, m0, n0, tid, wr, wc, hi, lr);
 }
 
 // ------------------------------------------------------------------ wgrad
@@ -1633,10 +1706,66 @@ bool launch_conv3x3_fwd_grouped(ConvFwdArgs a, hipStream_t stream) {
   return false;
 }
 
+// cross-block split-K of the 128-pixel halo tiles (KS above): when the grid
+// has at most a quarter of the resident slots in tiles, each tile's channel
+// blocks are split over S blocks (S a power of two dividing them, tiles x S
+// within the slots)
+static int fwd_ksplit(const ConvFwdArgs& a) {
+  HaloGeom hg;
+  if (a.kg != 0 || a.w_bt != 0) return 1;
+  if (halo_geom(a.H, a.W, a.K, 256, &hg) &&
+      static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) * 10 >= wgrad_slots() * 9)
+    return 1;  // (the 256-pixel path)
+  if (!halo_geom(a.H, a.W, a.K, 128, &hg)) return 1;
+  const int64_t tiles = static_cast<int64_t>((a.P + 127) / 128) * (a.K / 128);
+  const int ncb = a.C / 64;
+  if (tiles * 4 > wgrad_slots()) return 1;
+  int S = 1;
+  while (ncb % (2 * S) == 0 && tiles * 2 * S <= wgrad_slots()) S *= 2;
+  return S >= 4 ? S : 1;
+}
+
+int64_t conv3x3_fwd_split_floats(const ConvFwdArgs& a) {
+  const int S = fwd_ksplit(a);
+  if (S <= 1) return 0;
+  return static_cast<int64_t>((a.P + 127) / 128) * (a.K / 128) * (S + 1) * 128 * 128;
+}
+
+template <bool POOL>
+static void launch_fwd_ksplit(const ConvFwdArgs& a, const HaloGeom& hg, hipStream_t stream) {
+  constexpr int lds = halo_lds<128, 128>(), epi = 128 * (128 + 4) * 4;
+  static bool init = false;
+  if (!init) {
+    set_lds(reinterpret_cast<const void*>(conv_fwd_halo_kernel<128, POOL, false, 128, false, true>), lds);
+    set_lds(reinterpret_cast<const void*>(conv_fwd_combine_kernel<128, POOL, 128>), epi);
+    init = true;
+  }
+  const int tiles = ((a.P + 127) / 128) * (a.K / 128);
+  COMMEFF_LAUNCH((conv_fwd_halo_kernel<128, POOL, false, 128, false, true>), dim3(tiles * a.ksplit), dim3(256), lds,
+                 stream, a, hg);
+  // splits summed chip-wide into the tile buffer behind the partials, then the
+  // epilogue from the summed tile
+  constexpr int n4 = 128 * 128 / 4;
+  ConvFwdArgs b = a;
+  b.part = a.part + static_cast<size_t>(tiles) * a.ksplit * 128 * 128;
+  b.ksplit = 1;
+  COMMEFF_LAUNCH(conv_fwd_psum_kernel, dim3((tiles * n4 + 255) / 256), dim3(256), 0, stream,
+                 static_cast<const float*>(a.part), b.part, tiles, a.ksplit, n4);
+  COMMEFF_LAUNCH((conv_fwd_combine_kernel<128, POOL, 128>), dim3(tiles), dim3(256), epi, stream, b);
+}
+
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream) {
   a.div_w = make_fastdiv(static_cast<uint32_t>(a.W));
   a.div_h = make_fastdiv(static_cast<uint32_t>(a.H));
   HaloGeom hg;
+  const int ks = fwd_ksplit(a);
+  if (ks > 1) {
+    if (a.part == nullptr) throw std::runtime_error("conv3x3_fwd: split-K workspace not set");
+    a.ksplit = ks;
+    (void)halo_geom(a.H, a.W, a.K, 128, &hg);
+    if (a.pool == 2) launch_fwd_ksplit<true>(a, hg, stream); else launch_fwd_ksplit<false>(a, hg, stream);
+    return;
+  }
   // 256-pixel tiles when they still give ~every resident slot (2 per CU) a block
   if (halo_geom(a.H, a.W, a.K, 256, &hg) &&
       static_cast<int64_t>((a.P + 255) / 256) * (a.K / 128) * 10 >= wgrad_slots() * 9) {

@@ -281,6 +281,10 @@ struct ConvFwdArgs {
   // grouped input gradient (with w_gs != 0): w holds the CONV's weight rows
   // [C][3][3][kg] per group, read flipped and transposed (conv_fwd_halo_kernel BT)
   int w_bt = 0;
+  // split-K across blocks for grids of few tiles (conv3x3_fwd_split_floats > 0):
+  // fp32 partial tiles, summed by a combine kernel that runs the epilogue
+  float* part = nullptr;
+  int ksplit = 0;
 };
 struct ConvWgradArgs {
   const uint16_t* dy;  // [P, K]
@@ -315,6 +319,9 @@ struct ConvWgradArgs {
 bool conv3x3_supported(int C, int K);
 bool conv3x3_pool_supported(int H, int W, int K);
 void launch_conv3x3_fwd(ConvFwdArgs a, hipStream_t stream);
+// fp32 workspace (floats) the launch of a needs for its cross-block split-K
+// (0: none; the caller sets a.part to that many floats before launching)
+int64_t conv3x3_fwd_split_floats(const ConvFwdArgs& a);
 int conv3x3_wgrad_splits(int P, int H, int W, int K, int C);
 // dw [K][C][3][3] fp32 = beta * dw + sum_p dy x  (beta 0: overwrite)
 void launch_conv3x3_wgrad(ConvWgradArgs a, float* dw, float beta, hipStream_t stream);

@@ -14,7 +14,12 @@ for r in 1 2; do
       timeout -k 10 200 python $MICRO > $O/micro_${v}_$r.log 2>&1 || { tail -20 $O/micro_${v}_$r.log; exit 1; }
       echo "$v micro: $(grep '^{' $O/micro_${v}_$r.log | cut -c1-400)"
     fi
-    timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/b_${v}_$r.log 2>&1 || { tail -20 $O/b_${v}_$r.log; exit 1; }
-    python -c "import json; r=json.loads(open('$O/b_${v}_$r.log').read().strip().splitlines()[-1]); print('$v bench', r['value'], r['ms_per_step'])"
+    i=0
+    IFS=';' read -ra BL <<< "${BARGS_LIST:- }"
+    for ba in "${BL[@]}"; do
+      i=$((i + 1))
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 $ba > $O/b_${v}_${r}_$i.log 2>&1 || { tail -20 $O/b_${v}_${r}_$i.log; exit 1; }
+      python -c "import json; r=json.loads(open('$O/b_${v}_${r}_$i.log').read().strip().splitlines()[-1]); print('$v bench [$ba]', r['value'], r['ms_per_step'])"
+    done
   done
 done

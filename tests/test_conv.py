@@ -57,11 +57,17 @@ def test_fwd_matches_fp32(N, C, H, W, K, relu):
 
 
 @pytest.mark.parametrize("N,C,H,W,K,pool", [(500, 512, 4, 4, 512, False),   # ResNet-9 res3
-                                             (64, 256, 8, 8, 128, True)])
+                                             (64, 256, 8, 8, 128, True),
+                                             (65, 512, 4, 4, 512, False),    # res3, 13 clients
+                                             (65, 512, 8, 8, 256, False),    # layer-3 dgrad shape
+                                             (16, 512, 8, 8, 128, True)])
 def test_fwd_split_k_halo(N, C, H, W, K, pool):
-    """Grids under half the resident slots run split-K (two blocks per tile,
-    conv.hip SPLIT): fp32-close and bitwise run-to-run deterministic; the
-    residual epilogue (mask + addend) still applies once."""
+    """Grids under half the resident slots run split-K: two blocks per tile
+    inside one workgroup (conv.hip SPLIT), or -- at most a quarter of the
+    slots in tiles, e.g. the per-rank round of a strong-scaled 100-client round
+    on 8 GPUs -- across workgroups (KS: fp32 partial tiles + a combine kernel
+    running the epilogue).  fp32-close and bitwise run-to-run deterministic;
+    the residual epilogue (mask + addend) and the fused pool still apply once."""
     x, w = _inputs(N, C, H, W, K)
     wf, _ = ops.conv_weight_prep(w)
     ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), padding=1)
