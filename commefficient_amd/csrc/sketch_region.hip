@@ -210,7 +210,7 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
                        const int32_t* __restrict__ lists, const int32_t* __restrict__ goffs,
                        uint32_t q0, uint32_t q1, int vec4, const uint32_t* __restrict__ hint,
                        uint32_t* __restrict__ hist0, RegionMom mom, uint64_t* __restrict__ ballots,
-                       uint32_t* __restrict__ segtot, const int32_t* __restrict__ cpos) {
+                       uint32_t* __restrict__ segtot, const int32_t* __restrict__ cpos, uint32_t bpg) {
   // ballots (m == 64): per chunk of est the mask of keys >= hint, and the
   // per-segment (1,024 chunks) popcount totals: the top-k's candidate list
   // (csrc/topk.hip cand_compact_kernel)
@@ -225,7 +225,11 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
   constexpr int NR = RT > 0 ? RT : kMaxRows;
   extern __shared__ __attribute__((aligned(16))) float reg[];  // [r][g * m]
   const uint32_t r = RT > 0 ? static_cast<uint32_t>(RT) : r_rt;
-  const uint32_t grp = blockIdx.x + L.g0, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // bpg blocks per group (a shard of few groups): each stages the group's
+  // regions (read-only: the momentum ran in its own pass) and gathers its
+  // 1/bpg of the group's chunk list
+  const uint32_t gl = blockIdx.x / bpg, part = blockIdx.x - gl * bpg;
+  const uint32_t grp = gl + L.g0, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t W = blockDim.x >> 6, gm = g * m, rbase = grp * g;
   if (vec4) {
     // every row's staging loads of a pass issued before its stores (SU float4
@@ -243,7 +247,7 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
       for (int u = 0; u < SU; ++u) {
         const uint32_t e = min(e0 + u * blockDim.x, n4 - 1);  // (clamped: loads unconditional)
         const uint32_t j = e / q4, ee = e - j * q4;
-        o[u] = static_cast<size_t>(blockIdx.x) * L.gs + static_cast<size_t>(j) * L.rs + 4 * ee;
+        o[u] = static_cast<size_t>(gl) * L.gs + static_cast<size_t>(j) * L.rs + 4 * ee;
         di[u] = j * gm + 4 * ee;
         t[u] = *reinterpret_cast<const float4*>(table + o[u]);
         if (mom.mode != 0) {
@@ -275,7 +279,7 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
     }
   } else {
   for (uint32_t j = 0; j < r; ++j) {
-    const size_t o = static_cast<size_t>(blockIdx.x) * L.gs + static_cast<size_t>(j) * L.rs;
+    const size_t o = static_cast<size_t>(gl) * L.gs + static_cast<size_t>(j) * L.rs;
     float* src = table + o;
     float* dst = reg + j * gm;
     {
@@ -301,7 +305,9 @@ cs_region_query_kernel(float* __restrict__ table, float* __restrict__ est, uint3
   for (int j = 0; j < NR; ++j) pw[j] = (j < static_cast<int>(r) && lane < m) ? perm[j * m + lane] : 0u;
   __syncthreads();
   const int rr = static_cast<int>(r);
-  const int32_t l0 = goffs[grp], l1 = goffs[grp + 1];
+  const int32_t ga = goffs[grp], gb = goffs[grp + 1], gn = gb - ga;
+  const int32_t l0 = ga + static_cast<int32_t>((static_cast<int64_t>(gn) * part) / bpg);
+  const int32_t l1 = ga + static_cast<int32_t>((static_cast<int64_t>(gn) * (part + 1)) / bpg);
   // chunk ids and words of the next UQ chunks of this wave are in flight
   // while the current UQ are gathered (VECTOR loads for the words: lane j < r
   // fetches row j's word, readlane broadcasts -- a scalar load's wait would
@@ -454,12 +460,36 @@ void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t 
                             RegionLayout L, hipStream_t stream, const uint32_t* hint, uint32_t* hist0,
                             float* momV, const float* momG, float rho, float gscale, int mom_mode,
                             uint64_t* ballots, uint32_t* segtot, const int32_t* cpos) {
-  const RegionMom mom{momV, momG, rho, gscale, mom_mode};
+  RegionMom mom{momV, momG, rho, gscale, mom_mode};
   if (m != 64 || hist0 == nullptr) ballots = nullptr;
   if (q1 <= q0 || L.g1 <= L.g0) return;
   const int lds = static_cast<int>(r * g * m * 4);
   const int vec4 = ((g * m) % 4 == 0 && L.gs % 4 == 0 && L.rs % 4 == 0) ? 1 : 0;
-  const dim3 grid(L.g1 - L.g0), block(static_cast<uint32_t>(64 * (W > 16 ? 16 : W)));
+  // a group-major shard of few groups (the sharded server at N ranks: G / N
+  // groups) would leave most CUs idle at one block per group while each
+  // block's time stays that of a whole group: several blocks per group then,
+  // the server momentum in its own elementwise pass first (the staging blocks
+  // only read)
+  static const int cus = [] {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    return (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+               ? prop.multiProcessorCount : 256;
+  }();
+  const uint32_t ng = L.g1 - L.g0;
+  uint32_t bpg = 1;
+  const bool shard = L.rs == static_cast<uint32_t>(g * m) && L.gs == static_cast<uint32_t>(r * g * m);
+  if (shard && 2 * ng <= static_cast<uint32_t>(cus)) {
+    bpg = static_cast<uint32_t>(cus) / ng;
+    if (bpg > 16) bpg = 16;
+  }
+  if (bpg > 1 && mom.mode != 0) {
+    const int64_t n = static_cast<int64_t>(ng) * r * g * m;  // the shard's cells, contiguous
+    if (mom.mode == 1) launch_momentum_ef(momV, table, momG, n, rho, gscale, 1, stream);
+    else launch_momentum_ef(table, nullptr, momG, n, rho, gscale, 0, stream);
+    mom.mode = 0;
+  }
+  const dim3 grid(ng * bpg), block(static_cast<uint32_t>(64 * (W > 16 ? 16 : W)));
 #define COMMEFF_REGION_QRY(RR, HH)                                                                       \
   do {                                                                                                   \
     static int done = 0;                                                                                 \
@@ -468,7 +498,7 @@ void launch_cs_region_query(float* table, float* est, int64_t d, int r, int64_t 
                        static_cast<uint32_t>(d), L, static_cast<uint32_t>(m),                            \
                        static_cast<uint32_t>(g), static_cast<uint32_t>(nch), static_cast<uint32_t>(r),   \
                        perm, cinfo, lists, goffs, static_cast<uint32_t>(q0), static_cast<uint32_t>(q1),  \
-                       vec4, hint, hist0, mom, ballots, segtot, cpos);                                   \
+                       vec4, hint, hist0, mom, ballots, segtot, cpos, bpg);                              \
   } while (0)
   if (hist0 != nullptr) {
     if (r == 5) COMMEFF_REGION_QRY(5, true);

@@ -186,6 +186,35 @@ def test_region_gpu_deterministic_and_sharded():
         assert torch.equal(idx, ref_idx) and torch.equal(vals, ref_vals)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,rank,et", [(8, 3, "virtual"), (4, 0, "none"), (2, 1, "virtual")])
+def test_region_gpu_group_shard_topk_matches_cpu(world, rank, et):
+    """The sharded server's query + top-k on one rank's group-major shard
+    (G / world groups; with few groups the query runs several blocks per group
+    after a separate momentum pass, csrc/sketch_region.hip bpg) equals the CPU
+    path: momentum / error feedback bitwise, and the same (index, value) list."""
+    d, c, r, k = 6568640, 500000, 5, 50000
+    h = RegionHash(d, c, r, seed=5)
+    g = torch.Generator().manual_seed(world * 10 + rank)
+    E, V, G = (torch.randn(r, c, generator=g) for _ in range(3))
+    Gp = h.shard_groups(world)
+    g0 = rank * Gp
+    shard = lambda t: h.group_major(t, world)[g0:g0 + Gp].contiguous()  # noqa: E731
+    Ec, Vc, Gc = shard(E), shard(V), shard(G)
+    Eg, Vg, Gg = Ec.cuda(), Vc.cuda(), Gc.cuda()
+    src_c, src_g = (Ec, Eg) if et == "virtual" else (Vc, Vg)
+    li, lv, cmap = sketch_region.topk(h, src_g, k, None, mom=(Vg, Gg, 0.9, 0.01, et), g0=g0)
+    # momentum / error feedback (GPU: fmaf, CPU: two roundings)
+    sketch_region.topk(h, src_c, k, None, mom=(Vc, Gc, 0.9, 0.01, et), g0=g0)
+    torch.testing.assert_close(Vg.cpu(), Vc, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(Eg.cpu(), Ec, rtol=1e-6, atol=1e-6)
+    # the selection on the GPU's updated shard: the CPU query + top-k, bitwise
+    ci, cv, _ = sketch_region.topk(h, src_g.cpu(), k, None, g0=g0)
+    gi = cmap.long()[li // h.m] * h.m + li % h.m  # compact -> global coordinates
+    assert torch.equal(gi.cpu(), ci)
+    assert torch.equal(lv.cpu(), cv)
+
+
 def test_hot_chunks_are_filtered_by_the_median():
     # whole chunks of large values (a layer with big gradients) plus heavy
     # hitters elsewhere: independent per-row region assignments keep the
