@@ -1283,15 +1283,15 @@ class FedModel:
                 raise ValueError("--fedavg_engine native needs a GPU")
             return None
         if self._fa_native is None:
-            from .fedavg_native import ResNet18FedAvg
-            ok, why = ResNet18FedAvg.supported(self.model, self.args)
-            if not ok:
+            from .fedavg_native import engine_for
+            cls, why = engine_for(self.model, self.args)
+            if cls is None:
                 if mode == "native":
                     raise ValueError(f"--fedavg_engine native: {why}")
                 self._fa_native = False
             else:
                 names = [nm for nm, p in self.model.named_parameters() if p.requires_grad]
-                self._fa_native = ResNet18FedAvg(self.model, self.flat, names)
+                self._fa_native = cls(self.model, self.flat, names)
         return self._fa_native or None
 
     def _fedavg_native(self, eng, rb, order, starts, my_slots, mine, counts, W, out):
@@ -1332,10 +1332,11 @@ class FedModel:
             for b, s4 in zip(eng.blocks, acc_bufs):
                 dsts += [b.m1.running_mean, b.m2.running_mean, b.m1.running_var, b.m2.running_var]
                 srcs += list((s4 / len(mine)).to(b.m1.running_mean.dtype).unbind(0))
-            torch._foreach_copy_(dsts, srcs)
+            if dsts:  # (models without batch norm have none)
+                torch._foreach_copy_(dsts, srcs)
             # num_batches_tracked: every BatchNorm layer counts the local steps
             # (the engine advanced the first layer's counter)
-            nbt0 = eng.blocks[0].m1.num_batches_tracked
+            nbt0 = eng.blocks[0].m1.num_batches_tracked if eng.blocks else None
             for b in eng.blocks:
                 for m in (b.m1, b.m2):
                     if m.num_batches_tracked is not nbt0:

@@ -523,3 +523,215 @@ class ResNet18FedAvg:
         dy0 = ops.relu_mask(da, a0)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+
+
+class ResNet9FedAvg(ResNet18FedAvg):
+    """Explicit G-client forward / backward / local SGD of models.resnet9.ResNet9
+    (the headline model; BatchNorm off, as in the reference's FetchSGD / FedAvg
+    CIFAR runs, cv_train.py:357): prep conv3x3 + ReLU, layer1 conv + ReLU +
+    2x2 max-pool, res1 = x + relu(conv(relu(conv x))), layer2 / layer3 conv +
+    ReLU + pool, res3, 4x4 max-pool, linear (no bias) x 0.125 -- reference
+    /root/reference/CommEfficient/models/resnet9.py:32-148, local SGD
+    fed_worker.py:61-113.  Same layout and kernels as ResNet18FedAvg: client
+    rows (3x3 conv weights in the kernels' (k, r, s, c) order, bf16 mirror),
+    channel-stacked activations, the grouped halo convs (forward, input
+    gradient from the rows, weight gradient / fused SGD step), the grouped
+    stem GEMM, the ReLU + max-pool kernels of csrc/pool.hip on the stacked
+    channels, and a batched fp32 classifier on the weight rows."""
+
+    # (conv offset key, input channels key, output channels key, pool after)
+    _LAYERS = ("layer1", "res1.res1", "res1.res2", "layer2", "layer3", "res3.res1", "res3.res2")
+
+    @staticmethod
+    def supported(model, args) -> Tuple[bool, str]:
+        from ..models.resnet9 import ResNet9
+        if not isinstance(model, ResNet9):
+            return False, "not the ResNet9 of models/resnet9.py"
+        if getattr(args, "dtype", "bf16") != "bf16":
+            return False, "bf16 compute only"
+        if model.n.prep.do_batchnorm:
+            return False, "ResNet9 with BatchNorm"
+        n = model.n
+        if not (isinstance(n.pool, torch.nn.MaxPool2d) and n.linear.bias is None
+                and isinstance(n.layer1.pool, torch.nn.MaxPool2d)):
+            return False, "ResNet9 head / pools of another form"
+        ks = [n.layer1.pool.kernel_size, n.layer2.pool.kernel_size, n.layer3.pool.kernel_size, n.pool.kernel_size]
+        if [k if isinstance(k, int) else k[0] for k in ks] != [2, 2, 2, 4]:
+            return False, "ResNet9 pools must be 2, 2, 2 and 4"
+        chans = [model.channels[c] for c in ("prep", "layer1", "layer2", "layer3")]
+        if any(c % 64 for c in chans):
+            return False, "channel counts must be multiples of 64"
+        for p in model.parameters():
+            if not p.requires_grad:
+                return False, "frozen parameters"
+        return True, ""
+
+    def accepts(self, shape) -> Tuple[bool, str]:
+        """NCHW client batches of the stem's channels whose 8x-pooled map is the
+        4x4 the head pools whole (32 x 32 CIFAR images)."""
+        if len(shape) != 4:
+            return False, f"input of shape {tuple(shape)}: NCHW images expected"
+        _, c, h, w = shape
+        if c != self.cin0:
+            return False, f"{c} input channels, the stem takes {self.cin0}"
+        if h != 32 or w != 32:
+            return False, f"{h}x{w} images: the 4x4 max-pool head needs 32 x 32"
+        return True, ""
+
+    def __init__(self, model, flat, names: List[str]):
+        self.model = model
+        off = {nm: int(o) for nm, o in zip(names, flat.offsets)}
+        self.d = int(flat.d) if hasattr(flat, "d") else int(sum(flat.numels))
+        self.off = off
+        n = model.n
+        self.prep = off["n.prep.conv.weight"]
+        self.c0 = n.prep.conv.out_channels
+        self.cin0 = n.prep.conv.in_channels
+        self.blocks = []  # (no BatchNorm)
+        self.conv = {}
+        for key in self._LAYERS:
+            mod = n.get_submodule(key)
+            self.conv[key] = (off[f"n.{key}.conv.weight"], mod.conv.in_channels, mod.conv.out_channels)
+        self.fc_w = off["n.linear.weight"]
+        self.ncls = n.linear.out_features
+        self.feat = n.linear.in_features
+        self.scale = float(n.classifier.weight)
+
+    def _perm(self, device) -> torch.Tensor:
+        if getattr(self, "_perm_t", None) is None or self._perm_t.device != device:
+            import numpy as np
+            perm = np.arange(self.d, dtype=np.int64)
+            convs = [(self.prep, self.c0, self.cin0)] + [(o, K, C) for (o, C, K) in self.conv.values()]
+            for off, K, C in convs:
+                k, t, c = np.meshgrid(np.arange(K), np.arange(9), np.arange(C), indexing="ij")
+                perm[off:off + K * 9 * C] = off + ((k * C + c) * 9 + t).reshape(-1)
+            self._perm_t = torch.from_numpy(perm.astype(np.int32)).to(device)
+        return self._perm_t
+
+    def run(self, w0, x, y, G, n, bs, epochs, lr, decay, wd, clip, out, first_pass):
+        """As ResNet18FedAvg.run (no running statistics: returns an empty list)."""
+        ops = _ops()
+        dev = w0.device
+        d = self.d
+        ld = (d + 63) // 64 * 64
+        perm = self._perm(dev)
+        w0i = torch.empty(ld, device=dev, dtype=torch.float32)
+        w0b = torch.empty(ld, device=dev, dtype=torch.bfloat16)
+        ops.fa_gather_rows(w0i, w0b, w0, perm)
+        Wg = torch.empty((G, ld), device=dev, dtype=torch.float32)
+        Wb = torch.empty((G, ld), device=dev, dtype=torch.bfloat16)
+        fused = not clip
+        Gg = None if fused else torch.zeros((G, ld), device=dev, dtype=torch.float32)
+        loss_acc = torch.zeros(G, device=dev)
+        acc_acc = torch.zeros(G, device=dev)
+        steps = 0
+        xv = x.view(G, n, *x.shape[1:]) if bs < n else None
+        for _ in range(epochs):
+            for s0 in range(0, n, bs):
+                s1 = min(n, s0 + bs)
+                if bs < n:
+                    xb = xv[:, s0:s1].reshape(G * (s1 - s0), *x.shape[1:]).contiguous(
+                        memory_format=torch.channels_last)
+                    yb = y.view(G, n)[:, s0:s1].reshape(-1).contiguous()
+                else:
+                    xb, yb = x, y
+                W, Wbf, sld = (w0i, w0b, 0) if steps == 0 else (Wg, Wb, ld)
+                lr_t = float(lr * decay ** steps)
+                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, Wb, W, sld) if fused
+                        else _Sink(Gg, ld, 0.0, 1.0, None))
+                l, c = self._step9(xb, yb, G, s1 - s0, W, Wbf, sld, sink)
+                loss_acc += l
+                acc_acc += c
+                if not fused:
+                    ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip), lr_t, float(wd), Wb)
+                steps += 1
+        ops.fa_upload(out, w0i, Wg, ld, G, float(n), perm)
+        return loss_acc / steps, acc_acc / steps, []
+
+    def _step9(self, x, y, G, n, W, Wb, ld, sink):
+        ops = _ops()
+        # ---- stem (as ResNet18FedAvg._step): grouped column image x weight rows
+        C0, K0 = self.cin0, self.c0
+        Kc0 = (9 * C0 + 63) // 64 * 64 if _NATIVE_GMM[0] else (9 * C0 + 7) // 8 * 8
+        col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        col0g = col0.transpose(0, 1)[:, :, :9 * C0]
+        H, Wd = x.shape[2], x.shape[3]
+        y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
+                         memory_format=torch.channels_last)
+        w0rows = self._rows(Wb, ld, G, self.prep, K0, 9 * C0)
+        done = False
+        if _NATIVE_GMM[0] and Kc0 % 64 == 0:
+            pad = getattr(self, "_stem_img", None)
+            if pad is None or pad.shape != (G, K0, Kc0) or pad.device != x.device:
+                pad = self._stem_img = torch.zeros((G, K0, Kc0), device=x.device, dtype=torch.bfloat16)
+            pad[:, :, :9 * C0].copy_(w0rows)
+            done = ops.fa_gemm(col0.transpose(0, 1), pad, _gview(y0, G), False, 0.0)
+        if not done:
+            torch.bmm(col0g, w0rows.transpose(1, 2), out=_gview(y0, G))
+        a0 = ops.fa_ew(y0, None, 1)
+        cv = self.conv
+
+        def conv(xin, key):
+            off, C, K = cv[key]
+            return self._conv3(xin, Wb, ld, G, off, K, C)
+
+        # ---- forward (saving what the backward reads)
+        p1, c1 = ops.relu_maxpool(conv(a0, "layer1"), 2)
+        r1 = ops.fa_ew(conv(p1, "res1.res1"), None, 1)
+        r2 = ops.fa_ew(conv(r1, "res1.res2"), None, 1)
+        y1 = ops.fa_ew(p1, r2, 0)
+        p2, c2 = ops.relu_maxpool(conv(y1, "layer2"), 2)
+        p3, c3 = ops.relu_maxpool(conv(p2, "layer3"), 2)
+        s1 = ops.fa_ew(conv(p3, "res3.res1"), None, 1)
+        s2 = ops.fa_ew(conv(s1, "res3.res2"), None, 1)
+        y3 = ops.fa_ew(p3, s2, 0)
+        # ---- head: 4x4 max-pool (y3 >= 0: the ReLU is the identity) -> per-client
+        # fp32 features -> logits = 0.125 feat Wl^T (batched on the weight rows)
+        f16, c4 = ops.relu_maxpool(y3, 4)  # [n, G*512, 1, 1]
+        F_ = self.feat
+        feat = f16.view(n, G, F_).transpose(0, 1).float()  # [G, n, F]
+        Wl = self._rows(W, ld, G, self.fc_w, self.ncls, F_)
+        logits = torch.bmm(feat, Wl.transpose(1, 2)).mul_(self.scale)
+        loss, correct, gl = ops.ce_fwd(logits.reshape(G * n, self.ncls), y)
+        gl = gl.view(G, n, self.ncls)
+        a = self.scale / n
+        dfeat = torch.bmm(gl, Wl).mul_(a)  # (read before the rows may be updated in place)
+        gW = sink.dst[:, self.fc_w:self.fc_w + self.ncls * F_].view(G, self.ncls, F_)
+        torch.baddbmm(sink.src_rows(self.fc_w, self.ncls, F_), gl.transpose(1, 2), feat, beta=sink.beta,
+                      alpha=sink.alpha * a, out=gW)  # (the classifier reads the fp32 rows: no mirror)
+        dy3 = ops.relu_maxpool_backward(
+            dfeat.transpose(0, 1).reshape(n, G * F_, 1, 1).to(torch.bfloat16).contiguous(
+                memory_format=torch.channels_last), c4, 4)
+
+        def back(dy, xin, key, addend=None):
+            off, C, K = cv[key]
+            dx = self._conv3_dgrad(dy, Wb, ld, G, off, K, C, addend)
+            self._conv3_wgrad(dy, xin, G, sink, off, K, C)
+            return dx
+
+        # ---- res3: y3 = p3 + s2, s2 = relu(conv_b s1), s1 = relu(conv_a p3)
+        ds1 = back(ops.relu_mask(dy3, s2), s1, "res3.res2")
+        dp3 = back(ops.relu_mask(ds1, s1), p3, "res3.res1", dy3)
+        # ---- layer3, layer2 (relu + pool backward, then the conv)
+        dp2 = back(ops.relu_maxpool_backward(dp3, c3, 2), p2, "layer3")
+        dy1 = back(ops.relu_maxpool_backward(dp2, c2, 2), y1, "layer2")
+        # ---- res1
+        dr1 = back(ops.relu_mask(dy1, r2), r1, "res1.res2")
+        dp1 = back(ops.relu_mask(dr1, r1), p1, "res1.res1", dy1)
+        da0 = back(ops.relu_maxpool_backward(dp1, c1, 2), a0, "layer1")
+        # ---- stem weight gradient
+        dy0 = ops.relu_mask(da0, a0)
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+
+
+def engine_for(model, args):
+    """(engine class or None, why): the explicit G-client FedAvg program that
+    covers this model / configuration."""
+    why = []
+    for cls in (ResNet18FedAvg, ResNet9FedAvg):
+        ok, w = cls.supported(model, args)
+        if ok:
+            return cls, ""
+        why.append(f"{cls.__name__}: {w}")
+    return None, "; ".join(why)

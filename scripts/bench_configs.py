@@ -58,6 +58,14 @@ def cfg_args(name, N, b):
                    "--virtual_momentum", "0.9", "--num_clients", "10000", "--num_workers", str(W),
                    "--local_batch_size", "-1", "--fedavg_batch_size", "-1",
                    "--num_fedavg_epochs", "5", "--batchnorm"]
+    if name == "cifar10_resnet9_fedavg_local":
+        # the headline model under FedAvg: 5 local full-batch steps per client
+        W = b.clients or 100 * N
+        return W, ["--dataset_name", "CIFAR10", "--synthetic", "--model", "ResNet9",
+                   "--mode", "fedavg", "--error_type", "none", "--local_momentum", "0",
+                   "--virtual_momentum", "0.9", "--num_clients", "10000", "--num_workers", str(W),
+                   "--local_batch_size", "-1", "--fedavg_batch_size", "-1",
+                   "--num_fedavg_epochs", "5"]
     raise ValueError(name)
 
 
@@ -65,7 +73,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--config", required=True,
                    choices=["imagenet_local_topk", "gpt2_sketch", "cifar100_fedavg",
-                            "cifar100_fedavg_local"])
+                            "cifar100_fedavg_local", "cifar10_resnet9_fedavg_local"])
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--clients", type=int, default=0, help="clients per round (total)")
@@ -95,7 +103,7 @@ def main():
         from commefficient_amd.train import cv as drv
         from commefficient_amd.train.losses import cv_loss
         loader, _ = drv.get_data_loaders(args, ctx.device)
-        ncls = {"ImageNet": 1000, "CIFAR100": 100}[args.dataset_name]
+        ncls = {"ImageNet": 1000, "CIFAR100": 100, "CIFAR10": 10}[args.dataset_name]
         model = models.build_model(args, ncls)
         loss = vloss = cv_loss
         unit = "images/s"

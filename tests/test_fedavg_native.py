@@ -28,7 +28,12 @@ def test_supported_models():
     ok, _ = ResNet18FedAvg.supported(ResNet18(num_classes=100), _args())
     assert ok
     from commefficient_amd import models
+    from commefficient_amd.parallel.fedavg_native import ResNet9FedAvg, engine_for
     assert not ResNet18FedAvg.supported(models.ResNet9(), _args())[0]
+    assert ResNet9FedAvg.supported(models.ResNet9(), _args())[0]
+    assert not ResNet9FedAvg.supported(models.ResNet9(do_batchnorm=True), _args())[0]
+    assert engine_for(models.ResNet9(), _args())[0] is ResNet9FedAvg
+    assert engine_for(ResNet18(num_classes=100), _args())[0] is ResNet18FedAvg
     assert not ResNet18FedAvg.supported(ResNet18(num_classes=10), _args(["--dtype", "fp32"]))[0]
 
 
@@ -537,3 +542,54 @@ def _check_native_round(extra, G, n, passes=None):
             assert err <= 2 * bn_noise + 1e-2, (k, err, bn_noise)
         elif "num_batches" in k:
             assert b_n[k] == b_v[k], k
+
+
+# ------------------------------------------------------------ ResNet-9 engine
+def _round9(base, engine, dtype, G, n, extra, lr=0.05):
+    from commefficient_amd.parallel import dist
+    from commefficient_amd.parallel.fed_model import FedModel
+    from commefficient_amd.train.losses import cv_loss
+    dist.init("cuda")
+    args = parse_args(argv=["--dataset_name", "CIFAR10", "--mode", "fedavg", "--error_type", "none",
+                            "--local_momentum", "0", "--virtual_momentum", "0", "--num_workers", str(G),
+                            "--num_clients", str(G), "--local_batch_size", "-1", "--device", "cuda",
+                            "--dtype", dtype, "--fedavg_engine", engine] + extra, probe_port=False)
+    model = copy.deepcopy(base).cuda()
+    if dtype == "bf16":
+        model = model.to(memory_format=torch.channels_last)
+    fed = FedModel(model, cv_loss, args, num_clients=G)
+    fed.fedavg_lr = lr
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(G * n, 3, 32, 32, generator=g).cuda()
+    if dtype == "bf16":
+        x = x.bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (G * n,), generator=g).cuda()
+    out = fed((torch.arange(G).repeat_interleave(n), x, y))
+    torch.cuda.synchronize()
+    return fed._payload[:fed.d].clone(), out[0].clone(), fed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [
+    ["--fedavg_batch_size", "-1", "--num_fedavg_epochs", "2"],
+    ["--fedavg_batch_size", "2", "--num_fedavg_epochs", "1", "--weight_decay", "5e-4",
+     "--max_grad_norm", "2.0", "--fedavg_lr_decay", "0.9"],
+])
+def test_resnet9_native_round_matches_vmap_and_fp32(extra):
+    """The headline model's FedAvg round on the native G-client program
+    (ResNet9FedAvg: grouped halo convs, ReLU + max-pool kernels on the stacked
+    channels, batched classifier) vs the vmap composition (bf16) and the fp32
+    sequential path (fed_worker.py:61-113): as close to fp32 as bf16 vmap is."""
+    from commefficient_amd import models
+    torch.manual_seed(0)
+    base = models.ResNet9()
+    G, n = 5, 4
+    up_n, l_n, fed = _round9(base, "native", "bf16", G, n, extra)
+    assert fed._fa_native and type(fed._fa_native).__name__ == "ResNet9FedAvg"
+    up_v, l_v, _ = _round9(base, "vmap", "bf16", G, n, extra)
+    up_f, l_f, _ = _round9(base, "vmap", "fp32", G, n, extra + ["--fedavg_batched", "off"])
+    noise = ((up_v - up_f).norm() / up_f.norm()).item()
+    rel = ((up_n - up_f).norm() / up_f.norm()).item()
+    assert rel < 2 * noise + 2e-2, (rel, noise)
+    lnoise = (l_v - l_f).abs().max().item()
+    assert (l_n - l_f).abs().max().item() <= 2 * lnoise + 3e-2 * l_f.abs().max().item(), (l_n, l_v, l_f)
