@@ -528,12 +528,43 @@ __device__ __forceinline__ void load8f(const float* p, float (&f)[8]) {
 // POST (forward): y = relu(x A + B) + aux -- the residual add AFTER the ReLU
 // (models/fixup.py PreActBlock: relu(bn2(conv2 .)) + shortcut), the ReLU bits
 // of the pre-add value
+// the few-group forward's running-statistics update, done by the apply
+// kernel's first block (the finalize wrote every group's mean / var to gmv):
+// one launch fewer per BN, the channels' group sums in group order (as
+// bn_running_kernel)
+struct BnRun {
+  const float* gmv;
+  float* run_mean;
+  float* run_var;
+  int64_t* nbt;
+  int G;  // 0: no update
+  float momentum;
+};
+
+__device__ __forceinline__ void bn_running_update(const BnRun& r, int C, int M) {
+  if (r.nbt != nullptr && threadIdx.x == 0) *r.nbt += 1;
+  if (r.run_mean == nullptr) return;
+  const float unb = M > 1 ? static_cast<float>(M) / static_cast<float>(M - 1) : 1.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float ms = 0.f, vs = 0.f;
+    for (int g = 0; g < r.G; ++g) {
+      ms += r.gmv[static_cast<size_t>(g) * 2 * C + c];
+      vs += r.gmv[static_cast<size_t>(g) * 2 * C + C + c];
+    }
+    r.run_mean[c] = (1.f - r.momentum) * r.run_mean[c] + r.momentum * (ms / r.G);
+    r.run_var[c] = (1.f - r.momentum) * r.run_var[c] + r.momentum * (vs / r.G) * unb;
+  }
+}
+
+constexpr BnRun kNoRun{nullptr, nullptr, nullptr, nullptr, 0, 0.f};
+
 template <bool BWD, bool POST = false>
 __global__ void __launch_bounds__(256)
 bn_apply_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                 const uint8_t* __restrict__ ybits, const float* __restrict__ coef, int C, int M,
                 uint32_t nchunks, bool relu, uint16_t* __restrict__ out,
-                uint16_t* __restrict__ aux, uint8_t* __restrict__ bits_out) {
+                uint16_t* __restrict__ aux, uint8_t* __restrict__ bits_out, BnRun run) {
+  if (!BWD && run.G > 0 && blockIdx.x == 0) bn_running_update(run, C, M);
   const uint32_t CL = static_cast<uint32_t>(C) >> 3;
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nchunks; i += gridDim.x * 256u) {
     const uint32_t p = i / CL;
@@ -905,7 +936,7 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
                    momentum, run_mean, run_var, nbt);
     COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                    nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
-                   const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr);
+                   const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr, kNoRun);
     return;
   }
   COMMEFF_LAUNCH(bn_partial_kernel<false>, dim3(G * S), dim3(256), 0, stream, x, nullptr, nullptr,
@@ -914,16 +945,19 @@ void launch_bn_fwd(const uint16_t* x, const float* w, const float* b, int G, int
     // per-group mean / var behind the partial sums (bn_scratch_floats)
     float* gmv = part + static_cast<size_t>(G) * S * 2 * C;
     COMMEFF_LAUNCH(bn_fwd_finalize_group_kernel, dim3((C + 63) / 64, G), dim3(64 * kGL), 0, stream,
-                       x, part, w, b, C, M, S, eps, stat, ab, gmv);
-    COMMEFF_LAUNCH(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, gmv, C, M, G,
-                       momentum, run_mean, run_var, nbt);
+                   x, part, w, b, C, M, S, eps, stat, ab, gmv);
+    const BnRun run{gmv, run_mean, run_var, nbt, G, momentum};
+    COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
+                   nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
+                   const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr, run);
+    return;
   } else {
     COMMEFF_LAUNCH(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64 * kGL), 0, stream, x, part,
                        w, b, C, M, S, G, eps, momentum, stat, ab, run_mean, run_var, nbt);
   }
   COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                      nullptr, ab, C, M, static_cast<uint32_t>(nchunks), relu, y,
-                     const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr);
+                     const_cast<uint16_t*>(addend), relu ? relu_bits : nullptr, kNoRun);
 }
 
 void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
@@ -948,7 +982,7 @@ void launch_bn_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu,
   }
   const int64_t nchunks = static_cast<int64_t>(G) * M * (C / 8);
   COMMEFF_LAUNCH(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
-                     coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd, nullptr);
+                     coef, C, M, static_cast<uint32_t>(nchunks), false, dx, dadd, nullptr, kNoRun);
 }
 
 // channel block of the partial kernels: the largest power-of-two multiple of
@@ -992,10 +1026,10 @@ void launch_bn_cs_fwd(const uint16_t* x, const float* prm, int64_t ld, int64_t w
   if (post_add != nullptr)
     COMMEFF_LAUNCH((bn_apply_kernel<false, true>), dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
                    nullptr, ab, C, M, static_cast<uint32_t>(nchunks), true, y, const_cast<uint16_t*>(post_add),
-                   relu_bits);
+                   relu_bits, kNoRun);
   else
     COMMEFF_LAUNCH(bn_apply_kernel<false>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, nullptr,
-                   nullptr, ab, C, M, static_cast<uint32_t>(nchunks), true, y, nullptr, relu_bits);
+                   nullptr, ab, C, M, static_cast<uint32_t>(nchunks), true, y, nullptr, relu_bits, kNoRun);
 }
 
 void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_relu, const float* stat,
@@ -1018,7 +1052,7 @@ void launch_bn_cs_bwd(const uint16_t* x, const uint16_t* dy, const uint8_t* y_re
                  ld, woff, cg, C, M, S, coef, grad, gld, gwoff, gboff, beta, alpha, wsrc, sld);
   const int64_t nchunks = static_cast<int64_t>(M) * (C / 8);
   COMMEFF_LAUNCH(bn_apply_kernel<true>, dim3(apply_grid(nchunks)), dim3(256), 0, stream, x, dy, y_relu,
-                 coef, C, M, static_cast<uint32_t>(nchunks), false, dx, nullptr, nullptr);
+                 coef, C, M, static_cast<uint32_t>(nchunks), false, dx, nullptr, nullptr, kNoRun);
 }
 
 }  // namespace commeff

@@ -222,6 +222,21 @@ class NativeConv2d(nn.Conv2d):
         return self(x), x
 
 
+    def forward_pair(self, other: "NativeConv2d", x):
+        """(self(x), other(x)) for two 1x1 convs of one input (a downsampling
+        bottleneck's conv1 and shortcut conv): on the native path one autograd
+        node whose backward sums the two input gradients inside the dgrad GEMM."""
+        kinds = [conv2d_native_kind(x, m.weight, m.stride, m.padding, m.dilation, m.groups)
+                 if m.bias is None and m.padding_mode == "zeros" else "" for m in (self, other)]
+        if kinds == ["1x1", "1x1"] and tuple(self.stride) == (1, 1) and other.stride[0] == other.stride[1]:
+            ggs = []
+            for m in (self, other):
+                gg = _grouped.active() if m.weight.requires_grad else None
+                ggs.append(gg if gg is not None and gg.view(m.weight) is not None else None)
+            return _nn.conv1x1_pair(x, self.weight, other.weight, other.stride[0], *ggs)
+        return self(x), other(x)
+
+
 class NativeMaxPool2d(nn.MaxPool2d):
     """``nn.MaxPool2d`` whose bf16 channels_last case runs the native
     max-pool (csrc/im2col.hip: window codes + gather backward)."""

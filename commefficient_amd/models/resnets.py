@@ -93,6 +93,11 @@ class Bottleneck(nn.Module):
             # conv1 hands x through to the identity branch: its dgrad GEMM
             # adds the identity gradient (no separate accumulation pass)
             h, idt = self.conv1.forward_with_identity(x)
+        elif (isinstance(self.downsample, nn.Sequential) and len(self.downsample) == 2
+              and isinstance(self.downsample[0], NativeConv2d) and isinstance(self.conv1, NativeConv2d)):
+            # conv1 and the shortcut conv read x: one input-gradient pass
+            h, d = self.conv1.forward_pair(self.downsample[0], x)
+            idt = self.downsample[1](d)
         else:
             h, idt = self.conv1(x), self.downsample(x)
         out = _norm_relu(self.bn1, self.relu, h)

@@ -199,11 +199,16 @@ class prepared_conv_weights:
     server update); the native conv units of this forward pick them up
     instead of preparing their weight one by one."""
 
-    def __init__(self, weights):
+    def __init__(self, weights, plain=None):
         self.weights = [w for w in weights if w.is_cuda and w.dtype == torch.float32
                         and w.dim() == 4 and tuple(w.shape[2:]) == (3, 3)
                         and w.shape[1] % 64 == 0]
         self.keys = []
+        # ``plain`` = (flat fp32 buffer, 1x1 weights that are views into it):
+        # their bf16 GEMM operands come from ONE cast of the span they cover
+        # into a kept bf16 buffer (ResNet-101: 62 per-weight cast launches
+        # per round before)
+        self.plain = plain
 
     def __enter__(self):
         if self.weights and _CONV_BACKEND[0] == "native" and not _STOCK[0]:
@@ -227,12 +232,49 @@ class prepared_conv_weights:
                 key = (w.data_ptr(), w._version)
                 _PREP[key] = (out[2 * i], out[2 * i + 1])
                 self.keys.append(key)
+        if self.plain is not None and _CONV_BACKEND[0] == "native" and not _STOCK[0]:
+            self._cast_plain(*self.plain)
         return self
+
+    def _cast_plain(self, flat, ws):
+        if not (flat.is_cuda and flat.dtype == torch.float32 and flat.dim() == 1 and flat.is_contiguous()):
+            return
+        base, d = flat.data_ptr(), flat.numel()
+        offs = []
+        for w in ws:
+            o = (w.data_ptr() - base) // 4
+            if w.dtype == torch.float32 and w.is_contiguous() and 0 <= o and o + w.numel() <= d:
+                offs.append((w, o))
+        if not offs:
+            return
+        lo = min(o for _, o in offs)
+        hi = max(o + w.numel() for w, o in offs)
+        buf = _PLAIN_BUF.get("buf")
+        if buf is None or buf.numel() != d or buf.device != flat.device:
+            # kept across rounds: one stable address (recorded rounds read it)
+            buf = torch.empty(d, dtype=torch.bfloat16, device=flat.device)
+            _PLAIN_BUF["buf"] = buf
+        _ops().fa_cast_rows(buf, flat, d, 1, lo, hi - lo)
+        for w, o in offs:
+            key = (w.data_ptr(), w._version)
+            _PREP1[key] = buf[o:o + w.numel()].view(w.shape[0], -1)
+            self.keys.append(key)
 
     def __exit__(self, *exc):
         for k in self.keys:
             _PREP.pop(k, None)
+            _PREP1.pop(k, None)
         return False
+
+
+_PREP1: dict = {}  # (weight ptr, version) -> its bf16 [K, C] view (prepared_conv_weights plain)
+_PLAIN_BUF: dict = {}
+
+
+def _prep1(weight: torch.Tensor, k: int, c: int) -> torch.Tensor:
+    """bf16 [k, c] GEMM operand of a 1x1 conv weight: the prepared one, else a cast."""
+    hit = _PREP1.get((weight.data_ptr(), weight._version))
+    return hit if hit is not None else weight.detach().view(k, c).to(torch.bfloat16)
 
 
 def weights_begin_update(w_flat: torch.Tensor):
@@ -788,7 +830,7 @@ def _mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 # Opt-in (COMMEFF_BN_EPI=1): on the ResNet-101 round the epilogue cost
 # (+~20 us per forward GEMM: the 1x1 GEMMs run many waves of short-K tiles)
 # outweighed the statistics pass it removes (profiles/r4_experiments.md).
-_EPI = {"G": 0, "on": os.environ.get("COMMEFF_BN_EPI", "0") == "1", "last": None}
+_EPI = {"G": 0, "on": os.environ.get("COMMEFF_BN_EPI", "0") == "1", "last": None, "pair": None}
 
 
 def _mm_nt_conv(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -957,7 +999,7 @@ class _Conv1x1(torch.autograd.Function):
             h, w = (H - 1) // stride + 1, (W - 1) // stride + 1
         else:
             x2d, h, w = _nhwc2d(x), H, W
-        wb = weight.detach().view(k, c).to(torch.bfloat16)
+        wb = _prep1(weight, k, c)
         y2d = _mm_nt_conv(x2d, wb)
         ctx.save_for_backward(x2d, wb)
         ctx.weight, ctx.stride, ctx.gg = weight, stride, gg
@@ -1002,7 +1044,7 @@ class _Conv1x1Pass(torch.autograd.Function):
     def forward(ctx, x, weight, gg):
         n, c, h, w = x.shape
         k = weight.shape[0]
-        wb = weight.detach().view(k, c).to(torch.bfloat16)
+        wb = _prep1(weight, k, c)
         y2d = _mm_nt_conv(_nhwc2d(x), wb)
         ctx.save_for_backward(x, wb)
         ctx.weight, ctx.gg = weight, gg
@@ -1043,6 +1085,86 @@ class _Conv1x1Pass(torch.autograd.Function):
                 if into is not None:
                     _grad_written(ctx.weight)
         return gx, gw, None
+
+
+def _wgrad_1x1(ctx_weight, gg, g2d, x2d, k, c):
+    """dW of a 1x1 conv into its grouped rows / flat .grad (None) or returned."""
+    if gg is not None:
+        _wgrad_gemm(g2d, x2d, gg.view(ctx_weight).view(gg.G, k, c), gg.G)
+        return None
+    into = _grad_view(ctx_weight, (k, c))
+    gw = _wgrad_gemm(g2d, x2d, into)
+    if into is not None:
+        _grad_written(ctx_weight)
+        return None
+    return gw.view(k, c, 1, 1)
+
+
+class _Conv1x1Pair(torch.autograd.Function):
+    """(conv1x1(x, w1), conv1x1_stride_s(x, w2)): a downsampling bottleneck's
+    conv1 and shortcut conv read the same input; backward writes the
+    shortcut's input gradient (col2im onto the stride grid when s > 1) and the
+    conv1 dgrad GEMM accumulates into it in place -- no autograd accumulation
+    pass over the block input (4 stock bf16 adds per ResNet-101 round, 377 us)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2, stride, gg1, gg2):
+        n, c, H, W = x.shape
+        k1, k2 = w1.shape[0], w2.shape[0]
+        x2d = _nhwc2d(x)
+        w1b, w2b = _prep1(w1, k1, c), _prep1(w2, k2, c)
+        y1 = _mm_nt_conv(x2d, w1b)
+        st1, _EPI["last"] = _EPI["last"], None
+        if stride > 1:
+            xs = _ops().im2col(x, 1, 1, stride, 0, c)
+            h, w = (H - 1) // stride + 1, (W - 1) // stride + 1
+        else:
+            xs, h, w = x2d, H, W
+        y2 = _mm_nt_conv(xs, w2b)
+        # (the outputs' GEMM-epilogue BN moments, attached by conv1x1_pair)
+        _EPI["pair"], _EPI["last"] = (st1, _EPI["last"]), None
+        ctx.save_for_backward(x2d, xs, w1b, w2b)
+        ctx.w, ctx.gg, ctx.stride, ctx.dims = (w1, w2), (gg1, gg2), stride, (n, c, H, W, h, w)
+        return (y1.view(n, H, W, k1).permute(0, 3, 1, 2), y2.view(n, h, w, k2).permute(0, 3, 1, 2))
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        x2d, xs, w1b, w2b = ctx.saved_tensors
+        n, c, H, W, h, w = ctx.dims
+        k1, k2 = w1b.shape[0], w2b.shape[0]
+        s = ctx.stride
+
+        def flat2d(g):
+            return _nhwc2d(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        g1d = flat2d(g1) if g1 is not None else None
+        g2d = flat2d(g2) if g2 is not None else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            acc = None
+            if g2d is not None:
+                gsub = _mm_nn(g2d, w2b)
+                acc = _ops().col2im(gsub, n, H, W, c, 1, 1, s, 0) if s > 1 else gsub
+                acc2d = _nhwc2d(acc) if s > 1 else acc
+            if g1d is not None:
+                acc2d = _mm_nn(g1d, w1b, acc2d, in_place=True) if acc is not None else _mm_nn(g1d, w1b)
+            gx = acc2d.view(n, H, W, c).permute(0, 3, 1, 2)
+        gw1 = gw2 = None
+        if ctx.needs_input_grad[1] and g1d is not None:
+            gw1 = _wgrad_1x1(ctx.w[0], ctx.gg[0], g1d, x2d, k1, c)
+        if ctx.needs_input_grad[2] and g2d is not None:
+            gw2 = _wgrad_1x1(ctx.w[1], ctx.gg[1], g2d, xs, k2, c)
+        return gx, gw1, gw2, None, None, None
+
+
+def conv1x1_pair(x, w1, w2, stride: int, gg1=None, gg2=None):
+    """(conv1x1(x, w1), conv1x1(x, w2, stride)) with one input gradient pass."""
+    _EPI["last"] = _EPI["pair"] = None
+    y1, y2 = _Conv1x1Pair.apply(x, w1, w2, int(stride), gg1, gg2)
+    sts, _EPI["pair"] = _EPI["pair"], None
+    for y, st in zip((y1, y2), sts or (None, None)):
+        _EPI["last"] = st
+        _with_bnstats(y)
+    return y1, y2
 
 
 def conv1x1_passthrough(x, weight, gg=None):

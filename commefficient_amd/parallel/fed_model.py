@@ -566,7 +566,7 @@ class FedModel:
             def body():
                 self.flat.zero_grad()
                 data = rb.device_gather(parts[0].view(2, n_local))
-                with prepared_conv_weights(self._native_3x3_weights()):
+                with self._prepared_weights():
                     pe, ms = self._fwd_bwd(data[:-1], data[-1], None, groups=1,
                                            ex_groups=parts[1] if self._loss_groups else None)
                 tail = payload[self.main_numel:].view(n_res, W)
@@ -743,8 +743,7 @@ class FedModel:
         per_ex_all, metrics_all = [], []
         # the native 3x3 convs' bf16 weight images in ONE launch for the pass
         ovl = self._overlap_reducer(W, counts)
-        with (prepared_conv_weights(self._native_3x3_weights())
-              if self.device.type == "cuda" else nullcontext()):
+        with (self._prepared_weights() if self.device.type == "cuda" else nullcontext()):
             self._merged_microbatches(inputs, targets, n_local, mb, groups_total, counts, my_slots,
                                       slots_t, per_ex_all, metrics_all, ovl)
         self._overlap_round = ovl is not None
@@ -867,7 +866,7 @@ class FedModel:
         shared_w = (a.mode != "fedavg" and "weights" not in self.client_state.kinds
                     and not a.do_test)
         # ... and the native 3x3 convs share one batched bf16 weight preparation
-        prep = (prepared_conv_weights(self._native_3x3_weights())
+        prep = (self._prepared_weights()
                 if shared_w and self.device.type == "cuda" else nullcontext())
         with (self._autocast() if shared_w else nullcontext()), prep:
             if shared_w and self._grouped_ok(counts[my_slots]):
@@ -880,6 +879,19 @@ class FedModel:
             msum = torch.zeros(self._n_metrics_guess(), W, device=self.device)
         self._n_metrics = msum.shape[0]
         return out, msum
+
+    def _prepared_weights(self):
+        """The pass's bf16 conv operands: 3x3 images in one launch, 1x1 weights
+        from one cast of the flat weights (ops/nn.py prepared_conv_weights)."""
+        w1 = getattr(self, "_n1x1", None)
+        if w1 is None:
+            w1 = [m.weight for m in self.model.modules()
+                  if isinstance(m, NativeConv2d) and tuple(m.kernel_size) == (1, 1) and m.groups == 1
+                  and m.bias is None and m.weight.requires_grad]
+            self._n1x1 = w1
+        bound = getattr(self.flat, "bound", None)
+        return prepared_conv_weights(self._native_3x3_weights(),
+                                     plain=(bound, w1) if (w1 and bound is not None) else None)
 
     def _native_3x3_weights(self):
         ws = getattr(self, "_n3x3", None)

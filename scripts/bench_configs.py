@@ -192,6 +192,38 @@ def main():
         if ctx.is_main:
             os.makedirs(tp, exist_ok=True)
             prof.export_chrome_trace(os.path.join(tp, "trace.json"))
+    ss = os.environ.get("COMMEFF_STOCK_SITES")
+    if ss:  # 2 more rounds: call sites of stock (aten) ops that launch kernels
+        import collections
+        import traceback
+        from torch.utils._python_dispatch import TorchDispatchMode
+        quiet = ("empty", "view", "as_strided", "_reshape_alias", "t.default", "transpose", "expand",
+                 "slice", "select", "unsqueeze", "squeeze", "permute", "detach", "alias", "lift_fresh",
+                 "unbind", "split", "narrow", "set_", "is_", "record_stream", "item",
+                 "_local_scalar_dense", "resize_", "numpy_T")
+        sites = collections.Counter()
+
+        class _Sites(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                name = str(func)
+                if not any(q in name for q in quiet):
+                    st = [f for f in traceback.extract_stack()[:-1] if "commefficient_amd" in f.filename
+                          or "bench_configs" in f.filename]
+                    sites[(name, " <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}"
+                                             for f in reversed(st[-6:])))] += 1
+                return func(*args, **(kwargs or {}))
+        a0 = torch.cuda.memory_stats().get("num_device_alloc", 0)
+        with _Sites():
+            for i in range(b.warmup, b.warmup + min(2, b.steps)):
+                fed(batches_at[i])
+                fopt.step()
+            torch.cuda.synchronize()
+        if ctx.is_main:
+            with open(ss, "w") as f:
+                f.write(f"# device allocs in these 2 rounds: "
+                        f"{torch.cuda.memory_stats().get('num_device_alloc', 0) - a0}\n")
+                for (name, st), n in sites.most_common():
+                    f.write(f"{n / 2:6.1f}/round {name} | {st}\n")
     ex = sum(n_ex)
     if ctx.is_main:
         print(json.dumps({"config": b.config, "n_gpus": N, "value": round(ex / el, 1),

@@ -583,6 +583,41 @@ def test_conv1x1_passthrough_sums_identity_grad():
     _close(x.grad, xr.grad)
 
 
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv1x1_pair_sums_both_input_grads(stride):
+    """A downsampling bottleneck's conv1 + strided shortcut conv from one node
+    (ops/nn.py _Conv1x1Pair): outputs, dX (shortcut col2im + conv1 dgrad
+    accumulated in place) and both weight gradients vs the fp32 reference;
+    the bf16 operands of prepared_conv_weights(plain=...) give the same."""
+    from commefficient_amd.models.common import NativeConv2d
+    from commefficient_amd.ops.nn import prepared_conv_weights
+    torch.manual_seed(0)
+    c1 = NativeConv2d(256, 64, 1, bias=False).cuda()
+    c2 = NativeConv2d(256, 512, 1, stride=stride, bias=False).cuda()
+    x = _nhwc(torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    flat = torch.cat([c1.weight.detach().reshape(-1), torch.randn(7, device="cuda"),
+                      c2.weight.detach().reshape(-1)])
+    c1.weight.data = flat[:c1.weight.numel()].view_as(c1.weight)
+    c2.weight.data = flat[-c2.weight.numel():].view_as(c2.weight)
+    with prepared_conv_weights([], plain=(flat, [c1.weight, c2.weight])):
+        y1, y2 = c1.forward_pair(c2, x)
+    assert y2.shape == (4, 512, (14 - 1) // stride + 1, (14 - 1) // stride + 1)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    g1 = torch.randn(y1.shape, device="cuda", generator=g)
+    g2 = torch.randn(y2.shape, device="cuda", generator=g)
+    ((y1.float() * g1).sum() + (y2.float() * g2).sum()).backward()
+    xr = x.detach().float().requires_grad_(True)
+    w1r = c1.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    w2r = c2.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    y1r, y2r = F.conv2d(xr, w1r), F.conv2d(xr, w2r, stride=stride)
+    ((y1r * g1.to(torch.bfloat16).float()).sum() + (y2r * g2.to(torch.bfloat16).float()).sum()).backward()
+    _close(y1, y1r)
+    _close(y2, y2r)
+    _close(x.grad, xr.grad)
+    _close(c1.weight.grad, w1r.grad)
+    _close(c2.weight.grad, w2r.grad)
+
+
 @pytest.mark.parametrize("chain", ["pool_res", "pool_pool", "two_consumers", "pool_res_pool"])
 def test_fused_unpool_backward_bitwise(chain):
     """The relu + 2x2 max-pool backward fused into the consumer's dgrad
