@@ -44,7 +44,11 @@ def main():
     rows = []
     with open(a.trace) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            grid = r.get("Grid_Size_X") or r.get("Grid_Size") or ""
+            wg = r.get("Workgroup_Size_X") or r.get("Workgroup_Size") or ""
+            # (the grid in workgroups: rocprofv3 reports work-items)
+            nwg = str(int(grid) // max(1, int(wg))) if grid.isdigit() and wg.isdigit() else ""
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], nwg))
     rows.sort()
     if a.tail_ms > 0:
         t_end = max(r[1] for r in rows)
@@ -65,7 +69,7 @@ def main():
     calls = collections.Counter()
     idle = 0
     end = sel[0][0]
-    for s, e, k in sel:
+    for s, e, k, _ in sel:
         if s > end:
             idle += s - end
         end = max(end, e)
@@ -75,7 +79,7 @@ def main():
     if a.gaps:
         gap = collections.Counter()
         prev, end = None, sel[0][0]
-        for s, e, k in sel:
+        for s, e, k, _ in sel:
             if prev is not None and s > end:
                 gap[(short(prev)[:40], short(k)[:40])] += s - end
             if e >= end:
@@ -95,11 +99,11 @@ def sequence(rows, starts):
     n = min(len(sp) for sp in spans)
     spans = [sp for sp in spans if len(sp) == n]
     print(f"# launch order of one round ({len(spans)} rounds of {n} kernels averaged): "
-          "start offset us, duration us, kernel")
+          "start offset us, duration us, workgroups, kernel")
     for j in range(n):
         d = sum(sp[j][1] - sp[j][0] for sp in spans) / len(spans) / 1e3
         t = sum(sp[j][0] - sp[0][0] for sp in spans) / len(spans) / 1e3
-        print(f"{t:9.1f} {d:8.1f}  {short(spans[0][j][2])}")
+        print(f"{t:9.1f} {d:8.1f} {spans[0][j][3]:>6}  {short(spans[0][j][2])}")
 
 
 def per_round(rows, starts, top):
@@ -108,7 +112,7 @@ def per_round(rows, starts, top):
     spans = [rows[starts[i]:starts[i + 1]] for i in range(len(starts) - 1)]
     tot = collections.Counter()
     for sp in spans:
-        for s, e, k in sp:
+        for s, e, k, _ in sp:
             tot[short(k)] += e - s
     names = [k for k, _ in tot.most_common(top)]
     print("# round  wall_us  busy_us  idle_us  " + "  ".join(n[:28] for n in names))
@@ -116,7 +120,7 @@ def per_round(rows, starts, top):
         wall = sp[-1][1] - sp[0][0]
         busy = collections.Counter()
         idle, end = 0, sp[0][0]
-        for s, e, k in sp:
+        for s, e, k, _ in sp:
             if s > end:
                 idle += s - end
             end = max(end, e)
