@@ -1665,37 +1665,40 @@ void client_means_hip(at::Tensor out, at::TensorList rows, const at::Tensor& slo
                       cur_stream());
 }
 
-// fused per-example cross-entropy: (loss f32 [B], correct f32 [B], softmax - onehot [B, C])
+// fused per-example cross-entropy: (loss f32 [B], correct f32 [B], softmax - onehot [B, C]);
+// logits may be rows of a wider buffer (unit column stride, row stride >= C: the
+// tied LM head's padded logits), the gradient then has the same row stride
 std::tuple<at::Tensor, at::Tensor, at::Tensor> ce_fwd_hip(const at::Tensor& logits,
                                                           const at::Tensor& targets) {
-  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous() &&
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) >= logits.size(1) &&
                   (logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat),
-              "ce_fwd: logits must be contiguous bf16/f32 [B, C]");
+              "ce_fwd: logits must be bf16/f32 [B, C] rows with unit column stride");
   TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous() &&
                   targets.numel() == logits.size(0),
               "ce_fwd: targets must be contiguous int64 [B]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
-  const int64_t B = logits.size(0);
+  const int64_t B = logits.size(0), C = logits.size(1), ld = B > 1 ? logits.stride(0) : C;
   auto loss = at::empty({B}, logits.options().dtype(at::kFloat));
   auto correct = at::empty({B}, logits.options().dtype(at::kFloat));
-  auto grad = at::empty_like(logits);
+  auto grad = at::empty({B, ld}, logits.options()).narrow(1, 0, C);
   launch_ce_fwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16,
-                targets.data_ptr<int64_t>(), B, static_cast<int>(logits.size(1)),
+                targets.data_ptr<int64_t>(), B, static_cast<int>(C), ld,
                 loss.data_ptr<float>(), correct.data_ptr<float>(), grad.data_ptr(), cur_stream());
   return {loss, correct, grad};
 }
 
-// g [B, C] (bf16 / f32, contiguous) *= s [B] row by row, in place
+// g [B, C] (bf16 / f32, unit column stride) *= s [B] row by row, in place
 void scale_rows_hip(at::Tensor g, const at::Tensor& s) {
-  TORCH_CHECK(g.dim() == 2 && g.is_contiguous() &&
+  TORCH_CHECK(g.dim() == 2 && g.stride(1) == 1 && g.stride(0) >= g.size(1) &&
                   (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat),
-              "scale_rows: g must be contiguous bf16/f32 [B, C]");
+              "scale_rows: g must be bf16/f32 [B, C] rows with unit column stride");
   TORCH_CHECK(s.scalar_type() == at::kFloat && s.is_contiguous() && s.numel() == g.size(0) &&
                   s.device() == g.device(),
               "scale_rows: s must be contiguous f32 [B]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  const int64_t ld = g.size(0) > 1 ? g.stride(0) : g.size(1);
   launch_scale_rows(g.data_ptr(), g.scalar_type() == at::kBFloat16, s.data_ptr<float>(), g.size(0),
-                    static_cast<int>(g.size(1)), cur_stream());
+                    static_cast<int>(g.size(1)), ld, cur_stream());
 }
 
 // residual unit tail: out = relu(conv3x3(x, w)) + addend, and pre = relu(conv3x3(x, w))

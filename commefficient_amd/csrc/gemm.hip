@@ -79,7 +79,9 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 1, wc = wid & 1, hi = lane >> 5, lr = lane & 31;
   int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntn = a0.N / BN;
+  // (NT: N need not be a tile multiple -- B rows past N load the zero page,
+  // column chunks past N are not stored; the tied LM head's 50,257 rows)
+  const int ntn = (a0.N + BN - 1) / BN;
   GemmArgs a = a0;
   if (a0.G > 1) {  // group of this block (its tiles are consecutive)
     const int per_g = ((a0.M + Cfg::BM - 1) / Cfg::BM) * ntn;
@@ -121,7 +123,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
       b_ptr[j] = a.B + static_cast<int64_t>(row) * a.ldb + n0 + lc * 8;
     } else {
       const int row = s >> 3, lc = (s & 7) ^ sw_rd128(row);
-      b_ptr[j] = a.B + static_cast<int64_t>(n0 + row) * a.ldb + lc * 8;
+      b_ptr[j] = n0 + row < a.N ? a.B + static_cast<int64_t>(n0 + row) * a.ldb + lc * 8 : nullptr;
     }
   }
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
@@ -141,7 +143,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
     }
 #pragma unroll
     for (int j = 0; j < BLD; ++j) {
-      const uint16_t* src = NN ? b_ptr[j] + static_cast<int64_t>(kt) * GK * a.ldb : b_ptr[j] + kt * GK;
+      const uint16_t* src = NN ? b_ptr[j] + static_cast<int64_t>(kt) * GK * a.ldb
+                               : (b_ptr[j] != nullptr ? b_ptr[j] + kt * GK : zero);
       mm_glds16(src, base + Cfg::A_BYTES + j * 4096);
     }
   };
@@ -252,8 +255,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a0) {
   }
   for (int e = tid; e < Cfg::BM * CPR; e += 256) {
     const int row = e / CPR, cc = e - row * CPR, m = m0 + row;
-    if (m >= a.M) continue;
     const int n = n0 + cc * 8;
+    if (m >= a.M || n >= a.N) continue;  // (a chunk straddling N fills C's row padding)
     const float4 lo = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8);
     const float4 up = *reinterpret_cast<const float4*>(ct + row * LD + cc * 8 + 4);
     float v[8] = {lo.x, lo.y, lo.z, lo.w, up.x, up.y, up.z, up.w};
@@ -343,7 +346,7 @@ void launch_gemm_t(const GemmArgs& a, hipStream_t stream) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     init = true;
   }
-  const int tiles = ((a.M + 127) / 128) * (a.N / BN) * (a.G > 1 ? a.G : 1);
+  const int tiles = ((a.M + 127) / 128) * ((a.N + BN - 1) / BN) * (a.G > 1 ? a.G : 1);
   COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32, ST, IMP>), dim3(tiles), dim3(256), lds, stream, a);
 }
 
@@ -354,14 +357,18 @@ bool gemm_supported(int M, int N, int K, bool nn) {
   return M >= 1 && N >= 64 && N % 64 == 0 && K >= 64 && K % 64 == 0;
 }
 
+// NT with any N >= 64 (C's rows padded to a multiple of 8 columns; no bias /
+// activation / statistics on this path)
+bool gemm_supported_nedge(int M, int N, int K) { return M >= 1 && N >= 64 && K >= 64 && K % 64 == 0; }
+
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream) {
   if (a.M <= 0) return;
   // (256-row tiles with a 4-stage ring, one block per CU, measured equal or
   // slower on the GPT-2 and ResNet-101 shapes: these GEMMs are one wave of
   // tiles whose load / store phases set the time; profiles/r4_experiments.md)
   // 128-wide column tiles when they still give ~every resident slot (2 per CU) a block
-  const bool wide = a.N % 128 == 0 &&
-                    static_cast<int64_t>((a.M + 127) / 128) * (a.N / 128) * (a.G > 1 ? a.G : 1) >= 384;
+  const bool wide = (a.N % 128 == 0 || (!nn && a.N % 64 != 0)) &&
+                    static_cast<int64_t>((a.M + 127) / 128) * ((a.N + 127) / 128) * (a.G > 1 ? a.G : 1) >= 384;
   if (a.imp_C > 0) {  // implicit column image A (NT, bf16 out, no activation)
     if (a.stats != nullptr) {  // + BN moments (conv_nt_imp)
       if (wide) launch_gemm_t<128, false, 0, false, true, true>(a, stream);

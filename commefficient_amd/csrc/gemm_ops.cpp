@@ -49,8 +49,14 @@ at::Tensor mm_impl(const at::Tensor& a, const at::Tensor& b, bool nn, const c10:
     C.copy_(r);
     return C;
   }
-  TORCH_CHECK(gemm_supported(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), nn),
-              "mm: native GEMM needs N % 64 == 0 and K % 64 == 0");
+  // NT with N not a multiple of 64 (the tied LM head): C's rows must hold the
+  // 8-column chunk past N (a padded buffer), no bias / activation / beta
+  const bool nedge = !nn && N % 64 != 0 && act == 0 && !(bias.has_value() && bias->defined()) && beta == 0.0 &&
+                     C.stride(0) >= (N + 7) / 8 * 8 &&
+                     gemm_supported_nedge(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K));
+  TORCH_CHECK(nedge || gemm_supported(static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), nn),
+              "mm: native GEMM needs N % 64 == 0 (NT: or an output whose rows hold the chunk past N) and "
+              "K % 64 == 0");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0 &&
                   a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(C.data_ptr()) % 16 == 0 && C.stride(0) % 8 == 0 &&

@@ -447,8 +447,8 @@ struct ClientMeanRows {
 };
 void launch_client_means(const ClientMeanRows& rows, const int64_t* slot, int n, const void* counts,
                          bool counts_f32, int W, float* out, hipStream_t stream);
-void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, hipStream_t stream);
-void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
+void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, int64_t ldg, hipStream_t stream);
+void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, int64_t ldx, float* loss,
                    float* correct, void* grad, hipStream_t stream);
 
 // ----------------------------------------------------------------- pool --
@@ -594,6 +594,7 @@ struct GemmArgs {
   int imp_C = 0, imp_H = 0, imp_W = 0, imp_OH = 0, imp_OW = 0, imp_R = 3, imp_s = 1, imp_pad = 1;
 };
 bool gemm_supported(int M, int N, int K, bool nn);
+bool gemm_supported_nedge(int M, int N, int K);
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);
 struct GemmTnArgs {
   const uint16_t* A;

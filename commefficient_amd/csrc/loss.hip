@@ -45,20 +45,20 @@ __device__ __forceinline__ float wave_sum(float v) {
 template <typename T>
 __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ x,
                                                      const int64_t* __restrict__ tgt, int64_t B,
-                                                     int C, float* __restrict__ loss,
+                                                     int C, int64_t ldx, float* __restrict__ loss,
                                                      float* __restrict__ correct,
                                                      T* __restrict__ grad) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
-  const T* xr = x + row * C;
+  const T* xr = x + row * ldx;
   const int64_t t = tgt[row];
   if (t < 0 || t >= C) {  // ignored row (label -100): zero loss and gradient
     if (lane == 0) {
       loss[row] = 0.f;
       correct[row] = 0.f;
     }
-    for (int j = lane; j < C; j += 64) st<T>(grad, row * C + j, 0.f);
+    for (int j = lane; j < C; j += 64) st<T>(grad, row * ldx + j, 0.f);
     return;
   }
   // max and its first index
@@ -85,7 +85,122 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ x,
   const float inv = 1.f / s;
   for (int j = lane; j < C; j += 64) {
     const float p = __expf(ld<T>(xr, j) - m) * inv;
-    st<T>(grad, row * C + j, p - (j == t ? 1.f : 0.f));
+    st<T>(grad, row * ldx + j, p - (j == t ? 1.f : 0.f));
+  }
+}
+
+typedef uint32_t cev4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t ce_pack2(float lo, float hi) {
+  const __bf16 a = static_cast<__bf16>(lo), b = static_cast<__bf16>(hi);
+  return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, a)) |
+         (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, b)) << 16);
+}
+
+// (max, first argmax) of a 512-lane block: waves by shuffles, then the 8 wave
+// results in order through LDS (ties to the lower index, as torch.argmax)
+__device__ __forceinline__ void block_max_arg(float& m, int& mi, float* sm, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const int oi = __shfl_xor(mi, o, 64);
+    if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = m; si[w] = mi; }
+  __syncthreads();
+  m = sm[0];
+  mi = si[0];
+  for (int q = 1; q < 8; ++q)
+    if (sm[q] > m || (sm[q] == m && si[q] < mi)) { m = sm[q]; mi = si[q]; }
+}
+
+// Large vocabularies in a padded bf16 buffer (the tied GPT-2 LM head's logits,
+// C = 50,257 in rows of a multiple of 8, 16-byte aligned): one 512-lane block
+// per row holds the row in registers (NV 16-byte chunks a lane) -- ONE read of
+// the logits and one write of the gradient (the pad columns get 0), against
+// the two-pass scalar kernel below (145 us per GPT-2 round at 640 rows).
+template <int NV>
+__global__ void __launch_bounds__(512) ce_fwd_rowv_kernel(const uint16_t* __restrict__ x,
+                                                          const int64_t* __restrict__ tgt, int C, int64_t ldx,
+                                                          float* __restrict__ loss, float* __restrict__ correct,
+                                                          uint16_t* __restrict__ grad) {
+  __shared__ float sm[8], ss[8];
+  __shared__ int si[8];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const cev4* xr = reinterpret_cast<const cev4*>(x + row * ldx);
+  cev4* gr = reinterpret_cast<cev4*>(grad + row * ldx);
+  const int nvec = (C + 7) >> 3;
+  const int64_t t = tgt[row];
+  if (t < 0 || t >= C) {  // ignored row (label -100): zero loss and gradient
+    if (tid == 0) {
+      loss[row] = 0.f;
+      correct[row] = 0.f;
+    }
+    for (int i = tid; i < nvec; i += 512) gr[i] = cev4{0u, 0u, 0u, 0u};
+    return;
+  }
+  cev4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int idx = tid + i * 512;
+    v[i] = idx < nvec ? xr[idx] : cev4{0u, 0u, 0u, 0u};
+  }
+  float m = -__builtin_huge_valf();
+  int mi = C;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c0 = (tid + i * 512) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t wv = v[i][j >> 1];
+      const float f = __uint_as_float((j & 1) ? (wv & 0xffff0000u) : (wv << 16));
+      if (c0 + j < C && f > m) { m = f; mi = c0 + j; }
+    }
+  }
+  block_max_arg(m, mi, sm, si);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c0 = (tid + i * 512) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t wv = v[i][j >> 1];
+      const float f = __uint_as_float((j & 1) ? (wv & 0xffff0000u) : (wv << 16));
+      if (c0 + j < C) s += __expf(f - m);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((tid & 63) == 0) ss[tid >> 6] = s;
+  __syncthreads();
+  s = 0.f;
+  for (int q = 0; q < 8; ++q) s += ss[q];
+  if (tid == (t >> 3) % 512) {  // the lane holding the target
+    const int i = static_cast<int>((t >> 3) / 512), j = static_cast<int>(t & 7);
+    uint32_t wv = 0u;
+#pragma unroll
+    for (int q = 0; q < NV; ++q)
+      if (q == i) wv = v[q][j >> 1];
+    const float xt = __uint_as_float((j & 1) ? (wv & 0xffff0000u) : (wv << 16));
+    loss[row] = m + __logf(s) - xt;
+    correct[row] = mi == t ? 1.f : 0.f;
+  }
+  const float inv = 1.f / s;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int idx = tid + i * 512;
+    if (idx >= nvec) continue;
+    const int c0 = idx * 8;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t wv = v[i][j >> 1];
+      const float f = __uint_as_float((j & 1) ? (wv & 0xffff0000u) : (wv << 16));
+      o[j] = c0 + j < C ? __expf(f - m) * inv - (c0 + j == t ? 1.f : 0.f) : 0.f;
+    }
+    gr[idx] = cev4{ce_pack2(o[0], o[1]), ce_pack2(o[2], o[3]), ce_pack2(o[4], o[5]), ce_pack2(o[6], o[7])};
   }
 }
 
@@ -96,15 +211,15 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const T* __restrict__ x,
 template <typename T>
 __global__ void __launch_bounds__(256) ce_fwd_row_kernel(const T* __restrict__ x,
                                                          const int64_t* __restrict__ tgt, int C,
-                                                         float* __restrict__ loss,
+                                                         int64_t ldx, float* __restrict__ loss,
                                                          float* __restrict__ correct,
                                                          T* __restrict__ grad) {
   __shared__ float sm[256], ss[256];
   __shared__ int si[256];
   const int64_t row = blockIdx.x;
   const int tid = threadIdx.x;
-  const T* xr = x + row * C;
-  T* gr = grad + row * C;
+  const T* xr = x + row * ldx;
+  T* gr = grad + row * ldx;
   const int64_t t = tgt[row];
   if (t < 0 || t >= C) {  // ignored row (label -100): zero loss and gradient
     if (tid == 0) {
@@ -156,63 +271,92 @@ __global__ void __launch_bounds__(256) ce_fwd_row_kernel(const T* __restrict__ x
 // wave per row
 template <typename T>
 __global__ void __launch_bounds__(256) scale_rows_kernel(T* __restrict__ g, const float* __restrict__ s,
-                                                         int64_t B, int C) {
+                                                         int64_t B, int C, int64_t ldg) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
   const float f = s[row];
-  T* gr = g + row * C;
+  T* gr = g + row * ldg;
   for (int j = lane; j < C; j += 64) st<T>(gr, j, ld<T>(gr, j) * f);
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) scale_row_block_kernel(T* __restrict__ g, const float* __restrict__ s, int C) {
+__global__ void __launch_bounds__(256) scale_row_block_kernel(T* __restrict__ g, const float* __restrict__ s, int C,
+                                                              int64_t ldg) {
   const int64_t row = blockIdx.x;
   const float f = s[row];
-  T* gr = g + row * C;
+  T* gr = g + row * ldg;
   for (int j = threadIdx.x; j < C; j += 256) st<T>(gr, j, ld<T>(gr, j) * f);
+}
+
+// bf16 rows of a padded buffer (row stride % 8 == 0, 16-byte aligned): 16-byte
+// chunks, the pad columns past C (zero) scaled too
+__global__ void __launch_bounds__(256) scale_row_vec_kernel(uint16_t* __restrict__ g, const float* __restrict__ s,
+                                                            int C, int64_t ldg) {
+  const int64_t row = blockIdx.x;
+  const float f = s[row];
+  cev4* gr = reinterpret_cast<cev4*>(g + row * ldg);
+  const int nvec = (C + 7) >> 3;
+  for (int i = threadIdx.x; i < nvec; i += 256) {
+    const cev4 v = gr[i];
+    cev4 o;
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      o[h] = ce_pack2(__uint_as_float(v[h] << 16) * f, __uint_as_float(v[h] & 0xffff0000u) * f);
+    gr[i] = o;
+  }
 }
 
 }  // namespace
 
-void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, hipStream_t stream) {
+void launch_scale_rows(void* g, bool bf16, const float* s, int64_t B, int C, int64_t ldg, hipStream_t stream) {
   if (B == 0) return;
   if (C > 4096) {  // a block per (long) row
-    if (bf16)
+    if (bf16 && ldg % 8 == 0 && reinterpret_cast<uintptr_t>(g) % 16 == 0)
+      COMMEFF_LAUNCH(scale_row_vec_kernel, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
+                     static_cast<uint16_t*>(g), s, C, ldg);
+    else if (bf16)
       COMMEFF_LAUNCH(scale_row_block_kernel<uint16_t>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
-                     static_cast<uint16_t*>(g), s, C);
+                     static_cast<uint16_t*>(g), s, C, ldg);
     else
       COMMEFF_LAUNCH(scale_row_block_kernel<float>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
-                     static_cast<float*>(g), s, C);
+                     static_cast<float*>(g), s, C, ldg);
     return;
   }
   const dim3 grid(static_cast<uint32_t>((B + 3) / 4));
   if (bf16)
-    COMMEFF_LAUNCH(scale_rows_kernel<uint16_t>, grid, dim3(256), 0, stream, static_cast<uint16_t*>(g), s, B, C);
+    COMMEFF_LAUNCH(scale_rows_kernel<uint16_t>, grid, dim3(256), 0, stream, static_cast<uint16_t*>(g), s, B, C, ldg);
   else
-    COMMEFF_LAUNCH(scale_rows_kernel<float>, grid, dim3(256), 0, stream, static_cast<float*>(g), s, B, C);
+    COMMEFF_LAUNCH(scale_rows_kernel<float>, grid, dim3(256), 0, stream, static_cast<float*>(g), s, B, C, ldg);
 }
 
-void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, float* loss,
+void launch_ce_fwd(const void* x, bool bf16, const int64_t* tgt, int64_t B, int C, int64_t ldx, float* loss,
                    float* correct, void* grad, hipStream_t stream) {
   if (B == 0) return;
   if (C > 4096) {
+    constexpr int kNV = 13;  // 512 lanes x 13 chunks x 8 = 53,248 columns
+    if (bf16 && ldx % 8 == 0 && (C + 7) / 8 <= 512 * kNV && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+        reinterpret_cast<uintptr_t>(grad) % 16 == 0) {
+      COMMEFF_LAUNCH(ce_fwd_rowv_kernel<kNV>, dim3(static_cast<uint32_t>(B)), dim3(512), 0, stream,
+                     static_cast<const uint16_t*>(x), tgt, C, ldx, loss, correct, static_cast<uint16_t*>(grad));
+      return;
+    }
     if (bf16)
       COMMEFF_LAUNCH(ce_fwd_row_kernel<uint16_t>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
-                     static_cast<const uint16_t*>(x), tgt, C, loss, correct, static_cast<uint16_t*>(grad));
+                     static_cast<const uint16_t*>(x), tgt, C, ldx, loss, correct, static_cast<uint16_t*>(grad));
     else
       COMMEFF_LAUNCH(ce_fwd_row_kernel<float>, dim3(static_cast<uint32_t>(B)), dim3(256), 0, stream,
-                     static_cast<const float*>(x), tgt, C, loss, correct, static_cast<float*>(grad));
+                     static_cast<const float*>(x), tgt, C, ldx, loss, correct, static_cast<float*>(grad));
     return;
   }
   const dim3 grid(static_cast<uint32_t>((B + 3) / 4));
   if (bf16)
     COMMEFF_LAUNCH(ce_fwd_kernel<uint16_t>, grid, dim3(256), 0, stream,
-                       static_cast<const uint16_t*>(x), tgt, B, C, loss, correct,
+                       static_cast<const uint16_t*>(x), tgt, B, C, ldx, loss, correct,
                        static_cast<uint16_t*>(grad));
   else
     COMMEFF_LAUNCH(ce_fwd_kernel<float>, grid, dim3(256), 0, stream,
-                       static_cast<const float*>(x), tgt, B, C, loss, correct,
+                       static_cast<const float*>(x), tgt, B, C, ldx, loss, correct,
                        static_cast<float*>(grad));
 }
 

@@ -749,7 +749,10 @@ class _FusedCE(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, logits, targets):
-        loss, correct, gunit = _ops().ce_fwd(logits.contiguous(), targets.contiguous())
+        # (rows of a padded buffer -- the native LM head's logits -- are read
+        # in place; the unit gradient comes back in the same row layout)
+        x = logits if logits.stride(-1) == 1 else logits.contiguous()
+        loss, correct, gunit = _ops().ce_fwd(x, targets.contiguous())
         ctx.save_for_backward(gunit)
         ctx.mark_non_differentiable(correct)
         return loss, correct

@@ -245,13 +245,13 @@ def _gemm_tn_ok(sink: torch.Tensor, at: torch.Tensor, b: torch.Tensor) -> bool:
             and at.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and sink.data_ptr() % 16 == 0)
 
 
-def _acc_mm(sink: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
+def _acc_mm(sink: torch.Tensor, a: torch.Tensor, b: torch.Tensor, blas: bool = False) -> None:
     """sink (fp32) += a @ b (bf16 operands, fp32 accumulation and output).
     The weight gradients (a = X^T, a view of the token rows) run on the
-    native split-K TN GEMM (csrc/gemm_tn.hip) when the shapes fit, else on
-    hipBLASLt (COMMEFF_GEMM=blas: always)."""
+    native split-K TN GEMM (csrc/gemm_tn.hip) when the shapes fit, else (or
+    ``blas``) on hipBLASLt (COMMEFF_GEMM=blas: always)."""
     if sink.is_cuda:
-        if _gemm_tn_ok(sink, a.t(), b):
+        if not blas and _gemm_tn_ok(sink, a.t(), b):
             _ops().gemm_tn_acc(sink, a.t(), b)
             return
         torch.addmm(sink, a, b, out_dtype=torch.float32, out=sink)
@@ -316,7 +316,7 @@ def _side_colsum(part: torch.Tensor, q: int, sinks) -> None:
     _SIDE["pending"] = True
 
 
-def _wgrad(sink, a, b):
+def _wgrad(sink, a, b, blas: bool = False):
     if sink is None:
         return torch.mm(a, b)
     if sink.is_cuda and _SIDE["enabled"]:
@@ -324,14 +324,14 @@ def _wgrad(sink, a, b):
         side = _side_stream(sink.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            _acc_mm(sink, a, b)
+            _acc_mm(sink, a, b, blas)
         # the operands were allocated on the main stream: keep their memory
         # until the side stream has consumed them
         a.record_stream(side)
         b.record_stream(side)
         _SIDE["pending"] = True
         return None
-    _acc_mm(sink, a, b)
+    _acc_mm(sink, a, b, blas)
     return None
 
 
@@ -505,68 +505,62 @@ class _Linear(torch.autograd.Function):
 
 class _LMHead(torch.autograd.Function):
     """logits = h W^T of the tied LM head, W [V, H] bf16 (V = 50,257: no tile
-    multiple).  Native NT GEMM against a zero-padded copy of W [ceil128(V), H]
-    (one copy per call), the logits a [T, V] view of the padded product;
-    backward: dh on the native NN GEMM over the zero-padded gradient, dW
-    accumulated into the weight's fp32 gradient sink by the split-K TN GEMM on
-    the weight-gradient side stream (replaces three hipBLASLt GEMMs; reference
-    model: gpt2_train.py:262-273, HF GPT2DoubleHeadsModel.lm_head)."""
+    multiple).  Forward: the native NT GEMM with in-kernel N-edge masking (W's
+    rows past V load the zero page, chunks past V are not stored) into a bf16
+    buffer whose rows are padded to a multiple of 8 columns; the logits are a
+    [T, V] view of it, which the native cross-entropy reads and whose gradient
+    it writes in the same padded layout (pad columns 0).  Backward: dW from
+    that gradient straight into the tied weight's fp32 sink on the
+    weight-gradient side stream (hipBLASLt fp32-output GEMM; COMMEFF_LM_DW=tn:
+    the native TN GEMM with its M = V edge tile), dh = g W (K = 50,257, only
+    T x H outputs) on hipBLASLt.  No padded copies of W or of the gradient,
+    no bf16 dW + accumulation pass (HF's lm_head on hipBLASLt; reference
+    model: gpt2_train.py:262-273)."""
 
     @staticmethod
     def forward(ctx, h, W):
-        V, H = W.shape
-        Vp = -(-V // 128) * 128
-        Wp = torch.empty(Vp, H, dtype=W.dtype, device=W.device)
-        Wp[:V].copy_(W)
-        Wp[V:].zero_()
-        ctx.save_for_backward(h, Wp, W)
+        V = W.shape[0]
+        buf = torch.empty(h.shape[0], -(-V // 8) * 8, dtype=torch.bfloat16, device=h.device)
+        out = buf[:, :V]
+        _ops().mm_nt(h, W, None, out)
+        ctx.save_for_backward(h, W)
         ctx.sink = _sink(W)
-        return _ops().mm_nt(h, Wp)[:, :V]
+        return out
 
     @staticmethod
     def backward(ctx, g):
-        h, Wp, W = ctx.saved_tensors
-        V = W.shape[0]
-        T = g.shape[0]
-        g16 = torch.empty(T, Wp.shape[0], dtype=torch.bfloat16, device=g.device)
-        g16[:, :V].copy_(g)
-        g16[:, V:].zero_()
-        dh = None
-        if ctx.needs_input_grad[0]:
-            # dh = g Wp reduces over the 50k vocabulary rows with only T x H
-            # outputs (~60 tiles): the split-K TN GEMM over the transposed
-            # gradient [Vp, T] keeps every CU busy (the NN GEMM took 0.7 ms)
-            Tp = -(-T // 8) * 8
-            gt = torch.empty(Wp.shape[0], Tp, dtype=torch.bfloat16, device=g.device)
-            gt[:, :T].copy_(g16.t())
-            dh32 = torch.zeros(T, h.shape[1], dtype=torch.float32, device=g.device)
-            _ops().gemm_tn_acc(dh32, gt[:, :T], Wp)
-            dh = dh32.to(torch.bfloat16)
+        h, W = ctx.saved_tensors
+        g = g.to(torch.bfloat16)
+        if g.stride(1) != 1:
+            g = g.contiguous()
+        dh = torch.mm(g, W) if ctx.needs_input_grad[0] else None
         dW = None
         if ctx.needs_input_grad[1]:
             if ctx.sink is not None:
-                _wgrad(ctx.sink, g16[:, :V].t(), h)
+                # (hipBLASLt's fp32-output GEMM into the sink: 120 vs 150 us for
+                # the TN GEMM's 2,358 short-K (T = 640) tiles, scripts/dev/bench_lm_bwd.py)
+                _wgrad(ctx.sink, g.t(), h, blas=not _LM_DW_TN)
             else:
-                dW = torch.mm(g16[:, :V].t(), h, out_dtype=torch.float32).to(W.dtype)
+                dW = torch.mm(g.t(), h, out_dtype=torch.float32).to(W.dtype)
         return dh, dW
 
 
-# The native LM head is opt-in (COMMEFF_LM_HEAD=native): isolated, its forward
-# + backward took 699 vs 377 us for hipBLASLt at 560 tokens
-# (scripts/bench_lmhead.py; the padded weight copy, the transposed gradient and
-# the fp32 read-modify-write of the 50,257 x 768 gradient sink), with the
-# GPT-2 round's wall time unchanged (host-bound).
-_LM_NATIVE = os.environ.get("COMMEFF_LM_HEAD", "blas") == "native"
+# The native LM head (default; COMMEFF_LM_HEAD=blas: HF's lm_head module on
+# hipBLASLt).  Round 5's version copied W and the gradient into tile-padded
+# buffers every call and was slower than hipBLASLt (699 vs 377 us isolated).
+_LM_NATIVE = os.environ.get("COMMEFF_LM_HEAD", "native") == "native"
+_LM_DW_TN = os.environ.get("COMMEFF_LM_DW", "blas") == "tn"
 
 
 def lm_head(m, h: torch.Tensor) -> torch.Tensor:
     """The (tied) LM head of an HF double-heads model on h [..., H]: native
-    (``_LMHead``, opt-in) for bf16 CUDA operands, else the module itself."""
+    (``_LMHead``) for bf16 CUDA operands, else the module itself."""
     W = m.lm_head.weight
     H = h.shape[-1]
     h2 = h.reshape(-1, H)
     if (_LM_NATIVE and _GEMM["native"] and h.is_cuda and h.dtype == torch.bfloat16 and W.dtype == torch.bfloat16
-            and getattr(m.lm_head, "bias", None) is None and H % 64 == 0
+            and getattr(m.lm_head, "bias", None) is None and H % 64 == 0 and W.shape[0] >= 64
+            and W.is_contiguous() and W.data_ptr() % 16 == 0
             and h2.is_contiguous() and h2.data_ptr() % 16 == 0):
         return _LMHead.apply(h2, W).view(h.shape[:-1] + (W.shape[0],))
     return m.lm_head(h)

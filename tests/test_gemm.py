@@ -39,6 +39,22 @@ def _mk(M, N, K, dev, seed=0):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(640, 50257, 768), (300, 100, 128), (129, 1000, 64), (64, 64 + 7, 192)])
+def test_gemm_nt_n_edge_into_padded_rows(M, N, K):
+    """NT GEMM with N no tile multiple (the tied LM head, V = 50,257): B rows
+    past N read the zero page in-kernel, the output is a [M, N] view of rows
+    padded to a multiple of 8 columns; columns past the padded chunk are never
+    written."""
+    a, b, _ = _mk(M, N, K, "cuda", seed=3)
+    ld = -(-N // 8) * 8 + 16
+    buf = torch.full((M, ld), 7.0, device="cuda").to(torch.bfloat16)
+    out = buf[:, :N]
+    _ops().mm_nt(a, b, None, out)
+    assert _rel(out, a.float() @ b.float().t()) < 1e-2
+    assert torch.all(buf[:, -(-N // 8) * 8:] == 7.0)  # beyond the straddling chunk: untouched
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("layout", ["nt", "nn"])
 def test_gemm_matches_fp32(M, N, K, layout):

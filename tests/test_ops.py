@@ -482,6 +482,42 @@ def test_client_tail_matches_composition(device, has_w, has_u, has_e):
 
 
 @pytest.mark.gpu
+def test_fused_ce_padded_rows_vector_kernel():
+    """Logits as rows of a buffer padded to a multiple of 8 columns (the native
+    LM head's output; csrc/loss.hip ce_fwd_rowv_kernel): NaN pads are never
+    read, loss / top-1 / gradient match the fp32 reference, the gradient comes
+    back in the same row layout with zero pad columns, and the backward scale
+    keeps them zero."""
+    from commefficient_amd.ops.nn import cross_entropy_correct
+    torch.manual_seed(1)
+    V, B = 50257, 9
+    ld = -(-V // 8) * 8
+    buf = torch.full((B, ld), float("nan"), device="cuda").to(torch.bfloat16)
+    buf[:, :V] = (torch.randn(B, V, device="cuda") * 3).to(torch.bfloat16)
+    buf[3, 77] = buf[3, 4000] = 40.0  # a tie for the max: the lower index wins
+    tgt = torch.tensor([5, -100, 50256, 77, 0, 123, 4000, 50255, 8], device="cuda")
+    x = buf[:, :V].requires_grad_(True)
+    loss, correct = cross_entropy_correct(x, tgt)
+    w = torch.randn(B, device="cuda")
+    (loss * w).sum().backward()
+    xr = buf[:, :V].float().clone().requires_grad_(True)
+    ref = F.cross_entropy(xr, tgt, ignore_index=-100, reduction="none")
+    (ref * w).sum().backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+    keep = tgt >= 0
+    torch.testing.assert_close(correct[keep], (xr.argmax(1) == tgt).float()[keep])
+    assert correct[3] == 1.0
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-4)
+    # the op itself: the unit gradient in the logits' row layout, zero pad columns
+    _, _, gunit = torch.ops.commeff.ce_fwd(buf[:, :V], tgt)
+    assert gunit.stride(0) == ld
+    pads = torch.as_strided(gunit, (B, ld - V), (ld, 1), gunit.storage_offset() + V)
+    assert torch.all(pads == 0)
+    torch.ops.commeff.scale_rows(gunit, w)
+    assert torch.all(pads == 0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_fused_ce_ignore_rows_and_backward(dtype):
     """The GPT-2 LM loss at the labelled positions (train/losses.py): rows

@@ -8,6 +8,7 @@ the whole native GPT-2 hidden-state forward/backward against HF on the GPU.
 """
 import pytest
 import torch
+import torch.nn.functional as F
 
 from commefficient_amd.models.gpt2 import build_double_heads
 from commefficient_amd.ops import transformer as tx
@@ -504,11 +505,11 @@ def test_gemm_tn_wgrad_vs_fp32_reference_gpu(shape):
 def test_lm_head_native_vs_fp32_gpu(sinked, monkeypatch):
     """The tied LM head (vocabulary 50,257, no tile multiple) on the native
     GEMMs (ops/transformer.py _LMHead): logits, dh and dW (returned, or
-    accumulated into an fp32 gradient sink on the side stream by the split-K
-    TN GEMM with a partial edge tile) vs the fp32 products of the same bf16
-    operands."""
+    accumulated into an fp32 gradient sink on the side stream) vs the fp32
+    products of the same bf16 operands, for an external (unpadded) output
+    gradient."""
     V, H, T = 50257, 768, 600
-    monkeypatch.setattr(tx, "_LM_NATIVE", True)  # opt-in path (COMMEFF_LM_HEAD=native)
+    monkeypatch.setattr(tx, "_LM_NATIVE", True)
     g = torch.Generator().manual_seed(5)
     head = torch.nn.Linear(H, V, bias=False).to(torch.bfloat16).cuda()
     with torch.no_grad():
@@ -538,6 +539,45 @@ def test_lm_head_native_vs_fp32_gpu(sinked, monkeypatch):
         torch.testing.assert_close(sink - sink0, dw_ref, rtol=1e-3, atol=2e-2)
     else:
         assert rel(W.grad, dw_ref) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dw_tn", [False, True])
+def test_lm_head_native_ce_chain_padded_gradient(dw_tn, monkeypatch):
+    """LM head -> native cross-entropy on the padded logits -> backward: the
+    gradient stays in the padded layout end to end (no copies), dW goes into
+    the sink (hipBLASLt, or the TN GEMM's M = V edge tile), and the result
+    matches the fp32 chain on the same bf16 operands."""
+    from commefficient_amd.ops.nn import cross_entropy_correct
+    monkeypatch.setattr(tx, "_LM_DW_TN", dw_tn)
+    V, H, T = 50257, 768, 512
+    g = torch.Generator().manual_seed(7)
+    head = torch.nn.Linear(H, V, bias=False).to(torch.bfloat16).cuda()
+    with torch.no_grad():
+        head.weight.copy_((torch.randn(V, H, generator=g) * 0.05).to(torch.bfloat16))
+    m = type("M", (), {})()
+    m.lm_head = head
+    W = head.weight
+    h = torch.randn(T, H, generator=g).to(torch.bfloat16).cuda().requires_grad_(True)
+    tgt = torch.randint(0, V, (T,), generator=g).cuda()
+    tgt[::5] = -100
+    w = torch.rand(T, generator=g).cuda()
+    sink = torch.zeros(V, H, device="cuda")
+    with tx.grad_sinks({id(W): sink}):
+        logits = tx.lm_head(m, h)
+        assert logits.stride(0) == -(-V // 8) * 8  # the padded buffer itself
+        loss, _ = cross_entropy_correct(logits, tgt)
+        (loss * w).sum().backward()
+    tx.join_wgrad_stream()
+    torch.cuda.synchronize()
+    hr = h.detach().float().requires_grad_(True)
+    Wr = W.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(hr @ Wr.t(), tgt, ignore_index=-100, reduction="none")
+    (ref * w).sum().backward()
+    rel = lambda a, b: ((a.float() - b).abs().max() / b.abs().max()).item()  # noqa: E731
+    assert rel(loss, ref) < 1e-2
+    assert rel(h.grad, hr.grad) < 2e-2
+    assert rel(sink, Wr.grad) < 2e-2
 
 
 @pytest.mark.gpu
