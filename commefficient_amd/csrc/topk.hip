@@ -471,7 +471,8 @@ write_kernel(const float* __restrict__ x, int64_t n, int64_t span, WS ws, uint32
 
 struct CandWS {
   uint32_t* seg;       // kSegMax popcount totals
-  uint32_t* ctl;       // [0] list in use, [1] its length
+  uint32_t* ctl;       // [0] list in use, [1] its length, [2] fill-in mode (cand_scan_kernel)
+  uint32_t* segpre;    // kSegMax exclusive prefix of seg (cand_scan_kernel)
   uint64_t* ballots;   // one mask per chunk
   int32_t* cidx;       // cap
   float* cval;         // cap
@@ -487,6 +488,7 @@ CandWS carve_cand(void* base, int64_t n) {
   CandWS c;
   c.seg = reinterpret_cast<uint32_t*>(p); p += kSegMax * 4;
   c.ctl = reinterpret_cast<uint32_t*>(p); p += 16;
+  c.segpre = reinterpret_cast<uint32_t*>(p); p += kSegMax * 4;
   const int64_t nch = (n + 63) / 64;
   c.ballots = reinterpret_cast<uint64_t*>(p); p += nch * 8;
   const int64_t cap = cand_cap(n);
@@ -495,6 +497,9 @@ CandWS carve_cand(void* base, int64_t n) {
   return c;
 }
 
+// Small vectors (< 2,048 x 4,096 elements: the ResNet-9 headline's 6.57M):
+// one kernel, each block deriving the mode and its segment's prefix itself
+// (13.4 us at 6.57M against 4.7 + 11.1 for the scan pass + the kernel below).
 // block = kSub chunks (4,096 elements) of one segment, 256 threads of 16
 // consecutive elements (four 16-byte loads, all in flight at once); a
 // thread's output slot is the candidates before its segment (segment
@@ -502,7 +507,7 @@ CandWS carve_cand(void* base, int64_t n) {
 // before it inside the block (one scan)
 constexpr int kSub = 64;
 __global__ void __launch_bounds__(256)
-cand_compact_kernel(const float* __restrict__ x, int64_t n, WS ws, CandWS cw, uint32_t kk,
+cand_compact_small_kernel(const float* __restrict__ x, int64_t n, WS ws, CandWS cw, uint32_t kk,
                     const uint32_t* __restrict__ hint, int64_t cap) {
   __shared__ uint32_t h[kBins];
   __shared__ uint32_t wt[4], wt2[4], wt3[4];
@@ -535,22 +540,22 @@ cand_compact_kernel(const float* __restrict__ x, int64_t n, WS ws, CandWS cw, ui
     cw.ctl[1] = m_total;
   }
   if (!fill && !use) return;
-  // this thread's 16 elements (clamped loads; validity applied at use)
+  // this thread's 16 elements
   const int64_t e0 = cb0 * 64 + 16 * tid;
-  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0;
-  float v[16];
-  if (al) {
+  if (fill) {  // hist[3]: the keys < hint of this block's elements (clamped loads)
+    const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0;
+    float v[16];
+    if (al) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = min(e0 + 4 * u, n - 4);
-      const float4 q = *reinterpret_cast<const float4*>(x + i);
-      v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = min(e0 + 4 * u, n - 4);
+        const float4 q = *reinterpret_cast<const float4*>(x + i);
+        v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) v[t] = x[min(e0 + t, n - 1)];
     }
-  } else {
-#pragma unroll
-    for (int t = 0; t < 16; ++t) v[t] = x[min(e0 + t, n - 1)];
-  }
-  if (fill) {  // hist[3]: the keys < hint of this block's elements
     for (int b = tid; b < kBins; b += 256) h[b] = 0u;
     __syncthreads();
 #pragma unroll
@@ -563,18 +568,148 @@ cand_compact_kernel(const float* __restrict__ x, int64_t n, WS ws, CandWS cw, ui
       if (h[b] != 0u) atomicAdd(ws.hist[3] + b, h[b]);
     return;
   }
+  // the candidates only: the ballot bits say which elements are >= hint, so
+  // x is read at those (a few times k of n) instead of streamed whole
   const int64_t ch = cb0 + (tid >> 2);
   const uint64_t bal = cw.ballots[ch < nch ? ch : nch - 1];
   const uint32_t bits = (ch < nch) ? static_cast<uint32_t>(bal >> (16 * (tid & 3))) & 0xffffu : 0u;
   uint32_t blk_tot;
   uint32_t pos = before + block_excl_scan(static_cast<uint32_t>(__popc(bits)), wt, blk_tot);
+  for (uint32_t b = bits; b != 0u; b &= b - 1u) {
+    const int t = __builtin_ctz(b);
+    cw.cidx[pos] = static_cast<int32_t>(e0 + t);
+    cw.cval[pos] = x[e0 + t];
+    ++pos;
+  }
+}
+
+// One block, before the compaction: the mode (fill-in / candidate list /
+// full-vector fallback) from the integer totals, and the segments' exclusive
+// prefix -- every compaction block used to re-derive both from the 2,048 bins
+// and all segment totals (~20 KB of prologue reads per 4,096-element block:
+// the GPT-2 compaction took 320 us for 124M elements).
+__device__ __forceinline__ uint32_t block_excl_scan1024(uint32_t v, uint32_t* wt, uint32_t& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = v;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if ((bits >> t) & 1u) {
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wt[wave] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    before += w < wave ? wt[w] : 0u;
+    tot += wt[w];
+  }
+  total = tot;
+  return before + inc - v;
+}
+
+__global__ void __launch_bounds__(1024) cand_scan_kernel(WS ws, CandWS cw, int nseg, uint32_t kk, int64_t cap) {
+  __shared__ uint32_t wt[16];
+  const int tid = threadIdx.x;
+  uint32_t ht = 0;
+  for (int b = tid; b < kBins; b += 1024) ht += ws.hist[0][b];
+  uint32_t hist_total;
+  (void)block_excl_scan1024(ht, wt, hist_total);
+  __syncthreads();
+  uint32_t run = 0;
+  for (int base = 0; base < nseg; base += 1024) {
+    const int sg = base + tid;
+    const uint32_t v = sg < nseg ? cw.seg[sg] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan1024(v, wt, tot);
+    if (sg < nseg) cw.segpre[sg] = run + ex;
+    run += tot;
+    __syncthreads();  // (wt reuse)
+  }
+  if (tid == 0) {
+    const bool fill = hist_total < kk;
+    const bool use = !fill && static_cast<int64_t>(run) <= cap;
+    cw.ctl[0] = use ? 1u : 0u;
+    cw.ctl[1] = run;
+    cw.ctl[2] = fill ? 1u : 0u;
+  }
+}
+
+// block = IT x 64 chunks (IT x 4,096 elements) of one segment, 256 threads
+// of 16 consecutive elements per step (four 16-byte loads, all in flight at
+// once); a thread's output slot is the segment's prefix (cand_scan_kernel),
+// the ballot popcounts of the segment's chunks before the block, and one
+// block scan per step
+template <int IT>
+__global__ void __launch_bounds__(256)
+cand_compact_kernel(const float* __restrict__ x, int64_t n, WS ws, CandWS cw, const uint32_t* __restrict__ hint) {
+  __shared__ uint32_t h[kBins];
+  __shared__ uint32_t wt[4];
+  const int tid = threadIdx.x;
+  const bool fill = cw.ctl[2] != 0u, use = cw.ctl[0] != 0u;
+  if (!fill && !use) return;
+  const uint32_t lb = hint != nullptr ? hint[0] : 0u;
+  const int64_t nch = (n + 63) / 64;
+  const int64_t cb0 = static_cast<int64_t>(blockIdx.x) * 64 * IT;  // first chunk of the block
+  const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (n & 3) == 0;
+  auto load16 = [&](int64_t e0, float (&v)[16]) __attribute__((always_inline)) {
+    if (al) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = min(e0 + 4 * u, n - 4);
+        const float4 q = *reinterpret_cast<const float4*>(x + i);
+        v[4 * u] = q.x; v[4 * u + 1] = q.y; v[4 * u + 2] = q.z; v[4 * u + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) v[t] = x[min(e0 + t, n - 1)];
+    }
+  };
+  if (fill) {  // hist[3]: the keys < hint of this block's elements
+    for (int b = tid; b < kBins; b += 256) h[b] = 0u;
+    __syncthreads();
+    for (int it = 0; it < IT; ++it) {
+      const int64_t e0 = (cb0 + 64 * it) * 64 + 16 * tid;
+      float v[16];
+      load16(e0, v);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const uint32_t k = key_of(v[t]);
+        if (e0 + t < n && k < lb) atomicAdd(h + (k >> 20), 1u);
+      }
+    }
+    __syncthreads();
+    for (int b = tid; b < kBins; b += 256)
+      if (h[b] != 0u) atomicAdd(ws.hist[3] + b, h[b]);
+    return;
+  }
+  // candidates of the segment's chunks before this block (< kSegC of them)
+  const int seg = static_cast<int>(cb0 / kSegC);
+  uint32_t mb = 0;
+  for (int64_t ch = static_cast<int64_t>(seg) * kSegC + tid; ch < cb0; ch += 256)
+    mb += static_cast<uint32_t>(__popcll(cw.ballots[ch]));
+  uint32_t before;
+  (void)block_excl_scan(mb, wt, before);
+  __syncthreads();
+  uint32_t base = cw.segpre[seg] + before;
+  for (int it = 0; it < IT; ++it) {
+    const int64_t c0 = cb0 + 64 * it;
+    if (c0 >= nch) break;  // (block-uniform)
+    const int64_t e0 = c0 * 64 + 16 * tid;
+    const int64_t ch = c0 + (tid >> 2);
+    const uint64_t bal = cw.ballots[ch < nch ? ch : nch - 1];
+    const uint32_t bits = (ch < nch) ? static_cast<uint32_t>(bal >> (16 * (tid & 3))) & 0xffffu : 0u;
+    uint32_t tot;
+    uint32_t pos = base + block_excl_scan(static_cast<uint32_t>(__popc(bits)), wt, tot);
+    // (x read at the candidates only)
+    for (uint32_t b = bits; b != 0u; b &= b - 1u) {
+      const int t = __builtin_ctz(b);
       cw.cidx[pos] = static_cast<int32_t>(e0 + t);
-      cw.cval[pos] = v[t];
+      cw.cval[pos] = x[e0 + t];
       ++pos;
     }
+    base += tot;
+    __syncthreads();  // (wt reuse)
   }
 }
 
@@ -590,8 +725,8 @@ bool topk_cand_supported(int64_t n) {
 
 int64_t topk_cand_workspace_bytes(int64_t n) {
   const int64_t cap = cand_cap(n);
-  return 4 * kBins * 4 + 2 * kNB * 4 + 64 + kSegMax * 4 + 16 + ((n + 63) / 64) * 8 + ((cap * 4 + 15) / 16) * 16 +
-         cap * 4;
+  return 4 * kBins * 4 + 2 * kNB * 4 + 64 + kSegMax * 4 + 16 + kSegMax * 4 + ((n + 63) / 64) * 8 +
+         ((cap * 4 + 15) / 16) * 16 + cap * 4;
 }
 
 void topk_cand_prepare(void* workspace, hipStream_t stream) {
@@ -611,9 +746,27 @@ void launch_topk_cand_rest(const float* x, int64_t n, int64_t k, int64_t* idx, f
   WS w = carve(workspace);
   const CandWS cw = carve_cand(workspace, n);
   const uint32_t kk = static_cast<uint32_t>(k < n ? k : n);
-  const int nblk = static_cast<int>(((n + 63) / 64 + kSub - 1) / kSub);
-  COMMEFF_LAUNCH(cand_compact_kernel, dim3(nblk), dim3(256), 0, stream, x, n, w, cw, kk, hint,
-                     cand_cap(n));
+  const int64_t nch = (n + 63) / 64;
+  const int nseg = static_cast<int>((nch + kSegC - 1) / kSegC);
+  // chunks per compaction block: the most (<= 16 x 64, a divisor of a
+  // segment) that still leaves >= 2,048 blocks
+  int it = 16;
+  while (it > 1 && (nch + 64 * it - 1) / (64 * it) < 2048) it >>= 1;
+  if (it == 1) {
+    const int nblk = static_cast<int>((nch + kSub - 1) / kSub);
+    COMMEFF_LAUNCH(cand_compact_small_kernel, dim3(nblk), dim3(256), 0, stream, x, n, w, cw, kk, hint,
+                   cand_cap(n));
+  } else {
+    COMMEFF_LAUNCH(cand_scan_kernel, dim3(1), dim3(1024), 0, stream, w, cw, nseg, kk, cand_cap(n));
+  }
+  const dim3 grid(static_cast<uint32_t>((nch + 64 * it - 1) / (64 * it)));
+  switch (it) {
+    case 16: COMMEFF_LAUNCH(cand_compact_kernel<16>, grid, dim3(256), 0, stream, x, n, w, cw, hint); break;
+    case 8: COMMEFF_LAUNCH(cand_compact_kernel<8>, grid, dim3(256), 0, stream, x, n, w, cw, hint); break;
+    case 4: COMMEFF_LAUNCH(cand_compact_kernel<4>, grid, dim3(256), 0, stream, x, n, w, cw, hint); break;
+    case 2: COMMEFF_LAUNCH(cand_compact_kernel<2>, grid, dim3(256), 0, stream, x, n, w, cw, hint); break;
+    default: break;  // (the small-vector kernel above)
+  }
   const Cand cd{cw.ctl, cw.cval, cw.cidx};
   constexpr int nb = 256;  // candidate passes (the fallbacks stream x on these too)
   COMMEFF_LAUNCH((hist_kernel<1, true>), dim3(nb), dim3(256), 0, stream, x, n, w, kk, hint, cd);
