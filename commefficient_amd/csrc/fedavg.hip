@@ -275,19 +275,26 @@ __global__ void __launch_bounds__(256) avgmax_head_fwd_kernel(const bf16raw* __r
 }
 
 // dx[e][h][g*C + c] = df[g][e][c] / HW + (h == code ? df[g][e][C + c] : 0)
+// (df: S partial slabs [S][G][n][2C] summed in slab order -- the class-chunk
+// partials of fa_linear_kernel)
 __global__ void __launch_bounds__(256) avgmax_head_bwd_kernel(const float* __restrict__ df,
                                                               const uint8_t* __restrict__ codes, int n, int HW,
-                                                              int G, int C, bf16raw* __restrict__ dx) {
+                                                              int G, int C, bf16raw* __restrict__ dx, int S) {
   const int GC = G * C;
-  const int64_t total = static_cast<int64_t>(n) * HW * GC;
+  const int64_t total = static_cast<int64_t>(n) * HW * GC, slab = static_cast<int64_t>(G) * n * 2 * C;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
     const int gc = static_cast<int>(i % GC);
     const int64_t eh = i / GC;
     const int h = static_cast<int>(eh % HW), e = static_cast<int>(eh / HW);
     const int g = gc / C, c = gc - g * C;
     const float* f = df + (static_cast<int64_t>(g) * n + e) * 2 * C;
-    float v = f[c] / HW;
-    if (codes[static_cast<int64_t>(e) * GC + gc] == h) v += f[C + c];
+    float fa = f[c], fm = f[C + c];
+    for (int q = 1; q < S; ++q) {
+      fa += f[q * slab + c];
+      fm += f[q * slab + C + c];
+    }
+    float v = fa / HW;
+    if (codes[static_cast<int64_t>(e) * GC + gc] == h) v += fm;
     dx[i] = f2bf(v);
   }
 }
@@ -315,6 +322,181 @@ __global__ void __launch_bounds__(256) ew_bf16_kernel(const bf16raw* __restrict_
       }
     }
     reinterpret_cast<u4*>(y)[i] = o;
+  }
+}
+
+// ------------------------------------------------------------ classifier
+// The per-client classifier of a local step in two kernels (replacing three
+// batched hipBLASLt GEMMs, the loss kernel and the bias GEMM of the step in
+// fedavg_native.py's heads):
+//   fa_logits_kernel   grid (G, class blocks): logits = scale feat W^T (+ b),
+//                      a wave per class, lanes over the features (coalesced
+//                      row reads, 4 rows in flight a wave);
+//   fa_linear_kernel   grid (G, feature blocks of 256): every block redoes its
+//                      client's softmax from the logits (n x C values), then
+//                      streams the client's rows once -- for each class the
+//                      lanes' features accumulate the feature gradient
+//                      (scale / n) sum_c gl[i][c] W[c][f] with the step's
+//                      weights and write the SGD-updated weight beta src +
+//                      alpha (scale / n) sum_i gl[i][c] feat[i][f] (bias:
+//                      alpha / n); block 0 writes the loss and top-1.
+// Each block owns distinct columns of its client's rows: every row element is
+// read before it is rewritten by the same thread.
+template <typename TI>
+__device__ __forceinline__ float fa_ld(const TI* p, int64_t i) {
+  if constexpr (sizeof(TI) == 2) return bf2f(p[i]);
+  else return p[i];
+}
+
+template <typename TI, int NM>  // NM: the examples' register budget (>= n)
+__global__ void __launch_bounds__(256) fa_logits_kernel(FaLinearArgs a, float* __restrict__ logits) {
+  extern __shared__ float sf[];  // [n][F]
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = a.n, C = a.C, F = a.F;
+  const TI* feat = static_cast<const TI*>(a.feat) + g * a.fsg;
+  for (int e = tid; e < n * F; e += 256) {
+    const int i = e / F, f = e - i * F;
+    sf[e] = fa_ld(feat, i * a.fsn + f);
+  }
+  __syncthreads();
+  const float* Wg = a.W + g * a.wld + a.woff;
+  const int c_end = min(C, static_cast<int>(blockIdx.y + 1) * kFaCls);
+  for (int c0 = blockIdx.y * kFaCls + wv * 4; c0 < c_end; c0 += 16) {
+    float acc[4][NM];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < NM; ++i) acc[q][i] = 0.f;
+    for (int f = lane; f < F; f += 64) {
+      float w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = c0 + q < c_end ? Wg[static_cast<int64_t>(c0 + q) * F + f] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        if (i < n) {
+          const float x = sf[i * F + f];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q][i] = fmaf(w[q], x, acc[q][i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = c0 + q;
+      const float b = (a.boff >= 0 && c < c_end) ? a.W[g * a.wld + a.boff + c] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        if (i < n) {
+          float v = acc[q][i];
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+          if (lane == 0 && c < c_end) logits[(static_cast<int64_t>(g) * n + i) * C + c] = a.scale * v + b;
+        }
+      }
+    }
+  }
+}
+
+template <typename TI, typename TO, int NM>
+__global__ void __launch_bounds__(256) fa_linear_kernel(FaLinearArgs a, const float* __restrict__ logits) {
+  extern __shared__ float sm[];
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = a.n, C = a.C, F = a.F;
+  float* sg = sm;  // [n][C] softmax - onehot
+  for (int e = tid; e < n * C; e += 256) sg[e] = logits[static_cast<int64_t>(g) * n * C + e];
+  __syncthreads();
+  // cross-entropy: one wave per example (max with the first index, as torch.argmax)
+  for (int i = wv; i < n; i += 4) {
+    float* r = sg + i * C;
+    float m = -__builtin_huge_valf();
+    int mi = C;
+    for (int j = lane; j < C; j += 64)
+      if (r[j] > m) { m = r[j]; mi = j; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(m, o, 64);
+      const int oi = __shfl_xor(mi, o, 64);
+      if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
+    }
+    float sum = 0.f;
+    for (int j = lane; j < C; j += 64) sum += __expf(r[j] - m);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    int64_t t = a.y[static_cast<int64_t>(g) * n + i];
+    t = t < 0 ? 0 : (t >= C ? C - 1 : t);  // (labels are valid classes; clamped for memory safety)
+    const float xt = r[t];  // (read by every lane before any lane rewrites the row)
+    if (lane == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+      a.loss[static_cast<int64_t>(g) * n + i] = m + __logf(sum) - xt;
+      a.correct[static_cast<int64_t>(g) * n + i] = mi == t ? 1.f : 0.f;
+    }
+    const float inv = 1.f / sum;
+    for (int j = lane; j < C; j += 64) r[j] = __expf(r[j] - m) * inv - (j == t ? 1.f : 0.f);
+  }
+  __syncthreads();
+  const int f = blockIdx.y * 256 + tid;
+  // this block's classes (blockIdx.z: a chunk of a.ccs), its feature-gradient slab
+  const int cb = blockIdx.z * a.ccs, ce = min(C, cb + a.ccs);
+  const float sn = a.scale / n, ka = a.alpha * sn;
+  float* dst = a.dst + g * a.dld;
+  const float* src = a.src != nullptr ? a.src + g * a.sld : dst;
+  const float* Wg = a.W + g * a.wld + a.woff;
+  if (f < F) {
+    const TI* feat = static_cast<const TI*>(a.feat) + g * a.fsg;
+    float x[NM], d[NM];
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      x[i] = i < n ? fa_ld(feat, i * a.fsn + f) : 0.f;
+      d[i] = 0.f;
+    }
+    constexpr int U = 16;  // rows in flight (the loop is load-latency bound)
+    // (later steps update the rows the forward read: one load serves both)
+    const bool own = src + a.woff == Wg;
+    for (int c0 = cb; c0 < ce; c0 += U) {
+      float w[U], sv[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) w[q] = c0 + q < ce ? Wg[static_cast<int64_t>(c0 + q) * F + f] : 0.f;
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+        sv[q] = own ? w[q]
+                    : ((a.beta != 0.f && c0 + q < ce) ? src[a.woff + static_cast<int64_t>(c0 + q) * F + f] : 0.f);
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const int c = c0 + q;
+        if (c >= ce) break;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (i < n) {
+            const float gv = sg[i * C + c];
+            d[i] = fmaf(gv, w[q], d[i]);
+            s = fmaf(gv, x[i], s);
+          }
+        }
+        const int64_t o = a.woff + static_cast<int64_t>(c) * F + f;
+        const float nw = a.beta * sv[q] + ka * s;
+        dst[o] = nw;
+        if (a.mirror != nullptr) a.mirror[g * a.mld + o] = f2bf(nw);
+      }
+    }
+    TO* df = static_cast<TO*>(a.dfeat) + blockIdx.z * a.dss + g * a.dsg;
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      if (i < n) {
+        if constexpr (sizeof(TO) == 2) df[i * a.dsn + f] = f2bf(sn * d[i]);
+        else df[i * a.dsn + f] = sn * d[i];
+      }
+    }
+  }
+  if (a.boff >= 0 && blockIdx.y == 0) {
+    const float kb = a.alpha / n;
+    for (int c = cb + tid; c < ce; c += 256) {
+      float s = 0.f;
+      for (int i = 0; i < n; ++i) s += sg[i * C + c];
+      const int64_t o = a.boff + c;
+      const float nw = a.beta != 0.f ? a.beta * src[o] + kb * s : kb * s;
+      dst[o] = nw;
+      if (a.mirror != nullptr) a.mirror[g * a.mld + o] = f2bf(nw);
+    }
   }
 }
 
@@ -384,16 +566,55 @@ void launch_avgmax_head_fwd(const uint16_t* x, int n, int HW, int G, int C, floa
 }
 
 void launch_avgmax_head_bwd(const float* df, const uint8_t* codes, int n, int HW, int G, int C, uint16_t* dx,
-                            hipStream_t stream) {
+                            hipStream_t stream, int S) {
   const int64_t total = static_cast<int64_t>(n) * HW * G * C;
   if (total == 0) return;
   COMMEFF_LAUNCH(avgmax_head_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, stream, df, codes, n, HW, G, C,
-                 dx);
+                 dx, S);
 }
 
 void launch_ew_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n8, int mode, hipStream_t stream) {
   if (n8 == 0) return;
   COMMEFF_LAUNCH(ew_bf16_kernel, dim3(grid_for(n8)), dim3(256), 0, stream, a, b, y, n8, mode);
+}
+
+int64_t fa_linear_lds_bytes(int n, int C, int F) {
+  const int64_t a = static_cast<int64_t>(n) * F * 4, b = static_cast<int64_t>(n) * C * 4;
+  return a > b ? a : b;
+}
+
+template <int NM>
+void fa_linear_launch(const FaLinearArgs& a, int G, bool feat_bf16, bool dfeat_bf16, float* logits,
+                      hipStream_t stream) {
+  const int l1 = a.n * a.F * 4, l2 = a.n * a.C * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fa_logits_kernel<float, NM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kFaMaxLds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fa_logits_kernel<uint16_t, NM>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kFaMaxLds);
+    attr = true;
+  }
+  const dim3 g1(G, (a.C + kFaCls - 1) / kFaCls), g2(G, (a.F + 255) / 256, (a.C + a.ccs - 1) / a.ccs);
+  const float* lg = logits;
+  if (feat_bf16) {
+    COMMEFF_LAUNCH((fa_logits_kernel<uint16_t, NM>), g1, dim3(256), l1, stream, a, logits);
+    if (dfeat_bf16) COMMEFF_LAUNCH((fa_linear_kernel<uint16_t, uint16_t, NM>), g2, dim3(256), l2, stream, a, lg);
+    else COMMEFF_LAUNCH((fa_linear_kernel<uint16_t, float, NM>), g2, dim3(256), l2, stream, a, lg);
+  } else {
+    COMMEFF_LAUNCH((fa_logits_kernel<float, NM>), g1, dim3(256), l1, stream, a, logits);
+    if (dfeat_bf16) COMMEFF_LAUNCH((fa_linear_kernel<float, uint16_t, NM>), g2, dim3(256), l2, stream, a, lg);
+    else COMMEFF_LAUNCH((fa_linear_kernel<float, float, NM>), g2, dim3(256), l2, stream, a, lg);
+  }
+}
+
+void launch_fa_linear_ce(FaLinearArgs a, int G, bool feat_bf16, bool dfeat_bf16, float* logits, hipStream_t stream) {
+  if (G == 0 || a.n == 0) return;
+  if (a.ccs <= 0) a.ccs = a.C;
+  // (registers for the examples: a 32-wide budget for 5 examples spilled)
+  if (a.n <= 8) fa_linear_launch<8>(a, G, feat_bf16, dfeat_bf16, logits, stream);
+  else if (a.n <= 16) fa_linear_launch<16>(a, G, feat_bf16, dfeat_bf16, logits, stream);
+  else fa_linear_launch<kFaMaxN>(a, G, feat_bf16, dfeat_bf16, logits, stream);
 }
 
 }  // namespace commeff

@@ -28,7 +28,7 @@ void launch_cast_rows(uint16_t* Wb, const float* W, int64_t ld, int G, int64_t o
 void launch_avgmax_head_fwd(const uint16_t* x, int n, int HW, int G, int C, float* feat, uint8_t* codes,
                             hipStream_t stream);
 void launch_avgmax_head_bwd(const float* df, const uint8_t* codes, int n, int HW, int G, int C, uint16_t* dx,
-                            hipStream_t stream);
+                            hipStream_t stream, int S);
 void launch_ew_bf16(const uint16_t* a, const uint16_t* b, uint16_t* y, int64_t n8, int mode, hipStream_t stream);
 
 namespace {
@@ -248,18 +248,98 @@ std::tuple<at::Tensor, at::Tensor> fa_head_fwd(const at::Tensor& x, int64_t G) {
   return {feat, codes};
 }
 
+// the per-client classifier step (fedavg.hip fa_linear_ce_kernel): returns
+// (loss [G n], correct [G n]); writes dfeat and the updated rows of dst
+std::tuple<at::Tensor, at::Tensor> fa_linear_ce(const at::Tensor& feat, int64_t fsg, int64_t fsn, int64_t G,
+                                                int64_t n, const at::Tensor& W, int64_t wld, int64_t woff,
+                                                int64_t boff, int64_t C, int64_t F, double scale, const at::Tensor& y,
+                                                at::Tensor dfeat, int64_t dsg, int64_t dsn, at::Tensor dst, int64_t dld,
+                                                double beta, double alpha, const c10::optional<at::Tensor>& src,
+                                                int64_t sld, const c10::optional<at::Tensor>& mirror, int64_t mld,
+                                                int64_t dss, int64_t ccs) {
+  TORCH_CHECK(feat.is_cuda() && (feat.scalar_type() == at::kFloat || feat.scalar_type() == at::kBFloat16) &&
+                  (dfeat.scalar_type() == at::kFloat || dfeat.scalar_type() == at::kBFloat16),
+              "fa_linear_ce: feat / dfeat fp32 or bf16");
+  TORCH_CHECK(G >= 1 && n >= 1 && n <= kFaMaxN && C >= 1 && F >= 1 &&
+                  fa_linear_lds_bytes(static_cast<int>(n), static_cast<int>(C), static_cast<int>(F)) <= kFaMaxLds,
+              "fa_linear_ce: n <= ", kFaMaxN, " examples per client and n (F + C) floats of LDS");
+  auto span_ok = [](const at::Tensor& t, int64_t sg, int64_t sn, int64_t G, int64_t n, int64_t F) {
+    return t.is_contiguous() && sg >= 0 && sn >= 0 && (G - 1) * sg + (n - 1) * sn + F <= t.numel();
+  };
+  const int64_t S = ccs > 0 ? (C + ccs - 1) / ccs : 1;
+  TORCH_CHECK(span_ok(feat, fsg, fsn, G, n, F) && span_ok(dfeat, dsg, dsn, G, n, F) &&
+                  (S == 1 || (dss > 0 && (S - 1) * dss + (G - 1) * dsg + (n - 1) * dsn + F <= dfeat.numel())),
+              "fa_linear_ce: feat / dfeat spans (S class-chunk slabs dss apart)");
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && wld >= 0 && woff >= 0 &&
+                  (G - 1) * wld + woff + C * F <= W.numel() && (boff < 0 || (G - 1) * wld + boff + C <= W.numel()),
+              "fa_linear_ce: weight rows");
+  TORCH_CHECK(dst.scalar_type() == at::kFloat && dst.is_contiguous() && dld >= 0 &&
+                  (G - 1) * dld + woff + C * F <= dst.numel() && (boff < 0 || (G - 1) * dld + boff + C <= dst.numel()),
+              "fa_linear_ce: dst rows");
+  const bool hs = src.has_value() && src->defined();
+  if (hs)
+    TORCH_CHECK(src->scalar_type() == at::kFloat && src->is_contiguous() && sld >= 0 &&
+                    (G - 1) * sld + woff + C * F <= src->numel() &&
+                    (boff < 0 || (G - 1) * sld + boff + C <= src->numel()),
+                "fa_linear_ce: src rows");
+  const bool hm = mirror.has_value() && mirror->defined();
+  if (hm)
+    TORCH_CHECK(mirror->scalar_type() == at::kBFloat16 && mirror->is_contiguous() &&
+                    (G - 1) * mld + woff + C * F <= mirror->numel(),
+                "fa_linear_ce: mirror rows");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.is_contiguous() && y.numel() == G * n, "fa_linear_ce: y int64 [G n]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(feat.device());
+  auto loss = at::empty({G * n}, feat.options().dtype(at::kFloat));
+  auto correct = at::empty({G * n}, feat.options().dtype(at::kFloat));
+  FaLinearArgs a{};
+  a.feat = feat.data_ptr();
+  a.fsg = fsg;
+  a.fsn = fsn;
+  a.W = W.data_ptr<float>();
+  a.wld = wld;
+  a.woff = woff;
+  a.boff = boff;
+  a.y = y.data_ptr<int64_t>();
+  a.n = static_cast<int>(n);
+  a.C = static_cast<int>(C);
+  a.F = static_cast<int>(F);
+  a.scale = static_cast<float>(scale);
+  a.loss = loss.data_ptr<float>();
+  a.correct = correct.data_ptr<float>();
+  a.dfeat = dfeat.data_ptr();
+  a.dsg = dsg;
+  a.dsn = dsn;
+  a.dss = dss;
+  a.ccs = S == 1 ? 0 : static_cast<int>(ccs);
+  a.dst = dst.data_ptr<float>();
+  a.dld = dld;
+  a.beta = static_cast<float>(beta);
+  a.alpha = static_cast<float>(alpha);
+  a.src = hs ? src->data_ptr<float>() : nullptr;
+  a.sld = sld;
+  a.mirror = hm ? reinterpret_cast<uint16_t*>(mirror->data_ptr()) : nullptr;
+  a.mld = mld;
+  auto logits = at::empty({G * n * C}, feat.options().dtype(at::kFloat));
+  launch_fa_linear_ce(a, static_cast<int>(G), feat.scalar_type() == at::kBFloat16,
+                      dfeat.scalar_type() == at::kBFloat16, logits.data_ptr<float>(), stream_now());
+  return {loss, correct};
+}
+
 at::Tensor fa_head_bwd(const at::Tensor& df, const at::Tensor& codes, int64_t H, int64_t W) {
   TORCH_CHECK(df.is_cuda() && df.scalar_type() == at::kFloat && df.is_contiguous() && df.dim() == 3 &&
                   df.size(2) % 2 == 0,
-              "fa_head_bwd: df fp32 [G, n, 2C]");
-  const int64_t G = df.size(0), n = df.size(1), C = df.size(2) / 2;
+              "fa_head_bwd: df fp32 [S G, n, 2C] (S partial slabs, summed)");
+  const int64_t n = df.size(1), C = df.size(2) / 2;
   TORCH_CHECK(codes.scalar_type() == at::kByte && codes.is_contiguous() && codes.dim() == 2 &&
-                  codes.size(0) == n && codes.size(1) == G * C && H * W >= 1 && H * W <= 256,
+                  codes.size(0) == n && C >= 1 && codes.size(1) % C == 0 && H * W >= 1 && H * W <= 256,
               "fa_head_bwd: codes uint8 [n, G*C]");
+  const int64_t G = codes.size(1) / C, S = df.size(0) / (G > 0 ? G : 1);
+  TORCH_CHECK(G >= 1 && S >= 1 && S * G == df.size(0), "fa_head_bwd: df rows a multiple of the clients");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(df.device());
   auto dx = at::empty({n, G * C, H, W}, df.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
   launch_avgmax_head_bwd(df.data_ptr<float>(), codes.data_ptr<uint8_t>(), static_cast<int>(n),
-                         static_cast<int>(H * W), static_cast<int>(G), static_cast<int>(C), bfw(dx), stream_now());
+                         static_cast<int>(H * W), static_cast<int>(G), static_cast<int>(C), bfw(dx), stream_now(),
+                         static_cast<int>(S));
   return dx;
 }
 
@@ -669,6 +749,9 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_dgrad_image(Tensor Wb, int ld, int G, int off, int K, int C) -> Tensor");
   m.def("conv3x3_fwd_rows(Tensor x, Tensor w, int G, int off, int ld, int kg, Tensor? addend=None, "
         "bool bt=False) -> Tensor");
+  m.def("fa_linear_ce(Tensor feat, int fsg, int fsn, int G, int n, Tensor W, int wld, int woff, int boff, int C, "
+        "int F, float scale, Tensor y, Tensor(a!) dfeat, int dsg, int dsn, Tensor(b!) dst, int dld, float beta, "
+        "float alpha, Tensor? src, int sld, Tensor(c!)? mirror, int mld, int dss=0, int ccs=0) -> (Tensor, Tensor)");
   m.def("fa_head_fwd(Tensor x, int G) -> (Tensor, Tensor)");
   m.def("fa_head_bwd(Tensor df, Tensor codes, int H, int W) -> Tensor");
   m.def("fa_ew(Tensor a, Tensor? b, int mode) -> Tensor");
@@ -695,6 +778,7 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("fa_gather_rows", &fa_gather_rows);
   m.impl("fa_bcast_rows", &fa_bcast_rows);
   m.impl("fa_cast_rows", &fa_cast_rows);
+  m.impl("fa_linear_ce", &fa_linear_ce);
   m.impl("fa_dgrad_image", &fa_dgrad_image);
   m.impl("conv3x3_fwd_rows", &conv3x3_fwd_rows);
   m.impl("fa_head_fwd", &fa_head_fwd);

@@ -593,6 +593,33 @@ struct GemmArgs {
   // column k = tap * imp_C + c (imp_C % 64 == 0: a K-step stays in one tap)
   int imp_C = 0, imp_H = 0, imp_W = 0, imp_OH = 0, imp_OW = 0, imp_R = 3, imp_s = 1, imp_pad = 1;
 };
+// batched FedAvg per-client classifier + cross-entropy + SGD (fedavg.hip)
+constexpr int kFaMaxN = 32;             // examples per client
+constexpr int kFaMaxLds = 96 * 1024;    // n F (and n C) fp32
+constexpr int kFaCls = 16;              // classes per logits block
+struct FaLinearArgs {
+  const void* feat;       // (client g, example i, feature f) at g * fsg + i * fsn + f
+  int64_t fsg, fsn;
+  const float* W;         // weight rows: client g's [C][F] at g * wld + woff, bias at + boff (< 0: none)
+  int64_t wld, woff, boff;
+  const int64_t* y;       // [G n] targets in [0, C)
+  int n, C, F;
+  float scale;
+  float* loss;            // [G n]
+  float* correct;         // [G n]
+  void* dfeat;            // like feat: g * dsg + i * dsn + f (+ s * dss: the slab of class chunk s)
+  int64_t dsg, dsn, dss;
+  int ccs;                // classes per chunk (<= 0: all; > 0: ceil(C / ccs) partial dfeat slabs)
+  float* dst;             // updated rows: g * dld + woff / boff
+  int64_t dld;
+  float beta, alpha;
+  const float* src;       // beta's rows (nullptr: dst's own), g * sld
+  int64_t sld;
+  uint16_t* mirror;       // bf16 copy of the updated rows (nullptr: none), g * mld
+  int64_t mld;
+};
+int64_t fa_linear_lds_bytes(int n, int C, int F);
+void launch_fa_linear_ce(FaLinearArgs a, int G, bool feat_bf16, bool dfeat_bf16, float* logits, hipStream_t stream);
 bool gemm_supported(int M, int N, int K, bool nn);
 bool gemm_supported_nedge(int M, int N, int K);
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);

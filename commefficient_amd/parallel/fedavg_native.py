@@ -40,6 +40,7 @@ FedModel falls back to the vmap composition otherwise.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -247,6 +248,13 @@ class ResNet18FedAvg:
             if addend is not None:
                 dx = _ops().fa_ew(dx, addend, 0)
         return dx
+
+    # the per-client classifier step on the fused kernel (fedavg.hip
+    # fa_linear_ce_kernel; COMMEFF_FA_HEAD=0: batched GEMMs + the loss kernel)
+    _FUSED_HEAD = [os.environ.get("COMMEFF_FA_HEAD", "1") != "0"]
+
+    def _fused_head_ok(self, n: int, F: int) -> bool:
+        return self._FUSED_HEAD[0] and n <= 32 and n * (F + self.ncls) * 4 <= 96 * 1024
 
     _BMM_INTO = [True]
     # (128-channel input gradients from the rows themselves: 29.72 vs 30.53 ms
@@ -462,23 +470,35 @@ class ResNet18FedAvg:
             saved.append((xin, colx, h1, st1, bits1, a1, h2, st2, bits2))
         # ---- head: avg || max pool -> per-client linear -> cross entropy
         feat, codes = ops.fa_head_fwd(a, G)
-        # classifier rows of every client (the first step: the server row, batch stride 0)
-        Wfc = self._rows(W, ld, G, self.fc_w, self.ncls, self.feat)
-        bfc = self._rows(W, ld, G, self.fc_b, 1, self.ncls)
-        logits = torch.bmm(feat, Wfc.transpose(1, 2))
-        logits.baddbmm_(ones[:, :n], bfc)
-        loss, correct, gl = ops.ce_fwd(logits.view(G * n, self.ncls), y)
-        gl = gl.view(G, n, self.ncls)
-        inv = 1.0 / n
-        # (the feature gradient first: the classifier rows may be updated in place next)
-        dfeat = torch.empty_like(feat)
-        torch.baddbmm(dfeat, gl, Wfc, beta=0.0, alpha=inv, out=dfeat)
-        gW = sink.dst[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
-        torch.baddbmm(sink.src_rows(self.fc_w, self.ncls, self.feat), gl.transpose(1, 2), feat, beta=sink.beta,
-                      alpha=sink.alpha * inv, out=gW)
-        gb = sink.dst[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
-        torch.baddbmm(sink.src_rows(self.fc_b, 1, self.ncls), ones[:, :n].transpose(1, 2), gl, beta=sink.beta,
-                      alpha=sink.alpha * inv, out=gb)
+        if self._fused_head_ok(n, self.feat):
+            # classifier + loss + feature gradient + the rows' SGD step: logits
+            # kernel, then the update kernel over (client, features, 32-class
+            # chunks) whose partial feature gradients the pool backward sums
+            S = -(-self.ncls // 32)
+            dfeat = torch.empty((S * G, n, self.feat), device=feat.device, dtype=torch.float32)
+            loss, correct = ops.fa_linear_ce(feat, n * self.feat, self.feat, G, n, W, ld, self.fc_w, self.fc_b,
+                                             self.ncls, self.feat, 1.0, y, dfeat, n * self.feat, self.feat,
+                                             sink.dst, sink.ld, sink.beta, sink.alpha, sink.src, sink.sld,
+                                             None, 0,  # (the classifier reads the fp32 rows: no mirror)
+                                             G * n * self.feat, 32)
+        else:
+            dfeat = torch.empty_like(feat)
+            # classifier rows of every client (the first step: the server row, batch stride 0)
+            Wfc = self._rows(W, ld, G, self.fc_w, self.ncls, self.feat)
+            bfc = self._rows(W, ld, G, self.fc_b, 1, self.ncls)
+            logits = torch.bmm(feat, Wfc.transpose(1, 2))
+            logits.baddbmm_(ones[:, :n], bfc)
+            loss, correct, gl = ops.ce_fwd(logits.view(G * n, self.ncls), y)
+            gl = gl.view(G, n, self.ncls)
+            inv = 1.0 / n
+            # (the feature gradient first: the classifier rows may be updated in place next)
+            torch.baddbmm(dfeat, gl, Wfc, beta=0.0, alpha=inv, out=dfeat)
+            gW = sink.dst[:, self.fc_w:self.fc_w + self.ncls * self.feat].view(G, self.ncls, self.feat)
+            torch.baddbmm(sink.src_rows(self.fc_w, self.ncls, self.feat), gl.transpose(1, 2), feat,
+                          beta=sink.beta, alpha=sink.alpha * inv, out=gW)
+            gb = sink.dst[:, self.fc_b:self.fc_b + self.ncls].view(G, 1, self.ncls)
+            torch.baddbmm(sink.src_rows(self.fc_b, 1, self.ncls), ones[:, :n].transpose(1, 2), gl,
+                          beta=sink.beta, alpha=sink.alpha * inv, out=gb)
         da = ops.fa_head_bwd(dfeat, codes, a.shape[2], a.shape[3])
         # ---- blocks, last to first
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -687,21 +707,32 @@ class ResNet9FedAvg(ResNet18FedAvg):
         y3 = ops.fa_ew(p3, s2, 0)
         # ---- head: 4x4 max-pool (y3 >= 0: the ReLU is the identity) -> per-client
         # fp32 features -> logits = 0.125 feat Wl^T (batched on the weight rows)
-        f16, c4 = ops.relu_maxpool(y3, 4)  # [n, G*512, 1, 1]
+        f16, c4 = ops.relu_maxpool(y3, 4)  # [n, G*512, 1, 1]: (example, client, feature)
         F_ = self.feat
-        feat = f16.view(n, G, F_).transpose(0, 1).float()  # [G, n, F]
-        Wl = self._rows(W, ld, G, self.fc_w, self.ncls, F_)
-        logits = torch.bmm(feat, Wl.transpose(1, 2)).mul_(self.scale)
-        loss, correct, gl = ops.ce_fwd(logits.reshape(G * n, self.ncls), y)
-        gl = gl.view(G, n, self.ncls)
-        a = self.scale / n
-        dfeat = torch.bmm(gl, Wl).mul_(a)  # (read before the rows may be updated in place)
-        gW = sink.dst[:, self.fc_w:self.fc_w + self.ncls * F_].view(G, self.ncls, F_)
-        torch.baddbmm(sink.src_rows(self.fc_w, self.ncls, F_), gl.transpose(1, 2), feat, beta=sink.beta,
-                      alpha=sink.alpha * a, out=gW)  # (the classifier reads the fp32 rows: no mirror)
-        dy3 = ops.relu_maxpool_backward(
-            dfeat.transpose(0, 1).reshape(n, G * F_, 1, 1).to(torch.bfloat16).contiguous(
-                memory_format=torch.channels_last), c4, 4)
+        if self._fused_head_ok(n, F_):
+            # classifier + loss + feature gradient + the rows' SGD step in one
+            # kernel per client, the features read / their gradient written in
+            # the channel-stacked bf16 layout (the classifier reads the fp32
+            # rows: no mirror)
+            df16 = torch.empty_like(f16)
+            loss, correct = ops.fa_linear_ce(f16, F_, G * F_, G, n, W, ld, self.fc_w, -1, self.ncls, F_,
+                                             self.scale, y, df16, F_, G * F_, sink.dst, sink.ld, sink.beta,
+                                             sink.alpha, sink.src, sink.sld, None, 0)
+            dy3 = ops.relu_maxpool_backward(df16, c4, 4)
+        else:
+            feat = f16.view(n, G, F_).transpose(0, 1).float()  # [G, n, F]
+            Wl = self._rows(W, ld, G, self.fc_w, self.ncls, F_)
+            logits = torch.bmm(feat, Wl.transpose(1, 2)).mul_(self.scale)
+            loss, correct, gl = ops.ce_fwd(logits.reshape(G * n, self.ncls), y)
+            gl = gl.view(G, n, self.ncls)
+            a = self.scale / n
+            dfeat = torch.bmm(gl, Wl).mul_(a)  # (read before the rows may be updated in place)
+            gW = sink.dst[:, self.fc_w:self.fc_w + self.ncls * F_].view(G, self.ncls, F_)
+            torch.baddbmm(sink.src_rows(self.fc_w, self.ncls, F_), gl.transpose(1, 2), feat, beta=sink.beta,
+                          alpha=sink.alpha * a, out=gW)  # (the classifier reads the fp32 rows: no mirror)
+            dy3 = ops.relu_maxpool_backward(
+                dfeat.transpose(0, 1).reshape(n, G * F_, 1, 1).to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last), c4, 4)
 
         def back(dy, xin, key, addend=None):
             off, C, K = cv[key]

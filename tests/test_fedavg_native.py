@@ -442,6 +442,61 @@ def test_implicit_strided_column_image(C, K, H, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout,bias,shared,n,C", [("client", True, False, 5, 100), ("client", True, True, 7, 10),
+                                                    ("stacked", False, False, 5, 10), ("stacked", False, True, 32, 100)])
+def test_fa_linear_ce_matches_fp32(layout, bias, shared, n, C):
+    """The per-client classifier step in one kernel (fedavg.hip fa_linear_ce):
+    per-example loss / top-1, the feature gradient with the step's weights and
+    the SGD-updated classifier rows (+ bias) vs an fp32 reference; features
+    client-major fp32 ([G, n, F]) or channel-stacked bf16 ([n, G F]), weights
+    per client or the shared server row (ld 0) updated into client rows."""
+    torch.manual_seed(3)
+    G, F = 6, 512
+    scale = 1.0 if bias else 0.125
+    per = C * F + C
+    ld = per + 40
+    boff = C * F + 3 if bias else -1
+    woff = 3 if bias else 0
+    Wsrc = torch.randn(ld if shared else G * ld, device="cuda") * 0.05
+    wld = 0 if shared else ld
+    if layout == "client":
+        feat = torch.randn(G, n, F, device="cuda").relu()
+        fsg, fsn = n * F, F
+        ff = feat
+    else:
+        feat = torch.randn(n, G * F, device="cuda").relu().to(torch.bfloat16)
+        fsg, fsn = F, G * F
+        ff = feat.float().view(n, G, F).transpose(0, 1)
+    y = torch.randint(0, C, (G * n,), device="cuda")
+    dst = torch.full((G, ld), float("nan"), device="cuda")
+    beta, alpha = 1.0 - 0.05 * 5e-4, -0.05
+    # client-major fp32 features: 32-class chunks with partial feature-gradient slabs
+    S = -(-C // 32) if layout == "client" else 1
+    dfeat = torch.empty((S * feat.shape[0],) + tuple(feat.shape[1:]), device="cuda", dtype=feat.dtype)
+    loss, correct = _ops().fa_linear_ce(feat, fsg, fsn, G, n, Wsrc, wld, woff, boff, C, F, scale, y, dfeat,
+                                        fsg, fsn, dst, ld, beta, alpha, Wsrc, wld, None, 0,
+                                        feat.numel() if S > 1 else 0, 32 if S > 1 else 0)
+    dfeat = dfeat.view(S, *feat.shape).sum(0)
+    rows = Wsrc.view(1, ld).expand(G, ld) if shared else Wsrc.view(G, ld)
+    Wg = rows[:, woff:woff + C * F].view(G, C, F)
+    bg = rows[:, boff:boff + C] if bias else torch.zeros(G, C, device="cuda")
+    logits = scale * torch.bmm(ff, Wg.transpose(1, 2)) + bg[:, None, :]
+    ref_loss = torch.nn.functional.cross_entropy(logits.reshape(G * n, C), y, reduction="none")
+    torch.testing.assert_close(loss, ref_loss, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(correct, (logits.reshape(G * n, C).argmax(1) == y).float())
+    gl = torch.softmax(logits, -1) - torch.nn.functional.one_hot(y.view(G, n), C).float()
+    ref_df = torch.bmm(gl, Wg) * (scale / n)
+    got_df = dfeat.float() if layout == "client" else dfeat.float().view(n, G, F).transpose(0, 1)
+    tol = 1e-4 if layout == "client" else 1e-2
+    torch.testing.assert_close(got_df, ref_df, rtol=tol, atol=tol * ref_df.abs().max().item())
+    ref_w = beta * Wg + alpha * (scale / n) * torch.bmm(gl.transpose(1, 2), ff)
+    torch.testing.assert_close(dst[:, woff:woff + C * F].view(G, C, F), ref_w, rtol=1e-5, atol=1e-6)
+    if bias:
+        ref_b = beta * bg + alpha / n * gl.sum(1)
+        torch.testing.assert_close(dst[:, boff:boff + C], ref_b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
 def test_ew_add_relu():
     a = torch.randn(2, 64, 4, 4, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     b = torch.randn_like(a)
