@@ -631,7 +631,7 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
   g.N = static_cast<int>(N);
   g.T = static_cast<int>(P);
   g.G = static_cast<int>(G);
-  g.splits = 1;  // G clients x tiles: the chip is full without split-K
+  g.splits = 1;  // G clients x tiles: the chip is usually full without split-K
   g.beta = static_cast<float>(beta);
   g.alpha = static_cast<float>(alpha);
   g.mirror = mp;
@@ -659,7 +659,34 @@ bool fa_bmm_rows(const at::Tensor& A, const at::Tensor& B, at::Tensor dst, int64
     g.stage = 0;
     g.small = 1;
   }
-  launch_gemm_tn_acc(g, stream_now());
+  // few tiles over long K (the stem's [64 x 27] per client over 5,120 pixels:
+  // G one-tile blocks of 80 K-steps): split K over the free slots, fp32 slabs,
+  // then the reduction applies the SGD step (src / beta / alpha) and the mirror
+  at::Tensor slab;
+  {
+    static int cus = 0;
+    if (cus == 0) {
+      hipDeviceProp_t prop;
+      int dev = 0;
+      cus = 256;
+      if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+        cus = prop.multiProcessorCount;
+    }
+    const bool sm = g.small > 0 || (g.small < 0 && (K % 256 != 0 || N % 256 != 0));
+    const int64_t t = sm ? 128 : 256, slots = static_cast<int64_t>(cus) * (sm ? 2 : 1);
+    const int64_t blocks = G * ((K + t - 1) / t) * ((N + t - 1) / t);
+    const int64_t steps = (P + 63) / 64;
+    if (2 * blocks <= slots && (N * K) % 4 == 0 && (ld % 4) == 0) {
+      int64_t s = slots / blocks;
+      if (s > steps / 4) s = steps / 4;
+      if (s > 1) {
+        slab = at::empty({G * s, K, N}, A.options().dtype(at::kFloat));
+        g.slab = slab.data_ptr<float>();
+        g.splits = static_cast<int>(s);
+      }
+    }
+  }
+  launch_gemm_tn_acc(g, stream_now());  // (slab: stream-ordered reuse after this call)
   return true;
 }
 

@@ -317,7 +317,8 @@ __global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__
                                                              const float* __restrict__ slab, int M,
                                                              int N, int splits, int G, int64_t cg,
                                                              float beta, float alpha,
-                                                             uint16_t* __restrict__ mirror, int64_t mcg) {
+                                                             uint16_t* __restrict__ mirror, int64_t mcg,
+                                                             const float* __restrict__ src, int64_t scg) {
   const int64_t plane = static_cast<int64_t>(M) * N;
   const int64_t n4 = G * plane / 4;
   for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < n4;
@@ -336,7 +337,11 @@ __global__ void __launch_bounds__(256) gemm_tn_reduce_kernel(float* __restrict__
       s.w += v.w;
     }
     float4* c = reinterpret_cast<float4*>(C + g * cg + static_cast<int64_t>(m) * ldc + n);
-    float4 cv = *c;
+    // (src: beta scales those rows instead of C's -- the FedAvg engine's first
+    // local step reads the server row)
+    float4 cv = src != nullptr && !(beta == 1.f && alpha == 1.f)
+                    ? *reinterpret_cast<const float4*>(src + g * scg + static_cast<int64_t>(m) * ldc + n)
+                    : *c;
     if (beta == 1.f && alpha == 1.f) {
       cv.x += s.x;
       cv.y += s.y;
@@ -404,7 +409,8 @@ void launch_gemm_tn_acc(GemmTnArgs a, hipStream_t stream) {
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 2048) blocks = 2048;
     COMMEFF_LAUNCH(gemm_tn_reduce_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, stream,
-                       a.C, a.ldc, a.slab, a.M, a.N, a.splits, a.G, a.cg, a.beta, a.alpha, a.mirror, a.mcg);
+                       a.C, a.ldc, a.slab, a.M, a.N, a.splits, a.G, a.cg, a.beta, a.alpha, a.mirror, a.mcg,
+                       a.src, a.scg);
   }
 }
 

@@ -256,6 +256,8 @@ class ResNet18FedAvg:
     def _fused_head_ok(self, n: int, F: int) -> bool:
         return self._FUSED_HEAD[0] and n <= 32 and n * (F + self.ncls) * 4 <= 96 * 1024
 
+    # the stem's [64 x 27] weight updates on the TN GEMM too (COMMEFF_FA_STEM=blas: hipBLASLt)
+    _STEM_TN = [os.environ.get("COMMEFF_FA_STEM", "tn") == "tn"]
     _BMM_INTO = [True]
     # (128-channel input gradients from the rows themselves: 29.72 vs 30.53 ms
     # per round with the per-step flipped images, same-box A/B)
@@ -276,7 +278,8 @@ class ResNet18FedAvg:
         # (the stem's 27 columns stay on hipBLASLt: its [64 x 27] products over
         # 5,120 pixels are 100 one-tile blocks of 80 K-steps on the TN GEMM --
         # 31.43 vs 31.15 ms per round, same-box A/B)
-        if cls._TN[0] and n % 8 == 0 and _ops().fa_bmm_rows(A, B, sink.dst, sink.ld, off, sink.beta, sink.alpha, sink.mirror,
+        if cls._TN[0] and (n % 8 == 0 or cls._STEM_TN[0]) and _ops().fa_bmm_rows(
+                A, B, sink.dst, sink.ld, off, sink.beta, sink.alpha, sink.mirror,
                                              cls._TN[1], sink.src, sink.sld):
             return
         dst = sink.dst[:, off:off + K * n].view(G, K, n)

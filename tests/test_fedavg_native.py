@@ -326,7 +326,9 @@ def test_conv3x3_wgrad_rows_rsc_order(G, C, K, H):
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,N,Nfull,o,P,small", [(256, 2304, 2304, 0, 80, -1), (64, 64, 576, 256, 320, -1),
                                                  (512, 2304, 2304, 0, 17, 1), (128, 1152, 1152, 0, 200, 0),
-                                                 (72, 136, 136, 0, 50, 1), (64, 27, 32, 0, 300, 1)])
+                                                 (72, 136, 136, 0, 50, 1), (64, 27, 32, 0, 300, 1),
+                                                 # split-K (few tiles over long K) + the reduction's SGD step
+                                                 (64, 27, 32, 0, 5120, 1), (128, 1152, 1152, 0, 2048, 0)])
 def test_fa_bmm_rows_sgd_and_mirror(K, N, Nfull, o, P, small):
     """TN GEMM over channel-stacked operands into client rows: rows = beta rows
     + alpha A_g B_g with the bf16 mirror from the epilogue (fp32 reference)"""
