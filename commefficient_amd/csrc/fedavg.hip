@@ -500,6 +500,124 @@ __global__ void __launch_bounds__(256) fa_linear_kernel(FaLinearArgs a, const fl
   }
 }
 
+// ------------------------------------------------------------ Fixup scalars
+// Per-client scalar affine maps of the Fixup models (models/fixup.py: x + b,
+// x * s + b, relu, + residual), the scalars read from the clients' fp32 rows
+// (W[g * ld + off]; off < 0: none).  Activations bf16, channel-stacked
+// ([pixels][G C]: group of element e = (e mod G C) / C) or client-major (the
+// stem's input: group = e / per); 8 elements a thread, one group each.
+__device__ __forceinline__ int64_t fa_mem(const FaAffine& a, int g, int64_t eg) {
+  // element eg of group g -> memory offset
+  if (a.C > 0) {
+    const int64_t p = eg / a.C;
+    return p * a.GC + static_cast<int64_t>(g) * a.C + (eg - p * a.C);
+  }
+  return static_cast<int64_t>(g) * a.per + eg;
+}
+
+__global__ void __launch_bounds__(256) fa_affine_kernel(FaAffine a) {
+  const int64_t n8 = a.G * a.per / 8;
+  for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < n8; q += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t e = q * 8;
+    const int g = a.C > 0 ? static_cast<int>((e % a.GC) / a.C) : static_cast<int>(e / a.per);
+    const float sc = a.soff >= 0 ? a.W[g * a.ld + a.soff] : 1.f;
+    const float bi = a.boff >= 0 ? a.W[g * a.ld + a.boff] : 0.f;
+    const u4 xv = *reinterpret_cast<const u4*>(a.x + e);
+    u4 av = {0u, 0u, 0u, 0u};
+    if (a.add != nullptr) av = *reinterpret_cast<const u4*>(a.add + e);
+    u4 o;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      float v0 = fmaf(__uint_as_float(xv[h] << 16), sc, bi), v1 = fmaf(__uint_as_float(xv[h] & 0xffff0000u), sc, bi);
+      if (a.add != nullptr) {
+        v0 += __uint_as_float(av[h] << 16);
+        v1 += __uint_as_float(av[h] & 0xffff0000u);
+      }
+      if (a.relu) {
+        v0 = fmaxf(v0, 0.f);
+        v1 = fmaxf(v1, 0.f);
+      }
+      o[h] = static_cast<uint32_t>(f2bf(v0)) | (static_cast<uint32_t>(f2bf(v1)) << 16);
+    }
+    *reinterpret_cast<u4*>(a.y + e) = o;
+  }
+}
+
+// backward: dpre = dy (masked by y > 0 with relu), out1 = dpre * s (+ add2),
+// out2 = dpre; block (chunk, g) sums dpre and dpre * xs (no xs: dy itself,
+// unmasked) over its elements of group g (fixed-order tree):
+// part[(chunk * G + g) * 2 + {0, 1}]
+__global__ void __launch_bounds__(256) fa_affine_bwd_kernel(FaAffine a, FaAffineBwd b) {
+  __shared__ float red[2][256];
+  const int g = blockIdx.y, tid = threadIdx.x;
+  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * b.chunk;
+  const int64_t e1 = min(e0 + b.chunk, a.per);
+  const float sc = a.soff >= 0 ? a.W[g * a.ld + a.soff] : 1.f;
+  float s1 = 0.f, s2 = 0.f;
+  for (int64_t eg = e0 + 8 * tid; eg < e1; eg += 8 * 256) {
+    const int64_t m = fa_mem(a, g, eg);
+    const u4 dv = *reinterpret_cast<const u4*>(b.dy + m);
+    u4 yv = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu}, xv = {0u, 0u, 0u, 0u}, av = {0u, 0u, 0u, 0u};
+    if (b.yrelu != nullptr) yv = *reinterpret_cast<const u4*>(b.yrelu + m);
+    if (b.xs != nullptr) xv = *reinterpret_cast<const u4*>(b.xs + m);
+    if (b.add2 != nullptr) av = *reinterpret_cast<const u4*>(b.add2 + m);
+    u4 o1, o2;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      float d[2] = {__uint_as_float(dv[h] << 16), __uint_as_float(dv[h] & 0xffff0000u)};
+      if (b.xs == nullptr) s2 += d[0] + d[1];  // (no scale input: the second sum is of dy unmasked)
+      if (b.yrelu != nullptr) {  // relu'(pre) from the output: y > 0
+        if (!(__uint_as_float(yv[h] << 16) > 0.f)) d[0] = 0.f;
+        if (!(__uint_as_float(yv[h] & 0xffff0000u) > 0.f)) d[1] = 0.f;
+      }
+      s1 += d[0] + d[1];
+      if (b.xs != nullptr)
+        s2 = fmaf(d[0], __uint_as_float(xv[h] << 16), fmaf(d[1], __uint_as_float(xv[h] & 0xffff0000u), s2));
+      float r0 = d[0] * sc, r1 = d[1] * sc;
+      if (b.add2 != nullptr) {
+        r0 += __uint_as_float(av[h] << 16);
+        r1 += __uint_as_float(av[h] & 0xffff0000u);
+      }
+      o1[h] = static_cast<uint32_t>(f2bf(r0)) | (static_cast<uint32_t>(f2bf(r1)) << 16);
+      o2[h] = static_cast<uint32_t>(f2bf(d[0])) | (static_cast<uint32_t>(f2bf(d[1])) << 16);
+    }
+    if (b.out1 != nullptr) *reinterpret_cast<u4*>(b.out1 + m) = o1;
+    if (b.out2 != nullptr) *reinterpret_cast<u4*>(b.out2 + m) = o2;
+  }
+  red[0][tid] = s1;
+  red[1][tid] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[0][tid] += red[0][tid + o];
+      red[1][tid] += red[1][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    b.part[(static_cast<int64_t>(blockIdx.x) * a.G + g) * 2] = red[0][0];
+    b.part[(static_cast<int64_t>(blockIdx.x) * a.G + g) * 2 + 1] = red[1][0];
+  }
+}
+
+// the scalars' SGD step: grad = sum over the chunks in order; dst[boff] (the
+// bias: sum dpre) / dst[soff] (the scale: sum dpre x) = beta src + alpha grad
+__global__ void __launch_bounds__(256) fa_scalar_sgd_kernel(const float* __restrict__ part, int chunks, int G,
+                                                            float* __restrict__ dst, int64_t ld, int64_t boff,
+                                                            int64_t soff, float beta, float alpha,
+                                                            const float* __restrict__ src, int64_t sld) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= G) return;
+  float t1 = 0.f, t2 = 0.f;
+  for (int c = 0; c < chunks; ++c) {
+    t1 += part[(static_cast<int64_t>(c) * G + g) * 2];
+    t2 += part[(static_cast<int64_t>(c) * G + g) * 2 + 1];
+  }
+  const float* sr = src != nullptr ? src + g * sld : dst + g * ld;
+  if (boff >= 0) dst[g * ld + boff] = beta != 0.f ? beta * sr[boff] + alpha * t1 : alpha * t1;
+  if (soff >= 0) dst[g * ld + soff] = beta != 0.f ? beta * sr[soff] + alpha * t2 : alpha * t2;
+}
+
 }  // namespace
 
 void launch_weight_image(const float* W, int64_t ld, int G, int K, int C, int RS, int Kc, int kind,
@@ -615,6 +733,24 @@ void launch_fa_linear_ce(FaLinearArgs a, int G, bool feat_bf16, bool dfeat_bf16,
   if (a.n <= 8) fa_linear_launch<8>(a, G, feat_bf16, dfeat_bf16, logits, stream);
   else if (a.n <= 16) fa_linear_launch<16>(a, G, feat_bf16, dfeat_bf16, logits, stream);
   else fa_linear_launch<kFaMaxN>(a, G, feat_bf16, dfeat_bf16, logits, stream);
+}
+
+void launch_fa_affine(const FaAffine& a, hipStream_t stream) {
+  const int64_t n8 = a.G * a.per / 8;
+  if (n8 == 0) return;
+  COMMEFF_LAUNCH(fa_affine_kernel, dim3(grid_for(n8)), dim3(256), 0, stream, a);
+}
+
+void launch_fa_affine_bwd(const FaAffine& a, const FaAffineBwd& b, int chunks, hipStream_t stream) {
+  if (a.G == 0 || chunks == 0) return;
+  COMMEFF_LAUNCH(fa_affine_bwd_kernel, dim3(chunks, a.G), dim3(256), 0, stream, a, b);
+}
+
+void launch_fa_scalar_sgd(const float* part, int chunks, int G, float* dst, int64_t ld, int64_t boff, int64_t soff,
+                          float beta, float alpha, const float* src, int64_t sld, hipStream_t stream) {
+  if (G == 0) return;
+  COMMEFF_LAUNCH(fa_scalar_sgd_kernel, dim3((G + 255) / 256), dim3(256), 0, stream, part, chunks, G, dst, ld, boff,
+                 soff, beta, alpha, src, sld);
 }
 
 }  // namespace commeff

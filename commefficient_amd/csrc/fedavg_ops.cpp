@@ -9,6 +9,8 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace commeff {
@@ -323,6 +325,118 @@ std::tuple<at::Tensor, at::Tensor> fa_linear_ce(const at::Tensor& feat, int64_t 
   launch_fa_linear_ce(a, static_cast<int>(G), feat.scalar_type() == at::kBFloat16,
                       dfeat.scalar_type() == at::kBFloat16, logits.data_ptr<float>(), stream_now());
   return {loss, correct};
+}
+
+// ---- Fixup per-client scalars (fedavg.hip fa_affine*): x channel-stacked
+// [n, G C, H, W] bf16 channels_last, or client-major (client_major: the
+// stem's input [G n, C, H, W], any C)
+static FaAffine affine_args(const at::Tensor& x, int64_t G, bool client_major, const at::Tensor& W, int64_t ld,
+                            int64_t soff, int64_t boff, const char* what) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && G >= 1, what, ": bf16 4-D x");
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && ld >= 0 &&
+                  (G - 1) * ld + std::max(soff, boff) < W.numel(),
+              what, ": scalar rows");
+  FaAffine a{};
+  a.G = static_cast<int>(G);
+  a.W = W.data_ptr<float>();
+  a.ld = ld;
+  a.soff = soff;
+  a.boff = boff;
+  if (client_major) {
+    TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) || x.is_contiguous(), what, ": dense x");
+    TORCH_CHECK(x.numel() % (8 * G) == 0 && (x.numel() / G) % 8 == 0, what, ": 8-element client blocks");
+    a.per = x.numel() / G;
+    a.C = 0;
+    a.GC = 0;
+  } else {
+    check_cl_bf16(x, what);
+    const int64_t GC = x.size(1);
+    TORCH_CHECK(GC % G == 0 && (GC / G) % 8 == 0, what, ": G | channels, 8 | channels per client");
+    a.C = static_cast<int>(GC / G);
+    a.GC = GC;
+    a.per = x.numel() / G;
+  }
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, what, ": 16-byte aligned x");
+  return a;
+}
+
+// y = relu?(x * s_g + b_g (+ add))
+at::Tensor fa_affine(const at::Tensor& x, int64_t G, bool client_major, const at::Tensor& W, int64_t ld, int64_t soff,
+                     int64_t boff, const c10::optional<at::Tensor>& add, bool relu) {
+  FaAffine a = affine_args(x, G, client_major, W, ld, soff, boff, "fa_affine");
+  auto y = at::empty_like(x);
+  if (add.has_value() && add->defined()) {
+    TORCH_CHECK(add->sizes() == x.sizes() && add->strides() == x.strides() && add->scalar_type() == at::kBFloat16,
+                "fa_affine: add like x");
+    a.add = bf(*add);
+  }
+  a.x = bf(x);
+  a.y = bfw(y);
+  a.relu = relu ? 1 : 0;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  launch_fa_affine(a, stream_now());
+  return y;
+}
+
+// (out1 = dpre * s (+ add2) or undefined, out2 = dpre or undefined, partial sums [chunks, G, 2])
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_affine_bwd(const at::Tensor& dy, int64_t G, bool client_major,
+                                                             const at::Tensor& W, int64_t ld, int64_t soff,
+                                                             const c10::optional<at::Tensor>& yrelu,
+                                                             const c10::optional<at::Tensor>& xs,
+                                                             const c10::optional<at::Tensor>& add2, bool want1,
+                                                             bool want2) {
+  FaAffine a = affine_args(dy, G, client_major, W, ld, soff, -1, "fa_affine_bwd");
+  FaAffineBwd b{};
+  b.dy = bf(dy);
+  auto same = [&](const c10::optional<at::Tensor>& t, const char* nm) -> const uint16_t* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->sizes() == dy.sizes() && t->strides() == dy.strides() && t->scalar_type() == at::kBFloat16,
+                "fa_affine_bwd: ", nm, " like dy");
+    return bf(*t);
+  };
+  b.yrelu = same(yrelu, "y");
+  b.xs = same(xs, "xs");
+  b.add2 = same(add2, "add2");
+  at::Tensor o1, o2;
+  if (want1) {
+    o1 = at::empty_like(dy);
+    b.out1 = bfw(o1);
+  }
+  if (want2) {
+    o2 = at::empty_like(dy);
+    b.out2 = bfw(o2);
+  }
+  // chunks of ~8 K elements per block, at least one block per client
+  b.chunk = 8192;
+  const int64_t chunks = (a.per + b.chunk - 1) / b.chunk;
+  auto part = at::empty({chunks, G, 2}, dy.options().dtype(at::kFloat));
+  b.part = part.data_ptr<float>();
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  launch_fa_affine_bwd(a, b, static_cast<int>(chunks), stream_now());
+  return {o1, o2, part};
+}
+
+// dst[g ld + boff] / dst[g ld + soff] = beta src + alpha (sum of the partials' dpre / dpre x)
+void fa_scalar_sgd(const at::Tensor& part, at::Tensor dst, int64_t ld, int64_t boff, int64_t soff, double beta,
+                   double alpha, const c10::optional<at::Tensor>& src, int64_t sld) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 &&
+                  part.size(2) == 2,
+              "fa_scalar_sgd: part fp32 [chunks, G, 2]");
+  const int64_t G = part.size(1);
+  TORCH_CHECK(dst.scalar_type() == at::kFloat && dst.is_contiguous() && ld >= 0 &&
+                  (G - 1) * ld + std::max(boff, soff) < dst.numel(),
+              "fa_scalar_sgd: dst rows");
+  const float* sp = nullptr;
+  if (src.has_value() && src->defined()) {
+    TORCH_CHECK(src->scalar_type() == at::kFloat && src->is_contiguous() && sld >= 0 &&
+                    (G - 1) * sld + std::max(boff, soff) < src->numel(),
+                "fa_scalar_sgd: src rows");
+    sp = src->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
+  launch_fa_scalar_sgd(part.data_ptr<float>(), static_cast<int>(part.size(0)), static_cast<int>(G),
+                       dst.data_ptr<float>(), ld, boff, soff, static_cast<float>(beta), static_cast<float>(alpha), sp,
+                       sld, stream_now());
 }
 
 at::Tensor fa_head_bwd(const at::Tensor& df, const at::Tensor& codes, int64_t H, int64_t W) {
@@ -779,6 +893,12 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_linear_ce(Tensor feat, int fsg, int fsn, int G, int n, Tensor W, int wld, int woff, int boff, int C, "
         "int F, float scale, Tensor y, Tensor(a!) dfeat, int dsg, int dsn, Tensor(b!) dst, int dld, float beta, "
         "float alpha, Tensor? src, int sld, Tensor(c!)? mirror, int mld, int dss=0, int ccs=0) -> (Tensor, Tensor)");
+  m.def("fa_affine(Tensor x, int G, bool client_major, Tensor W, int ld, int soff, int boff, Tensor? add, "
+        "bool relu) -> Tensor");
+  m.def("fa_affine_bwd(Tensor dy, int G, bool client_major, Tensor W, int ld, int soff, Tensor? yrelu, "
+        "Tensor? xs, Tensor? add2, bool want1, bool want2) -> (Tensor, Tensor, Tensor)");
+  m.def("fa_scalar_sgd(Tensor part, Tensor(a!) dst, int ld, int boff, int soff, float beta, float alpha, "
+        "Tensor? src, int sld) -> ()");
   m.def("fa_head_fwd(Tensor x, int G) -> (Tensor, Tensor)");
   m.def("fa_head_bwd(Tensor df, Tensor codes, int H, int W) -> Tensor");
   m.def("fa_ew(Tensor a, Tensor? b, int mode) -> Tensor");
@@ -806,6 +926,9 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("fa_bcast_rows", &fa_bcast_rows);
   m.impl("fa_cast_rows", &fa_cast_rows);
   m.impl("fa_linear_ce", &fa_linear_ce);
+  m.impl("fa_affine", &fa_affine);
+  m.impl("fa_affine_bwd", &fa_affine_bwd);
+  m.impl("fa_scalar_sgd", &fa_scalar_sgd);
   m.impl("fa_dgrad_image", &fa_dgrad_image);
   m.impl("conv3x3_fwd_rows", &conv3x3_fwd_rows);
   m.impl("fa_head_fwd", &fa_head_fwd);

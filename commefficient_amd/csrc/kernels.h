@@ -620,6 +620,31 @@ struct FaLinearArgs {
 };
 int64_t fa_linear_lds_bytes(int n, int C, int F);
 void launch_fa_linear_ce(FaLinearArgs a, int G, bool feat_bf16, bool dfeat_bf16, float* logits, hipStream_t stream);
+// batched FedAvg per-client scalar affine maps of the Fixup models (fedavg.hip)
+struct FaAffine {
+  const uint16_t* x;      // bf16 activations
+  const uint16_t* add;    // + residual (nullptr: none)
+  uint16_t* y;
+  const float* W;         // client rows: scale at g * ld + soff, bias at + boff (< 0: none)
+  int64_t ld, soff, boff;
+  int64_t per;            // elements per client
+  int64_t GC;             // channel-stacked: G C channels a pixel (0 with C = 0: client-major)
+  int G, C, relu;
+};
+struct FaAffineBwd {
+  const uint16_t* dy;
+  const uint16_t* yrelu;  // the forward output (relu mask), nullptr: no relu
+  const uint16_t* xs;     // the scale's input (its gradient sum dpre x), nullptr: sum dy (unmasked) instead
+  const uint16_t* add2;   // + this to out1 (nullptr: none)
+  uint16_t* out1;         // dpre * s (+ add2), nullptr: not written
+  uint16_t* out2;         // dpre, nullptr: not written
+  float* part;            // [chunks][G][2] sums of dpre, dpre x
+  int64_t chunk;          // elements per block
+};
+void launch_fa_affine(const FaAffine& a, hipStream_t stream);
+void launch_fa_affine_bwd(const FaAffine& a, const FaAffineBwd& b, int chunks, hipStream_t stream);
+void launch_fa_scalar_sgd(const float* part, int chunks, int G, float* dst, int64_t ld, int64_t boff, int64_t soff,
+                          float beta, float alpha, const float* src, int64_t sld, hipStream_t stream);
 bool gemm_supported(int M, int N, int K, bool nn);
 bool gemm_supported_nedge(int M, int N, int K);
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);

@@ -759,11 +759,202 @@ class ResNet9FedAvg(ResNet18FedAvg):
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
 
 
+class FixupResNet9FedAvg(ResNet9FedAvg):
+    """Explicit G-client forward / backward / local SGD of models.fixup.FixupResNet9
+    (reference /root/reference/CommEfficient/models/fixup_resnet9.py:33-91):
+    ResNet9FedAvg's convolutions, pools and classifier, plus the per-client
+    Fixup scalars (``x + b`` before each conv, ``conv * s + b`` after) on the
+    native affine kernels (fedavg.hip fa_affine / fa_affine_bwd): the
+    scalars are read from the clients' fp32 rows, their gradients are
+    fixed-order per-client sums written by ``fa_scalar_sgd`` with the step's
+    SGD update.  The stem's input bias gradient is the sum of the stem's
+    column-image gradient over the in-image taps (the im2col of ones)."""
+
+    @staticmethod
+    def supported(model, args) -> Tuple[bool, str]:
+        from ..models.fixup import FixupResNet9
+        if not isinstance(model, FixupResNet9):
+            return False, "not the FixupResNet9 of models/fixup.py"
+        if getattr(args, "dtype", "bf16") != "bf16":
+            return False, "bf16 compute only"
+        pools = [model.layer1.pool, model.layer2.pool, model.layer3.pool, model.pool]
+        if not all(isinstance(q, torch.nn.MaxPool2d) for q in pools):
+            return False, "FixupResNet9 pools of another form"
+        ks = [q.kernel_size if isinstance(q.kernel_size, int) else q.kernel_size[0] for q in pools]
+        if ks != [2, 2, 2, 4] or len(model.layer2.blocks) != 0 or len(model.layer1.blocks) != 1 \
+                or len(model.layer3.blocks) != 1 or model.linear.bias is None:
+            return False, "FixupResNet9 of another topology"
+        if any(c % 64 for c in (model.channels[k] for k in ("prep", "layer1", "layer2", "layer3"))):
+            return False, "channel counts must be multiples of 64"
+        for p in model.parameters():
+            if not p.requires_grad:
+                return False, "frozen parameters"
+        return True, ""
+
+    def __init__(self, model, flat, names: List[str]):
+        self.model = model
+        off = {nm: int(o) for nm, o in zip(names, flat.offsets)}
+        self.d = int(flat.d) if hasattr(flat, "d") else int(sum(flat.numels))
+        self.off = off
+        self.prep = off["conv1.weight"]
+        self.c0 = model.conv1.out_channels
+        self.cin0 = model.conv1.in_channels
+        self.blocks = []  # (no BatchNorm)
+        self.conv = {}
+        for key, mod in (("layer1", model.layer1.conv), ("layer1.b1", model.layer1.blocks[0].conv1),
+                         ("layer1.b2", model.layer1.blocks[0].conv2), ("layer2", model.layer2.conv),
+                         ("layer3", model.layer3.conv), ("layer3.b1", model.layer3.blocks[0].conv1),
+                         ("layer3.b2", model.layer3.blocks[0].conv2)):
+            wname = {"layer1": "layer1.conv.weight", "layer1.b1": "layer1.blocks.0.conv1.weight",
+                     "layer1.b2": "layer1.blocks.0.conv2.weight", "layer2": "layer2.conv.weight",
+                     "layer3": "layer3.conv.weight", "layer3.b1": "layer3.blocks.0.conv1.weight",
+                     "layer3.b2": "layer3.blocks.0.conv2.weight"}[key]
+            self.conv[key] = (off[wname], mod.in_channels, mod.out_channels)
+        self.fc_w = off["linear.weight"]
+        self.fc_b = off["linear.bias"]
+        self.ncls = model.linear.out_features
+        self.feat = model.linear.in_features
+        self.scale = 1.0
+        self.sc = {k: v for k, v in off.items() if k.endswith(("bias1a", "bias1b", "bias2a", "bias2b", "scale"))
+                   or k == "bias2"}
+
+    def _ones_col(self, x, G, Kc0):
+        """im2col of an all-ones image of x's geometry: 1 at the in-image taps."""
+        key = (tuple(x.shape), G, Kc0, x.device)
+        if getattr(self, "_ones_key", None) != key:
+            ones = torch.ones_like(x)
+            c = _ops().im2col_grouped(ones, G, 3, 3, 1, 1, Kc0, True)
+            n, H, Wd = x.shape[0] // G, x.shape[2], x.shape[3]
+            self._ones = c.view(n, H, Wd, G * Kc0).permute(0, 3, 1, 2)  # channel-stacked view
+            self._ones_key = key
+        return self._ones
+
+    def _step9(self, x, y, G, n, W, Wb, ld, sink):
+        ops = _ops()
+        S = self.sc
+
+        def aff(t, s=None, b=None, add=None, relu=False, cm=False):
+            return ops.fa_affine(t, G, cm, W, ld, -1 if s is None else S[s], -1 if b is None else S[b], add, relu)
+
+        def sgd(part, b=None, s=None):
+            # (b: the bias gets sum dpre; s: the scale -- or, without a scale
+            # input, the unmasked sum -- gets the second sum)
+            ops.fa_scalar_sgd(part, sink.dst, sink.ld, -1 if b is None else S[b], -1 if s is None else S[s],
+                              sink.beta, sink.alpha, sink.src, sink.sld)
+
+        def conv(xin, key):
+            off, C, K = self.conv[key]
+            return self._conv3(xin, Wb, ld, G, off, K, C)
+
+        def back(dy, xin, key):
+            off, C, K = self.conv[key]
+            dx = self._conv3_dgrad(dy, Wb, ld, G, off, K, C)
+            self._conv3_wgrad(dy, xin, G, sink, off, K, C)
+            return dx
+
+        # ---- stem: relu(conv1(x + b1a) * s + b1b) on the column image of x + b1a
+        C0, K0 = self.cin0, self.c0
+        Kc0 = (9 * C0 + 63) // 64 * 64
+        N_, _, H, Wd = x.shape
+        ps = x.stride(3)
+        if x.stride(1) == 1 and ps >= C0 and x.stride(2) == ps * Wd and x.stride(0) == ps * H * Wd:
+            # (the augmentation kernel's images: channels innermost in a wider
+            # pixel -- the affine pass runs over the whole pixels, im2col reads C0)
+            xr = torch.as_strided(x, (N_, ps, H, Wd), (x.stride(0), 1, x.stride(2), ps))
+            xa = aff(xr, b="bias1a", cm=True)[:, :C0]
+        else:
+            xa = aff(x.contiguous(memory_format=torch.channels_last), b="bias1a", cm=True)
+        col0 = ops.im2col_grouped(xa, G, 3, 3, 1, 1, Kc0, True)
+        col0g = col0.transpose(0, 1)[:, :, :9 * C0]
+        y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
+                         memory_format=torch.channels_last)
+        w0rows = self._rows(Wb, ld, G, self.prep, K0, 9 * C0)
+        pad = getattr(self, "_stem_img", None)
+        if pad is None or pad.shape != (G, K0, Kc0) or pad.device != x.device:
+            pad = self._stem_img = torch.zeros((G, K0, Kc0), device=x.device, dtype=torch.bfloat16)
+        pad[:, :, :9 * C0].copy_(w0rows)
+        if not ops.fa_gemm(col0.transpose(0, 1), pad, _gview(y0, G), False, 0.0):
+            torch.bmm(col0g, w0rows.transpose(1, 2), out=_gview(y0, G))
+        a0 = aff(y0, s="scale", b="bias1b", relu=True)
+
+        def layer(xin, name, key):  # pool(relu(conv(x + b1a) * s + b1b))
+            xa_ = aff(xin, b=f"{name}.bias1a")
+            h = conv(xa_, key)
+            p, codes = ops.relu_maxpool(aff(h, s=f"{name}.scale", b=f"{name}.bias1b"), 2)
+            return (xa_, h, codes), p
+
+        def block(xin, name, k1, k2):  # relu(conv2(relu(conv1(x + b1a) + b1b) + b2a) * s + b2b + x)
+            xa_ = aff(xin, b=f"{name}.bias1a")
+            h1 = aff(conv(xa_, k1), b=f"{name}.bias1b", relu=True)
+            h1a = aff(h1, b=f"{name}.bias2a")
+            h2 = conv(h1a, k2)
+            out = aff(h2, s=f"{name}.scale", b=f"{name}.bias2b", add=xin, relu=True)
+            return (xa_, h1, h1a, h2, out), out
+
+        sv1, p1 = layer(a0, "layer1", "layer1")
+        sb1, y1 = block(p1, "layer1.blocks.0", "layer1.b1", "layer1.b2")
+        sv2, p2 = layer(y1, "layer2", "layer2")
+        sv3, p3 = layer(p2, "layer3", "layer3")
+        sb3, y3 = block(p3, "layer3.blocks.0", "layer3.b1", "layer3.b2")
+        # ---- head: 4x4 max-pool (y3 >= 0), + bias2, linear (+ bias) -> CE, one kernel pair
+        f16, c4 = ops.relu_maxpool(y3, 4)
+        F_ = self.feat
+        feat = aff(f16, b="bias2")
+        df16 = torch.empty_like(feat)
+        loss, correct = ops.fa_linear_ce(feat, F_, G * F_, G, n, W, ld, self.fc_w, self.fc_b, self.ncls, F_,
+                                         1.0, y, df16, F_, G * F_, sink.dst, sink.ld, sink.beta, sink.alpha,
+                                         sink.src, sink.sld, None, 0)
+        sgd(ops.fa_affine_bwd(df16, G, False, W, ld, -1, None, None, None, False, False)[2], b="bias2")
+        dy3 = ops.relu_maxpool_backward(df16, c4, 4)
+
+        def block_back(dy, saved, name, k1, k2):
+            xa_, h1, h1a, h2, out = saved
+            # relu(h2 s + b2b + x): dh2 = dpre s, the identity's gradient dpre
+            dh2, dpre, part = ops.fa_affine_bwd(dy, G, False, W, ld, S[f"{name}.scale"], out, h2, None, True, True)
+            sgd(part, b=f"{name}.bias2b", s=f"{name}.scale")
+            dh1a = back(dh2, h1a, k2)
+            # h1a = h1 + b2a (sum of dh1a), h1 = relu(c1 + b1b) (sum of the masked)
+            dc1, _, part = ops.fa_affine_bwd(dh1a, G, False, W, ld, -1, h1, None, None, True, False)
+            sgd(part, b=f"{name}.bias1b", s=f"{name}.bias2a")
+            dxa = back(dc1, xa_, k1)
+            # xa = x + b1a: sum of dxa; dx = dxa + the identity's gradient
+            dx, _, part = ops.fa_affine_bwd(dxa, G, False, W, ld, -1, None, None, dpre, True, False)
+            sgd(part, b=f"{name}.bias1a")
+            return dx
+
+        def layer_back(dp, xin, saved, name, key):
+            xa_, h, codes = saved
+            dhp = ops.relu_maxpool_backward(dp, codes, 2)  # (gradient of h s + b1b)
+            dh, _, part = ops.fa_affine_bwd(dhp, G, False, W, ld, S[f"{name}.scale"], None, h, None, True, False)
+            sgd(part, b=f"{name}.bias1b", s=f"{name}.scale")
+            dxa = back(dh, xa_, key)
+            sgd(ops.fa_affine_bwd(dxa, G, False, W, ld, -1, None, None, None, False, False)[2], b=f"{name}.bias1a")
+            return dxa  # (xa = x + b1a: the input's gradient is dxa itself)
+
+        dp3 = block_back(dy3, sb3, "layer3.blocks.0", "layer3.b1", "layer3.b2")
+        dp2 = layer_back(dp3, p2, sv3, "layer3", "layer3")
+        dy1 = layer_back(dp2, y1, sv2, "layer2", "layer2")
+        dp1 = block_back(dy1, sb1, "layer1.blocks.0", "layer1.b1", "layer1.b2")
+        da0 = layer_back(dp1, a0, sv1, "layer1", "layer1")
+        # ---- stem: relu(y0 s + b1b)
+        dy0, _, part = ops.fa_affine_bwd(da0, G, False, W, ld, S["scale"], a0, y0, None, True, False)
+        sgd(part, b="bias1b", s="scale")
+        # the input bias: sum of the stem's column-image gradient over the in-image taps
+        dcol = torch.empty((n, G * Kc0, H, Wd), device=x.device, dtype=torch.bfloat16,
+                           memory_format=torch.channels_last)
+        if not ops.fa_gemm(_gview(dy0, G), pad, _gview(dcol, G), True, 0.0):
+            torch.bmm(_gview(dy0, G), pad, out=_gview(dcol, G))
+        part = ops.fa_affine_bwd(dcol, G, False, W, ld, -1, None, self._ones_col(x, G, Kc0), None, False, False)[2]
+        sgd(part, s="bias1a")
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+
+
 def engine_for(model, args):
     """(engine class or None, why): the explicit G-client FedAvg program that
     covers this model / configuration."""
     why = []
-    for cls in (ResNet18FedAvg, ResNet9FedAvg):
+    for cls in (ResNet18FedAvg, ResNet9FedAvg, FixupResNet9FedAvg):
         ok, w = cls.supported(model, args)
         if ok:
             return cls, ""

@@ -34,6 +34,10 @@ def test_supported_models():
     assert not ResNet9FedAvg.supported(models.ResNet9(do_batchnorm=True), _args())[0]
     assert engine_for(models.ResNet9(), _args())[0] is ResNet9FedAvg
     assert engine_for(ResNet18(num_classes=100), _args())[0] is ResNet18FedAvg
+    from commefficient_amd.models.fixup import FixupResNet9
+    from commefficient_amd.parallel.fedavg_native import FixupResNet9FedAvg
+    assert engine_for(FixupResNet9(num_classes=10), _args())[0] is FixupResNet9FedAvg
+    assert not FixupResNet9FedAvg.supported(models.ResNet9(), _args())[0]
     assert not ResNet18FedAvg.supported(ResNet18(num_classes=10), _args(["--dtype", "fp32"]))[0]
 
 
@@ -650,3 +654,98 @@ def test_resnet9_native_round_matches_vmap_and_fp32(extra):
     assert rel < 2 * noise + 2e-2, (rel, noise)
     lnoise = (l_v - l_f).abs().max().item()
     assert (l_n - l_f).abs().max().item() <= 2 * lnoise + 3e-2 * l_f.abs().max().item(), (l_n, l_v, l_f)
+
+
+def _fixup9_perturbed():
+    """A FixupResNet9 whose zero-initialised parts (last convs, classifier,
+    scalars) are perturbed, so every gradient path is exercised."""
+    from commefficient_amd.models.fixup import FixupResNet9
+    torch.manual_seed(0)
+    m = FixupResNet9(num_classes=10)
+    g = torch.Generator().manual_seed(11)
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            if p.numel() == 1:
+                base = 1.0 if name.endswith("scale") else 0.0
+                p.fill_(base + 0.2 * torch.randn((), generator=g).item())
+            elif p.dim() == 4:
+                p.copy_(torch.randn(p.shape, generator=g) * (2.0 / (p.shape[1] * 9)) ** 0.5)
+            else:
+                p.copy_(torch.randn(p.shape, generator=g) * 0.05)
+    return m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["stacked", "client"])
+def test_fa_affine_forward_backward_and_scalar_sgd(layout):
+    """Per-client Fixup scalars (fedavg.hip fa_affine / fa_affine_bwd /
+    fa_scalar_sgd) vs torch on the same bf16 values: y = relu(x s_g + b_g +
+    add), dx = dpre s_g + add2, the per-client sums of dpre and dpre x (or of
+    dy unmasked), and the scalars' SGD step from a shared source row."""
+    torch.manual_seed(2)
+    G, n, C, H = 6, 3, 64, 8
+    ld, soff, boff = 40, 7, 13
+    W = torch.randn(G, ld, device="cuda")
+    if layout == "stacked":
+        x = torch.randn(n, G * C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        grp = lambda t: t.float().permute(0, 2, 3, 1).reshape(-1, G, C).transpose(0, 1).reshape(G, -1)  # noqa: E731
+        sv = lambda v: v.view(1, G, 1, 1, 1).expand(n, G, C, H, H).reshape(n, G * C, H, H)  # noqa: E731
+        cm = False
+    else:
+        x = torch.randn(G * n, 4, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        grp = lambda t: t.float().reshape(G, -1)  # noqa: E731
+        sv = lambda v: v.view(G, 1, 1, 1, 1).expand(G, n, 4, H, H).reshape(G * n, 4, H, H)  # noqa: E731
+        cm = True
+    add = torch.randn_like(x)
+    s_, b_ = W[:, soff], W[:, boff]
+    y = _ops().fa_affine(x, G, cm, W, ld, soff, boff, add, True)
+    ref = torch.relu(x.float() * sv(s_) + sv(b_) + add.float())
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    dy, add2 = torch.randn_like(x), torch.randn_like(x)
+    out1, out2, part = _ops().fa_affine_bwd(dy, G, cm, W, ld, soff, y, x, add2, True, True)
+    dpre = dy.float() * (y.float() > 0)
+    torch.testing.assert_close(out2.float(), dpre, rtol=0, atol=0)
+    torch.testing.assert_close(out1.float(), dpre * sv(s_) + add2.float(), rtol=1e-2, atol=2e-2)
+    sums = part.sum(0)
+    torch.testing.assert_close(sums[:, 0], grp(dpre).sum(1), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(sums[:, 1], (grp(dpre) * grp(x)).sum(1), rtol=1e-4, atol=1e-3)
+    # without the scale input the second sum is of dy unmasked
+    _, _, part2 = _ops().fa_affine_bwd(dy, G, cm, W, ld, -1, y, None, None, False, False)
+    torch.testing.assert_close(part2.sum(0)[:, 1], grp(dy).sum(1), rtol=1e-4, atol=1e-3)
+    # the SGD step into client rows from the shared server row
+    src = torch.randn(ld, device="cuda")
+    dst = torch.full((G, ld), float("nan"), device="cuda")
+    _ops().fa_scalar_sgd(part, dst, ld, boff, soff, 0.99, -0.1, src, 0)
+    torch.testing.assert_close(dst[:, boff], 0.99 * src[boff] - 0.1 * sums[:, 0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dst[:, soff], 0.99 * src[soff] - 0.1 * sums[:, 1], rtol=1e-5, atol=1e-5)
+    assert torch.isnan(dst[:, 0]).all()  # the rest of the rows untouched
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [
+    ["--fedavg_batch_size", "-1", "--num_fedavg_epochs", "2"],
+    ["--fedavg_batch_size", "2", "--num_fedavg_epochs", "1", "--weight_decay", "5e-4",
+     "--max_grad_norm", "2.0", "--fedavg_lr_decay", "0.9"],
+])
+def test_fixup_resnet9_native_round_matches_vmap_and_fp32(extra):
+    """FixupResNet9's FedAvg round on the native G-client program
+    (FixupResNet9FedAvg: the ResNet-9 kernels + per-client Fixup scalars) vs
+    the vmap composition (bf16) and the fp32 sequential path: as close to
+    fp32 as bf16 vmap is (reference models/fixup_resnet9.py, fed_worker.py:61-113)."""
+    base = _fixup9_perturbed()
+    G, n = 5, 4
+    up_n, l_n, fed = _round9(base, "native", "bf16", G, n, extra, lr=0.02)
+    assert fed._fa_native and type(fed._fa_native).__name__ == "FixupResNet9FedAvg"
+    up_v, l_v, _ = _round9(base, "vmap", "bf16", G, n, extra, lr=0.02)
+    up_f, l_f, _ = _round9(base, "vmap", "fp32", G, n, extra + ["--fedavg_batched", "off"], lr=0.02)
+    noise = ((up_v - up_f).norm() / up_f.norm()).item()
+    rel = ((up_n - up_f).norm() / up_f.norm()).item()
+    assert rel < 2 * noise + 2e-2, (rel, noise)
+    lnoise = (l_v - l_f).abs().max().item()
+    assert (l_n - l_f).abs().max().item() <= 2 * lnoise + 3e-2 * l_f.abs().max().item(), (l_n, l_v, l_f)
+    # the scalars moved like the fp32 path's (their own slice of the upload)
+    names = [nm for nm, _ in base.named_parameters()]
+    offs = dict(zip(names, fed.flat.offsets))
+    idx = torch.tensor([offs[nm] for nm, p in base.named_parameters() if p.numel() == 1], device="cuda")
+    torch.testing.assert_close(up_n[idx], up_f[idx], rtol=0.1, atol=0.1 * up_f[idx].abs().max().item())
+
