@@ -155,9 +155,10 @@ __global__ void __launch_bounds__(256) row_sgd_kernel(float* __restrict__ W, int
 // perm[j] of the flat vector; a bijection, so the scattered adds never collide)
 // 4 columns a thread (16-byte loads; ld % 4 == 0), 8 client rows' loads in
 // flight before they are added in client order (one row at a time: 3.5 TB/s)
+// (perm: internal position -> coordinate of out; < 0 or >= dout: layout padding, skipped)
 __global__ void __launch_bounds__(256) upload_kernel(float* __restrict__ out, const float* __restrict__ w0,
                                                      const float* __restrict__ W, int64_t ld, int G, int64_t d,
-                                                     float n, const int32_t* __restrict__ perm) {
+                                                     float n, const int32_t* __restrict__ perm, int64_t dout) {
   const int64_t d4 = d / 4;
   for (int64_t j4 = blockIdx.x * 256ll + threadIdx.x; j4 < d4; j4 += static_cast<int64_t>(gridDim.x) * 256) {
     const float4 w = reinterpret_cast<const float4*>(w0)[j4];
@@ -185,17 +186,20 @@ __global__ void __launch_bounds__(256) upload_kernel(float* __restrict__ out, co
       acc.w += w.w - v.w;
     }
     const int64_t j = j4 * 4;
-    out[perm != nullptr ? perm[j] : j] += n * acc.x;
-    out[perm != nullptr ? perm[j + 1] : j + 1] += n * acc.y;
-    out[perm != nullptr ? perm[j + 2] : j + 2] += n * acc.z;
-    out[perm != nullptr ? perm[j + 3] : j + 3] += n * acc.w;
+    const float a4[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t o = perm != nullptr ? perm[j + q] : j + q;
+      if (o >= 0 && o < dout) out[o] += n * a4[q];
+    }
   }
   // the last d % 4 columns
   for (int64_t j = d4 * 4 + blockIdx.x * 256ll + threadIdx.x; j < d; j += static_cast<int64_t>(gridDim.x) * 256) {
     const float w = w0[j];
     float acc = 0.f;
     for (int g = 0; g < G; ++g) acc += w - W[g * ld + j];
-    out[perm != nullptr ? perm[j] : j] += n * acc;
+    const int64_t o = perm != nullptr ? perm[j] : j;
+    if (o >= 0 && o < dout) out[o] += n * acc;
   }
 }
 
@@ -219,9 +223,11 @@ __global__ void __launch_bounds__(256) cast_rows_kernel(uint16_t* __restrict__ W
 // dst[j] = src[perm[j]] (the server weights in the engine's layout) and its bf16 copy
 __global__ void __launch_bounds__(256) gather_rows_kernel(float* __restrict__ dst, bf16raw* __restrict__ dstb,
                                                           const float* __restrict__ src,
-                                                          const int32_t* __restrict__ perm, int64_t d) {
+                                                          const int32_t* __restrict__ perm, int64_t d,
+                                                          int64_t dsrc) {
   for (int64_t j = blockIdx.x * 256ll + threadIdx.x; j < d; j += static_cast<int64_t>(gridDim.x) * 256) {
-    const float v = src[perm[j]];
+    const int32_t pj = perm[j];
+    const float v = pj >= 0 && pj < dsrc ? src[pj] : 0.f;  // (layout padding: 0)
     dst[j] = v;
     dstb[j] = f2bf(v);
   }
@@ -643,15 +649,17 @@ void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const f
 int row_sgd_parts() { return kRowParts; }
 
 void launch_fedavg_upload(float* out, const float* w0, const float* W, int64_t ld, int G, int64_t d, float n,
-                          const int32_t* perm, hipStream_t stream) {
+                          const int32_t* perm, hipStream_t stream, int64_t dout) {
   if (d == 0) return;
-  COMMEFF_LAUNCH(upload_kernel, dim3(grid_for(d)), dim3(256), 0, stream, out, w0, W, ld, G, d, n, perm);
+  COMMEFF_LAUNCH(upload_kernel, dim3(grid_for(d)), dim3(256), 0, stream, out, w0, W, ld, G, d, n, perm,
+                 dout < 0 ? d : dout);
 }
 
 void launch_gather_rows(float* dst, uint16_t* dstb, const float* src, const int32_t* perm, int64_t d,
-                        hipStream_t stream) {
+                        hipStream_t stream, int64_t dsrc) {
   if (d == 0) return;
-  COMMEFF_LAUNCH(gather_rows_kernel, dim3(grid_for(d)), dim3(256), 0, stream, dst, dstb, src, perm, d);
+  COMMEFF_LAUNCH(gather_rows_kernel, dim3(grid_for(d)), dim3(256), 0, stream, dst, dstb, src, perm, d,
+                 dsrc < 0 ? d : dsrc);
 }
 
 void launch_bcast_rows(float* W, int64_t ld, const float* src, int G, int64_t d4, hipStream_t stream) {

@@ -21,9 +21,9 @@ void launch_row_sgd(float* W, int64_t ld, const float* src, int64_t sld, const f
                     int64_t d4, float clip, float lr, float wd, float* part, uint16_t* Wb, hipStream_t stream);
 int row_sgd_parts();
 void launch_fedavg_upload(float* out, const float* w0, const float* W, int64_t ld, int G, int64_t d, float n,
-                          const int32_t* perm, hipStream_t stream);
+                          const int32_t* perm, hipStream_t stream, int64_t dout);
 void launch_gather_rows(float* dst, uint16_t* dstb, const float* src, const int32_t* perm, int64_t d,
-                        hipStream_t stream);
+                        hipStream_t stream, int64_t dsrc);
 void launch_dgrad_image(const uint16_t* src, int64_t ld, int G, int K, int C, uint16_t* dst, hipStream_t stream);
 void launch_bcast_rows(float* W, int64_t ld, const float* src, int G, int64_t d4, hipStream_t stream);
 void launch_cast_rows(uint16_t* Wb, const float* W, int64_t ld, int G, int64_t off, int64_t n, hipStream_t stream);
@@ -119,12 +119,15 @@ void fa_row_sgd(at::Tensor W, int64_t ld, const at::Tensor& src, int64_t sld, co
 }
 
 // out[j] += n sum_g (w0[j] - W[g*ld + j]), j < d
-// (perm: rows / w0 in the engine's layout, element j -> coordinate perm[j] of out)
+// (perm: rows / w0 in the engine's layout of D >= d positions, element j ->
+// coordinate perm[j] of out, < 0: layout padding)
 void fa_upload(at::Tensor out, const at::Tensor& w0, const at::Tensor& W, int64_t ld, int64_t rows, double n,
                const c10::optional<at::Tensor>& perm) {
-  const int64_t d = out.numel();
+  const int64_t dout = out.numel();
+  const bool hp = perm.has_value() && perm->defined();
+  const int64_t d = hp ? perm->numel() : dout;
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && w0.numel() >= d &&
-                  w0.scalar_type() == at::kFloat && w0.is_contiguous(),
+                  w0.scalar_type() == at::kFloat && w0.is_contiguous() && d >= dout,
               "fa_upload: out / w0 fp32 [d]");
   check_rows(W, ld, rows, 0, d, "fa_upload: W");
   TORCH_CHECK(ld % 4 == 0 && reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0 &&
@@ -132,13 +135,13 @@ void fa_upload(at::Tensor out, const at::Tensor& w0, const at::Tensor& W, int64_
               "fa_upload: rows of a multiple of 4 floats, 16-byte aligned");
   const int32_t* pp = nullptr;
   if (perm.has_value() && perm->defined()) {
-    TORCH_CHECK(perm->is_cuda() && perm->scalar_type() == at::kInt && perm->is_contiguous() && perm->numel() == d,
-                "fa_upload: perm int32 [d]");
+    TORCH_CHECK(perm->is_cuda() && perm->scalar_type() == at::kInt && perm->is_contiguous(),
+                "fa_upload: perm int32 [D]");
     pp = perm->data_ptr<int32_t>();
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
   launch_fedavg_upload(out.data_ptr<float>(), w0.data_ptr<float>(), W.data_ptr<float>(), ld,
-                       static_cast<int>(rows), d, static_cast<float>(n), pp, stream_now());
+                       static_cast<int>(rows), d, static_cast<float>(n), pp, stream_now(), dout);
 }
 
 // dst[j] = src[perm[j]], dstb = bf16(dst): the server weights in the engine's layout
@@ -147,11 +150,11 @@ void fa_gather_rows(at::Tensor dst, at::Tensor dstb, const at::Tensor& src, cons
   TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kInt && perm.is_contiguous(), "fa_gather_rows: perm int32");
   TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kFloat && dst.is_contiguous() && dst.numel() >= d &&
                   dstb.scalar_type() == at::kBFloat16 && dstb.is_contiguous() && dstb.numel() >= d &&
-                  src.scalar_type() == at::kFloat && src.is_contiguous() && src.numel() == d,
-              "fa_gather_rows: dst fp32, dstb bf16 >= d, src fp32 [d]");
+                  src.scalar_type() == at::kFloat && src.is_contiguous() && src.numel() <= d,
+              "fa_gather_rows: dst fp32, dstb bf16 >= D, src fp32 [<= D] (perm < 0: padding)");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dst.device());
   launch_gather_rows(dst.data_ptr<float>(), bfw(dstb), src.data_ptr<float>(), perm.data_ptr<int32_t>(), d,
-                     stream_now());
+                     stream_now(), src.numel());
 }
 
 // W[g] = src for every row g < rows (d floats, 16-byte aligned rows)

@@ -1339,17 +1339,19 @@ class FedModel:
             loss_rows.append(lm)
             acc_rows.append(am)
             slot_rows.append(slots)
+        # (the engine's BatchNorm blocks: the Fixup engines' blocks have none)
+        bn_blocks = [b for b in eng.blocks if getattr(b, "m1", None) is not None]
         with torch.no_grad():  # the clients' mean running statistics, written once
             dsts, srcs = [], []
-            for b, s4 in zip(eng.blocks, acc_bufs):
+            for b, s4 in zip(bn_blocks, acc_bufs):
                 dsts += [b.m1.running_mean, b.m2.running_mean, b.m1.running_var, b.m2.running_var]
                 srcs += list((s4 / len(mine)).to(b.m1.running_mean.dtype).unbind(0))
             if dsts:  # (models without batch norm have none)
                 torch._foreach_copy_(dsts, srcs)
             # num_batches_tracked: every BatchNorm layer counts the local steps
             # (the engine advanced the first layer's counter)
-            nbt0 = eng.blocks[0].m1.num_batches_tracked if eng.blocks else None
-            for b in eng.blocks:
+            nbt0 = bn_blocks[0].m1.num_batches_tracked if bn_blocks else None
+            for b in bn_blocks:
                 for m in (b.m1, b.m2):
                     if m.num_batches_tracked is not nbt0:
                         m.num_batches_tracked.copy_(nbt0)

@@ -151,10 +151,41 @@ class ResNet18FedAvg:
             return False, f"final feature map {h}x{w} > 256 pixels (fused pooling head)"
         return True, ""
 
+    def _aligned(self, names, flat) -> Dict[str, int]:
+        """Internal row offsets: every parameter starts on a 16-byte boundary
+        (the Fixup models' one-element scalars otherwise shift every conv
+        weight off the kernels' 16-byte loads); the gaps are layout padding
+        (perm -1: gathered as 0, never uploaded).  Sets the row length self.d."""
+        off, segs, io = {}, [], 0
+        for nm, fo, nel in zip(names, flat.offsets, flat.numels):
+            off[nm] = io
+            segs.append((io, int(fo), int(nel)))
+            io += (int(nel) + 7) // 8 * 8
+        self._segs = segs
+        self.d = io
+        return off
+
+    def _perm_convs(self, device, convs) -> torch.Tensor:
+        """int32 [d]: internal position -> flat coordinate (-1: padding); the
+        3x3 conv weights ``convs`` (internal offset, K, C) in the kernels'
+        (k, r, s, c) order, everything else in PyTorch's order."""
+        if getattr(self, "_perm_t", None) is None or self._perm_t.device != device:
+            import numpy as np
+            perm = np.full(self.d, -1, dtype=np.int64)
+            flat_of = {}
+            for io, fo, nel in self._segs:
+                perm[io:io + nel] = fo + np.arange(nel)
+                flat_of[io] = fo
+            for off, K, C in convs:
+                # internal (k, t, c) <- PyTorch (k, c, t)
+                k, t, c = np.meshgrid(np.arange(K), np.arange(9), np.arange(C), indexing="ij")
+                perm[off:off + K * 9 * C] = flat_of[off] + ((k * C + c) * 9 + t).reshape(-1)
+            self._perm_t = torch.from_numpy(perm.astype(np.int32)).to(device)
+        return self._perm_t
+
     def __init__(self, model, flat, names: List[str]):
         self.model = model
-        off = {nm: int(o) for nm, o in zip(names, flat.offsets)}
-        self.d = int(flat.d) if hasattr(flat, "d") else int(sum(flat.numels))
+        off = self._aligned(names, flat)
         self.off = off
         self.prep = off["prep.0.weight"]
         self.blocks: List[_Block] = []
@@ -187,18 +218,10 @@ class ResNet18FedAvg:
         the bf16 mirror then IS the grouped conv kernels' forward image and the column-GEMM image, and the weight
         gradients come out of the MFMA / GEMM reductions in that order -- and
         everything else in PyTorch's order."""
-        if getattr(self, "_perm_t", None) is None or self._perm_t.device != device:
-            import numpy as np
-            perm = np.arange(self.d, dtype=np.int64)
-            convs = [(self.prep, self.c0, self.cin0)]
-            for b in self.blocks:
-                convs += [(b.conv1, b.cout, b.cin), (b.conv2, b.cout, b.cout)]
-            for off, K, C in convs:
-                # internal (k, t, c) <- PyTorch (k, c, t)
-                k, t, c = np.meshgrid(np.arange(K), np.arange(9), np.arange(C), indexing="ij")
-                perm[off:off + K * 9 * C] = off + ((k * C + c) * 9 + t).reshape(-1)
-            self._perm_t = torch.from_numpy(perm.astype(np.int32)).to(device)
-        return self._perm_t
+        convs = [(self.prep, self.c0, self.cin0)]
+        for b in self.blocks:
+            convs += [(b.conv1, b.cout, b.cin), (b.conv2, b.cout, b.cout)]
+        return self._perm_convs(device, convs)
 
     @staticmethod
     def _rows(Wt: torch.Tensor, ld: int, G: int, off: int, K: int, n: int) -> torch.Tensor:
@@ -603,8 +626,7 @@ class ResNet9FedAvg(ResNet18FedAvg):
 
     def __init__(self, model, flat, names: List[str]):
         self.model = model
-        off = {nm: int(o) for nm, o in zip(names, flat.offsets)}
-        self.d = int(flat.d) if hasattr(flat, "d") else int(sum(flat.numels))
+        off = self._aligned(names, flat)
         self.off = off
         n = model.n
         self.prep = off["n.prep.conv.weight"]
@@ -621,15 +643,8 @@ class ResNet9FedAvg(ResNet18FedAvg):
         self.scale = float(n.classifier.weight)
 
     def _perm(self, device) -> torch.Tensor:
-        if getattr(self, "_perm_t", None) is None or self._perm_t.device != device:
-            import numpy as np
-            perm = np.arange(self.d, dtype=np.int64)
-            convs = [(self.prep, self.c0, self.cin0)] + [(o, K, C) for (o, C, K) in self.conv.values()]
-            for off, K, C in convs:
-                k, t, c = np.meshgrid(np.arange(K), np.arange(9), np.arange(C), indexing="ij")
-                perm[off:off + K * 9 * C] = off + ((k * C + c) * 9 + t).reshape(-1)
-            self._perm_t = torch.from_numpy(perm.astype(np.int32)).to(device)
-        return self._perm_t
+        return self._perm_convs(device, [(self.prep, self.c0, self.cin0)]
+                                + [(o, K, C) for (o, C, K) in self.conv.values()])
 
     def run(self, w0, x, y, G, n, bs, epochs, lr, decay, wd, clip, out, first_pass):
         """As ResNet18FedAvg.run (no running statistics: returns an empty list)."""
@@ -793,8 +808,7 @@ class FixupResNet9FedAvg(ResNet9FedAvg):
 
     def __init__(self, model, flat, names: List[str]):
         self.model = model
-        off = {nm: int(o) for nm, o in zip(names, flat.offsets)}
-        self.d = int(flat.d) if hasattr(flat, "d") else int(sum(flat.numels))
+        off = self._aligned(names, flat)
         self.off = off
         self.prep = off["conv1.weight"]
         self.c0 = model.conv1.out_channels
@@ -950,11 +964,190 @@ class FixupResNet9FedAvg(ResNet9FedAvg):
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
 
 
+class FixupResNet18FedAvg(ResNet18FedAvg):
+    """Explicit G-client forward / backward / local SGD of models.fixup.FixupResNet18
+    (reference /root/reference/CommEfficient/models/fixup_resnet18.py:24-135):
+    ResNet18FedAvg's stem, convolutions (stride-2 ones and their 1x1 shortcuts
+    on implicit column images), avg || max head and fused classifier, with the
+    blocks' BatchNorms replaced by the per-client Fixup scalars
+    ``relu(conv2(relu(conv1(x + a1a) + a1b) + a2a) * m + a2b + shortcut(x))``
+    on the affine kernels (see FixupResNet9FedAvg).  A strided block's input
+    bias gradient is the sum of conv1's column-image gradient over the
+    in-image taps, taken before the shortcut's gradient joins the centre tap."""
+
+    run = ResNet9FedAvg.run  # (no running statistics)
+
+    @staticmethod
+    def supported(model, args) -> Tuple[bool, str]:
+        from ..models.fixup import FixupResNet18
+        if not isinstance(model, FixupResNet18):
+            return False, "not the FixupResNet18 of models/fixup.py"
+        if getattr(args, "dtype", "bf16") != "bf16":
+            return False, "bf16 compute only"
+        for layer in model.layers:
+            for blk in layer:
+                if blk.conv1.in_channels % 64 or blk.conv1.out_channels % 64:
+                    return False, "channel counts must be multiples of 64"
+        if model.prep.out_channels % 64:
+            return False, "channel counts must be multiples of 64"
+        for p in model.parameters():
+            if not p.requires_grad:
+                return False, "frozen parameters"
+        return True, ""
+
+    def __init__(self, model, flat, names: List[str]):
+        self.model = model
+        off = self._aligned(names, flat)
+        self.off = off
+        self.prep = off["prep.weight"]
+        self.blocks: List[_Block] = []
+        self.fx = []  # per block: scalar offsets
+        for li, layer in enumerate(model.layers):
+            for bi, blk in enumerate(layer):
+                p = f"layers.{li}.{bi}."
+                b = _Block()
+                b.cin, b.cout = blk.conv1.in_channels, blk.conv1.out_channels
+                b.stride = blk.conv1.stride[0]
+                b.conv1, b.conv2 = off[p + "conv1.weight"], off[p + "conv2.weight"]
+                b.sc = off.get(p + "shortcut.weight")
+                if b.sc is None and (b.stride != 1 or b.cin != b.cout):
+                    raise ValueError("FixupResNet18FedAvg: block without a shortcut changes shape")
+                if b.sc is not None and b.stride != 2:
+                    raise ValueError("FixupResNet18FedAvg: stride-1 projection shortcuts are not wired")
+                self.blocks.append(b)
+                self.fx.append({k: off[p + k + (".scale" if k == "mul" else ".bias")]
+                                for k in ("add1a", "add1b", "add2a", "mul", "add2b")})
+        self.fc_w, self.fc_b = off["classifier.weight"], off["classifier.bias"]
+        self.ncls = model.classifier.out_features
+        self.feat = model.classifier.in_features
+        self.c0 = model.prep.out_channels
+        self.cin0 = model.prep.in_channels
+
+    def _ones_strided(self, xin, G, C):
+        """channel-stacked im2col (3 x 3, stride 2, pad 1) of an all-ones xin: 1 at the in-image taps"""
+        key = (tuple(xin.shape), G, C, xin.device)
+        cache = getattr(self, "_ones_s", None)
+        if cache is None:
+            cache = self._ones_s = {}
+        if key not in cache:
+            c = _ops().im2col_grouped(torch.ones_like(xin), G, 3, 3, 2, 1, 9 * C, False)
+            n_, _, Hi, Wi = xin.shape
+            Ho, Wo = (Hi - 1) // 2 + 1, (Wi - 1) // 2 + 1
+            cache[key] = c.view(n_, Ho, Wo, G * 9 * C).permute(0, 3, 1, 2)
+        return cache[key]
+
+    def _step9(self, x, y, G, n, W, Wb, ld, sink):
+        ops = _ops()
+
+        def aff(t, fx, s=None, b=None, add=None, relu=False):
+            return ops.fa_affine(t, G, False, W, ld, -1 if s is None else fx[s], -1 if b is None else fx[b],
+                                 add, relu)
+
+        def sgd(part, fx, b=None, s=None):
+            ops.fa_scalar_sgd(part, sink.dst, sink.ld, -1 if b is None else fx[b], -1 if s is None else fx[s],
+                              sink.beta, sink.alpha, sink.src, sink.sld)
+
+        # ---- stem (as ResNet18FedAvg._step): relu(conv(x))
+        C0, K0 = self.cin0, self.c0
+        Kc0 = (9 * C0 + 63) // 64 * 64
+        col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        col0g = col0.transpose(0, 1)[:, :, :9 * C0]
+        H, Wd = x.shape[2], x.shape[3]
+        y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
+                         memory_format=torch.channels_last)
+        w0rows = self._rows(Wb, ld, G, self.prep, K0, 9 * C0)
+        pad = getattr(self, "_stem_img", None)
+        if pad is None or pad.shape != (G, K0, Kc0) or pad.device != x.device:
+            pad = self._stem_img = torch.zeros((G, K0, Kc0), device=x.device, dtype=torch.bfloat16)
+        pad[:, :, :9 * C0].copy_(w0rows)
+        if not ops.fa_gemm(col0.transpose(0, 1), pad, _gview(y0, G), False, 0.0):
+            torch.bmm(col0g, w0rows.transpose(1, 2), out=_gview(y0, G))
+        a = ops.fa_ew(y0, None, 1)
+        a0 = a
+        saved = []
+        for b, fx in zip(self.blocks, self.fx):
+            xin = a
+            xa = aff(xin, fx, b="add1a")
+            if b.stride == 1:
+                c1 = self._conv3(xa, Wb, ld, G, b.conv1, b.cout, b.cin)
+                sc = xin
+            else:
+                nn_, _, Hi, Wi = xin.shape
+                Ho, Wo = (Hi - 1) // 2 + 1, (Wi - 1) // 2 + 1
+                c1 = torch.empty((nn_, G * b.cout, Ho, Wo), device=x.device, dtype=torch.bfloat16,
+                                 memory_format=torch.channels_last)
+                sc = torch.empty_like(c1)
+                P1 = nn_ * Ho * Wo
+                # conv1 over the implicit column image of x + a1a, the shortcut of x
+                if not (ops.fa_gemm(_carrier(xa, G, P1, 9 * b.cin), self._rows(Wb, ld, G, b.conv1, b.cout, 9 * b.cin),
+                                    _gview(c1, G), False, 0.0, xa, 3, 2, 1)
+                        and ops.fa_gemm(_carrier(xin, G, P1, b.cin), self._rows(Wb, ld, G, b.sc, b.cout, b.cin),
+                                        _gview(sc, G), False, 0.0, xin, 1, 2, 0)):
+                    raise RuntimeError("FixupResNet18FedAvg: implicit strided GEMM refused")
+            h1 = aff(c1, fx, b="add1b", relu=True)
+            h1a = aff(h1, fx, b="add2a")
+            h2 = self._conv3(h1a, Wb, ld, G, b.conv2, b.cout, b.cout)
+            a = aff(h2, fx, s="mul", b="add2b", add=sc, relu=True)
+            saved.append((xin, xa, h1, h1a, h2, a))
+        # ---- head: avg || max pool -> classifier (fused) -> cross entropy
+        feat, codes = ops.fa_head_fwd(a, G)
+        S_ = -(-self.ncls // 32)
+        dfeat = torch.empty((S_ * G, n, self.feat), device=feat.device, dtype=torch.float32)
+        loss, correct = ops.fa_linear_ce(feat, n * self.feat, self.feat, G, n, W, ld, self.fc_w, self.fc_b,
+                                         self.ncls, self.feat, 1.0, y, dfeat, n * self.feat, self.feat,
+                                         sink.dst, sink.ld, sink.beta, sink.alpha, sink.src, sink.sld,
+                                         None, 0, G * n * self.feat, 32)
+        da = ops.fa_head_bwd(dfeat, codes, a.shape[2], a.shape[3])
+        # ---- blocks, last to first
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            b, fx = self.blocks[bi], self.fx[bi]
+            xin, xa, h1, h1a, h2, out = saved[bi]
+            # relu(h2 m + a2b + sc): dh2 = dpre m, the shortcut's gradient dpre
+            dh2, dpre, part = ops.fa_affine_bwd(da, G, False, W, ld, fx["mul"], out, h2, None, True, True)
+            sgd(part, fx, b="add2b", s="mul")
+            dh1a = self._conv3_dgrad(dh2, Wb, ld, G, b.conv2, b.cout, b.cout)
+            self._conv3_wgrad(dh2, h1a, G, sink, b.conv2, b.cout, b.cout)
+            # h1a = h1 + a2a (sum of dh1a), h1 = relu(c1 + a1b) (sum of the masked)
+            dc1, _, part = ops.fa_affine_bwd(dh1a, G, False, W, ld, -1, h1, None, None, True, False)
+            sgd(part, fx, b="add1b", s="add2a")
+            if b.stride == 1:
+                dxa = self._conv3_dgrad(dc1, Wb, ld, G, b.conv1, b.cout, b.cin)
+                self._conv3_wgrad(dc1, xa, G, sink, b.conv1, b.cout, b.cin)
+                # xa = x + a1a: sum of dxa; dx = dxa + the identity's gradient
+                da, _, part = ops.fa_affine_bwd(dxa, G, False, W, ld, -1, None, None, dpre, True, False)
+                sgd(part, fx, b="add1a")
+            else:
+                nn_, _, Hi, Wi = xin.shape
+                Ho, Wo = (Hi - 1) // 2 + 1, (Wi - 1) // 2 + 1
+                P1 = nn_ * Ho * Wo
+                dcol = torch.empty((P1, G, 9 * b.cin), device=x.device, dtype=torch.bfloat16)
+                dcg = dcol.transpose(0, 1)
+                _gmm(_gview(dc1, G), self._rows(Wb, ld, G, b.conv1, b.cout, 9 * b.cin), dcg, True)
+                # the input bias: conv1's column-image gradient over the in-image taps
+                dcol4 = dcol.view(nn_, Ho, Wo, G * 9 * b.cin).permute(0, 3, 1, 2)
+                sgd(ops.fa_affine_bwd(dcol4, G, False, W, ld, -1, None, self._ones_strided(xin, G, b.cin), None,
+                                      False, False)[2], fx, s="add1a")
+                # then the shortcut's input gradient joins the centre tap before the gather
+                _gmm(_gview(dpre, G), self._rows(Wb, ld, G, b.sc, b.cout, b.cin), dcg[:, :, 4 * b.cin:5 * b.cin],
+                     True, 1.0)
+                A1, Asc = _gview(dc1, G).transpose(1, 2), _gview(dpre, G).transpose(1, 2)
+                if not (ops.fa_bmm_rows(A1, _carrier(xa, G, P1, 9 * b.cin), sink.dst, sink.ld, b.conv1, sink.beta,
+                                        sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xa, 3, 2, 1)
+                        and ops.fa_bmm_rows(Asc, _carrier(xin, G, P1, b.cin), sink.dst, sink.ld, b.sc, sink.beta,
+                                            sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xin, 1, 2, 0)):
+                    raise RuntimeError("FixupResNet18FedAvg: implicit strided weight update refused")
+                da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
+        # ---- stem weight gradient (ReLU backward through its output)
+        dy0 = ops.relu_mask(da, a0)
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+
+
 def engine_for(model, args):
     """(engine class or None, why): the explicit G-client FedAvg program that
     covers this model / configuration."""
     why = []
-    for cls in (ResNet18FedAvg, ResNet9FedAvg, FixupResNet9FedAvg):
+    for cls in (ResNet18FedAvg, ResNet9FedAvg, FixupResNet9FedAvg, FixupResNet18FedAvg):
         ok, w = cls.supported(model, args)
         if ok:
             return cls, ""

@@ -38,6 +38,9 @@ def test_supported_models():
     from commefficient_amd.parallel.fedavg_native import FixupResNet9FedAvg
     assert engine_for(FixupResNet9(num_classes=10), _args())[0] is FixupResNet9FedAvg
     assert not FixupResNet9FedAvg.supported(models.ResNet9(), _args())[0]
+    from commefficient_amd.models.fixup import FixupResNet18
+    from commefficient_amd.parallel.fedavg_native import FixupResNet18FedAvg
+    assert engine_for(FixupResNet18(num_classes=10), _args())[0] is FixupResNet18FedAvg
     assert not ResNet18FedAvg.supported(ResNet18(num_classes=10), _args(["--dtype", "fp32"]))[0]
 
 
@@ -55,7 +58,12 @@ def test_engine_layout_matches_parameter_order():
         _Flat.numels.append(p.numel())
         o += p.numel()
     eng = ResNet18FedAvg(m, _Flat, names)
-    assert eng.d == o
+    # rows: every parameter on a 16-byte boundary, padding between (perm -1)
+    assert o <= eng.d < o + 8 * len(names)
+    assert all(v % 8 == 0 for v in eng.off.values())
+    perm = eng._perm("cpu")
+    real = perm[perm >= 0]
+    assert real.numel() == o and torch.equal(real.sort().values, torch.arange(o, dtype=real.dtype))
     assert [b.stride for b in eng.blocks] == [1, 1, 2, 1, 2, 1, 2, 1]
     assert sum(b.sc is not None for b in eng.blocks) == 3
     assert eng.feat == 512 and eng.ncls == 100
@@ -656,12 +664,12 @@ def test_resnet9_native_round_matches_vmap_and_fp32(extra):
     assert (l_n - l_f).abs().max().item() <= 2 * lnoise + 3e-2 * l_f.abs().max().item(), (l_n, l_v, l_f)
 
 
-def _fixup9_perturbed():
-    """A FixupResNet9 whose zero-initialised parts (last convs, classifier,
+def _fixup9_perturbed(cls_name="FixupResNet9"):
+    """A Fixup model whose zero-initialised parts (last convs, classifier,
     scalars) are perturbed, so every gradient path is exercised."""
-    from commefficient_amd.models.fixup import FixupResNet9
+    from commefficient_amd.models import fixup
     torch.manual_seed(0)
-    m = FixupResNet9(num_classes=10)
+    m = getattr(fixup, cls_name)(num_classes=10)
     g = torch.Generator().manual_seed(11)
     with torch.no_grad():
         for name, p in m.named_parameters():
@@ -669,7 +677,11 @@ def _fixup9_perturbed():
                 base = 1.0 if name.endswith("scale") else 0.0
                 p.fill_(base + 0.2 * torch.randn((), generator=g).item())
             elif p.dim() == 4:
-                p.copy_(torch.randn(p.shape, generator=g) * (2.0 / (p.shape[1] * 9)) ** 0.5)
+                # (He init, damped in the deep model: 18 un-normalised layers
+                # would otherwise blow the logits up to losses of ~200, where
+                # bf16 rounding alone moves them by tens)
+                gain = 0.5 if cls_name == "FixupResNet18" else 1.0
+                p.copy_(torch.randn(p.shape, generator=g) * gain * (2.0 / (p.shape[1] * p.shape[2] * p.shape[3])) ** 0.5)
             else:
                 p.copy_(torch.randn(p.shape, generator=g) * 0.05)
     return m
@@ -727,15 +739,17 @@ def test_fa_affine_forward_backward_and_scalar_sgd(layout):
     ["--fedavg_batch_size", "2", "--num_fedavg_epochs", "1", "--weight_decay", "5e-4",
      "--max_grad_norm", "2.0", "--fedavg_lr_decay", "0.9"],
 ])
-def test_fixup_resnet9_native_round_matches_vmap_and_fp32(extra):
-    """FixupResNet9's FedAvg round on the native G-client program
-    (FixupResNet9FedAvg: the ResNet-9 kernels + per-client Fixup scalars) vs
-    the vmap composition (bf16) and the fp32 sequential path: as close to
-    fp32 as bf16 vmap is (reference models/fixup_resnet9.py, fed_worker.py:61-113)."""
-    base = _fixup9_perturbed()
+@pytest.mark.parametrize("model", ["FixupResNet9", "FixupResNet18"])
+def test_fixup_native_round_matches_vmap_and_fp32(extra, model):
+    """A Fixup model's FedAvg round on the native G-client program
+    (FixupResNet9FedAvg / FixupResNet18FedAvg: the ResNet-9 / ResNet-18
+    kernels + per-client Fixup scalars) vs the vmap composition (bf16) and the
+    fp32 sequential path: as close to fp32 as bf16 vmap is (reference
+    models/fixup_resnet9.py, fixup_resnet18.py, fed_worker.py:61-113)."""
+    base = _fixup9_perturbed(model)
     G, n = 5, 4
     up_n, l_n, fed = _round9(base, "native", "bf16", G, n, extra, lr=0.02)
-    assert fed._fa_native and type(fed._fa_native).__name__ == "FixupResNet9FedAvg"
+    assert fed._fa_native and type(fed._fa_native).__name__ == model + "FedAvg"
     up_v, l_v, _ = _round9(base, "vmap", "bf16", G, n, extra, lr=0.02)
     up_f, l_f, _ = _round9(base, "vmap", "fp32", G, n, extra + ["--fedavg_batched", "off"], lr=0.02)
     noise = ((up_v - up_f).norm() / up_f.norm()).item()
