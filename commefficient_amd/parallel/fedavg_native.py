@@ -418,7 +418,10 @@ class ResNet18FedAvg:
                 else:
                     W, Wbf, sld = Wg, Wb, ld
                 lr_t = float(lr * decay ** steps)
-                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, Wb, W, sld) if fused
+                # (the last step's updated weights are only uploaded from the
+                # fp32 rows: no bf16 mirror writes)
+                last = steps == epochs * ((n + bs - 1) // bs) - 1
+                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, None if last else Wb, W, sld) if fused
                         else _Sink(Gg, ld, 0.0, 1.0, None))
                 l, c = self._step(xb, yb, G, s1 - s0, W, Wbf, sld, sink, run, nbt, ones)
                 loss_acc += l
@@ -675,7 +678,10 @@ class ResNet9FedAvg(ResNet18FedAvg):
                     xb, yb = x, y
                 W, Wbf, sld = (w0i, w0b, 0) if steps == 0 else (Wg, Wb, ld)
                 lr_t = float(lr * decay ** steps)
-                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, Wb, W, sld) if fused
+                # (the last step's updated weights are only uploaded from the
+                # fp32 rows: no bf16 mirror writes)
+                last = steps == epochs * ((n + bs - 1) // bs) - 1
+                sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, None if last else Wb, W, sld) if fused
                         else _Sink(Gg, ld, 0.0, 1.0, None))
                 l, c = self._step9(xb, yb, G, s1 - s0, W, Wbf, sld, sink)
                 loss_acc += l
