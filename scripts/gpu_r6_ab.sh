@@ -1,9 +1,9 @@
 # A/B of an environment switch: conv tests, then conv_lab and the driver-shaped bench
-# alternating between VAR=A and VAR=B (default: the 3-slot conv ring vs the 2-slot one)
+# alternating over VALS of VAR (e.g. VAR=COMMEFF_FA_HEAD VALS="1 0")
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r6ab}; mkdir -p $O
-VAR=${VAR:-COMMEFF_CONV_IL}; VALS=${VALS:-"0 1 2"}
+VAR=${VAR:?set VAR to the switch under test}; VALS=${VALS:?set VALS}
 if [ -n "${TESTS-tests/test_conv.py}" ]; then
   timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu ${TESTS-tests/test_conv.py} > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
   tail -2 $O/tests.log

@@ -2,7 +2,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r6cfgab}; mkdir -p $O
-VAR=${VAR:-COMMEFF_TN_CUS}; VALS=${VALS:-"0 128"}; C=${CONFIG:-gpt2_sketch}
+VAR=${VAR:?set VAR to the switch under test}; VALS=${VALS:?set VALS}; C=${CONFIG:-gpt2_sketch}
 if [ -n "${TESTS:-}" ]; then
   timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu $TESTS > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
   tail -2 $O/tests.log
