@@ -58,6 +58,17 @@ def cfg_args(name, N, b):
                    "--virtual_momentum", "0.9", "--num_clients", "10000", "--num_workers", str(W),
                    "--local_batch_size", "-1", "--fedavg_batch_size", "-1",
                    "--num_fedavg_epochs", "5", "--batchnorm"]
+    if name == "imagenet_fixup50_uncompressed":
+        # the reference's ImageNet example run (imagenet.sh:2-21): FixupResNet50,
+        # uncompressed, 7 clients x 64 per round, virtual momentum. The script's
+        # --mixup/--mixup_alpha flags are undefined in the reference's parser
+        # (its mixup loss is unreachable, cv_train.py:74-80), so plain CE here.
+        W = b.clients or 7 * N
+        return W, ["--dataset_name", "ImageNet", "--synthetic", "--synthetic_size", str(W * 64 * 2),
+                   "--model", "FixupResNet50", "--mode", "uncompressed", "--error_type", "virtual",
+                   "--local_momentum", "0", "--virtual_momentum", "0.9", "--weight_decay", "1e-4",
+                   "--num_clients", str(W), "--num_workers", str(W), "--local_batch_size", "64",
+                   "--iid"]
     if name == "cifar10_resnet9_fedavg_local":
         # the headline model under FedAvg: 5 local full-batch steps per client
         W = b.clients or 100 * N
@@ -73,7 +84,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--config", required=True,
                    choices=["imagenet_local_topk", "gpt2_sketch", "cifar100_fedavg",
-                            "cifar100_fedavg_local", "cifar10_resnet9_fedavg_local"])
+                            "cifar100_fedavg_local", "cifar10_resnet9_fedavg_local",
+                            "imagenet_fixup50_uncompressed"])
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--clients", type=int, default=0, help="clients per round (total)")
@@ -184,7 +196,8 @@ def main():
     tp = os.environ.get("COMMEFF_TORCH_PROFILE")
     if tp:  # 3 more rounds under torch.profiler (host launch vs GPU start: scripts/launch_lag.py)
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        shapes = os.environ.get("COMMEFF_TORCH_PROFILE_SHAPES") == "1"
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=shapes) as prof:
             for i in range(b.warmup, b.warmup + min(3, b.steps)):
                 fed(batches_at[i])
                 fopt.step()
