@@ -509,7 +509,7 @@ __global__ void __launch_bounds__(256) fa_linear_kernel(FaLinearArgs a, const fl
 // ------------------------------------------------------------ Fixup scalars
 // Per-client scalar affine maps of the Fixup models (models/fixup.py: x + b,
 // x * s + b, relu, + residual), the scalars read from the clients' fp32 rows
-// (W[g * ld + off]; off < 0: none).  Activations bf16, channel-stacked
+// (S / B [g * ld]; nullptr: none; ld 0: one pair for every group).  Activations bf16, channel-stacked
 // ([pixels][G C]: group of element e = (e mod G C) / C) or client-major (the
 // stem's input: group = e / per); 8 elements a thread, one group each.
 __device__ __forceinline__ int64_t fa_mem(const FaAffine& a, int g, int64_t eg) {
@@ -526,8 +526,9 @@ __global__ void __launch_bounds__(256) fa_affine_kernel(FaAffine a) {
   for (int64_t q = blockIdx.x * 256ll + threadIdx.x; q < n8; q += static_cast<int64_t>(gridDim.x) * 256) {
     const int64_t e = q * 8;
     const int g = a.C > 0 ? static_cast<int>((e % a.GC) / a.C) : static_cast<int>(e / a.per);
-    const float sc = a.soff >= 0 ? a.W[g * a.ld + a.soff] : 1.f;
-    const float bi = a.boff >= 0 ? a.W[g * a.ld + a.boff] : 0.f;
+    const float sc = a.S != nullptr ? a.S[g * a.ld] : 1.f;
+    const float bi = a.B != nullptr ? a.B[g * a.ld] : 0.f;
+    const float po = a.P != nullptr ? a.P[g * a.ld] : 0.f;
     const u4 xv = *reinterpret_cast<const u4*>(a.x + e);
     u4 av = {0u, 0u, 0u, 0u};
     if (a.add != nullptr) av = *reinterpret_cast<const u4*>(a.add + e);
@@ -543,6 +544,8 @@ __global__ void __launch_bounds__(256) fa_affine_kernel(FaAffine a) {
         v0 = fmaxf(v0, 0.f);
         v1 = fmaxf(v1, 0.f);
       }
+      v0 += po;  // (relu(.) + post bias; 0 without one)
+      v1 += po;
       o[h] = static_cast<uint32_t>(f2bf(v0)) | (static_cast<uint32_t>(f2bf(v1)) << 16);
     }
     *reinterpret_cast<u4*>(a.y + e) = o;
@@ -558,7 +561,9 @@ __global__ void __launch_bounds__(256) fa_affine_bwd_kernel(FaAffine a, FaAffine
   const int g = blockIdx.y, tid = threadIdx.x;
   const int64_t e0 = static_cast<int64_t>(blockIdx.x) * b.chunk;
   const int64_t e1 = min(e0 + b.chunk, a.per);
-  const float sc = a.soff >= 0 ? a.W[g * a.ld + a.soff] : 1.f;
+  const float sc = a.S != nullptr ? a.S[g * a.ld] : 1.f;
+  const float bi = a.B != nullptr ? a.B[g * a.ld] : 0.f;
+  const bool sum_dy = b.xs == nullptr || b.mask_x;  // second sum: dy unmasked
   float s1 = 0.f, s2 = 0.f;
   for (int64_t eg = e0 + 8 * tid; eg < e1; eg += 8 * 256) {
     const int64_t m = fa_mem(a, g, eg);
@@ -571,13 +576,16 @@ __global__ void __launch_bounds__(256) fa_affine_bwd_kernel(FaAffine a, FaAffine
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       float d[2] = {__uint_as_float(dv[h] << 16), __uint_as_float(dv[h] & 0xffff0000u)};
-      if (b.xs == nullptr) s2 += d[0] + d[1];  // (no scale input: the second sum is of dy unmasked)
-      if (b.yrelu != nullptr) {  // relu'(pre) from the output: y > 0
+      if (sum_dy) s2 += d[0] + d[1];  // (no scale input / post bias: the second sum is of dy unmasked)
+      if (b.mask_x) {  // relu'(pre), pre = x s + b recomputed as the forward did
+        if (!(fmaf(__uint_as_float(xv[h] << 16), sc, bi) > 0.f)) d[0] = 0.f;
+        if (!(fmaf(__uint_as_float(xv[h] & 0xffff0000u), sc, bi) > 0.f)) d[1] = 0.f;
+      } else if (b.yrelu != nullptr) {  // relu'(pre) from the output: y > 0
         if (!(__uint_as_float(yv[h] << 16) > 0.f)) d[0] = 0.f;
         if (!(__uint_as_float(yv[h] & 0xffff0000u) > 0.f)) d[1] = 0.f;
       }
       s1 += d[0] + d[1];
-      if (b.xs != nullptr)
+      if (!sum_dy)
         s2 = fmaf(d[0], __uint_as_float(xv[h] << 16), fmaf(d[1], __uint_as_float(xv[h] & 0xffff0000u), s2));
       float r0 = d[0] * sc, r1 = d[1] * sc;
       if (b.add2 != nullptr) {
@@ -624,7 +632,36 @@ __global__ void __launch_bounds__(256) fa_scalar_sgd_kernel(const float* __restr
   if (soff >= 0) dst[g * ld + soff] = beta != 0.f ? beta * sr[soff] + alpha * t2 : alpha * t2;
 }
 
+// one group's partial sums [chunks][2] -> out[0..1], one block, fixed order
+// (strided per-thread sums, then a tree): the merged-batch Fixup scalars'
+// gradients (ops/fixup.py)
+__global__ void __launch_bounds__(256) fx_part_sum_kernel(const float* __restrict__ part, int chunks,
+                                                          float* __restrict__ out) {
+  __shared__ float red[2][256];
+  const int tid = threadIdx.x;
+  float t1 = 0.f, t2 = 0.f;
+  for (int c = tid; c < chunks; c += 256) {
+    t1 += part[2 * c];
+    t2 += part[2 * c + 1];
+  }
+  red[0][tid] = t1;
+  red[1][tid] = t2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[0][tid] += red[0][tid + o];
+      red[1][tid] += red[1][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid < 2) out[tid] = red[tid][0];
+}
+
 }  // namespace
+
+void launch_fx_part_sum(const float* part, int chunks, float* out, hipStream_t stream) {
+  COMMEFF_LAUNCH(fx_part_sum_kernel, dim3(1), dim3(256), 0, stream, part, chunks, out);
+}
 
 void launch_weight_image(const float* W, int64_t ld, int G, int K, int C, int RS, int Kc, int kind,
                          uint16_t* dst, hipStream_t stream) {

@@ -341,10 +341,9 @@ static FaAffine affine_args(const at::Tensor& x, int64_t G, bool client_major, c
               what, ": scalar rows");
   FaAffine a{};
   a.G = static_cast<int>(G);
-  a.W = W.data_ptr<float>();
+  a.S = soff >= 0 ? W.data_ptr<float>() + soff : nullptr;
+  a.B = boff >= 0 ? W.data_ptr<float>() + boff : nullptr;
   a.ld = ld;
-  a.soff = soff;
-  a.boff = boff;
   if (client_major) {
     TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) || x.is_contiguous(), what, ": dense x");
     TORCH_CHECK(x.numel() % (8 * G) == 0 && (x.numel() / G) % 8 == 0, what, ": 8-element client blocks");
@@ -417,6 +416,96 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fa_affine_bwd(const at::Tensor& d
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   launch_fa_affine_bwd(a, b, static_cast<int>(chunks), stream_now());
   return {o1, o2, part};
+}
+
+// ---- merged-batch Fixup scalars (ops/fixup.py): one scale / bias pair
+// (fp32 [1] parameters) over a whole dense bf16 activation, any layout
+static FaAffine fx_args(const at::Tensor& x, const c10::optional<at::Tensor>& s,
+                        const c10::optional<at::Tensor>& b, const char* what) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_non_overlapping_and_dense() &&
+                  x.numel() % 8 == 0 && x.numel() > 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              what, ": dense 16-byte aligned bf16 x, 8 | numel");
+  auto scalar = [&](const c10::optional<at::Tensor>& t, const char* nm) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->numel() == 1, what, ": fp32 scalar ", nm);
+    return t->data_ptr<float>();
+  };
+  FaAffine a{};
+  a.G = 1;
+  a.S = scalar(s, "scale");
+  a.B = scalar(b, "bias");
+  a.ld = 0;
+  a.per = x.numel();
+  return a;
+}
+
+// y = relu?(x * s + b (+ add)), one bf16 rounding
+at::Tensor fx_affine(const at::Tensor& x, const c10::optional<at::Tensor>& s, const c10::optional<at::Tensor>& b,
+                     const c10::optional<at::Tensor>& add, bool relu, const c10::optional<at::Tensor>& post) {
+  FaAffine a = fx_args(x, s, b, "fx_affine");
+  if (post.has_value() && post->defined()) {
+    TORCH_CHECK(relu && post->is_cuda() && post->scalar_type() == at::kFloat && post->numel() == 1,
+                "fx_affine: fp32 scalar post bias after a relu");
+    a.P = post->data_ptr<float>();
+  }
+  auto y = at::empty_like(x);
+  if (add.has_value() && add->defined()) {
+    TORCH_CHECK(add->sizes() == x.sizes() && add->strides() == x.strides() && add->scalar_type() == at::kBFloat16 &&
+                    reinterpret_cast<uintptr_t>(add->data_ptr()) % 16 == 0,
+                "fx_affine: add like x");
+    a.add = bf(*add);
+  }
+  a.x = bf(x);
+  a.y = bfw(y);
+  a.relu = relu ? 1 : 0;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  launch_fa_affine(a, stream_now());
+  return y;
+}
+
+// (dx = dpre * s or undefined, dadd = dpre or undefined, sums fp32 [2] =
+// {sum dpre, sum dpre xs -- without xs: sum dy unmasked}), dpre = dy masked
+// by yrelu > 0; the sums in a fixed order (deterministic)
+// mask_x: the relu mask recomputed from xs (x s + b > 0, b given), the second
+// sum of dy unmasked (the post bias's gradient)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fx_affine_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& s,
+                                                             const c10::optional<at::Tensor>& yrelu,
+                                                             const c10::optional<at::Tensor>& xs, bool want1,
+                                                             bool want2, const c10::optional<at::Tensor>& bias,
+                                                             bool mask_x) {
+  FaAffine a = fx_args(dy, s, bias, "fx_affine_bwd");
+  TORCH_CHECK(!mask_x || (xs.has_value() && xs->defined()), "fx_affine_bwd: mask_x needs xs");
+  FaAffineBwd b{};
+  b.dy = bf(dy);
+  auto same = [&](const c10::optional<at::Tensor>& t, const char* nm) -> const uint16_t* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->sizes() == dy.sizes() && t->strides() == dy.strides() && t->scalar_type() == at::kBFloat16 &&
+                    reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "fx_affine_bwd: ", nm, " like dy");
+    return bf(*t);
+  };
+  b.yrelu = same(yrelu, "y");
+  b.xs = same(xs, "xs");
+  b.mask_x = mask_x ? 1 : 0;
+  at::Tensor o1, o2;
+  if (want1) {
+    o1 = at::empty_like(dy);
+    b.out1 = bfw(o1);
+  }
+  if (want2) {
+    o2 = at::empty_like(dy);
+    b.out2 = bfw(o2);
+  }
+  // at most ~2K blocks (then one block folds their partials), 2K-element multiples
+  b.chunk = std::max<int64_t>(8192, ((a.per + 2047) / 2048 + 2047) / 2048 * 2048);
+  const int64_t chunks = (a.per + b.chunk - 1) / b.chunk;
+  auto part = at::empty({chunks, 1, 2}, dy.options().dtype(at::kFloat));
+  auto sums = at::empty({2}, dy.options().dtype(at::kFloat));
+  b.part = part.data_ptr<float>();
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  launch_fa_affine_bwd(a, b, static_cast<int>(chunks), stream_now());
+  launch_fx_part_sum(part.data_ptr<float>(), static_cast<int>(chunks), sums.data_ptr<float>(), stream_now());
+  return {o1, o2, sums};
 }
 
 // dst[g ld + boff] / dst[g ld + soff] = beta src + alpha (sum of the partials' dpre / dpre x)
@@ -896,6 +985,9 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("fa_linear_ce(Tensor feat, int fsg, int fsn, int G, int n, Tensor W, int wld, int woff, int boff, int C, "
         "int F, float scale, Tensor y, Tensor(a!) dfeat, int dsg, int dsn, Tensor(b!) dst, int dld, float beta, "
         "float alpha, Tensor? src, int sld, Tensor(c!)? mirror, int mld, int dss=0, int ccs=0) -> (Tensor, Tensor)");
+  m.def("fx_affine(Tensor x, Tensor? s, Tensor? b, Tensor? add, bool relu, Tensor? post) -> Tensor");
+  m.def("fx_affine_bwd(Tensor dy, Tensor? s, Tensor? yrelu, Tensor? xs, bool want1, bool want2, Tensor? b, "
+        "bool mask_x) -> (Tensor, Tensor, Tensor)");
   m.def("fa_affine(Tensor x, int G, bool client_major, Tensor W, int ld, int soff, int boff, Tensor? add, "
         "bool relu) -> Tensor");
   m.def("fa_affine_bwd(Tensor dy, int G, bool client_major, Tensor W, int ld, int soff, Tensor? yrelu, "
@@ -929,6 +1021,8 @@ TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("fa_bcast_rows", &fa_bcast_rows);
   m.impl("fa_cast_rows", &fa_cast_rows);
   m.impl("fa_linear_ce", &fa_linear_ce);
+  m.impl("fx_affine", &fx_affine);
+  m.impl("fx_affine_bwd", &fx_affine_bwd);
   m.impl("fa_affine", &fa_affine);
   m.impl("fa_affine_bwd", &fa_affine_bwd);
   m.impl("fa_scalar_sgd", &fa_scalar_sgd);

@@ -625,8 +625,10 @@ struct FaAffine {
   const uint16_t* x;      // bf16 activations
   const uint16_t* add;    // + residual (nullptr: none)
   uint16_t* y;
-  const float* W;         // client rows: scale at g * ld + soff, bias at + boff (< 0: none)
-  int64_t ld, soff, boff;
+  const float* S;         // scale of group g at S[g * ld] (nullptr: none)
+  const float* B;         // bias of group g at B[g * ld] (nullptr: none)
+  const float* P;         // post bias after the relu, P[g * ld] (nullptr: none)
+  int64_t ld;
   int64_t per;            // elements per client
   int64_t GC;             // channel-stacked: G C channels a pixel (0 with C = 0: client-major)
   int G, C, relu;
@@ -635,6 +637,7 @@ struct FaAffineBwd {
   const uint16_t* dy;
   const uint16_t* yrelu;  // the forward output (relu mask), nullptr: no relu
   const uint16_t* xs;     // the scale's input (its gradient sum dpre x), nullptr: sum dy (unmasked) instead
+  int mask_x;             // relu mask recomputed from xs (x s + b > 0, no add), second sum = dy unmasked
   const uint16_t* add2;   // + this to out1 (nullptr: none)
   uint16_t* out1;         // dpre * s (+ add2), nullptr: not written
   uint16_t* out2;         // dpre, nullptr: not written
@@ -643,6 +646,7 @@ struct FaAffineBwd {
 };
 void launch_fa_affine(const FaAffine& a, hipStream_t stream);
 void launch_fa_affine_bwd(const FaAffine& a, const FaAffineBwd& b, int chunks, hipStream_t stream);
+void launch_fx_part_sum(const float* part, int chunks, float* out, hipStream_t stream);
 void launch_fa_scalar_sgd(const float* part, int chunks, int G, float* dst, int64_t ld, int64_t boff, int64_t soff,
                           float beta, float alpha, const float* src, int64_t sld, hipStream_t stream);
 bool gemm_supported(int M, int N, int K, bool nn);

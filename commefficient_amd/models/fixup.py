@@ -14,6 +14,10 @@ fixup_resnet.py:4).
 Fixup init (Zhang et al. 2019): the first conv of each residual branch is He
 init scaled by L^(-1/(2m-2)) (m = convs per branch), the last conv and the
 classifier are zero-initialised.
+
+The scalar biases / scales run as ``ops.fixup.scalar_affine``: one bf16 pass
+each way on a GPU (the activations stay bf16, so every conv stays on the
+native kernels), the PyTorch composition elsewhere.
 """
 from __future__ import annotations
 
@@ -22,6 +26,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.fixup import scalar_affine as _sa
+from ..ops.nn import relu_maxpool
 from .common import (GhostBatchNorm2d, NativeConv2d, NativeLinear, NativeMaxPool2d, ScalarBias,
                      ScalarScale, conv1x1, conv3x3)
 
@@ -47,11 +53,10 @@ class FixupBasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        xa = x + self.bias1a
-        out = F.relu(self.conv1(xa) + self.bias1b)
-        out = self.conv2(out + self.bias2a) * self.scale + self.bias2b
+        xa = _sa(x, b=self.bias1a)
+        out = _sa(self.conv1(xa), b=self.bias1b, relu=True, post=self.bias2a)
         idt = self.downsample(xa) if self.downsample is not None else x
-        return F.relu(out + idt)
+        return _sa(self.conv2(out), s=self.scale, b=self.bias2b, add=idt, relu=True)
 
 
 class FixupLayer(nn.Module):
@@ -67,10 +72,26 @@ class FixupLayer(nn.Module):
         self.blocks = nn.Sequential(*[FixupBasicBlock(c_out, c_out) for _ in range(num_blocks)])
 
     def forward(self, x):
-        out = F.relu(self.conv(x + self.bias1a) * self.scale + self.bias1b)
-        if self.pool is not None:
-            out = self.pool(out)
+        out = self.conv(_sa(x, b=self.bias1a))
+        k = _pool2(self.pool)
+        if k:  # relu then max-pool, one native pass each way
+            out = relu_maxpool(_sa(out, s=self.scale, b=self.bias1b), k)
+        else:
+            out = _sa(out, s=self.scale, b=self.bias1b, relu=True)
+            if self.pool is not None:
+                out = self.pool(out)
         return self.blocks(out)
+
+
+def _pool2(pool) -> int:
+    """k of a plain non-overlapping k x k max-pool (else 0)."""
+    if type(pool) is not nn.MaxPool2d or pool.padding not in (0, (0, 0)) or pool.dilation not in (1, (1, 1)) \
+            or pool.ceil_mode or pool.return_indices:
+        return 0
+    k, st = pool.kernel_size, pool.stride
+    k = k if isinstance(k, int) else (k[0] if k[0] == k[1] else 0)
+    st = st if isinstance(st, int) else (st[0] if st[0] == st[1] else -1)
+    return k if st == k else 0
 
 
 class FixupResNet9(nn.Module):
@@ -102,10 +123,11 @@ class FixupResNet9(nn.Module):
                 nn.init.constant_(m.bias, 0)
 
     def forward(self, x):
-        out = F.relu(self.conv1(x + self.bias1a) * self.scale + self.bias1b)
+        out = _sa(self.conv1(_sa(x, b=self.bias1a)), s=self.scale, b=self.bias1b, relu=True)
         out = self.layer3(self.layer2(self.layer1(out)))
-        out = self.pool(out).flatten(1)
-        return self.linear(out + self.bias2)
+        k = _pool2(self.pool)
+        out = (relu_maxpool(out, k) if k else self.pool(out)).flatten(1)  # (out >= 0: relu is exact)
+        return self.linear(_sa(out, b=self.bias2))
 
 
 # ---------------------------------------------------------------- ResNet-18s
@@ -126,9 +148,9 @@ class FixupBlock18(nn.Module):
 
     def forward(self, x):
         sc = self.shortcut(x) if hasattr(self, "shortcut") else x
-        out = F.relu(self.add1b(self.conv1(self.add1a(x))))
-        out = self.add2b(self.mul(self.conv2(self.add2a(out))))
-        return F.relu(out + sc)
+        out = _sa(self.conv1(_sa(x, b=self.add1a.bias)), b=self.add1b.bias, relu=True, post=self.add2a.bias)
+        out = self.conv2(out)
+        return _sa(out, s=self.mul.scale, b=self.add2b.bias, add=sc, relu=True)
 
 
 class PreActBlock(nn.Module):
@@ -223,12 +245,15 @@ class FixupBottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        xa = x + self.bias1a
-        out = F.relu(self.conv1(xa) + self.bias1b)
-        out = F.relu(self.conv2(out + self.bias2a) + self.bias2b)
-        out = self.conv3(out + self.bias3a) * self.scale + self.bias3b
-        idt = self.downsample(xa) if self.downsample is not None else x
-        return F.relu(out + idt)
+        xa = _sa(x, b=self.bias1a)
+        if self.downsample is not None:
+            # conv1 and the shortcut read xa: one node, input gradients summed in the dgrad GEMM
+            out, idt = self.conv1.forward_pair(self.downsample, xa)
+        else:
+            out, idt = self.conv1(xa), x
+        out = _sa(out, b=self.bias1b, relu=True, post=self.bias2a)
+        out = _sa(self.conv2(out), b=self.bias2b, relu=True, post=self.bias3a)
+        return _sa(self.conv3(out), s=self.scale, b=self.bias3b, add=idt, relu=True)
 
 
 class FixupResNet(nn.Module):
@@ -268,9 +293,9 @@ class FixupResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(F.relu(self.conv1(x) + self.bias1))
+        x = self.maxpool(_sa(self.conv1(x), b=self.bias1, relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        return self.fc(self.avgpool(x).flatten(1) + self.bias2)
+        return self.fc(_sa(self.avgpool(x).flatten(1), b=self.bias2))
 
 
 class FixupResNet50(FixupResNet):
