@@ -38,12 +38,35 @@
 
 namespace commeff {
 
+// Two lanes: a tape may fork work onto a side stream (ops/lanes.py: the conv
+// weight gradients, which nothing in the backward waits for) and join it back.
+// lane[i]: 0 = the replaying stream, 1 = the side stream, 2 = fork (the side
+// stream waits for everything issued so far on the main one), 3 = join (the
+// main stream waits for the side one); forks / joins replay as event record +
+// stream wait pairs, on events created at the first replay.
 struct LaunchTape {
   std::vector<std::function<void(hipStream_t)>> ops;
+  std::vector<uint8_t> lane;
+  std::vector<hipEvent_t> events;  // one per fork / join, lazily created
+  int forks = 0;
+  bool open = false;  // a fork not yet joined (recording)
+  ~LaunchTape() {
+    for (hipEvent_t e : events)
+      if (e != nullptr) (void)hipEventDestroy(e);
+  }
 };
 
 // non-null while a tape records (set/cleared by the bindings, tape.cpp)
 LaunchTape* tape_active();
+// the side stream of the recording (nullptr: none); a launch issued on it is
+// recorded on lane 1
+hipStream_t tape_side_stream();
+
+inline void tape_push(LaunchTape* t, std::function<void(hipStream_t)> op, hipStream_t s) {
+  const hipStream_t side = tape_side_stream();
+  t->ops.emplace_back(std::move(op));
+  t->lane.push_back(side != nullptr && s == side ? 1 : 0);
+}
 
 [[noreturn]] inline void launch_failed(const char* name, hipError_t e, dim3 g, dim3 b, uint32_t sh) {
   (void)hipGetLastError();  // clear the sticky status
@@ -70,9 +93,12 @@ inline void tape_launch(const char* name, void (*k)(P...), dim3 g, dim3 b, uint3
   using Tup = std::tuple<std::decay_t<P>...>;
   Tup args(static_cast<std::decay_t<P>>(std::forward<A>(a))...);
   if (LaunchTape* t = tape_active()) {
-    t->ops.emplace_back([name, k, g, b, sh, args](hipStream_t st) mutable {
-      launch_from_tuple(name, k, g, b, sh, st, args, std::index_sequence_for<P...>{});
-    });
+    tape_push(
+        t,
+        [name, k, g, b, sh, args](hipStream_t st) mutable {
+          launch_from_tuple(name, k, g, b, sh, st, args, std::index_sequence_for<P...>{});
+        },
+        s);
   }
   launch_from_tuple(name, k, g, b, sh, s, args, std::index_sequence_for<P...>{});
 }
@@ -90,7 +116,7 @@ inline void memset_checked(void* p, int v, size_t n, hipStream_t s) {
 
 inline void tape_memset(void* p, int v, size_t n, hipStream_t s) {
   if (LaunchTape* t = tape_active()) {
-    t->ops.emplace_back([p, v, n](hipStream_t st) { memset_checked(p, v, n, st); });
+    tape_push(t, [p, v, n](hipStream_t st) { memset_checked(p, v, n, st); }, s);
   }
   memset_checked(p, v, n, s);
 }

@@ -5,7 +5,11 @@
 //                            is appended to a new tape; launches still execute,
 //                            or are captured when the stream is capturing)
 //   tape_end() -> id         stop recording, keep the tape
-//   tape_replay(id)          re-issue the recorded launches on the current stream
+//   tape_replay(id, side)    re-issue the recorded launches on the current stream
+//                            (lane-1 launches on stream ``side``, see launch.h)
+//   tape_fork(side), tape_join()
+//                            record a fork onto / a join from the side stream
+//   tape_forks(id)           forks in a tape
 //   tape_size(id), tape_free(id)
 //   graph_node_counts(g)     [kernel, memcpy, memset, other] nodes of a captured
 //                            hipGraph_t (torch.cuda.CUDAGraph.raw_cuda_graph()):
@@ -34,6 +38,7 @@ namespace commeff {
 
 namespace {
 std::atomic<LaunchTape*> g_active{nullptr};
+std::atomic<hipStream_t> g_side{nullptr};
 std::mutex g_mu;
 std::map<int64_t, std::unique_ptr<LaunchTape>> g_tapes;
 int64_t g_next = 1;
@@ -43,6 +48,7 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUD
 }  // namespace
 
 LaunchTape* tape_active() { return g_active.load(std::memory_order_acquire); }
+hipStream_t tape_side_stream() { return g_side.load(std::memory_order_acquire); }
 
 namespace {
 
@@ -56,7 +62,9 @@ void tape_begin() {
 int64_t tape_end() {
   std::lock_guard<std::mutex> lk(g_mu);
   TORCH_CHECK(g_recording, "tape_end: no tape is recording");
+  TORCH_CHECK(!g_recording->open, "tape_end: a fork onto the side stream was not joined");
   g_active.store(nullptr, std::memory_order_release);
+  g_side.store(nullptr, std::memory_order_release);
   const int64_t id = g_next++;
   g_tapes[id] = std::move(g_recording);
   return id;
@@ -68,19 +76,76 @@ LaunchTape* get(int64_t id) {
   return it->second.get();
 }
 
-void tape_replay(int64_t id) {
+// (recording only; the eager fork / join is the caller's stream wait)
+void tape_fork(int64_t side) {
+  LaunchTape* t = tape_active();
+  if (t == nullptr) return;
+  TORCH_CHECK(side != 0, "tape_fork: no side stream");
+  const hipStream_t hs = reinterpret_cast<hipStream_t>(static_cast<intptr_t>(side));
+  const hipStream_t prev = g_side.load(std::memory_order_acquire);
+  TORCH_CHECK(prev == nullptr || prev == hs, "tape_fork: one side stream per tape");
+  g_side.store(hs, std::memory_order_release);
+  t->ops.emplace_back([](hipStream_t) {});
+  t->lane.push_back(2);
+  t->forks += 1;
+  t->open = true;
+}
+
+void tape_join() {
+  LaunchTape* t = tape_active();
+  if (t == nullptr || !t->open) return;
+  t->ops.emplace_back([](hipStream_t) {});
+  t->lane.push_back(3);
+  t->open = false;
+}
+
+void tape_replay(int64_t id, int64_t side) {
   LaunchTape* t;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     t = get(id);
   }
   const hipStream_t s = cur_stream();
-  for (auto& op : t->ops) op(s);
+  if (t->forks == 0) {
+    for (auto& op : t->ops) op(s);
+    return;
+  }
+  TORCH_CHECK(side != 0, "tape_replay: the tape forks onto a side stream; pass one");
+  const hipStream_t ss = reinterpret_cast<hipStream_t>(static_cast<intptr_t>(side));
+  TORCH_CHECK(ss != s, "tape_replay: the side stream is the replaying stream");
+  if (t->events.empty()) {
+    size_t n = 0;
+    for (uint8_t l : t->lane) n += l >= 2;
+    t->events.assign(n, nullptr);
+    for (auto& e : t->events)
+      TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "hipEventCreate failed");
+  }
+  size_t ev = 0;
+  for (size_t i = 0; i < t->ops.size(); ++i) {
+    switch (t->lane[i]) {
+      case 0: t->ops[i](s); break;
+      case 1: t->ops[i](ss); break;
+      default: {
+        const bool fork = t->lane[i] == 2;
+        hipEvent_t e = t->events[ev++];
+        TORCH_CHECK(hipEventRecord(e, fork ? s : ss) == hipSuccess, "tape_replay: hipEventRecord failed");
+        TORCH_CHECK(hipStreamWaitEvent(fork ? ss : s, e, 0) == hipSuccess, "tape_replay: hipStreamWaitEvent failed");
+      }
+    }
+  }
 }
 
-int64_t tape_size(int64_t id) {
+int64_t tape_forks(int64_t id) {
   std::lock_guard<std::mutex> lk(g_mu);
-  return static_cast<int64_t>(get(id)->ops.size());
+  return get(id)->forks;
+}
+
+int64_t tape_size(int64_t id) {  // launches + memsets (not forks / joins)
+  std::lock_guard<std::mutex> lk(g_mu);
+  const LaunchTape* t = get(id);
+  int64_t n = 0;
+  for (uint8_t l : t->lane) n += l < 2;
+  return n;
 }
 
 void tape_free(int64_t id) {
@@ -145,7 +210,10 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("zero_(Tensor(a!) t) -> ()", &commeff::zero_);
   m.def("tape_begin() -> ()", &commeff::tape_begin);
   m.def("tape_end() -> int", &commeff::tape_end);
-  m.def("tape_replay(int id) -> ()", &commeff::tape_replay);
+  m.def("tape_replay(int id, int side=0) -> ()", &commeff::tape_replay);
+  m.def("tape_fork(int side) -> ()", &commeff::tape_fork);
+  m.def("tape_join() -> ()", &commeff::tape_join);
+  m.def("tape_forks(int id) -> int", &commeff::tape_forks);
   m.def("tape_size(int id) -> int", &commeff::tape_size);
   m.def("tape_free(int id) -> ()", &commeff::tape_free);
   m.def("graph_node_counts(int graph) -> int[]", &commeff::graph_node_counts);

@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 
 from .._ext import ops as _ops
+from . import lanes as _lanes
 
 
 class _ReluMaxPool(torch.autograd.Function):
@@ -304,11 +305,14 @@ def _wgrad_to(g: torch.Tensor, x: torch.Tensor, weight: torch.Tensor):
     """Weight gradient of a native conv.  When ``weight.grad`` already exists
     (FedModel keeps every .grad as a view of its flat gradient buffer) the
     split-K reduction accumulates straight into it and None is handed back to
-    autograd -- no separate dW tensor and no AccumulateGrad add pass."""
+    autograd -- no separate dW tensor and no AccumulateGrad add pass -- on the
+    side lane (ops/lanes.py: it overlaps the input gradients of the layers
+    below; the engine joins it after the backward)."""
     gr = weight.grad
     if (gr is not None and gr.dtype == torch.float32 and gr.is_contiguous()
             and gr.device == g.device and tuple(gr.shape) == tuple(weight.shape)):
-        _ops().conv3x3_wgrad_into(g, x, gr)
+        with _lanes.fork(g, x):
+            _ops().conv3x3_wgrad_into(g, x, gr)
         _grad_written(weight)
         return None
     return _ops().conv3x3_wgrad(g, x)
@@ -462,6 +466,8 @@ class _Conv3x3Act(torch.autograd.Function):
                 g = _ops().relu_maxpool_backward(gout, aux, ctx.pool_k)
             else:
                 g = _ops().relu_mask(gout, aux)
+        # (the weight gradient first: on the side lane it overlaps the dgrad)
+        gw = _wgrad_to(g, x, ctx.weight) if ctx.needs_input_grad[1] else None
         gx = None
         if ctx.needs_input_grad[0]:
             link = ctx.in_link
@@ -472,7 +478,6 @@ class _Conv3x3Act(torch.autograd.Function):
                 ctx.in_mask.src, ctx.in_mask.masked = gx, gxm
             else:
                 gx = _ops().conv3x3_fwd(g, wt, False)
-        gw = _wgrad_to(g, x, ctx.weight) if ctx.needs_input_grad[1] else None
         return gx, gw, None, None, None
 
 
@@ -510,8 +515,9 @@ class _ResidualUnit(torch.autograd.Function):
         g2 = ctx.out_mask.take(g)  # masked by the consumer's dgrad epilogue
         if g2 is None:
             g2 = _ops().relu_mask(g, y2)
-        g1 = _ops().conv3x3_fwd(g2, w2t, False, y1)  # masked by relu(conv1) > 0
         dw2 = _wgrad_to(g2, y1, ctx.w2) if ctx.needs_input_grad[2] else None
+        g1 = _ops().conv3x3_fwd(g2, w2t, False, y1)  # masked by relu(conv1) > 0
+        dw1 = _wgrad_to(g1, x, ctx.w1) if ctx.needs_input_grad[1] else None
         gx = None
         if ctx.needs_input_grad[0]:
             link = ctx.in_link
@@ -519,7 +525,6 @@ class _ResidualUnit(torch.autograd.Function):
                 gx = link.park(_ops().conv3x3_fwd_unpool(g1, w1t, g, link.idx), x)
             else:
                 gx = _ops().conv3x3_fwd(g1, w1t, False, None, g)
-        dw1 = _wgrad_to(g1, x, ctx.w1) if ctx.needs_input_grad[1] else None
         return gx, dw1, dw2, None
 
 

@@ -43,6 +43,7 @@ from ..ops.grouped import GroupedGrads, grouped_grads
 from ..ops.nn import (image_generation, invalidate_conv_images,
                       prepared_conv_weights, set_conv_image_cache)
 from ..ops import CSVec
+from ..ops import lanes as _lanes
 from ..ops import transformer as _tx
 from ..utils.logging import PhaseTimer
 from . import dist
@@ -348,6 +349,8 @@ class FedModel:
         sinks = (self.flat.grad_sink_map() if (shadow is not None and want_grad
                                                 and not self._overlap_armed) else None)
         _tx.set_wgrad_stream(getattr(self.args, "wgrad_stream", "on") == "on")
+        # conv weight gradients on the side lane, unless gradient hooks read them mid-backward
+        _lanes.set_enabled(getattr(self.args, "wgrad_stream", "on") == "on" and not self._overlap_armed)
         with (self._autocast(cache=not capture) if shadow is None else nullcontext()), \
                 _tx.grad_sinks(sinks):
             with (ghost_batchnorm(model, groups) if (groups > 1 and self.has_bn)
@@ -369,6 +372,7 @@ class FedModel:
                 if loss_weight is not None:
                     total = total * loss_weight
                 total.backward()
+            _lanes.join()  # side-lane conv weight gradients into flat.g
             if sinks is not None:
                 _tx.join_wgrad_stream()  # side-stream weight gradients into flat.g
             if shadow is not None and not self._overlap_armed:

@@ -25,7 +25,8 @@ A round of fixed geometry is therefore recorded ONCE and replayed:
   dependencies -- a launch that bypassed the tape (a PyTorch kernel, a copy)
   or work forked onto a second stream (a replay issues no cross-stream
   waits) makes the geometry fall back to the eager path for good (with a
-  one-line warning naming the counts).
+  one-line warning naming the counts) -- except the side lane's recorded
+  forks / joins (ops/lanes.py), which the tape replays with event waits.
 
 The HIP graph itself is never launched (ROCm 7.2's graph packet capture
 faulted on the second replay of this round in round 1 and was throughput-
@@ -43,6 +44,7 @@ from typing import Callable, List, Optional
 import torch
 
 from .._ext import ops as _ops
+from ..ops import lanes as _lanes
 
 _REC: Optional["_Recording"] = None
 
@@ -54,11 +56,13 @@ class _Recording:
 
     def cut(self, fn: Callable[[], None]):
         """End the current tape, add an eager step (a collective), open the next tape."""
+        _lanes.join()  # (a tape's side-lane work ends inside it)
         self.segments.append(("tape", _ops().tape_end()))
         self.segments.append(("call", fn))
         _ops().tape_begin()
 
     def close(self):
+        _lanes.join()
         self.segments.append(("tape", _ops().tape_end()))
 
 
@@ -85,11 +89,12 @@ class Replay:
         self.graph = graph
         self.result = result
         self.valid = True
+        self.side = 0  # the side lane's stream handle (tapes with forks)
 
     def run(self, call_ctx=None):
         for kind, x in self.segments:
             if kind == "tape":
-                _ops().tape_replay(x)
+                _ops().tape_replay(x, self.side)
             elif call_ctx is not None:
                 with call_ctx():
                     x()
@@ -172,7 +177,12 @@ class RoundTapes:
         n_tape = sum(int(_ops().tape_size(x)) for kind, x in rec.segments if kind == "tape")
         rep = Replay(rec.segments, g, result)
         self._live.append(rep)
-        chain = len(counts) < 7 or (counts[4] <= 1 and counts[5] <= 1 and counts[6] <= 1)
+        forks = sum(int(_ops().tape_forks(x)) for kind, x in rec.segments if kind == "tape")
+        if forks:
+            # replayed as recorded: lane-1 launches on the side lane's stream,
+            # between event waits at the recorded forks / joins
+            rep.side = _lanes.side_stream(self.device).cuda_stream
+        chain = forks > 0 or len(counts) < 7 or (counts[4] <= 1 and counts[5] <= 1 and counts[6] <= 1)
         if counts[1] or counts[3] or counts[0] + counts[2] != n_tape or not chain:
             warnings.warn(f"launch tape for {key!r} incomplete (graph nodes: {counts[0]} kernels, "
                           f"{counts[1]} copies, {counts[2]} memsets, {counts[3]} other; tape: "

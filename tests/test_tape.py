@@ -30,7 +30,44 @@ def test_tape_records_native_launches_and_refuses_foreign_kernels():
     assert bad is None and "foreign" in tapes.failed
 
 
-def _bench_engine(mode: str, tape: str, W: int = 40, n: int = 5):
+@pytest.mark.gpu
+def test_tape_side_lane_fork_join_replays():
+    """A fork onto the side lane (ops/lanes.py) is recorded and replayed
+    with event waits; the side work is ordered after the main work before it
+    and the main work after the join waits for it."""
+    from commefficient_amd import ops
+    from commefficient_amd.ops import lanes
+    from commefficient_amd.parallel.tape import RoundTapes
+    from commefficient_amd._ext import ops as _ops
+    dev = torch.device("cuda", 0)
+    a = torch.ones(1 << 20, device=dev)
+    b = torch.ones(1 << 20, device=dev)
+    out = torch.zeros(4, device=dev)
+    lanes.set_enabled(True)
+
+    def body():
+        ops.zero_(a)
+        with lanes.fork(a):
+            ops.zero_(b)
+        lanes.join()
+        ops.zero_(out)
+
+    tapes = RoundTapes(dev)
+    rep = tapes.record("lane", body)
+    assert rep is not None and rep.side != 0
+    assert sum(int(_ops().tape_forks(x)) for k, x in rep.segments if k == "tape") == 1
+    torch.cuda.synchronize()
+    assert a.sum().item() == a.numel() and b.sum().item() == b.numel()
+    for _ in range(3):
+        a.fill_(1.0)
+        b.fill_(1.0)
+        tapes.replay(rep)
+        torch.cuda.synchronize()
+        assert a.abs().sum().item() == 0 and b.abs().sum().item() == 0
+    assert not lanes.pending()
+
+
+def _bench_engine(mode: str, tape: str, W: int = 40, n: int = 5, more=()):
     from commefficient_amd import models
     from commefficient_amd.data import make_synthetic
     from commefficient_amd.data.device_loader import DeviceFedLoader
@@ -48,7 +85,7 @@ def _bench_engine(mode: str, tape: str, W: int = 40, n: int = 5):
     args = parse_args(argv=["--dataset_name", "CIFAR10", "--synthetic", "--synthetic_size", "2000",
                             "--mode", mode, "--num_clients", "400", "--num_workers", str(W),
                             "--local_batch_size", "-1", "--weight_decay", "5e-4", "--dtype", "bf16",
-                            "--device", "cuda", "--seed", "21", "--round_tape", tape] + extra,
+                            "--device", "cuda", "--seed", "21", "--round_tape", tape] + extra + list(more),
                       probe_port=False)
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
@@ -84,12 +121,14 @@ def _run(fed, opt, loader, ds, W, rounds):
 def test_taped_rounds_bitwise_equal_eager(mode):
     rounds = 7
     res = {}
-    for tape in ("off", "auto"):
-        fed, opt, loader, ds, W = _bench_engine(mode, tape)
+    # eager / taped, and taped without the conv weight gradients' side lane
+    for tape, more in (("off", ()), ("auto", ()), ("auto1", ("--wgrad_stream", "off"))):
+        fed, opt, loader, ds, W = _bench_engine(mode, tape[:4], more=more)
         losses, dls = _run(fed, opt, loader, ds, W, rounds)
         res[tape] = (fed.w.clone(), losses, dls, fed.accountant.last_mod.clone(), fed.server.V.clone())
-        if tape == "auto":
+        if tape != "off":
             assert fed.last_round.get("taped"), (fed.last_round, fed._tapes.last_counts)
             assert fed._tapes.replays >= 2 * (rounds - 2), fed._tapes.replays
-    for a, b in zip(res["off"], res["auto"]):
-        assert torch.equal(a, b), (a - b).abs().max()
+    for other in ("auto", "auto1"):
+        for a, b in zip(res["off"], res[other]):
+            assert torch.equal(a, b), (other, (a - b).abs().max())
