@@ -2463,6 +2463,11 @@ TORCH_LIBRARY(commeff, m) {
         "Tensor(e!)? dadd=None) -> (Tensor, Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, int splits=0) -> Tensor");
   m.def("conv3x3_wgrad_into(Tensor dy, Tensor x, Tensor(a!) dw, int splits=0) -> ()");
+  m.def("conv3x3_wgrad_auto_splits(int P, int H, int W, int K, int C) -> int",
+        [](int64_t P, int64_t H, int64_t W, int64_t K, int64_t C) -> int64_t {
+          return commeff::conv3x3_wgrad_splits(static_cast<int>(P), static_cast<int>(H), static_cast<int>(W),
+                                               static_cast<int>(K), static_cast<int>(C));
+        });
   m.def("conv3x3_fwd_grouped(Tensor x, Tensor w, int G) -> Tensor");
   m.def("conv3x3_wgrad_grouped_ch(Tensor dy, Tensor x, int G) -> Tensor");
   m.def("conv3x3_wgrad_grouped(Tensor dy, Tensor x, int G, Tensor(a!) dw) -> ()");
