@@ -8,6 +8,7 @@ composition (CPU runs, fp32 runs, odd shapes).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import weakref
 
@@ -800,6 +801,15 @@ def cross_entropy_correct(logits: torch.Tensor, targets: torch.Tensor):
 #   * grouped / dilated convs stay on MIOpen.
 # Under ``ops.grouped.grouped_grads`` every path writes per-group weight
 # gradients instead (see ops/grouped.py).
+def _wlane(weight: torch.Tensor, gg, *inputs):
+    """The side lane (ops/lanes.py) for a weight gradient accumulated into a
+    sink -- the flat gradient or per-group rows -- that nothing in the
+    backward reads; inline otherwise (a gradient handed back to autograd)."""
+    if gg is not None or _grad_view(weight, weight.shape) is not None:
+        return _lanes.fork(*inputs)
+    return contextlib.nullcontext()
+
+
 def _grad_view(weight: torch.Tensor, shape):
     """``weight.grad`` viewed as ``shape`` when it can receive an in-place fp32
     accumulation (FedModel keeps every .grad as a flat-buffer view)."""
@@ -1020,6 +1030,10 @@ class _Conv1x1(torch.autograd.Function):
         n, c, H, W, h, w = ctx.dims
         k = wb.shape[0]
         g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        gw = None
+        if ctx.needs_input_grad[1]:  # (first: on the side lane it overlaps the dgrad)
+            with _wlane(ctx.weight, ctx.gg, g2d, x2d):
+                gw = _wgrad_1x1(ctx.weight, ctx.gg, g2d, x2d, k, c)
         gx = None
         if ctx.needs_input_grad[0]:
             gsub = _mm_nn(g2d, wb)
@@ -1028,17 +1042,6 @@ class _Conv1x1(torch.autograd.Function):
                 gx = _ops().col2im(gsub, n, H, W, c, 1, 1, s, 0)
             else:
                 gx = gsub.view(n, h, w, c).permute(0, 3, 1, 2)
-        gw = None
-        if ctx.needs_input_grad[1]:
-            if ctx.gg is not None:
-                G = ctx.gg.G
-                _wgrad_gemm(g2d, x2d, ctx.gg.view(ctx.weight).view(G, k, c), G)
-            else:
-                into = _grad_view(ctx.weight, (k, c))
-                gw = _wgrad_gemm(g2d, x2d, into)
-                gw = None if into is not None else gw.view(k, c, 1, 1)
-                if into is not None:
-                    _grad_written(ctx.weight)
         return gx, gw, None, None
 
 
@@ -1064,6 +1067,11 @@ class _Conv1x1Pass(torch.autograd.Function):
         n, c, h, w = x.shape
         k = wb.shape[0]
         g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        gw = None
+        if ctx.needs_input_grad[1]:
+            x2d = _nhwc2d(x)
+            with _wlane(ctx.weight, ctx.gg, g2d, x2d):
+                gw = _wgrad_1x1(ctx.weight, ctx.gg, g2d, x2d, k, c)
         gx = None
         if ctx.needs_input_grad[0]:
             if gid is not None:
@@ -1081,17 +1089,6 @@ class _Conv1x1Pass(torch.autograd.Function):
             else:
                 gx2d = _mm_nn(g2d, wb)
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
-        gw = None
-        if ctx.needs_input_grad[1]:
-            if ctx.gg is not None:
-                G = ctx.gg.G
-                _wgrad_gemm(g2d, _nhwc2d(x), ctx.gg.view(ctx.weight).view(G, k, c), G)
-            else:
-                into = _grad_view(ctx.weight, (k, c))
-                gw = _wgrad_gemm(g2d, _nhwc2d(x), into)
-                gw = None if into is not None else gw.view(k, c, 1, 1)
-                if into is not None:
-                    _grad_written(ctx.weight)
         return gx, gw, None
 
 
@@ -1146,6 +1143,13 @@ class _Conv1x1Pair(torch.autograd.Function):
             return _nhwc2d(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
         g1d = flat2d(g1) if g1 is not None else None
         g2d = flat2d(g2) if g2 is not None else None
+        gw1 = gw2 = None
+        if ctx.needs_input_grad[1] and g1d is not None:
+            with _wlane(ctx.w[0], ctx.gg[0], g1d, x2d):
+                gw1 = _wgrad_1x1(ctx.w[0], ctx.gg[0], g1d, x2d, k1, c)
+        if ctx.needs_input_grad[2] and g2d is not None:
+            with _wlane(ctx.w[1], ctx.gg[1], g2d, xs):
+                gw2 = _wgrad_1x1(ctx.w[1], ctx.gg[1], g2d, xs, k2, c)
         gx = None
         if ctx.needs_input_grad[0]:
             acc = None
@@ -1156,11 +1160,6 @@ class _Conv1x1Pair(torch.autograd.Function):
             if g1d is not None:
                 acc2d = _mm_nn(g1d, w1b, acc2d, in_place=True) if acc is not None else _mm_nn(g1d, w1b)
             gx = acc2d.view(n, H, W, c).permute(0, 3, 1, 2)
-        gw1 = gw2 = None
-        if ctx.needs_input_grad[1] and g1d is not None:
-            gw1 = _wgrad_1x1(ctx.w[0], ctx.gg[0], g1d, x2d, k1, c)
-        if ctx.needs_input_grad[2] and g2d is not None:
-            gw2 = _wgrad_1x1(ctx.w[1], ctx.gg[1], g2d, xs, k2, c)
         return gx, gw1, gw2, None, None, None
 
 
@@ -1211,24 +1210,29 @@ class _Conv3x3(torch.autograd.Function):
     def backward(ctx, gy):
         x, wt = ctx.saved_tensors
         g = gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        gx = _ops().conv3x3_fwd(g, wt, False) if ctx.needs_input_grad[0] else None
         gw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1]:  # (first: on the side lane it overlaps the dgrad)
             w = ctx.weight
             native = w.shape[0] % 128 == 0  # the native wgrad tiles need K % 128 == 0
             if native and ctx.gg is not None:
                 # every group's split-K slabs in one launch + a per-group reduction
                 gv = ctx.gg.view(w)
-                _ops().conv3x3_wgrad_grouped(g, x, gv.shape[0], gv.view(gv.shape[0], -1))
+                with _lanes.fork(g, x):
+                    _ops().conv3x3_wgrad_grouped(g, x, gv.shape[0], gv.view(gv.shape[0], -1))
             elif native:
                 gw = _wgrad_to(g, x, w)
             elif (_IMP_COL[0] and _GEMM_NATIVE[0] and x.shape[1] % 8 == 0 and _gpu_bf16_nhwc(x)
                   and x.data_ptr() % 16 == 0 and (ctx.gg is None or x.shape[0] % ctx.gg.G == 0)):
                 # K % 128 != 0: the TN GEMM over the implicit column image of x
-                gw = _col_wgrad(_nhwc2d(g), x, w, ctx.gg, (1, 1))
+                g2 = _nhwc2d(g)
+                with _wlane(w, ctx.gg, g2, x):
+                    gw = _col_wgrad(g2, x, w, ctx.gg, (1, 1))
             else:  # column-image GEMM (csrc/im2col.hip)
                 col = _ops().im2col(x, 3, 3, 1, 1, 9 * x.shape[1])
-                gw = _col_wgrad(_nhwc2d(g), col, w, ctx.gg)
+                g2 = _nhwc2d(g)
+                with _wlane(w, ctx.gg, g2, col):
+                    gw = _col_wgrad(g2, col, w, ctx.gg)
+        gx = _ops().conv3x3_fwd(g, wt, False) if ctx.needs_input_grad[0] else None
         return gx, gw, None
 
 
@@ -1320,12 +1324,13 @@ class _ConvCol(torch.autograd.Function):
         col, wt = ctx.saved_tensors
         N, C, H, W, R, S, stride, pad = ctx.geo
         g2d = _nhwc2d(gy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        gw = None
+        if ctx.needs_input_grad[1]:
+            with _wlane(ctx.weight, ctx.gg, g2d, col):
+                gw = _col_wgrad(g2d, col, ctx.weight, ctx.gg, (stride, pad) if ctx.imp else None)
         gx = None
         if ctx.needs_input_grad[0]:
             gx = _ops().col2im(_mm_nn(g2d, wt), N, H, W, C, R, S, stride, pad)
-        gw = None
-        if ctx.needs_input_grad[1]:
-            gw = _col_wgrad(g2d, col, ctx.weight, ctx.gg, (stride, pad) if ctx.imp else None)
         return gx, gw, None, None, None
 
 
