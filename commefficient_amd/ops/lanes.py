@@ -7,7 +7,7 @@ gradient, read only by the encode after the whole backward).  On one stream
 they alternate: each kernel's tail of idle CUs and the small reduction
 kernels sit on the critical path.  ``fork(*inputs)`` runs the enclosed
 launches on a side stream after everything issued so far on the main stream
-(the inputs are kept alive for it), ``join()`` orders the main stream after
+(the inputs are kept alive until the join), ``join()`` orders the main stream after
 the side stream before the gradient is read (parallel/fed_model.py, after
 the backward).
 
@@ -27,7 +27,8 @@ import torch
 
 from .._ext import ops as _ops
 
-_STATE = {"enabled": os.environ.get("COMMEFF_CONV_LANE", "1") != "0", "stream": None, "pending": None}
+_STATE = {"enabled": os.environ.get("COMMEFF_CONV_LANE", "1") != "0", "stream": None, "pending": None,
+          "held": []}
 _ENV_ON = _STATE["enabled"]
 
 
@@ -57,8 +58,11 @@ def fork(*inputs: torch.Tensor):
     side = side_stream(t0.device)
     side.wait_stream(main)
     _ops().tape_fork(side.cuda_stream)
-    for t in inputs:
-        t.record_stream(side)  # allocated on the main stream: keep until the side lane read it
+    # inputs allocated on the main stream stay referenced until the join (not
+    # record_stream: its deferred frees kept the caching allocator growing --
+    # 16 -> 388 device allocations per 6 ImageNet rounds); freed after the
+    # main stream's wait on the side lane, any reuse is ordered after it
+    _STATE["held"].extend(inputs)
     _STATE["pending"] = main
     with torch.cuda.stream(side):
         yield
@@ -72,6 +76,7 @@ def join() -> None:
     _STATE["pending"] = None
     main.wait_stream(_STATE["stream"])
     _ops().tape_join()
+    _STATE["held"].clear()
 
 
 def pending() -> bool:
