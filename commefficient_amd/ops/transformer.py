@@ -39,6 +39,7 @@ import torch
 import torch.nn.functional as F
 
 from .._ext import ops as _ops
+from . import lanes as _lanes
 
 _M32 = 0xFFFFFFFF
 
@@ -259,13 +260,13 @@ def _acc_mm(sink: torch.Tensor, a: torch.Tensor, b: torch.Tensor, blas: bool = F
         sink.add_(a.float() @ b.float())
 
 
-# Weight-gradient GEMMs into the sinks run on a side stream: they have few
-# output tiles (768 x 768 .. 768 x 3072 over K = tokens: 36-144 tiles of
-# 128 x 128 on 256 CUs) and nothing in the backward waits for them, so they
-# overlap the input-gradient GEMMs, attention backward and junction kernels
-# of the layers below.  ``join_wgrad_stream()`` orders the main stream after
-# them before the flat gradient is read.
-_SIDE: dict = {"enabled": True, "stream": None, "pending": False}
+# Weight-gradient GEMMs into the sinks run on the side lane (ops/lanes.py):
+# they have few output tiles (768 x 768 .. 768 x 3072 over K = tokens: 36-144
+# tiles of 128 x 128 on 256 CUs) and nothing in the backward waits for them,
+# so they overlap the input-gradient GEMMs, attention backward and junction
+# kernels of the layers below.  ``join_wgrad_stream()`` orders the main
+# stream after them before the flat gradient is read.
+_SIDE: dict = {"enabled": True}
 
 
 def set_wgrad_stream(enabled: bool) -> None:
@@ -273,9 +274,7 @@ def set_wgrad_stream(enabled: bool) -> None:
 
 
 def join_wgrad_stream() -> None:
-    if _SIDE["pending"]:
-        torch.cuda.current_stream().wait_stream(_SIDE["stream"])
-        _SIDE["pending"] = False
+    _lanes.join()
 
 
 _ATTN = {"enabled": True}
@@ -283,12 +282,6 @@ _ATTN = {"enabled": True}
 
 def set_fused_attention(enabled: bool) -> None:
     _ATTN["enabled"] = bool(enabled)
-
-
-def _side_stream(device) -> "torch.cuda.Stream":
-    if _SIDE["stream"] is None:
-        _SIDE["stream"] = torch.cuda.Stream(device=device)
-    return _SIDE["stream"]
 
 
 # The junction backward's column sums (LayerNorm dgamma / dbeta, the branch
@@ -307,29 +300,16 @@ def _colsum_deferred(t: torch.Tensor, *sinks) -> bool:
 def _side_colsum(part: torch.Tensor, q: int, sinks) -> None:
     """sinks[i] += column sums of the block partials ``part`` (quantity i),
     on the weight-gradient side stream after the producing kernel."""
-    main = torch.cuda.current_stream()
-    side = _side_stream(part.device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
+    with _lanes.fork(part):
         _ops().colsum_into(part, q, *sinks)
-    part.record_stream(side)
-    _SIDE["pending"] = True
 
 
 def _wgrad(sink, a, b, blas: bool = False):
     if sink is None:
         return torch.mm(a, b)
     if sink.is_cuda and _SIDE["enabled"]:
-        main = torch.cuda.current_stream()
-        side = _side_stream(sink.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
+        with _lanes.fork(a, b):  # (the operands stay referenced until the join)
             _acc_mm(sink, a, b, blas)
-        # the operands were allocated on the main stream: keep their memory
-        # until the side stream has consumed them
-        a.record_stream(side)
-        b.record_stream(side)
-        _SIDE["pending"] = True
         return None
     _acc_mm(sink, a, b, blas)
     return None
