@@ -56,6 +56,10 @@ def fork(*inputs: torch.Tensor):
         return
     main = torch.cuda.current_stream(t0.device)
     side = side_stream(t0.device)
+    if main == side:  # (nested: already on the lane)
+        _STATE["held"].extend(inputs)
+        yield
+        return
     side.wait_stream(main)
     _ops().tape_fork(side.cuda_stream)
     # inputs allocated on the main stream stay referenced until the join (not

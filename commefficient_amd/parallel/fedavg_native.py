@@ -46,6 +46,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from .. import _ext
+from ..ops import lanes as _lanes
 
 
 def _ops():
@@ -296,7 +297,14 @@ class ResNet18FedAvg:
         """fp32 A_g @ B_g (bf16 operands) into the sink's rows at ``off`` (they
         are in the product's order): the gradient itself, or -- the fused SGD
         step -- rows = beta rows + alpha A_g @ B_g in the GEMM's epilogue, then
-        the bf16 mirror of the updated segment"""
+        the bf16 mirror of the updated segment.  On the side lane
+        (ops/lanes.py): the rows it updates were read by the layer's input
+        gradient, enqueued before; the step joins the lane before it returns."""
+        with _lanes.fork(A, B):
+            cls._bmm_rows_impl(sink, off, A, B)
+
+    @classmethod
+    def _bmm_rows_impl(cls, sink, off, A, B):
         G, K, n = A.shape[0], A.shape[1], B.shape[2]
         # (the stem's 27 columns stay on hipBLASLt: its [64 x 27] products over
         # 5,120 pixels are 100 one-tile blocks of 80 K-steps on the TN GEMM --
@@ -332,6 +340,11 @@ class ResNet18FedAvg:
             _ops().fa_cast_rows(sink.mirror, sink.dst, sink.ld, sink.dst.shape[0], off, n)
 
     def _conv3_wgrad(self, dy, x, G, sink, off, K, C):
+        # (on the side lane, after the layer's input gradient: see _bmm_rows)
+        with _lanes.fork(dy, x):
+            self._conv3_wgrad_impl(dy, x, G, sink, off, K, C)
+
+    def _conv3_wgrad_impl(self, dy, x, G, sink, off, K, C):
         # 32x32 maps on the grouped halo wgrad; 16x16 and smaller on the TN
         # GEMM over the implicit column image (27.59 vs 27.97 ms per round with
         # the halo kernel on 16x16 too, 27.88 with the TN GEMM on 32x32 too;
@@ -557,12 +570,16 @@ class ResNet18FedAvg:
                 dctr = dcg[:, :, 4 * b.cin:5 * b.cin]
                 _gmm(_gview(da, G), self._rows(Wb, ld, G, b.sc, b.cout, b.cin), dctr, True, 1.0)
                 A1, Asc = _gview(dh1, G).transpose(1, 2), _gview(da, G).transpose(1, 2)
-                if colx is None and not (
-                        ops.fa_bmm_rows(A1, _carrier(xin, G, P1, 9 * b.cin), sink.dst, sink.ld, b.conv1, sink.beta,
-                                        sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xin, 3, 2, 1)
-                        and ops.fa_bmm_rows(Asc, _carrier(xin, G, P1, b.cin), sink.dst, sink.ld, b.sc, sink.beta,
-                                            sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xin, 1, 2, 0)):
-                    raise RuntimeError("ResNet18FedAvg: implicit strided weight update refused after its forward")
+                if colx is None:
+                    with _lanes.fork(A1, Asc, xin):
+                        ok = (ops.fa_bmm_rows(A1, _carrier(xin, G, P1, 9 * b.cin), sink.dst, sink.ld, b.conv1,
+                                              sink.beta, sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld,
+                                              xin, 3, 2, 1)
+                              and ops.fa_bmm_rows(Asc, _carrier(xin, G, P1, b.cin), sink.dst, sink.ld, b.sc,
+                                                  sink.beta, sink.alpha, sink.mirror, self._TN[1], sink.src,
+                                                  sink.sld, xin, 1, 2, 0))
+                    if not ok:
+                        raise RuntimeError("ResNet18FedAvg: implicit strided weight update refused after its forward")
                 if colx is not None:
                     cg = colx.transpose(0, 1)
                     self._bmm_rows(sink, b.conv1, A1, cg)
@@ -571,6 +588,7 @@ class ResNet18FedAvg:
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        _lanes.join()  # (the next step reads the updated rows)
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
 
 
@@ -777,6 +795,7 @@ class ResNet9FedAvg(ResNet18FedAvg):
         # ---- stem weight gradient
         dy0 = ops.relu_mask(da0, a0)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        _lanes.join()  # (the next step reads the updated rows)
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
 
 
@@ -967,6 +986,7 @@ class FixupResNet9FedAvg(ResNet9FedAvg):
         part = ops.fa_affine_bwd(dcol, G, False, W, ld, -1, None, self._ones_col(x, G, Kc0), None, False, False)[2]
         sgd(part, s="bias1a")
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        _lanes.join()  # (the next step reads the updated rows)
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
 
 
@@ -1137,15 +1157,20 @@ class FixupResNet18FedAvg(ResNet18FedAvg):
                 _gmm(_gview(dpre, G), self._rows(Wb, ld, G, b.sc, b.cout, b.cin), dcg[:, :, 4 * b.cin:5 * b.cin],
                      True, 1.0)
                 A1, Asc = _gview(dc1, G).transpose(1, 2), _gview(dpre, G).transpose(1, 2)
-                if not (ops.fa_bmm_rows(A1, _carrier(xa, G, P1, 9 * b.cin), sink.dst, sink.ld, b.conv1, sink.beta,
-                                        sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xa, 3, 2, 1)
-                        and ops.fa_bmm_rows(Asc, _carrier(xin, G, P1, b.cin), sink.dst, sink.ld, b.sc, sink.beta,
-                                            sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld, xin, 1, 2, 0)):
+                with _lanes.fork(A1, Asc, xa, xin):
+                    ok = (ops.fa_bmm_rows(A1, _carrier(xa, G, P1, 9 * b.cin), sink.dst, sink.ld, b.conv1,
+                                          sink.beta, sink.alpha, sink.mirror, self._TN[1], sink.src, sink.sld,
+                                          xa, 3, 2, 1)
+                          and ops.fa_bmm_rows(Asc, _carrier(xin, G, P1, b.cin), sink.dst, sink.ld, b.sc,
+                                              sink.beta, sink.alpha, sink.mirror, self._TN[1], sink.src,
+                                              sink.sld, xin, 1, 2, 0))
+                if not ok:
                     raise RuntimeError("FixupResNet18FedAvg: implicit strided weight update refused")
                 da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        _lanes.join()  # (the next step reads the updated rows)
         return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
 
 
