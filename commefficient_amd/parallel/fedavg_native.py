@@ -53,6 +53,15 @@ def _ops():
     return _ext.ops()
 
 
+def _step_means(ts: List[torch.Tensor]) -> torch.Tensor:
+    """Per-client mean over the local steps of the per-step means of [G, n_s]
+    tensors: one stack + mean when every step has the same n (no per-step
+    reduction kernels)."""
+    if all(t.shape == ts[0].shape for t in ts):
+        return torch.stack(ts).mean(dim=(0, 2))
+    return sum(t.mean(1) for t in ts) / len(ts)
+
+
 def _gview(t: torch.Tensor, G: int) -> torch.Tensor:
     """[n, G*K, H, W] channels_last -> [G, n*H*W, K] strided view (per-client
     GEMM operand / output: batch stride K, row stride G*K)."""
@@ -223,6 +232,22 @@ class ResNet18FedAvg:
         for b in self.blocks:
             convs += [(b.conv1, b.cout, b.cin), (b.conv2, b.cout, b.cout)]
         return self._perm_convs(device, convs)
+
+    _col_cache = None
+    _col_ok = False
+
+    def _stem_col(self, x: torch.Tensor, G: int, Kc0: int) -> torch.Tensor:
+        """The stem's grouped column image of x; full-batch local steps read the
+        same input every step, so it is built once per round (``run`` resets the
+        cache)."""
+        key = (x.data_ptr(), tuple(x.shape), tuple(x.stride()), G, Kc0)
+        c = self._col_cache
+        if self._col_ok and c is not None and c[0] == key:
+            return c[1]
+        col = _ops().im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        if self._col_ok:
+            self._col_cache = (key, col)
+        return col
 
     @staticmethod
     def _rows(Wt: torch.Tensor, ld: int, G: int, off: int, K: int, n: int) -> torch.Tensor:
@@ -412,8 +437,9 @@ class ResNet18FedAvg:
             run_bufs.append(buf)
             run.append(tuple(buf[i].view(-1) for i in range(4)))
         nbt = self.blocks[0].m1.num_batches_tracked if first_pass else None
-        loss_acc = torch.zeros(G, device=dev)
-        acc_acc = torch.zeros(G, device=dev)
+        ls, cs = [], []  # per-step [G n] losses / correctness, reduced once at the end
+        self._col_cache = None
+        self._col_ok = bs >= n  # (full-batch steps: the same input every step)
         ones = torch.ones((G, max(n, bs), 1), device=dev)
         steps = 0
         xv = x.view(G, n, *x.shape[1:]) if bs < n else None
@@ -437,8 +463,8 @@ class ResNet18FedAvg:
                 sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, None if last else Wb, W, sld) if fused
                         else _Sink(Gg, ld, 0.0, 1.0, None))
                 l, c = self._step(xb, yb, G, s1 - s0, W, Wbf, sld, sink, run, nbt, ones)
-                loss_acc += l
-                acc_acc += c
+                ls.append(l.view(G, -1))
+                cs.append(c.view(G, -1))
                 if not fused:
                     ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip), lr_t, float(wd), Wb)
                 steps += 1
@@ -446,7 +472,7 @@ class ResNet18FedAvg:
         # running statistics: per-client copies summed for the caller's mean,
         # [4, C] fp64 per block (mean 1, mean 2, var 1, var 2)
         sums = [torch.sum(buf, dim=1, dtype=torch.float64) for buf in run_bufs]
-        return loss_acc / steps, acc_acc / steps, sums
+        return _step_means(ls), _step_means(cs), sums
 
     def _step(self, x, y, G, n, W, Wb, ld, sink, run, nbt, ones):
         """One local step of every client (fp32 rows W, bf16 mirror Wb, both
@@ -459,7 +485,7 @@ class ResNet18FedAvg:
         # the first 27)
         C0, K0 = self.cin0, self.c0
         Kc0 = (9 * C0 + 63) // 64 * 64 if _NATIVE_GMM[0] else (9 * C0 + 7) // 8 * 8
-        col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        col0 = self._stem_col(x, G, Kc0)
         col0g = col0.transpose(0, 1)[:, :, :9 * C0]
         H, Wd = x.shape[2], x.shape[3]
         y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
@@ -589,7 +615,7 @@ class ResNet18FedAvg:
         dy0 = ops.relu_mask(da, a0)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
         _lanes.join()  # (the next step reads the updated rows)
-        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+        return loss, correct
 
 
 class ResNet9FedAvg(ResNet18FedAvg):
@@ -681,8 +707,9 @@ class ResNet9FedAvg(ResNet18FedAvg):
         Wb = torch.empty((G, ld), device=dev, dtype=torch.bfloat16)
         fused = not clip
         Gg = None if fused else torch.zeros((G, ld), device=dev, dtype=torch.float32)
-        loss_acc = torch.zeros(G, device=dev)
-        acc_acc = torch.zeros(G, device=dev)
+        ls, cs = [], []
+        self._col_cache = None
+        self._col_ok = bs >= n
         steps = 0
         xv = x.view(G, n, *x.shape[1:]) if bs < n else None
         for _ in range(epochs):
@@ -702,20 +729,20 @@ class ResNet9FedAvg(ResNet18FedAvg):
                 sink = (_Sink(Wg, ld, 1.0 - lr_t * wd, -lr_t, None if last else Wb, W, sld) if fused
                         else _Sink(Gg, ld, 0.0, 1.0, None))
                 l, c = self._step9(xb, yb, G, s1 - s0, W, Wbf, sld, sink)
-                loss_acc += l
-                acc_acc += c
+                ls.append(l.view(G, -1))
+                cs.append(c.view(G, -1))
                 if not fused:
                     ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip), lr_t, float(wd), Wb)
                 steps += 1
         ops.fa_upload(out, w0i, Wg, ld, G, float(n), perm)
-        return loss_acc / steps, acc_acc / steps, []
+        return _step_means(ls), _step_means(cs), []
 
     def _step9(self, x, y, G, n, W, Wb, ld, sink):
         ops = _ops()
         # ---- stem (as ResNet18FedAvg._step): grouped column image x weight rows
         C0, K0 = self.cin0, self.c0
         Kc0 = (9 * C0 + 63) // 64 * 64 if _NATIVE_GMM[0] else (9 * C0 + 7) // 8 * 8
-        col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        col0 = self._stem_col(x, G, Kc0)
         col0g = col0.transpose(0, 1)[:, :, :9 * C0]
         H, Wd = x.shape[2], x.shape[3]
         y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
@@ -796,7 +823,7 @@ class ResNet9FedAvg(ResNet18FedAvg):
         dy0 = ops.relu_mask(da0, a0)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
         _lanes.join()  # (the next step reads the updated rows)
-        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+        return loss, correct
 
 
 class FixupResNet9FedAvg(ResNet9FedAvg):
@@ -987,7 +1014,7 @@ class FixupResNet9FedAvg(ResNet9FedAvg):
         sgd(part, s="bias1a")
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
         _lanes.join()  # (the next step reads the updated rows)
-        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+        return loss, correct
 
 
 class FixupResNet18FedAvg(ResNet18FedAvg):
@@ -1076,7 +1103,7 @@ class FixupResNet18FedAvg(ResNet18FedAvg):
         # ---- stem (as ResNet18FedAvg._step): relu(conv(x))
         C0, K0 = self.cin0, self.c0
         Kc0 = (9 * C0 + 63) // 64 * 64
-        col0 = ops.im2col_grouped(x, G, 3, 3, 1, 1, Kc0, True)
+        col0 = self._stem_col(x, G, Kc0)
         col0g = col0.transpose(0, 1)[:, :, :9 * C0]
         H, Wd = x.shape[2], x.shape[3]
         y0 = torch.empty((n, G * K0, H, Wd), device=x.device, dtype=torch.bfloat16,
@@ -1171,7 +1198,7 @@ class FixupResNet18FedAvg(ResNet18FedAvg):
         dy0 = ops.relu_mask(da, a0)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
         _lanes.join()  # (the next step reads the updated rows)
-        return loss.view(G, n).mean(1), correct.view(G, n).mean(1)
+        return loss, correct
 
 
 def engine_for(model, args):
