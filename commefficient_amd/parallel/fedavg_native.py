@@ -318,13 +318,16 @@ class ResNet18FedAvg:
     _TN = [True, 1]
 
     @classmethod
-    def _bmm_rows(cls, sink, off, A, B):
+    def _bmm_rows(cls, sink, off, A, B, lane: bool = True):
         """fp32 A_g @ B_g (bf16 operands) into the sink's rows at ``off`` (they
         are in the product's order): the gradient itself, or -- the fused SGD
         step -- rows = beta rows + alpha A_g @ B_g in the GEMM's epilogue, then
         the bf16 mirror of the updated segment.  On the side lane
         (ops/lanes.py): the rows it updates were read by the layer's input
         gradient, enqueued before; the step joins the lane before it returns."""
+        if not lane:
+            cls._bmm_rows_impl(sink, off, A, B)
+            return
         with _lanes.fork(A, B):
             cls._bmm_rows_impl(sink, off, A, B)
 
@@ -613,7 +616,9 @@ class ResNet18FedAvg:
                 da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)
-        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        # (the stem update on the main stream: it has nothing left to do while
+        # the lane finishes the last blocks' updates)
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
         _lanes.join()  # (the next step reads the updated rows)
         return loss, correct
 
@@ -821,7 +826,9 @@ class ResNet9FedAvg(ResNet18FedAvg):
         da0 = back(ops.relu_maxpool_backward(dp1, c1, 2), a0, "layer1")
         # ---- stem weight gradient
         dy0 = ops.relu_mask(da0, a0)
-        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        # (the stem update on the main stream: it has nothing left to do while
+        # the lane finishes the last blocks' updates)
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
         _lanes.join()  # (the next step reads the updated rows)
         return loss, correct
 
@@ -1012,7 +1019,9 @@ class FixupResNet9FedAvg(ResNet9FedAvg):
             torch.bmm(_gview(dy0, G), pad, out=_gview(dcol, G))
         part = ops.fa_affine_bwd(dcol, G, False, W, ld, -1, None, self._ones_col(x, G, Kc0), None, False, False)[2]
         sgd(part, s="bias1a")
-        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        # (the stem update on the main stream: it has nothing left to do while
+        # the lane finishes the last blocks' updates)
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
         _lanes.join()  # (the next step reads the updated rows)
         return loss, correct
 
@@ -1196,7 +1205,9 @@ class FixupResNet18FedAvg(ResNet18FedAvg):
                 da = ops.col2im_grouped(dcol, G, nn_, Hi, Wi, b.cin, 3, 3, 2, 1)
         # ---- stem weight gradient (ReLU backward through its output)
         dy0 = ops.relu_mask(da, a0)
-        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g)
+        # (the stem update on the main stream: it has nothing left to do while
+        # the lane finishes the last blocks' updates)
+        self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
         _lanes.join()  # (the next step reads the updated rows)
         return loss, correct
 
