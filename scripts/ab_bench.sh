@@ -3,7 +3,7 @@
 # alternates the variants ROUNDS times, one JSON line each into
 # gpurun_out/${TAG}_ab.jsonl.
 #   A="--wgrad-stream off" B="--wgrad-stream on" ROUNDS=3 bash scripts/ab_bench.sh
-# AENV / BENV: environment assignments for a variant (AENV="COMMEFF_X=0")
+# AENV / BENV: environment assignments for a variant (AENV="COMMEFF_CONV_LANE=0")
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 TAG=${TAG:-ab}

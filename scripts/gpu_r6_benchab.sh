@@ -1,5 +1,5 @@
 # A/B of an environment switch on the driver-shaped headline bench only,
-# alternating over VALS of VAR twice (e.g. VAR=COMMEFF_LANE_SPLIT_DIV VALS="1 2")
+# alternating over VALS of VAR twice (e.g. VAR=COMMEFF_CONV_LANE VALS="1 0")
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-r6benchab}; mkdir -p $O
