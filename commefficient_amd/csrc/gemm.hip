@@ -350,7 +350,47 @@ void launch_gemm_t(const GemmArgs& a, hipStream_t stream) {
   COMMEFF_LAUNCH((gemm_kernel<BN, NN, ACT, F32, ST, IMP>), dim3(tiles), dim3(256), lds, stream, a);
 }
 
+// split-K NN (mm_nn_splitk): out bf16 [M, N] = sum over the S fp32 partial
+// products part [S][M][N] in split order + the K tail [k0, k1) that no split
+// covered (the tied LM head's dh: K = 50,257 = 16 splits of 49 K-steps + 81
+// rows), one 8-column chunk per thread, fixed order: deterministic
+__global__ void __launch_bounds__(256) splitk_tail_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                          const uint16_t* __restrict__ A, int64_t lda,
+                                                          const uint16_t* __restrict__ B, int64_t ldb, int k0,
+                                                          int k1, uint16_t* __restrict__ out, int64_t ldo) {
+  const int n8 = N / 8;
+  const int64_t q = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (q >= static_cast<int64_t>(M) * n8) return;
+  const int m = static_cast<int>(q / n8), c = static_cast<int>(q - static_cast<int64_t>(m) * n8) * 8;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    const float* p = part + (static_cast<int64_t>(s) * M + m) * N + c;
+    const float4 lo = *reinterpret_cast<const float4*>(p), hi = *reinterpret_cast<const float4*>(p + 4);
+    v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
+    v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
+  }
+  const uint16_t* ar = A + static_cast<int64_t>(m) * lda;
+  for (int k = k0; k < k1; ++k) {
+    const float av = bf2f(ar[k]);
+    const v4u bv = *reinterpret_cast<const v4u*>(B + static_cast<int64_t>(k) * ldb + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaf(av, bf2f((bv[j >> 1] >> (16 * (j & 1))) & 0xffffu), v[j]);
+  }
+  v4u o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = pack_bf16(v[2 * j], v[2 * j + 1]);
+  *reinterpret_cast<v4u*>(out + static_cast<int64_t>(m) * ldo + c) = o;
+}
+
 }  // namespace
+
+void launch_splitk_tail(const float* part, int S, int M, int N, const uint16_t* A, int64_t lda, const uint16_t* B,
+                        int64_t ldb, int k0, int k1, uint16_t* out, int64_t ldo, hipStream_t stream) {
+  const int64_t n = static_cast<int64_t>(M) * (N / 8);
+  if (n == 0) return;
+  COMMEFF_LAUNCH(splitk_tail_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, stream, part, S,
+                 M, N, A, lda, B, ldb, k0, k1, out, ldo);
+}
 
 bool gemm_supported(int M, int N, int K, bool nn) {
   (void)nn;

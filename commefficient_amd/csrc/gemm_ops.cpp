@@ -92,6 +92,53 @@ at::Tensor mm_nn(const at::Tensor& a, const at::Tensor& b, const c10::optional<a
   return mm_impl(a, b, true, bias, out, beta, act, pre);
 }
 
+// a [M, K] b [K, N] -> bf16 [M, N] for a long K and few output tiles (the tied
+// LM head's dh = g W, K = 50,257, M x N = T x 768: 30 tiles): S groups of Kc
+// K-steps on the grouped NN GEMM into fp32 partials (splits ~ one wave of
+// 512 block slots, >= 16 K-steps each; the K tail past S Kc -- any K -- is
+// folded into the reduction kernel), then one fixed-order reduction.  Only a's
+// first K columns and b's first K rows are read.  CPU: the fp32 reference.
+at::Tensor mm_nn_splitk(const at::Tensor& a, const at::Tensor& b, int64_t splits) {
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+                  a.stride(1) == 1 && b.stride(1) == 1 && a.size(1) == b.size(0),
+              "mm_nn_splitk: bf16 a [M, K], b [K, N] with unit column strides");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  if (!a.is_cuda()) return at::mm(a.to(at::kFloat), b.to(at::kFloat)).to(at::kBFloat16);
+  TORCH_CHECK(N % 64 == 0 && N >= 64 && K >= 64 && M >= 1 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+              "mm_nn_splitk: N % 64 == 0, K >= 64, 16-byte aligned operands and row strides");
+  const int64_t steps = K / 64;
+  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  int64_t S = splits > 0 ? splits : std::max<int64_t>(1, std::min<int64_t>(16, 512 / tiles));
+  S = std::max<int64_t>(1, std::min<int64_t>(S, steps / 16 > 0 ? steps / 16 : 1));
+  const int64_t Kc = (steps / S) * 64, Kmain = S * Kc;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  const hipStream_t st = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  auto part = at::empty({S, M, N}, a.options().dtype(at::kFloat));
+  auto out = at::empty({M, N}, a.options());
+  GemmArgs g{};
+  g.A = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  g.lda = a.stride(0);
+  g.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  g.ldb = b.stride(0);
+  g.C = part.data_ptr();
+  g.ldc = N;
+  g.M = static_cast<int>(M);
+  g.N = static_cast<int>(N);
+  g.K = static_cast<int>(Kc);
+  g.beta = 0.f;
+  g.G = static_cast<int>(S);
+  g.sa = Kc;
+  g.sb = Kc * b.stride(0);
+  g.sc = M * N;
+  launch_gemm(g, true, 0, true, st);
+  launch_splitk_tail(part.data_ptr<float>(), static_cast<int>(S), static_cast<int>(M), static_cast<int>(N),
+                     g.A, a.stride(0), g.B, b.stride(0), static_cast<int>(Kmain), static_cast<int>(K),
+                     reinterpret_cast<uint16_t*>(out.data_ptr()), N, st);
+  return out;
+}
+
 // (a b^T bf16 [M, N], tile moments fp32 [ceil(M / 128), 4, N]): the forward
 // of a conv feeding a ghost batch norm of G groups of M / G rows, with the
 // norm's per-128-row-tile mean / M2 (split at group boundaries) written by the
@@ -218,6 +265,7 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
   m.def("mm_nn(Tensor a, Tensor b, Tensor? bias=None, Tensor(c!)? out=None, float beta=0.0, int act=0, "
         "Tensor(d!)? pre=None) -> Tensor");
   m.def("mm_nt_bnstats(Tensor a, Tensor b, int G) -> (Tensor, Tensor)");
+  m.def("mm_nn_splitk(Tensor a, Tensor b, int splits=0) -> Tensor");
   m.def("conv_nt_imp(Tensor x, Tensor w, int R, int stride, int pad, int G) -> (Tensor, Tensor)");
 }
 
@@ -225,11 +273,13 @@ TORCH_LIBRARY_IMPL(commeff, CPU, m) {
   m.impl("mm_nt", &commeff::mm_nt);
   m.impl("mm_nn", &commeff::mm_nn);
   m.impl("mm_nt_bnstats", &commeff::mm_nt_bnstats);
+  m.impl("mm_nn_splitk", &commeff::mm_nn_splitk);
 }
 
 TORCH_LIBRARY_IMPL(commeff, CUDA, m) {
   m.impl("mm_nt", &commeff::mm_nt);
   m.impl("mm_nn", &commeff::mm_nn);
   m.impl("mm_nt_bnstats", &commeff::mm_nt_bnstats);
+  m.impl("mm_nn_splitk", &commeff::mm_nn_splitk);
   m.impl("conv_nt_imp", &commeff::conv_nt_imp);
 }

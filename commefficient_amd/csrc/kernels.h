@@ -652,6 +652,8 @@ void launch_fa_scalar_sgd(const float* part, int chunks, int G, float* dst, int6
 bool gemm_supported(int M, int N, int K, bool nn);
 bool gemm_supported_nedge(int M, int N, int K);
 void launch_gemm(const GemmArgs& a, bool nn, int act, bool f32, hipStream_t stream);
+void launch_splitk_tail(const float* part, int S, int M, int N, const uint16_t* A, int64_t lda, const uint16_t* B,
+                        int64_t ldb, int k0, int k1, uint16_t* out, int64_t ldo, hipStream_t stream);
 struct GemmTnArgs {
   const uint16_t* A;
   int64_t lda;

@@ -493,7 +493,7 @@ class _LMHead(torch.autograd.Function):
     that gradient straight into the tied weight's fp32 sink on the
     weight-gradient side stream (hipBLASLt fp32-output GEMM; COMMEFF_LM_DW=tn:
     the native TN GEMM with its M = V edge tile), dh = g W (K = 50,257, only
-    T x H outputs) on hipBLASLt.  No padded copies of W or of the gradient,
+    T x H outputs) on the native split-K NN GEMM (``mm_nn_splitk``).  No padded copies of W or of the gradient,
     no bf16 dW + accumulation pass (HF's lm_head on hipBLASLt; reference
     model: gpt2_train.py:262-273)."""
 
@@ -513,7 +513,12 @@ class _LMHead(torch.autograd.Function):
         g = g.to(torch.bfloat16)
         if g.stride(1) != 1:
             g = g.contiguous()
-        dh = torch.mm(g, W) if ctx.needs_input_grad[0] else None
+        dh = None
+        if ctx.needs_input_grad[0]:
+            # split-K native NN GEMM (K = V, only T x H outputs; the K tail in its
+            # reduction), COMMEFF_LM_DH=blas: hipBLASLt
+            dh = (_ops().mm_nn_splitk(g, W) if _LM_DH_NATIVE and g.stride(0) % 8 == 0 and W.shape[1] % 64 == 0
+                  else torch.mm(g, W))
         dW = None
         if ctx.needs_input_grad[1]:
             if ctx.sink is not None:
@@ -530,6 +535,7 @@ class _LMHead(torch.autograd.Function):
 # buffers every call and was slower than hipBLASLt (699 vs 377 us isolated).
 _LM_NATIVE = os.environ.get("COMMEFF_LM_HEAD", "native") == "native"
 _LM_DW_TN = os.environ.get("COMMEFF_LM_DW", "blas") == "tn"
+_LM_DH_NATIVE = os.environ.get("COMMEFF_LM_DH", "native") == "native"
 
 
 def lm_head(m, h: torch.Tensor) -> torch.Tensor:

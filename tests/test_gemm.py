@@ -166,3 +166,25 @@ def test_gemm_tn_parts_sum_to_product(G, T, M, N):
     got = parts.view(G, S, M, N).sum(1)
     ref = torch.bmm(a.float().view(G, T, M).transpose(1, 2), b.float().view(G, T, N))
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3 * (T ** 0.5) / 10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,N,splits", [(77, 1017, 128, 0), (300, 4160, 256, 0), (640, 50257, 768, 0),
+                                          (130, 2111, 192, 3)])
+def test_mm_nn_splitk_matches_fp32(M, K, N, splits):
+    """Split-K NN GEMM with the K tail folded into the reduction (the tied LM
+    head's dh = g W, K = 50,257) vs an fp32 reference; a's rows padded (the CE
+    gradient's layout: only the first K columns are read)."""
+    from commefficient_amd._ext import ops as _ops
+    g = torch.Generator(device="cuda").manual_seed(13)
+    ld = -(-K // 8) * 8 + 8
+    abuf = torch.randn(M, ld, device="cuda", generator=g).to(torch.bfloat16)
+    abuf[:, K:] = float("nan")  # never read
+    a = abuf[:, :K]
+    b = (torch.randn(K, N, device="cuda", generator=g) * K ** -0.5).to(torch.bfloat16)
+    out = _ops().mm_nn_splitk(a, b, splits)
+    ref = a.float() @ b.float()
+    assert out.dtype == torch.bfloat16 and out.shape == (M, N)
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < 5e-3, err
+    assert torch.equal(out, _ops().mm_nn_splitk(a, b, splits))  # deterministic
