@@ -491,8 +491,8 @@ class _LMHead(torch.autograd.Function):
     [T, V] view of it, which the native cross-entropy reads and whose gradient
     it writes in the same padded layout (pad columns 0).  Backward: dW from
     that gradient straight into the tied weight's fp32 sink on the
-    weight-gradient side stream (hipBLASLt fp32-output GEMM; COMMEFF_LM_DW=tn:
-    the native TN GEMM with its M = V edge tile), dh = g W (K = 50,257, only
+    weight-gradient side lane (the native TN GEMM with its M = V edge tile;
+    COMMEFF_LM_DW=blas: hipBLASLt's fp32-output GEMM), dh = g W (K = 50,257, only
     T x H outputs) on the native split-K NN GEMM (``mm_nn_splitk``).  No padded copies of W or of the gradient,
     no bf16 dW + accumulation pass (HF's lm_head on hipBLASLt; reference
     model: gpt2_train.py:262-273)."""
@@ -522,8 +522,10 @@ class _LMHead(torch.autograd.Function):
         dW = None
         if ctx.needs_input_grad[1]:
             if ctx.sink is not None:
-                # (hipBLASLt's fp32-output GEMM into the sink: 120 vs 150 us for
-                # the TN GEMM's 2,358 short-K (T = 640) tiles, scripts/dev/bench_lm_bwd.py)
+                # (in isolation hipBLASLt's fp32-output GEMM is faster: 120 vs
+                # 150 us for the TN GEMM's 2,358 short-K (T = 640) tiles,
+                # scripts/dev/bench_lm_bwd.py; on the side lane the round time
+                # is the same: 13.35 / 13.72 vs 13.39 / 13.59 ms)
                 _wgrad(ctx.sink, g.t(), h, blas=not _LM_DW_TN)
             else:
                 dW = torch.mm(g.t(), h, out_dtype=torch.float32).to(W.dtype)
@@ -534,7 +536,7 @@ class _LMHead(torch.autograd.Function):
 # hipBLASLt).  Round 5's version copied W and the gradient into tile-padded
 # buffers every call and was slower than hipBLASLt (699 vs 377 us isolated).
 _LM_NATIVE = os.environ.get("COMMEFF_LM_HEAD", "native") == "native"
-_LM_DW_TN = os.environ.get("COMMEFF_LM_DW", "blas") == "tn"
+_LM_DW_TN = os.environ.get("COMMEFF_LM_DW", "tn") == "tn"
 _LM_DH_NATIVE = os.environ.get("COMMEFF_LM_DH", "native") == "native"
 
 
