@@ -472,7 +472,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fx_affine_bwd(const at::Tensor& d
                                                              const c10::optional<at::Tensor>& yrelu,
                                                              const c10::optional<at::Tensor>& xs, bool want1,
                                                              bool want2, const c10::optional<at::Tensor>& bias,
-                                                             bool mask_x) {
+                                                             bool mask_x, const c10::optional<at::Tensor>& add2) {
   FaAffine a = fx_args(dy, s, bias, "fx_affine_bwd");
   TORCH_CHECK(!mask_x || (xs.has_value() && xs->defined()), "fx_affine_bwd: mask_x needs xs");
   FaAffineBwd b{};
@@ -486,6 +486,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fx_affine_bwd(const at::Tensor& d
   };
   b.yrelu = same(yrelu, "y");
   b.xs = same(xs, "xs");
+  b.add2 = same(add2, "add2");  // out1 = dpre s + add2 (a second gradient of x)
   b.mask_x = mask_x ? 1 : 0;
   at::Tensor o1, o2;
   if (want1) {
@@ -987,7 +988,7 @@ TORCH_LIBRARY_FRAGMENT(commeff, m) {
         "float alpha, Tensor? src, int sld, Tensor(c!)? mirror, int mld, int dss=0, int ccs=0) -> (Tensor, Tensor)");
   m.def("fx_affine(Tensor x, Tensor? s, Tensor? b, Tensor? add, bool relu, Tensor? post) -> Tensor");
   m.def("fx_affine_bwd(Tensor dy, Tensor? s, Tensor? yrelu, Tensor? xs, bool want1, bool want2, Tensor? b, "
-        "bool mask_x) -> (Tensor, Tensor, Tensor)");
+        "bool mask_x, Tensor? add2=None) -> (Tensor, Tensor, Tensor)");
   m.def("fa_affine(Tensor x, int G, bool client_major, Tensor W, int ld, int soff, int boff, Tensor? add, "
         "bool relu) -> Tensor");
   m.def("fa_affine_bwd(Tensor dy, int G, bool client_major, Tensor W, int ld, int soff, Tensor? yrelu, "

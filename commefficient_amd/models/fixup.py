@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.fixup import fork_bias as _fork
 from ..ops.fixup import scalar_affine as _sa
 from ..ops.nn import relu_maxpool
 from .common import (GhostBatchNorm2d, NativeConv2d, NativeLinear, NativeMaxPool2d, ScalarBias,
@@ -53,9 +54,12 @@ class FixupBasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        xa = _sa(x, b=self.bias1a)
+        if self.downsample is None:  # (x + b1a and the identity: one backward pass)
+            xa, idt = _fork(x, self.bias1a)
+        else:
+            xa = _sa(x, b=self.bias1a)
+            idt = self.downsample(xa)
         out = _sa(self.conv1(xa), b=self.bias1b, relu=True, post=self.bias2a)
-        idt = self.downsample(xa) if self.downsample is not None else x
         return _sa(self.conv2(out), s=self.scale, b=self.bias2b, add=idt, relu=True)
 
 
@@ -147,8 +151,11 @@ class FixupBlock18(nn.Module):
             self.shortcut = conv1x1(in_channels, out_channels, stride)
 
     def forward(self, x):
-        sc = self.shortcut(x) if hasattr(self, "shortcut") else x
-        out = _sa(self.conv1(_sa(x, b=self.add1a.bias)), b=self.add1b.bias, relu=True, post=self.add2a.bias)
+        if hasattr(self, "shortcut"):
+            sc, xa = self.shortcut(x), _sa(x, b=self.add1a.bias)
+        else:
+            xa, sc = _fork(x, self.add1a.bias)
+        out = _sa(self.conv1(xa), b=self.add1b.bias, relu=True, post=self.add2a.bias)
         out = self.conv2(out)
         return _sa(out, s=self.mul.scale, b=self.add2b.bias, add=sc, relu=True)
 
@@ -245,12 +252,14 @@ class FixupBottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        xa = _sa(x, b=self.bias1a)
         if self.downsample is not None:
             # conv1 and the shortcut read xa: one node, input gradients summed in the dgrad GEMM
+            xa = _sa(x, b=self.bias1a)
             out, idt = self.conv1.forward_pair(self.downsample, xa)
         else:
-            out, idt = self.conv1(xa), x
+            # x + b1a and the identity: their gradients summed in the bias's backward pass
+            xa, idt = _fork(x, self.bias1a)
+            out = self.conv1(xa)
         out = _sa(out, b=self.bias1b, relu=True, post=self.bias2a)
         out = _sa(self.conv2(out), b=self.bias2b, relu=True, post=self.bias3a)
         return _sa(self.conv3(out), s=self.scale, b=self.bias3b, add=idt, relu=True)

@@ -29,6 +29,9 @@ from . import grouped as _grouped
 from . import nn as _nn
 
 
+_FORK = __import__("os").environ.get("COMMEFF_FX_FORK", "1") == "1"
+
+
 def _fmt(t: torch.Tensor):
     if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous():
         return torch.channels_last
@@ -71,7 +74,7 @@ class _FxAffine(torch.autograd.Function):
             want1, want2 = (need_x, need_add) if has_s else (need_x or need_add, False)
         else:
             want1, want2 = need_x and has_s, False
-        o1, o2, sums = _ops().fx_affine_bwd(dy, s, y, x, want1, want2, bm, has_post)
+        o1, o2, sums = _ops().fx_affine_bwd(dy, s, y, x, want1, want2, bm, has_post, None)
         dx = (o1 if want1 else dy) if need_x else None
         dadd = None
         if need_add:
@@ -80,6 +83,37 @@ class _FxAffine(torch.autograd.Function):
         db = sums[0:1] if (has_b and need_b) else None
         dpost = sums[1:2] if (has_post and ctx.needs_input_grad[5]) else None
         return dx, ds, db, dadd, None, dpost
+
+
+class _FxForkBias(torch.autograd.Function):
+    """(x + b, x) for a residual block whose input feeds both its first conv
+    (through the input bias) and the identity shortcut: the backward takes
+    both gradients and writes dx = dxa + didentity with b's gradient sum dxa
+    in ONE pass (fa_affine_bwd's add2) -- no separate sum pass and no
+    autograd accumulation pass over the block input."""
+
+    @staticmethod
+    def forward(ctx, x, b):
+        return _ops().fx_affine(x, None, b, None, False, None), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dxa, did):
+        ref = dxa if dxa is not None else did
+        if dxa is None:
+            return did, torch.zeros(1, device=did.device, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        dxa = _like(dxa, ref)
+        add2 = _like(did, dxa) if did is not None else None
+        o1, _, sums = _ops().fx_affine_bwd(dxa, None, None, None, add2 is not None, False, None, False, add2)
+        dx = o1 if add2 is not None else dxa
+        return dx, (sums[0:1] if ctx.needs_input_grad[1] else None)
+
+
+def fork_bias(x: torch.Tensor, b: torch.Tensor):
+    """(x + b, x): a block input's biased copy and its identity shortcut with
+    their two gradients summed in the bias's backward pass (native path)."""
+    if _FORK and native_ok(x, b) and x.requires_grad:
+        return _FxForkBias.apply(x, b.view(1))
+    return scalar_affine(x, b=b), x
 
 
 def native_ok(x: torch.Tensor, *others) -> bool:

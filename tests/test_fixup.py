@@ -103,6 +103,27 @@ def test_scalar_affine_post_bias_matches_fp32(has_b):
 
 
 @pytest.mark.gpu
+def test_fork_bias_sums_both_gradients():
+    """(x + b, x) with dx = dxa + didentity and db = sum dxa in one pass"""
+    from commefficient_amd.ops.fixup import fork_bias
+    g = torch.Generator(device="cuda").manual_seed(6)
+    shape = (4, 128, 6, 10)
+    x = torch.randn(shape, device="cuda", generator=g).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    b = (torch.randn(1, device="cuda", generator=g) * 0.3).requires_grad_(True)
+    w1 = torch.randn(shape, device="cuda", generator=g).to(torch.bfloat16)
+    w2 = torch.randn(shape, device="cuda", generator=g).to(torch.bfloat16)
+    xa, idt = fork_bias(x, b)
+    assert xa.dtype == torch.bfloat16
+    ((xa.float() * w1.float()).sum() + (idt.float() * w2.float()).sum()).backward()
+    torch.testing.assert_close(xa.float(), x.detach().float() + b.detach(), rtol=1e-2, atol=1e-2)
+    ref_dx = w1.float() + w2.float()
+    err = ((x.grad.float() - ref_dx).norm() / ref_dx.norm()).item()
+    assert err < 1e-2, err
+    torch.testing.assert_close(b.grad, w1.float().sum().view(1), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.gpu
 def test_scalar_affine_sums_deterministic_large():
     """many chunks (the two-level fold) and bit-identical reruns"""
     g = torch.Generator(device="cuda").manual_seed(5)
