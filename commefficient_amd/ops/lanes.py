@@ -11,6 +11,11 @@ launches on a side stream after everything issued so far on the main stream
 the side stream before the gradient is read (parallel/fed_model.py, after
 the backward).
 
+Users: the conv / 1x1 / column-image weight gradients of ops/nn.py, the
+GPT-2 weight-gradient GEMMs and column sums of ops/transformer.py, and the
+native FedAvg engines' fused weight updates (parallel/fedavg_native.py, joined
+at the end of every local step).
+
 Eager rounds use PyTorch stream waits; recorded rounds (parallel/tape.py)
 also append the fork / join to the launch tape (csrc/tape.cpp), which
 replays the lane-1 launches on the side stream between event waits.  The
