@@ -469,8 +469,10 @@ class ResNet18FedAvg:
                 ls.append(l.view(G, -1))
                 cs.append(c.view(G, -1))
                 if not fused:
+                    _lanes.join()  # (the gradient rows)
                     ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip), lr_t, float(wd), Wb)
                 steps += 1
+        _lanes.join()
         ops.fa_upload(out, w0i, Wg, ld, G, float(n), perm)
         # running statistics: per-client copies summed for the caller's mean,
         # [4, C] fp64 per block (mean 1, mean 2, var 1, var 2)
@@ -506,6 +508,7 @@ class ResNet18FedAvg:
         a = ops.fa_ew(y0, None, 1)
         a0 = a
         saved = []
+        _lanes.join()  # (the blocks read the rows the lane updated in the last step)
         for bi, b in enumerate(self.blocks):
             xin = a
             rm1, rm2, rv1, rv2 = run[bi]
@@ -619,7 +622,8 @@ class ResNet18FedAvg:
         # (the stem update on the main stream: it has nothing left to do while
         # the lane finishes the last blocks' updates)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
-        _lanes.join()  # (the next step reads the updated rows)
+        # (no join here: the next step's stem runs beside the lane's last
+        # updates; the step joins before its first block reads them)
         return loss, correct
 
 
@@ -737,8 +741,10 @@ class ResNet9FedAvg(ResNet18FedAvg):
                 ls.append(l.view(G, -1))
                 cs.append(c.view(G, -1))
                 if not fused:
+                    _lanes.join()  # (the gradient rows)
                     ops.fa_row_sgd(Wg, ld, W, sld, Gg, ld, G, d, float(clip), lr_t, float(wd), Wb)
                 steps += 1
+        _lanes.join()
         ops.fa_upload(out, w0i, Wg, ld, G, float(n), perm)
         return _step_means(ls), _step_means(cs), []
 
@@ -770,6 +776,7 @@ class ResNet9FedAvg(ResNet18FedAvg):
             return self._conv3(xin, Wb, ld, G, off, K, C)
 
         # ---- forward (saving what the backward reads)
+        _lanes.join()  # (the blocks read the rows the lane updated in the last step)
         p1, c1 = ops.relu_maxpool(conv(a0, "layer1"), 2)
         r1 = ops.fa_ew(conv(p1, "res1.res1"), None, 1)
         r2 = ops.fa_ew(conv(r1, "res1.res2"), None, 1)
@@ -829,7 +836,8 @@ class ResNet9FedAvg(ResNet18FedAvg):
         # (the stem update on the main stream: it has nothing left to do while
         # the lane finishes the last blocks' updates)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
-        _lanes.join()  # (the next step reads the updated rows)
+        # (no join here: the next step's stem runs beside the lane's last
+        # updates; the step joins before its first block reads them)
         return loss, correct
 
 
@@ -964,6 +972,7 @@ class FixupResNet9FedAvg(ResNet9FedAvg):
             out = aff(h2, s=f"{name}.scale", b=f"{name}.bias2b", add=xin, relu=True)
             return (xa_, h1, h1a, h2, out), out
 
+        _lanes.join()  # (the blocks read the rows the lane updated in the last step)
         sv1, p1 = layer(a0, "layer1", "layer1")
         sb1, y1 = block(p1, "layer1.blocks.0", "layer1.b1", "layer1.b2")
         sv2, p2 = layer(y1, "layer2", "layer2")
@@ -1022,7 +1031,8 @@ class FixupResNet9FedAvg(ResNet9FedAvg):
         # (the stem update on the main stream: it has nothing left to do while
         # the lane finishes the last blocks' updates)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
-        _lanes.join()  # (the next step reads the updated rows)
+        # (no join here: the next step's stem runs beside the lane's last
+        # updates; the step joins before its first block reads them)
         return loss, correct
 
 
@@ -1127,6 +1137,7 @@ class FixupResNet18FedAvg(ResNet18FedAvg):
         a = ops.fa_ew(y0, None, 1)
         a0 = a
         saved = []
+        _lanes.join()  # (the blocks read the rows the lane updated in the last step)
         for b, fx in zip(self.blocks, self.fx):
             xin = a
             xa = aff(xin, fx, b="add1a")
@@ -1208,7 +1219,8 @@ class FixupResNet18FedAvg(ResNet18FedAvg):
         # (the stem update on the main stream: it has nothing left to do while
         # the lane finishes the last blocks' updates)
         self._bmm_rows(sink, self.prep, _gview(dy0, G).transpose(1, 2), col0g, lane=False)
-        _lanes.join()  # (the next step reads the updated rows)
+        # (no join here: the next step's stem runs beside the lane's last
+        # updates; the step joins before its first block reads them)
         return loss, correct
 
 
