@@ -13,8 +13,9 @@ the backward).
 
 Users: the conv / 1x1 / column-image weight gradients of ops/nn.py, the
 GPT-2 weight-gradient GEMMs and column sums of ops/transformer.py, and the
-native FedAvg engines' fused weight updates (parallel/fedavg_native.py, joined
-at the end of every local step).
+native FedAvg engines' fused weight updates (parallel/fedavg_native.py: each
+local step joins before its first block reads the updated rows, so the next
+step's stem runs beside the lane's last updates).
 
 Eager rounds use PyTorch stream waits; recorded rounds (parallel/tape.py)
 also append the fork / join to the launch tape (csrc/tape.cpp), which
